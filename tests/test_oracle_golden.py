@@ -1,0 +1,218 @@
+"""Pin the CPU oracle (oracle/refcpu.c) against the reference's own committed
+generation files (golden vectors, tests/golden/).  Every comparison here is
+bit-exact (np.array_equal on float64).
+
+CMA-ES fixture: reference tests/python/plot/cmaes, N=10, lambda=32, mu=16,
+Logarithmic weights, seeds Normal 790510 / Uniform 790511, bounds +-25.
+TMCMC fixture: reference tests/python/plot/tmcmc, N=3, P=50, TargetCOV 0.8.
+"""
+import numpy as np
+import pytest
+
+import refcpu as R
+from golden_util import (CMAES_STATE_SCALARS, CMAES_STATE_VECTORS, cmaes_variables, load_cmaes, load_tmcmc,
+                         population)
+
+CM = load_cmaes()
+TM = load_tmcmc()
+N, LAM, MU = 10, 32, 16
+
+
+def by_gen(gens, g):
+    for x in gens:
+        if x["Current Generation"] == g:
+            return x
+    raise KeyError(g)
+
+
+def cmaes_from_fixture(g):
+    """Oracle CMA-ES handle holding the full state saved after generation g."""
+    st = by_gen(CM, g)
+    o = R.CMAES(N, LAM, MU)
+    o.option("Max Infeasible Resamplings", 10000)
+    for k, v in cmaes_variables(st).items():
+        o[k] = v
+    s = st["Solver"]
+    for k in CMAES_STATE_VECTORS:
+        o[k] = s[k]
+    for k in CMAES_STATE_SCALARS:
+        o[k] = s[k]
+    o.rng(0).from_hex(s["Normal Generator"]["Range"])
+    o.rng(1).from_hex(s["Uniform Generator"]["Range"])
+    return o
+
+
+def test_mt19937_seeding_matches_fixture():
+    s = by_gen(CM, 0)["Solver"]
+    # gen 0 is written before the solver ran: its RNGs are freshly seeded
+    for name, seed in (("Normal Generator", 790510), ("Uniform Generator", 790511)):
+        r = R.Rng(seed=seed)
+        assert r.to_hex() == s[name]["Range"]
+
+
+def test_tmcmc_seeding_matches_fixture():
+    g0 = TM[0]
+    for dist in g0["Distributions"]:
+        r = R.Rng(seed=dist["Random Seed"] & 0xFFFFFFFF)
+        assert r.to_hex() == dist["Range"]
+    for name in ("Multinomial Generator", "Multivariate Generator", "Uniform Generator"):
+        gs = g0["Solver"][name]
+        assert R.Rng(seed=gs["Random Seed"] & 0xFFFFFFFF).to_hex() == gs["Range"]
+
+
+def test_hypot_is_fdlibm():
+    L = R.lib()
+    assert L.kr_hypot(3.0, 4.0) == 5.0
+    assert L.kr_hypot(0.0, 0.0) == 0.0
+    assert L.kr_hypot(1e300, 1e300) == pytest.approx(1.4142135623730951e300, rel=1e-15)
+    assert L.kr_hypot(1e-310, 0.0) == 1e-310
+    assert np.isinf(L.kr_hypot(np.inf, np.nan))
+
+
+@pytest.mark.parametrize("k", range(1, 100))
+def test_eigensystem_bit_exact(k):
+    """gen k's C -> gen k+1's B (Covariance Eigenvector Matrix) and D."""
+    C = np.array(by_gen(CM, k)["Solver"]["Covariance Matrix"]).reshape(N, N)
+    nxt = by_gen(CM, k + 1)["Solver"]
+    A = np.tril(C) + np.tril(C, -1).T
+    ev, Q = R.eigen_symmv(A)
+    assert np.array_equal(Q.reshape(-1), np.array(nxt["Covariance Eigenvector Matrix"]))
+    assert np.array_equal(np.sqrt(ev), np.array(nxt["Axis Lengths"]))
+
+
+@pytest.mark.parametrize("k", [1, 2, 19, 49, 99])
+def test_cmaes_generation_teacher_forced(k):
+    """State after gen k + gen k+1's fitness values -> gen k+1 bit-exact:
+    eigensystem, the whole population (MT19937 + polar + B*D*z), sorting
+    index, mean, paths, covariance, sigma."""
+    o = cmaes_from_fixture(k)
+    nxt = by_gen(CM, k + 1)["Solver"]
+    o.prepare()
+    assert np.array_equal(o["Covariance Eigenvector Matrix"], np.array(nxt["Covariance Eigenvector Matrix"]))
+    assert np.array_equal(o["Sample Population"], population(by_gen(CM, k + 1)).reshape(-1))
+    assert o["Infeasible Sample Count"][0] == nxt["Infeasible Sample Count"]
+    o["Value Vector"] = nxt["Value Vector"]
+    o.update(k + 1)
+    assert list(o.sorting_index()) == nxt["Sorting Index"]
+    for key in ("Current Mean", "Previous Mean", "Evolution Path", "Conjugate Evolution Path", "Covariance Matrix"):
+        assert np.array_equal(o[key], np.array(nxt[key])), key
+    for key in ("Sigma", "Conjugate Evolution Path L2 Norm", "Best Ever Value", "Current Best Value",
+                "Maximum Diagonal Covariance Matrix Element", "Minimum Diagonal Covariance Matrix Element",
+                "Current Min Standard Deviation", "Current Max Standard Deviation"):
+        assert o[key][0] == nxt[key], key
+
+
+def test_cmaes_values_are_negative_sphere():
+    """The fixture objective is F = -0.5*sum(x^2); check the builtin."""
+    st = by_gen(CM, 5)["Solver"]
+    X = np.array(st["Sample Population"])
+    F = [R.objective("sphere", x) for x in X]
+    assert np.array_equal(np.array(F), np.array(st["Value Vector"]))
+
+
+def test_cmaes_initialize_matches_gen1_constants():
+    st1 = by_gen(CM, 1)
+    o = R.CMAES(N, LAM, MU)
+    for k, v in cmaes_variables(st1).items():
+        o[k] = v
+    o.initialize()
+    s = st1["Solver"]
+    for key in ("Effective Mu", "Cumulative Covariance", "Sigma Cumulation Factor", "Damp Factor",
+                "Chi Square Number", "Trace"):
+        assert o[key][0] == s[key], key
+    assert np.array_equal(o["Mu Weights"], np.array(s["Mu Weights"]))
+
+
+def test_cmaes_full_run_from_seed_reproduces_fixture():
+    """Seeded from scratch (experiment seed 790510), the oracle reproduces
+    generations 1..100 of the fixture with the fixture objective."""
+    st0 = by_gen(CM, 0)
+    o = R.CMAES(N, LAM, MU)
+    o.option("Max Infeasible Resamplings", 10000)
+    for k, v in cmaes_variables(st0).items():
+        o[k] = v
+    R.lib().kr_rng_seed(o.rng(0).ptr, 790510)
+    R.lib().kr_rng_seed(o.rng(1).ptr, 790511)
+    for g in range(1, 101):
+        o.generation(g, "sphere")
+        s = by_gen(CM, g)["Solver"]
+        assert list(o.sorting_index()) == s["Sorting Index"], g
+        assert np.array_equal(o["Sample Population"], population(by_gen(CM, g)).reshape(-1)), g
+        assert np.array_equal(o["Covariance Matrix"], np.array(s["Covariance Matrix"])), g
+        assert o["Sigma"][0] == s["Sigma"], g
+    assert o.rng(0).to_hex() == by_gen(CM, 100)["Solver"]["Normal Generator"]["Range"]
+
+
+# ------------------------------------------------------------------ TMCMC
+TN, TP = 3, 50
+
+
+def tmcmc_from_fixture(g):
+    st = by_gen(TM, g)
+    s = st["Solver"]
+    o = R.TMCMC(TN, TP)
+    o.option("Target Coefficient Of Variation", s["Target Coefficient Of Variation"])
+    o.option("Covariance Scaling", s["Covariance Scaling"])
+    o["Prior Minimum"] = [d["Minimum"] for d in st["Distributions"]]
+    o["Prior Maximum"] = [d["Maximum"] for d in st["Distributions"]]
+    for k in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Leaders LogPriors", "Covariance Matrix",
+              "Chain Lengths"):
+        if len(s[k]):
+            o[k] = s[k]
+    for k in ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", "Chain Count"):
+        o[k] = s[k]
+    o.rng(0).from_hex(s["Multinomial Generator"]["Range"])
+    o.rng(1).from_hex(s["Multivariate Generator"]["Range"])
+    o.rng(2).from_hex(s["Uniform Generator"]["Range"])
+    for i, d in enumerate(st["Distributions"]):
+        o.rng(3 + i).from_hex(d["Range"])
+    return o
+
+
+@pytest.mark.parametrize("k", range(0, 7))
+def test_tmcmc_generation_teacher_forced(k):
+    """State after gen k + gen k+1's candidate log-likelihoods (the reference
+    problem used a Python model) -> gen k+1 bit-exact: Cholesky + candidate
+    draws, accept/reject, annealing exponent (nmsimplex), log-evidence,
+    multinomial resampling -> chain leaders, mean and covariance."""
+    o = tmcmc_from_fixture(k)
+    nxt = by_gen(TM, k + 1)["Solver"]
+    g = k + 1
+    if g == 1:
+        o.initialize()
+    o.prepare(g)
+    cand = np.array(nxt["Chain Candidates"]).reshape(-1)
+    assert np.array_equal(o["Chain Candidates"], cand)
+    o["Chain Candidates LogLikelihoods"] = nxt["Chain Candidates LogLikelihoods"]
+    o["Chain Candidates LogPriors"] = nxt["Chain Candidates LogPriors"]
+    o.process_candidates(g)
+    assert o["Accepted Samples Count"][0] == nxt["Accepted Samples Count"]
+    assert np.array_equal(o["Sample LogLikelihood Database"], np.array(nxt["Sample LogLikelihood Database"]))
+    o.process_generation()
+    for key in ("Annealing Exponent", "LogEvidence", "Coefficient Of Variation", "Max Loglikelihood",
+                "Selection Acceptance Rate", "Proposals Acceptance Rate", "Chain Count"):
+        assert o[key][0] == nxt[key], key
+    for key in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Lengths", "Covariance Matrix", "Mean Theta"):
+        assert np.array_equal(o[key], np.array(nxt[key]).reshape(-1)), key
+    assert o.rng(0).to_hex() == nxt["Multinomial Generator"]["Range"]
+    assert o.rng(1).to_hex() == nxt["Multivariate Generator"]["Range"]
+    assert o.rng(2).to_hex() == nxt["Uniform Generator"]["Range"]
+
+
+def test_binomial_btpe_statistics():
+    """BTPE branch (n*p >= 14) is pinned by no fixture: check moments."""
+    r = R.Rng(seed=1337)
+    L = R.lib()
+    n, p = 2000, 0.3
+    xs = np.array([L.kr_ran_binomial(r.ptr, p, n) for _ in range(20000)], dtype=np.float64)
+    assert abs(xs.mean() - n * p) < 0.5
+    assert abs(xs.var() / (n * p * (1 - p)) - 1.0) < 0.05
+    assert xs.min() >= 0 and xs.max() <= n
+
+
+def test_multinomial_conserves_total():
+    r = R.Rng(seed=7)
+    w = np.random.default_rng(3).random(8192)
+    w /= w.sum()
+    n = R.multinomial(r, w, 8192)
+    assert int(n.sum()) == 8192
