@@ -1,0 +1,158 @@
+/*
+ * korali_amd.h — C-ABI of the MI355X-native population-generation engine.
+ *
+ * This is the drop-in boundary for Korali's population-based solver
+ * generation loop.  The reference calls GSL / gslcblas directly from its C++
+ * solver modules; each entry point below replaces one of those solver
+ * stages (reference paths relative to the korali root):
+ *
+ *   kg_cmaes_initialize   CMAES::setInitialConfiguration   CMAES.cpp.base:14-184
+ *                         (initMuWeights :233-284, initCovariance :286-313)
+ *   kg_cmaes_sample       CMAES::prepareGeneration         CMAES.cpp.base:439-492
+ *                         (updateEigensystem/eigen :869-938, sampleSingle
+ *                          :494-545, Optimizer::isSampleFeasible
+ *                          optimizer.cpp.base:5-14, Normal::getRandomNumber
+ *                          univariate/normal/normal.cpp.base:32-35)
+ *   kg_cmaes_eval_builtin Optimization::evaluate → user objective
+ *                         optimization.cpp.base:26-34, batched over λ
+ *   kg_cmaes_get_candidates / kg_cmaes_set_fitness
+ *                         KORALI_START/WAITALL/GET of CMAES::runGeneration
+ *                         CMAES.cpp.base:204-224 (host-callback objectives)
+ *   kg_cmaes_update       CMAES::updateDistribution        CMAES.cpp.base:547-688
+ *                         (sort_index :940-950, adaptC :690-718,
+ *                          updateSigma :720-761, numericalErrorTreatment :763-772)
+ *   kg_cmaes_generation   CMAES::runGeneration             CMAES.cpp.base:186-231
+ *   kg_cmaes_{get,set}_field / _{get,set}_rng
+ *                         Module::getConfiguration / setConfiguration of the
+ *                         solver state incl. RNG "Range" (distribution.cpp.base:10-62)
+ *
+ *   kg_tmcmc_*            TMCMC::runGeneration             TMCMC.cpp.base:107-157
+ *
+ * Conventions: every function returns 0 on success and non-zero on error;
+ * kg_last_error() returns the message (thread-local).  No C++ exceptions or
+ * torch types cross this boundary.  Host arrays are caller-owned and copied;
+ * device buffers are owned by the handle.  Matrices are row-major doubles,
+ * exactly as the reference stores them (std::vector<double> N*N).
+ */
+#ifndef KORALI_AMD_H
+#define KORALI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KG_ABI_VERSION 1
+
+const char *kg_last_error(void);
+int kg_abi_version(void);
+int kg_device_count(int *count);
+
+/* -------------------------------------------------------------- CMA-ES */
+typedef struct kg_cmaes_s *kg_cmaes_t;
+
+enum kg_mu_type { KG_MU_LOGARITHMIC = 0, KG_MU_LINEAR = 1, KG_MU_EQUAL = 2, KG_MU_PROPORTIONAL = 3 };
+enum kg_objective { KG_OBJ_NEGATIVE_ROSENBROCK = 0, KG_OBJ_NEGATIVE_ACKLEY = 1, KG_OBJ_NEGATIVE_SPHERE = 2 };
+/* Covariance rank-mu update: EXACT replays the reference's sequential
+ * per-element summation (bit-faithful); MFMA sums y_k y_k^T on the FP64
+ * matrix cores (v_mfma_f64_16x16x4f64), within 1e-12 relative. */
+enum kg_cov_mode { KG_COV_EXACT = 0, KG_COV_MFMA = 1 };
+
+typedef struct {
+  size_t variable_count;  /* N  (CMAES "Variable Count") */
+  size_t population_size; /* λ  ("Population Size") */
+  size_t mu_value;        /* μ  ("Mu Value"; 0 → λ/2, CMAES.cpp.base:27) */
+  int mu_type;            /* enum kg_mu_type ("Mu Type") */
+  double initial_sigma_cumulation_factor; /* ≤0 → formula default */
+  double initial_damp_factor;             /* ≤0 → formula default */
+  double initial_cumulative_covariance;   /* ≤0 or >1 → formula default */
+  int is_sigma_bounded;                   /* "Is Sigma Bounded" */
+  int diagonal_covariance;                /* "Diagonal Covariance" */
+  int mirrored_sampling;                  /* "Mirrored Sampling" (not yet on device: error) */
+  double max_infeasible_resamplings;      /* "Termination Criteria/Max Infeasible Resamplings" */
+  const double *lower_bound;              /* N, may be NULL → -inf */
+  const double *upper_bound;              /* N, may be NULL → +inf */
+  const double *initial_value;            /* N, NaN → midpoint of bounds */
+  const double *initial_std;              /* N, NaN → 0.3*(ub-lb) */
+  const double *min_std_update;           /* N, may be NULL → 0 */
+  uint64_t normal_seed;                   /* seed of the Normal generator (GSL mt19937) */
+  uint64_t uniform_seed;                  /* seed of the Uniform generator */
+  int cov_mode;                           /* enum kg_cov_mode */
+  int device;                             /* HIP device ordinal */
+  int store_bdz;                          /* also keep the BDZ matrix (state export) */
+} kg_cmaes_cfg;
+
+int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);
+int kg_cmaes_destroy(kg_cmaes_t h);
+int kg_cmaes_initialize(kg_cmaes_t h);
+int kg_cmaes_sample(kg_cmaes_t h);
+int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective);
+int kg_cmaes_get_candidates(kg_cmaes_t h, double *X, size_t ld);
+int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F);
+int kg_cmaes_update(kg_cmaes_t h, size_t generation);
+/* one whole generation, enqueued asynchronously (no host sync) */
+int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective);
+int kg_cmaes_synchronize(kg_cmaes_t h); /* waits and reports device-side errors */
+/* named state fields, keys as in the reference's solver JSON
+ * ("Sigma", "Covariance Matrix", "Current Mean", ...); sizes in doubles */
+int kg_cmaes_field_size(kg_cmaes_t h, const char *name, size_t *n);
+int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n);
+int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t n);
+int kg_cmaes_get_sorting_index(kg_cmaes_t h, uint64_t *out);
+/* GSL mt19937 state as Korali serialises it: 624 x uint64 words + int32 mti
+ * + 4 pad bytes = 5000 bytes.  which: 0 Normal, 1 Uniform generator. */
+int kg_cmaes_get_rng(kg_cmaes_t h, int which, void *state5000);
+int kg_cmaes_set_rng(kg_cmaes_t h, int which, const void *state5000);
+/* device pointer of a named buffer (zero-copy interop) and the HIP stream */
+int kg_cmaes_device_ptr(kg_cmaes_t h, const char *name, void **ptr);
+int kg_cmaes_stream(kg_cmaes_t h, void **stream);
+/* kernel timing probe: average device time (ms) of the named kernel family
+ * over the last generation(s) since the previous call, measured with HIP
+ * events on the handle's stream; enable with kg_cmaes_profile(h, 1). */
+int kg_cmaes_profile(kg_cmaes_t h, int enable);
+int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, size_t *count);
+
+/* --------------------------------------------------------------- TMCMC */
+typedef struct kg_tmcmc_s *kg_tmcmc_t;
+
+enum kg_likelihood { KG_LIK_GAUSSIAN = 0 }; /* -0.5*sum(x^2), model.py:32-37 */
+
+typedef struct {
+  size_t variable_count;  /* N */
+  size_t population_size; /* P ("Population Size") */
+  double max_chain_length;               /* must be 1 on device for now */
+  double default_burn_in;                /* must be 0 on device for now */
+  double target_cov;                     /* "Target Coefficient Of Variation" */
+  double covariance_scaling;             /* "Covariance Scaling" */
+  double min_annealing_exponent_update;
+  double max_annealing_exponent_update;
+  const double *prior_min;               /* N: Univariate/Uniform priors */
+  const double *prior_max;               /* N */
+  const uint64_t *prior_seeds;           /* N seeds of the prior generators */
+  uint64_t multinomial_seed, multivariate_seed, uniform_seed;
+  int likelihood;                        /* enum kg_likelihood */
+  int device;
+} kg_tmcmc_cfg;
+
+int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
+int kg_tmcmc_destroy(kg_tmcmc_t h);
+int kg_tmcmc_generation(kg_tmcmc_t h, size_t generation);
+int kg_tmcmc_synchronize(kg_tmcmc_t h);
+int kg_tmcmc_field_size(kg_tmcmc_t h, const char *name, size_t *n);
+int kg_tmcmc_get_field(kg_tmcmc_t h, const char *name, double *out, size_t n);
+int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t n);
+/* which: 0 Multinomial, 1 Multivariate, 2 Uniform, 3+k prior k */
+int kg_tmcmc_get_rng(kg_tmcmc_t h, int which, void *state5000);
+int kg_tmcmc_set_rng(kg_tmcmc_t h, int which, const void *state5000);
+/* teacher-forcing hooks used by the parity tests: run the stages of one
+ * generation separately, with externally supplied log-likelihoods */
+int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation);
+int kg_tmcmc_evaluate(kg_tmcmc_t h);
+int kg_tmcmc_process(kg_tmcmc_t h, size_t generation);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KORALI_AMD_H */

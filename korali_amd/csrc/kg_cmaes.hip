@@ -1,0 +1,1171 @@
+// kg_cmaes.hip — CMA-ES generation on the MI355X (CMAES.cpp.base, see
+// include/korali_amd.h for the per-entry-point reference map).
+//
+// HBM layout per handle (all FP64, row-major as the reference's vectors):
+//   X   λ x N   sample population        Z   (λ+R) x N  polar normals
+//   C,B N x N   covariance / eigenvectors D,mean,prevMean,pc,ps  N
+//   F   λ       fitness                  idx λ  sorting index (uint32)
+//   w   μ       recombination weights    sc  scalar block (σ, counters, ...)
+// One HIP stream per handle; a generation is a fixed kernel sequence with no
+// host synchronisation (device-side error flags are read at sync points).
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/korali_amd.h"
+#include "kg_common.hpp"
+#include "kg_rng.hpp"
+
+namespace kg {
+
+int launch_symmv(int N, int diagonal, const double *C, double *gA, double *gH, double *B, double *D, double *minEig,
+                 double *maxEig, double *eigenFailures, unsigned int *errors, hipStream_t s);
+
+struct CmaesScalars {
+  double sigma, trace, effectiveMu, cumulativeCovariance, sigmaCumulationFactor, dampFactor, chiSquareNumber;
+  double psNorm, bestEverValue, previousBestEverValue, previousBestValue, currentBestValue;
+  double currentMinStd, currentMaxStd, maxDiagC, minDiagC, minEig, maxEig;
+  double infeasibleSampleCount, bestValidSample, modelEvaluationCount, hsig, eigenFailures;
+  double ccov1, ccovmu;
+  unsigned int errors, pad;
+};
+
+// ----------------------------------------------------------------- init
+// setInitialConfiguration (CMAES.cpp.base:14-184), initMuWeights (:233-284),
+// initCovariance (:286-313); initial values/stds resolved on the host.
+__global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType, double initialSigmaCumulationFactor,
+                                              double initialDampFactor, double initialCumulativeCovariance,
+                                              const double *__restrict__ iv, const double *__restrict__ istd,
+                                              double *w, double *C, double *B, double *D, double *mean,
+                                              double *prevMean, double *pc, double *ps, CmaesScalars *sc) {
+  __shared__ double s1s2[2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < mu; i += blockDim.x) {
+    double v;
+    if (muType == KG_MU_LINEAR)
+      v = (double)(mu - i);
+    else if (muType == KG_MU_EQUAL || muType == KG_MU_PROPORTIONAL)
+      v = 1.;
+    else {
+      const double a = (double)mu, b = 0.5 * (double)lam;
+      v = log_cr((a > b ? a : b) + 0.5) - log_cr(i + 1.);
+    }
+    w[i] = v;
+  }
+  for (int i = tid; i < N * N; i += blockDim.x) {
+    C[i] = 0.0;
+    B[i] = 0.0;
+  }
+  for (int i = tid; i < N; i += blockDim.x) {
+    pc[i] = 0.0;
+    ps[i] = 0.0;
+    mean[i] = iv[i];
+    prevMean[i] = iv[i];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < mu; i++) {
+      s1 += w[i];
+      s2 += w[i] * w[i];
+    }
+    s1s2[0] = s1;
+    s1s2[1] = s2;
+  }
+  __syncthreads();
+  for (int i = tid; i < mu; i += blockDim.x) w[i] /= s1s2[0];
+  if (tid == 0) {
+    const double Nd = (double)N;
+    sc->bestEverValue = -INFINITY;
+    sc->previousBestEverValue = sc->bestEverValue;
+    sc->previousBestValue = sc->bestEverValue;
+    sc->currentBestValue = sc->bestEverValue;
+    sc->chiSquareNumber = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));
+    sc->bestValidSample = 0;
+    const double effMu = s1s2[0] * s1s2[0] / s1s2[1];
+    sc->effectiveMu = effMu;
+    if ((initialCumulativeCovariance <= 0) || (initialCumulativeCovariance > 1))
+      sc->cumulativeCovariance = (4.0 + effMu / (1.0 * N)) / (N + 4.0 + 2.0 * effMu / (1.0 * N));
+    else
+      sc->cumulativeCovariance = initialCumulativeCovariance;
+    double cs = initialSigmaCumulationFactor;
+    if (cs <= 0 || cs >= 1) cs = (effMu + 2.0) / (N + effMu + 3.0);
+    sc->sigmaCumulationFactor = cs;
+    double ds = initialDampFactor;
+    if (ds <= 0.0) {
+      const double t = sqrt((effMu - 1.0) / (N + 1.0)) - 1;
+      ds = (1.0 + 2 * (0.0 > t ? 0.0 : t)) + cs;
+    }
+    sc->dampFactor = ds;
+    // initCovariance
+    double trace = 0.0;
+    for (int i = 0; i < N; ++i) trace += istd[i] * istd[i];
+    sc->trace = trace;
+    sc->sigma = sqrt(trace / N);
+    for (int i = 0; i < N; ++i) {
+      B[i * N + i] = 1.0;
+      double v = istd[i] * sqrt(N / trace);
+      D[i] = v;
+      C[i * N + i] = v * v;
+    }
+    double mn = D[0], mx = D[0];
+    for (int i = 1; i < N; i++) {
+      if (D[i] < mn) mn = D[i];
+      if (D[i] > mx) mx = D[i];
+    }
+    sc->minEig = mn * mn;
+    sc->maxEig = mx * mx;
+    double maxd = C[0], mind = C[0];
+    for (int i = 1; i < N; ++i)
+      if (maxd < C[i * N + i]) maxd = C[i * N + i];
+    for (int i = 1; i < N; ++i)
+      if (mind > C[i * N + i]) mind = C[i * N + i];
+    sc->maxDiagC = maxd;
+    sc->minDiagC = mind;
+    sc->infeasibleSampleCount = 0;
+    sc->psNorm = 0.0;
+    sc->currentMinStd = INFINITY;
+    sc->currentMaxStd = -INFINITY;
+  }
+}
+
+// ------------------------------------------------------------ transform
+// sampleSingle (CMAES.cpp.base:494-545): x = m + σ B (D∘z), the B·aux sum in
+// the reference's order (e = 0..N-1 from 0.0, separate multiply and add);
+// isSampleFeasible (optimizer.cpp.base:5-14) folded into the epilogue.
+constexpr int TR_BM = 32, TR_BN = 64, TR_BK = 32;
+__global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal, const double *__restrict__ Z,
+                                                   const double *__restrict__ B, const double *__restrict__ D,
+                                                   const double *__restrict__ mean, const CmaesScalars *__restrict__ sc,
+                                                   const double *__restrict__ lb, const double *__restrict__ ub,
+                                                   double *__restrict__ X, double *__restrict__ BDZ,
+                                                   int *__restrict__ infeas) {
+  __shared__ double Za[TR_BK][TR_BM + 1];
+  __shared__ double Bt[TR_BK][TR_BN + 1];
+  const int tid = threadIdx.x;
+  const int nbn = (N + TR_BN - 1) / TR_BN;
+  const int i0 = (blockIdx.x / nbn) * TR_BM, d0 = (blockIdx.x % nbn) * TR_BN;
+  const int tx = tid & 31, ty = tid >> 5;  // dims tx, tx+32; cands ty + 8p
+  const double sigma = sc->sigma;
+  double acc[4][2];
+#pragma unroll
+  for (int p = 0; p < 4; p++) acc[p][0] = acc[p][1] = 0.0;
+  if (!diagonal) {
+    for (int k0 = 0; k0 < N; k0 += TR_BK) {
+      for (int q = tid; q < TR_BM * TR_BK; q += 256) {
+        const int c = q / TR_BK, kk = q % TR_BK;
+        const int i = i0 + c, e = k0 + kk;
+        Za[kk][c] = (i < rows && e < N) ? D[e] * Z[(size_t)i * N + e] : 0.0;
+      }
+      for (int q = tid; q < TR_BN * TR_BK; q += 256) {
+        const int dd = q / TR_BK, kk = q % TR_BK;
+        const int d = d0 + dd, e = k0 + kk;
+        Bt[kk][dd] = (d < N && e < N) ? B[(size_t)d * N + e] : 0.0;
+      }
+      __syncthreads();
+      const int kmax = (N - k0) < TR_BK ? (N - k0) : TR_BK;
+      for (int kk = 0; kk < kmax; kk++) {
+        const double b0 = Bt[kk][tx], b1 = Bt[kk][tx + 32];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+          const double a = Za[kk][ty + 8 * p];
+          acc[p][0] += b0 * a;
+          acc[p][1] += b1 * a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const int i = i0 + ty + 8 * p;
+    if (i >= rows) continue;
+    int bad = 0;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int d = d0 + tx + 32 * q;
+      if (d >= N) continue;
+      const double bdz = diagonal ? D[d] * Z[(size_t)i * N + d] : acc[p][q];
+      const double x = mean[d] + sigma * bdz;
+      X[(size_t)i * N + d] = x;
+      if (BDZ) BDZ[(size_t)i * N + d] = bdz;
+      if (!isfinite(x) || x < lb[d] || x > ub[d]) bad = 1;
+    }
+    if (bad) atomicOr(&infeas[i], 1);
+  }
+}
+
+// resampling (prepareGeneration :443-460): candidate i takes the next block
+// whose draw is feasible, or any block once the global infeasible counter
+// reaches Max Infeasible Resamplings.  Sequential (one thread): runs only
+// when some bound is finite.
+__global__ void k_select(int lam, int blocks, double maxRes, const int *__restrict__ infeas, int *__restrict__ assign,
+                         unsigned long long *__restrict__ used, CmaesScalars *sc) {
+  if (threadIdx.x != 0) return;
+  double count = sc->infeasibleSampleCount;
+  int j = 0;
+  for (int i = 0; i < lam; i++) {
+    for (;;) {
+      if (j >= blocks) {
+        sc->errors |= KG_ERR_RESAMPLE_RESERVE;
+        assign[i] = blocks - 1;
+        break;
+      }
+      const int feasible = infeas[j] ? 0 : 1;
+      if (!feasible) count += 1;
+      const int jj = j++;
+      if (feasible || !(count < maxRes)) {
+        assign[i] = jj;
+        break;
+      }
+    }
+  }
+  sc->infeasibleSampleCount = count;
+  *used = (unsigned long long)j;
+}
+
+__global__ void k_count_infeasible(int lam, const int *__restrict__ infeas, CmaesScalars *sc,
+                                   unsigned long long *used) {
+  // no reserve: every drawn candidate is kept; a non-finite or out-of-bound
+  // draw would have been redrawn by the reference → flag it
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < lam; i++)
+    if (infeas[i]) sc->errors |= KG_ERR_RESAMPLE_RESERVE;
+  *used = (unsigned long long)lam;
+}
+
+__global__ void k_gather_rows(int N, int lam, const int *__restrict__ assign, const double *__restrict__ Xall,
+                              double *__restrict__ X, const double *__restrict__ BDZall, double *__restrict__ BDZ) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)lam * N) return;
+  const int i = (int)(t / N), d = (int)(t % N);
+  X[t] = Xall[(size_t)assign[i] * N + d];
+  if (BDZ) BDZ[t] = BDZall[(size_t)assign[i] * N + d];
+}
+
+// ------------------------------------------------------------ objective
+// examples/optimization/stochastic/_model/model.py: negative_rosenbrock
+// (:23-34), negative_ackley (:37-62), negative_sphere; sequential in d.
+__global__ void __launch_bounds__(64) k_objective(int N, int lam, int obj, const double *__restrict__ X,
+                                                  double *__restrict__ F, CmaesScalars *sc) {
+  __shared__ double tile[64][65];
+  const int t = threadIdx.x;
+  const int c0 = blockIdx.x * 64;
+  const int i = c0 + t;
+  double r0 = 0.0, r1 = 0.0, prev = 0.0;
+  const double cc = 2. * 3.141592653589793;
+  for (int d0 = 0; d0 < N; d0 += 64) {
+    const int dn = (N - d0) < 64 ? (N - d0) : 64;
+    for (int r = 0; r < 64; r++) {
+      const int ii = c0 + r;
+      tile[r][t] = (ii < lam && t < dn) ? X[(size_t)ii * N + d0 + t] : 0.0;
+    }
+    __syncthreads();
+    if (i < lam) {
+      for (int dd = 0; dd < dn; dd++) {
+        const double x = tile[t][dd];
+        const int d = d0 + dd;
+        if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
+          if (d > 0) {
+            const double tt = x - prev * prev;
+            const double u = 1 - prev;
+            r0 += 100 * (tt * tt) + u * u;
+          }
+          prev = x;
+        } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
+          r0 += x * x;
+          r1 += cos(cc * x);
+        } else {
+          r0 += x * x;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (i >= lam) return;
+  double f;
+  if (obj == KG_OBJ_NEGATIVE_ROSENBROCK)
+    f = -r0;
+  else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
+    const double s1 = r0 / (double)N, s2 = r1 / (double)N;
+    const double e1 = 20. * exp_cr(-0.2 * sqrt(s1));
+    const double e2 = exp_cr(s2);
+    f = e1 + e2 - 20. - 2.718281828459045;
+  } else
+    f = -0.5 * r0;
+  F[i] = f;
+  if (!isfinite(f)) atomicOr(&sc->errors, KG_ERR_NONFINITE_F);
+}
+
+// ----------------------------------------------------------------- sort
+// sort_index (CMAES.cpp.base:940-950): descending F; ties by index (the
+// reference's std::sort leaves tie order unspecified).  Bitonic network:
+// chunks of SORT_CHUNK in LDS, wider strides in global passes.
+constexpr int SORT_CHUNK = 2048;
+__device__ inline bool before(double ka, unsigned ia, double kb, unsigned ib) {
+  return (ka > kb) || (ka == kb && ia < ib);
+}
+
+__global__ void __launch_bounds__(1024) k_sort_init(int lam, int P2, const double *__restrict__ F, double *key,
+                                                    unsigned *val) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P2) return;
+  key[i] = (i < lam) ? F[i] : -INFINITY;
+  val[i] = (i < lam) ? (unsigned)i : 0xffffffffu;
+}
+
+// local stages: for k in [kmin..kmax] (kmax <= SORT_CHUNK), or one k with all
+// j < SORT_CHUNK when kfixed > 0
+__global__ void __launch_bounds__(1024) k_sort_local(int P2, int kfixed, double *key, unsigned *val) {
+  __shared__ double sk[SORT_CHUNK];
+  __shared__ unsigned sv[SORT_CHUNK];
+  const int base = blockIdx.x * SORT_CHUNK;
+  for (int q = threadIdx.x; q < SORT_CHUNK; q += blockDim.x) {
+    sk[q] = key[base + q];
+    sv[q] = val[base + q];
+  }
+  __syncthreads();
+  const int kstart = kfixed ? kfixed : 2, kend = kfixed ? kfixed : SORT_CHUNK;
+  for (int k = kstart; k <= kend; k <<= 1) {
+    const int jstart = kfixed ? SORT_CHUNK / 2 : k / 2;
+    for (int j = jstart; j > 0; j >>= 1) {
+      for (int q = threadIdx.x; q < SORT_CHUNK; q += blockDim.x) {
+        const int l = q ^ j;
+        if (l > q) {
+          const int gi = base + q;
+          const bool asc = ((gi & k) == 0);
+          const double ka = sk[q], kb = sk[l];
+          const unsigned ia = sv[q], ib = sv[l];
+          const bool sw = asc ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
+          if (sw) {
+            sk[q] = kb;
+            sk[l] = ka;
+            sv[q] = ib;
+            sv[l] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int q = threadIdx.x; q < SORT_CHUNK; q += blockDim.x) {
+    key[base + q] = sk[q];
+    val[base + q] = sv[q];
+  }
+}
+
+__global__ void k_sort_global(int P2, int k, int j, double *key, unsigned *val) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P2) return;
+  const int l = q ^ j;
+  if (l <= q) return;
+  const bool asc = ((q & k) == 0);
+  const double ka = key[q], kb = key[l];
+  const unsigned ia = val[q], ib = val[l];
+  const bool sw = asc ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
+  if (sw) {
+    key[q] = kb;
+    key[l] = ka;
+    val[q] = ib;
+    val[l] = ia;
+  }
+}
+
+// small λ (< SORT_CHUNK): one block sorts everything
+__global__ void __launch_bounds__(1024) k_sort_small(int lam, int P2, const double *__restrict__ F, unsigned *out) {
+  __shared__ double sk[SORT_CHUNK];
+  __shared__ unsigned sv[SORT_CHUNK];
+  for (int q = threadIdx.x; q < P2; q += blockDim.x) {
+    sk[q] = (q < lam) ? F[q] : -INFINITY;
+    sv[q] = (q < lam) ? (unsigned)q : 0xffffffffu;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k / 2; j > 0; j >>= 1) {
+      for (int q = threadIdx.x; q < P2; q += blockDim.x) {
+        const int l = q ^ j;
+        if (l > q) {
+          const bool asc = ((q & k) == 0);
+          const double ka = sk[q], kb = sk[l];
+          const unsigned ia = sv[q], ib = sv[l];
+          const bool sw = asc ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
+          if (sw) {
+            sk[q] = kb;
+            sk[l] = ka;
+            sv[q] = ib;
+            sv[l] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int q = threadIdx.x; q < lam; q += blockDim.x) out[q] = sv[q];
+}
+
+__global__ void k_copy_idx(int lam, const unsigned *__restrict__ val, unsigned *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < lam) out[i] = val[i];
+}
+
+// --------------------------------------------------------------- update
+// updateDistribution :547-609 (best bookkeeping, proportional weights)
+__global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, unsigned long long gen,
+                                                     const double *__restrict__ X, const double *__restrict__ F,
+                                                     const unsigned *__restrict__ idx, double *w,
+                                                     double *currBestVars, double *bestEverVars, CmaesScalars *sc) {
+  __shared__ int flag;
+  const int tid = threadIdx.x;
+  const unsigned i0 = idx[0];
+  if (tid == 0) {
+    sc->bestValidSample = (double)i0;
+    sc->previousBestValue = sc->currentBestValue;
+    sc->currentBestValue = F[i0];
+    flag = (sc->currentBestValue > sc->bestEverValue || gen == 1) ? 1 : 0;
+    if (flag) {
+      sc->previousBestEverValue = sc->bestEverValue;
+      sc->bestEverValue = sc->currentBestValue;
+    }
+    if (muType == KG_MU_PROPORTIONAL) {
+      double valueSum = 0.;
+      for (int i = 0; i < mu; ++i) {
+        const double value = F[idx[i]];
+        w[i] = value;
+        valueSum += value;
+      }
+      for (int i = 0; i < mu; ++i) w[i] /= valueSum;
+    }
+  }
+  __syncthreads();
+  for (int d = tid; d < N; d += blockDim.x) {
+    const double v = X[(size_t)i0 * N + d];
+    currBestVars[d] = v;
+    if (flag) bestEverVars[d] = v;
+  }
+}
+
+// mean :603-609 and mean update :623-624 (sequential over the μ selected)
+__global__ void __launch_bounds__(64) k_mean(int N, int mu, const double *__restrict__ X,
+                                             const unsigned *__restrict__ idx, const double *__restrict__ w,
+                                             double *mean, double *prevMean, double *meanUpdate,
+                                             const CmaesScalars *__restrict__ sc) {
+  const int d = blockIdx.x * 64 + threadIdx.x;
+  if (d >= N) return;
+  const double prev = mean[d];
+  double acc = 0.;
+  int i = 0;
+  for (; i + 8 <= mu; i += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = w[i + q] * X[(size_t)idx[i + q] * N + d];
+#pragma unroll
+    for (int q = 0; q < 8; q++) acc += v[q];
+  }
+  for (; i < mu; i++) acc += w[i] * X[(size_t)idx[i] * N + d];
+  prevMean[d] = prev;
+  mean[d] = acc;
+  meanUpdate[d] = (acc - prev) / sc->sigma;
+}
+
+// evolution paths :626-662 (+ the adaptC constants :693-694)
+__global__ void __launch_bounds__(1024) k_paths(int N, int diagonal, unsigned long long gen,
+                                                const double *__restrict__ B, const double *__restrict__ D,
+                                                const double *__restrict__ meanUpdate, double *auxBDZ, double *ps,
+                                                double *pc, CmaesScalars *sc) {
+  __shared__ int hs;
+  const int tid = threadIdx.x;
+  const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
+  for (int d = tid; d < N; d += blockDim.x) {
+    double sum = 0.0;
+    if (diagonal)
+      sum = meanUpdate[d];
+    else
+      for (int e = 0; e < N; ++e) sum += B[(size_t)e * N + d] * meanUpdate[e];
+    auxBDZ[d] = sum / D[d];
+  }
+  __syncthreads();
+  const double fac = sqrt(cs * (2. - cs) * effMu);
+  for (int d = tid; d < N; d += blockDim.x) {
+    double sum = 0.0;
+    if (diagonal)
+      sum = auxBDZ[d];
+    else
+      for (int e = 0; e < N; ++e) sum += B[(size_t)d * N + e] * auxBDZ[e];
+    ps[d] = (1. - cs) * ps[d] + fac * sum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double nrm = 0.0;
+    for (int d = 0; d < N; ++d) nrm += ps[d] * ps[d];  // std::pow(x, 2.0) == x*x (CR)
+    nrm = sqrt(nrm);
+    sc->psNorm = nrm;
+    const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+                                                 sc->chiSquareNumber);
+    hs = hsig;
+    sc->hsig = hsig;
+    const double a = N + 1.3, b = N + 2.0;
+    const double ccov1 = 2.0 / (a * a + effMu);
+    double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (b * b + effMu);
+    if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+    sc->ccov1 = ccov1;
+    sc->ccovmu = ccovmu;
+  }
+  __syncthreads();
+  const double fac2 = sqrt(cc * (2. - cc) * effMu);
+  for (int d = tid; d < N; d += blockDim.x) pc[d] = (1. - cc) * pc[d] + hs * fac2 * meanUpdate[d];
+}
+
+// adaptC :690-707, exact: one thread per lower-triangle element, the rank-μ
+// sum sequential over k exactly as the reference evaluates it.
+constexpr int AC_T = 16, AC_K = 64;
+__device__ inline void tri_tile(int t, int &td, int &te) {
+  int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) / 2.0);
+  while ((r + 1) * (r + 2) / 2 <= t) r++;
+  while (r * (r + 1) / 2 > t) r--;
+  td = r;
+  te = t - r * (r + 1) / 2;
+}
+
+__global__ void __launch_bounds__(256) k_adaptC_exact(int N, int mu, int diagonal, const double *__restrict__ X,
+                                                      const unsigned *__restrict__ idx, const double *__restrict__ w,
+                                                      const double *__restrict__ prevMean,
+                                                      const double *__restrict__ pc, double *C,
+                                                      const CmaesScalars *__restrict__ sc) {
+  __shared__ double Yd[AC_K][AC_T], Ye[AC_K][AC_T], cw[AC_K];
+  int td, te;
+  tri_tile(blockIdx.x, td, te);
+  const int tid = threadIdx.x, ty = tid / AC_T, tx = tid % AC_T;
+  const int d = td * AC_T + ty, e = te * AC_T + tx;
+  const bool active = (d < N && e < N && e <= d && (!diagonal || e == d));
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double sigmasquare = sc->sigma * sc->sigma;
+  double c = 0.0;
+  if (active) {
+    const double Cde = C[(size_t)d * N + e];
+    c = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  }
+  for (int k0 = 0; k0 < mu; k0 += AC_K) {
+    const int kn = (mu - k0) < AC_K ? (mu - k0) : AC_K;
+    for (int q = tid; q < AC_K * AC_T; q += 256) {
+      const int kk = q / AC_T, cidx = q % AC_T;
+      double yd = 0.0, ye = 0.0;
+      if (kk < kn) {
+        const size_t row = (size_t)idx[k0 + kk] * N;
+        const int dd = td * AC_T + cidx, ee = te * AC_T + cidx;
+        if (dd < N) yd = X[row + dd] - prevMean[dd];
+        if (ee < N) ye = X[row + ee] - prevMean[ee];
+      }
+      Yd[kk][cidx] = yd;
+      Ye[kk][cidx] = ye;
+    }
+    for (int q = tid; q < kn; q += 256) cw[q] = ccovmu * w[k0 + q];
+    __syncthreads();
+    if (active)
+      for (int kk = 0; kk < kn; kk++) c += cw[kk] * Yd[kk][ty] * Ye[kk][tx] / sigmasquare;
+    __syncthreads();
+  }
+  if (active) {
+    C[(size_t)d * N + e] = c;
+    if (e < d) C[(size_t)e * N + d] = c;
+  }
+}
+
+// adaptC with the rank-μ sum on the FP64 matrix cores: per 16x16 tile of C
+// and K-slice, D += Ŷᵀ Y with v_mfma_f64_16x16x4f64 (one wave per tile and
+// slice), Ŷ_k = (cμ w_k / σ²) y_k.  The base terms are added by
+// k_adaptC_combine in the reference's order.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(64) k_rankmu_mfma(int N, int mu, int kslices, const double *__restrict__ X,
+                                                    const unsigned *__restrict__ idx, const double *__restrict__ w,
+                                                    const double *__restrict__ prevMean,
+                                                    const CmaesScalars *__restrict__ sc, double *__restrict__ part) {
+  int td, te;
+  tri_tile(blockIdx.x, td, te);
+  const int slice = blockIdx.y;
+  const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
+  const int d = td * 16 + li, e = te * 16 + li;
+  const double pmd = d < N ? prevMean[d] : 0.0, pme = e < N ? prevMean[e] : 0.0;
+  const double scale = sc->ccovmu / (sc->sigma * sc->sigma);
+  const int per = ((mu + kslices - 1) / kslices + 3) & ~3;
+  const int kbeg = slice * per, kend = (kbeg + per) < mu ? (kbeg + per) : mu;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = kbeg; k0 < kend; k0 += 4) {
+    const int k = k0 + lk;
+    double a = 0.0, b = 0.0;
+    if (k < kend) {
+      const size_t row = (size_t)idx[k] * N;
+      const double sk = scale * w[k];
+      if (d < N) a = sk * (X[row + d] - pmd);
+      if (e < N) b = X[row + e] - pme;
+    }
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  // C/D layout: col = lane & 15, row = (lane >> 4) + 4 * r
+  const size_t tiles = gridDim.x;
+  double *out = part + ((size_t)slice * tiles + blockIdx.x) * 256;
+#pragma unroll
+  for (int r = 0; r < 4; r++) out[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+}
+
+__global__ void __launch_bounds__(256) k_adaptC_combine(int N, int kslices, int ntiles, int diagonal,
+                                                        const double *__restrict__ part,
+                                                        const double *__restrict__ pc, double *C,
+                                                        const CmaesScalars *__restrict__ sc) {
+  int td, te;
+  tri_tile(blockIdx.x, td, te);
+  const int tid = threadIdx.x, ty = tid / 16, tx = tid % 16;
+  const int d = td * 16 + ty, e = te * 16 + tx;
+  if (!(d < N && e < N && e <= d && (!diagonal || e == d))) return;
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double Cde = C[(size_t)d * N + e];
+  double c = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  double s = 0.0;
+  for (int sl = 0; sl < kslices; sl++) s += part[((size_t)sl * ntiles + blockIdx.x) * 256 + ty * 16 + tx];
+  c += s;
+  C[(size_t)d * N + e] = c;
+  if (e < d) C[(size_t)e * N + d] = c;
+}
+
+// adaptC diag extrema :709-717, updateSigma :720-761, numericalErrorTreatment
+// :763-772, min/max standard deviation :679-687
+__global__ void k_sigma(int N, int mu, int isSigmaBounded, const double *__restrict__ C,
+                        const double *__restrict__ F, const unsigned *__restrict__ idx,
+                        const double *__restrict__ minStdUpdate, CmaesScalars *sc) {
+  if (threadIdx.x != 0) return;
+  double maxd = C[0], mind = C[0];
+  for (int d = 1; d < N; ++d) {
+    const double v = C[(size_t)d * N + d];
+    if (maxd < v)
+      maxd = v;
+    else if (mind > v)
+      mind = v;
+  }
+  sc->maxDiagC = maxd;
+  sc->minDiagC = mind;
+  const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
+  double sigma = sc->sigma;
+  sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
+  if (mu > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
+  const double ub = sqrt(sc->trace / N);
+  if (sigma > ub && isSigmaBounded) sigma = ub;
+  for (int d = 0; d < N; ++d) {
+    const double cdd = C[(size_t)d * N + d];
+    if (sigma * sqrt(cdd) < minStdUpdate[d]) sigma = (minStdUpdate[d]) / sqrt(cdd) * exp_cr(0.05 + cs / ds);
+  }
+  sc->sigma = sigma;
+  double mn = INFINITY, mx = -INFINITY;
+  for (int i = 0; i < N; ++i) {
+    const double s = sigma * sqrt(C[(size_t)i * N + i]);
+    mn = fmin(mn, s);
+    mx = fmax(mx, s);
+  }
+  sc->currentMinStd = mn;
+  sc->currentMaxStd = mx;
+}
+
+__global__ void k_add_evals(CmaesScalars *sc, double n) {
+  if (threadIdx.x == 0) sc->modelEvaluationCount += n;
+}
+
+}  // namespace kg
+
+// ===================================================================== ABI
+using namespace kg;
+
+struct kg_cmaes_s {
+  kg_cmaes_cfg cfg;
+  int N = 0, lam = 0, mu = 0, R = 0;
+  bool finiteBounds = false;
+  hipStream_t stream = nullptr;
+  double *mean = nullptr, *prevMean = nullptr, *C = nullptr, *B = nullptr, *D = nullptr, *pc = nullptr,
+         *ps = nullptr, *w = nullptr, *X = nullptr, *Xall = nullptr, *BDZ = nullptr, *BDZall = nullptr,
+         *F = nullptr, *Z = nullptr, *bestEverVars = nullptr, *currBestVars = nullptr, *meanUpdate = nullptr,
+         *auxBDZ = nullptr;
+  double *lb = nullptr, *ub = nullptr, *iv = nullptr, *istd = nullptr, *minstd = nullptr;
+  unsigned *idx = nullptr;
+  double *sortKey = nullptr;
+  unsigned *sortVal = nullptr;
+  CmaesScalars *sc = nullptr;
+  double *eigA = nullptr, *eigH = nullptr, *covPart = nullptr;
+  int *infeas = nullptr, *assign = nullptr;
+  unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
+  int kslices = 8;
+  MtStream normal, uniform;
+  // profiling
+  bool profile = false;
+  std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> pending;
+  std::map<std::string, std::pair<double, size_t>> prof;
+};
+
+namespace {
+
+struct Stage {
+  kg_cmaes_s *h;
+  std::string name;
+  hipEvent_t a = nullptr, b = nullptr;
+  Stage(kg_cmaes_s *h_, const char *n) : h(h_), name(n) {
+    if (h->profile) {
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, h->stream);
+    }
+  }
+  ~Stage() {
+    if (h->profile) {
+      (void)hipEventRecord(b, h->stream);
+      h->pending.emplace_back(name, a, b);
+    }
+  }
+};
+
+template <typename T>
+int dalloc(T **p, size_t n) {
+  if (n == 0) n = 1;
+  KG_HIP(hipMalloc(p, n * sizeof(T)));
+  KG_HIP(hipMemset(*p, 0, n * sizeof(T)));
+  return 0;
+}
+
+void gsl_seed_state(uint64_t seed, unsigned char *out5000) {
+  uint64_t mt[624];
+  uint64_t s = seed & 0xffffffffULL;
+  if (s == 0) s = 4357;
+  mt[0] = s;
+  for (int i = 1; i < 624; i++) mt[i] = (1812433253ULL * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint64_t)i) & 0xffffffffULL;
+  memset(out5000, 0, 5000);
+  memcpy(out5000, mt, sizeof(mt));
+  int32_t mti = 624;
+  memcpy(out5000 + 624 * 8, &mti, 4);
+}
+
+int check_errors(kg_cmaes_s *h) {
+  unsigned int e = 0, e1 = 0, e2 = 0;
+  KG_HIP(hipMemcpy(&e, &h->sc->errors, sizeof(e), hipMemcpyDeviceToHost));
+  KG_HIP(hipMemcpy(&e1, &h->normal.state()->errors, sizeof(e1), hipMemcpyDeviceToHost));
+  KG_HIP(hipMemcpy(&e2, &h->uniform.state()->errors, sizeof(e2), hipMemcpyDeviceToHost));
+  e |= e1 | e2;
+  if (e == 0) return 0;
+  std::string m = "korali_amd CMA-ES device error:";
+  if (e & KG_ERR_NONFINITE_F) m += " Non finite value of function evaluation detected.";
+  if (e & KG_ERR_RNG_UNDERRUN) m += " RNG stream underrun.";
+  if (e & KG_ERR_RESAMPLE_RESERVE) m += " Infeasible samples exceeded the device resampling reserve.";
+  if (e & KG_ERR_ZERO_LIST) m += " Too many zero mt19937 words pending.";
+  if (e & KG_ERR_EIGEN) m += " Eigen decomposition did not converge.";
+  set_error(m);
+  return 1;
+}
+
+struct FieldRef {
+  double *dev;
+  size_t n;
+};
+
+bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
+  const size_t N = h->N, L = h->lam;
+#define VEC(key, ptr, n) \
+  if (k == key) {        \
+    r = {ptr, n};        \
+    return true;         \
+  }
+  VEC("Current Mean", h->mean, N)
+  VEC("Previous Mean", h->prevMean, N)
+  VEC("Covariance Matrix", h->C, N * N)
+  VEC("Covariance Eigenvector Matrix", h->B, N * N)
+  VEC("Axis Lengths", h->D, N)
+  VEC("Evolution Path", h->pc, N)
+  VEC("Conjugate Evolution Path", h->ps, N)
+  VEC("Mu Weights", h->w, (size_t)h->mu)
+  VEC("Sample Population", h->X, L * N)
+  VEC("Value Vector", h->F, L)
+  VEC("Best Ever Variables", h->bestEverVars, N)
+  VEC("Current Best Variables", h->currBestVars, N)
+  VEC("Mean Update", h->meanUpdate, N)
+  VEC("Auxiliar BDZ Matrix", h->auxBDZ, N)
+  VEC("Lower Bound", h->lb, N)
+  VEC("Upper Bound", h->ub, N)
+  VEC("Initial Value", h->iv, N)
+  VEC("Initial Standard Deviation", h->istd, N)
+  VEC("Minimum Standard Deviation Update", h->minstd, N)
+  if (h->BDZ) VEC("BDZ Matrix", h->BDZ, L * N)
+#define SCA(key, fld) VEC(key, &h->sc->fld, 1)
+  SCA("Sigma", sigma)
+  SCA("Trace", trace)
+  SCA("Effective Mu", effectiveMu)
+  SCA("Cumulative Covariance", cumulativeCovariance)
+  SCA("Sigma Cumulation Factor", sigmaCumulationFactor)
+  SCA("Damp Factor", dampFactor)
+  SCA("Chi Square Number", chiSquareNumber)
+  SCA("Conjugate Evolution Path L2 Norm", psNorm)
+  SCA("Best Ever Value", bestEverValue)
+  SCA("Previous Best Ever Value", previousBestEverValue)
+  SCA("Previous Best Value", previousBestValue)
+  SCA("Current Best Value", currentBestValue)
+  SCA("Current Min Standard Deviation", currentMinStd)
+  SCA("Current Max Standard Deviation", currentMaxStd)
+  SCA("Maximum Diagonal Covariance Matrix Element", maxDiagC)
+  SCA("Minimum Diagonal Covariance Matrix Element", minDiagC)
+  SCA("Minimum Covariance Eigenvalue", minEig)
+  SCA("Maximum Covariance Eigenvalue", maxEig)
+  SCA("Infeasible Sample Count", infeasibleSampleCount)
+  SCA("Best Valid Sample", bestValidSample)
+  SCA("Model Evaluation Count", modelEvaluationCount)
+  SCA("Hsig", hsig)
+  SCA("Eigen Failures", eigenFailures)
+#undef SCA
+#undef VEC
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
+  KG_CHECK(cfg && out, "kg_cmaes_create: null argument");
+  KG_CHECK(cfg->variable_count >= 1, "'Variable Count' must be >= 1");
+  KG_CHECK(cfg->population_size > 1, "'Population Size' must be larger 1.");  // CMAES.cpp.base:26
+  KG_CHECK(!cfg->mirrored_sampling, "Mirrored Sampling is not supported by the device path yet");
+  KG_CHECK(cfg->variable_count <= 960, "device path supports up to 960 variables");
+  KG_CHECK(cfg->mu_type >= 0 && cfg->mu_type <= 3,
+           "Invalid setting of Mu Type (Linear, Equal, Logarithmic, or Proportional accepted).");
+  KG_HIP(hipSetDevice(cfg->device));
+  upload_dd_tables();
+  auto *h = new kg_cmaes_s();
+  h->cfg = *cfg;
+  const int N = (int)cfg->variable_count, L = (int)cfg->population_size;
+  h->N = N;
+  h->lam = L;
+  h->mu = (int)(cfg->mu_value ? cfg->mu_value : cfg->population_size / 2);
+  KG_CHECK(h->mu >= 1 && h->mu <= L, "'Mu Value' must be in [1, Population Size]");
+  std::vector<double> lb(N, -INFINITY), ub(N, INFINITY), iv(N, NAN), istd(N, NAN), minstd(N, 0.0);
+  for (int i = 0; i < N; i++) {
+    if (cfg->lower_bound) lb[i] = cfg->lower_bound[i];
+    if (cfg->upper_bound) ub[i] = cfg->upper_bound[i];
+    if (cfg->initial_value) iv[i] = cfg->initial_value[i];
+    if (cfg->initial_std) istd[i] = cfg->initial_std[i];
+    if (cfg->min_std_update) minstd[i] = cfg->min_std_update[i];
+    if (std::isfinite(lb[i]) || std::isfinite(ub[i])) h->finiteBounds = true;
+    // CMAES.cpp.base:111-126
+    if (!std::isfinite(iv[i])) {
+      if (!std::isfinite(lb[i]) || !std::isfinite(ub[i])) {
+        set_error("'Initial Value' of variable " + std::to_string(i) +
+                  " not defined, and cannot be inferred because variable bounds are not finite.");
+        delete h;
+        return 1;
+      }
+      iv[i] = (ub[i] + lb[i]) * 0.5;
+    }
+    if (!std::isfinite(istd[i])) {
+      if (!std::isfinite(lb[i]) || !std::isfinite(ub[i])) {
+        set_error("Initial Standard Deviation of variable " + std::to_string(i) +
+                  " not defined, and cannot be inferred because variable bounds are not finite.");
+        delete h;
+        return 1;
+      }
+      istd[i] = (ub[i] - lb[i]) * 0.3;
+    }
+  }
+  h->R = h->finiteBounds ? std::max(64, L / 4) : 0;
+  const size_t rows = (size_t)L + h->R;
+  int rc = 0;
+  rc |= dalloc(&h->mean, N) | dalloc(&h->prevMean, N) | dalloc(&h->C, (size_t)N * N) | dalloc(&h->B, (size_t)N * N);
+  rc |= dalloc(&h->D, N) | dalloc(&h->pc, N) | dalloc(&h->ps, N) | dalloc(&h->w, h->mu);
+  rc |= dalloc(&h->X, (size_t)L * N) | dalloc(&h->F, L) | dalloc(&h->Z, rows * N);
+  rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
+  rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
+  rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1) | dalloc(&h->eigA, (size_t)N * (N + 1)) | dalloc(&h->eigH, (size_t)N * N);
+  rc |= dalloc(&h->infeas, rows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
+  if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
+  if (h->R) {
+    rc |= dalloc(&h->Xall, rows * N);
+    if (cfg->store_bdz) rc |= dalloc(&h->BDZall, rows * N);
+  }
+  size_t P2 = 1;
+  while (P2 < (size_t)L) P2 <<= 1;
+  if (P2 < SORT_CHUNK) P2 = SORT_CHUNK;
+  rc |= dalloc(&h->sortKey, P2) | dalloc(&h->sortVal, P2);
+  const int nt = (N + 15) / 16;
+  rc |= dalloc(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
+  if (rc) {
+    delete h;
+    return 1;
+  }
+  KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  KG_HIP(hipMemcpy(h->lb, lb.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->ub, ub.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->iv, iv.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->istd, istd.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->minstd, minstd.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  const size_t words = h->normal.words_for_normals(rows * N);
+  if (h->normal.init(2 * words) || h->uniform.init(1 << 16)) {
+    delete h;
+    return 1;
+  }
+  unsigned char st[5000];
+  gsl_seed_state(cfg->normal_seed, st);
+  if (h->normal.import_gsl(st, h->stream)) return 1;
+  gsl_seed_state(cfg->uniform_seed, st);
+  if (h->uniform.import_gsl(st, h->stream)) return 1;
+  *out = h;
+  return 0;
+}
+
+int kg_cmaes_destroy(kg_cmaes_t h) {
+  if (!h) return 0;
+  (void)hipStreamSynchronize(h->stream);
+  for (void *p : {(void *)h->mean, (void *)h->prevMean, (void *)h->C, (void *)h->B, (void *)h->D, (void *)h->pc,
+                  (void *)h->ps, (void *)h->w, (void *)h->X, (void *)h->Xall, (void *)h->BDZ, (void *)h->BDZall,
+                  (void *)h->F, (void *)h->Z, (void *)h->bestEverVars, (void *)h->currBestVars,
+                  (void *)h->meanUpdate, (void *)h->auxBDZ, (void *)h->lb, (void *)h->ub, (void *)h->iv,
+                  (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
+                  (void *)h->sc, (void *)h->eigA, (void *)h->eigH, (void *)h->covPart, (void *)h->infeas,
+                  (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks})
+    if (p) (void)hipFree(p);
+  for (auto &t : h->pending) {
+    (void)hipEventDestroy(std::get<1>(t));
+    (void)hipEventDestroy(std::get<2>(t));
+  }
+  (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int kg_cmaes_initialize(kg_cmaes_t h) {
+  Stage st(h, "init");
+  hipLaunchKernelGGL(k_init, dim3(1), dim3(256), 0, h->stream, h->N, h->lam, h->mu, h->cfg.mu_type,
+                     h->cfg.initial_sigma_cumulation_factor, h->cfg.initial_damp_factor,
+                     h->cfg.initial_cumulative_covariance, h->iv, h->istd, h->w, h->C, h->B, h->D, h->mean,
+                     h->prevMean, h->pc, h->ps, h->sc);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+static int cmaes_eigen(kg_cmaes_t h) {
+  Stage st(h, "eigen");
+  return launch_symmv(h->N, h->cfg.diagonal_covariance, h->C, h->eigA, h->eigH, h->B, h->D, &h->sc->minEig,
+                      &h->sc->maxEig, &h->sc->eigenFailures, &h->sc->errors, h->stream);
+}
+
+int kg_cmaes_sample(kg_cmaes_t h) {
+  const int N = h->N, L = h->lam;
+  const size_t rows = (size_t)L + h->R;
+  if (cmaes_eigen(h)) return 1;
+  {
+    Stage st(h, "rng_polar");
+    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->stream)) return 1;
+  }
+  {
+    Stage st(h, "transform");
+    KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
+    const int nbn = (N + TR_BN - 1) / TR_BN;
+    const int nbm = (int)((rows + TR_BM - 1) / TR_BM);
+    hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)rows,
+                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub,
+                       h->R ? h->Xall : h->X, h->R ? h->BDZall : h->BDZ, h->infeas);
+    KG_HIP(hipGetLastError());
+    if (h->R) {
+      hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
+                         h->infeas, h->assign, h->usedBlocks, h->sc);
+      const size_t tot = (size_t)L * N;
+      hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, L, h->assign,
+                         h->Xall, h->X, h->BDZall, h->BDZ);
+    } else {
+      hipLaunchKernelGGL(k_count_infeasible, dim3(1), dim3(64), 0, h->stream, L, h->infeas, h->sc, h->usedBlocks);
+    }
+    KG_HIP(hipGetLastError());
+  }
+  {
+    Stage st(h, "rng_consume");
+    if (h->normal.consume_normals_dev(h->usedBlocks, N, h->blockEnd, h->stream)) return 1;
+  }
+  return 0;
+}
+
+int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective) {
+  KG_CHECK(objective >= 0 && objective <= 2, "unknown builtin objective");
+  Stage st(h, "objective");
+  hipLaunchKernelGGL(k_objective, dim3((h->lam + 63) / 64), dim3(64), 0, h->stream, h->N, h->lam, objective, h->X,
+                     h->F, h->sc);
+  hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int kg_cmaes_get_candidates(kg_cmaes_t h, double *X, size_t ld) {
+  const size_t N = h->N;
+  if (ld == 0) ld = N;
+  KG_HIP(hipMemcpy2DAsync(X, ld * sizeof(double), h->X, N * sizeof(double), N * sizeof(double), h->lam,
+                          hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F) {
+  for (int i = 0; i < h->lam; i++)
+    KG_CHECK(std::isfinite(F[i]), "Non finite value of function evaluation detected: " + std::to_string(F[i]));
+  KG_HIP(hipMemcpyAsync(h->F, F, h->lam * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
+  const int N = h->N, L = h->lam, mu = h->mu;
+  {
+    Stage st(h, "sort");
+    int P2 = 1;
+    while (P2 < L) P2 <<= 1;
+    if (P2 <= SORT_CHUNK) {
+      hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, h->stream, L, P2, h->F, h->idx);
+    } else {
+      hipLaunchKernelGGL(k_sort_init, dim3((P2 + 1023) / 1024), dim3(1024), 0, h->stream, L, P2, h->F, h->sortKey,
+                         h->sortVal);
+      hipLaunchKernelGGL(k_sort_local, dim3(P2 / SORT_CHUNK), dim3(1024), 0, h->stream, P2, 0, h->sortKey,
+                         h->sortVal);
+      for (int k = 2 * SORT_CHUNK; k <= P2; k <<= 1) {
+        for (int j = k / 2; j >= SORT_CHUNK; j >>= 1)
+          hipLaunchKernelGGL(k_sort_global, dim3((P2 + 255) / 256), dim3(256), 0, h->stream, P2, k, j, h->sortKey,
+                             h->sortVal);
+        hipLaunchKernelGGL(k_sort_local, dim3(P2 / SORT_CHUNK), dim3(1024), 0, h->stream, P2, k, h->sortKey,
+                           h->sortVal);
+      }
+      hipLaunchKernelGGL(k_copy_idx, dim3((L + 255) / 256), dim3(256), 0, h->stream, L, h->sortVal, h->idx);
+    }
+    KG_HIP(hipGetLastError());
+  }
+  {
+    Stage st(h, "mean_paths");
+    hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
+                       (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
+                       h->sc);
+    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->X, h->idx, h->w, h->mean,
+                       h->prevMean, h->meanUpdate, h->sc);
+    hipLaunchKernelGGL(k_paths, dim3(1), dim3(1024), 0, h->stream, N, h->cfg.diagonal_covariance,
+                       (unsigned long long)generation, h->B, h->D, h->meanUpdate, h->auxBDZ, h->ps, h->pc, h->sc);
+    KG_HIP(hipGetLastError());
+  }
+  {
+    Stage st(h, "covariance");
+    const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
+    if (h->cfg.cov_mode == KG_COV_MFMA) {
+      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->X,
+                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
+      hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
+                         h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc);
+    } else {
+      hipLaunchKernelGGL(k_adaptC_exact, dim3(ntiles), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
+                         h->X, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
+    }
+    KG_HIP(hipGetLastError());
+  }
+  {
+    Stage st(h, "sigma");
+    hipLaunchKernelGGL(k_sigma, dim3(1), dim3(64), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
+                       h->minstd, h->sc);
+    KG_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
+  if (generation == 1 && kg_cmaes_initialize(h)) return 1;
+  if (kg_cmaes_sample(h)) return 1;
+  if (kg_cmaes_eval_builtin(h, objective)) return 1;
+  return kg_cmaes_update(h, generation);
+}
+
+int kg_cmaes_synchronize(kg_cmaes_t h) {
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return check_errors(h);
+}
+
+int kg_cmaes_field_size(kg_cmaes_t h, const char *name, size_t *n) {
+  FieldRef r;
+  KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
+  *n = r.n;
+  return 0;
+}
+
+int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n) {
+  FieldRef r;
+  KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
+  KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
+  KG_HIP(hipMemcpyAsync(out, r.dev, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t n) {
+  FieldRef r;
+  KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
+  KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
+  KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_cmaes_get_sorting_index(kg_cmaes_t h, uint64_t *out) {
+  std::vector<unsigned> t(h->lam);
+  KG_HIP(hipMemcpyAsync(t.data(), h->idx, h->lam * sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  for (int i = 0; i < h->lam; i++) out[i] = t[i];
+  return 0;
+}
+
+int kg_cmaes_get_rng(kg_cmaes_t h, int which, void *state5000) {
+  KG_CHECK(which == 0 || which == 1, "rng index must be 0 (Normal) or 1 (Uniform)");
+  return (which == 0 ? h->normal : h->uniform).export_gsl(state5000, h->stream);
+}
+
+int kg_cmaes_set_rng(kg_cmaes_t h, int which, const void *state5000) {
+  KG_CHECK(which == 0 || which == 1, "rng index must be 0 (Normal) or 1 (Uniform)");
+  return (which == 0 ? h->normal : h->uniform).import_gsl(state5000, h->stream);
+}
+
+int kg_cmaes_device_ptr(kg_cmaes_t h, const char *name, void **ptr) {
+  FieldRef r;
+  KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
+  *ptr = r.dev;
+  return 0;
+}
+
+int kg_cmaes_stream(kg_cmaes_t h, void **stream) {
+  *stream = (void *)h->stream;
+  return 0;
+}
+
+int kg_cmaes_profile(kg_cmaes_t h, int enable) {
+  h->profile = enable != 0;
+  return 0;
+}
+
+int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, size_t *count) {
+  KG_HIP(hipStreamSynchronize(h->stream));
+  for (auto &t : h->pending) {
+    float ms = 0.f;
+    KG_HIP(hipEventElapsedTime(&ms, std::get<1>(t), std::get<2>(t)));
+    auto &p = h->prof[std::get<0>(t)];
+    p.first += ms;
+    p.second += 1;
+    (void)hipEventDestroy(std::get<1>(t));
+    (void)hipEventDestroy(std::get<2>(t));
+  }
+  h->pending.clear();
+  auto it = h->prof.find(stage);
+  if (it == h->prof.end()) {
+    *ms_total = 0;
+    *count = 0;
+  } else {
+    *ms_total = it->second.first;
+    *count = it->second.second;
+    h->prof.erase(it);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,47 @@
+// kg_common.hip — error plumbing, double-double constant tables, ABI info.
+#include <cmath>
+#include <mutex>
+
+#include "../../include/korali_amd.h"
+#include "kg_common.hpp"
+
+namespace kg {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error() { return g_last_error.c_str(); }
+
+__constant__ dd_tables c_dd_tab;
+
+// 1/q as an (unevaluated) double-double: hi = fl(1/q), lo = fl((1 - hi*q)/q)
+// with the residual 1 - hi*q exact via fma.
+static void dd_recip(double q, double &hi, double &lo) {
+  hi = 1.0 / q;
+  const double r = -std::fma(hi, q, -1.0);
+  lo = r / q;
+}
+
+void upload_dd_tables() {
+  static std::once_flag once;
+  static bool ok = false;
+  std::call_once(once, [] {
+    dd_tables t;
+    for (int j = 0; j < 22; j++) dd_recip(2.0 * j + 1.0, t.inv_odd_hi[j], t.inv_odd_lo[j]);
+    t.inv_int_hi[0] = t.inv_int_lo[0] = 0.0;
+    for (int j = 1; j < 15; j++) dd_recip((double)j, t.inv_int_hi[j], t.inv_int_lo[j]);
+    ok = hipMemcpyToSymbol(HIP_SYMBOL(c_dd_tab), &t, sizeof(t)) == hipSuccess;
+  });
+  (void)ok;
+}
+
+}  // namespace kg
+
+extern "C" {
+const char *kg_last_error(void) { return kg::last_error(); }
+int kg_abi_version(void) { return KG_ABI_VERSION; }
+int kg_device_count(int *count) {
+  KG_HIP(hipGetDeviceCount(count));
+  return 0;
+}
+}

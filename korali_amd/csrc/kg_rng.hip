@@ -1,0 +1,401 @@
+// kg_rng.hip — device GSL mt19937 stream: producer, polar normals, uniforms.
+// Semantics: GSL 2.6 rng/mt.c + randist/gauss.c (polar), as called by
+// Korali's Normal/Uniform distributions (univariate/normal/normal.cpp.base:
+// 32-35, univariate/uniform/uniform.cpp.base:30-36).
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "kg_rng.hpp"
+
+namespace kg {
+
+namespace {
+
+constexpr int POLAR_TPB = 256;     // threads per block
+constexpr int POLAR_APT = 8;       // attempts per thread
+constexpr int POLAR_APB = POLAR_TPB * POLAR_APT;
+
+// the stream position and zero-word list, read once per thread (the zero
+// list itself stays in global memory: it is empty except once per ~4e9 words)
+struct PosView {
+  unsigned long long pos;
+  unsigned int nzero;
+  const unsigned long long *zeros;
+};
+
+__device__ inline PosView pos_view(const StreamState *st) {
+  return {st->pos, st->nzero < KG_MAX_ZERO_WORDS ? st->nzero : KG_MAX_ZERO_WORDS, st->zeros};
+}
+
+__device__ inline unsigned long long compact_to_abs(const PosView &st, unsigned long long c) {
+  // absolute index of the c-th non-zero word at/after pos
+  unsigned long long j = st.pos + c;
+  if (st.nzero == 0) return j;
+  for (;;) {
+    unsigned int k = 0;
+    for (unsigned int i = 0; i < st.nzero; i++)
+      if (st.zeros[i] >= st.pos && st.zeros[i] <= j) k++;
+    const unsigned long long jn = st.pos + c + k;
+    if (jn == j) return j;
+    j = jn;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_mt_produce(uint32_t *__restrict__ ring, unsigned long long R, StreamState *st,
+                                                   unsigned long long ahead) {
+  __shared__ uint32_t L[1024];
+  const int lane = threadIdx.x;
+  const unsigned long long hi0 = st->hi;
+  unsigned long long target = st->pos + ahead;
+  const unsigned long long cap = st->lo + R;
+  if (target > cap) {
+    if (lane == 0) atomicOr(&st->errors, KG_ERR_RNG_UNDERRUN);
+    target = cap;
+  }
+  if (hi0 >= target) return;
+  for (int i = lane; i < MT_N; i += 64) {
+    const unsigned long long j = hi0 - MT_N + i;
+    L[j & 1023] = ring[j & (R - 1)];
+  }
+  __syncthreads();
+  for (unsigned long long c = hi0; c < target; c += 227) {
+    const int cnt = (int)((target - c) < 227 ? (target - c) : 227);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int idx = lane + 64 * q;
+      if (idx < cnt) {
+        const unsigned long long j = c + idx;
+        const uint32_t s = mt_next(L[(j - 624) & 1023], L[(j - 623) & 1023], L[(j - 227) & 1023]);
+        L[j & 1023] = s;
+        ring[j & (R - 1)] = s;
+        if (s == 0u) {  // tempered word is zero iff untempered is (bijection)
+          const unsigned int z = atomicAdd(&st->nzero, 1u);
+          if (z < KG_MAX_ZERO_WORDS)
+            st->zeros[z] = j;
+          else
+            atomicOr(&st->errors, KG_ERR_ZERO_LIST);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0) st->hi = target;
+}
+
+__device__ inline bool polar_pair(const uint32_t *__restrict__ ring, unsigned long long R, const PosView &st,
+                                  unsigned long long a, double &y, double &r2) {
+  const unsigned long long j0 = compact_to_abs(st, 2 * a), j1 = compact_to_abs(st, 2 * a + 1);
+  const uint32_t w0 = mt_temper(ring[j0 & (R - 1)]), w1 = mt_temper(ring[j1 & (R - 1)]);
+  const double u0 = w0 / 4294967296.0, u1 = w1 / 4294967296.0;
+  const double x = -1 + 2 * u0;
+  y = -1 + 2 * u1;
+  r2 = x * x + y * y;
+  return !(r2 > 1.0 || r2 == 0);
+}
+
+__global__ void __launch_bounds__(POLAR_TPB) k_polar_count(const uint32_t *__restrict__ ring, unsigned long long R,
+                                                          const StreamState *__restrict__ stp, unsigned long long A,
+                                                          unsigned int *__restrict__ counts) {
+  __shared__ unsigned int wsum[POLAR_TPB / 64];
+  const PosView st = pos_view(stp);
+  const unsigned long long base = (unsigned long long)blockIdx.x * POLAR_APB + threadIdx.x * POLAR_APT;
+  unsigned int c = 0;
+#pragma unroll
+  for (int q = 0; q < POLAR_APT; q++) {
+    const unsigned long long a = base + q;
+    double y, r2;
+    if (a < A && polar_pair(ring, R, st, a, y, r2)) c++;
+  }
+  // block reduction
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int t = 0;
+    for (int w = 0; w < POLAR_TPB / 64; w++) t += wsum[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of nb block counts (single block); offsets[nb] = total
+__global__ void __launch_bounds__(1024) k_scan_counts(const unsigned int *__restrict__ counts, unsigned long long *__restrict__ offsets,
+                                                      int nb, StreamState *st) {
+  __shared__ unsigned long long wtot[16];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + threadIdx.x;
+    unsigned long long v = (i < nb) ? counts[i] : 0;
+    // inclusive wave scan
+    unsigned long long x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      unsigned long long t = __shfl_up(x, off, 64);
+      if (lane >= off) x += t;
+    }
+    if (lane == 63) wtot[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long acc = 0;
+      for (int w = 0; w < 16; w++) {
+        unsigned long long t = wtot[w];
+        wtot[w] = acc;
+        acc += t;
+      }
+    }
+    __syncthreads();
+    const unsigned long long excl = carry + wtot[wid] + x - v;
+    if (i < nb) offsets[i] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = excl + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    offsets[nb] = carry;
+    st->total_normals = carry;
+  }
+}
+
+__global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__restrict__ ring, unsigned long long R,
+                                                            StreamState *__restrict__ stp, unsigned long long A,
+                                                            const unsigned long long *__restrict__ offsets,
+                                                            double *__restrict__ z, unsigned long long M,
+                                                            unsigned long long block_len,
+                                                            unsigned long long *__restrict__ block_end) {
+  __shared__ unsigned int woff[POLAR_TPB / 64];
+  const PosView st = pos_view(stp);
+  const unsigned long long base = (unsigned long long)blockIdx.x * POLAR_APB + threadIdx.x * POLAR_APT;
+  double yv[POLAR_APT], rv[POLAR_APT];
+  unsigned int acc = 0, mask = 0;
+#pragma unroll
+  for (int q = 0; q < POLAR_APT; q++) {
+    const unsigned long long a = base + q;
+    if (a < A && polar_pair(ring, R, st, a, yv[q], rv[q])) {
+      mask |= 1u << q;
+      acc++;
+    }
+  }
+  // exclusive scan of per-thread counts across the block
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned int x = acc;
+  for (int off = 1; off < 64; off <<= 1) {
+    unsigned int t = __shfl_up(x, off, 64);
+    if (lane >= off) x += t;
+  }
+  if (lane == 63) woff[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int s = 0;
+    for (int w = 0; w < POLAR_TPB / 64; w++) {
+      unsigned int t = woff[w];
+      woff[w] = s;
+      s += t;
+    }
+  }
+  __syncthreads();
+  unsigned long long k = offsets[blockIdx.x] + woff[wid] + (x - acc);
+#pragma unroll
+  for (int q = 0; q < POLAR_APT; q++) {
+    if (mask & (1u << q)) {
+      if (k < M) {
+        // gsl_ran_gaussian: sigma * y * sqrt(-2 log(r2) / r2); Normal adds mean 0
+        const double r2 = rv[q];
+        const double g = 1.0 * yv[q] * sqrt(-2.0 * log_cr(r2) / r2);
+        z[k] = 0.0 + g;
+        if (block_end && ((k + 1) % block_len) == 0) block_end[(k + 1) / block_len - 1] = base + q;
+        if (k == M - 1) stp->last_attempt = base + q;
+      }
+      k++;
+    }
+  }
+}
+
+// advance the stream by the words behind `attempts` polar attempts
+__global__ void k_consume(StreamState *st, unsigned long long normals_used, unsigned long long block_len,
+                          const unsigned long long *block_end, int use_block_end,
+                          const unsigned long long *used_blocks_dev) {
+  if (threadIdx.x != 0) return;
+  if (used_blocks_dev) normals_used = (*used_blocks_dev) * block_len;
+  if (normals_used == 0) return;
+  if (st->total_normals < normals_used) {
+    st->errors |= KG_ERR_RNG_UNDERRUN;
+    return;
+  }
+  const unsigned long long last = use_block_end ? block_end[normals_used / block_len - 1] : st->last_attempt;
+  const unsigned long long words = 2 * (last + 1);
+  const unsigned long long p = compact_to_abs(pos_view(st), words - 1) + 1;
+  if (p > st->hi) st->errors |= KG_ERR_RNG_UNDERRUN;
+  st->pos = p;
+  st->lo = 624ULL * ((p - 1) / 624ULL);
+  // drop zero records that are behind the new position
+  unsigned int w = 0;
+  for (unsigned int i = 0; i < st->nzero && i < KG_MAX_ZERO_WORDS; i++)
+    if (st->zeros[i] >= p) st->zeros[w++] = st->zeros[i];
+  st->nzero = w;
+}
+
+__global__ void k_uniforms(const uint32_t *__restrict__ ring, unsigned long long R, const StreamState *__restrict__ stp,
+                           double *__restrict__ u, unsigned long long M) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const unsigned long long j = stp->pos + i;
+  u[i] = mt_temper(ring[j & (R - 1)]) / 4294967296.0;
+}
+
+__global__ void k_consume_words(StreamState *st, unsigned long long words) {
+  if (threadIdx.x != 0 || words == 0) return;
+  const unsigned long long p = st->pos + words;
+  if (p > st->hi) st->errors |= KG_ERR_RNG_UNDERRUN;
+  st->pos = p;
+  st->lo = 624ULL * ((p - 1) / 624ULL);
+  unsigned int w = 0;
+  for (unsigned int i = 0; i < st->nzero && i < KG_MAX_ZERO_WORDS; i++)
+    if (st->zeros[i] >= p) st->zeros[w++] = st->zeros[i];
+  st->nzero = w;
+}
+
+unsigned long long next_pow2(unsigned long long x) {
+  unsigned long long r = 1;
+  while (r < x) r <<= 1;
+  return r;
+}
+
+}  // namespace
+
+MtStream::~MtStream() {
+  if (ring_) (void)hipFree(ring_);
+  if (st_) (void)hipFree(st_);
+  if (counts_) (void)hipFree(counts_);
+  if (offsets_) (void)hipFree(offsets_);
+}
+
+int MtStream::init(size_t capacity_words) {
+  R_ = next_pow2(capacity_words + 2 * MT_N + 4096);
+  KG_HIP(hipMalloc(&ring_, R_ * sizeof(uint32_t)));
+  KG_HIP(hipMalloc(&st_, sizeof(StreamState)));
+  KG_HIP(hipMemset(st_, 0, sizeof(StreamState)));
+  return 0;
+}
+
+int MtStream::ensure_scratch(size_t nb) {
+  if (nb <= scratch_blocks_) return 0;
+  if (counts_) KG_HIP(hipFree(counts_));
+  if (offsets_) KG_HIP(hipFree(offsets_));
+  KG_HIP(hipMalloc(&counts_, nb * sizeof(unsigned int)));
+  KG_HIP(hipMalloc(&offsets_, (nb + 1) * sizeof(unsigned long long)));
+  scratch_blocks_ = nb;
+  return 0;
+}
+
+int MtStream::import_gsl(const void *state5000, hipStream_t s) {
+  const unsigned char *b = (const unsigned char *)state5000;
+  std::vector<uint32_t> w(MT_N);
+  for (int i = 0; i < MT_N; i++) {
+    uint64_t v;
+    memcpy(&v, b + 8 * i, 8);
+    w[i] = (uint32_t)(v & 0xffffffffULL);
+  }
+  int32_t mti;
+  memcpy(&mti, b + 8 * MT_N, 4);
+  KG_CHECK(mti >= 0 && mti <= MT_N, "invalid mt19937 state (mti out of range)");
+  StreamState h;
+  memset(&h, 0, sizeof(h));
+  h.lo = 0;
+  h.pos = (unsigned long long)mti;
+  h.hi = MT_N;
+  for (int i = mti; i < MT_N; i++)
+    if (w[i] == 0 && h.nzero < KG_MAX_ZERO_WORDS) h.zeros[h.nzero++] = (unsigned long long)i;
+  KG_HIP(hipMemcpyAsync(ring_, w.data(), MT_N * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  KG_HIP(hipMemcpyAsync(st_, &h, sizeof(h), hipMemcpyHostToDevice, s));
+  KG_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int MtStream::produce(unsigned long long ahead, hipStream_t s) {
+  hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(64), 0, s, ring_, R_, st_, ahead);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::export_gsl(void *state5000, hipStream_t s) {
+  // the whole current block must exist
+  StreamState h;
+  KG_HIP(hipMemcpyAsync(&h, st_, sizeof(h), hipMemcpyDeviceToHost, s));
+  KG_HIP(hipStreamSynchronize(s));
+  if (h.hi < h.lo + MT_N) {
+    if (produce(h.lo + MT_N - h.pos, s)) return 1;
+    KG_HIP(hipMemcpyAsync(&h, st_, sizeof(h), hipMemcpyDeviceToHost, s));
+    KG_HIP(hipStreamSynchronize(s));
+  }
+  std::vector<uint32_t> w(MT_N);
+  const unsigned long long off = h.lo & (R_ - 1);
+  if (off + MT_N <= R_) {
+    KG_HIP(hipMemcpyAsync(w.data(), ring_ + off, MT_N * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  } else {
+    const size_t first = R_ - off;
+    KG_HIP(hipMemcpyAsync(w.data(), ring_ + off, first * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    KG_HIP(hipMemcpyAsync(w.data() + first, ring_, (MT_N - first) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  KG_HIP(hipStreamSynchronize(s));
+  unsigned char *b = (unsigned char *)state5000;
+  memset(b, 0, 5000);
+  for (int i = 0; i < MT_N; i++) {
+    uint64_t v = w[i];
+    memcpy(b + 8 * i, &v, 8);
+  }
+  int32_t mti = (int32_t)(h.pos - h.lo);
+  memcpy(b + 8 * MT_N, &mti, 4);
+  return 0;
+}
+
+size_t MtStream::words_for_normals(size_t M) const {
+  // attempts ~ M / (pi/4); 12 sigma margin of the geometric sum
+  const double A = (double)M * 1.2732395447351628 + 12.0 * std::sqrt((double)M * 0.3484) + 64.0;
+  return (size_t)(2.0 * A) + 64;
+}
+
+int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s) {
+  const unsigned long long words = words_for_normals(M);
+  const unsigned long long A = words / 2;
+  const size_t nb = (size_t)((A + POLAR_APB - 1) / POLAR_APB);
+  if (ensure_scratch(nb)) return 1;
+  if (produce(words + 2 * KG_MAX_ZERO_WORDS, s)) return 1;
+  hipLaunchKernelGGL(k_polar_count, dim3(nb), dim3(POLAR_TPB), 0, s, ring_, R_, st_, A, counts_);
+  KG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, counts_, offsets_, (int)nb, st_);
+  KG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_polar_scatter, dim3(nb), dim3(POLAR_TPB), 0, s, ring_, R_, st_, A, offsets_, z,
+                     (unsigned long long)M, (unsigned long long)(block_len ? block_len : 1), block_end);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::consume_normals(size_t used, size_t block_len, const unsigned long long *block_end, hipStream_t s) {
+  hipLaunchKernelGGL(k_consume, dim3(1), dim3(1), 0, s, st_, (unsigned long long)used,
+                     (unsigned long long)(block_len ? block_len : 1), block_end, block_end ? 1 : 0,
+                     (const unsigned long long *)nullptr);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::consume_normals_dev(const unsigned long long *used_blocks, size_t block_len,
+                                  const unsigned long long *block_end, hipStream_t s) {
+  hipLaunchKernelGGL(k_consume, dim3(1), dim3(1), 0, s, st_, 0ULL, (unsigned long long)block_len, block_end, 1,
+                     used_blocks);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::uniforms(double *u, size_t M, hipStream_t s) {
+  if (M == 0) return 0;
+  if (produce(M + 2, s)) return 1;
+  hipLaunchKernelGGL(k_uniforms, dim3((M + 255) / 256), dim3(256), 0, s, ring_, R_, st_, u, (unsigned long long)M);
+  KG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_consume_words, dim3(1), dim3(1), 0, s, st_, (unsigned long long)M);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace kg

@@ -1,0 +1,80 @@
+// kg_rng.hpp — a GSL mt19937 stream resident in HBM.
+//
+// The reference draws every normal of a generation from ONE sequential GSL
+// mt19937 stream (Normal::getRandomNumber → gsl_ran_gaussian, Marsaglia
+// polar on gsl_rng_uniform_pos; univariate/normal/normal.cpp.base:32-35).
+// The stream is a fixed sequence independent of the solver state, so the
+// device keeps its untempered words s_j (absolute index j) in a ring buffer:
+//
+//   s_j = s_{j-227} ^ twist(s_{j-624}, s_{j-623})      (GSL rng/mt.c)
+//
+// * k_mt_produce extends the generated frontier with one wavefront: 227
+//   independent words per step (the recurrence's minimum lag), LDS ring of
+//   the last 1024 words, coalesced stores to HBM.
+// * polar normals are then data-parallel: attempt a uses compacted words
+//   (2a, 2a+1) (zero words skipped, as uniform_pos does), an accept-count
+//   pass + block scan + scatter pass places normal k exactly where the
+//   sequential reference would, and the consumed-word count re-derives the
+//   exact GSL state (mt[624], mti) for export.
+#pragma once
+
+#include "kg_common.hpp"
+
+namespace kg {
+
+constexpr int KG_MAX_ZERO_WORDS = 64;
+
+struct StreamState {
+  unsigned long long lo;   // absolute index of the current GSL block start (624*b)
+  unsigned long long pos;  // next unconsumed absolute index
+  unsigned long long hi;   // generated frontier (exclusive)
+  unsigned int nzero;      // recorded zero words (absolute positions >= lo)
+  unsigned int errors;
+  unsigned long long zeros[KG_MAX_ZERO_WORDS];
+  unsigned long long last_attempt;  // polar: attempt index of the last consumed normal
+  unsigned long long total_normals; // polar: accepted normals available in the window
+};
+
+class MtStream {
+ public:
+  MtStream() = default;
+  ~MtStream();
+  // capacity: words the ring must hold beyond the current block
+  int init(size_t capacity_words);
+  int import_gsl(const void *state5000, hipStream_t s);
+  int export_gsl(void *state5000, hipStream_t s);
+  // make sure words [pos, pos + ahead) exist (device-side target)
+  int produce(unsigned long long ahead, hipStream_t s);
+
+  // Polar normals (gsl_ran_gaussian, sigma = 1, mean 0 added): M normals into
+  // z (device, sample-major).  If block_len > 0, block_end[b] receives the
+  // attempt index of normal (b+1)*block_len-1 (resampling support).  The
+  // stream is NOT advanced; call consume_normals() with the number of
+  // normals actually used.
+  int polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s);
+  // advance past `normals_used` normals (device-side: uses last attempt of
+  // normal normals_used-1 found in block_end[(normals_used/block_len)-1] or
+  // the polar pass's own record when block_end == nullptr)
+  int consume_normals(size_t normals_used, size_t block_len, const unsigned long long *block_end, hipStream_t s);
+  // same, with the number of consumed blocks of block_len normals read from
+  // device memory (decided on the device by the resampling pass)
+  int consume_normals_dev(const unsigned long long *used_blocks, size_t block_len,
+                          const unsigned long long *block_end, hipStream_t s);
+
+  // GSL gsl_rng_uniform draws: M uniforms (no zero skip) consumed at once
+  int uniforms(double *u, size_t M, hipStream_t s);
+
+  StreamState *state() { return st_; }
+  size_t words_for_normals(size_t M) const;
+
+ private:
+  uint32_t *ring_ = nullptr;
+  unsigned long long R_ = 0;  // power of two
+  StreamState *st_ = nullptr;
+  unsigned int *counts_ = nullptr;  // per-block accept counts
+  unsigned long long *offsets_ = nullptr;
+  size_t scratch_blocks_ = 0;
+  int ensure_scratch(size_t nblocks);
+};
+
+}  // namespace kg

@@ -1,0 +1,254 @@
+"""ctypes binding of the korali_amd C-ABI (include/korali_amd.h).
+
+The product path: every call here goes to the HIP kernels in
+korali_amd/libkorali_amd.so.  There is no CPU fallback — if the library is
+missing or no HIP device is present, construction raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libkorali_amd.so")
+_LIB = None
+
+MU_TYPES = {"logarithmic": 0, "linear": 1, "equal": 2, "proportional": 3}
+OBJECTIVES = {"negative rosenbrock": 0, "negative ackley": 1, "negative sphere": 2,
+              "rosenbrock": 0, "ackley": 1, "sphere": 2}
+COV_MODES = {"exact": 0, "mfma": 1}
+
+
+class KoraliDeviceError(RuntimeError):
+    pass
+
+
+class _CmaesCfg(C.Structure):
+    _fields_ = [
+        ("variable_count", C.c_size_t), ("population_size", C.c_size_t), ("mu_value", C.c_size_t),
+        ("mu_type", C.c_int), ("initial_sigma_cumulation_factor", C.c_double),
+        ("initial_damp_factor", C.c_double), ("initial_cumulative_covariance", C.c_double),
+        ("is_sigma_bounded", C.c_int), ("diagonal_covariance", C.c_int), ("mirrored_sampling", C.c_int),
+        ("max_infeasible_resamplings", C.c_double),
+        ("lower_bound", C.POINTER(C.c_double)), ("upper_bound", C.POINTER(C.c_double)),
+        ("initial_value", C.POINTER(C.c_double)), ("initial_std", C.POINTER(C.c_double)),
+        ("min_std_update", C.POINTER(C.c_double)),
+        ("normal_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("cov_mode", C.c_int), ("device", C.c_int),
+        ("store_bdz", C.c_int),
+    ]
+
+
+class _TmcmcCfg(C.Structure):
+    _fields_ = [
+        ("variable_count", C.c_size_t), ("population_size", C.c_size_t), ("max_chain_length", C.c_double),
+        ("default_burn_in", C.c_double), ("target_cov", C.c_double), ("covariance_scaling", C.c_double),
+        ("min_annealing_exponent_update", C.c_double), ("max_annealing_exponent_update", C.c_double),
+        ("prior_min", C.POINTER(C.c_double)), ("prior_max", C.POINTER(C.c_double)),
+        ("prior_seeds", C.POINTER(C.c_uint64)), ("multinomial_seed", C.c_uint64),
+        ("multivariate_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("likelihood", C.c_int),
+        ("device", C.c_int),
+    ]
+
+
+EXPORTED = [
+    "kg_last_error", "kg_abi_version", "kg_device_count",
+    "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
+    "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_update", "kg_cmaes_generation",
+    "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
+    "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
+    "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
+    "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
+    "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
+    "kg_tmcmc_evaluate", "kg_tmcmc_process",
+]
+
+
+def lib():
+    """Load libkorali_amd.so (raises if it is absent: no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise KoraliDeviceError(f"{LIB_PATH} not built; run `python -m korali_amd._build` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, sz, dp, cp, ip = C.c_void_p, C.c_size_t, C.POINTER(C.c_double), C.c_char_p, C.c_int
+        L.kg_last_error.restype = cp
+        L.kg_abi_version.restype = ip
+        L.kg_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.kg_cmaes_create.argtypes = [C.POINTER(_CmaesCfg), C.POINTER(vp)]
+        for f in ("kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_synchronize"):
+            getattr(L, f).argtypes = [vp]
+        L.kg_cmaes_eval_builtin.argtypes = [vp, ip]
+        L.kg_cmaes_get_candidates.argtypes = [vp, dp, sz]
+        L.kg_cmaes_set_fitness.argtypes = [vp, dp]
+        L.kg_cmaes_update.argtypes = [vp, sz]
+        L.kg_cmaes_generation.argtypes = [vp, sz, ip]
+        L.kg_cmaes_field_size.argtypes = [vp, cp, C.POINTER(sz)]
+        L.kg_cmaes_get_field.argtypes = [vp, cp, dp, sz]
+        L.kg_cmaes_set_field.argtypes = [vp, cp, dp, sz]
+        L.kg_cmaes_get_sorting_index.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.kg_cmaes_get_rng.argtypes = [vp, ip, vp]
+        L.kg_cmaes_set_rng.argtypes = [vp, ip, vp]
+        L.kg_cmaes_device_ptr.argtypes = [vp, cp, C.POINTER(vp)]
+        L.kg_cmaes_stream.argtypes = [vp, C.POINTER(vp)]
+        L.kg_cmaes_profile.argtypes = [vp, ip]
+        L.kg_cmaes_profile_read.argtypes = [vp, cp, dp, C.POINTER(sz)]
+        L.kg_tmcmc_create.argtypes = [C.POINTER(_TmcmcCfg), C.POINTER(vp)]
+        for f in ("kg_tmcmc_destroy", "kg_tmcmc_synchronize", "kg_tmcmc_evaluate"):
+            getattr(L, f).argtypes = [vp]
+        for f in ("kg_tmcmc_generation", "kg_tmcmc_prepare", "kg_tmcmc_process"):
+            getattr(L, f).argtypes = [vp, sz]
+        L.kg_tmcmc_field_size.argtypes = [vp, cp, C.POINTER(sz)]
+        L.kg_tmcmc_get_field.argtypes = [vp, cp, dp, sz]
+        L.kg_tmcmc_set_field.argtypes = [vp, cp, dp, sz]
+        L.kg_tmcmc_get_rng.argtypes = [vp, ip, vp]
+        L.kg_tmcmc_set_rng.argtypes = [vp, ip, vp]
+        _LIB = L
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        raise KoraliDeviceError(lib().kg_last_error().decode())
+
+
+def device_count():
+    n = C.c_int(0)
+    check(lib().kg_device_count(C.byref(n)))
+    return n.value
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _vec(x, n, default):
+    if x is None:
+        return np.full(n, default, dtype=np.float64)
+    a = np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=np.float64), (n,)))
+    return a
+
+
+class CmaesDevice:
+    """One CMA-ES solver instance resident on one MI355X (kg_cmaes_t)."""
+
+    def __init__(self, N, lam, mu=0, mu_type="Logarithmic", lower_bound=None, upper_bound=None, initial_value=None,
+                 initial_std=None, min_std_update=None, normal_seed=0, uniform_seed=0, cov_mode="exact",
+                 is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
+                 initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
+                 initial_cumulative_covariance=-1.0, device=0, store_bdz=False):
+        L = lib()
+        self.N, self.lam = int(N), int(lam)
+        self.mu = int(mu) if mu else self.lam // 2
+        self._arrays = [
+            _vec(lower_bound, self.N, -np.inf), _vec(upper_bound, self.N, np.inf),
+            _vec(initial_value, self.N, np.nan), _vec(initial_std, self.N, np.nan),
+            _vec(min_std_update, self.N, 0.0),
+        ]
+        cfg = _CmaesCfg()
+        cfg.variable_count, cfg.population_size, cfg.mu_value = self.N, self.lam, int(mu)
+        cfg.mu_type = MU_TYPES[mu_type.lower()] if isinstance(mu_type, str) else int(mu_type)
+        cfg.initial_sigma_cumulation_factor = initial_sigma_cumulation_factor
+        cfg.initial_damp_factor = initial_damp_factor
+        cfg.initial_cumulative_covariance = initial_cumulative_covariance
+        cfg.is_sigma_bounded, cfg.diagonal_covariance, cfg.mirrored_sampling = int(is_sigma_bounded), int(diagonal), 0
+        cfg.max_infeasible_resamplings = float(max_infeasible_resamplings)
+        (cfg.lower_bound, cfg.upper_bound, cfg.initial_value, cfg.initial_std,
+         cfg.min_std_update) = [_dptr(a) for a in self._arrays]
+        cfg.normal_seed, cfg.uniform_seed = int(normal_seed), int(uniform_seed)
+        cfg.cov_mode = COV_MODES[cov_mode.lower()] if isinstance(cov_mode, str) else int(cov_mode)
+        cfg.device, cfg.store_bdz = int(device), int(store_bdz)
+        h = C.c_void_p()
+        check(L.kg_cmaes_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.kg_cmaes_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # stages
+    def initialize(self):
+        check(self._L.kg_cmaes_initialize(self.h))
+
+    def sample(self):
+        check(self._L.kg_cmaes_sample(self.h))
+
+    def evaluate(self, objective):
+        check(self._L.kg_cmaes_eval_builtin(self.h, OBJECTIVES[objective.lower()] if isinstance(objective, str)
+                                            else int(objective)))
+
+    def update(self, generation):
+        check(self._L.kg_cmaes_update(self.h, int(generation)))
+
+    def generation(self, generation, objective):
+        obj = OBJECTIVES[objective.lower()] if isinstance(objective, str) else int(objective)
+        check(self._L.kg_cmaes_generation(self.h, int(generation), obj))
+
+    def synchronize(self):
+        check(self._L.kg_cmaes_synchronize(self.h))
+
+    # host-callback objectives
+    def candidates(self):
+        X = np.empty((self.lam, self.N))
+        check(self._L.kg_cmaes_get_candidates(self.h, _dptr(X), self.N))
+        return X
+
+    def set_fitness(self, F):
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        check(self._L.kg_cmaes_set_fitness(self.h, _dptr(F)))
+
+    # state
+    def field_size(self, name):
+        n = C.c_size_t()
+        check(self._L.kg_cmaes_field_size(self.h, name.encode(), C.byref(n)))
+        return n.value
+
+    def __getitem__(self, name):
+        n = self.field_size(name)
+        out = np.empty(n)
+        check(self._L.kg_cmaes_get_field(self.h, name.encode(), _dptr(out), n))
+        return out
+
+    def __setitem__(self, name, value):
+        a = np.ascontiguousarray(np.asarray(value, dtype=np.float64).reshape(-1))
+        check(self._L.kg_cmaes_set_field(self.h, name.encode(), _dptr(a), a.size))
+
+    def sorting_index(self):
+        out = np.empty(self.lam, dtype=np.uint64)
+        check(self._L.kg_cmaes_get_sorting_index(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
+
+    def get_rng(self, which):
+        buf = C.create_string_buffer(5000)
+        check(self._L.kg_cmaes_get_rng(self.h, int(which), buf))
+        return buf.raw
+
+    def set_rng(self, which, state):
+        assert len(state) == 5000
+        buf = C.create_string_buffer(bytes(state), 5000)
+        check(self._L.kg_cmaes_set_rng(self.h, int(which), buf))
+
+    def device_ptr(self, name):
+        p = C.c_void_p()
+        check(self._L.kg_cmaes_device_ptr(self.h, name.encode(), C.byref(p)))
+        return p.value
+
+    def stream(self):
+        p = C.c_void_p()
+        check(self._L.kg_cmaes_stream(self.h, C.byref(p)))
+        return p.value
+
+    def profile(self, enable=True):
+        check(self._L.kg_cmaes_profile(self.h, int(enable)))
+
+    def profile_read(self, stage):
+        ms, n = C.c_double(), C.c_size_t()
+        check(self._L.kg_cmaes_profile_read(self.h, stage.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One gpurun session: each GPU step under its own time limit; stop at the
+# first crash/timeout (exit >= 124), keep going on ordinary test failures.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${SESSION:-s}
+mkdir -p "$OUT"
+step() {
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "FATAL step $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke tests bench prof}; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 1200 python -m pytest tests -x -q -m gpu ;;
+    bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;
+    benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+  esac
+done
+echo "session done"
