@@ -9,6 +9,8 @@
 // One HIP stream per handle; a generation is a fixed kernel sequence with no
 // host synchronisation (device-side error flags are read at sync points).
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -22,7 +24,8 @@
 namespace kg {
 
 int launch_symmv(int N, int diagonal, const double *C, double *gA, double *gH, double *B, double *D, double *minEig,
-                 double *maxEig, double *eigenFailures, unsigned int *errors, hipStream_t s);
+                 double *maxEig, double *eigenFailures, unsigned int *errors, unsigned long long *trace,
+                 hipStream_t s);
 
 struct CmaesScalars {
   double sigma, trace, effectiveMu, cumulativeCovariance, sigmaCumulationFactor, dampFactor, chiSquareNumber;
@@ -139,10 +142,10 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
 constexpr int TR_BM = 32, TR_BN = 64, TR_BK = 32;
 __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal, const double *__restrict__ Z,
                                                    const double *__restrict__ B, const double *__restrict__ D,
-                                                   const double *__restrict__ mean, const CmaesScalars *__restrict__ sc,
+                                                   const double *__restrict__ mean, CmaesScalars *__restrict__ sc,
                                                    const double *__restrict__ lb, const double *__restrict__ ub,
                                                    double *__restrict__ X, double *__restrict__ BDZ,
-                                                   int *__restrict__ infeas) {
+                                                   int *__restrict__ infeas, int no_reserve) {
   __shared__ double Za[TR_BK][TR_BM + 1];
   __shared__ double Bt[TR_BK][TR_BN + 1];
   const int tid = threadIdx.x;
@@ -194,7 +197,14 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
       if (BDZ) BDZ[(size_t)i * N + d] = bdz;
       if (!isfinite(x) || x < lb[d] || x > ub[d]) bad = 1;
     }
-    if (bad) atomicOr(&infeas[i], 1);
+    if (bad) {
+      // no reserve (all bounds infinite): a non-finite draw would have been
+      // redrawn by the reference loop; report instead of diverging
+      if (no_reserve)
+        atomicOr(&sc->errors, KG_ERR_RESAMPLE_RESERVE);
+      else
+        atomicOr(&infeas[i], 1);
+    }
   }
 }
 
@@ -225,16 +235,6 @@ __global__ void k_select(int lam, int blocks, double maxRes, const int *__restri
   }
   sc->infeasibleSampleCount = count;
   *used = (unsigned long long)j;
-}
-
-__global__ void k_count_infeasible(int lam, const int *__restrict__ infeas, CmaesScalars *sc,
-                                   unsigned long long *used) {
-  // no reserve: every drawn candidate is kept; a non-finite or out-of-bound
-  // draw would have been redrawn by the reference → flag it
-  if (threadIdx.x != 0) return;
-  for (int i = 0; i < lam; i++)
-    if (infeas[i]) sc->errors |= KG_ERR_RESAMPLE_RESERVE;
-  *used = (unsigned long long)lam;
 }
 
 __global__ void k_gather_rows(int N, int lam, const int *__restrict__ assign, const double *__restrict__ Xall,
@@ -447,59 +447,95 @@ __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, 
   }
 }
 
-// mean :603-609 and mean update :623-624 (sequential over the μ selected)
-__global__ void __launch_bounds__(64) k_mean(int N, int mu, const double *__restrict__ X,
-                                             const unsigned *__restrict__ idx, const double *__restrict__ w,
-                                             double *mean, double *prevMean, double *meanUpdate,
-                                             const CmaesScalars *__restrict__ sc) {
+// gather the μ selected rows into Y (contiguous; shared by mean and adaptC)
+__global__ void __launch_bounds__(256) k_gather_selected(int N, int mu, const double *__restrict__ X,
+                                                         const unsigned *__restrict__ idx, double *__restrict__ Y) {
+  const int i = blockIdx.x;
+  const size_t src = (size_t)idx[i] * N;
+  for (int d = threadIdx.x; d < N; d += blockDim.x) Y[(size_t)i * N + d] = X[src + d];
+}
+
+// mean :603-609 and mean update :623-624 (sequential over the μ selected,
+// rows streamed from Y)
+__global__ void __launch_bounds__(64) k_mean(int N, int mu, const double *__restrict__ Y,
+                                             const double *__restrict__ w, double *mean, double *prevMean,
+                                             double *meanUpdate, const CmaesScalars *__restrict__ sc) {
   const int d = blockIdx.x * 64 + threadIdx.x;
   if (d >= N) return;
   const double prev = mean[d];
   double acc = 0.;
   int i = 0;
-  for (; i + 8 <= mu; i += 8) {
-    double v[8];
+  for (; i + 16 <= mu; i += 16) {
+    double v[16];
 #pragma unroll
-    for (int q = 0; q < 8; q++) v[q] = w[i + q] * X[(size_t)idx[i + q] * N + d];
+    for (int q = 0; q < 16; q++) v[q] = w[i + q] * Y[(size_t)(i + q) * N + d];
 #pragma unroll
-    for (int q = 0; q < 8; q++) acc += v[q];
+    for (int q = 0; q < 16; q++) acc += v[q];
   }
-  for (; i < mu; i++) acc += w[i] * X[(size_t)idx[i] * N + d];
+  for (; i < mu; i++) acc += w[i] * Y[(size_t)i * N + d];
   prevMean[d] = prev;
   mean[d] = acc;
   meanUpdate[d] = (acc - prev) / sc->sigma;
 }
 
-// evolution paths :626-662 (+ the adaptC constants :693-694)
+// evolution paths :626-662 (+ the adaptC constants :693-694).  Both
+// matrix-vector products keep the reference's sequential e-order per output;
+// B is staged through LDS in column chunks so row sweeps stay coalesced.
+constexpr int PA_EC = 16;
 __global__ void __launch_bounds__(1024) k_paths(int N, int diagonal, unsigned long long gen,
                                                 const double *__restrict__ B, const double *__restrict__ D,
                                                 const double *__restrict__ meanUpdate, double *auxBDZ, double *ps,
                                                 double *pc, CmaesScalars *sc) {
+  extern __shared__ __attribute__((aligned(16))) double psm[];
+  double *tile = psm;                       // N x (PA_EC+1)
+  double *sv = psm + (size_t)N * (PA_EC + 1);  // N: mean update, then aux, then ps
   __shared__ int hs;
   const int tid = threadIdx.x;
   const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
-  for (int d = tid; d < N; d += blockDim.x) {
-    double sum = 0.0;
+  for (int d = tid; d < N; d += blockDim.x) sv[d] = meanUpdate[d];
+  __syncthreads();
+  // aux[d] = (sum_e B[e][d] mu[e]) / D[d]   (column sweep: coalesced)
+  double a1 = 0.0;
+  if (tid < N) {
     if (diagonal)
-      sum = meanUpdate[d];
+      a1 = sv[tid];
     else
-      for (int e = 0; e < N; ++e) sum += B[(size_t)e * N + d] * meanUpdate[e];
-    auxBDZ[d] = sum / D[d];
+      for (int e = 0; e < N; ++e) a1 += B[(size_t)e * N + tid] * sv[e];
+    a1 = a1 / D[tid];
   }
   __syncthreads();
+  if (tid < N) {
+    sv[tid] = a1;
+    auxBDZ[tid] = a1;
+  }
+  __syncthreads();
+  // sum_e B[d][e] aux[e]   (row sweep through LDS chunks)
+  double sum = 0.0;
+  if (diagonal) {
+    if (tid < N) sum = sv[tid];
+  } else {
+    for (int e0 = 0; e0 < N; e0 += PA_EC) {
+      const int en = (N - e0) < PA_EC ? (N - e0) : PA_EC;
+      for (int q = tid; q < N * PA_EC; q += blockDim.x) {
+        const int d = q / PA_EC, ee = q % PA_EC;
+        tile[d * (PA_EC + 1) + ee] = (ee < en) ? B[(size_t)d * N + e0 + ee] : 0.0;
+      }
+      __syncthreads();
+      if (tid < N)
+        for (int ee = 0; ee < en; ++ee) sum += tile[tid * (PA_EC + 1) + ee] * sv[e0 + ee];
+      __syncthreads();
+    }
+  }
   const double fac = sqrt(cs * (2. - cs) * effMu);
-  for (int d = tid; d < N; d += blockDim.x) {
-    double sum = 0.0;
-    if (diagonal)
-      sum = auxBDZ[d];
-    else
-      for (int e = 0; e < N; ++e) sum += B[(size_t)d * N + e] * auxBDZ[e];
-    ps[d] = (1. - cs) * ps[d] + fac * sum;
+  if (tid < N) {
+    const double p = (1. - cs) * ps[tid] + fac * sum;
+    ps[tid] = p;
+    tile[tid] = p;
   }
   __syncthreads();
   if (tid == 0) {
     double nrm = 0.0;
-    for (int d = 0; d < N; ++d) nrm += ps[d] * ps[d];  // std::pow(x, 2.0) == x*x (CR)
+    for (int d = 0; d < N; ++d) nrm += tile[d] * tile[d];  // std::pow(x, 2.0) == x*x (CR)
     nrm = sqrt(nrm);
     sc->psNorm = nrm;
     const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
@@ -554,7 +590,7 @@ __global__ void __launch_bounds__(256) k_adaptC_exact(int N, int mu, int diagona
       const int kk = q / AC_T, cidx = q % AC_T;
       double yd = 0.0, ye = 0.0;
       if (kk < kn) {
-        const size_t row = (size_t)idx[k0 + kk] * N;
+        const size_t row = (size_t)(k0 + kk) * N;  // Y row k = X[idx[k]]
         const int dd = td * AC_T + cidx, ee = te * AC_T + cidx;
         if (dd < N) yd = X[row + dd] - prevMean[dd];
         if (ee < N) ye = X[row + ee] - prevMean[ee];
@@ -597,7 +633,7 @@ __global__ void __launch_bounds__(64) k_rankmu_mfma(int N, int mu, int kslices, 
     const int k = k0 + lk;
     double a = 0.0, b = 0.0;
     if (k < kend) {
-      const size_t row = (size_t)idx[k] * N;
+      const size_t row = (size_t)k * N;  // Y row k = X[idx[k]]
       const double sk = scale * w[k];
       if (d < N) a = sk * (X[row + d] - pmd);
       if (e < N) b = X[row + e] - pme;
@@ -632,40 +668,76 @@ __global__ void __launch_bounds__(256) k_adaptC_combine(int N, int kslices, int 
 }
 
 // adaptC diag extrema :709-717, updateSigma :720-761, numericalErrorTreatment
-// :763-772, min/max standard deviation :679-687
-__global__ void k_sigma(int N, int mu, int isSigmaBounded, const double *__restrict__ C,
-                        const double *__restrict__ F, const unsigned *__restrict__ idx,
-                        const double *__restrict__ minStdUpdate, CmaesScalars *sc) {
-  if (threadIdx.x != 0) return;
-  double maxd = C[0], mind = C[0];
-  for (int d = 1; d < N; ++d) {
-    const double v = C[(size_t)d * N + d];
-    if (maxd < v)
-      maxd = v;
-    else if (mind > v)
-      mind = v;
+// :763-772, min/max standard deviation :679-687.  (The reference's max/min
+// diagonal scan uses "else if"; a new maximum can never be a new minimum, so
+// plain extrema are identical.)
+__global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded, const double *__restrict__ C,
+                                               const double *__restrict__ F, const unsigned *__restrict__ idx,
+                                               const double *__restrict__ minStdUpdate, CmaesScalars *sc) {
+  __shared__ double ssig;
+  __shared__ int viol;
+  __shared__ double red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
+    double sigma = sc->sigma;
+    sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
+    if (mu > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
+    const double ub = sqrt(sc->trace / N);
+    if (sigma > ub && isSigmaBounded) sigma = ub;
+    ssig = sigma;
+    viol = 0;
   }
-  sc->maxDiagC = maxd;
-  sc->minDiagC = mind;
-  const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
-  double sigma = sc->sigma;
-  sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
-  if (mu > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
-  const double ub = sqrt(sc->trace / N);
-  if (sigma > ub && isSigmaBounded) sigma = ub;
-  for (int d = 0; d < N; ++d) {
+  __syncthreads();
+  for (int d = tid; d < N; d += blockDim.x)
+    if (ssig * sqrt(C[(size_t)d * N + d]) < minStdUpdate[d]) viol = 1;
+  __syncthreads();
+  if (viol && tid == 0) {
+    const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
+    double sigma = ssig;
+    for (int d = 0; d < N; ++d) {
+      const double cdd = C[(size_t)d * N + d];
+      if (sigma * sqrt(cdd) < minStdUpdate[d]) sigma = (minStdUpdate[d]) / sqrt(cdd) * exp_cr(0.05 + cs / ds);
+    }
+    ssig = sigma;
+  }
+  __syncthreads();
+  const double sigma = ssig;
+  double mxd = -INFINITY, mnd = INFINITY, mns = INFINITY, mxs = -INFINITY;
+  for (int d = tid; d < N; d += blockDim.x) {
     const double cdd = C[(size_t)d * N + d];
-    if (sigma * sqrt(cdd) < minStdUpdate[d]) sigma = (minStdUpdate[d]) / sqrt(cdd) * exp_cr(0.05 + cs / ds);
+    mxd = fmax(mxd, cdd);
+    mnd = fmin(mnd, cdd);
+    const double s = sigma * sqrt(cdd);
+    mns = fmin(mns, s);
+    mxs = fmax(mxs, s);
   }
-  sc->sigma = sigma;
-  double mn = INFINITY, mx = -INFINITY;
-  for (int i = 0; i < N; ++i) {
-    const double s = sigma * sqrt(C[(size_t)i * N + i]);
-    mn = fmin(mn, s);
-    mx = fmax(mx, s);
+  for (int off = 32; off > 0; off >>= 1) {
+    mxd = fmax(mxd, __shfl_xor(mxd, off, 64));
+    mnd = fmin(mnd, __shfl_xor(mnd, off, 64));
+    mns = fmin(mns, __shfl_xor(mns, off, 64));
+    mxs = fmax(mxs, __shfl_xor(mxs, off, 64));
   }
-  sc->currentMinStd = mn;
-  sc->currentMaxStd = mx;
+  if (lane == 0) {
+    red[wid][0] = mxd;
+    red[wid][1] = mnd;
+    red[wid][2] = mns;
+    red[wid][3] = mxs;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; w++) {
+      mxd = fmax(mxd, red[w][0]);
+      mnd = fmin(mnd, red[w][1]);
+      mns = fmin(mns, red[w][2]);
+      mxs = fmax(mxs, red[w][3]);
+    }
+    sc->maxDiagC = mxd;
+    sc->minDiagC = mnd;
+    sc->sigma = sigma;
+    sc->currentMinStd = mns;
+    sc->currentMaxStd = mxs;
+  }
 }
 
 __global__ void k_add_evals(CmaesScalars *sc, double n) {
@@ -691,10 +763,11 @@ struct kg_cmaes_s {
   double *sortKey = nullptr;
   unsigned *sortVal = nullptr;
   CmaesScalars *sc = nullptr;
-  double *eigA = nullptr, *eigH = nullptr, *covPart = nullptr;
+  double *eigA = nullptr, *eigH = nullptr, *covPart = nullptr, *Y = nullptr;
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
   int kslices = 8;
+  unsigned long long *eigTrace = nullptr;  // KORALI_AMD_TRACE_EIGEN: s_memtime per phase
   MtStream normal, uniform;
   // profiling
   bool profile = false;
@@ -878,6 +951,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->X, (size_t)L * N) | dalloc(&h->F, L) | dalloc(&h->Z, rows * N);
   rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
   rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
+  rc |= dalloc(&h->Y, (size_t)h->mu * N);
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1) | dalloc(&h->eigA, (size_t)N * (N + 1)) | dalloc(&h->eigH, (size_t)N * N);
   rc |= dalloc(&h->infeas, rows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
@@ -895,14 +969,24 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
+  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 16);
+  KG_HIP(hipFuncSetAttribute((const void *)k_paths, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  if (rc) {
+    delete h;
+    return 1;
+  }
   KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  {
+    const unsigned long long used = (unsigned long long)L;  // no-reserve path consumes exactly λ blocks
+    KG_HIP(hipMemcpy(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice));
+  }
   KG_HIP(hipMemcpy(h->lb, lb.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->ub, ub.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->iv, iv.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->istd, istd.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->minstd, minstd.data(), N * sizeof(double), hipMemcpyHostToDevice));
   const size_t words = h->normal.words_for_normals(rows * N);
-  if (h->normal.init(2 * words) || h->uniform.init(1 << 16)) {
+  if (h->normal.init(3 * words + 4096) || h->uniform.init(1 << 16)) {
     delete h;
     return 1;
   }
@@ -924,7 +1008,8 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->meanUpdate, (void *)h->auxBDZ, (void *)h->lb, (void *)h->ub, (void *)h->iv,
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
                   (void *)h->sc, (void *)h->eigA, (void *)h->eigH, (void *)h->covPart, (void *)h->infeas,
-                  (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks})
+                  (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y,
+                  (void *)h->eigTrace})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -948,12 +1033,13 @@ int kg_cmaes_initialize(kg_cmaes_t h) {
 static int cmaes_eigen(kg_cmaes_t h) {
   Stage st(h, "eigen");
   return launch_symmv(h->N, h->cfg.diagonal_covariance, h->C, h->eigA, h->eigH, h->B, h->D, &h->sc->minEig,
-                      &h->sc->maxEig, &h->sc->eigenFailures, &h->sc->errors, h->stream);
+                      &h->sc->maxEig, &h->sc->eigenFailures, &h->sc->errors, h->eigTrace, h->stream);
 }
 
 int kg_cmaes_sample(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
   const size_t rows = (size_t)L + h->R;
+  if (h->normal.prefetch(rows * N, h->stream)) return 1;  // overlaps the eigensolver
   if (cmaes_eigen(h)) return 1;
   {
     Stage st(h, "rng_polar");
@@ -961,12 +1047,12 @@ int kg_cmaes_sample(kg_cmaes_t h) {
   }
   {
     Stage st(h, "transform");
-    KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
+    if (h->R) KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
     const int nbn = (N + TR_BN - 1) / TR_BN;
     const int nbm = (int)((rows + TR_BM - 1) / TR_BM);
     hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)rows,
                        h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub,
-                       h->R ? h->Xall : h->X, h->R ? h->BDZall : h->BDZ, h->infeas);
+                       h->R ? h->Xall : h->X, h->R ? h->BDZall : h->BDZ, h->infeas, h->R ? 0 : 1);
     KG_HIP(hipGetLastError());
     if (h->R) {
       hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
@@ -974,8 +1060,6 @@ int kg_cmaes_sample(kg_cmaes_t h) {
       const size_t tot = (size_t)L * N;
       hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, L, h->assign,
                          h->Xall, h->X, h->BDZall, h->BDZ);
-    } else {
-      hipLaunchKernelGGL(k_count_infeasible, dim3(1), dim3(64), 0, h->stream, L, h->infeas, h->sc, h->usedBlocks);
     }
     KG_HIP(hipGetLastError());
   }
@@ -1043,29 +1127,32 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
                        (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
                        h->sc);
-    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->X, h->idx, h->w, h->mean,
+    hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y);
+    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->Y, h->w, h->mean,
                        h->prevMean, h->meanUpdate, h->sc);
-    hipLaunchKernelGGL(k_paths, dim3(1), dim3(1024), 0, h->stream, N, h->cfg.diagonal_covariance,
-                       (unsigned long long)generation, h->B, h->D, h->meanUpdate, h->auxBDZ, h->ps, h->pc, h->sc);
+    const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
+    hipLaunchKernelGGL(k_paths, dim3(1), dim3(N <= 1024 ? ((N + 63) / 64) * 64 : 1024), pbytes, h->stream, N,
+                       h->cfg.diagonal_covariance, (unsigned long long)generation, h->B, h->D, h->meanUpdate,
+                       h->auxBDZ, h->ps, h->pc, h->sc);
     KG_HIP(hipGetLastError());
   }
   {
     Stage st(h, "covariance");
     const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
     if (h->cfg.cov_mode == KG_COV_MFMA) {
-      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->X,
+      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->Y,
                          h->idx, h->w, h->prevMean, h->sc, h->covPart);
       hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc);
     } else {
       hipLaunchKernelGGL(k_adaptC_exact, dim3(ntiles), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
-                         h->X, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
+                         h->Y, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
     }
     KG_HIP(hipGetLastError());
   }
   {
     Stage st(h, "sigma");
-    hipLaunchKernelGGL(k_sigma, dim3(1), dim3(64), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
+    hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
                        h->minstd, h->sc);
     KG_HIP(hipGetLastError());
   }
@@ -1081,6 +1168,12 @@ int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
 
 int kg_cmaes_synchronize(kg_cmaes_t h) {
   KG_HIP(hipStreamSynchronize(h->stream));
+  if (h->eigTrace) {
+    unsigned long long t[16];
+    KG_HIP(hipMemcpy(t, h->eigTrace, sizeof(t), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[korali_amd eigen trace] A %llu B %llu C %llu D %llu (s_memtime ticks) qrsteps %llu\n",
+            t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[6]);
+  }
   return check_errors(h);
 }
 

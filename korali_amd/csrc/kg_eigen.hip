@@ -209,15 +209,19 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
 // Dynamic LDS: [matrix region N*(N+1) doubles if lds_mats] + vectors.
 // Vectors (doubles): x N, d N, sd N, tau N, gc 2N, gs 2N, ev N, scal 16; ints
 // perm N, misc 8.
+template <bool kLds>
 __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const double *__restrict__ C, double *gA,
                                                 double *gH, double *__restrict__ B, double *__restrict__ D,
                                                 double *minEig, double *maxEig, double *eigenFailures,
-                                                unsigned int *errors, int lds_mats) {
+                                                unsigned int *errors, unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wid = tid >> 6;
   const int lda = N + 1;
-  double *M = lds_mats ? smem : gA;  // A during phase A, Qt during B/C
-  double *vb = lds_mats ? smem + (size_t)N * lda : smem;
+  double *M = kLds ? smem : gA;  // A during phase A, Qt during B/C
+  double *vb = kLds ? smem + (size_t)N * lda : smem;
+#define KG_TRACE(i) \
+  if (trace && tid == 0) trace[i] = __builtin_amdgcn_s_memtime();
+  KG_TRACE(0)
   double *x = vb, *dv = vb + N, *sdv = vb + 2 * N, *tau = vb + 3 * N;
   double *gc = vb + 4 * N, *gs = vb + 6 * N, *ev = vb + 8 * N, *scal = vb + 9 * N;
   int *perm = (int *)(scal + 16);
@@ -422,6 +426,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
   }
   __syncthreads();
 
+  KG_TRACE(1)
   // ---------------------------------------------------------- phase B
   // Qt[col][row] = Q[row][col] = I
   for (int idx = tid; idx < N * lda; idx += nt) {
@@ -433,7 +438,9 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     const double ti = tau[i];
     if (ti == 0.0) continue;  // householder_hm returns early
     const int n = N - (i + 1);
-    const double *h = gH + (size_t)i * N;
+    for (int r = tid; r < n; r += nt) x[r] = gH[(size_t)i * N + r];
+    __syncthreads();
+    const double *h = x;
     for (int j = tid; j < n; j += nt) {
       double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
       double wj = col[0];
@@ -444,6 +451,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     __syncthreads();
   }
 
+  KG_TRACE(2)
   // ---------------------------------------------------------- phase C
   if (tid == 0) {
     chop_small(N, dv, sdv);
@@ -504,6 +512,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     if (misc[2 + buf] < 0) break;
   }
 
+  KG_TRACE(3)
+  if (trace && tid == 0) trace[6] = (unsigned long long)misc[5];
   // ---------------------------------------------------------- phase D
   for (int i = tid; i < N; i += nt) {
     ev[i] = dv[i];
@@ -571,6 +581,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     *minEig = scal[6];
     *maxEig = scal[7];
   }
+  KG_TRACE(4)
+#undef KG_TRACE
 }
 
 size_t symmv_lds_bytes(int N, bool lds_mats) {
@@ -580,17 +592,23 @@ size_t symmv_lds_bytes(int N, bool lds_mats) {
 }
 
 int launch_symmv(int N, int diagonal, const double *C, double *gA, double *gH, double *B, double *D, double *minEig,
-                 double *maxEig, double *eigenFailures, unsigned int *errors, hipStream_t s) {
+                 double *maxEig, double *eigenFailures, unsigned int *errors, unsigned long long *trace,
+                 hipStream_t s) {
   KG_CHECK(N >= 1 && N <= 960, "device eigensolver supports 1 <= N <= 960");
   const bool lds = (symmv_lds_bytes(N, true) <= 160 * 1024);
   const size_t bytes = symmv_lds_bytes(N, lds);
   static bool attr_set = false;
   if (!attr_set) {
-    KG_HIP(hipFuncSetAttribute((const void *)k_symmv, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    KG_HIP(hipFuncSetAttribute((const void *)k_symmv<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    KG_HIP(hipFuncSetAttribute((const void *)k_symmv<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_symmv, dim3(1), dim3(1024), bytes, s, N, diagonal, C, gA, gH, B, D, minEig, maxEig,
-                     eigenFailures, errors, lds ? 1 : 0);
+  if (lds)
+    hipLaunchKernelGGL(k_symmv<true>, dim3(1), dim3(1024), bytes, s, N, diagonal, C, gA, gH, B, D, minEig, maxEig,
+                       eigenFailures, errors, trace);
+  else
+    hipLaunchKernelGGL(k_symmv<false>, dim3(1), dim3(1024), bytes, s, N, diagonal, C, gA, gH, B, D, minEig, maxEig,
+                       eigenFailures, errors, trace);
   KG_HIP(hipGetLastError());
   return 0;
 }

@@ -265,6 +265,12 @@ unsigned long long next_pow2(unsigned long long x) {
 }  // namespace
 
 MtStream::~MtStream() {
+  if (side_) {
+    (void)hipStreamSynchronize(side_);
+    (void)hipStreamDestroy(side_);
+  }
+  if (ev_main_) (void)hipEventDestroy(ev_main_);
+  if (ev_side_) (void)hipEventDestroy(ev_side_);
   if (ring_) (void)hipFree(ring_);
   if (st_) (void)hipFree(st_);
   if (counts_) (void)hipFree(counts_);
@@ -356,11 +362,30 @@ size_t MtStream::words_for_normals(size_t M) const {
   return (size_t)(2.0 * A) + 64;
 }
 
+int MtStream::prefetch(size_t M, hipStream_t main) {
+  if (!side_) {
+    KG_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    KG_HIP(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
+    KG_HIP(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
+  }
+  const unsigned long long words = words_for_normals(M);
+  KG_HIP(hipEventRecord(ev_main_, main));
+  KG_HIP(hipStreamWaitEvent(side_, ev_main_, 0));
+  if (produce(2 * (words + 2 * KG_MAX_ZERO_WORDS), side_)) return 1;
+  KG_HIP(hipEventRecord(ev_side_, side_));
+  prefetch_pending_ = true;
+  return 0;
+}
+
 int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s) {
   const unsigned long long words = words_for_normals(M);
   const unsigned long long A = words / 2;
   const size_t nb = (size_t)((A + POLAR_APB - 1) / POLAR_APB);
   if (ensure_scratch(nb)) return 1;
+  if (prefetch_pending_) {
+    KG_HIP(hipStreamWaitEvent(s, ev_side_, 0));
+    prefetch_pending_ = false;
+  }
   if (produce(words + 2 * KG_MAX_ZERO_WORDS, s)) return 1;
   hipLaunchKernelGGL(k_polar_count, dim3(nb), dim3(POLAR_TPB), 0, s, ring_, R_, st_, A, counts_);
   KG_HIP(hipGetLastError());

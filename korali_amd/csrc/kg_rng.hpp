@@ -64,6 +64,11 @@ class MtStream {
   // GSL gsl_rng_uniform draws: M uniforms (no zero skip) consumed at once
   int uniforms(double *u, size_t M, hipStream_t s);
 
+  // Launch the producer for this and the next draw on a side stream so it
+  // runs concurrently with whatever the main stream does next (the
+  // eigendecomposition); polar_normals() then waits for it.
+  int prefetch(size_t M_normals, hipStream_t main);
+
   StreamState *state() { return st_; }
   size_t words_for_normals(size_t M) const;
 
@@ -74,6 +79,9 @@ class MtStream {
   unsigned int *counts_ = nullptr;  // per-block accept counts
   unsigned long long *offsets_ = nullptr;
   size_t scratch_blocks_ = 0;
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
+  bool prefetch_pending_ = false;
   int ensure_scratch(size_t nblocks);
 };
 

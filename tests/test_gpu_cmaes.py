@@ -110,7 +110,12 @@ def test_seeded_run_matches_oracle_bit_exact(Nv, lam, objective, gens):
         dev.generation(g, objective)
         dev.synchronize()
         assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
-        assert np.array_equal(dev["Value Vector"], o["Value Vector"]), g
+        if objective == "ackley":
+            # cos: OCML on the device vs glibc in the oracle (the reference's
+            # Python objective calls the platform libm) — 1e-15 relative
+            np.testing.assert_allclose(dev["Value Vector"], o["Value Vector"], rtol=1e-15, atol=0)
+        else:
+            assert np.array_equal(dev["Value Vector"], o["Value Vector"]), g
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
         for key in ("Current Mean", "Covariance Matrix", "Covariance Eigenvector Matrix", "Axis Lengths"):
             assert np.array_equal(dev[key], o[key]), (g, key)
@@ -126,15 +131,9 @@ def test_mfma_covariance_mode_within_tolerance():
     o, dev = oracle_and_device(Nv, lam, "rosenbrock", 1, cov_mode="mfma")
     for g in (1, 2):
         o.generation(g, "rosenbrock")
-        if g == 1:
-            dev.generation(g, "rosenbrock")
-        else:
-            # teacher-force the device with the oracle's state after gen 1
-            for key in ("Current Mean", "Previous Mean", "Covariance Matrix", "Evolution Path",
-                        "Conjugate Evolution Path"):
-                pass
-            dev.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
         dev.synchronize()
+        assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
         C_o, C_d = o["Covariance Matrix"], dev["Covariance Matrix"]
         rel = np.max(np.abs(C_d - C_o)) / np.max(np.abs(C_o))
