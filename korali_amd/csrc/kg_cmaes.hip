@@ -970,7 +970,11 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 16);
-  KG_HIP(hipFuncSetAttribute((const void *)k_paths, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  {
+    const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
+    if (pbytes > 64 * 1024)
+      KG_HIP(hipFuncSetAttribute((const void *)k_paths, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pbytes));
+  }
   if (rc) {
     delete h;
     return 1;
