@@ -1175,8 +1175,10 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
   if (h->eigTrace) {
     unsigned long long t[16];
     KG_HIP(hipMemcpy(t, h->eigTrace, sizeof(t), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[korali_amd eigen trace] A %llu B %llu C %llu D %llu (s_memtime ticks) qrsteps %llu\n",
-            t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[6]);
+    fprintf(stderr,
+            "[korali_amd eigen trace] A %llu B %llu C %llu D %llu (s_memtime ticks) qrsteps %llu | A: nrm2 %llu "
+            "dsymv %llu xv %llu dsyr2 %llu | C: chase %llu rotations %llu\n",
+            t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[6], t[7], t[8], t[9], t[10], t[11], t[12]);
   }
   return check_errors(h);
 }

@@ -222,6 +222,11 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
 #define KG_TRACE(i) \
   if (trace && tid == 0) trace[i] = __builtin_amdgcn_s_memtime();
   KG_TRACE(0)
+  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0}, tmark = 0, nrot = 0;
+#define KG_MARK() \
+  if (trace && tid == 0) tmark = __builtin_amdgcn_s_memtime();
+#define KG_ACC(k) \
+  if (trace && tid == 0) acc_t[k] += __builtin_amdgcn_s_memtime() - tmark;
   double *x = vb, *dv = vb + N, *sdv = vb + 2 * N, *tau = vb + 3 * N;
   double *gc = vb + 4 * N, *gs = vb + 6 * N, *ev = vb + 8 * N, *scal = vb + 9 * N;
   int *perm = (int *)(scal + 16);
@@ -287,6 +292,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     const int n = N - i - 1;
     double *v = M + (size_t)(i + 1) * lda + i;        // stride lda
     double *m = M + (size_t)(i + 1) * lda + (i + 1);  // lda
+    KG_MARK()
     if (wid == 0) {
       // gslcblas dnrm2 over v[1..n-1]: prefix max in parallel, the ssq
       // recurrence sequentially on uniform registers (every lane the same)
@@ -353,6 +359,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       }
     }
     __syncthreads();
+    KG_ACC(0)
     const double tau_i = scal[0];
     const int branch = (int)scal[4];
     if (branch != 0) {
@@ -366,6 +373,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     }
     __syncthreads();
     if (tau_i == 0.0) continue;
+    KG_MARK()
     // x = tau * m * v (dsymv RowMajor Lower, beta = 0), v0 := 1
     for (int j = tid; j < n; j += nt) {
       const double vj = (j == 0) ? 1.0 : v[(size_t)j * lda];
@@ -384,6 +392,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       x[j] = acc;
     }
     __syncthreads();
+    KG_ACC(1)
+    KG_MARK()
     if (wid == 0) {
       // xv = sum x[r] v[r] sequentially; alpha = -(tau/2) xv
       double xv = 0.0;
@@ -401,6 +411,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       for (int r = tid; r < n; r += nt) x[r] += alpha * ((r == 0) ? 1.0 : v[(size_t)r * lda]);
     }
     __syncthreads();
+    KG_ACC(2)
+    KG_MARK()
     // dsyr2 RowMajor Lower, alpha = -1
     for (int idx = tid; idx < n * n; idx += nt) {
       const int r = idx / n, j = idx % n;
@@ -412,6 +424,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       }
     }
     __syncthreads();
+    KG_ACC(3)
   }
   // tau[N-2] is never set by the loop (GSL's tau has N-1 entries; the last
   // one is unused by unpack)
@@ -478,8 +491,11 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
           a--;
         }
         nblk = b - a + 1;
+        KG_MARK()
         qrstep(nblk, dv + a, sdv + a, gc + buf * N, gs + buf * N);
         chop_small(nblk, dv + a, sdv + a);
+        KG_ACC(4)
+        nrot += nblk - 1;
         misc[buf] = a;
         if (++misc[5] > maxSteps) {
           atomicOr(errors, KG_ERR_EIGEN);
@@ -582,7 +598,13 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     *maxEig = scal[7];
   }
   KG_TRACE(4)
+  if (trace && tid == 0) {
+    for (int k = 0; k < 5; k++) trace[7 + k] = acc_t[k];
+    trace[12] = nrot;
+  }
 #undef KG_TRACE
+#undef KG_MARK
+#undef KG_ACC
 }
 
 size_t symmv_lds_bytes(int N, bool lds_mats) {
