@@ -175,8 +175,13 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
     return;
   }
   bq = sd[1];
+  // d[k+2], sd[k+2] read at step k were never written by this chase yet:
+  // load them one step ahead so LDS latency stays off the critical path
+  double dn = (n > 2) ? d[2] : 0.0, sdn = (n > 3) ? sd[2] : 0.0;
   int k;
   for (k = 0; k < n - 1; k++) {
+    const double dpf = (k + 3 < n) ? d[k + 3] : 0.0;
+    const double sdpf = (k + 4 < n) ? sd[k + 3] : 0.0;
     double c, s;
     create_givens(x, z, c, s);
     gc[k] = c;
@@ -192,8 +197,10 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
     zk = zp1;
     ap = aq1;
     bp = bq1;
-    if (k < n - 2) aq = d[k + 2];
-    if (k < n - 3) bq = sd[k + 2];
+    if (k < n - 2) aq = dn;
+    if (k < n - 3) bq = sdn;
+    dn = dpf;
+    sdn = sdpf;
     d[k] = ak;
     if (k > 0) sd[k - 1] = bk1;
     if (k < n - 2) sd[k + 1] = bp;
@@ -319,15 +326,19 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
             q = a / before;
           }
         }
+        // addends precomputed lane-parallel; zero elements add +0.0, which
+        // leaves ssq (>= 1) unchanged, so only new-maximum lanes branch
+        const double tq = (type == 2) ? q * q : 0.0;
+        const unsigned long long m1 = __ballot(type == 1);
         const int cnt = (n - base) < 64 ? (n - base) : 64;
+#pragma unroll 8
         for (int l = 0; l < cnt; l++) {
-          const int t = __builtin_amdgcn_readlane(type, l);
-          if (t == 0) continue;
-          const double qq = readlane_d(q, l);
-          if (t == 1)
+          if ((m1 >> l) & 1ULL) {
+            const double qq = readlane_d(q, l);
             ssq = 1.0 + ssq * qq * qq;
-          else
-            ssq += qq * qq;
+          } else {
+            ssq += readlane_d(tq, l);
+          }
         }
         scale_carry = fmax(scale_carry, readlane_d(pm, 63));
       }
@@ -377,17 +388,19 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     // x = tau * m * v (dsymv RowMajor Lower, beta = 0), v0 := 1
     for (int j = tid; j < n; j += nt) {
       const double vj = (j == 0) ? 1.0 : v[(size_t)j * lda];
-      double acc = 0.0;
-      for (int r = n - 1; r > j; r--) {
-        const double vr = v[(size_t)r * lda];  // r >= 1 here
-        acc += (tau_i * vr) * m[(size_t)r * lda + j];
+      // two independent sequential chains, interleaved:
+      //   acc: rows r = n-1 .. j+1 (descending)      t2: cols ii = 0 .. j-1
+      const int L1 = n - 1 - j, L2 = j, L = L1 > L2 ? L1 : L2;
+      double acc = 0.0, t2 = 0.0;
+#pragma unroll 4
+      for (int q = 0; q < L; q++) {
+        if (q < L1) {
+          const int r = n - 1 - q;
+          acc += (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j];
+        }
+        if (q < L2) t2 += ((q == 0) ? 1.0 : v[(size_t)q * lda]) * m[(size_t)j * lda + q];
       }
       acc += (tau_i * vj) * m[(size_t)j * lda + j];
-      double t2 = 0.0;
-      for (int ii = 0; ii < j; ii++) {
-        const double vi = (ii == 0) ? 1.0 : v[(size_t)ii * lda];
-        t2 += vi * m[(size_t)j * lda + ii];
-      }
       acc += tau_i * t2;
       x[j] = acc;
     }
@@ -401,6 +414,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
         const int r = base + lane;
         const double p = (r < n) ? x[r] * ((r == 0) ? 1.0 : v[(size_t)r * lda]) : 0.0;
         const int cnt = (n - base) < 64 ? (n - base) : 64;
+#pragma unroll 8
         for (int l = 0; l < cnt; l++) xv += readlane_d(p, l);
       }
       if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
@@ -414,12 +428,11 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     KG_ACC(2)
     KG_MARK()
     // dsyr2 RowMajor Lower, alpha = -1
-    for (int idx = tid; idx < n * n; idx += nt) {
-      const int r = idx / n, j = idx % n;
-      if (j <= r) {
-        const double vr = (r == 0) ? 1.0 : v[(size_t)r * lda];
+    for (int r = wid; r < n; r += (nt >> 6)) {
+      const double vr = (r == 0) ? 1.0 : v[(size_t)r * lda];
+      const double tmp1 = -1.0 * vr, tmp2 = -1.0 * x[r];
+      for (int j = lane; j <= r; j += 64) {
         const double vj = (j == 0) ? 1.0 : v[(size_t)j * lda];
-        const double tmp1 = -1.0 * vr, tmp2 = -1.0 * x[r];
         m[(size_t)r * lda + j] += tmp1 * x[j] + tmp2 * vj;
       }
     }
@@ -457,6 +470,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     for (int j = tid; j < n; j += nt) {
       double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
       double wj = col[0];
+#pragma unroll 8
       for (int r = 1; r < n; r++) wj += col[r] * h[r];
       col[0] = col[0] - ti * wj;
       for (int r = 1; r < n; r++) col[r] = col[r] - ti * h[r] * wj;
