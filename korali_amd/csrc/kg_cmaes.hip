@@ -969,7 +969,13 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
-  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 16);
+  if (getenv("KORALI_AMD_TRACE_EIGEN")) {
+    rc |= dalloc(&h->eigTrace, 16);
+    if (!rc && getenv("KORALI_AMD_EIGEN_NOAPPLY")) {  // timing diagnostic only: results become wrong
+      const unsigned long long one = 1;
+      KG_HIP(hipMemcpy(h->eigTrace + 15, &one, sizeof(one), hipMemcpyHostToDevice));
+    }
+  }
   {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)

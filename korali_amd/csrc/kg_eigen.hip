@@ -388,17 +388,26 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     // x = tau * m * v (dsymv RowMajor Lower, beta = 0), v0 := 1
     for (int j = tid; j < n; j += nt) {
       const double vj = (j == 0) ? 1.0 : v[(size_t)j * lda];
-      // two independent sequential chains, interleaved:
+      // two sequential chains, loads and products issued 16 at a time:
       //   acc: rows r = n-1 .. j+1 (descending)      t2: cols ii = 0 .. j-1
+      // Past its own length a chain adds +0.0, which is exact here (neither
+      // running sum can be -0.0: both start at +0.0 under round-to-nearest).
       const int L1 = n - 1 - j, L2 = j, L = L1 > L2 ? L1 : L2;
       double acc = 0.0, t2 = 0.0;
-#pragma unroll 4
-      for (int q = 0; q < L; q++) {
-        if (q < L1) {
+      for (int q0 = 0; q0 < L; q0 += 16) {
+        double p1[16], p2[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int q = q0 + u;
           const int r = n - 1 - q;
-          acc += (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j];
+          p1[u] = (q < L1) ? (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j] : 0.0;
+          p2[u] = (q < L2) ? ((q == 0) ? 1.0 : v[(size_t)q * lda]) * m[(size_t)j * lda + q] : 0.0;
         }
-        if (q < L2) t2 += ((q == 0) ? 1.0 : v[(size_t)q * lda]) * m[(size_t)j * lda + q];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          acc += p1[u];
+          t2 += p2[u];
+        }
       }
       acc += (tau_i * vj) * m[(size_t)j * lda + j];
       acc += tau_i * t2;
@@ -470,8 +479,13 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     for (int j = tid; j < n; j += nt) {
       double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
       double wj = col[0];
-#pragma unroll 8
-      for (int r = 1; r < n; r++) wj += col[r] * h[r];
+      for (int r0 = 1; r0 < n; r0 += 16) {
+        double p[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) p[u] = (r0 + u < n) ? col[r0 + u] * h[r0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding: wj is never -0.0 after col[0]+... (see dsymv)
+      }
       col[0] = col[0] - ti * wj;
       for (int r = 1; r < n; r++) col[r] = col[r] - ti * h[r] * wj;
     }
@@ -520,7 +534,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       }
       misc[4] = b;
       misc[2 + buf] = nblk;  // -1: converged
-    } else if (tid >= 64 && step > 0) {
+    } else if (tid >= 64 && step > 0 && !(trace && trace[15] == 1)) {
       const int pb = buf ^ 1;
       const int nblk = misc[2 + pb];
       if (nblk > 0) {
