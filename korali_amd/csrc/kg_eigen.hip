@@ -177,11 +177,11 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
   bq = sd[1];
   // d[k+2], sd[k+2] read at step k were never written by this chase yet:
   // load them one step ahead so LDS latency stays off the critical path
-  double dn = (n > 2) ? d[2] : 0.0, sdn = (n > 3) ? sd[2] : 0.0;
+  double dn = d[min(2, n - 1)], sdn = sd[min(2, n - 2)];
   int k;
   for (k = 0; k < n - 1; k++) {
-    const double dpf = (k + 3 < n) ? d[k + 3] : 0.0;
-    const double sdpf = (k + 4 < n) ? sd[k + 3] : 0.0;
+    const double dpf = d[min(k + 3, n - 1)];   // unconditional loads (values unused past the end)
+    const double sdpf = sd[min(k + 3, n - 2)];
     double c, s;
     create_givens(x, z, c, s);
     gc[k] = c;
@@ -306,7 +306,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       double scale_carry = 0.0, ssq = 1.0;
       for (int base = 1; base < n; base += 64) {
         const int r = base + lane;
-        const double a = (r < n) ? fabs(v[(size_t)r * lda]) : 0.0;
+        const double a_ = fabs(v[(size_t)min(r, n - 1) * lda]);
+        const double a = (r < n) ? a_ : 0.0;
         double pm = a;
         for (int off = 1; off < 64; off <<= 1) {
           const double t = __shfl_up(pm, off, 64);
@@ -398,10 +399,15 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
         double p1[16], p2[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
+          // unconditional loads from clamped (valid) addresses, then select:
+          // keeps every LDS read of the chunk in flight at once
           const int q = q0 + u;
-          const int r = n - 1 - q;
-          p1[u] = (q < L1) ? (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j] : 0.0;
-          p2[u] = (q < L2) ? ((q == 0) ? 1.0 : v[(size_t)q * lda]) * m[(size_t)j * lda + q] : 0.0;
+          const int r = max(n - 1 - q, 0), qc = min(q, n - 1);
+          const double pa = (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j];
+          const double vq = v[(size_t)qc * lda];
+          const double pb = ((q == 0) ? 1.0 : vq) * m[(size_t)j * lda + qc];
+          p1[u] = (q < L1) ? pa : 0.0;
+          p2[u] = (q < L2) ? pb : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 16; u++) {
@@ -420,8 +426,9 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       // xv = sum x[r] v[r] sequentially; alpha = -(tau/2) xv
       double xv = 0.0;
       for (int base = 0; base < n; base += 64) {
-        const int r = base + lane;
-        const double p = (r < n) ? x[r] * ((r == 0) ? 1.0 : v[(size_t)r * lda]) : 0.0;
+        const int r = base + lane, rc = min(r, n - 1);
+        const double p_ = x[rc] * ((rc == 0) ? 1.0 : v[(size_t)rc * lda]);
+        const double p = (r < n) ? p_ : 0.0;
         const int cnt = (n - base) < 64 ? (n - base) : 64;
 #pragma unroll 8
         for (int l = 0; l < cnt; l++) xv += readlane_d(p, l);
@@ -482,7 +489,11 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       for (int r0 = 1; r0 < n; r0 += 16) {
         double p[16];
 #pragma unroll
-        for (int u = 0; u < 16; u++) p[u] = (r0 + u < n) ? col[r0 + u] * h[r0 + u] : 0.0;
+        for (int u = 0; u < 16; u++) {
+          const int r = min(r0 + u, n - 1);
+          const double pr = col[r] * h[r];
+          p[u] = (r0 + u < n) ? pr : 0.0;
+        }
 #pragma unroll
         for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding: wj is never -0.0 after col[0]+... (see dsymv)
       }
