@@ -82,6 +82,9 @@ typedef struct {
   int cov_mode;                           /* enum kg_cov_mode */
   int device;                             /* HIP device ordinal */
   int store_bdz;                          /* also keep the BDZ matrix (state export) */
+  int eigen_device_chase;                 /* 0: implicit-QR Givens recurrence on the calling host
+                                             core, overlapped with the device unpack (default);
+                                             1: on one device lane.  Identical results. */
 } kg_cmaes_cfg;
 
 int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);

@@ -19,13 +19,12 @@
 
 #include "../../include/korali_amd.h"
 #include "kg_common.hpp"
+#include "kg_eigen.hpp"
 #include "kg_rng.hpp"
+#include <chrono>
 
 namespace kg {
 
-int launch_symmv(int N, int diagonal, const double *C, double *gA, double *gH, double *B, double *D, double *minEig,
-                 double *maxEig, double *eigenFailures, unsigned int *errors, unsigned long long *trace,
-                 hipStream_t s);
 
 struct CmaesScalars {
   double sigma, trace, effectiveMu, cumulativeCovariance, sigmaCumulationFactor, dampFactor, chiSquareNumber;
@@ -763,7 +762,8 @@ struct kg_cmaes_s {
   double *sortKey = nullptr;
   unsigned *sortVal = nullptr;
   CmaesScalars *sc = nullptr;
-  double *eigA = nullptr, *eigH = nullptr, *covPart = nullptr, *Y = nullptr;
+  double *covPart = nullptr, *Y = nullptr;
+  EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
   int kslices = 8;
@@ -795,6 +795,30 @@ struct Stage {
     }
   }
 };
+
+// eigensolver stage profiling: device stages by events, host stages by clock
+void eig_prof(void *ctx, const char *stage, int phase) {
+  auto *h = (kg_cmaes_s *)ctx;
+  if (!h->profile) return;
+  static thread_local hipEvent_t a;
+  static thread_local std::chrono::steady_clock::time_point t0;
+  if (phase == 0) {
+    (void)hipEventCreate(&a);
+    (void)hipEventRecord(a, h->stream);
+  } else if (phase == 1) {
+    hipEvent_t b;
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(b, h->stream);
+    h->pending.emplace_back(stage, a, b);
+  } else if (phase == 2) {
+    t0 = std::chrono::steady_clock::now();
+  } else {
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    auto &p = h->prof[stage];
+    p.first += ms;
+    p.second += 1;
+  }
+}
 
 template <typename T>
 int dalloc(T **p, size_t n) {
@@ -952,7 +976,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
   rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
   rc |= dalloc(&h->Y, (size_t)h->mu * N);
-  rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1) | dalloc(&h->eigA, (size_t)N * (N + 1)) | dalloc(&h->eigH, (size_t)N * N);
+  rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
   rc |= dalloc(&h->infeas, rows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
   if (h->R) {
@@ -969,13 +993,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
-  if (getenv("KORALI_AMD_TRACE_EIGEN")) {
-    rc |= dalloc(&h->eigTrace, 16);
-    if (!rc && getenv("KORALI_AMD_EIGEN_NOAPPLY")) {  // timing diagnostic only: results become wrong
-      const unsigned long long one = 1;
-      KG_HIP(hipMemcpy(h->eigTrace + 15, &one, sizeof(one), hipMemcpyHostToDevice));
-    }
-  }
+  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 16);
   {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)
@@ -986,6 +1004,16 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  {
+    const char *ev = getenv("KORALI_AMD_EIGEN_CHASE");
+    bool hostChase = !cfg->eigen_device_chase;
+    if (ev && std::string(ev) == "device") hostChase = false;
+    if (ev && std::string(ev) == "host") hostChase = true;
+    if (h->eig.init(N, hostChase)) {
+      delete h;
+      return 1;
+    }
+  }
   {
     const unsigned long long used = (unsigned long long)L;  // no-reserve path consumes exactly λ blocks
     KG_HIP(hipMemcpy(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice));
@@ -1017,7 +1045,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->F, (void *)h->Z, (void *)h->bestEverVars, (void *)h->currBestVars,
                   (void *)h->meanUpdate, (void *)h->auxBDZ, (void *)h->lb, (void *)h->ub, (void *)h->iv,
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
-                  (void *)h->sc, (void *)h->eigA, (void *)h->eigH, (void *)h->covPart, (void *)h->infeas,
+                  (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y,
                   (void *)h->eigTrace})
     if (p) (void)hipFree(p);
@@ -1042,8 +1070,9 @@ int kg_cmaes_initialize(kg_cmaes_t h) {
 
 static int cmaes_eigen(kg_cmaes_t h) {
   Stage st(h, "eigen");
-  return launch_symmv(h->N, h->cfg.diagonal_covariance, h->C, h->eigA, h->eigH, h->B, h->D, &h->sc->minEig,
-                      &h->sc->maxEig, &h->sc->eigenFailures, &h->sc->errors, h->eigTrace, h->stream);
+  h->eig.trace = h->eigTrace;
+  return h->eig.run(h->C, h->cfg.diagonal_covariance, h->B, h->D, &h->sc->minEig, &h->sc->maxEig,
+                    &h->sc->eigenFailures, &h->sc->errors, h->stream, eig_prof, h);
 }
 
 int kg_cmaes_sample(kg_cmaes_t h) {
@@ -1181,10 +1210,8 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
   if (h->eigTrace) {
     unsigned long long t[16];
     KG_HIP(hipMemcpy(t, h->eigTrace, sizeof(t), hipMemcpyDeviceToHost));
-    fprintf(stderr,
-            "[korali_amd eigen trace] A %llu B %llu C %llu D %llu (s_memtime ticks) qrsteps %llu | A: nrm2 %llu "
-            "dsymv %llu xv %llu dsyr2 %llu | C: chase %llu rotations %llu\n",
-            t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[6], t[7], t[8], t[9], t[10], t[11], t[12]);
+    fprintf(stderr, "[korali_amd tridiag trace, cumulative s_memtime ticks] nrm2 %llu dsymv %llu xv %llu dsyr2 %llu\n",
+            t[0], t[1], t[2], t[3]);
   }
   return check_errors(h);
 }

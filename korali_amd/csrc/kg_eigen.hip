@@ -21,13 +21,13 @@
 // Every +,-,*,/,sqrt is IEEE correctly rounded on gfx950 and the file is
 // compiled with -ffp-contract=off, so the result equals the oracle bit for
 // bit.
-#include "kg_common.hpp"
+#include "kg_eigen.hpp"
 
 namespace kg {
 
 namespace {
 
-__device__ inline double readlane_d(double x, int l) {
+__device__ __attribute__((unused)) inline double readlane_d(double x, int l) {
   const long long v = __double_as_longlong(x);
   int lo = (int)(v & 0xffffffffLL), hi = (int)(v >> 32);
   lo = __builtin_amdgcn_readlane(lo, l);
@@ -35,14 +35,16 @@ __device__ inline double readlane_d(double x, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ inline uint32_t hiw(double x) { return (uint32_t)(__double_as_longlong(x) >> 32); }
-__device__ inline uint32_t low(double x) { return (uint32_t)(__double_as_longlong(x) & 0xffffffffLL); }
-__device__ inline double sethi(double x, uint32_t h) {
-  return __longlong_as_double(((long long)h << 32) | (long long)low(x));
+__host__ __device__ inline uint32_t hiw(double x) { return (uint32_t)(__builtin_bit_cast(unsigned long long, x) >> 32); }
+__host__ __device__ inline uint32_t low(double x) {
+  return (uint32_t)(__builtin_bit_cast(unsigned long long, x) & 0xffffffffULL);
+}
+__host__ __device__ inline double sethi(double x, uint32_t h) {
+  return __builtin_bit_cast(double, ((unsigned long long)h << 32) | (unsigned long long)low(x));
 }
 
 // fdlibm __ieee754_hypot (glibc < 2.35), SURVEY.md Appendix A
-__device__ double hypot_fdlibm(double x, double y) {
+__host__ __device__ double hypot_fdlibm(double x, double y) {
   double a, b, t1, t2, y1, y2, w;
   int32_t j, k, ha, hb;
   ha = (int32_t)(hiw(x) & 0x7fffffff);
@@ -112,7 +114,7 @@ __device__ double hypot_fdlibm(double x, double y) {
 constexpr double EPS = 2.2204460492503131e-16;
 constexpr double DMIN = 2.2250738585072014e-308;
 
-__device__ inline void chop_small(int n, const double *d, double *sd) {
+__host__ __device__ inline void chop_small(int n, const double *d, double *sd) {
   double d_i = d[0];
   for (int i = 0; i + 1 < n; i++) {
     const double sd_i = sd[i], d_ip1 = d[i + 1];
@@ -121,7 +123,7 @@ __device__ inline void chop_small(int n, const double *d, double *sd) {
   }
 }
 
-__device__ inline void create_givens(double a, double b, double &c, double &s) {
+__host__ __device__ inline void create_givens(double a, double b, double &c, double &s) {
   if (b == 0) {
     c = 1;
     s = 0;
@@ -139,7 +141,7 @@ __device__ inline void create_givens(double a, double b, double &c, double &s) {
 }
 
 // eigen/qrstep.c qrstep on d[0..n), sd[0..n-1)
-__device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
+__host__ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
   double x, z, ak, bk, zk, ap, bp, aq, bq;
   double mu;
   {
@@ -177,11 +179,11 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
   bq = sd[1];
   // d[k+2], sd[k+2] read at step k were never written by this chase yet:
   // load them one step ahead so LDS latency stays off the critical path
-  double dn = d[min(2, n - 1)], sdn = sd[min(2, n - 2)];
+  double dn = d[n - 1 < 2 ? n - 1 : 2], sdn = sd[n - 2 < 2 ? n - 2 : 2];
   int k;
   for (k = 0; k < n - 1; k++) {
-    const double dpf = d[min(k + 3, n - 1)];   // unconditional loads (values unused past the end)
-    const double sdpf = sd[min(k + 3, n - 2)];
+    const double dpf = d[(k + 3 < n - 1) ? k + 3 : n - 1];  // unconditional loads (unused past the end)
+    const double sdpf = sd[(k + 3 < n - 2) ? k + 3 : n - 2];
     double c, s;
     create_givens(x, z, c, s);
     gc[k] = c;
@@ -216,55 +218,25 @@ __device__ void qrstep(int n, double *d, double *sd, double *gc, double *gs) {
 // Dynamic LDS: [matrix region N*(N+1) doubles if lds_mats] + vectors.
 // Vectors (doubles): x N, d N, sd N, tau N, gc 2N, gs 2N, ev N, scal 16; ints
 // perm N, misc 8.
+// ------------------------------------------------------------------------
+// Phase A: Householder tridiagonalisation (gsl_linalg_symmtd_decomp).
+// Outputs: Householder vectors H (row i = column i of A below the
+// diagonal), tau, diagonal d and sub-diagonal sd of the tridiagonal form.
 template <bool kLds>
-__global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const double *__restrict__ C, double *gA,
-                                                double *gH, double *__restrict__ B, double *__restrict__ D,
-                                                double *minEig, double *maxEig, double *eigenFailures,
-                                                unsigned int *errors, unsigned long long *trace) {
+__global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restrict__ C, double *gA, double *gH,
+                                                  double *tauOut, double *dOut, double *sdOut,
+                                                  unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wid = tid >> 6;
   const int lda = N + 1;
-  double *M = kLds ? smem : gA;  // A during phase A, Qt during B/C
+  double *M = kLds ? smem : gA;
   double *vb = kLds ? smem + (size_t)N * lda : smem;
-#define KG_TRACE(i) \
-  if (trace && tid == 0) trace[i] = __builtin_amdgcn_s_memtime();
-  KG_TRACE(0)
-  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0}, tmark = 0, nrot = 0;
+  double *x = vb, *scal = vb + N;
+  unsigned long long acc_t[4] = {0, 0, 0, 0}, tmark = 0;
 #define KG_MARK() \
   if (trace && tid == 0) tmark = __builtin_amdgcn_s_memtime();
 #define KG_ACC(k) \
   if (trace && tid == 0) acc_t[k] += __builtin_amdgcn_s_memtime() - tmark;
-  double *x = vb, *dv = vb + N, *sdv = vb + 2 * N, *tau = vb + 3 * N;
-  double *gc = vb + 4 * N, *gs = vb + 6 * N, *ev = vb + 8 * N, *scal = vb + 9 * N;
-  int *perm = (int *)(scal + 16);
-  int *misc = perm + N;  // [0..1] a, [2..3] n per buffer, [4] fail
-
-  if (diagonal) {
-    // CMAES::eigen, diagonal branch: Q = I, diag = diag(M) (no sort)
-    for (int i = tid; i < N; i += nt) ev[i] = C[i * N + i];
-    __syncthreads();
-    if (tid == 0) {
-      double mn = ev[0], mx = ev[0];
-      for (int i = 1; i < N; i++) {
-        if (ev[i] < mn) mn = ev[i];
-        if (ev[i] > mx) mx = ev[i];
-      }
-      scal[0] = mn;
-      scal[1] = mx;
-    }
-    __syncthreads();
-    if (scal[0] <= 0.0) {
-      if (tid == 0) *eigenFailures += 1.0;
-      return;
-    }
-    for (int idx = tid; idx < N * N; idx += nt) B[idx] = (idx / N == idx % N) ? 1.0 : 0.0;
-    for (int i = tid; i < N; i += nt) D[i] = sqrt(ev[i]);
-    if (tid == 0) {
-      *minEig = scal[0];
-      *maxEig = scal[1];
-    }
-    return;
-  }
 
   // symmetrise from the lower triangle (CMAES.cpp.base:908-913)
   for (int idx = tid; idx < N * N; idx += nt) {
@@ -272,29 +244,6 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     M[i * lda + j] = (j <= i) ? C[i * N + j] : C[j * N + i];
   }
   __syncthreads();
-
-  if (N == 1) {
-    if (tid == 0) {
-      ev[0] = M[0];
-      perm[0] = 0;
-      scal[0] = ev[0];
-      scal[1] = ev[0];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      if (ev[0] <= 0.0)
-        *eigenFailures += 1.0;
-      else {
-        B[0] = 1.0;
-        D[0] = sqrt(ev[0]);
-        *minEig = ev[0];
-        *maxEig = ev[0];
-      }
-    }
-    return;
-  }
-
-  // ---------------------------------------------------------- phase A
   for (int i = 0; i + 2 < N; i++) {
     const int n = N - i - 1;
     double *v = M + (size_t)(i + 1) * lda + i;        // stride lda
@@ -346,9 +295,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
       if (lane == 0) {
         double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
         int branch = 0;
-        double xnorm = (n - 1 == 1) ? fabs(v[lda]) : scale_carry * sqrt(ssq);
-        if (n - 1 == 0) xnorm = 0.0;
-        if (n > 1 && xnorm != 0) {
+        const double xnorm = (n - 1 == 1) ? fabs(v[lda]) : scale_carry * sqrt(ssq);
+        if (xnorm != 0) {
           const double alpha = v[0];
           beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
           tau_i = (beta - alpha) / beta;
@@ -367,7 +315,7 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
         scal[2] = f2;
         scal[3] = beta;
         scal[4] = (double)branch;
-        tau[i] = tau_i;
+        tauOut[i] = tau_i;
       }
     }
     __syncthreads();
@@ -399,8 +347,6 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
         double p1[16], p2[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
-          // unconditional loads from clamped (valid) addresses, then select:
-          // keeps every LDS read of the chunk in flight at once
           const int q = q0 + u;
           const int r = max(n - 1 - q, 0), qc = min(q, n - 1);
           const double pa = (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j];
@@ -455,22 +401,31 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     __syncthreads();
     KG_ACC(3)
   }
-  // tau[N-2] is never set by the loop (GSL's tau has N-1 entries; the last
-  // one is unused by unpack)
-  // save Householder vectors to global, diag / subdiag to LDS
+  // Householder vectors, diag / sub-diagonal
   for (int idx = tid; idx < N * N; idx += nt) {
     const int i = idx / N, r = idx % N;
     if (i + 2 < N && r < N - i - 1) gH[(size_t)i * N + r] = M[(size_t)(i + 1 + r) * lda + i];
   }
   for (int i = tid; i < N; i += nt) {
-    dv[i] = M[(size_t)i * lda + i];
-    if (i + 1 < N) sdv[i] = M[(size_t)(i + 1) * lda + i];
+    dOut[i] = M[(size_t)i * lda + i];
+    if (i + 1 < N) sdOut[i] = M[(size_t)(i + 1) * lda + i];
   }
-  __syncthreads();
+  if (trace && tid == 0)
+    for (int k = 0; k < 4; k++) trace[k] += acc_t[k];
+#undef KG_MARK
+#undef KG_ACC
+}
 
-  KG_TRACE(1)
-  // ---------------------------------------------------------- phase B
-  // Qt[col][row] = Q[row][col] = I
+// Phase B: Q = H_0 ... H_{N-3} (gsl_linalg_symmtd_unpack via
+// householder_hm), built transposed (Qt[col][row]) and stored to gQt.
+template <bool kLds>
+__global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict__ gH,
+                                                 const double *__restrict__ tau, double *gQt) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lda = N + 1;
+  double *M = kLds ? smem : gQt;
+  double *h = kLds ? smem + (size_t)N * lda : smem;
   for (int idx = tid; idx < N * lda; idx += nt) {
     const int c = idx / lda, r = idx % lda;
     M[idx] = (r < N && c == r) ? 1.0 : 0.0;
@@ -480,9 +435,8 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
     const double ti = tau[i];
     if (ti == 0.0) continue;  // householder_hm returns early
     const int n = N - (i + 1);
-    for (int r = tid; r < n; r += nt) x[r] = gH[(size_t)i * N + r];
+    for (int r = tid; r < n; r += nt) h[r] = gH[(size_t)i * N + r];
     __syncthreads();
-    const double *h = x;
     for (int j = tid; j < n; j += nt) {
       double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
       double wj = col[0];
@@ -495,182 +449,304 @@ __global__ void __launch_bounds__(1024) k_symmv(int N, int diagonal, const doubl
           p[u] = (r0 + u < n) ? pr : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding: wj is never -0.0 after col[0]+... (see dsymv)
+        for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding is exact (see k_tridiag)
       }
       col[0] = col[0] - ti * wj;
       for (int r = 1; r < n; r++) col[r] = col[r] - ti * h[r] * wj;
     }
     __syncthreads();
   }
+  if (kLds)
+    for (int idx = tid; idx < N * lda; idx += nt) gQt[idx] = M[idx];
+}
 
-  KG_TRACE(2)
-  // ---------------------------------------------------------- phase C
-  if (tid == 0) {
-    chop_small(N, dv, sdv);
-    misc[0] = misc[1] = 0;
-    misc[2] = misc[3] = 0;
-    misc[4] = N - 1;  // b
-    misc[5] = 0;      // steps
-  }
-  __syncthreads();
-  const int maxSteps = 64 * N + 1000;
-  for (int step = 0;; step++) {
-    const int buf = step & 1;
-    if (tid == 0) {
-      int b = misc[4];
-      int nblk = -1;
-      while (b > 0) {
-        if (sdv[b - 1] == 0.0 || isnan(sdv[b - 1])) {
-          b--;
-          continue;
-        }
-        int a = b - 1;
-        while (a > 0) {
-          if (sdv[a - 1] == 0.0) break;
-          a--;
-        }
-        nblk = b - a + 1;
-        KG_MARK()
-        qrstep(nblk, dv + a, sdv + a, gc + buf * N, gs + buf * N);
-        chop_small(nblk, dv + a, sdv + a);
-        KG_ACC(4)
-        nrot += nblk - 1;
-        misc[buf] = a;
-        if (++misc[5] > maxSteps) {
-          atomicOr(errors, KG_ERR_EIGEN);
-          nblk = -1;
-          b = 0;
-        }
-        break;
-      }
-      misc[4] = b;
-      misc[2 + buf] = nblk;  // -1: converged
-    } else if (tid >= 64 && step > 0 && !(trace && trace[15] == 1)) {
-      const int pb = buf ^ 1;
-      const int nblk = misc[2 + pb];
-      if (nblk > 0) {
-        const int a = misc[pb];
-        const double *c_ = gc + pb * N, *s_ = gs + pb * N;
-        for (int k = tid - 64; k < N; k += nt - 64) {
-          double qi = M[(size_t)a * lda + k];
-          for (int i = 0; i + 1 < nblk; i++) {
-            const double c = c_[i], s = s_[i];
-            const double qj = M[(size_t)(a + i + 1) * lda + k];
-            M[(size_t)(a + i) * lda + k] = qi * c - qj * s;
-            qi = qi * s + qj * c;
-          }
-          M[(size_t)(a + nblk - 1) * lda + k] = qi;
-        }
-      }
-    }
-    __syncthreads();
-    if (misc[2 + buf] < 0) break;
-  }
+// ------------------------------------------------------------------------
+// Phase C: the implicit-shift QR chase (eigen/symmv.c main loop + qrstep)
+// on the tridiagonal d/sd.  It only produces the rotation sequence: per QR
+// step a header (a, n) and n-1 Givens pairs (c, s); then the ABS_ASC
+// selection sort gives eval (sorted) and the column permutation.
+struct EigRec {
+  int *hdr;     // 2 per step: a, n
+  double *cs;   // 2 per rotation
+  int *meta;    // [0] steps [1] rotations [2] overflow/error
+  double *eval; // N sorted eigenvalues
+  int *perm;    // N: sorted column i = unsorted column perm[i]
+};
 
-  KG_TRACE(3)
-  if (trace && tid == 0) trace[6] = (unsigned long long)misc[5];
-  // ---------------------------------------------------------- phase D
-  for (int i = tid; i < N; i += nt) {
-    ev[i] = dv[i];
-    perm[i] = i;
-  }
-  __syncthreads();
-  if (wid == 0) {
-    for (int i = 0; i + 1 < N; i++) {
-      // first index of min |e| over positions >= i (strict <, as GSL)
-      double bv = INFINITY;
-      int bi = 0x7fffffff;
-      for (int j = i + lane; j < N; j += 64) {
-        const double a = fabs(ev[j]);
-        if (a < bv || (a == bv && j < bi)) {
-          bv = a;
-          bi = j;
-        }
-      }
-      for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(bv, off, 64);
-        const int oi = __shfl_xor(bi, off, 64);
-        if (ov < bv || (ov == bv && oi < bi)) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      // the arg-min must still honour 'strict <' against ev[i] itself
-      if (lane == 0) {
-        int k = i;
-        if (fabs(ev[bi]) < fabs(ev[i])) k = bi;
-        if (k != i) {
-          const double t = ev[i];
-          ev[i] = ev[k];
-          ev[k] = t;
-          const int p = perm[i];
-          perm[i] = perm[k];
-          perm[k] = p;
-        }
-      }
-      // single wave: order lane 0's LDS updates before the next sweep
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      __builtin_amdgcn_wave_barrier();
+EigenSolver::Rec::operator EigRec() const { return EigRec{hdr, cs, meta, eval, perm}; }
+
+__host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, int maxRot, double *gc, double *gs) {
+  chop_small(N, d, sd);
+  int b = N - 1, steps = 0, rot = 0, err = 0;
+  while (b > 0) {
+    if (sd[b - 1] == 0.0 || sd[b - 1] != sd[b - 1]) {  // == 0 or NaN
+      b--;
+      continue;
     }
-    if (lane == 0) {
-      double mn = ev[0], mx = ev[0];
-      for (int i = 1; i < N; i++) {
-        if (ev[i] < mn) mn = ev[i];
-        if (ev[i] > mx) mx = ev[i];
+    int a = b - 1;
+    while (a > 0) {
+      if (sd[a - 1] == 0.0) break;
+      a--;
+    }
+    const int nb = b - a + 1;
+    if (rot + nb - 1 > maxRot) {
+      err = 1;
+      break;
+    }
+    qrstep(nb, d + a, sd + a, gc, gs);
+    for (int k = 0; k + 1 < nb; k++) {
+      r.cs[2 * (rot + k)] = gc[k];
+      r.cs[2 * (rot + k) + 1] = gs[k];
+    }
+    r.hdr[2 * steps] = a;
+    r.hdr[2 * steps + 1] = nb;
+    steps++;
+    rot += nb - 1;
+    chop_small(nb, d + a, sd + a);
+  }
+  // gsl_eigen_symmv_sort(ABS_ASC): selection sort, strict < on |e|
+  for (int i = 0; i < N; i++) {
+    r.eval[i] = d[i];
+    r.perm[i] = i;
+  }
+  for (int i = 0; i + 1 < N; i++) {
+    int k = i;
+    double ek = r.eval[i];
+    for (int j = i + 1; j < N; j++)
+      if (fabs(r.eval[j]) < fabs(ek)) {
+        k = j;
+        ek = r.eval[j];
       }
-      scal[6] = mn;
-      scal[7] = mx;
+    if (k != i) {
+      const double t = r.eval[i];
+      r.eval[i] = r.eval[k];
+      r.eval[k] = t;
+      const int p = r.perm[i];
+      r.perm[i] = r.perm[k];
+      r.perm[k] = p;
     }
   }
+  r.meta[0] = steps;
+  r.meta[1] = rot;
+  r.meta[2] = err;
+  return err;
+}
+
+// device variant of phase C: one lane (the chase is a strict dependency
+// chain; see DESIGN.md for why the default runs it on the host core)
+__global__ void __launch_bounds__(64) k_chase(int N, const double *__restrict__ dIn, const double *__restrict__ sdIn,
+                                              EigRec r, int maxRot, double *work) {
+  if (threadIdx.x != 0) return;
+  double *d = work, *sd = work + N, *gc = work + 2 * N, *gs = work + 3 * N;
+  for (int i = 0; i < N; i++) {
+    d[i] = dIn[i];
+    if (i + 1 < N) sd[i] = sdIn[i];
+  }
+  qr_chase(N, d, sd, r, maxRot, gc, gs);
+}
+
+// Phase C application + phase D write-back (CMAES::updateEigensystem).
+// Row k of Q (a thread) replays every Givens rotation in GSL's order:
+// (Q[k][a+i], Q[k][a+i+1]) = (qi c - qj s, qi s + qj c).
+template <bool kLds>
+__global__ void __launch_bounds__(1024) k_apply(int N, const double *__restrict__ gQt, double *gWork, EigRec r,
+                                                double *__restrict__ B, double *__restrict__ D, double *minEig,
+                                                double *maxEig, double *eigenFailures, unsigned int *errors) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lda = N + 1;
+  double *M = kLds ? smem : gWork;
+  if (kLds)
+    for (int idx = tid; idx < N * lda; idx += nt) M[idx] = gQt[idx];
   __syncthreads();
-  if (scal[6] <= 0.0) {
+  const int steps = r.meta[0];
+  if (r.meta[2]) {
+    if (tid == 0) atomicOr(errors, KG_ERR_EIGEN);
+    return;
+  }
+  for (int k = tid; k < N; k += nt) {
+    int ro = 0;
+    for (int t = 0; t < steps; t++) {
+      const int a = r.hdr[2 * t], nb = r.hdr[2 * t + 1];
+      double qi = M[(size_t)a * lda + k];
+      for (int i = 0; i + 1 < nb; i++) {
+        const double c = r.cs[2 * (ro + i)], s = r.cs[2 * (ro + i) + 1];
+        const double qj = M[(size_t)(a + i + 1) * lda + k];
+        M[(size_t)(a + i) * lda + k] = qi * c - qj * s;
+        qi = qi * s + qj * c;
+      }
+      M[(size_t)(a + nb - 1) * lda + k] = qi;
+      ro += nb - 1;
+    }
+  }
+  __syncthreads();
+  // updateEigensystem: min/max eigenvalue; keep old B, D if min <= 0
+  double mn = r.eval[0], mx = r.eval[0];
+  for (int i = 1; i < N; i++) {
+    mn = fmin(mn, r.eval[i]);
+    mx = fmax(mx, r.eval[i]);
+  }
+  if (mn <= 0.0) {
     if (tid == 0) *eigenFailures += 1.0;
     return;
   }
   for (int idx = tid; idx < N * N; idx += nt) {
     const int d = idx / N, e = idx % N;
-    B[idx] = M[(size_t)perm[e] * lda + d];
+    B[idx] = M[(size_t)r.perm[e] * lda + d];
   }
-  for (int i = tid; i < N; i += nt) D[i] = sqrt(ev[i]);
+  for (int i = tid; i < N; i += nt) D[i] = sqrt(r.eval[i]);
   if (tid == 0) {
-    *minEig = scal[6];
-    *maxEig = scal[7];
+    *minEig = mn;
+    *maxEig = mx;
   }
-  KG_TRACE(4)
-  if (trace && tid == 0) {
-    for (int k = 0; k < 5; k++) trace[7 + k] = acc_t[k];
-    trace[12] = nrot;
-  }
-#undef KG_TRACE
-#undef KG_MARK
-#undef KG_ACC
 }
 
-size_t symmv_lds_bytes(int N, bool lds_mats) {
-  size_t v = (size_t)(9 * N + 16) * sizeof(double) + (size_t)(N + 8) * sizeof(int);
-  if (lds_mats) v += (size_t)N * (N + 1) * sizeof(double);
-  return (v + 15) & ~(size_t)15;
+// diagonal covariance (CMAES::eigen diagonal branch): Q = I, eval = diag(C)
+__global__ void __launch_bounds__(256) k_eigen_diag(int N, const double *__restrict__ C, double *B, double *D,
+                                                    double *minEig, double *maxEig, double *eigenFailures) {
+  __shared__ double mnmx[2];
+  if (threadIdx.x == 0) {
+    double mn = C[0], mx = C[0];
+    for (int i = 1; i < N; i++) {
+      const double v = C[(size_t)i * N + i];
+      if (v < mn) mn = v;
+      if (v > mx) mx = v;
+    }
+    mnmx[0] = mn;
+    mnmx[1] = mx;
+  }
+  __syncthreads();
+  if (mnmx[0] <= 0.0) {
+    if (threadIdx.x == 0) *eigenFailures += 1.0;
+    return;
+  }
+  for (int idx = threadIdx.x; idx < N * N; idx += blockDim.x) B[idx] = (idx / N == idx % N) ? 1.0 : 0.0;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) D[i] = sqrt(C[(size_t)i * N + i]);
+  if (threadIdx.x == 0) {
+    *minEig = mnmx[0];
+    *maxEig = mnmx[1];
+  }
 }
 
-int launch_symmv(int N, int diagonal, const double *C, double *gA, double *gH, double *B, double *D, double *minEig,
-                 double *maxEig, double *eigenFailures, unsigned int *errors, unsigned long long *trace,
-                 hipStream_t s) {
-  KG_CHECK(N >= 1 && N <= 960, "device eigensolver supports 1 <= N <= 960");
-  const bool lds = (symmv_lds_bytes(N, true) <= 160 * 1024);
-  const size_t bytes = symmv_lds_bytes(N, lds);
-  static bool attr_set = false;
-  if (!attr_set) {
-    KG_HIP(hipFuncSetAttribute((const void *)k_symmv<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    KG_HIP(hipFuncSetAttribute((const void *)k_symmv<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+// ------------------------------------------------------------------------
+// Orchestration
+size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
+bool eig_use_lds(int N) { return eig_mat_bytes(N) + (size_t)(N + 16) * sizeof(double) + 256 <= 160 * 1024; }
+
+int EigenSolver::init(int N_, bool hostChase_) {
+  N = N_;
+  hostChase = hostChase_;
+  maxRot = 64 * N * N + 4096;
+  const size_t mat = (size_t)N * (N + 1);
+  KG_HIP(hipMalloc(&gA, mat * sizeof(double)));
+  KG_HIP(hipMalloc(&gH, (size_t)N * N * sizeof(double)));
+  KG_HIP(hipMalloc(&gQt, mat * sizeof(double)));
+  KG_HIP(hipMalloc(&gWork, mat * sizeof(double)));
+  KG_HIP(hipMalloc(&tau, (size_t)N * sizeof(double)));
+  KG_HIP(hipMalloc(&dsd, 2 * (size_t)N * sizeof(double)));
+  KG_HIP(hipMalloc(&chaseWork, 4 * (size_t)N * sizeof(double)));
+  KG_HIP(hipMalloc(&dev.hdr, 2 * (size_t)(maxRot + N) * sizeof(int)));
+  KG_HIP(hipMalloc(&dev.cs, 2 * (size_t)maxRot * sizeof(double)));
+  KG_HIP(hipMalloc(&dev.meta, 4 * sizeof(int)));
+  KG_HIP(hipMalloc(&dev.eval, (size_t)N * sizeof(double)));
+  KG_HIP(hipMalloc(&dev.perm, (size_t)N * sizeof(int)));
+  KG_HIP(hipMemset(dev.meta, 0, 4 * sizeof(int)));
+  if (hostChase) {
+    KG_HIP(hipHostMalloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&host.hdr, 2 * (size_t)(maxRot + N) * sizeof(int), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&host.cs, 2 * (size_t)maxRot * sizeof(double), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&host.meta, 4 * sizeof(int), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&host.eval, (size_t)N * sizeof(double), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&host.perm, (size_t)N * sizeof(int), hipHostMallocDefault));
+    KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
+    hgc.resize(N);
+    hgs.resize(N);
+  } else {
+    KG_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
+    KG_HIP(hipEventCreateWithFlags(&ev_chase, hipEventDisableTiming));
   }
+  lds = eig_use_lds(N);
+  const int attr = 160 * 1024;
+  KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
+  KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
+  return 0;
+}
+
+EigenSolver::~EigenSolver() {
+  for (void *p : {(void *)gA, (void *)gH, (void *)gQt, (void *)gWork, (void *)tau, (void *)dsd, (void *)chaseWork,
+                  (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm})
+    if (p) (void)hipFree(p);
+  for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
+                  (void *)host.perm})
+    if (p) (void)hipHostFree(p);
+  if (side) (void)hipStreamDestroy(side);
+  if (ev_dsd) (void)hipEventDestroy(ev_dsd);
+  if (ev_chase) (void)hipEventDestroy(ev_chase);
+}
+
+int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+                     double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
+  if (diagonal) {
+    hipLaunchKernelGGL(k_eigen_diag, dim3(1), dim3(256), 0, s, N, C, B, D, minEig, maxEig, eigenFailures);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
+  const size_t matb = lds ? eig_mat_bytes(N) : 0;
+  double *d = dsd, *sd = dsd + N;
+  if (prof) prof(profCtx, "eigen_tridiag", 0);
   if (lds)
-    hipLaunchKernelGGL(k_symmv<true>, dim3(1), dim3(1024), bytes, s, N, diagonal, C, gA, gH, B, D, minEig, maxEig,
-                       eigenFailures, errors, trace);
+    hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), matb + (N + 16) * sizeof(double), s, N, C, gA, gH, tau,
+                       d, sd, trace);
   else
-    hipLaunchKernelGGL(k_symmv<false>, dim3(1), dim3(1024), bytes, s, N, diagonal, C, gA, gH, B, D, minEig, maxEig,
-                       eigenFailures, errors, trace);
+    hipLaunchKernelGGL(k_tridiag<false>, dim3(1), dim3(1024), (N + 16) * sizeof(double), s, N, C, gA, gH, tau, d, sd,
+                       trace);
   KG_HIP(hipGetLastError());
+  if (prof) prof(profCtx, "eigen_tridiag", 1);
+  EigRec devRec = dev;
+  if (hostChase) {
+    KG_HIP(hipMemcpyAsync(h_dsd, dsd, 2 * (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    KG_HIP(hipEventRecord(ev_dsd, s));
+  } else {
+    KG_HIP(hipEventRecord(ev_dsd, s));
+    KG_HIP(hipStreamWaitEvent(side, ev_dsd, 0));
+    hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, side, N, d, sd, devRec, maxRot, chaseWork);
+    KG_HIP(hipGetLastError());
+    KG_HIP(hipEventRecord(ev_chase, side));
+  }
+  if (prof) prof(profCtx, "eigen_unpack", 0);
+  if (lds)
+    hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + N * sizeof(double), s, N, gH, tau, gQt);
+  else
+    hipLaunchKernelGGL(k_unpack<false>, dim3(1), dim3(1024), N * sizeof(double), s, N, gH, tau, gQt);
+  KG_HIP(hipGetLastError());
+  if (prof) prof(profCtx, "eigen_unpack", 1);
+  if (hostChase) {
+    // the GPU unpacks Q while this core runs the serial Givens chase
+    KG_HIP(hipEventSynchronize(ev_dsd));
+    if (prof) prof(profCtx, "eigen_chase_host", 2);
+    EigRec hr = host;
+    qr_chase(N, h_dsd, h_dsd + N, hr, maxRot, hgc.data(), hgs.data());
+    if (prof) prof(profCtx, "eigen_chase_host", 3);
+    const int steps = host.meta[0], rot = host.meta[1];
+    KG_HIP(hipMemcpyAsync(dev.meta, host.meta, 4 * sizeof(int), hipMemcpyHostToDevice, s));
+    KG_HIP(hipMemcpyAsync(dev.hdr, host.hdr, 2 * (size_t)steps * sizeof(int), hipMemcpyHostToDevice, s));
+    if (rot) KG_HIP(hipMemcpyAsync(dev.cs, host.cs, 2 * (size_t)rot * sizeof(double), hipMemcpyHostToDevice, s));
+    KG_HIP(hipMemcpyAsync(dev.eval, host.eval, (size_t)N * sizeof(double), hipMemcpyHostToDevice, s));
+    KG_HIP(hipMemcpyAsync(dev.perm, host.perm, (size_t)N * sizeof(int), hipMemcpyHostToDevice, s));
+  } else {
+    KG_HIP(hipStreamWaitEvent(s, ev_chase, 0));
+  }
+  if (prof) prof(profCtx, "eigen_apply", 0);
+  if (lds)
+    hipLaunchKernelGGL(k_apply<true>, dim3(1), dim3(1024), matb, s, N, gQt, gWork, devRec, B, D, minEig, maxEig,
+                       eigenFailures, errors);
+  else
+    hipLaunchKernelGGL(k_apply<false>, dim3(1), dim3(1024), 0, s, N, gQt, gQt, devRec, B, D, minEig, maxEig,
+                       eigenFailures, errors);
+  KG_HIP(hipGetLastError());
+  if (prof) prof(profCtx, "eigen_apply", 1);
   return 0;
 }
 

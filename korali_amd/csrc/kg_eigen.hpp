@@ -1,0 +1,47 @@
+// kg_eigen.hpp — GSL-faithful symmetric eigensolver (gsl_eigen_symmv +
+// gsl_eigen_symmv_sort ABS_ASC) for CMAES::updateEigensystem.
+#pragma once
+
+#include <vector>
+
+#include "kg_common.hpp"
+
+namespace kg {
+
+struct EigRec;
+
+// profiling callback: phase 0/1 = begin/end of a device stage (events on the
+// stream), 2/3 = begin/end of a host stage (wall clock)
+typedef void (*ProfileFn)(void *ctx, const char *stage, int phase);
+
+class EigenSolver {
+ public:
+  ~EigenSolver();
+  // hostChase: run the serial implicit-QR Givens recurrence on the calling
+  // host core (overlapped with the device unpack); otherwise on one lane.
+  int init(int N, bool hostChase);
+  int run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+          double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
+  unsigned long long *trace = nullptr;  // optional device counters (k_tridiag sub-phases)
+  bool hostChase = true;
+
+ private:
+  int N = 0, maxRot = 0;
+  bool lds = true;
+  double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
+         *chaseWork = nullptr;
+  struct Rec {
+    int *hdr = nullptr;
+    double *cs = nullptr;
+    int *meta = nullptr;
+    double *eval = nullptr;
+    int *perm = nullptr;
+    operator EigRec() const;
+  } dev, host;
+  double *h_dsd = nullptr;
+  std::vector<double> hgc, hgs;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_dsd = nullptr, ev_chase = nullptr;
+};
+
+}  // namespace kg

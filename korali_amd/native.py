@@ -34,7 +34,7 @@ class _CmaesCfg(C.Structure):
         ("initial_value", C.POINTER(C.c_double)), ("initial_std", C.POINTER(C.c_double)),
         ("min_std_update", C.POINTER(C.c_double)),
         ("normal_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("cov_mode", C.c_int), ("device", C.c_int),
-        ("store_bdz", C.c_int),
+        ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int),
     ]
 
 
@@ -135,7 +135,7 @@ class CmaesDevice:
                  initial_std=None, min_std_update=None, normal_seed=0, uniform_seed=0, cov_mode="exact",
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
-                 initial_cumulative_covariance=-1.0, device=0, store_bdz=False):
+                 initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host"):
         L = lib()
         self.N, self.lam = int(N), int(lam)
         self.mu = int(mu) if mu else self.lam // 2
@@ -157,6 +157,7 @@ class CmaesDevice:
         cfg.normal_seed, cfg.uniform_seed = int(normal_seed), int(uniform_seed)
         cfg.cov_mode = COV_MODES[cov_mode.lower()] if isinstance(cov_mode, str) else int(cov_mode)
         cfg.device, cfg.store_bdz = int(device), int(store_bdz)
+        cfg.eigen_device_chase = 1 if eigen_chase == "device" else 0
         h = C.c_void_p()
         check(L.kg_cmaes_create(C.byref(cfg), C.byref(h)))
         self.h = h

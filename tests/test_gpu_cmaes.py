@@ -90,21 +90,25 @@ def test_seeded_100_generations_match_reference_fixture():
     assert dev.get_rng(0).hex().upper() == by_gen(100)["Solver"]["Normal Generator"]["Range"]
 
 
-def oracle_and_device(Nv, lam, objective, gens, cov_mode="exact", seed=1337, x0=0.0, s0=1.0):
+def oracle_and_device(Nv, lam, objective, gens, cov_mode="exact", seed=1337, x0=0.0, s0=1.0, eigen_chase="host"):
     o = R.CMAES(Nv, lam, 0)
     o["Initial Value"] = np.full(Nv, x0)
     o["Initial Standard Deviation"] = np.full(Nv, s0)
     R.lib().kr_rng_seed(o.rng(0).ptr, seed)
     R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
     dev = device_solver(Nv, lam, initial_value=np.full(Nv, x0), initial_std=np.full(Nv, s0), normal_seed=seed,
-                        uniform_seed=seed + 1, cov_mode=cov_mode)
+                        uniform_seed=seed + 1, cov_mode=cov_mode, eigen_chase=eigen_chase)
     return o, dev
 
 
-@pytest.mark.parametrize("Nv,lam,objective,gens", [(8, 16, "rosenbrock", 30), (32, 256, "ackley", 8),
-                                                   (128, 4096, "rosenbrock", 3)])
-def test_seeded_run_matches_oracle_bit_exact(Nv, lam, objective, gens):
-    o, dev = oracle_and_device(Nv, lam, objective, gens)
+@pytest.mark.parametrize("Nv,lam,objective,gens,chase", [(8, 16, "rosenbrock", 30, "host"),
+                                                         (32, 256, "ackley", 8, "host"),
+                                                         (128, 4096, "rosenbrock", 3, "host"),
+                                                         (128, 4096, "rosenbrock", 2, "device"),
+                                                         (200, 512, "rosenbrock", 2, "host")])
+def test_seeded_run_matches_oracle_bit_exact(Nv, lam, objective, gens, chase):
+    """N=200 exercises the global-memory (non-LDS) eigensolver variant."""
+    o, dev = oracle_and_device(Nv, lam, objective, gens, eigen_chase=chase)
     for g in range(1, gens + 1):
         o.generation(g, objective)
         dev.generation(g, objective)
