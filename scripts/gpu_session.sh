@@ -23,6 +23,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;
     benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac
 done
 echo "session done"
