@@ -125,15 +125,22 @@ enum kg_likelihood { KG_LIK_GAUSSIAN = 0 }; /* -0.5*sum(x^2), model.py:32-37 */
 typedef struct {
   size_t variable_count;  /* N */
   size_t population_size; /* P ("Population Size") */
-  double max_chain_length;               /* must be 1 on device for now */
-  double default_burn_in;                /* must be 0 on device for now */
+  double max_chain_length;               /* must be 1 on device for now ("Max Chain Length") */
+  double default_burn_in;                /* must be 0 on device for now ("Default Burn In") */
   double target_cov;                     /* "Target Coefficient Of Variation" */
   double covariance_scaling;             /* "Covariance Scaling" */
-  double min_annealing_exponent_update;
-  double max_annealing_exponent_update;
-  const double *prior_min;               /* N: Univariate/Uniform priors */
+  double min_annealing_exponent_update;  /* "Min Annealing Exponent Update" */
+  double max_annealing_exponent_update;  /* "Max Annealing Exponent Update" */
+  const double *prior_min;               /* N: Univariate/Uniform prior of each variable */
   const double *prior_max;               /* N */
-  const uint64_t *prior_seeds;           /* N seeds of the prior generators */
+  /* Korali draws variable d's generation-1 candidate from the distribution
+   * object _k->_distributions[_variables[d]->_distributionIndex]
+   * (TMCMC.cpp.base:218-220); variables that share a distribution share its
+   * RNG.  prior_distribution[d] is that index (NULL: variable d uses
+   * distribution d); prior_seeds[k] seeds distribution k. */
+  const int *prior_distribution;         /* N or NULL */
+  size_t distribution_count;             /* entries of prior_seeds (0: N) */
+  const uint64_t *prior_seeds;
   uint64_t multinomial_seed, multivariate_seed, uniform_seed;
   int likelihood;                        /* enum kg_likelihood */
   int device;
@@ -141,19 +148,28 @@ typedef struct {
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
 int kg_tmcmc_destroy(kg_tmcmc_t h);
+/* one whole generation (TMCMC::runGeneration) with the builtin likelihood */
 int kg_tmcmc_generation(kg_tmcmc_t h, size_t generation);
 int kg_tmcmc_synchronize(kg_tmcmc_t h);
 int kg_tmcmc_field_size(kg_tmcmc_t h, const char *name, size_t *n);
 int kg_tmcmc_get_field(kg_tmcmc_t h, const char *name, double *out, size_t n);
 int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t n);
-/* which: 0 Multinomial, 1 Multivariate, 2 Uniform, 3+k prior k */
+/* which: 0 Multinomial, 1 Multivariate, 2 Uniform, 3+k prior distribution k */
 int kg_tmcmc_get_rng(kg_tmcmc_t h, int which, void *state5000);
 int kg_tmcmc_set_rng(kg_tmcmc_t h, int which, const void *state5000);
-/* teacher-forcing hooks used by the parity tests: run the stages of one
- * generation separately, with externally supplied log-likelihoods */
+/* the stages of one generation:
+ *   prepare  = (gen 1: setInitialConfiguration :21-105) + prepareGeneration :159-227
+ *   evaluate = Bayesian::evaluate with the builtin likelihood (bayesian.cpp.base:24-84)
+ *   process  = processCandidate for every chain :229-252 + processGeneration :254-381 */
 int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation);
 int kg_tmcmc_evaluate(kg_tmcmc_t h);
 int kg_tmcmc_process(kg_tmcmc_t h, size_t generation);
+/* host-callback likelihoods (KORALI_START/WAITALL of TMCMC::runGeneration
+ * :114-144): read the P x N candidates, hand back logPrior / logLikelihood */
+int kg_tmcmc_get_candidates(kg_tmcmc_t h, double *X, size_t ld);
+int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double *log_likelihood);
+int kg_tmcmc_profile(kg_tmcmc_t h, int enable);
+int kg_tmcmc_profile_read(kg_tmcmc_t h, const char *stage, double *ms_total, size_t *count);
 
 #ifdef __cplusplus
 }

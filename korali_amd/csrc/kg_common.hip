@@ -22,17 +22,35 @@ static void dd_recip(double q, double &hi, double &lo) {
   lo = r / q;
 }
 
+static dd_tables make_tables() {
+  dd_tables t;
+  for (int j = 0; j < 22; j++) dd_recip(2.0 * j + 1.0, t.inv_odd_hi[j], t.inv_odd_lo[j]);
+  t.inv_int_hi[0] = t.inv_int_lo[0] = 0.0;
+  for (int j = 1; j < 15; j++) dd_recip((double)j, t.inv_int_hi[j], t.inv_int_lo[j]);
+  return t;
+}
+
+static const dd_tables &host_tables() {
+  static const dd_tables t = make_tables();
+  return t;
+}
+
 void upload_dd_tables() {
   static std::once_flag once;
   static bool ok = false;
   std::call_once(once, [] {
-    dd_tables t;
-    for (int j = 0; j < 22; j++) dd_recip(2.0 * j + 1.0, t.inv_odd_hi[j], t.inv_odd_lo[j]);
-    t.inv_int_hi[0] = t.inv_int_lo[0] = 0.0;
-    for (int j = 1; j < 15; j++) dd_recip((double)j, t.inv_int_hi[j], t.inv_int_lo[j]);
+    const dd_tables &t = host_tables();
     ok = hipMemcpyToSymbol(HIP_SYMBOL(c_dd_tab), &t, sizeof(t)) == hipSuccess;
   });
   (void)ok;
+}
+
+double host_log_cr(double x) {
+  if (!(x > 0.0) || std::isinf(x)) return std::log(x);
+  if (x == 1.0) return 0.0;
+  if (x < 2.2250738585072014e-308) return std::log(x);
+  const dd r = dd_log_tab(x, host_tables());
+  return r.hi + r.lo;
 }
 
 }  // namespace kg

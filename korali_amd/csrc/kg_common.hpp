@@ -109,8 +109,10 @@ void upload_dd_tables();  // host
 constexpr double LN2_HI = 6.93147180559945286227e-01;
 constexpr double LN2_LO = 2.31904681384629955842e-17;
 
-// log(x), x finite > 0 normal, as a double-double.
-__device__ inline dd dd_log(double x) {
+// log(x), x finite > 0 normal, as a double-double.  The table is passed in
+// so that the host (BTPE, log-evidence) evaluates the very same function.
+template <class Tab>
+__host__ __device__ inline dd dd_log_tab(double x, const Tab &t) {
   int k;
   double m = frexp(x, &k);  // x = m 2^k, m in [0.5, 1)
   if (m < 0.70710678118654752440) {
@@ -120,12 +122,17 @@ __device__ inline dd dd_log(double x) {
   // s = (m-1)/(m+1); m-1 exact (Sterbenz)
   dd s = dd_div(dd{m - 1.0, 0.0}, dd_ts(m, 1.0));
   dd z = dd_mul(s, s);
-  dd p{c_dd_tab.inv_odd_hi[21], c_dd_tab.inv_odd_lo[21]};
+  dd p{t.inv_odd_hi[21], t.inv_odd_lo[21]};
 #pragma unroll
-  for (int j = 20; j >= 0; j--) p = dd_add(dd_mul(p, z), dd{c_dd_tab.inv_odd_hi[j], c_dd_tab.inv_odd_lo[j]});
+  for (int j = 20; j >= 0; j--) p = dd_add(dd_mul(p, z), dd{t.inv_odd_hi[j], t.inv_odd_lo[j]});
   p = dd_mul(dd_mul_d(s, 2.0), p);
   return dd_add(dd_mul_d(dd{LN2_HI, LN2_LO}, (double)k), p);
 }
+
+__device__ inline dd dd_log(double x) { return dd_log_tab(x, c_dd_tab); }
+
+// host twin of log_cr (same double-double evaluation, host copy of the table)
+double host_log_cr(double x);
 
 // correctly rounded log for the inputs the solvers produce (finite, > 0)
 __device__ inline double log_cr(double x) {

@@ -44,6 +44,7 @@ class _TmcmcCfg(C.Structure):
         ("default_burn_in", C.c_double), ("target_cov", C.c_double), ("covariance_scaling", C.c_double),
         ("min_annealing_exponent_update", C.c_double), ("max_annealing_exponent_update", C.c_double),
         ("prior_min", C.POINTER(C.c_double)), ("prior_max", C.POINTER(C.c_double)),
+        ("prior_distribution", C.POINTER(C.c_int)), ("distribution_count", C.c_size_t),
         ("prior_seeds", C.POINTER(C.c_uint64)), ("multinomial_seed", C.c_uint64),
         ("multivariate_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("likelihood", C.c_int),
         ("device", C.c_int),
@@ -59,7 +60,8 @@ EXPORTED = [
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
-    "kg_tmcmc_evaluate", "kg_tmcmc_process",
+    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
+    "kg_tmcmc_profile", "kg_tmcmc_profile_read",
 ]
 
 
@@ -102,6 +104,10 @@ def lib():
         L.kg_tmcmc_set_field.argtypes = [vp, cp, dp, sz]
         L.kg_tmcmc_get_rng.argtypes = [vp, ip, vp]
         L.kg_tmcmc_set_rng.argtypes = [vp, ip, vp]
+        L.kg_tmcmc_get_candidates.argtypes = [vp, dp, sz]
+        L.kg_tmcmc_set_evaluations.argtypes = [vp, dp, dp]
+        L.kg_tmcmc_profile.argtypes = [vp, ip]
+        L.kg_tmcmc_profile_read.argtypes = [vp, cp, dp, C.POINTER(sz)]
         _LIB = L
     return _LIB
 
@@ -252,4 +258,113 @@ class CmaesDevice:
     def profile_read(self, stage):
         ms, n = C.c_double(), C.c_size_t()
         check(self._L.kg_cmaes_profile_read(self.h, stage.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+class TmcmcDevice:
+    """One TMCMC sampler instance (Version "TMCMC") on one MI355X (kg_tmcmc_t).
+
+    prior_min / prior_max: the Univariate/Uniform prior of every variable;
+    prior_distribution[d]: index of the distribution object variable d draws
+    from (variables sharing a distribution share its generator); prior_seeds[k]:
+    seed of distribution k.  Generator indices for get_rng / set_rng:
+    0 Multinomial, 1 Multivariate, 2 Uniform, 3 + k prior distribution k."""
+
+    def __init__(self, N, P, prior_min, prior_max, prior_seeds=None, prior_distribution=None,
+                 multinomial_seed=0, multivariate_seed=0, uniform_seed=0, target_cov=1.0, covariance_scaling=0.04,
+                 min_annealing_exponent_update=1e-5, max_annealing_exponent_update=1.0, max_chain_length=1,
+                 default_burn_in=0, likelihood=0, device=0):
+        L = lib()
+        self.N, self.P = int(N), int(P)
+        pdist = (np.arange(self.N, dtype=np.int32) if prior_distribution is None
+                 else np.ascontiguousarray(prior_distribution, dtype=np.int32))
+        ndist = int(pdist.max()) + 1
+        seeds = np.zeros(ndist, dtype=np.uint64) if prior_seeds is None else np.ascontiguousarray(
+            np.broadcast_to(np.asarray(prior_seeds, dtype=np.uint64), (ndist,)))
+        self._arrays = [_vec(prior_min, self.N, 0.0), _vec(prior_max, self.N, 1.0), pdist, seeds]
+        cfg = _TmcmcCfg()
+        cfg.variable_count, cfg.population_size = self.N, self.P
+        cfg.max_chain_length, cfg.default_burn_in = float(max_chain_length), float(default_burn_in)
+        cfg.target_cov, cfg.covariance_scaling = float(target_cov), float(covariance_scaling)
+        cfg.min_annealing_exponent_update = float(min_annealing_exponent_update)
+        cfg.max_annealing_exponent_update = float(max_annealing_exponent_update)
+        cfg.prior_min, cfg.prior_max = _dptr(self._arrays[0]), _dptr(self._arrays[1])
+        cfg.prior_distribution = pdist.ctypes.data_as(C.POINTER(C.c_int))
+        cfg.distribution_count = ndist
+        cfg.prior_seeds = seeds.ctypes.data_as(C.POINTER(C.c_uint64))
+        cfg.multinomial_seed, cfg.multivariate_seed, cfg.uniform_seed = (int(multinomial_seed),
+                                                                        int(multivariate_seed), int(uniform_seed))
+        cfg.likelihood, cfg.device = int(likelihood), int(device)
+        h = C.c_void_p()
+        check(L.kg_tmcmc_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.kg_tmcmc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare(self, generation):
+        check(self._L.kg_tmcmc_prepare(self.h, int(generation)))
+
+    def evaluate(self):
+        check(self._L.kg_tmcmc_evaluate(self.h))
+
+    def process(self, generation):
+        check(self._L.kg_tmcmc_process(self.h, int(generation)))
+
+    def generation(self, generation):
+        check(self._L.kg_tmcmc_generation(self.h, int(generation)))
+
+    def synchronize(self):
+        check(self._L.kg_tmcmc_synchronize(self.h))
+
+    def candidates(self):
+        X = np.empty((self.P, self.N))
+        check(self._L.kg_tmcmc_get_candidates(self.h, _dptr(X), self.N))
+        return X
+
+    def set_evaluations(self, log_prior, log_likelihood):
+        lp = np.ascontiguousarray(log_prior, dtype=np.float64)
+        ll = np.ascontiguousarray(log_likelihood, dtype=np.float64)
+        check(self._L.kg_tmcmc_set_evaluations(self.h, _dptr(lp), _dptr(ll)))
+
+    def field_size(self, name):
+        n = C.c_size_t()
+        check(self._L.kg_tmcmc_field_size(self.h, name.encode(), C.byref(n)))
+        return n.value
+
+    def __getitem__(self, name):
+        n = self.field_size(name)
+        out = np.empty(n)
+        check(self._L.kg_tmcmc_get_field(self.h, name.encode(), _dptr(out), n))
+        return out
+
+    def __setitem__(self, name, value):
+        a = np.ascontiguousarray(np.asarray(value, dtype=np.float64).reshape(-1))
+        check(self._L.kg_tmcmc_set_field(self.h, name.encode(), _dptr(a), a.size))
+
+    def get_rng(self, which):
+        buf = C.create_string_buffer(5000)
+        check(self._L.kg_tmcmc_get_rng(self.h, int(which), buf))
+        return buf.raw
+
+    def set_rng(self, which, state):
+        assert len(state) == 5000
+        buf = C.create_string_buffer(bytes(state), 5000)
+        check(self._L.kg_tmcmc_set_rng(self.h, int(which), buf))
+
+    def profile(self, enable=True):
+        check(self._L.kg_tmcmc_profile(self.h, int(enable)))
+
+    def profile_read(self, stage):
+        ms, n = C.c_double(), C.c_size_t()
+        check(self._L.kg_tmcmc_profile_read(self.h, stage.encode(), C.byref(ms), C.byref(n)))
         return ms.value, n.value

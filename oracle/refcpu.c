@@ -1565,6 +1565,7 @@ struct kr_tmcmc
   /* priors: uniform [priorMin, priorMax] per variable, RNG per variable */
   double *priorMin, *priorMax;
   kr_rng *priorRng;
+  int *priorMap; /* variable -> prior distribution (shared distributions share an RNG) */
   /* state */
   double *leaders, *leadersLL, *leadersLP, *candidates, *candidatesLL, *candidatesLP;
   double *chainLengths, *meanTheta, *cov, *chol;
@@ -1607,8 +1608,10 @@ kr_tmcmc *kr_tmcmc_new(size_t N, size_t P)
   AL(h->numSelections, P);
 #undef AL
   h->priorRng = (kr_rng *)calloc(N, sizeof(kr_rng));
+  h->priorMap = (int *)calloc(N, sizeof(int));
   for (i = 0; i < N; i++)
   {
+    h->priorMap[i] = (int)i;
     h->priorMin[i] = 0.0;
     h->priorMax[i] = 1.0;
     kr_rng_seed(&h->priorRng[i], 0);
@@ -1625,6 +1628,7 @@ void kr_tmcmc_free(kr_tmcmc *h)
   free(h->priorMin);
   free(h->priorMax);
   free(h->priorRng);
+  free(h->priorMap);
   free(h->leaders);
   free(h->leadersLL);
   free(h->leadersLP);
@@ -1694,6 +1698,14 @@ kr_rng *kr_tmcmc_rng(kr_tmcmc *h, int which)
   return &h->priorRng[which - 3];
 }
 
+/* _variables[d]->_distributionIndex (TMCMC.cpp.base:218-220): variables
+ * drawing from the same distribution object consume its one generator */
+void kr_tmcmc_set_prior_map(kr_tmcmc *h, const int *map)
+{
+  size_t d;
+  for (d = 0; d < h->N; d++) h->priorMap[d] = map[d];
+}
+
 void kr_tmcmc_set_option(kr_tmcmc *h, const char *name, double v)
 {
   if (strcmp(name, "Max Chain Length") == 0) h->maxChainLength = v;
@@ -1731,7 +1743,7 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
   {
     if (gen == 1)
     {
-      for (d = 0; d < N; d++) h->candidates[i * N + d] = kr_ran_flat(&h->priorRng[d], h->priorMin[d], h->priorMax[d]);
+      for (d = 0; d < N; d++) h->candidates[i * N + d] = kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
     }
     else
     {

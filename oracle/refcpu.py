@@ -68,6 +68,7 @@ def lib():
         L.kr_tmcmc_rng.argtypes = [vp, C.c_int]
         L.kr_tmcmc_rng.restype = vp
         L.kr_tmcmc_set_option.argtypes = [vp, cp, C.c_double]
+        L.kr_tmcmc_set_prior_map.argtypes = [vp, C.POINTER(C.c_int)]
         L.kr_tmcmc_initialize.argtypes = [vp]
         L.kr_tmcmc_prepare.argtypes = [vp, sz]
         L.kr_tmcmc_evaluate.argtypes = [vp]
@@ -231,6 +232,10 @@ class TMCMC:
 
     def option(self, name, value):
         self.L.kr_tmcmc_set_option(self.h, name.encode(), float(value))
+
+    def set_prior_map(self, dist_of_var):
+        m = (C.c_int * self.N)(*[int(v) for v in dist_of_var])
+        self.L.kr_tmcmc_set_prior_map(self.h, m)
 
     def initialize(self):
         self.L.kr_tmcmc_initialize(self.h)

@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1200 python -m pytest tests -x -q -m gpu ;;
+    tm) step tm 900 python -m pytest tests/test_gpu_tmcmc.py -q --maxfail=10 ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;
     benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;

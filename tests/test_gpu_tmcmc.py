@@ -1,0 +1,120 @@
+"""GPU parity: the HIP TMCMC path (through the C-ABI) against the oracle and
+the reference's golden generation files (tests/python/plot/tmcmc).
+
+Bar: bit-exact (np.array_equal / ==) for candidates, accept decisions, the
+annealing exponent, coefficient of variation, log-evidence, multinomial
+selections -> chain leaders, weighted mean and covariance, and the exported
+GSL generator states.
+"""
+import numpy as np
+import pytest
+
+import refcpu as R
+from golden_util import load_tmcmc
+
+pytestmark = pytest.mark.gpu
+
+TM = load_tmcmc()
+TN, TP = 3, 50
+
+
+def by_gen(g):
+    for x in TM:
+        if x["Current Generation"] == g:
+            return x
+    raise KeyError(g)
+
+
+def fixture_device(g):
+    from korali_amd.native import TmcmcDevice
+    st = by_gen(g)
+    s = st["Solver"]
+    dev = TmcmcDevice(TN, TP, prior_min=[d["Minimum"] for d in st["Distributions"]],
+                      prior_max=[d["Maximum"] for d in st["Distributions"]],
+                      target_cov=s["Target Coefficient Of Variation"], covariance_scaling=s["Covariance Scaling"])
+    for k in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Leaders LogPriors", "Covariance Matrix",
+              "Chain Lengths"):
+        if len(s[k]):
+            dev[k] = s[k]
+    for k in ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", "Chain Count"):
+        dev[k] = [s[k]]
+    dev.set_rng(0, bytes.fromhex(s["Multinomial Generator"]["Range"]))
+    dev.set_rng(1, bytes.fromhex(s["Multivariate Generator"]["Range"]))
+    dev.set_rng(2, bytes.fromhex(s["Uniform Generator"]["Range"]))
+    for i, d in enumerate(st["Distributions"]):
+        dev.set_rng(3 + i, bytes.fromhex(d["Range"]))
+    return dev
+
+
+@pytest.mark.parametrize("k", range(0, 7))
+def test_tmcmc_teacher_forced_generation_bit_exact(k):
+    """Fixture state after gen k + gen k+1's candidate log-likelihoods (the
+    reference problem used a Python model) -> gen k+1 on the device."""
+    dev = fixture_device(k)
+    nxt = by_gen(k + 1)["Solver"]
+    g = k + 1
+    dev.prepare(g)
+    assert np.array_equal(dev["Chain Candidates"], np.array(nxt["Chain Candidates"]).reshape(-1))
+    dev.set_evaluations(np.array(nxt["Chain Candidates LogPriors"]), np.array(nxt["Chain Candidates LogLikelihoods"]))
+    dev.process(g)
+    dev.synchronize()
+    assert dev["Accepted Samples Count"][0] == nxt["Accepted Samples Count"]
+    assert np.array_equal(dev["Sample LogLikelihood Database"], np.array(nxt["Sample LogLikelihood Database"]))
+    for key in ("Annealing Exponent", "LogEvidence", "Coefficient Of Variation", "Max Loglikelihood",
+                "Selection Acceptance Rate", "Proposals Acceptance Rate", "Chain Count"):
+        assert dev[key][0] == nxt[key], key
+    for key in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Lengths", "Covariance Matrix", "Mean Theta"):
+        assert np.array_equal(dev[key], np.array(nxt[key]).reshape(-1)), key
+    assert dev.get_rng(0).hex().upper() == nxt["Multinomial Generator"]["Range"]
+    assert dev.get_rng(1).hex().upper() == nxt["Multivariate Generator"]["Range"]
+    assert dev.get_rng(2).hex().upper() == nxt["Uniform Generator"]["Range"]
+
+
+VEC_KEYS = ("Chain Candidates", "Chain Candidates LogLikelihoods", "Chain Candidates LogPriors", "Chain Leaders",
+            "Chain Leaders LogLikelihoods", "Chain Leaders LogPriors", "Chain Lengths", "Mean Theta",
+            "Covariance Matrix", "Sample Database", "Sample LogLikelihood Database", "Num Selections")
+SCA_KEYS = ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", "Coefficient Of Variation",
+            "Max Loglikelihood", "Chain Count", "Accepted Samples Count", "Proposals Acceptance Rate",
+            "Selection Acceptance Rate", "Model Evaluation Count", "Min Search Iterations")
+
+
+def seeded_pair(N, P, shared_prior, seed=1337, target_cov=1.0):
+    """C3-style experiment: every variable with a U(-5, 5) prior, Gaussian
+    loglik -0.5|x|^2; seeds in Korali's consumption order (distributions,
+    then the solver's Multinomial, Multivariate, Uniform generators)."""
+    from korali_amd.native import TmcmcDevice
+    ndist = 1 if shared_prior else N
+    pdist = [0] * N if shared_prior else list(range(N))
+    seeds = [seed + k for k in range(ndist)]
+    sm, sv, su = seed + ndist, seed + ndist + 1, seed + ndist + 2
+    dev = TmcmcDevice(N, P, prior_min=[-5.0] * N, prior_max=[5.0] * N, prior_seeds=seeds, prior_distribution=pdist,
+                      multinomial_seed=sm, multivariate_seed=sv, uniform_seed=su, target_cov=target_cov)
+    o = R.TMCMC(N, P)
+    o.option("Target Coefficient Of Variation", target_cov)
+    o["Prior Minimum"] = [-5.0] * N
+    o["Prior Maximum"] = [5.0] * N
+    o.set_prior_map(pdist)
+    for k in range(ndist):
+        R.lib().kr_rng_seed(o.rng(3 + k).ptr, seeds[k])
+    R.lib().kr_rng_seed(o.rng(0).ptr, sm)
+    R.lib().kr_rng_seed(o.rng(1).ptr, sv)
+    R.lib().kr_rng_seed(o.rng(2).ptr, su)
+    return dev, o, ndist
+
+
+@pytest.mark.parametrize("N,P,gens,shared", [(4, 256, 12, True), (3, 500, 10, False), (32, 2048, 6, True)])
+def test_tmcmc_seeded_run_matches_oracle(N, P, gens, shared):
+    dev, o, ndist = seeded_pair(N, P, shared)
+    for g in range(1, gens + 1):
+        dev.generation(g)
+        o.generation(g)
+        dev.synchronize()
+        for key in VEC_KEYS:
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        for key in SCA_KEYS:
+            a, b = dev[key][0], o[key][0]
+            assert a == b or (np.isnan(a) and np.isnan(b)), (g, key, a, b)
+        if o["Annealing Exponent"][0] >= 1.0:
+            break
+    for which in range(3 + ndist):
+        assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
