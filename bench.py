@@ -49,13 +49,11 @@ STAGE_FLOPS = {
 }
 
 
-def cpu_baseline(seconds_budget=12.0):
-    """Time the CPU oracle (single thread) on a bounded sample of the same
-    workload: generations of C2 until ~seconds_budget of work."""
+def _cmaes_oracle_rate(variant, seconds_budget, max_gens):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refcpu as R
 
-    o = R.CMAES(N_VARS, LAMBDA, MU)
+    o = R.CMAES(N_VARS, LAMBDA, MU, variant=variant)
     o["Initial Value"] = np.zeros(N_VARS)
     o["Initial Standard Deviation"] = np.ones(N_VARS)
     R.lib().kr_rng_seed(o.rng(0).ptr, 1337)
@@ -66,12 +64,24 @@ def cpu_baseline(seconds_budget=12.0):
         g += 1
         o.generation(g, "rosenbrock")
         el = time.perf_counter() - t0
-        if el > seconds_budget or g >= 60:
+        if el > seconds_budget or g - 1 >= max_gens:
             break
-    gens = g - 1
+    return g - 1, el
+
+
+def cpu_baseline(seconds_budget=10.0):
+    """Time the CPU oracle (single thread) on a bounded sample of the same
+    workload.  `value` is the oracle built against the system libm
+    (oracle/librefcpu_libm.so: the speed the reference itself runs at on this
+    host — the conservative baseline); the bit-exact oracle, whose
+    correctly-rounded log/exp are slower, is reported beside it."""
+    gens, el = _cmaes_oracle_rate("libm", seconds_budget, 60)
+    gens_cr, el_cr = _cmaes_oracle_rate("cr", seconds_budget / 2, 20)
     return {"value": gens / el, "unit": "generations/s", "cores": 1, "kind": "port",
             "samples_per_sec": gens * LAMBDA / el,
-            "sample": f"{gens} generations of C2 (N=128, lambda=4096) after 1 warm-up, oracle/refcpu.c -O2, 1 thread"}
+            "bit_exact_port_value": gens_cr / el_cr,
+            "sample": f"{gens} generations of C2 (N=128, lambda=4096) after 1 warm-up, oracle/refcpu.c -O2 "
+                      f"with system libm (timing build), 1 thread; bit-exact CR build: {gens_cr} generations"}
 
 
 def main():
@@ -81,7 +91,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cov", default="mfma", choices=["exact", "mfma"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3"],
+                    help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192 (parity/perf case)")
     args = ap.parse_args()
+    if args.workload == "c3":
+        return run_c3(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -193,6 +207,117 @@ def main():
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------- C3 TMCMC
+C3_N, C3_P = 32, 8192
+
+
+def c3_stage_flops(N, P):
+    return {"draw": 2.0 * P * N * N / 2, "mean_cov": 3.0 * P * N * (N + 1) / 2 + 2.0 * P * N,
+            "evaluate": 3.0 * P * N, "cholesky": N ** 3 / 3.0}
+
+
+def c3_experiment(seed):
+    from korali_amd.native import TmcmcDevice
+    # one shared "Uniform 0" prior (U(-5,5)) for all 32 variables; seeds in
+    # Korali's consumption order: distribution, then Multinomial,
+    # Multivariate, Uniform generators of the solver
+    return TmcmcDevice(C3_N, C3_P, prior_min=[-5.0] * C3_N, prior_max=[5.0] * C3_N, prior_seeds=[seed],
+                       prior_distribution=[0] * C3_N, multinomial_seed=seed + 1, multivariate_seed=seed + 2,
+                       uniform_seed=seed + 3, target_cov=1.0, covariance_scaling=0.04)
+
+
+def c3_cpu_baseline(seconds_budget=10.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu as R
+
+    def rate(variant, budget, max_gens):
+        o = R.TMCMC(C3_N, C3_P, variant=variant)
+        o["Prior Minimum"] = [-5.0] * C3_N
+        o["Prior Maximum"] = [5.0] * C3_N
+        o.set_prior_map([0] * C3_N)
+        for i, sd in enumerate([1338, 1339, 1340, 1337]):
+            R.lib().kr_rng_seed(o.rng(i).ptr, sd)
+        g, t0 = 0, time.perf_counter()
+        while True:
+            g += 1
+            o.generation(g)
+            el = time.perf_counter() - t0
+            if el > budget or g >= max_gens or o["Annealing Exponent"][0] >= 1.0:
+                return g, el
+
+    g, el = rate("libm", seconds_budget, 12)
+    gc, elc = rate("cr", seconds_budget / 2, 3)
+    return {"value": g / el, "unit": "generations/s", "cores": 1, "kind": "port", "bit_exact_port_value": gc / elc,
+            "sample": f"first {g} generations of C3 (N=32, P=8192), oracle with system libm (timing build), "
+                      f"1 thread; bit-exact CR build: {gc} generations"}
+
+
+def run_c3(args):
+    from korali_amd import _build
+    if not os.path.exists(_build.LIB):
+        _build.build()
+    # warm-up: a throwaway run of W generations
+    dev = c3_experiment(999)
+    for g in range(1, args.warmup + 1):
+        dev.generation(g)
+        if dev["Annealing Exponent"][0] >= 1.0:
+            break
+    dev.synchronize()
+    dev.close()
+    # timed: K generations over successive complete runs (each run stops at
+    # annealing exponent 1, as Korali's TMCMC termination does)
+    exps = [c3_experiment(1337 + 10 * r) for r in range(max(2, args.steps // 8 + 2))]
+    done, runs, r, g = 0, 0, 0, 0
+    t0 = time.perf_counter()
+    while done < args.steps:
+        g += 1
+        exps[r].generation(g)
+        done += 1
+        if exps[r]["Annealing Exponent"][0] >= 1.0:
+            r, g, runs = r + 1, 0, runs + 1
+            if r == len(exps):
+                break
+    exps[min(r, len(exps) - 1)].synchronize()
+    elapsed = time.perf_counter() - t0
+    # stage times on a fresh run
+    dev = c3_experiment(4242)
+    dev.profile(True)
+    STAGES = ("cholesky", "prior_draw", "rng_polar", "draw", "evaluate", "accept", "min_search", "weights",
+              "multinomial", "mean_cov", "expand")
+    for g in range(1, 40):
+        dev.generation(g)
+        if dev["Annealing Exponent"][0] >= 1.0:
+            break
+    stages = {}
+    for st in STAGES:
+        ms, n = dev.profile_read(st)
+        if n:
+            stages[st] = ms / n
+    search = {"generations": g, "exact_host_evaluations_per_generation": dev["Exact Search Evaluations"][0] / g}
+    flops = c3_stage_flops(C3_N, C3_P)
+    kernels = {k: v for k, v in stages.items() if k in flops}
+    dominant = max(kernels, key=kernels.get)
+    achieved = flops[dominant] / (stages[dominant] * 1e-3) / 1e12
+    out = {
+        "metric": "TMCMC generations/sec, 32-dim Gaussian posterior, P=8192 chains",
+        "value": done / elapsed, "unit": "generations/s", "n_gpus": 1, "steps": done, "warmup": args.warmup,
+        "ms_per_step": elapsed / done * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C3: TMCMC, 32 variables with one shared U(-5,5) prior, loglik -0.5|x|^2, "
+                               "P=8192, Max Chain Length 1, Target CoV 1.0, Covariance Scaling 0.04; "
+                               "successive runs to annealing exponent 1", "complete_runs": runs},
+        "chain_steps_per_sec": done * C3_P / elapsed,
+        "stage_ms": stages,
+        "annealing_search": search,
+        "roofline": {"kernel": dominant, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "algorithmic_flops_per_launch": flops[dominant], "avg_launch_ms": stages[dominant]},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = c3_cpu_baseline()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

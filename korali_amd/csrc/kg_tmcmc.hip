@@ -19,6 +19,7 @@
 //            runs those chains ~8x faster than one GPU lane.
 // Results are identical to the reference's (tests/test_gpu_tmcmc.py).
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -270,15 +271,121 @@ __global__ void __launch_bounds__(1024) k_tm_max(int P, const double *__restrict
   }
 }
 
-// calculateSquaredCVDifference :683-703, the parallel part: for each search
-// point x_k, E_k[i] = exp((ll_i - ll_max) * (x_k - rho)).
-__global__ void k_tm_cv_exp(int P, int npts, const double *__restrict__ ll, const TmDev *__restrict__ dev, double rho,
-                            CvPoints pts, double *__restrict__ E) {
+// calculateSquaredCVDifference :683-703 for a batch of search points.
+// Grid (CV_BLOCKS, npts): every block takes a slice of the P exponentials
+//   E_k[i] = exp((ll_i - ll_max) (x_k - rho))           (kept for the exact tail)
+// and accumulates d = E - 1 (exact for E in [1/2, 1]: the shift keeps the
+// variance free of cancellation when the weights are nearly uniform) as
+// double-double sums of d and d^2; the last block of point k to finish
+// forms cv_k = sd(E_k) / mean(E_k).  cv is invariant to the normalisation
+// w = E / sum(E), so cv_k is the reference's coefficient of variation up to
+// the reference's own rounding; `ratio` = max(E)/mean(E) feeds the host's
+// bound on that rounding.
+struct CvOut {
+  double cv2, cv, ratio;
+  int flag;  // non-finite / degenerate: the host evaluates exactly
+  int pad;
+};
+struct CvPart {
+  double s_hi, s_lo, q_hi, q_lo, mx;
+  int bad, pad;
+};
+constexpr int CV_BLOCKS = 32;
+constexpr int CV_TPB = 256;
+__device__ inline dd dd_shfl_down(dd a, int off) { return dd{__shfl_down(a.hi, off, 64), __shfl_down(a.lo, off, 64)}; }
+__global__ void __launch_bounds__(CV_TPB) k_tm_cv_part(int P, const double *__restrict__ ll,
+                                                       const TmDev *__restrict__ dev, double rho, CvPoints pts,
+                                                       CvPart *__restrict__ part) {
+  __shared__ dd sh_s[CV_TPB / 64], sh_q[CV_TPB / 64];
+  __shared__ double sh_m[CV_TPB / 64];
+  __shared__ int sh_b[CV_TPB / 64];
+  const int k = blockIdx.y, b = blockIdx.x;
+  const double x = pts.x[k], llmax = dev->llmaxCv;
+  dd s{0.0, 0.0}, q{0.0, 0.0};
+  double mx = 0.0;
+  int bad = 0;
+  for (int i = b * CV_TPB + threadIdx.x; i < P; i += CV_BLOCKS * CV_TPB) {
+    const double e = exp_cr((ll[i] - llmax) * (x - rho));
+    if (!isfinite(e)) bad = 1;
+    const double d = e - 1.0;
+    s = dd_add(s, dd{d, 0.0});
+    q = dd_add(q, dd_tp(d, d));
+    mx = e > mx ? e : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s = dd_add(s, dd_shfl_down(s, off));
+    q = dd_add(q, dd_shfl_down(q, off));
+    mx = fmax(mx, __shfl_down(mx, off, 64));
+    bad |= __shfl_down(bad, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh_s[wid] = s;
+    sh_q[wid] = q;
+    sh_m[wid] = mx;
+    sh_b[wid] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < CV_TPB / 64; w++) {
+      s = dd_add(s, sh_s[w]);
+      q = dd_add(q, sh_q[w]);
+      mx = fmax(mx, sh_m[w]);
+      bad |= sh_b[w];
+    }
+    part[k * CV_BLOCKS + b] = CvPart{s.hi, s.lo, q.hi, q.lo, mx, bad, 0};
+  }
+}
+
+// one wave per point: combine the partials, form cv, and publish it to
+// host-coherent memory as 16-byte {value, sequence} records (each record
+// one PCIe write: the host sees the value once it sees the sequence, no
+// fence needed)
+__global__ void __launch_bounds__(64) k_tm_cv_final(int P, double target, const CvPart *__restrict__ part,
+                                                    double2 *__restrict__ rec, unsigned long long seq) {
+  const int k = blockIdx.x, j = threadIdx.x;
+  dd S{0.0, 0.0}, Q{0.0, 0.0};
+  double M = 0.0;
+  int B = 0;
+  if (j < CV_BLOCKS) {
+    const CvPart p = part[k * CV_BLOCKS + j];
+    S = dd{p.s_hi, p.s_lo};
+    Q = dd{p.q_hi, p.q_lo};
+    M = p.mx;
+    B = p.bad;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    S = dd_add(S, dd_shfl_down(S, off));
+    Q = dd_add(Q, dd_shfl_down(Q, off));
+    M = fmax(M, __shfl_down(M, off, 64));
+    B |= __shfl_down(B, off, 64);
+  }
+  if (j != 0) return;
+  const dd Pd{(double)P, 0.0};
+  const dd dmean = dd_div(S, Pd);                      // mean(d)
+  dd ss = dd_add(Q, dd_mul(dd{-S.hi, -S.lo}, dmean));  // sum (d - mean d)^2
+  const double var = (ss.hi + ss.lo) / (double)(P - 1);
+  const dd mean = dd_add(dmean, dd{1.0, 0.0});
+  const double meand = mean.hi + mean.lo;
+  const double cv = sqrt(var > 0.0 ? var : 0.0) / meand;
+  double c = cv - target;
+  c *= c;
+  const double ratio = M / meand;
+  const int flag = (B || !isfinite(c) || !(meand > 0.0) || !isfinite(ratio) || var < 0.0) ? 1 : 0;
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const double sq = __longlong_as_double((long long)seq);
+  d2v *r = (d2v *)(rec + 4 * k);
+  __builtin_nontemporal_store(d2v{c, sq}, r + 0);  // one 16-byte store each
+  __builtin_nontemporal_store(d2v{cv, sq}, r + 1);
+  __builtin_nontemporal_store(d2v{ratio, sq}, r + 2);
+  __builtin_nontemporal_store(d2v{(double)flag, sq}, r + 3);
+}
+
+// the exponentials of one search point, for the host's exact tail
+__global__ void k_tm_cv_exp(int P, const double *__restrict__ ll, const TmDev *__restrict__ dev, double rho, double x,
+                            double *__restrict__ E) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;
-  if (i >= P || k >= npts) return;
-  const double llmax = dev->llmaxCv;
-  E[(size_t)k * P + i] = exp_cr((ll[i] - llmax) * (pts.x[k] - rho));
+  if (i < P) E[i] = exp_cr((ll[i] - dev->llmaxCv) * (x - rho));
 }
 
 // processGeneration :284-296: w_i = exp(ll_i (rho - rho_prev) - max)
@@ -289,64 +396,134 @@ __global__ void k_tm_lw_exp(int P, const double *__restrict__ ll, double drho, c
   E[i] = exp_cr(ll[i] * drho - dev->lwmax);
 }
 
-// processGeneration :318-322: meanTheta_i = sum_j db[j][i] w_j, sequential in j
-__global__ void __launch_bounds__(64) k_tm_mean(int N, int P, const double *__restrict__ db,
-                                                const double *__restrict__ w, double *__restrict__ mean) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  double m = 0;
-  int j = 0;
-  for (; j + 8 <= P; j += 8) {
-    double v[8], ww[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      v[q] = db[(size_t)(j + q) * N + i];
-      ww[q] = w[j + q];
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) m += v[q] * ww[q];
-  }
-  for (; j < P; j++) m += db[(size_t)j * N + i] * w[j];
-  mean[i] = m;
+// processGeneration :318-329, the weighted mean and covariance of the
+// database, each output element one ordered P-long sum (the reference's
+// order, so the result is bit-identical):
+//   mean_i = sum_j db[j][i] w_j
+//   cov_ij = covScaling * s / (1 - sum w^2),  s = sum_k w_k (x_ki - m_i)(x_kj - m_j),  j >= i
+// One lane per output element in wave 0 of each workgroup; three more
+// waves stream the database and precompute the factors the reference forms
+// (left to right, so identical roundings):
+//   mean: T[k][i]  = db[k][i] * w_k
+//   cov : WD[k][i] = w_k * (db[k][i] - m_i),  D[k][i] = db[k][i] - m_j
+// into a double-buffered LDS tile of up to 256 rows; the computing wave
+// then does one LDS read (mean) or two and one multiply (cov) per add, and
+// its dependent add chain (14 cycles per add on gfx950,
+// tools/ubench_chain.hip) is the cost.
+constexpr int WS_TPB = 256, WS_LANES = 64, WS_MAXV = 32;
+__host__ __device__ inline int ws_rows(int N, bool cov) {
+  const int r = (WS_TPB * WS_MAXV / (cov ? 2 * N : N)) & ~7;
+  return r < 8 ? 8 : (r > 256 ? 256 : r);
 }
-
-// processGeneration :324-329: cov_ij = covScaling * s / (1 - sum w^2),
-// s = sum_k w_k (x_ki - m_i)(x_kj - m_j) sequential in k, j >= i; one lane
-// per (i, j) pair, database rows staged through LDS.
-constexpr int COV_ROWS = 64;
-__global__ void __launch_bounds__(256) k_tm_cov(int N, int P, const double *__restrict__ db,
-                                                const double *__restrict__ w, const double *__restrict__ mean,
-                                                double scaling, double denom, double *__restrict__ cov) {
-  extern __shared__ double rows[];  // COV_ROWS x N, then COV_ROWS weights
-  double *ws = rows + COV_ROWS * N;
-  const int npairs = N * (N + 1) / 2;
-  const int pidx = blockIdx.x * blockDim.x + threadIdx.x;
+__host__ __device__ inline size_t ws_lds_bytes(int N, bool cov) {
+  return 2 * (size_t)ws_rows(N, cov) * N * (cov ? 2 : 1) * sizeof(double);
+}
+template <bool COV>
+__global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *__restrict__ db,
+                                                    const double *__restrict__ w, const double *__restrict__ mean,
+                                                    const int2 *__restrict__ pairs, int nout, double scaling,
+                                                    double denom, double *__restrict__ out) {
+  extern __shared__ double sm[];
+  __shared__ double msh[TM_MAX_N];
+  const int rows = ws_rows(N, COV);
+  const int tile = rows * N;
+  const int buf = COV ? 2 * tile : tile;  // one buffer: T, or WD then D
+  const int nchunks = (P + rows - 1) / rows;
+  const int tid = threadIdx.x, oidx = blockIdx.x * WS_LANES + tid;
+  const bool active = tid < WS_LANES && oidx < nout;
   int pi = 0, pj = 0;
-  const bool active = pidx < npairs;
-  if (active) {  // pidx -> (i, j), row-major over the upper triangle
-    int rem = pidx, i = 0;
-    while (rem >= N - i) {
-      rem -= N - i;
-      i++;
-    }
-    pi = i;
-    pj = i + rem;
-  }
-  const double mi = active ? mean[pi] : 0.0, mj = active ? mean[pj] : 0.0;
-  double s = 0.0;
-  for (int k0 = 0; k0 < P; k0 += COV_ROWS) {
-    const int nk = min(COV_ROWS, P - k0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < nk * N; e += blockDim.x) rows[e] = db[(size_t)k0 * N + e];
-    for (int e = threadIdx.x; e < nk; e += blockDim.x) ws[e] = w[k0 + e];
-    __syncthreads();
-    if (active)
-      for (int k = 0; k < nk; k++) s += ws[k] * (rows[k * N + pi] - mi) * (rows[k * N + pj] - mj);
-  }
   if (active) {
-    const double v = scaling * s / denom;
-    cov[pi * N + pj] = v;
-    cov[pj * N + pi] = v;
+    if (COV) {
+      const int2 ij = pairs[oidx];
+      pi = ij.x;
+      pj = ij.y;
+    } else {
+      pi = oidx;
+    }
+  }
+  if (COV)
+    for (int i = tid; i < N; i += WS_TPB) msh[i] = mean[i];
+  // each thread's tile elements e = tid + v*WS_TPB: row e / N, column e % N
+  int col[WS_MAXV], row[WS_MAXV];
+#pragma unroll
+  for (int v = 0; v < WS_MAXV; v++) {
+    const int e = tid + v * WS_TPB;
+    row[v] = e / N;
+    col[v] = e - row[v] * N;
+  }
+  double xr[WS_MAXV], wr[WS_MAXV];
+  int lim = 0;
+  // branch-free loads (clamped indices, zeroed past the end): every lane
+  // issues its loads back to back, a tile costs one memory latency
+  auto fetch = [&](int c) {
+    const int r0 = c * rows, nk = min(rows, P - r0);
+    const double *base = db + (size_t)r0 * N;
+    lim = nk * N;
+#pragma unroll
+    for (int v = 0; v < WS_MAXV; v++) {
+      xr[v] = base[min(tid + v * WS_TPB, lim - 1)];
+      wr[v] = w[r0 + min(row[v], nk - 1)];
+    }
+  };
+  auto store = [&](double *b) {
+#pragma unroll
+    for (int v = 0; v < WS_MAXV; v++) {
+      const int e = tid + v * WS_TPB;
+      if (e < tile) {
+        const bool ok = e < lim;
+        if (COV) {
+          const double d = xr[v] - msh[col[v]];
+          b[e] = ok ? wr[v] * d : 0.0;
+          b[tile + e] = ok ? d : 0.0;
+        } else {
+          b[e] = ok ? xr[v] * wr[v] : 0.0;
+        }
+      }
+    }
+  };
+  __syncthreads();  // msh
+  fetch(0);
+  store(sm);
+  __syncthreads();
+  double acc = 0.0;
+  for (int c = 0; c < nchunks; c++) {
+    if (c + 1 < nchunks) fetch(c + 1);
+    const double *cur = sm + (c & 1) * buf;
+    const int nk = min(rows, P - c * rows);
+    if (active) {
+      // software-pipelined: the next 8 terms are read while the current 8
+      // are added, so the LDS latency stays off the add chain
+      const double *A = cur, *Bm = cur + tile;
+      auto term = [&](int r) { return COV ? A[r * N + pi] * Bm[r * N + pj] : A[r * N + pi]; };
+      int r = 0;
+      if (nk >= 16) {
+        double ta[8], tb[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) ta[q] = term(q);
+        for (; r + 16 <= nk; r += 16) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) tb[q] = term(r + 8 + q);
+#pragma unroll
+          for (int q = 0; q < 8; q++) acc += ta[q];
+          const int rn = min(r + 16, nk - 8);  // clamped prefetch, recomputed below if unused
+#pragma unroll
+          for (int q = 0; q < 8; q++) ta[q] = term(rn + q);
+#pragma unroll
+          for (int q = 0; q < 8; q++) acc += tb[q];
+        }
+      }
+      for (; r < nk; r++) acc += term(r);
+    }
+    if (c + 1 < nchunks) store(sm + ((c + 1) & 1) * buf);
+    __syncthreads();
+  }
+  if (!active) return;
+  if (COV) {
+    const double v = scaling * acc / denom;
+    out[pi * N + pj] = v;
+    out[pj * N + pi] = v;
+  } else {
+    out[pi] = acc;
   }
 }
 
@@ -573,12 +750,19 @@ struct kg_tmcmc_s {
          *dbLL = nullptr, *dbLP = nullptr, *numSel = nullptr, *pmin = nullptr, *pmax = nullptr,
          *negLogWidth = nullptr, *Z = nullptr, *U = nullptr, *Uprior = nullptr, *E = nullptr, *w = nullptr;
   unsigned long long *uoff = nullptr;
+  int2 *pairs = nullptr;    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
   unsigned *src = nullptr;
   unsigned char *acc = nullptr;
   TmDev *dev = nullptr;
   // pinned host staging
   double *hE = nullptr, *hW = nullptr, *hNsel = nullptr;
+  void *hCv = nullptr;                       // CvOut[CV_MAX_PTS + 1] (host)
+  double2 *hRec = nullptr, *dRec = nullptr;  // 4 x CV_MAX_PTS+1 records, host-coherent (+ device alias)
+  unsigned long long cvSeq = 0;
+  void *cvPart = nullptr;                  // CvPart[(CV_MAX_PTS + 1) * CV_BLOCKS]
+  bool exactSearch = false;                // KORALI_AMD_TMCMC_EXACT_SEARCH=1: every cv2 on the host
+  size_t exactEvals = 0;
   unsigned *hSrc = nullptr;
   TmDev *hDev = nullptr;
   std::vector<double> wtmp;
@@ -595,6 +779,7 @@ struct kg_tmcmc_s {
   double annealingExponent = 0, previousAnnealingExponent = 0, logEvidence = 0, coefficientOfVariation = 0,
          maxLoglikelihood = -INFINITY, chainCount = 0, acceptedSamplesCount = 0, proposalsAcceptanceRate = 0,
          selectionAcceptanceRate = 0, dbCount = 0, modelEvaluationCount = 0, minSearchIterations = 0;
+  double exactEvalsD = 0;  // diagnostics: host-exact cv2 evaluations so far
   bool devPending = false;  // accepted count / maxLoglikelihood not yet read back
   // profiling
   bool profile = false;
@@ -662,33 +847,166 @@ int tm_sync_dev(kg_tmcmc_s *h) {
   return 0;
 }
 
-// evaluates calculateSquaredCVDifference at batches of search points: the
-// exponentials on the device, the serial tail on the host
+// calculateSquaredCVDifference at the annealing search's points.  The
+// device returns cv2 for a whole batch of points from double-double sums; the
+// reference's own value differs from that by its rounding (std::accumulate,
+// the divisions by the sum, and the x87 `long double` gsl_stats recurrences),
+// bounded below.  Every comparison the simplex makes is decided on these
+// intervals when they are disjoint; otherwise both operands are evaluated
+// exactly as the reference does (cv2_tail on the host) and compared.  Values
+// that are stored (the minimum, the CoV) are always exact.  The simplex path
+// and every stored value are therefore the reference's.
+struct YV {
+  double y = 0, eps = 0, x = 0;
+  bool exact = false;
+};
+
 struct CvSearch {
   kg_tmcmc_s *h;
   double exponent, target;
+  bool exactOnly = false;
   double xs[CV_MAX_PTS];
   int n = 0;
-  int batch(const double *pts, int npts) {
-    CvPoints cp{};
-    n = std::min(npts, CV_MAX_PTS);
-    for (int k = 0; k < n; k++) cp.x[k] = xs[k] = pts[k];
-    const int P = h->P;
-    hipLaunchKernelGGL(k_tm_cv_exp, dim3(nblk(P, 256), n), dim3(256), 0, h->stream, P, n, h->dbLL, h->dev, exponent,
-                       cp, h->E);
-    KG_HIP(hipGetLastError());
-    KG_HIP(hipMemcpyAsync(h->hE, h->E, (size_t)n * P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    KG_HIP(hipStreamSynchronize(h->stream));
-    return 0;
-  }
-  // f(x); rc != 0 on a HIP error
-  double eval(double x, int &rc) {
-    for (int k = 0; k < n; k++)
-      if (memcmp(&xs[k], &x, sizeof(double)) == 0) return cv2_tail(h->hE + (size_t)k * h->P, h->P, target, h->wtmp.data());
-    rc |= batch(&x, 1);
-    return cv2_tail(h->hE, h->P, target, h->wtmp.data());
-  }
+  double spareX = 0;  // the point whose E / CvOut sit in the spare slot
+  bool spareValid = false;
+  size_t exactEvals = 0;
+  int launch(const double *pts, int npts, int slot0);
+  int batch(const double *pts, int npts);
+  int slot_of(double x, bool needOut);
+  int exact(YV &v);
+  int get(double x, YV &v);
+  int lt(YV &a, YV &b, bool &r);
+  int le(YV &a, YV &b, bool &r);
 };
+
+int CvSearch::launch(const double *pts, int npts, int slot0) {
+  CvPoints cp{};
+  for (int k = 0; k < npts; k++) cp.x[k] = pts[k];
+  const unsigned long long seq = ++h->cvSeq;
+  hipLaunchKernelGGL(k_tm_cv_part, dim3(CV_BLOCKS, npts), dim3(CV_TPB), 0, h->stream, h->P, h->dbLL, h->dev, exponent,
+                     cp, (CvPart *)h->cvPart + slot0 * CV_BLOCKS);
+  hipLaunchKernelGGL(k_tm_cv_final, dim3(npts), dim3(64), 0, h->stream, h->P, target,
+                     (const CvPart *)h->cvPart + slot0 * CV_BLOCKS, h->dRec + 4 * slot0, seq);
+  KG_HIP(hipGetLastError());
+  // wait on the results themselves (zero-copy), not on the stream
+  const auto t0 = std::chrono::steady_clock::now();
+  CvOut *res = (CvOut *)h->hCv;
+  for (int k = 0; k < npts; k++) {
+    volatile const unsigned long long *r = (volatile const unsigned long long *)(h->hRec + 4 * (slot0 + k));
+    unsigned spins = 0;
+    for (;;) {
+      bool ready = true;
+      for (int f = 0; f < 4; f++)
+        if (r[2 * f + 1] != seq) ready = false;
+      if (ready) break;
+      if (++spins % 4096 == 0) {
+        const hipError_t e = hipStreamQuery(h->stream);
+        if (e != hipSuccess && e != hipErrorNotReady) KG_HIP(e);
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+          set_error("kg_tmcmc: annealing-search kernel did not complete");
+          return 1;
+        }
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    CvOut &o = res[slot0 + k];
+    double v[4];
+    for (int f = 0; f < 4; f++) {
+      const unsigned long long bits = r[2 * f];
+      memcpy(&v[f], &bits, sizeof(double));
+    }
+    o.cv2 = v[0];
+    o.cv = v[1];
+    o.ratio = v[2];
+    o.flag = v[3] != 0.0 ? 1 : 0;
+  }
+  return 0;
+}
+
+int CvSearch::batch(const double *pts, int npts) {
+  n = std::min(npts, CV_MAX_PTS);
+  for (int k = 0; k < n; k++) xs[k] = pts[k];
+  return launch(pts, n, 0);
+}
+
+// slot holding x's exponentials and CvOut (evaluating x into the spare slot
+// if it is not in the current batch); -1 on error
+int CvSearch::slot_of(double x, bool) {
+  for (int k = 0; k < n; k++)
+    if (memcmp(&xs[k], &x, sizeof(double)) == 0) return k;
+  if (spareValid && memcmp(&spareX, &x, sizeof(double)) == 0) return CV_MAX_PTS;
+  if (launch(&x, 1, CV_MAX_PTS)) return -1;
+  spareX = x;
+  spareValid = true;
+  return CV_MAX_PTS;
+}
+
+// the reference's value at v.x, bit for bit
+int CvSearch::exact(YV &v) {
+  if (v.exact) return 0;
+  hipLaunchKernelGGL(k_tm_cv_exp, dim3(nblk(h->P, 256)), dim3(256), 0, h->stream, h->P, h->dbLL, h->dev, exponent,
+                     v.x, h->E);
+  KG_HIP(hipGetLastError());
+  KG_HIP(hipMemcpyAsync(h->hE, h->E, (size_t)h->P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  v.y = cv2_tail(h->hE, h->P, target, h->wtmp.data());
+  v.eps = 0;
+  v.exact = true;
+  exactEvals++;
+  return 0;
+}
+
+int CvSearch::get(double x, YV &v) {
+  const int slot = slot_of(x, true);
+  if (slot < 0) return 1;
+  const CvOut &o = ((const CvOut *)h->hCv)[slot];
+  v.x = x;
+  v.exact = false;
+  if (exactOnly || o.flag) return exact(v);
+  // |cv_ref - cv| <= dc: 1e-13 relative for the long
+  // double recurrences and final roundings (worst case ~2^-64 (3P + 10
+  // max/mean) + 4u ~ 2e-15 at P = 8192), 16u*max/mean for the rounding of
+  // each w_i = E_i / sum (worst case u*max/mean), 4u^2/cv second order
+  const double u = 1.1102230246251565e-16;
+  const double cv = fabs(o.cv);
+  const double dc = 1e-13 * cv + 16.0 * u * o.ratio + 4.0 * u * u / (cv > 1e-300 ? cv : 1e-300);
+  v.y = o.cv2;
+  v.eps = 2.0 * fabs(o.cv - target) * dc + dc * dc + 4.0 * u * fabs(o.cv2) + 1e-300;
+  if (!std::isfinite(v.eps)) return exact(v);
+  return 0;
+}
+
+int CvSearch::lt(YV &a, YV &b, bool &r) {
+  if (!(a.exact && b.exact)) {
+    if (a.y + a.eps < b.y - b.eps) {
+      r = true;
+      return 0;
+    }
+    if (a.y - a.eps > b.y + b.eps) {
+      r = false;
+      return 0;
+    }
+    if (exact(a) || exact(b)) return 1;
+  }
+  r = a.y < b.y;
+  return 0;
+}
+
+int CvSearch::le(YV &a, YV &b, bool &r) {
+  if (!(a.exact && b.exact)) {
+    if (a.y + a.eps < b.y - b.eps) {
+      r = true;
+      return 0;
+    }
+    if (a.y - a.eps > b.y + b.eps) {
+      r = false;
+      return 0;
+    }
+    if (exact(a) || exact(b)) return 1;
+  }
+  r = a.y <= b.y;
+  return 0;
+}
 
 double simplex_size(const double X[2]) {
   const double center = (X[0] + X[1]) / 2;
@@ -698,45 +1016,43 @@ double simplex_size(const double X[2]) {
   return ss / 2.0;
 }
 
+#define TRY(call) \
+  do {            \
+    if (call) return 1; \
+  } while (0)
+
 // minSearch :712-779: gsl_multimin_fminimizer_nmsimplex (v1) in one
 // dimension, x0 = exponent, step 1e-8, size tolerance 1e-12, <= 1000
-// iterations; each iteration's possible next points are evaluated on the
-// device in one batch.
+// iterations.  Each iteration's possible next points (reflection,
+// expansion, both contractions, both contract-by-best outcomes) are
+// evaluated on the device in one batch.  cv2 is never non-finite (the
+// reference maps that to 'Lowest'), so its isfinite() tests always pass.
 int min_search(kg_tmcmc_s *h, double exponent, double objCov, double &xmin, double &fmin, size_t &iters) {
   const size_t MaxIter = 1000;
   const double Tol = 1e-12, Step = 1e-8;
   CvSearch cv{h, exponent, objCov};
-  int rc = 0;
-  double X[2] = {exponent, exponent + Step}, Y[2];
-  if (cv.batch(X, 2)) return 1;
-  Y[0] = cv.eval(X[0], rc);
-  Y[1] = cv.eval(X[1], rc);
-  double xbest = X[0], fval = 0.0, size;
-  size_t iter = 0;
+  cv.exactOnly = h->exactSearch;
+  double X[2] = {exponent, exponent + Step};
+  YV Y[2];
+  TRY(cv.batch(X, 2));
+  TRY(cv.get(X[0], Y[0]));
+  TRY(cv.get(X[1], Y[1]));
+  size_t lo = 0, iter = 0;
+  bool r;
   int status;
   do {
     iter++;
-    size_t hi = 0, s_hi = 0, lo = 0;
-    double dhi = Y[0], ds_hi = Y[0], dlo = Y[0];
-    {
-      const double val = Y[1];
-      if (val < dlo) {
-        dlo = val;
-        lo = 1;
-      } else if (val > dhi) {
-        ds_hi = dhi;
-        s_hi = hi;
-        dhi = val;
-        hi = 1;
-      } else if (val > ds_hi) {
-        ds_hi = val;
-        s_hi = 1;
-      }
+    size_t hi = 0, s_hi = 0;
+    lo = 0;
+    TRY(cv.lt(Y[1], Y[0], r));
+    if (r) {
+      lo = 1;
+    } else {
+      TRY(cv.lt(Y[0], Y[1], r));
+      if (r) hi = 1;  // s_hi stays 0
     }
     const double mp = X[1 - hi];
     const double xc = mp - (-1.0) * (mp - X[hi]);
-    // speculative batch: reflection, expansion, both contractions and both
-    // contract-by-best outcomes
     {
       double pts[CV_MAX_PTS];
       int np = 0;
@@ -750,73 +1066,82 @@ int min_search(kg_tmcmc_s *h, double exponent, double objCov, double &xmin, doub
         for (size_t i = 0; i < 2; i++)
           if (i != lo) pts[np++] = 0.5 * (Xv[i] + Xv[lo]);
       }
-      if (cv.batch(pts, np)) return 1;
+      TRY(cv.batch(pts, np));
     }
-    double val = cv.eval(xc, rc);
-    if (std::isfinite(val) && val < Y[lo]) {
+    YV v;
+    TRY(cv.get(xc, v));
+    TRY(cv.lt(v, Y[lo], r));
+    if (r) {
+      YV v2;
       const double xc2 = mp - (-2.0) * (mp - X[hi]);
-      const double val2 = cv.eval(xc2, rc);
-      if (std::isfinite(val2) && val2 < Y[lo]) {
+      TRY(cv.get(xc2, v2));
+      TRY(cv.lt(v2, Y[lo], r));
+      if (r) {
         X[hi] = xc2;
-        Y[hi] = val2;
+        Y[hi] = v2;
       } else {
         X[hi] = xc;
-        Y[hi] = val;
-      }
-    } else if (!std::isfinite(val) || val > Y[s_hi]) {
-      if (std::isfinite(val) && val <= Y[hi]) {
-        X[hi] = xc;
-        Y[hi] = val;
-      }
-      const double xc2 = mp - 0.5 * (mp - X[hi]);
-      const double val2 = cv.eval(xc2, rc);
-      if (std::isfinite(val2) && val2 <= Y[hi]) {
-        X[hi] = xc2;
-        Y[hi] = val2;
-      } else {
-        for (size_t i = 0; i < 2; i++)
-          if (i != lo) {
-            X[i] = 0.5 * (X[i] + X[lo]);
-            Y[i] = cv.eval(X[i], rc);
-          }
+        Y[hi] = v;
       }
     } else {
-      X[hi] = xc;
-      Y[hi] = val;
-    }
-    // gsl_vector_min_index (NaN wins)
-    lo = 0;
-    {
-      double mn = Y[0];
-      for (size_t i = 0; i < 2; i++) {
-        if (Y[i] < mn) {
-          mn = Y[i];
-          lo = i;
+      TRY(cv.lt(Y[s_hi], v, r));
+      if (r) {
+        TRY(cv.le(v, Y[hi], r));
+        if (r) {
+          X[hi] = xc;
+          Y[hi] = v;
         }
-        if (Y[i] != Y[i]) {
-          lo = i;
-          break;
+        YV v2;
+        const double xc2 = mp - 0.5 * (mp - X[hi]);
+        TRY(cv.get(xc2, v2));
+        TRY(cv.le(v2, Y[hi], r));
+        if (r) {
+          X[hi] = xc2;
+          Y[hi] = v2;
+        } else {
+          for (size_t i = 0; i < 2; i++)
+            if (i != lo) {
+              X[i] = 0.5 * (X[i] + X[lo]);
+              TRY(cv.get(X[i], Y[i]));
+            }
         }
+      } else {
+        X[hi] = xc;
+        Y[hi] = v;
       }
     }
-    xbest = X[lo];
-    fval = Y[lo];
-    size = simplex_size(X);
-    status = (size < Tol) ? 0 : 1;
-  } while (status == 1 && iter < MaxIter && rc == 0);
-  if (rc) return 1;
+    // gsl_vector_min_index
+    TRY(cv.lt(Y[1], Y[0], r));
+    lo = r ? 1 : 0;
+    status = (simplex_size(X) < Tol) ? 0 : 1;
+  } while (status == 1 && iter < MaxIter);
+  TRY(cv.exact(Y[lo]));
   fmin = 0;
   xmin = 0.0;
-  if (fval <= Tol) {
-    fmin = fval;
-    xmin = xbest;
+  if (Y[lo].y <= Tol) {
+    fmin = Y[lo].y;
+    xmin = X[lo];
   }
   if (xmin >= 1.0) {
-    fmin = cv.eval(1.0, rc);
+    YV one;
+    one.x = 1.0;
+    TRY(cv.exact(one));
+    fmin = one.y;
     xmin = 1.0;
   }
   iters = iter;
-  return rc;
+  h->exactEvals += cv.exactEvals;
+  return 0;
+}
+
+// the reference's squared CoV difference at x, exactly
+int cv2_exact(kg_tmcmc_s *h, double exponent, double x, double &y) {
+  CvSearch cv{h, exponent, h->cfg.target_cov};
+  YV v;
+  v.x = x;
+  if (cv.exact(v)) return 1;
+  y = v.y;
+  return 0;
 }
 
 int tm_initialize(kg_tmcmc_s *h) {
@@ -877,6 +1202,7 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Database Entries", dbCount)
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Min Search Iterations", minSearchIterations)
+  SCA("Exact Search Evaluations", exactEvalsD)
 #undef VEC
 #undef SCA
   return false;
@@ -937,18 +1263,28 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   rc |= tdalloc(&h->cov, (size_t)N * N) | tdalloc(&h->chol, (size_t)N * N) | tdalloc(&h->db, PN);
   rc |= tdalloc(&h->dbLL, P) | tdalloc(&h->dbLP, P) | tdalloc(&h->numSel, P) | tdalloc(&h->pmin, N);
   rc |= tdalloc(&h->pmax, N) | tdalloc(&h->negLogWidth, N) | tdalloc(&h->Z, PN) | tdalloc(&h->U, P);
-  rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)CV_MAX_PTS * P) | tdalloc(&h->w, P);
+  rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)(CV_MAX_PTS + 1) * P) | tdalloc(&h->w, P);
   rc |= tdalloc(&h->uoff, N) | tdalloc(&h->ustride, N) | tdalloc(&h->src, P) | tdalloc(&h->acc, P);
-  rc |= tdalloc(&h->dev, 1);
+  rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
+  rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
   if (rc) {
     delete h;
     return 1;
   }
-  KG_HIP(hipHostMalloc(&h->hE, (size_t)CV_MAX_PTS * P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hE, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hSrc, (size_t)P * sizeof(unsigned), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hDev, sizeof(TmDev), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hCv, (CV_MAX_PTS + 1) * sizeof(CvOut), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc((void **)&h->hRec, 4 * (CV_MAX_PTS + 1) * sizeof(double2),
+                       hipHostMallocCoherent | hipHostMallocMapped));
+  memset(h->hRec, 0, 4 * (CV_MAX_PTS + 1) * sizeof(double2));
+  KG_HIP(hipHostGetDevicePointer((void **)&h->dRec, h->hRec, 0));
+  {
+    const char *ev = getenv("KORALI_AMD_TMCMC_EXACT_SEARCH");
+    h->exactSearch = ev && ev[0] == '1';
+  }
   h->wtmp.resize(P);
   h->nsel.resize(P);
   KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -957,12 +1293,23 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   KG_HIP(hipMemcpy(h->uoff, uoff.data(), N * sizeof(unsigned long long), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->ustride, ustride.data(), N * sizeof(int), hipMemcpyHostToDevice));
   {
+    std::vector<int2> pr;
+    for (int i = 0; i < N; i++)
+      for (int j = i; j < N; j++) pr.push_back(make_int2(i, j));
+    KG_HIP(hipMemcpy(h->pairs, pr.data(), pr.size() * sizeof(int2), hipMemcpyHostToDevice));
+  }
+  {
+    KG_HIP(hipFuncSetAttribute((const void *)k_tm_wsum<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)ws_lds_bytes(N, false)));
+    KG_HIP(hipFuncSetAttribute((const void *)k_tm_wsum<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)ws_lds_bytes(N, true)));
     const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)std::max(1, 256 / N) * N * sizeof(double);
     if (lbytes > 64 * 1024) {
       KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
       KG_HIP(hipFuncSetAttribute((const void *)k_tm_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)((size_t)N * (N + 1) * sizeof(double))));
     }
+
   }
   hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(N, 64)), dim3(64), 0, h->stream, N, h->pmin, h->pmax, h->negLogWidth);
   KG_HIP(hipGetLastError());
@@ -996,9 +1343,9 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->db, (void *)h->dbLL, (void *)h->dbLP, (void *)h->numSel, (void *)h->pmin,
                   (void *)h->pmax, (void *)h->negLogWidth, (void *)h->Z, (void *)h->U, (void *)h->Uprior,
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
-                  (void *)h->dev})
+                  (void *)h->dev, h->cvPart, (void *)h->pairs})
     if (p) (void)hipFree(p);
-  for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev})
+  for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec})
     if (p) (void)hipHostFree(p);
   for (auto *r : h->priorRng) delete r;
   for (auto &t : h->pending) {
@@ -1040,6 +1387,9 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
       TmStage st(h, "rng_polar");
       if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream)) return 1;
       if (h->multivariate.consume_normals(PN, N, nullptr, h->stream)) return 1;
+      // the next generation's words are produced on the side stream while
+      // this generation's search runs on the host
+      if (h->multivariate.prefetch(PN, h->stream)) return 1;
     }
     TmStage st(h, "draw");
     const int CB = std::max(1, 256 / N);
@@ -1104,21 +1454,23 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   }
   if (tm_sync_dev(h)) return 1;
   h->minSearchIterations = (double)iters;
+  h->exactEvalsD = (double)h->exactEvals;
   h->previousAnnealingExponent = h->annealingExponent;
   {
-    CvSearch cv{h, h->previousAnnealingExponent, h->cfg.target_cov};
-    int rc = 0;
-    if (xmin > h->previousAnnealingExponent + h->cfg.max_annealing_exponent_update) {
-      h->annealingExponent = h->previousAnnealingExponent + h->cfg.max_annealing_exponent_update;
-      h->coefficientOfVariation = sqrt(cv.eval(h->annealingExponent, rc)) + h->cfg.target_cov;
-    } else if (xmin < 1.0 && xmin < h->previousAnnealingExponent + h->cfg.min_annealing_exponent_update) {
-      h->annealingExponent = h->previousAnnealingExponent + h->cfg.min_annealing_exponent_update;
-      h->coefficientOfVariation = sqrt(cv.eval(h->annealingExponent, rc)) + h->cfg.target_cov;
+    const double pe = h->previousAnnealingExponent;
+    double y = 0;
+    if (xmin > pe + h->cfg.max_annealing_exponent_update) {
+      h->annealingExponent = pe + h->cfg.max_annealing_exponent_update;
+      if (cv2_exact(h, pe, h->annealingExponent, y)) return 1;
+      h->coefficientOfVariation = sqrt(y) + h->cfg.target_cov;
+    } else if (xmin < 1.0 && xmin < pe + h->cfg.min_annealing_exponent_update) {
+      h->annealingExponent = pe + h->cfg.min_annealing_exponent_update;
+      if (cv2_exact(h, pe, h->annealingExponent, y)) return 1;
+      h->coefficientOfVariation = sqrt(y) + h->cfg.target_cov;
     } else {
       h->annealingExponent = xmin;
       h->coefficientOfVariation = sqrt(fmin) + h->cfg.target_cov;
     }
-    if (rc) return 1;
   }
   const double drho = h->annealingExponent - h->previousAnnealingExponent;
   {
@@ -1159,11 +1511,11 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   KG_HIP(hipMemcpyAsync(h->src, h->hSrc, (size_t)P * sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
   {
     TmStage st(h, "mean_cov");
-    hipLaunchKernelGGL(k_tm_mean, dim3(nblk(N, 64)), dim3(64), 0, h->stream, N, P, h->db, h->w, h->mean);
     const int npairs = N * (N + 1) / 2;
-    const size_t cbytes = (size_t)COV_ROWS * N * sizeof(double) + COV_ROWS * sizeof(double);
-    hipLaunchKernelGGL(k_tm_cov, dim3(nblk(npairs, 256)), dim3(256), cbytes, h->stream, N, P, h->db, h->w, h->mean,
-                       h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
+    hipLaunchKernelGGL(k_tm_wsum<false>, dim3(nblk(N, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, false), h->stream, N, P,
+                       h->db, h->w, h->mean, h->pairs, N, 0.0, 1.0, h->mean);
+    hipLaunchKernelGGL(k_tm_wsum<true>, dim3(nblk(npairs, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, true), h->stream, N, P, h->db,
+                       h->w, h->mean, h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
     KG_HIP(hipGetLastError());
   }
   {

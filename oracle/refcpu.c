@@ -121,8 +121,15 @@ static dd_t dd_log(double x)
   return dd_add(dd_mul_d(DD_LN2, (double)k), p);
 }
 
+/* KR_LIBM_TIMING: timing-only build (librefcpu_libm.so) that calls the
+ * system libm instead of the correctly-rounded evaluations, i.e. runs at the
+ * speed the reference itself would on this host.  Not bit-exact; used only
+ * as the conservative CPU baseline in bench.py. */
 double kr_log_cr(double x)
 {
+#ifdef KR_LIBM_TIMING
+  return log(x);
+#endif
   if (!(x > 0.0) || isinf(x)) return log(x);
   if (x == 1.0) return 0.0;
   if (x < 2.2250738585072014e-308) return kr_log_cr(x * 18014398509481984.0) - 37.42994775023704; /* rare */
@@ -152,6 +159,9 @@ static dd_t dd_exp(dd_t a)
 
 double kr_exp_cr(double x)
 {
+#ifdef KR_LIBM_TIMING
+  return exp(x);
+#endif
   if (isnan(x)) return x;
   if (x > 709.0 || x < -708.0) return exp(x); /* out of the dd range: libm */
   if (x == 0.0) return 1.0;
@@ -163,6 +173,9 @@ double kr_exp_cr(double x)
 
 double kr_pow_cr(double x, double y)
 {
+#ifdef KR_LIBM_TIMING
+  return pow(x, y);
+#endif
   if (y == 2.0) return x * x;
   if (!(x > 0.0) || isinf(x) || isinf(y) || isnan(y)) return pow(x, y);
   {

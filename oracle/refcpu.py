@@ -10,17 +10,19 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = None
+_LIBS = {}
+# "cr": the bit-exact oracle; "libm": timing-only build with the system libm
+# log/exp/pow (the speed the reference itself would run at; not bit-exact)
+_VARIANTS = {"cr": "librefcpu.so", "libm": "librefcpu_libm.so"}
 
 
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
-def lib():
-    global _LIB
-    if _LIB is None:
-        path = os.path.join(_HERE, "librefcpu.so")
+def lib(variant="cr"):
+    if variant not in _LIBS:
+        path = os.path.join(_HERE, _VARIANTS[variant])
         if not os.path.exists(path):
             build()
         L = C.CDLL(path)
@@ -79,8 +81,8 @@ def lib():
         L.kr_tmcmc_minsearch.restype = sz
         L.kr_tmcmc_cv2.argtypes = [C.c_double, dp, sz, C.c_double, C.c_double]
         L.kr_tmcmc_cv2.restype = C.c_double
-        _LIB = L
-    return _LIB
+        _LIBS[variant] = L
+    return _LIBS[variant]
 
 
 RNG_BYTES = 5000
@@ -144,8 +146,8 @@ class CMAES:
     MU_TYPES = {"Logarithmic": 0, "Linear": 1, "Equal": 2, "Proportional": 3}
     OBJECTIVES = {"rosenbrock": 0, "ackley": 1, "sphere": 2}
 
-    def __init__(self, N, lam, mu=0):
-        self.L = lib()
+    def __init__(self, N, lam, mu=0, variant="cr"):
+        self.L = lib(variant)
         self.h = self.L.kr_cmaes_new(N, lam, mu)
         self.N, self.lam = N, lam
         self.mu = mu if mu else lam // 2
@@ -202,8 +204,8 @@ class CMAES:
 
 
 class TMCMC:
-    def __init__(self, N, P):
-        self.L = lib()
+    def __init__(self, N, P, variant="cr"):
+        self.L = lib(variant)
         self.h = self.L.kr_tmcmc_new(N, P)
         self.N, self.P = N, P
 

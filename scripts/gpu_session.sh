@@ -21,9 +21,11 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1200 python -m pytest tests -x -q -m gpu ;;
     tm) step tm 900 python -m pytest tests/test_gpu_tmcmc.py -q --maxfail=10 ;;
+    c3) step c3 600 python bench.py --workload c3 --steps ${C3_STEPS:-40} --warmup 3 ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;
     benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    profc3) step profc3 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c3" -o run --output-format csv -- python bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac

@@ -78,13 +78,13 @@ SCA_KEYS = ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", 
             "Selection Acceptance Rate", "Model Evaluation Count", "Min Search Iterations")
 
 
-def seeded_pair(N, P, shared_prior, seed=1337, target_cov=1.0):
+def seeded_pair(N, P, shared, seed=1337, target_cov=1.0):
     """C3-style experiment: every variable with a U(-5, 5) prior, Gaussian
     loglik -0.5|x|^2; seeds in Korali's consumption order (distributions,
     then the solver's Multinomial, Multivariate, Uniform generators)."""
     from korali_amd.native import TmcmcDevice
-    ndist = 1 if shared_prior else N
-    pdist = [0] * N if shared_prior else list(range(N))
+    ndist = 1 if shared else N
+    pdist = [0] * N if shared else list(range(N))
     seeds = [seed + k for k in range(ndist)]
     sm, sv, su = seed + ndist, seed + ndist + 1, seed + ndist + 2
     dev = TmcmcDevice(N, P, prior_min=[-5.0] * N, prior_max=[5.0] * N, prior_seeds=seeds, prior_distribution=pdist,
@@ -118,3 +118,33 @@ def test_tmcmc_seeded_run_matches_oracle(N, P, gens, shared):
             break
     for which in range(3 + ndist):
         assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
+
+
+@pytest.mark.parametrize("seed,target_cov", [(11, 0.5), (12, 2.0), (13, 1.0)])
+def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov):
+    """The annealing search decides on device-side interval estimates and
+    falls back to the host's exact evaluation only when they overlap: the
+    whole run must equal the all-exact search and the oracle."""
+    N, P = 6, 1024
+    runs = []
+    for exact in ("0", "1"):
+        monkeypatch.setenv("KORALI_AMD_TMCMC_EXACT_SEARCH", exact)
+        dev, o, ndist = seeded_pair(N, P, shared=True, seed=seed, target_cov=target_cov)
+        hist = []
+        for g in range(1, 30):
+            dev.generation(g)
+            hist.append((dev["Annealing Exponent"][0], dev["Coefficient Of Variation"][0], dev["LogEvidence"][0],
+                         dev["Covariance Matrix"].tobytes(), dev["Min Search Iterations"][0]))
+            if dev["Annealing Exponent"][0] >= 1.0:
+                break
+        runs.append((hist, dev["Exact Search Evaluations"][0]))
+        if exact == "0":
+            for g in range(1, len(hist) + 1):
+                o.generation(g)
+                assert o["Annealing Exponent"][0] == hist[g - 1][0], g
+                assert o["Coefficient Of Variation"][0] == hist[g - 1][1], g
+                assert o["LogEvidence"][0] == hist[g - 1][2], g
+                assert o["Covariance Matrix"].tobytes() == hist[g - 1][3], g
+    assert runs[0][0] == runs[1][0]
+    # the interval path needs far fewer exact host evaluations
+    assert runs[0][1] < runs[1][1]
