@@ -23,6 +23,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
@@ -401,33 +402,48 @@ __global__ void k_tm_lw_exp(int P, const double *__restrict__ ll, double drho, c
 // order, so the result is bit-identical):
 //   mean_i = sum_j db[j][i] w_j
 //   cov_ij = covScaling * s / (1 - sum w^2),  s = sum_k w_k (x_ki - m_i)(x_kj - m_j),  j >= i
-// One lane per output element in wave 0 of each workgroup; three more
-// waves stream the database and precompute the factors the reference forms
-// (left to right, so identical roundings):
+// The factors of every term are formed first by fully parallel kernels,
+// in the reference's operand order (left to right, identical roundings):
 //   mean: T[k][i]  = db[k][i] * w_k
-//   cov : WD[k][i] = w_k * (db[k][i] - m_i),  D[k][i] = db[k][i] - m_j
-// into a double-buffered LDS tile of up to 256 rows; the computing wave
-// then does one LDS read (mean) or two and one multiply (cov) per add, and
-// its dependent add chain (14 cycles per add on gfx950,
+//   cov : WD[k][i] = w_k * (db[k][i] - m_i),  D[k][i] = db[k][i] - m_i
+// (cov term = WD[k][i] * D[k][j]).  The ordered sums then use one lane per
+// output element in wave 0 of each workgroup; three more waves stream the
+// factor rows into a double-buffered LDS tile (16-byte loads, all in flight
+// at once), the computing wave reads the next terms while adding the
+// current ones, and its dependent add chain (14 cycles per add on gfx950,
 // tools/ubench_chain.hip) is the cost.
-constexpr int WS_TPB = 256, WS_LANES = 64, WS_MAXV = 32;
+__global__ void k_tm_factors_mean(int N, int P, const double *__restrict__ db, const double *__restrict__ w,
+                                  double *__restrict__ T) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < (size_t)P * N) T[e] = db[e] * w[e / N];
+}
+__global__ void k_tm_factors_cov(int N, int P, const double *__restrict__ db, const double *__restrict__ w,
+                                 const double *__restrict__ mean, double *__restrict__ WD, double *__restrict__ D) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)P * N) return;
+  const double d = db[e] - mean[e % N];
+  WD[e] = w[e / N] * d;
+  D[e] = d;
+}
+
+constexpr int WS_TPB = 256, WS_LANES = 64, WS_MAXV = 16;  // 16 x 16-byte loads per thread per array
 __host__ __device__ inline int ws_rows(int N, bool cov) {
-  const int r = (WS_TPB * WS_MAXV / (cov ? 2 * N : N)) & ~7;
+  const int r = (WS_TPB * WS_MAXV * 2 / (cov ? 2 * N : N)) & ~7;
   return r < 8 ? 8 : (r > 256 ? 256 : r);
 }
 __host__ __device__ inline size_t ws_lds_bytes(int N, bool cov) {
   return 2 * (size_t)ws_rows(N, cov) * N * (cov ? 2 : 1) * sizeof(double);
 }
 template <bool COV>
-__global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *__restrict__ db,
-                                                    const double *__restrict__ w, const double *__restrict__ mean,
-                                                    const int2 *__restrict__ pairs, int nout, double scaling,
-                                                    double denom, double *__restrict__ out) {
+__global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *__restrict__ A,
+                                                    const double *__restrict__ B, const int2 *__restrict__ pairs,
+                                                    int nout, double scaling, double denom,
+                                                    double *__restrict__ out) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
   extern __shared__ double sm[];
-  __shared__ double msh[TM_MAX_N];
   const int rows = ws_rows(N, COV);
-  const int tile = rows * N;
-  const int buf = COV ? 2 * tile : tile;  // one buffer: T, or WD then D
+  const int tile = rows * N;              // even: rows is a multiple of 8
+  const int buf = COV ? 2 * tile : tile;  // one buffer: A tile, then B tile
   const int nchunks = (P + rows - 1) / rows;
   const int tid = threadIdx.x, oidx = blockIdx.x * WS_LANES + tid;
   const bool active = tid < WS_LANES && oidx < nout;
@@ -441,47 +457,42 @@ __global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *
       pi = oidx;
     }
   }
-  if (COV)
-    for (int i = tid; i < N; i += WS_TPB) msh[i] = mean[i];
-  // each thread's tile elements e = tid + v*WS_TPB: row e / N, column e % N
-  int col[WS_MAXV], row[WS_MAXV];
-#pragma unroll
-  for (int v = 0; v < WS_MAXV; v++) {
-    const int e = tid + v * WS_TPB;
-    row[v] = e / N;
-    col[v] = e - row[v] * N;
-  }
-  double xr[WS_MAXV], wr[WS_MAXV];
+  d2v ra[WS_MAXV], rb[WS_MAXV];
   int lim = 0;
-  // branch-free loads (clamped indices, zeroed past the end): every lane
-  // issues its loads back to back, a tile costs one memory latency
+  // branch-free 16-byte loads (clamped pair index, zeroed past the end; the
+  // factor arrays carry 2 doubles of padding)
   auto fetch = [&](int c) {
     const int r0 = c * rows, nk = min(rows, P - r0);
-    const double *base = db + (size_t)r0 * N;
+    const d2v *a = (const d2v *)(A + (size_t)r0 * N), *b = (const d2v *)(B + (size_t)r0 * N);
     lim = nk * N;
+    const int lastp = (lim - 1) >> 1;
 #pragma unroll
     for (int v = 0; v < WS_MAXV; v++) {
-      xr[v] = base[min(tid + v * WS_TPB, lim - 1)];
-      wr[v] = w[r0 + min(row[v], nk - 1)];
+      if (v * WS_TPB * 2 < tile) {  // uniform
+        const int pidx = min(tid + v * WS_TPB, lastp);
+        ra[v] = a[pidx];
+        if (COV) rb[v] = b[pidx];
+      }
     }
   };
-  auto store = [&](double *b) {
+  auto store = [&](double *dst) {
 #pragma unroll
     for (int v = 0; v < WS_MAXV; v++) {
-      const int e = tid + v * WS_TPB;
+      const int e = 2 * (tid + v * WS_TPB);
       if (e < tile) {
-        const bool ok = e < lim;
+        d2v x = ra[v];
+        x.x = e < lim ? x.x : 0.0;
+        x.y = e + 1 < lim ? x.y : 0.0;
+        *(d2v *)(dst + e) = x;
         if (COV) {
-          const double d = xr[v] - msh[col[v]];
-          b[e] = ok ? wr[v] * d : 0.0;
-          b[tile + e] = ok ? d : 0.0;
-        } else {
-          b[e] = ok ? xr[v] * wr[v] : 0.0;
+          d2v y = rb[v];
+          y.x = e < lim ? y.x : 0.0;
+          y.y = e + 1 < lim ? y.y : 0.0;
+          *(d2v *)(dst + tile + e) = y;
         }
       }
     }
   };
-  __syncthreads();  // msh
   fetch(0);
   store(sm);
   __syncthreads();
@@ -493,8 +504,8 @@ __global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *
     if (active) {
       // software-pipelined: the next 8 terms are read while the current 8
       // are added, so the LDS latency stays off the add chain
-      const double *A = cur, *Bm = cur + tile;
-      auto term = [&](int r) { return COV ? A[r * N + pi] * Bm[r * N + pj] : A[r * N + pi]; };
+      const double *Ta = cur, *Tb = cur + tile;
+      auto term = [&](int r) { return COV ? Ta[r * N + pi] * Tb[r * N + pj] : Ta[r * N + pi]; };
       int r = 0;
       if (nk >= 16) {
         double ta[8], tb[8];
@@ -750,7 +761,8 @@ struct kg_tmcmc_s {
          *dbLL = nullptr, *dbLP = nullptr, *numSel = nullptr, *pmin = nullptr, *pmax = nullptr,
          *negLogWidth = nullptr, *Z = nullptr, *U = nullptr, *Uprior = nullptr, *E = nullptr, *w = nullptr;
   unsigned long long *uoff = nullptr;
-  int2 *pairs = nullptr;    // upper-triangle (i, j), j >= i, row-major
+  int2 *pairs = nullptr;
+  double *fA = nullptr, *fB = nullptr;  // P x N term factors of the ordered sums (+2 padding)    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
   unsigned *src = nullptr;
   unsigned char *acc = nullptr;
@@ -1266,6 +1278,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)(CV_MAX_PTS + 1) * P) | tdalloc(&h->w, P);
   rc |= tdalloc(&h->uoff, N) | tdalloc(&h->ustride, N) | tdalloc(&h->src, P) | tdalloc(&h->acc, P);
   rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
+  rc |= tdalloc(&h->fA, PN + 2) | tdalloc(&h->fB, PN + 2);
   rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
   if (rc) {
     delete h;
@@ -1338,12 +1351,14 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
 int kg_tmcmc_destroy(kg_tmcmc_t h) {
   if (!h) return 0;
   (void)hipStreamSynchronize(h->stream);
+
   for (void *p : {(void *)h->leaders, (void *)h->leadLL, (void *)h->leadLP, (void *)h->cand, (void *)h->candLL,
                   (void *)h->candLP, (void *)h->chainLen, (void *)h->mean, (void *)h->cov, (void *)h->chol,
                   (void *)h->db, (void *)h->dbLL, (void *)h->dbLP, (void *)h->numSel, (void *)h->pmin,
                   (void *)h->pmax, (void *)h->negLogWidth, (void *)h->Z, (void *)h->U, (void *)h->Uprior,
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
-                  (void *)h->dev, h->cvPart, (void *)h->pairs})
+                  (void *)h->dev, h->cvPart, (void *)h->pairs,
+                  (void *)h->fA, (void *)h->fB})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec})
     if (p) (void)hipHostFree(p);
@@ -1512,10 +1527,13 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   {
     TmStage st(h, "mean_cov");
     const int npairs = N * (N + 1) / 2;
+    hipLaunchKernelGGL(k_tm_factors_mean, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->fA);
     hipLaunchKernelGGL(k_tm_wsum<false>, dim3(nblk(N, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, false), h->stream, N, P,
-                       h->db, h->w, h->mean, h->pairs, N, 0.0, 1.0, h->mean);
-    hipLaunchKernelGGL(k_tm_wsum<true>, dim3(nblk(npairs, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, true), h->stream, N, P, h->db,
-                       h->w, h->mean, h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
+                       h->fA, h->fA, h->pairs, N, 0.0, 1.0, h->mean);
+    hipLaunchKernelGGL(k_tm_factors_cov, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->mean,
+                       h->fA, h->fB);
+    hipLaunchKernelGGL(k_tm_wsum<true>, dim3(nblk(npairs, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, true), h->stream,
+                       N, P, h->fA, h->fB, h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
     KG_HIP(hipGetLastError());
   }
   {
