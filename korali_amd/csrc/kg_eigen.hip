@@ -431,14 +431,17 @@ __global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict
     M[idx] = (r < N && c == r) ? 1.0 : 0.0;
   }
   __syncthreads();
+  double *wsh = h + N;  // w_j = col_j . h (phase 1 result)
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   for (int i = N - 3; i >= 0; i--) {
     const double ti = tau[i];
     if (ti == 0.0) continue;  // householder_hm returns early
     const int n = N - (i + 1);
     for (int r = tid; r < n; r += nt) h[r] = gH[(size_t)i * N + r];
     __syncthreads();
+    // phase 1: w_j = sum_r Q[i+1+r][i+1+j] h[r], one ordered chain per j
     for (int j = tid; j < n; j += nt) {
-      double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
+      const double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
       double wj = col[0];
       for (int r0 = 1; r0 < n; r0 += 16) {
         double p[16];
@@ -451,8 +454,14 @@ __global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict
 #pragma unroll
         for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding is exact (see k_tridiag)
       }
-      col[0] = col[0] - ti * wj;
-      for (int r = 1; r < n; r++) col[r] = col[r] - ti * h[r] * wj;
+      wsh[j] = wj;
+    }
+    __syncthreads();
+    // phase 2 (every wave): Q[.][j] -= tau h w_j, element-parallel
+    for (int j = wid; j < n; j += nw) {
+      double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);
+      const double wj = wsh[j];
+      for (int r = lane; r < n; r += 64) col[r] = (r == 0) ? col[0] - ti * wj : col[r] - ti * h[r] * wj;
     }
     __syncthreads();
   }
@@ -545,6 +554,15 @@ __global__ void __launch_bounds__(64) k_chase(int N, const double *__restrict__ 
   qr_chase(N, d, sd, r, maxRot, gc, gs);
 }
 
+// rotations per LDS chunk of k_apply: what fits after the matrix, and at
+// least one whole QR step (<= N - 1 rotations)
+__host__ __device__ inline int apply_cap(int N, bool lds) {
+  const long long avail = 160LL * 1024 - (lds ? (long long)N * (N + 1) * 8 : 0) - 1024;
+  long long c = avail / 16;
+  if (c > 8192) c = 8192;
+  return (int)(c < N ? N : c);
+}
+
 // Phase C application + phase D write-back (CMAES::updateEigensystem).
 // Row k of Q (a thread) replays every Givens rotation in GSL's order:
 // (Q[k][a+i], Q[k][a+i+1]) = (qi c - qj s, qi s + qj c).
@@ -564,22 +582,57 @@ __global__ void __launch_bounds__(1024) k_apply(int N, const double *__restrict_
     if (tid == 0) atomicOr(errors, KG_ERR_EIGEN);
     return;
   }
-  for (int k = tid; k < N; k += nt) {
-    int ro = 0;
-    for (int t = 0; t < steps; t++) {
-      const int a = r.hdr[2 * t], nb = r.hdr[2 * t + 1];
-      double qi = M[(size_t)a * lda + k];
-      for (int i = 0; i + 1 < nb; i++) {
-        const double c = r.cs[2 * (ro + i)], s = r.cs[2 * (ro + i) + 1];
-        const double qj = M[(size_t)(a + i + 1) * lda + k];
-        M[(size_t)(a + i) * lda + k] = qi * c - qj * s;
-        qi = qi * s + qj * c;
-      }
-      M[(size_t)(a + nb - 1) * lda + k] = qi;
-      ro += nb - 1;
+  // The rotation stream is staged through LDS in chunks of whole QR steps
+  // (cooperative loads, then broadcast reads); row k's thread replays the
+  // chunk with the rows of the current step prefetched 8 ahead (a step only
+  // reads rows it has not written yet).
+  double *csh = smem + (kLds ? (size_t)N * lda : 0);
+  const int cap = apply_cap(N, kLds);  // rotations per chunk
+  int t0 = 0, ro0 = 0;
+  while (t0 < steps) {
+    int t1 = t0, nrot = 0;
+    while (t1 < steps && nrot + (r.hdr[2 * t1 + 1] - 1) <= cap) {
+      nrot += r.hdr[2 * t1 + 1] - 1;
+      t1++;
     }
+    for (int idx = tid; idx < 2 * nrot; idx += nt) csh[idx] = r.cs[2 * (size_t)ro0 + idx];
+    __syncthreads();
+    for (int k = tid; k < N; k += nt) {
+      int ro = 0;
+      for (int t = t0; t < t1; t++) {
+        const int a = r.hdr[2 * t], nb = r.hdr[2 * t + 1];
+        double *col = M + (size_t)a * lda + k;  // col[i * lda] = Q[a+i][k]
+        double qi = col[0];
+        const double *cs = csh + 2 * ro;
+        int i = 0;
+        for (; i + 8 < nb; i += 8) {
+          double qj[8], c[8], sn[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            qj[u] = col[(size_t)(i + 1 + u) * lda];
+            c[u] = cs[2 * (i + u)];
+            sn[u] = cs[2 * (i + u) + 1];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            col[(size_t)(i + u) * lda] = qi * c[u] - qj[u] * sn[u];
+            qi = qi * sn[u] + qj[u] * c[u];
+          }
+        }
+        for (; i + 1 < nb; i++) {
+          const double c = cs[2 * i], sn = cs[2 * i + 1];
+          const double qj = col[(size_t)(i + 1) * lda];
+          col[(size_t)i * lda] = qi * c - qj * sn;
+          qi = qi * sn + qj * c;
+        }
+        col[(size_t)(nb - 1) * lda] = qi;
+        ro += nb - 1;
+      }
+    }
+    __syncthreads();
+    t0 = t1;
+    ro0 += nrot;
   }
-  __syncthreads();
   // updateEigensystem: min/max eigenvalue; keep old B, D if min <= 0
   double mn = r.eval[0], mx = r.eval[0];
   for (int i = 1; i < N; i++) {
@@ -631,7 +684,7 @@ __global__ void __launch_bounds__(256) k_eigen_diag(int N, const double *__restr
 // ------------------------------------------------------------------------
 // Orchestration
 size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
-bool eig_use_lds(int N) { return eig_mat_bytes(N) + (size_t)(N + 16) * sizeof(double) + 256 <= 160 * 1024; }
+bool eig_use_lds(int N) { return eig_mat_bytes(N) + (size_t)(2 * N + 16) * sizeof(double) + 256 <= 160 * 1024; }
 
 int EigenSolver::init(int N_, bool hostChase_) {
   N = N_;
@@ -717,9 +770,9 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   }
   if (prof) prof(profCtx, "eigen_unpack", 0);
   if (lds)
-    hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + N * sizeof(double), s, N, gH, tau, gQt);
+    hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + 2 * N * sizeof(double), s, N, gH, tau, gQt);
   else
-    hipLaunchKernelGGL(k_unpack<false>, dim3(1), dim3(1024), N * sizeof(double), s, N, gH, tau, gQt);
+    hipLaunchKernelGGL(k_unpack<false>, dim3(1), dim3(1024), 2 * N * sizeof(double), s, N, gH, tau, gQt);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_unpack", 1);
   if (hostChase) {
@@ -740,11 +793,11 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   }
   if (prof) prof(profCtx, "eigen_apply", 0);
   if (lds)
-    hipLaunchKernelGGL(k_apply<true>, dim3(1), dim3(1024), matb, s, N, gQt, gWork, devRec, B, D, minEig, maxEig,
-                       eigenFailures, errors);
+    hipLaunchKernelGGL(k_apply<true>, dim3(1), dim3(1024), matb + 16 * (size_t)apply_cap(N, true), s, N, gQt, gWork,
+                       devRec, B, D, minEig, maxEig, eigenFailures, errors);
   else
-    hipLaunchKernelGGL(k_apply<false>, dim3(1), dim3(1024), 0, s, N, gQt, gQt, devRec, B, D, minEig, maxEig,
-                       eigenFailures, errors);
+    hipLaunchKernelGGL(k_apply<false>, dim3(1), dim3(1024), 16 * (size_t)apply_cap(N, false), s, N, gQt, gQt, devRec,
+                       B, D, minEig, maxEig, eigenFailures, errors);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_apply", 1);
   return 0;
