@@ -232,6 +232,9 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
   double *M = kLds ? smem : gA;
   double *vb = kLds ? smem + (size_t)N * lda : smem;
   double *x = vb, *scal = vb + N;
+  double *sv = vb + N + 16;  // staged addends of a serial chain (wave 0); t2 of dsymv
+  double *tv = sv + (N > 64 ? N : 64);  // tau * v_r, contiguous (dsymv)
+  double *vv = tv + N;       // v_r with v_0 = 1, contiguous (dsymv)
   unsigned long long acc_t[4] = {0, 0, 0, 0}, tmark = 0;
 #define KG_MARK() \
   if (trace && tid == 0) tmark = __builtin_amdgcn_s_memtime();
@@ -277,19 +280,35 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
           }
         }
         // addends precomputed lane-parallel; zero elements add +0.0, which
-        // leaves ssq (>= 1) unchanged, so only new-maximum lanes branch
+        // leaves ssq (>= 1) unchanged.  The serial recurrence then runs on
+        // values staged in LDS, 8 in flight, new-maximum lanes (a handful
+        // per vector) taking the rescaling branch.
         const double tq = (type == 2) ? q * q : 0.0;
         const unsigned long long m1 = __ballot(type == 1);
         const int cnt = (n - base) < 64 ? (n - base) : 64;
-#pragma unroll 8
-        for (int l = 0; l < cnt; l++) {
-          if ((m1 >> l) & 1ULL) {
-            const double qq = readlane_d(q, l);
-            ssq = 1.0 + ssq * qq * qq;
+        sv[lane] = (type == 1) ? q : tq;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int l0 = 0; l0 < cnt; l0 += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];  // lanes past n staged +0.0
+          const unsigned bits = (unsigned)((m1 >> l0) & 0xffULL);
+          if (bits == 0) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) ssq += t[u];
           } else {
-            ssq += readlane_d(tq, l);
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              if ((bits >> u) & 1u)
+                ssq = 1.0 + ssq * t[u] * t[u];
+              else
+                ssq += t[u];
+            }
           }
         }
+        __builtin_amdgcn_wave_barrier();
         scale_carry = fmax(scale_carry, readlane_d(pm, 63));
       }
       if (lane == 0) {
@@ -335,49 +354,80 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
     if (tau_i == 0.0) continue;
     KG_MARK()
     // x = tau * m * v (dsymv RowMajor Lower, beta = 0), v0 := 1
-    for (int j = tid; j < n; j += nt) {
-      const double vj = (j == 0) ? 1.0 : v[(size_t)j * lda];
-      // two sequential chains, loads and products issued 16 at a time:
-      //   acc: rows r = n-1 .. j+1 (descending)      t2: cols ii = 0 .. j-1
-      // Past its own length a chain adds +0.0, which is exact here (neither
-      // running sum can be -0.0: both start at +0.0 under round-to-nearest).
-      const int L1 = n - 1 - j, L2 = j, L = L1 > L2 ? L1 : L2;
-      double acc = 0.0, t2 = 0.0;
-      for (int q0 = 0; q0 < L; q0 += 16) {
-        double p1[16], p2[16];
+    for (int r = tid; r < n; r += nt) {
+      const double vr = (r == 0) ? 1.0 : v[(size_t)r * lda];
+      vv[r] = vr;
+      tv[r] = tau_i * vr;
+    }
+    __syncthreads();
+    // The two sequential chains of output j run on different waves (all four
+    // SIMDs busy), products formed inline, 8 at a time, loads unconditional:
+    //   acc_j: rows r = n-1 .. j+1 (descending) of (tau v_r) m[r][j]   (thread j)
+    //   t2_j : cols q = 0 .. j-1 of v_q m[j][q]                        (thread 128 + j)
+    // then x_j = (acc_j + (tau v_j) m[j][j]) + tau t2_j.
+    double *t2b = sv;  // t2 of every j (sv holds max(N, 64) doubles)
+    const int half = (nt / 2) & ~63;
+    if (tid < half) {
+      for (int j = tid; j < n; j += half) {
+        double acc = 0.0;
+        int r = n - 1;
+        const double *mc = m + j;
+        for (; r - 7 > j; r -= 8) {
+          double p[8];
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-          const int q = q0 + u;
-          const int r = max(n - 1 - q, 0), qc = min(q, n - 1);
-          const double pa = (tau_i * v[(size_t)r * lda]) * m[(size_t)r * lda + j];
-          const double vq = v[(size_t)qc * lda];
-          const double pb = ((q == 0) ? 1.0 : vq) * m[(size_t)j * lda + qc];
-          p1[u] = (q < L1) ? pa : 0.0;
-          p2[u] = (q < L2) ? pb : 0.0;
-        }
+          for (int u = 0; u < 8; u++) p[u] = tv[r - u] * mc[(size_t)(r - u) * lda];
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-          acc += p1[u];
-          t2 += p2[u];
+          for (int u = 0; u < 8; u++) acc += p[u];
         }
+        for (; r > j; r--) acc += tv[r] * mc[(size_t)r * lda];
+        x[j] = acc;
       }
-      acc += (tau_i * vj) * m[(size_t)j * lda + j];
-      acc += tau_i * t2;
+    } else {
+      for (int j = tid - half; j < n; j += nt - half) {
+        const double *mj = m + (size_t)j * lda;
+        double t2 = 0.0;
+        int q = 0;
+        for (; q + 8 <= j; q += 8) {
+          double p[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) p[u] = vv[q + u] * mj[q + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t2 += p[u];
+        }
+        for (; q < j; q++) t2 += vv[q] * mj[q];
+        t2b[j] = t2;
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += nt) {
+      double acc = x[j];
+      acc += tv[j] * m[(size_t)j * lda + j];
+      acc += tau_i * t2b[j];
       x[j] = acc;
     }
     __syncthreads();
     KG_ACC(1)
     KG_MARK()
     if (wid == 0) {
-      // xv = sum x[r] v[r] sequentially; alpha = -(tau/2) xv
+      // xv = sum x[r] v[r] sequentially (products lane-parallel, staged in
+      // LDS, 8 in flight; +0.0 padding is exact); alpha = -(tau/2) xv
       double xv = 0.0;
       for (int base = 0; base < n; base += 64) {
         const int r = base + lane, rc = min(r, n - 1);
-        const double p_ = x[rc] * ((rc == 0) ? 1.0 : v[(size_t)rc * lda]);
-        const double p = (r < n) ? p_ : 0.0;
+        const double p_ = x[rc] * vv[rc];
+        sv[lane] = (r < n) ? p_ : 0.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int cnt = (n - base) < 64 ? (n - base) : 64;
-#pragma unroll 8
-        for (int l = 0; l < cnt; l++) xv += readlane_d(p, l);
+        for (int l0 = 0; l0 < cnt; l0 += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) xv += t[u];
+        }
+        __builtin_amdgcn_wave_barrier();
       }
       if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
     }
@@ -684,7 +734,8 @@ __global__ void __launch_bounds__(256) k_eigen_diag(int N, const double *__restr
 // ------------------------------------------------------------------------
 // Orchestration
 size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
-bool eig_use_lds(int N) { return eig_mat_bytes(N) + (size_t)(2 * N + 16) * sizeof(double) + 256 <= 160 * 1024; }
+size_t tridiag_vec_bytes(int N) { return (size_t)(3 * N + 16 + (N > 64 ? N : 64)) * sizeof(double); }
+bool eig_use_lds(int N) { return eig_mat_bytes(N) + tridiag_vec_bytes(N) + 256 <= 160 * 1024; }
 
 int EigenSolver::init(int N_, bool hostChase_) {
   N = N_;
@@ -750,10 +801,10 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
   if (lds)
-    hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), matb + (N + 16) * sizeof(double), s, N, C, gA, gH, tau,
-                       d, sd, trace);
+    hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), matb + tridiag_vec_bytes(N), s, N, C, gA, gH, tau, d, sd,
+                       trace);
   else
-    hipLaunchKernelGGL(k_tridiag<false>, dim3(1), dim3(1024), (N + 16) * sizeof(double), s, N, C, gA, gH, tau, d, sd,
+    hipLaunchKernelGGL(k_tridiag<false>, dim3(1), dim3(1024), tridiag_vec_bytes(N), s, N, C, gA, gH, tau, d, sd,
                        trace);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_tridiag", 1);

@@ -42,45 +42,45 @@ __device__ inline unsigned long long compact_to_abs(const PosView &st, unsigned 
   }
 }
 
-__global__ void __launch_bounds__(64) k_mt_produce(uint32_t *__restrict__ ring, unsigned long long R, StreamState *st,
-                                                   unsigned long long ahead) {
+// One workgroup, 4 waves: every step produces the next 227 words (the
+// recurrence's lag: s_j needs s_{j-624}, s_{j-623}, s_{j-227}), one word per
+// thread, from a 1024-word LDS window; one barrier per step.
+constexpr int MT_TPB = 256;
+__global__ void __launch_bounds__(MT_TPB) k_mt_produce(uint32_t *__restrict__ ring, unsigned long long R,
+                                                       StreamState *st, unsigned long long ahead) {
   __shared__ uint32_t L[1024];
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x;
   const unsigned long long hi0 = st->hi;
   unsigned long long target = st->pos + ahead;
   const unsigned long long cap = st->lo + R;
   if (target > cap) {
-    if (lane == 0) atomicOr(&st->errors, KG_ERR_RNG_UNDERRUN);
+    if (t == 0) atomicOr(&st->errors, KG_ERR_RNG_UNDERRUN);
     target = cap;
   }
   if (hi0 >= target) return;
-  for (int i = lane; i < MT_N; i += 64) {
+  for (int i = t; i < MT_N; i += MT_TPB) {
     const unsigned long long j = hi0 - MT_N + i;
     L[j & 1023] = ring[j & (R - 1)];
   }
   __syncthreads();
   for (unsigned long long c = hi0; c < target; c += 227) {
     const int cnt = (int)((target - c) < 227 ? (target - c) : 227);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int idx = lane + 64 * q;
-      if (idx < cnt) {
-        const unsigned long long j = c + idx;
-        const uint32_t s = mt_next(L[(j - 624) & 1023], L[(j - 623) & 1023], L[(j - 227) & 1023]);
-        L[j & 1023] = s;
-        ring[j & (R - 1)] = s;
-        if (s == 0u) {  // tempered word is zero iff untempered is (bijection)
-          const unsigned int z = atomicAdd(&st->nzero, 1u);
-          if (z < KG_MAX_ZERO_WORDS)
-            st->zeros[z] = j;
-          else
-            atomicOr(&st->errors, KG_ERR_ZERO_LIST);
-        }
+    if (t < cnt) {
+      const unsigned long long j = c + t;
+      const uint32_t s = mt_next(L[(j - 624) & 1023], L[(j - 623) & 1023], L[(j - 227) & 1023]);
+      L[j & 1023] = s;
+      ring[j & (R - 1)] = s;
+      if (s == 0u) {  // tempered word is zero iff untempered is (bijection)
+        const unsigned int z = atomicAdd(&st->nzero, 1u);
+        if (z < KG_MAX_ZERO_WORDS)
+          st->zeros[z] = j;
+        else
+          atomicOr(&st->errors, KG_ERR_ZERO_LIST);
       }
     }
     __syncthreads();
   }
-  if (lane == 0) st->hi = target;
+  if (t == 0) st->hi = target;
 }
 
 __device__ inline bool polar_pair(const uint32_t *__restrict__ ring, unsigned long long R, const PosView &st,
@@ -320,7 +320,7 @@ int MtStream::import_gsl(const void *state5000, hipStream_t s) {
 }
 
 int MtStream::produce(unsigned long long ahead, hipStream_t s) {
-  hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(64), 0, s, ring_, R_, st_, ahead);
+  hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(MT_TPB), 0, s, ring_, R_, st_, ahead);
   KG_HIP(hipGetLastError());
   return 0;
 }
