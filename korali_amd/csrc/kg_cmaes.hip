@@ -1210,8 +1210,12 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
   if (h->eigTrace) {
     unsigned long long t[16];
     KG_HIP(hipMemcpy(t, h->eigTrace, sizeof(t), hipMemcpyDeviceToHost));
-    fprintf(stderr, "[korali_amd tridiag trace, cumulative s_memtime ticks] nrm2 %llu dsymv %llu xv %llu dsyr2 %llu\n",
-            t[0], t[1], t[2], t[3]);
+    int steps = 0, rots = 0;
+    h->eig.last_counts(steps, rots);
+    fprintf(stderr,
+            "[korali_amd tridiag trace, cumulative s_memtime ticks] nrm2 %llu dsymv %llu xv %llu dsyr2 %llu; last QR: "
+            "%d steps, %d rotations\n[korali_amd apply trace] groups %llu time-units %llu steps %llu ticks %llu\n",
+            t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7]);
   }
   return check_errors(h);
 }

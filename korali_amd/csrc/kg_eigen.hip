@@ -604,84 +604,178 @@ __global__ void __launch_bounds__(64) k_chase(int N, const double *__restrict__ 
   qr_chase(N, d, sd, r, maxRot, gc, gs);
 }
 
-// rotations per LDS chunk of k_apply: what fits after the matrix, and at
-// least one whole QR step (<= N - 1 rotations)
-__host__ __device__ inline int apply_cap(int N, bool lds) {
-  const long long avail = 160LL * 1024 - (lds ? (long long)N * (N + 1) * 8 : 0) - 1024;
-  long long c = avail / 16;
-  if (c > 8192) c = 8192;
-  return (int)(c < N ? N : c);
+// Phase C application + phase D write-back (CMAES::updateEigensystem).
+// Row k of Q replays every Givens rotation in GSL's order:
+//   (Q[k][a+i], Q[k][a+i+1]) <- (qi c - qj s, qi s + qj c)
+// Rows are independent: workgroups own APPLY_ROWS rows each (their own
+// LDS copy).  Along a row the rotations are a dependency chain, but QR step
+// t+1 only needs the entries step t has finished: rotation i of step t+1
+// touches columns a'+i, a'+i+1, final in step t after its rotation
+// (a'-a)+i+1.  A team of APPLY_TEAM lanes per row therefore runs
+// APPLY_TEAM consecutive steps at once in lockstep, lane s lagging lane s-1
+// by 2 + (a_s - a_{s-1}) rotations -- for steps whose column range is
+// nested in the previous one's (a_s >= a_{s-1}, a_s + nb_s <= a_{s-1} +
+// nb_{s-1}); any other step starts a new group.  Every entry still sees the
+// same operations in the same order, so the result is GSL's bit for bit.
+constexpr int APPLY_TEAM = 16, APPLY_ROWS = 16, APPLY_TPB = APPLY_TEAM * APPLY_ROWS;
+
+// x of lane l-1 (row_shr:1 within each 16-lane DPP row = one team; the
+// team's lane 0 gets 0 and never uses it)
+__device__ inline double dpp_shr1(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), 0x111, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), 0x111, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int APPLY_HCAP = 256;  // step headers per LDS chunk
+// rotations per LDS chunk: up to 4096, what fits next to the rows (>= N - 1,
+// one whole QR step, for every N the CMA-ES path accepts)
+__host__ __device__ inline int apply_cap(int N) {
+  const long long avail = 160LL * 1024 - (long long)N * (APPLY_ROWS + 1) * 8 - 8 * APPLY_HCAP - 16 - 512;
+  const long long c = avail / 16;
+  return (int)(c > 4096 ? 4096 : c);
+}
+__host__ __device__ inline size_t apply_lds_bytes(int N) {
+  return (size_t)N * (APPLY_ROWS + 1) * sizeof(double) + 16 * (size_t)apply_cap(N) + 8 * APPLY_HCAP + 16;
 }
 
-// Phase C application + phase D write-back (CMAES::updateEigensystem).
-// Row k of Q (a thread) replays every Givens rotation in GSL's order:
-// (Q[k][a+i], Q[k][a+i+1]) = (qi c - qj s, qi s + qj c).
-template <bool kLds>
-__global__ void __launch_bounds__(1024) k_apply(int N, const double *__restrict__ gQt, double *gWork, EigRec r,
-                                                double *__restrict__ B, double *__restrict__ D, double *minEig,
-                                                double *maxEig, double *eigenFailures, unsigned int *errors) {
+__global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__restrict__ gQt, EigRec r,
+                                                     double *__restrict__ B, double *__restrict__ D, double *minEig,
+                                                     double *maxEig, double *eigenFailures, unsigned int *errors,
+                                                     unsigned long long *trace) {
+  unsigned long long ngroups = 0, nunits = 0, tstart = __builtin_amdgcn_s_memtime();
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int lda = N + 1;
-  double *M = kLds ? smem : gWork;
-  if (kLds)
-    for (int idx = tid; idx < N * lda; idx += nt) M[idx] = gQt[idx];
-  __syncthreads();
-  const int steps = r.meta[0];
+  const int tid = threadIdx.x, lda = N + 1;
+  const int S = APPLY_ROWS + 1;                  // Lq[c * S + kl] = Q[k0 + kl][c]
+  const int k0 = blockIdx.x * APPLY_ROWS;
+  const int nrows = min(APPLY_ROWS, N - k0);
+  double *Lq = smem;
+  const int cap = apply_cap(N);
+  double *csh = Lq + (size_t)N * S;              // cap (c, s) pairs
+  int *hsh = (int *)(csh + 2 * (size_t)cap);      // APPLY_HCAP (a, nb)
+  int *chunk = hsh + 2 * APPLY_HCAP;
   if (r.meta[2]) {
-    if (tid == 0) atomicOr(errors, KG_ERR_EIGEN);
+    if (tid == 0 && blockIdx.x == 0) atomicOr(errors, KG_ERR_EIGEN);
     return;
   }
-  // The rotation stream is staged through LDS in chunks of whole QR steps
-  // (cooperative loads, then broadcast reads); row k's thread replays the
-  // chunk with the rows of the current step prefetched 8 ahead (a step only
-  // reads rows it has not written yet).
-  double *csh = smem + (kLds ? (size_t)N * lda : 0);
-  const int cap = apply_cap(N, kLds);  // rotations per chunk
+  for (int idx = tid; idx < N * APPLY_ROWS; idx += APPLY_TPB) {
+    const int c = idx / APPLY_ROWS, kl = idx % APPLY_ROWS;
+    Lq[c * S + kl] = (kl < nrows) ? gQt[(size_t)c * lda + k0 + kl] : 0.0;
+  }
+  const int steps = r.meta[0];
+  const int kl = tid / APPLY_TEAM, s = tid % APPLY_TEAM;
+  const int lane = tid & 63;
   int t0 = 0, ro0 = 0;
+  __syncthreads();
   while (t0 < steps) {
-    int t1 = t0, nrot = 0;
-    while (t1 < steps && nrot + (r.hdr[2 * t1 + 1] - 1) <= cap) {
-      nrot += r.hdr[2 * t1 + 1] - 1;
-      t1++;
-    }
-    for (int idx = tid; idx < 2 * nrot; idx += nt) csh[idx] = r.cs[2 * (size_t)ro0 + idx];
+    const int hn = min(APPLY_HCAP, steps - t0);
+    for (int idx = tid; idx < 2 * hn; idx += APPLY_TPB) hsh[idx] = r.hdr[2 * (size_t)t0 + idx];
     __syncthreads();
-    for (int k = tid; k < N; k += nt) {
-      int ro = 0;
-      for (int t = t0; t < t1; t++) {
-        const int a = r.hdr[2 * t], nb = r.hdr[2 * t + 1];
-        double *col = M + (size_t)a * lda + k;  // col[i * lda] = Q[a+i][k]
-        double qi = col[0];
-        const double *cs = csh + 2 * ro;
-        int i = 0;
-        for (; i + 8 < nb; i += 8) {
-          double qj[8], c[8], sn[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            qj[u] = col[(size_t)(i + 1 + u) * lda];
-            c[u] = cs[2 * (i + u)];
-            sn[u] = cs[2 * (i + u) + 1];
-          }
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            col[(size_t)(i + u) * lda] = qi * c[u] - qj[u] * sn[u];
-            qi = qi * sn[u] + qj[u] * c[u];
-          }
+    if (tid < 64) {  // wave 0: the longest prefix of whole steps with <= cap rotations
+      int base = 0, carry = 0, t1 = hn;
+      for (; base < hn; base += 64) {
+        const int t = base + lane;
+        int v = (t < hn) ? hsh[2 * t + 1] - 1 : 0;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_up(v, off, 64);
+          if (lane >= off) v += u;
         }
-        for (; i + 1 < nb; i++) {
-          const double c = cs[2 * i], sn = cs[2 * i + 1];
-          const double qj = col[(size_t)(i + 1) * lda];
-          col[(size_t)i * lda] = qi * c - qj * sn;
-          qi = qi * sn + qj * c;
+        const unsigned long long over = __ballot(t < hn && carry + v > cap);
+        if (over) {
+          t1 = base + __builtin_ctzll(over);
+          carry += (t1 > base) ? __shfl(v, t1 - base - 1, 64) : 0;
+          break;
         }
-        col[(size_t)(nb - 1) * lda] = qi;
-        ro += nb - 1;
+        carry += __shfl(v, 63, 64);
+      }
+      if (lane == 0) {
+        chunk[0] = t1;
+        chunk[1] = carry;
       }
     }
     __syncthreads();
-    t0 = t1;
+    const int tn = chunk[0], nrot = chunk[1];
+    for (int idx = tid; idx < 2 * nrot; idx += APPLY_TPB) csh[idx] = r.cs[2 * (size_t)ro0 + idx];
+    __syncthreads();
+    double *col = Lq + kl;  // col[c * S] = Q[k0 + kl][c]
+    int t = 0, ro = 0;
+    while (t < tn) {
+      // group of up to APPLY_TEAM nested steps (uniform across the workgroup)
+      int my_a = 0, my_nb = 0, my_d = -1, my_ro = 0;
+      int pa = hsh[2 * t], pnb = hsh[2 * t + 1], pd = 0, pro = ro, T = pnb - 1, K = 1;
+      if (s == 0) {
+        my_a = pa;
+        my_nb = pnb;
+        my_d = 0;
+        my_ro = pro;
+      }
+      while (K < APPLY_TEAM && t + K < tn) {
+        const int a2 = hsh[2 * (t + K)], nb2 = hsh[2 * (t + K) + 1];
+        if (a2 < pa || a2 + nb2 > pa + pnb) break;
+        const int d2 = pd + 2 + (a2 - pa), ro2 = pro + pnb - 1;
+        if (s == K) {
+          my_a = a2;
+          my_nb = nb2;
+          my_d = d2;
+          my_ro = ro2;
+        }
+        T = max(T, d2 + nb2 - 1);
+        pa = a2;
+        pnb = nb2;
+        pd = d2;
+        pro = ro2;
+        K++;
+      }
+      // Systolic replay: lane s's qj at time tau is exactly the entry lane
+      // s-1 finalised at tau-1 ("emit": its rotation output, or its carry
+      // one unit after its last rotation), passed by a DPP row shift; lane 0
+      // reads LDS (entries final since the previous group).  Every lane
+      // also stores what it finalises, so LDS holds the group's result.
+      const double *cs = csh + 2 * my_ro;
+      const bool act = my_d >= 0 && kl < nrows;
+      const int last = act ? my_nb - 1 : 0;  // i == last: emit the carry
+      // branch-free body: every lane computes, selects keep the state, the
+      // only predicated instruction is the store (issue slots, not latency,
+      // bound this loop: one wave64 VALU op = 4 cycles)
+      auto clampi = [&](int i1) { return i1 < 0 ? 0 : (i1 > last - 1 ? (last > 0 ? last - 1 : 0) : i1); };
+      int ic = clampi(-my_d);
+      double cN = cs[2 * ic], sN = cs[2 * ic + 1], qjN = col[(size_t)(my_a + ic + 1) * S];
+      double qi = col[(size_t)my_a * S], emit = 0.0;
+      T += 1;  // the carry unit of the slowest lane
+      for (int tau = 0; tau < T; tau++) {
+        const double vin = dpp_shr1(emit);
+        const int i = tau - my_d;
+        const double c = cN, sn = sN, qjl = qjN;
+        ic = clampi(i + 1);
+        cN = cs[2 * ic];
+        sN = cs[2 * ic + 1];
+        qjN = col[(size_t)(my_a + ic + 1) * S];
+        qi = (s > 0 && i == -1) ? vin : qi;
+        const double qj = (s == 0) ? qjl : vin;
+        const double out = qi * c - qj * sn;
+        const double qn = qi * sn + qj * c;
+        const bool inrot = act && i >= 0 && i < last;
+        const bool store = act && i >= 0 && i <= last;
+        const double e = inrot ? out : qi;
+        if (store) col[(size_t)(my_a + i) * S] = e;
+        emit = store ? e : emit;
+        qi = inrot ? qn : qi;
+      }
+      T -= 1;
+      t += K;
+      ro = pro + pnb - 1;
+      ngroups++;
+      nunits += T;
+    }
+    __syncthreads();
+    t0 += tn;
     ro0 += nrot;
+  }
+  if (trace && tid == 0 && blockIdx.x == 0) {
+    trace[4] += ngroups;
+    trace[5] += nunits;
+    trace[6] += steps;
+    trace[7] += __builtin_amdgcn_s_memtime() - tstart;
   }
   // updateEigensystem: min/max eigenvalue; keep old B, D if min <= 0
   double mn = r.eval[0], mx = r.eval[0];
@@ -690,17 +784,19 @@ __global__ void __launch_bounds__(1024) k_apply(int N, const double *__restrict_
     mx = fmax(mx, r.eval[i]);
   }
   if (mn <= 0.0) {
-    if (tid == 0) *eigenFailures += 1.0;
+    if (tid == 0 && blockIdx.x == 0) *eigenFailures += 1.0;
     return;
   }
-  for (int idx = tid; idx < N * N; idx += nt) {
-    const int d = idx / N, e = idx % N;
-    B[idx] = M[(size_t)r.perm[e] * lda + d];
+  for (int idx = tid; idx < nrows * N; idx += APPLY_TPB) {
+    const int kk = idx / N, e = idx % N;
+    B[(size_t)(k0 + kk) * N + e] = Lq[(size_t)r.perm[e] * S + kk];
   }
-  for (int i = tid; i < N; i += nt) D[i] = sqrt(r.eval[i]);
-  if (tid == 0) {
-    *minEig = mn;
-    *maxEig = mx;
+  if (blockIdx.x == 0) {
+    for (int i = tid; i < N; i += APPLY_TPB) D[i] = sqrt(r.eval[i]);
+    if (tid == 0) {
+      *minEig = mn;
+      *maxEig = mx;
+    }
   }
 }
 
@@ -774,7 +870,8 @@ int EigenSolver::init(int N_, bool hostChase_) {
   const int attr = 160 * 1024;
   KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
   KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N)));
   return 0;
 }
 
@@ -843,12 +940,8 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
     KG_HIP(hipStreamWaitEvent(s, ev_chase, 0));
   }
   if (prof) prof(profCtx, "eigen_apply", 0);
-  if (lds)
-    hipLaunchKernelGGL(k_apply<true>, dim3(1), dim3(1024), matb + 16 * (size_t)apply_cap(N, true), s, N, gQt, gWork,
-                       devRec, B, D, minEig, maxEig, eigenFailures, errors);
-  else
-    hipLaunchKernelGGL(k_apply<false>, dim3(1), dim3(1024), 16 * (size_t)apply_cap(N, false), s, N, gQt, gQt, devRec,
-                       B, D, minEig, maxEig, eigenFailures, errors);
+  hipLaunchKernelGGL(k_apply, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS), dim3(APPLY_TPB), apply_lds_bytes(N), s, N, gQt,
+                     devRec, B, D, minEig, maxEig, eigenFailures, errors, trace);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_apply", 1);
   return 0;

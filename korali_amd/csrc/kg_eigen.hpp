@@ -23,6 +23,11 @@ class EigenSolver {
   int run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
           double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
   unsigned long long *trace = nullptr;  // optional device counters (k_tridiag sub-phases)
+  // QR steps / Givens rotations of the last host chase (diagnostics)
+  void last_counts(int &steps, int &rotations) const {
+    steps = (hostChase && host.meta) ? host.meta[0] : -1;
+    rotations = (hostChase && host.meta) ? host.meta[1] : -1;
+  }
   bool hostChase = true;
 
  private:
