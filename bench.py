@@ -49,6 +49,34 @@ STAGE_FLOPS = {
 }
 
 
+# kernels behind each profiled stage (names as in profiles/<round>/*_pmc_traffic.csv)
+STAGE_KERNELS = {
+    "eigen_tridiag": ["kg::k_tridiag<true>"], "eigen_unpack": ["kg::k_unpack<true>"], "eigen_apply": ["kg::k_apply"],
+    "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
+    "covariance": ["kg::k_rankmu_mfma", "kg::k_adaptC_combine"],
+    "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
+    "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", "kg::k_mean", "kg::k_paths"],
+}
+PROFILE_ROUND = "r1"
+
+
+def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
+    """HBM bytes per launch of a stage's kernels from the committed PMC passes
+    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
+    import csv
+    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, csv_name)
+    if stage not in STAGE_KERNELS or not os.path.exists(path):
+        return None, None
+    rows = {r["kernel"]: r for r in csv.DictReader(open(path))}
+    tot, raw = 0.0, 0.0
+    for k in STAGE_KERNELS[stage]:
+        if k not in rows:
+            return None, None
+        tot += (float(rows[k]["fetch_KB_x2"]) + float(rows[k]["write_KB"])) * 1024
+        raw += (float(rows[k]["fetch_KB_raw"]) + float(rows[k]["write_KB"])) * 1024
+    return tot, raw
+
+
 def _cmaes_oracle_rate(variant, seconds_budget, max_gens):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refcpu as R
@@ -174,6 +202,7 @@ def main():
     dom_ms = stages[dominant]
     flops = STAGE_FLOPS.get(dominant, 0.0)
     achieved = flops / (dom_ms * 1e-3) / 1e12
+    traffic, traffic_raw = pmc_traffic(dominant)
     F_gen = 2 * LAMBDA * N_VARS ** 2 + 2 * MU * N_VARS ** 2 + 10 * N_VARS ** 3 + 8 * LAMBDA * N_VARS
     B_gen = 8 * (2 * LAMBDA * N_VARS + MU * N_VARS + 4 * N_VARS ** 2) + 24 * LAMBDA
     t_roof = max(F_gen / (FP64_PEAK_TFLOPS * 1e12), B_gen / (HBM_PEAK_GBS * 1e9))
@@ -199,7 +228,9 @@ def main():
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
         "roofline": {"kernel": dominant, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_raw_fetch": traffic_raw,
+                     "traffic_source": f"profiles/{PROFILE_ROUND}/c2_pmc_traffic.csv" if traffic else None,
                      "algorithmic_flops_per_launch": flops, "avg_launch_ms": dom_ms},
     }
     if not args.no_cpu_baseline:
