@@ -165,7 +165,13 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation);
 int kg_tmcmc_evaluate(kg_tmcmc_t h);
 int kg_tmcmc_process(kg_tmcmc_t h, size_t generation);
 /* host-callback likelihoods (KORALI_START/WAITALL of TMCMC::runGeneration
- * :114-144): read the P x N candidates, hand back logPrior / logLikelihood */
+ * :114-144): kg_tmcmc_evaluate_prior forms the uniform log-priors on the
+ * device ("Chain Candidates LogPriors"; -inf prior -> logLikelihood -inf,
+ * bayesian.cpp.base:56-77), then the host reads the P x N candidates, runs
+ * the model where the prior is finite and hands back the log-likelihoods
+ * (set_field "Chain Candidates LogLikelihoods"), or sets both at once with
+ * kg_tmcmc_set_evaluations. */
+int kg_tmcmc_evaluate_prior(kg_tmcmc_t h);
 int kg_tmcmc_get_candidates(kg_tmcmc_t h, double *X, size_t ld);
 int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double *log_likelihood);
 int kg_tmcmc_profile(kg_tmcmc_t h, int enable);

@@ -1,10 +1,15 @@
 """Build the in-tree native libraries (no JIT cache, nothing installed).
 
-  korali_amd/libkorali_amd.so   HIP kernels + C-ABI (include/korali_amd.h),
-                                gfx950 code objects, hipcc
+  korali_amd/libkorali_amd.so      HIP kernels + C-ABI (include/korali_amd.h),
+                                   gfx950 code objects, hipcc
+  korali_amd/libkorali_engine.so   C++ korali::Engine / Experiment / Sample
+                                   (korali_amd/engine/korali.hpp) on the C-ABI
+  korali_amd/libkorali*.so         the `libkorali` Python module (pybind11)
 """
 import os
 import subprocess
+import sys
+import sysconfig
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -30,14 +35,39 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+ENGINE = os.path.join(PKG, "engine")
+ENGINE_LIB = os.path.join(PKG, "libkorali_engine.so")
+PYMOD = os.path.join(PKG, "libkorali" + sysconfig.get_config_var("EXT_SUFFIX"))
+CXX = os.environ.get("CXX", "g++")
+CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-result"]
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+
+
 def build(force=False, verbose=False):
     deps = sources() + [os.path.join(ROOT, "include", "korali_amd.h")]
     if force or _stale(LIB, deps):
-        cmd = [HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip")]
-        if verbose:
-            print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        _run([HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip")], verbose)
+    build_engine(force, verbose)
     return LIB
+
+
+def build_engine(force=False, verbose=False):
+    srcs = [os.path.join(ENGINE, f) for f in ("json.cpp", "engine.cpp")]
+    hdrs = [os.path.join(ENGINE, f) for f in ("json.hpp", "korali.hpp")] + [os.path.join(ROOT, "include", "korali_amd.h")]
+    link = ["-L" + PKG, "-lkorali_amd", "-Wl,-rpath,$ORIGIN"]
+    if force or _stale(ENGINE_LIB, srcs + hdrs + [LIB]):
+        _run([CXX] + CXXFLAGS + ["-o", ENGINE_LIB] + srcs + link, verbose)
+    pysrc = os.path.join(ENGINE, "pybind.cpp")
+    if force or _stale(PYMOD, srcs + hdrs + [pysrc, LIB]):
+        import pybind11
+        inc = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+        _run([CXX] + CXXFLAGS + ["-fvisibility=hidden"] + inc + ["-o", PYMOD, pysrc] + srcs + link, verbose)
+    return PYMOD
 
 
 if __name__ == "__main__":

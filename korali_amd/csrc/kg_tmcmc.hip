@@ -165,10 +165,10 @@ __global__ void k_tm_evaluate(int N, int P, int lik, const double *__restrict__ 
   candLP[c] = lp;
   double ll = -INFINITY;
   if (!(isinf(lp) && lp < 0)) {
+    if (lik < 0) return;  // prior only: the host evaluates the likelihood model
     double ss = 0.0;
     for (int d = 0; d < N; d++) ss += x[d] * x[d];
     ll = -0.5 * ss;
-    (void)lik;
   }
   candLL[c] = ll;
 }
@@ -1422,6 +1422,15 @@ int kg_tmcmc_evaluate(kg_tmcmc_t h) {
                      h->cand, h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP);
   KG_HIP(hipGetLastError());
   h->modelEvaluationCount += h->P;
+  return 0;
+}
+
+int kg_tmcmc_evaluate_prior(kg_tmcmc_t h) {
+  TmStage st(h, "evaluate");
+  hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, -1, h->cand,
+                     h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP);
+  KG_HIP(hipGetLastError());
+  KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
 

@@ -1,0 +1,825 @@
+// engine.cpp — korali::Engine running CMA-ES / TMCMC experiments on the
+// korali_amd C-ABI (include/korali_amd.h).
+//
+// Mirrors, for the solvers on this path, the reference's host side:
+//   Engine::run                          source/engine.cpp:69-128
+//   Experiment::initialize / run / saveState
+//                                        source/modules/experiment/experiment.cpp.base:39-153, 165-251
+//   Module::getModule (type strings)     source/modules/module.cpp:87-182
+//   Distribution seeding / Range         source/modules/distribution/distribution.cpp.base:10-62
+//   Optimization::evaluate               source/modules/problem/optimization/optimization.cpp.base:26-34
+//   Bayesian::evaluate (+ Custom)        source/modules/problem/bayesian/bayesian.cpp.base:24-84
+//   CMAES / TMCMC termination criteria   CMAES.config, optimizer.config, solver.config, TMCMC.config
+// The generation loop itself (sampling, evaluation dispatch, update) runs on
+// the device through kg_cmaes_* / kg_tmcmc_*; user functions are called
+// from this thread in sample order (Sequential conduit semantics).
+#include <algorithm>
+#include <cctype>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "../../include/korali_amd.h"
+#include "korali.hpp"
+
+namespace korali {
+
+namespace {
+
+[[noreturn]] void fail(const char *fmt, ...) {
+  char buf[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  throw KoraliError(std::string("[Korali] Error: ") + buf);
+}
+
+void check(int rc) {
+  if (rc != 0) fail("%s", kg_last_error());
+}
+
+// Module::getModule: whitespace removed, case-insensitive compare
+std::string canon(const std::string &s) {
+  std::string r;
+  for (char c : s)
+    if (!isspace((unsigned char)c)) r += (char)tolower((unsigned char)c);
+  return r;
+}
+
+double num(Json &j, const char *key, double def) {
+  if (!j.contains(key) || j[key].is_null()) j[key] = def;
+  return j[key].getDouble();
+}
+bool flag(Json &j, const char *key, bool def) {
+  if (!j.contains(key) || j[key].is_null()) j[key] = def;
+  return j[key].getBool();
+}
+std::string str(Json &j, const char *key, const std::string &def) {
+  if (!j.contains(key) || j[key].is_null()) j[key] = def;
+  return j[key].getString();
+}
+unsigned long long uint(Json &j, const char *key, unsigned long long def) {
+  if (!j.contains(key) || j[key].is_null()) j[key] = def;
+  return j[key].getUInt();
+}
+
+std::string hexState(const unsigned char *b) {
+  static const char *hx = "0123456789ABCDEF";
+  std::string s(10000, '0');
+  for (int i = 0; i < 5000; i++) {
+    s[2 * i] = hx[b[i] >> 4];
+    s[2 * i + 1] = hx[b[i] & 15];
+  }
+  return s;
+}
+bool parseHexState(const std::string &s, unsigned char *b) {
+  if (s.size() != 10000) return false;
+  auto v = [](char c) { return c >= 'a' ? c - 'a' + 10 : c >= 'A' ? c - 'A' + 10 : c - '0'; };
+  for (int i = 0; i < 5000; i++) b[i] = (unsigned char)(v(s[2 * i]) * 16 + v(s[2 * i + 1]));
+  return true;
+}
+
+// ------------------------------------------------------------- logging
+struct Logger {
+  int level = 2;  // Silent 0, Minimal 1, Normal 2, Detailed 3
+  void set(const std::string &v) {
+    const std::string c = canon(v);
+    level = c == "silent" ? 0 : c == "minimal" ? 1 : c == "normal" ? 2 : c == "detailed" ? 3 : -1;
+    if (level < 0) fail("Unrecognized verbosity level '%s'.", v.c_str());
+  }
+  void log(int l, const char *fmt, ...) const {
+    if (level < l) return;
+    va_list ap;
+    va_start(ap, fmt);
+    printf("[Korali] ");
+    vprintf(fmt, ap);
+    va_end(ap);
+    fflush(stdout);
+  }
+};
+
+// seed assignment in configuration order (distribution.cpp.base:32-43):
+// a generator keeps its seed only when states are preserved
+struct Seeder {
+  unsigned long long counter;
+  bool preserve;
+  unsigned long long assign(Json &gen) {
+    unsigned long long s = gen.contains("Random Seed") ? gen["Random Seed"].getUInt() : 0;
+    if (s == 0 || !preserve) s = counter++;
+    gen["Random Seed"] = s;
+    return s;
+  }
+  // saved GSL state to restore (Preserve Random Number Generator States)
+  bool range(Json &gen, unsigned char *state) {
+    return preserve && gen.contains("Range") && gen["Range"].is_string() && parseHexState(gen["Range"].getString(), state);
+  }
+};
+
+struct VariableSpec {
+  std::string name;
+  double lb, ub, iv, istd, minstd;
+  int dist = -1;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------ modules
+struct SolverModule {
+  virtual ~SolverModule() = default;
+  virtual void runGeneration(size_t gen) = 0;
+  // criteria evaluated before generation `gen` (experiment.cpp.base:56)
+  virtual void checkTermination(size_t gen, std::vector<std::string> &met) = 0;
+  virtual void getConfiguration(Json &solver) = 0;
+  virtual void finalize(Json &js) = 0;
+  virtual void printAfter(const Logger &log) = 0;
+  virtual std::string type() const = 0;
+};
+
+namespace {
+
+std::vector<VariableSpec> readVariables(Json &js) {
+  std::vector<VariableSpec> vs;
+  if (!js.contains("Variables") || js["Variables"].size() == 0) fail("No variables have been defined.");
+  for (size_t i = 0; i < js["Variables"].size(); i++) {
+    Json &v = js["Variables"][i];
+    VariableSpec s;
+    s.name = str(v, "Name", "X" + std::to_string(i));
+    s.lb = num(v, "Lower Bound", -INFINITY);
+    s.ub = num(v, "Upper Bound", INFINITY);
+    s.iv = num(v, "Initial Value", NAN);
+    s.istd = num(v, "Initial Standard Deviation", NAN);
+    s.minstd = num(v, "Minimum Standard Deviation Update", 0.0);
+    if (num(v, "Granularity", 0.0) != 0.0)
+      fail("Variable '%s': discrete variables (Granularity) are not supported by the device path.", s.name.c_str());
+    vs.push_back(s);
+  }
+  return vs;
+}
+
+Json matrixJson(const std::vector<double> &a, size_t rows, size_t cols) {
+  Json m = Json::array();
+  for (size_t r = 0; r < rows; r++) m.push_back(std::vector<double>(a.begin() + r * cols, a.begin() + (r + 1) * cols));
+  return m;
+}
+
+std::vector<double> flatten(Json &j) {
+  std::vector<double> v;
+  for (const auto &x : j.elements()) {
+    if (x.is_array())
+      for (const auto &y : x.elements()) v.push_back(y.getDouble());
+    else
+      v.push_back(x.getDouble());
+  }
+  return v;
+}
+
+// ------------------------------------------------------------- CMA-ES
+// CMAES.cpp.base on the device (kg_cmaes_*); state names as in CMAES.config
+const char *CMAES_VECTORS[] = {"Current Mean", "Previous Mean", "Covariance Matrix", "Covariance Eigenvector Matrix",
+                               "Axis Lengths", "Evolution Path", "Conjugate Evolution Path", "Mu Weights",
+                               "Value Vector", "Best Ever Variables", "Current Best Variables"};
+const char *CMAES_SCALARS[] = {"Sigma", "Trace", "Effective Mu", "Cumulative Covariance", "Sigma Cumulation Factor",
+                               "Damp Factor", "Chi Square Number", "Conjugate Evolution Path L2 Norm",
+                               "Best Ever Value", "Previous Best Ever Value", "Previous Best Value",
+                               "Current Best Value", "Current Min Standard Deviation",
+                               "Current Max Standard Deviation", "Maximum Diagonal Covariance Matrix Element",
+                               "Minimum Diagonal Covariance Matrix Element", "Minimum Covariance Eigenvalue",
+                               "Maximum Covariance Eigenvalue", "Infeasible Sample Count", "Model Evaluation Count"};
+
+struct CmaesModule : SolverModule {
+  kg_cmaes_t h = nullptr;
+  size_t N = 0, lam = 0, mu = 0;
+  int objective = -1;  // builtin kernel, or -1: host function
+  size_t fn = 0;
+  std::vector<VariableSpec> vars;
+  double maxGenerations, maxModelEvaluations, maxInfeasible, maxCondition, minStd, maxStd, maxValue, minValueDiff;
+  Json *solverJs = nullptr;
+
+  ~CmaesModule() override {
+    if (h) kg_cmaes_destroy(h);
+  }
+
+  CmaesModule(Json &js, Seeder &seeds, bool resume) {
+    Json &sv = js["Solver"];
+    Json &pb = js["Problem"];
+    solverJs = &sv;
+    if (canon(str(pb, "Type", "")) != "optimization")
+      fail("Solver CMAES requires a problem of type 'Optimization' (is '%s').", pb["Type"].getString().c_str());
+    vars = readVariables(js);
+    N = vars.size();
+    lam = uint(sv, "Population Size", 0);
+    if (lam <= 1) fail("'Population Size' must be larger 1.");
+    mu = uint(sv, "Mu Value", 0);
+    const std::string muType = str(sv, "Mu Type", "Logarithmic");
+    const std::string mt = canon(muType);
+    const int muTypeId = mt == "logarithmic" ? KG_MU_LOGARITHMIC
+                         : mt == "linear"    ? KG_MU_LINEAR
+                         : mt == "equal"     ? KG_MU_EQUAL
+                         : mt == "proportional" ? KG_MU_PROPORTIONAL
+                                                : -1;
+    if (muTypeId < 0)
+      fail("Invalid setting of Mu Type (%s) (Linear, Equal, Logarithmic, or Proportional accepted).", muType.c_str());
+    if (flag(sv, "Mirrored Sampling", false)) fail("'Mirrored Sampling' is not supported by the device path yet.");
+    if (flag(sv, "Use Gradient Information", false))
+      fail("'Use Gradient Information' is not supported by the device path.");
+    if (pb.contains("Constraints") && pb["Constraints"].size() > 0)
+      fail("Constrained CMA-ES ('Constraints') is not supported by the device path.");
+    Json &tc = sv["Termination Criteria"];
+    maxGenerations = num(tc, "Max Generations", 1e10);
+    maxModelEvaluations = num(tc, "Max Model Evaluations", 1e9);
+    maxInfeasible = num(tc, "Max Infeasible Resamplings", INFINITY);
+    maxCondition = num(tc, "Max Condition Covariance Matrix", INFINITY);
+    minStd = num(tc, "Min Standard Deviation", -INFINITY);
+    maxStd = num(tc, "Max Standard Deviation", INFINITY);
+    maxValue = num(tc, "Max Value", INFINITY);
+    minValueDiff = num(tc, "Min Value Difference Threshold", -INFINITY);
+
+    if (pb.contains("Objective Kernel")) {
+      const std::string k = canon(pb["Objective Kernel"].getString());
+      objective = (k == "negativerosenbrock" || k == "rosenbrock")   ? KG_OBJ_NEGATIVE_ROSENBROCK
+                  : (k == "negativeackley" || k == "ackley")         ? KG_OBJ_NEGATIVE_ACKLEY
+                  : (k == "negativesphere" || k == "sphere")         ? KG_OBJ_NEGATIVE_SPHERE
+                                                                     : -2;
+      if (objective == -2) fail("Unknown 'Objective Kernel' '%s'.", pb["Objective Kernel"].getString().c_str());
+    } else {
+      if (!pb.contains("Objective Function")) fail("Problem 'Optimization' requires an 'Objective Function'.");
+      fn = pb["Objective Function"].getUInt();
+    }
+
+    std::vector<double> lb(N), ub(N), iv(N), istd(N), minstd(N);
+    for (size_t i = 0; i < N; i++) {
+      lb[i] = vars[i].lb;
+      ub[i] = vars[i].ub;
+      iv[i] = vars[i].iv;
+      istd[i] = vars[i].istd;
+      minstd[i] = vars[i].minstd;
+    }
+    // generators in CMAES.config Internal Settings order: Normal, Uniform
+    Json &gn = sv["Normal Generator"], &gu = sv["Uniform Generator"];
+    gn["Type"] = "Univariate/Normal";
+    gn["Mean"] = 0.0;
+    gn["Standard Deviation"] = 1.0;
+    gu["Type"] = "Univariate/Uniform";
+    gu["Minimum"] = 0.0;
+    gu["Maximum"] = 1.0;
+    kg_cmaes_cfg c{};
+    c.variable_count = N;
+    c.population_size = lam;
+    c.mu_value = mu;
+    c.mu_type = muTypeId;
+    c.initial_sigma_cumulation_factor = num(sv, "Initial Sigma Cumulation Factor", -1.0);
+    c.initial_damp_factor = num(sv, "Initial Damp Factor", -1.0);
+    c.initial_cumulative_covariance = num(sv, "Initial Cumulative Covariance", -1.0);
+    c.is_sigma_bounded = flag(sv, "Is Sigma Bounded", false);
+    c.diagonal_covariance = flag(sv, "Diagonal Covariance", false);
+    c.mirrored_sampling = 0;
+    c.max_infeasible_resamplings = maxInfeasible;
+    c.lower_bound = lb.data();
+    c.upper_bound = ub.data();
+    c.initial_value = iv.data();
+    c.initial_std = istd.data();
+    c.min_std_update = minstd.data();
+    c.normal_seed = seeds.assign(gn);
+    c.uniform_seed = seeds.assign(gu);
+    const std::string cu = canon(str(sv, "Covariance Update", "Exact"));
+    if (cu != "exact" && cu != "mfma") fail("'Covariance Update' must be 'Exact' or 'MFMA'.");
+    c.cov_mode = cu == "mfma" ? KG_COV_MFMA : KG_COV_EXACT;
+    c.device = js.contains("Device") ? (int)js["Device"].getInt() : 0;
+    c.store_bdz = 0;
+    c.eigen_device_chase = 0;
+    check(kg_cmaes_create(&c, &h));
+    if (mu == 0) mu = lam / 2;
+    unsigned char st[5000];
+    if (seeds.range(gn, st)) check(kg_cmaes_set_rng(h, 0, st));
+    if (seeds.range(gu, st)) check(kg_cmaes_set_rng(h, 1, st));
+    if (resume) restore(sv);
+  }
+
+  // CMAES::setConfiguration of a saved state (loadState + resume)
+  void restore(Json &sv) {
+    check(kg_cmaes_initialize(h));  // derived constants; saved state overrides
+    for (const char *k : CMAES_VECTORS)
+      if (sv.contains(k) && sv[k].is_array() && sv[k].size()) {
+        std::vector<double> v = flatten(sv[k]);
+        size_t n = 0;
+        check(kg_cmaes_field_size(h, k, &n));
+        if (v.size() == n) check(kg_cmaes_set_field(h, k, v.data(), n));
+      }
+    for (const char *k : CMAES_SCALARS)
+      if (sv.contains(k) && sv[k].is_number()) {
+        const double v = sv[k].getDouble();
+        check(kg_cmaes_set_field(h, k, &v, 1));
+      }
+  }
+
+  void runGeneration(size_t gen) override {
+    if (gen == 1) check(kg_cmaes_initialize(h));
+    check(kg_cmaes_sample(h));
+    if (objective >= 0) {
+      check(kg_cmaes_eval_builtin(h, objective));
+    } else {
+      // KORALI_START every sample, KORALI_WAITALL (CMAES.cpp.base:204-224)
+      std::vector<double> X(lam * N), F(lam);
+      check(kg_cmaes_get_candidates(h, X.data(), N));
+      Function &f = getFunction(fn);
+      for (size_t i = 0; i < lam; i++) {
+        Sample s;
+        s["Module"] = "Problem";
+        s["Operation"] = "Evaluate";
+        s["Sample Id"] = (unsigned long long)i;
+        s["Current Generation"] = (unsigned long long)gen;
+        s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
+        f(s);
+        if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
+        F[i] = s["F(x)"].getDouble();
+        if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
+      }
+      check(kg_cmaes_set_fitness(h, F.data()));
+    }
+    check(kg_cmaes_update(h, gen));
+    check(kg_cmaes_synchronize(h));
+  }
+
+  double field(const char *k) {
+    double v;
+    check(kg_cmaes_get_field(h, k, &v, 1));
+    return v;
+  }
+
+  void checkTermination(size_t gen, std::vector<std::string> &met) override {
+    const double evals = field("Model Evaluation Count");
+    if (gen > maxGenerations) met.push_back("Max Generations");
+    if (maxModelEvaluations <= evals) met.push_back("Max Model Evaluations");
+    if (gen <= 1) return;
+    if (maxInfeasible > 0 && field("Infeasible Sample Count") >= maxInfeasible)
+      met.push_back("Max Infeasible Resamplings");
+    if (field("Maximum Covariance Eigenvalue") >= maxCondition * field("Minimum Covariance Eigenvalue"))
+      met.push_back("Max Condition Covariance Matrix");
+    if (field("Current Min Standard Deviation") <= minStd) met.push_back("Min Standard Deviation");
+    if (field("Current Max Standard Deviation") >= maxStd) met.push_back("Max Standard Deviation");
+    if (field("Best Ever Value") > maxValue) met.push_back("Max Value");
+    if (std::fabs(field("Current Best Value") - field("Previous Best Value")) < minValueDiff)
+      met.push_back("Min Value Difference Threshold");
+  }
+
+  void getConfiguration(Json &sv) override {
+    for (const char *k : CMAES_VECTORS) {
+      size_t n = 0;
+      check(kg_cmaes_field_size(h, k, &n));
+      std::vector<double> v(n);
+      check(kg_cmaes_get_field(h, k, v.data(), n));
+      sv[k] = v;
+    }
+    for (const char *k : CMAES_SCALARS) sv[k] = field(k);
+    {
+      std::vector<double> X(lam * N);
+      check(kg_cmaes_get_field(h, "Sample Population", X.data(), X.size()));
+      sv["Sample Population"] = matrixJson(X, lam, N);
+      std::vector<uint64_t> idx(lam);
+      check(kg_cmaes_get_sorting_index(h, idx.data()));
+      Json si = Json::array();
+      for (auto i : idx) si.push_back((unsigned long long)i);
+      sv["Sorting Index"] = si;
+    }
+    sv["Variable Count"] = (unsigned long long)N;
+    sv["Mu Value"] = (unsigned long long)mu;
+    unsigned char st[5000];
+    check(kg_cmaes_get_rng(h, 0, st));
+    sv["Normal Generator"]["Range"] = hexState(st);
+    check(kg_cmaes_get_rng(h, 1, st));
+    sv["Uniform Generator"]["Range"] = hexState(st);
+  }
+
+  void finalize(Json &js) override {
+    // CMAES::finalize (CMAES.cpp.base:994-999)
+    js["Results"]["Best Sample"]["F(x)"] = field("Best Ever Value");
+    std::vector<double> b(N);
+    check(kg_cmaes_get_field(h, "Best Ever Variables", b.data(), N));
+    js["Results"]["Best Sample"]["Parameters"] = b;
+  }
+
+  void printAfter(const Logger &log) override {
+    log.log(2, "Sigma:                        %+6.3e\n", field("Sigma"));
+    log.log(2, "Current Function Value: Max = %+6.3e - Best = %+6.3e\n", field("Current Best Value"),
+            field("Best Ever Value"));
+    log.log(2, "Diagonal Covariance:    Min = %+6.3e -  Max = %+6.3e\n",
+            field("Minimum Diagonal Covariance Matrix Element"), field("Maximum Diagonal Covariance Matrix Element"));
+    log.log(2, "Covariance Eigenvalues: Min = %+6.3e -  Max = %+6.3e\n", field("Minimum Covariance Eigenvalue"),
+            field("Maximum Covariance Eigenvalue"));
+  }
+
+  std::string type() const override { return "Optimizer/CMAES"; }
+};
+
+// --------------------------------------------------------------- TMCMC
+const char *TMCMC_VECTORS[] = {"Chain Leaders LogLikelihoods", "Chain Leaders LogPriors", "Chain Lengths",
+                               "Mean Theta", "Covariance Matrix", "Chain Candidates LogLikelihoods",
+                               "Chain Candidates LogPriors", "Sample LogLikelihood Database",
+                               "Sample LogPrior Database", "Num Selections"};
+const char *TMCMC_MATRICES[] = {"Chain Leaders", "Chain Candidates", "Sample Database"};
+const char *TMCMC_SCALARS[] = {"Annealing Exponent", "Previous Annealing Exponent", "LogEvidence",
+                               "Coefficient Of Variation", "Max Loglikelihood", "Chain Count",
+                               "Accepted Samples Count", "Proposals Acceptance Rate", "Selection Acceptance Rate",
+                               "Database Entries", "Model Evaluation Count"};
+
+struct TmcmcModule : SolverModule {
+  kg_tmcmc_t h = nullptr;
+  size_t N = 0, P = 0, ndist = 0;
+  bool builtin = false;
+  size_t fn = 0;
+  double maxGenerations, maxModelEvaluations, targetExponent;
+
+  ~TmcmcModule() override {
+    if (h) kg_tmcmc_destroy(h);
+  }
+
+  TmcmcModule(Json &js, Seeder &seeds, std::vector<uint64_t> &distSeeds,
+              std::vector<std::vector<unsigned char>> &distStates, bool resume) {
+    Json &sv = js["Solver"];
+    Json &pb = js["Problem"];
+    const std::string pt = canon(str(pb, "Type", ""));
+    if (pt != "bayesian/custom")
+      fail("The device TMCMC path supports problems of type 'Bayesian/Custom' (is '%s').", pb["Type"].getString().c_str());
+    if (canon(str(sv, "Version", "TMCMC")) != "tmcmc") fail("Only Version 'TMCMC' is supported by the device path.");
+    std::vector<VariableSpec> vars = readVariables(js);
+    N = vars.size();
+    P = uint(sv, "Population Size", 0);
+    if (P < 2) fail("TMCMC 'Population Size' must be at least 2.");
+    const double mcl = num(sv, "Max Chain Length", 1);
+    if (mcl == 0) fail("Max Chain Length must be greater 0.");
+    if (mcl != 1) fail("The device TMCMC path supports 'Max Chain Length' 1 only.");
+    if (num(sv, "Burn In", 0) != 0) fail("The device TMCMC path supports 'Burn In' 0 only.");
+    if (sv.contains("Per Generation Burn In") && sv["Per Generation Burn In"].size() > 0)
+      fail("'Per Generation Burn In' is not supported by the device path.");
+    const double covScaling = num(sv, "Covariance Scaling", 0.04);
+    if (covScaling <= 0.0) fail("Covariance Scaling must be larger 0.0 (is %lf).\n", covScaling);
+    Json &tc = sv["Termination Criteria"];
+    maxGenerations = num(tc, "Max Generations", 1e10);
+    maxModelEvaluations = num(tc, "Max Model Evaluations", 1e9);
+    targetExponent = num(tc, "Target Annealing Exponent", 1.0);
+
+    // priors: each variable's Univariate/Uniform distribution
+    Json &ds = js["Distributions"];
+    ndist = ds.size();
+    std::vector<double> pmin(N), pmax(N);
+    std::vector<int> pdist(N);
+    for (size_t i = 0; i < N; i++) {
+      Json &v = js["Variables"][i];
+      if (!v.contains("Prior Distribution")) fail("Variable '%s' has no 'Prior Distribution'.", vars[i].name.c_str());
+      const std::string pn = v["Prior Distribution"].getString();
+      int k = -1;
+      for (size_t d = 0; d < ndist; d++)
+        if (ds[d].contains("Name") && ds[d]["Name"].getString() == pn) k = (int)d;
+      if (k < 0) fail("Did not find a distribution named '%s'.", pn.c_str());
+      if (canon(ds[k]["Type"].getString()) != "univariate/uniform")
+        fail("The device TMCMC path supports 'Univariate/Uniform' priors (distribution '%s').", pn.c_str());
+      pmin[i] = ds[k]["Minimum"].getDouble();
+      pmax[i] = ds[k]["Maximum"].getDouble();
+      pdist[i] = k;
+    }
+    if (pb.contains("Likelihood Kernel")) {
+      if (canon(pb["Likelihood Kernel"].getString()) != "gaussian")
+        fail("Unknown 'Likelihood Kernel' '%s'.", pb["Likelihood Kernel"].getString().c_str());
+      builtin = true;
+    } else {
+      if (!pb.contains("Likelihood Model")) fail("Problem 'Bayesian/Custom' requires a 'Likelihood Model'.");
+      fn = pb["Likelihood Model"].getUInt();
+    }
+    // generators in TMCMC.config order: Multinomial, Multivariate, Uniform
+    Json &gm = sv["Multinomial Generator"], &gv = sv["Multivariate Generator"], &gu = sv["Uniform Generator"];
+    gm["Type"] = "Specific/Multinomial";
+    gv["Type"] = "Multivariate/Normal";
+    gu["Type"] = "Univariate/Uniform";
+    gu["Minimum"] = 0.0;
+    gu["Maximum"] = 1.0;
+    kg_tmcmc_cfg c{};
+    c.variable_count = N;
+    c.population_size = P;
+    c.max_chain_length = 1;
+    c.default_burn_in = 0;
+    c.target_cov = num(sv, "Target Coefficient Of Variation", 1.0);
+    c.covariance_scaling = covScaling;
+    c.min_annealing_exponent_update = num(sv, "Min Annealing Exponent Update", 1e-5);
+    c.max_annealing_exponent_update = num(sv, "Max Annealing Exponent Update", 1.0);
+    c.prior_min = pmin.data();
+    c.prior_max = pmax.data();
+    c.prior_distribution = pdist.data();
+    c.distribution_count = ndist;
+    c.prior_seeds = distSeeds.data();
+    c.multinomial_seed = seeds.assign(gm);
+    c.multivariate_seed = seeds.assign(gv);
+    c.uniform_seed = seeds.assign(gu);
+    c.likelihood = KG_LIK_GAUSSIAN;
+    c.device = js.contains("Device") ? (int)js["Device"].getInt() : 0;
+    check(kg_tmcmc_create(&c, &h));
+    unsigned char st[5000];
+    if (seeds.range(gm, st)) check(kg_tmcmc_set_rng(h, 0, st));
+    if (seeds.range(gv, st)) check(kg_tmcmc_set_rng(h, 1, st));
+    if (seeds.range(gu, st)) check(kg_tmcmc_set_rng(h, 2, st));
+    for (size_t d = 0; d < ndist; d++)
+      if (!distStates[d].empty()) check(kg_tmcmc_set_rng(h, 3 + (int)d, distStates[d].data()));
+    if (resume) restore(sv);
+  }
+
+  void restore(Json &sv) {
+    for (const char *k : TMCMC_VECTORS)
+      if (sv.contains(k) && sv[k].is_array() && sv[k].size()) {
+        std::vector<double> v = flatten(sv[k]);
+        size_t n = 0;
+        check(kg_tmcmc_field_size(h, k, &n));
+        if (v.size() == n) check(kg_tmcmc_set_field(h, k, v.data(), n));
+      }
+    for (const char *k : TMCMC_MATRICES)
+      if (sv.contains(k) && sv[k].is_array() && sv[k].size()) {
+        std::vector<double> v = flatten(sv[k]);
+        size_t n = 0;
+        check(kg_tmcmc_field_size(h, k, &n));
+        if (v.size() == n) check(kg_tmcmc_set_field(h, k, v.data(), n));
+      }
+    for (const char *k : TMCMC_SCALARS)
+      if (sv.contains(k) && sv[k].is_number()) {
+        const double v = sv[k].getDouble();
+        check(kg_tmcmc_set_field(h, k, &v, 1));
+      }
+  }
+
+  double field(const char *k) {
+    double v;
+    check(kg_tmcmc_get_field(h, k, &v, 1));
+    return v;
+  }
+
+  void runGeneration(size_t gen) override {
+    check(kg_tmcmc_prepare(h, gen));
+    if (builtin) {
+      check(kg_tmcmc_evaluate(h));
+    } else {
+      // Bayesian::evaluate per chain: prior on the device, the likelihood
+      // model only where the prior is finite (bayesian.cpp.base:56-77)
+      check(kg_tmcmc_evaluate_prior(h));
+      std::vector<double> X(P * N), LP(P), LL(P);
+      check(kg_tmcmc_get_candidates(h, X.data(), N));
+      check(kg_tmcmc_get_field(h, "Chain Candidates LogPriors", LP.data(), P));
+      Function &f = getFunction(fn);
+      for (size_t i = 0; i < P; i++) {
+        if (std::isinf(LP[i]) && LP[i] < 0) {
+          LL[i] = -INFINITY;
+          continue;
+        }
+        Sample s;
+        s["Module"] = "Problem";
+        s["Operation"] = "Evaluate";
+        s["Sample Id"] = (unsigned long long)i;
+        s["Current Generation"] = (unsigned long long)gen;
+        s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
+        f(s);
+        if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
+        LL[i] = s["logLikelihood"].getDouble();
+        if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);
+      }
+      check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
+    }
+    check(kg_tmcmc_process(h, gen));
+    check(kg_tmcmc_synchronize(h));
+  }
+
+  void checkTermination(size_t gen, std::vector<std::string> &met) override {
+    if (gen > maxGenerations) met.push_back("Max Generations");
+    if (maxModelEvaluations <= field("Model Evaluation Count")) met.push_back("Max Model Evaluations");
+    if (field("Previous Annealing Exponent") >= targetExponent) met.push_back("Target Annealing Exponent");
+  }
+
+  void getConfiguration(Json &sv) override {
+    for (const char *k : TMCMC_VECTORS) {
+      size_t n = 0;
+      check(kg_tmcmc_field_size(h, k, &n));
+      std::vector<double> v(n);
+      check(kg_tmcmc_get_field(h, k, v.data(), n));
+      sv[k] = v;
+    }
+    for (const char *k : TMCMC_MATRICES) {
+      size_t n = 0;
+      check(kg_tmcmc_field_size(h, k, &n));
+      std::vector<double> v(n);
+      check(kg_tmcmc_get_field(h, k, v.data(), n));
+      sv[k] = matrixJson(v, n / N, N);
+    }
+    for (const char *k : TMCMC_SCALARS) sv[k] = field(k);
+    unsigned char st[5000];
+    check(kg_tmcmc_get_rng(h, 0, st));
+    sv["Multinomial Generator"]["Range"] = hexState(st);
+    check(kg_tmcmc_get_rng(h, 1, st));
+    sv["Multivariate Generator"]["Range"] = hexState(st);
+    check(kg_tmcmc_get_rng(h, 2, st));
+    sv["Uniform Generator"]["Range"] = hexState(st);
+  }
+
+  void saveDistributions(Json &js) {
+    unsigned char st[5000];
+    for (size_t d = 0; d < ndist; d++) {
+      check(kg_tmcmc_get_rng(h, 3 + (int)d, st));
+      js["Distributions"][d]["Range"] = hexState(st);
+    }
+  }
+
+  void finalize(Json &js) override {
+    // TMCMC::finalize: the last generation's sample database is the posterior
+    size_t n = 0;
+    check(kg_tmcmc_field_size(h, "Sample Database", &n));
+    std::vector<double> v(n);
+    check(kg_tmcmc_get_field(h, "Sample Database", v.data(), n));
+    js["Results"]["Posterior Sample Database"] = matrixJson(v, n / N, N);
+    js["Results"]["Log Evidence"] = field("LogEvidence");
+  }
+
+  void printAfter(const Logger &log) override {
+    log.log(2, "Acceptance Rate (proposals / selections): (%.2f%% / %.2f%%)\n",
+            100 * field("Proposals Acceptance Rate"), 100 * field("Selection Acceptance Rate"));
+    log.log(2, "Coefficient of Variation: %.2f%%\n", 100.0 * field("Coefficient Of Variation"));
+    log.log(2, "Annealing Exponent:       %.3e\n", field("Annealing Exponent"));
+  }
+
+  std::string type() const override { return "Sampler/TMCMC"; }
+};
+
+bool dirExists(const std::string &p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+}  // namespace
+
+struct ExperimentState {
+  std::unique_ptr<SolverModule> solver;
+  Logger log;
+};
+
+Experiment::Experiment() : _state(new ExperimentState()) {}
+Experiment::~Experiment() = default;
+Experiment::Experiment(Experiment &&) noexcept = default;
+Experiment &Experiment::operator=(Experiment &&) noexcept = default;
+
+bool Experiment::loadState(const std::string &path) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  _js = Json::parse(ss.str());
+  return true;
+}
+
+namespace {
+
+void makeDirs(const std::string &path) {
+  for (size_t p = 1; p <= path.size(); p++)
+    if (p == path.size() || path[p] == '/') {
+      const std::string d = path.substr(0, p);
+      if (!dirExists(d)) mkdir(d.c_str(), 0775);
+    }
+}
+
+void saveState(Json &js, size_t gen) {
+  Json &fo = js["File Output"];
+  std::string path = fo["Path"].getString();
+  if (path.empty()) path = ".";
+  if (path[0] != '/') path = "./" + path;  // experiment.cpp.base:136
+  makeDirs(path);
+  char name[64];
+  if (fo["Use Multiple Files"].getBool())
+    snprintf(name, sizeof(name), "gen%08zu.json", gen);
+  else
+    snprintf(name, sizeof(name), "genLatest.json");
+  const std::string file = path + "/" + name;
+  {
+    std::ofstream out(file);
+    if (!out) fail("Error trying to save result file: %s.\n", file.c_str());
+    out << js.dump(2);
+  }
+  const std::string link_ = path + "/latest";
+  remove(link_.c_str());
+  if (link(file.c_str(), link_.c_str()) != 0) {
+    // hard links unsupported: fall back to a copy
+    std::ifstream src(file);
+    std::ofstream dst(link_);
+    dst << src.rdbuf();
+  }
+}
+
+void runExperiment(Experiment &e) {
+  Json &js = e._js;
+  ExperimentState &st = *e._state;
+  // experiment.config Module Defaults
+  num(js, "Random Seed", 0);
+  flag(js, "Preserve Random Number Generator States", false);
+  Json &fo = js["File Output"];
+  flag(fo, "Enabled", true);
+  str(fo, "Path", "_korali_result");
+  uint(fo, "Frequency", 1);
+  flag(fo, "Use Multiple Files", true);
+  Json &co = js["Console Output"];
+  st.log.set(str(co, "Verbosity", "Normal"));
+  const unsigned long long consoleFreq = uint(co, "Frequency", 1);
+  flag(js, "Store Sample Information", false);
+  if (!js.contains("Current Generation")) js["Current Generation"] = 0ULL;
+  if (!js.contains("Distributions")) js["Distributions"] = Json::array();
+  size_t gen = (size_t)js["Current Generation"].getUInt();
+  const bool resume = gen > 0;
+  if (resume && js.contains("Is Finished") && js["Is Finished"].getBool()) {
+    // a finished experiment continues only if a termination limit was raised
+  }
+  js["Is Finished"] = false;
+  // Experiment::setSeed: 0 -> time
+  if (!resume && js["Random Seed"].getUInt() == 0)
+    js["Random Seed"] = (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::high_resolution_clock::now().time_since_epoch())
+                            .count();
+  Seeder seeds{js["Random Seed"].getUInt(), js["Preserve Random Number Generator States"].getBool()};
+  // distributions first (experiment.cpp:255-340), in order
+  std::vector<uint64_t> distSeeds;
+  std::vector<std::vector<unsigned char>> distStates;
+  for (size_t d = 0; d < js["Distributions"].size(); d++) {
+    Json &dj = js["Distributions"][d];
+    distSeeds.push_back(seeds.assign(dj));
+    std::vector<unsigned char> stt(5000);
+    if (seeds.range(dj, stt.data()))
+      distStates.push_back(stt);
+    else
+      distStates.emplace_back();
+  }
+  Json &sv = js["Solver"];
+  if (!sv.contains("Type")) fail("No solver type specified ('Solver' / 'Type').");
+  const std::string stype = canon(sv["Type"].getString());
+  TmcmcModule *tm = nullptr;
+  if (stype == "optimizer/cmaes" || stype == "cmaes") {
+    st.solver.reset(new CmaesModule(js, seeds, resume));
+  } else if (stype == "sampler/tmcmc" || stype == "tmcmc") {
+    tm = new TmcmcModule(js, seeds, distSeeds, distStates, resume);
+    st.solver.reset(tm);
+  } else {
+    fail("Unrecognized solver type '%s' (the device path provides Optimizer/CMAES and Sampler/TMCMC).",
+         sv["Type"].getString().c_str());
+  }
+  js["Random Seed"] = seeds.counter;
+  SolverModule &solver = *st.solver;
+  const bool fileOut = fo["Enabled"].getBool();
+  const size_t fileFreq = (size_t)fo["Frequency"].getUInt();
+  auto save = [&]() {
+    js["Current Generation"] = (unsigned long long)gen;
+    solver.getConfiguration(sv);
+    if (tm) tm->saveDistributions(js);
+    saveState(js, gen);
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  if (gen == 0 && fileOut) save();
+  gen++;
+  std::vector<std::string> met;
+  for (;;) {
+    met.clear();
+    solver.checkTermination(gen, met);
+    if (!met.empty()) break;
+    if (consoleFreq > 0 && gen % consoleFreq == 0) {
+      st.log.log(1, "--------------------------------------------------------------------\n");
+      st.log.log(1, "Current Generation: #%zu\n", gen);
+    }
+    const auto g0 = std::chrono::steady_clock::now();
+    solver.runGeneration(gen);
+    const auto g1 = std::chrono::steady_clock::now();
+    if (consoleFreq > 0 && gen % consoleFreq == 0) {
+      solver.printAfter(st.log);
+      st.log.log(3, "Experiment: 0 - Generation Time: %.3fs\n", std::chrono::duration<double>(g1 - g0).count());
+    }
+    if (fileOut && fileFreq > 0 && gen % fileFreq == 0) save();
+    gen++;
+  }
+  const auto t1 = std::chrono::steady_clock::now();
+  gen--;
+  js["Is Finished"] = true;
+  solver.finalize(js);
+  js["Current Generation"] = (unsigned long long)gen;
+  solver.getConfiguration(sv);
+  if (tm) tm->saveDistributions(js);
+  if (fileOut) saveState(js, gen);
+  st.log.log(1, "--------------------------------------------------------------------\n");
+  st.log.log(1, "%s finished correctly.\n", solver.type().c_str());
+  for (const auto &m : met) st.log.log(2, "Termination Criterion Met: %s\n", m.c_str());
+  st.log.log(2, "Final Generation: %zu\n", gen);
+  st.log.log(2, "Elapsed Time: %.3fs\n", std::chrono::duration<double>(t1 - t0).count());
+  st.solver.reset();  // release the device handle
+}
+
+}  // namespace
+
+void Engine::run(Experiment &e) { runExperiment(e); }
+
+void Engine::run(std::vector<Experiment> &es) {
+  for (auto &e : es) runExperiment(e);
+}
+
+}  // namespace korali

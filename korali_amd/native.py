@@ -60,7 +60,7 @@ EXPORTED = [
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
-    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
+    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read",
 ]
 
@@ -95,7 +95,7 @@ def lib():
         L.kg_cmaes_profile.argtypes = [vp, ip]
         L.kg_cmaes_profile_read.argtypes = [vp, cp, dp, C.POINTER(sz)]
         L.kg_tmcmc_create.argtypes = [C.POINTER(_TmcmcCfg), C.POINTER(vp)]
-        for f in ("kg_tmcmc_destroy", "kg_tmcmc_synchronize", "kg_tmcmc_evaluate"):
+        for f in ("kg_tmcmc_destroy", "kg_tmcmc_synchronize", "kg_tmcmc_evaluate", "kg_tmcmc_evaluate_prior"):
             getattr(L, f).argtypes = [vp]
         for f in ("kg_tmcmc_generation", "kg_tmcmc_prepare", "kg_tmcmc_process"):
             getattr(L, f).argtypes = [vp, sz]
@@ -325,6 +325,9 @@ class TmcmcDevice:
 
     def synchronize(self):
         check(self._L.kg_tmcmc_synchronize(self.h))
+
+    def evaluate_prior(self):
+        check(self._L.kg_tmcmc_evaluate_prior(self.h))
 
     def candidates(self):
         X = np.empty((self.P, self.N))

@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1200 python -m pytest tests -x -q -m gpu ;;
+    eng) step eng 900 python -m pytest tests/test_gpu_engine.py -q --maxfail=20 ;;
     tm) step tm 900 python -m pytest tests/test_gpu_tmcmc.py -q --maxfail=10 ;;
     c3) step c3 600 python bench.py --workload c3 --steps ${C3_STEPS:-40} --warmup 3 ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;

@@ -1,0 +1,108 @@
+"""CPU tests of the korali API host logic (korali_amd/engine): the JSON
+surface of Experiment / Sample and configuration validation, which all run
+before any device call."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import korali
+
+
+def test_json_surface_nested_set_get():
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Variables"][0]["Name"] = "X0"
+    e["Variables"][2]["Name"] = "X2"
+    e["Solver"]["Population Size"] = 8
+    e["Solver"]["Termination Criteria"]["Max Generations"] = 100
+    e["Vector"] = np.arange(4.0)
+    e["Seed"] = 1621436249288981838  # > 2^53: kept exactly
+    assert e["Problem"]["Type"] == "Optimization"
+    assert e["Variables"][2]["Name"] == "X2"
+    assert len(e["Variables"]) == 3
+    assert e["Solver"]["Population Size"] == 8
+    assert e["Vector"] == [0.0, 1.0, 2.0, 3.0]
+    assert e["Seed"] == 1621436249288981838
+    assert isinstance(e["Solver"], korali.koraliJson)
+    d = json.loads(e.dump())
+    assert d["Solver"]["Termination Criteria"]["Max Generations"] == 100
+
+
+def test_functions_are_stored_by_index():
+    e = korali.Experiment()
+    e["Problem"]["Objective Function"] = lambda s: None
+    e["Problem"]["Likelihood Model"] = lambda s: None
+    assert e["Problem"]["Likelihood Model"] == e["Problem"]["Objective Function"] + 1
+
+
+def test_non_finite_numbers_round_trip(tmp_path):
+    e = korali.Experiment()
+    e["A"] = float("inf")
+    e["B"] = float("-inf")
+    e["C"] = float("nan")
+    e["D"] = 0.1
+    p = tmp_path / "s.json"
+    p.write_text(e.dump())
+    r = korali.Experiment()
+    assert r.loadState(str(p))
+    assert r["A"] == float("inf") and r["B"] == float("-inf") and np.isnan(r["C"]) and r["D"] == 0.1
+
+
+def base_cmaes():
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Function"] = lambda s: None
+    e["Variables"][0]["Name"] = "X"
+    e["Variables"][0]["Lower Bound"] = -1.0
+    e["Variables"][0]["Upper Bound"] = 1.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = 8
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    return e
+
+
+@pytest.mark.parametrize("key,value,msg", [
+    ("Population Size", 1, "'Population Size' must be larger 1"),
+    ("Mu Type", "Quadratic", "Invalid setting of Mu Type"),
+    ("Mirrored Sampling", True, "Mirrored Sampling"),
+    ("Type", "Optimizer/DEA", "Unrecognized solver type"),
+])
+def test_configuration_errors_before_device(key, value, msg):
+    e = base_cmaes()
+    e["Solver"][key] = value
+    with pytest.raises(korali.KoraliError, match=msg):
+        korali.Engine().run(e)
+
+
+def test_type_strings_ignore_case_and_whitespace():
+    e = base_cmaes()
+    e["Solver"]["Type"] = " optimizer / CMAES "
+    e["Solver"]["Population Size"] = 1
+    # reaches CMAES validation: the type was recognised
+    with pytest.raises(korali.KoraliError, match="Population Size"):
+        korali.Engine().run(e)
+
+
+def test_tmcmc_prior_validation():
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lambda s: None
+    e["Distributions"][0]["Name"] = "N 0"
+    e["Distributions"][0]["Type"] = "Univariate/Normal"
+    e["Variables"][0]["Name"] = "a"
+    e["Variables"][0]["Prior Distribution"] = "N 0"
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    e["Solver"]["Population Size"] = 100
+    e["File Output"]["Enabled"] = False
+    with pytest.raises(korali.KoraliError, match="Univariate/Uniform"):
+        korali.Engine().run(e)
+
+
+def test_native_modules_are_in_tree():
+    import korali_amd
+    pkg = os.path.dirname(korali_amd.__file__)
+    assert os.path.exists(os.path.join(pkg, "libkorali_engine.so"))
+    assert os.path.dirname(korali.Engine.__module__ and __import__("korali_amd.libkorali").libkorali.__file__) == pkg

@@ -1,0 +1,248 @@
+"""GPU tests of the korali API (korali/ -> korali_amd/engine, C++ over the
+C-ABI): the reference's own statistical scripts, re-run through `import
+korali`, and parity of the engine's result files with the reference's
+committed ones (tests/python/plot/cmaes, same configuration and seed).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import cmaes_variables, load_cmaes
+
+pytestmark = pytest.mark.gpu
+
+CM = load_cmaes()
+
+
+def by_gen(g):
+    for x in CM:
+        if x["Current Generation"] == g:
+            return x
+    raise KeyError(g)
+
+
+# tests/statistical/optimizers/correctness/model: minimum -0.5 area
+def evalmodel(s):
+    x = s["Parameters"][0]
+    r = x * x + math.sin(x)
+    s["F(x)"] = -r
+
+
+# examples/optimization/stochastic/_model/model.py negative_sphere (F part)
+def negative_sphere(p):
+    x = p["Parameters"]
+    res = 0.
+    for i in range(len(x)):
+        res += x[i]**2
+    p["F(x)"] = -0.5 * res
+
+
+def lgaussian_custom(s):  # tests/statistical/samplers/mean/model/model.py
+    x0 = s["Parameters"][0]
+    r = -0.5 * ((x0 + 2.0)**2 / (9.0)) - 0.5 * math.log(2 * math.pi * 9)
+    s["logLikelihood"] = r
+
+
+def cmaes_1d(**solver):
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Function"] = evalmodel
+    e["Variables"][0]["Name"] = "X"
+    e["Variables"][0]["Lower Bound"] = -10.0
+    e["Variables"][0]["Upper Bound"] = +10.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = 8
+    e["Solver"]["Termination Criteria"]["Max Generations"] = 100
+    for k, v in solver.items():
+        e["Solver"][k.replace("_", " ")] = v
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["File Output"]["Enabled"] = False
+    e["Random Seed"] = 1337
+    return e
+
+
+@pytest.mark.parametrize("cfg,tol", [({}, 1e-4), ({"Diagonal Covariance": True}, 1e-4), ({"Mu Type": "Linear"}, 1e-4),
+                                     ({"Mu Type": "Logarithmic"}, 1e-4),
+                                     ({"Mu Type": "Proportional", "Population Size": 64}, 1e-3),
+                                     ({"Mu Type": "Equal", "Population Size": 64}, 1e-3)])
+def test_statistical_cmaes_correctness(cfg, tol):
+    """tests/statistical/optimizers/correctness/run-cmaes.py: checkMin(e, 0.23246, tol)."""
+    import korali
+    e = cmaes_1d()
+    for k, v in cfg.items():
+        e["Solver"][k] = v
+    korali.Engine().run(e)
+    assert np.isclose(0.23246, e["Solver"]["Best Ever Value"], atol=tol)
+    assert e["Results"]["Best Sample"]["F(x)"] == e["Solver"]["Best Ever Value"]
+
+
+def test_unsupported_features_fail_loudly():
+    import korali
+    e = cmaes_1d()
+    e["Solver"]["Mirrored Sampling"] = True
+    with pytest.raises(korali.KoraliError, match="Mirrored Sampling"):
+        korali.Engine().run(e)
+
+
+def test_statistical_tmcmc_gaussian():
+    """tests/statistical/samplers/mean/run-tmcmc-gaussian.py."""
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lgaussian_custom
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    e["Solver"]["Population Size"] = 5000
+    e["Distributions"][0]["Name"] = "Uniform 0"
+    e["Distributions"][0]["Type"] = "Univariate/Uniform"
+    e["Distributions"][0]["Minimum"] = -15.0
+    e["Distributions"][0]["Maximum"] = +15.0
+    e["Variables"][0]["Name"] = "a"
+    e["Variables"][0]["Prior Distribution"] = "Uniform 0"
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["Random Seed"] = 1337
+    korali.Engine().run(e)
+    samples = np.reshape(e["Solver"]["Sample Database"], (-1, 1))
+    assert np.isclose(-2.0, samples.mean(), atol=0.05)
+    assert np.isclose(3.0, samples.std(), atol=0.05)
+    assert e["Solver"]["Annealing Exponent"] == 1.0
+
+
+def fixture_experiment(path, max_gen=100):
+    """The configuration behind tests/python/plot/cmaes (gen00000000.json)."""
+    import korali
+    v = cmaes_variables(by_gen(0))
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Function"] = negative_sphere
+    for i in range(10):
+        e["Variables"][i]["Name"] = "X" + str(i)
+        e["Variables"][i]["Lower Bound"] = v["Lower Bound"][i]
+        e["Variables"][i]["Upper Bound"] = v["Upper Bound"][i]
+        e["Variables"][i]["Initial Standard Deviation"] = v["Initial Standard Deviation"][i]
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = 32
+    e["Solver"]["Termination Criteria"]["Max Generations"] = max_gen
+    e["Solver"]["Termination Criteria"]["Min Value Difference Threshold"] = 1e-32
+    e["Solver"]["Termination Criteria"]["Max Infeasible Resamplings"] = 10000
+    e["Random Seed"] = 790510
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["File Output"]["Path"] = str(path)
+    return e
+
+
+def read_gen(path, g):
+    with open(os.path.join(path, "gen%08d.json" % g)) as f:
+        return json.load(f)
+
+
+def test_engine_reproduces_reference_result_files(tmp_path):
+    """Same experiment as the reference's committed CMA-ES result files:
+    every committed generation's population, sorting index, mean,
+    covariance, sigma and generator states are reproduced bit for bit."""
+    import korali
+    out = tmp_path / "res"
+    e = fixture_experiment(out)
+    korali.Engine().run(e)
+    assert e["Current Generation"] == 100
+    for ref in CM:
+        g = ref["Current Generation"]
+        if g == 0:
+            continue
+        mine = read_gen(out, g)["Solver"]
+        s = ref["Solver"]
+        assert np.array_equal(np.array(mine["Sample Population"]), np.array(s["Sample Population"])), g
+        assert mine["Sorting Index"] == s["Sorting Index"], g
+        for k in ("Current Mean", "Covariance Matrix", "Evolution Path", "Conjugate Evolution Path"):
+            assert np.array_equal(np.array(mine[k]), np.array(s[k])), (g, k)
+        assert mine["Sigma"] == s["Sigma"], g
+        assert mine["Best Ever Value"] == s["Best Ever Value"], g
+        if "Normal Generator" in s:
+            assert mine["Normal Generator"]["Range"] == s["Normal Generator"]["Range"], g
+    final = read_gen(out, 100)
+    assert final["Is Finished"] is True
+    assert os.path.exists(os.path.join(out, "latest"))
+
+
+def test_engine_resume_from_result_file_is_bit_exact(tmp_path):
+    """Experiment.loadState + Preserve Random Number Generator States: a run
+    resumed from generation 50's file ends exactly like the straight run."""
+    import korali
+    a = tmp_path / "a"
+    e = fixture_experiment(a)
+    korali.Engine().run(e)
+    r = korali.Experiment()
+    assert r.loadState(str(a / "gen00000050.json"))
+    r["Preserve Random Number Generator States"] = True
+    r["Problem"]["Objective Function"] = negative_sphere
+    r["File Output"]["Path"] = str(tmp_path / "b")
+    korali.Engine().run(r)
+    sa, sb = read_gen(a, 100)["Solver"], read_gen(tmp_path / "b", 100)["Solver"]
+    for k in ("Sample Population", "Current Mean", "Covariance Matrix", "Sigma", "Best Ever Value"):
+        assert sa[k] == sb[k], k
+    assert sa["Normal Generator"]["Range"] == sb["Normal Generator"]["Range"]
+
+
+def test_objective_kernel_equals_callback():
+    """The device-batched objective (extension key) gives the same run as
+    the host callback of the same function."""
+    import korali
+    runs = []
+    for kernel in (False, True):
+        e = korali.Experiment()
+        e["Problem"]["Type"] = "Optimization"
+        if kernel:
+            e["Problem"]["Objective Kernel"] = "Negative Sphere"
+        else:
+            e["Problem"]["Objective Function"] = negative_sphere
+        for i in range(6):
+            e["Variables"][i]["Name"] = "X" + str(i)
+            e["Variables"][i]["Initial Value"] = 1.0
+            e["Variables"][i]["Initial Standard Deviation"] = 0.5
+        e["Solver"]["Type"] = "Optimizer/CMAES"
+        e["Solver"]["Population Size"] = 24
+        e["Solver"]["Termination Criteria"]["Max Generations"] = 40
+        e["Random Seed"] = 4242
+        e["Console Output"]["Verbosity"] = "Silent"
+        e["File Output"]["Enabled"] = False
+        korali.Engine().run(e)
+        runs.append((e["Solver"]["Best Ever Value"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sigma"]))
+    assert runs[0] == runs[1]
+
+
+def test_tmcmc_likelihood_kernel_equals_callback():
+    import korali
+
+    def lg(s):
+        ss = 0.0
+        for x in s["Parameters"]:
+            ss += x**2
+        s["logLikelihood"] = -0.5 * ss
+
+    runs = []
+    for kernel in (False, True):
+        e = korali.Experiment()
+        e["Problem"]["Type"] = "Bayesian/Custom"
+        if kernel:
+            e["Problem"]["Likelihood Kernel"] = "Gaussian"
+        else:
+            e["Problem"]["Likelihood Model"] = lg
+        e["Distributions"][0]["Name"] = "Uniform 0"
+        e["Distributions"][0]["Type"] = "Univariate/Uniform"
+        e["Distributions"][0]["Minimum"] = -5.0
+        e["Distributions"][0]["Maximum"] = 5.0
+        for i in range(4):
+            e["Variables"][i]["Name"] = "X" + str(i)
+            e["Variables"][i]["Prior Distribution"] = "Uniform 0"
+        e["Solver"]["Type"] = "Sampler/TMCMC"
+        e["Solver"]["Population Size"] = 1000
+        e["Random Seed"] = 7
+        e["Console Output"]["Verbosity"] = "Silent"
+        e["File Output"]["Enabled"] = False
+        korali.Engine().run(e)
+        runs.append((e["Solver"]["LogEvidence"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sample Database"]))
+    assert runs[0] == runs[1]
