@@ -112,6 +112,41 @@ def cpu_baseline(seconds_budget=10.0):
                       f"with system libm (timing build), 1 thread; bit-exact CR build: {gens_cr} generations"}
 
 
+def engine_rate(steps, warmup, cov):
+    """The same C2 experiment through the korali API (C++ engine: termination
+    checks and bookkeeping every generation, as Korali's Experiment::run
+    does).  Warm-up generations run first; the timed call resumes the
+    in-memory state for `steps` more generations."""
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Kernel"] = "Negative Rosenbrock"
+    for i in range(N_VARS):
+        e["Variables"][i]["Name"] = "X" + str(i)
+        e["Variables"][i]["Initial Value"] = 0.0
+        e["Variables"][i]["Initial Standard Deviation"] = 1.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = LAMBDA
+    e["Solver"]["Covariance Update"] = "MFMA" if cov == "mfma" else "Exact"
+    e["Solver"]["Termination Criteria"]["Max Generations"] = warmup
+    e["Random Seed"] = 1337
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    k = korali.Engine()
+    k.run(e)
+    e["Preserve Random Number Generator States"] = True
+    # each resumed run() re-creates the device handle from the saved state;
+    # two runs of different length cancel that fixed cost
+    short = max(1, steps // 8)
+    times = []
+    for n in (short, steps):
+        e["Solver"]["Termination Criteria"]["Max Generations"] = e["Current Generation"] + n
+        t0 = time.perf_counter()
+        k.run(e)
+        times.append(time.perf_counter() - t0)
+    return (steps - short) / (times[1] - times[0])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,6 +226,8 @@ def main():
     dev.profile(False)
 
     best = float(dev["Best Ever Value"][0])
+    dev.close()
+    eng = engine_rate(args.steps, args.warmup, args.cov) if world == 1 else None
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -224,6 +261,7 @@ def main():
                    "population": LAMBDA, "variables": N_VARS, "covariance_update": args.cov,
                    "parallelism": f"replicas{world}"},
         "samples_per_sec": gens_per_s * LAMBDA,
+        "engine_generations_per_sec": eng,
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},

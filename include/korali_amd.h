@@ -103,6 +103,8 @@ int kg_cmaes_synchronize(kg_cmaes_t h); /* waits and reports device-side errors 
 int kg_cmaes_field_size(kg_cmaes_t h, const char *name, size_t *n);
 int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n);
 int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t n);
+/* several scalar fields with one device read (termination checks, logging) */
+int kg_cmaes_get_fields(kg_cmaes_t h, const char *const *names, size_t count, double *out);
 int kg_cmaes_get_sorting_index(kg_cmaes_t h, uint64_t *out);
 /* GSL mt19937 state as Korali serialises it: 624 x uint64 words + int32 mti
  * + 4 pad bytes = 5000 bytes.  which: 0 Normal, 1 Uniform generator. */

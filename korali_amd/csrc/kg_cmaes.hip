@@ -840,12 +840,17 @@ void gsl_seed_state(uint64_t seed, unsigned char *out5000) {
   memcpy(out5000 + 624 * 8, &mti, 4);
 }
 
+__global__ void k_collect_errors(CmaesScalars *sc, const StreamState *a, const StreamState *b) {
+  sc->errors |= a->errors | b->errors;
+}
+
 int check_errors(kg_cmaes_s *h) {
-  unsigned int e = 0, e1 = 0, e2 = 0;
-  KG_HIP(hipMemcpy(&e, &h->sc->errors, sizeof(e), hipMemcpyDeviceToHost));
-  KG_HIP(hipMemcpy(&e1, &h->normal.state()->errors, sizeof(e1), hipMemcpyDeviceToHost));
-  KG_HIP(hipMemcpy(&e2, &h->uniform.state()->errors, sizeof(e2), hipMemcpyDeviceToHost));
-  e |= e1 | e2;
+  // one read: the generators' flags are folded into the scalar block first
+  unsigned int e = 0;
+  hipLaunchKernelGGL(k_collect_errors, dim3(1), dim3(1), 0, h->stream, h->sc, h->normal.state(), h->uniform.state());
+  KG_HIP(hipGetLastError());
+  KG_HIP(hipMemcpyAsync(&e, &h->sc->errors, sizeof(e), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
   if (e == 0) return 0;
   std::string m = "korali_amd CMA-ES device error:";
   if (e & KG_ERR_NONFINITE_F) m += " Non finite value of function evaluation detected.";
@@ -1242,6 +1247,26 @@ int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t 
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_cmaes_get_fields(kg_cmaes_t h, const char *const *names, size_t count, double *out) {
+  // one copy of the scalar block serves every scalar name
+  CmaesScalars hs;
+  KG_HIP(hipMemcpyAsync(&hs, h->sc, sizeof(hs), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i < count; i++) {
+    FieldRef r;
+    KG_CHECK(field_ref(h, names[i], r), std::string("unknown CMA-ES field: ") + names[i]);
+    const char *base = (const char *)h->sc;
+    const char *p = (const char *)r.dev;
+    if (r.n == 1 && p >= base && p < base + sizeof(CmaesScalars)) {
+      memcpy(&out[i], (const char *)&hs + (p - base), sizeof(double));
+    } else {
+      KG_CHECK(r.n == 1, std::string("kg_cmaes_get_fields: not a scalar field: ") + names[i]);
+      KG_HIP(hipMemcpy(&out[i], r.dev, sizeof(double), hipMemcpyDeviceToHost));
+    }
+  }
   return 0;
 }
 

@@ -344,7 +344,7 @@ struct CmaesModule : SolverModule {
       check(kg_cmaes_set_fitness(h, F.data()));
     }
     check(kg_cmaes_update(h, gen));
-    check(kg_cmaes_synchronize(h));
+    check(kg_cmaes_synchronize(h));  // device-side error flags -> KoraliError
   }
 
   double field(const char *k) {
@@ -354,19 +354,22 @@ struct CmaesModule : SolverModule {
   }
 
   void checkTermination(size_t gen, std::vector<std::string> &met) override {
-    const double evals = field("Model Evaluation Count");
+    static const char *names[] = {"Model Evaluation Count",         "Infeasible Sample Count",
+                                  "Maximum Covariance Eigenvalue",  "Minimum Covariance Eigenvalue",
+                                  "Current Min Standard Deviation", "Current Max Standard Deviation",
+                                  "Best Ever Value",                "Current Best Value",
+                                  "Previous Best Value"};
+    double v[9];
+    check(kg_cmaes_get_fields(h, names, 9, v));
     if (gen > maxGenerations) met.push_back("Max Generations");
-    if (maxModelEvaluations <= evals) met.push_back("Max Model Evaluations");
+    if (maxModelEvaluations <= v[0]) met.push_back("Max Model Evaluations");
     if (gen <= 1) return;
-    if (maxInfeasible > 0 && field("Infeasible Sample Count") >= maxInfeasible)
-      met.push_back("Max Infeasible Resamplings");
-    if (field("Maximum Covariance Eigenvalue") >= maxCondition * field("Minimum Covariance Eigenvalue"))
-      met.push_back("Max Condition Covariance Matrix");
-    if (field("Current Min Standard Deviation") <= minStd) met.push_back("Min Standard Deviation");
-    if (field("Current Max Standard Deviation") >= maxStd) met.push_back("Max Standard Deviation");
-    if (field("Best Ever Value") > maxValue) met.push_back("Max Value");
-    if (std::fabs(field("Current Best Value") - field("Previous Best Value")) < minValueDiff)
-      met.push_back("Min Value Difference Threshold");
+    if (maxInfeasible > 0 && v[1] >= maxInfeasible) met.push_back("Max Infeasible Resamplings");
+    if (v[2] >= maxCondition * v[3]) met.push_back("Max Condition Covariance Matrix");
+    if (v[4] <= minStd) met.push_back("Min Standard Deviation");
+    if (v[5] >= maxStd) met.push_back("Max Standard Deviation");
+    if (v[6] > maxValue) met.push_back("Max Value");
+    if (std::fabs(v[7] - v[8]) < minValueDiff) met.push_back("Min Value Difference Threshold");
   }
 
   void getConfiguration(Json &sv) override {

@@ -56,7 +56,7 @@ EXPORTED = [
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
     "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_update", "kg_cmaes_generation",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
-    "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
+    "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
@@ -88,6 +88,7 @@ def lib():
         L.kg_cmaes_get_field.argtypes = [vp, cp, dp, sz]
         L.kg_cmaes_set_field.argtypes = [vp, cp, dp, sz]
         L.kg_cmaes_get_sorting_index.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.kg_cmaes_get_fields.argtypes = [vp, C.POINTER(cp), sz, dp]
         L.kg_cmaes_get_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_set_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_device_ptr.argtypes = [vp, cp, C.POINTER(vp)]
