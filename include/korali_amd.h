@@ -119,6 +119,13 @@ int kg_cmaes_stream(kg_cmaes_t h, void **stream);
 int kg_cmaes_profile(kg_cmaes_t h, int enable);
 int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, size_t *count);
 
+/* ------------------------------------------------------------ testing */
+/* Host reference of the mt19937 jump-ahead the chunked device producer
+ * uses: out = the 624 untempered words `distance` positions after window624
+ * (window624 = 624 consecutive untempered words of a GSL mt19937 stream,
+ * not starting at the seeding word 0).  Runs on the host, no device needed. */
+int kg_debug_mt_jump(const uint32_t *window624, uint64_t distance, uint32_t *out624);
+
 /* --------------------------------------------------------------- TMCMC */
 typedef struct kg_tmcmc_s *kg_tmcmc_t;
 

@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(64) k_objective(int N, int lam, int obj, const
           prev = x;
         } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
           r0 += x * x;
-          r1 += cos(cc * x);
+          r1 += cos_cr(cc * x);
         } else {
           r0 += x * x;
         }
@@ -858,6 +858,7 @@ int check_errors(kg_cmaes_s *h) {
   if (e & KG_ERR_RESAMPLE_RESERVE) m += " Infeasible samples exceeded the device resampling reserve.";
   if (e & KG_ERR_ZERO_LIST) m += " Too many zero mt19937 words pending.";
   if (e & KG_ERR_EIGEN) m += " Eigen decomposition did not converge.";
+  if (e & KG_ERR_SYNC_TIMEOUT) m += " An in-launch workgroup hand-off timed out.";
   set_error(m);
   return 1;
 }

@@ -51,7 +51,63 @@ enum : uint32_t {
   KG_ERR_ZERO_LIST = 1u << 3,       // > KG_MAX_ZERO_WORDS zero MT words pending
   KG_ERR_EIGEN = 1u << 4,           // QR iteration did not converge
   KG_ERR_CHOLESKY = 1u << 5,        // covariance not positive definite
+  KG_ERR_SYNC_TIMEOUT = 1u << 6,    // an in-launch workgroup hand-off timed out
 };
+
+// In-launch workgroup hand-off (MI355X_MICROARCH.md, inter-workgroup
+// visibility, R2 granules): a double travels as two 8-byte {tag, half}
+// granules stored write-through (agent-scope relaxed atomics: sc1) and read
+// back with sc1 loads until both tags match; the data is its own flag, so no
+// fence is involved.  Buffers are zeroed before every launch, tags are
+// phase + 1.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+constexpr unsigned KG_SPIN_LIMIT = 1u << 21;  // ~seconds: a hang becomes an error
+
+__device__ inline void put_granule_dbl(unsigned long long *p, unsigned tag, double x) {
+  gu64_t *g = (gu64_t *)p;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (b & 0xffffffffULL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// All threads of the workgroup: element e < count comes from granules
+// base[2*idx(e)], idx(e) = e for e < count-1, the last element (when
+// lastIdx >= 0) from base[2*lastIdx].  Returns false when the spin limit or
+// another workgroup's abort ended the wait.
+__device__ inline bool poll_granule_dbls(unsigned long long *base, int count, int lastIdx, unsigned tag,
+                                         double *dst, unsigned long long *abortw, unsigned *errors) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  gu64_t *g = (gu64_t *)base;
+  for (int e0 = 0; e0 < count; e0 += nt) {
+    const int e = e0 + t;
+    bool done = e >= count;
+    const int gi = (lastIdx >= 0 && e == count - 1) ? lastIdx : e;
+    unsigned spins = 0;
+    for (;;) {
+      if (!done) {
+        const unsigned long long lo = __hip_atomic_load(g + 2 * gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(g + 2 * gi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag) {
+          dst[e] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffULL)));
+          done = true;
+        }
+      }
+      if (__all(done)) break;
+      ++spins;
+      if ((spins & 255u) == 0) {
+        if (__hip_atomic_load((gu64_t *)abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+        if (spins > KG_SPIN_LIMIT) {
+          __hip_atomic_store((gu64_t *)abortw, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          atomicOr(errors, KG_ERR_SYNC_TIMEOUT);
+          return false;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
 
 // ------------------------------------------------------- double-double math
 struct dd {
@@ -173,6 +229,53 @@ __device__ inline double pow_cr(double x, double y) {
   if (l.hi > 709.0 || l.hi < -708.0) return pow(x, y);
   l = dd_exp(l);
   return l.hi + l.lo;
+}
+
+// cos(x) correctly rounded (for |x| < 2^30): Cody-Waite reduction by a
+// triple-double pi/2 with exact products, then the Taylor series of cos or
+// sin of the reduced argument in double-double (15 terms, |r| <= pi/4,
+// ~2^-104 relative) and one final rounding.  Branch-free in the quadrant
+// so a wavefront runs one instruction stream.  The oracle evaluates the
+// same sequence (oracle/refcpu.c kr_cos_cr), so Ackley objectives agree bit
+// for bit.
+__host__ __device__ inline double cos_cr(double x) {
+  if (!(fabs(x) < 1073741824.0)) return cos(x);  // NaN / inf / huge: never produced by the objectives
+  constexpr double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
+  constexpr double INV_PIO2 = 0x1.45f306dc9c883p-1;
+  constexpr double CH[15] = {0x1p+0, -0x1p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+                             -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37,
+                             0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62,
+                             -0x1.0ce396db7f853p-70, 0x1.f2cf01972f578p-80, -0x1.88e85fc6a4e5ap-89,
+                             0x1.0a18a2635085dp-98};
+  constexpr double CL[15] = {0.0, 0.0, 0x1.5555555555555p-59, 0x1.f49f49f49f49fp-65, 0x1.a01a01a01a01ap-76,
+                             -0x1.cbbc05b4fa99ap-76, -0x1.2aec959e14c06p-83, -0x1.05d6f8a2efd1fp-92,
+                             0x1.1d8656b0ee8cbp-101, -0x1.eec01221a8b0bp-107, 0x1.ea72b4afe3c2fp-120,
+                             0x1.aebcdbd20331cp-124, -0x1.9ada5fcc1ab14p-135, 0x1.71c37ebd16540p-143,
+                             0x1.b9e2e28e1aa54p-153};
+  constexpr double SH[15] = {0x1p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+                             0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33,
+                             -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57,
+                             0x1.71b8ef6dcf572p-66, -0x1.761b41316381ap-75, 0x1.3f3ccdd165fa9p-84,
+                             -0x1.d1ab1c2dccea3p-94, 0x1.259f98b4358adp-103};
+  constexpr double SL[15] = {0.0, -0x1.5555555555555p-57, 0x1.1111111111111p-63, -0x1.a01a01a01a01ap-73,
+                             -0x1.c154f8ddc6c00p-73, 0x1.c062e06d1f209p-80, 0x1.f28e0cc748ebep-87,
+                             -0x1.1d8656b0ee8cbp-97, 0x1.ac981465ddc6cp-103, -0x1.2650f61dbdcb4p-112,
+                             -0x1.d043ae40c4647p-120, 0x1.3423c7d91404fp-130, -0x1.58ddadf344487p-139,
+                             -0x1.054d0c78aea14p-149, 0x1.eaf8c39dd9bc5p-157};
+  const double kd = floor(x * INV_PIO2 + 0.5);
+  const dd t1 = dd_tp(kd, P1), t2 = dd_tp(kd, P2);
+  dd r = dd_add(dd{x, 0.0}, dd{-t1.hi, -t1.lo});
+  r = dd_add(r, dd{-t2.hi, -t2.lo});
+  r = dd_add(r, dd{-(kd * P3), 0.0});
+  const int q = (int)((long long)kd & 3);
+  const bool odd = (q & 1) != 0;
+  const dd z = dd_mul(r, r);
+  dd p{odd ? SH[14] : CH[14], odd ? SL[14] : CL[14]};
+#pragma unroll
+  for (int j = 13; j >= 0; j--) p = dd_add(dd_mul(p, z), dd{odd ? SH[j] : CH[j], odd ? SL[j] : CL[j]});
+  p = dd_mul(p, odd ? r : dd{1.0, 0.0});
+  const double v = p.hi + p.lo;
+  return (q == 1 || q == 2) ? -v : v;
 }
 
 // ---------------------------------------------------------------- mt19937

@@ -520,6 +520,346 @@ __global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict
 }
 
 // ------------------------------------------------------------------------
+// Phases A and B for N > 128 (the matrix no longer fits one CU's LDS):
+// many workgroups, each holding a few FULL rows of the symmetric matrix in
+// LDS (rows round-robin, row r on workgroup r % P).  Symmetric storage makes
+// every gslcblas chain of a row local to its owner:
+//   dsymv  x_j = (sum_{c desc} (tau v_c) m[j][c] + (tau v_j) m[j][j]) + tau sum_{c asc} v_c m[j][c]
+//          (column j of the lower triangle is row j of the upper one);
+//   dsyr2  m[a][b] += (-v_a) x_b + (-x_a) v_b with a >= b, applied to both
+//          (a,b) and (b,a), so the two copies stay bit-identical.
+// Per Householder step two in-launch hand-offs (R2 granules): the pivot
+// row's owner broadcasts (tau, v); every owner publishes its x_j and every
+// workgroup gathers the whole x (xv is then recomputed redundantly).  Every
+// step has slots of its own (no slot is ever rewritten within a launch, so
+// no workgroup can miss a value however far the others run ahead; tau = 0
+// steps skip the x exchange).
+constexpr int TMW_TPB = 256;
+constexpr int TMW_MAXP = 64;
+
+__host__ __device__ inline int tmw_rows(int N) { return (N + TMW_MAXP - 1) / TMW_MAXP; }
+__host__ __device__ inline int tmw_groups(int N) { return (N + tmw_rows(N) - 1) / tmw_rows(N); }
+size_t tmw_lds_bytes(int N) {
+  return ((size_t)tmw_rows(N) * (N + 1) + 3 * (size_t)N + 64 + 16 + 2 * 16) * sizeof(double);
+}
+// comm buffer (u64 words): v granules [N][2(N+1)] (tau in element N), x
+// granules [N][2N], abort word (+ pad to 16 bytes)
+size_t tmw_comm_words(int N) { return 2 * (size_t)N * (N + 1) + 2 * (size_t)N * N + 2; }
+
+__global__ void __launch_bounds__(TMW_TPB) k_tridiag_mw(int N, const double *__restrict__ C, double *gH,
+                                                        double *tauOut, double *dOut, double *sdOut,
+                                                        unsigned long long *comm, unsigned int *errors) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int P = gridDim.x, g = blockIdx.x, RW = tmw_rows(N), lda = N + 1;
+  double *M = smem;                     // local row k = global row g + k P
+  double *vloc = M + (size_t)RW * lda;  // v with v_0 = 1
+  double *tv = vloc + N;                // tau v
+  double *xl = tv + N;                  // x
+  double *sv = xl + N;                  // 64: staged chain addends
+  double *scal = sv + 64;               // 16 scalars
+  double *accb = scal + 16;             // 16: dsymv acc per local row
+  double *t2b = accb + 16;              // 16: dsymv t2 per local row
+  unsigned long long *gv = comm, *gx = comm + 2 * (size_t)N * (N + 1);
+  unsigned long long *abortw = gx + 2 * (size_t)N * N;
+
+  for (int idx = tid; idx < RW * N; idx += nt) {
+    const int k = idx / N, c = idx % N, r = g + k * P;
+    if (r < N) M[(size_t)k * lda + c] = (c <= r) ? C[(size_t)r * N + c] : C[(size_t)c * N + r];
+  }
+  const int maxRow = g + ((N - 1 - g) / P) * P;  // largest row owned
+  __syncthreads();
+  for (int i = 0; i + 2 < N; i++) {
+    if (maxRow < i) break;  // nothing left to own or to update
+    const int n = N - i - 1;
+    const unsigned tag = (unsigned)i + 1u;
+    unsigned long long *gvp = gv + (size_t)i * 2 * (N + 1), *gxp = gx + (size_t)i * 2 * N;
+    if (i % P == g) {
+      // ---- pivot row i: Householder vector of v = row i, columns i+1.. (== column i below the diagonal)
+      double *v = M + (size_t)(i / P) * lda + i + 1;
+      if (wid == 0) {
+        double scale_carry = 0.0, ssq = 1.0;  // gslcblas dnrm2 over v[1..n-1] (see k_tridiag)
+        for (int base = 1; base < n; base += 64) {
+          const int r = base + lane;
+          const double a_ = fabs(v[min(r, n - 1)]);
+          const double a = (r < n) ? a_ : 0.0;
+          double pm = a;
+          for (int off = 1; off < 64; off <<= 1) {
+            const double t = __shfl_up(pm, off, 64);
+            if (lane >= off) pm = fmax(pm, t);
+          }
+          double before = __shfl_up(pm, 1, 64);
+          if (lane == 0) before = 0.0;
+          before = fmax(before, scale_carry);
+          int type = 0;
+          double q = 0.0;
+          if (r < n && a != 0.0) {
+            if (before < a) {
+              type = 1;
+              q = before / a;
+            } else {
+              type = 2;
+              q = a / before;
+            }
+          }
+          const double tq = (type == 2) ? q * q : 0.0;
+          const unsigned long long m1 = __ballot(type == 1);
+          const int cnt = (n - base) < 64 ? (n - base) : 64;
+          sv[lane] = (type == 1) ? q : tq;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          for (int l0 = 0; l0 < cnt; l0 += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
+            const unsigned bits = (unsigned)((m1 >> l0) & 0xffULL);
+            if (bits == 0) {
+#pragma unroll
+              for (int u = 0; u < 8; u++) ssq += t[u];
+            } else {
+#pragma unroll
+              for (int u = 0; u < 8; u++) {
+                if ((bits >> u) & 1u)
+                  ssq = 1.0 + ssq * t[u] * t[u];
+                else
+                  ssq += t[u];
+              }
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          scale_carry = fmax(scale_carry, readlane_d(pm, 63));
+        }
+        if (lane == 0) {
+          double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
+          int branch = 0;
+          const double xnorm = (n - 1 == 1) ? fabs(v[1]) : scale_carry * sqrt(ssq);
+          if (xnorm != 0) {
+            const double alpha = v[0];
+            beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
+            tau_i = (beta - alpha) / beta;
+            const double s = alpha - beta;
+            if (fabs(s) > DMIN) {
+              f1 = 1.0 / s;
+              branch = 1;
+            } else {
+              f1 = EPS / s;
+              f2 = 1.0 / EPS;
+              branch = 2;
+            }
+          }
+          scal[0] = tau_i;
+          scal[1] = f1;
+          scal[2] = f2;
+          scal[3] = beta;
+          scal[4] = (double)branch;
+          tauOut[i] = tau_i;
+        }
+      }
+      __syncthreads();
+      const int branch = (int)scal[4];
+      if (branch != 0) {
+        const double f1 = scal[1], f2 = scal[2];
+        for (int r = 1 + tid; r < n; r += nt) {
+          double t = v[r] * f1;
+          if (branch == 2) t = t * f2;
+          v[r] = t;
+        }
+      }
+      __syncthreads();
+      if (branch != 0 && tid == 0) v[0] = scal[3];
+      __syncthreads();
+      for (int r = tid; r < n; r += nt) {
+        gH[(size_t)i * N + r] = v[r];
+        const double vr = (r == 0) ? 1.0 : v[r];
+        vloc[r] = vr;
+        put_granule_dbl(gvp + 2 * r, tag, vr);
+      }
+      if (tid == 0) put_granule_dbl(gvp + 2 * N, tag, scal[0]);
+    } else {
+      // (v_0..v_{n-1}, tau) from the pivot's owner; tau lands in vloc[n]
+      const bool ok = poll_granule_dbls(gvp, n + 1, N, tag, vloc, abortw, errors);
+      if (__syncthreads_or(!ok)) return;
+      if (tid == 0) scal[0] = vloc[n];
+    }
+    __syncthreads();
+    const double tau_i = scal[0];
+    if (tau_i == 0.0) continue;  // householder_transform gave tau = 0: no update
+    for (int r = tid; r < n; r += nt) tv[r] = tau_i * vloc[r];
+    __syncthreads();
+    // ---- dsymv chains of the owned active rows (rows i+1..N-1)
+    if (wid < 2 && lane < RW) {
+      const int r = g + lane * P;
+      if (r > i && r < N) {
+        const double *row = M + (size_t)lane * lda;
+        const int jr = r - i - 1;
+        if (wid == 0) {
+          double acc = 0.0;  // columns c = N-1 .. r+1, descending
+          int c = N - 1;
+          for (; c - 7 > r; c -= 8) {
+            double p[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) p[u] = tv[c - u - i - 1] * row[c - u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += p[u];
+          }
+          for (; c > r; c--) acc += tv[c - i - 1] * row[c];
+          accb[lane] = acc + tv[jr] * row[r];
+        } else {
+          double t2 = 0.0;  // columns c = i+1 .. r-1, ascending
+          int c = i + 1;
+          for (; c + 8 <= r; c += 8) {
+            double p[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) p[u] = vloc[c + u - i - 1] * row[c + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t2 += p[u];
+          }
+          for (; c < r; c++) t2 += vloc[c - i - 1] * row[c];
+          t2b[lane] = t2;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < RW) {
+      const int r = g + tid * P;
+      if (r > i && r < N) put_granule_dbl(gxp + 2 * (r - i - 1), tag, accb[tid] + tau_i * t2b[tid]);
+    }
+    {
+      const bool ok = poll_granule_dbls(gxp, n, -1, tag, xl, abortw, errors);
+      if (__syncthreads_or(!ok)) return;
+    }
+    // ---- xv = sum x_r v_r (sequential, staged) and alpha = -(tau/2) xv
+    if (wid == 0) {
+      double xv = 0.0;
+      for (int base = 0; base < n; base += 64) {
+        const int r = base + lane, rc = min(r, n - 1);
+        const double p_ = xl[rc] * vloc[rc];
+        sv[lane] = (r < n) ? p_ : 0.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int cnt = (n - base) < 64 ? (n - base) : 64;
+        for (int l0 = 0; l0 < cnt; l0 += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) xv += t[u];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
+    }
+    __syncthreads();
+    {
+      const double alpha = scal[5];
+      for (int r = tid; r < n; r += nt) xl[r] += alpha * vloc[r];
+    }
+    __syncthreads();
+    // ---- dsyr2 (alpha = -1) on the owned active rows, both triangles
+    for (int idx = tid; idx < RW * n; idx += nt) {
+      const int k = idx / n, jj = idx % n, r = g + k * P;
+      if (r <= i || r >= N) continue;
+      const int jr = r - i - 1;
+      const int a = jr > jj ? jr : jj, b = jr > jj ? jj : jr;
+      const double tmp1 = -1.0 * vloc[a], tmp2 = -1.0 * xl[a];
+      M[(size_t)k * lda + i + 1 + jj] += tmp1 * xl[b] + tmp2 * vloc[b];
+    }
+    __syncthreads();
+  }
+  for (int k = tid; k < RW; k += nt) {
+    const int r = g + k * P;
+    if (r < N) {
+      dOut[r] = M[(size_t)k * lda + r];
+      if (r + 1 < N) sdOut[r] = M[(size_t)k * lda + r + 1];
+    }
+  }
+}
+
+// Phase B for N > 128: the columns of Q are independent under
+// householder_hm, so workgroups own UMW_COLS columns each (Q^T rows in LDS)
+// and apply all reflectors without talking to each other; the next
+// reflector row streams into a second LDS buffer while the current one is
+// applied.
+constexpr int UMW_COLS = 4;
+constexpr int UMW_TPB = 256;
+__host__ __device__ inline int umw_groups(int N) { return (N + UMW_COLS - 1) / UMW_COLS; }
+size_t umw_lds_bytes(int N) { return ((size_t)UMW_COLS * (N + 1) + 2 * (size_t)N + 16) * sizeof(double); }
+
+__global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__restrict__ gH,
+                                                       const double *__restrict__ tau, double *gQt) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int P = gridDim.x, g = blockIdx.x, lda = N + 1;
+  double *Q = smem;                              // local k = column g + k P of Q
+  double *hb = Q + (size_t)UMW_COLS * lda;       // 2 x N
+  double *w = hb + 2 * (size_t)N;                // UMW_COLS
+  for (int idx = tid; idx < UMW_COLS * lda; idx += nt) {
+    const int k = idx / lda, r = idx % lda;
+    Q[idx] = (r < N && r == g + k * P) ? 1.0 : 0.0;
+  }
+  constexpr int PF = 4;  // prefetch registers per thread (N <= 1024)
+  if (N >= 3)
+    for (int r = tid; r < N - (N - 3) - 1; r += nt) hb[r] = gH[(size_t)(N - 3) * N + r];
+  __syncthreads();
+  int buf = 0;
+  for (int i = N - 3; i >= 0; i--) {
+    const int n = N - i - 1;
+    const double ti = tau[i];
+    const double *h = hb + (size_t)buf * N;
+    double pf[PF];
+    if (i > 0) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        const int r = tid + u * nt;
+        pf[u] = (r < n + 1) ? gH[(size_t)(i - 1) * N + r] : 0.0;
+      }
+    }
+    if (ti != 0.0) {
+      if (wid == 0 && lane < UMW_COLS) {
+        const int c = g + lane * P;
+        if (c > i && c < N) {
+          const double *col = Q + (size_t)lane * lda + (i + 1);
+          double wj = col[0];
+          int r = 1;
+          for (; r + 8 <= n; r += 8) {
+            double p[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) p[u] = col[r + u] * h[r + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) wj += p[u];
+          }
+          for (; r < n; r++) wj += col[r] * h[r];
+          w[lane] = wj;
+        }
+      }
+      __syncthreads();
+      for (int idx = tid; idx < UMW_COLS * n; idx += nt) {
+        const int k = idx / n, r = idx % n, c = g + k * P;
+        if (c <= i || c >= N) continue;
+        double *col = Q + (size_t)k * lda + (i + 1);
+        const double wj = w[k];
+        col[r] = (r == 0) ? col[0] - ti * wj : col[r] - ti * h[r] * wj;
+      }
+    }
+    if (i > 0) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        const int r = tid + u * nt;
+        if (r < n + 1) hb[(size_t)(buf ^ 1) * N + r] = pf[u];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  for (int idx = tid; idx < UMW_COLS * lda; idx += nt) {
+    const int k = idx / lda, r = idx % lda, c = g + k * P;
+    if (c < N) gQt[(size_t)c * lda + r] = Q[idx];
+  }
+}
+
+// ------------------------------------------------------------------------
 // Phase C: the implicit-shift QR chase (eigen/symmv.c main loop + qrstep)
 // on the tridiagonal d/sd.  It only produces the rotation sequence: per QR
 // step a header (a, n) and n-1 Givens pairs (c, s); then the ABS_ASC
@@ -867,6 +1207,13 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipEventCreateWithFlags(&ev_chase, hipEventDisableTiming));
   }
   lds = eig_use_lds(N);
+  if (!lds) {
+    KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
+    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)tmw_lds_bytes(N)));
+    KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)umw_lds_bytes(N)));
+  }
   const int attr = 160 * 1024;
   KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
   KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
@@ -877,7 +1224,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
 
 EigenSolver::~EigenSolver() {
   for (void *p : {(void *)gA, (void *)gH, (void *)gQt, (void *)gWork, (void *)tau, (void *)dsd, (void *)chaseWork,
-                  (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm})
+                  (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm, (void *)comm})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
                   (void *)host.perm})
@@ -900,9 +1247,11 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   if (lds)
     hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), matb + tridiag_vec_bytes(N), s, N, C, gA, gH, tau, d, sd,
                        trace);
-  else
-    hipLaunchKernelGGL(k_tridiag<false>, dim3(1), dim3(1024), tridiag_vec_bytes(N), s, N, C, gA, gH, tau, d, sd,
-                       trace);
+  else {
+    KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), tmw_lds_bytes(N), s, N, C, gH, tau, d, sd,
+                       comm, errors);
+  }
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_tridiag", 1);
   EigRec devRec = dev;
@@ -920,7 +1269,7 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   if (lds)
     hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + 2 * N * sizeof(double), s, N, gH, tau, gQt);
   else
-    hipLaunchKernelGGL(k_unpack<false>, dim3(1), dim3(1024), 2 * N * sizeof(double), s, N, gH, tau, gQt);
+    hipLaunchKernelGGL(k_unpack_mw, dim3(umw_groups(N)), dim3(UMW_TPB), umw_lds_bytes(N), s, N, gH, tau, gQt);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_unpack", 1);
   if (hostChase) {

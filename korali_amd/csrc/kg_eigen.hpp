@@ -35,6 +35,7 @@ class EigenSolver {
   bool lds = true;
   double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
          *chaseWork = nullptr;
+  unsigned long long *comm = nullptr;  // in-launch hand-off granules (N > 128 tridiagonalisation)
   struct Rec {
     int *hdr = nullptr;
     double *cs = nullptr;

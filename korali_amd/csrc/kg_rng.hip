@@ -2,7 +2,9 @@
 // Semantics: GSL 2.6 rng/mt.c + randist/gauss.c (polar), as called by
 // Korali's Normal/Uniform distributions (univariate/normal/normal.cpp.base:
 // 32-35, univariate/uniform/uniform.cpp.base:30-36).
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -82,6 +84,129 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_produce(uint32_t *__restrict__ ri
   }
   if (t == 0) st->hi = target;
 }
+
+// ---- chunked production (see kg_rng.hpp ChunkPlan, kg_mtjump.hip) ----
+// out[m] = XOR_{i: bit i of poly} seq[m + i], m < 624 (256 threads, three
+// outputs each; the bit loop is uniform, the reads consecutive across lanes)
+__device__ inline void mt_combine(const uint32_t *seq, const uint64_t *__restrict__ poly, uint32_t *out) {
+  const int t = threadIdx.x;
+  const int m2 = (t + 512 < MT_N) ? t + 512 : MT_N - 1;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int w = 0; w < MT_POLY_WORDS; w++) {
+    uint64_t bits = poly[w];
+    while (bits) {
+      const int i = w * 64 + __builtin_ctzll(bits);
+      bits &= bits - 1;
+      a0 ^= seq[t + i];
+      a1 ^= seq[t + 256 + i];
+      a2 ^= seq[m2 + i];
+    }
+  }
+  out[t] = a0;
+  out[t + 256] = a1;
+  if (t + 512 < MT_N) out[t + 512] = a2;
+}
+
+// seq[624 .. MT_SEQ) from the window seq[0..624); optionally also stored to
+// the ring at absolute positions base + k - 624 (zero words recorded)
+__device__ inline void mt_fill_seq(uint32_t *seq, uint32_t *ring, unsigned long long R, StreamState *st,
+                                   unsigned long long base) {
+  const int t = threadIdx.x;
+  for (int k0 = MT_N; k0 < MT_SEQ; k0 += 227) {
+    const int k = k0 + t;
+    if (t < 227 && k < MT_SEQ) {
+      const uint32_t v = mt_next(seq[k - 624], seq[k - 623], seq[k - 227]);
+      seq[k] = v;
+      if (ring) {
+        const unsigned long long j = base + (unsigned long long)(k - MT_N);
+        ring[j & (R - 1)] = v;
+        if (v == 0u) {
+          const unsigned int z = atomicAdd(&st->nzero, 1u);
+          if (z < KG_MAX_ZERO_WORDS)
+            st->zeros[z] = j;
+          else
+            atomicOr(&st->errors, KG_ERR_ZERO_LIST);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_mt_plan(StreamState *st, ChunkPlan *plan, unsigned long long ahead, unsigned long long R,
+                          unsigned long long W, unsigned long long K) {
+  if (threadIdx.x != 0) return;
+  unsigned long long target = st->pos + ahead;
+  const unsigned long long cap = st->lo + R, hi = st->hi;
+  if (target > cap) {
+    st->errors |= KG_ERR_RNG_UNDERRUN;
+    target = cap;
+  }
+  unsigned long long n = 0;
+  if (hi < target) {
+    n = (target - hi + W - 1) / W;
+    if (n > K) n = K;
+    while (n > 0 && hi + n * W > cap) n--;
+  }
+  plan->c_first = hi / W;
+  plan->n = n;
+  st->hi = hi + n * W;
+}
+
+__global__ void __launch_bounds__(MT_TPB) k_mt_chunks(uint32_t *__restrict__ ring, unsigned long long R,
+                                                     StreamState *st, const ChunkPlan *__restrict__ plan,
+                                                     uint32_t *__restrict__ seeds, unsigned long long K,
+                                                     unsigned long long W, const uint64_t *__restrict__ jumpPoly) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t msm[];
+  uint32_t *seq = msm, *roll = msm + ((MT_SEQ + 3) & ~3);
+  const ChunkPlan pl = *plan;
+  if (blockIdx.x >= pl.n) return;
+  const int t = threadIdx.x;
+  const unsigned long long c = pl.c_first + blockIdx.x;
+  const uint32_t *src = seeds + (size_t)(c % (2 * K)) * MT_N;
+  for (int i = t; i < MT_N; i += MT_TPB) seq[i] = src[i];
+  __syncthreads();
+  const unsigned long long base = c * W;
+  mt_fill_seq(seq, ring, R, st, base);  // words base .. base + MT_SEQ - 625
+  // rest of the chunk from a rolling 1024-word window
+  const unsigned long long j0 = base + (MT_SEQ - MT_N);
+  for (int i = t; i < MT_N; i += MT_TPB) roll[(j0 - MT_N + i) & 1023] = seq[MT_SEQ - MT_N + i];
+  __syncthreads();
+  for (unsigned long long c0 = j0; c0 < base + W; c0 += 227) {
+    const unsigned long long j = c0 + t;
+    if (t < 227 && j < base + W) {
+      const uint32_t v = mt_next(roll[(j - 624) & 1023], roll[(j - 623) & 1023], roll[(j - 227) & 1023]);
+      roll[j & 1023] = v;
+      ring[j & (R - 1)] = v;
+      if (v == 0u) {
+        const unsigned int z = atomicAdd(&st->nzero, 1u);
+        if (z < KG_MAX_ZERO_WORDS)
+          st->zeros[z] = j;
+        else
+          atomicOr(&st->errors, KG_ERR_ZERO_LIST);
+      }
+    }
+    __syncthreads();
+  }
+  // seed chunk c + K: jump this chunk's start window by K*W words
+  mt_combine(seq, jumpPoly, seeds + (size_t)((c + K) % (2 * K)) * MT_N);
+}
+
+// initial seeds: chunk c0 + k (2^l <= k < 2^(l+1)) from chunk c0 + k - 2^l
+__global__ void __launch_bounds__(MT_TPB) k_mt_jump_level(uint32_t *__restrict__ seeds, unsigned long long K,
+                                                         unsigned long long c0, int l,
+                                                         const uint64_t *__restrict__ poly) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t msm[];
+  const unsigned long long k = (1ULL << l) + blockIdx.x;
+  if (k >= K) return;
+  const uint32_t *src = seeds + (size_t)((c0 + k - (1ULL << l)) % (2 * K)) * MT_N;
+  for (int i = threadIdx.x; i < MT_N; i += MT_TPB) msm[i] = src[i];
+  __syncthreads();
+  mt_fill_seq(msm, nullptr, 0, nullptr, 0);
+  mt_combine(msm, poly, seeds + (size_t)((c0 + k) % (2 * K)) * MT_N);
+}
+
+size_t mt_chunk_lds_bytes() { return (size_t)(((MT_SEQ + 3) & ~3) + 1024) * sizeof(uint32_t); }
 
 __device__ inline bool polar_pair(const uint32_t *__restrict__ ring, unsigned long long R, const PosView &st,
                                   unsigned long long a, double &y, double &r2) {
@@ -265,6 +390,9 @@ unsigned long long next_pow2(unsigned long long x) {
 }  // namespace
 
 MtStream::~MtStream() {
+  if (seeds_) (void)hipFree(seeds_);
+  if (polys_) (void)hipFree(polys_);
+  if (plan_) (void)hipFree(plan_);
   if (side_) {
     (void)hipStreamSynchronize(side_);
     (void)hipStreamDestroy(side_);
@@ -277,7 +405,29 @@ MtStream::~MtStream() {
   if (offsets_) (void)hipFree(offsets_);
 }
 
-int MtStream::init(size_t capacity_words) {
+int MtStream::init(size_t capacity_words, size_t parallel_min) {
+  if (const char *e = getenv("KORALI_AMD_MT_PARALLEL_MIN")) parallel_min = (size_t)strtoull(e, nullptr, 10);
+  par_ = capacity_words >= parallel_min;
+  if (par_) {
+    int lw = 19;
+    if (const char *e = getenv("KORALI_AMD_MT_CHUNK_LOG2")) lw = atoi(e);
+    KG_CHECK(lw >= 15 && lw <= 26, "KORALI_AMD_MT_CHUNK_LOG2 must be in [15, 26]");
+    W_ = 1ULL << lw;
+    K_ = 256;
+    int lk = 0;
+    while ((1 << lk) < K_) lk++;
+    KG_HIP(hipMalloc(&seeds_, 2 * (size_t)K_ * MT_N * sizeof(uint32_t)));
+    KG_HIP(hipMalloc(&plan_, sizeof(ChunkPlan)));
+    KG_HIP(hipMalloc(&polys_, (size_t)(lk + 1) * MT_POLY_WORDS * sizeof(uint64_t)));
+    std::vector<uint64_t> hp((size_t)(lk + 1) * MT_POLY_WORDS);
+    for (int l = 0; l <= lk; l++)
+      if (mt_jump_poly_pow2(lw + l, hp.data() + (size_t)l * MT_POLY_WORDS)) return 1;
+    KG_HIP(hipMemcpy(polys_, hp.data(), hp.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    const int lds = (int)mt_chunk_lds_bytes();
+    KG_HIP(hipFuncSetAttribute((const void *)k_mt_chunks, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    KG_HIP(hipFuncSetAttribute((const void *)k_mt_jump_level, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    capacity_words += W_;  // production rounds up to whole chunks
+  }
   R_ = next_pow2(capacity_words + 2 * MT_N + 4096);
   KG_HIP(hipMalloc(&ring_, R_ * sizeof(uint32_t)));
   KG_HIP(hipMalloc(&st_, sizeof(StreamState)));
@@ -315,11 +465,47 @@ int MtStream::import_gsl(const void *state5000, hipStream_t s) {
     if (w[i] == 0 && h.nzero < KG_MAX_ZERO_WORDS) h.zeros[h.nzero++] = (unsigned long long)i;
   KG_HIP(hipMemcpyAsync(ring_, w.data(), MT_N * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   KG_HIP(hipMemcpyAsync(st_, &h, sizeof(h), hipMemcpyHostToDevice, s));
+  if (par_ && seed_chunks(h.pos, s)) return 1;
   KG_HIP(hipStreamSynchronize(s));
   return 0;
 }
 
+int MtStream::seed_chunks(unsigned long long pos, hipStream_t s) {
+  // serial up to the first chunk boundary W exactly (pos + ahead = W), whose
+  // start window seeds chunk 1; chunks 2..K by log-depth jumps (level l
+  // jumps 2^l W words)
+  hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(MT_TPB), 0, s, ring_, R_, st_, W_ - pos);
+  KG_HIP(hipGetLastError());
+  const int K = K_;
+  KG_HIP(hipMemcpyAsync(seeds_ + (size_t)(1 % (2 * K)) * MT_N, ring_ + ((W_ - MT_N) & (R_ - 1)),
+                        MT_N * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  for (int l = 0; (1 << l) < K; l++) {
+    const int cnt = std::min(1 << l, K - (1 << l));
+    hipLaunchKernelGGL(k_mt_jump_level, dim3(cnt), dim3(MT_TPB), mt_chunk_lds_bytes(), s, seeds_,
+                       (unsigned long long)K, 1ULL, l, (const uint64_t *)(polys_ + (size_t)l * MT_POLY_WORDS));
+    KG_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+int MtStream::produce_chunks(unsigned long long ahead, hipStream_t s) {
+  int lk = 0;
+  while ((1 << lk) < K_) lk++;
+  const unsigned long long per = (unsigned long long)K_ * W_;
+  const unsigned long long launches = (ahead + W_) / per + 1;
+  for (unsigned long long q = 0; q < launches; q++) {
+    hipLaunchKernelGGL(k_mt_plan, dim3(1), dim3(1), 0, s, st_, plan_, ahead, R_, W_, (unsigned long long)K_);
+    KG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_mt_chunks, dim3(K_), dim3(MT_TPB), mt_chunk_lds_bytes(), s, ring_, R_, st_,
+                       (const ChunkPlan *)plan_, seeds_, (unsigned long long)K_, W_,
+                       (const uint64_t *)(polys_ + (size_t)lk * MT_POLY_WORDS));
+    KG_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
 int MtStream::produce(unsigned long long ahead, hipStream_t s) {
+  if (par_) return produce_chunks(ahead, s);
   hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(MT_TPB), 0, s, ring_, R_, st_, ahead);
   KG_HIP(hipGetLastError());
   return 0;

@@ -24,6 +24,23 @@ namespace kg {
 
 constexpr int KG_MAX_ZERO_WORDS = 64;
 
+// jump-ahead (kg_mtjump.hip): characteristic polynomial degree and the
+// 64-bit words of a polynomial of degree < MT_L
+constexpr int MT_L = 19937;
+constexpr int MT_POLY_WORDS = (MT_L + 64) / 64;  // 312
+constexpr int MT_SEQ = MT_N + MT_L - 1;          // words a jump reads (20560)
+int mt_poly_degree();
+int mt_jump_poly_pow2(int e, uint64_t *out);     // x^(2^e) mod P
+int mt_jump_host(const uint32_t *window, unsigned long long J, uint32_t *out);
+
+// chunked parallel production: chunk c = words [cW, (c+1)W) of the stream
+// (positions relative to the import point), made by its own workgroup from
+// a start window seeds[c mod 2K]; producing chunk c also jumps its window
+// K*W words ahead to seed chunk c+K.
+struct ChunkPlan {
+  unsigned long long c_first, n;
+};
+
 struct StreamState {
   unsigned long long lo;   // absolute index of the current GSL block start (624*b)
   unsigned long long pos;  // next unconsumed absolute index
@@ -39,8 +56,12 @@ class MtStream {
  public:
   MtStream() = default;
   ~MtStream();
-  // capacity: words the ring must hold beyond the current block
-  int init(size_t capacity_words);
+  // capacity: words the ring must hold beyond the current block.  Streams
+  // whose demand reaches `parallel_min` words use the chunked multi-
+  // workgroup producer (env KORALI_AMD_MT_PARALLEL_MIN / KORALI_AMD_MT_CHUNK_LOG2
+  // override the threshold and chunk size for tests).
+  int init(size_t capacity_words, size_t parallel_min = 8u << 20);
+  bool parallel() const { return par_; }
   int import_gsl(const void *state5000, hipStream_t s);
   int export_gsl(void *state5000, hipStream_t s);
   // make sure words [pos, pos + ahead) exist (device-side target)
@@ -83,6 +104,15 @@ class MtStream {
   hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
   bool prefetch_pending_ = false;
   int ensure_scratch(size_t nblocks);
+  // chunked producer state
+  bool par_ = false;
+  unsigned long long W_ = 0;  // chunk words (power of two, >= MT_SEQ)
+  int K_ = 0;                 // chunks per launch / seed lead
+  uint32_t *seeds_ = nullptr; // [2K][624]
+  uint64_t *polys_ = nullptr; // x^(2^l W) mod P, l = 0..log2 K
+  ChunkPlan *plan_ = nullptr;
+  int seed_chunks(unsigned long long pos, hipStream_t s);
+  int produce_chunks(unsigned long long ahead, hipStream_t s);
 };
 
 }  // namespace kg

@@ -61,7 +61,7 @@ EXPORTED = [
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
     "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
-    "kg_tmcmc_profile", "kg_tmcmc_profile_read",
+    "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump",
 ]
 
 

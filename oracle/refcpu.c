@@ -186,6 +186,57 @@ double kr_pow_cr(double x, double y)
   }
 }
 
+/* Correctly-rounded cos for the Ackley objective (model.py:37-62 calls
+ * np.cos; the platform libm / SIMD cos is not correctly rounded, so both
+ * the oracle and the device pin the CR value).  Cody-Waite reduction by a
+ * triple-double pi/2 with exact products, then the Taylor series of cos or
+ * sin of r (|r| <= pi/4) in double-double, rounded once.  Same operation
+ * sequence as korali_amd/csrc/kg_common.hpp cos_cr. */
+static const double KR_CH[15] = {0x1p+0, -0x1p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+  -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+  -0x1.6827863b97d97p-53, 0x1.e542ba4020225p-62, -0x1.0ce396db7f853p-70, 0x1.f2cf01972f578p-80,
+  -0x1.88e85fc6a4e5ap-89, 0x1.0a18a2635085dp-98};
+static const double KR_CL[15] = {0.0, 0.0, 0x1.5555555555555p-59, 0x1.f49f49f49f49fp-65, 0x1.a01a01a01a01ap-76,
+  -0x1.cbbc05b4fa99ap-76, -0x1.2aec959e14c06p-83, -0x1.05d6f8a2efd1fp-92, 0x1.1d8656b0ee8cbp-101,
+  -0x1.eec01221a8b0bp-107, 0x1.ea72b4afe3c2fp-120, 0x1.aebcdbd20331cp-124, -0x1.9ada5fcc1ab14p-135,
+  0x1.71c37ebd16540p-143, 0x1.b9e2e28e1aa54p-153};
+static const double KR_SH[15] = {0x1p+0, -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+  0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41,
+  0x1.952c77030ad4ap-49, -0x1.2f49b46814157p-57, 0x1.71b8ef6dcf572p-66, -0x1.761b41316381ap-75,
+  0x1.3f3ccdd165fa9p-84, -0x1.d1ab1c2dccea3p-94, 0x1.259f98b4358adp-103};
+static const double KR_SL[15] = {0.0, -0x1.5555555555555p-57, 0x1.1111111111111p-63, -0x1.a01a01a01a01ap-73,
+  -0x1.c154f8ddc6c00p-73, 0x1.c062e06d1f209p-80, 0x1.f28e0cc748ebep-87, -0x1.1d8656b0ee8cbp-97,
+  0x1.ac981465ddc6cp-103, -0x1.2650f61dbdcb4p-112, -0x1.d043ae40c4647p-120, 0x1.3423c7d91404fp-130,
+  -0x1.58ddadf344487p-139, -0x1.054d0c78aea14p-149, 0x1.eaf8c39dd9bc5p-157};
+
+double kr_cos_cr(double x)
+{
+#ifdef KR_LIBM_TIMING
+  return cos(x);
+#endif
+  const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
+  const double INV_PIO2 = 0x1.45f306dc9c883p-1;
+  double kd, v;
+  dd_t t1, t2, r, z, p;
+  int q, odd, j;
+  if (!(fabs(x) < 1073741824.0)) return cos(x);
+  kd = floor(x * INV_PIO2 + 0.5);
+  t1 = dd_two_prod(kd, P1);
+  t2 = dd_two_prod(kd, P2);
+  r = dd_add(dd_from(x), (dd_t){-t1.hi, -t1.lo});
+  r = dd_add(r, (dd_t){-t2.hi, -t2.lo});
+  r = dd_add(r, (dd_t){-(kd * P3), 0.0});
+  q = (int)((long long)kd & 3);
+  odd = q & 1;
+  z = dd_mul(r, r);
+  p = odd ? (dd_t){KR_SH[14], KR_SL[14]} : (dd_t){KR_CH[14], KR_CL[14]};
+  for (j = 13; j >= 0; j--)
+    p = dd_add(dd_mul(p, z), odd ? (dd_t){KR_SH[j], KR_SL[j]} : (dd_t){KR_CH[j], KR_CL[j]});
+  p = dd_mul(p, odd ? r : dd_from(1.0));
+  v = p.hi + p.lo;
+  return (q == 1 || q == 2) ? -v : v;
+}
+
 /* ======================================================================
  * mt19937, GSL semantics (rng/mt.c, 2002 seeding)
  * Korali: distribution.cpp.base:32-62 (gsl_rng_alloc(gsl_rng_default))
@@ -976,7 +1027,7 @@ double kr_obj_negative_ackley(const double *x, size_t n)
   for (i = 0; i < n; i++)
   {
     sum1 += x[i] * x[i];
-    sum2 += cos(c * x[i]);
+    sum2 += kr_cos_cr(c * x[i]);
   }
   sum1 /= (double)n;
   sum2 /= (double)n;

@@ -59,6 +59,9 @@ double kr_stats_mean(const double *x, size_t n);
 double kr_stats_sd_m(const double *x, size_t n, double mean);
 
 /* ---------------- objectives (examples/optimization/stochastic/_model) -- */
+/* correctly-rounded cos / exp (double-double, one rounding) */
+double kr_cos_cr(double x);
+double kr_exp_cr(double x);
 double kr_obj_negative_rosenbrock(const double *x, size_t n);
 double kr_obj_negative_ackley(const double *x, size_t n);
 double kr_obj_negative_sphere(const double *x, size_t n); /* -0.5*sum x^2 */

@@ -28,6 +28,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     profc3) step profc3 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c3" -o run --output-format csv -- python bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    c4) step c4 600 python tools/probe_c4.py ${C4_ARGS:-512 65536 3} ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac
 done

@@ -105,21 +105,20 @@ def oracle_and_device(Nv, lam, objective, gens, cov_mode="exact", seed=1337, x0=
                                                          (32, 256, "ackley", 8, "host"),
                                                          (128, 4096, "rosenbrock", 3, "host"),
                                                          (128, 4096, "rosenbrock", 2, "device"),
-                                                         (200, 512, "rosenbrock", 2, "host")])
+                                                         (200, 512, "rosenbrock", 2, "host"),
+                                                         (512, 1024, "rosenbrock", 2, "host")])
 def test_seeded_run_matches_oracle_bit_exact(Nv, lam, objective, gens, chase):
-    """N=200 exercises the global-memory (non-LDS) eigensolver variant."""
+    """N=200 and N=512 exercise the multi-workgroup eigensolver variant
+    (rows / columns spread over workgroups, in-launch hand-offs)."""
     o, dev = oracle_and_device(Nv, lam, objective, gens, eigen_chase=chase)
     for g in range(1, gens + 1):
         o.generation(g, objective)
         dev.generation(g, objective)
         dev.synchronize()
         assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
-        if objective == "ackley":
-            # cos: OCML on the device vs glibc in the oracle (the reference's
-            # Python objective calls the platform libm) — 1e-15 relative
-            np.testing.assert_allclose(dev["Value Vector"], o["Value Vector"], rtol=1e-15, atol=0)
-        else:
-            assert np.array_equal(dev["Value Vector"], o["Value Vector"]), g
+        # Ackley: correctly-rounded cos on both sides (kg_common.hpp cos_cr,
+        # refcpu.c kr_cos_cr), so every objective value is bit-exact too
+        assert np.array_equal(dev["Value Vector"], o["Value Vector"]), g
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
         for key in ("Current Mean", "Covariance Matrix", "Covariance Eigenvector Matrix", "Axis Lengths"):
             assert np.array_equal(dev[key], o[key]), (g, key)
@@ -162,3 +161,22 @@ def test_large_population_sort_matches_numpy():
     dev.synchronize()
     ref = np.lexsort((np.arange(lam), -F))
     assert np.array_equal(dev.sorting_index(), ref)
+
+
+@pytest.mark.parametrize("log2w", [15, 17])
+def test_chunked_mt_producer_bit_exact(monkeypatch, log2w):
+    """The multi-workgroup mt19937 producer (chunks of 2^log2w words seeded
+    by GF(2) jumps, kg_mtjump.hip) forced on a C2-sized stream: populations,
+    selection, update and the exported generator state stay bit-exact."""
+    monkeypatch.setenv("KORALI_AMD_MT_PARALLEL_MIN", "0")
+    monkeypatch.setenv("KORALI_AMD_MT_CHUNK_LOG2", str(log2w))
+    o, dev = oracle_and_device(128, 4096, "rosenbrock", 3)
+    for g in (1, 2, 3):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        assert np.array_equal(dev["Current Mean"], o["Current Mean"]), g
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+    assert dev.get_rng(1) == o.rng(1).get_bytes()

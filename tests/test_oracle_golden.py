@@ -216,3 +216,36 @@ def test_multinomial_conserves_total():
     w /= w.sum()
     n = R.multinomial(r, w, 8192)
     assert int(n.sum()) == 8192
+
+
+def _decimal_cos(x):
+    """cos(x) to ~70 digits (decimal Taylor after reduction by a 110-digit
+    pi/2): the exact value the correctly-rounded cos must round."""
+    from decimal import Decimal as D, localcontext
+    with localcontext() as ctx:
+        ctx.prec = 80
+        pi = D("3.14159265358979323846264338327950288419716939937510582097494459230781640628620899862803482534211706798")
+        xd = D(x)
+        k = (xd / (pi / 2)).to_integral_value()
+        r = xd - k * (pi / 2)
+        q = int(k) % 4
+        odd = q % 2 == 1
+        s, t, n = D(0), (r if odd else D(1)), (1 if odd else 0)
+        while abs(t) > D(10) ** -75:
+            s += t
+            t = -t * r * r / ((n + 1) * (n + 2))
+            n += 2
+        return float(-s if q in (1, 2) else s)
+
+
+def test_cos_is_correctly_rounded():
+    """kr_cos_cr (the Ackley objective's cos; the device runs the same
+    sequence) equals the correctly rounded cos, including arguments next
+    to multiples of pi/2 that 2*pi*x produces for x on a quarter grid."""
+    import ctypes
+    f = R.lib().kr_cos_cr
+    f.restype, f.argtypes = ctypes.c_double, [ctypes.c_double]
+    rng = np.random.default_rng(11)
+    xs = list(rng.uniform(-80, 80, 400)) + list(2 * np.pi * np.arange(-40, 41) / 4) + [0.0, 1e-300, -3e-9]
+    for x in xs:
+        assert f(float(x)) == _decimal_cos(float(x)), x
