@@ -154,11 +154,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cov", default="mfma", choices=["exact", "mfma"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3"],
-                    help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192 (parity/perf case)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+                    help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192; c4: CMA-ES 512-dim Ackley, "
+                         "lambda=65536, population sharded over the ranks")
     args = ap.parse_args()
     if args.workload == "c3":
         return run_c3(args)
+    if args.workload == "c4":
+        return run_c4(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -387,6 +390,88 @@ def run_c3(args):
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = c3_cpu_baseline()
     print(json.dumps(out), flush=True)
+
+
+# ----------------------------------------------------------------- C4 sharded
+C4_N, C4_L = 512, 65536
+
+
+def run_c4(args):
+    """BASELINE.json configs[3]: CMA-ES, 512-dim negative Ackley
+    (model.py:37-62), λ = 65536, μ = 32768, x0 = 2, σ0 = 1, seed 1337.  With
+    N > 1 ranks the population is sharded (korali_amd/sharded.py: RCCL
+    all-gather of fitnesses, sum all-reduce of the mean / rank-μ partials);
+    total work is fixed, so scaling is strong."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    kw = dict(initial_value=np.full(C4_N, 2.0), initial_std=np.ones(C4_N), normal_seed=1337, uniform_seed=1338)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        from korali_amd.sharded import ShardedCmaes
+        solver = ShardedCmaes(C4_N, C4_L, dist, device=local_rank, transport="device", **kw)
+        dev = solver.dev
+    else:
+        from korali_amd.native import CmaesDevice
+        dev = CmaesDevice(C4_N, C4_L, cov_mode="mfma", **kw)
+        solver = dev
+
+    def step(g):
+        solver.generation(g, "ackley")
+
+    gen = 0
+    for _ in range(args.warmup):
+        gen += 1
+        step(gen)
+    dev.synchronize()
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        gen += 1
+        step(gen)
+    dev.synchronize()
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dev.profile(True)
+    STAGES = ("eigen", "eigen_tridiag", "eigen_unpack", "eigen_chase_host", "eigen_apply", "rng_polar", "transform",
+              "objective", "sort", "mean_paths", "covariance", "sigma")
+    for st in ("init",) + STAGES:
+        dev.profile_read(st)
+    for _ in range(2):
+        gen += 1
+        step(gen)
+    dev.synchronize()
+    stages = {}
+    for st in STAGES:
+        ms, n = dev.profile_read(st)
+        if n:
+            stages[st] = ms / n
+    dev.profile(False)
+    best = float(dev["Best Ever Value"][0])
+    if rank == 0:
+        print(json.dumps({
+            "metric": "CMA-ES generations/sec, 512-dim Ackley lambda=65536 (C4)", "value": args.steps / elapsed,
+            "unit": "generations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768 Logarithmic, x0=2, "
+                                   "sigma0=1, seed 1337", "parallelism": f"population-shard{world}"},
+            "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
+            "stage_ms_rank0": stages, "cpu_baseline": None}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

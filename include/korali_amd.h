@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 1
+#define KG_ABI_VERSION 2
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -85,6 +85,8 @@ typedef struct {
   int eigen_device_chase;                 /* 0: implicit-QR Givens recurrence on the calling host
                                              core, overlapped with the device unpack (default);
                                              1: on one device lane.  Identical results. */
+  int shard_rank;                         /* population sharding: this rank's index */
+  int shard_count;                        /* ranks sharing one population; 0 or 1 = unsharded */
 } kg_cmaes_cfg;
 
 int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);
@@ -97,6 +99,16 @@ int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F);
 int kg_cmaes_update(kg_cmaes_t h, size_t generation);
 /* one whole generation, enqueued asynchronously (no host sync) */
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective);
+/* Population sharding over shard_count ranks (one handle per rank, state
+ * replicated, λ % shard_count == 0, unbounded variables).  kg_cmaes_sample
+ * and kg_cmaes_eval_builtin then cover only rows [rank λ/S, (rank+1) λ/S);
+ * the caller all-gathers "Value Vector" (λ doubles, shards in rank order),
+ * runs kg_cmaes_update_partial, sum-all-reduces "Shard Partials" and
+ * finishes with kg_cmaes_update_finalize.  Every rank then holds the same
+ * state; mean and rank-μ sums are added per shard (within 1e-12 of the
+ * sequential order), the sort and selection are replicated bit-exactly. */
+int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation);
+int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation);
 int kg_cmaes_synchronize(kg_cmaes_t h); /* waits and reports device-side errors */
 /* named state fields, keys as in the reference's solver JSON
  * ("Sigma", "Covariance Matrix", "Current Mean", ...); sizes in doubles */

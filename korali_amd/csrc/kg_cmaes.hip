@@ -32,7 +32,7 @@ struct CmaesScalars {
   double currentMinStd, currentMaxStd, maxDiagC, minDiagC, minEig, maxEig;
   double infeasibleSampleCount, bestValidSample, modelEvaluationCount, hsig, eigenFailures;
   double ccov1, ccovmu;
-  unsigned int errors, pad;
+  unsigned int errors, bestFlag;  // bestFlag: best-ever improved this generation
 };
 
 // ----------------------------------------------------------------- init
@@ -424,6 +424,7 @@ __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, 
     sc->previousBestValue = sc->currentBestValue;
     sc->currentBestValue = F[i0];
     flag = (sc->currentBestValue > sc->bestEverValue || gen == 1) ? 1 : 0;
+    sc->bestFlag = (unsigned)flag;
     if (flag) {
       sc->previousBestEverValue = sc->bestEverValue;
       sc->bestEverValue = sc->currentBestValue;
@@ -439,6 +440,7 @@ __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, 
     }
   }
   __syncthreads();
+  if (!X) return;  // population shards: the best row arrives through the partials
   for (int d = tid; d < N; d += blockDim.x) {
     const double v = X[(size_t)i0 * N + d];
     currBestVars[d] = v;
@@ -649,7 +651,7 @@ __global__ void __launch_bounds__(64) k_rankmu_mfma(int N, int mu, int kslices, 
 __global__ void __launch_bounds__(256) k_adaptC_combine(int N, int kslices, int ntiles, int diagonal,
                                                         const double *__restrict__ part,
                                                         const double *__restrict__ pc, double *C,
-                                                        const CmaesScalars *__restrict__ sc) {
+                                                        const CmaesScalars *__restrict__ sc, int scaleByCcovmu) {
   int td, te;
   tri_tile(blockIdx.x, td, te);
   const int tid = threadIdx.x, ty = tid / 16, tx = tid % 16;
@@ -661,9 +663,133 @@ __global__ void __launch_bounds__(256) k_adaptC_combine(int N, int kslices, int 
   double c = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
   double s = 0.0;
   for (int sl = 0; sl < kslices; sl++) s += part[((size_t)sl * ntiles + blockIdx.x) * 256 + ty * 16 + tx];
-  c += s;
+  c += scaleByCcovmu ? ccovmu * s : s;
   C[(size_t)d * N + e] = c;
   if (e < d) C[(size_t)e * N + d] = c;
+}
+
+// ------------------------------------------------------ population shards
+// ranks own rows [r0, r1) of the population.  After the
+// fitness all-gather every rank sorts the whole vector (identical index);
+// each then sums mean and rank-μ terms over the selected rows it owns, the
+// caller sum-all-reduces the partials, and every rank finishes the update.
+
+// selected positions k < mu with idx[k] in [r0, r1), ascending k
+__global__ void __launch_bounds__(1024) k_shard_select(int mu, int r0, int r1, const unsigned *__restrict__ idx,
+                                                       int *__restrict__ kidx, int *__restrict__ cnt) {
+  __shared__ int wtot[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int base = 0; base < mu; base += 1024) {
+    const int k = base + threadIdx.x;
+    const int own = (k < mu && (int)idx[k] >= r0 && (int)idx[k] < r1) ? 1 : 0;
+    const unsigned long long bal = __ballot(own);
+    const int before = __popcll(bal & ((1ULL << lane) - 1ULL));
+    if (lane == 0) wtot[wid] = __popcll(bal);
+    __syncthreads();
+    int woff = carry;
+    for (int q = 0; q < wid; q++) woff += wtot[q];
+    if (own) kidx[woff + before] = k;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int q = 0; q < 16; q++) carry += wtot[q];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *cnt = carry;
+}
+
+__global__ void __launch_bounds__(128) k_gather_owned(int N, const double *__restrict__ X,
+                                                      const unsigned *__restrict__ idx, const int *__restrict__ kidx,
+                                                      const int *__restrict__ cnt, double *__restrict__ Y) {
+  const int j = blockIdx.x;
+  if (j >= *cnt) return;
+  const size_t src = (size_t)idx[kidx[j]] * N;
+  for (int d = threadIdx.x; d < N; d += blockDim.x) Y[(size_t)j * N + d] = X[src + d];
+}
+
+// part[d] = sum_j w[kidx[j]] Y[j][d] (ascending k); part[N + d] = best row
+// if this rank owns it, else 0
+__global__ void __launch_bounds__(64) k_shard_mean(int N, int r0, int r1, const int *__restrict__ cntp,
+                                                   const double *__restrict__ Y, const double *__restrict__ w,
+                                                   const int *__restrict__ kidx, const double *__restrict__ X,
+                                                   const unsigned *__restrict__ idx, double *__restrict__ part) {
+  const int d = blockIdx.x * 64 + threadIdx.x;
+  if (d >= N) return;
+  const int cnt = *cntp;
+  double acc = 0.;
+  int j = 0;
+  for (; j + 16 <= cnt; j += 16) {
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) v[q] = w[kidx[j + q]] * Y[(size_t)(j + q) * N + d];
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc += v[q];
+  }
+  for (; j < cnt; j++) acc += w[kidx[j]] * Y[(size_t)j * N + d];
+  part[d] = acc;
+  const int i0 = (int)idx[0];
+  part[N + d] = (i0 >= r0 && i0 < r1) ? X[(size_t)i0 * N + d] : 0.0;
+}
+
+// rank-μ partial on the matrix cores: as k_rankmu_mfma over the owned
+// selected rows, weights w_k / σ² (cμ is applied after the reduction)
+__global__ void __launch_bounds__(64) k_rankmu_mfma_shard(int N, const int *__restrict__ cntp, int kslices,
+                                                          const double *__restrict__ Y, const int *__restrict__ kidx,
+                                                          const double *__restrict__ w,
+                                                          const double *__restrict__ prevMean,
+                                                          const CmaesScalars *__restrict__ sc,
+                                                          double *__restrict__ part) {
+  int td, te;
+  tri_tile(blockIdx.x, td, te);
+  const int slice = blockIdx.y;
+  const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
+  const int d = td * 16 + li, e = te * 16 + li;
+  const double pmd = d < N ? prevMean[d] : 0.0, pme = e < N ? prevMean[e] : 0.0;
+  const double scale = 1.0 / (sc->sigma * sc->sigma);
+  const int cnt = *cntp;
+  const int per = ((cnt + kslices - 1) / kslices + 3) & ~3;
+  const int kbeg = slice * per, kend = (kbeg + per) < cnt ? (kbeg + per) : cnt;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = kbeg; k0 < kend; k0 += 4) {
+    const int k = k0 + lk;
+    double a = 0.0, b = 0.0;
+    if (k < kend) {
+      const size_t row = (size_t)k * N;
+      const double sk = scale * w[kidx[k]];
+      if (d < N) a = sk * (Y[row + d] - pmd);
+      if (e < N) b = Y[row + e] - pme;
+    }
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  const size_t tiles = gridDim.x;
+  double *out = part + ((size_t)slice * tiles + blockIdx.x) * 256;
+#pragma unroll
+  for (int r = 0; r < 4; r++) out[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+}
+
+__global__ void __launch_bounds__(256) k_part_reduce(int kslices, int ntiles, const double *__restrict__ slices,
+                                                     double *__restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+  for (int sl = 0; sl < kslices; sl++) s += slices[(size_t)sl * ntiles * 256 + t];
+  out[t] = s;
+}
+
+// after the all-reduce: mean (:603-609, :623-624) and best variables
+__global__ void __launch_bounds__(256) k_shard_finalize(int N, const double *__restrict__ part, double *mean,
+                                                        double *prevMean, double *meanUpdate, double *currBestVars,
+                                                        double *bestEverVars, const CmaesScalars *__restrict__ sc) {
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= N) return;
+  const double acc = part[d], prev = mean[d];
+  prevMean[d] = prev;
+  mean[d] = acc;
+  meanUpdate[d] = (acc - prev) / sc->sigma;
+  const double v = part[N + d];
+  currBestVars[d] = v;
+  if (sc->bestFlag) bestEverVars[d] = v;
 }
 
 // adaptC diag extrema :709-717, updateSigma :720-761, numericalErrorTreatment
@@ -767,6 +893,10 @@ struct kg_cmaes_s {
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
   int kslices = 8;
+  // population shards
+  int shards = 1, shardRank = 0, r0 = 0, r1 = 0;
+  int *kidx = nullptr, *shardCnt = nullptr;
+  double *part = nullptr;  // "Shard Partials": mean (N), best row (N), rank-mu tiles
   unsigned long long *eigTrace = nullptr;  // KORALI_AMD_TRACE_EIGEN: s_memtime per phase
   MtStream normal, uniform;
   // profiling
@@ -895,6 +1025,10 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
   VEC("Initial Standard Deviation", h->istd, N)
   VEC("Minimum Standard Deviation Update", h->minstd, N)
   if (h->BDZ) VEC("BDZ Matrix", h->BDZ, L * N)
+  if (h->part) {
+    const size_t nt = (N + 15) / 16;
+    VEC("Shard Partials", h->part, 2 * N + nt * (nt + 1) / 2 * 256)
+  }
 #define SCA(key, fld) VEC(key, &h->sc->fld, 1)
   SCA("Sigma", sigma)
   SCA("Trace", trace)
@@ -974,6 +1108,17 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     }
   }
   h->R = h->finiteBounds ? std::max(64, L / 4) : 0;
+  h->shards = cfg->shard_count > 1 ? cfg->shard_count : 1;
+  h->shardRank = h->shards > 1 ? cfg->shard_rank : 0;
+  if (h->shards > 1 && (L % h->shards != 0 || h->finiteBounds || cfg->shard_rank < 0 ||
+                        cfg->shard_rank >= h->shards || cfg->diagonal_covariance)) {
+    set_error("population sharding needs Population Size divisible by the shard count, unbounded variables, "
+              "a full covariance and 0 <= shard_rank < shard_count");
+    delete h;
+    return 1;
+  }
+  h->r0 = h->shardRank * (L / h->shards);
+  h->r1 = h->r0 + L / h->shards;
   const size_t rows = (size_t)L + h->R;
   int rc = 0;
   rc |= dalloc(&h->mean, N) | dalloc(&h->prevMean, N) | dalloc(&h->C, (size_t)N * N) | dalloc(&h->B, (size_t)N * N);
@@ -995,6 +1140,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->sortKey, P2) | dalloc(&h->sortVal, P2);
   const int nt = (N + 15) / 16;
   rc |= dalloc(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
+  rc |= dalloc(&h->kidx, h->mu) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
   if (rc) {
     delete h;
     return 1;
@@ -1053,7 +1199,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
                   (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y,
-                  (void *)h->eigTrace})
+                  (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -1088,16 +1234,22 @@ int kg_cmaes_sample(kg_cmaes_t h) {
   if (cmaes_eigen(h)) return 1;
   {
     Stage st(h, "rng_polar");
-    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->stream)) return 1;
+    const bool shard = h->shards > 1;
+    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->stream, shard ? (size_t)h->r0 * N : 0,
+                                shard ? (size_t)h->r1 * N : (size_t)-1))
+      return 1;
   }
   {
     Stage st(h, "transform");
     if (h->R) KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
     const int nbn = (N + TR_BN - 1) / TR_BN;
-    const int nbm = (int)((rows + TR_BM - 1) / TR_BM);
-    hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)rows,
-                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub,
-                       h->R ? h->Xall : h->X, h->R ? h->BDZall : h->BDZ, h->infeas, h->R ? 0 : 1);
+    const size_t trows = h->R ? rows : (size_t)(h->r1 - h->r0);  // a shard transforms its own rows only
+    const int nbm = (int)((trows + TR_BM - 1) / TR_BM);
+    double *xo = h->R ? h->Xall : h->X + (size_t)h->r0 * N;
+    double *bo = h->R ? h->BDZall : (h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr);
+    hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)trows,
+                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
+                       h->infeas, h->R ? 0 : 1);
     KG_HIP(hipGetLastError());
     if (h->R) {
       hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
@@ -1118,8 +1270,9 @@ int kg_cmaes_sample(kg_cmaes_t h) {
 int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective) {
   KG_CHECK(objective >= 0 && objective <= 2, "unknown builtin objective");
   Stage st(h, "objective");
-  hipLaunchKernelGGL(k_objective, dim3((h->lam + 63) / 64), dim3(64), 0, h->stream, h->N, h->lam, objective, h->X,
-                     h->F, h->sc);
+  const int rows = h->r1 - h->r0;
+  hipLaunchKernelGGL(k_objective, dim3((rows + 63) / 64), dim3(64), 0, h->stream, h->N, rows, objective,
+                     h->X + (size_t)h->r0 * h->N, h->F + h->r0, h->sc);
   hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
   KG_HIP(hipGetLastError());
   return 0;
@@ -1143,8 +1296,8 @@ int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F) {
   return 0;
 }
 
-int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
-  const int N = h->N, L = h->lam, mu = h->mu;
+static int cmaes_sort(kg_cmaes_t h) {
+  const int L = h->lam;
   {
     Stage st(h, "sort");
     int P2 = 1;
@@ -1167,34 +1320,11 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
   }
-  {
-    Stage st(h, "mean_paths");
-    hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
-                       (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
-                       h->sc);
-    hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y);
-    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->Y, h->w, h->mean,
-                       h->prevMean, h->meanUpdate, h->sc);
-    const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
-    hipLaunchKernelGGL(k_paths, dim3(1), dim3(N <= 1024 ? ((N + 63) / 64) * 64 : 1024), pbytes, h->stream, N,
-                       h->cfg.diagonal_covariance, (unsigned long long)generation, h->B, h->D, h->meanUpdate,
-                       h->auxBDZ, h->ps, h->pc, h->sc);
-    KG_HIP(hipGetLastError());
-  }
-  {
-    Stage st(h, "covariance");
-    const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
-    if (h->cfg.cov_mode == KG_COV_MFMA) {
-      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->Y,
-                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
-      hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
-                         h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc);
-    } else {
-      hipLaunchKernelGGL(k_adaptC_exact, dim3(ntiles), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
-                         h->Y, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
-    }
-    KG_HIP(hipGetLastError());
-  }
+  return 0;
+}
+
+static int cmaes_sigma(kg_cmaes_t h) {
+  const int N = h->N, mu = h->mu;
   {
     Stage st(h, "sigma");
     hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
@@ -1204,7 +1334,96 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
   return 0;
 }
 
+static int cmaes_paths(kg_cmaes_t h, size_t generation) {
+  const int N = h->N;
+  const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
+  hipLaunchKernelGGL(k_paths, dim3(1), dim3(N <= 1024 ? ((N + 63) / 64) * 64 : 1024), pbytes, h->stream, N,
+                     h->cfg.diagonal_covariance, (unsigned long long)generation, h->B, h->D, h->meanUpdate,
+                     h->auxBDZ, h->ps, h->pc, h->sc);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
+  KG_CHECK(h->shards == 1, "a population-sharded handle updates through kg_cmaes_update_partial / _finalize");
+  const int N = h->N, mu = h->mu;
+  if (cmaes_sort(h)) return 1;
+  {
+    Stage st(h, "mean_paths");
+    hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
+                       (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
+                       h->sc);
+    hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y);
+    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->Y, h->w, h->mean,
+                       h->prevMean, h->meanUpdate, h->sc);
+    if (cmaes_paths(h, generation)) return 1;
+  }
+  {
+    Stage st(h, "covariance");
+    const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
+    if (h->cfg.cov_mode == KG_COV_MFMA) {
+      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->Y,
+                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
+      hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
+                         h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
+    } else {
+      hipLaunchKernelGGL(k_adaptC_exact, dim3(ntiles), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
+                         h->Y, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
+    }
+    KG_HIP(hipGetLastError());
+  }
+  if (cmaes_sigma(h)) return 1;
+  return 0;
+}
+
+int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
+  const int N = h->N, mu = h->mu;
+  if (cmaes_sort(h)) return 1;
+  {
+    Stage st(h, "mean_paths");
+    hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
+                       (unsigned long long)generation, (const double *)nullptr, h->F, h->idx, h->w, h->currBestVars,
+                       h->bestEverVars, h->sc);
+    hipLaunchKernelGGL(k_shard_select, dim3(1), dim3(1024), 0, h->stream, mu, h->r0, h->r1, h->idx, h->kidx,
+                       h->shardCnt);
+    hipLaunchKernelGGL(k_gather_owned, dim3(mu), dim3(128), 0, h->stream, N, h->X, h->idx, h->kidx, h->shardCnt, h->Y);
+    hipLaunchKernelGGL(k_shard_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, h->r0, h->r1, h->shardCnt, h->Y,
+                       h->w, h->kidx, h->X, h->idx, h->part);
+    KG_HIP(hipGetLastError());
+  }
+  {
+    Stage st(h, "covariance");
+    const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
+    hipLaunchKernelGGL(k_rankmu_mfma_shard, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, h->shardCnt,
+                       h->kslices, h->Y, h->kidx, h->w, h->mean, h->sc, h->covPart);  // mean not yet advanced
+    hipLaunchKernelGGL(k_part_reduce, dim3(ntiles), dim3(256), 0, h->stream, h->kslices, ntiles, h->covPart,
+                       h->part + 2 * (size_t)N);
+    KG_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
+  const int N = h->N;
+  {
+    Stage st(h, "mean_paths");
+    hipLaunchKernelGGL(k_shard_finalize, dim3((N + 255) / 256), dim3(256), 0, h->stream, N, h->part, h->mean,
+                       h->prevMean, h->meanUpdate, h->currBestVars, h->bestEverVars, h->sc);
+    KG_HIP(hipGetLastError());
+    if (cmaes_paths(h, generation)) return 1;
+  }
+  {
+    Stage st(h, "covariance");
+    const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
+    hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, 1, ntiles,
+                       h->cfg.diagonal_covariance, h->part + 2 * (size_t)N, h->pc, h->C, h->sc, 1);
+    KG_HIP(hipGetLastError());
+  }
+  return cmaes_sigma(h);
+}
+
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
+  KG_CHECK(h->shards == 1, "a population-sharded generation needs the caller's collectives between its stages");
   if (generation == 1 && kg_cmaes_initialize(h)) return 1;
   if (kg_cmaes_sample(h)) return 1;
   if (kg_cmaes_eval_builtin(h, objective)) return 1;

@@ -288,7 +288,8 @@ __global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__r
                                                             const unsigned long long *__restrict__ offsets,
                                                             double *__restrict__ z, unsigned long long M,
                                                             unsigned long long block_len,
-                                                            unsigned long long *__restrict__ block_end) {
+                                                            unsigned long long *__restrict__ block_end,
+                                                            unsigned long long k_lo, unsigned long long k_hi) {
   __shared__ unsigned int woff[POLAR_TPB / 64];
   const PosView st = pos_view(stp);
   const unsigned long long base = (unsigned long long)blockIdx.x * POLAR_APB + threadIdx.x * POLAR_APT;
@@ -326,9 +327,12 @@ __global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__r
     if (mask & (1u << q)) {
       if (k < M) {
         // gsl_ran_gaussian: sigma * y * sqrt(-2 log(r2) / r2); Normal adds mean 0
-        const double r2 = rv[q];
-        const double g = 1.0 * yv[q] * sqrt(-2.0 * log_cr(r2) / r2);
-        z[k] = 0.0 + g;
+        // (only normals k in [k_lo, k_hi) are materialised: a population shard)
+        if (k >= k_lo && k < k_hi) {
+          const double r2 = rv[q];
+          const double g = 1.0 * yv[q] * sqrt(-2.0 * log_cr(r2) / r2);
+          z[k - k_lo] = 0.0 + g;
+        }
         if (block_end && ((k + 1) % block_len) == 0) block_end[(k + 1) / block_len - 1] = base + q;
         if (k == M - 1) stp->last_attempt = base + q;
       }
@@ -563,7 +567,8 @@ int MtStream::prefetch(size_t M, hipStream_t main) {
   return 0;
 }
 
-int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s) {
+int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s,
+                            size_t k_lo, size_t k_hi) {
   const unsigned long long words = words_for_normals(M);
   const unsigned long long A = words / 2;
   const size_t nb = (size_t)((A + POLAR_APB - 1) / POLAR_APB);
@@ -578,7 +583,8 @@ int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, counts_, offsets_, (int)nb, st_);
   KG_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_polar_scatter, dim3(nb), dim3(POLAR_TPB), 0, s, ring_, R_, st_, A, offsets_, z,
-                     (unsigned long long)M, (unsigned long long)(block_len ? block_len : 1), block_end);
+                     (unsigned long long)M, (unsigned long long)(block_len ? block_len : 1), block_end,
+                     (unsigned long long)k_lo, (unsigned long long)(k_hi < M ? k_hi : M));
   KG_HIP(hipGetLastError());
   return 0;
 }

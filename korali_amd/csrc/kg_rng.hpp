@@ -72,7 +72,10 @@ class MtStream {
   // attempt index of normal (b+1)*block_len-1 (resampling support).  The
   // stream is NOT advanced; call consume_normals() with the number of
   // normals actually used.
-  int polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s);
+  // Normals k outside [k_lo, k_hi) are counted (stream positions stay exact)
+  // but not written; z receives normal k at z[k - k_lo].
+  int polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s,
+                    size_t k_lo = 0, size_t k_hi = (size_t)-1);
   // advance past `normals_used` normals (device-side: uses last attempt of
   // normal normals_used-1 found in block_end[(normals_used/block_len)-1] or
   // the polar pass's own record when block_end == nullptr)

@@ -34,7 +34,7 @@ class _CmaesCfg(C.Structure):
         ("initial_value", C.POINTER(C.c_double)), ("initial_std", C.POINTER(C.c_double)),
         ("min_std_update", C.POINTER(C.c_double)),
         ("normal_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("cov_mode", C.c_int), ("device", C.c_int),
-        ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int),
+        ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int), ("shard_rank", C.c_int), ("shard_count", C.c_int),
     ]
 
 
@@ -55,6 +55,7 @@ EXPORTED = [
     "kg_last_error", "kg_abi_version", "kg_device_count",
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
     "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_update", "kg_cmaes_generation",
+    "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
@@ -83,6 +84,9 @@ def lib():
         L.kg_cmaes_get_candidates.argtypes = [vp, dp, sz]
         L.kg_cmaes_set_fitness.argtypes = [vp, dp]
         L.kg_cmaes_update.argtypes = [vp, sz]
+        L.kg_cmaes_update_partial.argtypes = [vp, sz]
+        L.kg_cmaes_update_finalize.argtypes = [vp, sz]
+        L.kg_debug_mt_jump.argtypes = [vp, C.c_uint64, vp]
         L.kg_cmaes_generation.argtypes = [vp, sz, ip]
         L.kg_cmaes_field_size.argtypes = [vp, cp, C.POINTER(sz)]
         L.kg_cmaes_get_field.argtypes = [vp, cp, dp, sz]
@@ -142,7 +146,8 @@ class CmaesDevice:
                  initial_std=None, min_std_update=None, normal_seed=0, uniform_seed=0, cov_mode="exact",
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
-                 initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host"):
+                 initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host", shard_rank=0,
+                 shard_count=1):
         L = lib()
         self.N, self.lam = int(N), int(lam)
         self.mu = int(mu) if mu else self.lam // 2
@@ -165,6 +170,8 @@ class CmaesDevice:
         cfg.cov_mode = COV_MODES[cov_mode.lower()] if isinstance(cov_mode, str) else int(cov_mode)
         cfg.device, cfg.store_bdz = int(device), int(store_bdz)
         cfg.eigen_device_chase = 1 if eigen_chase == "device" else 0
+        cfg.shard_rank, cfg.shard_count = int(shard_rank), int(shard_count)
+        self.shard_rank, self.shard_count = int(shard_rank), max(1, int(shard_count))
         h = C.c_void_p()
         check(L.kg_cmaes_create(C.byref(cfg), C.byref(h)))
         self.h = h
@@ -194,6 +201,12 @@ class CmaesDevice:
 
     def update(self, generation):
         check(self._L.kg_cmaes_update(self.h, int(generation)))
+
+    def update_partial(self, generation):
+        check(self._L.kg_cmaes_update_partial(self.h, int(generation)))
+
+    def update_finalize(self, generation):
+        check(self._L.kg_cmaes_update_finalize(self.h, int(generation)))
 
     def generation(self, generation, objective):
         obj = OBJECTIVES[objective.lower()] if isinstance(objective, str) else int(objective)

@@ -1,0 +1,124 @@
+"""Population-sharded CMA-ES over torch.distributed.
+
+One process per GPU; every rank holds the replicated solver state (mean, C,
+B, D, paths, σ, generator states) in its own kg_cmaes_t handle created with
+shard_rank / shard_count.  Per generation (CMAES::runGeneration,
+CMAES.cpp.base:186-231):
+
+  1. eigendecomposition — replicated (deterministic kernels: identical bits);
+  2. the mt19937 polar stream is counted whole on every rank (its positions
+     are global), but each rank materialises and transforms only the normals
+     of its rows [r λ/S, (r+1) λ/S) and evaluates only those candidates;
+  3. all-gather of the per-candidate fitnesses (λ doubles) — the one
+     exchange the selection needs;
+  4. replicated sort (identical sorting index everywhere, bit-exact);
+  5. each rank sums the mean and rank-μ terms of the selected rows it owns,
+     plus the best row if it owns it; one sum all-reduce of those partials
+     (2N + N(N+16)/2 doubles); every rank then finishes the update.
+
+The collectives go through torch.distributed: backend "nccl" is RCCL over
+xGMI on ROCm, and the tensors alias the handle's device buffers (zero copy,
+ordered on the handle's HIP stream).  transport="host" stages the two
+buffers through host memory instead, for the gloo backend (several ranks on
+one device, CPU-only process groups).
+
+Summation order of mean and rank-μ differs from the sequential reference by
+rounding only (≤1e-12 relative; selection and resampling indices are
+bit-exact for identical state), exactly as SURVEY.md §8(e) item 5 states.
+"""
+import numpy as np
+
+from .native import CmaesDevice
+
+
+class _DeviceArray:
+    """__cuda_array_interface__ view of a device buffer (torch.as_tensor
+    wraps it without copying)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": "<f8", "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def shard_range(lam, world, rank):
+    """Rows [r0, r1) of the population owned by `rank` (λ % world == 0)."""
+    if lam % world:
+        raise ValueError(f"Population Size {lam} is not divisible by {world} ranks")
+    per = lam // world
+    return rank * per, (rank + 1) * per
+
+
+def allgather_shards(dist, local, world, group=None):
+    """Host transport: concatenate every rank's equal-size shard in rank
+    order (numpy in, numpy out)."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(local))
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return torch.cat(parts).numpy()
+
+
+def allreduce_sum(dist, arr, group=None):
+    """Host transport: element-wise sum over ranks (numpy in, numpy out)."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float64).copy())
+    dist.all_reduce(t, group=group)
+    return t.numpy()
+
+
+class ShardedCmaes:
+    """CMA-ES generation loop with the population split across the ranks of
+    a torch.distributed group (one kg_cmaes_t per rank)."""
+
+    def __init__(self, N, lam, dist, group=None, device=0, transport="device", **cmaes_kw):
+        self.dist, self.group = dist, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.N, self.lam = int(N), int(lam)
+        self.r0, self.r1 = shard_range(self.lam, self.world, self.rank)
+        cmaes_kw.setdefault("cov_mode", "mfma")
+        self.dev = CmaesDevice(N, lam, shard_rank=self.rank, shard_count=self.world, device=device, **cmaes_kw)
+        self.transport = transport
+        if transport == "device":
+            import torch
+            dv = torch.device("cuda", device)
+            self._F = torch.as_tensor(_DeviceArray(self.dev.device_ptr("Value Vector"), self.lam), device=dv)
+            n = self.dev.field_size("Shard Partials")
+            self._P = torch.as_tensor(_DeviceArray(self.dev.device_ptr("Shard Partials"), n), device=dv)
+            self._stream = torch.cuda.ExternalStream(self.dev.stream(), device=dv)
+        elif transport != "host":
+            raise ValueError("transport must be 'device' or 'host'")
+
+    def _exchange_fitness(self):
+        if self.transport == "device":
+            import torch
+            with torch.cuda.stream(self._stream):
+                self.dist.all_gather_into_tensor(self._F, self._F[self.r0:self.r1].clone(), group=self.group)
+        else:
+            F = self.dev["Value Vector"]
+            self.dev["Value Vector"] = allgather_shards(self.dist, F[self.r0:self.r1], self.world, self.group)
+
+    def _reduce_partials(self):
+        if self.transport == "device":
+            import torch
+            with torch.cuda.stream(self._stream):
+                self.dist.all_reduce(self._P, group=self.group)
+        else:
+            self.dev["Shard Partials"] = allreduce_sum(self.dist, self.dev["Shard Partials"], self.group)
+
+    def generation(self, generation, objective):
+        d = self.dev
+        if generation == 1:
+            d.initialize()
+        d.sample()
+        d.evaluate(objective)
+        self._exchange_fitness()
+        d.update_partial(generation)
+        self._reduce_partials()
+        d.update_finalize(generation)
+
+    def synchronize(self):
+        self.dev.synchronize()
+
+    def close(self):
+        self.dev.close()

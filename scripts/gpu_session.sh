@@ -29,6 +29,9 @@ for s in ${STEPS:-smoke tests bench prof}; do
     profc3) step profc3 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c3" -o run --output-format csv -- python bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     c4) step c4 600 python tools/probe_c4.py ${C4_ARGS:-512 65536 3} ;;
+    shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
+    cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
+    benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac
 done

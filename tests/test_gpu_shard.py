@@ -1,0 +1,33 @@
+"""Population sharding on one device: S ranks (gloo,
+host-staged collectives) against the unsharded handle — fitness all-gather,
+replicated sort and state bit-identical across ranks, own rows bit-exact,
+mean / covariance / σ within the partial-sum tolerance."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("ranks,N,lam,gens,obj,backend", [(2, 32, 256, 6, "rosenbrock", "gloo"),
+                                                          (4, 200, 1024, 3, "ackley", "gloo"),
+                                                          (1, 64, 512, 4, "rosenbrock", "nccl")])
+def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend):
+    """gloo: several ranks on the one device, host-staged collectives;
+    nccl: the RCCL zero-copy device transport (one rank: one device here)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "tools", "shard_check.py"),
+           str(N), str(lam), str(gens), obj, backend]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "SHARD_CHECK PASS" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
