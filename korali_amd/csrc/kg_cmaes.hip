@@ -1145,7 +1145,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
-  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 16);
+  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32);
   {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)
@@ -1433,14 +1433,17 @@ int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
 int kg_cmaes_synchronize(kg_cmaes_t h) {
   KG_HIP(hipStreamSynchronize(h->stream));
   if (h->eigTrace) {
-    unsigned long long t[16];
+    unsigned long long t[32];
     KG_HIP(hipMemcpy(t, h->eigTrace, sizeof(t), hipMemcpyDeviceToHost));
     int steps = 0, rots = 0;
     h->eig.last_counts(steps, rots);
     fprintf(stderr,
             "[korali_amd tridiag trace, cumulative s_memtime ticks] nrm2 %llu dsymv %llu xv %llu dsyr2 %llu; last QR: "
-            "%d steps, %d rotations\n[korali_amd apply trace] groups %llu time-units %llu steps %llu ticks %llu\n",
-            t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7]);
+            "%d steps, %d rotations\n[korali_amd apply trace] groups %llu time-units %llu steps %llu ticks %llu\n"
+            "[korali_amd multi-workgroup tridiag, writer wg] dnrm2 %llu householder %llu dsymv-stage %llu dsymv-chain "
+            "%llu x-gather %llu xv-stage %llu xv-chain %llu alpha %llu pivot-poll %llu update %llu\n",
+            t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7], t[16], t[17], t[18], t[19], t[20], t[21],
+            t[22], t[23], t[24], t[25]);
   }
   return check_errors(h);
 }

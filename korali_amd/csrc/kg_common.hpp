@@ -71,25 +71,27 @@ __device__ inline void put_granule_dbl(unsigned long long *p, unsigned tag, doub
   __hip_atomic_store(g + 1, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// All threads of the workgroup: element e < count comes from granules
-// base[2*idx(e)], idx(e) = e for e < count-1, the last element (when
-// lastIdx >= 0) from base[2*lastIdx].  Returns false when the spin limit or
+// All threads of the workgroup gather two granule segments in one polling
+// sweep: element e < countA from baseA[2e] into dstA[e], then countB
+// elements from baseB into dstB.  Returns false when the spin limit or
 // another workgroup's abort ended the wait.
-__device__ inline bool poll_granule_dbls(unsigned long long *base, int count, int lastIdx, unsigned tag,
-                                         double *dst, unsigned long long *abortw, unsigned *errors) {
-  const int t = threadIdx.x, nt = blockDim.x;
-  gu64_t *g = (gu64_t *)base;
+__device__ inline bool poll_granule_dbls(unsigned long long *baseA, int countA, double *dstA,
+                                         unsigned long long *baseB, int countB, double *dstB, unsigned tag,
+                                         unsigned long long *abortw, unsigned *errors) {
+  const int t = threadIdx.x, nt = blockDim.x, count = countA + countB;
   for (int e0 = 0; e0 < count; e0 += nt) {
     const int e = e0 + t;
     bool done = e >= count;
-    const int gi = (lastIdx >= 0 && e == count - 1) ? lastIdx : e;
+    const bool inA = e < countA;
+    gu64_t *g = (gu64_t *)(inA ? baseA + 2 * (size_t)e : baseB + 2 * (size_t)(e - countA));
+    double *dst = inA ? dstA + e : dstB + (e - countA);
     unsigned spins = 0;
     for (;;) {
       if (!done) {
-        const unsigned long long lo = __hip_atomic_load(g + 2 * gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long hi = __hip_atomic_load(g + 2 * gi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag) {
-          dst[e] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffULL)));
+          *dst = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffULL)));
           done = true;
         }
       }
@@ -292,6 +294,33 @@ __host__ __device__ inline uint32_t mt_temper(uint32_t k) {
 __host__ __device__ inline uint32_t mt_next(uint32_t a624, uint32_t a623, uint32_t a227) {
   uint32_t y = (a624 & 0x80000000u) | (a623 & 0x7fffffffu);
   return a227 ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// acc + t(0) + t(1) + ... + t(cnt-1), added strictly left to right (the
+// reference's sequential order), with the next 8 terms evaluated while the
+// current 8 are added: the LDS loads behind t() overlap the dependent
+// 14-cycle FP64 add chain instead of preceding every group of 8.
+template <class T>
+__device__ __forceinline__ double ordered_sum(double acc, int cnt, T t) {
+  int q = 0;
+  if (cnt >= 8) {
+    double cur[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = t(u);
+    for (q = 8; q + 8 <= cnt; q += 8) {
+      double nx[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) nx[u] = t(q + u);
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc += cur[u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) cur[u] = nx[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += cur[u];
+  }
+  for (; q < cnt; q++) acc += t(q);
+  return acc;
 }
 
 // block-id remap so that consecutive tiles land on one XCD (speed only)

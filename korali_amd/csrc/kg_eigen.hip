@@ -21,6 +21,8 @@
 // Every +,-,*,/,sqrt is IEEE correctly rounded on gfx950 and the file is
 // compiled with -ffp-contract=off, so the result equals the oracle bit for
 // bit.
+#include <cstdlib>
+
 #include "kg_eigen.hpp"
 
 namespace kg {
@@ -213,6 +215,98 @@ __host__ __device__ void qrstep(int n, double *d, double *sd, double *gc, double
   sd[k - 1] = bk;
 }
 
+// DPP lane moves of a double (both halves; lanes without a source get 0.0)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_d(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), CTRL, ROWMASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, ROWMASK, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// inclusive prefix max over the wave of values >= 0 (identity 0.0):
+// row_shr 1/2/4/8 inside rows of 16, then row_bcast 15 / 31 across rows
+__device__ __forceinline__ double wave_prefix_max_nonneg(double x) {
+  x = fmax(x, dpp_d<0x111, 0xf>(x));
+  x = fmax(x, dpp_d<0x112, 0xf>(x));
+  x = fmax(x, dpp_d<0x114, 0xf>(x));
+  x = fmax(x, dpp_d<0x118, 0xf>(x));
+  x = fmax(x, dpp_d<0x142, 0xa>(x));
+  x = fmax(x, dpp_d<0x143, 0xc>(x));
+  return x;
+}
+
+// gslcblas dnrm2 of m elements x[k*stride], k < m, by one wave (every lane
+// returns the result): scale = running max |x| (prefix max, lane-parallel),
+// the addends (|x|/scale)^2 and rescale ratios staged in LDS (sv: m doubles,
+// msk: ceil(m/64) words marking new-maximum elements), then the ssq
+// recurrence in the reference's order with the next 8 addends loaded while
+// the current 8 are added.  Zero elements add +0.0 (ssq >= 1: exact).
+__device__ double dnrm2_wave(const double *x, int stride, int m, double *sv, unsigned long long *msk) {
+  const int lane = threadIdx.x & 63;
+  double carry = 0.0;
+  const int m8 = (m + 7) & ~7;  // staged length: zero addends (exact) pad to whole batches
+  for (int base = 0; base < m8; base += 64) {
+    const int e = base + lane;
+    const double a_ = fabs(x[(size_t)min(e, m - 1) * stride]);
+    const double a = (e < m) ? a_ : 0.0;
+    const double pm = wave_prefix_max_nonneg(a);  // DPP: no LDS round trips
+    const double before = fmax(dpp_d<0x138, 0xf>(pm), carry);  // wave_shr:1, lane 0 gets 0.0
+    int type = 0;
+    double q = 0.0;
+    if (e < m && a != 0.0) {
+      if (before < a) {
+        type = 1;
+        q = before / a;
+      } else {
+        type = 2;
+        q = a / before;
+      }
+    }
+    const unsigned long long b1 = __ballot(type == 1);
+    if (e < m8) sv[e] = (type == 1) ? q : ((type == 2) ? q * q : 0.0);
+    if (lane == 0) msk[base >> 6] = b1;
+    carry = fmax(carry, readlane_d(pm, 63));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double ssq = 1.0;
+  // one mask word per 64 (uniform, loaded once), values two batches deep
+#define KG_NRM2_STEP8(T, BITS)                        \
+  {                                                   \
+    const unsigned bits_ = (BITS);                    \
+    if (bits_ == 0) {                                 \
+      _Pragma("unroll") for (int u = 0; u < 8; u++) ssq += T[u]; \
+    } else {                                          \
+      _Pragma("unroll") for (int u = 0; u < 8; u++) { \
+        if ((bits_ >> u) & 1u)                        \
+          ssq = 1.0 + ssq * T[u] * T[u];              \
+        else                                          \
+          ssq += T[u];                                \
+      }                                               \
+    }                                                 \
+  }
+  for (int c0 = 0; c0 < m8; c0 += 64) {
+    const unsigned long long mw = msk[c0 >> 6];
+    const int cn = (m8 - c0) < 64 ? (m8 - c0) : 64;
+    double a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = sv[c0 + u];
+    for (int e = 0; e < cn; e += 16) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) b[u] = sv[c0 + e + 8 + u];
+      KG_NRM2_STEP8(a, (unsigned)((mw >> e) & 0xffULL))
+      if (e + 8 >= cn) break;
+#pragma unroll
+      for (int u = 0; u < 8; u++) a[u] = sv[c0 + e + 16 + u];
+      KG_NRM2_STEP8(b, (unsigned)((mw >> (e + 8)) & 0xffULL))
+    }
+  }
+#undef KG_NRM2_STEP8
+  __builtin_amdgcn_wave_barrier();
+  return (m == 1) ? fabs(x[0]) : carry * sqrt(ssq);
+}
+
 }  // namespace
 
 // Dynamic LDS: [matrix region N*(N+1) doubles if lds_mats] + vectors.
@@ -233,7 +327,7 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
   double *vb = kLds ? smem + (size_t)N * lda : smem;
   double *x = vb, *scal = vb + N;
   double *sv = vb + N + 16;  // staged addends of a serial chain (wave 0); t2 of dsymv
-  double *tv = sv + (N > 64 ? N : 64);  // tau * v_r, contiguous (dsymv)
+  double *tv = sv + (N > 64 ? N : 64) + 8;  // tau * v_r, contiguous (dsymv); sv padded for dnrm2_wave
   double *vv = tv + N;       // v_r with v_0 = 1, contiguous (dsymv)
   unsigned long long acc_t[4] = {0, 0, 0, 0}, tmark = 0;
 #define KG_MARK() \
@@ -253,68 +347,11 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
     double *m = M + (size_t)(i + 1) * lda + (i + 1);  // lda
     KG_MARK()
     if (wid == 0) {
-      // gslcblas dnrm2 over v[1..n-1]: prefix max in parallel, the ssq
-      // recurrence sequentially on uniform registers (every lane the same)
-      double scale_carry = 0.0, ssq = 1.0;
-      for (int base = 1; base < n; base += 64) {
-        const int r = base + lane;
-        const double a_ = fabs(v[(size_t)min(r, n - 1) * lda]);
-        const double a = (r < n) ? a_ : 0.0;
-        double pm = a;
-        for (int off = 1; off < 64; off <<= 1) {
-          const double t = __shfl_up(pm, off, 64);
-          if (lane >= off) pm = fmax(pm, t);
-        }
-        double before = __shfl_up(pm, 1, 64);
-        if (lane == 0) before = 0.0;
-        before = fmax(before, scale_carry);
-        int type = 0;
-        double q = 0.0;
-        if (r < n && a != 0.0) {
-          if (before < a) {
-            type = 1;
-            q = before / a;
-          } else {
-            type = 2;
-            q = a / before;
-          }
-        }
-        // addends precomputed lane-parallel; zero elements add +0.0, which
-        // leaves ssq (>= 1) unchanged.  The serial recurrence then runs on
-        // values staged in LDS, 8 in flight, new-maximum lanes (a handful
-        // per vector) taking the rescaling branch.
-        const double tq = (type == 2) ? q * q : 0.0;
-        const unsigned long long m1 = __ballot(type == 1);
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        sv[lane] = (type == 1) ? q : tq;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int l0 = 0; l0 < cnt; l0 += 8) {
-          double t[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];  // lanes past n staged +0.0
-          const unsigned bits = (unsigned)((m1 >> l0) & 0xffULL);
-          if (bits == 0) {
-#pragma unroll
-            for (int u = 0; u < 8; u++) ssq += t[u];
-          } else {
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-              if ((bits >> u) & 1u)
-                ssq = 1.0 + ssq * t[u] * t[u];
-              else
-                ssq += t[u];
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        scale_carry = fmax(scale_carry, readlane_d(pm, 63));
-      }
+      // gslcblas dnrm2 over v[1..n-1]
+      const double xnorm = dnrm2_wave(v + lda, lda, n - 1, sv, (unsigned long long *)(scal + 8));
       if (lane == 0) {
         double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
         int branch = 0;
-        const double xnorm = (n - 1 == 1) ? fabs(v[lda]) : scale_carry * sqrt(ssq);
         if (xnorm != 0) {
           const double alpha = v[0];
           beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
@@ -369,33 +406,14 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
     const int half = (nt / 2) & ~63;
     if (tid < half) {
       for (int j = tid; j < n; j += half) {
-        double acc = 0.0;
-        int r = n - 1;
         const double *mc = m + j;
-        for (; r - 7 > j; r -= 8) {
-          double p[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) p[u] = tv[r - u] * mc[(size_t)(r - u) * lda];
-#pragma unroll
-          for (int u = 0; u < 8; u++) acc += p[u];
-        }
-        for (; r > j; r--) acc += tv[r] * mc[(size_t)r * lda];
-        x[j] = acc;
+        // rows r = n-1 .. j+1 (descending)
+        x[j] = ordered_sum(0.0, n - 1 - j, [&](int q) { return tv[n - 1 - q] * mc[(size_t)(n - 1 - q) * lda]; });
       }
     } else {
       for (int j = tid - half; j < n; j += nt - half) {
         const double *mj = m + (size_t)j * lda;
-        double t2 = 0.0;
-        int q = 0;
-        for (; q + 8 <= j; q += 8) {
-          double p[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) p[u] = vv[q + u] * mj[q + u];
-#pragma unroll
-          for (int u = 0; u < 8; u++) t2 += p[u];
-        }
-        for (; q < j; q++) t2 += vv[q] * mj[q];
-        t2b[j] = t2;
+        t2b[j] = ordered_sum(0.0, j, [&](int q) { return vv[q] * mj[q]; });
       }
     }
     __syncthreads();
@@ -408,27 +426,12 @@ __global__ void __launch_bounds__(1024) k_tridiag(int N, const double *__restric
     __syncthreads();
     KG_ACC(1)
     KG_MARK()
+    // xv = sum x[r] v[r] sequentially: products staged by all threads (tv is
+    // free after dsymv), one ordered chain on wave 0; alpha = -(tau/2) xv
+    for (int r = tid; r < n; r += nt) tv[r] = x[r] * vv[r];
+    __syncthreads();
     if (wid == 0) {
-      // xv = sum x[r] v[r] sequentially (products lane-parallel, staged in
-      // LDS, 8 in flight; +0.0 padding is exact); alpha = -(tau/2) xv
-      double xv = 0.0;
-      for (int base = 0; base < n; base += 64) {
-        const int r = base + lane, rc = min(r, n - 1);
-        const double p_ = x[rc] * vv[rc];
-        sv[lane] = (r < n) ? p_ : 0.0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        for (int l0 = 0; l0 < cnt; l0 += 8) {
-          double t[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
-#pragma unroll
-          for (int u = 0; u < 8; u++) xv += t[u];
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
+      const double xv = ordered_sum(0.0, n, [&](int q) { return tv[q]; });
       if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
     }
     __syncthreads();
@@ -492,19 +495,7 @@ __global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict
     // phase 1: w_j = sum_r Q[i+1+r][i+1+j] h[r], one ordered chain per j
     for (int j = tid; j < n; j += nt) {
       const double *col = M + (size_t)(i + 1 + j) * lda + (i + 1);  // Q[i+1+r][i+1+j], r = 0..n-1
-      double wj = col[0];
-      for (int r0 = 1; r0 < n; r0 += 16) {
-        double p[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-          const int r = min(r0 + u, n - 1);
-          const double pr = col[r] * h[r];
-          p[u] = (r0 + u < n) ? pr : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++) wj += p[u];  // +0.0 padding is exact (see k_tridiag)
-      }
-      wsh[j] = wj;
+      wsh[j] = ordered_sum(col[0], n - 1, [&](int q) { return col[1 + q] * h[1 + q]; });
     }
     __syncthreads();
     // phase 2 (every wave): Q[.][j] -= tau h w_j, element-parallel
@@ -520,259 +511,300 @@ __global__ void __launch_bounds__(1024) k_unpack(int N, const double *__restrict
 }
 
 // ------------------------------------------------------------------------
-// Phases A and B for N > 128 (the matrix no longer fits one CU's LDS):
-// many workgroups, each holding a few FULL rows of the symmetric matrix in
-// LDS (rows round-robin, row r on workgroup r % P).  Symmetric storage makes
+// Phase A for N > 128 (the matrix no longer fits one CU's LDS): many
+// workgroups, each holding a few FULL rows of the symmetric matrix in LDS
+// (rows round-robin, row r on workgroup r % P).  Symmetric storage makes
 // every gslcblas chain of a row local to its owner:
 //   dsymv  x_j = (sum_{c desc} (tau v_c) m[j][c] + (tau v_j) m[j][j]) + tau sum_{c asc} v_c m[j][c]
 //          (column j of the lower triangle is row j of the upper one);
 //   dsyr2  m[a][b] += (-v_a) x_b + (-x_a) v_b with a >= b, applied to both
 //          (a,b) and (b,a), so the two copies stay bit-identical.
-// Per Householder step two in-launch hand-offs (R2 granules): the pivot
-// row's owner broadcasts (tau, v); every owner publishes its x_j and every
-// workgroup gathers the whole x (xv is then recomputed redundantly).  Every
-// step has slots of its own (no slot is ever rewritten within a launch, so
-// no workgroup can miss a value however far the others run ahead; tau = 0
-// steps skip the x exchange).
+// One in-launch hand-off per Householder step (R2 granules, slots per step
+// so nothing is ever overwritten within a launch): every owner publishes its
+// x_j and every workgroup gathers the whole x.  Everything else of the step
+// is recomputed redundantly by every workgroup with identical operands:
+// xv and alpha, the next pivot row (its owner publishes it one step ahead,
+// off the critical path; every workgroup applies the step's rank-2 update to
+// it), its dnrm2 / Householder scalars and the scaled v.  Chains add
+// products staged in LDS by all threads (an add-only chain runs at the
+// FP64 add latency; tools/ubench_chain2.hip).
 constexpr int TMW_TPB = 256;
-constexpr int TMW_MAXP = 64;
 
-__host__ __device__ inline int tmw_rows(int N) { return (N + TMW_MAXP - 1) / TMW_MAXP; }
-__host__ __device__ inline int tmw_groups(int N) { return (N + tmw_rows(N) - 1) / tmw_rows(N); }
-size_t tmw_lds_bytes(int N) {
-  return ((size_t)tmw_rows(N) * (N + 1) + 3 * (size_t)N + 64 + 16 + 2 * 16) * sizeof(double);
+__host__ __device__ inline size_t tmw_lds_doubles(int N, int RW) {
+  return 2 * (size_t)RW * (N + 1) + 5 * (size_t)N + 4 * 16 + 32;  // +32: chain read-ahead slack
 }
-// comm buffer (u64 words): v granules [N][2(N+1)] (tau in element N), x
-// granules [N][2N], abort word (+ pad to 16 bytes)
-size_t tmw_comm_words(int N) { return 2 * (size_t)N * (N + 1) + 2 * (size_t)N * N + 2; }
+__host__ __device__ inline int tmw_rows(int N) {
+  int rw = (N + 63) / 64;
+  while (rw > 1 && tmw_lds_doubles(N, rw) * sizeof(double) > 150 * 1024) rw--;
+  return rw;
+}
+__host__ __device__ inline int tmw_groups(int N) { return (N + tmw_rows(N) - 1) / tmw_rows(N); }
+size_t tmw_lds_bytes(int N) { return tmw_lds_doubles(N, tmw_rows(N)) * sizeof(double); }
+// comm buffer (u64 words): x granules [N][2N], pivot-row granules [N][2N],
+// abort word (+ pad to 16 bytes)
+size_t tmw_comm_words(int N) { return 4 * (size_t)N * N + 2; }
+
+// Add-only ordered chains over values staged in LDS (one lane): the next 8
+// values are loaded while the current 8 are added (two register sets, no
+// copies), so LDS latency hides behind the 14-cycle dependent FP64 adds.
+// They read up to 16 values past the end (ascending) or before the start
+// (descending); those reads stay inside the kernel's LDS and are not added.
+__device__ __forceinline__ double staged_chain(double acc, const double *p, int cnt) {
+  double a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) a[u] = p[u];
+  int q = 0;
+  for (; q + 16 <= cnt; q += 16) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = p[q + 8 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = p[q + 16 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += b[u];
+  }
+  if (q + 8 <= cnt) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = p[q + 8 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+    q += 8;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += b[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += a[u];
+  }
+  return acc;
+}
+// acc + p[cnt-1] + p[cnt-2] + ... + p[0]
+__device__ __forceinline__ double staged_chain_desc(double acc, const double *p, int cnt) {
+  const double *e = p + cnt - 1;  // e[-j] = p[cnt-1-j]
+  double a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) a[u] = e[-u];
+  int q = 0;
+  for (; q + 16 <= cnt; q += 16) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = e[-(q + 8 + u)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = e[-(q + 16 + u)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += b[u];
+  }
+  if (q + 8 <= cnt) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = e[-(q + 8 + u)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+    q += 8;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += b[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += a[u];
+  }
+  return acc;
+}
 
 __global__ void __launch_bounds__(TMW_TPB) k_tridiag_mw(int N, const double *__restrict__ C, double *gH,
                                                         double *tauOut, double *dOut, double *sdOut,
-                                                        unsigned long long *comm, unsigned int *errors) {
+                                                        unsigned long long *comm, unsigned int *errors,
+                                                        unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
   const int P = gridDim.x, g = blockIdx.x, RW = tmw_rows(N), lda = N + 1;
-  double *M = smem;                     // local row k = global row g + k P
-  double *vloc = M + (size_t)RW * lda;  // v with v_0 = 1
-  double *tv = vloc + N;                // tau v
-  double *xl = tv + N;                  // x
-  double *sv = xl + N;                  // 64: staged chain addends
-  double *scal = sv + 64;               // 16 scalars
-  double *accb = scal + 16;             // 16: dsymv acc per local row
-  double *t2b = accb + 16;              // 16: dsymv t2 per local row
-  unsigned long long *gv = comm, *gx = comm + 2 * (size_t)N * (N + 1);
-  unsigned long long *abortw = gx + 2 * (size_t)N * N;
+  double *M = smem;                         // local row k = global row g + k P
+  double *Pr = M + (size_t)RW * lda;        // staged dsymv products, same shape
+  double *prow = Pr + (size_t)RW * lda;     // current pivot row, indexed by column
+  double *nrow = prow + N;                  // next pivot row as published (before this step's update)
+  double *vloc = nrow + N;                  // v with v_0 = 1
+  double *tv = vloc + N;                    // tau v; also dnrm2 / xv staging
+  double *xl = tv + N;                      // x
+  double *scal = xl + N;                    // 16 scalars
+  double *accb = scal + 16;                 // 16: dsymv acc per local row
+  double *t2b = accb + 16;                  // 16: dsymv t2 per local row
+  unsigned long long *mskb = (unsigned long long *)(t2b + 16);  // 16: dnrm2 rescale masks
+  unsigned long long *gx = comm, *grow = comm + 2 * (size_t)N * N, *abortw = comm + 4 * (size_t)N * N;
+  const int writer = (N - 1) % P;  // owns row N-1: runs every step, writes the per-step outputs
 
   for (int idx = tid; idx < RW * N; idx += nt) {
     const int k = idx / N, c = idx % N, r = g + k * P;
     if (r < N) M[(size_t)k * lda + c] = (c <= r) ? C[(size_t)r * N + c] : C[(size_t)c * N + r];
   }
+  for (int c = tid; c < N; c += nt) {
+    prow[c] = C[(size_t)c * N];                             // row 0 (symmetrised: column 0)
+    nrow[c] = (c >= 1) ? C[(size_t)c * N + 1] : C[1];       // row 1 before any update
+  }
   const int maxRow = g + ((N - 1 - g) / P) * P;  // largest row owned
+  const bool tr = trace && g == writer && tid == 0;
+  unsigned long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+#define TMW_MARK(k)                                               \
+  if (tr) {                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    tacc[k] += t_ - tm;                                           \
+    tm = t_;                                                      \
+  }
   __syncthreads();
   for (int i = 0; i + 2 < N; i++) {
-    if (maxRow < i) break;  // nothing left to own or to update
+    if (maxRow < i) break;  // no active rows left (never the writer)
     const int n = N - i - 1;
     const unsigned tag = (unsigned)i + 1u;
-    unsigned long long *gvp = gv + (size_t)i * 2 * (N + 1), *gxp = gx + (size_t)i * 2 * N;
-    if (i % P == g) {
-      // ---- pivot row i: Householder vector of v = row i, columns i+1.. (== column i below the diagonal)
-      double *v = M + (size_t)(i / P) * lda + i + 1;
-      if (wid == 0) {
-        double scale_carry = 0.0, ssq = 1.0;  // gslcblas dnrm2 over v[1..n-1] (see k_tridiag)
-        for (int base = 1; base < n; base += 64) {
-          const int r = base + lane;
-          const double a_ = fabs(v[min(r, n - 1)]);
-          const double a = (r < n) ? a_ : 0.0;
-          double pm = a;
-          for (int off = 1; off < 64; off <<= 1) {
-            const double t = __shfl_up(pm, off, 64);
-            if (lane >= off) pm = fmax(pm, t);
+    unsigned long long *gxp = gx + (size_t)i * 2 * N, *growp = grow + (size_t)i * 2 * N;
+    // owner of row i+1 publishes it (state after step i-1) for step i's end
+    if (i >= 1 && i + 4 <= N && (i + 1) % P == g) {
+      const double *row = M + (size_t)((i + 1) / P) * lda;
+      for (int c = i + 2 + tid; c < N; c += nt) put_granule_dbl(growp + 2 * c, tag, row[c]);
+    }
+    // ---- Householder vector of the pivot row i (redundant on every workgroup)
+    const double *v = prow + i + 1;  // v[0] = alpha, v[1..n-1]
+    if (wid == 0) {
+      const double xnorm = dnrm2_wave(v + 1, 1, n - 1, tv, mskb);
+      TMW_MARK(0)
+      if (lane == 0) {
+        double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
+        int branch = 0;
+        if (xnorm != 0) {
+          const double alpha = v[0];
+          beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
+          tau_i = (beta - alpha) / beta;
+          const double s = alpha - beta;
+          if (fabs(s) > DMIN) {
+            f1 = 1.0 / s;
+            branch = 1;
+          } else {
+            f1 = EPS / s;
+            f2 = 1.0 / EPS;
+            branch = 2;
           }
-          double before = __shfl_up(pm, 1, 64);
-          if (lane == 0) before = 0.0;
-          before = fmax(before, scale_carry);
-          int type = 0;
-          double q = 0.0;
-          if (r < n && a != 0.0) {
-            if (before < a) {
-              type = 1;
-              q = before / a;
-            } else {
-              type = 2;
-              q = a / before;
-            }
-          }
-          const double tq = (type == 2) ? q * q : 0.0;
-          const unsigned long long m1 = __ballot(type == 1);
-          const int cnt = (n - base) < 64 ? (n - base) : 64;
-          sv[lane] = (type == 1) ? q : tq;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          for (int l0 = 0; l0 < cnt; l0 += 8) {
-            double t[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
-            const unsigned bits = (unsigned)((m1 >> l0) & 0xffULL);
-            if (bits == 0) {
-#pragma unroll
-              for (int u = 0; u < 8; u++) ssq += t[u];
-            } else {
-#pragma unroll
-              for (int u = 0; u < 8; u++) {
-                if ((bits >> u) & 1u)
-                  ssq = 1.0 + ssq * t[u] * t[u];
-                else
-                  ssq += t[u];
-              }
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-          scale_carry = fmax(scale_carry, readlane_d(pm, 63));
         }
-        if (lane == 0) {
-          double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
-          int branch = 0;
-          const double xnorm = (n - 1 == 1) ? fabs(v[1]) : scale_carry * sqrt(ssq);
-          if (xnorm != 0) {
-            const double alpha = v[0];
-            beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
-            tau_i = (beta - alpha) / beta;
-            const double s = alpha - beta;
-            if (fabs(s) > DMIN) {
-              f1 = 1.0 / s;
-              branch = 1;
-            } else {
-              f1 = EPS / s;
-              f2 = 1.0 / EPS;
-              branch = 2;
-            }
-          }
-          scal[0] = tau_i;
-          scal[1] = f1;
-          scal[2] = f2;
-          scal[3] = beta;
-          scal[4] = (double)branch;
+        scal[0] = tau_i;
+        scal[1] = f1;
+        scal[2] = f2;
+        scal[3] = branch ? beta : v[0];  // v_0 after householder_transform
+        scal[4] = (double)branch;
+        if (g == writer) {
           tauOut[i] = tau_i;
+          sdOut[i] = scal[3];
         }
       }
-      __syncthreads();
-      const int branch = (int)scal[4];
-      if (branch != 0) {
-        const double f1 = scal[1], f2 = scal[2];
-        for (int r = 1 + tid; r < n; r += nt) {
-          double t = v[r] * f1;
-          if (branch == 2) t = t * f2;
-          v[r] = t;
-        }
-      }
-      __syncthreads();
-      if (branch != 0 && tid == 0) v[0] = scal[3];
-      __syncthreads();
-      for (int r = tid; r < n; r += nt) {
-        gH[(size_t)i * N + r] = v[r];
-        const double vr = (r == 0) ? 1.0 : v[r];
-        vloc[r] = vr;
-        put_granule_dbl(gvp + 2 * r, tag, vr);
-      }
-      if (tid == 0) put_granule_dbl(gvp + 2 * N, tag, scal[0]);
-    } else {
-      // (v_0..v_{n-1}, tau) from the pivot's owner; tau lands in vloc[n]
-      const bool ok = poll_granule_dbls(gvp, n + 1, N, tag, vloc, abortw, errors);
-      if (__syncthreads_or(!ok)) return;
-      if (tid == 0) scal[0] = vloc[n];
     }
     __syncthreads();
     const double tau_i = scal[0];
-    if (tau_i == 0.0) continue;  // householder_transform gave tau = 0: no update
-    for (int r = tid; r < n; r += nt) tv[r] = tau_i * vloc[r];
-    __syncthreads();
-    // ---- dsymv chains of the owned active rows (rows i+1..N-1)
-    if (wid < 2 && lane < RW) {
-      const int r = g + lane * P;
-      if (r > i && r < N) {
-        const double *row = M + (size_t)lane * lda;
-        const int jr = r - i - 1;
-        if (wid == 0) {
-          double acc = 0.0;  // columns c = N-1 .. r+1, descending
-          int c = N - 1;
-          for (; c - 7 > r; c -= 8) {
-            double p[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) p[u] = tv[c - u - i - 1] * row[c - u];
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc += p[u];
-          }
-          for (; c > r; c--) acc += tv[c - i - 1] * row[c];
-          accb[lane] = acc + tv[jr] * row[r];
-        } else {
-          double t2 = 0.0;  // columns c = i+1 .. r-1, ascending
-          int c = i + 1;
-          for (; c + 8 <= r; c += 8) {
-            double p[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) p[u] = vloc[c + u - i - 1] * row[c + u];
-#pragma unroll
-            for (int u = 0; u < 8; u++) t2 += p[u];
-          }
-          for (; c < r; c++) t2 += vloc[c - i - 1] * row[c];
-          t2b[lane] = t2;
+    {
+      const int branch = (int)scal[4];
+      const double f1 = scal[1], f2 = scal[2];
+      for (int r = tid; r < n; r += nt) {
+        double t = v[r];
+        if (r > 0 && branch != 0) {
+          t = t * f1;
+          if (branch == 2) t = t * f2;
         }
+        if (g == writer) gH[(size_t)i * N + r] = (r == 0) ? scal[3] : t;
+        vloc[r] = (r == 0) ? 1.0 : t;
+        tv[r] = tau_i * ((r == 0) ? 1.0 : t);
       }
     }
     __syncthreads();
-    if (tid < RW) {
-      const int r = g + tid * P;
-      if (r > i && r < N) put_granule_dbl(gxp + 2 * (r - i - 1), tag, accb[tid] + tau_i * t2b[tid]);
-    }
-    {
-      const bool ok = poll_granule_dbls(gxp, n, -1, tag, xl, abortw, errors);
-      if (__syncthreads_or(!ok)) return;
-    }
-    // ---- xv = sum x_r v_r (sequential, staged) and alpha = -(tau/2) xv
-    if (wid == 0) {
-      double xv = 0.0;
-      for (int base = 0; base < n; base += 64) {
-        const int r = base + lane, rc = min(r, n - 1);
-        const double p_ = xl[rc] * vloc[rc];
-        sv[lane] = (r < n) ? p_ : 0.0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int cnt = (n - base) < 64 ? (n - base) : 64;
-        for (int l0 = 0; l0 < cnt; l0 += 8) {
-          double t[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) t[u] = sv[l0 + u];
-#pragma unroll
-          for (int u = 0; u < 8; u++) xv += t[u];
+    TMW_MARK(1)
+    if (tau_i != 0.0) {
+      // ---- dsymv: products staged by all threads, then the row chains
+      for (int k = 0; k < RW; k++) {
+        const int r = g + k * P;
+        if (r <= i || r >= N) continue;  // uniform
+        for (int q = tid; q < n; q += nt) {
+          const int c = i + 1 + q;
+          Pr[(size_t)k * lda + c] = ((c > r) ? tv[q] : vloc[q]) * M[(size_t)k * lda + c];
         }
-        __builtin_amdgcn_wave_barrier();
       }
-      if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
+      __syncthreads();
+      TMW_MARK(2)
+      if (wid < 2 && lane < RW) {
+        const int r = g + lane * P;
+        if (r > i && r < N) {
+          const double *pr = Pr + (size_t)lane * lda;
+          if (wid == 0)  // columns c = N-1 .. r+1, descending, then the diagonal
+            accb[lane] = staged_chain_desc(0.0, pr + r + 1, N - 1 - r) + tv[r - i - 1] * M[(size_t)lane * lda + r];
+          else  // columns c = i+1 .. r-1, ascending
+            t2b[lane] = staged_chain(0.0, pr + i + 1, r - i - 1);
+        }
+      }
+      __syncthreads();
+      if (tid < RW) {
+        const int r = g + tid * P;
+        if (r > i && r < N) put_granule_dbl(gxp + 2 * (r - i - 1), tag, accb[tid] + tau_i * t2b[tid]);
+      }
+      TMW_MARK(3)
+      {
+        // x of this step and, in the same sweep, the next pivot row as published
+        const int nb = (i >= 1 && i + 3 < N) ? n - 1 : 0;
+        const bool ok = poll_granule_dbls(gxp, n, xl, growp + 2 * (i + 2), nb, nrow + i + 2, tag, abortw, errors);
+        if (__syncthreads_or(!ok)) return;
+      }
+      TMW_MARK(4)
+      // ---- xv = sum x_r v_r (products staged in tv, one ordered chain); alpha = -(tau/2) xv
+      for (int r = tid; r < n; r += nt) tv[r] = xl[r] * vloc[r];
+      __syncthreads();
+      TMW_MARK(5)
+      if (tid == 0) scal[5] = -(tau_i / 2.0) * staged_chain(0.0, tv, n);
+      __syncthreads();
+      TMW_MARK(6)
+      {
+        const double alpha = scal[5];
+        for (int r = tid; r < n; r += nt) xl[r] += alpha * vloc[r];
+      }
+      __syncthreads();
+      TMW_MARK(7)
     }
-    __syncthreads();
-    {
-      const double alpha = scal[5];
-      for (int r = tid; r < n; r += nt) xl[r] += alpha * vloc[r];
+    // ---- next pivot row (i+1): as published (or from C at i = 0), plus this step's rank-2 update
+    if (i + 3 < N) {
+      if (i >= 1 && tau_i == 0.0) {  // (with tau != 0 it came with x)
+        const bool ok = poll_granule_dbls(growp + 2 * (i + 2), n - 1, nrow + i + 2, growp, 0, nrow, tag, abortw,
+                                          errors);
+        if (__syncthreads_or(!ok)) return;
+      }
+      TMW_MARK(8)
+      for (int c = i + 2 + tid; c < N; c += nt) {
+        double t = nrow[c];
+        if (tau_i != 0.0) {
+          const int a = c - i - 1;
+          const double tmp1 = -1.0 * vloc[a], tmp2 = -1.0 * xl[a];
+          t += tmp1 * xl[0] + tmp2 * vloc[0];
+        }
+        prow[c] = t;
+      }
     }
-    __syncthreads();
     // ---- dsyr2 (alpha = -1) on the owned active rows, both triangles
-    for (int idx = tid; idx < RW * n; idx += nt) {
-      const int k = idx / n, jj = idx % n, r = g + k * P;
-      if (r <= i || r >= N) continue;
-      const int jr = r - i - 1;
-      const int a = jr > jj ? jr : jj, b = jr > jj ? jj : jr;
-      const double tmp1 = -1.0 * vloc[a], tmp2 = -1.0 * xl[a];
-      M[(size_t)k * lda + i + 1 + jj] += tmp1 * xl[b] + tmp2 * vloc[b];
-    }
+    if (tau_i != 0.0)
+      for (int k = 0; k < RW; k++) {
+        const int r = g + k * P;
+        if (r <= i || r >= N) continue;  // uniform
+        const int jr = r - i - 1;
+        double *row = M + (size_t)k * lda + i + 1;
+        for (int jj = tid; jj < n; jj += nt) {
+          const int a = jr > jj ? jr : jj, b = jr > jj ? jj : jr;
+          const double tmp1 = -1.0 * vloc[a], tmp2 = -1.0 * xl[a];
+          row[jj] += tmp1 * xl[b] + tmp2 * vloc[b];
+        }
+      }
     __syncthreads();
+    TMW_MARK(9)
   }
+#undef TMW_MARK
+  if (tr)
+    for (int k = 0; k < 10; k++) trace[16 + k] += tacc[k];
   for (int k = tid; k < RW; k += nt) {
     const int r = g + k * P;
     if (r < N) {
       dOut[r] = M[(size_t)k * lda + r];
-      if (r + 1 < N) sdOut[r] = M[(size_t)k * lda + r + 1];
+      if (r == N - 2) sdOut[r] = M[(size_t)k * lda + r + 1];
     }
   }
 }
@@ -785,7 +817,7 @@ __global__ void __launch_bounds__(TMW_TPB) k_tridiag_mw(int N, const double *__r
 constexpr int UMW_COLS = 4;
 constexpr int UMW_TPB = 256;
 __host__ __device__ inline int umw_groups(int N) { return (N + UMW_COLS - 1) / UMW_COLS; }
-size_t umw_lds_bytes(int N) { return ((size_t)UMW_COLS * (N + 1) + 2 * (size_t)N + 16) * sizeof(double); }
+size_t umw_lds_bytes(int N) { return (2 * (size_t)UMW_COLS * (N + 1) + 3 * (size_t)N + 16 + 32) * sizeof(double); }
 
 __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__restrict__ gH,
                                                        const double *__restrict__ tau, double *gQt) {
@@ -795,6 +827,9 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
   double *Q = smem;                              // local k = column g + k P of Q
   double *hb = Q + (size_t)UMW_COLS * lda;       // 2 x N
   double *w = hb + 2 * (size_t)N;                // UMW_COLS
+  double *ts = w + 16;                           // tau, N (kept off the per-step critical path)
+  double *Pq = ts + N;                           // staged products col[r] h[r], UMW_COLS x lda
+  for (int i = tid; i < N; i += nt) ts[i] = tau[i];
   for (int idx = tid; idx < UMW_COLS * lda; idx += nt) {
     const int k = idx / lda, r = idx % lda;
     Q[idx] = (r < N && r == g + k * P) ? 1.0 : 0.0;
@@ -806,7 +841,7 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
   int buf = 0;
   for (int i = N - 3; i >= 0; i--) {
     const int n = N - i - 1;
-    const double ti = tau[i];
+    const double ti = ts[i];
     const double *h = hb + (size_t)buf * N;
     double pf[PF];
     if (i > 0) {
@@ -817,30 +852,23 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
       }
     }
     if (ti != 0.0) {
-      if (wid == 0 && lane < UMW_COLS) {
-        const int c = g + lane * P;
-        if (c > i && c < N) {
-          const double *col = Q + (size_t)lane * lda + (i + 1);
-          double wj = col[0];
-          int r = 1;
-          for (; r + 8 <= n; r += 8) {
-            double p[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) p[u] = col[r + u] * h[r + u];
-#pragma unroll
-            for (int u = 0; u < 8; u++) wj += p[u];
-          }
-          for (; r < n; r++) wj += col[r] * h[r];
-          w[lane] = wj;
-        }
+      for (int k = 0; k < UMW_COLS; k++) {
+        const int c = g + k * P;
+        if (c <= i || c >= N) continue;  // uniform
+        for (int r = 1 + tid; r < n; r += nt) Pq[(size_t)k * lda + r] = Q[(size_t)k * lda + i + 1 + r] * h[r];
       }
       __syncthreads();
-      for (int idx = tid; idx < UMW_COLS * n; idx += nt) {
-        const int k = idx / n, r = idx % n, c = g + k * P;
-        if (c <= i || c >= N) continue;
+      if (tid < UMW_COLS) {
+        const int c = g + tid * P;
+        if (c > i && c < N) w[tid] = staged_chain(Q[(size_t)tid * lda + i + 1], Pq + (size_t)tid * lda + 1, n - 1);
+      }
+      __syncthreads();
+      for (int k = 0; k < UMW_COLS; k++) {
+        const int c = g + k * P;
+        if (c <= i || c >= N) continue;  // uniform
         double *col = Q + (size_t)k * lda + (i + 1);
         const double wj = w[k];
-        col[r] = (r == 0) ? col[0] - ti * wj : col[r] - ti * h[r] * wj;
+        for (int r = tid; r < n; r += nt) col[r] = (r == 0) ? col[0] - ti * wj : col[r] - ti * h[r] * wj;
       }
     }
     if (i > 0) {
@@ -1170,8 +1198,10 @@ __global__ void __launch_bounds__(256) k_eigen_diag(int N, const double *__restr
 // ------------------------------------------------------------------------
 // Orchestration
 size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
-size_t tridiag_vec_bytes(int N) { return (size_t)(3 * N + 16 + (N > 64 ? N : 64)) * sizeof(double); }
-bool eig_use_lds(int N) { return eig_mat_bytes(N) + tridiag_vec_bytes(N) + 256 <= 160 * 1024; }
+size_t tridiag_vec_bytes(int N) { return (size_t)(3 * N + 16 + (N > 64 ? N : 64) + 8) * sizeof(double); }
+// one-workgroup phases (matrix in LDS) below N = 96; above, the multi-workgroup
+// ones measured faster (C2, N = 128: 0.89 + 0.21 ms vs 0.95 + 0.38 ms)
+bool eig_use_lds(int N) { return N < 96 && eig_mat_bytes(N) + tridiag_vec_bytes(N) + 256 <= 160 * 1024; }
 
 int EigenSolver::init(int N_, bool hostChase_) {
   N = N_;
@@ -1207,6 +1237,8 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipEventCreateWithFlags(&ev_chase, hipEventDisableTiming));
   }
   lds = eig_use_lds(N);
+  if (const char *e = getenv("KORALI_AMD_EIGEN_MW_MIN"))  // multi-workgroup phases from this N up
+    if (N >= atoi(e)) lds = false;
   if (!lds) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1250,7 +1282,7 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   else {
     KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), tmw_lds_bytes(N), s, N, C, gH, tau, d, sd,
-                       comm, errors);
+                       comm, errors, trace);
   }
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_tridiag", 1);

@@ -180,3 +180,18 @@ def test_chunked_mt_producer_bit_exact(monkeypatch, log2w):
         assert np.array_equal(dev["Current Mean"], o["Current Mean"]), g
     assert dev.get_rng(0) == o.rng(0).get_bytes()
     assert dev.get_rng(1) == o.rng(1).get_bytes()
+
+
+@pytest.mark.parametrize("Nv,lam", [(16, 64), (128, 4096)])
+def test_multi_workgroup_eigen_forced_bit_exact(monkeypatch, Nv, lam):
+    """The multi-workgroup tridiagonalisation / unpack (in-launch hand-offs,
+    redundant pivot rows) forced below its default threshold: bit-exact."""
+    monkeypatch.setenv("KORALI_AMD_EIGEN_MW_MIN", "0")
+    o, dev = oracle_and_device(Nv, lam, "rosenbrock", 4)
+    for g in (1, 2, 3, 4):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Current Mean", "Covariance Matrix"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
