@@ -51,7 +51,7 @@ STAGE_FLOPS = {
 
 # kernels behind each profiled stage (names as in profiles/<round>/*_pmc_traffic.csv)
 STAGE_KERNELS = {
-    "eigen_tridiag": ["kg::k_tridiag<true>"], "eigen_unpack": ["kg::k_unpack<true>"], "eigen_apply": ["kg::k_apply"],
+    "eigen_tridiag": ["kg::k_tridiag_mw"], "eigen_unpack": ["kg::k_unpack_mw"], "eigen_apply": ["kg::k_apply"],
     "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
     "covariance": ["kg::k_rankmu_mfma", "kg::k_adaptC_combine"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],

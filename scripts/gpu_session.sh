@@ -27,6 +27,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     profc3) step profc3 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c3" -o run --output-format csv -- python bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
+    profc4) step profc4 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c4" -o run --output-format csv -- python bench.py --workload c4 --steps 10 --warmup 2 ;;
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     c4) step c4 600 python tools/probe_c4.py ${C4_ARGS:-512 65536 3} ;;
     shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
