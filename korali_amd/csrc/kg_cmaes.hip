@@ -248,24 +248,38 @@ __global__ void k_gather_rows(int N, int lam, const int *__restrict__ assign, co
 // ------------------------------------------------------------ objective
 // examples/optimization/stochastic/_model/model.py: negative_rosenbrock
 // (:23-34), negative_ackley (:37-62), negative_sphere; sequential in d.
-__global__ void __launch_bounds__(64) k_objective(int N, int lam, int obj, const double *__restrict__ X,
-                                                  double *__restrict__ F, CmaesScalars *sc) {
-  __shared__ double tile[64][65];
-  const int t = threadIdx.x;
-  const int c0 = blockIdx.x * 64;
-  const int i = c0 + t;
+// 64 candidates per workgroup: all 256 threads load a 64 x 32 tile of the
+// population (coalesced, 8 independent loads each) and, for Ackley, evaluate
+// its cosines in parallel; the candidates' sums (sequential in d, the
+// reference's order) then run on one wave.
+constexpr int OB_C = 64, OB_D = 32;
+__global__ void __launch_bounds__(256) k_objective(int N, int lam, int obj, const double *__restrict__ X,
+                                                   double *__restrict__ F, CmaesScalars *sc) {
+  __shared__ double tile[OB_C][OB_D + 1];
+  __shared__ double ctile[OB_C][OB_D + 1];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * OB_C;
+  const int i = c0 + tid;
   double r0 = 0.0, r1 = 0.0, prev = 0.0;
   const double cc = 2. * 3.141592653589793;
-  for (int d0 = 0; d0 < N; d0 += 64) {
-    const int dn = (N - d0) < 64 ? (N - d0) : 64;
-    for (int r = 0; r < 64; r++) {
-      const int ii = c0 + r;
-      tile[r][t] = (ii < lam && t < dn) ? X[(size_t)ii * N + d0 + t] : 0.0;
+  for (int d0 = 0; d0 < N; d0 += OB_D) {
+    const int dn = (N - d0) < OB_D ? (N - d0) : OB_D;
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = tid + 256 * u, row = e >> 5, col = e & 31, ii = c0 + row;
+      v[u] = (ii < lam && col < dn) ? X[(size_t)ii * N + d0 + col] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = tid + 256 * u, row = e >> 5, col = e & 31;
+      tile[row][col] = v[u];
+      if (obj == KG_OBJ_NEGATIVE_ACKLEY) ctile[row][col] = cos_cr(cc * v[u]);
     }
     __syncthreads();
-    if (i < lam) {
+    if (tid < OB_C && i < lam) {
       for (int dd = 0; dd < dn; dd++) {
-        const double x = tile[t][dd];
+        const double x = tile[tid][dd];
         const int d = d0 + dd;
         if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
           if (d > 0) {
@@ -276,7 +290,7 @@ __global__ void __launch_bounds__(64) k_objective(int N, int lam, int obj, const
           prev = x;
         } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
           r0 += x * x;
-          r1 += cos_cr(cc * x);
+          r1 += ctile[tid][dd];
         } else {
           r0 += x * x;
         }
@@ -284,7 +298,7 @@ __global__ void __launch_bounds__(64) k_objective(int N, int lam, int obj, const
     }
     __syncthreads();
   }
-  if (i >= lam) return;
+  if (tid >= OB_C || i >= lam) return;
   double f;
   if (obj == KG_OBJ_NEGATIVE_ROSENBROCK)
     f = -r0;
@@ -405,6 +419,36 @@ __global__ void __launch_bounds__(1024) k_sort_small(int lam, int P2, const doub
   for (int q = threadIdx.x; q < lam; q += blockDim.x) out[q] = sv[q];
 }
 
+// Rank sort for populations up to RANK_MAX: rank(i) = #{j : j before i}
+// (descending F, ties by index — the same total order as the bitonic
+// network), every key against every key in parallel: workgroup b ranks keys
+// 16b..16b+15, its 16 thread groups each scanning one sixteenth of the
+// population (LDS broadcast reads).  One launch instead of the bitonic
+// network's many.
+constexpr int RANK_MAX = 16384;
+__global__ void __launch_bounds__(256) k_rank_sort(int lam, const double *__restrict__ F, unsigned *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) double rk[];
+  __shared__ unsigned part[16][17];
+  for (int q = threadIdx.x; q < lam; q += blockDim.x) rk[q] = F[q];
+  __syncthreads();
+  const int li = threadIdx.x & 15, p = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + li;
+  const double ki = (i < lam) ? rk[i] : 0.0;
+  const int per = (lam + 15) / 16, j0 = p * per, j1 = min(lam, j0 + per);
+  unsigned c = 0;
+  for (int j = j0; j < j1; j++) {
+    const double kj = rk[j];
+    c += (kj > ki || (kj == ki && j < i)) ? 1u : 0u;
+  }
+  part[p][li] = c;
+  __syncthreads();
+  if (threadIdx.x < 16 && i < lam) {
+    unsigned r = 0;
+    for (int q = 0; q < 16; q++) r += part[q][threadIdx.x];
+    out[r] = (unsigned)i;
+  }
+}
+
 __global__ void k_copy_idx(int lam, const unsigned *__restrict__ val, unsigned *__restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < lam) out[i] = val[i];
@@ -456,27 +500,64 @@ __global__ void __launch_bounds__(256) k_gather_selected(int N, int mu, const do
   for (int d = threadIdx.x; d < N; d += blockDim.x) Y[(size_t)i * N + d] = X[src + d];
 }
 
-// mean :603-609 and mean update :623-624 (sequential over the μ selected,
-// rows streamed from Y)
-__global__ void __launch_bounds__(64) k_mean(int N, int mu, const double *__restrict__ Y,
-                                             const double *__restrict__ w, double *mean, double *prevMean,
-                                             double *meanUpdate, const CmaesScalars *__restrict__ sc) {
-  const int d = blockIdx.x * 64 + threadIdx.x;
-  if (d >= N) return;
-  const double prev = mean[d];
+// mean :603-609 and mean update :623-624.  The sum over the μ selected rows
+// is sequential per d (the reference's order); a workgroup owns MN_D columns:
+// all its threads stream the products w_i Y[i][d] into LDS, 256 rows at a
+// time (next chunk loaded while the current one is summed), and MN_D lanes
+// of wave 0 add them in order (an add-only chain at the FP64 add latency).
+constexpr int MN_D = 8, MN_R = 256;
+__global__ void __launch_bounds__(256) k_mean(int N, int mu, const double *__restrict__ Y,
+                                              const double *__restrict__ w, double *mean, double *prevMean,
+                                              double *meanUpdate, const CmaesScalars *__restrict__ sc) {
+  __shared__ double buf[2][MN_R][MN_D + 1];
+  const int tid = threadIdx.x;
+  const int d0 = blockIdx.x * MN_D;
+  const int nd = (N - d0) < MN_D ? (N - d0) : MN_D;
+  const int nchunks = (mu + MN_R - 1) / MN_R;
+  double v[8];
+  auto fetch = [&](int chunk) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = tid + 256 * u, r = e >> 3, c = e & 7, i = chunk * MN_R + r;
+      v[u] = (i < mu && c < nd) ? w[i] * Y[(size_t)i * N + d0 + c] : 0.0;
+    }
+  };
+  auto put = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = tid + 256 * u;
+      buf[b][e >> 3][e & 7] = v[u];
+    }
+  };
+  fetch(0);
+  put(0);
+  __syncthreads();
   double acc = 0.;
-  int i = 0;
-  for (; i + 16 <= mu; i += 16) {
-    double v[16];
+  for (int ch = 0; ch < nchunks; ch++) {
+    if (ch + 1 < nchunks) fetch(ch + 1);
+    if (tid < nd) {
+      const int rn = (mu - ch * MN_R) < MN_R ? (mu - ch * MN_R) : MN_R;
+      const double(*bb)[MN_D + 1] = buf[ch & 1];
+      int r = 0;
+      for (; r + 8 <= rn; r += 8) {
+        double t[8];
 #pragma unroll
-    for (int q = 0; q < 16; q++) v[q] = w[i + q] * Y[(size_t)(i + q) * N + d];
+        for (int u = 0; u < 8; u++) t[u] = bb[r + u][tid];
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc += v[q];
+        for (int u = 0; u < 8; u++) acc += t[u];
+      }
+      for (; r < rn; r++) acc += bb[r][tid];
+    }
+    if (ch + 1 < nchunks) put((ch + 1) & 1);
+    __syncthreads();
   }
-  for (; i < mu; i++) acc += w[i] * Y[(size_t)i * N + d];
-  prevMean[d] = prev;
-  mean[d] = acc;
-  meanUpdate[d] = (acc - prev) / sc->sigma;
+  if (tid < nd) {
+    const int d = d0 + tid;
+    const double prev = mean[d];
+    prevMean[d] = prev;
+    mean[d] = acc;
+    meanUpdate[d] = (acc - prev) / sc->sigma;
+  }
 }
 
 // evolution paths :626-662 (+ the adaptC constants :693-694).  Both
@@ -1146,6 +1227,9 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32);
+  if (L <= RANK_MAX && (size_t)L * sizeof(double) > 64 * 1024)
+    KG_HIP(hipFuncSetAttribute((const void *)k_rank_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)((size_t)L * sizeof(double))));
   {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)
@@ -1271,7 +1355,7 @@ int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective) {
   KG_CHECK(objective >= 0 && objective <= 2, "unknown builtin objective");
   Stage st(h, "objective");
   const int rows = h->r1 - h->r0;
-  hipLaunchKernelGGL(k_objective, dim3((rows + 63) / 64), dim3(64), 0, h->stream, h->N, rows, objective,
+  hipLaunchKernelGGL(k_objective, dim3((rows + OB_C - 1) / OB_C), dim3(256), 0, h->stream, h->N, rows, objective,
                      h->X + (size_t)h->r0 * h->N, h->F + h->r0, h->sc);
   hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
   KG_HIP(hipGetLastError());
@@ -1302,7 +1386,10 @@ static int cmaes_sort(kg_cmaes_t h) {
     Stage st(h, "sort");
     int P2 = 1;
     while (P2 < L) P2 <<= 1;
-    if (P2 <= SORT_CHUNK) {
+    if (L <= RANK_MAX && L > 256) {
+      hipLaunchKernelGGL(k_rank_sort, dim3((L + 15) / 16), dim3(256), (size_t)L * sizeof(double), h->stream, L, h->F,
+                         h->idx);
+    } else if (P2 <= SORT_CHUNK) {
       hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, h->stream, L, P2, h->F, h->idx);
     } else {
       hipLaunchKernelGGL(k_sort_init, dim3((P2 + 1023) / 1024), dim3(1024), 0, h->stream, L, P2, h->F, h->sortKey,
@@ -1354,7 +1441,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                        (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
                        h->sc);
     hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y);
-    hipLaunchKernelGGL(k_mean, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->Y, h->w, h->mean,
+    hipLaunchKernelGGL(k_mean, dim3((N + MN_D - 1) / MN_D), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
                        h->prevMean, h->meanUpdate, h->sc);
     if (cmaes_paths(h, generation)) return 1;
   }
