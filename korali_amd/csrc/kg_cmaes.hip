@@ -1528,9 +1528,10 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
             "[korali_amd tridiag trace, cumulative s_memtime ticks] nrm2 %llu dsymv %llu xv %llu dsyr2 %llu; last QR: "
             "%d steps, %d rotations\n[korali_amd apply trace] groups %llu time-units %llu steps %llu ticks %llu\n"
             "[korali_amd multi-workgroup tridiag, writer wg] dnrm2 %llu householder %llu dsymv-stage %llu dsymv-chain "
-            "%llu x-gather %llu xv-stage %llu xv-chain %llu alpha %llu pivot-poll %llu update %llu\n",
+            "%llu x-gather %llu xv-stage %llu xv-chain %llu alpha %llu pivot-poll %llu update %llu\n"
+            "[korali_amd streamed apply] batches %llu steps-before-chase-done %llu ticks-to-first-batch %llu\n",
             t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7], t[16], t[17], t[18], t[19], t[20], t[21],
-            t[22], t[23], t[24], t[25]);
+            t[22], t[23], t[24], t[25], t[26], t[27], t[28]);
   }
   return check_errors(h);
 }

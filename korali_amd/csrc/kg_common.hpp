@@ -61,6 +61,7 @@ enum : uint32_t {
 // fence is involved.  Buffers are zeroed before every launch, tags are
 // phase + 1.
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) int gu32i_t;
 constexpr unsigned KG_SPIN_LIMIT = 1u << 21;  // ~seconds: a hang becomes an error
 
 __device__ inline void put_granule_dbl(unsigned long long *p, unsigned tag, double x) {

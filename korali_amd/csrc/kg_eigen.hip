@@ -21,6 +21,7 @@
 // Every +,-,*,/,sqrt is IEEE correctly rounded on gfx950 and the file is
 // compiled with -ffp-contract=off, so the result equals the oracle bit for
 // bit.
+#include <chrono>
 #include <cstdlib>
 
 #include "kg_eigen.hpp"
@@ -902,7 +903,28 @@ struct EigRec {
 
 EigenSolver::Rec::operator EigRec() const { return EigRec{hdr, cs, meta, eval, perm}; }
 
-__host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, int maxRot, double *gc, double *gs) {
+// progress word of a streamed chase: seq (24 bits) | done (1) | QR steps (39)
+__host__ __device__ inline unsigned long long chase_word(unsigned long long seq, int done, unsigned long long steps) {
+  return ((seq & 0xffffffULL) << 40) | ((unsigned long long)(done ? 1 : 0) << 39) | steps;
+}
+__host__ __device__ inline void chase_publish(unsigned long long *prog, unsigned long long w) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  if (prog) {
+    // host-coherent pinned memory may be write-combining on the CPU side:
+    // sfence drains the step's headers / rotations before the progress word,
+    // and the progress word itself right away
+    __builtin_ia32_sfence();
+    __atomic_store_n(prog, w, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+  }
+#else
+  (void)prog;
+  (void)w;
+#endif
+}
+
+__host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, int maxRot, double *gc, double *gs,
+                                        unsigned long long *prog = nullptr, unsigned long long seq = 0) {
   chop_small(N, d, sd);
   int b = N - 1, steps = 0, rot = 0, err = 0;
   while (b > 0) {
@@ -929,6 +951,7 @@ __host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, 
     r.hdr[2 * steps + 1] = nb;
     steps++;
     rot += nb - 1;
+    chase_publish(prog, chase_word(seq, 0, (unsigned long long)steps));
     chop_small(nb, d + a, sd + a);
   }
   // gsl_eigen_symmv_sort(ABS_ASC): selection sort, strict < on |e|
@@ -956,6 +979,7 @@ __host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, 
   r.meta[0] = steps;
   r.meta[1] = rot;
   r.meta[2] = err;
+  chase_publish(prog, chase_word(seq, 1, (unsigned long long)steps));
   return err;
 }
 
@@ -996,6 +1020,7 @@ __device__ inline double dpp_shr1(double x) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 constexpr int APPLY_HCAP = 256;  // step headers per LDS chunk
+constexpr int APPLY_MINSTEP = 16;  // streamed apply: smallest batch of new steps worth a chunk
 // rotations per LDS chunk: up to 4096, what fits next to the rows (>= N - 1,
 // one whole QR step, for every N the CMA-ES path accepts)
 __host__ __device__ inline int apply_cap(int N) {
@@ -1007,10 +1032,144 @@ __host__ __device__ inline size_t apply_lds_bytes(int N) {
   return (size_t)N * (APPLY_ROWS + 1) * sizeof(double) + 16 * (size_t)apply_cap(N) + 8 * APPLY_HCAP + 16;
 }
 
+// system-scope loads of host-coherent memory the host chase writes while
+// the kernel runs (bypass every GPU cache: no stale line from an earlier
+// generation can be read)
+__device__ inline int ld_sys(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline double ld_sys(const double *p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+// agent-scope (sc1) loads / stores of the device staging copy (R1 hand-off)
+__device__ inline int ld_agt(const int *p) {
+  return __hip_atomic_load((const gu32i_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double ld_agt(const double *p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((const gu64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ inline void st_agt(int *p, int v) {
+  __hip_atomic_store((gu32i_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_agt(double *p, double v) {
+  __hip_atomic_store((gu64_t *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Streamed chase, fetcher workgroup: copies what the host chase publishes
+// (host-coherent memory, read ONCE here) into the device staging buffers,
+// then publishes a device progress word; the apply workgroups read only
+// device memory.
+__device__ void apply_fetcher(int N, EigRec hr, EigRec dr, unsigned long long *hprog, unsigned long long *dprog,
+                              unsigned long long seq, unsigned int *errors, int *sh) {
+  const int tid = threadIdx.x;
+  int t0 = 0, ro0 = 0;
+  for (;;) {
+    if (tid == 0) {
+      unsigned long long w = 0;
+      int state = 0;
+      for (unsigned spins = 0;; spins++) {
+        w = __hip_atomic_load(hprog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((w >> 40) == (seq & 0xffffffULL) && (((w >> 39) & 1ULL) || (long long)(w & 0x7fffffffffULL) > t0)) {
+          state = (int)((w >> 39) & 1ULL);
+          break;
+        }
+        if (spins > KG_SPIN_LIMIT) {
+          atomicOr(errors, KG_ERR_SYNC_TIMEOUT);
+          state = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      sh[0] = (int)(w & 0x7fffffffffULL);
+      sh[1] = state;
+      sh[2] = 0;
+    }
+    __syncthreads();
+    const int avail = sh[0], state = sh[1];
+    if (state == 2) {
+      // publish "done" with an error so the apply workgroups stop waiting
+      if (tid == 0) {
+        st_agt(dr.meta + 2, 1);
+        __hip_atomic_store((gu64_t *)dprog, chase_word(seq, 1, (unsigned long long)t0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    // headers of the new steps and their rotation count; host reads are
+    // PCIe round trips, so every thread keeps 16 of them in flight
+    int rc = 0;
+    for (int t = t0 + tid; t < avail; t += APPLY_TPB * 8) {
+      int a[8], nb[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int tt = t + u * APPLY_TPB;
+        a[u] = (tt < avail) ? ld_sys(hr.hdr + 2 * (size_t)tt) : 0;
+        nb[u] = (tt < avail) ? ld_sys(hr.hdr + 2 * (size_t)tt + 1) : 1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int tt = t + u * APPLY_TPB;
+        if (tt < avail) {
+          st_agt(dr.hdr + 2 * (size_t)tt, a[u]);
+          st_agt(dr.hdr + 2 * (size_t)tt + 1, nb[u]);
+          rc += nb[u] - 1;
+        }
+      }
+    }
+    atomicAdd(&sh[2], rc);
+    __syncthreads();
+    const int nrot = sh[2];
+    {
+      const double *src = hr.cs + 2 * (size_t)ro0;
+      double *dst = dr.cs + 2 * (size_t)ro0;
+      const int tot = 2 * nrot;
+      for (int q = tid; q < tot; q += APPLY_TPB * 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int qq = q + u * APPLY_TPB;
+          v[u] = (qq < tot) ? ld_sys(src + qq) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int qq = q + u * APPLY_TPB;
+          if (qq < tot) st_agt(dst + qq, v[u]);
+        }
+      }
+    }
+    if (state == 1) {
+      for (int i = tid; i < N; i += APPLY_TPB) {
+        st_agt(dr.eval + i, ld_sys(hr.eval + i));
+        st_agt(dr.perm + i, ld_sys(hr.perm + i));
+      }
+      if (tid < 3) st_agt(dr.meta + tid, ld_sys(hr.meta + tid));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (R1)
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store((gu64_t *)dprog, chase_word(seq, state, (unsigned long long)avail), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    t0 = avail;
+    ro0 += nrot;
+    if (state == 1) return;
+  }
+}
+
+// kStream: the Givens chase runs on the host WHILE this kernel applies its
+// rotations: headers / rotations / eigenvalues are read from host-coherent
+// memory, a chunk as soon as the chase has published it (progress word with
+// a per-generation sequence number), so the apply trails the chase by about
+// one chunk instead of starting after it.
+template <bool kStream>
 __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__restrict__ gQt, EigRec r,
                                                      double *__restrict__ B, double *__restrict__ D, double *minEig,
                                                      double *maxEig, double *eigenFailures, unsigned int *errors,
-                                                     unsigned long long *trace) {
+                                                     unsigned long long *trace, unsigned long long *prog,
+                                                     unsigned long long seq, EigRec hr, unsigned long long *hprog) {
   unsigned long long ngroups = 0, nunits = 0, tstart = __builtin_amdgcn_s_memtime();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lda = N + 1;
@@ -1022,7 +1181,11 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   double *csh = Lq + (size_t)N * S;              // cap (c, s) pairs
   int *hsh = (int *)(csh + 2 * (size_t)cap);      // APPLY_HCAP (a, nb)
   int *chunk = hsh + 2 * APPLY_HCAP;
-  if (r.meta[2]) {
+  if (kStream && blockIdx.x == gridDim.x - 1) {  // the extra workgroup: fetcher
+    apply_fetcher(N, hr, r, hprog, prog, seq, errors, chunk);
+    return;
+  }
+  if (!kStream && r.meta[2]) {
     if (tid == 0 && blockIdx.x == 0) atomicOr(errors, KG_ERR_EIGEN);
     return;
   }
@@ -1030,14 +1193,55 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     const int c = idx / APPLY_ROWS, kl = idx % APPLY_ROWS;
     Lq[c * S + kl] = (kl < nrows) ? gQt[(size_t)c * lda + k0 + kl] : 0.0;
   }
-  const int steps = r.meta[0];
   const int kl = tid / APPLY_TEAM, s = tid % APPLY_TEAM;
   const int lane = tid & 63;
   int t0 = 0, ro0 = 0;
+  unsigned long long nchunks = 0, t_at_done = 0, tfirst = 0;
   __syncthreads();
-  while (t0 < steps) {
-    const int hn = min(APPLY_HCAP, steps - t0);
-    for (int idx = tid; idx < 2 * hn; idx += APPLY_TPB) hsh[idx] = r.hdr[2 * (size_t)t0 + idx];
+  for (;;) {
+    int avail;
+    if (kStream) {
+      if (tid == 0) {
+        unsigned long long w = 0;
+        int state = 0;
+        for (unsigned spins = 0;; spins++) {
+          w = __hip_atomic_load((gu64_t *)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // proceed on a batch of >= APPLY_MINSTEP new steps (the systolic groups
+          // need nested steps to fill a team) or when the chase is done
+          if ((w >> 40) == (seq & 0xffffffULL) &&
+              (((w >> 39) & 1ULL) || (long long)(w & 0x7fffffffffULL) >= t0 + APPLY_MINSTEP)) {
+            state = (int)((w >> 39) & 1ULL);
+            break;
+          }
+          if (spins > KG_SPIN_LIMIT) {
+            atomicOr(errors, KG_ERR_SYNC_TIMEOUT);
+            state = 2;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        chunk[2] = (int)(w & 0x7fffffffffULL);
+        chunk[3] = state;
+      }
+      __syncthreads();
+      avail = chunk[2];
+      const int state = chunk[3];
+      __syncthreads();
+      if (state == 2) return;  // the host never published: give up (error raised)
+      if (state == 1 && t_at_done == 0) t_at_done = (unsigned long long)t0 + 1;
+      if (nchunks == 0) tfirst = __builtin_amdgcn_s_memtime() - tstart;
+      nchunks++;
+      if (avail <= t0) {
+        if (state == 1) break;
+        continue;
+      }
+    } else {
+      avail = r.meta[0];
+      if (t0 >= avail) break;
+    }
+    const int hn = min(APPLY_HCAP, avail - t0);
+    for (int idx = tid; idx < 2 * hn; idx += APPLY_TPB)
+      hsh[idx] = kStream ? ld_agt(r.hdr + 2 * (size_t)t0 + idx) : r.hdr[2 * (size_t)t0 + idx];
     __syncthreads();
     if (tid < 64) {  // wave 0: the longest prefix of whole steps with <= cap rotations
       int base = 0, carry = 0, t1 = hn;
@@ -1063,7 +1267,8 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     }
     __syncthreads();
     const int tn = chunk[0], nrot = chunk[1];
-    for (int idx = tid; idx < 2 * nrot; idx += APPLY_TPB) csh[idx] = r.cs[2 * (size_t)ro0 + idx];
+    for (int idx = tid; idx < 2 * nrot; idx += APPLY_TPB)
+      csh[idx] = kStream ? ld_agt(r.cs + 2 * (size_t)ro0 + idx) : r.cs[2 * (size_t)ro0 + idx];
     __syncthreads();
     double *col = Lq + kl;  // col[c * S] = Q[k0 + kl][c]
     int t = 0, ro = 0;
@@ -1142,14 +1347,28 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   if (trace && tid == 0 && blockIdx.x == 0) {
     trace[4] += ngroups;
     trace[5] += nunits;
-    trace[6] += steps;
+    trace[6] += t0;
     trace[7] += __builtin_amdgcn_s_memtime() - tstart;
+    trace[26] += nchunks;
+    trace[27] += t_at_done ? t_at_done - 1 : 0;  // steps applied before the chase finished
+    trace[28] += tfirst;                          // ticks from kernel start to the first batch
+  }
+  if (kStream && ld_agt(r.meta + 2)) {  // the chase failed after streaming part of its steps
+    if (tid == 0 && blockIdx.x == 0) atomicOr(errors, KG_ERR_EIGEN);
+    return;
   }
   // updateEigensystem: min/max eigenvalue; keep old B, D if min <= 0
-  double mn = r.eval[0], mx = r.eval[0];
+  double *evs = csh;  // the rotation chunk is consumed: stage eval / perm in LDS
+  int *pms = (int *)(csh + N);
+  for (int i = tid; i < N; i += APPLY_TPB) {
+    evs[i] = kStream ? ld_agt(r.eval + i) : r.eval[i];
+    pms[i] = kStream ? ld_agt(r.perm + i) : r.perm[i];
+  }
+  __syncthreads();
+  double mn = evs[0], mx = evs[0];
   for (int i = 1; i < N; i++) {
-    mn = fmin(mn, r.eval[i]);
-    mx = fmax(mx, r.eval[i]);
+    mn = fmin(mn, evs[i]);
+    mx = fmax(mx, evs[i]);
   }
   if (mn <= 0.0) {
     if (tid == 0 && blockIdx.x == 0) *eigenFailures += 1.0;
@@ -1157,10 +1376,10 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   }
   for (int idx = tid; idx < nrows * N; idx += APPLY_TPB) {
     const int kk = idx / N, e = idx % N;
-    B[(size_t)(k0 + kk) * N + e] = Lq[(size_t)r.perm[e] * S + kk];
+    B[(size_t)(k0 + kk) * N + e] = Lq[(size_t)pms[e] * S + kk];
   }
   if (blockIdx.x == 0) {
-    for (int i = tid; i < N; i += APPLY_TPB) D[i] = sqrt(r.eval[i]);
+    for (int i = tid; i < N; i += APPLY_TPB) D[i] = sqrt(evs[i]);
     if (tid == 0) {
       *minEig = mn;
       *maxEig = mx;
@@ -1195,6 +1414,21 @@ __global__ void __launch_bounds__(256) k_eigen_diag(int N, const double *__restr
   }
 }
 
+// The tridiagonal (d, sd) straight into host-coherent memory, then a
+// sequence flag: the host chase starts as soon as it sees the flag (busy
+// poll), with no DMA completion or event wake-up in between.
+__global__ void __launch_bounds__(256) k_publish_dsd(int N, const double *__restrict__ dsd, double *hdsd,
+                                                     unsigned long long *hflag, unsigned long long seq) {
+  for (int i = threadIdx.x; i < 2 * N; i += blockDim.x)
+    __hip_atomic_store((unsigned long long *)(hdsd + i), (unsigned long long)__double_as_longlong(dsd[i]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the values before the flag
+    __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ------------------------------------------------------------------------
 // Orchestration
 size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
@@ -1206,7 +1440,7 @@ bool eig_use_lds(int N) { return N < 96 && eig_mat_bytes(N) + tridiag_vec_bytes(
 int EigenSolver::init(int N_, bool hostChase_) {
   N = N_;
   hostChase = hostChase_;
-  maxRot = 64 * N * N + 4096;
+  maxRot = 8 * N * N + 65536;  // GSL's implicit QR needs ~1.1 N^2 rotations
   const size_t mat = (size_t)N * (N + 1);
   KG_HIP(hipMalloc(&gA, mat * sizeof(double)));
   KG_HIP(hipMalloc(&gH, (size_t)N * N * sizeof(double)));
@@ -1222,12 +1456,25 @@ int EigenSolver::init(int N_, bool hostChase_) {
   KG_HIP(hipMalloc(&dev.perm, (size_t)N * sizeof(int)));
   KG_HIP(hipMemset(dev.meta, 0, 4 * sizeof(int)));
   if (hostChase) {
-    KG_HIP(hipHostMalloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocDefault));
-    KG_HIP(hipHostMalloc(&host.hdr, 2 * (size_t)(maxRot + N) * sizeof(int), hipHostMallocDefault));
-    KG_HIP(hipHostMalloc(&host.cs, 2 * (size_t)maxRot * sizeof(double), hipHostMallocDefault));
-    KG_HIP(hipHostMalloc(&host.meta, 4 * sizeof(int), hipHostMallocDefault));
-    KG_HIP(hipHostMalloc(&host.eval, (size_t)N * sizeof(double), hipHostMallocDefault));
-    KG_HIP(hipHostMalloc(&host.perm, (size_t)N * sizeof(int), hipHostMallocDefault));
+    KG_HIP(hipHostMalloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    KG_HIP(hipHostGetDevicePointer((void **)&d_dsd_map, h_dsd, 0));
+    // written by the host chase while k_apply<true> reads them: host-coherent, mapped
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    KG_HIP(hipHostMalloc(&host.hdr, 2 * (size_t)(maxRot + N) * sizeof(int), fl));
+    KG_HIP(hipHostMalloc(&host.cs, 2 * (size_t)maxRot * sizeof(double), fl));
+    KG_HIP(hipHostMalloc(&host.meta, 4 * sizeof(int), fl));
+    KG_HIP(hipHostMalloc(&host.eval, (size_t)N * sizeof(double), fl));
+    KG_HIP(hipHostMalloc(&host.perm, (size_t)N * sizeof(int), fl));
+    KG_HIP(hipHostMalloc(&hprog, 2 * sizeof(unsigned long long), fl));
+    hprog[0] = hprog[1] = 0;
+    KG_HIP(hipHostGetDevicePointer((void **)&hmap.hdr, host.hdr, 0));
+    KG_HIP(hipHostGetDevicePointer((void **)&hmap.cs, host.cs, 0));
+    KG_HIP(hipHostGetDevicePointer((void **)&hmap.meta, host.meta, 0));
+    KG_HIP(hipHostGetDevicePointer((void **)&hmap.eval, host.eval, 0));
+    KG_HIP(hipHostGetDevicePointer((void **)&hmap.perm, host.perm, 0));
+    KG_HIP(hipHostGetDevicePointer((void **)&dprog, hprog, 0));
+    KG_HIP(hipMalloc(&dprogDev, 2 * sizeof(unsigned long long)));
+    KG_HIP(hipMemset(dprogDev, 0, 2 * sizeof(unsigned long long)));
     KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
     hgc.resize(N);
     hgs.resize(N);
@@ -1249,17 +1496,20 @@ int EigenSolver::init(int N_, bool hostChase_) {
   const int attr = 160 * 1024;
   KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
   KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize,
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N)));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)apply_lds_bytes(N)));
   return 0;
 }
 
 EigenSolver::~EigenSolver() {
   for (void *p : {(void *)gA, (void *)gH, (void *)gQt, (void *)gWork, (void *)tau, (void *)dsd, (void *)chaseWork,
-                  (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm, (void *)comm})
+                  (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm, (void *)comm,
+                  (void *)dprogDev})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
-                  (void *)host.perm})
+                  (void *)host.perm, (void *)hprog})
     if (p) (void)hipHostFree(p);
   if (side) (void)hipStreamDestroy(side);
   if (ev_dsd) (void)hipEventDestroy(ev_dsd);
@@ -1288,8 +1538,9 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   if (prof) prof(profCtx, "eigen_tridiag", 1);
   EigRec devRec = dev;
   if (hostChase) {
-    KG_HIP(hipMemcpyAsync(h_dsd, dsd, 2 * (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
-    KG_HIP(hipEventRecord(ev_dsd, s));
+    dsdSeq = chaseSeq + 1;
+    hipLaunchKernelGGL(k_publish_dsd, dim3(1), dim3(256), 0, s, N, (const double *)dsd, d_dsd_map, dprog + 1, dsdSeq);
+    KG_HIP(hipGetLastError());
   } else {
     KG_HIP(hipEventRecord(ev_dsd, s));
     KG_HIP(hipStreamWaitEvent(side, ev_dsd, 0));
@@ -1305,25 +1556,40 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_unpack", 1);
   if (hostChase) {
-    // the GPU unpacks Q while this core runs the serial Givens chase
-    KG_HIP(hipEventSynchronize(ev_dsd));
+    // the apply kernel is queued behind the unpack and consumes the Givens
+    // rotations as this core's serial chase publishes them
+    const unsigned long long seq = ++chaseSeq;
+    if (prof) prof(profCtx, "eigen_apply", 0);
+    EigRec mr = hmap;
+    // one workgroup per 16 rows + the fetcher workgroup
+    hipLaunchKernelGGL(k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1), dim3(APPLY_TPB), apply_lds_bytes(N),
+                       s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace, dprogDev, seq, mr, dprog);
+    KG_HIP(hipGetLastError());
+    if (prof) prof(profCtx, "eigen_dsd_wait", 2);
+    {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)
+      const auto t0 = std::chrono::steady_clock::now();
+      while (__atomic_load_n(hprog + 1, __ATOMIC_ACQUIRE) != dsdSeq) {
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+          KG_HIP(hipStreamSynchronize(s));  // surfaces a device fault, if any
+          KG_CHECK(false, "eigensolver: tridiagonal never arrived on the host");
+        }
+      }
+    }
+    if (prof) prof(profCtx, "eigen_dsd_wait", 3);
     if (prof) prof(profCtx, "eigen_chase_host", 2);
     EigRec hr = host;
-    qr_chase(N, h_dsd, h_dsd + N, hr, maxRot, hgc.data(), hgs.data());
+    chase_publish(hprog, chase_word(seq, 0, 0));
+    qr_chase(N, h_dsd, h_dsd + N, hr, maxRot, hgc.data(), hgs.data(), hprog, seq);
     if (prof) prof(profCtx, "eigen_chase_host", 3);
-    const int steps = host.meta[0], rot = host.meta[1];
-    KG_HIP(hipMemcpyAsync(dev.meta, host.meta, 4 * sizeof(int), hipMemcpyHostToDevice, s));
-    KG_HIP(hipMemcpyAsync(dev.hdr, host.hdr, 2 * (size_t)steps * sizeof(int), hipMemcpyHostToDevice, s));
-    if (rot) KG_HIP(hipMemcpyAsync(dev.cs, host.cs, 2 * (size_t)rot * sizeof(double), hipMemcpyHostToDevice, s));
-    KG_HIP(hipMemcpyAsync(dev.eval, host.eval, (size_t)N * sizeof(double), hipMemcpyHostToDevice, s));
-    KG_HIP(hipMemcpyAsync(dev.perm, host.perm, (size_t)N * sizeof(int), hipMemcpyHostToDevice, s));
   } else {
     KG_HIP(hipStreamWaitEvent(s, ev_chase, 0));
+    if (prof) prof(profCtx, "eigen_apply", 0);
+    hipLaunchKernelGGL(k_apply<false>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS), dim3(APPLY_TPB), apply_lds_bytes(N),
+                       s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace,
+                       (unsigned long long *)nullptr, 0ULL, devRec, (unsigned long long *)nullptr);
+    KG_HIP(hipGetLastError());
   }
-  if (prof) prof(profCtx, "eigen_apply", 0);
-  hipLaunchKernelGGL(k_apply, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS), dim3(APPLY_TPB), apply_lds_bytes(N), s, N, gQt,
-                     devRec, B, D, minEig, maxEig, eigenFailures, errors, trace);
-  KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_apply", 1);
   return 0;
 }

@@ -43,8 +43,12 @@ class EigenSolver {
     double *eval = nullptr;
     int *perm = nullptr;
     operator EigRec() const;
-  } dev, host;
-  double *h_dsd = nullptr;
+  } dev, host, hmap;  // hmap: device aliases of the host-coherent chase buffers
+  unsigned long long *hprog = nullptr, *dprog = nullptr;  // streamed-chase progress word (host / device view)
+  unsigned long long chaseSeq = 0;
+  unsigned long long *dprogDev = nullptr;  // fetcher -> apply progress word (device memory)
+  double *h_dsd = nullptr, *d_dsd_map = nullptr;  // host-coherent d/sd and its device alias
+  unsigned long long dsdSeq = 0;
   std::vector<double> hgc, hgs;
   hipStream_t side = nullptr;
   hipEvent_t ev_dsd = nullptr, ev_chase = nullptr;

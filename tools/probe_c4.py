@@ -17,7 +17,7 @@ for g in range(2, 2 + gens):
 dev.synchronize()
 print("gens/s %.2f  ms/gen %.2f" % (gens / (time.perf_counter() - t0), (time.perf_counter() - t0) / gens * 1e3), flush=True)
 dev.profile(True)
-STAGES = ("eigen", "eigen_tridiag", "eigen_unpack", "eigen_chase_host", "eigen_apply", "rng_polar", "transform",
+STAGES = ("eigen", "eigen_tridiag", "eigen_unpack", "eigen_dsd_wait", "eigen_chase_host", "eigen_apply", "rng_polar", "transform",
           "rng_consume", "objective", "sort", "mean_paths", "covariance", "sigma")
 for st in ("init",) + STAGES:
     dev.profile_read(st)
