@@ -534,12 +534,19 @@ constexpr int TMW_TPB = 256;
 __host__ __device__ inline size_t tmw_lds_doubles(int N, int RW) {
   return 2 * (size_t)RW * (N + 1) + 5 * (size_t)N + 4 * 16 + 32;  // +32: chain read-ahead slack
 }
-__host__ __device__ inline int tmw_rows(int N) {
-  int rw = (N + 63) / 64;
+// rows per workgroup (<= 16): default spreads the rows over up to 256
+// workgroups (measured: more workgroups, fewer rows each, is faster — C2
+// 0.86 ms with 1 row vs 1.09 ms with 16; C4 7.4 ms with 2 vs 7.9 with 8);
+// KORALI_AMD_TMW_ROWS overrides
+int tmw_rows(int N) {
+  int rw = (N + 255) / 256;
+  if (const char *e = getenv("KORALI_AMD_TMW_ROWS")) rw = atoi(e);
+  if (rw < 1) rw = 1;
+  if (rw > 16) rw = 16;
   while (rw > 1 && tmw_lds_doubles(N, rw) * sizeof(double) > 150 * 1024) rw--;
   return rw;
 }
-__host__ __device__ inline int tmw_groups(int N) { return (N + tmw_rows(N) - 1) / tmw_rows(N); }
+int tmw_groups(int N) { return (N + tmw_rows(N) - 1) / tmw_rows(N); }
 size_t tmw_lds_bytes(int N) { return tmw_lds_doubles(N, tmw_rows(N)) * sizeof(double); }
 // comm buffer (u64 words): x granules [N][2N], pivot-row granules [N][2N],
 // abort word (+ pad to 16 bytes)
@@ -621,7 +628,7 @@ __global__ void __launch_bounds__(TMW_TPB) k_tridiag_mw(int N, const double *__r
                                                         unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
-  const int P = gridDim.x, g = blockIdx.x, RW = tmw_rows(N), lda = N + 1;
+  const int P = gridDim.x, g = blockIdx.x, RW = (N + P - 1) / P, lda = N + 1;
   double *M = smem;                         // local row k = global row g + k P
   double *Pr = M + (size_t)RW * lda;        // staged dsymv products, same shape
   double *prow = Pr + (size_t)RW * lda;     // current pivot row, indexed by column
