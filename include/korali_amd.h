@@ -146,8 +146,8 @@ enum kg_likelihood { KG_LIK_GAUSSIAN = 0 }; /* -0.5*sum(x^2), model.py:32-37 */
 typedef struct {
   size_t variable_count;  /* N */
   size_t population_size; /* P ("Population Size") */
-  double max_chain_length;               /* must be 1 on device for now ("Max Chain Length") */
-  double default_burn_in;                /* must be 0 on device for now ("Default Burn In") */
+  double max_chain_length;               /* "Max Chain Length" (>= 1) */
+  double default_burn_in;                /* "Burn In" (TMCMC.config "Default Burn In", >= 0) */
   double target_cov;                     /* "Target Coefficient Of Variation" */
   double covariance_scaling;             /* "Covariance Scaling" */
   double min_annealing_exponent_update;  /* "Min Annealing Exponent Update" */
@@ -165,6 +165,10 @@ typedef struct {
   uint64_t multinomial_seed, multivariate_seed, uniform_seed;
   int likelihood;                        /* enum kg_likelihood */
   int device;
+  /* "Per Generation Burn In": entry k is the burn-in of generation k+2
+   * (setBurnIn, TMCMC.cpp.base:781-789); NULL / 0 entries: Burn In only */
+  const double *per_generation_burn_in;
+  size_t per_generation_burn_in_count;
 } kg_tmcmc_cfg;
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
@@ -179,19 +183,31 @@ int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t 
 int kg_tmcmc_get_rng(kg_tmcmc_t h, int which, void *state5000);
 int kg_tmcmc_set_rng(kg_tmcmc_t h, int which, const void *state5000);
 /* the stages of one generation:
- *   prepare  = (gen 1: setInitialConfiguration :21-105) + prepareGeneration :159-227
+ *   prepare  = (gen 1: setInitialConfiguration :21-105) + prepareGeneration :159-227;
+ *              the first candidate of every started chain is pending evaluation
  *   evaluate = Bayesian::evaluate with the builtin likelihood (bayesian.cpp.base:24-84)
- *   process  = processCandidate for every chain :229-252 + processGeneration :254-381 */
+ *              of the pending candidates
+ *   advance  = one step of every unfinished chain (runGeneration's WAITANY loop
+ *              :112-144 + processCandidate :229-252): accept / reject, database
+ *              entry past the burn-in, and the next candidate of chains with
+ *              steps left, which become pending; *pending = their number.
+ *              Chains run Chain Lengths[c] + Current Burn In steps, in the
+ *              Sequential conduit's chain-major RNG order.
+ *   process  = the remaining steps (builtin likelihood) + processGeneration :254-381 */
 int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation);
 int kg_tmcmc_evaluate(kg_tmcmc_t h);
+int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending);
+/* P flags: 1 where the chain's candidate awaits evaluation */
+int kg_tmcmc_get_pending(kg_tmcmc_t h, unsigned char *mask);
 int kg_tmcmc_process(kg_tmcmc_t h, size_t generation);
-/* host-callback likelihoods (KORALI_START/WAITALL of TMCMC::runGeneration
- * :114-144): kg_tmcmc_evaluate_prior forms the uniform log-priors on the
- * device ("Chain Candidates LogPriors"; -inf prior -> logLikelihood -inf,
- * bayesian.cpp.base:56-77), then the host reads the P x N candidates, runs
- * the model where the prior is finite and hands back the log-likelihoods
- * (set_field "Chain Candidates LogLikelihoods"), or sets both at once with
- * kg_tmcmc_set_evaluations. */
+/* host-callback likelihoods (KORALI_START/WAITANY of TMCMC::runGeneration
+ * :114-144): kg_tmcmc_evaluate_prior forms the uniform log-priors of the
+ * pending candidates on the device ("Chain Candidates LogPriors"; -inf prior
+ * -> logLikelihood -inf, bayesian.cpp.base:56-77), then the host reads the
+ * P x N candidates, runs the model for pending chains whose prior is finite
+ * and hands both back with kg_tmcmc_set_evaluations (entries of chains that
+ * are not pending are ignored), then calls kg_tmcmc_advance; repeat while
+ * chains are pending, then kg_tmcmc_process. */
 int kg_tmcmc_evaluate_prior(kg_tmcmc_t h);
 int kg_tmcmc_get_candidates(kg_tmcmc_t h, double *X, size_t ld);
 int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double *log_likelihood);

@@ -1,6 +1,6 @@
 // kg_tmcmc.hip — TMCMC generation (TMCMC::runGeneration, TMCMC.cpp.base:107-157)
-// on the device, Version "TMCMC", Max Chain Length 1, Burn In 0 (the C3
-// configuration).
+// on the device, Version "TMCMC" with any Max Chain Length / Burn In / Per
+// Generation Burn In.
 //
 // Work split (same rationale as the eigensolver):
 //   device — Cholesky of the proposal covariance, P x N polar normals from the
@@ -104,12 +104,26 @@ __global__ void __launch_bounds__(256) k_tm_cholesky(int N, const double *__rest
 }
 
 // --------------------------------------------------------- candidates
+// Step schedule of chain c in one generation (host-computed prefix sums over
+// the chains in chain order, the Sequential conduit's completion order):
+// S steps (Chain Lengths[c] + Current Burn In), its first Uniform draw u0,
+// its first row z0 of the extra Multivariate normals (one row per candidate
+// after the first), its first database entry db0.
+struct ChainSched {
+  unsigned S, u0, z0, db0;
+};
+
 // generateCandidate :560-566 -> gsl_ran_multivariate_gaussian (normals from
 // the polar pass, dtrmv Lower/NoTrans/NonUnit in gslcblas order, + zero mean)
 // then + leader.  One thread per (chain, i): x_i = (sum_{j<i} z_j L_ij) + z_i L_ii.
+// kRound: the candidate after step s of chain c (only chains with S > s;
+// normal row z0 + s - 1), which then becomes pending; otherwise row c for
+// every chain (prepareGeneration :222-225).
+template <bool kRound>
 __global__ void __launch_bounds__(256) k_tm_draw(int N, int P, const double *__restrict__ Z,
                                                  const double *__restrict__ Lg, const double *__restrict__ leaders,
-                                                 double *__restrict__ cand) {
+                                                 double *__restrict__ cand, const ChainSched *__restrict__ sch,
+                                                 int s, unsigned char *__restrict__ pend) {
   extern __shared__ double sm[];
   const int S = N + 1;
   double *Ls = sm;            // N x (N+1)
@@ -119,12 +133,24 @@ __global__ void __launch_bounds__(256) k_tm_draw(int N, int P, const double *__r
   for (int e = threadIdx.x; e < N * N; e += blockDim.x) Ls[(e / N) * S + e % N] = Lg[e];
   for (int e = threadIdx.x; e < CB * N; e += blockDim.x) {
     const int c = c0 + e / N;
-    zs[e] = c < P ? Z[(size_t)c * N + e % N] : 0.0;
+    double z = 0.0;
+    if (c < P) {
+      if (!kRound)
+        z = Z[(size_t)c * N + e % N];
+      else if ((int)sch[c].S > s)
+        z = Z[((size_t)sch[c].z0 + s - 1) * N + e % N];
+    }
+    zs[e] = z;
   }
   __syncthreads();
   for (int e = threadIdx.x; e < CB * N; e += blockDim.x) {
     const int cl = e / N, i = e % N, c = c0 + cl;
     if (c >= P) continue;
+    if (kRound) {
+      const bool more = (int)sch[c].S > s;
+      if (i == 0) pend[c] = more ? 1 : 0;
+      if (!more) continue;
+    }
     const double *z = zs + cl * N;
     const double *Li = Ls + i * S;
     double temp = 0.0;
@@ -156,9 +182,9 @@ __global__ void k_tm_prior(int N, int P, const double *__restrict__ U, const uns
 __global__ void k_tm_evaluate(int N, int P, int lik, const double *__restrict__ cand,
                               const double *__restrict__ negLogWidth, const double *__restrict__ pmin,
                               const double *__restrict__ pmax, double *__restrict__ candLL,
-                              double *__restrict__ candLP) {
+                              double *__restrict__ candLP, const unsigned char *__restrict__ pend) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= P) return;
+  if (c >= P || !pend[c]) return;
   const double *x = cand + (size_t)c * N;
   double lp = 0.0;
   for (int d = 0; d < N; d++) lp += (x[d] >= pmin[d] && x[d] <= pmax[d]) ? negLogWidth[d] : -INFINITY;
@@ -171,6 +197,22 @@ __global__ void k_tm_evaluate(int N, int P, int lik, const double *__restrict__ 
     ll = -0.5 * ss;
   }
   candLL[c] = ll;
+}
+
+// host-evaluated log-prior / log-likelihood of the pending chains
+__global__ void k_tm_set_pending(int P, const unsigned char *__restrict__ pend, const double *__restrict__ lp,
+                                 const double *__restrict__ ll, double *__restrict__ candLP,
+                                 double *__restrict__ candLL) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P || !pend[c]) return;
+  candLP[c] = lp[c];
+  candLL[c] = ll[c];
+}
+
+// chains c < started are pending their first evaluation (runGeneration :114-130)
+__global__ void k_tm_pend_init(int P, int started, unsigned char *__restrict__ pend) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < P) pend[c] = c < started ? 1 : 0;
 }
 
 __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const double *__restrict__ pmax,
@@ -217,6 +259,57 @@ __global__ void k_tm_copy_rows(int N, int P, const unsigned char *__restrict__ a
     leaders[e] = v;
   }
   db[e] = v;
+}
+
+// step s (1-based) of every chain with S >= s (runGeneration :132-143 +
+// processCandidate :229-252): one Uniform (u0 + s - 1), accept if P > U or
+// generation 1, counted and entered into the database only past the burn-in
+// B (entry db0 + s - B - 1).
+__global__ void k_tm_round_accept(int nc, int s, int B, int gen1, double rho, const ChainSched *__restrict__ sch,
+                                  const double *__restrict__ U, const double *__restrict__ candLL,
+                                  const double *__restrict__ candLP, double *__restrict__ leadLL,
+                                  double *__restrict__ leadLP, double *__restrict__ dbLL, double *__restrict__ dbLP,
+                                  unsigned char *__restrict__ acc, TmDev *dev) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  bool counted = false;
+  if (c < nc) {
+    const ChainSched q = sch[c];
+    if ((int)q.S >= s) {
+      double p = 0.0;
+      const double lpc = candLP[c], llc = candLL[c];
+      if (isfinite(lpc) && isfinite(llc)) p = exp_cr((llc - leadLL[c]) * rho + (lpc - leadLP[c]));
+      const bool a = (p > U[(size_t)q.u0 + s - 1]) || gen1;
+      acc[c] = a ? 1 : 0;
+      if (a) {
+        leadLL[c] = llc;
+        leadLP[c] = lpc;
+      }
+      if (s > B) {
+        const size_t k = (size_t)q.db0 + s - B - 1;
+        dbLL[k] = leadLL[c];
+        dbLP[k] = leadLP[c];
+        counted = a;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(counted);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&dev->accepted, (unsigned int)__popcll(m));
+}
+
+__global__ void k_tm_round_rows(int N, int nc, int s, int B, const ChainSched *__restrict__ sch,
+                                const unsigned char *__restrict__ acc, const double *__restrict__ cand,
+                                double *__restrict__ leaders, double *__restrict__ db) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)nc * N) return;
+  const int c = (int)(e / N);
+  const ChainSched q = sch[c];
+  if ((int)q.S < s) return;
+  double v = leaders[e];
+  if (acc[c]) {
+    v = cand[e];
+    leaders[e] = v;
+  }
+  if (s > B) db[((size_t)q.db0 + s - B - 1) * N + e % N] = v;
 }
 
 // first-index maximum of a_i = v_i * scale (scale applied when use_scale),
@@ -538,21 +631,27 @@ __global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *
   }
 }
 
-// leader expansion :331-360 with Max Chain Length 1: leader j = database
-// entry src[j], chain length 1
-__global__ void k_tm_expand(int N, int P, const unsigned *__restrict__ src, const double *__restrict__ db,
+// leader expansion :331-360: leader j < count = database entry src[j] with
+// chain length len[j]; chain lengths past count are 0 and those leaders keep
+// their previous rows (std::fill of _chainLengths, :329)
+__global__ void k_tm_expand(int N, int P, int count, const unsigned *__restrict__ src,
+                            const double *__restrict__ len, const double *__restrict__ db,
                             const double *__restrict__ dbLL, const double *__restrict__ dbLP,
                             double *__restrict__ leaders, double *__restrict__ leadLL, double *__restrict__ leadLP,
                             double *__restrict__ chainLen) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)P * N) return;
   const int j = (int)(e / N), d = (int)(e % N);
+  if (j >= count) {
+    if (d == 0) chainLen[j] = 0.0;
+    return;
+  }
   const unsigned s = src[j];
   leaders[e] = db[(size_t)s * N + d];
   if (d == 0) {
     leadLL[j] = dbLL[s];
     leadLP[j] = dbLP[s];
-    chainLen[j] = 1.0;
+    chainLen[j] = len[j];
   }
 }
 
@@ -765,8 +864,13 @@ struct kg_tmcmc_s {
   double *fA = nullptr, *fB = nullptr;  // P x N term factors of the ordered sums (+2 padding)    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
   unsigned *src = nullptr;
-  unsigned char *acc = nullptr;
+  unsigned char *acc = nullptr, *pend = nullptr;
   TmDev *dev = nullptr;
+  // chain steps (Max Chain Length > 1 / burn-in): per-chain schedule, the
+  // generation's Uniform draws and its extra Multivariate normals
+  ChainSched *sch = nullptr, *hSch = nullptr;
+  double *Zx = nullptr, *dLen = nullptr, *hLenD = nullptr;
+  size_t capU = 0, capZx = 0;
   // pinned host staging
   double *hE = nullptr, *hW = nullptr, *hNsel = nullptr;
   void *hCv = nullptr;                       // CvOut[CV_MAX_PTS + 1] (host)
@@ -779,6 +883,11 @@ struct kg_tmcmc_s {
   TmDev *hDev = nullptr;
   std::vector<double> wtmp;
   std::vector<unsigned> nsel;
+  std::vector<double> perGenBurnIn;  // "Per Generation Burn In"
+  std::vector<unsigned> hLen;        // host mirror of "Chain Lengths"
+  int step = 0, maxSteps = 1;        // chain steps done / needed this generation
+  size_t pendingCount = 0;           // chains whose candidate awaits evaluation
+  bool rounds = false;               // this generation needs the general step schedule
   // per-distribution prior layout
   std::vector<int> distOf;           // variable -> distribution
   std::vector<size_t> distVars;      // variables per distribution
@@ -790,7 +899,8 @@ struct kg_tmcmc_s {
   // scalars (TMCMC.config internal settings)
   double annealingExponent = 0, previousAnnealingExponent = 0, logEvidence = 0, coefficientOfVariation = 0,
          maxLoglikelihood = -INFINITY, chainCount = 0, acceptedSamplesCount = 0, proposalsAcceptanceRate = 0,
-         selectionAcceptanceRate = 0, dbCount = 0, modelEvaluationCount = 0, minSearchIterations = 0;
+         selectionAcceptanceRate = 0, dbCount = 0, modelEvaluationCount = 0, minSearchIterations = 0,
+         currentBurnIn = 0;
   double exactEvalsD = 0;  // diagnostics: host-exact cv2 evaluations so far
   bool devPending = false;  // accepted count / maxLoglikelihood not yet read back
   // profiling
@@ -1165,6 +1275,63 @@ int tm_initialize(kg_tmcmc_s *h) {
   h->chainCount = h->P;
   hipLaunchKernelGGL(k_tm_fill, dim3(nblk(h->P, 256)), dim3(256), 0, h->stream, h->chainLen, (size_t)h->P, 1.0);
   KG_HIP(hipGetLastError());
+  h->hLen.assign(h->P, 1u);
+  return 0;
+}
+
+// setBurnIn :781-789
+double tm_burn_in(const kg_tmcmc_s *h, size_t gen) {
+  if (gen <= 1) return 0.0;
+  if (gen - 2 < h->perGenBurnIn.size()) return h->perGenBurnIn[gen - 2];
+  return h->cfg.default_burn_in;
+}
+
+template <typename T>
+int tm_ensure(T **p, size_t &cap, size_t n) {
+  if (n <= cap) return 0;
+  if (*p) KG_HIP(hipFree(*p));
+  *p = nullptr;
+  cap = 0;
+  if (tdalloc(p, n)) return 1;
+  cap = n;
+  return 0;
+}
+
+// The first step of every chain needs no Uniform index bookkeeping when all
+// chains run exactly one step (Max Chain Length 1 selections, no burn-in):
+// chain c draws Uniform c and writes database entry c.  Otherwise the step
+// schedule (prefix sums in chain order) is built here and uploaded.
+int tm_schedule(kg_tmcmc_s *h) {
+  const size_t nc = (size_t)h->chainCount, B = (size_t)h->currentBurnIn;
+  KG_CHECK(nc <= (size_t)h->P && h->hLen.size() == (size_t)h->P, "inconsistent Chain Count / Chain Lengths");
+  h->rounds = !(B == 0 && nc == (size_t)h->P);
+  h->step = 0;
+  h->maxSteps = 1;
+  if (!h->rounds) return 0;
+  size_t u = 0, z = 0, db = 0;
+  for (size_t c = 0; c < nc; c++) {
+    const size_t S = h->hLen[c] + B;
+    KG_CHECK(S >= 1, "a started chain has zero steps (Chain Lengths 0 with Burn In 0)");
+    h->hSch[c] = ChainSched{(unsigned)S, (unsigned)u, (unsigned)z, (unsigned)db};
+    u += S;
+    z += S - 1;
+    db += h->hLen[c];
+    h->maxSteps = std::max(h->maxSteps, (int)S);
+  }
+  KG_CHECK(db == (size_t)h->P, "the chain lengths of the started chains must sum to the population size");
+  KG_CHECK(u < (1ull << 32) && z < (1ull << 32), "chain schedule exceeds 32-bit indexing");
+  KG_HIP(hipMemcpyAsync(h->sch, h->hSch, nc * sizeof(ChainSched), hipMemcpyHostToDevice, h->stream));
+  // the generation's Uniform draws (one per step, chain-major) and its extra
+  // candidates' normals (after prepareGeneration's P x N)
+  if (tm_ensure(&h->U, h->capU, u)) return 1;
+  if (h->uniform.uniforms(h->U, u, h->stream)) return 1;
+  const size_t M = z * (size_t)h->N;
+  if (M) {
+    if (tm_ensure(&h->Zx, h->capZx, M)) return 1;
+    TmStage st(h, "rng_polar");
+    if (h->multivariate.polar_normals(h->Zx, M, h->N, nullptr, h->stream)) return 1;
+    if (h->multivariate.consume_normals(M, h->N, nullptr, h->stream)) return 1;
+  }
   return 0;
 }
 
@@ -1214,6 +1381,7 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Database Entries", dbCount)
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Min Search Iterations", minSearchIterations)
+  SCA("Current Burn In", currentBurnIn)
   SCA("Exact Search Evaluations", exactEvalsD)
 #undef VEC
 #undef SCA
@@ -1229,8 +1397,14 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   KG_CHECK(cfg->variable_count >= 1 && cfg->variable_count <= (size_t)TM_MAX_N,
            "device TMCMC path supports 1..120 variables");
   KG_CHECK(cfg->population_size >= 2, "TMCMC 'Population Size' must be at least 2");
-  KG_CHECK(cfg->max_chain_length == 1.0, "device TMCMC path supports 'Max Chain Length' 1 only");
-  KG_CHECK(cfg->default_burn_in == 0.0, "device TMCMC path supports 'Default Burn In' 0 only");
+  KG_CHECK(cfg->max_chain_length >= 1.0 && cfg->max_chain_length == floor(cfg->max_chain_length),
+           "Max Chain Length must be a positive integer");
+  KG_CHECK(cfg->default_burn_in >= 0.0 && cfg->default_burn_in == floor(cfg->default_burn_in),
+           "Burn In must be a non-negative integer");
+  for (size_t k = 0; k < cfg->per_generation_burn_in_count; k++)
+    KG_CHECK(cfg->per_generation_burn_in && cfg->per_generation_burn_in[k] >= 0.0 &&
+                 cfg->per_generation_burn_in[k] == floor(cfg->per_generation_burn_in[k]),
+             "Per Generation Burn In entries must be non-negative integers");
   KG_CHECK(cfg->covariance_scaling > 0.0, "Covariance Scaling must be larger 0.0");  // TMCMC.cpp.base:28
   KG_CHECK(cfg->prior_min && cfg->prior_max, "prior_min / prior_max are required");
   KG_CHECK(cfg->likelihood == KG_LIK_GAUSSIAN, "unknown builtin likelihood");
@@ -1238,6 +1412,11 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   upload_dd_tables();
   auto *h = new kg_tmcmc_s();
   h->cfg = *cfg;
+  h->cfg.per_generation_burn_in = nullptr;
+  if (cfg->per_generation_burn_in_count)
+    h->perGenBurnIn.assign(cfg->per_generation_burn_in, cfg->per_generation_burn_in + cfg->per_generation_burn_in_count);
+  double maxBurn = cfg->default_burn_in;
+  for (double b : h->perGenBurnIn) maxBurn = std::max(maxBurn, b);
   const int N = (int)cfg->variable_count, P = (int)cfg->population_size;
   h->N = N;
   h->P = P;
@@ -1275,8 +1454,10 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   rc |= tdalloc(&h->cov, (size_t)N * N) | tdalloc(&h->chol, (size_t)N * N) | tdalloc(&h->db, PN);
   rc |= tdalloc(&h->dbLL, P) | tdalloc(&h->dbLP, P) | tdalloc(&h->numSel, P) | tdalloc(&h->pmin, N);
   rc |= tdalloc(&h->pmax, N) | tdalloc(&h->negLogWidth, N) | tdalloc(&h->Z, PN) | tdalloc(&h->U, P);
+  h->capU = P;
   rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)(CV_MAX_PTS + 1) * P) | tdalloc(&h->w, P);
   rc |= tdalloc(&h->uoff, N) | tdalloc(&h->ustride, N) | tdalloc(&h->src, P) | tdalloc(&h->acc, P);
+  rc |= tdalloc(&h->pend, P) | tdalloc(&h->sch, P) | tdalloc(&h->dLen, P);
   rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
   rc |= tdalloc(&h->fA, PN + 2) | tdalloc(&h->fB, PN + 2);
   rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
@@ -1288,6 +1469,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   KG_HIP(hipHostMalloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hSrc, (size_t)P * sizeof(unsigned), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hSch, (size_t)P * sizeof(ChainSched), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hLenD, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hDev, sizeof(TmDev), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hCv, (CV_MAX_PTS + 1) * sizeof(CvOut), hipHostMallocDefault));
   KG_HIP(hipHostMalloc((void **)&h->hRec, 4 * (CV_MAX_PTS + 1) * sizeof(double2),
@@ -1318,7 +1501,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
                                (int)ws_lds_bytes(N, true)));
     const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)std::max(1, 256 / N) * N * sizeof(double);
     if (lbytes > 64 * 1024) {
-      KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
+      KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
+      KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
       KG_HIP(hipFuncSetAttribute((const void *)k_tm_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)((size_t)N * (N + 1) * sizeof(double))));
     }
@@ -1326,7 +1510,11 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   }
   hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(N, 64)), dim3(64), 0, h->stream, N, h->pmin, h->pmax, h->negLogWidth);
   KG_HIP(hipGetLastError());
-  if (h->multivariate.init(3 * h->multivariate.words_for_normals(PN) + 4096) || h->uniform.init(4 * (size_t)P + 4096)) {
+  // per generation: P x N normals for prepareGeneration and up to
+  // P (1 + burn-in) x N for the chains' later steps; one Uniform per step
+  const size_t steps = (size_t)P * (size_t)(1.0 + maxBurn);
+  if (h->multivariate.init(3 * h->multivariate.words_for_normals(PN + steps * N) + 4096) ||
+      h->uniform.init(4 * steps + 4096)) {
     delete h;
     return 1;
   }
@@ -1344,6 +1532,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     if (h->priorRng[k]->import_gsl(st, h->stream)) return 1;
   }
   h->chainCount = P;
+  h->hLen.assign(P, 1u);
   *out = h;
   return 0;
 }
@@ -1357,10 +1546,12 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->db, (void *)h->dbLL, (void *)h->dbLP, (void *)h->numSel, (void *)h->pmin,
                   (void *)h->pmax, (void *)h->negLogWidth, (void *)h->Z, (void *)h->U, (void *)h->Uprior,
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
-                  (void *)h->dev, h->cvPart, (void *)h->pairs,
+                  (void *)h->dev, h->cvPart, (void *)h->pairs, (void *)h->pend, (void *)h->sch, (void *)h->Zx,
+                  (void *)h->dLen,
                   (void *)h->fA, (void *)h->fB})
     if (p) (void)hipFree(p);
-  for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec})
+  for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
+                  (void *)h->hSch, (void *)h->hLenD})
     if (p) (void)hipHostFree(p);
   for (auto *r : h->priorRng) delete r;
   for (auto &t : h->pending) {
@@ -1378,6 +1569,7 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   if (generation == 1 && tm_initialize(h)) return 1;
   if (tm_sync_dev(h)) return 1;
   // prepareGeneration :161-170
+  h->currentBurnIn = tm_burn_in(h, generation);
   h->acceptedSamplesCount = 0;
   h->maxLoglikelihood = -INFINITY;
   h->dbCount = 0;
@@ -1409,27 +1601,37 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
     TmStage st(h, "draw");
     const int CB = std::max(1, 256 / N);
     const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)CB * N * sizeof(double);
-    hipLaunchKernelGGL(k_tm_draw, dim3(nblk(P, CB)), dim3(256), lbytes, h->stream, N, P, h->Z, h->chol, h->leaders,
-                       h->cand);
+    hipLaunchKernelGGL(k_tm_draw<false>, dim3(nblk(P, CB)), dim3(256), lbytes, h->stream, N, P, h->Z, h->chol,
+                       h->leaders, h->cand, (const ChainSched *)nullptr, 0, (unsigned char *)nullptr);
     KG_HIP(hipGetLastError());
   }
-  return 0;
+  // chains c < Chain Count start with their prepared candidate (:114-130)
+  hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, (int)h->chainCount, h->pend);
+  KG_HIP(hipGetLastError());
+  h->pendingCount = (size_t)h->chainCount;
+  return tm_schedule(h);
 }
 
 int kg_tmcmc_evaluate(kg_tmcmc_t h) {
   TmStage st(h, "evaluate");
   hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, h->cfg.likelihood,
-                     h->cand, h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP);
+                     h->cand, h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP, h->pend);
   KG_HIP(hipGetLastError());
-  h->modelEvaluationCount += h->P;
+  h->modelEvaluationCount += (double)h->pendingCount;  // _modelEvaluationCount++ per started sample (:127)
   return 0;
 }
 
 int kg_tmcmc_evaluate_prior(kg_tmcmc_t h) {
   TmStage st(h, "evaluate");
   hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, -1, h->cand,
-                     h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP);
+                     h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP, h->pend);
   KG_HIP(hipGetLastError());
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_tmcmc_get_pending(kg_tmcmc_t h, unsigned char *mask) {
+  KG_HIP(hipMemcpyAsync(mask, h->pend, (size_t)h->P, hipMemcpyDeviceToHost, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -1444,24 +1646,74 @@ int kg_tmcmc_get_candidates(kg_tmcmc_t h, double *X, size_t ld) {
 }
 
 int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double *log_likelihood) {
-  KG_HIP(hipMemcpyAsync(h->candLP, log_prior, h->P * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  KG_HIP(hipMemcpyAsync(h->candLL, log_likelihood, h->P * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  const size_t P = h->P;
+  KG_HIP(hipMemcpyAsync(h->E, log_prior, P * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipMemcpyAsync(h->E + P, log_likelihood, P * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_tm_set_pending, dim3(nblk(P, 256)), dim3(256), 0, h->stream, (int)P, h->pend, h->E, h->E + P,
+                     h->candLP, h->candLL);
+  KG_HIP(hipGetLastError());
   KG_HIP(hipStreamSynchronize(h->stream));
-  h->modelEvaluationCount += h->P;
+  h->modelEvaluationCount += (double)h->pendingCount;
+  return 0;
+}
+
+int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending) {
+  const int N = h->N, P = h->P;
+  KG_CHECK(h->step < h->maxSteps, "kg_tmcmc_advance: every chain has finished this generation");
+  const int s = ++h->step;
+  if (!h->rounds) {
+    // every chain runs one step: Uniform c, database entry c
+    TmStage st(h, "accept");
+    if (h->uniform.uniforms(h->U, P, h->stream)) return 1;
+    hipLaunchKernelGGL(k_tm_accept, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, generation == 1 ? 1 : 0,
+                       h->annealingExponent, h->U, h->candLL, h->candLP, h->leadLL, h->leadLP, h->dbLL, h->dbLP,
+                       h->acc, h->dev);
+    hipLaunchKernelGGL(k_tm_copy_rows, dim3(nblk((size_t)P * N, 256)), dim3(256), 0, h->stream, N, P, h->acc,
+                       h->cand, h->leaders, h->db);
+    KG_HIP(hipGetLastError());
+    h->pendingCount = 0;
+  } else {
+    const int nc = (int)h->chainCount, B = (int)h->currentBurnIn;
+    {
+      TmStage st(h, "accept");
+      hipLaunchKernelGGL(k_tm_round_accept, dim3(nblk(nc, 256)), dim3(256), 0, h->stream, nc, s, B,
+                         generation == 1 ? 1 : 0, h->annealingExponent, h->sch, h->U, h->candLL, h->candLP,
+                         h->leadLL, h->leadLP, h->dbLL, h->dbLP, h->acc, h->dev);
+      hipLaunchKernelGGL(k_tm_round_rows, dim3(nblk((size_t)nc * N, 256)), dim3(256), 0, h->stream, N, nc, s, B,
+                         h->sch, h->acc, h->cand, h->leaders, h->db);
+      KG_HIP(hipGetLastError());
+    }
+    size_t more = 0;
+    for (int c = 0; c < nc; c++) more += (int)h->hSch[c].S > s;
+    if (more) {
+      TmStage st(h, "draw");
+      const int CB = std::max(1, 256 / N);
+      const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)CB * N * sizeof(double);
+      hipLaunchKernelGGL(k_tm_draw<true>, dim3(nblk(nc, CB)), dim3(256), lbytes, h->stream, N, nc, h->Zx, h->chol,
+                         h->leaders, h->cand, h->sch, s, h->pend);
+      KG_HIP(hipGetLastError());
+    } else {
+      hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, 0, h->pend);
+      KG_HIP(hipGetLastError());
+    }
+    h->pendingCount = more;
+  }
+  if (h->pendingCount == 0) h->step = h->maxSteps;
+  if (pending) *pending = h->pendingCount;
   return 0;
 }
 
 int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   const int N = h->N, P = h->P;
   const size_t PN = (size_t)P * N;
+  // the chains' remaining steps with the builtin likelihood
+  while (h->step < h->maxSteps) {
+    size_t more = 0;
+    if (kg_tmcmc_advance(h, generation, &more)) return 1;
+    if (more && kg_tmcmc_evaluate(h)) return 1;
+  }
   {
     TmStage st(h, "accept");
-    if (h->uniform.uniforms(h->U, P, h->stream)) return 1;
-    hipLaunchKernelGGL(k_tm_accept, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, generation == 1 ? 1 : 0,
-                       h->annealingExponent, h->U, h->candLL, h->candLP, h->leadLL, h->leadLP, h->dbLL, h->dbLP,
-                       h->acc, h->dev);
-    hipLaunchKernelGGL(k_tm_copy_rows, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->acc, h->cand,
-                       h->leaders, h->db);
     hipLaunchKernelGGL(k_tm_max, dim3(1), dim3(1024), 0, h->stream, P, h->dbLL, 1.0, 0, &h->dev->llmaxCv,
                        &h->dev->maxLoglikelihood);
     KG_HIP(hipGetLastError());
@@ -1507,7 +1759,7 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
     KG_HIP(hipMemcpyAsync(h->hDev, h->dev, sizeof(TmDev), hipMemcpyDeviceToHost, h->stream));
     KG_HIP(hipStreamSynchronize(h->stream));
   }
-  size_t zeroCount = 0, leaderId = 0;
+  size_t zeroCount = 0, leaderId = 0, total = 0;
   double sumw2 = 0.0;
   {
     HostClock hc(h, "multinomial");
@@ -1524,15 +1776,29 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
     for (int i = 0; i < P; i++) sw += wt[i];
     for (int i = 0; i < P; i++) wt[i] = wt[i] / sw;
     for (int i = 0; i < P; i++) sumw2 += wt[i] * wt[i];
+    // leaders and chain lengths :329-360 ("uniform splitting" of selections
+    // above Max Chain Length)
+    const unsigned mcl = (unsigned)h->cfg.max_chain_length;
     for (int i = 0; i < P; i++) {
-      if (h->nsel[i] == 0) zeroCount++;
-      for (unsigned t = 0; t < h->nsel[i]; t++) h->hSrc[leaderId++] = (unsigned)i;
+      unsigned n = h->nsel[i];
+      if (n == 0) zeroCount++;
+      while (n > 0) {
+        const unsigned len = n > mcl ? mcl - (n % mcl != 0 ? 1u : 0u) : n;
+        h->hSrc[leaderId] = (unsigned)i;
+        h->hLenD[leaderId] = (double)len;
+        h->hLen[leaderId] = len;
+        n -= len;
+        total += len;
+        leaderId++;
+      }
     }
+    for (size_t j = leaderId; j < (size_t)P; j++) h->hLen[j] = 0;
   }
-  KG_CHECK(leaderId == (size_t)P, "multinomial selections do not sum to the population size");
+  KG_CHECK(total == (size_t)P, "multinomial selections do not sum to the population size");
   KG_HIP(hipMemcpyAsync(h->w, h->hW, (size_t)P * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipMemcpyAsync(h->numSel, h->hNsel, (size_t)P * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  KG_HIP(hipMemcpyAsync(h->src, h->hSrc, (size_t)P * sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipMemcpyAsync(h->src, h->hSrc, leaderId * sizeof(unsigned), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipMemcpyAsync(h->dLen, h->hLenD, leaderId * sizeof(double), hipMemcpyHostToDevice, h->stream));
   {
     TmStage st(h, "mean_cov");
     const int npairs = N * (N + 1) / 2;
@@ -1547,8 +1813,8 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   }
   {
     TmStage st(h, "expand");
-    hipLaunchKernelGGL(k_tm_expand, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->src, h->db, h->dbLL,
-                       h->dbLP, h->leaders, h->leadLL, h->leadLP, h->chainLen);
+    hipLaunchKernelGGL(k_tm_expand, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, (int)leaderId, h->src,
+                       h->dLen, h->db, h->dbLL, h->dbLP, h->leaders, h->leadLL, h->leadLP, h->chainLen);
     KG_HIP(hipGetLastError());
   }
   h->proposalsAcceptanceRate = (1.0 * h->acceptedSamplesCount) / P;
@@ -1599,6 +1865,11 @@ int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t 
   }
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
+  if (r.dev == h->chainLen)
+    for (size_t c = 0; c < n; c++) {
+      KG_CHECK(in[c] >= 0 && in[c] == floor(in[c]), "Chain Lengths must be non-negative integers");
+      h->hLen[c] = (unsigned)in[c];
+    }
   if (r.dev == h->pmin || r.dev == h->pmax) {
     hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(h->N, 64)), dim3(64), 0, h->stream, h->N, h->pmin, h->pmax,
                        h->negLogWidth);

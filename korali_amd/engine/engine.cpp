@@ -430,7 +430,7 @@ const char *TMCMC_MATRICES[] = {"Chain Leaders", "Chain Candidates", "Sample Dat
 const char *TMCMC_SCALARS[] = {"Annealing Exponent", "Previous Annealing Exponent", "LogEvidence",
                                "Coefficient Of Variation", "Max Loglikelihood", "Chain Count",
                                "Accepted Samples Count", "Proposals Acceptance Rate", "Selection Acceptance Rate",
-                               "Database Entries", "Model Evaluation Count"};
+                               "Database Entries", "Model Evaluation Count", "Current Burn In"};
 
 struct TmcmcModule : SolverModule {
   kg_tmcmc_t h = nullptr;
@@ -456,11 +456,11 @@ struct TmcmcModule : SolverModule {
     P = uint(sv, "Population Size", 0);
     if (P < 2) fail("TMCMC 'Population Size' must be at least 2.");
     const double mcl = num(sv, "Max Chain Length", 1);
-    if (mcl == 0) fail("Max Chain Length must be greater 0.");
-    if (mcl != 1) fail("The device TMCMC path supports 'Max Chain Length' 1 only.");
-    if (num(sv, "Burn In", 0) != 0) fail("The device TMCMC path supports 'Burn In' 0 only.");
-    if (sv.contains("Per Generation Burn In") && sv["Per Generation Burn In"].size() > 0)
-      fail("'Per Generation Burn In' is not supported by the device path.");
+    if (mcl == 0) fail("Max Chain Length must be greater 0.");  // TMCMC.cpp.base:32
+    const double burnIn = num(sv, "Burn In", 0);
+    std::vector<double> perGenBurnIn;
+    if (sv.contains("Per Generation Burn In") && sv["Per Generation Burn In"].is_array())
+      perGenBurnIn = flatten(sv["Per Generation Burn In"]);
     const double covScaling = num(sv, "Covariance Scaling", 0.04);
     if (covScaling <= 0.0) fail("Covariance Scaling must be larger 0.0 (is %lf).\n", covScaling);
     Json &tc = sv["Termination Criteria"];
@@ -505,8 +505,10 @@ struct TmcmcModule : SolverModule {
     kg_tmcmc_cfg c{};
     c.variable_count = N;
     c.population_size = P;
-    c.max_chain_length = 1;
-    c.default_burn_in = 0;
+    c.max_chain_length = mcl;
+    c.default_burn_in = burnIn;
+    c.per_generation_burn_in = perGenBurnIn.empty() ? nullptr : perGenBurnIn.data();
+    c.per_generation_burn_in_count = perGenBurnIn.size();
     c.target_cov = num(sv, "Target Coefficient Of Variation", 1.0);
     c.covariance_scaling = covScaling;
     c.min_annealing_exponent_update = num(sv, "Min Annealing Exponent Update", 1e-5);
@@ -564,30 +566,35 @@ struct TmcmcModule : SolverModule {
     if (builtin) {
       check(kg_tmcmc_evaluate(h));
     } else {
-      // Bayesian::evaluate per chain: prior on the device, the likelihood
-      // model only where the prior is finite (bayesian.cpp.base:56-77)
-      check(kg_tmcmc_evaluate_prior(h));
+      // runGeneration's WAITANY loop :112-144: every round evaluates the
+      // pending candidate of each unfinished chain (Bayesian::evaluate per
+      // sample, the likelihood model only where the prior is finite,
+      // bayesian.cpp.base:56-77), then advances every chain one step
       std::vector<double> X(P * N), LP(P), LL(P);
-      check(kg_tmcmc_get_candidates(h, X.data(), N));
-      check(kg_tmcmc_get_field(h, "Chain Candidates LogPriors", LP.data(), P));
+      std::vector<unsigned char> pend(P);
       Function &f = getFunction(fn);
-      for (size_t i = 0; i < P; i++) {
-        if (std::isinf(LP[i]) && LP[i] < 0) {
+      for (size_t pending = 1; pending;) {
+        check(kg_tmcmc_evaluate_prior(h));
+        check(kg_tmcmc_get_pending(h, pend.data()));
+        check(kg_tmcmc_get_candidates(h, X.data(), N));
+        check(kg_tmcmc_get_field(h, "Chain Candidates LogPriors", LP.data(), P));
+        for (size_t i = 0; i < P; i++) {
           LL[i] = -INFINITY;
-          continue;
+          if (!pend[i] || (std::isinf(LP[i]) && LP[i] < 0)) continue;
+          Sample s;
+          s["Module"] = "Problem";
+          s["Operation"] = "Evaluate";
+          s["Sample Id"] = (unsigned long long)i;
+          s["Current Generation"] = (unsigned long long)gen;
+          s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
+          f(s);
+          if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
+          LL[i] = s["logLikelihood"].getDouble();
+          if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);
         }
-        Sample s;
-        s["Module"] = "Problem";
-        s["Operation"] = "Evaluate";
-        s["Sample Id"] = (unsigned long long)i;
-        s["Current Generation"] = (unsigned long long)gen;
-        s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
-        f(s);
-        if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
-        LL[i] = s["logLikelihood"].getDouble();
-        if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);
+        check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
+        check(kg_tmcmc_advance(h, gen, &pending));
       }
-      check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
     }
     check(kg_tmcmc_process(h, gen));
     check(kg_tmcmc_synchronize(h));

@@ -47,7 +47,8 @@ class _TmcmcCfg(C.Structure):
         ("prior_distribution", C.POINTER(C.c_int)), ("distribution_count", C.c_size_t),
         ("prior_seeds", C.POINTER(C.c_uint64)), ("multinomial_seed", C.c_uint64),
         ("multivariate_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("likelihood", C.c_int),
-        ("device", C.c_int),
+        ("device", C.c_int), ("per_generation_burn_in", C.POINTER(C.c_double)),
+        ("per_generation_burn_in_count", C.c_size_t),
     ]
 
 
@@ -61,7 +62,7 @@ EXPORTED = [
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
-    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
+    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_advance", "kg_tmcmc_get_pending", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump",
 ]
 
@@ -111,6 +112,8 @@ def lib():
         L.kg_tmcmc_set_rng.argtypes = [vp, ip, vp]
         L.kg_tmcmc_get_candidates.argtypes = [vp, dp, sz]
         L.kg_tmcmc_set_evaluations.argtypes = [vp, dp, dp]
+        L.kg_tmcmc_advance.argtypes = [vp, sz, C.POINTER(sz)]
+        L.kg_tmcmc_get_pending.argtypes = [vp, C.POINTER(C.c_ubyte)]
         L.kg_tmcmc_profile.argtypes = [vp, ip]
         L.kg_tmcmc_profile_read.argtypes = [vp, cp, dp, C.POINTER(sz)]
         _LIB = L
@@ -287,7 +290,7 @@ class TmcmcDevice:
     def __init__(self, N, P, prior_min, prior_max, prior_seeds=None, prior_distribution=None,
                  multinomial_seed=0, multivariate_seed=0, uniform_seed=0, target_cov=1.0, covariance_scaling=0.04,
                  min_annealing_exponent_update=1e-5, max_annealing_exponent_update=1.0, max_chain_length=1,
-                 default_burn_in=0, likelihood=0, device=0):
+                 default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0):
         L = lib()
         self.N, self.P = int(N), int(P)
         pdist = (np.arange(self.N, dtype=np.int32) if prior_distribution is None
@@ -295,7 +298,8 @@ class TmcmcDevice:
         ndist = int(pdist.max()) + 1
         seeds = np.zeros(ndist, dtype=np.uint64) if prior_seeds is None else np.ascontiguousarray(
             np.broadcast_to(np.asarray(prior_seeds, dtype=np.uint64), (ndist,)))
-        self._arrays = [_vec(prior_min, self.N, 0.0), _vec(prior_max, self.N, 1.0), pdist, seeds]
+        pgb = np.ascontiguousarray(per_generation_burn_in, dtype=np.float64).reshape(-1)
+        self._arrays = [_vec(prior_min, self.N, 0.0), _vec(prior_max, self.N, 1.0), pdist, seeds, pgb]
         cfg = _TmcmcCfg()
         cfg.variable_count, cfg.population_size = self.N, self.P
         cfg.max_chain_length, cfg.default_burn_in = float(max_chain_length), float(default_burn_in)
@@ -309,6 +313,8 @@ class TmcmcDevice:
         cfg.multinomial_seed, cfg.multivariate_seed, cfg.uniform_seed = (int(multinomial_seed),
                                                                         int(multivariate_seed), int(uniform_seed))
         cfg.likelihood, cfg.device = int(likelihood), int(device)
+        cfg.per_generation_burn_in = _dptr(pgb) if pgb.size else None
+        cfg.per_generation_burn_in_count = pgb.size
         h = C.c_void_p()
         check(L.kg_tmcmc_create(C.byref(cfg), C.byref(h)))
         self.h = h
@@ -333,6 +339,18 @@ class TmcmcDevice:
 
     def process(self, generation):
         check(self._L.kg_tmcmc_process(self.h, int(generation)))
+
+    def advance(self, generation):
+        """One step of every unfinished chain; returns how many chains now
+        have a candidate pending evaluation."""
+        n = C.c_size_t()
+        check(self._L.kg_tmcmc_advance(self.h, int(generation), C.byref(n)))
+        return n.value
+
+    def pending(self):
+        m = np.zeros(self.P, dtype=np.uint8)
+        check(self._L.kg_tmcmc_get_pending(self.h, m.ctypes.data_as(C.POINTER(C.c_ubyte))))
+        return m.astype(bool)
 
     def generation(self, generation):
         check(self._L.kg_tmcmc_generation(self.h, int(generation)))

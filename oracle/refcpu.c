@@ -1626,6 +1626,9 @@ struct kr_tmcmc
   size_t N, P;
   /* options */
   double maxChainLength, burnIn, targetCOV, covScaling, minAnnealingExponentUpdate, maxAnnealingExponentUpdate;
+  double *perGenBurnIn; /* "Per Generation Burn In": entry k applies to generation k+2 */
+  size_t perGenBurnInCount;
+  double currentBurnIn;
   /* priors: uniform [priorMin, priorMax] per variable, RNG per variable */
   double *priorMin, *priorMax;
   kr_rng *priorRng;
@@ -1707,6 +1710,7 @@ void kr_tmcmc_free(kr_tmcmc *h)
   free(h->dbLL);
   free(h->dbLP);
   free(h->numSelections);
+  free(h->perGenBurnIn);
   free(h);
 }
 
@@ -1748,6 +1752,7 @@ double *kr_tmcmc_field(kr_tmcmc *h, const char *name, size_t *len)
   SCA("Database Entries", dbCount)
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Min Search Iterations", minSearchIterations)
+  SCA("Current Burn In", currentBurnIn)
 #undef VEC
 #undef SCA
   if (len) *len = 0;
@@ -1780,6 +1785,22 @@ void kr_tmcmc_set_option(kr_tmcmc *h, const char *name, double v)
   else if (strcmp(name, "Max Annealing Exponent Update") == 0) h->maxAnnealingExponentUpdate = v;
 }
 
+void kr_tmcmc_set_per_generation_burn_in(kr_tmcmc *h, const double *v, size_t n)
+{
+  free(h->perGenBurnIn);
+  h->perGenBurnIn = (double *)calloc(n ? n : 1, sizeof(double));
+  if (n) memcpy(h->perGenBurnIn, v, n * sizeof(double));
+  h->perGenBurnInCount = n;
+}
+
+/* setBurnIn, TMCMC.cpp.base:781-789 */
+static double tm_burn_in(const kr_tmcmc *h, size_t gen)
+{
+  if (gen <= 1) return 0.0;
+  if (gen - 2 < h->perGenBurnInCount) return h->perGenBurnIn[gen - 2];
+  return h->burnIn;
+}
+
 /* setInitialConfiguration, TMCMC.cpp.base:21-105 */
 void kr_tmcmc_initialize(kr_tmcmc *h)
 {
@@ -1792,12 +1813,26 @@ void kr_tmcmc_initialize(kr_tmcmc *h)
   for (i = 0; i < h->P; i++) h->chainLengths[i] = 1;
 }
 
-/* prepareGeneration, TMCMC.cpp.base:159-227 (burn-in 0 after gen 1 when
- * Default Burn In is 0; setBurnIn :781-789) */
+/* generateCandidate :560-566 -> multivariate::Normal::getRandomVector
+ * (gsl_ran_multivariate_gaussian: N polar normals, dtrmv, + zero mean), then
+ * + leader */
+static void tm_generate_candidate(kr_tmcmc *h, size_t i)
+{
+  const size_t N = h->N;
+  size_t d;
+  double *x = h->candidates + i * N;
+  for (d = 0; d < N; d++) x[d] = kr_ran_gaussian(&h->multivariate, 1.0);
+  kr_dtrmv_lower(N, h->chol, x);
+  for (d = 0; d < N; d++) x[d] = x[d] + 0.0;
+  for (d = 0; d < N; d++) x[d] += h->leaders[i * N + d];
+}
+
+/* prepareGeneration, TMCMC.cpp.base:159-227 (setBurnIn :781-789) */
 void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
 {
   const size_t N = h->N;
   size_t i, d;
+  h->currentBurnIn = tm_burn_in(h, gen);
   h->acceptedSamplesCount = 0;
   h->maxLoglikelihood = -INFINITY;
   h->dbCount = 0;
@@ -1810,63 +1845,78 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
       for (d = 0; d < N; d++) h->candidates[i * N + d] = kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
     }
     else
-    {
-      double *x = h->candidates + i * N;
-      for (d = 0; d < N; d++) x[d] = kr_ran_gaussian(&h->multivariate, 1.0);
-      kr_dtrmv_lower(N, h->chol, x);
-      for (d = 0; d < N; d++) x[d] = x[d] + 0.0;
-      for (d = 0; d < N; d++) x[d] += h->leaders[i * N + d];
-    }
+      tm_generate_candidate(h, i);
   }
 }
 
 /* Bayesian::evaluate (bayesian.cpp.base:24-84): logPrior = sum of uniform
  * log-densities (uniform.cpp.base:38-44); -inf prior -> -inf loglik without
  * calling the model; else builtin Gaussian loglik (model.py:32-37). */
-void kr_tmcmc_evaluate(kr_tmcmc *h)
+static void tm_evaluate_one(kr_tmcmc *h, size_t i)
 {
   const size_t N = h->N;
-  size_t i, d;
-  for (i = 0; i < h->P; i++)
+  size_t d;
+  const double *x = h->candidates + i * N;
+  double lp = 0.0;
+  for (d = 0; d < N; d++)
   {
-    const double *x = h->candidates + i * N;
-    double lp = 0.0;
-    for (d = 0; d < N; d++)
-    {
-      const double aux = -kr_log_cr(h->priorMax[d] - h->priorMin[d]);
-      lp += (x[d] >= h->priorMin[d] && x[d] <= h->priorMax[d]) ? aux : -INFINITY;
-    }
-    h->candidatesLP[i] = lp;
-    h->candidatesLL[i] = isinf(lp) && lp < 0 ? -INFINITY : kr_loglik_gaussian(x, N);
-    h->modelEvaluationCount += 1;
+    const double aux = -kr_log_cr(h->priorMax[d] - h->priorMin[d]);
+    lp += (x[d] >= h->priorMin[d] && x[d] <= h->priorMax[d]) ? aux : -INFINITY;
   }
+  h->candidatesLP[i] = lp;
+  h->candidatesLL[i] = isinf(lp) && lp < 0 ? -INFINITY : kr_loglik_gaussian(x, N);
+  h->modelEvaluationCount += 1;
 }
 
-/* processCandidate + calculateAcceptanceProbability + updateDatabase,
- * TMCMC.cpp.base:229-252, 611-633; chains processed in chain order */
+/* the first step of every started chain (runGeneration :114-130 starts
+ * chains c < Chain Count) */
+void kr_tmcmc_evaluate(kr_tmcmc *h)
+{
+  size_t i;
+  for (i = 0; i < (size_t)h->chainCount; i++) tm_evaluate_one(h, i);
+}
+
+/* runGeneration's WAITANY loop :112-144 with processCandidate +
+ * calculateAcceptanceProbability + updateDatabase (:229-252, :611-633).
+ * With the Sequential conduit the waitAny scan (conduit.cpp.base:180-210)
+ * always hands the single worker to the lowest-index started sample, and a
+ * finished chain is restarted before the next scan, so every step of chain
+ * c completes before chain c+1's first: chain-major order.  Step s of chain
+ * c (1-based, S = Chain Lengths[c] + Current Burn In steps): one Uniform,
+ * accept if P > U or generation 1 (counted only past the burn-in), a new
+ * candidate (N Multivariate normals) while s < S, a database entry past the
+ * burn-in.  Step 1's candidate was evaluated by kr_tmcmc_evaluate. */
 void kr_tmcmc_process_candidates(kr_tmcmc *h, size_t gen)
 {
   const size_t N = h->N;
-  size_t c;
+  const size_t B = (size_t)h->currentBurnIn;
+  size_t c, s;
   for (c = 0; c < (size_t)h->chainCount; c++)
   {
-    double P = 0.0, U;
-    if (isfinite(h->candidatesLP[c]) && isfinite(h->candidatesLL[c]))
-      P = kr_exp_cr((h->candidatesLL[c] - h->leadersLL[c]) * h->annealingExponent + (h->candidatesLP[c] - h->leadersLP[c]));
-    U = kr_ran_flat(&h->uniform, 0.0, 1.0);
-    if (P > U || gen == 1)
+    const size_t S = (size_t)h->chainLengths[c] + B;
+    for (s = 1; s <= S; s++)
     {
-      memcpy(h->leaders + c * N, h->candidates + c * N, sizeof(double) * N);
-      h->leadersLP[c] = h->candidatesLP[c];
-      h->leadersLL[c] = h->candidatesLL[c];
-      h->acceptedSamplesCount++;
-    }
-    {
-      const size_t k = (size_t)h->dbCount;
-      memcpy(h->dbX + k * N, h->leaders + c * N, sizeof(double) * N);
-      h->dbLP[k] = h->leadersLP[c];
-      h->dbLL[k] = h->leadersLL[c];
-      h->dbCount += 1;
+      double P = 0.0, U;
+      if (s > 1) tm_evaluate_one(h, c);
+      if (isfinite(h->candidatesLP[c]) && isfinite(h->candidatesLL[c]))
+        P = kr_exp_cr((h->candidatesLL[c] - h->leadersLL[c]) * h->annealingExponent + (h->candidatesLP[c] - h->leadersLP[c]));
+      U = kr_ran_flat(&h->uniform, 0.0, 1.0);
+      if (P > U || gen == 1)
+      {
+        memcpy(h->leaders + c * N, h->candidates + c * N, sizeof(double) * N);
+        h->leadersLP[c] = h->candidatesLP[c];
+        h->leadersLL[c] = h->candidatesLL[c];
+        if (s > B) h->acceptedSamplesCount++;
+      }
+      if (s < S) tm_generate_candidate(h, c);
+      if (s > B && (size_t)h->dbCount < h->P) /* sum of chain lengths = P */
+      {
+        const size_t k = (size_t)h->dbCount;
+        memcpy(h->dbX + k * N, h->leaders + c * N, sizeof(double) * N);
+        h->dbLP[k] = h->leadersLP[c];
+        h->dbLL[k] = h->leadersLL[c];
+        h->dbCount += 1;
+      }
     }
   }
 }

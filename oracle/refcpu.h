@@ -95,6 +95,7 @@ double *kr_tmcmc_field(kr_tmcmc *h, const char *name, size_t *len);
 kr_rng *kr_tmcmc_rng(kr_tmcmc *h, int which); /* 0 multinomial 1 multivariate 2 uniform 3+k prior k */
 void kr_tmcmc_set_option(kr_tmcmc *h, const char *name, double value);
 void kr_tmcmc_set_prior_map(kr_tmcmc *h, const int *map);
+void kr_tmcmc_set_per_generation_burn_in(kr_tmcmc *h, const double *v, size_t n); /* setBurnIn :781-789 */
 void kr_tmcmc_initialize(kr_tmcmc *h);                   /* setInitialConfiguration :21-105 */
 void kr_tmcmc_prepare(kr_tmcmc *h, size_t generation);   /* prepareGeneration :159-227 */
 /* evaluate candidates with the builtin Gaussian likelihood + uniform priors */

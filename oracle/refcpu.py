@@ -71,6 +71,7 @@ def lib(variant="cr"):
         L.kr_tmcmc_rng.restype = vp
         L.kr_tmcmc_set_option.argtypes = [vp, cp, C.c_double]
         L.kr_tmcmc_set_prior_map.argtypes = [vp, C.POINTER(C.c_int)]
+        L.kr_tmcmc_set_per_generation_burn_in.argtypes = [vp, dp, sz]
         L.kr_tmcmc_initialize.argtypes = [vp]
         L.kr_tmcmc_prepare.argtypes = [vp, sz]
         L.kr_tmcmc_evaluate.argtypes = [vp]
@@ -238,6 +239,10 @@ class TMCMC:
     def set_prior_map(self, dist_of_var):
         m = (C.c_int * self.N)(*[int(v) for v in dist_of_var])
         self.L.kr_tmcmc_set_prior_map(self.h, m)
+
+    def set_per_generation_burn_in(self, values):
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        self.L.kr_tmcmc_set_per_generation_burn_in(self.h, v.ctypes.data_as(C.POINTER(C.c_double)), v.size)
 
     def initialize(self):
         self.L.kr_tmcmc_initialize(self.h)

@@ -246,3 +246,101 @@ def test_tmcmc_likelihood_kernel_equals_callback():
         korali.Engine().run(e)
         runs.append((e["Solver"]["LogEvidence"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sample Database"]))
     assert runs[0] == runs[1]
+
+
+def tmcmc_1d(model, **solver):
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    if model is None:
+        e["Problem"]["Likelihood Kernel"] = "Gaussian"
+    else:
+        e["Problem"]["Likelihood Model"] = model
+    e["Distributions"][0]["Name"] = "Uniform 0"
+    e["Distributions"][0]["Type"] = "Univariate/Uniform"
+    e["Distributions"][0]["Minimum"] = -20.0
+    e["Distributions"][0]["Maximum"] = +20.0
+    e["Variables"][0]["Name"] = "X"
+    e["Variables"][0]["Prior Distribution"] = "Uniform 0"
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    for k, v in solver.items():
+        e["Solver"][k] = v
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["File Output"]["Enabled"] = False
+    e["Random Seed"] = 0xC0FFEE
+    return e
+
+
+def test_statistical_run_tmcmc_2_burn_in():
+    """tests/statistical/samplers/correctness/run-tmcmc-2.py (Burn In 3):
+    checkMean(e, 0.0, 0.05), checkStd(e, 1.0, 0.05)."""
+    import korali
+
+    def model(s):  # correctness/model/model.py
+        v = s["Parameters"][0]
+        s["logLikelihood"] = -0.5 * v * v
+
+    e = tmcmc_1d(model, **{"Population Size": 5000, "Covariance Scaling": 0.01, "Burn In": 3,
+                           "Target Coefficient Of Variation": 0.4})
+    korali.Engine().run(e)
+    samples = np.array(e["Solver"]["Sample Database"])
+    assert np.isclose(0.0, samples.mean(), atol=0.05)
+    assert np.isclose(1.0, samples.std(), atol=0.05)
+
+
+def test_tmcmc_specifics_burn_in_and_rho_updates(tmp_path):
+    """tests/statistical/samplers/detailed/tmcmc/tmcmc-specifics.py: Burn In 5,
+    Per Generation Burn In [10, 7], rho updates within [1e-3, 0.2]; the
+    result files carry Burn In and Current Burn In per generation."""
+    import korali
+
+    def model(s):  # detailed/tmcmc/helpers: loglik -v^2
+        v = s["Parameters"][0]
+        s["logLikelihood"] = -v * v
+
+    e = tmcmc_1d(model, **{"Population Size": 5000, "Covariance Scaling": 0.001, "Burn In": 5,
+                           "Per Generation Burn In": [10, 7], "Max Chain Length": 1,
+                           "Target Coefficient Of Variation": 0.5, "Min Annealing Exponent Update": 1e-3,
+                           "Max Annealing Exponent Update": 0.2})
+    e["Distributions"][0]["Minimum"] = -10.0
+    e["Distributions"][0]["Maximum"] = +10.0
+    e["Random Seed"] = 314
+    e["File Output"]["Enabled"] = True
+    e["File Output"]["Path"] = str(tmp_path)
+    korali.Engine().run(e)
+    files = sorted(f for f in os.listdir(tmp_path) if f.startswith("gen"))
+    assert len(files) > 5
+    burn = [0, 0, 10, 7] + [5] * 100
+    prev = 0.0
+    for f in files:
+        with open(os.path.join(tmp_path, f)) as fh:
+            d = json.load(fh)
+        g = d["Current Generation"]
+        if g == 0:
+            continue
+        assert d["Solver"]["Burn In"] == 5
+        assert d["Solver"]["Current Burn In"] == burn[g]
+        rho = d["Solver"]["Annealing Exponent"]
+        assert rho - prev <= 0.2 + 1e-12
+        assert rho >= prev + 1e-3 - 1e-12 or rho == 1.0
+        prev = rho
+
+
+@pytest.mark.parametrize("solver", [{"Burn In": 2, "Max Chain Length": 3}, {"Max Chain Length": 4},
+                                    {"Burn In": 1, "Per Generation Burn In": [3, 0]}])
+def test_tmcmc_chain_steps_kernel_equals_callback(solver):
+    """Multi-step chains through the engine: the host-callback rounds
+    (WAITANY loop) and the device likelihood kernel give identical runs."""
+    import korali
+
+    def model(s):
+        v = s["Parameters"][0]
+        s["logLikelihood"] = -0.5 * v * v
+
+    runs = []
+    for m in (model, None):
+        e = tmcmc_1d(m, **{"Population Size": 700, **solver})
+        korali.Engine().run(e)
+        runs.append((e["Solver"]["LogEvidence"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sample Database"],
+                     e["Solver"]["Model Evaluation Count"], e["Solver"]["Chain Lengths"]))
+    assert runs[0] == runs[1]

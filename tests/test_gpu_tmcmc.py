@@ -78,7 +78,7 @@ SCA_KEYS = ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", 
             "Selection Acceptance Rate", "Model Evaluation Count", "Min Search Iterations")
 
 
-def seeded_pair(N, P, shared, seed=1337, target_cov=1.0):
+def seeded_pair(N, P, shared, seed=1337, target_cov=1.0, max_chain_length=1, burn_in=0, per_generation_burn_in=()):
     """C3-style experiment: every variable with a U(-5, 5) prior, Gaussian
     loglik -0.5|x|^2; seeds in Korali's consumption order (distributions,
     then the solver's Multinomial, Multivariate, Uniform generators)."""
@@ -88,9 +88,15 @@ def seeded_pair(N, P, shared, seed=1337, target_cov=1.0):
     seeds = [seed + k for k in range(ndist)]
     sm, sv, su = seed + ndist, seed + ndist + 1, seed + ndist + 2
     dev = TmcmcDevice(N, P, prior_min=[-5.0] * N, prior_max=[5.0] * N, prior_seeds=seeds, prior_distribution=pdist,
-                      multinomial_seed=sm, multivariate_seed=sv, uniform_seed=su, target_cov=target_cov)
+                      multinomial_seed=sm, multivariate_seed=sv, uniform_seed=su, target_cov=target_cov,
+                      max_chain_length=max_chain_length, default_burn_in=burn_in,
+                      per_generation_burn_in=per_generation_burn_in)
     o = R.TMCMC(N, P)
     o.option("Target Coefficient Of Variation", target_cov)
+    o.option("Max Chain Length", max_chain_length)
+    o.option("Default Burn In", burn_in)
+    if len(per_generation_burn_in):
+        o.set_per_generation_burn_in(per_generation_burn_in)
     o["Prior Minimum"] = [-5.0] * N
     o["Prior Maximum"] = [5.0] * N
     o.set_prior_map(pdist)
@@ -148,3 +154,69 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
     assert runs[0][0] == runs[1][0]
     # the interval path needs far fewer exact host evaluations
     assert runs[0][1] < runs[1][1]
+
+
+def compare_state(dev, o, g):
+    for key in VEC_KEYS:
+        assert np.array_equal(dev[key], o[key]), (g, key)
+    for key in SCA_KEYS + ("Current Burn In", "Database Entries"):
+        a, b = dev[key][0], o[key][0]
+        assert a == b or (np.isnan(a) and np.isnan(b)), (g, key, a, b)
+
+
+@pytest.mark.parametrize("N,P,mcl,burn,pergen", [(4, 256, 1, 2, ()), (3, 500, 3, 0, ()), (5, 300, 4, 1, (3, 0, 2)),
+                                                 (32, 1024, 2, 1, ())])
+def test_tmcmc_chain_steps_match_oracle(N, P, mcl, burn, pergen):
+    """Max Chain Length > 1 / Burn In / Per Generation Burn In: several steps
+    per chain in the Sequential conduit's chain-major RNG order, leader
+    splitting, database and counters — bit-exact against the oracle."""
+    dev, o, ndist = seeded_pair(N, P, True, seed=99, max_chain_length=mcl, burn_in=burn, per_generation_burn_in=pergen)
+    split = False
+    for g in range(1, 30):
+        dev.generation(g)
+        o.generation(g)
+        dev.synchronize()
+        compare_state(dev, o, g)
+        split |= o["Chain Count"][0] < P
+        if o["Previous Annealing Exponent"][0] >= 1.0:
+            break
+    if mcl > 1:
+        assert split
+    for which in range(3 + ndist):
+        assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
+
+
+def test_tmcmc_host_evaluated_rounds_match_oracle():
+    """The host-callback protocol (evaluate_prior -> pending -> candidates ->
+    set_evaluations -> advance, repeated while chains are pending) with the
+    likelihood formed in Python, against the oracle's builtin run."""
+    N, P = 3, 400
+    dev, o, ndist = seeded_pair(N, P, True, seed=5, max_chain_length=3, burn_in=2)
+    for g in range(1, 12):
+        lens, cc = dev["Chain Lengths"], int(dev["Chain Count"][0])
+        dev.prepare(g)
+        rounds = 0
+        while True:
+            dev.evaluate_prior()
+            pend = dev.pending()
+            X = dev.candidates()
+            lp = dev["Chain Candidates LogPriors"]
+            ll = np.full(P, -np.inf)
+            for i in np.nonzero(pend)[0]:
+                if np.isinf(lp[i]) and lp[i] < 0:
+                    continue
+                ss = 0.0
+                for x in X[i]:
+                    ss += x * x
+                ll[i] = -0.5 * ss
+            dev.set_evaluations(lp, ll)
+            rounds += 1
+            if dev.advance(g) == 0:
+                break
+        dev.process(g)
+        dev.synchronize()
+        o.generation(g)
+        compare_state(dev, o, g)
+        assert rounds == (1 if g == 1 else int(np.max(lens[:cc])) + 2)
+        if o["Previous Annealing Exponent"][0] >= 1.0:
+            break
