@@ -169,6 +169,11 @@ typedef struct {
    * (setBurnIn, TMCMC.cpp.base:781-789); NULL / 0 entries: Burn In only */
   const double *per_generation_burn_in;
   size_t per_generation_burn_in_count;
+  /* chain sharding: shard_count ranks, one handle each,
+   * state replicated; 0 = unsharded (kg_tmcmc_process), >= 1 = sharded
+   * (the partial / exchange / finalize protocol below, also for one rank) */
+  int shard_rank;
+  int shard_count;
 } kg_tmcmc_cfg;
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
@@ -200,6 +205,23 @@ int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending);
 /* P flags: 1 where the chain's candidate awaits evaluation */
 int kg_tmcmc_get_pending(kg_tmcmc_t h, unsigned char *mask);
 int kg_tmcmc_process(kg_tmcmc_t h, size_t generation);
+/* Chain sharding over shard_count ranks: each rank draws, evaluates and steps
+ * only its contiguous share of the started chains (it counts the whole
+ * Multivariate / Uniform streams, so positions stay global).  Then
+ *   kg_tmcmc_process_partial  - remaining steps + packs the rank's database,
+ *                               leader and candidate rows and its accepted
+ *                               count into "Shard Exchange" (int64 words,
+ *                               INT64_MIN where the rank owns nothing),
+ *   caller                    - MAX all-reduce of "Shard Exchange" viewed as
+ *                               int64 (exact bits of every owner), on the
+ *                               handle's stream (kg_tmcmc_stream),
+ *   kg_tmcmc_process_finalize - unpacks, then processGeneration :254-381
+ *                               replicated: every rank's state stays
+ *                               bit-identical to the unsharded run. */
+int kg_tmcmc_process_partial(kg_tmcmc_t h, size_t generation);
+int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation);
+int kg_tmcmc_device_ptr(kg_tmcmc_t h, const char *name, void **ptr);
+int kg_tmcmc_stream(kg_tmcmc_t h, void **stream);
 /* host-callback likelihoods (KORALI_START/WAITANY of TMCMC::runGeneration
  * :114-144): kg_tmcmc_evaluate_prior forms the uniform log-priors of the
  * pending candidates on the device ("Chain Candidates LogPriors"; -inf prior

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
+#include <climits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -119,26 +120,28 @@ struct ChainSched {
 // kRound: the candidate after step s of chain c (only chains with S > s;
 // normal row z0 + s - 1), which then becomes pending; otherwise row c for
 // every chain (prepareGeneration :222-225).
+// Chains [c_lo, c_hi) (a shard's own chains); Z holds the rows from c_lo
+// (prepare) or from extra-normal row zbase (kRound).
 template <bool kRound>
-__global__ void __launch_bounds__(256) k_tm_draw(int N, int P, const double *__restrict__ Z,
+__global__ void __launch_bounds__(256) k_tm_draw(int N, int c_lo, int P, const double *__restrict__ Z,
                                                  const double *__restrict__ Lg, const double *__restrict__ leaders,
                                                  double *__restrict__ cand, const ChainSched *__restrict__ sch,
-                                                 int s, unsigned char *__restrict__ pend) {
+                                                 int s, unsigned zbase, unsigned char *__restrict__ pend) {
   extern __shared__ double sm[];
   const int S = N + 1;
   double *Ls = sm;            // N x (N+1)
   double *zs = sm + N * S;    // CB x N
   const int CB = max(1, 256 / N);
-  const int c0 = blockIdx.x * CB;
+  const int c0 = c_lo + blockIdx.x * CB;
   for (int e = threadIdx.x; e < N * N; e += blockDim.x) Ls[(e / N) * S + e % N] = Lg[e];
   for (int e = threadIdx.x; e < CB * N; e += blockDim.x) {
     const int c = c0 + e / N;
     double z = 0.0;
     if (c < P) {
       if (!kRound)
-        z = Z[(size_t)c * N + e % N];
+        z = Z[(size_t)(c - c_lo) * N + e % N];
       else if ((int)sch[c].S > s)
-        z = Z[((size_t)sch[c].z0 + s - 1) * N + e % N];
+        z = Z[((size_t)sch[c].z0 + s - 1 - zbase) * N + e % N];
     }
     zs[e] = z;
   }
@@ -209,10 +212,11 @@ __global__ void k_tm_set_pending(int P, const unsigned char *__restrict__ pend, 
   candLL[c] = ll[c];
 }
 
-// chains c < started are pending their first evaluation (runGeneration :114-130)
-__global__ void k_tm_pend_init(int P, int started, unsigned char *__restrict__ pend) {
+// started chains c in [lo, hi) (this shard's) are pending their first
+// evaluation (runGeneration :114-130)
+__global__ void k_tm_pend_init(int P, int lo, int hi, unsigned char *__restrict__ pend) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < P) pend[c] = c < started ? 1 : 0;
+  if (c < P) pend[c] = (c >= lo && c < hi) ? 1 : 0;
 }
 
 __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const double *__restrict__ pmax,
@@ -225,11 +229,11 @@ __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const d
 // (:229-252, :611-633): P = exp((ll_c - ll_l) rho + (lp_c - lp_l)) if both
 // candidate values are finite, else 0; one Uniform draw per chain (always);
 // accept if P > U or generation 1.  Chain c's database entry is its leader.
-__global__ void k_tm_accept(int P, int gen1, double rho, const double *__restrict__ U,
+__global__ void k_tm_accept(int c_lo, int P, int gen1, double rho, const double *__restrict__ U,
                             const double *__restrict__ candLL, const double *__restrict__ candLP,
                             double *__restrict__ leadLL, double *__restrict__ leadLP, double *__restrict__ dbLL,
                             double *__restrict__ dbLP, unsigned char *__restrict__ acc, TmDev *dev) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = c_lo + blockIdx.x * blockDim.x + threadIdx.x;
   bool a = false;
   if (c < P) {
     double p = 0.0;
@@ -248,9 +252,9 @@ __global__ void k_tm_accept(int P, int gen1, double rho, const double *__restric
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(&dev->accepted, (unsigned int)__popcll(m));
 }
 
-__global__ void k_tm_copy_rows(int N, int P, const unsigned char *__restrict__ acc, const double *__restrict__ cand,
-                               double *__restrict__ leaders, double *__restrict__ db) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_tm_copy_rows(int N, int c_lo, int P, const unsigned char *__restrict__ acc,
+                               const double *__restrict__ cand, double *__restrict__ leaders, double *__restrict__ db) {
+  const size_t e = (size_t)c_lo * N + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)P * N) return;
   const int c = (int)(e / N);
   double v = leaders[e];
@@ -265,12 +269,12 @@ __global__ void k_tm_copy_rows(int N, int P, const unsigned char *__restrict__ a
 // processCandidate :229-252): one Uniform (u0 + s - 1), accept if P > U or
 // generation 1, counted and entered into the database only past the burn-in
 // B (entry db0 + s - B - 1).
-__global__ void k_tm_round_accept(int nc, int s, int B, int gen1, double rho, const ChainSched *__restrict__ sch,
-                                  const double *__restrict__ U, const double *__restrict__ candLL,
-                                  const double *__restrict__ candLP, double *__restrict__ leadLL,
-                                  double *__restrict__ leadLP, double *__restrict__ dbLL, double *__restrict__ dbLP,
-                                  unsigned char *__restrict__ acc, TmDev *dev) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_tm_round_accept(int c_lo, int nc, int s, int B, int gen1, double rho,
+                                  const ChainSched *__restrict__ sch, const double *__restrict__ U,
+                                  const double *__restrict__ candLL, const double *__restrict__ candLP,
+                                  double *__restrict__ leadLL, double *__restrict__ leadLP, double *__restrict__ dbLL,
+                                  double *__restrict__ dbLP, unsigned char *__restrict__ acc, TmDev *dev) {
+  const int c = c_lo + blockIdx.x * blockDim.x + threadIdx.x;
   bool counted = false;
   if (c < nc) {
     const ChainSched q = sch[c];
@@ -296,10 +300,10 @@ __global__ void k_tm_round_accept(int nc, int s, int B, int gen1, double rho, co
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(&dev->accepted, (unsigned int)__popcll(m));
 }
 
-__global__ void k_tm_round_rows(int N, int nc, int s, int B, const ChainSched *__restrict__ sch,
+__global__ void k_tm_round_rows(int N, int c_lo, int nc, int s, int B, const ChainSched *__restrict__ sch,
                                 const unsigned char *__restrict__ acc, const double *__restrict__ cand,
                                 double *__restrict__ leaders, double *__restrict__ db) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t e = (size_t)c_lo * N + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)nc * N) return;
   const int c = (int)(e / N);
   const ChainSched q = sch[c];
@@ -660,6 +664,59 @@ __global__ void k_tm_fill(double *p, size_t n, double v) {
   if (i < n) p[i] = v;
 }
 
+// ------------------------------------------------------- chain sharding
+// After its chains finished, a shard's rows of the database, leaders and
+// candidates (+ log-likelihoods / log-priors) and its accepted count travel
+// in one buffer of 64-bit words: own entries carry their IEEE bits, all
+// others INT64_MIN (the bits of -0.0).  A MAX all-reduce over the int64 view
+// then yields every owner's exact bits (max(INT64_MIN, x) = x for every
+// pattern x, including -0.0 itself), so the replicated state stays
+// bit-identical to the unsharded run.
+constexpr int XS_SECTIONS = 10;
+struct XchSec {
+  double *p;          // device array
+  unsigned long long off, n;  // offset in the exchange buffer, words
+  unsigned long long lo, hi;  // owned words [lo, hi) of the array
+};
+struct XchMap {
+  XchSec s[XS_SECTIONS];
+  int ns;
+};
+
+__global__ void k_tm_pack(XchMap m, unsigned long long total, long long *__restrict__ xch,
+                          const TmDev *__restrict__ dev, int rank) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  long long v = LLONG_MIN;
+  int k = 0;
+  while (k + 1 < m.ns && i >= m.s[k + 1].off) k++;
+  const XchSec q = m.s[k];
+  const unsigned long long j = i - q.off;
+  if (q.p) {
+    if (j >= q.lo && j < q.hi) v = __double_as_longlong(q.p[j]);
+  } else if ((int)j == rank) {
+    v = (long long)dev->accepted;  // accepted-count slots, one per rank
+  }
+  xch[i] = v;
+}
+
+__global__ void k_tm_unpack(XchMap m, unsigned long long total, const long long *__restrict__ xch, TmDev *dev,
+                            int world) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int k = 0;
+  while (k + 1 < m.ns && i >= m.s[k + 1].off) k++;
+  const XchSec q = m.s[k];
+  const unsigned long long j = i - q.off;
+  if (q.p) {
+    q.p[j] = __longlong_as_double(xch[i]);
+  } else if (j == 0) {
+    unsigned long long a = 0;
+    for (int r = 0; r < world; r++) a += (unsigned long long)xch[i + r];
+    dev->accepted = (unsigned int)a;
+  }
+}
+
 // ------------------------------------------------------------ host side
 // GSL mt19937 (rng/mt.c) for the Multinomial generator, whose consumption is
 // data-dependent and runs with the multinomial on the host.
@@ -886,7 +943,15 @@ struct kg_tmcmc_s {
   std::vector<double> perGenBurnIn;  // "Per Generation Burn In"
   std::vector<unsigned> hLen;        // host mirror of "Chain Lengths"
   int step = 0, maxSteps = 1;        // chain steps done / needed this generation
-  size_t pendingCount = 0;           // chains whose candidate awaits evaluation
+  size_t pendingCount = 0;           // own chains whose candidate awaits evaluation
+  // chain sharding: this rank's started chains [ca, cb), the rows it owns of
+  // candidates / leaders [ca, cbp) (the last rank also owns the chains that
+  // were not started), its database entries [dba, dbb), its first extra
+  // normal row zbase
+  int rank = 0, world = 1;
+  size_t ca = 0, cb = 0, cbp = 0, dba = 0, dbb = 0, zbase = 0;
+  long long *xch = nullptr;  // "Shard Exchange" (sharded handles only)
+  size_t xchWords = 0;
   bool rounds = false;               // this generation needs the general step schedule
   // per-distribution prior layout
   std::vector<int> distOf;           // variable -> distribution
@@ -1302,12 +1367,16 @@ int tm_ensure(T **p, size_t &cap, size_t n) {
 // chain c draws Uniform c and writes database entry c.  Otherwise the step
 // schedule (prefix sums in chain order) is built here and uploaded.
 int tm_schedule(kg_tmcmc_s *h) {
-  const size_t nc = (size_t)h->chainCount, B = (size_t)h->currentBurnIn;
-  KG_CHECK(nc <= (size_t)h->P && h->hLen.size() == (size_t)h->P, "inconsistent Chain Count / Chain Lengths");
-  h->rounds = !(B == 0 && nc == (size_t)h->P);
+  const size_t nc = (size_t)h->chainCount, B = (size_t)h->currentBurnIn, P = h->P;
+  KG_CHECK(nc <= P && h->hLen.size() == P, "inconsistent Chain Count / Chain Lengths");
+  h->rounds = !(B == 0 && nc == P);
   h->step = 0;
   h->maxSteps = 1;
-  if (!h->rounds) return 0;
+  if (!h->rounds) {
+    h->dba = h->ca;
+    h->dbb = h->cb;
+    return 0;
+  }
   size_t u = 0, z = 0, db = 0;
   for (size_t c = 0; c < nc; c++) {
     const size_t S = h->hLen[c] + B;
@@ -1318,21 +1387,60 @@ int tm_schedule(kg_tmcmc_s *h) {
     db += h->hLen[c];
     h->maxSteps = std::max(h->maxSteps, (int)S);
   }
-  KG_CHECK(db == (size_t)h->P, "the chain lengths of the started chains must sum to the population size");
+  KG_CHECK(db == P, "the chain lengths of the started chains must sum to the population size");
   KG_CHECK(u < (1ull << 32) && z < (1ull << 32), "chain schedule exceeds 32-bit indexing");
+  auto at = [&](size_t c, int f) -> size_t {  // prefix sums at chain c (c == nc: totals)
+    if (c < nc) return f == 0 ? h->hSch[c].z0 : h->hSch[c].db0;
+    return f == 0 ? z : db;
+  };
+  h->zbase = at(h->ca, 0);
+  const size_t zend = at(h->cb, 0);
+  h->dba = at(h->ca, 1);
+  h->dbb = at(h->cb, 1);
   KG_HIP(hipMemcpyAsync(h->sch, h->hSch, nc * sizeof(ChainSched), hipMemcpyHostToDevice, h->stream));
   // the generation's Uniform draws (one per step, chain-major) and its extra
-  // candidates' normals (after prepareGeneration's P x N)
+  // candidates' normals (after prepareGeneration's P x N); a shard counts
+  // the whole stream but materialises only its chains' rows
   if (tm_ensure(&h->U, h->capU, u)) return 1;
   if (h->uniform.uniforms(h->U, u, h->stream)) return 1;
   const size_t M = z * (size_t)h->N;
   if (M) {
-    if (tm_ensure(&h->Zx, h->capZx, M)) return 1;
+    if (tm_ensure(&h->Zx, h->capZx, std::max<size_t>(1, (zend - h->zbase) * h->N))) return 1;
     TmStage st(h, "rng_polar");
-    if (h->multivariate.polar_normals(h->Zx, M, h->N, nullptr, h->stream)) return 1;
+    if (h->multivariate.polar_normals(h->Zx, M, h->N, nullptr, h->stream, h->zbase * h->N, zend * h->N)) return 1;
     if (h->multivariate.consume_normals(M, h->N, nullptr, h->stream)) return 1;
   }
   return 0;
+}
+
+// this rank's share of the started chains (contiguous, in chain order)
+void tm_shard_ranges(kg_tmcmc_s *h) {
+  const size_t nc = (size_t)h->chainCount, W = h->world, r = h->rank;
+  h->ca = nc * r / W;
+  h->cb = nc * (r + 1) / W;
+  h->cbp = (r + 1 == W) ? (size_t)h->P : h->cb;
+}
+
+XchMap tm_xch_map(kg_tmcmc_s *h, size_t &total) {
+  const size_t N = h->N, P = h->P;
+  XchMap m{};
+  unsigned long long off = 0;
+  auto add = [&](double *p, size_t n, size_t lo, size_t hi) {
+    m.s[m.ns++] = XchSec{p, off, n, lo, hi};
+    off += n;
+  };
+  add(h->db, P * N, h->dba * N, h->dbb * N);
+  add(h->dbLL, P, h->dba, h->dbb);
+  add(h->dbLP, P, h->dba, h->dbb);
+  add(h->leaders, P * N, h->ca * N, h->cbp * N);
+  add(h->leadLL, P, h->ca, h->cbp);
+  add(h->leadLP, P, h->ca, h->cbp);
+  add(h->cand, P * N, h->ca * N, h->cbp * N);
+  add(h->candLL, P, h->ca, h->cbp);
+  add(h->candLP, P, h->ca, h->cbp);
+  add(nullptr, (size_t)h->world, 0, 0);
+  total = off;
+  return m;
 }
 
 struct TmField {
@@ -1369,6 +1477,10 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   VEC("Sample LogLikelihood Database", h->dbLL, P)
   VEC("Sample LogPrior Database", h->dbLP, P)
   VEC("Num Selections", h->numSel, P)
+  if (k == "Shard Exchange" && h->xch) {
+    r = {(double *)h->xch, nullptr, h->xchWords};
+    return true;
+  }
   SCA("Annealing Exponent", annealingExponent)
   SCA("Previous Annealing Exponent", previousAnnealingExponent)
   SCA("LogEvidence", logEvidence)
@@ -1413,6 +1525,12 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   auto *h = new kg_tmcmc_s();
   h->cfg = *cfg;
   h->cfg.per_generation_burn_in = nullptr;
+  h->world = cfg->shard_count > 1 ? cfg->shard_count : 1;
+  h->rank = h->world > 1 ? cfg->shard_rank : 0;
+  if (h->rank < 0 || h->rank >= h->world) {
+    delete h;
+    KG_CHECK(false, "shard_rank out of range");
+  }
   if (cfg->per_generation_burn_in_count)
     h->perGenBurnIn.assign(cfg->per_generation_burn_in, cfg->per_generation_burn_in + cfg->per_generation_burn_in_count);
   double maxBurn = cfg->default_burn_in;
@@ -1458,6 +1576,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)(CV_MAX_PTS + 1) * P) | tdalloc(&h->w, P);
   rc |= tdalloc(&h->uoff, N) | tdalloc(&h->ustride, N) | tdalloc(&h->src, P) | tdalloc(&h->acc, P);
   rc |= tdalloc(&h->pend, P) | tdalloc(&h->sch, P) | tdalloc(&h->dLen, P);
+  h->xchWords = 3 * (PN + 2 * (size_t)P) + h->world;
+  if (cfg->shard_count >= 1) rc |= tdalloc(&h->xch, h->xchWords);  // explicitly sharded (even one rank)
   rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
   rc |= tdalloc(&h->fA, PN + 2) | tdalloc(&h->fB, PN + 2);
   rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
@@ -1547,7 +1667,7 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->pmax, (void *)h->negLogWidth, (void *)h->Z, (void *)h->U, (void *)h->Uprior,
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
                   (void *)h->dev, h->cvPart, (void *)h->pairs, (void *)h->pend, (void *)h->sch, (void *)h->Zx,
-                  (void *)h->dLen,
+                  (void *)h->dLen, (void *)h->xch,
                   (void *)h->fA, (void *)h->fB})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
@@ -1570,6 +1690,8 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   if (tm_sync_dev(h)) return 1;
   // prepareGeneration :161-170
   h->currentBurnIn = tm_burn_in(h, generation);
+  tm_shard_ranges(h);
+
   h->acceptedSamplesCount = 0;
   h->maxLoglikelihood = -INFINITY;
   h->dbCount = 0;
@@ -1592,7 +1714,7 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   } else {
     {
       TmStage st(h, "rng_polar");
-      if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream)) return 1;
+      if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream, h->ca * N, h->cbp * N)) return 1;
       if (h->multivariate.consume_normals(PN, N, nullptr, h->stream)) return 1;
       // the next generation's words are produced on the side stream while
       // this generation's search runs on the host
@@ -1601,14 +1723,19 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
     TmStage st(h, "draw");
     const int CB = std::max(1, 256 / N);
     const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)CB * N * sizeof(double);
-    hipLaunchKernelGGL(k_tm_draw<false>, dim3(nblk(P, CB)), dim3(256), lbytes, h->stream, N, P, h->Z, h->chol,
-                       h->leaders, h->cand, (const ChainSched *)nullptr, 0, (unsigned char *)nullptr);
+    if (h->cbp > h->ca)
+      hipLaunchKernelGGL(k_tm_draw<false>, dim3(nblk(h->cbp - h->ca, CB)), dim3(256), lbytes, h->stream, N, (int)h->ca,
+                         (int)h->cbp, h->Z, h->chol, h->leaders, h->cand, (const ChainSched *)nullptr, 0, 0u,
+                         (unsigned char *)nullptr);
     KG_HIP(hipGetLastError());
   }
-  // chains c < Chain Count start with their prepared candidate (:114-130)
-  hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, (int)h->chainCount, h->pend);
+  // started chains (c < Chain Count) begin with their prepared candidate
+  // (:114-130); _modelEvaluationCount++ per started sample (:127)
+  hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, (int)h->ca, (int)h->cb,
+                     h->pend);
   KG_HIP(hipGetLastError());
-  h->pendingCount = (size_t)h->chainCount;
+  h->pendingCount = h->cb - h->ca;
+  h->modelEvaluationCount += h->chainCount;
   return tm_schedule(h);
 }
 
@@ -1617,7 +1744,6 @@ int kg_tmcmc_evaluate(kg_tmcmc_t h) {
   hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, h->cfg.likelihood,
                      h->cand, h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP, h->pend);
   KG_HIP(hipGetLastError());
-  h->modelEvaluationCount += (double)h->pendingCount;  // _modelEvaluationCount++ per started sample (:127)
   return 0;
 }
 
@@ -1653,7 +1779,6 @@ int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double
                      h->candLP, h->candLL);
   KG_HIP(hipGetLastError());
   KG_HIP(hipStreamSynchronize(h->stream));
-  h->modelEvaluationCount += (double)h->pendingCount;
   return 0;
 }
 
@@ -1665,52 +1790,81 @@ int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending) {
     // every chain runs one step: Uniform c, database entry c
     TmStage st(h, "accept");
     if (h->uniform.uniforms(h->U, P, h->stream)) return 1;
-    hipLaunchKernelGGL(k_tm_accept, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, generation == 1 ? 1 : 0,
-                       h->annealingExponent, h->U, h->candLL, h->candLP, h->leadLL, h->leadLP, h->dbLL, h->dbLP,
-                       h->acc, h->dev);
-    hipLaunchKernelGGL(k_tm_copy_rows, dim3(nblk((size_t)P * N, 256)), dim3(256), 0, h->stream, N, P, h->acc,
-                       h->cand, h->leaders, h->db);
-    KG_HIP(hipGetLastError());
-    h->pendingCount = 0;
-  } else {
-    const int nc = (int)h->chainCount, B = (int)h->currentBurnIn;
-    {
-      TmStage st(h, "accept");
-      hipLaunchKernelGGL(k_tm_round_accept, dim3(nblk(nc, 256)), dim3(256), 0, h->stream, nc, s, B,
-                         generation == 1 ? 1 : 0, h->annealingExponent, h->sch, h->U, h->candLL, h->candLP,
-                         h->leadLL, h->leadLP, h->dbLL, h->dbLP, h->acc, h->dev);
-      hipLaunchKernelGGL(k_tm_round_rows, dim3(nblk((size_t)nc * N, 256)), dim3(256), 0, h->stream, N, nc, s, B,
-                         h->sch, h->acc, h->cand, h->leaders, h->db);
+    const int a = (int)h->ca, b = (int)h->cb;
+    if (b > a) {
+      hipLaunchKernelGGL(k_tm_accept, dim3(nblk(b - a, 256)), dim3(256), 0, h->stream, a, b, generation == 1 ? 1 : 0,
+                         h->annealingExponent, h->U, h->candLL, h->candLP, h->leadLL, h->leadLP, h->dbLL, h->dbLP,
+                         h->acc, h->dev);
+      hipLaunchKernelGGL(k_tm_copy_rows, dim3(nblk((size_t)(b - a) * N, 256)), dim3(256), 0, h->stream, N, a, b,
+                         h->acc, h->cand, h->leaders, h->db);
       KG_HIP(hipGetLastError());
     }
-    size_t more = 0;
-    for (int c = 0; c < nc; c++) more += (int)h->hSch[c].S > s;
-    if (more) {
+    h->pendingCount = 0;
+    h->step = h->maxSteps;
+  } else {
+    const int a = (int)h->ca, b = (int)h->cb, B = (int)h->currentBurnIn;
+    if (b > a) {
+      TmStage st(h, "accept");
+      hipLaunchKernelGGL(k_tm_round_accept, dim3(nblk(b - a, 256)), dim3(256), 0, h->stream, a, b, s, B,
+                         generation == 1 ? 1 : 0, h->annealingExponent, h->sch, h->U, h->candLL, h->candLP,
+                         h->leadLL, h->leadLP, h->dbLL, h->dbLP, h->acc, h->dev);
+      hipLaunchKernelGGL(k_tm_round_rows, dim3(nblk((size_t)(b - a) * N, 256)), dim3(256), 0, h->stream, N, a, b, s,
+                         B, h->sch, h->acc, h->cand, h->leaders, h->db);
+      KG_HIP(hipGetLastError());
+    }
+    size_t more = 0, mine = 0;
+    for (int c = 0; c < (int)h->chainCount; c++)
+      if ((int)h->hSch[c].S > s) {
+        more++;
+        mine += (c >= a && c < b);
+      }
+    if (mine) {
       TmStage st(h, "draw");
       const int CB = std::max(1, 256 / N);
       const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)CB * N * sizeof(double);
-      hipLaunchKernelGGL(k_tm_draw<true>, dim3(nblk(nc, CB)), dim3(256), lbytes, h->stream, N, nc, h->Zx, h->chol,
-                         h->leaders, h->cand, h->sch, s, h->pend);
+      hipLaunchKernelGGL(k_tm_draw<true>, dim3(nblk(b - a, CB)), dim3(256), lbytes, h->stream, N, a, b, h->Zx,
+                         h->chol, h->leaders, h->cand, h->sch, s, (unsigned)h->zbase, h->pend);
       KG_HIP(hipGetLastError());
     } else {
-      hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, 0, h->pend);
+      hipLaunchKernelGGL(k_tm_pend_init, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, 0, 0, h->pend);
       KG_HIP(hipGetLastError());
     }
-    h->pendingCount = more;
+    h->pendingCount = mine;
+    h->modelEvaluationCount += (double)more;  // the next step's started samples (:127)
+    if (s >= h->maxSteps) h->step = h->maxSteps;
   }
-  if (h->pendingCount == 0) h->step = h->maxSteps;
   if (pending) *pending = h->pendingCount;
   return 0;
 }
 
-int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
-  const int N = h->N, P = h->P;
-  const size_t PN = (size_t)P * N;
+int kg_tmcmc_process_partial(kg_tmcmc_t h, size_t generation) {
   // the chains' remaining steps with the builtin likelihood
   while (h->step < h->maxSteps) {
     size_t more = 0;
     if (kg_tmcmc_advance(h, generation, &more)) return 1;
     if (more && kg_tmcmc_evaluate(h)) return 1;
+  }
+  if (h->xch) {
+    size_t total = 0;
+    const XchMap m = tm_xch_map(h, total);
+    hipLaunchKernelGGL(k_tm_pack, dim3(nblk(total, 256)), dim3(256), 0, h->stream, m, (unsigned long long)total,
+                       h->xch, h->dev, h->rank);
+    KG_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
+  (void)generation;
+  const int N = h->N, P = h->P;
+  const size_t PN = (size_t)P * N;
+  KG_CHECK(h->step >= h->maxSteps, "kg_tmcmc_process_finalize: chains have steps left (call process_partial)");
+  if (h->xch) {
+    size_t total = 0;
+    const XchMap m = tm_xch_map(h, total);
+    hipLaunchKernelGGL(k_tm_unpack, dim3(nblk(total, 256)), dim3(256), 0, h->stream, m, (unsigned long long)total,
+                       h->xch, h->dev, h->world);
+    KG_HIP(hipGetLastError());
   }
   {
     TmStage st(h, "accept");
@@ -1825,6 +1979,12 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
   return 0;
 }
 
+int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
+  KG_CHECK(h->world == 1, "sharded TMCMC over several ranks: call process_partial, all-reduce 'Shard Exchange', process_finalize");
+  if (kg_tmcmc_process_partial(h, generation)) return 1;
+  return kg_tmcmc_process_finalize(h, generation);
+}
+
 int kg_tmcmc_generation(kg_tmcmc_t h, size_t generation) {
   if (kg_tmcmc_prepare(h, generation)) return 1;
   if (kg_tmcmc_evaluate(h)) return 1;
@@ -1895,6 +2055,18 @@ int kg_tmcmc_set_rng(kg_tmcmc_t h, int which, const void *state5000) {
   if (which == 0) return h->multinomialRng.load((const unsigned char *)state5000);
   MtStream &m = which == 1 ? h->multivariate : which == 2 ? h->uniform : *h->priorRng[which - 3];
   return m.import_gsl(state5000, h->stream);
+}
+
+int kg_tmcmc_device_ptr(kg_tmcmc_t h, const char *name, void **ptr) {
+  TmField r;
+  KG_CHECK(tm_field(h, name, r) && r.dev, std::string("unknown TMCMC device field: ") + name);
+  *ptr = r.dev;
+  return 0;
+}
+
+int kg_tmcmc_stream(kg_tmcmc_t h, void **stream) {
+  *stream = (void *)h->stream;
+  return 0;
 }
 
 int kg_tmcmc_profile(kg_tmcmc_t h, int enable) {

@@ -48,7 +48,7 @@ class _TmcmcCfg(C.Structure):
         ("prior_seeds", C.POINTER(C.c_uint64)), ("multinomial_seed", C.c_uint64),
         ("multivariate_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("likelihood", C.c_int),
         ("device", C.c_int), ("per_generation_burn_in", C.POINTER(C.c_double)),
-        ("per_generation_burn_in_count", C.c_size_t),
+        ("per_generation_burn_in_count", C.c_size_t), ("shard_rank", C.c_int), ("shard_count", C.c_int),
     ]
 
 
@@ -62,7 +62,8 @@ EXPORTED = [
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
-    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_advance", "kg_tmcmc_get_pending", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
+    "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_advance", "kg_tmcmc_get_pending",
+    "kg_tmcmc_process_partial", "kg_tmcmc_process_finalize", "kg_tmcmc_device_ptr", "kg_tmcmc_stream", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump",
 ]
 
@@ -103,7 +104,10 @@ def lib():
         L.kg_tmcmc_create.argtypes = [C.POINTER(_TmcmcCfg), C.POINTER(vp)]
         for f in ("kg_tmcmc_destroy", "kg_tmcmc_synchronize", "kg_tmcmc_evaluate", "kg_tmcmc_evaluate_prior"):
             getattr(L, f).argtypes = [vp]
-        for f in ("kg_tmcmc_generation", "kg_tmcmc_prepare", "kg_tmcmc_process"):
+        L.kg_tmcmc_device_ptr.argtypes = [vp, cp, C.POINTER(vp)]
+        L.kg_tmcmc_stream.argtypes = [vp, C.POINTER(vp)]
+        for f in ("kg_tmcmc_generation", "kg_tmcmc_prepare", "kg_tmcmc_process", "kg_tmcmc_process_partial",
+                  "kg_tmcmc_process_finalize"):
             getattr(L, f).argtypes = [vp, sz]
         L.kg_tmcmc_field_size.argtypes = [vp, cp, C.POINTER(sz)]
         L.kg_tmcmc_get_field.argtypes = [vp, cp, dp, sz]
@@ -290,7 +294,7 @@ class TmcmcDevice:
     def __init__(self, N, P, prior_min, prior_max, prior_seeds=None, prior_distribution=None,
                  multinomial_seed=0, multivariate_seed=0, uniform_seed=0, target_cov=1.0, covariance_scaling=0.04,
                  min_annealing_exponent_update=1e-5, max_annealing_exponent_update=1.0, max_chain_length=1,
-                 default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0):
+                 default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0, shard_rank=0, shard_count=0):
         L = lib()
         self.N, self.P = int(N), int(P)
         pdist = (np.arange(self.N, dtype=np.int32) if prior_distribution is None
@@ -315,6 +319,7 @@ class TmcmcDevice:
         cfg.likelihood, cfg.device = int(likelihood), int(device)
         cfg.per_generation_burn_in = _dptr(pgb) if pgb.size else None
         cfg.per_generation_burn_in_count = pgb.size
+        cfg.shard_rank, cfg.shard_count = int(shard_rank), int(shard_count)
         h = C.c_void_p()
         check(L.kg_tmcmc_create(C.byref(cfg), C.byref(h)))
         self.h = h
@@ -339,6 +344,22 @@ class TmcmcDevice:
 
     def process(self, generation):
         check(self._L.kg_tmcmc_process(self.h, int(generation)))
+
+    def process_partial(self, generation):
+        check(self._L.kg_tmcmc_process_partial(self.h, int(generation)))
+
+    def process_finalize(self, generation):
+        check(self._L.kg_tmcmc_process_finalize(self.h, int(generation)))
+
+    def device_ptr(self, name):
+        p = C.c_void_p()
+        check(self._L.kg_tmcmc_device_ptr(self.h, name.encode(), C.byref(p)))
+        return p.value
+
+    def stream(self):
+        p = C.c_void_p()
+        check(self._L.kg_tmcmc_stream(self.h, C.byref(p)))
+        return p.value
 
     def advance(self, generation):
         """One step of every unfinished chain; returns how many chains now

@@ -1,4 +1,5 @@
-"""Population-sharded CMA-ES over torch.distributed.
+"""Population-sharded CMA-ES and chain-sharded TMCMC
+(§8 f2) over torch.distributed.
 
 One process per GPU; every rank holds the replicated solver state (mean, C,
 B, D, paths, σ, generator states) in its own kg_cmaes_t handle created with
@@ -28,15 +29,15 @@ bit-exact for identical state), exactly as SURVEY.md §8(e) item 5 states.
 """
 import numpy as np
 
-from .native import CmaesDevice
+from .native import CmaesDevice, TmcmcDevice
 
 
 class _DeviceArray:
     """__cuda_array_interface__ view of a device buffer (torch.as_tensor
     wraps it without copying)."""
 
-    def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": "<f8", "data": (int(ptr), False),
+    def __init__(self, ptr, n, typestr="<f8"):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(ptr), False),
                                          "version": 3, "strides": None}
 
 
@@ -56,6 +57,17 @@ def allgather_shards(dist, local, world, group=None):
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t, group=group)
     return torch.cat(parts).numpy()
+
+
+def allreduce_max_bits(dist, arr, group=None):
+    """Host transport: element-wise MAX over ranks of the 64-bit patterns of a
+    float64 array (int64 view).  With non-owned entries set to INT64_MIN (the
+    bits of -0.0) this gathers every owner's exact bits."""
+    import torch
+    bits = np.ascontiguousarray(arr, dtype=np.float64).view(np.int64).copy()
+    t = torch.from_numpy(bits)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.numpy().view(np.float64)
 
 
 def allreduce_sum(dist, arr, group=None):
@@ -116,6 +128,59 @@ class ShardedCmaes:
         d.update_partial(generation)
         self._reduce_partials()
         d.update_finalize(generation)
+
+    def synchronize(self):
+        self.dev.synchronize()
+
+    def close(self):
+        self.dev.close()
+
+
+class ShardedTmcmc:
+    """TMCMC generation loop with the started chains split across the ranks
+    of a torch.distributed group (one kg_tmcmc_t per rank, state
+    replicated).  Per generation (TMCMC::runGeneration, TMCMC.cpp.base:
+    107-157): Cholesky replicated; each rank draws, evaluates and steps only
+    its contiguous share of the chains (the Multivariate / Uniform streams are
+    counted whole, so positions are global); one MAX all-reduce over the
+    int64 bits of the "Shard Exchange" buffer gathers the database, leader and
+    candidate rows and accepted counts exactly; processGeneration (annealing
+    search, multinomial resampling, weighted mean / covariance, leader
+    expansion) then runs replicated, so every rank holds the unsharded run's
+    state bit for bit."""
+
+    def __init__(self, N, P, dist, group=None, device=0, transport="device", **tmcmc_kw):
+        self.dist, self.group = dist, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.dev = TmcmcDevice(N, P, shard_rank=self.rank, shard_count=self.world, device=device, **tmcmc_kw)
+        self.transport = transport
+        if transport == "device":
+            import torch
+            dv = torch.device("cuda", device)
+            n = self.dev.field_size("Shard Exchange")
+            self._X = torch.as_tensor(_DeviceArray(self.dev.device_ptr("Shard Exchange"), n, "<i8"), device=dv)
+            self._stream = torch.cuda.ExternalStream(self.dev.stream(), device=dv)
+        elif transport != "host":
+            raise ValueError("transport must be 'device' or 'host'")
+
+    def _exchange(self):
+        if self.world == 1:
+            return
+        if self.transport == "device":
+            import torch
+            with torch.cuda.stream(self._stream):
+                self.dist.all_reduce(self._X, op=self.dist.ReduceOp.MAX, group=self.group)
+        else:
+            self.dev["Shard Exchange"] = allreduce_max_bits(self.dist, self.dev["Shard Exchange"], self.group)
+
+    def generation(self, generation):
+        d = self.dev
+        d.prepare(generation)
+        d.evaluate()
+        d.process_partial(generation)
+        self._exchange()
+        d.process_finalize(generation)
 
     def synchronize(self):
         self.dev.synchronize()

@@ -31,3 +31,17 @@ def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend)
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "SHARD_CHECK PASS" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("ranks,N,P,gens,mcl,burn,backend", [(2, 4, 600, 8, 1, 0, "gloo"), (3, 3, 500, 8, 3, 1, "gloo"),
+                                                             (4, 32, 1024, 4, 2, 2, "gloo"),
+                                                             (1, 8, 512, 5, 2, 1, "nccl")])
+def test_sharded_tmcmc_matches_unsharded(ranks, N, P, gens, mcl, burn, backend):
+    """Chain sharding: every rank's state bit-identical to
+    the unsharded run after the MAX all-reduce of the exchange words."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.join(ROOT, "tools", "shard_check_tmcmc.py"), str(N), str(P), str(gens), str(mcl), str(burn), backend]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "SHARD_CHECK PASS" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from korali_amd.sharded import allgather_shards, allreduce_sum, shard_range
+from korali_amd.sharded import allgather_shards, allreduce_max_bits, allreduce_sum, shard_range
 
 
 def test_shard_range_partitions_population():
@@ -49,3 +49,34 @@ def test_host_transport_collectives_world2():
     expect = (1.0 + 2.0) * np.array([1.0, 0.5, 0.25, 1e-300, -2.0])
     for _, _, red in res:
         assert red == expect.tolist()
+
+
+def _max_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    vals = np.array([-0.0, 0.0, np.inf, -np.inf, np.nan, 1e-310, -3.5, 2.0 ** 60, -1e300, 7.0, -0.0, 5.0])
+    own = np.arange(vals.size) % world == rank
+    bits = vals.view(np.int64).copy()
+    bits[~own] = np.iinfo(np.int64).min      # INT64_MIN = bits of -0.0
+    got = allreduce_max_bits(dist, bits.view(np.float64))
+    q.put((rank, got.view(np.int64).tolist() == vals.view(np.int64).tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_max_bits_allreduce_gathers_exact_patterns(world):
+    """TMCMC chain sharding's exchange (kg_tmcmc_process_partial/finalize):
+    owners' IEEE bit patterns (incl. -0.0, NaN, subnormals) survive a MAX
+    all-reduce over the int64 view with INT64_MIN elsewhere."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_max_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok in res)
