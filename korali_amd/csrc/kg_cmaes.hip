@@ -494,10 +494,16 @@ __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, 
 
 // gather the μ selected rows into Y (contiguous; shared by mean and adaptC)
 __global__ void __launch_bounds__(256) k_gather_selected(int N, int mu, const double *__restrict__ X,
-                                                         const unsigned *__restrict__ idx, double *__restrict__ Y) {
+                                                         const unsigned *__restrict__ idx, double *__restrict__ Y,
+                                                         const double *__restrict__ mean,
+                                                         double *__restrict__ prevMean) {
   const int i = blockIdx.x;
   const size_t src = (size_t)idx[i] * N;
   for (int d = threadIdx.x; d < N; d += blockDim.x) Y[(size_t)i * N + d] = X[src + d];
+  // m_prev (updateDistribution :603): read by k_mean and, concurrently, by
+  // the rank-mu sum on the second stream
+  if (i == 0)
+    for (int d = threadIdx.x; d < N; d += blockDim.x) prevMean[d] = mean[d];
 }
 
 // mean :603-609 and mean update :623-624.  The sum over the μ selected rows
@@ -553,8 +559,7 @@ __global__ void __launch_bounds__(256) k_mean(int N, int mu, const double *__res
   }
   if (tid < nd) {
     const int d = d0 + tid;
-    const double prev = mean[d];
-    prevMean[d] = prev;
+    const double prev = prevMean[d];  // copied by k_gather_selected
     mean[d] = acc;
     meanUpdate[d] = (acc - prev) / sc->sigma;
   }
@@ -707,7 +712,13 @@ __global__ void __launch_bounds__(64) k_rankmu_mfma(int N, int mu, int kslices, 
   const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
   const int d = td * 16 + li, e = te * 16 + li;
   const double pmd = d < N ? prevMean[d] : 0.0, pme = e < N ? prevMean[e] : 0.0;
-  const double scale = sc->ccovmu / (sc->sigma * sc->sigma);
+  // c_mu from mu_eff with k_paths' formula (CMAES.cpp.base:693-694): this
+  // kernel runs concurrently with k_paths, which stores the same value
+  const double effMu = sc->effectiveMu, ca = N + 1.3, cb = N + 2.0;
+  const double ccov1 = 2.0 / (ca * ca + effMu);
+  double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (cb * cb + effMu);
+  if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+  const double scale = ccovmu / (sc->sigma * sc->sigma);
   const int per = ((mu + kslices - 1) / kslices + 3) & ~3;
   const int kbeg = slice * per, kend = (kbeg + per) < mu ? (kbeg + per) : mu;
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -960,6 +971,8 @@ struct kg_cmaes_s {
   int N = 0, lam = 0, mu = 0, R = 0;
   bool finiteBounds = false;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // the rank-mu sum, concurrent with the mean and the paths
+  hipEvent_t evY = nullptr, evC = nullptr;
   double *mean = nullptr, *prevMean = nullptr, *C = nullptr, *B = nullptr, *D = nullptr, *pc = nullptr,
          *ps = nullptr, *w = nullptr, *X = nullptr, *Xall = nullptr, *BDZ = nullptr, *BDZall = nullptr,
          *F = nullptr, *Z = nullptr, *bestEverVars = nullptr, *currBestVars = nullptr, *meanUpdate = nullptr,
@@ -1240,6 +1253,9 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  KG_HIP(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+  KG_HIP(hipEventCreateWithFlags(&h->evY, hipEventDisableTiming));
+  KG_HIP(hipEventCreateWithFlags(&h->evC, hipEventDisableTiming));
   {
     const char *ev = getenv("KORALI_AMD_EIGEN_CHASE");
     bool hostChase = !cfg->eigen_device_chase;
@@ -1289,6 +1305,12 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
     (void)hipEventDestroy(std::get<1>(t));
     (void)hipEventDestroy(std::get<2>(t));
   }
+  if (h->stream2) {
+    (void)hipStreamSynchronize(h->stream2);
+    (void)hipStreamDestroy(h->stream2);
+  }
+  if (h->evY) (void)hipEventDestroy(h->evY);
+  if (h->evC) (void)hipEventDestroy(h->evC);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -1315,13 +1337,18 @@ int kg_cmaes_sample(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
   const size_t rows = (size_t)L + h->R;
   if (h->normal.prefetch(rows * N, h->stream)) return 1;  // overlaps the eigensolver
+  {
+    // the polar pass reads only the generator stream: it runs on the
+    // producer's side stream too, concurrently with the eigensolver
+    const bool shard = h->shards > 1;
+    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->normal.side_stream(),
+                                shard ? (size_t)h->r0 * N : 0, shard ? (size_t)h->r1 * N : (size_t)-1))
+      return 1;
+  }
   if (cmaes_eigen(h)) return 1;
   {
-    Stage st(h, "rng_polar");
-    const bool shard = h->shards > 1;
-    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->stream, shard ? (size_t)h->r0 * N : 0,
-                                shard ? (size_t)h->r1 * N : (size_t)-1))
-      return 1;
+    Stage st(h, "rng_polar");  // what of the producer + polar pass the eigensolver did not hide
+    if (h->normal.join(h->stream)) return 1;
   }
   {
     Stage st(h, "transform");
@@ -1440,7 +1467,19 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
                        (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
                        h->sc);
-    hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y);
+    hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y, h->mean,
+                       h->prevMean);
+    if (h->cfg.cov_mode == KG_COV_MFMA) {
+      // the rank-mu sum needs only Y, the weights and m_prev: it runs on the
+      // second stream while the mean and the evolution paths are computed
+      const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
+      KG_HIP(hipEventRecord(h->evY, h->stream));
+      KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
+      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream2, N, mu, h->kslices, h->Y,
+                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
+      KG_HIP(hipGetLastError());
+      KG_HIP(hipEventRecord(h->evC, h->stream2));
+    }
     hipLaunchKernelGGL(k_mean, dim3((N + MN_D - 1) / MN_D), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
                        h->prevMean, h->meanUpdate, h->sc);
     if (cmaes_paths(h, generation)) return 1;
@@ -1449,8 +1488,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     Stage st(h, "covariance");
     const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
     if (h->cfg.cov_mode == KG_COV_MFMA) {
-      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, mu, h->kslices, h->Y,
-                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
+      KG_HIP(hipStreamWaitEvent(h->stream, h->evC, 0));
       hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
@@ -1529,9 +1567,11 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
             "%d steps, %d rotations\n[korali_amd apply trace] groups %llu time-units %llu steps %llu ticks %llu\n"
             "[korali_amd multi-workgroup tridiag, writer wg] dnrm2 %llu householder %llu dsymv-stage %llu dsymv-chain "
             "%llu x-gather %llu xv-stage %llu xv-chain %llu alpha %llu pivot-poll %llu update %llu\n"
-            "[korali_amd streamed apply] batches %llu steps-before-chase-done %llu ticks-to-first-batch %llu\n",
+            "[korali_amd streamed apply] batches %llu steps-before-chase-done %llu ticks-to-first-batch %llu\n"
+            "[korali_amd one-workgroup tridiag] householder %llu barrier %llu dsymv %llu xv %llu x-update %llu "
+            "pivot-update %llu chain-w0 %llu chain-w3 %llu\n",
             t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7], t[16], t[17], t[18], t[19], t[20], t[21],
-            t[22], t[23], t[24], t[25], t[26], t[27], t[28]);
+            t[22], t[23], t[24], t[25], t[26], t[27], t[28], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]);
   }
   return check_errors(h);
 }

@@ -308,6 +308,67 @@ __device__ double dnrm2_wave(const double *x, int stride, int m, double *sv, uns
   return (m == 1) ? fabs(x[0]) : carry * sqrt(ssq);
 }
 
+// dnrm2_wave for m <= 128 (the one-workgroup tridiagonalisation): both
+// 64-element chunks are staged at once (independent DPP prefix maxima, one
+// division per element — before / a for a new maximum, a / before otherwise —
+// as a select of operands, no divergent branches), the rescale masks stay in
+// scalar registers; the ordered ssq recurrence is dnrm2_wave's.
+__device__ double dnrm2_wave128(const double *x, int m, double *sv) {
+  const int lane = threadIdx.x & 63;
+  const int m8 = (m + 7) & ~7;
+  const int e0 = lane, e1 = lane + 64;
+  const double r0 = fabs(x[min(e0, m - 1)]), r1 = fabs(x[min(e1, m - 1)]);
+  const double a0 = e0 < m ? r0 : 0.0, a1 = e1 < m ? r1 : 0.0;
+  const double pm0 = wave_prefix_max_nonneg(a0), pm1 = wave_prefix_max_nonneg(a1);
+  const double c0 = readlane_d(pm0, 63);
+  const double b0 = dpp_d<0x138, 0xf>(pm0);            // before, chunk 0 (lane 0: 0.0)
+  const double b1 = fmax(dpp_d<0x138, 0xf>(pm1), c0);  // before, chunk 1
+  const bool z0 = e0 < m && a0 != 0.0, z1 = e1 < m && a1 != 0.0;
+  const bool n0 = z0 && b0 < a0, n1 = z1 && b1 < a1;
+  const double q0 = (n0 ? b0 : a0) / (n0 ? a0 : b0), q1 = (n1 ? b1 : a1) / (n1 ? a1 : b1);
+  const unsigned long long k0 = __ballot(n0), k1 = __ballot(n1);
+  if (e0 < m8) sv[e0] = n0 ? q0 : (z0 ? q0 * q0 : 0.0);
+  if (e1 < m8) sv[e1] = n1 ? q1 : (z1 ? q1 * q1 : 0.0);
+  const double carry = fmax(c0, readlane_d(pm1, 63));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double ssq = 1.0;
+#define KG_NRM2_STEP8(T, BITS)                        \
+  {                                                   \
+    const unsigned bits_ = (BITS);                    \
+    if (bits_ == 0) {                                 \
+      _Pragma("unroll") for (int u = 0; u < 8; u++) ssq += T[u]; \
+    } else {                                          \
+      _Pragma("unroll") for (int u = 0; u < 8; u++) { \
+        if ((bits_ >> u) & 1u)                        \
+          ssq = 1.0 + ssq * T[u] * T[u];              \
+        else                                          \
+          ssq += T[u];                                \
+      }                                               \
+    }                                                 \
+  }
+  for (int cb = 0; cb < m8; cb += 64) {
+    const unsigned long long mw = cb ? k1 : k0;
+    const int cn = (m8 - cb) < 64 ? (m8 - cb) : 64;
+    double a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = sv[cb + u];
+    for (int e = 0; e < cn; e += 16) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) b[u] = sv[cb + e + 8 + u];
+      KG_NRM2_STEP8(a, (unsigned)((mw >> e) & 0xffULL))
+      if (e + 8 >= cn) break;
+#pragma unroll
+      for (int u = 0; u < 8; u++) a[u] = sv[cb + e + 16 + u];
+      KG_NRM2_STEP8(b, (unsigned)((mw >> (e + 8)) & 0xffULL))
+    }
+  }
+#undef KG_NRM2_STEP8
+  __builtin_amdgcn_wave_barrier();
+  return (m == 1) ? fabs(x[0]) : carry * sqrt(ssq);
+}
+
 }  // namespace
 
 // Dynamic LDS: [matrix region N*(N+1) doubles if lds_mats] + vectors.
@@ -817,6 +878,237 @@ __global__ void __launch_bounds__(TMW_TPB) k_tridiag_mw(int N, const double *__r
   }
 }
 
+// ------------------------------------------------------------------------
+// Phase A in ONE workgroup for N <= 128 (the full symmetric matrix in LDS,
+// 132 KB at N = 128): no in-launch hand-offs at all.  Per Householder step i
+// (n = N-i-1), with the same operations in the same order as k_tridiag_mw:
+//   A  wave 0: dnrm2 of the pivot row, the Householder scalars (every lane
+//      redundantly, no broadcast), the scaled v / tau v and the outputs;
+//      waves 1..15 meanwhile finish the previous step's rank-2 update
+//   E  dsymv: waves 0-1 run the descending chains, waves 2-3 the ascending
+//      chains of rows i+1.., one SIMD each, products formed inline 8 ahead
+//   G  x_j = acc_j + tau t2_j and the xv products (all threads)
+//   I  wave 0: the xv chain, alpha
+//   K  x += alpha v
+//   M  rank-2 update of the trailing block: wave 0 updates the next pivot
+//      row first and goes straight on to the next step's dnrm2 while waves
+//      1..15 update rows i+2.. (the column below the pivot is never read
+//      again and is skipped).  Its element formula needs no case split:
+//        m[a][b] += (-v_a) x_b + (-x_a) v_b   (a >= b, dsyr2 Lower)
+//      has the same two rounded products as (-v_b) x_a + (-x_b) v_a, so both
+//      triangles get fl(m + fl(fl(-v_r x_c) + fl(-x_r v_c))) for row r.
+// v is double-buffered across steps because A of step i+1 (wave 0) writes it
+// while the rank-2 update of step i still reads it.
+constexpr int T1_TPB = 1024;
+__host__ __device__ inline size_t t1_lds_doubles(int N) {
+  return (size_t)N * (N + 1) + 2 * (128 + (size_t)(N + 32)) + (N + 64) + 3 * (size_t)(N + 32) + 16 + 8;
+}
+bool t1_fits(int N) { return N >= 3 && N <= 128 && t1_lds_doubles(N) * sizeof(double) <= 160 * 1024; }
+
+// acc = 0 + sum_{t < T} a[S t] b[S t] (S = -1 descending, +1 ascending), T
+// wave-uniform; products of the next 8 formed while the current 8 are added,
+// p / q swapping roles.  Callers align every lane's own chain to the end of
+// the T steps: its leading steps read zero-padded operands (0 x finite =
+// +-0.0, and a sum that starts at +0.0 is unchanged by adding +-0.0 under
+// round-to-nearest), so no lane needs a mask.
+template <int S>
+__device__ __forceinline__ double padded_chain(const double *a, const double *b, int T_) {
+  const int T = __builtin_amdgcn_readfirstlane(T_);
+  double acc = 0.0;
+  int t = 0;
+  if (T >= 8) {
+    double p[8], q[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) p[u] = a[S * u] * b[S * u];
+    t = 8;
+    for (; t + 16 <= T; t += 16) {
+      const double *at = a + S * t, *bt = b + S * t;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        q[u] = at[S * u] * bt[S * u];
+        acc += p[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        p[u] = at[S * (8 + u)] * bt[S * (8 + u)];
+        acc += q[u];
+      }
+    }
+    if (t + 8 <= T) {
+      const double *at = a + S * t, *bt = b + S * t;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        q[u] = at[S * u] * bt[S * u];
+        acc += p[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) p[u] = q[u];
+      t += 8;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += p[u];
+  }
+  for (; t < T; t++) acc += a[S * t] * b[S * t];
+  return acc;
+}
+
+__global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__restrict__ C, double *gH,
+                                                        double *tauOut, double *dOut, double *sdOut,
+                                                        unsigned long long *trace) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int lda = N + 1, VS = N + 32;
+  double *M = smem;                    // row r at r*lda; column N is a zero pad
+  double *vbuf = M + (size_t)N * lda;  // v (v_0 = 1), two buffers (step parity),
+                                       // each after 128 zeros
+  double *tv = vbuf + 2 * (128 + VS);  // tau v, zeros from index n to n+63
+  double *xl = tv + (N + 64);          // x
+  double *t2b = xl + VS;               // ascending dsymv chains
+  double *sv = t2b + VS;               // dnrm2 addends, then the xv products
+  double *scal = sv + VS;              // 16 scalars
+  unsigned long long *msk = (unsigned long long *)(scal + 16);  // dnrm2 rescale masks
+  const bool tr = trace && tid == 0;
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+#define T1_MARK(k)                                                \
+  if (tr) {                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    tacc[k] += t_ - tm;                                           \
+    tm = t_;                                                      \
+  }
+  // zero everything first: the padded dsymv chains read the pad column, the
+  // zeros around v / tau v and (past row N-1) the vectors, all finite
+  for (size_t idx = tid; idx < t1_lds_doubles(N); idx += nt) smem[idx] = 0.0;
+  __syncthreads();
+  for (int idx = tid; idx < N * N; idx += nt) {
+    const int r = idx / N, c = idx % N;
+    M[(size_t)r * lda + c] = (c <= r) ? C[(size_t)r * N + c] : C[(size_t)c * N + r];
+  }
+  __syncthreads();
+  for (int i = 0; i + 2 < N; i++) {
+    const int n = N - i - 1;
+    double *vloc = vbuf + 128 + (i & 1) * (128 + VS);
+    // ---- A: Householder vector of pivot row i (wave 0; every lane holds the scalars)
+    if (wid == 0) {
+      const double *v = M + (size_t)i * lda + i + 1;  // v[0] = alpha, v[1..n-1]
+      const double xnorm = dnrm2_wave128(v + 1, n - 1, sv);
+      double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
+      int branch = 0;
+      if (xnorm != 0) {
+        const double alpha = v[0];
+        beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fdlibm(alpha, xnorm);
+        tau_i = (beta - alpha) / beta;
+        const double sgap = alpha - beta;
+        if (fabs(sgap) > DMIN) {
+          f1 = 1.0 / sgap;
+          branch = 1;
+        } else {
+          f1 = EPS / sgap;
+          f2 = 1.0 / EPS;
+          branch = 2;
+        }
+      }
+      const double v0out = branch ? beta : v[0];
+      for (int r = lane; r < n; r += 64) {
+        double t = v[r];
+        if (r > 0 && branch != 0) {
+          t = t * f1;
+          if (branch == 2) t = t * f2;
+        }
+        gH[(size_t)i * N + r] = (r == 0) ? v0out : t;
+        const double vr = (r == 0) ? 1.0 : t;
+        vloc[r] = vr;
+        tv[r] = tau_i * vr;
+      }
+      tv[n + lane] = 0.0;  // the descending chains' leading pad
+      if (lane == 0) {
+        scal[0] = tau_i;
+        tauOut[i] = tau_i;
+        sdOut[i] = v0out;
+      }
+    }
+    T1_MARK(0)
+    __syncthreads();
+    T1_MARK(1)
+    const double tau_i = scal[0];
+    if (tau_i == 0.0) continue;  // no update this step (uniform)
+    // ---- E: dsymv chains of rows r = i+1+j, every lane's chain aligned to
+    // the end of its wave's T steps (leading steps read the zero pads)
+    if (wid < 4) {
+      const unsigned long long te0 = (trace && lane == 0) ? __builtin_amdgcn_s_memtime() : 0;
+      const int j = lane + 64 * (wid & 1);
+      const int r = i + 1 + (j < n ? j : n - 1);
+      const double *row = M + (size_t)r * lda;
+      const int lo = 64 * (wid & 1);                     // smallest j of this wave
+      const int hi = min(n, lo + 64) - 1;                // largest active j
+      if (wid < 2) {  // c = N-1 .. r+1 descending (n-1-j terms), then the diagonal
+        const int sh = j - lo;
+        const double acc = padded_chain<-1>(tv + (n - 1) + sh, row + (N - 1) + sh, n - 1 - lo);
+        if (j < n) xl[j] = acc + tv[j] * row[r];
+      } else {  // c = i+1 .. r-1 ascending (j terms)
+        const int sh = j - hi;
+        const double acc = padded_chain<1>(vloc + sh, row + i + 1 + sh, hi);
+        if (j < n) t2b[j] = acc;
+      }
+      if (trace && lane == 0 && (wid == 0 || wid == 3)) {
+        __builtin_amdgcn_s_waitcnt(0);
+        trace[wid == 0 ? 14 : 15] += __builtin_amdgcn_s_memtime() - te0;  // one writer per slot
+      }
+    }
+    __syncthreads();
+    T1_MARK(2)
+    // ---- G, I, K on wave 0 alone (two elements per lane, no block barriers):
+    // x = acc + tau t2 and the xv products, the xv chain, alpha = -(tau/2) xv,
+    // x += alpha v
+    if (wid == 0) {
+      for (int r = lane; r < n; r += 64) {
+        const double x = xl[r] + tau_i * t2b[r];
+        xl[r] = x;
+        sv[r] = x * vloc[r];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double alpha = -(tau_i / 2.0) * staged_chain(0.0, sv, n);
+      T1_MARK(3)
+      for (int r = lane; r < n; r += 64) xl[r] += alpha * vloc[r];
+    }
+    __syncthreads();
+    T1_MARK(4)
+    // ---- M: rank-2 update (both triangles), next pivot row first on wave 0
+    if (wid == 0) {
+      double *row = M + (size_t)(i + 1) * lda + i + 1;
+      const double x0 = xl[0], v0 = vloc[0];
+      for (int jj = lane; jj < n; jj += 64) {
+        const double tmp1 = -1.0 * vloc[jj], tmp2 = -1.0 * xl[jj];
+        row[jj] += tmp1 * x0 + tmp2 * v0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (n > 1) {
+      // lane's columns jj = 1 + lane, 65 + lane (n <= 128)
+      const int ja = 1 + lane, jb = 65 + lane;
+      const double xa = ja < n ? xl[ja] : 0.0, va = ja < n ? vloc[ja] : 0.0;
+      const double xb = jb < n ? xl[jb] : 0.0, vb = jb < n ? vloc[jb] : 0.0;
+      for (int jr = wid; jr < n; jr += 15) {
+        double *row = M + (size_t)(i + 1 + jr) * lda + i + 1;
+        const double nvr = -1.0 * vloc[jr], nxr = -1.0 * xl[jr];
+        if (ja < n) row[ja] += nvr * xa + nxr * va;
+        if (jb < n) row[jb] += nvr * xb + nxr * vb;
+      }
+    }
+    T1_MARK(5)
+  }
+  __syncthreads();
+#undef T1_MARK
+  if (tr)
+    for (int k = 0; k < 6; k++) trace[8 + k] += tacc[k];
+  for (int r = tid; r < N; r += nt) {
+    dOut[r] = M[(size_t)r * lda + r];
+    if (r == N - 2) sdOut[r] = M[(size_t)r * lda + r + 1];
+  }
+}
+
 // Phase B for N > 128: the columns of Q are independent under
 // householder_hm, so workgroups own UMW_COLS columns each (Q^T rows in LDS)
 // and apply all reflectors without talking to each other; the next
@@ -1017,6 +1309,7 @@ __global__ void __launch_bounds__(64) k_chase(int N, const double *__restrict__ 
 // nb_{s-1}); any other step starts a new group.  Every entry still sees the
 // same operations in the same order, so the result is GSL's bit for bit.
 constexpr int APPLY_TEAM = 16, APPLY_ROWS = 16, APPLY_TPB = APPLY_TEAM * APPLY_ROWS;
+constexpr int APF = 4;  // apply: rotations prefetched ahead of the systolic replay
 
 // x of lane l-1 (row_shr:1 within each 16-lane DPP row = one team; the
 // team's lane 0 gets 0 and never uses it)
@@ -1031,12 +1324,14 @@ constexpr int APPLY_MINSTEP = 16;  // streamed apply: smallest batch of new step
 // rotations per LDS chunk: up to 4096, what fits next to the rows (>= N - 1,
 // one whole QR step, for every N the CMA-ES path accepts)
 __host__ __device__ inline int apply_cap(int N) {
-  const long long avail = 160LL * 1024 - (long long)N * (APPLY_ROWS + 1) * 8 - 8 * APPLY_HCAP - 16 - 512;
+  const long long avail =
+      160LL * 1024 - (long long)N * (APPLY_ROWS + 1) * 8 - 8 * APPLY_HCAP - 16 - 8 * APPLY_TPB - 512;
   const long long c = avail / 16;
   return (int)(c > 4096 ? 4096 : c);
 }
 __host__ __device__ inline size_t apply_lds_bytes(int N) {
-  return (size_t)N * (APPLY_ROWS + 1) * sizeof(double) + 16 * (size_t)apply_cap(N) + 8 * APPLY_HCAP + 16;
+  return (size_t)N * (APPLY_ROWS + 1) * sizeof(double) + 16 * (size_t)apply_cap(N) + 8 * APPLY_HCAP + 16 +
+         8 * APPLY_TPB;
 }
 
 // system-scope loads of host-coherent memory the host chase writes while
@@ -1188,6 +1483,7 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   double *csh = Lq + (size_t)N * S;              // cap (c, s) pairs
   int *hsh = (int *)(csh + 2 * (size_t)cap);      // APPLY_HCAP (a, nb)
   int *chunk = hsh + 2 * APPLY_HCAP;
+  double *dummy = (double *)(chunk + 4) + threadIdx.x;  // stores of lanes with nothing to store
   if (kStream && blockIdx.x == gridDim.x - 1) {  // the extra workgroup: fetcher
     apply_fetcher(N, hr, r, hprog, prog, seq, errors, chunk);
     return;
@@ -1314,32 +1610,45 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
       const double *cs = csh + 2 * my_ro;
       const bool act = my_d >= 0 && kl < nrows;
       const int last = act ? my_nb - 1 : 0;  // i == last: emit the carry
-      // branch-free body: every lane computes, selects keep the state, the
-      // only predicated instruction is the store (issue slots, not latency,
-      // bound this loop: one wave64 VALU op = 4 cycles)
+      // branch-free body: every lane computes, selects keep the state, and
+      // lanes with nothing to store write their own dummy slot.  The (c, s)
+      // pair and the LDS entry of rotation i are loaded APF iterations ahead
+      // into a register ring, so no iteration waits on an LDS round trip.
       auto clampi = [&](int i1) { return i1 < 0 ? 0 : (i1 > last - 1 ? (last > 0 ? last - 1 : 0) : i1); };
-      int ic = clampi(-my_d);
-      double cN = cs[2 * ic], sN = cs[2 * ic + 1], qjN = col[(size_t)(my_a + ic + 1) * S];
+      double cR[APF], sR[APF], qR[APF];
+#pragma unroll
+      for (int p = 0; p < APF; p++) {
+        const int icp = clampi(p - my_d);
+        cR[p] = cs[2 * icp];
+        sR[p] = cs[2 * icp + 1];
+        qR[p] = col[(size_t)(my_a + icp + 1) * S];
+      }
       double qi = col[(size_t)my_a * S], emit = 0.0;
       T += 1;  // the carry unit of the slowest lane
-      for (int tau = 0; tau < T; tau++) {
-        const double vin = dpp_shr1(emit);
-        const int i = tau - my_d;
-        const double c = cN, sn = sN, qjl = qjN;
-        ic = clampi(i + 1);
-        cN = cs[2 * ic];
-        sN = cs[2 * ic + 1];
-        qjN = col[(size_t)(my_a + ic + 1) * S];
-        qi = (s > 0 && i == -1) ? vin : qi;
-        const double qj = (s == 0) ? qjl : vin;
-        const double out = qi * c - qj * sn;
-        const double qn = qi * sn + qj * c;
-        const bool inrot = act && i >= 0 && i < last;
-        const bool store = act && i >= 0 && i <= last;
-        const double e = inrot ? out : qi;
-        if (store) col[(size_t)(my_a + i) * S] = e;
-        emit = store ? e : emit;
-        qi = inrot ? qn : qi;
+      for (int tau0 = 0; tau0 < T; tau0 += APF) {
+#pragma unroll
+        for (int p = 0; p < APF; p++) {
+          const int tau = tau0 + p;
+          if (tau >= T) break;  // T is the same for the whole workgroup
+          const double vin = dpp_shr1(emit);
+          const int i = tau - my_d;
+          const double c = cR[p], sn = sR[p], qjl = qR[p];
+          const int icn = clampi(i + APF);
+          cR[p] = cs[2 * icn];
+          sR[p] = cs[2 * icn + 1];
+          qR[p] = col[(size_t)(my_a + icn + 1) * S];
+          qi = (s > 0 && i == -1) ? vin : qi;
+          const double qj = (s == 0) ? qjl : vin;
+          const double out = qi * c - qj * sn;
+          const double qn = qi * sn + qj * c;
+          const bool inrot = act && i >= 0 && i < last;
+          const bool store = act && i >= 0 && i <= last;
+          const double e = inrot ? out : qi;
+          double *dst = store ? col + (size_t)(my_a + (store ? i : 0)) * S : dummy;
+          *dst = e;
+          emit = store ? e : emit;
+          qi = inrot ? qn : qi;
+        }
       }
       T -= 1;
       t += K;
@@ -1493,7 +1802,21 @@ int EigenSolver::init(int N_, bool hostChase_) {
   lds = eig_use_lds(N);
   if (const char *e = getenv("KORALI_AMD_EIGEN_MW_MIN"))  // multi-workgroup phases from this N up
     if (N >= atoi(e)) lds = false;
-  if (!lds) {
+  // tridiagonalisation: one workgroup with the whole matrix in LDS while it
+  // fits (no in-launch hand-offs), multi-workgroup above;
+  // KORALI_AMD_TRIDIAG = lds | 1wg | mw forces one
+  tri = t1_fits(N) ? 1 : (lds ? 0 : 2);
+  if (const char *e = getenv("KORALI_AMD_TRIDIAG")) {
+    if (!strcmp(e, "lds") && eig_use_lds(N)) tri = 0;
+    if (!strcmp(e, "1wg") && t1_fits(N)) tri = 1;
+    if (!strcmp(e, "mw")) tri = 2;
+  } else if (getenv("KORALI_AMD_EIGEN_MW_MIN") && !lds) {
+    tri = 2;
+  }
+  if (tri == 1)
+    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(t1_lds_doubles(N) * sizeof(double))));
+  if (!lds || tri == 2) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)tmw_lds_bytes(N)));
@@ -1533,9 +1856,12 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
-  if (lds)
-    hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), matb + tridiag_vec_bytes(N), s, N, C, gA, gH, tau, d, sd,
-                       trace);
+  if (tri == 1)
+    hipLaunchKernelGGL(k_tridiag_1wg, dim3(1), dim3(T1_TPB), t1_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
+                       sd, trace);
+  else if (tri == 0)
+    hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), eig_mat_bytes(N) + tridiag_vec_bytes(N), s, N, C, gA, gH,
+                       tau, d, sd, trace);
   else {
     KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), tmw_lds_bytes(N), s, N, C, gH, tau, d, sd,

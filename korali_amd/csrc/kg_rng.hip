@@ -567,6 +567,14 @@ int MtStream::prefetch(size_t M, hipStream_t main) {
   return 0;
 }
 
+int MtStream::join(hipStream_t main) {
+  if (!side_) return 0;
+  KG_HIP(hipEventRecord(ev_side_, side_));
+  KG_HIP(hipStreamWaitEvent(main, ev_side_, 0));
+  prefetch_pending_ = false;
+  return 0;
+}
+
 int MtStream::polar_normals(double *z, size_t M, size_t block_len, unsigned long long *block_end, hipStream_t s,
                             size_t k_lo, size_t k_hi) {
   const unsigned long long words = words_for_normals(M);

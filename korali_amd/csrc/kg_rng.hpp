@@ -93,6 +93,11 @@ class MtStream {
   // eigendecomposition); polar_normals() then waits for it.
   int prefetch(size_t M_normals, hipStream_t main);
 
+  // the producer's side stream (created by the first prefetch), and a join
+  // that makes `main` wait for everything queued on it so far
+  hipStream_t side_stream() const { return side_; }
+  int join(hipStream_t main);
+
   StreamState *state() { return st_; }
   size_t words_for_normals(size_t M) const;
 

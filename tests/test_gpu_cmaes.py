@@ -195,3 +195,20 @@ def test_multi_workgroup_eigen_forced_bit_exact(monkeypatch, Nv, lam):
         for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Current Mean", "Covariance Matrix"):
             assert np.array_equal(dev[key], o[key]), (g, key)
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+
+
+@pytest.mark.parametrize("Nv,lam,kind", [(16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
+                                         (40, 128, "lds")])
+def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
+    """Each tridiagonalisation kernel (one workgroup with the matrix in LDS,
+    the multi-workgroup one, the older LDS one) forced: bit-exact B, D and
+    the generation's outputs against the oracle."""
+    monkeypatch.setenv("KORALI_AMD_TRIDIAG", kind)
+    o, dev = oracle_and_device(Nv, lam, "rosenbrock", 4)
+    for g in (1, 2, 3, 4):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Current Mean", "Covariance Matrix"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
