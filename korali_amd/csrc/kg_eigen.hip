@@ -1625,11 +1625,13 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
       }
       double qi = col[(size_t)my_a * S], emit = 0.0;
       T += 1;  // the carry unit of the slowest lane
+      // whole trips of APF units: a unit past T finds every lane past its
+      // last rotation (no store, no state change), so no trip ends early and
+      // the ring registers keep fixed roles (no copies, loads stay in flight)
       for (int tau0 = 0; tau0 < T; tau0 += APF) {
 #pragma unroll
         for (int p = 0; p < APF; p++) {
           const int tau = tau0 + p;
-          if (tau >= T) break;  // T is the same for the whole workgroup
           const double vin = dpp_shr1(emit);
           const int i = tau - my_d;
           const double c = cR[p], sn = sR[p], qjl = qR[p];
