@@ -51,7 +51,10 @@ STAGE_FLOPS = {
 
 # kernels behind each profiled stage (names as in profiles/<round>/*_pmc_traffic.csv)
 STAGE_KERNELS = {
-    "eigen_tridiag": ["kg::k_tridiag_mw"], "eigen_unpack": ["kg::k_unpack_mw"], "eigen_apply": ["kg::k_apply"],
+    # a tuple lists alternatives (the kernel the size selects); template
+    # instances match their base name
+    "eigen_tridiag": [("kg::k_tridiag_1wg", "kg::k_tridiag_mw", "kg::k_tridiag")],
+    "eigen_unpack": [("kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
     "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
     "covariance": ["kg::k_rankmu_mfma", "kg::k_adaptC_combine"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
@@ -68,12 +71,21 @@ def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
     if stage not in STAGE_KERNELS or not os.path.exists(path):
         return None, None
     rows = {r["kernel"]: r for r in csv.DictReader(open(path))}
+
+    def find(k):
+        for alt in (k if isinstance(k, tuple) else (k,)):
+            for name, r in rows.items():
+                if name == alt or name.startswith(alt + "<"):
+                    return r
+        return None
+
     tot, raw = 0.0, 0.0
     for k in STAGE_KERNELS[stage]:
-        if k not in rows:
+        r = find(k)
+        if r is None:
             return None, None
-        tot += (float(rows[k]["fetch_KB_x2"]) + float(rows[k]["write_KB"])) * 1024
-        raw += (float(rows[k]["fetch_KB_raw"]) + float(rows[k]["write_KB"])) * 1024
+        tot += (float(r["fetch_KB_x2"]) + float(r["write_KB"])) * 1024
+        raw += (float(r["fetch_KB_raw"]) + float(r["write_KB"])) * 1024
     return tot, raw
 
 

@@ -42,6 +42,16 @@ const char *last_error();
     }                             \
   } while (0)
 
+// Zero-fill device memory and wait for it.  hipMemset runs on the null
+// stream, which does not order against the non-blocking streams the handles
+// launch on: a fill still queued could land after (and clobber) the first
+// stream-ordered writes, so every fill completes before it returns.
+inline int zero_fill(void *p, size_t bytes) {
+  KG_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
+  KG_HIP(hipStreamSynchronize(nullptr));
+  return 0;
+}
+
 // Device-side error flags (bitmask in the scalar block; read back at sync
 // points and turned into KORALI_LOG_ERROR-style messages by the host).
 enum : uint32_t {

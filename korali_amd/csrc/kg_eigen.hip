@@ -1118,7 +1118,18 @@ constexpr int UMW_COLS = 4;
 constexpr int UMW_TPB = 256;
 __host__ __device__ inline int umw_groups(int N) { return (N + UMW_COLS - 1) / UMW_COLS; }
 size_t umw_lds_bytes(int N) { return (2 * (size_t)UMW_COLS * (N + 1) + 3 * (size_t)N + 16 + 32) * sizeof(double); }
+// kAllH: every reflector row staged in LDS up front (packed: row i holds its
+// N-i-1 entries), so no step waits on a global load; used while it fits
+// (KORALI_AMD_UNPACK_ALLH=0 forces the streamed rows)
+__host__ __device__ inline size_t umw_hoff(int N, int i) { return (size_t)i * (N - 1) - (size_t)i * (i - 1) / 2; }
+size_t umw_hall_doubles(int N) { return N >= 3 ? umw_hoff(N, N - 2) : 0; }
+bool umw_all_fits(int N) {
+  if (const char *e = getenv("KORALI_AMD_UNPACK_ALLH"))
+    if (!atoi(e)) return false;
+  return N >= 3 && umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double) <= 150 * 1024;
+}
 
+template <bool kAllH>
 __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__restrict__ gH,
                                                        const double *__restrict__ tau, double *gQt) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1135,16 +1146,34 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
     Q[idx] = (r < N && r == g + k * P) ? 1.0 : 0.0;
   }
   constexpr int PF = 4;  // prefetch registers per thread (N <= 1024)
-  if (N >= 3)
+  double *Hs = Pq + (size_t)UMW_COLS * lda;
+  if (kAllH) {
+    // rows 0..N-3 over the (N-2) x N rectangle of gH, eight loads in flight per thread
+    const int tot = (N - 2) * N;
+    for (int q0 = tid; q0 < tot; q0 += nt * 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * nt, i = q / N, r = q - i * N;
+        v[u] = (q < tot && r < N - i - 1) ? gH[q] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * nt, i = q / N, r = q - i * N;
+        if (q < tot && r < N - i - 1) Hs[umw_hoff(N, i) + r] = v[u];
+      }
+    }
+  } else if (N >= 3) {
     for (int r = tid; r < N - (N - 3) - 1; r += nt) hb[r] = gH[(size_t)(N - 3) * N + r];
+  }
   __syncthreads();
   int buf = 0;
   for (int i = N - 3; i >= 0; i--) {
     const int n = N - i - 1;
     const double ti = ts[i];
-    const double *h = hb + (size_t)buf * N;
+    const double *h = kAllH ? Hs + umw_hoff(N, i) : hb + (size_t)buf * N;
     double pf[PF];
-    if (i > 0) {
+    if (!kAllH && i > 0) {
 #pragma unroll
       for (int u = 0; u < PF; u++) {
         const int r = tid + u * nt;
@@ -1171,7 +1200,7 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
         for (int r = tid; r < n; r += nt) col[r] = (r == 0) ? col[0] - ti * wj : col[r] - ti * h[r] * wj;
       }
     }
-    if (i > 0) {
+    if (!kAllH && i > 0) {
 #pragma unroll
       for (int u = 0; u < PF; u++) {
         const int r = tid + u * nt;
@@ -1360,6 +1389,25 @@ __device__ inline void st_agt(double *p, double v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// LDS fill from the device staging copy: eight agent-scope loads in flight
+// per thread (each is an L2 round trip; one at a time they serialise)
+template <typename T>
+__device__ inline void fill_agt(T *dst, const T *src, int n, int tid) {
+  for (int q = tid; q < n; q += APPLY_TPB * 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int qq = q + u * APPLY_TPB;
+      v[u] = (qq < n) ? ld_agt(src + qq) : T(0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int qq = q + u * APPLY_TPB;
+      if (qq < n) dst[qq] = v[u];
+    }
+  }
+}
+
 // Streamed chase, fetcher workgroup: copies what the host chase publishes
 // (host-coherent memory, read ONCE here) into the device staging buffers,
 // then publishes a device progress word; the apply workgroups read only
@@ -1543,8 +1591,10 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
       if (t0 >= avail) break;
     }
     const int hn = min(APPLY_HCAP, avail - t0);
-    for (int idx = tid; idx < 2 * hn; idx += APPLY_TPB)
-      hsh[idx] = kStream ? ld_agt(r.hdr + 2 * (size_t)t0 + idx) : r.hdr[2 * (size_t)t0 + idx];
+    if (kStream)
+      fill_agt(hsh, r.hdr + 2 * (size_t)t0, 2 * hn, tid);
+    else
+      for (int idx = tid; idx < 2 * hn; idx += APPLY_TPB) hsh[idx] = r.hdr[2 * (size_t)t0 + idx];
     __syncthreads();
     if (tid < 64) {  // wave 0: the longest prefix of whole steps with <= cap rotations
       int base = 0, carry = 0, t1 = hn;
@@ -1570,8 +1620,10 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     }
     __syncthreads();
     const int tn = chunk[0], nrot = chunk[1];
-    for (int idx = tid; idx < 2 * nrot; idx += APPLY_TPB)
-      csh[idx] = kStream ? ld_agt(r.cs + 2 * (size_t)ro0 + idx) : r.cs[2 * (size_t)ro0 + idx];
+    if (kStream)
+      fill_agt(csh, r.cs + 2 * (size_t)ro0, 2 * nrot, tid);
+    else
+      for (int idx = tid; idx < 2 * nrot; idx += APPLY_TPB) csh[idx] = r.cs[2 * (size_t)ro0 + idx];
     __syncthreads();
     double *col = Lq + kl;  // col[c * S] = Q[k0 + kl][c]
     int t = 0, ro = 0;
@@ -1772,7 +1824,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
   KG_HIP(hipMalloc(&dev.meta, 4 * sizeof(int)));
   KG_HIP(hipMalloc(&dev.eval, (size_t)N * sizeof(double)));
   KG_HIP(hipMalloc(&dev.perm, (size_t)N * sizeof(int)));
-  KG_HIP(hipMemset(dev.meta, 0, 4 * sizeof(int)));
+  if (zero_fill(dev.meta, 4 * sizeof(int))) return 1;
   if (hostChase) {
     KG_HIP(hipHostMalloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
     KG_HIP(hipHostGetDevicePointer((void **)&d_dsd_map, h_dsd, 0));
@@ -1792,7 +1844,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.perm, host.perm, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&dprog, hprog, 0));
     KG_HIP(hipMalloc(&dprogDev, 2 * sizeof(unsigned long long)));
-    KG_HIP(hipMemset(dprogDev, 0, 2 * sizeof(unsigned long long)));
+    if (zero_fill(dprogDev, 2 * sizeof(unsigned long long))) return 1;
     KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
     hgc.resize(N);
     hgs.resize(N);
@@ -1822,8 +1874,12 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)tmw_lds_bytes(N)));
-    KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)umw_lds_bytes(N)));
+    if (umw_all_fits(N))
+      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double))));
+    else
+      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)umw_lds_bytes(N)));
   }
   const int attr = 160 * 1024;
   KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
@@ -1886,8 +1942,12 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   if (prof) prof(profCtx, "eigen_unpack", 0);
   if (lds)
     hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + 2 * N * sizeof(double), s, N, gH, tau, gQt);
+  else if (umw_all_fits(N))
+    hipLaunchKernelGGL(k_unpack_mw<true>, dim3(umw_groups(N)), dim3(UMW_TPB),
+                       umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double), s, N, gH, tau, gQt);
   else
-    hipLaunchKernelGGL(k_unpack_mw, dim3(umw_groups(N)), dim3(UMW_TPB), umw_lds_bytes(N), s, N, gH, tau, gQt);
+    hipLaunchKernelGGL(k_unpack_mw<false>, dim3(umw_groups(N)), dim3(UMW_TPB), umw_lds_bytes(N), s, N, gH, tau,
+                       gQt);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_unpack", 1);
   if (hostChase) {

@@ -435,7 +435,7 @@ int MtStream::init(size_t capacity_words, size_t parallel_min) {
   R_ = next_pow2(capacity_words + 2 * MT_N + 4096);
   KG_HIP(hipMalloc(&ring_, R_ * sizeof(uint32_t)));
   KG_HIP(hipMalloc(&st_, sizeof(StreamState)));
-  KG_HIP(hipMemset(st_, 0, sizeof(StreamState)));
+  if (zero_fill(st_, sizeof(StreamState))) return 1;
   return 0;
 }
 

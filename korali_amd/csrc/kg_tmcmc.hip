@@ -1012,7 +1012,7 @@ template <typename T>
 int tdalloc(T **p, size_t n) {
   if (n == 0) n = 1;
   KG_HIP(hipMalloc(p, n * sizeof(T)));
-  KG_HIP(hipMemset(*p, 0, n * sizeof(T)));
+  if (zero_fill(*p, n * sizeof(T))) return 1;
   return 0;
 }
 

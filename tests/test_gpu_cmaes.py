@@ -197,6 +197,21 @@ def test_multi_workgroup_eigen_forced_bit_exact(monkeypatch, Nv, lam):
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
 
 
+@pytest.mark.parametrize("Nv,lam", [(16, 64), (128, 4096)])
+def test_unpack_streamed_reflector_rows_bit_exact(monkeypatch, Nv, lam):
+    """The multi-workgroup unpack with reflector rows streamed step by step
+    (the N > ~150 form) forced where the all-rows-in-LDS form is the default."""
+    monkeypatch.setenv("KORALI_AMD_EIGEN_MW_MIN", "0")
+    monkeypatch.setenv("KORALI_AMD_UNPACK_ALLH", "0")
+    o, dev = oracle_and_device(Nv, lam, "rosenbrock", 4)
+    for g in (1, 2, 3):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Current Mean", "Covariance Matrix"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+
+
 @pytest.mark.parametrize("Nv,lam,kind", [(16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
                                          (40, 128, "lds")])
 def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):

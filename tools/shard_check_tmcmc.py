@@ -36,7 +36,9 @@ def main():
               multinomial_seed=78, multivariate_seed=79, uniform_seed=80, max_chain_length=mcl, default_burn_in=burn)
     sh = ShardedTmcmc(N, P, dist, device=0, transport="device" if backend == "nccl" else "host", **kw)
     ref = TmcmcDevice(N, P, **kw) if rank == 0 else None
+    ref2 = TmcmcDevice(N, P, **kw) if rank == 0 and os.environ.get("KORALI_AMD_SHARD_REF2") else None
     ok = True
+    prev_nc = P
     for g in range(1, gens + 1):
         sh.generation(g)
         sh.synchronize()
@@ -53,11 +55,24 @@ def main():
                 a, b = sh.dev[k], ref[k]
                 if a.tobytes() != b.tobytes():
                     print(f"gen {g}: {k} differs from the unsharded run", flush=True)
+                    if k in ("Chain Candidates", "Sample Database", "Chain Leaders"):
+                        ra, rb = np.asarray(a).reshape(P, -1), np.asarray(b).reshape(P, -1)
+                        rows = np.nonzero((ra != rb).any(axis=1))[0]
+                        print(f"   rows {rows[:12].tolist()} ({len(rows)}) of {P}; chain count before {prev_nc}", flush=True)
                     ok = False
+            if ref2 is not None:
+                ref2.generation(g)
+                ref2.synchronize()
+                for k in KEYS:
+                    if ref2[k].tobytes() != ref[k].tobytes():
+                        print(f"gen {g}: {k}: unsharded runs disagree", flush=True)
+                    if ref2[k].tobytes() != sh.dev[k].tobytes():
+                        print(f"gen {g}: {k}: sharded differs from the second unsharded run", flush=True)
             for which in range(4):
                 if sh.dev.get_rng(which) != ref.get_rng(which):
                     print(f"gen {g}: generator {which} state differs", flush=True)
                     ok = False
+        prev_nc = int(sh.dev["Chain Count"][0])
         if sh.dev["Previous Annealing Exponent"][0] >= 1.0:
             break
     flag = [ok]
@@ -65,8 +80,9 @@ def main():
     if rank == 0:
         print("SHARD_CHECK", "PASS" if flag[0] else "FAIL", flush=True)
     sh.close()
-    if ref is not None:
-        ref.close()
+    for r in (ref, ref2):
+        if r is not None:
+            r.close()
     dist.destroy_process_group()
     sys.exit(0 if flag[0] else 1)
 
