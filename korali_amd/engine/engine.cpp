@@ -14,14 +14,20 @@
 // the device through kg_cmaes_* / kg_tmcmc_*; user functions are called
 // from this thread in sample order (Sequential conduit semantics).
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <fstream>
+#include <functional>
+#include <mutex>
 #include <sstream>
+#include <thread>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -122,6 +128,117 @@ struct Seeder {
   }
 };
 
+// ------------------------------------------------------------- conduits
+// Host-callback dispatch (the Engine's "Conduit").  Sequential
+// (conduit/sequential/sequential.cpp.base:80-92): the engine thread calls
+// the user function for every sample in Sample Id order.  Concurrent
+// (conduit/concurrent/concurrent.cpp.base:18-231 forks "Concurrent Jobs"
+// worker processes and ships each sample's JSON through pipes): here that
+// many threads of this process share the batch of one generation (CMA-ES)
+// or of one chain round (TMCMC), the engine thread being one of them.
+// Results land by Sample Id, so completion order never reaches the solver
+// and a run is bit-identical to the Sequential one; of several failing
+// samples the lowest Sample Id's error is raised, as in a Sequential run.
+// User functions must be safe to call from several threads (Python
+// callbacks take the GIL, which the engine releases while it runs).
+class Conduit {
+ public:
+  explicit Conduit(size_t jobs) : jobs_(jobs < 1 ? 1 : jobs) {
+    for (size_t t = 1; t < jobs_; t++) pool_.emplace_back([this] { serve(); });
+  }
+  ~Conduit() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    wake_.notify_all();
+    for (auto &t : pool_) t.join();
+  }
+  Conduit(const Conduit &) = delete;
+  Conduit &operator=(const Conduit &) = delete;
+
+  void evaluateBatch(size_t n, const std::function<void(size_t)> &body) {
+    if (pool_.empty() || n <= 1) {
+      for (size_t i = 0; i < n; i++) body(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      body_ = &body;
+      n_ = n;
+      next_.store(0);
+      busy_ = pool_.size();
+      err_ = nullptr;
+      errAt_ = n;
+      batch_++;
+    }
+    wake_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return busy_ == 0; });
+    body_ = nullptr;
+    if (err_) std::rethrow_exception(err_);
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      try {
+        (*body_)(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(m_);
+        if (i < errAt_) {
+          errAt_ = i;
+          err_ = std::current_exception();
+        }
+        next_.store(n_);  // hand out nothing more; lower ids are already running
+      }
+    }
+  }
+  void serve() {
+    size_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        wake_.wait(g, [&] { return stop_ || batch_ != seen; });
+        if (stop_) return;
+        seen = batch_;
+      }
+      work();
+      std::lock_guard<std::mutex> g(m_);
+      if (--busy_ == 0) done_.notify_all();
+    }
+  }
+  size_t jobs_;
+  std::vector<std::thread> pool_;
+  std::mutex m_;
+  std::condition_variable wake_, done_;
+  const std::function<void(size_t)> *body_ = nullptr;
+  size_t n_ = 0, busy_ = 0, errAt_ = 0, batch_ = 0;
+  std::atomic<size_t> next_{0};
+  std::exception_ptr err_;
+  bool stop_ = false;
+};
+
+// Engine::initialize (engine.cpp:39) + Conduit module defaults
+std::unique_ptr<Conduit> makeConduit(Json &js) {
+  Json &c = js["Conduit"];
+  const std::string t = canon(str(c, "Type", "Sequential"));
+  if (t == "sequential") return std::unique_ptr<Conduit>(new Conduit(1));
+  if (t == "concurrent") {
+    const double jobs = num(c, "Concurrent Jobs", 1);  // concurrent.config default
+    if (!(jobs >= 1) || jobs != std::floor(jobs))  // concurrent.cpp.base:23
+      fail("You need to define at least 1 concurrent job(s) for external models \n");
+    return std::unique_ptr<Conduit>(new Conduit((size_t)jobs));
+  }
+  if (t == "distributed")
+    fail("The Distributed conduit (MPI worker teams) is not part of the device path: shard the population or the "
+         "TMCMC chains across GPUs with korali_amd.sharded over torch.distributed instead.");
+  fail("Unrecognized conduit type '%s' (Sequential or Concurrent).", c["Type"].getString().c_str());
+}
+
 struct VariableSpec {
   std::string name;
   double lb, ub, iv, istd, minstd;
@@ -132,6 +249,7 @@ struct VariableSpec {
 
 // ------------------------------------------------------------ modules
 struct SolverModule {
+  Conduit *conduit = nullptr;  // the engine's sample dispatch (host callbacks)
   virtual ~SolverModule() = default;
   virtual void runGeneration(size_t gen) = 0;
   // criteria evaluated before generation `gen` (experiment.cpp.base:56)
@@ -329,7 +447,7 @@ struct CmaesModule : SolverModule {
       std::vector<double> X(lam * N), F(lam);
       check(kg_cmaes_get_candidates(h, X.data(), N));
       Function &f = getFunction(fn);
-      for (size_t i = 0; i < lam; i++) {
+      conduit->evaluateBatch(lam, [&](size_t i) {
         Sample s;
         s["Module"] = "Problem";
         s["Operation"] = "Evaluate";
@@ -340,7 +458,7 @@ struct CmaesModule : SolverModule {
         if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
         F[i] = s["F(x)"].getDouble();
         if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
-      }
+      });
       check(kg_cmaes_set_fitness(h, F.data()));
     }
     check(kg_cmaes_update(h, gen));
@@ -578,9 +696,13 @@ struct TmcmcModule : SolverModule {
         check(kg_tmcmc_get_pending(h, pend.data()));
         check(kg_tmcmc_get_candidates(h, X.data(), N));
         check(kg_tmcmc_get_field(h, "Chain Candidates LogPriors", LP.data(), P));
+        std::vector<size_t> todo;
         for (size_t i = 0; i < P; i++) {
           LL[i] = -INFINITY;
-          if (!pend[i] || (std::isinf(LP[i]) && LP[i] < 0)) continue;
+          if (pend[i] && !(std::isinf(LP[i]) && LP[i] < 0)) todo.push_back(i);
+        }
+        conduit->evaluateBatch(todo.size(), [&](size_t k) {
+          const size_t i = todo[k];
           Sample s;
           s["Module"] = "Problem";
           s["Operation"] = "Evaluate";
@@ -591,7 +713,7 @@ struct TmcmcModule : SolverModule {
           if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
           LL[i] = s["logLikelihood"].getDouble();
           if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);
-        }
+        });
         check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
         check(kg_tmcmc_advance(h, gen, &pending));
       }
@@ -722,7 +844,7 @@ void saveState(Json &js, size_t gen) {
   }
 }
 
-void runExperiment(Experiment &e) {
+void runExperiment(Experiment &e, Conduit &conduit) {
   Json &js = e._js;
   ExperimentState &st = *e._state;
   // experiment.config Module Defaults
@@ -778,6 +900,7 @@ void runExperiment(Experiment &e) {
   }
   js["Random Seed"] = seeds.counter;
   SolverModule &solver = *st.solver;
+  solver.conduit = &conduit;
   const bool fileOut = fo["Enabled"].getBool();
   const size_t fileFreq = (size_t)fo["Frequency"].getUInt();
   auto save = [&]() {
@@ -826,10 +949,25 @@ void runExperiment(Experiment &e) {
 
 }  // namespace
 
-void Engine::run(Experiment &e) { runExperiment(e); }
+// Engine::run (engine.cpp:69-128): the conduit lives for the whole run
+void Engine::run(Experiment &e) {
+  std::unique_ptr<Conduit> c = makeConduit(_js);
+  runExperiment(e, *c);
+}
 
 void Engine::run(std::vector<Experiment> &es) {
-  for (auto &e : es) runExperiment(e);
+  std::unique_ptr<Conduit> c = makeConduit(_js);
+  for (auto &e : es) runExperiment(e, *c);
+}
+
+void Engine::run(const std::vector<Experiment *> &es) {
+  std::unique_ptr<Conduit> c = makeConduit(_js);
+  for (auto *e : es) runExperiment(*e, *c);
+}
+
+void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &body) {
+  Conduit c(jobs);
+  c.evaluateBatch(n, body);
 }
 
 }  // namespace korali

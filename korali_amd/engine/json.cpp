@@ -4,15 +4,17 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <mutex>
 
 namespace korali {
 
 namespace {
 // never destroyed: entries may hold Python callables, which must not be
-// released after the interpreter has finalised
-std::vector<Function> &functionTable() {
-  static auto *t = new std::vector<Function>();
+// released after the interpreter has finalised.  A deque: references handed
+// out by getFunction stay valid while other threads register functions.
+std::deque<Function> &functionTable() {
+  static auto *t = new std::deque<Function>();
   return *t;
 }
 std::mutex &functionMutex() {

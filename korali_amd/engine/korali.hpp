@@ -59,11 +59,21 @@ class Experiment {
   std::unique_ptr<ExperimentState> _state;
 };
 
+// Engine (source/engine.hpp): its own JSON holds the conduit,
+//   k["Conduit"]["Type"] = "Sequential" (default) | "Concurrent";
+//   k["Conduit"]["Concurrent Jobs"] = n   (Concurrent: n evaluation threads)
 class Engine {
  public:
+  Json &operator[](const std::string &key) { return _js[key]; }
   void run(Experiment &e);
   void run(std::vector<Experiment> &es);
+  void run(const std::vector<Experiment *> &es);
+  Json _js;
 };
+
+// The conduit's batch dispatch on its own (tests): body(i) for i < n on
+// `jobs` threads, the lowest failing index's exception rethrown.
+void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &body);
 
 // thrown for every configuration or runtime error (KORALI_LOG_ERROR)
 class KoraliError : public std::runtime_error {

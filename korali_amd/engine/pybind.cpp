@@ -170,10 +170,36 @@ PYBIND11_MODULE(libkorali, m) {
       .def("loadState", &korali::Experiment::loadState)
       .def("dump", [](korali::Experiment &e) { return e._js.dump(2); });
 
+  // run() releases the GIL: Python callbacks re-acquire it per sample, so a
+  // Concurrent conduit's threads can evaluate samples whose code drops it
+  // (NumPy, I/O, native extensions)
   py::class_<korali::Engine>(m, "Engine")
       .def(py::init<>())
-      .def("run", [](korali::Engine &k, korali::Experiment &e) { k.run(e); })
-      .def("run", [](korali::Engine &k, py::list es) {
-        for (auto x : es) k.run(x.cast<korali::Experiment &>());
-      });
+      .def("run",
+           [](korali::Engine &k, korali::Experiment &e) {
+             py::gil_scoped_release nogil;
+             k.run(e);
+           })
+      .def("run",
+           [](korali::Engine &k, py::list es) {
+             std::vector<korali::Experiment *> v;
+             for (auto x : es) v.push_back(&x.cast<korali::Experiment &>());
+             py::gil_scoped_release nogil;
+             k.run(v);
+           })
+      .def("__getitem__",
+           [](py::object self, py::handle k) {
+             auto &e = self.cast<korali::Engine &>();
+             return child(JsonRef{&e._js, {}, self}, key(k));
+           })
+      .def("__setitem__", [](korali::Engine &e, const std::string &k, py::handle v) { e[k] = toJson(v); });
+
+  // test hook: the conduit's batch dispatch with a Python body
+  m.def("_conduit_evaluate", [](size_t jobs, size_t n, py::function body) {
+    py::gil_scoped_release nogil;
+    korali::conduitEvaluate(jobs, n, [&body](size_t i) {
+      py::gil_scoped_acquire g;
+      body(i);
+    });
+  });
 }

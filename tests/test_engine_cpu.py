@@ -106,3 +106,60 @@ def test_native_modules_are_in_tree():
     pkg = os.path.dirname(korali_amd.__file__)
     assert os.path.exists(os.path.join(pkg, "libkorali_engine.so"))
     assert os.path.dirname(korali.Engine.__module__ and __import__("korali_amd.libkorali").libkorali.__file__) == pkg
+
+
+def test_engine_conduit_json_surface():
+    k = korali.Engine()
+    k["Conduit"]["Type"] = "Concurrent"
+    k["Conduit"]["Concurrent Jobs"] = 4
+    assert k["Conduit"]["Type"] == "Concurrent"
+    assert k["Conduit"]["Concurrent Jobs"] == 4
+
+
+@pytest.mark.parametrize("conduit,msg", [
+    ({"Type": "Distributed"}, "Distributed conduit"),
+    ({"Type": "Concurrent", "Concurrent Jobs": 0}, "at least 1 concurrent job"),
+    ({"Type": "Pipes"}, "Unrecognized conduit type"),
+])
+def test_conduit_configuration_errors(conduit, msg):
+    k = korali.Engine()
+    for key, v in conduit.items():
+        k["Conduit"][key] = v
+    with pytest.raises(korali.KoraliError, match=msg):
+        k.run(base_cmaes())
+
+
+@pytest.mark.parametrize("jobs", [1, 3, 8])
+def test_conduit_batch_runs_every_sample_once(jobs):
+    """The Concurrent conduit's dispatch (the engine's thread pool): every
+    Sample Id exactly once, results by id, whatever the completion order."""
+    from korali_amd import libkorali
+    out = [None] * 257
+    calls = []
+
+    def body(i):
+        calls.append(i)
+        out[i] = i * i
+
+    libkorali._conduit_evaluate(jobs, len(out), body)
+    assert sorted(calls) == list(range(len(out)))
+    assert out == [i * i for i in range(len(out))]
+
+
+def test_conduit_batch_raises_lowest_failing_sample():
+    """Of several failing samples the lowest Sample Id's error is raised, as a
+    Sequential run would raise it."""
+    from korali_amd import libkorali
+    import threading
+    gate = threading.Event()
+
+    def body(i):
+        if i == 40:
+            gate.wait(2.0)  # a later failure is recorded first
+            raise ValueError("sample 40")
+        if i == 41:
+            gate.set()
+            raise ValueError("sample 41")
+
+    with pytest.raises(ValueError, match="sample 40"):
+        libkorali._conduit_evaluate(4, 100, body)

@@ -344,3 +344,84 @@ def test_tmcmc_chain_steps_kernel_equals_callback(solver):
         runs.append((e["Solver"]["LogEvidence"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sample Database"],
                      e["Solver"]["Model Evaluation Count"], e["Solver"]["Chain Lengths"]))
     assert runs[0] == runs[1]
+
+
+def run_with_conduit(e, conduit):
+    import korali
+    k = korali.Engine()
+    for key, v in conduit.items():
+        k["Conduit"][key] = v
+    k.run(e)
+    return e
+
+
+@pytest.mark.parametrize("jobs", [2, 8])
+def test_concurrent_conduit_equals_sequential_cmaes(jobs):
+    """f3: host-callback objectives through the Concurrent conduit (a thread
+    pool sharing each generation's batch) give the Sequential run bit for bit."""
+    import korali
+
+    def model(s):
+        x = np.asarray(s["Parameters"])
+        s["F(x)"] = -float(np.sum(100.0 * (x[1:] - x[:-1] ** 2) ** 2 + (1.0 - x[:-1]) ** 2))
+
+    runs = []
+    for conduit in ({"Type": "Sequential"}, {"Type": "Concurrent", "Concurrent Jobs": jobs}):
+        e = korali.Experiment()
+        e["Problem"]["Type"] = "Optimization"
+        e["Problem"]["Objective Function"] = model
+        for i in range(8):
+            e["Variables"][i]["Name"] = "X" + str(i)
+            e["Variables"][i]["Initial Value"] = 0.0
+            e["Variables"][i]["Initial Standard Deviation"] = 1.0
+        e["Solver"]["Type"] = "Optimizer/CMAES"
+        e["Solver"]["Population Size"] = 64
+        e["Solver"]["Termination Criteria"]["Max Generations"] = 30
+        e["Random Seed"] = 1337
+        e["Console Output"]["Verbosity"] = "Silent"
+        e["File Output"]["Enabled"] = False
+        run_with_conduit(e, conduit)
+        runs.append((e["Solver"]["Best Ever Value"], e["Solver"]["Covariance Matrix"], e["Solver"]["Sigma"],
+                     e["Solver"]["Current Mean"]))
+    assert runs[0] == runs[1]
+
+
+def test_concurrent_conduit_equals_sequential_tmcmc_chain_rounds():
+    """TMCMC chain rounds (Burn In, Max Chain Length) through the Concurrent
+    conduit: the Sequential conduit's chain-major result, bit for bit (the
+    reference's Concurrent run is completion-order dependent here)."""
+
+    def model(s):
+        v = s["Parameters"][0]
+        s["logLikelihood"] = -0.5 * v * v
+
+    runs = []
+    for conduit in ({"Type": "Sequential"}, {"Type": "Concurrent", "Concurrent Jobs": 6}):
+        e = tmcmc_1d(model, **{"Population Size": 600, "Burn In": 2, "Max Chain Length": 3})
+        run_with_conduit(e, conduit)
+        runs.append((e["Solver"]["LogEvidence"], e["Solver"]["Sample Database"], e["Solver"]["Chain Lengths"],
+                     e["Solver"]["Model Evaluation Count"]))
+    assert runs[0] == runs[1]
+
+
+def test_concurrent_conduit_raises_the_callback_error():
+    import korali
+
+    def model(s):
+        if s["Sample Id"] == 17:
+            raise ValueError("model failed on sample 17")
+        s["F(x)"] = -float(np.sum(np.asarray(s["Parameters"]) ** 2))
+
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Function"] = model
+    e["Variables"][0]["Name"] = "X"
+    e["Variables"][0]["Initial Value"] = 0.0
+    e["Variables"][0]["Initial Standard Deviation"] = 1.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = 32
+    e["Solver"]["Termination Criteria"]["Max Generations"] = 3
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["File Output"]["Enabled"] = False
+    with pytest.raises(ValueError, match="sample 17"):
+        run_with_conduit(e, {"Type": "Concurrent", "Concurrent Jobs": 4})
