@@ -57,7 +57,7 @@ def build(force=False, verbose=False):
 
 
 def build_engine(force=False, verbose=False):
-    srcs = [os.path.join(ENGINE, f) for f in ("json.cpp", "engine.cpp")]
+    srcs = [os.path.join(ENGINE, f) for f in ("json.cpp", "engine.cpp", "likelihood.cpp")]
     hdrs = [os.path.join(ENGINE, f) for f in ("json.hpp", "korali.hpp")] + [os.path.join(ROOT, "include", "korali_amd.h")]
     link = ["-L" + PKG, "-lkorali_amd", "-Wl,-rpath,$ORIGIN"]
     if force or _stale(ENGINE_LIB, srcs + hdrs + [LIB]):

@@ -553,8 +553,10 @@ const char *TMCMC_SCALARS[] = {"Annealing Exponent", "Previous Annealing Exponen
 struct TmcmcModule : SolverModule {
   kg_tmcmc_t h = nullptr;
   size_t N = 0, P = 0, ndist = 0;
-  bool builtin = false;
+  bool builtin = false, reference = false;
   size_t fn = 0;
+  std::vector<double> referenceData;  // Bayesian/Reference
+  std::string likelihoodModel;
   double maxGenerations, maxModelEvaluations, targetExponent;
 
   ~TmcmcModule() override {
@@ -566,8 +568,10 @@ struct TmcmcModule : SolverModule {
     Json &sv = js["Solver"];
     Json &pb = js["Problem"];
     const std::string pt = canon(str(pb, "Type", ""));
-    if (pt != "bayesian/custom")
-      fail("The device TMCMC path supports problems of type 'Bayesian/Custom' (is '%s').", pb["Type"].getString().c_str());
+    if (pt != "bayesian/custom" && pt != "bayesian/reference")
+      fail("The device TMCMC path supports problems of type 'Bayesian/Custom' and 'Bayesian/Reference' (is '%s').",
+           pb["Type"].getString().c_str());
+    reference = pt == "bayesian/reference";
     if (canon(str(sv, "Version", "TMCMC")) != "tmcmc") fail("Only Version 'TMCMC' is supported by the device path.");
     std::vector<VariableSpec> vars = readVariables(js);
     N = vars.size();
@@ -605,7 +609,19 @@ struct TmcmcModule : SolverModule {
       pmax[i] = ds[k]["Maximum"].getDouble();
       pdist[i] = k;
     }
-    if (pb.contains("Likelihood Kernel")) {
+    if (reference) {
+      // Reference::initialize (reference.cpp.base:17-23) + the model checks
+      // of evaluateLoglikelihood (:25-44)
+      if (!pb.contains("Computational Model") || !pb["Computational Model"].is_integer())
+        fail("Problem 'Bayesian/Reference' requires a 'Computational Model' function.");
+      fn = pb["Computational Model"].getUInt();
+      if (pb.contains("Reference Data") && pb["Reference Data"].is_array()) referenceData = flatten(pb["Reference Data"]);
+      likelihoodModel = str(pb, "Likelihood Model", "");
+      if (referenceData.empty())
+        fail("Bayesian (%s) problems require defining reference data.\n", likelihoodModel.c_str());
+      if (!isReferenceLikelihoodModel(likelihoodModel))
+        fail("Bayesian problem (%s) not recognized.\n", likelihoodModel.c_str());
+    } else if (pb.contains("Likelihood Kernel")) {
       if (canon(pb["Likelihood Kernel"].getString()) != "gaussian")
         fail("Unknown 'Likelihood Kernel' '%s'.", pb["Likelihood Kernel"].getString().c_str());
       builtin = true;
@@ -710,6 +726,11 @@ struct TmcmcModule : SolverModule {
           s["Current Generation"] = (unsigned long long)gen;
           s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
           f(s);
+          if (reference) {
+            // Reference::evaluateLoglikelihood: sample.run(_computationalModel), then the model
+            s["logLikelihood"] = referenceLoglikelihood(likelihoodModel, referenceData, s);
+            if (std::isnan(s["logLikelihood"].getDouble())) fail("Sample %zu returned NaN logLikelihood evaluation.\n", i);
+          }
           if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
           LL[i] = s["logLikelihood"].getDouble();
           if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);

@@ -75,6 +75,13 @@ class Engine {
 // `jobs` threads, the lowest failing index's exception rethrown.
 void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &body);
 
+// Bayesian/Reference likelihood models (likelihood.cpp,
+// reference.cpp.base:25-229): the log-likelihood of reference data y given the
+// entries a computational model wrote into s; throws KoraliError like
+// KORALI_LOG_ERROR on malformed entries.
+double referenceLoglikelihood(const std::string &model, const std::vector<double> &y, Sample &s);
+bool isReferenceLikelihoodModel(const std::string &model);
+
 // thrown for every configuration or runtime error (KORALI_LOG_ERROR)
 class KoraliError : public std::runtime_error {
  public:

@@ -17,6 +17,7 @@ using korali::Json;
 namespace {
 
 Json toJson(const py::handle &o);
+bool jsonRefValue(const py::handle &o, Json &out);  // o is a koraliJson proxy: its value
 
 py::object toPy(const Json &j) {
   switch (j.type()) {
@@ -42,6 +43,10 @@ py::object toPy(const Json &j) {
 
 Json toJson(const py::handle &o) {
   if (o.is_none()) return Json();
+  {
+    Json v;
+    if (jsonRefValue(o, v)) return v;
+  }
   if (py::isinstance<py::bool_>(o)) return Json(o.cast<bool>());
   if (py::isinstance<py::int_>(o)) {
     const py::int_ i = py::reinterpret_borrow<py::int_>(o);
@@ -130,6 +135,13 @@ Key key(const py::handle &k) {
   return k.cast<std::string>();
 }
 
+bool jsonRefValue(const py::handle &o, Json &out) {
+  if (!py::isinstance<JsonRef>(o)) return false;
+  const Json *j = o.cast<const JsonRef &>().find();
+  out = j ? *j : Json();
+  return true;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(libkorali, m) {
@@ -143,6 +155,16 @@ PYBIND11_MODULE(libkorali, m) {
              JsonRef c{r.root, r.path, r.keep};
              c.path.push_back(key(k));
              c.make() = toJson(v);
+           })
+      // s["Reference Evaluations"] = []; s["Reference Evaluations"] += [v]
+      // (the reference's model scripts): extend the array in place
+      .def("__iadd__",
+           [](py::object self, py::iterable items) {
+             Json &j = self.cast<const JsonRef &>().make();
+             if (j.is_null()) j = Json::array();
+             if (!j.is_array()) throw py::type_error("+= on a non-array Korali JSON entry");
+             for (auto x : items) j.push_back(toJson(x));
+             return self;
            })
       .def("__len__", [](const JsonRef &r) { Json *j = r.find(); return j ? j->size() : (size_t)0; })
       .def("__contains__", [](const JsonRef &r, const std::string &k) { Json *j = r.find(); return j && j->contains(k); })
@@ -193,6 +215,13 @@ PYBIND11_MODULE(libkorali, m) {
              return child(JsonRef{&e._js, {}, self}, key(k));
            })
       .def("__setitem__", [](korali::Engine &e, const std::string &k, py::handle v) { e[k] = toJson(v); });
+
+  // test hook: a Bayesian/Reference likelihood model on one sample's entries
+  m.def("_reference_loglikelihood", [](const std::string &model, const std::vector<double> &y, py::dict entries) {
+    korali::Sample s;
+    for (auto kv : entries) s[py::str(kv.first).cast<std::string>()] = toJson(kv.second);
+    return korali::referenceLoglikelihood(model, y, s);
+  });
 
   // test hook: the conduit's batch dispatch with a Python body
   m.def("_conduit_evaluate", [](size_t jobs, size_t n, py::function body) {

@@ -425,3 +425,71 @@ def test_concurrent_conduit_raises_the_callback_error():
     e["File Output"]["Enabled"] = False
     with pytest.raises(ValueError, match="sample 17"):
         run_with_conduit(e, {"Type": "Concurrent", "Concurrent Jobs": 4})
+
+
+# tests/statistical/bayesian/_model/model.py: linear model a*x + b with noise sigma
+REF_X = [1.0, 2.0, 3.0, 4.0, 5.0]
+REF_Y = [3.21, 4.14, 4.94, 6.06, 6.84]
+
+
+def linear_reference_model(s):  # model.py:8-21, the reference's own list-append idiom
+    a = s["Parameters"][0]
+    b = s["Parameters"][1]
+    sig = s["Parameters"][2]
+    s["Reference Evaluations"] = []
+    s["Standard Deviation"] = []
+    for x in REF_X:
+        s["Reference Evaluations"] += [a * x + b]
+        s["Standard Deviation"] += [sig]
+
+
+def test_bayesian_reference_reproduces_reference_tmcmc_result_files(tmp_path):
+    """The experiment behind tests/python/plot/tmcmc (Bayesian/Reference,
+    Normal likelihood, 3 Uniform(0,5) priors, P=50, Target CoV 0.8, seed of
+    gen00000000.json) run through korali.Engine: every committed generation's
+    candidates, likelihoods, accept counts, annealing exponent, evidence,
+    chain leaders, mean, covariance and generator states, bit for bit."""
+    import korali
+    from golden_util import load_tmcmc
+    TM = load_tmcmc()
+    g0 = TM[0]
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Reference"
+    e["Problem"]["Likelihood Model"] = "Normal"
+    e["Problem"]["Reference Data"] = REF_Y
+    e["Problem"]["Computational Model"] = linear_reference_model
+    for i, d in enumerate(g0["Distributions"]):
+        e["Distributions"][i]["Name"] = d["Name"]
+        e["Distributions"][i]["Type"] = "Univariate/Uniform"
+        e["Distributions"][i]["Minimum"] = d["Minimum"]
+        e["Distributions"][i]["Maximum"] = d["Maximum"]
+    for i, v in enumerate(g0["Variables"]):
+        e["Variables"][i]["Name"] = v["Name"]
+        e["Variables"][i]["Prior Distribution"] = v["Prior Distribution"]
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    e["Solver"]["Population Size"] = 50
+    e["Solver"]["Target Coefficient Of Variation"] = 0.8
+    e["Random Seed"] = g0["Distributions"][0]["Random Seed"]
+    e["Store Sample Information"] = True
+    e["Console Output"]["Verbosity"] = "Silent"
+    out = tmp_path / "tm"
+    e["File Output"]["Path"] = str(out)
+    korali.Engine().run(e)
+    assert e["Current Generation"] == TM[-1]["Current Generation"]
+    for ref in TM[1:]:
+        g = ref["Current Generation"]
+        mine, s = read_gen(out, g)["Solver"], ref["Solver"]
+        # log-priors are not compared: the committed files were written by a
+        # reference version whose Uniform log-density was 0 inside the support
+        # (every LogPriors entry is 0.0); the current uniform.cpp.base gives
+        # -log(max - min).  A constant prior cancels in every acceptance ratio
+        # (TMCMC.cpp.base:632), so nothing else depends on it.
+        for k in ("Chain Candidates", "Chain Candidates LogLikelihoods", "Chain Leaders",
+                  "Chain Leaders LogLikelihoods", "Chain Lengths", "Mean Theta", "Covariance Matrix",
+                  "Sample Database", "Sample LogLikelihood Database"):
+            assert np.array_equal(np.array(mine[k], dtype=float), np.array(s[k], dtype=float)), (g, k)
+        for k in ("Annealing Exponent", "LogEvidence", "Coefficient Of Variation", "Max Loglikelihood",
+                  "Accepted Samples Count", "Chain Count", "Proposals Acceptance Rate", "Selection Acceptance Rate"):
+            assert mine[k] == s[k], (g, k)
+        for k in ("Multinomial Generator", "Multivariate Generator", "Uniform Generator"):
+            assert mine[k]["Range"] == s[k]["Range"], (g, k)
