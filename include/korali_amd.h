@@ -96,6 +96,10 @@ int kg_cmaes_sample(kg_cmaes_t h);
 int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective);
 int kg_cmaes_get_candidates(kg_cmaes_t h, double *X, size_t ld);
 int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F);
+/* Bayesian problems (F(x) = logPosterior, bayesian.cpp.base:79-84): like
+ * kg_cmaes_set_fitness, but -inf (a candidate outside the prior's support)
+ * is a valid value; NaN and +inf are still rejected.  Ties sort by index. */
+int kg_cmaes_set_log_posterior(kg_cmaes_t h, const double *F);
 int kg_cmaes_update(kg_cmaes_t h, size_t generation);
 /* one whole generation, enqueued asynchronously (no host sync) */
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective);

@@ -1398,14 +1398,19 @@ int kg_cmaes_get_candidates(kg_cmaes_t h, double *X, size_t ld) {
   return 0;
 }
 
-int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F) {
+static int cmaes_upload_fitness(kg_cmaes_t h, const double *F, bool allow_neg_inf) {
   for (int i = 0; i < h->lam; i++)
-    KG_CHECK(std::isfinite(F[i]), "Non finite value of function evaluation detected: " + std::to_string(F[i]));
+    KG_CHECK(std::isfinite(F[i]) || (allow_neg_inf && F[i] == -INFINITY),
+             "Non finite value of function evaluation detected: " + std::to_string(F[i]));
   KG_HIP(hipMemcpyAsync(h->F, F, h->lam * sizeof(double), hipMemcpyHostToDevice, h->stream));
   hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
+
+int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F) { return cmaes_upload_fitness(h, F, false); }
+
+int kg_cmaes_set_log_posterior(kg_cmaes_t h, const double *F) { return cmaes_upload_fitness(h, F, true); }
 
 static int cmaes_sort(kg_cmaes_t h) {
   const int L = h->lam;

@@ -247,6 +247,97 @@ struct VariableSpec {
 
 }  // namespace
 
+// Bayesian::evaluate on the host (bayesian.cpp.base:24-84) for solvers that
+// see a Bayesian problem through F(x) = logPosterior (CMA-ES MAP estimation):
+// the log-prior of each variable's Univariate/Uniform or Univariate/Normal
+// prior (uniform.cpp.base / normal.cpp.base getLogDensity), then the
+// likelihood only where the prior is finite: a Custom 'Likelihood Model', or a
+// Reference 'Computational Model' + likelihood model (likelihood.cpp).
+struct BayesianEvaluator {
+  struct Prior {
+    bool normal;
+    double a, b, aux;  // uniform: min, max, -log(max - min); normal: mean, sd, log-normalisation
+  };
+  std::vector<Prior> priors;
+  bool reference = false;
+  size_t fn = 0;
+  std::vector<double> referenceData;
+  std::string likelihoodModel;
+
+  BayesianEvaluator(Json &js, const std::string &type) {
+    Json &pb = js["Problem"];
+    reference = type == "bayesian/reference";
+    if (reference) {
+      if (!pb.contains("Computational Model") || !pb["Computational Model"].is_integer())
+        fail("Problem 'Bayesian/Reference' requires a 'Computational Model' function.");
+      fn = pb["Computational Model"].getUInt();
+      if (pb.contains("Reference Data") && pb["Reference Data"].is_array())
+        for (const Json &x : pb["Reference Data"].elements()) referenceData.push_back(x.getDouble());
+      likelihoodModel = str(pb, "Likelihood Model", "");
+      if (referenceData.empty()) fail("Bayesian (%s) problems require defining reference data.\n", likelihoodModel.c_str());
+      if (!isReferenceLikelihoodModel(likelihoodModel)) fail("Bayesian problem (%s) not recognized.\n", likelihoodModel.c_str());
+    } else {
+      if (!pb.contains("Likelihood Model") || !pb["Likelihood Model"].is_integer())
+        fail("Problem 'Bayesian/Custom' requires a 'Likelihood Model' function.");
+      fn = pb["Likelihood Model"].getUInt();
+    }
+    Json &ds = js["Distributions"];
+    for (size_t i = 0; i < js["Variables"].size(); i++) {  // Bayesian::initialize :6-22
+      Json &v = js["Variables"][i];
+      const std::string pn = v.contains("Prior Distribution") ? v["Prior Distribution"].getString() : "";
+      int k = -1;
+      for (size_t d = 0; d < ds.size(); d++)
+        if (ds[d].contains("Name") && ds[d]["Name"].getString() == pn) k = (int)d;
+      if (k < 0) fail("Did not find distribution %s, specified by variable %s\n", pn.c_str(), str(v, "Name", "").c_str());
+      const std::string t = canon(ds[k]["Type"].getString());
+      Prior p{};
+      if (t == "univariate/uniform") {
+        p.a = num(ds[k], "Minimum", NAN);
+        p.b = num(ds[k], "Maximum", NAN);
+        p.aux = p.b - p.a <= 0.0 ? NAN : -std::log(p.b - p.a);
+      } else if (t == "univariate/normal") {
+        p.normal = true;
+        p.a = num(ds[k], "Mean", NAN);
+        p.b = num(ds[k], "Standard Deviation", NAN);
+        if (p.b <= 0.0) fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", p.b);
+        p.aux = -0.5 * std::log(2 * M_PI) - std::log(p.b);
+      } else {
+        fail("Bayesian problems on this path support 'Univariate/Uniform' and 'Univariate/Normal' priors (distribution '%s').",
+             pn.c_str());
+      }
+      priors.push_back(p);
+    }
+  }
+
+  // evaluateLogPosterior (:56-77); F(x) = logP(x) = logPosterior (:79-84)
+  void evaluate(Sample &s, const std::vector<double> &x, size_t id) {
+    double logPrior = 0.0;
+    for (size_t i = 0; i < x.size(); i++) {
+      const Prior &p = priors[i];
+      if (p.normal) {
+        const double d = (x[i] - p.a) / p.b;
+        logPrior += p.aux - 0.5 * d * d;
+      } else {
+        logPrior += (x[i] >= p.a && x[i] <= p.b) ? p.aux : -INFINITY;
+      }
+    }
+    s["logPrior"] = logPrior;
+    if (logPrior == -INFINITY) {
+      s["logLikelihood"] = -INFINITY;
+      s["logPosterior"] = -INFINITY;
+    } else {
+      getFunction(fn)(s);
+      if (reference) s["logLikelihood"] = referenceLoglikelihood(likelihoodModel, referenceData, s);
+      if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", id);
+      const double ll = s["logLikelihood"].getDouble();
+      if (std::isnan(ll)) fail("Sample %zu returned NaN logLikelihood evaluation.\n", id);
+      s["logPosterior"] = logPrior + ll;
+    }
+    s["F(x)"] = s["logPosterior"];
+    s["logP(x)"] = s["logPosterior"];
+  }
+};
+
 // ------------------------------------------------------------ modules
 struct SolverModule {
   Conduit *conduit = nullptr;  // the engine's sample dispatch (host callbacks)
@@ -316,6 +407,7 @@ struct CmaesModule : SolverModule {
   size_t N = 0, lam = 0, mu = 0;
   int objective = -1;  // builtin kernel, or -1: host function
   size_t fn = 0;
+  std::unique_ptr<BayesianEvaluator> bayesian;  // Bayesian problems: F(x) = logPosterior
   std::vector<VariableSpec> vars;
   double maxGenerations, maxModelEvaluations, maxInfeasible, maxCondition, minStd, maxStd, maxValue, minValueDiff;
   Json *solverJs = nullptr;
@@ -328,8 +420,10 @@ struct CmaesModule : SolverModule {
     Json &sv = js["Solver"];
     Json &pb = js["Problem"];
     solverJs = &sv;
-    if (canon(str(pb, "Type", "")) != "optimization")
-      fail("Solver CMAES requires a problem of type 'Optimization' (is '%s').", pb["Type"].getString().c_str());
+    const std::string pt = canon(str(pb, "Type", ""));
+    if (pt != "optimization" && pt != "bayesian/custom" && pt != "bayesian/reference")
+      fail("Solver CMAES requires a problem of type 'Optimization', 'Bayesian/Custom' or 'Bayesian/Reference' (is '%s').",
+           pb["Type"].getString().c_str());
     vars = readVariables(js);
     N = vars.size();
     lam = uint(sv, "Population Size", 0);
@@ -359,7 +453,9 @@ struct CmaesModule : SolverModule {
     maxValue = num(tc, "Max Value", INFINITY);
     minValueDiff = num(tc, "Min Value Difference Threshold", -INFINITY);
 
-    if (pb.contains("Objective Kernel")) {
+    if (pt != "optimization") {
+      bayesian.reset(new BayesianEvaluator(js, pt));
+    } else if (pb.contains("Objective Kernel")) {
       const std::string k = canon(pb["Objective Kernel"].getString());
       objective = (k == "negativerosenbrock" || k == "rosenbrock")   ? KG_OBJ_NEGATIVE_ROSENBROCK
                   : (k == "negativeackley" || k == "ackley")         ? KG_OBJ_NEGATIVE_ACKLEY
@@ -446,20 +542,26 @@ struct CmaesModule : SolverModule {
       // KORALI_START every sample, KORALI_WAITALL (CMAES.cpp.base:204-224)
       std::vector<double> X(lam * N), F(lam);
       check(kg_cmaes_get_candidates(h, X.data(), N));
-      Function &f = getFunction(fn);
+      Function *f = bayesian ? nullptr : &getFunction(fn);
       conduit->evaluateBatch(lam, [&](size_t i) {
         Sample s;
         s["Module"] = "Problem";
         s["Operation"] = "Evaluate";
         s["Sample Id"] = (unsigned long long)i;
         s["Current Generation"] = (unsigned long long)gen;
-        s["Parameters"] = std::vector<double>(X.begin() + i * N, X.begin() + (i + 1) * N);
-        f(s);
+        std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
+        s["Parameters"] = x;
+        if (bayesian) {  // Bayesian::evaluate: -Inf outside the prior's support is a valid F(x)
+          bayesian->evaluate(s, x, i);
+          F[i] = s["F(x)"].getDouble();
+          return;
+        }
+        (*f)(s);
         if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
         F[i] = s["F(x)"].getDouble();
         if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
       });
-      check(kg_cmaes_set_fitness(h, F.data()));
+      check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
     }
     check(kg_cmaes_update(h, gen));
     check(kg_cmaes_synchronize(h));  // device-side error flags -> KoraliError

@@ -55,7 +55,7 @@ class _TmcmcCfg(C.Structure):
 EXPORTED = [
     "kg_last_error", "kg_abi_version", "kg_device_count",
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
-    "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_update", "kg_cmaes_generation",
+    "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_set_log_posterior", "kg_cmaes_update", "kg_cmaes_generation",
     "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
@@ -85,6 +85,7 @@ def lib():
         L.kg_cmaes_eval_builtin.argtypes = [vp, ip]
         L.kg_cmaes_get_candidates.argtypes = [vp, dp, sz]
         L.kg_cmaes_set_fitness.argtypes = [vp, dp]
+        L.kg_cmaes_set_log_posterior.argtypes = [vp, dp]
         L.kg_cmaes_update.argtypes = [vp, sz]
         L.kg_cmaes_update_partial.argtypes = [vp, sz]
         L.kg_cmaes_update_finalize.argtypes = [vp, sz]
@@ -231,6 +232,11 @@ class CmaesDevice:
     def set_fitness(self, F):
         F = np.ascontiguousarray(F, dtype=np.float64)
         check(self._L.kg_cmaes_set_fitness(self.h, _dptr(F)))
+
+    def set_log_posterior(self, F):
+        """Bayesian problems: F(x) = logPosterior, -inf allowed."""
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        check(self._L.kg_cmaes_set_log_posterior(self.h, _dptr(F)))
 
     # state
     def field_size(self, name):

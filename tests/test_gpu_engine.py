@@ -493,3 +493,79 @@ def test_bayesian_reference_reproduces_reference_tmcmc_result_files(tmp_path):
             assert mine[k] == s[k], (g, k)
         for k in ("Multinomial Generator", "Multivariate Generator", "Uniform Generator"):
             assert mine[k]["Range"] == s[k]["Range"], (g, k)
+
+
+def ref_linear_experiment(problem_type):
+    """examples/bayesian.inference/reference/run-cmaes.py (MAP estimate)."""
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = problem_type
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = 24
+    e["Solver"]["Termination Criteria"]["Max Generations"] = 100
+    e["Distributions"][0]["Name"] = "Uniform 0"
+    e["Distributions"][0]["Type"] = "Univariate/Uniform"
+    e["Distributions"][0]["Minimum"] = 0.0
+    e["Distributions"][0]["Maximum"] = +5.0
+    for i, n in enumerate(("a", "b", "[Sigma]")):
+        e["Variables"][i]["Name"] = n
+        e["Variables"][i]["Prior Distribution"] = "Uniform 0"
+        e["Variables"][i]["Initial Value"] = +2.5
+        e["Variables"][i]["Initial Standard Deviation"] = +0.5
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["Random Seed"] = 1337
+    return e
+
+
+def test_cmaes_bayesian_reference_finds_the_analytic_map():
+    """Uniform priors: the MAP is the least-squares line with sigma^2 = RSS/n;
+    candidates outside the priors' support (sigma < 0 near the optimum) get
+    F(x) = -inf, as Bayesian::evaluate gives them."""
+    import korali
+    e = ref_linear_experiment("Bayesian/Reference")
+    e["Problem"]["Likelihood Model"] = "Normal"
+    e["Problem"]["Reference Data"] = REF_Y
+    e["Problem"]["Computational Model"] = linear_reference_model
+    korali.Engine().run(e)
+    A = np.stack([REF_X, np.ones(5)], 1)
+    (a, b), rss = np.linalg.lstsq(A, np.array(REF_Y), rcond=None)[:2]
+    sig = math.sqrt(rss[0] / 5)
+    best = -3 * math.log(5.0) - 5 * math.log(sig) - 0.5 * (5 * math.log(2 * math.pi) + 5)
+    p = e["Results"]["Best Sample"]["Parameters"]
+    assert np.allclose(p, [a, b, sig], rtol=1e-3, atol=1e-3), (p, a, b, sig)
+    assert e["Solver"]["Best Ever Value"] == pytest.approx(best, rel=1e-8)
+
+
+def test_cmaes_bayesian_custom_equals_optimization_objective():
+    """Bayesian/Custom through CMA-ES is the Optimization run of
+    F = logPrior + logLikelihood (same seed, candidates inside the support):
+    identical generations, bit for bit."""
+    import korali
+
+    def loglik(s):
+        a, b, sig = s["Parameters"][0], s["Parameters"][1], s["Parameters"][2]
+        s["logLikelihood"] = -sum((y - (a * x + b))**2 for x, y in zip(REF_X, REF_Y)) - 0.1 * sig * sig
+
+    def objective(s):
+        lp = 0.0
+        for _ in range(3):
+            lp += -math.log(5.0)
+        loglik(s)
+        s["F(x)"] = lp + s["logLikelihood"]
+
+    eb = ref_linear_experiment("Bayesian/Custom")
+    eb["Problem"]["Likelihood Model"] = loglik
+    eb["Solver"]["Termination Criteria"]["Max Generations"] = 8
+    eo = ref_linear_experiment("Optimization")
+    eo["Problem"]["Objective Function"] = objective
+    eo["Solver"]["Termination Criteria"]["Max Generations"] = 8
+    for i in range(3):
+        eo["Variables"][i]["Lower Bound"] = 0.0
+        eo["Variables"][i]["Upper Bound"] = 5.0
+        eb["Variables"][i]["Lower Bound"] = 0.0
+        eb["Variables"][i]["Upper Bound"] = 5.0
+    korali.Engine().run(eb)
+    korali.Engine().run(eo)
+    for k in ("Current Mean", "Covariance Matrix", "Sigma", "Best Ever Value", "Sample Population"):
+        assert eb["Solver"][k] == eo["Solver"][k], k

@@ -150,3 +150,11 @@ def test_sample_entries_extend_in_place():
     s["Reference Evaluations"] += [1.5]
     s["Reference Evaluations"] += [2.5]
     assert s["Reference Evaluations"] == [1.5, 2.5]
+
+
+def test_cmaes_bayesian_prior_validation_before_device():
+    e = reference_experiment()
+    e["Solver"] = {"Type": "Optimizer/CMAES", "Population Size": 8}
+    e["Distributions"][2]["Type"] = "Univariate/Exponential"
+    with pytest.raises(korali.KoraliError, match="Univariate/Normal"):
+        korali.Engine().run(e)
