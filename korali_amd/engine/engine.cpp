@@ -890,7 +890,8 @@ struct TmcmcModule : SolverModule {
     check(kg_tmcmc_field_size(h, "Sample Database", &n));
     std::vector<double> v(n);
     check(kg_tmcmc_get_field(h, "Sample Database", v.data(), n));
-    js["Results"]["Posterior Sample Database"] = matrixJson(v, n / N, N);
+    js["Results"]["Sample Database"] = matrixJson(v, n / N, N);  // TMCMC.cpp.base:791-795
+    js["Results"]["Posterior Sample Database"] = js["Results"]["Sample Database"];
     js["Results"]["Log Evidence"] = field("LogEvidence");
   }
 

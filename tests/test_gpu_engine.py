@@ -110,6 +110,8 @@ def test_statistical_tmcmc_gaussian():
     assert np.isclose(-2.0, samples.mean(), atol=0.05)
     assert np.isclose(3.0, samples.std(), atol=0.05)
     assert e["Solver"]["Annealing Exponent"] == 1.0
+    # TMCMC::finalize (TMCMC.cpp.base:791-795)
+    assert np.array_equal(np.reshape(e["Results"]["Sample Database"], (-1, 1)), samples)
 
 
 def fixture_experiment(path, max_gen=100):
