@@ -338,6 +338,18 @@ struct BayesianEvaluator {
   }
 };
 
+Json bayesianEvaluate(Json &experiment, const std::vector<double> &x) {
+  const std::string pt = canon(str(experiment["Problem"], "Type", ""));
+  if (pt != "bayesian/custom" && pt != "bayesian/reference") fail("Not a Bayesian problem ('%s').", pt.c_str());
+  BayesianEvaluator b(experiment, pt);
+  if (x.size() != b.priors.size()) fail("Expected %zu parameters, got %zu.", b.priors.size(), x.size());
+  Sample s;
+  s["Parameters"] = x;
+  s["Sample Id"] = 0ULL;
+  b.evaluate(s, x, 0);
+  return s._js;
+}
+
 // ------------------------------------------------------------ modules
 struct SolverModule {
   Conduit *conduit = nullptr;  // the engine's sample dispatch (host callbacks)

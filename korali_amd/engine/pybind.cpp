@@ -223,6 +223,16 @@ PYBIND11_MODULE(libkorali, m) {
     return korali::referenceLoglikelihood(model, y, s);
   });
 
+  // test hook: Bayesian::evaluate of one parameter vector (CMA-ES on Bayesian problems)
+  m.def("_bayesian_evaluate", [](korali::Experiment &e, const std::vector<double> &x) {
+    Json out;
+    {
+      py::gil_scoped_release nogil;  // the model callbacks take the GIL themselves
+      out = korali::bayesianEvaluate(e._js, x);
+    }
+    return toPy(out);
+  });
+
   // test hook: the conduit's batch dispatch with a Python body
   m.def("_conduit_evaluate", [](size_t jobs, size_t n, py::function body) {
     py::gil_scoped_release nogil;

@@ -158,3 +158,45 @@ def test_cmaes_bayesian_prior_validation_before_device():
     e["Distributions"][2]["Type"] = "Univariate/Exponential"
     with pytest.raises(korali.KoraliError, match="Univariate/Normal"):
         korali.Engine().run(e)
+
+
+def test_bayesian_evaluate_reference_and_priors():
+    """Bayesian::evaluate (bayesian.cpp.base:24-84) as CMA-ES sees it: Uniform
+    log-density -log(max - min), the model skipped outside the support."""
+    calls = []
+
+    def model(s):
+        calls.append(1)
+        a, b, sig = s["Parameters"][0], s["Parameters"][1], s["Parameters"][2]
+        s["Reference Evaluations"] = [a * x + b for x in X]
+        s["Standard Deviation"] = [sig] * len(X)
+
+    e = reference_experiment()
+    e["Problem"]["Computational Model"] = model
+    out = L._bayesian_evaluate(e, [0.9, 2.2, 0.3])
+    lp = 0.0
+    for _ in range(3):
+        lp += -math.log(5.0)
+    ll = L._reference_loglikelihood("Normal", Y, linear_model([0.9, 2.2, 0.3]))
+    assert out["logPrior"] == lp and out["logLikelihood"] == ll
+    assert out["F(x)"] == out["logPosterior"] == out["logP(x)"] == lp + ll
+    assert len(calls) == 1
+    out = L._bayesian_evaluate(e, [0.9, 2.2, -0.1])  # sigma outside Uniform(0, 5)
+    assert out["F(x)"] == -math.inf and out["logLikelihood"] == -math.inf and len(calls) == 1
+
+
+def test_bayesian_evaluate_custom_with_normal_prior():
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lambda s: s.__setitem__("logLikelihood", -2.0 * s["Parameters"][0] ** 2)
+    e["Distributions"][0]["Name"] = "N"
+    e["Distributions"][0]["Type"] = "Univariate/Normal"
+    e["Distributions"][0]["Mean"] = 1.0
+    e["Distributions"][0]["Standard Deviation"] = 2.0
+    e["Variables"][0]["Name"] = "x"
+    e["Variables"][0]["Prior Distribution"] = "N"
+    out = L._bayesian_evaluate(e, [0.5])
+    d = (0.5 - 1.0) / 2.0
+    assert out["logPrior"] == (-0.5 * math.log(2 * math.pi) - math.log(2.0)) - 0.5 * d * d
+    assert out["F(x)"] == out["logPrior"] + (-0.5)
+    assert out["logPrior"] == pytest.approx(st.norm.logpdf(0.5, 1.0, 2.0), rel=1e-15)
