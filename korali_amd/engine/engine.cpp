@@ -63,6 +63,14 @@ double num(Json &j, const char *key, double def) {
   if (!j.contains(key) || j[key].is_null()) j[key] = def;
   return j[key].getDouble();
 }
+// a mandatory numeric setting (generated setConfiguration, source_builders.py:72-75)
+double mandatory(Json &j, const char *key, const char *module) {
+  if (!j.contains(key) || j[key].is_null())
+    fail(" + No value provided for mandatory setting: ['%s'] required by %s.\n", key, module);
+  const double v = j[key].getDouble();
+  if (!std::isfinite(v)) fail(" + Non-finite value provided for mandatory setting: ['%s'] required by %s.\n", key, module);
+  return v;
+}
 bool flag(Json &j, const char *key, bool def) {
   if (!j.contains(key) || j[key].is_null()) j[key] = def;
   return j[key].getBool();
@@ -292,14 +300,14 @@ struct BayesianEvaluator {
       const std::string t = canon(ds[k]["Type"].getString());
       Prior p{};
       if (t == "univariate/uniform") {
-        p.a = num(ds[k], "Minimum", NAN);
-        p.b = num(ds[k], "Maximum", NAN);
+        p.a = mandatory(ds[k], "Minimum", "Distributions");
+        p.b = mandatory(ds[k], "Maximum", "Distributions");
         p.aux = p.b - p.a <= 0.0 ? NAN : -std::log(p.b - p.a);
       } else if (t == "univariate/normal") {
         p.normal = true;
-        p.a = num(ds[k], "Mean", NAN);
-        p.b = num(ds[k], "Standard Deviation", NAN);
-        if (p.b <= 0.0) fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", p.b);
+        p.a = mandatory(ds[k], "Mean", "Distributions");
+        p.b = mandatory(ds[k], "Standard Deviation", "Distributions");
+        if (!(p.b > 0.0)) fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", p.b);
         p.aux = -0.5 * std::log(2 * M_PI) - std::log(p.b);
       } else {
         fail("Bayesian problems on this path support 'Univariate/Uniform' and 'Univariate/Normal' priors (distribution '%s').",
@@ -719,8 +727,8 @@ struct TmcmcModule : SolverModule {
       if (k < 0) fail("Did not find a distribution named '%s'.", pn.c_str());
       if (canon(ds[k]["Type"].getString()) != "univariate/uniform")
         fail("The device TMCMC path supports 'Univariate/Uniform' priors (distribution '%s').", pn.c_str());
-      pmin[i] = ds[k]["Minimum"].getDouble();
-      pmax[i] = ds[k]["Maximum"].getDouble();
+      pmin[i] = mandatory(ds[k], "Minimum", "Distributions");
+      pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
       pdist[i] = k;
     }
     if (reference) {
@@ -902,9 +910,7 @@ struct TmcmcModule : SolverModule {
     check(kg_tmcmc_field_size(h, "Sample Database", &n));
     std::vector<double> v(n);
     check(kg_tmcmc_get_field(h, "Sample Database", v.data(), n));
-    js["Results"]["Sample Database"] = matrixJson(v, n / N, N);  // TMCMC.cpp.base:791-795
-    js["Results"]["Posterior Sample Database"] = js["Results"]["Sample Database"];
-    js["Results"]["Log Evidence"] = field("LogEvidence");
+    js["Results"]["Sample Database"] = matrixJson(v, n / N, N);  // TMCMC.cpp.base:791-795 (the only key it writes)
   }
 
   void printAfter(const Logger &log) override {

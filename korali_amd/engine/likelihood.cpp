@@ -56,10 +56,11 @@ std::vector<double> vec(Sample &s, const char *key, const std::string &model, si
   if (!s.contains(key)) lfail("This Bayesian (%s) problem requires a '%s' entry in the sample.\n", model.c_str(), key);
   Json &j = s[key];
   std::vector<double> v;
-  if (j.is_array())
-    for (const Json &x : j.elements()) v.push_back(x.getDouble());
-  else if (j.is_number())
-    v.push_back(j.getDouble());
+  // KORALI_GET(std::vector<double>, ...) (sample.hpp:174-190): only an array converts
+  if (!j.is_array())
+    lfail("Missing or incorrect value ['%s'] for the sample.\n + Cause: type must be array, but is %s\n", key,
+          j.is_number() ? "number" : "not an array");
+  for (const Json &x : j.elements()) v.push_back(x.getDouble());
   if (v.size() != nd)
     lfail("This Bayesian (%s) problem requires a %lu-sized %s array. Provided: %lu.\n", model.c_str(), (unsigned long)nd, key,
           (unsigned long)v.size());
@@ -112,7 +113,11 @@ double betaInc(double a, double b, double x) {
   return 1.0 - pre * betaCf(b, a, 1.0 - x) / b;
 }
 
-// gsl_cdf_tdist_P (cdf/tdist.c): the lower tail through the incomplete beta
+// Student-t lower tail P(T <= x) through the regularised incomplete beta.
+// NOT GSL-equal: gsl_cdf_tdist_P (cdf/tdist.c) switches to a Cornish-Fisher
+// expansion for nu > 30 and x^2 < 10 nu and uses other beta_inc forms on its
+// remaining branches; this returns the exact tail on every branch (parity with
+// GSL unpinned; the Positive StudentT likelihood is off the north-star path).
 double tdistP(double x, double nu) {
   const double t = nu / (nu + x * x);
   const double tail = 0.5 * betaInc(nu / 2, 0.5, t);  // P(T > |x|)

@@ -76,7 +76,7 @@ Json toJson(const py::handle &o) {
   }
   // numpy scalars and other numbers
   if (py::hasattr(o, "__float__")) return Json(o.cast<double>());
-  throw std::runtime_error("cannot store a value of type " + std::string(py::str(o.get_type())) + " in Korali JSON");
+  throw std::runtime_error("cannot store a value of type " + std::string(py::str(py::type::handle_of(o))) + " in Korali JSON");
 }
 
 using Key = std::variant<std::string, size_t>;

@@ -229,13 +229,19 @@ class CmaesDevice:
         check(self._L.kg_cmaes_get_candidates(self.h, _dptr(X), self.N))
         return X
 
-    def set_fitness(self, F):
+    def _fitness_arg(self, F):
         F = np.ascontiguousarray(F, dtype=np.float64)
+        if F.shape != (self.lam,):
+            raise ValueError("fitness vector has shape %s, expected (%d,)" % (F.shape, self.lam))
+        return F
+
+    def set_fitness(self, F):
+        F = self._fitness_arg(F)
         check(self._L.kg_cmaes_set_fitness(self.h, _dptr(F)))
 
     def set_log_posterior(self, F):
         """Bayesian problems: F(x) = logPosterior, -inf allowed."""
-        F = np.ascontiguousarray(F, dtype=np.float64)
+        F = self._fitness_arg(F)
         check(self._L.kg_cmaes_set_log_posterior(self.h, _dptr(F)))
 
     # state

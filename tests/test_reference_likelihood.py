@@ -200,3 +200,31 @@ def test_bayesian_evaluate_custom_with_normal_prior():
     assert out["logPrior"] == (-0.5 * math.log(2 * math.pi) - math.log(2.0)) - 0.5 * d * d
     assert out["F(x)"] == out["logPrior"] + (-0.5)
     assert out["logPrior"] == pytest.approx(st.norm.logpdf(0.5, 1.0, 2.0), rel=1e-15)
+
+
+@pytest.mark.parametrize("dist,drop", [("Univariate/Normal", "Standard Deviation"), ("Univariate/Normal", "Mean"),
+                                       ("Univariate/Uniform", "Minimum"), ("Univariate/Uniform", "Maximum")])
+def test_bayesian_prior_mandatory_settings(dist, drop):
+    """A missing prior parameter fails at configuration time with the
+    generated setConfiguration's message (source_builders.py:72-75)."""
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lambda s: s.__setitem__("logLikelihood", 0.0)
+    e["Distributions"][0]["Name"] = "P"
+    e["Distributions"][0]["Type"] = dist
+    params = {"Mean": 0.0, "Standard Deviation": 1.0} if "Normal" in dist else {"Minimum": 0.0, "Maximum": 1.0}
+    for k, v in params.items():
+        if k != drop:
+            e["Distributions"][0][k] = v
+    e["Variables"][0]["Name"] = "x"
+    e["Variables"][0]["Prior Distribution"] = "P"
+    with pytest.raises(korali.KoraliError, match="No value provided for mandatory setting: \\['%s'\\]" % drop):
+        L._bayesian_evaluate(e, [0.5])
+
+
+def test_reference_likelihood_rejects_scalar_where_array_expected():
+    """KORALI_GET(std::vector<double>, ...) does not convert a scalar."""
+    s = linear_model([0.9, 2.2, 0.3])
+    s["Standard Deviation"] = 0.3
+    with pytest.raises(korali.KoraliError, match="Standard Deviation"):
+        L._reference_loglikelihood("Normal", Y, s)
