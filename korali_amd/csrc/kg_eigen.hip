@@ -954,7 +954,7 @@ __device__ __forceinline__ double padded_chain(const double *a, const double *b,
 
 __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__restrict__ C, double *gH,
                                                         double *tauOut, double *dOut, double *sdOut,
-                                                        unsigned long long *trace) {
+                                                        unsigned long long *trace, int xflags) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
   const int lda = N + 1, VS = N + 32;
@@ -968,7 +968,9 @@ __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__r
   double *scal = sv + VS;              // 16 scalars
   unsigned long long *msk = (unsigned long long *)(scal + 16);  // dnrm2 rescale masks
   const bool tr = trace && tid == 0;
-  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+  if ((xflags & 1) && wid == 0) __builtin_amdgcn_s_setprio(3);
+  if ((xflags & 4) && wid > 0 && wid < 4) __builtin_amdgcn_s_setprio(2);
 #define T1_MARK(k)                                                \
   if (tr) {                                                       \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
@@ -991,6 +993,11 @@ __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__r
     if (wid == 0) {
       const double *v = M + (size_t)i * lda + i + 1;  // v[0] = alpha, v[1..n-1]
       const double xnorm = dnrm2_wave128(v + 1, n - 1, sv);
+      if (tr) {
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+        tacc[6] += t_ - tm;
+        tm = t_;
+      }
       double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
       int branch = 0;
       if (xnorm != 0) {
@@ -1008,6 +1015,11 @@ __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__r
         }
       }
       const double v0out = branch ? beta : v[0];
+      if (tr) {
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+        tacc[7] += t_ - tm;
+        tm = t_;
+      }
       for (int r = lane; r < n; r += 64) {
         double t = v[r];
         if (r > 0 && branch != 0) {
@@ -1101,8 +1113,11 @@ __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__r
   }
   __syncthreads();
 #undef T1_MARK
-  if (tr)
+  if (tr) {
     for (int k = 0; k < 6; k++) trace[8 + k] += tacc[k];
+    trace[29] += tacc[6];
+    trace[30] += tacc[7];
+  }
   for (int r = tid; r < N; r += nt) {
     dOut[r] = M[(size_t)r * lda + r];
     if (r == N - 2) sdOut[r] = M[(size_t)r * lda + r + 1];
@@ -1867,6 +1882,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
   } else if (getenv("KORALI_AMD_EIGEN_MW_MIN") && !lds) {
     tri = 2;
   }
+  if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
   if (tri == 1)
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(t1_lds_doubles(N) * sizeof(double))));
@@ -1916,7 +1932,7 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   if (prof) prof(profCtx, "eigen_tridiag", 0);
   if (tri == 1)
     hipLaunchKernelGGL(k_tridiag_1wg, dim3(1), dim3(T1_TPB), t1_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
-                       sd, trace);
+                       sd, trace, t1flags);
   else if (tri == 0)
     hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), eig_mat_bytes(N) + tridiag_vec_bytes(N), s, N, C, gA, gH,
                        tau, d, sd, trace);

@@ -778,7 +778,7 @@ double btpe_tail(double y1) {
   return (13860.0 - (462.0 - (132.0 - (99.0 - 140.0 / y2) / y2) / y2) / y2) / y1 / 166320.0;
 }
 
-unsigned binomial(HostMt &r, double p, unsigned n) {
+unsigned binomial(HostMt &r, double p, unsigned n, double *btpeDraws) {
   if (n == 0) return 0;
   bool flip = false;
   if (p > 0.5) {
@@ -803,6 +803,7 @@ unsigned binomial(HostMt &r, double p, unsigned n) {
       if (done) break;
     }
   } else {
+    *btpeDraws += 1.0;  // diagnostics: draws that took the BTPE branch
     const double ffm = np + p;
     const int m = (int)ffm;
     const double fm = m, xm = fm + 0.5, npq = np * q;
@@ -868,12 +869,12 @@ unsigned binomial(HostMt &r, double p, unsigned n) {
 
 // gsl_ran_multinomial (randist/multinomial.c), Multinomial::getSelections
 // (specific/multinomial/multinomial.cpp.base:7-10)
-void multinomial(HostMt &r, size_t K, unsigned N, const double *p, unsigned *n) {
+void multinomial(HostMt &r, size_t K, unsigned N, const double *p, unsigned *n, double *btpeDraws) {
   double norm = 0.0, sum_p = 0.0;
   unsigned sum_n = 0;
   for (size_t k = 0; k < K; k++) norm += p[k];
   for (size_t k = 0; k < K; k++) {
-    n[k] = p[k] > 0.0 ? binomial(r, p[k] / (norm - sum_p), N - sum_n) : 0;
+    n[k] = p[k] > 0.0 ? binomial(r, p[k] / (norm - sum_p), N - sum_n, btpeDraws) : 0;
     sum_p += p[k];
     sum_n += n[k];
   }
@@ -967,6 +968,7 @@ struct kg_tmcmc_s {
          selectionAcceptanceRate = 0, dbCount = 0, modelEvaluationCount = 0, minSearchIterations = 0,
          currentBurnIn = 0;
   double exactEvalsD = 0;  // diagnostics: host-exact cv2 evaluations so far
+  double btpeDraws = 0;    // diagnostics: multinomial binomials drawn by BTPE (n p >= 14)
   bool devPending = false;  // accepted count / maxLoglikelihood not yet read back
   // profiling
   bool profile = false;
@@ -1495,6 +1497,7 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Min Search Iterations", minSearchIterations)
   SCA("Current Burn In", currentBurnIn)
   SCA("Exact Search Evaluations", exactEvalsD)
+  SCA("BTPE Binomial Draws", btpeDraws)
 #undef VEC
 #undef SCA
   return false;
@@ -1923,7 +1926,7 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
     for (int i = 0; i < P; i++) sw += h->hE[i];
     for (int i = 0; i < P; i++) wt[i] = h->hE[i] / sw;
     h->logEvidence += host_log_cr(sw) + lwmax - host_log_cr((double)P);
-    multinomial(h->multinomialRng, P, (unsigned)P, wt, h->nsel.data());
+    multinomial(h->multinomialRng, P, (unsigned)P, wt, h->nsel.data(), &h->btpeDraws);
     for (int i = 0; i < P; i++) h->hNsel[i] = h->nsel[i];
     for (int i = 0; i < P; i++) wt[i] = wt[i] * h->nsel[i];
     sw = 0.0;

@@ -14,6 +14,22 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Threads for the data-parallel loops of the checker (OpenMP build only).
+ * Every parallel loop computes independent outputs, each with the
+ * reference's own operation order, so results do not depend on the thread
+ * count; the CPU-baseline timing sets 1 (the reference is single-threaded). */
+void kr_set_threads(int n)
+{
+#ifdef _OPENMP
+  omp_set_num_threads(n < 1 ? 1 : n);
+#else
+  (void)n;
+#endif
+}
 
 #define KR_DBL_EPSILON 2.2204460492503131e-16
 #define KR_DBL_MIN 2.2250738585072014e-308
@@ -101,6 +117,15 @@ static inline dd_t dd_from(double a) { return (dd_t){a, 0.0}; }
 
 static const dd_t DD_LN2 = {6.93147180559945286227e-01, 2.31904681384629955842e-17};
 
+/* 1/(2j+1), j = 0..21, as double-doubles (the series coefficients of
+ * dd_log, computed once at load by the same dd_div) */
+static dd_t dd_log_inv_odd[22];
+__attribute__((constructor)) static void dd_log_init(void)
+{
+  int j;
+  for (j = 0; j < 22; j++) dd_log_inv_odd[j] = dd_div(dd_from(1.0), dd_from(2.0 * j + 1.0));
+}
+
 /* log(x) for finite x > 0 as a double-double: x = m 2^k, m in
  * [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m-1)/(m+1). */
 static dd_t dd_log(double x)
@@ -115,8 +140,8 @@ static dd_t dd_log(double x)
   }
   s = dd_div(dd_from(m - 1.0), dd_two_sum(m, 1.0));
   z = dd_mul(s, s);
-  p = dd_div(dd_from(1.0), dd_from(43.0));
-  for (j = 20; j >= 0; j--) p = dd_add(dd_mul(p, z), dd_div(dd_from(1.0), dd_from(2.0 * j + 1.0)));
+  p = dd_log_inv_odd[21];
+  for (j = 20; j >= 0; j--) p = dd_add(dd_mul(p, z), dd_log_inv_odd[j]);
   p = dd_mul(dd_mul_d(s, 2.0), p);
   return dd_add(dd_mul_d(DD_LN2, (double)k), p);
 }
@@ -304,6 +329,31 @@ double kr_rng_uniform_pos(kr_rng *r)
   return x;
 }
 
+/* n draws of 0 + gsl_ran_gaussian(r, 1.0) in stream order: the accept /
+ * reject loop consumes the generator serially, the log / sqrt of each
+ * accepted pair (the same expression as kr_ran_gaussian) run in parallel */
+void kr_ran_gaussian_n(kr_rng *r, size_t n, double *out)
+{
+  double *r2v = (double *)malloc(sizeof(double) * n);
+  long i;
+  size_t k;
+  for (k = 0; k < n; k++)
+  {
+    double x, y, r2;
+    do
+    {
+      x = -1 + 2 * kr_rng_uniform_pos(r);
+      y = -1 + 2 * kr_rng_uniform_pos(r);
+      r2 = x * x + y * y;
+    } while (r2 > 1.0 || r2 == 0);
+    out[k] = y;
+    r2v[k] = r2;
+  }
+#pragma omp parallel for schedule(static)
+  for (i = 0; i < (long)n; i++) out[i] = 0.0 + 1.0 * out[i] * sqrt(-2.0 * kr_log_cr(r2v[i]) / r2v[i]);
+  free(r2v);
+}
+
 /* gsl_ran_gaussian (randist/gauss.c, polar Box-Muller); Korali
  * univariate/normal/normal.cpp.base:32-35 */
 double kr_ran_gaussian(kr_rng *r, double sigma)
@@ -348,6 +398,9 @@ static double btpe_stirling(double y1)
  * otherwise).  The BTPE branch is restated from Kachitvichyanukul &
  * Schmeiser (1988) as GSL implements it; no reference fixture reaches it
  * (parity unpinned for that branch). */
+static unsigned long long kr_btpe_count; /* draws that took the BTPE branch */
+unsigned long long kr_btpe_draws(void) { return kr_btpe_count; }
+
 unsigned int kr_ran_binomial(kr_rng *rng, double p, unsigned int n)
 {
   int ix;
@@ -398,6 +451,7 @@ unsigned int kr_ran_binomial(kr_rng *rng, double p, unsigned int n)
     double p4 = p3 + c / lambda_r;
     double var, accept;
     double u, v;
+    kr_btpe_count++;
   TryAgain:
     u = kr_rng_uniform(rng) * p4;
     v = kr_rng_uniform(rng);
@@ -1414,6 +1468,44 @@ static int cmaes_feasible(const kr_cmaes *h, const double *x)
   return 1;
 }
 
+/* x_i = m + sigma B (D o z_i) for samples [0, lambda) from normals drawn in
+ * stream order beforehand (the loop of sampleSingle, CMAES.cpp.base:494-545,
+ * per sample; samples are independent) */
+static void cmaes_sample_all(kr_cmaes *h, const double *Z)
+{
+  const size_t N = h->N;
+  long i;
+#pragma omp parallel
+  {
+    double *aux = (double *)malloc(sizeof(double) * N);
+#pragma omp for schedule(static)
+    for (i = 0; i < (long)h->lambda; ++i)
+    {
+      const double *z = Z + (size_t)i * N;
+      double *bdz = h->BDZ + (size_t)i * N, *x = h->X + (size_t)i * N;
+      size_t d, e;
+      for (d = 0; d < N; ++d)
+      {
+        if (h->diagonal)
+        {
+          bdz[d] = h->D[d] * z[d];
+          x[d] = h->currentMean[d] + h->sigma * bdz[d];
+        }
+        else
+          aux[d] = h->D[d] * z[d];
+      }
+      if (!h->diagonal)
+        for (d = 0; d < N; ++d)
+        {
+          bdz[d] = 0.0;
+          for (e = 0; e < N; ++e) bdz[d] += h->B[d * N + e] * aux[e];
+          x[d] = h->currentMean[d] + h->sigma * bdz[d];
+        }
+    }
+    free(aux);
+  }
+}
+
 /* draw loop of prepareGeneration, CMAES.cpp.base:443-491 */
 void kr_cmaes_sample_only(kr_cmaes *h)
 {
@@ -1422,6 +1514,26 @@ void kr_cmaes_sample_only(kr_cmaes *h)
   double *r1 = (double *)malloc(sizeof(double) * N), *r2 = (double *)malloc(sizeof(double) * N);
   if (!h->mirrored)
   {
+    /* fast form: draw every normal first (stream order), transform the
+     * samples in parallel, then check feasibility in sample order; on the
+     * first infeasible sample rewind the generator and replay the
+     * reference's sequential resampling loop below */
+    kr_rng saved = h->normal;
+    double *Z = (double *)malloc(sizeof(double) * N * h->lambda);
+    int all_ok = 1;
+    kr_ran_gaussian_n(&h->normal, h->lambda * N, Z);
+    cmaes_sample_all(h, Z);
+    for (i = 0; i < h->lambda && all_ok; ++i) all_ok = cmaes_feasible(h, h->X + i * N);
+    if (all_ok && !h->diagonal)
+      for (d = 0; d < N; ++d) h->auxBDZ[d] = h->D[d] * Z[(h->lambda - 1) * N + d];
+    free(Z);
+    if (all_ok)
+    {
+      free(r1);
+      free(r2);
+      return;
+    }
+    h->normal = saved;
     for (i = 0; i < h->lambda; ++i)
     {
       int ok;
@@ -1469,17 +1581,18 @@ void kr_cmaes_prepare(kr_cmaes *h)
 
 void kr_cmaes_evaluate(kr_cmaes *h, int objective)
 {
-  size_t i;
-  for (i = 0; i < h->lambda; i++)
+  long i;
+#pragma omp parallel for schedule(static)
+  for (i = 0; i < (long)h->lambda; i++)
   {
-    const double *x = h->X + i * h->N;
+    const double *x = h->X + (size_t)i * h->N;
     double f;
     if (objective == 0) f = kr_obj_negative_rosenbrock(x, h->N);
     else if (objective == 1) f = kr_obj_negative_ackley(x, h->N);
     else f = kr_obj_negative_sphere(x, h->N);
     h->F[i] = f;
-    h->modelEvaluationCount += 1;
   }
+  h->modelEvaluationCount += (double)h->lambda;
 }
 
 /* sort_index, CMAES.cpp.base:940-950: std::sort descending.  Ties are
@@ -1528,11 +1641,16 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
     }
     for (i = 0; i < mu; ++i) h->muWeights[i] /= valueSum;
   }
-  for (d = 0; d < N; ++d)
   {
-    h->previousMean[d] = h->currentMean[d];
-    h->currentMean[d] = 0.;
-    for (i = 0; i < mu; ++i) h->currentMean[d] += h->muWeights[i] * h->X[h->sortingIndex[i] * N + d];
+    long dd;
+#pragma omp parallel for schedule(static)
+    for (dd = 0; dd < (long)N; ++dd)
+    {
+      size_t ii;
+      h->previousMean[dd] = h->currentMean[dd];
+      h->currentMean[dd] = 0.;
+      for (ii = 0; ii < mu; ++ii) h->currentMean[dd] += h->muWeights[ii] * h->X[h->sortingIndex[ii] * N + dd];
+    }
   }
   for (d = 0; d < N; ++d) h->meanUpdate[d] = (h->currentMean[d] - h->previousMean[d]) / h->sigma;
   for (d = 0; d < N; ++d)
@@ -1566,18 +1684,28 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
   ccovmu = 2.0 * (h->effectiveMu - 2. + 1. / h->effectiveMu) / (kr_pow_cr(N + 2.0, 2) + h->effectiveMu);
   if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
   sigmasquare = h->sigma * h->sigma;
-  for (d = 0; d < N; ++d)
-    for (e = h->diagonal ? d : 0; e <= d; ++e)
+  {
+    /* every element (d, e <= d) is one sequential sum over k in the
+     * reference's order; rows are independent */
+    long dd;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (dd = (long)N - 1; dd >= 0; --dd)
     {
-      double c = (1 - ccov1 - ccovmu) * h->C[d * N + e] + ccov1 * (h->pc[d] * h->pc[e] + (1 - hsig) * h->cumulativeCovariance * (2. - h->cumulativeCovariance) * h->C[d * N + e]);
-      for (k = 0; k < mu; ++k)
+      size_t ee, kk;
+      const size_t d1 = (size_t)dd;
+      for (ee = h->diagonal ? d1 : 0; ee <= d1; ++ee)
       {
-        const double *xk = h->X + h->sortingIndex[k] * N;
-        c += ccovmu * h->muWeights[k] * (xk[d] - h->previousMean[d]) * (xk[e] - h->previousMean[e]) / sigmasquare;
+        double c = (1 - ccov1 - ccovmu) * h->C[d1 * N + ee] + ccov1 * (h->pc[d1] * h->pc[ee] + (1 - hsig) * h->cumulativeCovariance * (2. - h->cumulativeCovariance) * h->C[d1 * N + ee]);
+        for (kk = 0; kk < mu; ++kk)
+        {
+          const double *xk = h->X + h->sortingIndex[kk] * N;
+          c += ccovmu * h->muWeights[kk] * (xk[d1] - h->previousMean[d1]) * (xk[ee] - h->previousMean[ee]) / sigmasquare;
+        }
+        h->C[d1 * N + ee] = c;
+        if (ee < d1) h->C[ee * N + d1] = c;
       }
-      h->C[d * N + e] = c;
-      if (e < d) h->C[e * N + d] = c;
     }
+  }
   h->maxDiagC = h->minDiagC = h->C[0];
   for (d = 1; d < N; ++d)
   {

@@ -39,10 +39,13 @@ typedef struct
 } kr_rng;
 
 void kr_rng_seed(kr_rng *r, uint64_t seed);
+void kr_set_threads(int n);
+unsigned long long kr_btpe_draws(void); /* binomial draws that took the BTPE branch so far */ /* OpenMP checker build: threads of the data-parallel loops */
 uint32_t kr_rng_get(kr_rng *r);
 double kr_rng_uniform(kr_rng *r);
 double kr_rng_uniform_pos(kr_rng *r);
 double kr_ran_gaussian(kr_rng *r, double sigma);
+void kr_ran_gaussian_n(kr_rng *r, size_t n, double *out); /* n x (0 + gaussian(1)), stream order */
 double kr_ran_flat(kr_rng *r, double a, double b);
 unsigned int kr_ran_binomial(kr_rng *r, double p, unsigned int n);
 void kr_ran_multinomial(kr_rng *r, size_t K, unsigned int N, const double *p, unsigned int *n);

@@ -28,6 +28,8 @@ def lib(variant="cr"):
         L = C.CDLL(path)
         vp, sz, dp, cp = C.c_void_p, C.c_size_t, C.POINTER(C.c_double), C.c_char_p
         L.kr_rng_seed.argtypes = [vp, C.c_uint64]
+        L.kr_set_threads.argtypes = [C.c_int]
+        L.kr_btpe_draws.restype = C.c_ulonglong
         L.kr_rng_get.argtypes = [vp]
         L.kr_rng_get.restype = C.c_uint32
         L.kr_ran_gaussian.argtypes = [vp, C.c_double]

@@ -19,7 +19,9 @@ step() {
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 1200 python -m pytest tests -x -q -m gpu ;;
+    tests) step tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
+    trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c4.py ;;
     eng) step eng 900 python -m pytest tests/test_gpu_engine.py -q --maxfail=20 ;;
     tm) step tm 900 python -m pytest tests/test_gpu_tmcmc.py -q --maxfail=10 ;;
     c3) step c3 600 python bench.py --workload c3 --steps ${C3_STEPS:-40} --warmup 3 ;;
