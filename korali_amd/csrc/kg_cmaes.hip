@@ -33,6 +33,7 @@ struct CmaesScalars {
   double infeasibleSampleCount, bestValidSample, modelEvaluationCount, hsig, eigenFailures;
   double ccov1, ccovmu;
   unsigned int errors, bestFlag;  // bestFlag: best-ever improved this generation
+  unsigned int rmuOutOfRange;     // k_rankmu_prep: some rank-mu factor outside the Markstein range
 };
 
 // ----------------------------------------------------------------- init
@@ -469,6 +470,7 @@ __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, 
     sc->currentBestValue = F[i0];
     flag = (sc->currentBestValue > sc->bestEverValue || gen == 1) ? 1 : 0;
     sc->bestFlag = (unsigned)flag;
+    sc->rmuOutOfRange = 0u;  // set again by this generation's k_rankmu_prep
     if (flag) {
       sc->previousBestEverValue = sc->bestEverValue;
       sc->bestEverValue = sc->currentBestValue;
@@ -504,6 +506,209 @@ __global__ void __launch_bounds__(256) k_gather_selected(int N, int mu, const do
   // the rank-mu sum on the second stream
   if (i == 0)
     for (int d = threadIdx.x; d < N; d += blockDim.x) prevMean[d] = mean[d];
+}
+
+// ------------------------------------------------ exact rank-mu (adaptC)
+// The reference adds, for every lower-triangle element (d, e) and k < mu in
+// order (CMAES.cpp.base:700-707),
+//   c += ccovmu * w_k * (x_kd - m_d) * (x_ke - m_e) / sigma^2
+// = fl(fl(T_kd * Yc_ke) / s2)  with  Yc_kd = fl(x_kd - m_d),
+//   T_kd = fl(fl(ccovmu w_k) Yc_kd),  s2 = fl(sigma sigma).
+// k_rankmu_prep forms Yc (k-major, the e side) and T (transposed, d-major,
+// the d side) once; k_adaptC_exact2 then spends per term one product, the
+// Markstein-corrected quotient  q0 = p y, r = fma(-q0, s2, p),
+// q = fma(r, y, q0)  (y = fl(1/s2); q == fl(p / s2) exactly whenever p and
+// s2 stay far from underflow / overflow, Markstein's theorem) and the
+// ordered add.  The range condition is checked here on every factor
+// (exponents within +-450, nonzero, finite; then |p| in [2^-900, 2^900]);
+// if any factor leaves it the generation uses true division throughout.
+constexpr int RP_T = 32;
+__device__ inline bool rmu_in_range(double v) {
+  const int ex = (int)((__double_as_longlong(v) >> 52) & 0x7ff) - 1023;  // zero / subnormal: -1023
+  return ex >= -450 && ex <= 450;
+}
+__global__ void __launch_bounds__(256) k_rankmu_prep(int N, int mu, const double *__restrict__ Y,
+                                                     const double *__restrict__ w,
+                                                     const double *__restrict__ prevMean,
+                                                     CmaesScalars *sc, double *__restrict__ Yc,
+                                                     double *__restrict__ Tt) {
+  __shared__ double tile[RP_T][RP_T + 1];
+  const int k0 = blockIdx.x * RP_T, d0 = blockIdx.y * RP_T;
+  const int tx = threadIdx.x % RP_T, ty = threadIdx.x / RP_T;  // 32 x 8
+  // c_mu from mu_eff with k_paths' formula (CMAES.cpp.base:693-694)
+  const double effMu = sc->effectiveMu, ca = N + 1.3, cb = N + 2.0;
+  const double ccov1 = 2.0 / (ca * ca + effMu);
+  double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (cb * cb + effMu);
+  if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+  bool ok = true;
+  for (int r = ty; r < RP_T; r += 8) {
+    const int k = k0 + r, d = d0 + tx;
+    double t = 0.0;
+    if (k < mu && d < N) {
+      const double yc = Y[(size_t)k * N + d] - prevMean[d];
+      Yc[(size_t)k * N + d] = yc;
+      t = (ccovmu * w[k]) * yc;
+      ok = ok && rmu_in_range(yc) && rmu_in_range(t);
+    }
+    tile[r][tx] = t;
+  }
+  __syncthreads();
+  for (int r = ty; r < RP_T; r += 8) {
+    const int d = d0 + r, k = k0 + tx;
+    if (d < N && k < mu) Tt[(size_t)d * mu + k] = tile[tx][r];
+  }
+  if (__syncthreads_or(!ok) && threadIdx.x == 0) atomicOr(&sc->rmuOutOfRange, 1u);
+}
+
+// one wave per row d (4 rows per workgroup), one lane per column e (64
+// columns per workgroup).  Per chunk of AX_K k: the workgroup stages the
+// Yc rows of its 64 columns and the T values of its 4 rows in LDS (the next
+// chunk's global loads are in flight while the current chunk is summed);
+// each lane then runs its ordered chain reading Yc[k][lane] and the
+// wave-uniform T[k][d] (broadcast) from LDS.
+constexpr int AX_K = 64, AX_B = 16;
+template <bool kMarkstein>
+__device__ __forceinline__ double rankmu_term(double c, double t, double yc, double s2, double y) {
+  const double p = t * yc;
+  double q;
+  if (kMarkstein) {
+    const double q0 = p * y;
+    const double r = __builtin_fma(-q0, s2, p);
+    q = __builtin_fma(r, y, q0);
+  } else {
+    q = p / s2;
+  }
+  return c + q;
+}
+template <bool kMarkstein>
+__device__ __forceinline__ double rankmu_quot(double t, double yc, double s2, double y) {
+  const double p = t * yc;
+  if (kMarkstein) {
+    const double q0 = p * y;
+    const double r = __builtin_fma(-q0, s2, p);
+    return __builtin_fma(r, y, q0);
+  }
+  return p / s2;
+}
+template <bool kMarkstein>
+__device__ __forceinline__ double rankmu_chunk(double c, const double *__restrict__ ys, const double *__restrict__ ts,
+                                               int cnt, double s2, double y) {
+  if (cnt == AX_K) {
+    // operands of the next 16 terms are read from LDS while the current 16
+    // quotients (independent) are formed and added in order
+    double ya[AX_B], ta[AX_B], yb[AX_B], tb[AX_B];
+#pragma unroll
+    for (int u = 0; u < AX_B; u++) {
+      ya[u] = ys[u * 64];
+      ta[u] = ts[u];
+    }
+#pragma unroll
+    for (int j = 0; j < AX_K / AX_B; j += 2) {
+#pragma unroll
+      for (int u = 0; u < AX_B; u++) {
+        yb[u] = ys[((j + 1) * AX_B + u) * 64];
+        tb[u] = ts[(j + 1) * AX_B + u];
+      }
+      double q[AX_B];
+#pragma unroll
+      for (int u = 0; u < AX_B; u++) q[u] = rankmu_quot<kMarkstein>(ta[u], ya[u], s2, y);
+#pragma unroll
+      for (int u = 0; u < AX_B; u++) c += q[u];
+      if (j + 2 < AX_K / AX_B) {
+#pragma unroll
+        for (int u = 0; u < AX_B; u++) {
+          ya[u] = ys[((j + 2) * AX_B + u) * 64];
+          ta[u] = ts[(j + 2) * AX_B + u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < AX_B; u++) q[u] = rankmu_quot<kMarkstein>(tb[u], yb[u], s2, y);
+#pragma unroll
+      for (int u = 0; u < AX_B; u++) c += q[u];
+    }
+  } else {
+    for (int u = 0; u < cnt; u++) c = rankmu_term<kMarkstein>(c, ts[u], ys[u * 64], s2, y);
+  }
+  return c;
+}
+template <bool kMarkstein>
+__device__ __forceinline__ double rankmu_rows(double c, const double *__restrict__ Yc, const double *__restrict__ Tt,
+                                              int N, int mu, int d0, int e0, int wid, int lane, double s2, double y,
+                                              double (*Ys)[AX_K][64], double (*Ts)[4][AX_K]) {
+  const int tid = threadIdx.x;
+  // staging: thread t loads Yc[k0 + t/16 + 16 j][e0 + 4 (t%16) .. +3] for
+  // j < 4 (16-B vector loads), and T[d0 + t/64][k0 + t%64]
+  const int kr = tid >> 4, ec = (tid & 15) * 4;
+  double2 yv[4][2];
+  double tv = 0.0;
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = k0 + kr + 16 * j;
+      const double *src = Yc + (size_t)(k < mu ? k : mu - 1) * N + e0 + ec;  // clamped rows are never summed
+      if ((N & 1) == 0 && e0 + ec + 3 < N) {  // 16-B aligned rows
+        yv[j][0] = *(const double2 *)src;
+        yv[j][1] = *(const double2 *)(src + 2);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) ((double *)&yv[j][0])[q] = (e0 + ec + q < N) ? src[q] : 0.0;
+      }
+    }
+    const int dr = d0 + (tid >> 6), kk = k0 + (tid & 63);
+    tv = (dr < N && kk < mu) ? Tt[(size_t)dr * mu + kk] : 0.0;
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      double *dst = &Ys[buf][kr + 16 * j][ec];
+      *(double2 *)dst = yv[j][0];
+      *(double2 *)(dst + 2) = yv[j][1];
+    }
+    Ts[buf][tid >> 6][tid & 63] = tv;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < mu; k0 += AX_K) {
+    const bool more = k0 + AX_K < mu;
+    if (more) load(k0 + AX_K);  // in flight during the chunk below
+    c = rankmu_chunk<kMarkstein>(c, &Ys[buf][0][lane], &Ts[buf][wid][0], min(AX_K, mu - k0), s2, y);
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  return c;
+}
+
+__global__ void __launch_bounds__(256) k_adaptC_exact2(int N, int mu, int diagonal, const double *__restrict__ Yc,
+                                                       const double *__restrict__ Tt,
+                                                       const double *__restrict__ pc, double *C,
+                                                       const CmaesScalars *__restrict__ sc) {
+  __shared__ __attribute__((aligned(16))) double Ys[2][AX_K][64];
+  __shared__ double Ts[2][4][AX_K];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int d0 = blockIdx.x * 4, e0 = blockIdx.y * 64;
+  if (e0 > d0 + 3) return;  // workgroup-uniform: entirely above the diagonal
+  const int d = d0 + wid, e = e0 + lane;
+  const bool active = d < N && e < N && e <= d && (!diagonal || e == d);
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double s2 = sc->sigma * sc->sigma;
+  double c = 0.0;
+  if (active) {
+    const double Cde = C[(size_t)d * N + e];
+    c = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  }
+  const int ex = (int)((__double_as_longlong(s2) >> 52) & 0x7ff) - 1023;
+  if (__builtin_amdgcn_readfirstlane((int)(sc->rmuOutOfRange == 0u && ex >= -100 && ex <= 100)))
+    c = rankmu_rows<true>(c, Yc, Tt, N, mu, d0, e0, wid, lane, s2, 1.0 / s2, Ys, Ts);
+  else
+    c = rankmu_rows<false>(c, Yc, Tt, N, mu, d0, e0, wid, lane, s2, 0.0, Ys, Ts);
+  if (active) {
+    C[(size_t)d * N + e] = c;
+    if (e < d) C[(size_t)e * N + d] = c;
+  }
 }
 
 // mean :603-609 and mean update :623-624.  The sum over the μ selected rows
@@ -983,6 +1188,7 @@ struct kg_cmaes_s {
   unsigned *sortVal = nullptr;
   CmaesScalars *sc = nullptr;
   double *covPart = nullptr, *Y = nullptr;
+  double *Yc = nullptr, *Tt = nullptr;  // exact rank-mu factors (k_rankmu_prep)
   EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
@@ -1221,6 +1427,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
   rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
   rc |= dalloc(&h->Y, (size_t)h->mu * N);
+  if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->mu * N) | dalloc(&h->Tt, (size_t)h->mu * N);
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
   rc |= dalloc(&h->infeas, rows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
@@ -1298,7 +1505,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->meanUpdate, (void *)h->auxBDZ, (void *)h->lb, (void *)h->ub, (void *)h->iv,
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
                   (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
-                  (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y,
+                  (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y, (void *)h->Yc, (void *)h->Tt,
                   (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
@@ -1474,17 +1681,21 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                        h->sc);
     hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y, h->mean,
                        h->prevMean);
+    // the rank-mu sum (MFMA) or its exact factors need only Y, the weights
+    // and m_prev: they run on the second stream while the mean and the
+    // evolution paths are computed
+    KG_HIP(hipEventRecord(h->evY, h->stream));
+    KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
     if (h->cfg.cov_mode == KG_COV_MFMA) {
-      // the rank-mu sum needs only Y, the weights and m_prev: it runs on the
-      // second stream while the mean and the evolution paths are computed
       const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
-      KG_HIP(hipEventRecord(h->evY, h->stream));
-      KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
       hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream2, N, mu, h->kslices, h->Y,
                          h->idx, h->w, h->prevMean, h->sc, h->covPart);
-      KG_HIP(hipGetLastError());
-      KG_HIP(hipEventRecord(h->evC, h->stream2));
+    } else {
+      hipLaunchKernelGGL(k_rankmu_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0,
+                         h->stream2, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
     }
+    KG_HIP(hipGetLastError());
+    KG_HIP(hipEventRecord(h->evC, h->stream2));
     hipLaunchKernelGGL(k_mean, dim3((N + MN_D - 1) / MN_D), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
                        h->prevMean, h->meanUpdate, h->sc);
     if (cmaes_paths(h, generation)) return 1;
@@ -1497,8 +1708,9 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
       hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
-      hipLaunchKernelGGL(k_adaptC_exact, dim3(ntiles), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
-                         h->Y, h->idx, h->w, h->prevMean, h->pc, h->C, h->sc);
+      KG_HIP(hipStreamWaitEvent(h->stream, h->evC, 0));
+      hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
+                         h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
     }
     KG_HIP(hipGetLastError());
   }
