@@ -1786,9 +1786,9 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
             "%llu x-gather %llu xv-stage %llu xv-chain %llu alpha %llu pivot-poll %llu update %llu\n"
             "[korali_amd streamed apply] batches %llu steps-before-chase-done %llu ticks-to-first-batch %llu\n"
             "[korali_amd one-workgroup tridiag] householder %llu barrier %llu dsymv %llu xv %llu x-update %llu "
-            "pivot-update %llu chain-w0 %llu chain-w3 %llu (A: dnrm2 %llu scalars %llu)\n",
+            "pivot-update %llu chain-w0 %llu chain-w3 %llu (A: dnrm2 %llu [of which pre-chain %llu] scalars %llu)\n",
             t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7], t[16], t[17], t[18], t[19], t[20], t[21],
-            t[22], t[23], t[24], t[25], t[26], t[27], t[28], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15], t[29], t[30]);
+            t[22], t[23], t[24], t[25], t[26], t[27], t[28], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15], t[29], t[31], t[30]);
   }
   return check_errors(h);
 }

@@ -114,6 +114,33 @@ __host__ __device__ double hypot_fdlibm(double x, double y) {
   return w;
 }
 
+// hypot_fdlibm for the device's Householder step: the same arithmetic on
+// fdlibm's common path (no range rescaling needed: both high words in
+// [0x20b00000, 0x5f300000]) with both of its final formulas formed and one
+// selected, so no divergent branches sit on the critical path; anything
+// else falls back to hypot_fdlibm.
+__device__ __forceinline__ double hypot_fast(double x, double y) {
+  int32_t ha = (int32_t)(hiw(x) & 0x7fffffff), hb = (int32_t)(hiw(y) & 0x7fffffff);
+  const bool sw = hb > ha;
+  double a = sw ? y : x, b = sw ? x : y;
+  const int32_t h1 = sw ? hb : ha, h2 = sw ? ha : hb;
+  ha = h1;
+  hb = h2;
+  a = sethi(a, (uint32_t)ha);
+  b = sethi(b, (uint32_t)hb);
+  const bool common = (ha - hb) <= 0x3c00000 && ha <= 0x5f300000 && hb >= 0x20b00000;
+  if (!__builtin_amdgcn_readfirstlane((int)common)) return hypot_fdlibm(x, y);
+  const double w = a - b;
+  // w > b
+  const double t1a = sethi(0.0, (uint32_t)ha), t2a = a - t1a;
+  const double ra = t1a * t1a - (b * (-b) - t2a * (a + t1a));
+  // w <= b
+  const double a2 = a + a, y1 = sethi(0.0, (uint32_t)hb), y2 = b - y1;
+  const double t1b = sethi(0.0, (uint32_t)(ha + 0x00100000)), t2b = a2 - t1b;
+  const double rb = t1b * y1 - (w * (-w) - (t1b * y2 + t2b * b));
+  return sqrt(w > b ? ra : rb);
+}
+
 constexpr double EPS = 2.2204460492503131e-16;
 constexpr double DMIN = 2.2250738585072014e-308;
 
@@ -234,6 +261,34 @@ __device__ __forceinline__ double wave_prefix_max_nonneg(double x) {
   x = fmax(x, dpp_d<0x142, 0xa>(x));
   x = fmax(x, dpp_d<0x143, 0xc>(x));
   return x;
+}
+
+// v_max_f64 without the canonicalising self-max the compiler adds to fmax
+// (the operands here are |x| of finite values or 0.0, never NaN)
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// wave_prefix_max_nonneg of two independent vectors, level by level (the
+// two dependency chains interleave)
+__device__ __forceinline__ void wave_prefix_max2_nonneg(double x, double y, double &px, double &py) {
+#define KG_PM2(CTRL, RM)                   \
+  {                                        \
+    const double dx = dpp_d<CTRL, RM>(x);  \
+    const double dy = dpp_d<CTRL, RM>(y);  \
+    x = vmax_f64(x, dx);                   \
+    y = vmax_f64(y, dy);                   \
+  }
+  KG_PM2(0x111, 0xf)
+  KG_PM2(0x112, 0xf)
+  KG_PM2(0x114, 0xf)
+  KG_PM2(0x118, 0xf)
+  KG_PM2(0x142, 0xa)
+  KG_PM2(0x143, 0xc)
+#undef KG_PM2
+  px = x;
+  py = y;
 }
 
 // gslcblas dnrm2 of m elements x[k*stride], k < m, by one wave (every lane
@@ -1124,6 +1179,851 @@ __global__ void __launch_bounds__(T1_TPB) k_tridiag_1wg(int N, const double *__r
   }
 }
 
+// ------------------------------------------------------------------------
+// Phase A in ONE workgroup, version 2 (the default for N <= 128): the
+// trailing block is stored as its STRICTLY UPPER triangle (zeros on and
+// below the diagonal; the diagonal lives in its own vector).  Then every
+// gslcblas dsymv chain walks a zero-padded sequence without any lane mask:
+//   descending (rows r, lockstep over columns c = N-1, N-2, ...):
+//     acc_r += tv_c M[r][c]   — M[r][c] = 0 for c <= r adds +-0.0 to an
+//     accumulator that started at +0.0 and so is never -0.0: unchanged
+//   ascending (c = i+1, i+2, ...): t2_r += v_c M[c][r]  (M[c][r] = m[r][c]
+//     for c < r by symmetry, 0 for c >= r)
+// and the rank-2 update touches only the upper triangle and the diagonal
+// (half of the full symmetric update).  Both chain reads are conflict-free
+// (a column walk over rows of stride N+1, a row walk over consecutive r);
+// the vector operand is a broadcast.  dnrm2's ssq chain takes its rare
+// rescaling steps (a new running maximum) through scalar branches, so the
+// common step is one dependent add.  Operation order is the reference's
+// throughout, so the result is bit-identical to
+// k_tridiag_1wg and the oracle.
+constexpr int T2_TPB = 1024, T2_VP = 16;  // T2_VP: pad before / after each vector (chain read-ahead)
+__host__ __device__ inline size_t t2_vec(int N) { return (size_t)N + 2 * T2_VP; }
+__host__ __device__ inline size_t t2_lds_doubles(int N) {
+  // M | dg | vA[2] | tvA[2] | xA[2] | xd | t2 | sv (192) | scal
+  return (size_t)N * (N + 1) + 9 * t2_vec(N) + 192 + 16;
+}
+bool t2_fits(int N) { return N >= 3 && N <= 128 && t2_lds_doubles(N) * sizeof(double) <= 160 * 1024; }
+
+// s_waitcnt lgkmcnt(K) alone (vmcnt / expcnt left at their maxima).  An
+// explicit wait satisfies the compiler's own wait insertion for every LDS
+// load it covers, so a batch of adds that follows waits once, not per
+// value (a wait per dependent add costs ~4 cycles of the ~8 of the add).
+#define KG_WAIT_LGKM(K) __builtin_amdgcn_s_waitcnt(0xC07F | ((K) << 8))
+
+// acc = 0 + sum_{t < T} w[S t] m[S t ms] in order (T wave-uniform); the next
+// 8 steps' operands are read while the current 8 are multiplied and added
+// (two register sets, roles alternating).  Scheduling barriers keep the
+// read-ahead where it is written and one explicit wait per batch replaces
+// the compiler's wait per operand (KG_WAIT_LGKM: the compiler still adds a
+// wait for anything the explicit one does not cover, so the count only
+// tunes speed, never correctness).  Reads run at most 8 steps past T (in
+// bounds by the LDS layout) and are not added.
+#define KG_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+template <int S>
+__device__ __forceinline__ double lockstep_chain(const double *w, const double *m, int ms, int T_) {
+  const int T = __builtin_amdgcn_readfirstlane(T_);
+  double acc = 0.0;
+  double wa[8], ma[8], wb[8], mb[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    wa[u] = w[S * u];
+    ma[u] = m[S * u * ms];
+  }
+  int t = 0;
+  for (; t + 16 <= T; t += 16) {
+    const double *wt = w + S * (t + 8), *mt = m + S * (t + 8) * ms;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      wb[u] = wt[S * u];
+      mb[u] = mt[S * u * ms];
+    }
+    KG_SCHED_FENCE();
+    KG_WAIT_LGKM(12);
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += wa[u] * ma[u];
+    KG_SCHED_FENCE();
+    wt = w + S * (t + 16);
+    mt = m + S * (t + 16) * ms;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      wa[u] = wt[S * u];
+      ma[u] = mt[S * u * ms];
+    }
+    KG_SCHED_FENCE();
+    KG_WAIT_LGKM(12);
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += wb[u] * mb[u];
+    KG_SCHED_FENCE();
+  }
+  if (t + 8 <= T) {
+    const double *wt = w + S * (t + 8), *mt = m + S * (t + 8) * ms;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      wb[u] = wt[S * u];
+      mb[u] = mt[S * u * ms];
+    }
+    KG_SCHED_FENCE();
+    KG_WAIT_LGKM(12);
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += wa[u] * ma[u];
+    t += 8;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (t + u < T) acc += wb[u] * mb[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (t + u < T) acc += wa[u] * ma[u];
+  }
+  return acc;
+}
+
+// ordered add-only chain acc + x_0 + ... + x_{cnt-1} over values held one
+// per lane (x_e in lane e of v0 for e < 64, of v1 for e >= 64; cnt <= 128),
+// each read into scalar registers with v_readlane (no LDS traffic); every
+// lane returns the sum
+__device__ __forceinline__ double lane_sum(double acc, double v0, double v1, int cnt_) {
+  const int cnt = __builtin_amdgcn_readfirstlane(cnt_);
+  const long long b0 = __double_as_longlong(v0), b1 = __double_as_longlong(v1);
+  const int l0 = (int)b0, h0 = (int)(b0 >> 32), l1 = (int)b1, h1 = (int)(b1 >> 32);
+#define KG_LANE_STEP(L, H, E)                                                                        \
+  acc += __longlong_as_double(((long long)__builtin_amdgcn_readlane(H, E) << 32) |                    \
+                              (unsigned int)__builtin_amdgcn_readlane(L, E))
+  int e = 0;
+  for (; e + 8 <= min(cnt, 64); e += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) KG_LANE_STEP(l0, h0, e + u);
+  }
+  for (; e < min(cnt, 64); e++) KG_LANE_STEP(l0, h0, e);
+  for (; e + 8 <= cnt; e += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) KG_LANE_STEP(l1, h1, e - 64 + u);
+  }
+  for (; e < cnt; e++) KG_LANE_STEP(l1, h1, e - 64);
+#undef KG_LANE_STEP
+  return acc;
+}
+
+
+// staged_sum reading pairs with 16-byte LDS loads (p 16-byte aligned): the
+// next 8 values are in flight (4 loads) while the current 8 are added after
+// ONE wait
+__device__ __forceinline__ double staged_sum_v2(double acc, const double *p, int cnt_) {
+  const int cnt = __builtin_amdgcn_readfirstlane(cnt_);
+  const double2 *q2 = (const double2 *)p;
+  double2 a[4], b[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) a[u] = q2[u];
+  int q = 0;
+  for (; q + 16 <= cnt; q += 16) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) b[u] = q2[(q >> 1) + 4 + u];
+    KG_WAIT_LGKM(4);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      acc += a[u].x;
+      acc += a[u].y;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) a[u] = q2[(q >> 1) + 8 + u];
+    KG_WAIT_LGKM(4);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      acc += b[u].x;
+      acc += b[u].y;
+    }
+  }
+  if (q + 8 <= cnt) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) b[u] = q2[(q >> 1) + 4 + u];
+    KG_WAIT_LGKM(4);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      acc += a[u].x;
+      acc += a[u].y;
+    }
+    q += 8;
+    KG_WAIT_LGKM(0);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (q + 2 * u < cnt) acc += b[u].x;
+      if (q + 2 * u + 1 < cnt) acc += b[u].y;
+    }
+  } else {
+    KG_WAIT_LGKM(0);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (q + 2 * u < cnt) acc += a[u].x;
+      if (q + 2 * u + 1 < cnt) acc += a[u].y;
+    }
+  }
+  return acc;
+}
+
+// acc + p[0] + ... + p[cnt-1] (p an LDS address, wave-uniform; 0 <= cnt
+// <= 128) as ONE straight-line inline-assembly sequence: the next 8 values
+// are in flight (8 ds_read_b64) while the current 8 are added after a
+// single counted wait; the only branches are forward exits to the tail.
+// (Compiled code waits before every add and hoists the loads next to their
+// uses, ~15 cycles per element; a dependent FP64 add is 8.3, an LDS-fed
+// add chain waiting once per 8 values 10.6 — tools/ubench_issue.hip.)
+// Reads run up to 16 values past cnt (callers pad) and are not added.
+__device__ __forceinline__ double lds_chain_add(double acc, const double *p, int cnt) {
+  const unsigned va = (unsigned)(size_t)(const __attribute__((address_space(3))) double *)p;
+  int rem = __builtin_amdgcn_readfirstlane(cnt);
+  double a[8], b[8];
+  asm volatile(
+"ds_read_b64 %[a0], %[va] offset:0\n"
+"ds_read_b64 %[a1], %[va] offset:8\n"
+"ds_read_b64 %[a2], %[va] offset:16\n"
+"ds_read_b64 %[a3], %[va] offset:24\n"
+"ds_read_b64 %[a4], %[va] offset:32\n"
+"ds_read_b64 %[a5], %[va] offset:40\n"
+"ds_read_b64 %[a6], %[va] offset:48\n"
+"ds_read_b64 %[a7], %[va] offset:56\n"
+"ds_read_b64 %[b0], %[va] offset:64\n"
+"ds_read_b64 %[b1], %[va] offset:72\n"
+"ds_read_b64 %[b2], %[va] offset:80\n"
+"ds_read_b64 %[b3], %[va] offset:88\n"
+"ds_read_b64 %[b4], %[va] offset:96\n"
+"ds_read_b64 %[b5], %[va] offset:104\n"
+"ds_read_b64 %[b6], %[va] offset:112\n"
+"ds_read_b64 %[b7], %[va] offset:120\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:128\n"
+"ds_read_b64 %[a1], %[va] offset:136\n"
+"ds_read_b64 %[a2], %[va] offset:144\n"
+"ds_read_b64 %[a3], %[va] offset:152\n"
+"ds_read_b64 %[a4], %[va] offset:160\n"
+"ds_read_b64 %[a5], %[va] offset:168\n"
+"ds_read_b64 %[a6], %[va] offset:176\n"
+"ds_read_b64 %[a7], %[va] offset:184\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:192\n"
+"ds_read_b64 %[b1], %[va] offset:200\n"
+"ds_read_b64 %[b2], %[va] offset:208\n"
+"ds_read_b64 %[b3], %[va] offset:216\n"
+"ds_read_b64 %[b4], %[va] offset:224\n"
+"ds_read_b64 %[b5], %[va] offset:232\n"
+"ds_read_b64 %[b6], %[va] offset:240\n"
+"ds_read_b64 %[b7], %[va] offset:248\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:256\n"
+"ds_read_b64 %[a1], %[va] offset:264\n"
+"ds_read_b64 %[a2], %[va] offset:272\n"
+"ds_read_b64 %[a3], %[va] offset:280\n"
+"ds_read_b64 %[a4], %[va] offset:288\n"
+"ds_read_b64 %[a5], %[va] offset:296\n"
+"ds_read_b64 %[a6], %[va] offset:304\n"
+"ds_read_b64 %[a7], %[va] offset:312\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:320\n"
+"ds_read_b64 %[b1], %[va] offset:328\n"
+"ds_read_b64 %[b2], %[va] offset:336\n"
+"ds_read_b64 %[b3], %[va] offset:344\n"
+"ds_read_b64 %[b4], %[va] offset:352\n"
+"ds_read_b64 %[b5], %[va] offset:360\n"
+"ds_read_b64 %[b6], %[va] offset:368\n"
+"ds_read_b64 %[b7], %[va] offset:376\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:384\n"
+"ds_read_b64 %[a1], %[va] offset:392\n"
+"ds_read_b64 %[a2], %[va] offset:400\n"
+"ds_read_b64 %[a3], %[va] offset:408\n"
+"ds_read_b64 %[a4], %[va] offset:416\n"
+"ds_read_b64 %[a5], %[va] offset:424\n"
+"ds_read_b64 %[a6], %[va] offset:432\n"
+"ds_read_b64 %[a7], %[va] offset:440\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:448\n"
+"ds_read_b64 %[b1], %[va] offset:456\n"
+"ds_read_b64 %[b2], %[va] offset:464\n"
+"ds_read_b64 %[b3], %[va] offset:472\n"
+"ds_read_b64 %[b4], %[va] offset:480\n"
+"ds_read_b64 %[b5], %[va] offset:488\n"
+"ds_read_b64 %[b6], %[va] offset:496\n"
+"ds_read_b64 %[b7], %[va] offset:504\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:512\n"
+"ds_read_b64 %[a1], %[va] offset:520\n"
+"ds_read_b64 %[a2], %[va] offset:528\n"
+"ds_read_b64 %[a3], %[va] offset:536\n"
+"ds_read_b64 %[a4], %[va] offset:544\n"
+"ds_read_b64 %[a5], %[va] offset:552\n"
+"ds_read_b64 %[a6], %[va] offset:560\n"
+"ds_read_b64 %[a7], %[va] offset:568\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:576\n"
+"ds_read_b64 %[b1], %[va] offset:584\n"
+"ds_read_b64 %[b2], %[va] offset:592\n"
+"ds_read_b64 %[b3], %[va] offset:600\n"
+"ds_read_b64 %[b4], %[va] offset:608\n"
+"ds_read_b64 %[b5], %[va] offset:616\n"
+"ds_read_b64 %[b6], %[va] offset:624\n"
+"ds_read_b64 %[b7], %[va] offset:632\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:640\n"
+"ds_read_b64 %[a1], %[va] offset:648\n"
+"ds_read_b64 %[a2], %[va] offset:656\n"
+"ds_read_b64 %[a3], %[va] offset:664\n"
+"ds_read_b64 %[a4], %[va] offset:672\n"
+"ds_read_b64 %[a5], %[va] offset:680\n"
+"ds_read_b64 %[a6], %[va] offset:688\n"
+"ds_read_b64 %[a7], %[va] offset:696\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:704\n"
+"ds_read_b64 %[b1], %[va] offset:712\n"
+"ds_read_b64 %[b2], %[va] offset:720\n"
+"ds_read_b64 %[b3], %[va] offset:728\n"
+"ds_read_b64 %[b4], %[va] offset:736\n"
+"ds_read_b64 %[b5], %[va] offset:744\n"
+"ds_read_b64 %[b6], %[va] offset:752\n"
+"ds_read_b64 %[b7], %[va] offset:760\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:768\n"
+"ds_read_b64 %[a1], %[va] offset:776\n"
+"ds_read_b64 %[a2], %[va] offset:784\n"
+"ds_read_b64 %[a3], %[va] offset:792\n"
+"ds_read_b64 %[a4], %[va] offset:800\n"
+"ds_read_b64 %[a5], %[va] offset:808\n"
+"ds_read_b64 %[a6], %[va] offset:816\n"
+"ds_read_b64 %[a7], %[va] offset:824\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:832\n"
+"ds_read_b64 %[b1], %[va] offset:840\n"
+"ds_read_b64 %[b2], %[va] offset:848\n"
+"ds_read_b64 %[b3], %[va] offset:856\n"
+"ds_read_b64 %[b4], %[va] offset:864\n"
+"ds_read_b64 %[b5], %[va] offset:872\n"
+"ds_read_b64 %[b6], %[va] offset:880\n"
+"ds_read_b64 %[b7], %[va] offset:888\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:896\n"
+"ds_read_b64 %[a1], %[va] offset:904\n"
+"ds_read_b64 %[a2], %[va] offset:912\n"
+"ds_read_b64 %[a3], %[va] offset:920\n"
+"ds_read_b64 %[a4], %[va] offset:928\n"
+"ds_read_b64 %[a5], %[va] offset:936\n"
+"ds_read_b64 %[a6], %[va] offset:944\n"
+"ds_read_b64 %[a7], %[va] offset:952\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[b0], %[va] offset:960\n"
+"ds_read_b64 %[b1], %[va] offset:968\n"
+"ds_read_b64 %[b2], %[va] offset:976\n"
+"ds_read_b64 %[b3], %[va] offset:984\n"
+"ds_read_b64 %[b4], %[va] offset:992\n"
+"ds_read_b64 %[b5], %[va] offset:1000\n"
+"ds_read_b64 %[b6], %[va] offset:1008\n"
+"ds_read_b64 %[b7], %[va] offset:1016\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 2f\n"
+"v_add_f64 %[acc], %[acc], %[a0]\n"
+"v_add_f64 %[acc], %[acc], %[a1]\n"
+"v_add_f64 %[acc], %[acc], %[a2]\n"
+"v_add_f64 %[acc], %[acc], %[a3]\n"
+"v_add_f64 %[acc], %[acc], %[a4]\n"
+"v_add_f64 %[acc], %[acc], %[a5]\n"
+"v_add_f64 %[acc], %[acc], %[a6]\n"
+"v_add_f64 %[acc], %[acc], %[a7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"ds_read_b64 %[a0], %[va] offset:1024\n"
+"ds_read_b64 %[a1], %[va] offset:1032\n"
+"ds_read_b64 %[a2], %[va] offset:1040\n"
+"ds_read_b64 %[a3], %[va] offset:1048\n"
+"ds_read_b64 %[a4], %[va] offset:1056\n"
+"ds_read_b64 %[a5], %[va] offset:1064\n"
+"ds_read_b64 %[a6], %[va] offset:1072\n"
+"ds_read_b64 %[a7], %[va] offset:1080\n"
+"s_waitcnt lgkmcnt(8)\n s_cmp_lt_i32 %[rem], 8\n s_cbranch_scc1 3f\n"
+"v_add_f64 %[acc], %[acc], %[b0]\n"
+"v_add_f64 %[acc], %[acc], %[b1]\n"
+"v_add_f64 %[acc], %[acc], %[b2]\n"
+"v_add_f64 %[acc], %[acc], %[b3]\n"
+"v_add_f64 %[acc], %[acc], %[b4]\n"
+"v_add_f64 %[acc], %[acc], %[b5]\n"
+"v_add_f64 %[acc], %[acc], %[b6]\n"
+"v_add_f64 %[acc], %[acc], %[b7]\n"
+"s_sub_i32 %[rem], %[rem], 8\n"
+"s_branch 9f\n"
+"2:\n"
+"s_cmp_lt_i32 %[rem], 1\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a0]\n"
+"s_cmp_lt_i32 %[rem], 2\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a1]\n"
+"s_cmp_lt_i32 %[rem], 3\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a2]\n"
+"s_cmp_lt_i32 %[rem], 4\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a3]\n"
+"s_cmp_lt_i32 %[rem], 5\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a4]\n"
+"s_cmp_lt_i32 %[rem], 6\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a5]\n"
+"s_cmp_lt_i32 %[rem], 7\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[a6]\n"
+"s_branch 9f\n"
+"3:\n"
+"s_cmp_lt_i32 %[rem], 1\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b0]\n"
+"s_cmp_lt_i32 %[rem], 2\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b1]\n"
+"s_cmp_lt_i32 %[rem], 3\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b2]\n"
+"s_cmp_lt_i32 %[rem], 4\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b3]\n"
+"s_cmp_lt_i32 %[rem], 5\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b4]\n"
+"s_cmp_lt_i32 %[rem], 6\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b5]\n"
+"s_cmp_lt_i32 %[rem], 7\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b6]\n"
+"9:\n s_waitcnt lgkmcnt(0)\n"
+      : [acc] "+v"(acc), [rem] "+s"(rem), [a0] "=&v"(a[0]), [a1] "=&v"(a[1]), [a2] "=&v"(a[2]), [a3] "=&v"(a[3]), [a4] "=&v"(a[4]), [a5] "=&v"(a[5]), [a6] "=&v"(a[6]), [a7] "=&v"(a[7]), [b0] "=&v"(b[0]), [b1] "=&v"(b[1]), [b2] "=&v"(b[2]), [b3] "=&v"(b[3]), [b4] "=&v"(b[4]), [b5] "=&v"(b[5]), [b6] "=&v"(b[6]), [b7] "=&v"(b[7])
+      : [va] "v"(va)
+      : "scc", "memory");
+  return acc;
+}
+
+// staged_sum with the loads 16 ahead: three register sets of 8 rotate
+// (a wait covers only the batch it consumes); reads up to 24 past cnt
+__device__ __forceinline__ double staged_sum3(double acc, const double *p, int cnt_) {
+  const int cnt = __builtin_amdgcn_readfirstlane(cnt_);
+  double a[8], b[8], c[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    a[u] = p[u];
+    b[u] = p[8 + u];
+  }
+  int q = 0;
+  for (; q + 24 <= cnt; q += 24) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) c[u] = p[q + 16 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = p[q + 24 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += b[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = p[q + 32 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += c[u];
+  }
+  // tail: fewer than 24 left; a holds q..q+7, b holds q+8..q+15
+#pragma unroll
+  for (int u = 0; u < 8; u++)
+    if (q + u < cnt) acc += a[u];
+#pragma unroll
+  for (int u = 0; u < 8; u++)
+    if (q + 8 + u < cnt) acc += b[u];
+  if (q + 16 < cnt) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) c[u] = p[q + 16 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + 16 + u < cnt) acc += c[u];
+  }
+  return acc;
+}
+
+// ordered add-only chain acc + p[0] + ... + p[cnt-1] over LDS values, 8
+// loaded ahead (reads up to 8 past cnt, not added)
+__device__ __forceinline__ double staged_sum(double acc, const double *p, int cnt_) {
+  const int cnt = __builtin_amdgcn_readfirstlane(cnt_);
+  double a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) a[u] = p[u];
+  int q = 0;
+  for (; q + 16 <= cnt; q += 16) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = p[q + 8 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = p[q + 16 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += b[u];
+  }
+  if (q + 8 <= cnt) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = p[q + 8 + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += a[u];
+    q += 8;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += b[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q + u < cnt) acc += a[u];
+  }
+  return acc;
+}
+
+// rescale flags of the 8 addends e .. e+7 (e a multiple of 8)
+__device__ __forceinline__ unsigned nrm2_bits(unsigned long long k0, unsigned long long k1, int e) {
+  return (unsigned)(((e < 64) ? (k0 >> e) : (k1 >> (e - 64))) & 0xffULL);
+}
+// 8 steps of dnrm2's ssq recurrence: ssq += t (plain) or ssq = 1 + ssq t t
+// (a new running maximum, rare: taken through scalar branches so the plain
+// step stays one dependent add)
+__device__ __forceinline__ double nrm2_batch(double ssq, const double (&t)[8], unsigned bits) {
+  if (bits == 0u) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) ssq += t[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if ((bits >> u) & 1u) {
+        __asm__ volatile("" ::: "memory");
+        ssq = 1.0 + ssq * t[u] * t[u];
+      } else {
+        ssq += t[u];
+      }
+    }
+  }
+  return ssq;
+}
+
+// gslcblas dnrm2 of m <= 128 elements held in registers (element e = lane in
+// x0, e = 64 + lane in x1; only e < m are read), by one wave; every lane
+// returns the result.  Addends staged in sv (m rounded up to 8, zero-padded:
+// +0.0 leaves ssq >= 1 unchanged).
+__device__ double dnrm2_regs(double x0, double x1, int m, double *sv, bool tr, unsigned long long *tacc,
+                             unsigned long long &tm) {
+  const int lane = threadIdx.x & 63;
+  const int m8 = (m + 7) & ~7;
+  const int e0 = lane, e1 = lane + 64;
+  const double a0 = e0 < m ? fabs(x0) : 0.0, a1 = e1 < m ? fabs(x1) : 0.0;
+  double pm0, pm1;
+  wave_prefix_max2_nonneg(a0, a1, pm0, pm1);
+  const double c0 = readlane_d(pm0, 63);
+  const double b0 = dpp_d<0x138, 0xf>(pm0);            // running max before e0 (lane 0: 0.0)
+  const double b1 = fmax(dpp_d<0x138, 0xf>(pm1), c0);  // before e1
+  const bool z0 = a0 != 0.0, z1 = a1 != 0.0;           // zero elements are skipped by dnrm2
+  const bool n0 = z0 && b0 < a0, n1 = z1 && b1 < a1;   // a new running maximum
+  // one division per element, operands selected (zeros: 0 / 1), no branches
+  const double q0 = (z0 ? (n0 ? b0 : a0) : 0.0) / (z0 ? (n0 ? a0 : b0) : 1.0);
+  const double q1 = (z1 ? (n1 ? b1 : a1) : 0.0) / (z1 ? (n1 ? a1 : b1) : 1.0);
+  const unsigned long long k0 = __ballot(n0), k1 = __ballot(n1);
+  sv[e0] = n0 ? q0 : q0 * q0;  // e >= m: q = 0 (sv holds 192 doubles)
+  sv[e1] = n1 ? q1 : q1 * q1;
+  const double carry = fmax(c0, readlane_d(pm1, 63));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (tr) {
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();
+    tacc[0] += t_ - tm;
+    tm = t_;
+  }
+  // the ssq recurrence in the reference's order: batches of 8 addends, the
+  // next batch loaded while the current one is added (two register sets,
+  // roles alternating: a wait covers only the batch it consumes)
+  double ssq = 1.0;
+  double a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) a[u] = sv[u];
+  for (int e = 0; e < m8; e += 16) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) b[u] = sv[e + 8 + u];  // sv has 64 doubles of slack
+    ssq = nrm2_batch(ssq, a, nrm2_bits(k0, k1, e));
+    if (e + 8 >= m8) break;
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = sv[e + 16 + u];
+    ssq = nrm2_batch(ssq, b, nrm2_bits(k0, k1, e + 8));
+  }
+  __builtin_amdgcn_wave_barrier();
+  return (m == 1) ? fabs(x0) : carry * sqrt(ssq);
+}
+
+__global__ void __launch_bounds__(T2_TPB) k_tridiag_1wg2(int N, const double *__restrict__ C, double *gH,
+                                                         double *tauOut, double *dOut, double *sdOut,
+                                                         unsigned long long *trace) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int lda = N + 1, VS = (int)t2_vec(N);
+  double *M = smem;                       // strictly upper triangle, row r at r*lda
+  double *dg = M + (size_t)N * lda + T2_VP;  // diagonal
+  double *vbase = dg - T2_VP + VS;        // vA[2], tvA[2], xA[2]: absolute column index
+  auto vA = [&](int p) { return vbase + (size_t)p * VS + T2_VP; };
+  auto tvA = [&](int p) { return vbase + (size_t)(2 + p) * VS + T2_VP; };
+  auto xA = [&](int p) { return vbase + (size_t)(4 + p) * VS + T2_VP; };
+  double *xd = vbase + (size_t)6 * VS + T2_VP;  // descending chain + diagonal term, by j
+  double *t2 = xd + VS;                          // ascending chain, by j
+  double *sv = t2 + VS - T2_VP;                  // 192: dnrm2 addends, then the xv products
+  double *scal = sv + 192;                       // 16 scalars
+  const bool tr = trace && tid == 0;
+  unsigned long long tacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+#define T2_MARK(k)                                                \
+  if (tr) {                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    tacc[k] += t_ - tm;                                           \
+    tm = t_;                                                      \
+  }
+  for (size_t idx = tid; idx < t2_lds_doubles(N); idx += nt) smem[idx] = 0.0;
+  __syncthreads();
+  // symmetrise from the lower triangle (CMAES.cpp.base:908-913): upper
+  // element (r, c > r) = C[c][r]; diagonal C[r][r]
+  for (int idx = tid; idx < N * N; idx += nt) {
+    const int r = idx / N, c = idx % N;
+    if (c > r) M[(size_t)r * lda + c] = C[(size_t)c * N + r];
+    else if (c == r) dg[r] = C[(size_t)r * N + r];
+  }
+  __syncthreads();
+  for (int i = 0; i + 2 < N; i++) {
+    const int n = N - i - 1, par = i & 1;
+    double *va = vA(par), *tva = tvA(par), *xa = xA(par);
+    // ---- A (wave 0): Householder vector of pivot row i; alpha = M[i][i+1],
+    // dnrm2 over x_e = M[i][i+2+e], e < n-1
+    if (wid == 0) {
+      const double *prow = M + (size_t)i * lda;
+      const int m = n - 1;
+      const double alpha = prow[i + 1];
+      const double x0 = prow[i + 2 + min(lane, m - 1)], x1 = prow[i + 2 + min(lane + 64, m - 1)];
+      const double xnorm = dnrm2_regs(x0, x1, m, sv, tr, tacc + 8, tm);
+      T2_MARK(6)
+      double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
+      int branch = 0;
+      if (xnorm != 0) {
+        beta = -(alpha >= 0.0 ? 1.0 : -1.0) * hypot_fast(alpha, xnorm);
+        const double sgap = alpha - beta;
+        const bool big = fabs(sgap) > DMIN;
+        tau_i = (beta - alpha) / beta;
+        f1 = (big ? 1.0 : EPS) / sgap;  // independent of tau: both divisions in flight
+        f2 = big ? 1.0 : 1.0 / EPS;
+        branch = big ? 1 : 2;
+      }
+      const double v0out = branch ? beta : alpha;
+      T2_MARK(7)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int e = lane + 64 * h;
+        if (e < m) {
+          double t = h ? x1 : x0;
+          if (branch != 0) {
+            t = t * f1;
+            if (branch == 2) t = t * f2;
+          }
+          gH[(size_t)i * N + 1 + e] = t;
+          va[i + 2 + e] = t;
+          tva[i + 2 + e] = tau_i * t;
+        }
+      }
+      if (lane == 0) {
+        gH[(size_t)i * N] = v0out;
+        va[i + 1] = 1.0;
+        tva[i + 1] = tau_i * 1.0;
+        scal[0] = tau_i;
+        tauOut[i] = tau_i;
+        sdOut[i] = v0out;
+      }
+    }
+    T2_MARK(0)
+    __syncthreads();
+    T2_MARK(1)
+    const double tau_i = scal[0];
+    if (tau_i == 0.0) continue;  // no update this step (uniform)
+    // ---- E: dsymv chains, lockstep over columns; wave 0/1 descending for
+    // rows j < 64 / j >= 64, wave 2/3 ascending (row r = i+1+j)
+    if (wid < 4) {
+      const int h = wid & 1, j = lane + 64 * h;
+      const bool valid = j < n;
+      const int r = valid ? i + 1 + j : N - 1;  // invalid lanes walk a zero row / discard
+      if (wid < 2) {
+        // c = N-1 down to r+1, then the diagonal term: T = n-1-jmin steps
+        const double acc = lockstep_chain<-1>(tva + (N - 1), M + (size_t)r * lda + (N - 1), 1, max(0, n - 1 - 64 * h));
+        if (valid) xd[j] = acc + tva[r] * dg[r];
+      } else {
+        // c = i+1 up to r-1: T = largest j of the wave
+        const double acc =
+            lockstep_chain<1>(va + (i + 1), M + (size_t)(i + 1) * lda + r, lda, 64 * h < n ? min(n, 64 * h + 64) - 1 : 0);
+        if (valid) t2[j] = acc;
+      }
+    }
+    T2_MARK(2)
+    __syncthreads();
+    T2_MARK(3)
+    // ---- G, I, K (wave 0): x = xd + tau t2 and the xv products, the xv
+    // chain, alpha = -(tau/2) xv, x += alpha v
+    if (wid == 0) {
+      double xr[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int j = lane + 64 * h;
+        xr[h] = 0.0;
+        if (j < n) {
+          xr[h] = xd[j] + tau_i * t2[j];
+          sv[j] = xr[h] * va[i + 1 + j];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double alpha = -(tau_i / 2.0) * lds_chain_add(0.0, sv, n);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int j = lane + 64 * h;
+        if (j < n) xa[i + 1 + j] = xr[h] + alpha * va[i + 1 + j];
+      }
+    }
+    T2_MARK(4)
+    __syncthreads();
+    // ---- M: rank-2 update of the upper triangle and the diagonal; wave 0
+    // updates the next pivot row (i+1) and goes straight on to its dnrm2
+    const int r1 = i + 1;
+    if (wid == 0) {
+      const double nvr = -1.0 * va[r1], nxr = -1.0 * xa[r1];
+      double *row = M + (size_t)r1 * lda;
+      for (int c = r1 + 1 + lane; c < N; c += 64) row[c] += nvr * xa[c] + nxr * va[c];
+      if (lane == 0) dg[r1] += nvr * xa[r1] + nxr * va[r1];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      // rows r = i+2+jr (jr < n-1) over waves 1..15; lane's columns c = r+1+lane, r+65+lane
+      for (int jr = wid - 1; jr < n - 1; jr += 15) {
+        const int r = r1 + 1 + jr;
+        const double nvr = -1.0 * va[r], nxr = -1.0 * xa[r];
+        double *row = M + (size_t)r * lda;
+        for (int c = r + 1 + lane; c < N; c += 64) row[c] += nvr * xa[c] + nxr * va[c];
+      }
+      // diagonal entries of rows i+2.. (threads 64 .. 64+n-2)
+      const int q = tid - 64;
+      if (q < n - 1) {
+        const int r = r1 + 1 + q;
+        const double nvr = -1.0 * va[r], nxr = -1.0 * xa[r];
+        dg[r] += nvr * xa[r] + nxr * va[r];
+      }
+    }
+    T2_MARK(5)
+  }
+  __syncthreads();
+#undef T2_MARK
+  if (tr) {
+    for (int k = 0; k < 6; k++) trace[8 + k] += tacc[k];
+    trace[29] += tacc[6];
+    trace[30] += tacc[7];
+    trace[31] += tacc[8];
+  }
+  for (int r = tid; r < N; r += nt) {
+    dOut[r] = dg[r];
+    if (r == N - 2) sdOut[r] = M[(size_t)r * lda + r + 1];
+  }
+}
+
 // Phase B for N > 128: the columns of Q are independent under
 // householder_hm, so workgroups own UMW_COLS columns each (Q^T rows in LDS)
 // and apply all reflectors without talking to each other; the next
@@ -1874,10 +2774,11 @@ int EigenSolver::init(int N_, bool hostChase_) {
   // tridiagonalisation: one workgroup with the whole matrix in LDS while it
   // fits (no in-launch hand-offs), multi-workgroup above;
   // KORALI_AMD_TRIDIAG = lds | 1wg | mw forces one
-  tri = t1_fits(N) ? 1 : (lds ? 0 : 2);
+  tri = t2_fits(N) ? 3 : (t1_fits(N) ? 1 : (lds ? 0 : 2));
   if (const char *e = getenv("KORALI_AMD_TRIDIAG")) {
     if (!strcmp(e, "lds") && eig_use_lds(N)) tri = 0;
     if (!strcmp(e, "1wg") && t1_fits(N)) tri = 1;
+    if (!strcmp(e, "1wg2") && t2_fits(N)) tri = 3;
     if (!strcmp(e, "mw")) tri = 2;
   } else if (getenv("KORALI_AMD_EIGEN_MW_MIN") && !lds) {
     tri = 2;
@@ -1886,6 +2787,9 @@ int EigenSolver::init(int N_, bool hostChase_) {
   if (tri == 1)
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(t1_lds_doubles(N) * sizeof(double))));
+  if (tri == 3)
+    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(t2_lds_doubles(N) * sizeof(double))));
   if (!lds || tri == 2) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1930,7 +2834,10 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
-  if (tri == 1)
+  if (tri == 3)
+    hipLaunchKernelGGL(k_tridiag_1wg2, dim3(1), dim3(T2_TPB), t2_lds_doubles(N) * sizeof(double), s, N, C, gH, tau,
+                       d, sd, trace);
+  else if (tri == 1)
     hipLaunchKernelGGL(k_tridiag_1wg, dim3(1), dim3(T1_TPB), t1_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
                        sd, trace, t1flags);
   else if (tri == 0)
