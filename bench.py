@@ -89,39 +89,79 @@ def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
     return tot, raw
 
 
-def _cmaes_oracle_rate(variant, seconds_budget, max_gens):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+class pinned_core:
+    """Pin the calling process to one core for the CPU-baseline timing
+    (`taskset -c <core>`), restoring the affinity after."""
+
+    def __init__(self):
+        self.saved = os.sched_getaffinity(0)
+        self.core = min(self.saved)
+
+    def __enter__(self):
+        os.sched_setaffinity(0, {self.core})
+        return self.core
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.saved)
+
+
+def _cmaes_oracle_rate(variant, warmup, gens_min, seconds_budget, N=N_VARS, lam=LAMBDA, objective="rosenbrock",
+                       x0=0.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refcpu as R
 
-    o = R.CMAES(N_VARS, LAMBDA, MU, variant=variant)
-    o["Initial Value"] = np.zeros(N_VARS)
-    o["Initial Standard Deviation"] = np.ones(N_VARS)
-    R.lib().kr_rng_seed(o.rng(0).ptr, 1337)
-    R.lib().kr_rng_seed(o.rng(1).ptr, 1338)
-    o.generation(1, "rosenbrock")  # warm-up (includes initialisation)
-    g, t0 = 1, time.perf_counter()
+    R.lib(variant).kr_set_threads(1)  # the reference is single-threaded (no OpenMP in CMAES)
+    o = R.CMAES(N, lam, lam // 2, variant=variant)
+    o["Initial Value"] = np.full(N, x0)
+    o["Initial Standard Deviation"] = np.ones(N)
+    R.lib(variant).kr_rng_seed(o.rng(0).ptr, 1337)
+    R.lib(variant).kr_rng_seed(o.rng(1).ptr, 1338)
+    g = 0
+    for _ in range(warmup):  # warm-up (includes initialisation)
+        g += 1
+        o.generation(g, objective)
+    n, t0 = 0, time.perf_counter()
     while True:
         g += 1
-        o.generation(g, "rosenbrock")
+        n += 1
+        o.generation(g, objective)
         el = time.perf_counter() - t0
-        if el > seconds_budget or g - 1 >= max_gens:
+        if n >= gens_min and el > seconds_budget:
             break
-    return g - 1, el
+        if el > 4 * seconds_budget:  # hard bound on a slow host
+            break
+    return n, el
 
 
-def cpu_baseline(seconds_budget=10.0):
-    """Time the CPU oracle (single thread) on a bounded sample of the same
-    workload.  `value` is the oracle built against the system libm
-    (oracle/librefcpu_libm.so: the speed the reference itself runs at on this
-    host — the conservative baseline); the bit-exact oracle, whose
-    correctly-rounded log/exp are slower, is reported beside it."""
-    gens, el = _cmaes_oracle_rate("libm", seconds_budget, 60)
-    gens_cr, el_cr = _cmaes_oracle_rate("cr", seconds_budget / 2, 20)
+def cpu_baseline(seconds_budget=6.0):
+    """The reference's arithmetic on this host's CPU: the
+    oracle restatement, -O3 without -march, one thread pinned to one core,
+    10 warm-up generations then at least 100 timed generations of C2.
+    `value` is the build against the system libm (the speed the reference
+    itself runs at here — the conservative baseline, variant (i): solver
+    arithmetic with an inline objective, no per-sample dispatch); the
+    bit-exact build (correctly rounded log/exp, slower) is reported beside it
+    on a shorter sample."""
+    with pinned_core() as core:
+        gens, el = _cmaes_oracle_rate("libm", 10, 100, seconds_budget)
+        gens_cr, el_cr = _cmaes_oracle_rate("cr", 2, 10, seconds_budget / 2)
     return {"value": gens / el, "unit": "generations/s", "cores": 1, "kind": "port",
             "samples_per_sec": gens * LAMBDA / el,
             "bit_exact_port_value": gens_cr / el_cr,
-            "sample": f"{gens} generations of C2 (N=128, lambda=4096) after 1 warm-up, oracle/refcpu.c -O2 "
-                      f"with system libm (timing build), 1 thread; bit-exact CR build: {gens_cr} generations"}
+            "cpu": f"{cpu_model()}, 1 of {os.cpu_count()} cores (pinned to core {core})",
+            "sample": f"{gens} generations of C2 (N=128, lambda=4096) after 10 warm-up, oracle/refcpu.c -O3 "
+                      f"(no -march) with system libm, 1 thread, variant (i) inline objective; bit-exact CR build: "
+                      f"{gens_cr} generations after 2 warm-up"}
 
 
 def engine_rate(steps, warmup, cov):
@@ -149,6 +189,7 @@ def engine_rate(steps, warmup, cov):
     e["Preserve Random Number Generator States"] = True
     # each resumed run() re-creates the device handle from the saved state;
     # two runs of different length cancel that fixed cost
+    steps = max(steps, 100)
     short = max(1, steps // 8)
     times = []
     for n in (short, steps):
@@ -164,7 +205,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--cov", default="mfma", choices=["exact", "mfma"])
+    ap.add_argument("--cov", default="exact", choices=["exact", "mfma"],
+                    help="exact (default): bit-exact rank-mu order, the reference's trajectory; mfma: FP64 matrix "
+                         "cores, <= 1e-12 per step (reported beside the exact rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
                     help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192; c4: CMA-ES 512-dim Ackley, "
@@ -243,6 +286,23 @@ def main():
     best = float(dev["Best Ever Value"][0])
     dev.close()
     eng = engine_rate(args.steps, args.warmup, args.cov) if world == 1 else None
+    # the other covariance mode on this rank alone (reported beside `value`)
+    alt = "mfma" if args.cov == "exact" else "exact"
+    adev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
+                       normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=alt,
+                       device=local_rank if world > 1 else 0)
+    g2 = 0
+    for _ in range(args.warmup):
+        g2 += 1
+        adev.generation(g2, "rosenbrock")
+    adev.synchronize()
+    ta = time.perf_counter()
+    for _ in range(args.steps):
+        g2 += 1
+        adev.generation(g2, "rosenbrock")
+    adev.synchronize()
+    alt_rate = args.steps / (time.perf_counter() - ta)
+    adev.close()
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -277,10 +337,14 @@ def main():
                    "parallelism": f"replicas{world}"},
         "samples_per_sec": gens_per_s * LAMBDA,
         "engine_generations_per_sec": eng,
+        f"{alt}_covariance_generations_per_sec_per_gpu": alt_rate,
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
-        "roofline": {"kernel": dominant, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+        "roofline": {"kernel": dominant, "bound": "mfma",
+                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the kernel is a "
+                                   "dependent FP64 VALU chain (GSL operation order), far below it by construction",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_raw_fetch": traffic_raw,
                      "traffic_source": f"profiles/{PROFILE_ROUND}/c2_pmc_traffic.csv" if traffic else None,
@@ -312,30 +376,39 @@ def c3_experiment(seed):
                        uniform_seed=seed + 3, target_cov=1.0, covariance_scaling=0.04)
 
 
-def c3_cpu_baseline(seconds_budget=10.0):
+def c3_cpu_baseline(seconds_budget=30.0):
+    """The whole C3 run (run to completion) on the libm
+    oracle, one thread pinned to one core; the bit-exact build on its first
+    3 generations beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refcpu as R
 
     def rate(variant, budget, max_gens):
+        L = R.lib(variant)
+        L.kr_set_threads(1)
         o = R.TMCMC(C3_N, C3_P, variant=variant)
         o["Prior Minimum"] = [-5.0] * C3_N
         o["Prior Maximum"] = [5.0] * C3_N
         o.set_prior_map([0] * C3_N)
         for i, sd in enumerate([1338, 1339, 1340, 1337]):
-            R.lib().kr_rng_seed(o.rng(i).ptr, sd)
+            L.kr_rng_seed(o.rng(i).ptr, sd)
         g, t0 = 0, time.perf_counter()
         while True:
             g += 1
             o.generation(g)
             el = time.perf_counter() - t0
-            if el > budget or g >= max_gens or o["Annealing Exponent"][0] >= 1.0:
+            # Korali terminates one generation after the exponent reaches 1
+            if el > budget or g >= max_gens or o["Previous Annealing Exponent"][0] >= 1.0:
                 return g, el
 
-    g, el = rate("libm", seconds_budget, 12)
-    gc, elc = rate("cr", seconds_budget / 2, 3)
+    with pinned_core() as core:
+        g, el = rate("libm", seconds_budget, 40)
+        gc, elc = rate("cr", seconds_budget / 4, 3)
     return {"value": g / el, "unit": "generations/s", "cores": 1, "kind": "port", "bit_exact_port_value": gc / elc,
-            "sample": f"first {g} generations of C3 (N=32, P=8192), oracle with system libm (timing build), "
-                      f"1 thread; bit-exact CR build: {gc} generations"}
+            "chain_steps_per_sec": g * C3_P / el,
+            "cpu": f"{cpu_model()}, 1 of {os.cpu_count()} cores (pinned to core {core})",
+            "sample": f"the whole C3 run ({g} generations, N=32, P=8192, to termination), oracle/refcpu.c -O3 with "
+                      f"system libm, 1 thread; bit-exact CR build: first {gc} generations"}
 
 
 def run_c3(args):
@@ -395,7 +468,10 @@ def run_c3(args):
         "chain_steps_per_sec": done * C3_P / elapsed,
         "stage_ms": stages,
         "annealing_search": search,
-        "roofline": {"kernel": dominant, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+        "roofline": {"kernel": dominant, "bound": "mfma",
+                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the kernel is a "
+                                   "dependent FP64 VALU chain (GSL operation order), far below it by construction",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                      "algorithmic_flops_per_launch": flops[dominant], "avg_launch_ms": stages[dominant]},
     }
@@ -406,6 +482,21 @@ def run_c3(args):
 
 # ----------------------------------------------------------------- C4 sharded
 C4_N, C4_L = 512, 65536
+
+
+def c4_cpu_baseline():
+    """Bounded CPU sample for C4: the libm oracle, one pinned thread, N = 512
+    Ackley at lambda = 8192 (one rank's shard at 8 GPUs; a full C4
+    generation takes minutes on one core): 1 warm-up + 1 timed generation,
+    reported as samples/s (comparable with the device's samples_per_sec)."""
+    lam = 8192
+    with pinned_core() as core:
+        gens, el = _cmaes_oracle_rate("libm", 1, 1, 0.0, N=C4_N, lam=lam, objective="ackley", x0=2.0)
+    return {"value": gens * lam / el, "unit": "samples/s", "cores": 1, "kind": "port",
+            "generations_per_sec_at_sample": gens / el,
+            "cpu": f"{cpu_model()}, 1 of {os.cpu_count()} cores (pinned to core {core})",
+            "sample": f"{gens} generation(s) of N=512 Ackley at lambda=8192, mu=4096 (one rank's shard of C4) after "
+                      f"1 warm-up, oracle/refcpu.c -O3 with system libm, 1 thread"}
 
 
 def run_c4(args):
@@ -481,7 +572,8 @@ def run_c4(args):
             "config": {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768 Logarithmic, x0=2, "
                                    "sigma0=1, seed 1337", "parallelism": f"population-shard{world}"},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
-            "stage_ms_rank0": stages, "cpu_baseline": None}), flush=True)
+            "stage_ms_rank0": stages,
+            "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -101,7 +101,14 @@ int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F);
  * is a valid value; NaN and +inf are still rejected.  Ties sort by index. */
 int kg_cmaes_set_log_posterior(kg_cmaes_t h, const double *F);
 int kg_cmaes_update(kg_cmaes_t h, size_t generation);
-/* one whole generation, enqueued asynchronously (no host sync) */
+/* One whole generation (CMAES::runGeneration).  The device work is enqueued
+ * on the handle's stream, but the call itself BLOCKS the calling thread for
+ * part of it: with the default host-side Givens chase (cfg eigen_device_chase = 0)
+ * the thread waits for the generation's tridiagonal form and then runs the
+ * implicit-QR chase itself (kg_eigen.hip EigenSolver::run), streaming the
+ * rotations to the device; the call returns once the chase is done and the
+ * rest of the generation is queued.  With the device chase (eigen_device_chase =
+ * 1, bit-identical, slower) the call only enqueues. */
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective);
 /* Population sharding over shard_count ranks (one handle per rank, state
  * replicated, λ % shard_count == 0, unbounded variables).  kg_cmaes_sample

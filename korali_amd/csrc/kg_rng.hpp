@@ -57,10 +57,10 @@ class MtStream {
   MtStream() = default;
   ~MtStream();
   // capacity: words the ring must hold beyond the current block.  Streams
-  // whose demand reaches `parallel_min` words use the chunked multi-
-  // workgroup producer (env KORALI_AMD_MT_PARALLEL_MIN / KORALI_AMD_MT_CHUNK_LOG2
+  // whose demand reaches `parallel_min` words (1 M: C2 and up) use the
+  // chunked multi-workgroup producer (env KORALI_AMD_MT_PARALLEL_MIN / KORALI_AMD_MT_CHUNK_LOG2
   // override the threshold and chunk size for tests).
-  int init(size_t capacity_words, size_t parallel_min = 8u << 20);
+  int init(size_t capacity_words, size_t parallel_min = 1u << 20);
   bool parallel() const { return par_; }
   int import_gsl(const void *state5000, hipStream_t s);
   int export_gsl(void *state5000, hipStream_t s);

@@ -1,0 +1,36 @@
+#!/bin/bash
+# round-2 profile session: every GPU step under its own time limit; stop at
+# the first crash / timeout.  Outputs under gpurun_out/r2/ (copied to
+# profiles/r2/ afterwards).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+R=$PWD
+O=$R/gpurun_out/r2
+mkdir -p $O
+step() {
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a "$O/steps.log"
+  (cd /tmp && timeout -k 10 "$secs" "$@") > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$O/steps.log"
+  tail -3 "$O/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "FATAL step $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-tests}; do
+  case $s in
+    tests) step tests 1000 python -u -m pytest $R/tests -x -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
+    avail) step avail 60 rocprofv3 --list-avail ;;
+    bench) step bench 300 python $R/bench.py --steps 200 --warmup 10 ;;
+    c3) step c3 400 python $R/bench.py --workload c3 --steps 40 --warmup 3 ;;
+    c4) step c4 400 python $R/bench.py --workload c4 --steps 20 --warmup 3 ;;
+    prof) step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    profc3) step profc3 300 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python $R/bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
+    profc4) step profc4 300 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmcf) step pmcf 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmcw) step pmcw 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmcm) step pmcm 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --cov mfma --no-cpu-baseline ;;
+    pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
+  esac
+done
+echo "session done"
