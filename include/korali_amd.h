@@ -110,6 +110,24 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation);
  * rest of the generation is queued.  With the device chase (eigen_device_chase =
  * 1, bit-identical, slower) the call only enqueues. */
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective);
+/* The next generation's first half ahead of time: the generator prefetch /
+ * polar pass and the eigendecomposition's tridiagonalisation and unpack,
+ * which touch only workspace (no state a result file holds), so a caller
+ * can enqueue them before deciding whether that generation will run (the
+ * engine does, before its termination check).  kg_cmaes_sample completes
+ * it; without this call kg_cmaes_sample does both halves. */
+int kg_cmaes_begin_sample(kg_cmaes_t h);
+/* The termination scalars of the last kg_cmaes_update without a stream
+ * synchronisation: the device publishes them (and the error flags) into
+ * host-coherent memory at the end of the update; this spins until they
+ * arrive.  out[] = Model Evaluation Count, Infeasible Sample Count, Maximum
+ * Covariance Eigenvalue, Minimum Covariance Eigenvalue, Current Min Standard
+ * Deviation, Current Max Standard Deviation, Best Ever Value, Current Best
+ * Value, Previous Best Value.  Device-side errors are reported as by
+ * kg_cmaes_synchronize.  (Experiment::run's check, experiment.cpp.base:56-99
+ * + the generated CMAES/optimizer/solver checkTermination.) */
+#define KG_TERMINATION_FIELDS 9
+int kg_cmaes_wait_termination_fields(kg_cmaes_t h, double *out);
 /* Population sharding over shard_count ranks (one handle per rank, state
  * replicated, λ % shard_count == 0, unbounded variables).  kg_cmaes_sample
  * and kg_cmaes_eval_builtin then cover only rows [rank λ/S, (rank+1) λ/S);

@@ -67,7 +67,22 @@ def build_engine(force=False, verbose=False):
         import pybind11
         inc = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
         _run([CXX] + CXXFLAGS + ["-fvisibility=hidden"] + inc + ["-o", PYMOD, pysrc] + srcs + link, verbose)
+    build_cxx_example(force, verbose)
     return PYMOD
+
+
+# a C++ problem definition in the reference's own idioms, linked against the
+# engine (tests/test_cxx_api.py runs it)
+CXX_EXAMPLE_SRC = os.path.join(ROOT, "tests", "cxx", "reference_idioms.cpp")
+CXX_EXAMPLE = os.path.join(ROOT, "tests", "cxx", "reference_idioms")
+
+
+def build_cxx_example(force=False, verbose=False):
+    hdrs = [os.path.join(ENGINE, f) for f in ("json.hpp", "korali.hpp")]
+    if os.path.exists(CXX_EXAMPLE_SRC) and (force or _stale(CXX_EXAMPLE, [CXX_EXAMPLE_SRC, ENGINE_LIB] + hdrs)):
+        _run([CXX, "-O1", "-std=c++17", "-I" + ENGINE, "-o", CXX_EXAMPLE, CXX_EXAMPLE_SRC, "-L" + PKG,
+              "-lkorali_engine", "-Wl,-rpath," + PKG], verbose)
+    return CXX_EXAMPLE
 
 
 if __name__ == "__main__":

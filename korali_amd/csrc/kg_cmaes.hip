@@ -1171,6 +1171,29 @@ __global__ void k_add_evals(CmaesScalars *sc, double n) {
 // ===================================================================== ABI
 using namespace kg;
 
+// what Experiment::run's termination check reads after every generation
+// (engine.cpp CmaesModule::checkTermination), in one host-coherent record
+struct TermSummary {
+  double f[KG_TERMINATION_FIELDS];
+  unsigned int errors, pad;
+  unsigned long long seq;  // written last (system-scope release)
+};
+
+// (the same publication protocol as kg_eigen.hip k_publish_dsd: relaxed
+// system-scope stores of the payload, release fence, release store of seq)
+__global__ void k_summary(const CmaesScalars *sc, const StreamState *a, const StreamState *b, TermSummary *out,
+                          unsigned long long seq) {
+  const double f[KG_TERMINATION_FIELDS] = {sc->modelEvaluationCount, sc->infeasibleSampleCount, sc->maxEig,
+                                           sc->minEig, sc->currentMinStd, sc->currentMaxStd, sc->bestEverValue,
+                                           sc->currentBestValue, sc->previousBestValue};
+  for (int i = 0; i < KG_TERMINATION_FIELDS; i++)
+    __hip_atomic_store((unsigned long long *)&out->f[i], (unsigned long long)__double_as_longlong(f[i]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&out->errors, sc->errors | a->errors | b->errors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __atomic_thread_fence(__ATOMIC_RELEASE);
+  __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct kg_cmaes_s {
   kg_cmaes_cfg cfg;
   int N = 0, lam = 0, mu = 0, R = 0;
@@ -1198,6 +1221,11 @@ struct kg_cmaes_s {
   int *kidx = nullptr, *shardCnt = nullptr;
   double *part = nullptr;  // "Shard Partials": mean (N), best row (N), rank-mu tiles
   unsigned long long *eigTrace = nullptr;  // KORALI_AMD_TRACE_EIGEN: s_memtime per phase
+  // termination scalars + error flags of the last update, written by the
+  // device into host-coherent memory (kg_cmaes_wait_termination_fields)
+  TermSummary *summary = nullptr, *summaryDev = nullptr;
+  unsigned long long updates = 0;
+  bool sampleBegun = false;  // kg_cmaes_begin_sample enqueued the next draw's first half
   MtStream normal, uniform;
   // profiling
   bool profile = false;
@@ -1447,6 +1475,12 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32);
+  if (hipHostMalloc(&h->summary, sizeof(TermSummary), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&h->summaryDev, h->summary, 0) != hipSuccess) {
+    delete h;
+    KG_CHECK(false, "hipHostMalloc of the termination summary failed");
+  }
+  memset(h->summary, 0, sizeof(TermSummary));
   if (L <= RANK_MAX && (size_t)L * sizeof(double) > 64 * 1024)
     KG_HIP(hipFuncSetAttribute((const void *)k_rank_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)((size_t)L * sizeof(double))));
@@ -1499,6 +1533,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
 int kg_cmaes_destroy(kg_cmaes_t h) {
   if (!h) return 0;
   (void)hipStreamSynchronize(h->stream);
+  if (h->summary) (void)hipHostFree(h->summary);
   for (void *p : {(void *)h->mean, (void *)h->prevMean, (void *)h->C, (void *)h->B, (void *)h->D, (void *)h->pc,
                   (void *)h->ps, (void *)h->w, (void *)h->X, (void *)h->Xall, (void *)h->BDZ, (void *)h->BDZall,
                   (void *)h->F, (void *)h->Z, (void *)h->bestEverVars, (void *)h->currBestVars,
@@ -1540,18 +1575,33 @@ static int cmaes_eigen(kg_cmaes_t h) {
                     &h->sc->eigenFailures, &h->sc->errors, h->stream, eig_prof, h);
 }
 
-int kg_cmaes_sample(kg_cmaes_t h) {
+static int cmaes_draw_begin(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
   const size_t rows = (size_t)L + h->R;
   if (h->normal.prefetch(rows * N, h->stream)) return 1;  // overlaps the eigensolver
-  {
-    // the polar pass reads only the generator stream: it runs on the
-    // producer's side stream too, concurrently with the eigensolver
-    const bool shard = h->shards > 1;
-    if (h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->normal.side_stream(),
-                                shard ? (size_t)h->r0 * N : 0, shard ? (size_t)h->r1 * N : (size_t)-1))
-      return 1;
-  }
+  // the polar pass reads only the generator stream: it runs on the
+  // producer's side stream too, concurrently with the eigensolver
+  const bool shard = h->shards > 1;
+  return h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->normal.side_stream(),
+                                 shard ? (size_t)h->r0 * N : 0, shard ? (size_t)h->r1 * N : (size_t)-1);
+}
+
+int kg_cmaes_begin_sample(kg_cmaes_t h) {
+  if (h->sampleBegun) return 0;
+  if (cmaes_draw_begin(h)) return 1;
+  h->eig.trace = h->eigTrace;
+  if (h->eig.run_begin(h->C, h->cfg.diagonal_covariance, h->B, h->D, &h->sc->minEig, &h->sc->maxEig,
+                       &h->sc->eigenFailures, &h->sc->errors, h->stream, eig_prof, h))
+    return 1;
+  h->sampleBegun = true;
+  return 0;
+}
+
+int kg_cmaes_sample(kg_cmaes_t h) {
+  const int N = h->N, L = h->lam;
+  const size_t rows = (size_t)L + h->R;
+  if (!h->sampleBegun && cmaes_draw_begin(h)) return 1;
+  h->sampleBegun = false;
   if (cmaes_eigen(h)) return 1;
   {
     Stage st(h, "rng_polar");  // what of the producer + polar pass the eigensolver did not hide
@@ -1660,6 +1710,13 @@ static int cmaes_sigma(kg_cmaes_t h) {
   return 0;
 }
 
+static int cmaes_publish_summary(kg_cmaes_t h) {
+  hipLaunchKernelGGL(k_summary, dim3(1), dim3(1), 0, h->stream, h->sc, h->normal.state(), h->uniform.state(),
+                     h->summaryDev, ++h->updates);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
 static int cmaes_paths(kg_cmaes_t h, size_t generation) {
   const int N = h->N;
   const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
@@ -1715,7 +1772,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     KG_HIP(hipGetLastError());
   }
   if (cmaes_sigma(h)) return 1;
-  return 0;
+  return cmaes_publish_summary(h);
 }
 
 int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
@@ -1770,6 +1827,29 @@ int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
   if (kg_cmaes_sample(h)) return 1;
   if (kg_cmaes_eval_builtin(h, objective)) return 1;
   return kg_cmaes_update(h, generation);
+}
+
+int kg_cmaes_wait_termination_fields(kg_cmaes_t h, double *out) {
+  // the record of the last kg_cmaes_update; spin on host-coherent memory
+  // (microseconds) instead of synchronising the stream, which may already
+  // hold the next generation's first half (kg_cmaes_begin_sample)
+  const unsigned long long want = h->updates;
+  KG_CHECK(want > 0, "kg_cmaes_wait_termination_fields before any kg_cmaes_update");
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) < want) {
+    __builtin_ia32_pause();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+      KG_HIP(hipStreamSynchronize(h->stream));  // surfaces a device fault, if any
+      if (check_errors(h)) return 1;
+      KG_CHECK(false, "termination summary never arrived");
+    }
+  }
+  if (h->summary->errors) {
+    KG_HIP(hipStreamSynchronize(h->stream));
+    return check_errors(h);
+  }
+  for (int i = 0; i < KG_TERMINATION_FIELDS; i++) out[i] = h->summary->f[i];
+  return 0;
 }
 
 int kg_cmaes_synchronize(kg_cmaes_t h) {

@@ -2824,13 +2824,14 @@ EigenSolver::~EigenSolver() {
   if (ev_chase) (void)hipEventDestroy(ev_chase);
 }
 
-int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
-                     double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
-  if (diagonal) {
-    hipLaunchKernelGGL(k_eigen_diag, dim3(1), dim3(256), 0, s, N, C, B, D, minEig, maxEig, eigenFailures);
-    KG_HIP(hipGetLastError());
-    return 0;
-  }
+// Phase A and B (+ the tridiagonal's hand-off to the chase): they touch only
+// the solver's workspace, so a caller may enqueue them ahead of time (the
+// next generation's, before its termination check) and complete the
+// decomposition with run_finish.
+int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+                           double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
+  begun = true;
+  if (diagonal) return 0;  // k_eigen_diag runs in run_finish
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
@@ -2873,6 +2874,21 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
                        gQt);
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_unpack", 1);
+  return 0;
+}
+
+// Phases C and D: the Givens chase and the rotations' application (and the
+// whole diagonal-covariance case)
+int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+                            double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof,
+                            void *profCtx) {
+  begun = false;
+  if (diagonal) {
+    hipLaunchKernelGGL(k_eigen_diag, dim3(1), dim3(256), 0, s, N, C, B, D, minEig, maxEig, eigenFailures);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
+  EigRec devRec = dev;
   if (hostChase) {
     // the apply kernel is queued behind the unpack and consumes the Givens
     // rotations as this core's serial chase publishes them
@@ -2910,6 +2926,12 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
   }
   if (prof) prof(profCtx, "eigen_apply", 1);
   return 0;
+}
+
+int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+                     double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
+  if (!begun && run_begin(C, diagonal, B, D, minEig, maxEig, eigenFailures, errors, s, prof, profCtx)) return 1;
+  return run_finish(C, diagonal, B, D, minEig, maxEig, eigenFailures, errors, s, prof, profCtx);
 }
 
 }  // namespace kg

@@ -22,6 +22,12 @@ class EigenSolver {
   int init(int N, bool hostChase);
   int run(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
           double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
+  // run = run_begin (tridiagonalisation, unpack: workspace only) + run_finish
+  int run_begin(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+          double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
+  int run_finish(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
+          double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
+  bool begun = false;
   int t1flags = 0;  // KORALI_AMD_T1_FLAGS: experiment switches of k_tridiag_1wg
   unsigned long long *trace = nullptr;  // optional device counters (k_tridiag sub-phases)
   // QR steps / Givens rotations of the last host chase (diagnostics)

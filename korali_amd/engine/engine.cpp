@@ -409,6 +409,106 @@ std::vector<double> flatten(Json &j) {
   return v;
 }
 
+// ------------------------------------------------ unrecognised settings
+// Every generated Module::setConfiguration erases the keys it consumes and
+// fails on whatever is left (source_builders.py:164-170, e.g. the generated
+// CMAES.cpp:1781): a misspelt key is an error, not a silently applied
+// default.  The accepted names are the reference's .config keys of the
+// module and its parents (Configuration Settings, Termination Criteria,
+// Internal Settings) plus this build's extension keys and the state keys it
+// writes into result files.
+using KeyList = std::initializer_list<const char *>;
+const KeyList SOLVER_KEYS = {"Type", "Variable Count", "Model Evaluation Count", "Termination Criteria"};
+const KeyList SOLVER_TERMINATION = {"Max Model Evaluations", "Max Generations"};
+const KeyList OPTIMIZER_KEYS = {"Current Best Value", "Previous Best Value", "Best Ever Value", "Best Ever Variables"};
+const KeyList OPTIMIZER_TERMINATION = {"Max Value", "Min Value Difference Threshold"};
+const KeyList CMAES_KEYS = {
+    // Configuration Settings (CMAES.config)
+    "Population Size", "Mu Value", "Mu Type", "Initial Sigma Cumulation Factor", "Initial Damp Factor",
+    "Use Gradient Information", "Gradient Step Size", "Is Sigma Bounded", "Initial Cumulative Covariance",
+    "Diagonal Covariance", "Mirrored Sampling", "Viability Population Size", "Viability Mu Value",
+    "Max Covariance Matrix Corrections", "Target Success Rate", "Covariance Matrix Adaption Strength",
+    "Normal Vector Learning Rate", "Global Success Learning Rate",
+    // Internal Settings
+    "Normal Generator", "Uniform Generator", "Is Viability Regime", "Value Vector", "Gradients",
+    "Current Population Size", "Current Mu Value", "Mu Weights", "Effective Mu", "Sigma Cumulation Factor",
+    "Damp Factor", "Cumulative Covariance", "Chi Square Number", "Covariance Eigenvalue Evaluation Frequency", "Sigma",
+    "Trace", "Sample Population", "Finished Sample Count", "Current Best Variables", "Previous Best Ever Value",
+    "Sorting Index", "Covariance Matrix", "Auxiliar Covariance Matrix", "Covariance Eigenvector Matrix",
+    "Auxiliar Covariance Eigenvector Matrix", "Axis Lengths", "Auxiliar Axis Lengths", "BDZ Matrix",
+    "Auxiliar BDZ Matrix", "Current Mean", "Previous Mean", "Mean Update", "Evolution Path",
+    "Conjugate Evolution Path", "Conjugate Evolution Path L2 Norm", "Infeasible Sample Count",
+    "Maximum Diagonal Covariance Matrix Element", "Minimum Diagonal Covariance Matrix Element",
+    "Maximum Covariance Eigenvalue", "Minimum Covariance Eigenvalue", "Is Eigensystem Updated",
+    "Viability Indicator", "Has Constraints", "Covariance Matrix Adaption Factor", "Best Valid Sample",
+    "Global Success Rate", "Viability Function Value", "Resampled Parameter Count",
+    "Covariance Matrix Adaptation Count", "Viability Boundaries", "Viability Improvement",
+    "Max Constraint Violation Count", "Sample Constraint Violation Counts", "Constraint Evaluations",
+    "Normal Constraint Approximation", "Best Constraint Evaluations", "Has Discrete Variables", "Discrete Mutations",
+    "Number Of Discrete Mutations", "Number Masking Matrix Entries", "Masking Matrix", "Masking Matrix Sigma",
+    "Chi Square Number Discrete Mutations", "Current Min Standard Deviation", "Current Max Standard Deviation",
+    "Constraint Evaluation Count",
+    // extension (include/korali_amd.h)
+    "Covariance Update"};
+const KeyList CMAES_TERMINATION = {"Max Infeasible Resamplings", "Max Condition Covariance Matrix",
+                                   "Min Standard Deviation", "Max Standard Deviation"};
+const KeyList TMCMC_KEYS = {
+    // Configuration Settings (TMCMC.config)
+    "Version", "Population Size", "Max Chain Length", "Burn In", "Per Generation Burn In",
+    "Target Coefficient Of Variation", "Covariance Scaling", "Min Annealing Exponent Update",
+    "Max Annealing Exponent Update", "Step Size", "Domain Extension Factor",
+    // Internal Settings
+    "Multinomial Generator", "Multivariate Generator", "Uniform Generator", "Current Burn In",
+    "Chain Pending Evaluation", "Chain Pending Gradient", "Chain Candidates", "Chain Candidates LogLikelihoods",
+    "Chain Candidates LogPriors", "Chain Candidates Gradients", "Chain Candidates Errors",
+    "Chain Candidates Covariance", "Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Leaders LogPriors",
+    "Chain Leaders Gradients", "Chain Leaders Errors", "Chain Leaders Covariance", "Finished Chains Count",
+    "Current Chain Step", "Chain Lengths", "Coefficient Of Variation", "Chain Count", "Annealing Exponent",
+    "Previous Annealing Exponent", "Num Finite Prior Evaluations", "Num Finite Likelihood Evaluations",
+    "Accepted Samples Count", "LogEvidence", "Proposals Acceptance Rate", "Selection Acceptance Rate",
+    "Covariance Matrix", "Max Loglikelihood", "Mean Theta", "Sample Database", "Sample LogLikelihood Database",
+    "Sample LogPrior Database", "Sample Gradient Database", "Sample Error Database", "Sample Covariances Database",
+    "Upper Extended Boundaries", "Lower Extended Boundaries", "Num LU Decomposition Failures Proposal",
+    "Num Eigen Decomposition Failures Proposal", "Num Inversion Failures Proposal", "Num Negative Definite Proposals",
+    "Num Cholesky Decomposition Failures Proposal", "Num Covariance Corrections",
+    // state this build writes
+    "Database Entries", "Num Selections"};
+const KeyList TMCMC_TERMINATION = {"Target Annealing Exponent"};
+// problems (optimization.config, bayesian/*.config) + the extension kernels
+const KeyList OPTIMIZATION_KEYS = {"Type", "Num Objectives", "Objective Function", "Constraints",
+                                   "Has Discrete Variables", "Objective Kernel"};
+const KeyList BAYESIAN_CUSTOM_KEYS = {"Type", "Likelihood Model", "Likelihood Kernel"};
+const KeyList BAYESIAN_REFERENCE_KEYS = {"Type", "Computational Model", "Reference Data", "Likelihood Model"};
+
+void rejectProblemUnrecognised(Json &pb, const std::string &canonType);
+
+bool inList(const std::string &k, std::initializer_list<KeyList> lists) {
+  for (const KeyList &l : lists)
+    for (const char *a : l)
+      if (k == a) return true;
+  return false;
+}
+
+void rejectUnrecognised(Json &mod, const char *moduleName, std::initializer_list<KeyList> keys,
+                        std::initializer_list<KeyList> termination) {
+  Json left = Json::object();
+  for (const auto &kv : mod.items()) {
+    if (kv.first == "Termination Criteria" && kv.second.is_object() && termination.size()) {
+      for (const auto &tv : kv.second.items())
+        if (!inList(tv.first, termination)) left["Termination Criteria"][tv.first] = tv.second;
+      continue;
+    }
+    if (!inList(kv.first, keys)) left[kv.first] = kv.second;
+  }
+  if (left.size()) fail(" + Unrecognized settings for Korali module: %s: \n%s\n", moduleName, left.dump(2).c_str());
+}
+
+void rejectProblemUnrecognised(Json &pb, const std::string &pt) {
+  if (pt == "optimization") rejectUnrecognised(pb, "Optimization", {OPTIMIZATION_KEYS}, {});
+  else if (pt == "bayesian/custom") rejectUnrecognised(pb, "Custom", {BAYESIAN_CUSTOM_KEYS}, {});
+  else if (pt == "bayesian/reference") rejectUnrecognised(pb, "Reference", {BAYESIAN_REFERENCE_KEYS}, {});
+}
+
 // ------------------------------------------------------------- CMA-ES
 // CMAES.cpp.base on the device (kg_cmaes_*); state names as in CMAES.config
 const char *CMAES_VECTORS[] = {"Current Mean", "Previous Mean", "Covariance Matrix", "Covariance Eigenvector Matrix",
@@ -431,6 +531,7 @@ struct CmaesModule : SolverModule {
   std::vector<VariableSpec> vars;
   double maxGenerations, maxModelEvaluations, maxInfeasible, maxCondition, minStd, maxStd, maxValue, minValueDiff;
   Json *solverJs = nullptr;
+  bool updated = false;  // kg_cmaes_update ran on this handle (its termination record exists)
 
   ~CmaesModule() override {
     if (h) kg_cmaes_destroy(h);
@@ -444,6 +545,9 @@ struct CmaesModule : SolverModule {
     if (pt != "optimization" && pt != "bayesian/custom" && pt != "bayesian/reference")
       fail("Solver CMAES requires a problem of type 'Optimization', 'Bayesian/Custom' or 'Bayesian/Reference' (is '%s').",
            pb["Type"].getString().c_str());
+    rejectUnrecognised(sv, "CMAES", {SOLVER_KEYS, OPTIMIZER_KEYS, CMAES_KEYS},
+                       {SOLVER_TERMINATION, OPTIMIZER_TERMINATION, CMAES_TERMINATION});
+    rejectProblemUnrecognised(pb, pt);
     vars = readVariables(js);
     N = vars.size();
     lam = uint(sv, "Population Size", 0);
@@ -584,7 +688,12 @@ struct CmaesModule : SolverModule {
       check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
     }
     check(kg_cmaes_update(h, gen));
-    check(kg_cmaes_synchronize(h));  // device-side error flags -> KoraliError
+    updated = true;
+    // enqueue the next generation's first half (generator prefetch, the
+    // eigendecomposition's tridiagonalisation and unpack: workspace only)
+    // before the termination check, so the device never idles while the
+    // host decides; device-side errors surface in checkTermination
+    check(kg_cmaes_begin_sample(h));
   }
 
   double field(const char *k) {
@@ -599,8 +708,11 @@ struct CmaesModule : SolverModule {
                                   "Current Min Standard Deviation", "Current Max Standard Deviation",
                                   "Best Ever Value",                "Current Best Value",
                                   "Previous Best Value"};
-    double v[9];
-    check(kg_cmaes_get_fields(h, names, 9, v));
+    double v[KG_TERMINATION_FIELDS];
+    if (updated)  // published by the device at the end of the update, no stream synchronisation
+      check(kg_cmaes_wait_termination_fields(h, v));
+    else
+      check(kg_cmaes_get_fields(h, names, KG_TERMINATION_FIELDS, v));
     if (gen > maxGenerations) met.push_back("Max Generations");
     if (maxModelEvaluations <= v[0]) met.push_back("Max Model Evaluations");
     if (gen <= 1) return;
@@ -693,6 +805,8 @@ struct TmcmcModule : SolverModule {
     if (pt != "bayesian/custom" && pt != "bayesian/reference")
       fail("The device TMCMC path supports problems of type 'Bayesian/Custom' and 'Bayesian/Reference' (is '%s').",
            pb["Type"].getString().c_str());
+    rejectUnrecognised(sv, "TMCMC", {SOLVER_KEYS, TMCMC_KEYS}, {SOLVER_TERMINATION, TMCMC_TERMINATION});
+    rejectProblemUnrecognised(pb, pt);
     reference = pt == "bayesian/reference";
     if (canon(str(sv, "Version", "TMCMC")) != "tmcmc") fail("Only Version 'TMCMC' is supported by the device path.");
     std::vector<VariableSpec> vars = readVariables(js);
@@ -936,6 +1050,11 @@ struct ExperimentState {
 };
 
 Experiment::Experiment() : _state(new ExperimentState()) {}
+
+std::vector<std::vector<float>> Experiment::getEvaluation(const std::vector<std::vector<std::vector<float>>> &) {
+  // experiment.cpp.base:219-229: only a Learner solver evaluates input batches
+  fail("This solver does not support evaluation operations.\n");
+}
 Experiment::~Experiment() = default;
 Experiment::Experiment(Experiment &&) noexcept = default;
 Experiment &Experiment::operator=(Experiment &&) noexcept = default;

@@ -17,6 +17,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace korali {
@@ -101,6 +102,25 @@ class Json {
   template <typename T>
   T get() const;
 
+  // implicit conversion to a value type, as knlohmann::json allows
+  // (examples/features/running.cxx/_model/direct.hpp:8:
+  //  `float x = k["Parameters"][0];`, `std::vector<double> p = s["Parameters"];`)
+  template <typename T, typename = typename std::enable_if<!std::is_pointer<T>::value &&
+                                                           !std::is_same<T, Json>::value>::type>
+  operator T() const {
+    return get<T>();
+  }
+  // comparisons with plain values (sample.cpp: `(*_self)["Module"] == "Solver"`)
+  bool operator==(const char *v) const { return is_string() && s_ == v; }
+  bool operator==(const std::string &v) const { return is_string() && s_ == v; }
+  bool operator==(bool v) const { return is_bool() && b_ == v; }
+  bool operator==(double v) const { return is_number() && getDouble() == v; }
+  bool operator==(int v) const { return is_number() && getDouble() == (double)v; }
+  template <typename T>
+  bool operator!=(const T &v) const {
+    return !(*this == v);
+  }
+
   std::string dump(int indent = -1) const;
 
  private:
@@ -131,5 +151,54 @@ template <>
 inline std::string Json::get<std::string>() const { return getString(); }
 template <>
 inline std::vector<double> Json::get<std::vector<double>>() const { return getDoubleVector(); }
+template <>
+inline long long Json::get<long long>() const { return getInt(); }
+template <>
+inline unsigned Json::get<unsigned>() const { return (unsigned)getUInt(); }
+template <>
+inline unsigned long long Json::get<unsigned long long>() const { return getUInt(); }
+template <>
+inline Json Json::get<Json>() const { return *this; }
+template <>
+inline std::vector<float> Json::get<std::vector<float>>() const {
+  std::vector<float> v;
+  for (double x : getDoubleVector()) v.push_back((float)x);
+  return v;
+}
+template <>
+inline std::vector<int> Json::get<std::vector<int>>() const {
+  std::vector<int> v;
+  for (const Json &x : elements()) v.push_back((int)x.getInt());
+  if (!is_array()) throw std::runtime_error("JSON value is not an array");
+  return v;
+}
+template <>
+inline std::vector<size_t> Json::get<std::vector<size_t>>() const {
+  std::vector<size_t> v;
+  for (const Json &x : elements()) v.push_back((size_t)x.getUInt());
+  if (!is_array()) throw std::runtime_error("JSON value is not an array");
+  return v;
+}
+template <>
+inline std::vector<std::string> Json::get<std::vector<std::string>>() const {
+  std::vector<std::string> v;
+  for (const Json &x : elements()) v.push_back(x.getString());
+  if (!is_array()) throw std::runtime_error("JSON value is not an array");
+  return v;
+}
+template <>
+inline std::vector<std::vector<double>> Json::get<std::vector<std::vector<double>>>() const {
+  std::vector<std::vector<double>> v;
+  for (const Json &x : elements()) v.push_back(x.getDoubleVector());
+  if (!is_array()) throw std::runtime_error("JSON value is not an array");
+  return v;
+}
+template <>
+inline std::vector<std::vector<float>> Json::get<std::vector<std::vector<float>>>() const {
+  std::vector<std::vector<float>> v;
+  for (const Json &x : elements()) v.push_back(x.get<std::vector<float>>());
+  if (!is_array()) throw std::runtime_error("JSON value is not an array");
+  return v;
+}
 
 }  // namespace korali

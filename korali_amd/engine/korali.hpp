@@ -5,6 +5,7 @@
 //
 //   #include <korali.hpp>
 //   void model(korali::Sample &s) { auto x = KORALI_GET(std::vector<double>, s, "Parameters"); s["F(x)"] = ...; }
+//   void direct(korali::Sample &k) { float x = k["Parameters"][0]; k["F(x)"] = -0.5 * x * x; }
 //   korali::Engine k; korali::Experiment e;
 //   e["Problem"]["Type"] = "Optimization";
 //   e["Problem"]["Objective Function"] = &model;
@@ -21,22 +22,78 @@
 //   "Device": HIP device ordinal of the experiment
 #pragma once
 
+#include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "json.hpp"
 
 namespace korali {
 
-// KORALI_GET(TYPE, SAMPLE, KEY): typed read of a sample entry (sample.hpp:25)
-#define KORALI_GET(TYPE, SAMPLE, KEY) ((SAMPLE)[KEY].template get<TYPE>())
+// thrown for every configuration or runtime error (KORALI_LOG_ERROR)
+class KoraliError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// KORALI_GET(TYPE, SAMPLE, KEY, ...): typed read of a (nested) sample entry,
+// failing with the reference's messages (sample.hpp:25-26, :115-131)
+#define KORALI_GET(TYPE, SAMPLE, ...) (SAMPLE).template get<TYPE>(__FILE__, __LINE__, __VA_ARGS__)
 
 class Sample {
  public:
   Json &operator[](const std::string &key) { return _js[key]; }
+  Json &operator[](size_t key) { return _js[key]; }
   bool contains(const std::string &key) const { return _js.contains(key); }
+  // Sample::update (sample.cpp:31-34) hands control back to the engine so it
+  // can process messages the model sent mid-evaluation.  CMA-ES and TMCMC
+  // exchange no such messages and every sample runs to completion on the
+  // evaluating thread, so there is nothing to hand over: a no-op.
+  void update() {}
+
+  template <typename T, typename... Key>
+  T get(const char *fileName, int lineNumber, const Key &...key) {
+    const Json *j = &_js;
+    std::string path;
+    if (!walk(j, path, key...))
+      fail(fileName, lineNumber, "Requesting non existing value " + path + " from sample.\n");
+    try {
+      return j->template get<T>();
+    } catch (const std::exception &e) {
+      fail(fileName, lineNumber,
+           "Missing or incorrect value " + path + " for the sample.\n + Cause: " + std::string(e.what()) + "\n");
+    }
+  }
+
   Json _js;
+
+ private:
+  static bool step(const Json *&j, std::string &path, const std::string &k) {
+    path += "[\"" + k + "\"]";
+    if (!j->contains(k)) return false;
+    j = &j->at(k);
+    return true;
+  }
+  static bool step(const Json *&j, std::string &path, const char *k) { return step(j, path, std::string(k)); }
+  template <typename I, typename = typename std::enable_if<std::is_integral<I>::value>::type>
+  static bool step(const Json *&j, std::string &path, I idx) {
+    path += "[" + std::to_string((long long)idx) + "]";
+    if (!j->is_array() || (size_t)idx >= j->size()) return false;
+    j = &j->at((size_t)idx);
+    return true;
+  }
+  static bool walk(const Json *&, std::string &) { return true; }
+  template <typename K, typename... Rest>
+  static bool walk(const Json *&j, std::string &path, const K &k, const Rest &...rest) {
+    return step(j, path, k) && walk(j, path, rest...);
+  }
+  [[noreturn]] static void fail(const char *fileName, int lineNumber, const std::string &msg) {
+    // Logger::logError (logger.cpp:83-99): message + " + From file:line\n"
+    throw KoraliError(msg + " + From " + fileName + ":" + std::to_string(lineNumber) + "\n");
+  }
 };
 
 struct ExperimentState;  // solver module + bookkeeping (engine.cpp)
@@ -54,6 +111,9 @@ class Experiment {
   // Experiment::loadState (experiment.cpp.base:150-153): the full JSON of a
   // result file; a following run() resumes from it bit for bit.
   bool loadState(const std::string &path);
+  // Experiment::getEvaluation (experiment.cpp.base:219-229): only learner
+  // solvers evaluate batches; CMA-ES and TMCMC raise the reference's error
+  std::vector<std::vector<float>> getEvaluation(const std::vector<std::vector<std::vector<float>>> &inputBatch);
 
   Json _js;
   std::unique_ptr<ExperimentState> _state;
@@ -85,11 +145,5 @@ bool isReferenceLikelihoodModel(const std::string &model);
 // Distributions / Variables (the host evaluation CMA-ES uses on Bayesian
 // problems); returns the sample's JSON (logPrior, logLikelihood, F(x), ...)
 Json bayesianEvaluate(Json &experiment, const std::vector<double> &x);
-
-// thrown for every configuration or runtime error (KORALI_LOG_ERROR)
-class KoraliError : public std::runtime_error {
- public:
-  using std::runtime_error::runtime_error;
-};
 
 }  // namespace korali

@@ -179,7 +179,8 @@ PYBIND11_MODULE(libkorali, m) {
              return child(JsonRef{&s._js, {}, self}, key(k));
            })
       .def("__setitem__", [](korali::Sample &s, const std::string &k, py::handle v) { s[k] = toJson(v); })
-      .def("__contains__", [](korali::Sample &s, const std::string &k) { return s.contains(k); });
+      .def("__contains__", [](korali::Sample &s, const std::string &k) { return s.contains(k); })
+      .def("update", &korali::Sample::update);
 
   py::class_<korali::Experiment>(m, "Experiment")
       .def(py::init<>())
@@ -190,6 +191,7 @@ PYBIND11_MODULE(libkorali, m) {
            })
       .def("__setitem__", [](korali::Experiment &e, const std::string &k, py::handle v) { e[k] = toJson(v); })
       .def("loadState", &korali::Experiment::loadState)
+      .def("getEvaluation", &korali::Experiment::getEvaluation)
       .def("dump", [](korali::Experiment &e) { return e._js.dump(2); });
 
   // run() releases the GIL: Python callbacks re-acquire it per sample, so a

@@ -56,7 +56,7 @@ EXPORTED = [
     "kg_last_error", "kg_abi_version", "kg_device_count",
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
     "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_set_log_posterior", "kg_cmaes_update", "kg_cmaes_generation",
-    "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
+    "kg_cmaes_begin_sample", "kg_cmaes_wait_termination_fields", "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
@@ -80,7 +80,8 @@ def lib():
         L.kg_abi_version.restype = ip
         L.kg_device_count.argtypes = [C.POINTER(C.c_int)]
         L.kg_cmaes_create.argtypes = [C.POINTER(_CmaesCfg), C.POINTER(vp)]
-        for f in ("kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_synchronize"):
+        for f in ("kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_synchronize",
+                  "kg_cmaes_begin_sample"):
             getattr(L, f).argtypes = [vp]
         L.kg_cmaes_eval_builtin.argtypes = [vp, ip]
         L.kg_cmaes_get_candidates.argtypes = [vp, dp, sz]
@@ -96,6 +97,7 @@ def lib():
         L.kg_cmaes_set_field.argtypes = [vp, cp, dp, sz]
         L.kg_cmaes_get_sorting_index.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.kg_cmaes_get_fields.argtypes = [vp, C.POINTER(cp), sz, dp]
+        L.kg_cmaes_wait_termination_fields.argtypes = [vp, dp]
         L.kg_cmaes_get_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_set_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_device_ptr.argtypes = [vp, cp, C.POINTER(vp)]

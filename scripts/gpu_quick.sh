@@ -2,7 +2,7 @@
 # quick GPU check: eigen/CMA-ES parity tests, then the C2 bench (exact) and the tridiag trace
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_cmaes.py tests/test_gpu_engine.py -x -q --timeout 300 --timeout-method thread > gpurun_out/q_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_cmaes.py tests/test_gpu_engine.py tests/test_cxx_api.py tests/test_gpu_tmcmc.py -x -q --timeout 300 --timeout-method thread > gpurun_out/q_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/q_tests.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python bench.py --steps 200 --warmup 10 --cov ${COV:-exact} --no-cpu-baseline > gpurun_out/q_bench.log 2>&1 || exit $?
