@@ -45,6 +45,7 @@ STAGE_FLOPS = {
     "eigen_apply": 6.0 * 1.1 * N_VARS ** 3,
     "transform": 2.0 * LAMBDA * N_VARS ** 2,
     "covariance": 2.0 * MU * N_VARS ** 2,  # full-GEMM count of the rank-mu sum
+    "rankmu_mfma": 2.0 * MU * N_VARS ** 2,
     "objective": 8.0 * LAMBDA * N_VARS,
 }
 
@@ -53,10 +54,11 @@ STAGE_FLOPS = {
 STAGE_KERNELS = {
     # a tuple lists alternatives (the kernel the size selects); template
     # instances match their base name
-    "eigen_tridiag": [("kg::k_tridiag_1wg", "kg::k_tridiag_mw", "kg::k_tridiag")],
+    "eigen_tridiag": [("kg::k_tridiag_1wg2", "kg::k_tridiag_1wg", "kg::k_tridiag_mw", "kg::k_tridiag")],
     "eigen_unpack": [("kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
     "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
-    "covariance": ["kg::k_rankmu_mfma", "kg::k_adaptC_combine"],
+    "covariance": [("kg::k_adaptC_exact2", "kg::k_adaptC_combine")],
+    "rankmu_mfma": ["kg::k_rankmu_tile"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
     "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", "kg::k_mean", "kg::k_paths"],
 }
@@ -87,6 +89,19 @@ def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
         tot += (float(r["fetch_KB_x2"]) + float(r["write_KB"])) * 1024
         raw += (float(r["fetch_KB_raw"]) + float(r["write_KB"])) * 1024
     return tot, raw
+
+
+def rankmu_roofline(ms, mu, n, csv_name):
+    """The rank-mu MFMA kernel (k_rankmu_tile) against the FP64 matrix peak:
+    algorithmic work 2 mu N^2 (the full-GEMM count; the kernel forms only the
+    lower tiles), HIP events around its launch on its own stream."""
+    flops = 2.0 * mu * n * n
+    achieved = flops / (ms * 1e-3) / 1e12
+    traffic, raw = pmc_traffic("rankmu_mfma", csv_name)
+    return {"kernel": "kg::k_rankmu_tile", "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "avg_launch_ms": ms,
+            "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": 8.0 * (mu * n + n * n),
+            "traffic": traffic, "traffic_source": f"profiles/{PROFILE_ROUND}/{csv_name}" if traffic else None}
 
 
 def cpu_model():
@@ -269,7 +284,7 @@ def main():
     dev.profile(True)
     prof_steps = min(args.steps, 20)
     STAGES = ("eigen", "eigen_tridiag", "eigen_unpack", "eigen_chase_host", "eigen_apply", "rng_polar", "transform",
-              "rng_consume", "objective", "sort", "mean_paths", "covariance", "sigma")
+              "rng_consume", "objective", "sort", "mean_paths", "covariance", "rankmu_mfma", "sigma")
     for st in ("init",) + STAGES:
         dev.profile_read(st)
     for _ in range(prof_steps):
@@ -302,6 +317,22 @@ def main():
         adev.generation(g2, "rosenbrock")
     adev.synchronize()
     alt_rate = args.steps / (time.perf_counter() - ta)
+    mfma_kernel = None
+    if alt == "mfma" or args.cov == "mfma":
+        pdev = adev if alt == "mfma" else None
+        if pdev is not None:
+            pdev.profile(True)
+            pdev.profile_read("rankmu_mfma")
+            for _ in range(20):
+                g2 += 1
+                pdev.generation(g2, "rosenbrock")
+            pdev.synchronize()
+            ms, n = pdev.profile_read("rankmu_mfma")
+        else:
+            ms, n = stages.get("rankmu_mfma", 0.0), 1
+        if n:
+            ms = ms / n if pdev is not None else ms
+            mfma_kernel = rankmu_roofline(ms, MU, N_VARS, "c2_pmc_traffic.csv")
     adev.close()
     if rank != 0:
         if dist is not None:
@@ -309,7 +340,8 @@ def main():
         return
 
     gens_per_s = args.steps * world / elapsed
-    kernels = {k: v for k, v in stages.items() if k not in ("eigen", "eigen_chase_host")}
+    # rankmu_mfma runs on the second stream, beside mean_paths
+    kernels = {k: v for k, v in stages.items() if k not in ("eigen", "eigen_chase_host", "rankmu_mfma")}
     dominant = max(kernels, key=kernels.get)
     dom_ms = stages[dominant]
     flops = STAGE_FLOPS.get(dominant, 0.0)
@@ -338,6 +370,7 @@ def main():
         "samples_per_sec": gens_per_s * LAMBDA,
         "engine_generations_per_sec": eng,
         f"{alt}_covariance_generations_per_sec_per_gpu": alt_rate,
+        "rankmu_mfma_roofline": mfma_kernel,
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
@@ -549,7 +582,7 @@ def run_c4(args):
         elapsed = float(t.item())
     dev.profile(True)
     STAGES = ("eigen", "eigen_tridiag", "eigen_unpack", "eigen_chase_host", "eigen_apply", "rng_polar", "transform",
-              "objective", "sort", "mean_paths", "covariance", "sigma")
+              "objective", "sort", "mean_paths", "covariance", "rankmu_mfma", "sigma")
     for st in ("init",) + STAGES:
         dev.profile_read(st)
     for _ in range(2):
@@ -573,6 +606,8 @@ def run_c4(args):
                                    "sigma0=1, seed 1337", "parallelism": f"population-shard{world}"},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
             "stage_ms_rank0": stages,
+            "rankmu_mfma_roofline": rankmu_roofline(stages["rankmu_mfma"], C4_L // 2, C4_N, "c4_pmc_traffic.csv")
+            if "rankmu_mfma" in stages else None,
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
     if dist is not None:
         dist.destroy_process_group()

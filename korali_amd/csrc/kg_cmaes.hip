@@ -902,47 +902,143 @@ __global__ void __launch_bounds__(256) k_adaptC_exact(int N, int mu, int diagona
   }
 }
 
-// adaptC with the rank-μ sum on the FP64 matrix cores: per 16x16 tile of C
-// and K-slice, D += Ŷᵀ Y with v_mfma_f64_16x16x4f64 (one wave per tile and
-// slice), Ŷ_k = (cμ w_k / σ²) y_k.  The base terms are added by
-// k_adaptC_combine in the reference's order.
+// adaptC with the rank-μ sum on the FP64 matrix cores (the "MFMA"
+// covariance mode): Σ_k ŷ_k y_kᵀ over the lower 64x64 tiles of C, Ŷ_k =
+// (cμ w_k / σ²) y_k, y_k = x_sel(k) - m_prev.  One 256-thread workgroup per
+// (64x64 tile, K-slice); each wave owns a 32x32 quarter as 2x2
+// v_mfma_f64_16x16x4f64 accumulators fed from LDS.  The slice's rows are
+// staged 32 at a time (centred and scaled while staging, coalesced 16-B
+// loads prefetched into registers one chunk ahead).  Workgroup ids are
+// dealt to the 8 XCDs round-robin, so all tiles of one K-slice are given
+// ids of one XCD: the slice's rows come from HBM once into that XCD's L2
+// and are re-read there by the slice's tiles.  Partial sums go to
+// part[slice][16x16 tile] for k_adaptC_combine / k_part_reduce, which add
+// the slices and the base terms in a fixed order (deterministic).
+// SHARD: rows are the rank's owned selected rows (count on the device),
+// weights w[kidx[j]], scale 1/σ² (cμ applied after the all-reduce).
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-__global__ void __launch_bounds__(64) k_rankmu_mfma(int N, int mu, int kslices, const double *__restrict__ X,
-                                                    const unsigned *__restrict__ idx, const double *__restrict__ w,
-                                                    const double *__restrict__ prevMean,
-                                                    const CmaesScalars *__restrict__ sc, double *__restrict__ part) {
+constexpr int RT_T = 64, RT_KC = 32, RT_LD = RT_T + 16;  // LDS row stride: the 4 k-rows of a fragment in 2 bank halves
+
+inline int rankmu_grid(int N, int kslices) {
+  const int nt = (N + RT_T - 1) / RT_T;
+  return nt * (nt + 1) / 2 * kslices;
+}
+
+inline int rankmu_kslices(int N, int rows) {
+  const int nt = (N + RT_T - 1) / RT_T, ntiles = nt * (nt + 1) / 2;
+  int want = (1024 + 8 * ntiles - 1) / (8 * ntiles), cap = rows / (8 * 64);
+  if (cap < 1) cap = 1;
+  if (want > cap) want = cap;
+  if (want < 1) want = 1;
+  return 8 * want;
+}
+
+template <bool SHARD>
+__global__ void __launch_bounds__(256) k_rankmu_tile(int N, int rowsIn, const int *__restrict__ rowsp, int kslices,
+                                                     const double *__restrict__ Y, const int *__restrict__ kidx,
+                                                     const double *__restrict__ w, const double *__restrict__ pm,
+                                                     const CmaesScalars *__restrict__ sc, double *__restrict__ part) {
+  __shared__ double As[RT_KC][RT_LD], Bs[RT_KC][RT_LD];
+  const int nt = (N + RT_T - 1) / RT_T, ntiles = nt * (nt + 1) / 2;
+  const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+  const int slice = xcd + 8 * (local / ntiles);
   int td, te;
-  tri_tile(blockIdx.x, td, te);
-  const int slice = blockIdx.y;
-  const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
-  const int d = td * 16 + li, e = te * 16 + li;
-  const double pmd = d < N ? prevMean[d] : 0.0, pme = e < N ? prevMean[e] : 0.0;
-  // c_mu from mu_eff with k_paths' formula (CMAES.cpp.base:693-694): this
-  // kernel runs concurrently with k_paths, which stores the same value
-  const double effMu = sc->effectiveMu, ca = N + 1.3, cb = N + 2.0;
-  const double ccov1 = 2.0 / (ca * ca + effMu);
-  double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (cb * cb + effMu);
-  if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
-  const double scale = ccovmu / (sc->sigma * sc->sigma);
-  const int per = ((mu + kslices - 1) / kslices + 3) & ~3;
-  const int kbeg = slice * per, kend = (kbeg + per) < mu ? (kbeg + per) : mu;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = kbeg; k0 < kend; k0 += 4) {
-    const int k = k0 + lk;
-    double a = 0.0, b = 0.0;
-    if (k < kend) {
-      const size_t row = (size_t)k * N;  // Y row k = X[idx[k]]
-      const double sk = scale * w[k];
-      if (d < N) a = sk * (X[row + d] - pmd);
-      if (e < N) b = X[row + e] - pme;
-    }
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  tri_tile(local % ntiles, td, te);
+  const bool diagTile = td == te;
+  double scale;
+  if (SHARD) {
+    scale = 1.0 / (sc->sigma * sc->sigma);
+  } else {
+    // c_mu from mu_eff with k_paths' formula (CMAES.cpp.base:693-694): this
+    // kernel runs concurrently with k_paths, which stores the same value
+    const double effMu = sc->effectiveMu, ca = N + 1.3, cb = N + 2.0;
+    const double ccov1 = 2.0 / (ca * ca + effMu);
+    double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (cb * cb + effMu);
+    if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+    scale = ccovmu / (sc->sigma * sc->sigma);
   }
-  // C/D layout: col = lane & 15, row = (lane >> 4) + 4 * r
-  const size_t tiles = gridDim.x;
-  double *out = part + ((size_t)slice * tiles + blockIdx.x) * 256;
+  const int rows = SHARD ? *rowsp : rowsIn;
+  const int per = (((rows + kslices - 1) / kslices) + 3) & ~3;
+  const int kbeg = slice * per, kend = (kbeg + per) < rows ? (kbeg + per) : rows;
+  // staging role: rows r0 + 8q (q < 4) of a chunk, columns 2c, 2c+1 of the tile
+  const int t = threadIdx.x, sr = t >> 5, c2 = 2 * (t & 31);
+  const int colA = td * RT_T + c2, colB = te * RT_T + c2;
+  const bool evenN = (N & 1) == 0;
+  const double pa0 = colA < N ? pm[colA] : 0.0, pa1 = colA + 1 < N ? pm[colA + 1] : 0.0;
+  const double pb0 = colB < N ? pm[colB] : 0.0, pb1 = colB + 1 < N ? pm[colB + 1] : 0.0;
+  double ra[4][2], rb[4][2], rs[4];
+  auto load = [&](int k0) {
 #pragma unroll
-  for (int r = 0; r < 4; r++) out[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+    for (int q = 0; q < 4; q++) {
+      const int k = k0 + sr + 8 * q;
+      ra[q][0] = ra[q][1] = rb[q][0] = rb[q][1] = 0.0;
+      rs[q] = 0.0;
+      if (k < kend) {
+        rs[q] = scale * w[SHARD ? kidx[k] : k];
+        const double *row = Y + (size_t)k * N;
+        if (evenN) {
+          if (colA < N) {
+            const double2 v = *reinterpret_cast<const double2 *>(row + colA);
+            ra[q][0] = v.x, ra[q][1] = v.y;
+          }
+          if (!diagTile && colB < N) {
+            const double2 v = *reinterpret_cast<const double2 *>(row + colB);
+            rb[q][0] = v.x, rb[q][1] = v.y;
+          }
+        } else {
+          if (colA < N) ra[q][0] = row[colA];
+          if (colA + 1 < N) ra[q][1] = row[colA + 1];
+          if (!diagTile && colB < N) rb[q][0] = row[colB];
+          if (!diagTile && colB + 1 < N) rb[q][1] = row[colB + 1];
+        }
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int r = sr + 8 * q;
+      // rows past the slice end have rs = 0: their ŷ is 0 and y finite
+      const double a0 = ra[q][0] - pa0, a1 = ra[q][1] - pa1;
+      const double b0 = diagTile ? a0 : rb[q][0] - pb0, b1 = diagTile ? a1 : rb[q][1] - pb1;
+      *reinterpret_cast<double2 *>(&As[r][c2]) = make_double2(rs[q] * a0, rs[q] * a1);
+      *reinterpret_cast<double2 *>(&Bs[r][c2]) = make_double2(b0, b1);
+    }
+  };
+  const int lane = t & 63, wave = t >> 6, wr = wave >> 1, wc = wave & 1, li = lane & 15, lk = lane >> 4;
+  const bool computes = !(diagTile && wc > wr);  // the upper quarter of a diagonal tile is not needed
+  dbl4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += RT_KC) {
+    __syncthreads();  // the previous chunk's fragments are read
+    stage();
+    __syncthreads();
+    if (k0 + RT_KC < kend) load(k0 + RT_KC);  // in flight during this chunk's MFMAs
+    if (computes) {
+#pragma unroll
+      for (int kk = 0; kk < RT_KC; kk += 4) {
+        const double a0 = As[kk + lk][wr * 32 + li], a1 = As[kk + lk][wr * 32 + 16 + li];
+        const double b0 = Bs[kk + lk][wc * 32 + li], b1 = Bs[kk + lk][wc * 32 + 16 + li];
+        acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+      }
+    }
+  }
+  if (!computes) return;
+  // C/D layout: col = lane & 15, row = (lane >> 4) + 4 r; 16x16 tiles of the
+  // lower triangle indexed TD (TD + 1) / 2 + TE
+  const int nt16 = (N + 15) / 16, ntiles16 = nt16 * (nt16 + 1) / 2;
+  const dbl4 *accs[4] = {&acc00, &acc01, &acc10, &acc11};
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int TD = td * 4 + wr * 2 + (b >> 1), TE = te * 4 + wc * 2 + (b & 1);
+    if (TE > TD || TD >= nt16) continue;
+    double *out = part + ((size_t)slice * ntiles16 + (size_t)TD * (TD + 1) / 2 + TE) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; r++) out[(lk + 4 * r) * 16 + li] = (*accs[b])[r];
+  }
 }
 
 __global__ void __launch_bounds__(256) k_adaptC_combine(int N, int kslices, int ntiles, int diagonal,
@@ -1028,42 +1124,6 @@ __global__ void __launch_bounds__(64) k_shard_mean(int N, int r0, int r1, const 
   part[d] = acc;
   const int i0 = (int)idx[0];
   part[N + d] = (i0 >= r0 && i0 < r1) ? X[(size_t)i0 * N + d] : 0.0;
-}
-
-// rank-μ partial on the matrix cores: as k_rankmu_mfma over the owned
-// selected rows, weights w_k / σ² (cμ is applied after the reduction)
-__global__ void __launch_bounds__(64) k_rankmu_mfma_shard(int N, const int *__restrict__ cntp, int kslices,
-                                                          const double *__restrict__ Y, const int *__restrict__ kidx,
-                                                          const double *__restrict__ w,
-                                                          const double *__restrict__ prevMean,
-                                                          const CmaesScalars *__restrict__ sc,
-                                                          double *__restrict__ part) {
-  int td, te;
-  tri_tile(blockIdx.x, td, te);
-  const int slice = blockIdx.y;
-  const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
-  const int d = td * 16 + li, e = te * 16 + li;
-  const double pmd = d < N ? prevMean[d] : 0.0, pme = e < N ? prevMean[e] : 0.0;
-  const double scale = 1.0 / (sc->sigma * sc->sigma);
-  const int cnt = *cntp;
-  const int per = ((cnt + kslices - 1) / kslices + 3) & ~3;
-  const int kbeg = slice * per, kend = (kbeg + per) < cnt ? (kbeg + per) : cnt;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = kbeg; k0 < kend; k0 += 4) {
-    const int k = k0 + lk;
-    double a = 0.0, b = 0.0;
-    if (k < kend) {
-      const size_t row = (size_t)k * N;
-      const double sk = scale * w[kidx[k]];
-      if (d < N) a = sk * (Y[row + d] - pmd);
-      if (e < N) b = Y[row + e] - pme;
-    }
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-  }
-  const size_t tiles = gridDim.x;
-  double *out = part + ((size_t)slice * tiles + blockIdx.x) * 256;
-#pragma unroll
-  for (int r = 0; r < 4; r++) out[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
 }
 
 __global__ void __launch_bounds__(256) k_part_reduce(int kslices, int ntiles, const double *__restrict__ slices,
@@ -1215,7 +1275,7 @@ struct kg_cmaes_s {
   EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
-  int kslices = 8;
+  int kslices = 8;  // rank-mu K-slices (rankmu_kslices), a multiple of the 8 XCDs
   // population shards
   int shards = 1, shardRank = 0, r0 = 0, r1 = 0;
   int *kidx = nullptr, *shardCnt = nullptr;
@@ -1239,16 +1299,17 @@ struct Stage {
   kg_cmaes_s *h;
   std::string name;
   hipEvent_t a = nullptr, b = nullptr;
-  Stage(kg_cmaes_s *h_, const char *n) : h(h_), name(n) {
+  hipStream_t s;
+  Stage(kg_cmaes_s *h_, const char *n, hipStream_t on = nullptr) : h(h_), name(n), s(on ? on : h_->stream) {
     if (h->profile) {
       (void)hipEventCreate(&a);
       (void)hipEventCreate(&b);
-      (void)hipEventRecord(a, h->stream);
+      (void)hipEventRecord(a, s);
     }
   }
   ~Stage() {
     if (h->profile) {
-      (void)hipEventRecord(b, h->stream);
+      (void)hipEventRecord(b, s);
       h->pending.emplace_back(name, a, b);
     }
   }
@@ -1468,6 +1529,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   if (P2 < SORT_CHUNK) P2 = SORT_CHUNK;
   rc |= dalloc(&h->sortKey, P2) | dalloc(&h->sortVal, P2);
   const int nt = (N + 15) / 16;
+  h->kslices = rankmu_kslices(N, h->mu);
   rc |= dalloc(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
   rc |= dalloc(&h->kidx, h->mu) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
   if (rc) {
@@ -1744,9 +1806,10 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     KG_HIP(hipEventRecord(h->evY, h->stream));
     KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
     if (h->cfg.cov_mode == KG_COV_MFMA) {
-      const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
-      hipLaunchKernelGGL(k_rankmu_mfma, dim3(ntiles, h->kslices), dim3(64), 0, h->stream2, N, mu, h->kslices, h->Y,
-                         h->idx, h->w, h->prevMean, h->sc, h->covPart);
+      Stage st(h, "rankmu_mfma", h->stream2);
+      hipLaunchKernelGGL(k_rankmu_tile<false>, dim3(rankmu_grid(N, h->kslices)), dim3(256), 0, h->stream2, N, mu,
+                         (const int *)nullptr, h->kslices, h->Y, (const int *)nullptr, h->w, h->prevMean, h->sc,
+                         h->covPart);
     } else {
       hipLaunchKernelGGL(k_rankmu_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0,
                          h->stream2, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
@@ -1793,8 +1856,8 @@ int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
   {
     Stage st(h, "covariance");
     const int nt = (N + 15) / 16, ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL(k_rankmu_mfma_shard, dim3(ntiles, h->kslices), dim3(64), 0, h->stream, N, h->shardCnt,
-                       h->kslices, h->Y, h->kidx, h->w, h->mean, h->sc, h->covPart);  // mean not yet advanced
+    hipLaunchKernelGGL(k_rankmu_tile<true>, dim3(rankmu_grid(N, h->kslices)), dim3(256), 0, h->stream, N, 0,
+                       h->shardCnt, h->kslices, h->Y, h->kidx, h->w, h->mean, h->sc, h->covPart);  // mean not yet advanced
     hipLaunchKernelGGL(k_part_reduce, dim3(ntiles), dim3(256), 0, h->stream, h->kslices, ntiles, h->covPart,
                        h->part + 2 * (size_t)N);
     KG_HIP(hipGetLastError());
