@@ -486,6 +486,456 @@ __global__ void k_tm_cv_exp(int P, const double *__restrict__ ll, const TmDev *_
   if (i < P) E[i] = exp_cr((ll[i] - dev->llmaxCv) * (x - rho));
 }
 
+// minSearch :712-779 on the device: the whole one-dimensional nmsimplex
+// loop (the host's min_search below, comparison for comparison) in one
+// cooperative launch.  Workgroup 0 runs the simplex; NM_W worker
+// workgroups hold P/NM_W log-likelihoods each in LDS and evaluate the
+// points of a round (every possible next point of an iteration, as the
+// host's batches) as double-double sums of d = E - 1 with the device exp
+// (<= 1 ulp; its error joins the bound as 16 u max/mean).  A round is one
+// agent-scope release/acquire broadcast of the points and one fan-in of
+// per-worker partial records, which the controller adds in a fixed tree
+// (deterministic).  Comparisons are decided on the same rigorous
+// intervals as the host path, so each one equals the comparison of the
+// reference's values.  Values the intervals cannot separate (or
+// degenerate ones) need the reference's exact value, which only the host
+// forms (x87 long double recurrences, cv2_tail): the search then stops
+// with status 1 and names the points; the host evaluates them and
+// relaunches with the values in `tab`, where every later evaluation of
+// those points finds them, so the search replays identically up to that
+// comparison and then decides it exactly, as the host path does.  On
+// success the final simplex and the iteration count are left for the
+// exact stored minimum (k_tm_nm_exp): one round trip per generation
+// instead of one per iteration.
+constexpr int NM_TAB = 8, NM_PTS = 8, NM_W = 64, NM_TPB = 256, NM_LDS = 4096;
+struct NmTab {
+  double x[NM_TAB], y[NM_TAB];
+  int n;
+};
+struct NmOut {
+  double X[2], y[2], need[2];
+  long long iters;
+  int status, lo, nneed, loExact;  // status 0 done, 1 exact values needed, 2 no progress (the host searches)
+  unsigned evals, rounds;
+  // phase times (s_memrealtime, 100 MHz ticks): controller publish+wait,
+  // combine, simplex logic; worker 1 wait, evaluate, reduce+publish
+  unsigned long long tc[3], tw[3];
+};
+struct NmPart {
+  double s_hi, s_lo, q_hi, q_lo, mx, flags;  // flags: bit 0 non-finite, bit 1 some argument != 0
+};
+struct NmSync {
+  double x[NM_PTS];
+  unsigned long long n, quit;
+  unsigned long long seq;         // round published by the controller
+  unsigned long long done[NM_W];  // round each worker has published
+  NmPart part[NM_W][NM_PTS];
+};
+struct NmVal {
+  double x, y, eps;
+  int exact;
+};
+constexpr unsigned long long NM_SPIN_LIMIT = 1ull << 24;
+
+// Hand-offs between the controller and the workers (MI355X_MICROARCH.md,
+// inter-workgroup visibility, the sc1 form): every handed-off byte is
+// stored and loaded with agent-scope relaxed atomics (global_store/load
+// sc1, write-through / L1-bypassing), every storing wave drains its stores
+// (vmcnt(0)) before a workgroup barrier, then one lane stores the flag
+// (sc1); the consumer polls the flag with sc1 loads and loads the bytes
+// with sc1 loads after its poll matched (other waves behind a barrier).
+// No L2 write-back or invalidate per round.
+__device__ inline unsigned long long nm_ld(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double nm_ldd(const double *p) {
+  return __longlong_as_double((long long)nm_ld((const unsigned long long *)p));
+}
+__device__ inline void nm_st(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void nm_std(double *p, double v) { nm_st((unsigned long long *)p, (unsigned long long)__double_as_longlong(v)); }
+__device__ inline void nm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ inline NmPart nm_part_add(NmPart a, NmPart b) {
+  const dd s = dd_add(dd{a.s_hi, a.s_lo}, dd{b.s_hi, b.s_lo}), q = dd_add(dd{a.q_hi, a.q_lo}, dd{b.q_hi, b.q_lo});
+  const int f = (int)a.flags | (int)b.flags;
+  return NmPart{s.hi, s.lo, q.hi, q.lo, fmax(a.mx, b.mx), (double)f};
+}
+// down-shift within 32-lane segments
+__device__ inline NmPart nm_part_shfl32(NmPart a, int off) {
+  return NmPart{__shfl_down(a.s_hi, off, 32), __shfl_down(a.s_lo, off, 32), __shfl_down(a.q_hi, off, 32),
+                __shfl_down(a.q_lo, off, 32), __shfl_down(a.mx, off, 32), __shfl_down(a.flags, off, 32)};
+}
+__device__ inline NmPart nm_part_ld(const NmPart *p) {
+  const double *d = (const double *)p;
+  return NmPart{nm_ldd(d), nm_ldd(d + 1), nm_ldd(d + 2), nm_ldd(d + 3), nm_ldd(d + 4), nm_ldd(d + 5)};
+}
+__device__ inline void nm_part_st(NmPart *p, const NmPart &v) {
+  double *d = (double *)p;
+  nm_std(d, v.s_hi);
+  nm_std(d + 1, v.s_lo);
+  nm_std(d + 2, v.q_hi);
+  nm_std(d + 3, v.q_lo);
+  nm_std(d + 4, v.mx);
+  nm_std(d + 5, v.flags);
+}
+
+__global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__restrict__ ll,
+                                                          const TmDev *__restrict__ dev, double rho, double target,
+                                                          NmTab tab, NmSync *__restrict__ S, NmOut *__restrict__ out) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 5, sub = tid & 31;  // point / segment lane of the 32-wide reductions
+  const double llmax = dev->llmaxCv;
+  if (blockIdx.x > 0) {
+    // ------------------------------------------------------------ worker
+    __shared__ double sll[NM_LDS];
+    __shared__ double sx[NM_PTS];
+    __shared__ int sn, squit;
+    __shared__ NmPart red[NM_PTS][NM_TPB];
+    const int w = blockIdx.x - 1, chunk = (P + NM_W - 1) / NM_W;
+    const int i0 = w * chunk < P ? w * chunk : P, i1 = (w + 1) * chunk < P ? (w + 1) * chunk : P;
+    const bool inLds = chunk <= NM_LDS;
+    if (inLds)
+      for (int i = i0 + tid; i < i1; i += NM_TPB) sll[i - i0] = ll[i];
+    unsigned long long tw0 = 0, tw1 = 0, tw2 = 0;
+    for (unsigned long long round = 1;; round++) {
+      const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) {
+        unsigned long long spins = 0;
+        while (nm_ld(&S->seq) < round && ++spins < NM_SPIN_LIMIT) __builtin_amdgcn_s_sleep(1);
+        if (spins >= NM_SPIN_LIMIT) {
+          squit = 1;
+        } else {
+          squit = (int)nm_ld(&S->quit);
+          sn = (int)nm_ld(&S->n);
+          for (int k = 0; k < NM_PTS; k++) sx[k] = nm_ldd(&S->x[k]);
+        }
+      }
+      __syncthreads();
+      if (squit) {
+        if (tid == 0 && w == 0) out->tw[0] = tw0, out->tw[1] = tw1, out->tw[2] = tw2;
+        return;
+      }
+      const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
+      const int n = sn;
+      NmPart acc[NM_PTS];
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++) acc[k] = NmPart{0, 0, 0, 0, 0, 0};
+      int fl[NM_PTS];
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++) fl[k] = 0;
+      for (int i = i0 + tid; i < i1; i += NM_TPB) {
+        const double a = (inLds ? sll[i - i0] : ll[i]) - llmax;
+#pragma unroll
+        for (int k = 0; k < NM_PTS; k++) {
+          if (k < n) {
+            const double arg = a * (sx[k] - rho);
+            const double e = exp(arg);
+            fl[k] |= (!isfinite(e) ? 1 : 0) | (arg != 0.0 ? 2 : 0);
+            const double d = e - 1.0;
+            const dd s2 = dd_add(dd{acc[k].s_hi, acc[k].s_lo}, dd{d, 0.0});
+            const dd q2 = dd_add(dd{acc[k].q_hi, acc[k].q_lo}, dd_tp(d, d));
+            acc[k].s_hi = s2.hi, acc[k].s_lo = s2.lo, acc[k].q_hi = q2.hi, acc[k].q_lo = q2.lo;
+            acc[k].mx = e > acc[k].mx ? e : acc[k].mx;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++) {
+        acc[k].flags = (double)fl[k];
+        if (k < n) red[k][tid] = acc[k];
+      }
+      __syncthreads();
+      const unsigned long long tcomp = __builtin_amdgcn_s_memrealtime();
+      // point grp: 8 serial adds per segment lane, then a 32-lane tree
+      if (grp < n) {
+        NmPart v = red[grp][sub];
+        for (int j = 1; j < NM_TPB / 32; j++) v = nm_part_add(v, red[grp][sub + 32 * j]);
+        for (int off = 16; off > 0; off >>= 1) v = nm_part_add(v, nm_part_shfl32(v, off));
+        if (sub == 0) nm_part_st(&S->part[w][grp], v);
+        nm_drain();
+      }
+      __syncthreads();  // every storing wave has drained its stores
+      if (tid == 0) nm_st(&S->done[w], round);
+      const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+      tw0 += tb - ta;
+      tw1 += tcomp - tb;
+      tw2 += te - tcomp;
+    }
+  }
+  // -------------------------------------------------------------- controller
+  __shared__ NmVal val[NM_PTS];
+  __shared__ double spts[NM_PTS];
+  __shared__ int sfail;
+  unsigned long long round = 0;
+  unsigned evals = 0;
+  int status = 0, nneed = 0;
+  double need0 = 0.0, need1 = 0.0;
+  auto request = [&](const NmVal &v) __attribute__((always_inline)) {
+    // branch-free (keeps need0 / need1 in registers)
+    const bool first = !v.exact && nneed == 0;
+    const bool second = !v.exact && nneed == 1 && __double_as_longlong(v.x) != __double_as_longlong(need0);
+    need0 = first ? v.x : need0;
+    need1 = second ? v.x : need1;
+    nneed += (first || second) ? 1 : 0;
+    status = 1;
+  };
+  // the last round's points and values stay in LDS (spts, val, sbn) until
+  // the next round
+  __shared__ int sbn;
+  // one round over pts[0..n): broadcast, fan-in, fixed-order combine
+  unsigned long long tc0 = 0, tc1 = 0, tc2 = 0, tlast = __builtin_amdgcn_s_memrealtime();
+  const dd invP = dd_div(dd{1.0, 0.0}, dd{(double)P, 0.0});
+  auto run_round = [&](const double *pts, int n) __attribute__((always_inline)) {
+    const unsigned long long ra = __builtin_amdgcn_s_memrealtime();
+    tc2 += ra - tlast;
+    round++;
+    evals += n;
+    __syncthreads();  // every thread has read the previous round's spts / val
+    if (tid == 0) {
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++) {
+        const double x = k < n ? pts[k] : 0.0;
+        nm_std(&S->x[k], x);
+        spts[k] = x;
+      }
+      nm_st(&S->n, (unsigned long long)n);
+      nm_st(&S->quit, 0ull);
+      sbn = n;
+      nm_drain();
+      nm_st(&S->seq, round);
+    }
+    if (wid == 0) {
+      unsigned long long spins = 0;
+      for (;;) {
+        const bool ok = nm_ld(&S->done[lane]) >= round;  // NM_W == 64: one lane per worker
+        if (__all(ok)) break;
+        if (++spins >= NM_SPIN_LIMIT) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0) sfail = spins >= NM_SPIN_LIMIT;
+    }
+    __syncthreads();
+    const unsigned long long rb = __builtin_amdgcn_s_memrealtime();
+    // point grp over the 64 workers' records: 2 per segment lane, then a 32-lane tree
+    if (grp < n) {
+      const int k = grp;
+      NmPart v = nm_part_add(nm_part_ld(&S->part[sub][k]), nm_part_ld(&S->part[sub + 32][k]));
+      for (int off = 16; off > 0; off >>= 1) v = nm_part_add(v, nm_part_shfl32(v, off));
+      if (sub == 0) {
+        const dd Sd{v.s_hi, v.s_lo}, Qd{v.q_hi, v.q_lo};
+        const dd dmean = dd_mul(Sd, invP);
+        const dd ss = dd_add(Qd, dd_mul(dd{-Sd.hi, -Sd.lo}, dmean));
+        const double var = (ss.hi + ss.lo) / (double)(P - 1);
+        const dd mean = dd_add(dmean, dd{1.0, 0.0});
+        const double meand = mean.hi + mean.lo;
+        const double cv = sqrt(var > 0.0 ? var : 0.0) / meand;
+        double c = cv - target;
+        c *= c;
+        const double ratio = v.mx / meand;
+        // CvSearch::get's bound, plus 16 u max/mean for the device exp
+        const double u = 1.1102230246251565e-16, acv = fabs(cv);
+        const double dc = 1e-13 * acv + 32.0 * u * ratio + 4.0 * u * u / (acv > 1e-300 ? acv : 1e-300);
+        const double eps = 2.0 * fabs(cv - target) * dc + dc * dc + 4.0 * u * fabs(c) + 1e-300;
+        // every argument exactly 0: every E is exactly 1 and cv2_tail gives target^2
+        const int vf = (int)v.flags;
+        const bool allOne = vf == 0 && P > 1;
+        const bool bad = (vf & 1) || !isfinite(c) || !(meand > 0.0) || !isfinite(ratio) || var < 0.0 ||
+                         !isfinite(eps);
+        const double x = spts[k];
+        val[k] = allOne ? NmVal{x, target * target, 0.0, 1} : NmVal{x, c, eps, bad ? -1 : 0};
+      }
+    }
+    __syncthreads();
+    if (sfail) status = 2;
+    tlast = __builtin_amdgcn_s_memrealtime();
+    tc0 += rb - ra;
+    tc1 += tlast - rb;
+  };
+  // the value at x; `slot` is where the round's batch put x (checked)
+  auto get = [&](double x, NmVal &v, int slot) __attribute__((always_inline)) {
+    bool found = false;
+    if (tab.n > 0) {
+#pragma unroll
+      for (int t = 0; t < NM_TAB; t++)
+        if (!found && t < tab.n && __double_as_longlong(tab.x[t]) == __double_as_longlong(x)) {
+          v = NmVal{x, tab.y[t], 0.0, 1};
+          found = true;
+        }
+      if (found) return;
+    }
+    if (slot < sbn && __double_as_longlong(spts[slot]) == __double_as_longlong(x)) {
+      v = val[slot];
+      found = true;
+    }
+    for (int k = 0; !found && k < sbn; k++)
+      if (__double_as_longlong(spts[k]) == __double_as_longlong(x)) {
+        v = val[k];
+        found = true;
+        break;
+      }
+    if (!found) {
+      double one[NM_PTS] = {x, 0, 0, 0, 0, 0, 0, 0};
+      run_round(one, 1);
+      v = val[0];
+    }
+    if (v.exact < 0) {  // degenerate: the host's exact value decides
+      v.exact = 0;
+      request(v);
+    }
+  };
+  // a < b (or a <= b): exact values compare exactly, others on their
+  // intervals; undecidable -> request the inexact operands
+  auto cmp = [&](const NmVal &a, const NmVal &b, bool orEqual) __attribute__((always_inline)) -> bool {
+    if (a.exact && b.exact) return orEqual ? a.y <= b.y : a.y < b.y;
+    if (a.y + a.eps < b.y - b.eps) return true;
+    if (a.y - a.eps > b.y + b.eps) return false;
+    request(a);
+    request(b);
+    return false;
+  };
+  const int MaxIter = 1000;
+  const double Tol = 1e-12, Step = 1e-8;
+  double X0 = rho, X1 = rho + Step;
+  NmVal Y0, Y1;
+  long long iter = 0;
+  int lo = 0;
+  {
+    const double p2[NM_PTS] = {X0, X1, 0, 0, 0, 0, 0, 0};
+    run_round(p2, 2);
+    get(X0, Y0, 0);
+    if (!status) get(X1, Y1, 1);
+  }
+  while (status == 0) {
+    iter++;
+    int hi = 0;
+    lo = 0;
+    if (cmp(Y1, Y0, false)) {
+      lo = 1;
+    } else {
+      if (status) break;
+      if (cmp(Y0, Y1, false)) hi = 1;
+    }
+    if (status) break;
+    const double Xhi = hi ? X1 : X0, Xlo = lo ? X1 : X0;
+    const double mp = hi ? X0 : X1;
+    const double xc = mp - (-1.0) * (mp - Xhi);
+    {
+      // every point this iteration may evaluate (the host's batch)
+      double pts[NM_PTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int np = 0;
+      pts[np++] = xc;
+      pts[np++] = mp - (-2.0) * (mp - Xhi);
+      pts[np++] = mp - 0.5 * (mp - Xhi);
+      pts[np++] = mp - 0.5 * (mp - xc);
+      // shrink towards lo, with and without X[hi] = xc (1-D: the vertex != lo)
+      const double Xo = lo ? X0 : X1;  // the vertex that is not lo
+      const double XoR = (hi == lo) ? Xo : xc, XloR = (hi == lo) ? xc : Xlo;
+      pts[np++] = 0.5 * (Xo + Xlo);
+      pts[np++] = 0.5 * (XoR + XloR);
+      run_round(pts, np);
+      if (status) break;
+    }
+    NmVal v;
+    get(xc, v, 0);
+    if (status) break;
+    const NmVal Ylo = lo ? Y1 : Y0;
+    const bool better = cmp(v, Ylo, false);
+    if (status) break;
+    if (better) {
+      NmVal v2;
+      const double xc2 = mp - (-2.0) * (mp - Xhi);
+      get(xc2, v2, 1);
+      if (status) break;
+      const bool b2 = cmp(v2, Ylo, false);
+      if (status) break;
+      const double nx = b2 ? xc2 : xc;
+      const NmVal ny = b2 ? v2 : v;
+      if (hi) X1 = nx, Y1 = ny;
+      else X0 = nx, Y0 = ny;
+    } else {
+      const bool worse = cmp(Y0, v, false);  // Y[s_hi], s_hi = 0
+      if (status) break;
+      if (worse) {
+        const bool r1 = cmp(v, hi ? Y1 : Y0, true);
+        if (status) break;
+        if (r1) {
+          if (hi) X1 = xc, Y1 = v;
+          else X0 = xc, Y0 = v;
+        }
+        NmVal v2;
+        const double xh = hi ? X1 : X0;
+        const double xc2 = mp - 0.5 * (mp - xh);
+        get(xc2, v2, r1 ? 3 : 2);
+        if (status) break;
+        const bool r2 = cmp(v2, hi ? Y1 : Y0, true);
+        if (status) break;
+        if (r2) {
+          if (hi) X1 = xc2, Y1 = v2;
+          else X0 = xc2, Y0 = v2;
+        } else {
+          // X[i] = 0.5 (X[i] + X[lo]) for i != lo
+          if (lo == 0) {
+            X1 = 0.5 * (X1 + X0);
+            get(X1, Y1, r1 ? 5 : 4);
+          } else {
+            X0 = 0.5 * (X0 + X1);
+            get(X0, Y0, r1 ? 5 : 4);
+          }
+          if (status) break;
+        }
+      } else {
+        if (hi) X1 = xc, Y1 = v;
+        else X0 = xc, Y0 = v;
+      }
+    }
+    const bool r = cmp(Y1, Y0, false);
+    if (status) break;
+    lo = r ? 1 : 0;
+    const double center = (X0 + X1) / 2;
+    double ssz = 0.0;
+    ssz += fabs(X0 - center);
+    ssz += fabs(X1 - center);
+    if (!(ssz / 2.0 < Tol) && iter < MaxIter) continue;
+    break;
+  }
+  if (tid == 0) {
+    nm_st(&S->quit, 1ull);
+    nm_drain();
+    nm_st(&S->seq, round + 1);  // workers leave
+    const NmVal Ylo = lo ? Y1 : Y0;
+    out->X[0] = X0;
+    out->X[1] = X1;
+    out->y[0] = Y0.y;
+    out->y[1] = Y1.y;
+    out->need[0] = need0;
+    out->need[1] = need1;
+    out->iters = iter;
+    out->status = status;
+    out->lo = lo;
+    out->nneed = nneed;
+    out->loExact = status ? 0 : Ylo.exact;
+    out->evals = evals;
+    out->rounds = (unsigned)round;
+    out->tc[0] = tc0;
+    out->tc[1] = tc1;
+    out->tc[2] = tc2 + (__builtin_amdgcn_s_memrealtime() - tlast);
+  }
+}
+
+// the exponentials (exp_cr, k_tm_cv_exp's values) of the points whose
+// exact value the host forms next: X[lo] after a finished search, the
+// requested points after status 1
+__global__ void k_tm_nm_exp(int P, const double *__restrict__ ll, const TmDev *__restrict__ dev, double rho,
+                            const NmOut *__restrict__ o, double *__restrict__ E) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+  if (i >= P) return;
+  const int nE = o->status == 1 ? o->nneed : (o->status == 0 && !o->loExact ? 1 : 0);
+  if (j >= nE) return;
+  const double x = o->status == 1 ? o->need[j] : o->X[o->lo];
+  E[(size_t)j * P + i] = exp_cr((ll[i] - dev->llmaxCv) * (x - rho));
+}
+
 // processGeneration :284-296: w_i = exp(ll_i (rho - rho_prev) - max)
 __global__ void k_tm_lw_exp(int P, const double *__restrict__ ll, double drho, const TmDev *__restrict__ dev,
                             double *__restrict__ E) {
@@ -936,6 +1386,11 @@ struct kg_tmcmc_s {
   unsigned long long cvSeq = 0;
   void *cvPart = nullptr;                  // CvPart[(CV_MAX_PTS + 1) * CV_BLOCKS]
   bool exactSearch = false;                // KORALI_AMD_TMCMC_EXACT_SEARCH=1: every cv2 on the host
+  bool hostSearch = false;                 // KORALI_AMD_TMCMC_HOST_SEARCH=1: simplex loop on the host (min_search)
+  NmOut *dNm = nullptr, *hNm = nullptr;    // k_tm_nm_search result (device, pinned host)
+  NmSync *nmSync = nullptr;                // its controller / worker hand-off records
+  size_t nmRelaunches = 0, nmFallbacks = 0, nmEvals = 0, nmRounds = 0;
+  double nmTime[6] = {0, 0, 0, 0, 0, 0};  // ms: controller wait, combine, logic; worker wait, evaluate, reduce
   size_t exactEvals = 0;
   unsigned *hSrc = nullptr;
   TmDev *hDev = nullptr;
@@ -967,7 +1422,8 @@ struct kg_tmcmc_s {
          maxLoglikelihood = -INFINITY, chainCount = 0, acceptedSamplesCount = 0, proposalsAcceptanceRate = 0,
          selectionAcceptanceRate = 0, dbCount = 0, modelEvaluationCount = 0, minSearchIterations = 0,
          currentBurnIn = 0;
-  double exactEvalsD = 0;  // diagnostics: host-exact cv2 evaluations so far
+  double exactEvalsD = 0;
+  double nmRelaunchesD = 0, nmEvalsD = 0, nmRoundsD = 0, nmFallbacksD = 0;  // diagnostics: device-search relaunches after host-exact values  // diagnostics: host-exact cv2 evaluations so far
   double btpeDraws = 0;    // diagnostics: multinomial binomials drawn by BTPE (n p >= 14)
   bool devPending = false;  // accepted count / maxLoglikelihood not yet read back
   // profiling
@@ -1323,6 +1779,79 @@ int min_search(kg_tmcmc_s *h, double exponent, double objCov, double &xmin, doub
   return 0;
 }
 
+// minSearch with the simplex loop on the device (k_tm_nm_search): one
+// launch and one round trip per generation, plus one per comparison the
+// intervals could not decide (the host forms those values exactly and
+// relaunches).  Equal to min_search result for result.
+int cv2_exact(kg_tmcmc_s *h, double exponent, double x, double &y);
+
+int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmin, double &fmin, size_t &iters) {
+  const double Tol = 1e-12;
+  const int P = h->P;
+  NmTab tab{};
+  for (;;) {
+    KG_HIP(hipMemsetAsync(h->nmSync, 0, sizeof(NmSync), h->stream));
+    int Pa = P;
+    const double *llp = h->dbLL;
+    const TmDev *devp = h->dev;
+    double rho = exponent, tgt = objCov;
+    NmSync *syncp = h->nmSync;
+    NmOut *outp = h->dNm;
+    void *args[] = {&Pa, (void *)&llp, (void *)&devp, &rho, &tgt, &tab, &syncp, &outp};
+    // co-residency of the controller and its workers is guaranteed by the
+    // cooperative launch (it fails rather than under-schedules)
+    if (hipLaunchCooperativeKernel((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      h->nmFallbacks++;
+      return min_search(h, exponent, objCov, xmin, fmin, iters);
+    }
+    hipLaunchKernelGGL(k_tm_nm_exp, dim3(nblk(P, 256), 2), dim3(256), 0, h->stream, P, h->dbLL, h->dev, exponent,
+                       h->dNm, h->E);
+    KG_HIP(hipGetLastError());
+    KG_HIP(hipMemcpyAsync(h->hNm, h->dNm, sizeof(NmOut), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipMemcpyAsync(h->hE, h->E, (size_t)P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    const NmOut o = *h->hNm;
+    h->nmEvals += o.evals;
+    h->nmRounds += o.rounds;
+    for (int q = 0; q < 3; q++) h->nmTime[q] += o.tc[q] * 1e-5, h->nmTime[3 + q] += o.tw[q] * 1e-5;  // ms
+    if (o.status == 0) {
+      double ylo = o.y[o.lo];
+      if (!o.loExact) {
+        ylo = cv2_tail(h->hE, P, objCov, h->wtmp.data());
+        h->exactEvals++;
+      }
+      fmin = 0;
+      xmin = 0.0;
+      if (ylo <= Tol) {
+        fmin = ylo;
+        xmin = o.X[o.lo];
+      }
+      if (xmin >= 1.0) {
+        double y1 = 0;
+        if (cv2_exact(h, exponent, 1.0, y1)) return 1;
+        fmin = y1;
+        xmin = 1.0;
+      }
+      iters = (size_t)o.iters;
+      return 0;
+    }
+    if (o.status != 1 || o.nneed < 1 || tab.n + o.nneed > NM_TAB) {  // the host search decides
+      h->nmFallbacks++;
+      return min_search(h, exponent, objCov, xmin, fmin, iters);
+    }
+    if (o.nneed > 1) KG_HIP(hipMemcpy(h->hE + P, h->E + P, (size_t)P * sizeof(double), hipMemcpyDeviceToHost));
+    for (int j = 0; j < o.nneed; j++) {
+      tab.x[tab.n] = o.need[j];
+      tab.y[tab.n] = cv2_tail(h->hE + (size_t)j * P, P, objCov, h->wtmp.data());
+      tab.n++;
+      h->exactEvals++;
+    }
+    h->nmRelaunches++;
+  }
+}
+
 // the reference's squared CoV difference at x, exactly
 int cv2_exact(kg_tmcmc_s *h, double exponent, double x, double &y) {
   CvSearch cv{h, exponent, h->cfg.target_cov};
@@ -1447,7 +1976,7 @@ XchMap tm_xch_map(kg_tmcmc_s *h, size_t &total) {
 
 struct TmField {
   double *dev;   // device vector, or nullptr for a host scalar
-  double *host;  // host scalar
+  double *host;  // host scalar (or host array of n)
   size_t n;
 };
 
@@ -1497,6 +2026,14 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Min Search Iterations", minSearchIterations)
   SCA("Current Burn In", currentBurnIn)
   SCA("Exact Search Evaluations", exactEvalsD)
+  SCA("Device Search Relaunches", nmRelaunchesD)
+  SCA("Device Search Evaluations", nmEvalsD)
+  SCA("Device Search Rounds", nmRoundsD)
+  if (k == "Device Search Phase Times") {  // ms: controller wait, combine, logic; worker wait, evaluate, reduce
+    r = {nullptr, h->nmTime, 6};
+    return true;
+  }
+  SCA("Device Search Fallbacks", nmFallbacksD)
   SCA("BTPE Binomial Draws", btpeDraws)
 #undef VEC
 #undef SCA
@@ -1584,11 +2121,13 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
   rc |= tdalloc(&h->fA, PN + 2) | tdalloc(&h->fB, PN + 2);
   rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
+  rc |= tdalloc((char **)&h->dNm, sizeof(NmOut)) | tdalloc((char **)&h->nmSync, sizeof(NmSync));
   if (rc) {
     delete h;
     return 1;
   }
-  KG_HIP(hipHostMalloc(&h->hE, (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hE, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hNm, sizeof(NmOut), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hSrc, (size_t)P * sizeof(unsigned), hipHostMallocDefault));
@@ -1603,6 +2142,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   {
     const char *ev = getenv("KORALI_AMD_TMCMC_EXACT_SEARCH");
     h->exactSearch = ev && ev[0] == '1';
+    const char *hs = getenv("KORALI_AMD_TMCMC_HOST_SEARCH");
+    h->hostSearch = hs && hs[0] == '1';
   }
   h->wtmp.resize(P);
   h->nsel.resize(P);
@@ -1671,10 +2212,10 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
                   (void *)h->dev, h->cvPart, (void *)h->pairs, (void *)h->pend, (void *)h->sch, (void *)h->Zx,
                   (void *)h->dLen, (void *)h->xch,
-                  (void *)h->fA, (void *)h->fB})
+                  (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
-                  (void *)h->hSch, (void *)h->hLenD})
+                  (void *)h->hSch, (void *)h->hLenD, (void *)h->hNm})
     if (p) (void)hipHostFree(p);
   for (auto *r : h->priorRng) delete r;
   for (auto &t : h->pending) {
@@ -1883,11 +2424,17 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
   size_t iters = 0;
   {
     HostClock hc(h, "min_search");
-    if (min_search(h, h->annealingExponent, h->cfg.target_cov, xmin, fmin, iters)) return 1;
+    const bool onHost = h->exactSearch || h->hostSearch;
+    if ((onHost ? min_search : min_search_device)(h, h->annealingExponent, h->cfg.target_cov, xmin, fmin, iters))
+      return 1;
   }
   if (tm_sync_dev(h)) return 1;
   h->minSearchIterations = (double)iters;
   h->exactEvalsD = (double)h->exactEvals;
+  h->nmRelaunchesD = (double)h->nmRelaunches;
+  h->nmEvalsD = (double)h->nmEvals;
+  h->nmRoundsD = (double)h->nmRounds;
+  h->nmFallbacksD = (double)h->nmFallbacks;
   h->previousAnnealingExponent = h->annealingExponent;
   {
     const double pe = h->previousAnnealingExponent;
@@ -2009,7 +2556,7 @@ int kg_tmcmc_get_field(kg_tmcmc_t h, const char *name, double *out, size_t n) {
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
   if (tm_sync_dev(h)) return 1;
   if (r.host) {
-    *out = *r.host;
+    for (size_t q = 0; q < n; q++) out[q] = r.host[q];
     return 0;
   }
   KG_HIP(hipMemcpyAsync(out, r.dev, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
@@ -2023,7 +2570,7 @@ int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t 
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
   if (tm_sync_dev(h)) return 1;
   if (r.host) {
-    *r.host = *in;
+    for (size_t q = 0; q < n; q++) r.host[q] = in[q];
     return 0;
   }
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));

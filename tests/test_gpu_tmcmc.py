@@ -128,13 +128,16 @@ def test_tmcmc_seeded_run_matches_oracle(N, P, gens, shared):
 
 @pytest.mark.parametrize("seed,target_cov", [(11, 0.5), (12, 2.0), (13, 1.0)])
 def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov):
-    """The annealing search decides on device-side interval estimates and
-    falls back to the host's exact evaluation only when they overlap: the
-    whole run must equal the all-exact search and the oracle."""
+    """The annealing search decides on interval estimates and falls back to
+    the host's exact evaluation only when they overlap, with the simplex loop
+    on the device (default: k_tm_nm_search, relaunched with host-exact
+    values) or on the host (min_search): both runs must equal the all-exact
+    search and the oracle."""
     N, P = 6, 1024
     runs = []
-    for exact in ("0", "1"):
+    for exact, host in (("0", "0"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("KORALI_AMD_TMCMC_EXACT_SEARCH", exact)
+        monkeypatch.setenv("KORALI_AMD_TMCMC_HOST_SEARCH", host)
         dev, o, ndist = seeded_pair(N, P, shared=True, seed=seed, target_cov=target_cov)
         hist = []
         for g in range(1, 30):
@@ -144,7 +147,7 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
             if dev["Annealing Exponent"][0] >= 1.0:
                 break
         runs.append((hist, dev["Exact Search Evaluations"][0]))
-        if exact == "0":
+        if exact == "0" and host == "0":
             for g in range(1, len(hist) + 1):
                 o.generation(g)
                 assert o["Annealing Exponent"][0] == hist[g - 1][0], g
@@ -152,8 +155,9 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
                 assert o["LogEvidence"][0] == hist[g - 1][2], g
                 assert o["Covariance Matrix"].tobytes() == hist[g - 1][3], g
     assert runs[0][0] == runs[1][0]
-    # the interval path needs far fewer exact host evaluations
-    assert runs[0][1] < runs[1][1]
+    assert runs[2][0] == runs[1][0]
+    # the interval paths need far fewer exact host evaluations
+    assert runs[0][1] < runs[1][1] and runs[2][1] < runs[1][1]
 
 
 def compare_state(dev, o, g):
