@@ -61,8 +61,10 @@ STAGE_KERNELS = {
     "rankmu_mfma": ["kg::k_rankmu_tile"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
     "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", "kg::k_mean", "kg::k_paths"],
+    # C3 (TMCMC): the weighted mean / covariance stage
+    "mean_cov": ["kg::k_tm_factors_mean", "kg::k_tm_wsum<false>", "kg::k_tm_factors_cov", "kg::k_tm_wsum<true>"],
 }
-PROFILE_ROUND = "r1"
+PROFILE_ROUND = "r2"
 
 
 def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
@@ -471,6 +473,8 @@ def run_c3(args):
                 break
     exps[min(r, len(exps) - 1)].synchronize()
     elapsed = time.perf_counter() - t0
+    for e in exps:
+        e.close()
     # stage times on a fresh run
     dev = c3_experiment(4242)
     dev.profile(True)
@@ -485,11 +489,15 @@ def run_c3(args):
         ms, n = dev.profile_read(st)
         if n:
             stages[st] = ms / n
-    search = {"generations": g, "exact_host_evaluations_per_generation": dev["Exact Search Evaluations"][0] / g}
+    search = {"generations": g, "exact_host_evaluations_per_generation": dev["Exact Search Evaluations"][0] / g,
+              "device_search_rounds_per_generation": dev["Device Search Rounds"][0] / g,
+              "device_search_relaunches": dev["Device Search Relaunches"][0]}
+    dev.close()
     flops = c3_stage_flops(C3_N, C3_P)
     kernels = {k: v for k, v in stages.items() if k in flops}
     dominant = max(kernels, key=kernels.get)
     achieved = flops[dominant] / (stages[dominant] * 1e-3) / 1e12
+    c3_traffic, _ = pmc_traffic(dominant, "c3_pmc_traffic.csv")
     out = {
         "metric": "TMCMC generations/sec, 32-dim Gaussian posterior, P=8192 chains",
         "value": done / elapsed, "unit": "generations/s", "n_gpus": 1, "steps": done, "warmup": args.warmup,
@@ -505,7 +513,8 @@ def run_c3(args):
                      "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the kernel is a "
                                    "dependent FP64 VALU chain (GSL operation order), far below it by construction",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": c3_traffic,
+                     "traffic_source": f"profiles/{PROFILE_ROUND}/c3_pmc_traffic.csv" if c3_traffic else None,
                      "algorithmic_flops_per_launch": flops[dominant], "avg_launch_ms": stages[dominant]},
     }
     if not args.no_cpu_baseline:

@@ -926,7 +926,8 @@ inline int rankmu_grid(int N, int kslices) {
 
 inline int rankmu_kslices(int N, int rows) {
   const int nt = (N + RT_T - 1) / RT_T, ntiles = nt * (nt + 1) / 2;
-  int want = (1024 + 8 * ntiles - 1) / (8 * ntiles), cap = rows / (8 * 64);
+  // >= 256 rows per slice: the partial tiles written stay well below the rows read
+  int want = (1024 + 8 * ntiles - 1) / (8 * ntiles), cap = rows / (8 * 256);
   if (cap < 1) cap = 1;
   if (want > cap) want = cap;
   if (want < 1) want = 1;

@@ -30,6 +30,12 @@ for s in ${STEPS:-tests}; do
     pmcf) step pmcf 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcw) step pmcw 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmcm) step pmcm 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --cov mfma --no-cpu-baseline ;;
+    pmcf3) step pmcf3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c3 -o run --output-format csv -- python $R/bench.py --workload c3 --steps 12 --warmup 1 --no-cpu-baseline ;;
+    pmcw3) step pmcw3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c3 -o run --output-format csv -- python $R/bench.py --workload c3 --steps 12 --warmup 1 --no-cpu-baseline ;;
+    pmcf4) step pmcf4 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    pmcw4) step pmcw4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c2.py ;;
+    trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c4.py ;;
     pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac
 done

@@ -4,7 +4,7 @@ device evaluations (cv at one point over the P log-likelihoods)."""
 import os
 import sys
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from korali_amd.native import TmcmcDevice
 
 for P in [int(a) for a in sys.argv[1:]] or [1024, 8192]:

@@ -2,7 +2,7 @@
 import os
 import sys
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["KORALI_AMD_TRACE_EIGEN"] = "1"
 import numpy as np
 from korali_amd.native import CmaesDevice

@@ -4,7 +4,7 @@ counters, and a bit-identity check of B against variant 0."""
 import os
 import sys
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["KORALI_AMD_TRACE_EIGEN"] = "1"
 import numpy as np
 from korali_amd.native import CmaesDevice
