@@ -203,6 +203,14 @@ typedef struct {
    * (the partial / exchange / finalize protocol below, also for one rank) */
   int shard_rank;
   int shard_count;
+  /* "Version" (TMCMC.config): 0 TMCMC, 1 mTMCMC — gradient / Fisher
+   * information proposals per chain (TMCMC.cpp.base:383-681), with the
+   * reference's constraints (:48-83: Max Chain Length 1, Step Size >= 0,
+   * Domain Extension Factor >= 0, Uniform priors) and this implementation's
+   * (burn-in 0, unsharded, N <= 128, likelihoods set by the caller) */
+  int version;
+  double step_size;               /* "Step Size" (default 0.1) */
+  double domain_extension_factor; /* "Domain Extension Factor" (default 0.2) */
 } kg_tmcmc_cfg;
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
@@ -262,6 +270,14 @@ int kg_tmcmc_stream(kg_tmcmc_t h, void **stream);
 int kg_tmcmc_evaluate_prior(kg_tmcmc_t h);
 int kg_tmcmc_get_candidates(kg_tmcmc_t h, double *X, size_t ld);
 int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double *log_likelihood);
+/* mTMCMC, generations > 1, after kg_tmcmc_set_evaluations:
+ * calculateGradients + calculateProposals (TMCMC.cpp.base:383-558) from
+ * every candidate's "logLikelihood Gradient" (P x N) and "Fisher
+ * Information" (P x N x N, row-major), as Bayesian/Reference computes them
+ * (reference.cpp.base:231-621); rows of chains whose candidate log-prior or
+ * log-likelihood is not finite are not read.  Also forms the proposal
+ * log-density ratios of the acceptance step (:634-677). */
+int kg_tmcmc_set_gradients(kg_tmcmc_t h, const double *grad, const double *fisher);
 int kg_tmcmc_profile(kg_tmcmc_t h, int enable);
 int kg_tmcmc_profile_read(kg_tmcmc_t h, const char *stage, double *ms_total, size_t *count);
 

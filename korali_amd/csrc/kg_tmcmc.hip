@@ -33,6 +33,7 @@
 
 #include "../../include/korali_amd.h"
 #include "kg_common.hpp"
+#include "kg_mtmcmc.hpp"
 #include "kg_rng.hpp"
 
 namespace kg {
@@ -229,16 +230,25 @@ __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const d
 // (:229-252, :611-633): P = exp((ll_c - ll_l) rho + (lp_c - lp_l)) if both
 // candidate values are finite, else 0; one Uniform draw per chain (always);
 // accept if P > U or generation 1.  Chain c's database entry is its leader.
+// mTMCMC (:634-677, `mode` non-null): chains with mode[c] = 1 (leader and
+// candidate without errors) add the proposal log-density ratio extra[c] =
+// log q(leader | candidate) - log q(candidate | leader), formed on the host.
 __global__ void k_tm_accept(int c_lo, int P, int gen1, double rho, const double *__restrict__ U,
                             const double *__restrict__ candLL, const double *__restrict__ candLP,
                             double *__restrict__ leadLL, double *__restrict__ leadLP, double *__restrict__ dbLL,
-                            double *__restrict__ dbLP, unsigned char *__restrict__ acc, TmDev *dev) {
+                            double *__restrict__ dbLP, unsigned char *__restrict__ acc, TmDev *dev,
+                            const double *__restrict__ extra, const unsigned char *__restrict__ mode) {
   const int c = c_lo + blockIdx.x * blockDim.x + threadIdx.x;
   bool a = false;
   if (c < P) {
     double p = 0.0;
     const double lpc = candLP[c], llc = candLL[c];
-    if (isfinite(lpc) && isfinite(llc)) p = exp_cr((llc - leadLL[c]) * rho + (lpc - leadLP[c]));
+    if (isfinite(lpc) && isfinite(llc)) {
+      if (mode && mode[c])
+        p = exp_cr((llc - leadLL[c]) * rho + extra[c] + (lpc - leadLP[c]));
+      else
+        p = exp_cr((llc - leadLL[c]) * rho + (lpc - leadLP[c]));
+    }
     a = (p > U[c]) || gen1;
     acc[c] = a ? 1 : 0;
     if (a) {
@@ -1359,6 +1369,17 @@ double cv2_tail(const double *E, size_t n, double target, double *w) {
 using namespace kg;
 
 struct kg_tmcmc_s {
+  // mTMCMC (cfg.version == 1): per-chain errors / gradients / proposal
+  // covariances of leaders (L), candidates (C) and database entries (D) on
+  // the host (kg_mtmcmc.hpp), the acceptance's proposal-density ratio and
+  // its mode on the device
+  bool mt = false;
+  std::vector<double> mtLE, mtCE, mtDE, mtLG, mtCG, mtDG, mtLC, mtCC, mtDC, mtUpper, mtLower;
+  std::vector<double> mtCand, mtLead, mtExtra;
+  std::vector<unsigned char> mtMode;
+  double *mtExtraDev = nullptr;
+  unsigned char *mtModeDev = nullptr;
+  double numCovarianceCorrections = 0;
   kg_tmcmc_cfg cfg;
   int N = 0, P = 0, ndist = 0;
   hipStream_t stream = nullptr;
@@ -2029,6 +2050,21 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Device Search Relaunches", nmRelaunchesD)
   SCA("Device Search Evaluations", nmEvalsD)
   SCA("Device Search Rounds", nmRoundsD)
+  SCA("Num Covariance Corrections", numCovarianceCorrections)
+  if (h->mt) {
+    const std::pair<const char *, std::vector<double> *> mtf[] = {
+        {"Chain Leaders Errors", &h->mtLE},         {"Chain Candidates Errors", &h->mtCE},
+        {"Sample Error Database", &h->mtDE},        {"Chain Leaders Gradients", &h->mtLG},
+        {"Chain Candidates Gradients", &h->mtCG},   {"Sample Gradient Database", &h->mtDG},
+        {"Chain Leaders Covariance", &h->mtLC},     {"Chain Candidates Covariance", &h->mtCC},
+        {"Sample Covariances Database", &h->mtDC},  {"Upper Extended Boundaries", &h->mtUpper},
+        {"Lower Extended Boundaries", &h->mtLower}};
+    for (const auto &f : mtf)
+      if (k == f.first) {
+        r = {nullptr, f.second->data(), f.second->size()};
+        return true;
+      }
+  }
   if (k == "Device Search Phase Times") {  // ms: controller wait, combine, logic; worker wait, evaluate, reduce
     r = {nullptr, h->nmTime, 6};
     return true;
@@ -2060,6 +2096,17 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   KG_CHECK(cfg->covariance_scaling > 0.0, "Covariance Scaling must be larger 0.0");  // TMCMC.cpp.base:28
   KG_CHECK(cfg->prior_min && cfg->prior_max, "prior_min / prior_max are required");
   KG_CHECK(cfg->likelihood == KG_LIK_GAUSSIAN, "unknown builtin likelihood");
+  KG_CHECK(cfg->version == 0 || cfg->version == 1, "TMCMC 'Version' must be TMCMC or mTMCMC");
+  if (cfg->version == 1) {  // TMCMC.cpp.base:48-55
+    KG_CHECK(cfg->max_chain_length == 1.0,
+             "Current version of 'mTMCMC' supports only 'Max Chain Length' of 1 (BASIS).");
+    KG_CHECK(cfg->step_size >= 0.0, "Step Size lower than 0.0");
+    KG_CHECK(cfg->domain_extension_factor >= 0.0, "Domain Extension Factor lower than 0.0");
+    KG_CHECK(cfg->default_burn_in == 0.0 && cfg->per_generation_burn_in_count == 0,
+             "mTMCMC: burn-in is not supported by this implementation");
+    KG_CHECK(cfg->shard_count <= 1, "mTMCMC runs unsharded");
+    KG_CHECK(cfg->variable_count <= 128, "mTMCMC: at most 128 variables");
+  }
   KG_HIP(hipSetDevice(cfg->device));
   upload_dd_tables();
   auto *h = new kg_tmcmc_s();
@@ -2197,6 +2244,32 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   }
   h->chainCount = P;
   h->hLen.assign(P, 1u);
+  if (cfg->version == 1) {
+    // TMCMC.cpp.base:57-82: errors start at -1; extended prior boundaries
+    h->mt = true;
+    const size_t PN = (size_t)P * N, PNN = PN * N;
+    h->mtLE.assign(P, -1.0);
+    h->mtCE.assign(P, -1.0);
+    h->mtDE.assign(P, -1.0);
+    h->mtLG.assign(PN, 0.0);
+    h->mtCG.assign(PN, 0.0);
+    h->mtDG.assign(PN, 0.0);
+    h->mtLC.assign(PNN, 0.0);
+    h->mtCC.assign(PNN, 0.0);
+    h->mtDC.assign(PNN, 0.0);
+    h->mtUpper.resize(N);
+    h->mtLower.resize(N);
+    for (int d = 0; d < N; d++) {
+      const double width = cfg->prior_max[d] - cfg->prior_min[d];
+      h->mtUpper[d] = cfg->prior_max[d] + width * cfg->domain_extension_factor;
+      h->mtLower[d] = cfg->prior_min[d] - width * cfg->domain_extension_factor;
+    }
+    h->mtCand.assign(PN, 0.0);
+    h->mtLead.assign(PN, 0.0);
+    h->mtExtra.assign(P, 0.0);
+    h->mtMode.assign(P, 0);
+    if (tdalloc(&h->mtExtraDev, P) || tdalloc(&h->mtModeDev, P)) return 1;
+  }
   *out = h;
   return 0;
 }
@@ -2212,7 +2285,8 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
                   (void *)h->dev, h->cvPart, (void *)h->pairs, (void *)h->pend, (void *)h->sch, (void *)h->Zx,
                   (void *)h->dLen, (void *)h->xch,
-                  (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync})
+                  (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync, (void *)h->mtExtraDev,
+                  (void *)h->mtModeDev})
     if (p) (void)hipFree(p);
   for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
                   (void *)h->hSch, (void *)h->hLenD, (void *)h->hNm})
@@ -2224,6 +2298,65 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
   }
   (void)hipStreamDestroy(h->stream);
   delete h;
+  return 0;
+}
+
+// generateCandidate, mTMCMC branch (TMCMC.cpp.base:567-608), every chain in
+// order: a leader without errors proposes from N(leader, step Sigma_l) plus
+// the drift (step/2) Sigma_l g_l (a failed Cholesky draws nothing and keeps
+// the old candidate); a leader with errors from N(leader, Sigma).  The
+// Multivariate normals are drawn on the device (exact stream positions:
+// N per drawing chain), the N x N per-chain algebra on the host.
+static int tm_mt_candidates(kg_tmcmc_s *h) {
+  const int N = h->N, P = h->P;
+  const size_t NN = (size_t)N * N, PN = (size_t)P * N;
+  std::vector<double> Lg(NN), S((size_t)P * NN), z;
+  std::vector<unsigned char> draws(P);
+  KG_HIP(hipMemcpyAsync(Lg.data(), h->chol, NN * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipMemcpyAsync(h->mtLead.data(), h->leaders, PN * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipMemcpyAsync(h->mtCand.data(), h->cand, PN * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  size_t M = 0;
+  for (int c = 0; c < P; c++) {
+    if (h->mtLE[c] == 0.0) {
+      double *Sc = S.data() + (size_t)c * NN;
+      for (size_t k = 0; k < NN; k++) Sc[k] = h->mtLC[(size_t)c * NN + k] * h->cfg.step_size;
+      draws[c] = mt::cholesky(N, Sc) ? 1 : 0;
+    } else {
+      draws[c] = 1;
+    }
+    if (draws[c]) M += N;
+  }
+  if (M) {
+    TmStage st(h, "rng_polar");
+    if (h->multivariate.polar_normals(h->Z, M, N, nullptr, h->stream)) return 1;
+    if (h->multivariate.consume_normals(M, N, nullptr, h->stream)) return 1;
+    if (h->multivariate.prefetch(PN, h->stream)) return 1;
+    z.resize(M);
+    KG_HIP(hipMemcpyAsync(z.data(), h->Z, M * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  }
+  KG_HIP(hipStreamSynchronize(h->stream));
+  TmStage st(h, "draw");
+  size_t k = 0;
+  const double alpha = 0.5 * h->cfg.step_size;
+  for (int c = 0; c < P; c++) {
+    double *x = h->mtCand.data() + (size_t)c * N;
+    const double *lead = h->mtLead.data() + (size_t)c * N;
+    if (h->mtLE[c] == 0.0) {
+      if (!draws[c]) continue;
+      for (int d = 0; d < N; d++) x[d] = z[k + d];
+      k += N;
+      mt::dtrmv_lower(N, S.data() + (size_t)c * NN, x);
+      for (int d = 0; d < N; d++) x[d] = x[d] + lead[d];  // gsl_vector_add(result, mu = leader)
+      mt::dgemv_add(N, alpha, h->mtLC.data() + (size_t)c * NN, h->mtLG.data() + (size_t)c * N, x);
+    } else {
+      for (int d = 0; d < N; d++) x[d] = z[k + d];
+      k += N;
+      mt::dtrmv_lower(N, Lg.data(), x);
+      for (int d = 0; d < N; d++) x[d] = x[d] + lead[d];
+    }
+  }
+  KG_HIP(hipMemcpyAsync(h->cand, h->mtCand.data(), PN * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
 
@@ -2247,6 +2380,19 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
                        h->chol, h->dev);
     KG_HIP(hipGetLastError());
   }
+  if (h->mt) {
+    // prepareGeneration :174-200: this generation's candidates start
+    // without errors (generation 1: -1), the leaders' proposals and
+    // gradients re-annealed
+    const double fc = h->previousAnnealingExponent / h->annealingExponent;
+    const double fg = h->annealingExponent / h->previousAnnealingExponent;
+    h->numCovarianceCorrections = 0;
+    for (int c = 0; c < P; c++) h->mtCE[c] = generation > 1 ? 0.0 : -1.0;
+    for (double &v : h->mtLC) v *= fc;
+    for (double &v : h->mtLG) v *= fg;
+    std::fill(h->mtMode.begin(), h->mtMode.end(), (unsigned char)0);
+    KG_HIP(hipMemsetAsync(h->mtModeDev, 0, (size_t)P, h->stream));
+  }
   if (generation == 1) {
     TmStage st(h, "prior_draw");
     for (int k = 0; k < h->ndist; k++)
@@ -2255,6 +2401,8 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
     hipLaunchKernelGGL(k_tm_prior, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->Uprior, h->uoff, h->ustride,
                        h->pmin, h->pmax, h->cand);
     KG_HIP(hipGetLastError());
+  } else if (h->mt) {
+    if (tm_mt_candidates(h)) return 1;
   } else {
     {
       TmStage st(h, "rng_polar");
@@ -2326,6 +2474,101 @@ int kg_tmcmc_set_evaluations(kg_tmcmc_t h, const double *log_prior, const double
   return 0;
 }
 
+int kg_tmcmc_set_gradients(kg_tmcmc_t h, const double *grad, const double *fisher) {
+  KG_CHECK(h->mt, "kg_tmcmc_set_gradients: the handle is not mTMCMC");
+  KG_CHECK(grad && fisher, "kg_tmcmc_set_gradients: null argument");
+  const int N = h->N, P = h->P;
+  const size_t NN = (size_t)N * N;
+  std::vector<double> lp(P), ll(P);
+  KG_HIP(hipMemcpyAsync(lp.data(), h->candLP, P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipMemcpyAsync(ll.data(), h->candLL, P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  const double rho = h->annealingExponent, chi2inv = mt::chi2inv_068(N);
+  const int chains = (int)h->chainCount;
+  // calculateGradients :383-403
+  for (int c = 0; c < chains; c++) {
+    if (!(std::isfinite(lp[c]) && std::isfinite(ll[c]))) continue;
+    for (int d = 0; d < N; d++) h->mtCG[(size_t)c * N + d] = grad[(size_t)c * N + d] * rho;
+  }
+  // calculateProposals :405-558
+  std::vector<double> F(NN), Finv(NN), E(NN), ev(N), c0(N), c1(N);
+  std::vector<size_t> perm(N);
+  for (int c = 0; c < chains; c++) {
+    if (!(std::isfinite(lp[c]) && std::isfinite(ll[c]))) continue;
+    const double *cand = h->mtCand.data() + (size_t)c * N;
+    double *CC = h->mtCC.data() + (size_t)c * NN;
+    for (size_t k = 0; k < NN; k++) CC[k] = 0.0;
+    for (size_t k = 0; k < NN; k++) F[k] = fisher[(size_t)c * NN + k] * rho;
+    mt::lu_decomp(N, F.data(), perm.data());
+    mt::lu_invert(N, F.data(), perm.data(), Finv.data());
+    mt::symmv_unsorted(N, Finv.data(), ev.data(), E.data());
+    bool correction = false;
+    for (int d = 0; d < N; d++) {
+      double scale = std::sqrt(ev[d] * chi2inv);
+      const double before = scale;
+      for (int e = 0; e < N; e++) c0[e] = cand[e] + (1.0 * scale) * E[(size_t)e * N + d];
+      for (int e = 0; e < N; e++) c1[e] = cand[e] + (-1.0 * scale) * E[(size_t)e * N + d];
+      for (int e = 0; e < N; e++) {
+        const double up = h->mtUpper[e] - cand[e], lo = cand[e] - h->mtLower[e];
+        const double inv = 1.0 / E[(size_t)e * N + d];
+        double v;
+        if (c0[e] - h->mtUpper[e] > 0.) {
+          v = std::fabs(inv * up);
+          scale = (v < scale) ? v : scale;
+        }
+        if (h->mtLower[e] - c0[e] > 0.) {
+          v = std::fabs(inv * lo);
+          scale = (v < scale) ? v : scale;
+        }
+        if (c1[e] - h->mtUpper[e] > 0.) {
+          v = std::fabs(inv * up);
+          scale = (v < scale) ? v : scale;
+        }
+        if (h->mtLower[e] - c1[e] > 0.) {
+          v = std::fabs(inv * lo);
+          scale = (v < scale) ? v : scale;
+        }
+      }
+      ev[d] = scale * scale / chi2inv;
+      if (before != scale) correction = true;
+    }
+    if (correction) h->numCovarianceCorrections += 1;
+    for (int d = 0; d < N; d++) {
+      const double f = std::sqrt(ev[d]);
+      for (int e = 0; e < N; e++) E[(size_t)e * N + d] *= f;
+    }
+    for (int i = 0; i < N; i++)  // gslcblas dgemm NoTrans / Trans, alpha 1, beta 0
+      for (int j = 0; j < N; j++) {
+        double temp = 0.0;
+        for (int q = 0; q < N; q++) temp += E[(size_t)i * N + q] * E[(size_t)j * N + q];
+        CC[(size_t)i * N + j] = 0.0 + 1.0 * temp;
+      }
+  }
+  // calculateAcceptanceProbability :634-673: the proposal log-density ratio
+  // of chains whose leader and candidate have no errors
+  std::vector<double> mL(N), mC(N), L(NN);
+  const double alpha = 0.5 * h->cfg.step_size;
+  for (int c = 0; c < chains; c++) {
+    h->mtMode[c] = (h->mtLE[c] == 0.0 && h->mtCE[c] == 0.0) ? 1 : 0;
+    h->mtExtra[c] = 0.0;
+    if (!h->mtMode[c] || !(std::isfinite(lp[c]) && std::isfinite(ll[c]))) continue;
+    const double *LC = h->mtLC.data() + (size_t)c * NN;
+    const double *lead = h->mtLead.data() + (size_t)c * N, *cand = h->mtCand.data() + (size_t)c * N;
+    for (int d = 0; d < N; d++) mL[d] = lead[d], mC[d] = cand[d];
+    mt::dgemv_add(N, alpha, LC, h->mtLG.data() + (size_t)c * N, mL.data());
+    mt::dgemv_add(N, alpha, LC, h->mtCG.data() + (size_t)c * N, mC.data());
+    for (size_t k = 0; k < NN; k++) L[k] = LC[k] * h->cfg.step_size;
+    (void)mt::cholesky(N, L.data());  // gsl_linalg_cholesky_decomp1; failure leaves the partial factor
+    const double lpC = mt::mvn_log_pdf(N, cand, mL.data(), L.data());
+    const double lpL = mt::mvn_log_pdf(N, lead, mC.data(), L.data());
+    h->mtExtra[c] = lpL - lpC;
+  }
+  KG_HIP(hipMemcpyAsync(h->mtExtraDev, h->mtExtra.data(), P * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipMemcpyAsync(h->mtModeDev, h->mtMode.data(), (size_t)P, hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending) {
   const int N = h->N, P = h->P;
   KG_CHECK(h->step < h->maxSteps, "kg_tmcmc_advance: every chain has finished this generation");
@@ -2338,10 +2581,29 @@ int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending) {
     if (b > a) {
       hipLaunchKernelGGL(k_tm_accept, dim3(nblk(b - a, 256)), dim3(256), 0, h->stream, a, b, generation == 1 ? 1 : 0,
                          h->annealingExponent, h->U, h->candLL, h->candLP, h->leadLL, h->leadLP, h->dbLL, h->dbLP,
-                         h->acc, h->dev);
+                         h->acc, h->dev, h->mt ? h->mtExtraDev : (const double *)nullptr,
+                         h->mt ? h->mtModeDev : (const unsigned char *)nullptr);
       hipLaunchKernelGGL(k_tm_copy_rows, dim3(nblk((size_t)(b - a) * N, 256)), dim3(256), 0, h->stream, N, a, b,
                          h->acc, h->cand, h->leaders, h->db);
       KG_HIP(hipGetLastError());
+      if (h->mt) {
+        // processCandidate :239-244 and updateDatabase :617-622 for the
+        // errors / gradients / proposals (chain c's entry is c)
+        const size_t NN = (size_t)N * N;
+        std::vector<unsigned char> acc(P);
+        KG_HIP(hipMemcpyAsync(acc.data(), h->acc, (size_t)P, hipMemcpyDeviceToHost, h->stream));
+        KG_HIP(hipStreamSynchronize(h->stream));
+        for (int c = a; c < b; c++) {
+          if (acc[c]) {
+            h->mtLE[c] = h->mtCE[c];
+            std::copy_n(h->mtCG.begin() + (size_t)c * N, N, h->mtLG.begin() + (size_t)c * N);
+            std::copy_n(h->mtCC.begin() + (size_t)c * NN, NN, h->mtLC.begin() + (size_t)c * NN);
+          }
+          h->mtDE[c] = h->mtLE[c];
+          std::copy_n(h->mtLG.begin() + (size_t)c * N, N, h->mtDG.begin() + (size_t)c * N);
+          std::copy_n(h->mtLC.begin() + (size_t)c * NN, NN, h->mtDC.begin() + (size_t)c * NN);
+        }
+      }
     }
     h->pendingCount = 0;
     h->step = h->maxSteps;
@@ -2497,6 +2759,25 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
       }
     }
     for (size_t j = leaderId; j < (size_t)P; j++) h->hLen[j] = 0;
+    if (h->mt) {
+      // :339-344 leaders take their entry's errors / gradients / proposals;
+      // :362-372 then anneal them
+      const size_t NN = (size_t)N * N;
+      for (size_t j = 0; j < leaderId; j++) {
+        const size_t i = h->hSrc[j];
+        h->mtLE[j] = h->mtDE[i];
+        std::copy_n(h->mtDG.begin() + i * N, N, h->mtLG.begin() + j * N);
+        std::copy_n(h->mtDC.begin() + i * NN, NN, h->mtLC.begin() + j * NN);
+      }
+      if (h->previousAnnealingExponent > 0.0) {
+        const double f = h->annealingExponent / h->previousAnnealingExponent;
+        for (int i = 0; i < P; i++) {
+          if (h->mtLE[i] != 0.0) continue;
+          for (int d = 0; d < N; d++) h->mtLG[(size_t)i * N + d] *= f;
+          for (size_t q = 0; q < NN; q++) h->mtLC[(size_t)i * NN + q] *= f;
+        }
+      }
+    }
   }
   KG_CHECK(total == (size_t)P, "multinomial selections do not sum to the population size");
   KG_HIP(hipMemcpyAsync(h->w, h->hW, (size_t)P * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -2536,6 +2817,8 @@ int kg_tmcmc_process(kg_tmcmc_t h, size_t generation) {
 }
 
 int kg_tmcmc_generation(kg_tmcmc_t h, size_t generation) {
+  KG_CHECK(!h->mt, "mTMCMC needs the problem's gradients: evaluate on the host (kg_tmcmc_set_evaluations, "
+                   "kg_tmcmc_set_gradients)");
   if (kg_tmcmc_prepare(h, generation)) return 1;
   if (kg_tmcmc_evaluate(h)) return 1;
   return kg_tmcmc_process(h, generation);

@@ -49,6 +49,7 @@ class _TmcmcCfg(C.Structure):
         ("multivariate_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("likelihood", C.c_int),
         ("device", C.c_int), ("per_generation_burn_in", C.POINTER(C.c_double)),
         ("per_generation_burn_in_count", C.c_size_t), ("shard_rank", C.c_int), ("shard_count", C.c_int),
+        ("version", C.c_int), ("step_size", C.c_double), ("domain_extension_factor", C.c_double),
     ]
 
 
@@ -64,6 +65,7 @@ EXPORTED = [
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
     "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_advance", "kg_tmcmc_get_pending",
     "kg_tmcmc_process_partial", "kg_tmcmc_process_finalize", "kg_tmcmc_device_ptr", "kg_tmcmc_stream", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
+    "kg_tmcmc_set_gradients",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump",
 ]
 
@@ -119,6 +121,7 @@ def lib():
         L.kg_tmcmc_set_rng.argtypes = [vp, ip, vp]
         L.kg_tmcmc_get_candidates.argtypes = [vp, dp, sz]
         L.kg_tmcmc_set_evaluations.argtypes = [vp, dp, dp]
+        L.kg_tmcmc_set_gradients.argtypes = [vp, dp, dp]
         L.kg_tmcmc_advance.argtypes = [vp, sz, C.POINTER(sz)]
         L.kg_tmcmc_get_pending.argtypes = [vp, C.POINTER(C.c_ubyte)]
         L.kg_tmcmc_profile.argtypes = [vp, ip]
@@ -308,7 +311,8 @@ class TmcmcDevice:
     def __init__(self, N, P, prior_min, prior_max, prior_seeds=None, prior_distribution=None,
                  multinomial_seed=0, multivariate_seed=0, uniform_seed=0, target_cov=1.0, covariance_scaling=0.04,
                  min_annealing_exponent_update=1e-5, max_annealing_exponent_update=1.0, max_chain_length=1,
-                 default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0, shard_rank=0, shard_count=0):
+                 default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0, shard_rank=0, shard_count=0,
+                 version=0, step_size=0.1, domain_extension_factor=0.2):
         L = lib()
         self.N, self.P = int(N), int(P)
         pdist = (np.arange(self.N, dtype=np.int32) if prior_distribution is None
@@ -334,6 +338,8 @@ class TmcmcDevice:
         cfg.per_generation_burn_in = _dptr(pgb) if pgb.size else None
         cfg.per_generation_burn_in_count = pgb.size
         cfg.shard_rank, cfg.shard_count = int(shard_rank), int(shard_count)
+        cfg.version = 1 if version in (1, "mTMCMC") else 0
+        cfg.step_size, cfg.domain_extension_factor = float(step_size), float(domain_extension_factor)
         h = C.c_void_p()
         check(L.kg_tmcmc_create(C.byref(cfg), C.byref(h)))
         self.h = h
@@ -405,6 +411,15 @@ class TmcmcDevice:
         lp = np.ascontiguousarray(log_prior, dtype=np.float64)
         ll = np.ascontiguousarray(log_likelihood, dtype=np.float64)
         check(self._L.kg_tmcmc_set_evaluations(self.h, _dptr(lp), _dptr(ll)))
+
+    def set_gradients(self, grad, fisher):
+        """mTMCMC: every candidate's log-likelihood gradient (P x N) and Fisher
+        information (P x N x N); kg_tmcmc_set_gradients."""
+        g = np.ascontiguousarray(grad, dtype=np.float64).reshape(-1)
+        f = np.ascontiguousarray(fisher, dtype=np.float64).reshape(-1)
+        if g.size != self.P * self.N or f.size != self.P * self.N * self.N:
+            raise ValueError("set_gradients: expected P x N gradients and P x N x N Fisher informations")
+        check(self._L.kg_tmcmc_set_gradients(self.h, _dptr(g), _dptr(f)))
 
     def field_size(self, name):
         n = C.c_size_t()

@@ -890,7 +890,11 @@ static void qrstep(size_t n, double *d, double *sd, double *gc, double *gs)
   sd[k - 1] = bk;
 }
 
-size_t kr_eigen_symmv(size_t N, double *A, double *eval, double *evec)
+static size_t eigen_symmv(size_t N, double *A, double *eval, double *evec, int sort);
+size_t kr_eigen_symmv(size_t N, double *A, double *eval, double *evec) { return eigen_symmv(N, A, eval, evec, 1); }
+/* gsl_eigen_symmv without gsl_eigen_symmv_sort (TMCMC.cpp.base:468) */
+size_t kr_eigen_symmv_unsorted(size_t N, double *A, double *eval, double *evec) { return eigen_symmv(N, A, eval, evec, 0); }
+static size_t eigen_symmv(size_t N, double *A, double *eval, double *evec, int sort)
 {
   size_t i, steps = 0;
   double *d, *sd, *gc, *gs;
@@ -957,7 +961,7 @@ size_t kr_eigen_symmv(size_t N, double *A, double *eval, double *evec)
   for (i = 0; i < N; i++) eval[i] = d[i];
 
   /* gsl_eigen_symmv_sort(ABS_ASC): selection sort, strict < on |e| */
-  for (i = 0; i + 1 < N; i++)
+  for (i = 0; sort && i + 1 < N; i++)
   {
     size_t j, k = i;
     double ek = eval[i];
@@ -1770,6 +1774,12 @@ struct kr_tmcmc
   double chainCount, acceptedSamplesCount, proposalsAcceptanceRate, selectionAcceptanceRate;
   double dbCount, modelEvaluationCount, minSearchIterations;
   kr_rng multinomial, multivariate, uniform;
+  /* mTMCMC (TMCMC.cpp.base:48-83, :146-157, :174-200, :383-558, :567-609,
+   * :634-681): errors / gradients / proposal covariances of the chain
+   * leaders (L*), candidates (C*) and database (D*); errors held as doubles */
+  double version, stepSize, domainExtensionFactor, numCovarianceCorrections;
+  double *upperExt, *lowerExt;
+  double *LE, *CE, *DE, *LG, *CG, *DG, *LC, *CC, *DC;
 };
 
 kr_tmcmc *kr_tmcmc_new(size_t N, size_t P)
@@ -1839,6 +1849,17 @@ void kr_tmcmc_free(kr_tmcmc *h)
   free(h->dbLP);
   free(h->numSelections);
   free(h->perGenBurnIn);
+  free(h->upperExt);
+  free(h->lowerExt);
+  free(h->LE);
+  free(h->CE);
+  free(h->DE);
+  free(h->LG);
+  free(h->CG);
+  free(h->DG);
+  free(h->LC);
+  free(h->CC);
+  free(h->DC);
   free(h);
 }
 
@@ -1881,6 +1902,21 @@ double *kr_tmcmc_field(kr_tmcmc *h, const char *name, size_t *len)
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Min Search Iterations", minSearchIterations)
   SCA("Current Burn In", currentBurnIn)
+  SCA("Num Covariance Corrections", numCovarianceCorrections)
+  if (h->LE)
+  {
+    VEC("Chain Leaders Errors", h->LE, P)
+    VEC("Chain Candidates Errors", h->CE, P)
+    VEC("Sample Error Database", h->DE, P)
+    VEC("Chain Leaders Gradients", h->LG, P * N)
+    VEC("Chain Candidates Gradients", h->CG, P * N)
+    VEC("Sample Gradient Database", h->DG, P * N)
+    VEC("Chain Leaders Covariance", h->LC, P * N * N)
+    VEC("Chain Candidates Covariance", h->CC, P * N * N)
+    VEC("Sample Covariances Database", h->DC, P * N * N)
+    VEC("Upper Extended Boundaries", h->upperExt, N)
+    VEC("Lower Extended Boundaries", h->lowerExt, N)
+  }
 #undef VEC
 #undef SCA
   if (len) *len = 0;
@@ -1911,6 +1947,9 @@ void kr_tmcmc_set_option(kr_tmcmc *h, const char *name, double v)
   else if (strcmp(name, "Covariance Scaling") == 0) h->covScaling = v;
   else if (strcmp(name, "Min Annealing Exponent Update") == 0) h->minAnnealingExponentUpdate = v;
   else if (strcmp(name, "Max Annealing Exponent Update") == 0) h->maxAnnealingExponentUpdate = v;
+  else if (strcmp(name, "Version") == 0) h->version = v; /* 0 TMCMC, 1 mTMCMC */
+  else if (strcmp(name, "Step Size") == 0) h->stepSize = v;
+  else if (strcmp(name, "Domain Extension Factor") == 0) h->domainExtensionFactor = v;
 }
 
 void kr_tmcmc_set_per_generation_burn_in(kr_tmcmc *h, const double *v, size_t n)
@@ -1939,6 +1978,32 @@ void kr_tmcmc_initialize(kr_tmcmc *h)
   h->maxLoglikelihood = -INFINITY;
   h->chainCount = (double)h->P;
   for (i = 0; i < h->P; i++) h->chainLengths[i] = 1;
+  if (h->version == 1.0 && !h->LE)
+  {
+    const size_t N = h->N, P = h->P;
+#define AL(p, n) p = (double *)calloc((n), sizeof(double))
+    AL(h->upperExt, N);
+    AL(h->lowerExt, N);
+    AL(h->LE, P);
+    AL(h->CE, P);
+    AL(h->DE, P);
+    AL(h->LG, P * N);
+    AL(h->CG, P * N);
+    AL(h->DG, P * N);
+    AL(h->LC, P * N * N);
+    AL(h->CC, P * N * N);
+    AL(h->DC, P * N * N);
+#undef AL
+    /* :57-59 errors start at -1; :76-82 extended boundaries */
+    for (i = 0; i < P; i++) h->CE[i] = h->LE[i] = h->DE[i] = -1;
+    for (i = 0; i < N; i++)
+    {
+      const double width = h->priorMax[i] - h->priorMin[i];
+      h->upperExt[i] = h->priorMax[i] + width * h->domainExtensionFactor;
+      h->lowerExt[i] = h->priorMin[i] - width * h->domainExtensionFactor;
+    }
+  }
+  if (h->LE) h->numCovarianceCorrections = 0;
 }
 
 /* generateCandidate :560-566 -> multivariate::Normal::getRandomVector
@@ -1955,6 +2020,299 @@ static void tm_generate_candidate(kr_tmcmc *h, size_t i)
   for (d = 0; d < N; d++) x[d] += h->leaders[i * N + d];
 }
 
+/* gslcblas dgemv RowMajor NoTrans, beta = 1: y_i += alpha (sum_j A_ij x_j) */
+static void mt_dgemv_add(size_t N, double alpha, const double *A, const double *x, double *y)
+{
+  size_t i, j;
+  for (i = 0; i < N; i++)
+  {
+    double temp = 0.0;
+    for (j = 0; j < N; j++) temp += A[i * N + j] * x[j];
+    y[i] += alpha * temp;
+  }
+}
+
+/* generateCandidate, mTMCMC branch (:567-608): a leader without errors
+ * proposes from N(leader + (step/2) Sigma_l g_l, step Sigma_l) (the mean
+ * vector, then the drift added by dgemv); a failed Cholesky draws nothing
+ * and leaves the candidate as it was; a leader with errors proposes from
+ * N(leader, Sigma) with the population covariance. */
+static void mt_generate_candidate(kr_tmcmc *h, size_t i)
+{
+  const size_t N = h->N;
+  size_t d;
+  double *x = h->candidates + i * N;
+  if (h->LE[i] == 0)
+  {
+    double *S = (double *)malloc(sizeof(double) * N * N);
+    for (d = 0; d < N * N; d++) S[d] = h->LC[i * N * N + d] * h->stepSize;
+    if (kr_cholesky(N, S) == 0)
+    {
+      for (d = 0; d < N; d++) x[d] = kr_ran_gaussian(&h->multivariate, 1.0);
+      kr_dtrmv_lower(N, S, x);
+      for (d = 0; d < N; d++) x[d] = x[d] + h->leaders[i * N + d];
+      mt_dgemv_add(N, 0.5 * h->stepSize, h->LC + i * N * N, h->LG + i * N, x);
+    }
+    free(S);
+  }
+  if (h->LE[i] != 0)
+  {
+    for (d = 0; d < N; d++) x[d] = kr_ran_gaussian(&h->multivariate, 1.0);
+    kr_dtrmv_lower(N, h->chol, x);
+    for (d = 0; d < N; d++) x[d] = x[d] + h->leaders[i * N + d];
+  }
+}
+
+/* ---- mTMCMC linear algebra (GSL 2.6 is absent here: the Level-2 forms of
+ * linalg/lu.c, linalg/luinv via LU_svx, randist/mvgauss.c, gslcblas
+ * dtrsv / dgemm loop orders; parity with GSL itself is unpinned) ---- */
+
+/* gsl_cdf_chisq_Pinv(0.68, N), N = 1..128 (tools/make_chi2_table.py) */
+static const double MT_CHI2_068[128] = {
+  0.988946481478023, 2.27886856637673, 3.505882355768179, 4.695422319122993,
+  5.8608022596974125, 7.009169946950603, 8.144788668939585, 9.270418200246363,
+  10.387958013319528, 11.498778181311328, 12.603903905356493, 13.704125276314006,
+  14.800066067589455, 15.892228745155391, 16.98102499350416, 18.066797057367218,
+  19.149833056062814, 20.230378223312684, 21.308643320753227, 22.38481104613223,
+  23.459040989954513, 24.53147352253592, 25.602232880235793, 26.67142964341346,
+  27.739162746301982, 28.805521122384825, 29.870585062847724, 30.934427346913328,
+  31.997114189146984, 33.05870603866459, 34.119258257565306, 35.17882170015321,
+  36.237443210107635, 37.29516604936419, 38.35203026982309, 39.40807303692524,
+  40.46332891249609, 41.517830102949176, 42.571606677894444, 43.6246867633504,
+  44.67709671307324, 45.728861260956485, 46.78000365699435, 47.83054578892401,
+  48.880508291347134, 49.929910643870045, 50.97877125958297, 52.02710756501539,
+  53.074936072549725, 54.122272446144436, 55.16913156110684, 56.215527558560616,
+  57.26147389517232, 58.30698338863145, 59.35206825931891, 60.39674016854704,
+  61.44101025370968, 62.48488916064193, 63.528387073455576, 64.57151374208671,
+  65.61427850776624, 66.65669032660158, 67.69875779143783, 68.74048915214941,
+  69.78189233449768, 70.82297495767644, 71.86374435065521, 72.90420756741935,
+  73.9443714011968, 74.98424239775245, 76.0238268678238, 77.06313089876471,
+  78.10216036545802, 79.14092094055236, 80.17941810407355, 81.21765715245671,
+  82.2556432070412, 83.29338122206687, 84.33087599220691, 85.36813215966977,
+  86.4051542208999, 87.44194653290452, 88.47851331923188, 89.51485867562381,
+  90.55098657536443, 91.5869008743443, 92.62260531585866, 93.65810353515641,
+  94.6933990637555, 95.72849533353936, 96.7633956806475, 97.79810334917329,
+  98.83262149467973, 99.86695318754488, 100.90110141614619, 101.93506908989364,
+  102.96885904212003, 104.00247403283672, 105.03591675136242, 106.06918981883199,
+  107.10229579059188, 108.13523715848865, 109.1680163530559, 110.20063574560554,
+  111.2330976502281, 112.26540432570714, 113.29755797735193, 114.32956075875305,
+  115.36141477346426, 116.39312207661503, 117.4246846764566, 118.45610453584531,
+  119.48738357366618, 120.5185236661994, 121.5495266484329, 122.58039431532332,
+  123.6111284230079, 124.64173068996958, 125.67220279815764, 126.70254639406568,
+  127.73276308976914, 128.76285446392407, 129.79282206272907, 130.82266740085166,
+  131.85239196232124, 132.88199720138954, 133.91148454336053, 134.9408553853905,
+};
+
+double kr_chi2inv_068(size_t N) { return (N >= 1 && N <= 128) ? MT_CHI2_068[N - 1] : NAN; }
+
+/* gsl_linalg_LU_decomp: partial pivoting, row operations, perm[] */
+static void mt_lu_decomp(size_t N, double *A, size_t *perm)
+{
+  size_t i, j, k;
+  for (i = 0; i < N; i++) perm[i] = i;
+  for (j = 0; j + 1 < N; j++)
+  {
+    double ajj, max = fabs(A[j * N + j]);
+    size_t ip = j;
+    for (i = j + 1; i < N; i++)
+    {
+      const double aij = fabs(A[i * N + j]);
+      if (aij > max)
+      {
+        max = aij;
+        ip = i;
+      }
+    }
+    if (ip != j)
+    {
+      size_t t;
+      for (k = 0; k < N; k++)
+      {
+        const double q = A[j * N + k];
+        A[j * N + k] = A[ip * N + k];
+        A[ip * N + k] = q;
+      }
+      t = perm[j];
+      perm[j] = perm[ip];
+      perm[ip] = t;
+    }
+    ajj = A[j * N + j];
+    if (ajj != 0.0)
+      for (i = j + 1; i < N; i++)
+      {
+        const double aij = A[i * N + j] / ajj;
+        A[i * N + j] = aij;
+        for (k = j + 1; k < N; k++) A[i * N + k] = A[i * N + k] - aij * A[j * N + k];
+      }
+  }
+}
+
+/* gsl_linalg_LU_invert: identity columns through LU_svx (permute, dtrsv
+ * Lower Unit, dtrsv Upper NonUnit) */
+static void mt_lu_invert(size_t N, const double *LU, const size_t *perm, double *inv)
+{
+  size_t c, i, j;
+  double *x = (double *)malloc(sizeof(double) * N), *y = (double *)malloc(sizeof(double) * N);
+  for (c = 0; c < N; c++)
+  {
+    for (i = 0; i < N; i++) y[i] = (i == c) ? 1.0 : 0.0;
+    for (i = 0; i < N; i++) x[i] = y[perm[i]]; /* gsl_permute_vector: v'_i = v_{p_i} */
+    for (i = 1; i < N; i++)
+    {
+      double tmp = x[i];
+      for (j = 0; j < i; j++) tmp -= LU[i * N + j] * x[j];
+      x[i] = tmp;
+    }
+    x[N - 1] = x[N - 1] / LU[(N - 1) * N + (N - 1)];
+    for (i = N - 1; i > 0 && i--;)
+    {
+      double tmp = x[i];
+      for (j = i + 1; j < N; j++) tmp -= LU[i * N + j] * x[j];
+      x[i] = tmp / LU[i * N + i];
+    }
+    for (i = 0; i < N; i++) inv[i * N + c] = x[i];
+  }
+  free(x);
+  free(y);
+}
+
+/* gsl_ran_multivariate_gaussian_log_pdf with the lower Cholesky factor L */
+static double mt_mvn_log_pdf(size_t N, const double *x, const double *mu, const double *L)
+{
+  size_t i, j;
+  double quad = 0.0, logdet = 0.0;
+  double *w = (double *)malloc(sizeof(double) * N);
+  for (i = 0; i < N; i++) w[i] = x[i] - mu[i];
+  w[0] = w[0] / L[0];
+  for (i = 1; i < N; i++)
+  {
+    double tmp = w[i];
+    for (j = 0; j < i; j++) tmp -= L[i * N + j] * w[j];
+    w[i] = tmp / L[i * N + i];
+  }
+  for (i = 0; i < N; i++) quad += w[i] * w[i];
+  for (i = 0; i < N; i++) logdet += kr_log_cr(L[i * N + i]);
+  free(w);
+  return -0.5 * quad - logdet - 0.5 * (double)N * kr_log_cr(2.0 * 3.14159265358979323846);
+}
+
+/* calculateGradients + calculateProposals (:383-558) for the chains whose
+ * candidate has a finite log-prior and log-likelihood; grad (P x N) and
+ * fim (P x N x N) are the problem's "logLikelihood Gradient" and "Fisher
+ * Information" of every candidate (rows of other chains are not read). */
+void kr_tmcmc_set_gradients(kr_tmcmc *h, const double *grad, const double *fim)
+{
+  const size_t N = h->N, NN = N * N;
+  const double chi2inv = kr_chi2inv_068(N);
+  double *F = (double *)malloc(sizeof(double) * NN), *Finv = (double *)malloc(sizeof(double) * NN);
+  double *ev = (double *)malloc(sizeof(double) * N), *E = (double *)malloc(sizeof(double) * NN);
+  double *c0 = (double *)malloc(sizeof(double) * N), *c1 = (double *)malloc(sizeof(double) * N);
+  size_t *perm = (size_t *)malloc(sizeof(size_t) * N);
+  size_t c, d, e, i, j, k;
+  for (c = 0; c < (size_t)h->chainCount; c++)
+  {
+    if (!(isfinite(h->candidatesLP[c]) && isfinite(h->candidatesLL[c]))) continue;
+    for (d = 0; d < N; d++) h->CG[c * N + d] = grad[c * N + d] * h->annealingExponent;
+  }
+  for (c = 0; c < (size_t)h->chainCount; c++)
+  {
+    const double *cand = h->candidates + c * N;
+    double *CC = h->CC + c * NN;
+    int correction = 0;
+    if (!(isfinite(h->candidatesLP[c]) && isfinite(h->candidatesLL[c]))) continue;
+    for (k = 0; k < NN; k++) CC[k] = 0.0;
+    for (k = 0; k < NN; k++) F[k] = fim[c * NN + k] * h->annealingExponent;
+    mt_lu_decomp(N, F, perm);
+    mt_lu_invert(N, F, perm, Finv);
+    /* gsl_eigen_symmv, unsorted */
+    kr_eigen_symmv_unsorted(N, Finv, ev, E);
+    for (d = 0; d < N; d++)
+    {
+      double scale = sqrt(ev[d] * chi2inv);
+      const double before = scale;
+      for (e = 0; e < N; e++) c0[e] = cand[e] + (1.0 * scale) * E[e * N + d];
+      for (e = 0; e < N; e++) c1[e] = cand[e] + (-1.0 * scale) * E[e * N + d];
+      for (e = 0; e < N; e++)
+      {
+        const double up = h->upperExt[e] - cand[e], lo = cand[e] - h->lowerExt[e];
+        double len, v;
+        len = c0[e] - h->upperExt[e];
+        if (len > 0.)
+        {
+          v = fabs(1.0 / E[e * N + d] * up);
+          scale = (v < scale) ? v : scale;
+        }
+        len = h->lowerExt[e] - c0[e];
+        if (len > 0.)
+        {
+          v = fabs(1.0 / E[e * N + d] * lo);
+          scale = (v < scale) ? v : scale;
+        }
+        len = c1[e] - h->upperExt[e];
+        if (len > 0.)
+        {
+          v = fabs(1.0 / E[e * N + d] * up);
+          scale = (v < scale) ? v : scale;
+        }
+        len = h->lowerExt[e] - c1[e];
+        if (len > 0.)
+        {
+          v = fabs(1.0 / E[e * N + d] * lo);
+          scale = (v < scale) ? v : scale;
+        }
+      }
+      ev[d] = scale * scale / chi2inv;
+      if (before != scale) correction = 1;
+    }
+    if (correction) h->numCovarianceCorrections += 1;
+    for (d = 0; d < N; d++)
+    {
+      const double f = sqrt(ev[d]);
+      for (e = 0; e < N; e++) E[e * N + d] *= f;
+    }
+    /* gslcblas dgemm RowMajor NoTrans/Trans, alpha 1, beta 0 */
+    for (i = 0; i < N; i++)
+      for (j = 0; j < N; j++)
+      {
+        double temp = 0.0;
+        for (k = 0; k < N; k++) temp += E[i * N + k] * E[j * N + k];
+        CC[i * N + j] = 0.0 + 1.0 * temp;
+      }
+  }
+  free(F);
+  free(Finv);
+  free(ev);
+  free(E);
+  free(c0);
+  free(c1);
+  free(perm);
+}
+
+/* calculateAcceptanceProbability, mTMCMC branch (:634-677) */
+static double mt_acceptance(kr_tmcmc *h, size_t c)
+{
+  const size_t N = h->N, NN = N * N;
+  const double *LC = h->LC + c * NN;
+  double *mL = (double *)malloc(sizeof(double) * N), *mC = (double *)malloc(sizeof(double) * N);
+  double *L = (double *)malloc(sizeof(double) * NN);
+  double lpC, lpL, P;
+  size_t k;
+  memcpy(mL, h->leaders + c * N, sizeof(double) * N);
+  memcpy(mC, h->candidates + c * N, sizeof(double) * N);
+  mt_dgemv_add(N, 0.5 * h->stepSize, LC, h->LG + c * N, mL);
+  mt_dgemv_add(N, 0.5 * h->stepSize, LC, h->CG + c * N, mC);
+  for (k = 0; k < NN; k++) L[k] = LC[k] * h->stepSize;
+  kr_cholesky(N, L);
+  lpC = mt_mvn_log_pdf(N, h->candidates + c * N, mL, L);
+  lpL = mt_mvn_log_pdf(N, h->leaders + c * N, mC, L);
+  P = kr_exp_cr((h->candidatesLL[c] - h->leadersLL[c]) * h->annealingExponent + (lpL - lpC) +
+                (h->candidatesLP[c] - h->leadersLP[c]));
+  free(mL);
+  free(mC);
+  free(L);
+  return P;
+}
+
 /* prepareGeneration, TMCMC.cpp.base:159-227 (setBurnIn :781-789) */
 void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
 {
@@ -1964,6 +2322,20 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
   h->acceptedSamplesCount = 0;
   h->maxLoglikelihood = -INFINITY;
   h->dbCount = 0;
+  if (h->LE)
+  {
+    /* :174-200: error flags of this generation's candidates, then the
+     * leaders' proposals and gradients re-annealed */
+    const double fc = h->previousAnnealingExponent / h->annealingExponent;
+    const double fg = h->annealingExponent / h->previousAnnealingExponent;
+    h->numCovarianceCorrections = 0;
+    for (i = 0; i < h->P; i++) h->CE[i] = gen > 1 ? 0 : -1;
+    for (i = 0; i < h->P; i++)
+    {
+      for (d = 0; d < N * N; d++) h->LC[i * N * N + d] *= fc;
+      for (d = 0; d < N; d++) h->LG[i * N + d] *= fg;
+    }
+  }
   memcpy(h->chol, h->cov, sizeof(double) * N * N);
   kr_cholesky(N, h->chol);
   for (i = 0; i < h->P; i++)
@@ -1972,6 +2344,8 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
     {
       for (d = 0; d < N; d++) h->candidates[i * N + d] = kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
     }
+    else if (h->LE)
+      mt_generate_candidate(h, i);
     else
       tm_generate_candidate(h, i);
   }
@@ -2027,13 +2401,24 @@ void kr_tmcmc_process_candidates(kr_tmcmc *h, size_t gen)
       double P = 0.0, U;
       if (s > 1) tm_evaluate_one(h, c);
       if (isfinite(h->candidatesLP[c]) && isfinite(h->candidatesLL[c]))
-        P = kr_exp_cr((h->candidatesLL[c] - h->leadersLL[c]) * h->annealingExponent + (h->candidatesLP[c] - h->leadersLP[c]));
+      {
+        if (h->LE && h->LE[c] == 0 && h->CE[c] == 0)
+          P = mt_acceptance(h, c);
+        else
+          P = kr_exp_cr((h->candidatesLL[c] - h->leadersLL[c]) * h->annealingExponent + (h->candidatesLP[c] - h->leadersLP[c]));
+      }
       U = kr_ran_flat(&h->uniform, 0.0, 1.0);
       if (P > U || gen == 1)
       {
         memcpy(h->leaders + c * N, h->candidates + c * N, sizeof(double) * N);
         h->leadersLP[c] = h->candidatesLP[c];
         h->leadersLL[c] = h->candidatesLL[c];
+        if (h->LE)
+        {
+          h->LE[c] = h->CE[c];
+          memcpy(h->LG + c * N, h->CG + c * N, sizeof(double) * N);
+          memcpy(h->LC + c * N * N, h->CC + c * N * N, sizeof(double) * N * N);
+        }
         if (s > B) h->acceptedSamplesCount++;
       }
       if (s < S) tm_generate_candidate(h, c);
@@ -2043,6 +2428,12 @@ void kr_tmcmc_process_candidates(kr_tmcmc *h, size_t gen)
         memcpy(h->dbX + k * N, h->leaders + c * N, sizeof(double) * N);
         h->dbLP[k] = h->leadersLP[c];
         h->dbLL[k] = h->leadersLL[c];
+        if (h->LE)
+        {
+          h->DE[k] = h->LE[c];
+          memcpy(h->DG + k * N, h->LG + c * N, sizeof(double) * N);
+          memcpy(h->DC + k * N * N, h->LC + c * N * N, sizeof(double) * N * N);
+        }
         h->dbCount += 1;
       }
     }
@@ -2314,6 +2705,12 @@ void kr_tmcmc_process_generation(kr_tmcmc *h)
       memcpy(newLeaders + leaderId * N, h->dbX + i * N, sizeof(double) * N);
       h->leadersLP[leaderId] = h->dbLP[i];
       h->leadersLL[leaderId] = h->dbLL[i];
+      if (h->LE)
+      {
+        h->LE[leaderId] = h->DE[i];
+        memcpy(h->LG + leaderId * N, h->DG + i * N, sizeof(double) * N);
+        memcpy(h->LC + leaderId * N * N, h->DC + i * N * N, sizeof(double) * N * N);
+      }
       if (nsel[i] > h->maxChainLength)
       {
         const size_t mcl = (size_t)h->maxChainLength;
@@ -2328,6 +2725,17 @@ void kr_tmcmc_process_generation(kr_tmcmc *h)
     }
   }
   memcpy(h->leaders, newLeaders, sizeof(double) * leaderId * N);
+  /* :362-372 anneal the leaders' gradients and proposals */
+  if (h->LE && h->previousAnnealingExponent > 0.0)
+  {
+    const double f = h->annealingExponent / h->previousAnnealingExponent;
+    for (i = 0; i < P; i++)
+    {
+      if (h->LE[i] != 0) continue;
+      for (j = 0; j < N; j++) h->LG[i * N + j] *= f;
+      for (j = 0; j < N * N; j++) h->LC[i * N * N + j] *= f;
+    }
+  }
   h->proposalsAcceptanceRate = (1.0 * h->acceptedSamplesCount) / P;
   h->selectionAcceptanceRate = (1.0 * (P - zeroCount)) / P;
   h->maxLoglikelihood = h->dbLL[0];

@@ -56,6 +56,8 @@ double kr_dnrm2(size_t n, const double *x, size_t inc);
 /* gsl_eigen_symmv + gsl_eigen_symmv_sort(ABS_ASC); A (row-major n x n) is
  * destroyed; evec row-major, column i = eigenvector i.  Returns #qrsteps. */
 size_t kr_eigen_symmv(size_t n, double *A, double *eval, double *evec);
+size_t kr_eigen_symmv_unsorted(size_t n, double *A, double *eval, double *evec);
+double kr_chi2inv_068(size_t n); /* gsl_cdf_chisq_Pinv(0.68, n), n <= 128 */
 int kr_cholesky(size_t n, double *A); /* 0 ok, 1 not positive definite */
 void kr_dtrmv_lower(size_t n, const double *L, double *x);
 double kr_stats_mean(const double *x, size_t n);
@@ -106,6 +108,11 @@ void kr_tmcmc_evaluate(kr_tmcmc *h);
 /* processCandidate for every chain in chain order (Sequential conduit) */
 void kr_tmcmc_process_candidates(kr_tmcmc *h, size_t generation);
 void kr_tmcmc_process_generation(kr_tmcmc *h);           /* :254-381 */
+/* mTMCMC (set_option "Version" 1, "Step Size", "Domain Extension Factor"
+ * before kr_tmcmc_initialize): calculateGradients + calculateProposals
+ * :383-558 from every candidate's gradient (P x N) and Fisher information
+ * (P x N x N); call after the evaluations, generations > 1 */
+void kr_tmcmc_set_gradients(kr_tmcmc *h, const double *grad, const double *fim);
 void kr_tmcmc_generation(kr_tmcmc *h, size_t generation);
 /* nmsimplex min search (minSearch :712-779); returns #iterations */
 size_t kr_tmcmc_minsearch(const double *loglike, size_t Ns, double exponent, double objCov, double *xmin, double *fmin);

@@ -79,6 +79,9 @@ def lib(variant="cr"):
         L.kr_tmcmc_evaluate.argtypes = [vp]
         L.kr_tmcmc_process_candidates.argtypes = [vp, sz]
         L.kr_tmcmc_process_generation.argtypes = [vp]
+        L.kr_tmcmc_set_gradients.argtypes = [vp, dp, dp]
+        L.kr_chi2inv_068.argtypes = [sz]
+        L.kr_chi2inv_068.restype = C.c_double
         L.kr_tmcmc_generation.argtypes = [vp, sz]
         L.kr_tmcmc_minsearch.argtypes = [dp, sz, C.c_double, C.c_double, dp, dp]
         L.kr_tmcmc_minsearch.restype = sz
@@ -254,6 +257,14 @@ class TMCMC:
 
     def evaluate(self):
         self.L.kr_tmcmc_evaluate(self.h)
+
+    def set_gradients(self, grad, fim):
+        """mTMCMC: every candidate's log-likelihood gradient (P x N) and Fisher
+        information (P x N x N); kr_tmcmc_set_gradients."""
+        g = np.ascontiguousarray(grad, dtype=np.float64).reshape(-1)
+        f = np.ascontiguousarray(fim, dtype=np.float64).reshape(-1)
+        dp = C.POINTER(C.c_double)
+        self.L.kr_tmcmc_set_gradients(self.h, g.ctypes.data_as(dp), f.ctypes.data_as(dp))
 
     def process_candidates(self, gen):
         self.L.kr_tmcmc_process_candidates(self.h, gen)

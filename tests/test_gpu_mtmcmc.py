@@ -1,0 +1,106 @@
+"""mTMCMC (TMCMC.cpp.base:48-83, :146-157, :174-200, :339-372, :383-681) on
+the device handle against the oracle restatement, on the reference's own
+mTMCMC example (examples/bayesian.inference/reference/run-mtmcmc.py: linear
+model, Normal likelihood with gradients, three Uniform(0, 5) priors sharing
+one distribution).  The likelihood, its gradient and the Fisher
+information are formed in numpy (tests/mtmcmc_model.py) and handed to both
+sides, as Bayesian/Reference hands them to the solver.
+
+Bar: bit-exact (np.array_equal) on candidates, leaders, errors, gradients,
+proposal covariances, database, annealing exponents, CoV, evidence,
+selections, mean and covariance.  GSL parity of the per-chain LU / inverse
+/ chi-square quantile / Gaussian log-density is unpinned (no reference
+fixture covers mTMCMC)."""
+import numpy as np
+import pytest
+
+import refcpu as R
+from mtmcmc_model import evaluate
+from test_gpu_tmcmc import SCA_KEYS, VEC_KEYS
+
+pytestmark = pytest.mark.gpu
+
+MT_KEYS = ("Chain Leaders Errors", "Chain Candidates Errors", "Sample Error Database", "Chain Leaders Gradients",
+           "Chain Candidates Gradients", "Sample Gradient Database", "Chain Leaders Covariance",
+           "Chain Candidates Covariance", "Sample Covariances Database", "Upper Extended Boundaries",
+           "Lower Extended Boundaries")
+
+
+def mt_pair(P, seed, step=0.1, ext=0.2):
+    from korali_amd.native import TmcmcDevice
+    N = 3
+    dev = TmcmcDevice(N, P, prior_min=[0.0] * N, prior_max=[5.0] * N, prior_seeds=[seed], prior_distribution=[0] * N,
+                      multinomial_seed=seed + 1, multivariate_seed=seed + 2, uniform_seed=seed + 3, version="mTMCMC",
+                      step_size=step, domain_extension_factor=ext)
+    o = R.TMCMC(N, P)
+    o.option("Version", 1)
+    o.option("Step Size", step)
+    o.option("Domain Extension Factor", ext)
+    o["Prior Minimum"] = [0.0] * N
+    o["Prior Maximum"] = [5.0] * N
+    o.set_prior_map([0] * N)
+    R.lib().kr_rng_seed(o.rng(3).ptr, seed)
+    for w in range(3):
+        R.lib().kr_rng_seed(o.rng(w).ptr, seed + 1 + w)
+    return dev, o
+
+
+def compare(dev, o, g):
+    for key in VEC_KEYS + MT_KEYS:
+        a, b = dev[key], o[key]
+        assert np.array_equal(a, b, equal_nan=True), (g, key, np.max(np.abs(a - b)))
+    for key in SCA_KEYS + ("Num Covariance Corrections",):
+        if key == "Model Evaluation Count":
+            continue
+        a, b = dev[key][0], o[key][0]
+        assert a == b or (np.isnan(a) and np.isnan(b)), (g, key, a, b)
+
+
+@pytest.mark.parametrize("P,seed", [(500, 11), (2000, 3)])
+def test_mtmcmc_matches_oracle_to_completion(P, seed):
+    dev, o = mt_pair(P, seed)
+    N = 3
+    corrections = 0
+    for g in range(1, 40):
+        if g == 1:
+            o.initialize()
+        dev.prepare(g)
+        o.prepare(g)
+        X = dev.candidates()
+        assert np.array_equal(X.reshape(-1), o["Chain Candidates"]), g
+        lp, ll, gr, fim = evaluate(X.reshape(P, N))
+        dev.set_evaluations(lp, ll)
+        o["Chain Candidates LogPriors"] = lp
+        o["Chain Candidates LogLikelihoods"] = ll
+        if g > 1:
+            dev.set_gradients(gr, fim)
+            o.set_gradients(gr, fim)
+        assert dev.advance(g) == 0
+        o.process_candidates(g)
+        dev.process(g)
+        o.process_generation()
+        dev.synchronize()
+        compare(dev, o, g)
+        corrections += dev["Num Covariance Corrections"][0]
+        if o["Previous Annealing Exponent"][0] >= 1.0:
+            break
+    assert o["Previous Annealing Exponent"][0] >= 1.0
+    assert corrections > 0  # the boundary correction of the proposals ran
+    assert np.count_nonzero(dev["Chain Leaders Errors"] == 0) > P // 2  # gradient proposals in use
+    for which in range(4):
+        assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
+    dev.close()
+
+
+def test_mtmcmc_constraints():
+    """TMCMC.cpp.base:48-55 (+ this implementation's burn-in / sharding limits)."""
+    from korali_amd.native import KoraliDeviceError, TmcmcDevice
+    kw = dict(prior_min=[0.0] * 3, prior_max=[5.0] * 3, version="mTMCMC")
+    for bad in (dict(max_chain_length=2), dict(step_size=-1.0), dict(domain_extension_factor=-0.1),
+                dict(default_burn_in=1)):
+        with pytest.raises(KoraliDeviceError):
+            TmcmcDevice(3, 100, **kw, **bad)
+    dev = TmcmcDevice(3, 100, **kw)
+    with pytest.raises(KoraliDeviceError):
+        dev.generation(1)  # the builtin likelihood has no gradients
+    dev.close()

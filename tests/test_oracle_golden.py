@@ -249,3 +249,40 @@ def test_cos_is_correctly_rounded():
     xs = list(rng.uniform(-80, 80, 400)) + list(2 * np.pi * np.arange(-40, 41) / 4) + [0.0, 1e-300, -3e-9]
     for x in xs:
         assert f(float(x)) == _decimal_cos(float(x)), x
+
+
+def test_oracle_mtmcmc_posterior_of_the_reference_example():
+    """The oracle's mTMCMC restatement on the reference's mTMCMC example
+    (run-mtmcmc.py, P = 400): it reaches annealing exponent 1 with the
+    gradient proposals in use and a posterior mean near the least-squares
+    fit of the example's data (a = 0.907, b = 2.307).  Statistical only:
+    no reference fixture covers mTMCMC."""
+    from mtmcmc_model import evaluate
+    N, P = 3, 400
+    o = R.TMCMC(N, P)
+    o["Prior Minimum"] = np.zeros(N)
+    o["Prior Maximum"] = np.full(N, 5.0)
+    o.option("Version", 1)
+    o.option("Step Size", 0.1)
+    o.option("Domain Extension Factor", 0.2)
+    o.set_prior_map([0, 0, 0])
+    for w in range(4):
+        R.lib().kr_rng_seed(o.rng(w).ptr, 100 + w)
+    for g in range(1, 40):
+        if g == 1:
+            o.initialize()
+        o.prepare(g)
+        lp, ll, gr, fim = evaluate(o["Chain Candidates"].reshape(P, N).copy())
+        o["Chain Candidates LogPriors"] = lp
+        o["Chain Candidates LogLikelihoods"] = ll
+        if g > 1:
+            o.set_gradients(gr, fim)
+        o.process_candidates(g)
+        o.process_generation()
+        if o["Previous Annealing Exponent"][0] >= 1.0:
+            break
+    assert o["Previous Annealing Exponent"][0] >= 1.0
+    assert np.count_nonzero(o["Chain Leaders Errors"] == 0) > P // 2
+    m = o["Mean Theta"]
+    assert abs(m[0] - 0.907) < 0.25 and abs(m[1] - 2.307) < 0.8 and 0.2 < m[2] < 2.0, m
+    assert R.lib().kr_chi2inv_068(3) == 3.505882355768179
