@@ -779,6 +779,11 @@ const char *TMCMC_VECTORS[] = {"Chain Leaders LogLikelihoods", "Chain Leaders Lo
                                "Chain Candidates LogPriors", "Sample LogLikelihood Database",
                                "Sample LogPrior Database", "Num Selections"};
 const char *TMCMC_MATRICES[] = {"Chain Leaders", "Chain Candidates", "Sample Database"};
+// mTMCMC state (TMCMC.config names), flattened per chain
+const char *MTMCMC_VECTORS[] = {"Chain Leaders Errors",       "Chain Candidates Errors",     "Sample Error Database",
+                                "Chain Leaders Gradients",    "Chain Candidates Gradients",  "Sample Gradient Database",
+                                "Chain Leaders Covariance",   "Chain Candidates Covariance", "Sample Covariances Database",
+                                "Upper Extended Boundaries",  "Lower Extended Boundaries"};
 const char *TMCMC_SCALARS[] = {"Annealing Exponent", "Previous Annealing Exponent", "LogEvidence",
                                "Coefficient Of Variation", "Max Loglikelihood", "Chain Count",
                                "Accepted Samples Count", "Proposals Acceptance Rate", "Selection Acceptance Rate",
@@ -787,7 +792,7 @@ const char *TMCMC_SCALARS[] = {"Annealing Exponent", "Previous Annealing Exponen
 struct TmcmcModule : SolverModule {
   kg_tmcmc_t h = nullptr;
   size_t N = 0, P = 0, ndist = 0;
-  bool builtin = false, reference = false;
+  bool builtin = false, reference = false, mtmcmc = false;
   size_t fn = 0;
   std::vector<double> referenceData;  // Bayesian/Reference
   std::string likelihoodModel;
@@ -808,7 +813,13 @@ struct TmcmcModule : SolverModule {
     rejectUnrecognised(sv, "TMCMC", {SOLVER_KEYS, TMCMC_KEYS}, {SOLVER_TERMINATION, TMCMC_TERMINATION});
     rejectProblemUnrecognised(pb, pt);
     reference = pt == "bayesian/reference";
-    if (canon(str(sv, "Version", "TMCMC")) != "tmcmc") fail("Only Version 'TMCMC' is supported by the device path.");
+    const std::string version = canon(str(sv, "Version", "TMCMC"));
+    if (version != "tmcmc" && version != "mtmcmc")
+      fail("Unrecognized value (%s) provided for mandatory setting: ['Version'] required by TMCMC.\n",
+           sv["Version"].getString().c_str());
+    mtmcmc = version == "mtmcmc";
+    // TMCMC.cpp.base:48-55
+    if (mtmcmc && !reference) fail("mTMCMC works only for problems of type 'Bayesian/Reference'\n");
     std::vector<VariableSpec> vars = readVariables(js);
     N = vars.size();
     P = uint(sv, "Population Size", 0);
@@ -839,8 +850,10 @@ struct TmcmcModule : SolverModule {
       for (size_t d = 0; d < ndist; d++)
         if (ds[d].contains("Name") && ds[d]["Name"].getString() == pn) k = (int)d;
       if (k < 0) fail("Did not find a distribution named '%s'.", pn.c_str());
-      if (canon(ds[k]["Type"].getString()) != "univariate/uniform")
+      if (canon(ds[k]["Type"].getString()) != "univariate/uniform") {
+        if (mtmcmc) fail("Only 'Univariate/Uniform' priors allowed (is %s).\n", ds[k]["Type"].getString().c_str());
         fail("The device TMCMC path supports 'Univariate/Uniform' priors (distribution '%s').", pn.c_str());
+      }
       pmin[i] = mandatory(ds[k], "Minimum", "Distributions");
       pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
       pdist[i] = k;
@@ -893,6 +906,15 @@ struct TmcmcModule : SolverModule {
     c.uniform_seed = seeds.assign(gu);
     c.likelihood = KG_LIK_GAUSSIAN;
     c.device = js.contains("Device") ? (int)js["Device"].getInt() : 0;
+    c.version = mtmcmc ? 1 : 0;
+    c.step_size = num(sv, "Step Size", 0.1);
+    c.domain_extension_factor = num(sv, "Domain Extension Factor", 0.2);
+    if (mtmcmc) {
+      if (mcl != 1) fail("Current version of 'mTMCMC' supports only 'Max Chain Length' of 1 (BASIS).");
+      if (c.step_size < 0.0) fail("Step Size lower than 0.0 (is %lf)\n", c.step_size);
+      if (c.domain_extension_factor < 0.0)
+        fail("Domain Extension Factor lower than 0.0 (is %lf)\n", c.domain_extension_factor);
+    }
     check(kg_tmcmc_create(&c, &h));
     unsigned char st[5000];
     if (seeds.range(gm, st)) check(kg_tmcmc_set_rng(h, 0, st));
@@ -923,6 +945,14 @@ struct TmcmcModule : SolverModule {
         const double v = sv[k].getDouble();
         check(kg_tmcmc_set_field(h, k, &v, 1));
       }
+    if (mtmcmc)
+      for (const char *k : MTMCMC_VECTORS)
+        if (sv.contains(k) && sv[k].is_array() && sv[k].size()) {
+          std::vector<double> v = flatten(sv[k]);
+          size_t n = 0;
+          check(kg_tmcmc_field_size(h, k, &n));
+          if (v.size() == n) check(kg_tmcmc_set_field(h, k, v.data(), n));
+        }
   }
 
   double field(const char *k) {
@@ -942,6 +972,12 @@ struct TmcmcModule : SolverModule {
       // bayesian.cpp.base:56-77), then advances every chain one step
       std::vector<double> X(P * N), LP(P), LL(P);
       std::vector<unsigned char> pend(P);
+      // mTMCMC (generations > 1): calculateGradients / calculateProposals
+      // :383-558 from each finite sample's "logLikelihood Gradient" and
+      // "Fisher Information" (Reference::evaluate*, from the model outputs
+      // the evaluation stored in the sample)
+      const bool grads = mtmcmc && gen > 1;
+      std::vector<double> G(grads ? P * N : 0), FIM(grads ? P * N * N : 0);
       Function &f = getFunction(fn);
       for (size_t pending = 1; pending;) {
         check(kg_tmcmc_evaluate_prior(h));
@@ -970,8 +1006,15 @@ struct TmcmcModule : SolverModule {
           if (!s.contains("logLikelihood")) fail("The likelihood model did not assign 'logLikelihood' for sample %zu.", i);
           LL[i] = s["logLikelihood"].getDouble();
           if (std::isnan(LL[i])) fail("Non finite value of log-likelihood detected: %f\n", LL[i]);
+          if (grads && std::isfinite(LL[i]) && std::isfinite(LP[i])) {
+            const auto g = referenceLoglikelihoodGradient(likelihoodModel, referenceData, s, N);
+            const auto F = referenceFisherInformation(likelihoodModel, referenceData, s, N);
+            std::copy(g.begin(), g.end(), G.begin() + i * N);
+            std::copy(F.begin(), F.end(), FIM.begin() + i * N * N);
+          }
         });
         check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
+        if (grads) check(kg_tmcmc_set_gradients(h, G.data(), FIM.data()));
         check(kg_tmcmc_advance(h, gen, &pending));
       }
     }
@@ -1001,6 +1044,16 @@ struct TmcmcModule : SolverModule {
       sv[k] = matrixJson(v, n / N, N);
     }
     for (const char *k : TMCMC_SCALARS) sv[k] = field(k);
+    if (mtmcmc) {
+      for (const char *k : MTMCMC_VECTORS) {
+        size_t n = 0;
+        check(kg_tmcmc_field_size(h, k, &n));
+        std::vector<double> v(n);
+        check(kg_tmcmc_get_field(h, k, v.data(), n));
+        sv[k] = v;
+      }
+      sv["Num Covariance Corrections"] = field("Num Covariance Corrections");
+    }
     unsigned char st[5000];
     check(kg_tmcmc_get_rng(h, 0, st));
     sv["Multinomial Generator"]["Range"] = hexState(st);

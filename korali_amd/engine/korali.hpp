@@ -141,6 +141,10 @@ void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &b
 // KORALI_LOG_ERROR on malformed entries.
 double referenceLoglikelihood(const std::string &model, const std::vector<double> &y, Sample &s);
 bool isReferenceLikelihoodModel(const std::string &model);
+std::vector<double> referenceLoglikelihoodGradient(const std::string &model, const std::vector<double> &y, Sample &s,
+                                                   size_t nth);
+std::vector<double> referenceFisherInformation(const std::string &model, const std::vector<double> &y, Sample &s,
+                                               size_t nth);
 // Bayesian::evaluate of one parameter vector under an experiment's Problem /
 // Distributions / Variables (the host evaluation CMA-ES uses on Bayesian
 // problems); returns the sample's JSON (logPrior, logLikelihood, F(x), ...)

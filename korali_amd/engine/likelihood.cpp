@@ -235,6 +235,71 @@ double referenceLoglikelihood(const std::string &model, const std::vector<double
   lfail("Bayesian problem (%s) not recognized.\n", model.c_str());
 }
 
+// the model's per-datum derivative arrays (KORALI_GET of
+// std::vector<std::vector<double>>): nd rows of nth values
+static std::vector<std::vector<double>> mat(Sample &s, const char *key, size_t nd, size_t nth, const char *what) {
+  if (!s.contains(key) || !s[key].is_array())
+    lfail("Missing or incorrect value ['%s'] for the sample.\n", key);
+  std::vector<std::vector<double>> m;
+  for (const Json &row : s[key].elements()) {
+    std::vector<double> r;
+    if (row.is_array())
+      for (const Json &x : row.elements()) r.push_back(x.getDouble());
+    m.push_back(r);
+  }
+  if (m.size() != nd)
+    lfail("Bayesian problem requires a gradient of the %s for each reference evaluation (provided %zu required %zu).",
+          what, m.size(), nd);
+  for (auto &r : m)
+    if (r.size() != nth)
+      lfail("Bayesian Reference %s gradient calculation requires gradients of size %zu (provided size %zu)\n", what, nth,
+            r.size());
+  return m;
+}
+
+// Reference::evaluateLoglikelihoodGradient, Normal (reference.cpp.base:231-286):
+// sum over data of -g'/g + (y - f) f'/g^2 + (y - f)^2 g'/g^3
+std::vector<double> referenceLoglikelihoodGradient(const std::string &model, const std::vector<double> &y, Sample &s,
+                                                   size_t nth) {
+  if (model != "Normal") lfail("Gradient not yet implemented for logLikelihood model of type '%s'.", model.c_str());
+  const size_t nd = y.size();
+  auto f = vec(s, "Reference Evaluations", model, nd);
+  auto g = vec(s, "Standard Deviation", model, nd);
+  auto gF = mat(s, "Gradient Mean", nd, nth, "Mean");
+  auto gG = mat(s, "Gradient Standard Deviation", nd, nth, "Standard Deviation");
+  std::vector<double> out(nth, 0.0);
+  for (size_t i = 0; i < nd; ++i) {
+    const double inv = 1.0 / g[i], inv2 = inv * inv, inv3 = inv2 * inv;
+    const double dif = y[i] - f[i];
+    for (size_t d = 0; d < nth; ++d)
+      out[d] += -inv * gG[i][d] + inv2 * dif * gF[i][d] + inv3 * dif * dif * gG[i][d];
+  }
+  return out;
+}
+
+// Reference::evaluateFisherInformation, Normal (reference.cpp.base:514-566)
+std::vector<double> referenceFisherInformation(const std::string &model, const std::vector<double> &y, Sample &s,
+                                               size_t nth) {
+  if (model != "Normal") lfail("Fisher Information not yet implemented for logLikelihood model of type '%s'.", model.c_str());
+  const size_t nd = y.size();
+  auto g = vec(s, "Standard Deviation", model, nd);
+  auto gF = mat(s, "Gradient Mean", nd, nth, "Mean");
+  auto gG = mat(s, "Gradient Standard Deviation", nd, nth, "Standard Deviation");
+  std::vector<double> F(nth * nth, 0.0);
+  for (size_t i = 0; i < nd; ++i) {
+    const double var = g[i] * g[i], vinv = 1. / var;
+    for (size_t k = 0; k < nth; ++k) {
+      for (size_t l = 0; l < k; ++l) {
+        const double t = vinv * gF[i][k] * gF[i][l] + 2. * vinv * gG[i][k] * gG[i][l];
+        F[k * nth + l] += t;
+        F[l * nth + k] += t;
+      }
+      F[k * nth + k] += (vinv * gF[i][k] * gF[i][k] + 2. * vinv * gG[i][k] * gG[i][k]);
+    }
+  }
+  return F;
+}
+
 bool isReferenceLikelihoodModel(const std::string &model) {
   for (const char *m : {"Normal", "Positive Normal", "StudentT", "Positive StudentT", "Poisson", "Geometric", "Negative Binomial"})
     if (model == m) return true;

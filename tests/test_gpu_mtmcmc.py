@@ -104,3 +104,82 @@ def test_mtmcmc_constraints():
     with pytest.raises(KoraliDeviceError):
         dev.generation(1)  # the builtin likelihood has no gradients
     dev.close()
+
+
+REF_X = [1.0, 2.0, 3.0, 4.0, 5.0]
+REF_Y = [3.21, 4.14, 4.94, 6.06, 6.84]
+
+
+def model_with_gradients(s):  # _model/model.py:20-39, the reference's list-append idiom
+    a = s["Parameters"][0]
+    b = s["Parameters"][1]
+    sig = s["Parameters"][2]
+    s["Reference Evaluations"] = []
+    s["Standard Deviation"] = []
+    s["Gradient Mean"] = []
+    s["Gradient Standard Deviation"] = []
+    for x in REF_X:
+        s["Reference Evaluations"] += [a * x + b]
+        s["Standard Deviation"] += [sig]
+        s["Gradient Mean"] += [[x, 1.0, 0.0]]
+        s["Gradient Standard Deviation"] += [[0.0, 0.0, 1.0]]
+
+
+def mtmcmc_experiment(P=1000, problem="Bayesian/Reference"):
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = problem
+    if problem == "Bayesian/Reference":
+        e["Problem"]["Likelihood Model"] = "Normal"
+        e["Problem"]["Reference Data"] = REF_Y
+        e["Problem"]["Computational Model"] = model_with_gradients
+    else:
+        e["Problem"]["Likelihood Model"] = lambda s: None
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    e["Solver"]["Version"] = "mTMCMC"
+    e["Solver"]["Population Size"] = P
+    e["Distributions"][0]["Name"] = "Uniform 0"
+    e["Distributions"][0]["Type"] = "Univariate/Uniform"
+    e["Distributions"][0]["Minimum"] = 0.0
+    e["Distributions"][0]["Maximum"] = +5.0
+    for i, n in enumerate(("a", "b", "[Sigma]")):
+        e["Variables"][i]["Name"] = n
+        e["Variables"][i]["Prior Distribution"] = "Uniform 0"
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["Random Seed"] = 4321
+    return e
+
+
+def test_engine_runs_the_reference_mtmcmc_example():
+    """examples/bayesian.inference/reference/run-mtmcmc.py through
+    korali.Engine (P = 1000): runs to annealing exponent 1 with the gradient
+    proposals in use, the posterior mean near the example's least-squares
+    fit, the mTMCMC state in the solver's configuration."""
+    import korali
+    e = mtmcmc_experiment()
+    korali.Engine().run(e)
+    sv = e["Solver"]
+    assert sv["Previous Annealing Exponent"] >= 1.0
+    err = np.asarray(sv["Chain Leaders Errors"], dtype=float)
+    assert np.count_nonzero(err == 0) > 500
+    assert len(sv["Chain Leaders Covariance"]) == 1000 * 9
+    db = np.asarray(sv["Sample Database"], dtype=float).reshape(-1, 3)
+    m = db.mean(0)
+    assert abs(m[0] - 0.907) < 0.2 and abs(m[1] - 2.307) < 0.7 and 0.05 < m[2] < 2.0, m
+
+
+def test_engine_mtmcmc_constraints():
+    """TMCMC.cpp.base:48-55 through the API: Bayesian/Reference only, Max
+    Chain Length 1, non-negative Step Size."""
+    import korali
+    with pytest.raises(Exception, match="mTMCMC works only for problems of type 'Bayesian/Reference'"):
+        korali.Engine().run(mtmcmc_experiment(50, "Bayesian/Custom"))
+    e = mtmcmc_experiment(50)
+    e["Solver"]["Max Chain Length"] = 2
+    with pytest.raises(Exception, match="supports only 'Max Chain Length' of 1"):
+        korali.Engine().run(e)
+    e = mtmcmc_experiment(50)
+    e["Solver"]["Step Size"] = -1.0
+    with pytest.raises(Exception, match="Step Size lower than 0.0"):
+        korali.Engine().run(e)
