@@ -160,6 +160,21 @@ def _cmaes_oracle_rate(variant, warmup, gens_min, seconds_budget, N=N_VARS, lam=
     return n, el
 
 
+def _dispatch_rate(seconds_budget):
+    """BASELINE.md §2 variant (ii): generations/s of C2 with per-sample JSON
+    dispatch (oracle/dispatch_baseline, built by `make -C oracle`), or None
+    when the binary is absent."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "dispatch_baseline")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe, str(N_VARS), str(LAMBDA), "10", "100", str(seconds_budget)], capture_output=True,
+                       text=True, timeout=60 * seconds_budget + 120)
+    if r.returncode != 0:
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])["generations_per_sec"]
+
+
 def cpu_baseline(seconds_budget=6.0):
     """The reference's arithmetic on this host's CPU: the
     oracle restatement, -O3 without -march, one thread pinned to one core,
@@ -172,9 +187,13 @@ def cpu_baseline(seconds_budget=6.0):
     with pinned_core() as core:
         gens, el = _cmaes_oracle_rate("libm", 10, 100, seconds_budget)
         gens_cr, el_cr = _cmaes_oracle_rate("cr", 2, 10, seconds_budget / 2)
+        v2 = _dispatch_rate(seconds_budget)
     return {"value": gens / el, "unit": "generations/s", "cores": 1, "kind": "port",
             "samples_per_sec": gens * LAMBDA / el,
             "bit_exact_port_value": gens_cr / el_cr,
+            "variant_ii_value": v2,
+            "variant_ii": "the same loop with every sample dispatched as a korali::Json Sample through a "
+                          "Sequential-conduit loop (oracle/dispatch_baseline.cpp, -O3, system libm), 10 warm-up",
             "cpu": f"{cpu_model()}, 1 of {os.cpu_count()} cores (pinned to core {core})",
             "sample": f"{gens} generations of C2 (N=128, lambda=4096) after 10 warm-up, oracle/refcpu.c -O3 "
                       f"(no -march) with system libm, 1 thread, variant (i) inline objective; bit-exact CR build: "
