@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
                                                    const double *__restrict__ mean, CmaesScalars *__restrict__ sc,
                                                    const double *__restrict__ lb, const double *__restrict__ ub,
                                                    double *__restrict__ X, double *__restrict__ BDZ,
-                                                   int *__restrict__ infeas, int no_reserve) {
+                                                   int *__restrict__ infeas, int no_reserve, int mirrored) {
   __shared__ double Za[TR_BK][TR_BM + 1];
   __shared__ double Bt[TR_BK][TR_BN + 1];
   const int tid = threadIdx.x;
@@ -161,7 +161,13 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
       for (int q = tid; q < TR_BM * TR_BK; q += 256) {
         const int c = q / TR_BK, kk = q % TR_BK;
         const int i = i0 + c, e = k0 + kk;
-        Za[kk][c] = (i < rows && e < N) ? D[e] * Z[(size_t)i * N + e] : 0.0;
+        // Mirrored Sampling (:461-491): rows 2j and 2j+1 take z_j and -z_j
+        double z = 0.0;
+        if (i < rows && e < N) {
+          z = Z[(size_t)(mirrored ? (i >> 1) : i) * N + e];
+          if (mirrored && (i & 1)) z = -z;
+        }
+        Za[kk][c] = (i < rows && e < N) ? D[e] * z : 0.0;
       }
       for (int q = tid; q < TR_BN * TR_BK; q += 256) {
         const int dd = q / TR_BK, kk = q % TR_BK;
@@ -191,7 +197,12 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
     for (int q = 0; q < 2; q++) {
       const int d = d0 + tx + 32 * q;
       if (d >= N) continue;
-      const double bdz = diagonal ? D[d] * Z[(size_t)i * N + d] : acc[p][q];
+      double zd = 0.0;
+      if (diagonal) {
+        zd = Z[(size_t)(mirrored ? (i >> 1) : i) * N + d];
+        if (mirrored && (i & 1)) zd = -zd;
+      }
+      const double bdz = diagonal ? D[d] * zd : acc[p][q];
       const double x = mean[d] + sigma * bdz;
       X[(size_t)i * N + d] = x;
       if (BDZ) BDZ[(size_t)i * N + d] = bdz;
@@ -229,6 +240,38 @@ __global__ void k_select(int lam, int blocks, double maxRes, const int *__restri
       const int jj = j++;
       if (feasible || !(count < maxRes)) {
         assign[i] = jj;
+        break;
+      }
+    }
+  }
+  sc->infeasibleSampleCount = count;
+  *used = (unsigned long long)j;
+}
+
+// Mirrored Sampling's resampling (:461-491): pair p takes the next block j
+// (rows 2j, 2j+1) of which either draw is feasible; each infeasible draw
+// counts
+__global__ void k_select_mirrored(int pairs, int blocks, double maxRes, const int *__restrict__ infeas,
+                                  int *__restrict__ assign, unsigned long long *__restrict__ used, CmaesScalars *sc) {
+  if (threadIdx.x != 0) return;
+  double count = sc->infeasibleSampleCount;
+  int j = 0;
+  for (int p = 0; p < pairs; p++) {
+    for (;;) {
+      if (j >= blocks) {
+        sc->errors |= KG_ERR_RESAMPLE_RESERVE;
+        assign[2 * p] = 2 * (blocks - 1);
+        assign[2 * p + 1] = 2 * (blocks - 1) + 1;
+        break;
+      }
+      const int ok1 = infeas[2 * j] ? 0 : 1;
+      if (!ok1) count += 1;
+      const int ok2 = infeas[2 * j + 1] ? 0 : 1;
+      if (!ok2) count += 1;
+      const int jj = j++;
+      if (ok1 || ok2 || !(count < maxRes)) {
+        assign[2 * p] = 2 * jj;
+        assign[2 * p + 1] = 2 * jj + 1;
         break;
       }
     }
@@ -1276,6 +1319,8 @@ struct kg_cmaes_s {
   EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
+  bool mirrored = false;  // "Mirrored Sampling": blocks of N normals feed two rows
+  size_t blocks = 0;      // normal blocks drawn per generation (λ or λ/2, + the reserve R)
   int kslices = 8;  // rank-mu K-slices (rankmu_kslices), a multiple of the 8 XCDs
   // population shards
   int shards = 1, shardRank = 0, r0 = 0, r1 = 0;
@@ -1456,7 +1501,9 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   KG_CHECK(cfg && out, "kg_cmaes_create: null argument");
   KG_CHECK(cfg->variable_count >= 1, "'Variable Count' must be >= 1");
   KG_CHECK(cfg->population_size > 1, "'Population Size' must be larger 1.");  // CMAES.cpp.base:26
-  KG_CHECK(!cfg->mirrored_sampling, "Mirrored Sampling is not supported by the device path yet");
+  KG_CHECK(!cfg->mirrored_sampling || cfg->population_size % 2 == 0,
+           "Mirrored Sampling can only be applied with an even Sample Population");  // CMAES.cpp.base:91
+  KG_CHECK(!cfg->mirrored_sampling || cfg->shard_count <= 1, "Mirrored Sampling runs unsharded");
   KG_CHECK(cfg->variable_count <= 960, "device path supports up to 960 variables");
   KG_CHECK(cfg->mu_type >= 0 && cfg->mu_type <= 3,
            "Invalid setting of Mu Type (Linear, Equal, Logarithmic, or Proportional accepted).");
@@ -1509,7 +1556,10 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   }
   h->r0 = h->shardRank * (L / h->shards);
   h->r1 = h->r0 + L / h->shards;
+  h->mirrored = cfg->mirrored_sampling != 0;
+  h->blocks = (h->mirrored ? (size_t)L / 2 : (size_t)L) + h->R;
   const size_t rows = (size_t)L + h->R;
+  const size_t xrows = h->mirrored ? 2 * h->blocks : rows;  // transformed rows (Xall, infeasibility flags)
   int rc = 0;
   rc |= dalloc(&h->mean, N) | dalloc(&h->prevMean, N) | dalloc(&h->C, (size_t)N * N) | dalloc(&h->B, (size_t)N * N);
   rc |= dalloc(&h->D, N) | dalloc(&h->pc, N) | dalloc(&h->ps, N) | dalloc(&h->w, h->mu);
@@ -1519,11 +1569,11 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->Y, (size_t)h->mu * N);
   if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->mu * N) | dalloc(&h->Tt, (size_t)h->mu * N);
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
-  rc |= dalloc(&h->infeas, rows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
+  rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
   if (h->R) {
-    rc |= dalloc(&h->Xall, rows * N);
-    if (cfg->store_bdz) rc |= dalloc(&h->BDZall, rows * N);
+    rc |= dalloc(&h->Xall, xrows * N);
+    if (cfg->store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
   }
   size_t P2 = 1;
   while (P2 < (size_t)L) P2 <<= 1;
@@ -1571,7 +1621,8 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     }
   }
   {
-    const unsigned long long used = (unsigned long long)L;  // no-reserve path consumes exactly λ blocks
+    // the no-reserve path consumes exactly λ blocks (λ/2 when mirrored)
+    const unsigned long long used = (unsigned long long)(h->mirrored ? L / 2 : L);
     KG_HIP(hipMemcpy(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice));
   }
   KG_HIP(hipMemcpy(h->lb, lb.data(), N * sizeof(double), hipMemcpyHostToDevice));
@@ -1639,8 +1690,8 @@ static int cmaes_eigen(kg_cmaes_t h) {
 }
 
 static int cmaes_draw_begin(kg_cmaes_t h) {
-  const int N = h->N, L = h->lam;
-  const size_t rows = (size_t)L + h->R;
+  const int N = h->N;
+  const size_t rows = h->blocks;
   if (h->normal.prefetch(rows * N, h->stream)) return 1;  // overlaps the eigensolver
   // the polar pass reads only the generator stream: it runs on the
   // producer's side stream too, concurrently with the eigensolver
@@ -1662,7 +1713,7 @@ int kg_cmaes_begin_sample(kg_cmaes_t h) {
 
 int kg_cmaes_sample(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
-  const size_t rows = (size_t)L + h->R;
+  const size_t rows = h->mirrored ? 2 * h->blocks : (size_t)L + h->R;  // transformed rows
   if (!h->sampleBegun && cmaes_draw_begin(h)) return 1;
   h->sampleBegun = false;
   if (cmaes_eigen(h)) return 1;
@@ -1680,11 +1731,15 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     double *bo = h->R ? h->BDZall : (h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr);
     hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)trows,
                        h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
-                       h->infeas, h->R ? 0 : 1);
+                       h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
     KG_HIP(hipGetLastError());
     if (h->R) {
-      hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
-                         h->infeas, h->assign, h->usedBlocks, h->sc);
+      if (h->mirrored)
+        hipLaunchKernelGGL(k_select_mirrored, dim3(1), dim3(64), 0, h->stream, L / 2, (int)h->blocks,
+                           h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->sc);
+      else
+        hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
+                           h->infeas, h->assign, h->usedBlocks, h->sc);
       const size_t tot = (size_t)L * N;
       hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, L, h->assign,
                          h->Xall, h->X, h->BDZall, h->BDZ);

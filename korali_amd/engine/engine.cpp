@@ -562,7 +562,10 @@ struct CmaesModule : SolverModule {
                                                 : -1;
     if (muTypeId < 0)
       fail("Invalid setting of Mu Type (%s) (Linear, Equal, Logarithmic, or Proportional accepted).", muType.c_str());
-    if (flag(sv, "Mirrored Sampling", false)) fail("'Mirrored Sampling' is not supported by the device path yet.");
+    const bool mirrored = flag(sv, "Mirrored Sampling", false);
+    if (mirrored && uint(sv, "Population Size", 0) % 2 == 1)  // CMAES.cpp.base:89-92
+      fail("Mirrored Sampling can only be applied with an even Sample Population (is %zu)",
+           (size_t)uint(sv, "Population Size", 0));
     if (flag(sv, "Use Gradient Information", false))
       fail("'Use Gradient Information' is not supported by the device path.");
     if (pb.contains("Constraints") && pb["Constraints"].size() > 0)
@@ -617,7 +620,7 @@ struct CmaesModule : SolverModule {
     c.initial_cumulative_covariance = num(sv, "Initial Cumulative Covariance", -1.0);
     c.is_sigma_bounded = flag(sv, "Is Sigma Bounded", false);
     c.diagonal_covariance = flag(sv, "Diagonal Covariance", false);
-    c.mirrored_sampling = 0;
+    c.mirrored_sampling = mirrored ? 1 : 0;
     c.max_infeasible_resamplings = maxInfeasible;
     c.lower_bound = lb.data();
     c.upper_bound = ub.data();

@@ -160,7 +160,7 @@ class CmaesDevice:
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
                  initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host", shard_rank=0,
-                 shard_count=1):
+                 shard_count=1, mirrored=False):
         L = lib()
         self.N, self.lam = int(N), int(lam)
         self.mu = int(mu) if mu else self.lam // 2
@@ -175,7 +175,8 @@ class CmaesDevice:
         cfg.initial_sigma_cumulation_factor = initial_sigma_cumulation_factor
         cfg.initial_damp_factor = initial_damp_factor
         cfg.initial_cumulative_covariance = initial_cumulative_covariance
-        cfg.is_sigma_bounded, cfg.diagonal_covariance, cfg.mirrored_sampling = int(is_sigma_bounded), int(diagonal), 0
+        cfg.is_sigma_bounded, cfg.diagonal_covariance = int(is_sigma_bounded), int(diagonal)
+        cfg.mirrored_sampling = int(bool(mirrored))
         cfg.max_infeasible_resamplings = float(max_infeasible_resamplings)
         (cfg.lower_bound, cfg.upper_bound, cfg.initial_value, cfg.initial_std,
          cfg.min_std_update) = [_dptr(a) for a in self._arrays]

@@ -227,3 +227,76 @@ def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
         for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Current Mean", "Covariance Matrix"):
             assert np.array_equal(dev[key], o[key]), (g, key)
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+
+
+@pytest.mark.parametrize("Nv,lam,bound,gens,diag", [(8, 16, None, 20, False), (8, 16, 1.5, 20, False),
+                                                    (32, 256, 3.0, 6, False), (16, 64, 2.0, 10, True)])
+def test_mirrored_sampling_matches_oracle_bit_exact(Nv, lam, bound, gens, diag):
+    """Mirrored Sampling (CMAES.cpp.base:461-491): rows 2j / 2j+1 from z_j and
+    -z_j, a pair redrawn only when both of its samples are infeasible (each
+    infeasible draw counted); unbounded and bounded, full and diagonal
+    covariance, against the oracle bit for bit."""
+    seed = 77
+    o = R.CMAES(Nv, lam, 0)
+    o["Initial Value"] = np.zeros(Nv)
+    o["Initial Standard Deviation"] = np.ones(Nv)
+    o.option("Mirrored Sampling", 1)
+    if diag:
+        o.option("Diagonal Covariance", 1)
+    kw = {}
+    if bound is not None:
+        o["Lower Bound"] = np.full(Nv, -bound)
+        o["Upper Bound"] = np.full(Nv, bound)
+        kw = dict(lower_bound=np.full(Nv, -bound), upper_bound=np.full(Nv, bound))
+    R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+    R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+    dev = device_solver(Nv, lam, initial_value=np.zeros(Nv), initial_std=np.ones(Nv), normal_seed=seed,
+                        uniform_seed=seed + 1, mirrored=True, diagonal=diag, **kw)
+    for g in range(1, gens + 1):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        X = dev["Sample Population"].reshape(lam, Nv)
+        assert np.array_equal(X, o["Sample Population"].reshape(lam, Nv)), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        for key in ("Current Mean", "Covariance Matrix", "Axis Lengths"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        assert dev["Sigma"][0] == o["Sigma"][0], g
+        assert dev["Infeasible Sample Count"][0] == o["Infeasible Sample Count"][0], g
+    if bound is not None:
+        assert o["Infeasible Sample Count"][0] > 0  # the pair resampling ran
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+    dev.close()
+
+
+def test_mfma_covariance_mode_trajectory():
+    """The MFMA rank-mu mode over a whole trajectory (no re-sync): mean and
+    covariance stay within 1e-6 relative of the bit-exact trajectory (the
+    north star's tolerance) while the selection agrees, and the generation at
+    which the first selection index differs is reported, not hidden."""
+    Nv, lam, gens = 32, 256, 40
+    seed = 9
+    ex = device_solver(Nv, lam, initial_value=np.zeros(Nv), initial_std=np.ones(Nv), normal_seed=seed,
+                       uniform_seed=seed + 1, cov_mode="exact")
+    mf = device_solver(Nv, lam, initial_value=np.zeros(Nv), initial_std=np.ones(Nv), normal_seed=seed,
+                       uniform_seed=seed + 1, cov_mode="mfma")
+    first_split, worst = None, 0.0
+    for g in range(1, gens + 1):
+        ex.generation(g, "rosenbrock")
+        mf.generation(g, "rosenbrock")
+        ex.synchronize()
+        mf.synchronize()
+        same = np.array_equal(ex.sorting_index(), mf.sorting_index())
+        if not same:
+            first_split = g
+            break
+        for key in ("Current Mean", "Covariance Matrix"):
+            a, b = ex[key], mf[key]
+            rel = np.max(np.abs(a - b)) / np.max(np.abs(a))
+            worst = max(worst, rel)
+            assert rel < 1e-6, (g, key, rel)
+    print(f"MFMA trajectory: max relative deviation {worst:.3e}; first differing selection at generation "
+          f"{first_split} of {gens}")
+    assert first_split is None or first_split > 3
+    ex.close()
+    mf.close()
