@@ -67,7 +67,7 @@ def base_cmaes():
 @pytest.mark.parametrize("key,value,msg", [
     ("Population Size", 1, "'Population Size' must be larger 1"),
     ("Mu Type", "Quadratic", "Invalid setting of Mu Type"),
-    ("Mirrored Sampling", True, "Mirrored Sampling"),
+    ("Use Gradient Information", True, "Use Gradient Information"),
     ("Type", "Optimizer/DEA", "Unrecognized solver type"),
 ])
 def test_configuration_errors_before_device(key, value, msg):
