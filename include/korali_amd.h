@@ -87,6 +87,12 @@ typedef struct {
                                              1: on one device lane.  Identical results. */
   int shard_rank;                         /* population sharding: this rank's index */
   int shard_count;                        /* ranks sharing one population; 0 or 1 = unsharded */
+  /* "Use Gradient Information" / "Gradient Step Size" (CMAES.cpp.base:82-87,
+   * :611-621): the mean moves by sum_i w_i step / sqrt(N) g_(i) after the
+   * weighted recombination; the samples' gradients come through
+   * kg_cmaes_set_gradients (host-evaluated objectives only, unsharded) */
+  int use_gradients;
+  double gradient_step_size;
 } kg_cmaes_cfg;
 
 int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);
@@ -100,6 +106,9 @@ int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F);
  * kg_cmaes_set_fitness, but -inf (a candidate outside the prior's support)
  * is a valid value; NaN and +inf are still rejected.  Ties sort by index. */
 int kg_cmaes_set_log_posterior(kg_cmaes_t h, const double *F);
+/* the samples' "Gradient" (lambda x N, row i = sample i), with
+ * use_gradients, after kg_cmaes_set_fitness and before kg_cmaes_update */
+int kg_cmaes_set_gradients(kg_cmaes_t h, const double *G);
 int kg_cmaes_update(kg_cmaes_t h, size_t generation);
 /* One whole generation (CMAES::runGeneration).  The device work is enqueued
  * on the handle's stream, but the call itself BLOCKS the calling thread for

@@ -760,6 +760,22 @@ __global__ void __launch_bounds__(256) k_adaptC_exact2(int N, int mu, int diagon
 // time (next chunk loaded while the current one is summed), and MN_D lanes
 // of wave 0 add them in order (an add-only chain at the FP64 add latency).
 constexpr int MN_D = 8, MN_R = 256;
+// the gradient-informed mean step (CMAES.cpp.base:611-621), after k_mean:
+// mean_d += ((w_i step) / sqrt(N)) g_(i),d in selection order, then the
+// mean update again
+__global__ void k_mean_gradient(int N, int mu, double step, const double *__restrict__ G,
+                                const unsigned *__restrict__ idx, const double *__restrict__ w, double *mean,
+                                const double *__restrict__ prevMean, double *meanUpdate,
+                                const CmaesScalars *__restrict__ sc) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= N) return;
+  const double rn = sqrt((double)N);
+  double acc = mean[d];
+  for (int i = 0; i < mu; i++) acc += w[i] * step / rn * G[(size_t)idx[i] * N + d];
+  mean[d] = acc;
+  meanUpdate[d] = (acc - prevMean[d]) / sc->sigma;
+}
+
 __global__ void __launch_bounds__(256) k_mean(int N, int mu, const double *__restrict__ Y,
                                               const double *__restrict__ w, double *mean, double *prevMean,
                                               double *meanUpdate, const CmaesScalars *__restrict__ sc) {
@@ -1320,6 +1336,7 @@ struct kg_cmaes_s {
   int *infeas = nullptr, *assign = nullptr;
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
   bool mirrored = false;  // "Mirrored Sampling": blocks of N normals feed two rows
+  double *G = nullptr;    // samples' gradients (use_gradients)
   size_t blocks = 0;      // normal blocks drawn per generation (λ or λ/2, + the reserve R)
   int kslices = 8;  // rank-mu K-slices (rankmu_kslices), a multiple of the 8 XCDs
   // population shards
@@ -1504,6 +1521,9 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   KG_CHECK(!cfg->mirrored_sampling || cfg->population_size % 2 == 0,
            "Mirrored Sampling can only be applied with an even Sample Population");  // CMAES.cpp.base:91
   KG_CHECK(!cfg->mirrored_sampling || cfg->shard_count <= 1, "Mirrored Sampling runs unsharded");
+  KG_CHECK(!cfg->use_gradients || cfg->gradient_step_size > 0.0,
+           "Gradient Step Size must be larger than 0.0");  // CMAES.cpp.base:86
+  KG_CHECK(!cfg->use_gradients || cfg->shard_count <= 1, "Use Gradient Information runs unsharded");
   KG_CHECK(cfg->variable_count <= 960, "device path supports up to 960 variables");
   KG_CHECK(cfg->mu_type >= 0 && cfg->mu_type <= 3,
            "Invalid setting of Mu Type (Linear, Equal, Logarithmic, or Proportional accepted).");
@@ -1571,6 +1591,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
   rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
+  if (cfg->use_gradients) rc |= dalloc(&h->G, (size_t)L * N);
   if (h->R) {
     rc |= dalloc(&h->Xall, xrows * N);
     if (cfg->store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
@@ -1655,7 +1676,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
                   (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y, (void *)h->Yc, (void *)h->Tt,
-                  (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part})
+                  (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -1787,6 +1808,14 @@ int kg_cmaes_set_fitness(kg_cmaes_t h, const double *F) { return cmaes_upload_fi
 
 int kg_cmaes_set_log_posterior(kg_cmaes_t h, const double *F) { return cmaes_upload_fitness(h, F, true); }
 
+int kg_cmaes_set_gradients(kg_cmaes_t h, const double *G) {
+  KG_CHECK(h->G, "kg_cmaes_set_gradients: the handle was created without use_gradients");
+  KG_CHECK(G, "kg_cmaes_set_gradients: null argument");
+  KG_HIP(hipMemcpyAsync(h->G, G, (size_t)h->lam * h->N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));  // G may be a caller's temporary
+  return 0;
+}
+
 static int cmaes_sort(kg_cmaes_t h) {
   const int L = h->lam;
   {
@@ -1874,6 +1903,9 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     KG_HIP(hipEventRecord(h->evC, h->stream2));
     hipLaunchKernelGGL(k_mean, dim3((N + MN_D - 1) / MN_D), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
                        h->prevMean, h->meanUpdate, h->sc);
+    if (h->G)
+      hipLaunchKernelGGL(k_mean_gradient, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->cfg.gradient_step_size,
+                         h->G, h->idx, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     if (cmaes_paths(h, generation)) return 1;
   }
   {

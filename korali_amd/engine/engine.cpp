@@ -532,6 +532,7 @@ struct CmaesModule : SolverModule {
   double maxGenerations, maxModelEvaluations, maxInfeasible, maxCondition, minStd, maxStd, maxValue, minValueDiff;
   Json *solverJs = nullptr;
   bool updated = false;  // kg_cmaes_update ran on this handle (its termination record exists)
+  bool useGradients = false;  // "Use Gradient Information" (CMAES.cpp.base:82-87, :199, :226, :611-621)
 
   ~CmaesModule() override {
     if (h) kg_cmaes_destroy(h);
@@ -566,8 +567,13 @@ struct CmaesModule : SolverModule {
     if (mirrored && uint(sv, "Population Size", 0) % 2 == 1)  // CMAES.cpp.base:89-92
       fail("Mirrored Sampling can only be applied with an even Sample Population (is %zu)",
            (size_t)uint(sv, "Population Size", 0));
-    if (flag(sv, "Use Gradient Information", false))
-      fail("'Use Gradient Information' is not supported by the device path.");
+    useGradients = flag(sv, "Use Gradient Information", false);
+    const double gradientStep = num(sv, "Gradient Step Size", 0.01);
+    if (useGradients && gradientStep <= 0.)  // CMAES.cpp.base:86
+      fail("Gradient Step Size must be larger than 0.0 (is %f)", gradientStep);
+    if (useGradients && (pt != "optimization" || pb.contains("Objective Kernel")))
+      fail("'Use Gradient Information' needs an Optimization problem with an 'Objective Function' that sets "
+           "'Gradient'.");
     if (pb.contains("Constraints") && pb["Constraints"].size() > 0)
       fail("Constrained CMA-ES ('Constraints') is not supported by the device path.");
     Json &tc = sv["Termination Criteria"];
@@ -621,6 +627,8 @@ struct CmaesModule : SolverModule {
     c.is_sigma_bounded = flag(sv, "Is Sigma Bounded", false);
     c.diagonal_covariance = flag(sv, "Diagonal Covariance", false);
     c.mirrored_sampling = mirrored ? 1 : 0;
+    c.use_gradients = useGradients ? 1 : 0;
+    c.gradient_step_size = gradientStep;
     c.max_infeasible_resamplings = maxInfeasible;
     c.lower_bound = lb.data();
     c.upper_bound = ub.data();
@@ -667,13 +675,13 @@ struct CmaesModule : SolverModule {
       check(kg_cmaes_eval_builtin(h, objective));
     } else {
       // KORALI_START every sample, KORALI_WAITALL (CMAES.cpp.base:204-224)
-      std::vector<double> X(lam * N), F(lam);
+      std::vector<double> X(lam * N), F(lam), G(useGradients ? lam * N : 0);
       check(kg_cmaes_get_candidates(h, X.data(), N));
       Function *f = bayesian ? nullptr : &getFunction(fn);
       conduit->evaluateBatch(lam, [&](size_t i) {
         Sample s;
         s["Module"] = "Problem";
-        s["Operation"] = "Evaluate";
+        s["Operation"] = useGradients ? "Evaluate With Gradients" : "Evaluate";
         s["Sample Id"] = (unsigned long long)i;
         s["Current Generation"] = (unsigned long long)gen;
         std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
@@ -686,9 +694,23 @@ struct CmaesModule : SolverModule {
         (*f)(s);
         if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
         F[i] = s["F(x)"].getDouble();
+        if (useGradients) {  // Optimization::evaluateWithGradients (optimization.cpp.base:47-63)
+          const std::vector<double> g = KORALI_GET(std::vector<double>, s, "Gradient");
+          if (g.size() != N)
+            fail("Size of sample's gradient evaluations vector (%lu) is different from the number of problem "
+                 "variables defined (%lu).\n",
+                 (unsigned long)g.size(), (unsigned long)N);
+          if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
+          for (size_t d = 0; d < N; d++) {
+            if (!std::isfinite(g[d]))
+              fail("Non finite value of gradient evaluation detected for variable %lu: %f\n", (unsigned long)d, g[d]);
+            G[i * N + d] = g[d];
+          }
+        }
         if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
       });
       check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
+      if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
     }
     check(kg_cmaes_update(h, gen));
     updated = true;

@@ -35,6 +35,7 @@ class _CmaesCfg(C.Structure):
         ("min_std_update", C.POINTER(C.c_double)),
         ("normal_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("cov_mode", C.c_int), ("device", C.c_int),
         ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int), ("shard_rank", C.c_int), ("shard_count", C.c_int),
+        ("use_gradients", C.c_int), ("gradient_step_size", C.c_double),
     ]
 
 
@@ -57,7 +58,7 @@ EXPORTED = [
     "kg_last_error", "kg_abi_version", "kg_device_count",
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
     "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_set_log_posterior", "kg_cmaes_update", "kg_cmaes_generation",
-    "kg_cmaes_begin_sample", "kg_cmaes_wait_termination_fields", "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
+    "kg_cmaes_begin_sample", "kg_cmaes_wait_termination_fields", "kg_cmaes_set_gradients", "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
@@ -89,6 +90,7 @@ def lib():
         L.kg_cmaes_get_candidates.argtypes = [vp, dp, sz]
         L.kg_cmaes_set_fitness.argtypes = [vp, dp]
         L.kg_cmaes_set_log_posterior.argtypes = [vp, dp]
+        L.kg_cmaes_set_gradients.argtypes = [vp, dp]
         L.kg_cmaes_update.argtypes = [vp, sz]
         L.kg_cmaes_update_partial.argtypes = [vp, sz]
         L.kg_cmaes_update_finalize.argtypes = [vp, sz]
@@ -160,7 +162,7 @@ class CmaesDevice:
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
                  initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host", shard_rank=0,
-                 shard_count=1, mirrored=False):
+                 shard_count=1, mirrored=False, gradient_step_size=None):
         L = lib()
         self.N, self.lam = int(N), int(lam)
         self.mu = int(mu) if mu else self.lam // 2
@@ -177,6 +179,7 @@ class CmaesDevice:
         cfg.initial_cumulative_covariance = initial_cumulative_covariance
         cfg.is_sigma_bounded, cfg.diagonal_covariance = int(is_sigma_bounded), int(diagonal)
         cfg.mirrored_sampling = int(bool(mirrored))
+        cfg.use_gradients, cfg.gradient_step_size = int(gradient_step_size is not None), float(gradient_step_size or 0.0)
         cfg.max_infeasible_resamplings = float(max_infeasible_resamplings)
         (cfg.lower_bound, cfg.upper_bound, cfg.initial_value, cfg.initial_std,
          cfg.min_std_update) = [_dptr(a) for a in self._arrays]
@@ -244,6 +247,13 @@ class CmaesDevice:
     def set_fitness(self, F):
         F = self._fitness_arg(F)
         check(self._L.kg_cmaes_set_fitness(self.h, _dptr(F)))
+
+    def set_gradients(self, G):
+        """Use Gradient Information: every sample's gradient (lambda x N)."""
+        G = np.ascontiguousarray(G, dtype=np.float64)
+        if G.size != self.lam * self.N:
+            raise ValueError(f"set_gradients: expected {self.lam} x {self.N} gradients, got {G.shape}")
+        check(self._L.kg_cmaes_set_gradients(self.h, _dptr(G)))
 
     def set_log_posterior(self, F):
         """Bayesian problems: F(x) = logPosterior, -inf allowed."""

@@ -1134,6 +1134,11 @@ struct kr_cmaes
   double currentMinStd, currentMaxStd, maxDiagC, minDiagC, minEig, maxEig;
   double infeasibleSampleCount, bestValidSample, modelEvaluationCount, hsig, eigenFailures;
   kr_rng normal, uniform;
+  /* "Use Gradient Information" (CMAES.cpp.base:82-87, :611-621): the
+   * samples' "Gradient" (lambda x N) and the step size */
+  int useGradients;
+  double gradientStepSize;
+  double *gradients;
 };
 
 kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
@@ -1188,6 +1193,7 @@ kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
 void kr_cmaes_free(kr_cmaes *h)
 {
   if (!h) return;
+  free(h->gradients);
   free(h->lowerBound);
   free(h->upperBound);
   free(h->initialValue);
@@ -1240,6 +1246,7 @@ double *kr_cmaes_field(kr_cmaes *h, const char *name, size_t *len)
   VEC("Sample Population", h->X, h->lambda * N)
   VEC("BDZ Matrix", h->BDZ, h->lambda * N)
   VEC("Value Vector", h->F, h->lambda)
+  if (h->gradients) VEC("Gradients", h->gradients, h->lambda * h->N)
   VEC("Best Ever Variables", h->bestEverVariables, N)
   VEC("Current Best Variables", h->currentBestVariables, N)
   VEC("Mean Update", h->meanUpdate, N)
@@ -1285,6 +1292,12 @@ void kr_cmaes_set_option(kr_cmaes *h, const char *name, double v)
   else if (strcmp(name, "Is Sigma Bounded") == 0) h->isSigmaBounded = (int)v;
   else if (strcmp(name, "Diagonal Covariance") == 0) h->diagonal = (int)v;
   else if (strcmp(name, "Mirrored Sampling") == 0) h->mirrored = (int)v;
+  else if (strcmp(name, "Use Gradient Information") == 0)
+  {
+    h->useGradients = (int)v;
+    if (h->useGradients && !h->gradients) h->gradients = (double *)calloc(h->lambda * h->N, sizeof(double));
+  }
+  else if (strcmp(name, "Gradient Step Size") == 0) h->gradientStepSize = v;
   else if (strcmp(name, "Max Infeasible Resamplings") == 0) h->maxInfeasibleResamplings = v;
 }
 
@@ -1655,6 +1668,13 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
       h->currentMean[dd] = 0.;
       for (ii = 0; ii < mu; ++ii) h->currentMean[dd] += h->muWeights[ii] * h->X[h->sortingIndex[ii] * N + dd];
     }
+  }
+  if (h->useGradients)
+  {
+    /* :611-621 (its l2update is computed there but never used) */
+    for (d = 0; d < N; ++d)
+      for (i = 0; i < mu; ++i)
+        h->currentMean[d] += h->muWeights[i] * h->gradientStepSize / sqrt((double)N) * h->gradients[h->sortingIndex[i] * N + d];
   }
   for (d = 0; d < N; ++d) h->meanUpdate[d] = (h->currentMean[d] - h->previousMean[d]) / h->sigma;
   for (d = 0; d < N; ++d)

@@ -67,13 +67,21 @@ def base_cmaes():
 @pytest.mark.parametrize("key,value,msg", [
     ("Population Size", 1, "'Population Size' must be larger 1"),
     ("Mu Type", "Quadratic", "Invalid setting of Mu Type"),
-    ("Use Gradient Information", True, "Use Gradient Information"),
     ("Type", "Optimizer/DEA", "Unrecognized solver type"),
 ])
 def test_configuration_errors_before_device(key, value, msg):
     e = base_cmaes()
     e["Solver"][key] = value
     with pytest.raises(korali.KoraliError, match=msg):
+        korali.Engine().run(e)
+
+
+def test_gradient_step_size_checked_before_device():
+    """CMAES.cpp.base:86, with Use Gradient Information."""
+    e = base_cmaes()
+    e["Solver"]["Use Gradient Information"] = True
+    e["Solver"]["Gradient Step Size"] = 0.0
+    with pytest.raises(korali.KoraliError, match="Gradient Step Size must be larger than 0.0"):
         korali.Engine().run(e)
 
 

@@ -571,3 +571,51 @@ def test_cmaes_bayesian_custom_equals_optimization_objective():
     korali.Engine().run(eo)
     for k in ("Current Mean", "Covariance Matrix", "Sigma", "Best Ever Value", "Sample Population"):
         assert eb["Solver"][k] == eo["Solver"][k], k
+
+
+def test_cmaes_gradient_information_through_the_api():
+    """'Use Gradient Information' (CMAES.cpp.base:82-87, :199, :226,
+    :611-621; Optimization::evaluateWithGradients): the objective receives
+    Operation 'Evaluate With Gradients' and sets 'Gradient'; the run
+    optimises a 6-dim negative sphere; a wrong gradient size and a
+    non-positive step size fail with the reference's messages."""
+    import korali
+    ops = set()
+
+    def sphere(s):
+        ops.add(s["Operation"])
+        x = np.array(s["Parameters"])
+        s["F(x)"] = float(-0.5 * np.sum(x * x))
+        s["Gradient"] = list(-x)
+
+    def experiment(fn, step=0.1):
+        e = korali.Experiment()
+        e["Problem"]["Type"] = "Optimization"
+        e["Problem"]["Objective Function"] = fn
+        for i in range(6):
+            e["Variables"][i]["Name"] = f"x{i}"
+            e["Variables"][i]["Initial Value"] = 2.0
+            e["Variables"][i]["Initial Standard Deviation"] = 0.5
+        e["Solver"]["Type"] = "Optimizer/CMAES"
+        e["Solver"]["Population Size"] = 16
+        e["Solver"]["Use Gradient Information"] = True
+        e["Solver"]["Gradient Step Size"] = step
+        e["Solver"]["Termination Criteria"]["Max Generations"] = 60
+        e["File Output"]["Enabled"] = False
+        e["Console Output"]["Verbosity"] = "Silent"
+        e["Random Seed"] = 5
+        return e
+
+    e = experiment(sphere)
+    korali.Engine().run(e)
+    assert ops == {"Evaluate With Gradients"}
+    assert e["Results"]["Best Sample"]["F(x)"] > -1e-3
+
+    def short_gradient(s):
+        s["F(x)"] = 0.0
+        s["Gradient"] = [0.0]
+
+    with pytest.raises(Exception, match="Size of sample's gradient evaluations vector"):
+        korali.Engine().run(experiment(short_gradient))
+    with pytest.raises(Exception, match="Gradient Step Size must be larger than 0.0"):
+        korali.Engine().run(experiment(sphere, step=0.0))
