@@ -290,6 +290,72 @@ int kg_tmcmc_set_gradients(kg_tmcmc_t h, const double *grad, const double *fishe
 int kg_tmcmc_profile(kg_tmcmc_t h, int enable);
 int kg_tmcmc_profile_read(kg_tmcmc_t h, const char *stage, double *ms_total, size_t *count);
 
+/* ---------------------------------------------------------------- VRACER
+ * The VRACER agent with the continuous Normal
+ * policy, its critic/policy network and the CartPole environment of
+ * examples/learning/reinforcement/cartpole, all on the device:
+ *
+ *   kg_vracer_create              Agent::initialize + VRACER::initializeAgent
+ *                                 agent.cpp.base:9-154, VRACER.cpp.base:10-63,
+ *                                 continuous.cpp.base:9-93 (Normal transforms)
+ *   kg_vracer_run_policy          VRACER::runPolicy              VRACER.cpp.base:183-205
+ *   kg_vracer_environment_step    one action of every concurrent environment
+ *                                 (continuous.cpp.base:95-150) + Agent::processEpisode
+ *                                 of the episodes that ended (agent.cpp.base:376-572)
+ *   kg_vracer_train_policy        VRACER::trainPolicy x updates  VRACER.cpp.base:65-181
+ *                                 (generateMiniBatch :574-597, updateExperienceMetadata
+ *                                 :599-735, DeepSupervisor::runGeneration, fAdam)
+ *   kg_vracer_training_step       the body of Agent::trainingGeneration's loop
+ *                                 (agent.cpp.base:176-235): environment step, then
+ *                                 as many policy updates as Experiences Between
+ *                                 Policy Updates allows
+ *   kg_vracer_{get,set}_field / _scalar   replay memory, hyperparameters and agent
+ *                                 state (the reference's serialized agent fields)
+ * Float32 throughout, as the reference.  Hyperparameters are Korali's vector:
+ * per layer [W (out x in, row-major), b]. */
+typedef struct kg_vracer_s *kg_vracer_t;
+typedef struct {
+  size_t state_size, action_size;          /* Variables of Type State / Action */
+  size_t hidden_size, hidden_layers;       /* Linear + Elementwise/Tanh hidden layers */
+  size_t environments;                     /* Concurrent Environments */
+  size_t environment_count;                /* Problem / Environment Count */
+  size_t mini_batch_size;                  /* Mini Batch / Size */
+  size_t replay_maximum_size, replay_start_size;   /* Experience Replay sizes */
+  size_t max_episode_steps;                /* the environment's truncation length */
+  double experiences_between_policy_updates;
+  double discount_factor, learning_rate, importance_weight_truncation_level;
+  double off_policy_cutoff_scale, off_policy_target, off_policy_annealing_rate, off_policy_refer_beta;
+  int l2_regularization_enabled;
+  double l2_regularization_importance;
+  const double *initial_exploration_noise; /* action_size values */
+  uint64_t seed;                           /* action-noise / mini-batch stream key */
+  int device;
+} kg_vracer_config;
+
+int kg_vracer_create(const kg_vracer_config *cfg, kg_vracer_t *out);
+int kg_vracer_destroy(kg_vracer_t h);
+int kg_vracer_hyperparameter_count(kg_vracer_t h, size_t *n);
+int kg_vracer_field_size(kg_vracer_t h, const char *name, size_t *elem_bytes, size_t *count);
+int kg_vracer_get_field(kg_vracer_t h, const char *name, void *dst, size_t bytes);
+int kg_vracer_set_field(kg_vracer_t h, const char *name, const void *src, size_t bytes);
+int kg_vracer_get_scalar(kg_vracer_t h, const char *name, double *v);
+int kg_vracer_set_scalar(kg_vracer_t h, const char *name, double v);
+int kg_vracer_run_policy(kg_vracer_t h, const float *states, size_t n, float *out);
+/* Use the given standard normals (environments x action_size) for the next
+ * environment step's actions instead of the device stream (testing). */
+int kg_vracer_set_action_noise(kg_vracer_t h, const float *noise, size_t n);
+int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences);
+int kg_vracer_train_policy(kg_vracer_t h, size_t updates);
+int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *sorted_ids, size_t count);
+int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates);
+int kg_vracer_synchronize(kg_vracer_t h);
+int kg_vracer_stream(kg_vracer_t h, void **stream);
+/* Stage timers (HIP events on the handle's stream): "environment_step",
+ * "update", "gemm_rollout" (hidden-layer MFMA products of the rollout
+ * forward), "gemm_update".  profile_read returns and resets a stage's total. */
+int kg_vracer_profile(kg_vracer_t h, int enable);
+int kg_vracer_profile_read(kg_vracer_t h, const char *stage, double *ms_total, size_t *count);
+
 #ifdef __cplusplus
 }
 #endif

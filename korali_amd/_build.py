@@ -20,8 +20,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KORALI_AMD_ARCH", "gfx950")
 # -ffp-contract=off: no implicit FMA anywhere (bit-faithful replay of the
 # reference's x86-64 SSE2 double arithmetic); explicit fma() is kept.
+# -amdgpu-sdwa-peephole=false: no SDWA (sub-dword addressing) forms.  The
+# peephole emitted v_xor_b32_sdwa in exactly one kernel (the CartPole reset's
+# mt19937 tempering) and that kernel memory-faulted on MI355X with arguments
+# verified intact; with plain VOP2 forms it runs.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}",
-         "-Wno-unused-result"]
+         "-Wno-unused-result", "-mllvm", "-amdgpu-sdwa-peephole=false"]
 
 
 def sources():

@@ -1,0 +1,1229 @@
+// kg_vracer.hip — VRACER on MI355X.
+//
+// The agent's whole training loop runs on the device: E concurrent CartPole
+// environments step together (one thread per environment, the episode kept
+// in HBM until it ends), finished episodes are appended to a device-resident
+// replay memory (SoA ring in HBM, the reference's cBuffer view: logical 0 =
+// oldest), and every policy update — mini-batch draw + sort, the critic/policy
+// network forward on 2B rows (mini-batch states + their truncated states),
+// REF-ER metadata, retrace chains, the VRACER loss gradient, the backward pass
+// and fAdam — is a short chain of kernels with no host round trip.  Dense
+// layers run on the FP32 matrix cores (v_mfma_f32_16x16x4_f32: exact f32
+// products, f32 accumulation) from LDS-staged 64x64 tiles; the layers whose
+// other dimension is the state / action size run on the VALU.
+//
+// Reference (paths relative to the korali root):
+//   Agent::trainingGeneration / processEpisode / generateMiniBatch /
+//   updateExperienceMetadata        solver/agent/agent.cpp.base:162-735
+//   VRACER::trainPolicy / calculatePolicyGradients / runPolicy
+//                                   solver/agent/continuous/VRACER/VRACER.cpp.base:65-205
+//   Continuous (Normal policy)      solver/agent/continuous/continuous.cpp.base:34-61,
+//                                   :137-150, :278-440, :697-732
+//   DeepSupervisor::runGeneration   solver/learner/deepSupervisor/deepSupervisor.cpp.base:97-161
+//   Linear / Output layers          neuralNetwork/layer/{linear,output}/*.cpp.base
+//   fAdam::processResult            solver/learner/deepSupervisor/optimizers/fAdam.cpp:64-91
+//   CartPole environment            examples/learning/reinforcement/cartpole/_model
+// The CPU restatement is oracle/vracer_ref.py (test infrastructure only).
+#include "kg_common.hpp"
+#include "../../include/korali_amd.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace kg {
+namespace vr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MAXA = 4;  // action dimensions supported by the device kernels
+constexpr int MAXO = 1 + 2 * MAXA;
+constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
+enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
+enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u };
+
+// Device-resident agent scalars (float where the reference keeps float).
+struct State {
+  float lr, beta, cutoff, off_ratio, eta, b1p, b2p, pad0;
+  long long off_count, update_count;
+  unsigned long long total;       // experiences ever appended (ring position)
+  unsigned long long size;        // replay memory size
+  unsigned long long episode;     // _currentEpisode
+  unsigned long long sample_id;   // _currentSampleID (next environment launch)
+  unsigned long long mb_counter;  // philox counter of the mini-batch uniforms
+  unsigned long long env_step;    // philox counter of the action noise
+  unsigned long long step_new, step_base, step_episodes, step_episode_base, step_sample_base;
+  unsigned long long experience_count;
+  unsigned errors, pad1;
+  double step_reward_sum;         // cumulative rewards of the episodes finished by the last step
+};
+
+struct Params {  // launch-constant configuration
+  int S, A, H, L, O, E, B, T;     // T = max episode steps
+  long long R;                    // replay memory capacity
+  int env_count, l2;
+  float gamma, lr0, iw_trunc, cutoff_scale, off_target, anneal, l2imp;
+  float scale[MAXO], shift[MAXO];
+  int soft[MAXO];
+  unsigned long long seed;
+};
+
+// ---------------------------------------------------------------- philox
+struct u4 {
+  unsigned x, y, z, w;
+};
+__host__ __device__ inline u4 philox4x32(u4 c, unsigned k0, unsigned k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x, p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    c = u4{(unsigned)(p1 >> 32) ^ c.y ^ k0, (unsigned)p1, (unsigned)(p0 >> 32) ^ c.w ^ k1, (unsigned)p0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+// Two standard normals (Box-Muller in double) from one philox block; the
+// stream is keyed by (seed, purpose) and counted by (a, b).
+__device__ inline void philox_normals(unsigned long long seed, unsigned purpose, unsigned long long a, unsigned b,
+                                      float &n0, float &n1) {
+  const u4 r = philox4x32(u4{(unsigned)a, (unsigned)(a >> 32), b, purpose}, (unsigned)seed, (unsigned)(seed >> 32));
+  const double u1 = ((double)r.x + 1.0) * 2.3283064365386963e-10;  // (0, 1]
+  const double u2 = (double)r.y * 2.3283064365386963e-10;          // [0, 1)
+  const double rad = sqrt(-2.0 * log(u1));
+  n0 = (float)(rad * cos(6.283185307179586 * u2));
+  n1 = (float)(rad * sin(6.283185307179586 * u2));
+}
+__device__ inline float philox_uniform24(unsigned long long seed, unsigned long long ctr) {
+  const u4 r = philox4x32(u4{(unsigned)ctr, (unsigned)(ctr >> 32), 0u, 0x4D42u}, (unsigned)seed, (unsigned)(seed >> 32));
+  return (float)(r.x >> 8) * 5.9604644775390625e-08f;  // [0, 1)
+}
+
+// ------------------------------------------------------- Normal policy math
+// auxiliar/math.hpp:269-274 with T = float: 2*M_PI and KORALI_EPSILON
+// promote the expressions to double; norm and d are stored as float.
+__device__ inline float normal_logp(float x, float mean, float sigma) {
+  const float norm = (float)(-0.5 * log(2.0 * M_PI * (double)sigma * (double)sigma));
+  const float d = (float)((double)(x - mean) / ((double)sigma + 0.00000000001));
+  return (float)((double)norm - 0.5 * (double)d * (double)d);
+}
+
+// ------------------------------------------------------------ layer kernels
+// Input layer (K = state size): H = tanh(X W1^T + b1), one thread per output.
+__global__ void k_vr_fwd_in(int M, int S, int H, const float *__restrict__ X, const float *__restrict__ W,
+                            const float *__restrict__ b, float *__restrict__ Y) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)M * H) return;
+  const int m = (int)(t / H), o = (int)(t % H);
+  float acc = 0.f;
+  for (int i = 0; i < S; i++) acc += W[o * S + i] * X[(long long)m * S + i];
+  Y[t] = tanhf(acc + b[o]);
+}
+
+// Output layer (N = 1 + 2A): Linear + Output-layer transformation
+// (output.cpp.base:140-160: Softplus 0.5 (x + sqrt(1 + x^2)) in double, then
+// Scale and Shift in float).
+__global__ void k_vr_fwd_out(int M, int H, int O, const float *__restrict__ Hs, const float *__restrict__ W,
+                             const float *__restrict__ b, float *__restrict__ out, Params P) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)M * O) return;
+  const int m = (int)(t / O), o = (int)(t % O);
+  const float4 *h4 = reinterpret_cast<const float4 *>(Hs + (long long)m * H);
+  const float4 *w4 = reinterpret_cast<const float4 *>(W + (long long)o * H);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int i = 0; i < H / 4; i++) {
+    const float4 h = h4[i], w = w4[i];
+    a0 += w.x * h.x, a1 += w.y * h.y, a2 += w.z * h.z, a3 += w.w * h.w;
+  }
+  float x = ((a0 + a1) + (a2 + a3)) + b[o];
+  if (P.soft[o]) x = (float)(0.5 * ((double)x + sqrt(1.0 + (double)x * (double)x)));
+  out[t] = x * P.scale[o] + P.shift[o];
+}
+
+// C[m][n] = sum_k A(m,k) B(n,k) on v_mfma_f32_16x16x4_f32, 64x64 tile per
+// 256-thread workgroup (each wave a 32x32 quarter as 2x2 16x16 accumulators),
+// A and B staged 32 k-columns at a time through LDS with any element strides
+// (so the same kernel serves X W^T, W^T-side and batch-reduction products).
+// Epilogues: bias + tanh (forward), times (1 - T^2) (tanh backward), plain.
+enum : int { EP_STORE = 0, EP_BIAS_TANH = 1, EP_DTANH = 2 };
+template <int EP>
+__global__ __launch_bounds__(256) void k_vr_gemm(int M, int N, int K, const float *__restrict__ A, long long sam,
+                                                 long long sak, const float *__restrict__ B, long long sbn,
+                                                 long long sbk, float *__restrict__ C, long long ldc,
+                                                 const float *__restrict__ bias, const float *__restrict__ T,
+                                                 long long ldt) {
+  __shared__ float As[32][68];
+  __shared__ float Bs[32][68];
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 1, wc = wave & 1, li = lane & 15,
+            lk = lane >> 4;
+  f32x4 acc00 = {0.f, 0.f, 0.f, 0.f}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+  for (int k0 = 0; k0 < K; k0 += 32) {
+#pragma unroll
+    for (int e0 = 0; e0 < 2048; e0 += 256) {
+      const int e = e0 + t;
+      int mm, kk;
+      if (sak == 1) kk = e & 31, mm = e >> 5;
+      else mm = e & 63, kk = e >> 6;
+      const int gm = m0 + mm, gk = k0 + kk;
+      As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.f;
+      int nn, kb;
+      if (sbk == 1) kb = e & 31, nn = e >> 5;
+      else nn = e & 63, kb = e >> 6;
+      const int gn = n0 + nn, gkb = k0 + kb;
+      Bs[kb][nn] = (gn < N && gkb < K) ? B[gn * sbn + gkb * sbk] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 4) {
+      const float a0 = As[kk + lk][wr * 32 + li], a1 = As[kk + lk][wr * 32 + 16 + li];
+      const float b0 = Bs[kk + lk][wc * 32 + li], b1 = Bs[kk + lk][wc * 32 + 16 + li];
+      acc00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc11, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C/D layout of the f32 16x16x4 form: col = lane & 15, row = 4 (lane >> 4) + reg
+  const f32x4 *accs[4] = {&acc00, &acc01, &acc10, &acc11};
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int col = n0 + wc * 32 + (q & 1) * 16 + li;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = m0 + wr * 32 + (q >> 1) * 16 + lk * 4 + r;
+      if (row >= M || col >= N) continue;
+      float v = (*accs[q])[r];
+      if (EP == EP_BIAS_TANH) v = tanhf(v + bias[col]);
+      if (EP == EP_DTANH) {
+        const float y = T[row * ldt + col];
+        v = v * (1.0f - y * y);
+      }
+      C[row * ldc + col] = v;
+    }
+  }
+}
+
+// Output-layer backward (output.cpp.base:170-210) and the last Linear's data
+// gradient: dZ = transformed G; dH[b][i] = (sum_o dZ[b][o] W[o][i]) (1 - h^2).
+__global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, const float *__restrict__ out,
+                             const float *__restrict__ W, const float *__restrict__ Hs, float *__restrict__ dZ,
+                             float *__restrict__ dH, Params P) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)Bn * H) return;
+  const int b = (int)(t / H), i = (int)(t % H);
+  float dz[MAXO];
+  float acc = 0.f;
+  for (int o = 0; o < O; o++) {
+    float x = out[b * O + o], g = G[b * O + o];
+    x = x - P.shift[o];
+    x = x / P.scale[o];
+    g = g * P.scale[o];
+    if (P.soft[o]) {
+      const float nnx = x - 0.25f / x;
+      g = (float)((double)g * 0.5 * (1.0 + (double)nnx / sqrt((double)nnx * (double)nnx + 1.0)));
+    }
+    dz[o] = g;
+    acc += dz[o] * W[o * H + i];
+  }
+  if (i == 0)
+    for (int o = 0; o < O; o++) dZ[b * O + o] = dz[o];
+  const float y = Hs[(long long)b * H + i];
+  dH[t] = acc * (1.0f - y * y);
+}
+
+// Weight gradients of a layer with a small dimension, and bias gradients:
+// dW[o][i] = sum_b G[b][o] Act[b][i] for i < Ni, db[o] = sum_b G[b][o]
+// (linear.cpp.base:337-350: summed over the batch, in batch order).
+__global__ void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
+                                 const float *__restrict__ Act, int lda, float *__restrict__ dW,
+                                 float *__restrict__ db) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= No * (Ni + 1)) return;
+  const int o = t / (Ni + 1), i = t % (Ni + 1);
+  float acc = 0.f;
+  if (i < Ni) {
+    for (int b = 0; b < Bn; b++) acc += G[b * ldg + o] * Act[(long long)b * lda + i];
+    dW[o * Ni + i] = acc;
+  } else {
+    acc = G[o];
+    for (int b = 1; b < Bn; b++) acc += G[b * ldg + o];
+    db[o] = acc;
+  }
+}
+
+// fAdam::processResult (fAdam.cpp:64-91), optional L2 term
+// (deepSupervisor.cpp.base:147-153); eta and the beta powers were advanced
+// by the metadata kernel of the same update.
+__global__ void k_vr_adam(long long n, float *__restrict__ theta, const float *__restrict__ grad,
+                          float *__restrict__ m1, float *__restrict__ m2, const State *__restrict__ st, int l2,
+                          float l2imp) {
+  const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-08f;
+  const float f1 = 1.0f / (1.0f - st->b1p), f2 = 1.0f / (1.0f - st->b2p);
+  float g = grad[j];
+  if (l2) g -= l2imp * theta[j];
+  const float m = b1 * m1[j] - (1.0f - b1) * g;
+  const float v = b2 * m2[j] + (1.0f - b2) * g * g;
+  m1[j] = m;
+  m2[j] = v;
+  theta[j] -= st->eta / (sqrtf(v * f2) + eps) * m * f1;
+}
+
+// ------------------------------------------------------------ replay memory
+struct Replay {
+  float *st, *act, *rew, *tst, *exp_pol, *cur_pol, *exp_v, *v, *ret, *iw, *tiw, *tv;
+  int *env, *term, *onp, *ep_pos;
+  long long *ep_id;
+};
+__device__ inline long long phys(const State *s, long long R, long long i) {
+  return (long long)((s->total - s->size + (unsigned long long)i) % (unsigned long long)R);
+}
+
+// generateMiniBatch (agent.cpp.base:574-597): B uniforms -> floor(x (size-1)),
+// sorted (bitonic in LDS); gathers the mini-batch states into rows [0, B) and
+// their truncated states into rows [B, 2B) of X.
+__global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Replay er, unsigned *mb,
+                                                       const unsigned *forced, float *X) {
+  __shared__ unsigned key[MAXB];
+  const int t = threadIdx.x, nt = blockDim.x, B = P.B;
+  int n2 = 1;
+  while (n2 < B) n2 <<= 1;
+  const unsigned long long ctr = st->mb_counter;
+  const float sz1 = (float)(st->size - 1);
+  for (int i = t; i < n2; i += nt) {
+    unsigned id = 0xffffffffu;
+    if (i < B) {
+      id = forced ? forced[i] : (unsigned)floorf(philox_uniform24(P.seed, ctr + i) * sz1);
+      if (id >= st->size) id = (unsigned)(st->size - 1);  // never reached for ids the host checked
+    }
+    key[i] = id;
+  }
+  __syncthreads();
+  for (int k = 2; k <= n2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < n2; i += nt) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned a = key[i], c = key[l];
+          if ((a > c) == ((i & k) == 0)) key[i] = c, key[l] = a;
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = t; i < B * P.S; i += nt) {
+    const int b = i / P.S, k = i % P.S;
+    const long long p = phys(st, P.R, key[b]);
+    X[(long long)b * P.S + k] = er.st[p * P.S + k];
+    X[(long long)(B + b) * P.S + k] = er.tst[p * P.S + k];
+  }
+  for (int i = t; i < B; i += nt) mb[i] = key[i];
+  __syncthreads();
+  if (t == 0) st->mb_counter = ctr + (forced ? 0 : (unsigned long long)B);
+}
+
+// updateExperienceMetadata (agent.cpp.base:599-735) + the VRACER loss
+// gradient (VRACER.cpp.base:89-181) + the REF-ER schedule (agent.cpp.base:
+// 221-231), one workgroup: phases separated by workgroup barriers.
+__global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
+                                                  const float *__restrict__ out, float *__restrict__ G) {
+  __shared__ int s_delta;
+  const int t = threadIdx.x, nt = blockDim.x, B = P.B, A = P.A, O = P.O;
+  const float cutoff = st->cutoff, beta = st->beta;
+  if (t == 0) s_delta = 0;
+  __syncthreads();
+  int delta = 0;
+  for (int b = t; b < B; b += nt) {
+    if (b > 0 && mb[b] == mb[b - 1]) continue;
+    const long long p = phys(st, P.R, mb[b]);
+    const float *cur = out + (long long)b * O + 1;
+    float lc = 0.f, lo = 0.f;
+    for (int i = 0; i < A; i++) {
+      const float a = er.act[p * A + i];
+      lc += normal_logp(a, cur[i], cur[A + i]);
+      lo += normal_logp(a, er.exp_pol[p * 2 * A + i], er.exp_pol[p * 2 * A + A + i]);
+    }
+    float liw = lc - lo;
+    if (liw > 7.f) liw = 7.f;
+    if (liw < -7.f) liw = -7.f;
+    if (!isfinite(liw)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_IW);
+    const float iw = expf(liw);
+    const float tiw = iw < P.iw_trunc ? iw : P.iw_trunc;  // std::min(level, iw)
+    const int onp = (iw > 1.0f / cutoff) && (iw < cutoff);
+    const int was = er.onp[p];
+    if (was && !onp) delta++;
+    if (!was && onp) delta--;
+    const float V = out[(long long)b * O];
+    if (!isfinite(V)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_VALUE);
+    for (int i = 0; i < 2 * A; i++) er.cur_pol[p * 2 * A + i] = cur[i];
+    er.v[p] = V;
+    er.tv[p] = er.term[p] == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
+    er.iw[p] = iw;
+    er.onp[p] = onp;
+    er.tiw[p] = tiw;
+  }
+  if (delta) atomicAdd(&s_delta, delta);
+  __threadfence_block();
+  __syncthreads();
+  if (t == 0) {
+    st->off_count += s_delta;
+    st->off_ratio = (float)st->off_count / (float)st->size;
+    st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)st->update_count);
+  }
+  // retrace chains of the oldest mini-batch entries of each episode
+  for (int b = t; b < B; b += nt) {
+    const long long pe = phys(st, P.R, mb[b]);
+    if (b < B - 1 && er.ep_id[pe] == er.ep_id[phys(st, P.R, mb[b + 1])]) continue;
+    const long long end = mb[b];
+    long long start = end - er.ep_pos[pe];
+    if (start < 0) start = 0;
+    float retV = 0.0f;
+    if (er.term[pe] == TRUNCATED) retV = er.tv[pe];
+    if (er.term[pe] == NON_TERMINAL) retV = er.ret[phys(st, P.R, end + 1)];
+    for (long long c = end; c >= start; c--) {
+      const long long pc = phys(st, P.R, c);
+      const float curV = er.v[pc];
+      retV = curV + er.tiw[pc] * (er.rew[pc] + P.gamma * retV - curV);
+      er.ret[pc] = retV;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (int b = t; b < B; b += nt) {
+    const long long p = phys(st, P.R, mb[b]);
+    const float V = er.v[p];
+    const float *cur = er.cur_pol + p * 2 * A, *old = er.exp_pol + p * 2 * A;
+    float g[MAXO];
+    g[0] = er.ret[p] - V;
+    for (int i = 1; i < O; i++) g[i] = 0.f;
+    if (er.onp[p]) {
+      float q = er.rew[p];
+      if (er.term[p] == NON_TERMINAL) q += P.gamma * er.ret[phys(st, P.R, (long long)mb[b] + 1)];
+      if (er.term[p] == TRUNCATED) q += P.gamma * er.tv[p];
+      const float loss = q - V;
+      float pg[2 * MAXA];
+      float lc = 0.f, lo = 0.f;
+      for (int i = 0; i < A; i++) {
+        const float a = er.act[p * A + i], cm = cur[i], cs = cur[A + i];
+        const float dif = a - cm;
+        const float inv_var = 1.f / (cs * cs);
+        pg[i] = dif * inv_var;
+        pg[A + i] = (dif * dif) * (inv_var / cs) - 1.f / cs;
+        lc += normal_logp(a, cm, cs);
+        lo += normal_logp(a, old[i], old[A + i]);
+      }
+      const float iwg = expf(lc - lo);
+      for (int i = 0; i < 2 * A; i++) g[1 + i] = beta * loss * (pg[i] * iwg);
+    }
+    const float klm = -(1.0f - beta);
+    for (int i = 0; i < A; i++) {
+      const float om = old[i], osd = old[A + i], cm = cur[i], cs = cur[A + i];
+      const float inv_sig = (float)(1. / (double)cs);
+      const float inv_var = (float)(1. / (double)(cs * cs));
+      const float inv_sig3 = (float)(1. / (double)(cs * cs * cs));
+      const float d = cm - om;
+      const float kl_mean = d * inv_var;
+      const float kl_sig = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
+      g[1 + i] += klm * kl_mean;
+      g[1 + A + i] += klm * kl_sig;
+    }
+    for (int i = 0; i < O; i++) {
+      if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
+      G[(long long)b * O + i] = g[i];
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    // the learner's eta for this update, then agent.cpp.base:221-231
+    st->eta = st->lr;
+    st->b1p = st->b1p * 0.9f;
+    st->b2p = st->b2p * 0.999f;
+    st->update_count += 1;
+    st->lr = P.lr0 / (1.0f + P.anneal * (float)st->update_count);
+    if (st->off_ratio > P.off_target) st->beta = (1.0f - st->lr) * st->beta;
+    else st->beta = (1.0f - st->lr) * st->beta + st->lr;
+  }
+}
+
+// ---------------------------------------------------------------- CartPole
+// examples/learning/reinforcement/cartpole/_model/cartpole.py (RK4 step of
+// dt = 0.02 in place of scipy's adaptive dopri5) and env.py (3 reward
+// variants, reset seeded with numpy's legacy mt19937 by sampleId*1024 + launchId).
+__device__ inline void cp_system(const double *y, double act, double *d) {
+  const double mp = 0.1, mc = 1.0, l = 0.5, g = 9.81;
+  const double th = y[2], w = y[3];
+  const double c = cos(th), s = sin(th);
+  const double tot = mp + mc;
+  const double tmp = (act + l * w * w * s) / tot;
+  const double wdot = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * c * c / tot));
+  const double vdot = tmp - l * wdot * c / tot;
+  d[0] = y[1], d[1] = vdot, d[2] = w, d[3] = wdot;
+}
+__device__ inline bool cp_failed(const double *u) {
+  return fabs(u[0]) > 2.4 || fabs(u[2]) > M_PI / 15;
+}
+// numpy RandomState(seed).uniform(-0.05, 0.05, 4): init_genrand, one twist of
+// the first 8 words, tempering, random_double = (a>>5, b>>6) / 2^53.
+__device__ inline void cp_reset(unsigned seed, double *u) {
+  unsigned lo[9], hi[8];
+  unsigned x = seed;
+  for (int i = 0; i <= 404; i++) {
+    if (i > 0) x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+    if (i <= 8) lo[i] = x;
+    if (i >= 397) hi[i - 397] = x;
+  }
+  unsigned out[8];
+  for (int i = 0; i < 8; i++) {
+    const unsigned y = (lo[i] & 0x80000000u) | (lo[i + 1] & 0x7fffffffu);
+    unsigned z = hi[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    z ^= z >> 11;
+    z ^= (z << 7) & 0x9d2c5680u;
+    z ^= (z << 15) & 0xefc60000u;
+    z ^= z >> 18;
+    out[i] = z;
+  }
+  const double low = -0.05, range = 0.05 - -0.05;
+  for (int k = 0; k < 4; k++) {
+    const double d = ((double)(out[2 * k] >> 5) * 67108864.0 + (double)(out[2 * k + 1] >> 6)) / 9007199254740992.0;
+    u[k] = low + range * d;
+  }
+}
+
+struct Envs {
+  double *u;          // E x 4 CartPole state
+  int *t, *env_id;    // steps taken in the episode, environment id
+  unsigned long long *sample;
+  float *cum;         // cumulative training reward of the running episode
+  int *fin, *len;     // finished flag (termination) and episode length after the step
+  long long *off;     // exclusive prefix of finished lengths
+  int *rank;          // rank of the finished episode in environment order
+  int *fin_env;       // environment of the finished episode of each rank
+  float *eb_st, *eb_act, *eb_pol, *eb_v, *eb_rew;  // E x T episode buffers
+  float *rewards;     // cumulative rewards of the episodes finished by the last step (by rank)
+};
+
+__global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long sample0, const int *only_fin) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E) return;
+  const unsigned long long sid = sample0 + e;
+  double u[4];
+  cp_reset((unsigned)(sid * 1024ull + sid), u);
+  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = u[k], X[e * 4 + k] = (float)u[k];
+  ev.t[e] = 0;
+  ev.sample[e] = sid;
+  ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
+  ev.cum[e] = 0.f;
+  (void)only_fin;
+}
+
+// One action of every environment (continuous.cpp.base:95-150 Normal policy:
+// action = mean + sigma N(0,1)); the experience is kept in the episode buffer.
+__global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restrict__ out, float *X,
+                             const float *__restrict__ forced_noise) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E) return;
+  const int A = P.A, S = P.S, O = P.O;
+  const int t = ev.t[e];
+  const long long slot = (long long)e * P.T + t;
+  const float V = out[(long long)e * O];
+  float act[MAXA];
+  for (int i = 0; i < A; i += 2) {
+    float n0, n1;
+    if (forced_noise) {
+      n0 = forced_noise[e * A + i];
+      n1 = i + 1 < A ? forced_noise[e * A + i + 1] : 0.f;
+    } else {
+      philox_normals(P.seed, 0x4E4Fu, st->env_step, (unsigned)(e * MAXA + i), n0, n1);
+    }
+    act[i] = out[(long long)e * O + 1 + i] + out[(long long)e * O + 1 + A + i] * n0;
+    if (i + 1 < A) act[i + 1] = out[(long long)e * O + 2 + i] + out[(long long)e * O + 2 + A + i] * n1;
+  }
+  for (int k = 0; k < S; k++) ev.eb_st[slot * S + k] = X[(long long)e * S + k];
+  for (int i = 0; i < A; i++) ev.eb_act[slot * A + i] = act[i];
+  for (int i = 0; i < 2 * A; i++) ev.eb_pol[slot * 2 * A + i] = out[(long long)e * O + 1 + i];
+  ev.eb_v[slot] = V;
+  // CartPole::advance: F clipped to [-10, 10], one RK4 step
+  double F = (double)act[0];
+  if (F > 10.0) F = 10.0;
+  else if (F < -10.0) F = -10.0;
+  double y[4], k1[4], k2[4], k3[4], k4[4], tmp[4];
+  for (int k = 0; k < 4; k++) y[k] = ev.u[e * 4 + k];
+  const double h = 0.02;
+  cp_system(y, F, k1);
+  for (int k = 0; k < 4; k++) tmp[k] = y[k] + 0.5 * h * k1[k];
+  cp_system(tmp, F, k2);
+  for (int k = 0; k < 4; k++) tmp[k] = y[k] + 0.5 * h * k2[k];
+  cp_system(tmp, F, k3);
+  for (int k = 0; k < 4; k++) tmp[k] = y[k] + h * k3[k];
+  cp_system(tmp, F, k4);
+  for (int k = 0; k < 4; k++) y[k] = y[k] + (h / 6.0) * (((k1[k] + 2.0 * k2[k]) + 2.0 * k3[k]) + k4[k]);
+  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = y[k], X[e * 4 + k] = (float)y[k];
+  const bool failed = cp_failed(y);
+  const double r = 1.0 - 1.0 * (failed ? 1.0 : 0.0);
+  const int vid = ev.env_id[e] % 3;
+  const float rew = (float)(vid == 0 ? r : vid == 1 ? r - 1.0 : r * 0.1);
+  ev.eb_rew[slot] = rew;
+  ev.cum[e] += rew;
+  const int steps = t + 1;
+  ev.t[e] = steps;
+  ev.len[e] = steps;
+  ev.fin[e] = failed ? TERMINAL : (steps >= P.T ? TRUNCATED : NON_TERMINAL);
+}
+
+// Finished episodes in environment order (the order attendAgent visits them):
+// exclusive prefix of their lengths, ranks, and the scalar bookkeeping.
+__global__ __launch_bounds__(1024) void k_vr_scan(Params P, State *st, Envs ev) {
+  __shared__ long long s_len[1024];
+  __shared__ int s_cnt[1024];
+  const int t = threadIdx.x, nt = blockDim.x, E = P.E;
+  const int per = (E + nt - 1) / nt, e0 = t * per, e1 = min(E, e0 + per);
+  long long L = 0;
+  int c = 0;
+  for (int e = e0; e < e1; e++)
+    if (ev.fin[e]) L += ev.len[e], c++;
+  s_len[t] = L, s_cnt[t] = c;
+  __syncthreads();
+  for (int d = 1; d < nt; d <<= 1) {  // inclusive Hillis-Steele scan
+    long long lv = t >= d ? s_len[t - d] : 0;
+    int cv = t >= d ? s_cnt[t - d] : 0;
+    __syncthreads();
+    s_len[t] += lv, s_cnt[t] += cv;
+    __syncthreads();
+  }
+  L = s_len[t] - L, c = s_cnt[t] - c;
+  for (int e = e0; e < e1; e++) {
+    ev.off[e] = L;
+    ev.rank[e] = c;
+    if (ev.fin[e]) ev.fin_env[c] = e, L += ev.len[e], c++;
+  }
+  if (t == nt - 1) {
+    const unsigned long long add = (unsigned long long)s_len[nt - 1], neps = (unsigned long long)s_cnt[nt - 1];
+    st->step_base = st->total;
+    st->step_new = add;
+    st->step_episodes = neps;
+    st->step_episode_base = st->episode;
+    st->step_sample_base = st->sample_id;
+    st->total += add;
+    st->size = st->size + add < (unsigned long long)P.R ? st->size + add : (unsigned long long)P.R;
+    st->episode += neps;
+    st->sample_id += neps;
+    st->experience_count += add;
+    st->env_step += 1;
+    st->step_reward_sum = 0.0;
+  }
+}
+
+// processEpisode (agent.cpp.base:376-572) for every finished episode at once:
+// one workgroup per environment copies its episode into the replay memory,
+// counts evicted off-policy entries, sets the initial retrace values (the
+// reference's last-two-entries window, see oracle/vracer_ref.py) and resets
+// the environment for its next launch.
+__global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay er, Envs ev,
+                                                   const float *__restrict__ outF, float *X) {
+  const int e = blockIdx.x;
+  const int term = ev.fin[e];
+  if (!term) return;
+  const int t = threadIdx.x, nt = blockDim.x, S = P.S, A = P.A;
+  const int len = ev.len[e], rank = ev.rank[e];
+  const long long off = ev.off[e];
+  const unsigned long long base = st->step_base, nnew = st->step_new;
+  const long long R = P.R;
+  for (int k = t; k < len; k += nt) {
+    const long long j = off + k;
+    if ((long long)nnew - j > R) continue;  // overwritten within this batch
+    const long long abs_i = (long long)base + j, p = abs_i % R;
+    const long long prev = abs_i - R;  // absolute index of the evicted occupant
+    if (prev >= 0 && prev < (long long)base && er.onp[p] == 0)
+      atomicAdd((unsigned long long *)&st->off_count, (unsigned long long)(-1ll));
+    const long long slot = (long long)e * P.T + k;
+    const int tk = k == len - 1 ? term : NON_TERMINAL;
+    for (int q = 0; q < S; q++) {
+      er.st[p * S + q] = ev.eb_st[slot * S + q];
+      er.tst[p * S + q] = tk == TRUNCATED ? X[(long long)e * S + q] : 0.f;
+    }
+    for (int i = 0; i < A; i++) er.act[p * A + i] = ev.eb_act[slot * A + i];
+    for (int i = 0; i < 2 * A; i++) er.exp_pol[p * 2 * A + i] = er.cur_pol[p * 2 * A + i] = ev.eb_pol[slot * 2 * A + i];
+    er.rew[p] = ev.eb_rew[slot];
+    er.env[p] = ev.env_id[e];
+    er.term[p] = tk;
+    er.exp_v[p] = er.v[p] = ev.eb_v[slot];
+    er.ret[p] = 0.f;
+    er.iw[p] = 1.f;
+    er.tiw[p] = 1.f;
+    er.tv[p] = 0.f;
+    er.onp[p] = 1;
+    er.ep_id[p] = (long long)(st->step_episode_base + rank);
+    er.ep_pos[p] = k;
+  }
+  __syncthreads();
+  if (t == 0) {
+    // initial retrace values (agent.cpp.base:520-555)
+    float retV = 0.0f;
+    if (term == TRUNCATED) retV += P.gamma * outF[(long long)e * P.O];
+    const long long endj = off + len - 1;
+    // the next finished episode (rank + 1) rewrites our last entry when it has one experience
+    bool own_end = true;
+    if ((unsigned long long)(rank + 1) < st->step_episodes && ev.len[ev.fin_env[rank + 1]] == 1) own_end = false;
+    retV = P.gamma * retV + ev.eb_rew[(long long)e * P.T + len - 1];
+    if (own_end) er.ret[((long long)base + endj) % R] = retV;
+    const long long prevj = endj - 1;
+    if ((long long)base + prevj >= 0) {
+      float r;
+      if (len >= 2) r = ev.eb_rew[(long long)e * P.T + len - 2];
+      else if (rank > 0) {
+        const int pe = ev.fin_env[rank - 1];
+        r = ev.eb_rew[(long long)pe * P.T + ev.len[pe] - 1];
+      } else r = er.rew[((long long)base + prevj) % R];
+      retV = P.gamma * retV + r;
+      er.ret[((long long)base + prevj) % R] = retV;
+    }
+    ev.rewards[rank] = ev.cum[e];
+    atomicAdd(&st->step_reward_sum, (double)ev.cum[e]);
+    // reset for the next launch (env.py: cart.reset(sampleId * 1024 + launchId))
+    const unsigned long long sid = st->step_sample_base + (unsigned long long)rank + (unsigned long long)P.E;
+    double u[4];
+    cp_reset((unsigned)(sid * 1024ull + sid), u);
+    for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = (float)u[q];
+    ev.t[e] = 0;
+    ev.sample[e] = sid;
+    ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
+    ev.cum[e] = 0.f;
+  }
+}
+
+__global__ void k_vr_init_state(State *st, float lr, float beta, float cutoff) {
+  if (threadIdx.x || blockIdx.x) return;
+  State s = {};
+  s.lr = lr, s.beta = beta, s.cutoff = cutoff, s.eta = lr, s.b1p = 1.0f, s.b2p = 1.0f;
+  *st = s;
+}
+
+}  // namespace vr
+}  // namespace kg
+
+// ======================================================================= host
+using namespace kg::vr;
+
+struct kg_vracer_s {
+  Params P;
+  int device;
+  hipStream_t stream;
+  size_t nparam;
+  std::vector<size_t> offW, offb;  // per layer
+  float *theta, *grad, *m1, *m2;
+  float *X;          // E x S current environment states
+  float *Xmb;        // 2B x S mini-batch (+ truncated) states
+  float *Xs;         // rowsMax x S run_policy staging
+  float *acts;       // L x rowsMax x H activations
+  float *out, *outF; // rowsMax x O
+  float *G, *dZ, *dHa, *dHb;
+  unsigned *mb, *forced_mb;
+  float *forced_noise;
+  int use_forced_noise;
+  State *st, *st_host;
+  Replay er;
+  Envs ev;
+  size_t rowsMax;
+  // stage timers (kg_vracer_profile): HIP events on the handle's stream
+  int prof = 0;
+  struct Ev {
+    std::string stage;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> events;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, std::pair<double, size_t>> totals;
+  // session counters of Agent::trainingGeneration (agent.cpp.base:176-235)
+  unsigned long long session_experiences, session_updates, until_start, start_size;
+  double ebpu;
+};
+
+namespace {
+
+int vr_alloc(void **p, size_t bytes) {
+  KG_HIP(hipMalloc(p, bytes ? bytes : 16));
+  return kg::zero_fill(*p, bytes ? bytes : 16);
+}
+#define VR_ALLOC(ptr, bytes)                                   \
+  do {                                                         \
+    if (vr_alloc((void **)&(ptr), (bytes))) return 1;          \
+  } while (0)
+
+unsigned vr_blocks(long long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// Scoped stage timer: events recorded on the handle's stream around a stage.
+struct VrStage {
+  kg_vracer_t h;
+  size_t idx = (size_t)-1;
+  VrStage(kg_vracer_t h_, const char *name) : h(h_) {
+    if (!h->prof) return;
+    auto take = [&]() {
+      hipEvent_t e = nullptr;
+      if (!h->pool.empty()) {
+        e = h->pool.back();
+        h->pool.pop_back();
+      } else if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+      }
+      return e;
+    };
+    hipEvent_t a = take(), b = take();
+    if (!a || !b) return;
+    if (hipEventRecord(a, h->stream) != hipSuccess) return;
+    h->events.push_back({name, a, b});
+    idx = h->events.size() - 1;
+  }
+  ~VrStage() {
+    if (idx != (size_t)-1) (void)hipEventRecord(h->events[idx].b, h->stream);
+  }
+};
+
+int vr_collect(kg_vracer_t h) {
+  for (auto &e : h->events) {
+    KG_HIP(hipEventSynchronize(e.b));
+    float ms = 0.f;
+    KG_HIP(hipEventElapsedTime(&ms, e.a, e.b));
+    auto &t = h->totals[e.stage];
+    t.first += ms;
+    t.second += 1;
+    h->pool.push_back(e.a);
+    h->pool.push_back(e.b);
+  }
+  h->events.clear();
+  return 0;
+}
+
+int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
+  const Params &P = h->P;
+  KG_CHECK((size_t)M <= h->rowsMax, "vracer: forward batch exceeds the allocated rows");
+  float *a1 = h->acts;
+  hipLaunchKernelGGL(k_vr_fwd_in, dim3(vr_blocks((long long)M * P.H, 256)), dim3(256), 0, h->stream, M, P.S, P.H, X,
+                     h->theta + h->offW[0], h->theta + h->offb[0], a1);
+  VrStage tg(h, M == P.E ? "gemm_rollout" : (M == 2 * P.B ? "gemm_update" : "gemm_other"));
+  for (int l = 1; l < P.L; l++) {
+    float *prev = h->acts + (size_t)(l - 1) * h->rowsMax * P.H, *cur = h->acts + (size_t)l * h->rowsMax * P.H;
+    hipLaunchKernelGGL(k_vr_gemm<EP_BIAS_TANH>, dim3(vr_blocks(P.H, 64), vr_blocks(M, 64)), dim3(256), 0, h->stream, M, P.H,
+                       P.H, prev, (long long)P.H, 1ll, h->theta + h->offW[l], (long long)P.H, 1ll, cur, (long long)P.H,
+                       h->theta + h->offb[l], (const float *)nullptr, 0ll);
+  }
+  const float *last = h->acts + (size_t)(P.L - 1) * h->rowsMax * P.H;
+  hipLaunchKernelGGL(k_vr_fwd_out, dim3(vr_blocks((long long)M * P.O, 256)), dim3(256), 0, h->stream, M, P.H, P.O, last,
+                     h->theta + h->offW[P.L], h->theta + h->offb[P.L], out, P);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int vr_update(kg_vracer_t h, const unsigned *forced) {
+  const Params &P = h->P;
+  const int B = P.B;
+  KG_CHECK(h->st_host->size >= 2, "vracer: policy updates need at least two experiences in the replay memory");
+  VrStage tu(h, "update");
+  hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
+  if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
+  hipLaunchKernelGGL(k_vr_meta, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, (const unsigned *)h->mb,
+                     (const float *)h->out, h->G);
+  // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
+  const size_t rs = h->rowsMax * P.H;
+  const float *lastA = h->acts + (size_t)(P.L - 1) * rs;
+  hipLaunchKernelGGL(k_vr_bwd_out, dim3(vr_blocks((long long)B * P.H, 256)), dim3(256), 0, h->stream, B, P.H, P.O,
+                     (const float *)h->G, (const float *)h->out, (const float *)(h->theta + h->offW[P.L]), lastA, h->dZ,
+                     h->dHa, P);
+  hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.O * (P.H + 1), 256)), dim3(256), 0, h->stream, P.O, P.H, B,
+                     (const float *)h->dZ, P.O, lastA, P.H, h->grad + h->offW[P.L], h->grad + h->offb[P.L]);
+  float *dcur = h->dHa, *dnext = h->dHb;
+  for (int l = P.L - 1; l >= 1; l--) {
+    const float *ain = h->acts + (size_t)(l - 1) * rs;
+    // dW_l[o][i] = sum_b dH[b][o] a_{l-1}[b][i]
+    hipLaunchKernelGGL(k_vr_gemm<EP_STORE>, dim3(vr_blocks(P.H, 64), vr_blocks(P.H, 64)), dim3(256), 0, h->stream, P.H, P.H,
+                       B, (const float *)dcur, 1ll, (long long)P.H, ain, 1ll, (long long)P.H, h->grad + h->offW[l],
+                       (long long)P.H, (const float *)nullptr, (const float *)nullptr, 0ll);
+    hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.H, 256)), dim3(256), 0, h->stream, P.H, 0, B,
+                       (const float *)dcur, P.H, ain, P.H, (float *)nullptr, h->grad + h->offb[l]);
+    // dH_{l-1} = (dH W_l) * (1 - a_{l-1}^2)
+    hipLaunchKernelGGL(k_vr_gemm<EP_DTANH>, dim3(vr_blocks(P.H, 64), vr_blocks(B, 64)), dim3(256), 0, h->stream, B, P.H,
+                       P.H, (const float *)dcur, (long long)P.H, 1ll, (const float *)(h->theta + h->offW[l]), 1ll,
+                       (long long)P.H, dnext, (long long)P.H, (const float *)nullptr, ain, (long long)P.H);
+    float *tmp = dcur;
+    dcur = dnext, dnext = tmp;
+  }
+  hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.H * (P.S + 1), 256)), dim3(256), 0, h->stream, P.H, P.S, B,
+                     (const float *)dcur, P.H, (const float *)h->Xmb, P.S, h->grad + h->offW[0],
+                     h->grad + h->offb[0]);
+  hipLaunchKernelGGL(k_vr_adam, dim3(vr_blocks((long long)h->nparam, 256)), dim3(256), 0, h->stream,
+                     (long long)h->nparam, h->theta, (const float *)h->grad, h->m1, h->m2, (const State *)h->st, P.l2,
+                     P.l2imp);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int vr_read_state(kg_vracer_t h) {
+  KG_HIP(hipMemcpyAsync(h->st_host, h->st, sizeof(State), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  if (h->st_host->errors) {
+    const unsigned e = h->st_host->errors;
+    if (e & ERR_NONFINITE_GRADIENT) kg::set_error("Gradient loss returned an invalid value (VRACER.cpp.base:173-175)");
+    else if (e & ERR_NONFINITE_VALUE) kg::set_error("Calculated state value returned an invalid value (agent.cpp.base:629-630)");
+    else kg::set_error("NaN detected in the calculation of importance weight (continuous.cpp.base:391)");
+    return 1;
+  }
+  return 0;
+}
+
+struct VrField {
+  void *ptr;
+  size_t elem, count;
+};
+bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
+  const Params &P = h->P;
+  const size_t R = (size_t)P.R, E = (size_t)P.E;
+  struct {
+    const char *n;
+    void *p;
+    size_t elem, count;
+  } tab[] = {
+      {"state", h->er.st, 4, R * P.S},         {"action", h->er.act, 4, R * P.A},
+      {"reward", h->er.rew, 4, R},             {"environment_id", h->er.env, 4, R},
+      {"termination", h->er.term, 4, R},       {"truncated_state", h->er.tst, 4, R * P.S},
+      {"exp_policy", h->er.exp_pol, 4, R * 2 * P.A}, {"cur_policy", h->er.cur_pol, 4, R * 2 * P.A},
+      {"exp_state_value", h->er.exp_v, 4, R},  {"state_value", h->er.v, 4, R},
+      {"retrace", h->er.ret, 4, R},            {"importance_weight", h->er.iw, 4, R},
+      {"truncated_importance_weight", h->er.tiw, 4, R}, {"truncated_state_value", h->er.tv, 4, R},
+      {"on_policy", h->er.onp, 4, R},          {"episode_id", h->er.ep_id, 8, R},
+      {"episode_pos", h->er.ep_pos, 4, R},     {"hyperparameters", h->theta, 4, h->nparam},
+      {"adam_first_moment", h->m1, 4, h->nparam}, {"adam_second_moment", h->m2, 4, h->nparam},
+      {"gradient", h->grad, 4, h->nparam},     {"env_states", h->X, 4, E * P.S},
+      {"env_u", h->ev.u, 8, E * 4},            {"env_steps", h->ev.t, 4, E},
+      {"env_ids", h->ev.env_id, 4, E},         {"env_sample_ids", h->ev.sample, 8, E},
+      {"finished_rewards", h->ev.rewards, 4, E}, {"finished_env", h->ev.fin_env, 4, E},
+      {"mini_batch", h->mb, 4, (size_t)P.B},   {"loss_gradient", h->G, 4, (size_t)P.B * P.O},
+      {"policy_output", h->out, 4, h->rowsMax * P.O},
+  };
+  for (auto &x : tab)
+    if (!strcmp(x.n, name)) {
+      f = VrField{x.p, x.elem, x.count};
+      return true;
+    }
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
+  KG_CHECK(c && out, "vracer: null argument");
+  KG_CHECK(c->state_size >= 1 && c->action_size >= 1 && c->action_size <= (size_t)MAXA,
+           "vracer: action size must be 1..4 and state size >= 1");
+  KG_CHECK(c->state_size == 4 && c->action_size == 1,
+           "vracer: the device environment is the CartPole of examples/learning/reinforcement/cartpole (4 states, 1 action)");
+  KG_CHECK(c->hidden_size % 64 == 0 && c->hidden_size >= 64, "vracer: hidden layer width must be a multiple of 64");
+  KG_CHECK(c->hidden_layers >= 1, "vracer: at least one hidden layer");
+  KG_CHECK(c->mini_batch_size >= 2 && c->mini_batch_size <= (size_t)MAXB, "vracer: Mini Batch Size must be 2..2048");
+  KG_CHECK(c->environments >= 1 && c->environments <= (1u << 20), "vracer: Concurrent Environments out of range");
+  KG_CHECK(c->environment_count >= 1, "vracer: Environment Count must be >= 1");
+  KG_CHECK(c->replay_maximum_size >= 2 && c->replay_start_size <= c->replay_maximum_size,
+           "vracer: Experience Replay Start Size must not exceed Maximum Size");
+  KG_CHECK(c->max_episode_steps >= 1, "vracer: episodes need at least one step");
+  KG_CHECK(c->off_policy_cutoff_scale >= 0.0, "Experience Replay Cutoff Scale must be larger 0.0");
+  for (size_t i = 0; i < c->action_size; i++)
+    KG_CHECK(c->initial_exploration_noise && c->initial_exploration_noise[i] > 0.0,
+             "Provided initial noise for an action variable is not defined or negative.");
+  KG_HIP(hipSetDevice(c->device));
+  auto *h = new kg_vracer_s();
+  Params &P = h->P;
+  P.S = (int)c->state_size, P.A = (int)c->action_size, P.H = (int)c->hidden_size, P.L = (int)c->hidden_layers;
+  P.O = 1 + 2 * P.A, P.E = (int)c->environments, P.B = (int)c->mini_batch_size, P.T = (int)c->max_episode_steps;
+  P.R = (long long)c->replay_maximum_size;
+  P.env_count = (int)c->environment_count;
+  P.l2 = c->l2_regularization_enabled ? 1 : 0;
+  P.gamma = (float)c->discount_factor, P.lr0 = (float)c->learning_rate, P.iw_trunc = (float)c->importance_weight_truncation_level;
+  P.cutoff_scale = (float)c->off_policy_cutoff_scale, P.off_target = (float)c->off_policy_target;
+  P.anneal = (float)c->off_policy_annealing_rate, P.l2imp = (float)c->l2_regularization_importance;
+  P.seed = c->seed;
+  for (int o = 0; o < MAXO; o++) P.scale[o] = 1.f, P.shift[o] = 0.f, P.soft[o] = 0;
+  for (int i = 0; i < P.A; i++) {
+    P.scale[1 + P.A + i] = 2.0f * (float)c->initial_exploration_noise[i];
+    P.soft[1 + P.A + i] = 1;
+  }
+  h->device = c->device;
+  h->ebpu = c->experiences_between_policy_updates;
+  h->start_size = c->replay_start_size;
+  h->until_start = c->replay_start_size;
+  // hyperparameter layout: [W (out x in), b] per layer (linear.cpp.base:28-49)
+  std::vector<int> sz{P.S};
+  for (int l = 0; l < P.L; l++) sz.push_back(P.H);
+  sz.push_back(P.O);
+  size_t k = 0;
+  for (size_t l = 0; l + 1 < sz.size(); l++) {
+    h->offW.push_back(k);
+    k += (size_t)sz[l] * sz[l + 1];
+    h->offb.push_back(k);
+    k += (size_t)sz[l + 1];
+  }
+  h->nparam = k;
+  h->rowsMax = std::max((size_t)P.E, (size_t)2 * P.B);
+  const size_t R = (size_t)P.R, E = (size_t)P.E, ET = E * (size_t)P.T;
+  int rc = 0;
+  auto alloc = [&](auto *&p, size_t bytes) {
+    if (!rc && vr_alloc((void **)&p, bytes)) rc = 1;
+  };
+  hipError_t se = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (se != hipSuccess) {
+    delete h;
+    kg::set_error(std::string("hipStreamCreate: ") + hipGetErrorString(se));
+    return 1;
+  }
+  alloc(h->theta, k * 4), alloc(h->grad, k * 4), alloc(h->m1, k * 4), alloc(h->m2, k * 4);
+  alloc(h->X, E * P.S * 4), alloc(h->Xmb, 2 * (size_t)P.B * P.S * 4), alloc(h->Xs, h->rowsMax * P.S * 4);
+  alloc(h->acts, (size_t)P.L * h->rowsMax * P.H * 4);
+  alloc(h->out, h->rowsMax * P.O * 4), alloc(h->outF, h->rowsMax * P.O * 4);
+  alloc(h->G, (size_t)P.B * P.O * 4), alloc(h->dZ, (size_t)P.B * P.O * 4);
+  alloc(h->dHa, (size_t)P.B * P.H * 4), alloc(h->dHb, (size_t)P.B * P.H * 4);
+  alloc(h->mb, (size_t)P.B * 4), alloc(h->forced_mb, (size_t)P.B * 4), alloc(h->forced_noise, E * P.A * 4);
+  alloc(h->st, sizeof(State));
+  Replay &er = h->er;
+  alloc(er.st, R * P.S * 4), alloc(er.act, R * P.A * 4), alloc(er.rew, R * 4), alloc(er.tst, R * P.S * 4);
+  alloc(er.exp_pol, R * 2 * P.A * 4), alloc(er.cur_pol, R * 2 * P.A * 4), alloc(er.exp_v, R * 4), alloc(er.v, R * 4);
+  alloc(er.ret, R * 4), alloc(er.iw, R * 4), alloc(er.tiw, R * 4), alloc(er.tv, R * 4);
+  alloc(er.env, R * 4), alloc(er.term, R * 4), alloc(er.onp, R * 4), alloc(er.ep_pos, R * 4), alloc(er.ep_id, R * 8);
+  Envs &ev = h->ev;
+  alloc(ev.u, E * 4 * 8), alloc(ev.t, E * 4), alloc(ev.env_id, E * 4), alloc(ev.sample, E * 8), alloc(ev.cum, E * 4);
+  alloc(ev.fin, E * 4), alloc(ev.len, E * 4), alloc(ev.off, E * 8), alloc(ev.rank, E * 4), alloc(ev.fin_env, E * 4);
+  alloc(ev.eb_st, ET * P.S * 4), alloc(ev.eb_act, ET * P.A * 4), alloc(ev.eb_pol, ET * 2 * P.A * 4);
+  alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
+  if (!rc && hipHostMalloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
+    kg::set_error("vracer: hipHostMalloc failed");
+    rc = 1;
+  }
+  if (!rc) memset(h->st_host, 0, sizeof(State));
+  if (rc) {
+    kg_vracer_destroy(h);
+    return 1;
+  }
+  hipLaunchKernelGGL(k_vr_init_state, dim3(1), dim3(1), 0, h->stream, h->st, P.lr0, (float)c->off_policy_refer_beta,
+                     P.cutoff_scale);
+  // the first launch of every environment: sample ids 0 .. E-1
+  hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->ev, h->X, 0ull,
+                     (const int *)nullptr);
+  KG_HIP(hipGetLastError());
+  if (vr_read_state(h)) return 1;
+  *out = h;
+  return 0;
+}
+
+int kg_vracer_destroy(kg_vracer_t h) {
+  if (!h) return 0;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  void *ptrs[] = {h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
+                  h->dHb, h->mb, h->forced_mb, h->forced_noise, h->st, h->er.st, h->er.act, h->er.rew, h->er.tst,
+                  h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
+                  h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.t, h->ev.env_id,
+                  h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
+                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (h->st_host) (void)hipHostFree(h->st_host);
+  for (auto &e : h->events) (void)hipEventDestroy(e.a), (void)hipEventDestroy(e.b);
+  for (auto e : h->pool) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int kg_vracer_hyperparameter_count(kg_vracer_t h, size_t *n) {
+  KG_CHECK(h && n, "vracer: null argument");
+  *n = h->nparam;
+  return 0;
+}
+
+int kg_vracer_field_size(kg_vracer_t h, const char *name, size_t *elem_bytes, size_t *count) {
+  KG_CHECK(h && name, "vracer: null argument");
+  VrField f;
+  KG_CHECK(vr_field(h, name, f), std::string("vracer: unknown field '") + name + "'");
+  if (elem_bytes) *elem_bytes = f.elem;
+  if (count) *count = f.count;
+  return 0;
+}
+
+int kg_vracer_get_field(kg_vracer_t h, const char *name, void *dst, size_t bytes) {
+  KG_CHECK(h && name && dst, "vracer: null argument");
+  VrField f;
+  KG_CHECK(vr_field(h, name, f), std::string("vracer: unknown field '") + name + "'");
+  KG_CHECK(bytes <= f.elem * f.count, "vracer: field read exceeds its size");
+  KG_HIP(hipMemcpyAsync(dst, f.ptr, bytes, hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_vracer_set_field(kg_vracer_t h, const char *name, const void *src, size_t bytes) {
+  KG_CHECK(h && name && src, "vracer: null argument");
+  VrField f;
+  KG_CHECK(vr_field(h, name, f), std::string("vracer: unknown field '") + name + "'");
+  KG_CHECK(bytes <= f.elem * f.count, "vracer: field write exceeds its size");
+  KG_HIP(hipMemcpyAsync(f.ptr, src, bytes, hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+static const char *const kScalarNames[] = {"learning_rate", "refer_beta", "off_policy_cutoff", "off_policy_ratio",
+                                           "adam_eta", "adam_beta1_pow", "adam_beta2_pow", "off_policy_count",
+                                           "policy_update_count", "total", "size", "current_episode",
+                                           "current_sample_id", "mini_batch_counter", "environment_step",
+                                           "step_new_experiences", "step_episodes", "experience_count",
+                                           "step_reward_sum"};
+
+int kg_vracer_get_scalar(kg_vracer_t h, const char *name, double *v) {
+  KG_CHECK(h && name && v, "vracer: null argument");
+  KG_HIP(hipMemcpyAsync(h->st_host, h->st, sizeof(State), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  const State &s = *h->st_host;
+  const double vals[] = {s.lr, s.beta, s.cutoff, s.off_ratio, s.eta, s.b1p, s.b2p, (double)s.off_count,
+                         (double)s.update_count, (double)s.total, (double)s.size, (double)s.episode,
+                         (double)s.sample_id, (double)s.mb_counter, (double)s.env_step, (double)s.step_new,
+                         (double)s.step_episodes, (double)s.experience_count, s.step_reward_sum};
+  for (size_t i = 0; i < sizeof(vals) / sizeof(vals[0]); i++)
+    if (!strcmp(kScalarNames[i], name)) {
+      *v = vals[i];
+      return 0;
+    }
+  kg::set_error(std::string("vracer: unknown scalar '") + name + "'");
+  return 1;
+}
+
+int kg_vracer_set_scalar(kg_vracer_t h, const char *name, double v) {
+  KG_CHECK(h && name, "vracer: null argument");
+  KG_HIP(hipMemcpyAsync(h->st_host, h->st, sizeof(State), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  State &s = *h->st_host;
+  const std::string n(name);
+  if (n == "learning_rate") s.lr = (float)v;
+  else if (n == "refer_beta") s.beta = (float)v;
+  else if (n == "off_policy_cutoff") s.cutoff = (float)v;
+  else if (n == "off_policy_ratio") s.off_ratio = (float)v;
+  else if (n == "off_policy_count") s.off_count = (long long)v;
+  else if (n == "policy_update_count") s.update_count = (long long)v;
+  else if (n == "total") s.total = (unsigned long long)v;
+  else if (n == "size") s.size = (unsigned long long)v;
+  else if (n == "current_episode") s.episode = (unsigned long long)v;
+  else if (n == "mini_batch_counter") s.mb_counter = (unsigned long long)v;
+  else if (n == "experience_count") s.experience_count = (unsigned long long)v;
+  else {
+    kg::set_error("vracer: scalar '" + n + "' is not settable");
+    return 1;
+  }
+  KG_HIP(hipMemcpyAsync(h->st, h->st_host, sizeof(State), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_vracer_run_policy(kg_vracer_t h, const float *states, size_t n, float *out) {
+  KG_CHECK(h && states && out, "vracer: null argument");
+  KG_CHECK(n <= h->rowsMax, "vracer: run_policy batch exceeds max(Concurrent Environments, 2 x Mini Batch Size)");
+  KG_HIP(hipMemcpyAsync(h->Xs, states, n * h->P.S * 4, hipMemcpyHostToDevice, h->stream));
+  if (vr_forward(h, h->Xs, (int)n, h->out)) return 1;
+  KG_HIP(hipMemcpyAsync(out, h->out, n * h->P.O * 4, hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_vracer_set_action_noise(kg_vracer_t h, const float *noise, size_t n) {
+  KG_CHECK(h, "vracer: null argument");
+  if (!noise) {
+    h->use_forced_noise = 0;
+    return 0;
+  }
+  KG_CHECK(n == (size_t)h->P.E * h->P.A, "vracer: action noise must hold Concurrent Environments x action size values");
+  KG_HIP(hipMemcpyAsync(h->forced_noise, noise, n * 4, hipMemcpyHostToDevice, h->stream));
+  h->use_forced_noise = 1;
+  return 0;
+}
+
+int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
+  KG_CHECK(h, "vracer: null argument");
+  const Params &P = h->P;
+  {
+  VrStage te(h, "environment_step");
+  if (vr_forward(h, h->X, P.E, h->out)) return 1;
+  hipLaunchKernelGGL(k_vr_env_act, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->st, h->ev,
+                     (const float *)h->out, h->X, h->use_forced_noise ? (const float *)h->forced_noise : nullptr);
+  h->use_forced_noise = 0;
+  if (vr_forward(h, h->X, P.E, h->outF)) return 1;  // V of truncated states (agent.cpp.base:530-545)
+  hipLaunchKernelGGL(k_vr_scan, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->ev);
+  hipLaunchKernelGGL(k_vr_append, dim3(P.E), dim3(256), 0, h->stream, P, h->st, h->er, h->ev, (const float *)h->outF,
+                     h->X);
+  KG_HIP(hipGetLastError());
+  }
+  if (vr_read_state(h)) return 1;
+  h->session_experiences += h->st_host->step_new;
+  if (new_experiences) *new_experiences = (size_t)h->st_host->step_new;
+  return 0;
+}
+
+int kg_vracer_train_policy(kg_vracer_t h, size_t updates) {
+  KG_CHECK(h, "vracer: null argument");
+  for (size_t u = 0; u < updates; u++)
+    if (vr_update(h, nullptr)) return 1;
+  h->session_updates += updates;
+  return 0;
+}
+
+int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *ids, size_t count) {
+  KG_CHECK(h && ids, "vracer: null argument");
+  KG_CHECK(count == (size_t)h->P.B, "vracer: the mini-batch must hold Mini Batch Size ids");
+  for (size_t i = 1; i < count; i++) KG_CHECK(ids[i - 1] <= ids[i], "vracer: mini-batch ids must be sorted");
+  KG_CHECK(ids[count - 1] < h->st_host->size, "vracer: mini-batch id beyond the replay memory size");
+  KG_HIP(hipMemcpyAsync(h->forced_mb, ids, count * 4, hipMemcpyHostToDevice, h->stream));
+  if (vr_update(h, h->forced_mb)) return 1;
+  h->session_updates += 1;
+  return 0;
+}
+
+int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates) {
+  KG_CHECK(h, "vracer: null argument");
+  size_t added = 0;
+  if (kg_vracer_environment_step(h, &added)) return 1;
+  size_t n = 0;
+  // Agent::trainingGeneration (agent.cpp.base:201-231)
+  if (h->st_host->experience_count >= h->start_size)
+    while ((double)h->session_experiences > h->ebpu * (double)(h->session_updates + n) + (double)h->until_start) n++;
+  if (n && kg_vracer_train_policy(h, n)) return 1;
+  if (new_experiences) *new_experiences = added;
+  if (updates) *updates = n;
+  return 0;
+}
+
+int kg_vracer_synchronize(kg_vracer_t h) {
+  KG_CHECK(h, "vracer: null argument");
+  return vr_read_state(h);
+}
+
+int kg_vracer_profile(kg_vracer_t h, int enable) {
+  KG_CHECK(h, "vracer: null argument");
+  if (vr_collect(h)) return 1;
+  h->prof = enable ? 1 : 0;
+  h->totals.clear();
+  return 0;
+}
+
+int kg_vracer_profile_read(kg_vracer_t h, const char *stage, double *ms_total, size_t *count) {
+  KG_CHECK(h && stage && ms_total && count, "vracer: null argument");
+  if (vr_collect(h)) return 1;
+  auto it = h->totals.find(stage);
+  *ms_total = it == h->totals.end() ? 0.0 : it->second.first;
+  *count = it == h->totals.end() ? 0 : it->second.second;
+  if (it != h->totals.end()) h->totals.erase(it);
+  return 0;
+}
+
+int kg_vracer_stream(kg_vracer_t h, void **stream) {
+  KG_CHECK(h && stream, "vracer: null argument");
+  *stream = (void *)h->stream;
+  return 0;
+}
+
+}  // extern "C"

@@ -6,3 +6,4 @@
 #include "kg_eigen.hip"
 #include "kg_cmaes.hip"
 #include "kg_tmcmc.hip"
+#include "kg_vracer.hip"

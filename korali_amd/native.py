@@ -68,6 +68,12 @@ EXPORTED = [
     "kg_tmcmc_process_partial", "kg_tmcmc_process_finalize", "kg_tmcmc_device_ptr", "kg_tmcmc_stream", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
     "kg_tmcmc_set_gradients",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump",
+    # VRACER (korali_amd/vracer.py binds their argument types)
+    "kg_vracer_create", "kg_vracer_destroy", "kg_vracer_hyperparameter_count", "kg_vracer_field_size",
+    "kg_vracer_get_field", "kg_vracer_set_field", "kg_vracer_get_scalar", "kg_vracer_set_scalar",
+    "kg_vracer_run_policy", "kg_vracer_set_action_noise", "kg_vracer_environment_step", "kg_vracer_train_policy",
+    "kg_vracer_train_policy_minibatch", "kg_vracer_training_step", "kg_vracer_synchronize", "kg_vracer_stream",
+    "kg_vracer_profile", "kg_vracer_profile_read",
 ]
 
 

@@ -83,8 +83,8 @@ def test_statistical_cmaes_correctness(cfg, tol):
 def test_unsupported_features_fail_loudly():
     import korali
     e = cmaes_1d()
-    e["Solver"]["Mirrored Sampling"] = True
-    with pytest.raises(korali.KoraliError, match="Mirrored Sampling"):
+    e["Variables"][0]["Granularity"] = 0.5
+    with pytest.raises(korali.KoraliError, match="Granularity"):
         korali.Engine().run(e)
 
 

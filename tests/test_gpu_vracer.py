@@ -1,0 +1,206 @@
+"""GPU parity of the VRACER agent (korali_amd/csrc/kg_vracer.hip) against the
+oracle's restatement (oracle/vracer_ref.py), through the C-ABI.
+
+Float32 like the reference; the device reassociates the matrix products
+(MFMA 16x16x4 tiles) and uses the device libm, so values are compared with
+float32 tolerances (written per check); discrete outcomes (termination,
+episode ids, mini-batch ids, on-policy flags, counters) must be equal.
+Reference parity is unpinned (no VRACER fixtures in the reference)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import vracer_ref as V  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+S, A = 4, 1
+
+
+def theta_for(H, L, seed, spread=0.15):
+    n = V.hyperparameter_count(S, H, L, A)
+    rng = np.random.default_rng(seed)
+    th = V.initial_hyperparameters(S, H, L, A, rng.uniform(-1, 1, n))
+    return (th + spread * rng.standard_normal(n) / np.sqrt(H)).astype(f32)
+
+
+def device(**kw):
+    from korali_amd.vracer import VracerDevice
+    return VracerDevice(**kw)
+
+
+def close(a, b, rtol, atol):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + rtol * np.abs(b))
+    assert err.max() <= 0, f"max excess {err.max():.3e} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+@pytest.mark.parametrize("H,L,n", [(64, 1, 37), (256, 2, 500), (128, 3, 4096)])
+def test_run_policy_matches_oracle(H, L, n):
+    th = theta_for(H, L, 1, spread=1.0)
+    d = device(hidden_size=H, hidden_layers=L, environments=4096, mini_batch_size=64, replay_maximum_size=1024,
+               replay_start_size=512, initial_exploration_noise=0.7, hyperparameters=th)
+    X = np.random.default_rng(2).standard_normal((n, S)).astype(f32)
+    out = d.run_policy(X)
+    ref, _ = V.forward(th, X, S, H, L, A, 0.7)
+    close(out, ref, 2e-5, 2e-5)  # float32 sums of <= 256 terms in another order
+    assert np.all(out[:, 2] > 0)
+
+
+def fill_replay(H, L, E, steps, max_size, seed=3):
+    th = theta_for(H, L, seed)
+    ag = V.Agent(S, A, H, L, th, max_size=max_size)
+    ro = V.Rollouts(ag, E, max_steps=40)
+    for s in range(steps):
+        ro.step(V.action_noise(seed, s, E, A))
+    return ag, th
+
+
+def load_replay(d, ag):
+    er, n = ag.er, ag.size()
+    d.set("state", np.stack(er["state"]))
+    d.set("action", np.stack(er["action"]))
+    d.set("reward", np.array(er["reward"], f32))
+    d.set("environment_id", np.array(er["env"]))
+    d.set("termination", np.array(er["term"]))
+    d.set("truncated_state", np.stack(er["tstate"]))
+    d.set("exp_policy", np.stack(er["exp_pol"]))
+    d.set("cur_policy", np.stack(er["cur_pol"]))
+    d.set("exp_state_value", np.array(er["exp_v"], f32))
+    d.set("state_value", np.array(er["v"], f32))
+    d.set("retrace", np.array(er["ret"], f32))
+    d.set("importance_weight", np.array(er["iw"], f32))
+    d.set("truncated_importance_weight", np.array(er["tiw"], f32))
+    d.set("truncated_state_value", np.array(er["tv"], f32))
+    d.set("on_policy", np.array(er["onp"], np.int32))
+    d.set("episode_id", np.array(er["ep_id"], np.int64))
+    d.set("episode_pos", np.array(er["ep_pos"], np.int32))
+    d.set_scalar("total", n)
+    d.set_scalar("size", n)
+    d.set_scalar("off_policy_count", ag.off_count)
+    d.set_scalar("current_episode", ag.current_episode)
+    d.set_scalar("experience_count", ag.experience_count)
+
+
+@pytest.mark.parametrize("H,L,B", [(64, 2, 32), (256, 2, 256)])
+def test_policy_updates_match_oracle(H, L, B):
+    """VRACER::trainPolicy on a replay memory filled by the oracle's rollouts:
+    five updates with given sorted mini-batches (metadata, retrace, loss
+    gradient, backward, fAdam and the REF-ER schedule)."""
+    ag, th = fill_replay(H, L, 8, 90, 600)
+    d = device(hidden_size=H, hidden_layers=L, environments=8, mini_batch_size=B, replay_maximum_size=600,
+               replay_start_size=100, hyperparameters=th)
+    load_replay(d, ag)
+    rng = np.random.default_rng(9)
+    for u in range(5):
+        ids = np.sort(rng.integers(0, ag.size() - 1, B)).astype(np.uint32)
+        ids[1] = ids[0]  # a duplicate entry (updateExperienceMetadata's unique filter)
+        ids.sort()
+        G, grad = ag.train_policy([int(i) for i in ids])
+        d.train_minibatch(ids)
+        close(d.get("loss_gradient").reshape(B, -1), G, 1e-3, 1e-4)
+        close(d.get("gradient"), grad, 2e-3, 2e-3 * np.abs(grad).max())
+        close(d.hyperparameters, ag.theta, 1e-4, 1e-6)
+        assert np.array_equal(d.get("on_policy")[:ag.size()], np.array(ag.er["onp"], np.int32))
+        close(d.get("retrace")[:ag.size()], np.array(ag.er["ret"], f32), 1e-4, 1e-5)
+        close(d.get("importance_weight")[:ag.size()], np.array(ag.er["iw"], f32), 1e-4, 1e-6)
+        assert d.scalar("policy_update_count") == ag.update_count
+        assert d.scalar("off_policy_count") == ag.off_count
+        assert np.isclose(d.scalar("refer_beta"), float(ag.beta), rtol=1e-6)
+        assert np.isclose(d.scalar("learning_rate"), float(ag.lr), rtol=1e-7)
+        assert np.isclose(d.scalar("off_policy_cutoff"), float(ag.cutoff), rtol=1e-7)
+
+
+def test_environment_steps_match_oracle():
+    """Concurrent CartPole environments with the same action noise: episodes,
+    terminations, the replay memory in processEpisode order, initial retrace
+    values, relaunch sample ids — 120 steps, eviction included."""
+    H, L, E, R = 64, 2, 16, 700
+    th = theta_for(H, L, 4, spread=0.6)
+    ag = V.Agent(S, A, H, L, th, max_size=R)
+    ro = V.Rollouts(ag, E, max_steps=40)
+    d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=32, replay_maximum_size=R,
+               replay_start_size=R, max_episode_steps=40, hyperparameters=th, seed=4)
+    rng = np.random.default_rng(5)
+    total = 0
+    for s in range(120):
+        z = rng.standard_normal((E, A)).astype(f32)
+        new_ref, _ = ro.step(z)
+        new_dev = d.environment_step(noise=z)
+        assert new_dev == new_ref, s
+        total += new_ref
+    assert total > R  # the ring wrapped
+    n = ag.size()
+    assert d.scalar("size") == n and d.scalar("total") == total and d.scalar("current_episode") == ag.current_episode
+    # device ring -> logical order
+    start = (total - n) % R
+    order = (start + np.arange(n)) % R
+    er = ag.er
+    assert np.array_equal(d.get("termination")[order], np.array(er["term"]))
+    assert np.array_equal(d.get("episode_id")[order], np.array(er["ep_id"]))
+    assert np.array_equal(d.get("episode_pos")[order], np.array(er["ep_pos"]))
+    assert np.array_equal(d.get("environment_id")[order], np.array(er["env"]))
+    assert np.array_equal(d.get("reward")[order], np.array(er["reward"], f32))
+    close(d.get("state").reshape(R, S)[order], np.stack(er["state"]), 1e-5, 1e-6)
+    close(d.get("action")[order], np.concatenate(er["action"]), 1e-5, 1e-5)
+    close(d.get("exp_policy").reshape(R, 2)[order], np.stack(er["exp_pol"]), 1e-5, 1e-6)
+    close(d.get("retrace")[order], np.array(er["ret"], f32), 1e-5, 1e-5)
+    close(d.get("truncated_state").reshape(R, S)[order], np.stack(er["tstate"]), 1e-5, 1e-6)
+    assert np.array_equal(d.get("env_sample_ids"), np.array(ro.sample, np.uint64))
+    # actions differ in the last float32 bits (reassociated MFMA sums), so do the states
+    close(d.get("env_u").reshape(E, 4), np.stack([c.u for c in ro.carts]), 1e-5, 1e-6)
+
+
+def test_training_loop_matches_oracle_end_to_end():
+    """kg_vracer_training_step with the device's own streams (action noise,
+    mini-batch uniforms; the oracle draws the same philox blocks) — the
+    body of Agent::trainingGeneration: environment step, then as many updates
+    as Experiences Between Policy Updates allows once the start size is reached."""
+    H, L, E, R, B = 64, 2, 8, 400, 32
+    th = theta_for(H, L, 6)
+    seed = 77
+    ag = V.Agent(S, A, H, L, th, max_size=R)
+    ro = V.Rollouts(ag, E, max_steps=30)
+    d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=B, replay_maximum_size=R,
+               replay_start_size=150, max_episode_steps=30, experiences_between_policy_updates=4.0,
+               hyperparameters=th, seed=seed)
+    session_exp, updates, mb_ctr = 0, 0, 0
+    for s in range(70):
+        new_ref, _ = ro.step(V.action_noise(seed, s, E, A))
+        session_exp += new_ref
+        n = 0
+        if ag.experience_count >= 150:
+            while session_exp > 4.0 * (updates + n) + 150:
+                n += 1
+        for _ in range(n):
+            ids = ag.minibatch_ids(V.minibatch_uniforms(seed, mb_ctr, B))
+            mb_ctr += B
+            ag.train_policy(ids)
+        updates += n
+        new_dev, n_dev = d.training_step()
+        assert (new_dev, n_dev) == (new_ref, n), s
+    assert updates > 10
+    close(d.hyperparameters, ag.theta, 1e-3, 1e-5)
+    assert d.scalar("policy_update_count") == ag.update_count
+
+
+def test_c5_shape_runs():
+    """Config C5: 4096 concurrent environments, 2x256 hidden layers, mini-batch
+    256 — a few training steps with updates; all values finite, counters
+    consistent with the reference's update rule."""
+    d = device(environments=4096, hidden_size=256, hidden_layers=2, mini_batch_size=256,
+               replay_maximum_size=262144, replay_start_size=8192, experiences_between_policy_updates=64.0, seed=1)
+    th = theta_for(256, 2, 8)
+    d.set("hyperparameters", th)
+    tot, ups = 0, 0
+    for _ in range(40):
+        n, u = d.training_step()
+        tot += n
+        ups += u
+    assert tot == d.scalar("experience_count") and ups == d.scalar("policy_update_count") > 0
+    assert np.all(np.isfinite(d.hyperparameters))
+    assert np.all(np.isfinite(d.get("retrace")[:int(d.scalar("size"))]))
