@@ -245,14 +245,16 @@ def main():
                     help="exact (default): bit-exact rank-mu order, the reference's trajectory; mfma: FP64 matrix "
                          "cores, <= 1e-12 per step (reported beside the exact rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192; c4: CMA-ES 512-dim Ackley, "
-                         "lambda=65536, population sharded over the ranks")
+                         "lambda=65536, population sharded over the ranks; c5: VRACER, 4096 CartPole rollouts")
     args = ap.parse_args()
     if args.workload == "c3":
         return run_c3(args)
     if args.workload == "c4":
         return run_c4(args)
+    if args.workload == "c5":
+        return run_c5(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -639,6 +641,139 @@ def run_c4(args):
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------- C5 VRACER
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 matrix (= FP32 vector) peak, MI355X_MICROARCH.md
+C5 = dict(environments=4096, hidden_size=256, hidden_layers=2, mini_batch_size=256, replay_maximum_size=262144,
+          replay_start_size=131072, experiences_between_policy_updates=1.0, max_episode_steps=500,
+          environment_count=3, discount_factor=0.99, learning_rate=1e-4, initial_exploration_noise=1.0)
+
+
+def c5_update_flops(S=4, H=256, L=2, A=1, B=256):
+    """Algorithmic FLOPs of one VRACER::trainPolicy: the critic/policy forward on
+    2B rows (mini-batch + truncated states) and the backward on B rows."""
+    O = 1 + 2 * A
+    fwd = 2 * (2 * B) * (S * H + (L - 1) * H * H + H * O)
+    bwd = 2 * B * (H * O) * 2 + (L - 1) * 2 * (2 * B * H * H) + 2 * B * S * H
+    return fwd + bwd
+
+
+def c5_cpu_baseline(seconds_budget=15.0):
+    """The NumPy restatement (oracle/vracer_ref.py) on one core: environment
+    steps of the same 4096 CartPole rollouts and policy updates of the same
+    network, timed separately on bounded samples."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vracer_ref as V
+    try:
+        from threadpoolctl import threadpool_limits
+        limit = threadpool_limits(1)
+    except Exception:  # noqa: BLE001
+        limit = None
+    S, A, H, L, E = 4, 1, C5["hidden_size"], C5["hidden_layers"], C5["environments"]
+    n = V.hyperparameter_count(S, H, L, A)
+    th = V.initial_hyperparameters(S, H, L, A, np.random.default_rng(0).uniform(-1, 1, n))
+    ag = V.Agent(S, A, H, L, th, max_size=C5["replay_maximum_size"], discount=C5["discount_factor"],
+                 learning_rate=C5["learning_rate"])
+    ro = V.Rollouts(ag, E, max_steps=C5["max_episode_steps"])
+    t0, steps, exps = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < seconds_budget / 2 or steps < 2:
+        new, _ = ro.step(V.action_noise(1, steps, E, A))
+        steps, exps = steps + 1, exps + new
+    env_s = (time.perf_counter() - t0) / steps
+    # policy updates on a replay memory of synthetic 50-step episodes (the
+    # update cost does not depend on the values)
+    rng = np.random.default_rng(2)
+    while ag.size() < 8192:
+        T = 50
+        ag.process_episode(int(rng.integers(3)), rng.standard_normal((T, S)).astype(np.float32),
+                           rng.standard_normal((T, A)).astype(np.float32), np.ones(T, np.float32),
+                           np.abs(rng.standard_normal((T, 2 * A))).astype(np.float32) + 0.5,
+                           rng.standard_normal(T).astype(np.float32), V.TERMINAL)
+    t0, ups = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds_budget / 2 or ups < 3:
+        ag.train_policy(ag.minibatch_ids(V.minibatch_uniforms(1, ups * C5["mini_batch_size"], C5["mini_batch_size"])))
+        ups += 1
+    upd_s = (time.perf_counter() - t0) / ups
+    if limit is not None:
+        limit.unregister() if hasattr(limit, "unregister") else None
+    # steady state of the benchmark: one environment step of E actions plus
+    # E / Experiences Between Policy Updates updates
+    per_step = env_s + E / C5["experiences_between_policy_updates"] * upd_s
+    return {"value": E / per_step, "unit": "experiences/s", "cores": 1, "kind": "port",
+            "updates_per_sec": 1.0 / upd_s, "environment_step_ms": env_s * 1e3, "update_ms": upd_s * 1e3,
+            "cpu": cpu_model(),
+            "sample": f"oracle/vracer_ref.py (NumPy, 1 BLAS thread): {steps} environment steps of {E} CartPole "
+                      f"rollouts and {ups} policy updates (mini-batch {C5['mini_batch_size']}, 2x{H} tanh); value = "
+                      f"E / (env step + E/EBPU updates)"}
+
+
+def run_c5(args):
+    """BASELINE.json configs[4]: VRACER agent (Normal policy), 4096 concurrent
+    CartPole environments (examples/learning/reinforcement/cartpole), critic/
+    policy 2 x 256 tanh, mini-batch 256, Experiences Between Policy Updates 1
+    (the cartpole example's), replay 262144 / start 131072.  A step is one
+    iteration of Agent::trainingGeneration's loop: every environment takes an
+    action, finished episodes enter the replay memory, then the policy
+    updates the experience count allows (kg_vracer_training_step)."""
+    from korali_amd.vracer import VracerDevice
+    d = VracerDevice(seed=1337, **C5)
+    # warm-up: fill the replay memory to its start size, then W steps
+    filled = 0
+    while d.scalar("experience_count") < C5["replay_start_size"]:
+        d.training_step()
+        filled += 1
+    for _ in range(args.warmup):
+        d.training_step()
+    d.synchronize()
+    exps, ups = 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n, u = d.training_step()
+        exps, ups = exps + n, ups + u
+    d.synchronize()
+    elapsed = time.perf_counter() - t0
+    # stage timers on a few more steps
+    d.profile(True)
+    for _ in range(3):
+        d.training_step()
+    d.synchronize()
+    stages = {}
+    for st in ("environment_step", "update", "gemm_rollout", "gemm_update"):
+        ms, cnt = d.profile_read(st)
+        if cnt:
+            stages[st] = ms / cnt
+    d.profile(False)
+    E, H = C5["environments"], C5["hidden_size"]
+    gemm_flops = 2.0 * E * H * H * (C5["hidden_layers"] - 1)  # hidden-layer products of one rollout forward
+    gemm_ms = stages.get("gemm_rollout")
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
+    upd_flops = c5_update_flops(H=H, L=C5["hidden_layers"], B=C5["mini_batch_size"])
+    upd_ms = stages.get("update")
+    finished = d.get("finished_rewards")
+    out = {
+        "metric": "VRACER experiences/sec, 4096 concurrent CartPole rollouts, 2x256 policy (C5)",
+        "value": exps / elapsed, "unit": "experiences/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C5: VRACER Normal policy, CartPole env (examples/learning/reinforcement/cartpole, "
+                               "RK4), 4096 concurrent environments, 2x256 tanh, mini-batch 256, EBPU 1, "
+                               "replay 262144 (start 131072)", "fill_steps": filled},
+        "policy_updates_per_sec": ups / elapsed, "updates": ups, "experiences": exps,
+        "stage_ms": stages,
+        "update_roofline": {"flops_per_update": upd_flops, "avg_update_ms": upd_ms,
+                            "achieved_tflops": upd_flops / (upd_ms * 1e-3) / 1e12 if upd_ms else None,
+                            "peak": FP32_PEAK_TFLOPS,
+                            "frac": upd_flops / (upd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS if upd_ms else None},
+        "roofline": {"kernel": "kg::vr::k_vr_gemm<1> (rollout forward, hidden layer)", "bound": "mfma",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": None,
+                     "algorithmic_flops_per_launch": gemm_flops, "avg_launch_ms": gemm_ms},
+        "mean_recent_episode_reward": float(np.mean(finished[finished != 0])) if np.any(finished != 0) else None,
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = c5_cpu_baseline()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -125,86 +125,131 @@ __global__ void k_vr_fwd_in(int M, int S, int H, const float *__restrict__ X, co
 
 // Output layer (N = 1 + 2A): Linear + Output-layer transformation
 // (output.cpp.base:140-160: Softplus 0.5 (x + sqrt(1 + x^2)) in double, then
-// Scale and Shift in float).
-__global__ void k_vr_fwd_out(int M, int H, int O, const float *__restrict__ Hs, const float *__restrict__ W,
-                             const float *__restrict__ b, float *__restrict__ out, Params P) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long long)M * O) return;
-  const int m = (int)(t / O), o = (int)(t % O);
-  const float4 *h4 = reinterpret_cast<const float4 *>(Hs + (long long)m * H);
-  const float4 *w4 = reinterpret_cast<const float4 *>(W + (long long)o * H);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  for (int i = 0; i < H / 4; i++) {
-    const float4 h = h4[i], w = w4[i];
-    a0 += w.x * h.x, a1 += w.y * h.y, a2 += w.z * h.z, a3 += w.w * h.w;
+// Scale and Shift in float).  One wave per row: each lane takes H/64
+// consecutive columns, the O partial sums are reduced across the wave.
+__global__ __launch_bounds__(256) void k_vr_fwd_out(int M, int H, int O, const float *__restrict__ Hs,
+                                                    const float *__restrict__ W, const float *__restrict__ b,
+                                                    float *__restrict__ out, Params P) {
+  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float acc[MAXO];
+  for (int o = 0; o < O; o++) acc[o] = 0.f;
+  const float *h = Hs + (long long)m * H;
+  for (int i = lane; i < H; i += 64) {
+    const float x = h[i];
+    for (int o = 0; o < O; o++) acc[o] += W[o * H + i] * x;
   }
-  float x = ((a0 + a1) + (a2 + a3)) + b[o];
-  if (P.soft[o]) x = (float)(0.5 * ((double)x + sqrt(1.0 + (double)x * (double)x)));
-  out[t] = x * P.scale[o] + P.shift[o];
+  for (int o = 0; o < O; o++)
+    for (int d = 32; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d, 64);
+  if (lane < O) {
+    float x = 0.f;
+    for (int o = 0; o < O; o++)
+      if (o == lane) x = acc[o];
+    x = x + b[lane];
+    if (P.soft[lane]) x = (float)(0.5 * ((double)x + sqrt(1.0 + (double)x * (double)x)));
+    out[(long long)m * O + lane] = x * P.scale[lane] + P.shift[lane];
+  }
 }
 
-// C[m][n] = sum_k A(m,k) B(n,k) on v_mfma_f32_16x16x4_f32, 64x64 tile per
-// 256-thread workgroup (each wave a 32x32 quarter as 2x2 16x16 accumulators),
-// A and B staged 32 k-columns at a time through LDS with any element strides
-// (so the same kernel serves X W^T, W^T-side and batch-reduction products).
-// Epilogues: bias + tanh (forward), times (1 - T^2) (tanh backward), plain.
+// C[m][n] = sum_k A(m,k) B(n,k) on v_mfma_f32_16x16x4_f32.  These products
+// are small (M, N <= 4096 x 256, K <= 512) and sit on the per-update latency
+// chain, so a workgroup owns a 32x32 tile and stages its whole A and B panels
+// (up to 256 k-columns at a time) in LDS with every load in flight at once;
+// each wave then computes one 16x16 block over the panel with two
+// interleaved accumulators (the 40-cycle dependent MFMA latency hidden behind
+// the 32-cycle issue).  Any element strides (X W^T, W^T-side and
+// batch-reduction products share the kernel).  Epilogues: bias + tanh
+// (forward), times (1 - T^2) (tanh backward), plain.
 enum : int { EP_STORE = 0, EP_BIAS_TANH = 1, EP_DTANH = 2 };
+constexpr int GT = 32, GK = 256, GP = GT + 1;
 template <int EP>
 __global__ __launch_bounds__(256) void k_vr_gemm(int M, int N, int K, const float *__restrict__ A, long long sam,
                                                  long long sak, const float *__restrict__ B, long long sbn,
                                                  long long sbk, float *__restrict__ C, long long ldc,
                                                  const float *__restrict__ bias, const float *__restrict__ T,
-                                                 long long ldt) {
-  __shared__ float As[32][68];
-  __shared__ float Bs[32][68];
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 1, wc = wave & 1, li = lane & 15,
+                                                 long long ldt, int vec) {
+  __shared__ float As[GK][GP];
+  __shared__ float Bs[GK][GP];
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, br = wave >> 1, bc = wave & 1, li = lane & 15,
             lk = lane >> 4;
-  f32x4 acc00 = {0.f, 0.f, 0.f, 0.f}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
-  for (int k0 = 0; k0 < K; k0 += 32) {
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  for (int k0 = 0; k0 < K; k0 += GK) {
+    const int kc = min(GK, K - k0);
+    if (vec && m0 + GT <= M && n0 + GT <= N) {
+      // full tile, 16-byte aligned strides: every thread issues all its float4
+      // loads (8 per panel at kc = 256) before the first LDS store
+      float4 ra[8], rb[8];
+      const int nv = GT * kc / 4;  // float4s per panel (kc % 4 == 0)
 #pragma unroll
-    for (int e0 = 0; e0 < 2048; e0 += 256) {
-      const int e = e0 + t;
-      int mm, kk;
-      if (sak == 1) kk = e & 31, mm = e >> 5;
-      else mm = e & 63, kk = e >> 6;
-      const int gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.f;
-      int nn, kb;
-      if (sbk == 1) kb = e & 31, nn = e >> 5;
-      else nn = e & 63, kb = e >> 6;
-      const int gn = n0 + nn, gkb = k0 + kb;
-      Bs[kb][nn] = (gn < N && gkb < K) ? B[gn * sbn + gkb * sbk] : 0.f;
+      for (int q = 0; q < 8; q++) {
+        const int e = t + 256 * q;
+        if (e < nv) {
+          if (sak == 1) ra[q] = *reinterpret_cast<const float4 *>(A + (m0 + e / (kc / 4)) * sam + k0 + 4 * (e % (kc / 4)));
+          else ra[q] = *reinterpret_cast<const float4 *>(A + (long long)(k0 + e / 8) * sak + m0 + 4 * (e % 8));
+          if (sbk == 1) rb[q] = *reinterpret_cast<const float4 *>(B + (n0 + e / (kc / 4)) * sbn + k0 + 4 * (e % (kc / 4)));
+          else rb[q] = *reinterpret_cast<const float4 *>(B + (long long)(k0 + e / 8) * sbk + n0 + 4 * (e % 8));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int e = t + 256 * q;
+        if (e < nv) {
+          if (sak == 1) {
+            const int r = e / (kc / 4), k = 4 * (e % (kc / 4));
+            As[k][r] = ra[q].x, As[k + 1][r] = ra[q].y, As[k + 2][r] = ra[q].z, As[k + 3][r] = ra[q].w;
+          } else {
+            const int k = e / 8, r = 4 * (e % 8);
+            As[k][r] = ra[q].x, As[k][r + 1] = ra[q].y, As[k][r + 2] = ra[q].z, As[k][r + 3] = ra[q].w;
+          }
+          if (sbk == 1) {
+            const int r = e / (kc / 4), k = 4 * (e % (kc / 4));
+            Bs[k][r] = rb[q].x, Bs[k + 1][r] = rb[q].y, Bs[k + 2][r] = rb[q].z, Bs[k + 3][r] = rb[q].w;
+          } else {
+            const int k = e / 8, r = 4 * (e % 8);
+            Bs[k][r] = rb[q].x, Bs[k][r + 1] = rb[q].y, Bs[k][r + 2] = rb[q].z, Bs[k][r + 3] = rb[q].w;
+          }
+        }
+      }
+      for (int e = t; e < GT * (GK - kc); e += 256) {  // zero rows past kc (MFMA reads up to kc rounded to 8)
+        const int k = kc + e / GT, r = e % GT;
+        As[k][r] = 0.f, Bs[k][r] = 0.f;
+      }
+    } else
+    // stage: element (r, k) of the 32-row panel; k fastest when k is the contiguous stride
+    for (int e = t; e < GT * GK; e += 256) {
+      int r, k;
+      if (sak == 1) k = e % GK, r = e / GK;
+      else r = e % GT, k = e / GT;
+      const int gm = m0 + r;
+      As[k][r] = (k < kc && gm < M) ? A[gm * sam + (long long)(k0 + k) * sak] : 0.f;
+      if (sbk == 1) k = e % GK, r = e / GK;
+      else r = e % GT, k = e / GT;
+      const int gn = n0 + r;
+      Bs[k][r] = (k < kc && gn < N) ? B[gn * sbn + (long long)(k0 + k) * sbk] : 0.f;
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 32; kk += 4) {
-      const float a0 = As[kk + lk][wr * 32 + li], a1 = As[kk + lk][wr * 32 + 16 + li];
-      const float b0 = Bs[kk + lk][wc * 32 + li], b1 = Bs[kk + lk][wc * 32 + 16 + li];
-      acc00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc11, 0, 0, 0);
+    const int kr = (kc + 7) & ~7;
+    for (int kk = 0; kk < kr; kk += 8) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(As[kk + lk][br * 16 + li], Bs[kk + lk][bc * 16 + li], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(As[kk + 4 + lk][br * 16 + li], Bs[kk + 4 + lk][bc * 16 + li], acc1,
+                                                  0, 0, 0);
     }
     __syncthreads();
   }
   // C/D layout of the f32 16x16x4 form: col = lane & 15, row = 4 (lane >> 4) + reg
-  const f32x4 *accs[4] = {&acc00, &acc01, &acc10, &acc11};
+  const int col = n0 + bc * 16 + li;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int col = n0 + wc * 32 + (q & 1) * 16 + li;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int row = m0 + wr * 32 + (q >> 1) * 16 + lk * 4 + r;
-      if (row >= M || col >= N) continue;
-      float v = (*accs[q])[r];
-      if (EP == EP_BIAS_TANH) v = tanhf(v + bias[col]);
-      if (EP == EP_DTANH) {
-        const float y = T[row * ldt + col];
-        v = v * (1.0f - y * y);
-      }
-      C[row * ldc + col] = v;
+  for (int r = 0; r < 4; r++) {
+    const int row = m0 + br * 16 + lk * 4 + r;
+    if (row >= M || col >= N) continue;
+    float v = acc0[r] + acc1[r];
+    if (EP == EP_BIAS_TANH) v = tanhf(v + bias[col]);
+    if (EP == EP_DTANH) {
+      const float y = T[row * ldt + col];
+      v = v * (1.0f - y * y);
     }
+    C[row * ldc + col] = v;
   }
 }
 
@@ -238,21 +283,31 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
 
 // Weight gradients of a layer with a small dimension, and bias gradients:
 // dW[o][i] = sum_b G[b][o] Act[b][i] for i < Ni, db[o] = sum_b G[b][o]
-// (linear.cpp.base:337-350: summed over the batch, in batch order).
-__global__ void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
-                                 const float *__restrict__ Act, int lda, float *__restrict__ dW,
-                                 float *__restrict__ db) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= No * (Ni + 1)) return;
-  const int o = t / (Ni + 1), i = t % (Ni + 1);
+// (linear.cpp.base:337-350: summed over the batch).  One workgroup per
+// (o, column chunk): CW columns x (256 / CW) batch lanes, partial sums
+// reduced through LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
+                                                        const float *__restrict__ Act, int lda,
+                                                        float *__restrict__ dW, float *__restrict__ db, int CW) {
+  __shared__ float part[256];
+  const int o = blockIdx.x, t = threadIdx.x, lanes = 256 / CW, c = t % CW, l = t / CW;
+  const int i = blockIdx.y * CW + c;
   float acc = 0.f;
-  if (i < Ni) {
-    for (int b = 0; b < Bn; b++) acc += G[b * ldg + o] * Act[(long long)b * lda + i];
-    dW[o * Ni + i] = acc;
-  } else {
-    acc = G[o];
-    for (int b = 1; b < Bn; b++) acc += G[b * ldg + o];
-    db[o] = acc;
+  if (i <= Ni)
+#pragma unroll 4
+    for (int b = l; b < Bn; b += lanes) {
+      const float g = G[b * ldg + o];
+      acc += i < Ni ? g * Act[(long long)b * lda + i] : g;
+    }
+  part[t] = acc;
+  __syncthreads();
+  for (int w = lanes >> 1; w > 0; w >>= 1) {
+    if (l < w) part[t] += part[t + w * CW];
+    __syncthreads();
+  }
+  if (l == 0 && i <= Ni) {
+    if (i < Ni) dW[o * Ni + i] = part[c];
+    else db[o] = part[c];
   }
 }
 
@@ -385,11 +440,24 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
     float retV = 0.0f;
     if (er.term[pe] == TRUNCATED) retV = er.tv[pe];
     if (er.term[pe] == NON_TERMINAL) retV = er.ret[phys(st, P.R, end + 1)];
-    for (long long c = end; c >= start; c--) {
-      const long long pc = phys(st, P.R, c);
-      const float curV = er.v[pc];
-      retV = curV + er.tiw[pc] * (er.rew[pc] + P.gamma * retV - curV);
-      er.ret[pc] = retV;
+    // the chain's inputs are loaded 16 entries at a time ahead of the
+    // dependent recurrence (agent.cpp.base:717-733, same operation order)
+    for (long long c = end; c >= start;) {
+      const int n = (int)min(16ll, c - start + 1);
+      float vv[16], tw[16], rw[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (j < n) {
+          const long long pc = phys(st, P.R, c - j);
+          vv[j] = er.v[pc], tw[j] = er.tiw[pc], rw[j] = er.rew[pc];
+        }
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (j < n) {
+          retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
+          er.ret[phys(st, P.R, c - j)] = retV;
+        }
+      c -= n;
     }
   }
   __threadfence_block();
@@ -798,6 +866,16 @@ int vr_collect(kg_vracer_t h) {
   return 0;
 }
 
+template <int EP>
+void vr_gemm(kg_vracer_t h, int M, int N, int K, const float *A, long long sam, long long sak, const float *Bm,
+             long long sbn, long long sbk, float *C, long long ldc, const float *bias, const float *T, long long ldt) {
+  auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+  const bool vec = al(A) && al(Bm) && K % 4 == 0 && (sak == 1 ? sam % 4 == 0 : (sam == 1 && sak % 4 == 0)) &&
+                   (sbk == 1 ? sbn % 4 == 0 : (sbn == 1 && sbk % 4 == 0));
+  hipLaunchKernelGGL(k_vr_gemm<EP>, dim3(vr_blocks(N, GT), vr_blocks(M, GT)), dim3(256), 0, h->stream, M, N, K, A, sam,
+                     sak, Bm, sbn, sbk, C, ldc, bias, T, ldt, vec ? 1 : 0);
+}
+
 int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
   const Params &P = h->P;
   KG_CHECK((size_t)M <= h->rowsMax, "vracer: forward batch exceeds the allocated rows");
@@ -807,15 +885,22 @@ int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
   VrStage tg(h, M == P.E ? "gemm_rollout" : (M == 2 * P.B ? "gemm_update" : "gemm_other"));
   for (int l = 1; l < P.L; l++) {
     float *prev = h->acts + (size_t)(l - 1) * h->rowsMax * P.H, *cur = h->acts + (size_t)l * h->rowsMax * P.H;
-    hipLaunchKernelGGL(k_vr_gemm<EP_BIAS_TANH>, dim3(vr_blocks(P.H, 64), vr_blocks(M, 64)), dim3(256), 0, h->stream, M, P.H,
-                       P.H, prev, (long long)P.H, 1ll, h->theta + h->offW[l], (long long)P.H, 1ll, cur, (long long)P.H,
-                       h->theta + h->offb[l], (const float *)nullptr, 0ll);
+    vr_gemm<EP_BIAS_TANH>(h, M, P.H, P.H, prev, P.H, 1, h->theta + h->offW[l], P.H, 1, cur, P.H,
+                          h->theta + h->offb[l], nullptr, 0);
   }
   const float *last = h->acts + (size_t)(P.L - 1) * h->rowsMax * P.H;
-  hipLaunchKernelGGL(k_vr_fwd_out, dim3(vr_blocks((long long)M * P.O, 256)), dim3(256), 0, h->stream, M, P.H, P.O, last,
+  hipLaunchKernelGGL(k_vr_fwd_out, dim3(vr_blocks(M, 4)), dim3(256), 0, h->stream, M, P.H, P.O, last,
                      h->theta + h->offW[P.L], h->theta + h->offb[P.L], out, P);
   KG_HIP(hipGetLastError());
   return 0;
+}
+
+void vr_wgrad(kg_vracer_t h, int No, int Ni, int Bn, const float *G, int ldg, const float *Act, int lda, float *dW,
+              float *db) {
+  int cw = 1;
+  while (cw < Ni + 1 && cw < 16) cw <<= 1;  // >= 16 batch lanes: <= B/16 loads per thread
+  hipLaunchKernelGGL(k_vr_wgrad_small, dim3(No, vr_blocks(Ni + 1, cw)), dim3(256), 0, h->stream, No, Ni, Bn, G, ldg, Act,
+                     lda, dW, db, cw);
 }
 
 int vr_update(kg_vracer_t h, const unsigned *forced) {
@@ -833,27 +918,19 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   hipLaunchKernelGGL(k_vr_bwd_out, dim3(vr_blocks((long long)B * P.H, 256)), dim3(256), 0, h->stream, B, P.H, P.O,
                      (const float *)h->G, (const float *)h->out, (const float *)(h->theta + h->offW[P.L]), lastA, h->dZ,
                      h->dHa, P);
-  hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.O * (P.H + 1), 256)), dim3(256), 0, h->stream, P.O, P.H, B,
-                     (const float *)h->dZ, P.O, lastA, P.H, h->grad + h->offW[P.L], h->grad + h->offb[P.L]);
+  vr_wgrad(h, P.O, P.H, B, h->dZ, P.O, lastA, P.H, h->grad + h->offW[P.L], h->grad + h->offb[P.L]);
   float *dcur = h->dHa, *dnext = h->dHb;
   for (int l = P.L - 1; l >= 1; l--) {
     const float *ain = h->acts + (size_t)(l - 1) * rs;
     // dW_l[o][i] = sum_b dH[b][o] a_{l-1}[b][i]
-    hipLaunchKernelGGL(k_vr_gemm<EP_STORE>, dim3(vr_blocks(P.H, 64), vr_blocks(P.H, 64)), dim3(256), 0, h->stream, P.H, P.H,
-                       B, (const float *)dcur, 1ll, (long long)P.H, ain, 1ll, (long long)P.H, h->grad + h->offW[l],
-                       (long long)P.H, (const float *)nullptr, (const float *)nullptr, 0ll);
-    hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.H, 256)), dim3(256), 0, h->stream, P.H, 0, B,
-                       (const float *)dcur, P.H, ain, P.H, (float *)nullptr, h->grad + h->offb[l]);
+    vr_gemm<EP_STORE>(h, P.H, P.H, B, dcur, 1, P.H, ain, 1, P.H, h->grad + h->offW[l], P.H, nullptr, nullptr, 0);
+    vr_wgrad(h, P.H, 0, B, dcur, P.H, ain, P.H, nullptr, h->grad + h->offb[l]);
     // dH_{l-1} = (dH W_l) * (1 - a_{l-1}^2)
-    hipLaunchKernelGGL(k_vr_gemm<EP_DTANH>, dim3(vr_blocks(P.H, 64), vr_blocks(B, 64)), dim3(256), 0, h->stream, B, P.H,
-                       P.H, (const float *)dcur, (long long)P.H, 1ll, (const float *)(h->theta + h->offW[l]), 1ll,
-                       (long long)P.H, dnext, (long long)P.H, (const float *)nullptr, ain, (long long)P.H);
+    vr_gemm<EP_DTANH>(h, B, P.H, P.H, dcur, P.H, 1, h->theta + h->offW[l], 1, P.H, dnext, P.H, nullptr, ain, P.H);
     float *tmp = dcur;
     dcur = dnext, dnext = tmp;
   }
-  hipLaunchKernelGGL(k_vr_wgrad_small, dim3(vr_blocks(P.H * (P.S + 1), 256)), dim3(256), 0, h->stream, P.H, P.S, B,
-                     (const float *)dcur, P.H, (const float *)h->Xmb, P.S, h->grad + h->offW[0],
-                     h->grad + h->offb[0]);
+  vr_wgrad(h, P.H, P.S, B, dcur, P.H, h->Xmb, P.S, h->grad + h->offW[0], h->grad + h->offb[0]);
   hipLaunchKernelGGL(k_vr_adam, dim3(vr_blocks((long long)h->nparam, 256)), dim3(256), 0, h->stream,
                      (long long)h->nparam, h->theta, (const float *)h->grad, h->m1, h->m2, (const State *)h->st, P.l2,
                      P.l2imp);
