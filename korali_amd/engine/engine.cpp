@@ -26,6 +26,7 @@
 #include <fstream>
 #include <functional>
 #include <mutex>
+#include <random>
 #include <sstream>
 #include <thread>
 #include <sys/stat.h>
@@ -1183,6 +1184,260 @@ void saveState(Json &js, size_t gen) {
   }
 }
 
+// ------------------------------------------------------------- VRACER
+// Agent / Continuous / VRACER (agent.cpp.base, continuous.cpp.base,
+// VRACER.cpp.base) on the device (kg_vracer_*): the environment is the
+// device CartPole of examples/learning/reinforcement/cartpole, selected by
+// the extension key Problem/"Environment Kernel" (a host "Environment
+// Function" cannot run inside the device rollouts and fails loudly).
+const KeyList AGENT_KEYS = {
+    // agent.config Configuration Settings
+    "Mode", "Testing", "Training", "Concurrent Environments", "Episodes Per Generation", "Mini Batch",
+    "Time Sequence Length", "Learning Rate", "L2 Regularization", "Neural Network", "Discount Factor",
+    "Importance Weight Truncation Level", "Experience Replay", "Experiences Between Policy Updates",
+    "State Rescaling", "Reward", "Multi Agent Relationship", "Multi Agent Correlation", "Multi Agent Sampling",
+    // continuous.config / VRACER.config
+    "Policy", "Normal Generator", "Statistics",
+    // Internal Settings
+    "Action Lower Bounds", "Action Upper Bounds", "Current Episode", "Current Learning Rate", "Policy Update Count",
+    "Current Sample ID", "Uniform Generator", "Experience Count", "Experience Count Per Environment",
+    "Agent Count", "Action Shifts", "Action Scales"};
+const KeyList AGENT_TERMINATION = {"Max Episodes", "Max Experiences", "Max Policy Updates"};
+const KeyList RL_KEYS = {"Type", "Environment Function", "Environment Kernel", "Environment Count",
+                         "Actions Between Policy Updates", "Agents Per Environment", "Policies Per Environment",
+                         "Testing Frequency", "Policy Testing Episodes", "Custom Settings", "Max Episode Steps",
+                         "State Vector Size", "Action Vector Size", "State Vector Indexes", "Action Vector Indexes"};
+
+struct VracerModule : SolverModule {
+  kg_vracer_t h = nullptr;
+  double maxGenerations = 1e10;
+  unsigned long long maxEpisodes = 0, maxExperiences = 0, maxPolicyUpdates = 0, episodesPerGeneration = 1,
+                     averageDepth = 100;
+  unsigned long long sessionEpisodes = 0, sessionGeneration = 1;
+  std::vector<float> rewardHistory;
+  float lastReward = 0.f, bestReward = -INFINITY, averageReward = 0.f;
+  Json *solverJs = nullptr;
+
+  ~VracerModule() override {
+    if (h) kg_vracer_destroy(h);
+  }
+
+  VracerModule(Json &js, Seeder &seeds, bool resume) {
+    Json &sv = js["Solver"];
+    Json &pb = js["Problem"];
+    solverJs = &sv;
+    const std::string pt = canon(str(pb, "Type", ""));
+    if (pt != "reinforcementlearning/continuous")
+      fail("Solver VRACER requires a problem of type 'Reinforcement Learning / Continuous' (is '%s').",
+           pb["Type"].getString().c_str());
+    rejectUnrecognised(sv, "VRACER", {SOLVER_KEYS, AGENT_KEYS}, {SOLVER_TERMINATION, AGENT_TERMINATION});
+    rejectUnrecognised(pb, "Continuous", {RL_KEYS}, {});
+    if (resume) fail("Resuming a VRACER experiment is not supported by the device path.");
+    if (!pb.contains("Environment Kernel"))
+      fail("Problem 'Reinforcement Learning / Continuous' on the device needs 'Environment Kernel' (\"CartPole\": the "
+           "environment of examples/learning/reinforcement/cartpole); a host 'Environment Function' cannot run "
+           "inside the device rollouts.");
+    if (canon(pb["Environment Kernel"].getString()) != "cartpole")
+      fail("Unknown 'Environment Kernel' '%s' (the device provides \"CartPole\").",
+           pb["Environment Kernel"].getString().c_str());
+    if (uint(pb, "Agents Per Environment", 1) != 1) fail("'Agents Per Environment' > 1 is not supported by the device path.");
+    const unsigned long long envCount = uint(pb, "Environment Count", 1);
+    uint(pb, "Actions Between Policy Updates", 0);  // the device policy is always the current one
+    const unsigned long long maxSteps = uint(pb, "Max Episode Steps", 500);  // env.py maxSteps
+    // variables (reinforcementLearning.cpp.base:40-53; continuous.cpp.base:44-50)
+    size_t nState = 0, nAction = 0;
+    double noise = 0.0;
+    if (!js.contains("Variables") || js["Variables"].size() == 0) fail("No variables have been defined.");
+    for (size_t i = 0; i < js["Variables"].size(); i++) {
+      Json &v = js["Variables"][i];
+      const std::string t = canon(str(v, "Type", "State"));
+      if (t == "state") nState++;
+      else if (t == "action") {
+        nAction++;
+        noise = num(v, "Initial Exploration Noise", -1.0);
+        if (noise <= 0.0)
+          fail("Provided initial noise (%f) for action variable %zu is not defined or negative.\n", noise, i);
+        const double lb = num(v, "Lower Bound", -INFINITY), ub = num(v, "Upper Bound", INFINITY);
+        if (ub - lb <= 0.0) fail("Upper (%f) and Lower Bound (%f) of action variable %zu invalid.\n", ub, lb, i);
+      } else fail("Variable %zu: unknown Type '%s' (State or Action).", i, v["Type"].getString().c_str());
+    }
+    if (nAction == 0) fail("No action variables have been defined.\n");
+    if (nState == 0) fail("No state variables have been defined.\n");
+    if (nState != 4 || nAction != 1)
+      fail("The CartPole environment kernel has 4 state variables and 1 action variable (%zu / %zu given).", nState,
+           nAction);
+    if (canon(str(sv, "Mode", "Training")) != "training") fail("Only 'Mode' = 'Training' is supported by the device path.");
+    if (canon(str(sv["Policy"], "Distribution", "Normal")) != "normal")
+      fail("Policy Distribution '%s' is not supported by the device path (Normal).",
+           sv["Policy"]["Distribution"].getString().c_str());
+    if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
+    if (flag(sv["State Rescaling"], "Enabled", false)) fail("State Rescaling is not supported by the device path.");
+    if (flag(sv["Reward"]["Rescaling"], "Enabled", false)) fail("Reward Rescaling is not supported by the device path.");
+    if (flag(sv["Reward"]["Outbound Penalization"], "Enabled", false))
+      fail("Reward Outbound Penalization is not supported by the device path.");
+    Json &nn = sv["Neural Network"];
+    if (canon(str(nn, "Optimizer", "Adam")) != "adam")
+      fail("Neural Network Optimizer '%s' is not supported by the device path (Adam).", nn["Optimizer"].getString().c_str());
+    str(nn, "Engine", "Korali");
+    // hidden layers: [Layer/Linear (H), Layer/Activation (Elementwise/Tanh)] x L
+    if (!nn.contains("Hidden Layers") || nn["Hidden Layers"].size() == 0 || nn["Hidden Layers"].size() % 2)
+      fail("'Neural Network' / 'Hidden Layers' must be pairs of Layer/Linear and Layer/Activation (Elementwise/Tanh).");
+    size_t H = 0, L = nn["Hidden Layers"].size() / 2;
+    for (size_t l = 0; l < L; l++) {
+      Json &lin = nn["Hidden Layers"][2 * l];
+      Json &act = nn["Hidden Layers"][2 * l + 1];
+      if (canon(str(lin, "Type", "")) != "layer/linear" || canon(str(act, "Type", "")) != "layer/activation" ||
+          canon(str(act, "Function", "")) != "elementwise/tanh")
+        fail("Hidden layer pair %zu must be Layer/Linear followed by Layer/Activation with Elementwise/Tanh.", l);
+      const size_t oc = (size_t)uint(lin, "Output Channels", 0);
+      if (l == 0) H = oc;
+      if (oc != H || H == 0 || H % 64)
+        fail("Hidden layers must share one width that is a multiple of 64 on the device path (layer %zu: %zu).", l, oc);
+    }
+    Json &er = sv["Experience Replay"];
+    Json &op = er["Off Policy"];
+    kg_vracer_config c{};
+    c.state_size = 4, c.action_size = 1, c.hidden_size = H, c.hidden_layers = L;
+    c.environments = (size_t)uint(sv, "Concurrent Environments", 1);
+    c.environment_count = (size_t)envCount;
+    c.mini_batch_size = (size_t)uint(sv["Mini Batch"], "Size", 256);
+    str(sv["Mini Batch"], "Strategy", "Uniform");
+    size_t maxSize = (size_t)uint(er, "Maximum Size", 0), startSize = (size_t)uint(er, "Start Size", 0);
+    if (maxSize == 0) maxSize = (size_t)(std::pow(2, 14) * std::sqrt(4.0 + 1.0));  // agent.cpp.base:37-38
+    if (startSize == 0) startSize = maxSize;
+    er["Maximum Size"] = (unsigned long long)maxSize, er["Start Size"] = (unsigned long long)startSize;
+    flag(er, "Serialize", true);
+    c.replay_maximum_size = maxSize, c.replay_start_size = startSize;
+    c.max_episode_steps = (size_t)maxSteps;
+    c.experiences_between_policy_updates = mandatory(sv, "Experiences Between Policy Updates", "VRACER");
+    c.discount_factor = num(sv, "Discount Factor", 0.995);
+    c.learning_rate = mandatory(sv, "Learning Rate", "VRACER");
+    c.importance_weight_truncation_level = num(sv, "Importance Weight Truncation Level", 1.0);
+    c.off_policy_cutoff_scale = num(op, "Cutoff Scale", 4.0);
+    c.off_policy_target = num(op, "Target", 0.1);
+    c.off_policy_annealing_rate = num(op, "Annealing Rate", 0.0);
+    c.off_policy_refer_beta = num(op, "REFER Beta", 0.3);
+    c.l2_regularization_enabled = flag(sv["L2 Regularization"], "Enabled", false) ? 1 : 0;
+    c.l2_regularization_importance = num(sv["L2 Regularization"], "Importance", 1e-4);
+    c.initial_exploration_noise = &noise;
+    c.seed = seeds.counter++;
+    c.device = 0;
+    episodesPerGeneration = uint(sv, "Episodes Per Generation", 1);
+    averageDepth = uint(sv["Training"], "Average Depth", 100);
+    Json &tc = sv["Termination Criteria"];
+    maxGenerations = num(tc, "Max Generations", 1e10);
+    maxEpisodes = uint(tc, "Max Episodes", 0);
+    maxExperiences = uint(tc, "Max Experiences", 0);
+    maxPolicyUpdates = uint(tc, "Max Policy Updates", 0);
+    check(kg_vracer_create(&c, &h));
+    // initial hyperparameters (linear.cpp.base:28-49): Xavier-scaled U(-1, 1)
+    // weights, zero biases, output layer Weight Scaling 0.001 (VRACER.cpp.base:38).
+    // The uniform stream is this build's (std::mt19937 seeded from the
+    // experiment's seed counter), not GSL's: initial weights are not pinned.
+    size_t n = 0;
+    check(kg_vracer_hyperparameter_count(h, &n));
+    std::vector<float> theta(n);
+    std::mt19937 mt((unsigned)seeds.counter++);
+    std::uniform_real_distribution<float> U(-1.0f, 1.0f);
+    std::vector<size_t> sizes{4};
+    for (size_t l = 0; l < L; l++) sizes.push_back(H);
+    sizes.push_back(3);
+    size_t k = 0;
+    for (size_t l = 0; l + 1 < sizes.size(); l++) {
+      const size_t ic = sizes[l], oc = sizes[l + 1];
+      const float scale = l + 2 == sizes.size() ? 0.001f : 1.0f;
+      const float xav = std::sqrt(6.0f) / std::sqrt((float)(oc + ic));
+      for (size_t i = 0; i < ic * oc; i++) theta[k++] = scale * xav * U(mt);
+      for (size_t i = 0; i < oc; i++) theta[k++] = 0.0f;
+    }
+    if (sv["Training"].contains("Current Policy") && sv["Training"]["Current Policy"].contains("Policy") &&
+        sv["Training"]["Current Policy"]["Policy"].size() == n) {
+      auto v = flatten(sv["Training"]["Current Policy"]["Policy"]);
+      for (size_t i = 0; i < n; i++) theta[i] = (float)v[i];
+    }
+    check(kg_vracer_set_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
+  }
+
+  double scalar(const char *name) {
+    double v = 0.0;
+    check(kg_vracer_get_scalar(h, name, &v));
+    return v;
+  }
+
+  // Agent::trainingGeneration (agent.cpp.base:162-265)
+  void runGeneration(size_t) override {
+    while (sessionEpisodes < episodesPerGeneration * sessionGeneration) {
+      size_t added = 0, updates = 0;
+      check(kg_vracer_training_step(h, &added, &updates));
+      const size_t finished = (size_t)scalar("step_episodes");
+      if (finished) {
+        std::vector<float> r(finished);
+        check(kg_vracer_get_field(h, "finished_rewards", r.data(), finished * sizeof(float)));
+        for (float x : r) {
+          rewardHistory.push_back(x);
+          lastReward = x;
+          bestReward = std::max(bestReward, x);
+        }
+        sessionEpisodes += finished;
+      }
+    }
+    const size_t n = rewardHistory.size(), d = (size_t)std::min<unsigned long long>(averageDepth, n);
+    averageReward = 0.f;
+    for (size_t i = n - d; i < n; i++) averageReward += rewardHistory[i];
+    if (d) averageReward /= (float)d;
+    sessionGeneration++;
+  }
+
+  void checkTermination(size_t gen, std::vector<std::string> &met) override {
+    if ((double)gen > maxGenerations) met.push_back("Max Generations");
+    if (gen == 1) return;
+    if (maxEpisodes > 0 && scalar("current_episode") >= (double)maxEpisodes) met.push_back("Max Episodes");
+    if (maxExperiences > 0 && scalar("experience_count") >= (double)maxExperiences) met.push_back("Max Experiences");
+    if (maxPolicyUpdates > 0 && scalar("policy_update_count") >= (double)maxPolicyUpdates)
+      met.push_back("Max Policy Updates");
+  }
+
+  void getConfiguration(Json &sv) override {
+    sv["Current Episode"] = (unsigned long long)scalar("current_episode");
+    sv["Experience Count"] = (unsigned long long)scalar("experience_count");
+    sv["Policy Update Count"] = (unsigned long long)scalar("policy_update_count");
+    sv["Current Learning Rate"] = scalar("learning_rate");
+    sv["Experience Replay"]["Off Policy"]["Count"] = (unsigned long long)scalar("off_policy_count");
+    sv["Experience Replay"]["Off Policy"]["Ratio"] = scalar("off_policy_ratio");
+    sv["Experience Replay"]["Off Policy"]["Current Cutoff"] = scalar("off_policy_cutoff");
+    sv["Experience Replay"]["Off Policy"]["REFER Beta"] = scalar("refer_beta");
+    sv["Training"]["Reward History"] = std::vector<double>(rewardHistory.begin(), rewardHistory.end());
+    sv["Training"]["Average Reward"] = (double)averageReward;
+    sv["Training"]["Last Reward"] = (double)lastReward;
+    sv["Training"]["Best Reward"] = (double)bestReward;
+    size_t n = 0;
+    check(kg_vracer_hyperparameter_count(h, &n));
+    std::vector<float> theta(n);
+    check(kg_vracer_get_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
+    sv["Training"]["Current Policy"]["Policy"] = std::vector<double>(theta.begin(), theta.end());
+  }
+
+  void finalize(Json &) override {}
+
+  void printAfter(const Logger &log) override {
+    log.log(2, "Experience Replay Statistics:\n");
+    log.log(2, " + Experience Memory Size:      %.0f/%.0f\n", scalar("size"),
+            (*solverJs)["Experience Replay"]["Maximum Size"].getDouble());
+    log.log(2, " + Total Episodes Count:        %.0f\n", scalar("current_episode"));
+    log.log(2, " + Total Experience Count:      %.0f\n", scalar("experience_count"));
+    log.log(2, "Off-Policy Statistics:\n");
+    log.log(2, " + Count (Ratio/Target):        %.0f (%.3f)\n", scalar("off_policy_count"), scalar("off_policy_ratio"));
+    log.log(2, " + REFER Beta Factor:           %f\n", scalar("refer_beta"));
+    log.log(2, "Training Statistics:\n");
+    log.log(2, " + Policy Update Count:         %.0f\n", scalar("policy_update_count"));
+    log.log(2, " + Latest Reward:               %f\n", lastReward);
+    log.log(2, " + %zu-Episode Average Reward:  %f\n", (size_t)averageDepth, averageReward);
+    log.log(2, " + Best Reward:                 %f\n", bestReward);
+  }
+
+  std::string type() const override { return "Agent/Continuous/VRACER"; }
+};
+
 void runExperiment(Experiment &e, Conduit &conduit) {
   Json &js = e._js;
   ExperimentState &st = *e._state;
@@ -1233,8 +1488,11 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   } else if (stype == "sampler/tmcmc" || stype == "tmcmc") {
     tm = new TmcmcModule(js, seeds, distSeeds, distStates, resume);
     st.solver.reset(tm);
+  } else if (stype == "agent/continuous/vracer" || stype == "vracer") {
+    st.solver.reset(new VracerModule(js, seeds, resume));
   } else {
-    fail("Unrecognized solver type '%s' (the device path provides Optimizer/CMAES and Sampler/TMCMC).",
+    fail("Unrecognized solver type '%s' (the device path provides Optimizer/CMAES, Sampler/TMCMC and "
+         "Agent/Continuous/VRACER).",
          sv["Type"].getString().c_str());
   }
   js["Random Seed"] = seeds.counter;

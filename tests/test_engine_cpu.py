@@ -171,3 +171,31 @@ def test_conduit_batch_raises_lowest_failing_sample():
 
     with pytest.raises(ValueError, match="sample 40"):
         libkorali._conduit_evaluate(4, 100, body)
+
+
+# ------------------------------------------------- VRACER configuration
+from vracer_cases import cartpole_vracer  # noqa: E402
+
+
+@pytest.mark.parametrize("edit,msg", [
+    (lambda e: e["Solver"].__setitem__("Mini Batch Sise", 3), "Unrecognized settings"),
+    (lambda e: e["Problem"].__setitem__("Environment Kernel", "Pendulum"), "Unknown 'Environment Kernel'"),
+    (lambda e: e["Variables"][4].__setitem__("Initial Exploration Noise", -1.0), "initial noise"),
+    (lambda e: e["Solver"]["Policy"].__setitem__("Distribution", "Clipped Normal"), "Policy Distribution"),
+    (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][2].__setitem__("Output Channels", 96), "multiple of 64"),
+    (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][1].__setitem__("Function", "Elementwise/ReLU"),
+     "Elementwise/Tanh"),
+    (lambda e: e["Solver"]["State Rescaling"].__setitem__("Enabled", True), "State Rescaling"),
+    (lambda e: e["Solver"]["Neural Network"].__setitem__("Optimizer", "RMSProp"), "Adam"),
+])
+def test_vracer_configuration_errors_before_device(edit, msg):
+    e = cartpole_vracer()
+    edit(e)
+    with pytest.raises(korali.KoraliError, match=msg):
+        korali.Engine().run(e)
+
+
+def test_vracer_needs_device_environment():
+    e = cartpole_vracer(kernel=None)
+    with pytest.raises(korali.KoraliError, match="Environment Kernel"):
+        korali.Engine().run(e)

@@ -619,3 +619,21 @@ def test_cmaes_gradient_information_through_the_api():
         korali.Engine().run(experiment(short_gradient))
     with pytest.raises(Exception, match="Gradient Step Size must be larger than 0.0"):
         korali.Engine().run(experiment(sphere, step=0.0))
+
+
+def test_vracer_cartpole_through_korali_engine():
+    """examples/learning/reinforcement/cartpole/run-vracer.py's configuration
+    (Normal policy, device CartPole kernel) through korali.Engine: generations
+    of 10 episodes, policy updates once 1000 experiences are stored, the
+    solver state written back (counters, reward history, current policy)."""
+    import korali
+    from vracer_cases import cartpole_vracer
+    e = cartpole_vracer(max_generations=30, environments=64, hidden=64)
+    korali.Engine().run(e)
+    sv = e["Solver"]
+    assert sv["Current Episode"] >= 290
+    assert sv["Experience Count"] >= 1000 and sv["Policy Update Count"] > 0
+    hist = np.array(sv["Training"]["Reward History"])
+    assert hist.size == sv["Current Episode"] and np.all(np.isfinite(hist))
+    assert len(sv["Training"]["Current Policy"]["Policy"]) == (4 * 64 + 64) + (64 * 64 + 64) + (64 * 3 + 3)
+    assert np.isfinite(sv["Training"]["Average Reward"])
