@@ -371,9 +371,12 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
       }
       __syncthreads();
     }
+  const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
   for (int i = t; i < B * P.S; i += nt) {
     const int b = i / P.S, k = i % P.S;
-    const long long p = phys(st, P.R, key[b]);
+    unsigned long long q = base + key[b];
+    if (q >= R) q -= R;
+    const long long p = (long long)q;
     X[(long long)b * P.S + k] = er.st[p * P.S + k];
     X[(long long)(B + b) * P.S + k] = er.tst[p * P.S + k];
   }
@@ -388,14 +391,24 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
 __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                   const float *__restrict__ out, float *__restrict__ G) {
   __shared__ int s_delta;
+  __shared__ unsigned s_mb[MAXB + 1];
   const int t = threadIdx.x, nt = blockDim.x, B = P.B, A = P.A, O = P.O;
+  // every scalar read once into registers: the replay stores below may alias
+  // the state struct for the compiler, which would otherwise reload it per use
   const float cutoff = st->cutoff, beta = st->beta;
+  const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+  auto ph = [&](long long i) -> long long {
+    unsigned long long q = base + (unsigned long long)i;
+    if (q >= R) q -= R;
+    return (long long)q;
+  };
   if (t == 0) s_delta = 0;
+  for (int b = t; b < B; b += nt) s_mb[b] = mb[b];
   __syncthreads();
   int delta = 0;
   for (int b = t; b < B; b += nt) {
-    if (b > 0 && mb[b] == mb[b - 1]) continue;
-    const long long p = phys(st, P.R, mb[b]);
+    if (b > 0 && s_mb[b] == s_mb[b - 1]) continue;
+    const long long p = ph(s_mb[b]);
     const float *cur = out + (long long)b * O + 1;
     float lc = 0.f, lo = 0.f;
     for (int i = 0; i < A; i++) {
@@ -432,14 +445,14 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
   }
   // retrace chains of the oldest mini-batch entries of each episode
   for (int b = t; b < B; b += nt) {
-    const long long pe = phys(st, P.R, mb[b]);
-    if (b < B - 1 && er.ep_id[pe] == er.ep_id[phys(st, P.R, mb[b + 1])]) continue;
-    const long long end = mb[b];
+    const long long pe = ph(s_mb[b]);
+    if (b < B - 1 && er.ep_id[pe] == er.ep_id[ph(s_mb[b + 1])]) continue;
+    const long long end = s_mb[b];
     long long start = end - er.ep_pos[pe];
     if (start < 0) start = 0;
     float retV = 0.0f;
     if (er.term[pe] == TRUNCATED) retV = er.tv[pe];
-    if (er.term[pe] == NON_TERMINAL) retV = er.ret[phys(st, P.R, end + 1)];
+    if (er.term[pe] == NON_TERMINAL) retV = er.ret[ph(end + 1)];
     // the chain's inputs are loaded 16 entries at a time ahead of the
     // dependent recurrence (agent.cpp.base:717-733, same operation order)
     for (long long c = end; c >= start;) {
@@ -448,14 +461,14 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
 #pragma unroll
       for (int j = 0; j < 16; j++)
         if (j < n) {
-          const long long pc = phys(st, P.R, c - j);
+          const long long pc = ph(c - j);
           vv[j] = er.v[pc], tw[j] = er.tiw[pc], rw[j] = er.rew[pc];
         }
 #pragma unroll
       for (int j = 0; j < 16; j++)
         if (j < n) {
           retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
-          er.ret[phys(st, P.R, c - j)] = retV;
+          er.ret[ph(c - j)] = retV;
         }
       c -= n;
     }
@@ -463,7 +476,7 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
   __threadfence_block();
   __syncthreads();
   for (int b = t; b < B; b += nt) {
-    const long long p = phys(st, P.R, mb[b]);
+    const long long p = ph(s_mb[b]);
     const float V = er.v[p];
     const float *cur = er.cur_pol + p * 2 * A, *old = er.exp_pol + p * 2 * A;
     float g[MAXO];
@@ -471,7 +484,7 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
     for (int i = 1; i < O; i++) g[i] = 0.f;
     if (er.onp[p]) {
       float q = er.rew[p];
-      if (er.term[p] == NON_TERMINAL) q += P.gamma * er.ret[phys(st, P.R, (long long)mb[b] + 1)];
+      if (er.term[p] == NON_TERMINAL) q += P.gamma * er.ret[ph((long long)s_mb[b] + 1)];
       if (er.term[p] == TRUNCATED) q += P.gamma * er.tv[p];
       const float loss = q - V;
       float pg[2 * MAXA];
@@ -699,7 +712,8 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
   const int t = threadIdx.x, nt = blockDim.x, S = P.S, A = P.A;
   const int len = ev.len[e], rank = ev.rank[e];
   const long long off = ev.off[e];
-  const unsigned long long base = st->step_base, nnew = st->step_new;
+  const unsigned long long base = st->step_base, nnew = st->step_new, ep0 = st->step_episode_base,
+                           neps = st->step_episodes, sid0 = st->step_sample_base;
   const long long R = P.R;
   for (int k = t; k < len; k += nt) {
     const long long j = off + k;
@@ -725,7 +739,7 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     er.tiw[p] = 1.f;
     er.tv[p] = 0.f;
     er.onp[p] = 1;
-    er.ep_id[p] = (long long)(st->step_episode_base + rank);
+    er.ep_id[p] = (long long)(ep0 + rank);
     er.ep_pos[p] = k;
   }
   __syncthreads();
@@ -736,7 +750,7 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     const long long endj = off + len - 1;
     // the next finished episode (rank + 1) rewrites our last entry when it has one experience
     bool own_end = true;
-    if ((unsigned long long)(rank + 1) < st->step_episodes && ev.len[ev.fin_env[rank + 1]] == 1) own_end = false;
+    if ((unsigned long long)(rank + 1) < neps && ev.len[ev.fin_env[rank + 1]] == 1) own_end = false;
     retV = P.gamma * retV + ev.eb_rew[(long long)e * P.T + len - 1];
     if (own_end) er.ret[((long long)base + endj) % R] = retV;
     const long long prevj = endj - 1;
@@ -753,7 +767,7 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     ev.rewards[rank] = ev.cum[e];
     atomicAdd(&st->step_reward_sum, (double)ev.cum[e]);
     // reset for the next launch (env.py: cart.reset(sampleId * 1024 + launchId))
-    const unsigned long long sid = st->step_sample_base + (unsigned long long)rank + (unsigned long long)P.E;
+    const unsigned long long sid = sid0 + (unsigned long long)rank + (unsigned long long)P.E;
     double u[4];
     cp_reset((unsigned)(sid * 1024ull + sid), u);
     for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = (float)u[q];
