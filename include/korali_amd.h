@@ -330,6 +330,8 @@ typedef struct {
   const double *initial_exploration_noise; /* action_size values */
   uint64_t seed;                           /* action-noise / mini-batch stream key */
   int device;
+  int policy_distribution;                 /* Policy / Distribution: 0 Normal, 1 Clipped Normal */
+  const double *action_lower_bounds, *action_upper_bounds;  /* action_size values (may be NULL for Normal) */
 } kg_vracer_config;
 
 int kg_vracer_create(const kg_vracer_config *cfg, kg_vracer_t *out);

@@ -70,6 +70,8 @@ struct Params {  // launch-constant configuration
   float scale[MAXO], shift[MAXO];
   int soft[MAXO];
   unsigned long long seed;
+  int clipped;                    // Policy Distribution: 0 Normal, 1 Clipped Normal
+  float lb[MAXA], ub[MAXA];       // action bounds (Variables' Lower / Upper Bound)
 };
 
 // ---------------------------------------------------------------- philox
@@ -109,6 +111,31 @@ __device__ inline float normal_logp(float x, float mean, float sigma) {
   const float norm = (float)(-0.5 * log(2.0 * M_PI * (double)sigma * (double)sigma));
   const float d = (float)((double)(x - mean) / ((double)sigma + 0.00000000001));
   return (float)((double)norm - 0.5 * (double)d * (double)d);
+}
+
+// Clipped Normal pieces (auxiliar/math.hpp:297-328, T = float): z is rounded
+// to float, log(0.5) + log erfc in double.  GSL's gsl_sf_log_erfc is
+// restated as log(erfc(x)) with the asymptotic series where erfc underflows.
+__device__ inline double log_erfc_d(double x) {
+  if (x < 26.0) return log(erfc(x));
+  const double x2 = x * x, h = 1.0 / (2.0 * x2);
+  return -x2 - log(x) - 0.57236494292470008707 + log(1.0 - h + 3.0 * h * h - 15.0 * h * h * h);
+}
+__device__ inline float normal_logcdf(float x, float mean, float sigma) {
+  const float z = (float)((double)(x - mean) / ((double)sigma * M_SQRT2));
+  return (float)(log(0.5) + log_erfc_d(-(double)z));
+}
+__device__ inline float normal_logccdf(float x, float mean, float sigma) {
+  const float z = (float)((double)(x - mean) / ((double)sigma * M_SQRT2));
+  return (float)(log(0.5) + log_erfc_d((double)z));
+}
+// log-density of one action component (continuous.cpp.base:283-340)
+__device__ inline float policy_logp(const Params &P, int i, float a, float m, float s) {
+  if (P.clipped) {
+    if (a <= P.lb[i]) return normal_logcdf(P.lb[i], m, s);
+    if (P.ub[i] <= a) return normal_logccdf(P.ub[i], m, s);
+  }
+  return normal_logp(a, m, s);
 }
 
 // ------------------------------------------------------------ layer kernels
@@ -413,8 +440,8 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
     float lc = 0.f, lo = 0.f;
     for (int i = 0; i < A; i++) {
       const float a = er.act[p * A + i];
-      lc += normal_logp(a, cur[i], cur[A + i]);
-      lo += normal_logp(a, er.exp_pol[p * 2 * A + i], er.exp_pol[p * 2 * A + A + i]);
+      lc += policy_logp(P, i, a, cur[i], cur[A + i]);
+      lo += policy_logp(P, i, a, er.exp_pol[p * 2 * A + i], er.exp_pol[p * 2 * A + A + i]);
     }
     float liw = lc - lo;
     if (liw > 7.f) liw = 7.f;
@@ -492,11 +519,36 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
       for (int i = 0; i < A; i++) {
         const float a = er.act[p * A + i], cm = cur[i], cs = cur[A + i];
         const float dif = a - cm;
-        const float inv_var = 1.f / (cs * cs);
-        pg[i] = dif * inv_var;
-        pg[A + i] = (dif * dif) * (inv_var / cs) - 1.f / cs;
-        lc += normal_logp(a, cm, cs);
-        lo += normal_logp(a, old[i], old[A + i]);
+        if (!P.clipped) {  // continuous.cpp.base:404-440
+          const float inv_var = 1.f / (cs * cs);
+          pg[i] = dif * inv_var;
+          pg[A + i] = (dif * dif) * (inv_var / cs) - 1.f / cs;
+          lc += normal_logp(a, cm, cs);
+          lo += normal_logp(a, old[i], old[A + i]);
+        } else {  // continuous.cpp.base:482-560
+          const float inv_sig = 1.f / cs;
+          if (a <= P.lb[i]) {
+            const float lcdf = normal_logcdf(P.lb[i], cm, cs);
+            const float r = expf(normal_logp(P.lb[i], cm, cs) - lcdf);
+            pg[i] = -r;
+            pg[A + i] = -dif * inv_sig * r;
+            lc += lcdf;
+            lo += normal_logcdf(P.lb[i], old[i], old[A + i]);
+          } else if (P.ub[i] <= a) {
+            const float lccdf = normal_logccdf(P.ub[i], cm, cs);
+            const float r = expf(normal_logp(P.ub[i], cm, cs) - lccdf);
+            pg[i] = r;
+            pg[A + i] = dif * inv_sig * r;
+            lc += lccdf;
+            lo += normal_logccdf(P.ub[i], old[i], old[A + i]);
+          } else {
+            const float inv_sig3 = inv_sig * inv_sig * inv_sig;
+            pg[i] = dif * inv_sig * inv_sig;
+            pg[A + i] = dif * dif * inv_sig3 - inv_sig;
+            lc += normal_logp(a, cm, cs);
+            lo += normal_logp(a, old[i], old[A + i]);
+          }
+        }
       }
       const float iwg = expf(lc - lo);
       for (int i = 0; i < 2 * A; i++) g[1 + i] = beta * loss * (pg[i] * iwg);
@@ -508,8 +560,29 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
       const float inv_var = (float)(1. / (double)(cs * cs));
       const float inv_sig3 = (float)(1. / (double)(cs * cs * cs));
       const float d = cm - om;
-      const float kl_mean = d * inv_var;
-      const float kl_sig = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
+      float kl_mean = d * inv_var;
+      float kl_sig = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
+      if (P.clipped) {  // continuous.cpp.base:734-777
+        const float lb = P.lb[i], ub = P.ub[i];
+        const float oldVar = osd * osd, oldInvSig = 1.f / osd, curInvSig = 1.f / cs;
+        const float curInvVar = 1.f / (cs * cs), curInvSig3 = 1.f / (cs * cs * cs), muDif = om - cm;
+        const float invSqrt2Pi = (float)(M_SQRT1_2 * sqrt(M_1_PI));
+        const float oldAdjLb = (lb - om) * oldInvSig, oldAdjUb = (ub - om) * oldInvSig;
+        const float curAdjLb = (lb - cm) * curInvSig, curAdjUb = (ub - cm) * curInvSig;
+        const float erfLb = (float)erf(M_SQRT1_2 * (double)oldAdjLb), erfUb = (float)erf(M_SQRT1_2 * (double)oldAdjUb);
+        const float expLb = expf(-0.5f * oldAdjLb * oldAdjLb), expUb = expf(-0.5f * oldAdjUb * oldAdjUb);
+        const float cdfA = expf(normal_logcdf(lb, om, osd) + normal_logp(lb, cm, cs) - normal_logcdf(lb, cm, cs));
+        const float ccdfB = expf(normal_logccdf(ub, om, osd) + normal_logp(ub, cm, cs) - normal_logccdf(ub, cm, cs));
+        kl_mean = cdfA;
+        kl_mean -= 0.5f * muDif * curInvVar * (erfUb - erfLb);
+        kl_mean += invSqrt2Pi * osd * curInvVar * (expUb - expLb);
+        kl_mean -= ccdfB;
+        kl_sig = curAdjLb * cdfA;
+        kl_sig += 0.5f * (curInvSig - muDif * muDif * curInvSig3 - oldVar * curInvSig3) * (erfUb - erfLb);
+        kl_sig += invSqrt2Pi * curInvSig3 * (oldVar * oldAdjUb + 2.f * osd * muDif) * expUb;
+        kl_sig -= invSqrt2Pi * curInvSig3 * (oldVar * oldAdjLb + 2.f * osd * muDif) * expLb;
+        kl_sig -= curAdjUb * ccdfB;
+      }
       g[1 + i] += klm * kl_mean;
       g[1 + A + i] += klm * kl_sig;
     }
@@ -624,6 +697,11 @@ __global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restri
     act[i] = out[(long long)e * O + 1 + i] + out[(long long)e * O + 1 + A + i] * n0;
     if (i + 1 < A) act[i + 1] = out[(long long)e * O + 2 + i] + out[(long long)e * O + 2 + A + i] * n1;
   }
+  if (P.clipped)  // continuous.cpp.base:172-183
+    for (int i = 0; i < A; i++) {
+      if (act[i] >= P.ub[i]) act[i] = P.ub[i];
+      if (act[i] <= P.lb[i]) act[i] = P.lb[i];
+    }
   for (int k = 0; k < S; k++) ev.eb_st[slot * S + k] = X[(long long)e * S + k];
   for (int i = 0; i < A; i++) ev.eb_act[slot * A + i] = act[i];
   for (int i = 0; i < 2 * A; i++) ev.eb_pol[slot * 2 * A + i] = out[(long long)e * O + 1 + i];
@@ -1024,6 +1102,13 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   for (size_t i = 0; i < c->action_size; i++)
     KG_CHECK(c->initial_exploration_noise && c->initial_exploration_noise[i] > 0.0,
              "Provided initial noise for an action variable is not defined or negative.");
+  KG_CHECK(c->policy_distribution == 0 || c->policy_distribution == 1,
+           "vracer: policy distribution must be 0 (Normal) or 1 (Clipped Normal)");
+  if (c->policy_distribution == 1)
+    for (size_t i = 0; i < c->action_size; i++)
+      KG_CHECK(c->action_lower_bounds && c->action_upper_bounds && std::isfinite(c->action_lower_bounds[i]) &&
+                   std::isfinite(c->action_upper_bounds[i]),
+               "Provided bound for an action variable is non-finite, but the distribution (Clipped Normal) is bounded.");
   KG_HIP(hipSetDevice(c->device));
   auto *h = new kg_vracer_s();
   Params &P = h->P;
@@ -1037,9 +1122,14 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.anneal = (float)c->off_policy_annealing_rate, P.l2imp = (float)c->l2_regularization_importance;
   P.seed = c->seed;
   for (int o = 0; o < MAXO; o++) P.scale[o] = 1.f, P.shift[o] = 0.f, P.soft[o] = 0;
+  P.clipped = c->policy_distribution == 1 ? 1 : 0;
   for (int i = 0; i < P.A; i++) {
     P.scale[1 + P.A + i] = 2.0f * (float)c->initial_exploration_noise[i];
     P.soft[1 + P.A + i] = 1;
+    P.lb[i] = c->action_lower_bounds ? (float)c->action_lower_bounds[i] : -INFINITY;
+    P.ub[i] = c->action_upper_bounds ? (float)c->action_upper_bounds[i] : INFINITY;
+    // bounded distributions shift the means by the action shift (continuous.cpp.base:20-30, :53-54)
+    if (P.clipped) P.shift[1 + i] = (P.ub[i] + P.lb[i]) * 0.5f;
   }
   h->device = c->device;
   h->ebpu = c->experiences_between_policy_updates;

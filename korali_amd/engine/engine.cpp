@@ -1246,7 +1246,7 @@ struct VracerModule : SolverModule {
     const unsigned long long maxSteps = uint(pb, "Max Episode Steps", 500);  // env.py maxSteps
     // variables (reinforcementLearning.cpp.base:40-53; continuous.cpp.base:44-50)
     size_t nState = 0, nAction = 0;
-    double noise = 0.0;
+    double noise = 0.0, actLb = -INFINITY, actUb = INFINITY;
     if (!js.contains("Variables") || js["Variables"].size() == 0) fail("No variables have been defined.");
     for (size_t i = 0; i < js["Variables"].size(); i++) {
       Json &v = js["Variables"][i];
@@ -1259,6 +1259,7 @@ struct VracerModule : SolverModule {
           fail("Provided initial noise (%f) for action variable %zu is not defined or negative.\n", noise, i);
         const double lb = num(v, "Lower Bound", -INFINITY), ub = num(v, "Upper Bound", INFINITY);
         if (ub - lb <= 0.0) fail("Upper (%f) and Lower Bound (%f) of action variable %zu invalid.\n", ub, lb, i);
+        actLb = lb, actUb = ub;
       } else fail("Variable %zu: unknown Type '%s' (State or Action).", i, v["Type"].getString().c_str());
     }
     if (nAction == 0) fail("No action variables have been defined.\n");
@@ -1267,9 +1268,13 @@ struct VracerModule : SolverModule {
       fail("The CartPole environment kernel has 4 state variables and 1 action variable (%zu / %zu given).", nState,
            nAction);
     if (canon(str(sv, "Mode", "Training")) != "training") fail("Only 'Mode' = 'Training' is supported by the device path.");
-    if (canon(str(sv["Policy"], "Distribution", "Normal")) != "normal")
-      fail("Policy Distribution '%s' is not supported by the device path (Normal).",
+    const std::string dist = canon(str(sv["Policy"], "Distribution", "Normal"));
+    if (dist != "normal" && dist != "clippednormal")
+      fail("Policy Distribution '%s' is not supported by the device path (Normal, Clipped Normal).",
            sv["Policy"]["Distribution"].getString().c_str());
+    if (dist == "clippednormal" && !(std::isfinite(actLb) && std::isfinite(actUb)))  // continuous.cpp.base:20-26
+      fail("Provided bounds (%f, %f) for the action variable are non-finite, but the distribution (%s) is bounded.\n",
+           actLb, actUb, sv["Policy"]["Distribution"].getString().c_str());
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
     if (flag(sv["State Rescaling"], "Enabled", false)) fail("State Rescaling is not supported by the device path.");
     if (flag(sv["Reward"]["Rescaling"], "Enabled", false)) fail("Reward Rescaling is not supported by the device path.");
@@ -1320,6 +1325,8 @@ struct VracerModule : SolverModule {
     c.l2_regularization_enabled = flag(sv["L2 Regularization"], "Enabled", false) ? 1 : 0;
     c.l2_regularization_importance = num(sv["L2 Regularization"], "Importance", 1e-4);
     c.initial_exploration_noise = &noise;
+    c.policy_distribution = dist == "clippednormal" ? 1 : 0;
+    c.action_lower_bounds = &actLb, c.action_upper_bounds = &actUb;
     c.seed = seeds.counter++;
     c.device = 0;
     episodesPerGeneration = uint(sv, "Episodes Per Generation", 1);

@@ -31,7 +31,8 @@ class _VracerCfg(C.Structure):
         ("off_policy_target", C.c_double), ("off_policy_annealing_rate", C.c_double),
         ("off_policy_refer_beta", C.c_double), ("l2_regularization_enabled", C.c_int),
         ("l2_regularization_importance", C.c_double), ("initial_exploration_noise", C.POINTER(C.c_double)),
-        ("seed", C.c_uint64), ("device", C.c_int),
+        ("seed", C.c_uint64), ("device", C.c_int), ("policy_distribution", C.c_int),
+        ("action_lower_bounds", C.POINTER(C.c_double)), ("action_upper_bounds", C.POINTER(C.c_double)),
     ]
 
 
@@ -80,19 +81,27 @@ class VracerDevice:
                  learning_rate=1e-4, importance_weight_truncation_level=1.0, off_policy_cutoff_scale=4.0,
                  off_policy_target=0.1, off_policy_annealing_rate=0.0, off_policy_refer_beta=0.3,
                  l2_regularization_enabled=False, l2_regularization_importance=1e-4, initial_exploration_noise=1.0,
-                 seed=0, device=0, hyperparameters=None):
+                 seed=0, device=0, hyperparameters=None, policy_distribution="Normal", action_lower_bound=-np.inf,
+                 action_upper_bound=np.inf):
         L = _lib()
         self.S, self.A, self.H, self.L = state_size, action_size, hidden_size, hidden_layers
         self.E, self.B, self.O = environments, mini_batch_size, 1 + 2 * action_size
         noise = np.ascontiguousarray(np.broadcast_to(np.asarray(initial_exploration_noise, np.float64),
                                                      (action_size,)))
         self._noise = noise
+        pol = {"normal": 0, "clippednormal": 1}.get(policy_distribution.replace(" ", "").lower())
+        if pol is None:
+            raise KoraliDeviceError(f"Policy Distribution '{policy_distribution}' is not supported on the device")
+        self._lb = np.ascontiguousarray(np.broadcast_to(np.asarray(action_lower_bound, np.float64), (action_size,)))
+        self._ub = np.ascontiguousarray(np.broadcast_to(np.asarray(action_upper_bound, np.float64), (action_size,)))
         cfg = _VracerCfg(state_size, action_size, hidden_size, hidden_layers, environments, environment_count,
                          mini_batch_size, replay_maximum_size, replay_start_size, max_episode_steps,
                          experiences_between_policy_updates, discount_factor, learning_rate,
                          importance_weight_truncation_level, off_policy_cutoff_scale, off_policy_target,
                          off_policy_annealing_rate, off_policy_refer_beta, int(bool(l2_regularization_enabled)),
-                         l2_regularization_importance, noise.ctypes.data_as(C.POINTER(C.c_double)), seed, device)
+                         l2_regularization_importance, noise.ctypes.data_as(C.POINTER(C.c_double)), seed, device,
+                         pol, self._lb.ctypes.data_as(C.POINTER(C.c_double)),
+                         self._ub.ctypes.data_as(C.POINTER(C.c_double)))
         h = C.c_void_p()
         check(L.kg_vracer_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -84,21 +84,23 @@ def unpack(theta, S, H, L, A):
     return layers
 
 
-def output_transform(A, initial_noise):
+def output_transform(A, initial_noise, mean_shift=None):
     """continuous.cpp.base:34-61 (Normal): [V | means | sigmas]; means Identity,
     scale 1, shift = action shift (0 for the unbounded Normal policy); sigmas
     Softplus with scale 2 * Initial Exploration Noise."""
     noise = np.broadcast_to(np.asarray(initial_noise, dtype=f32), (A,))
     scale = np.concatenate([[f32(1.0)], np.ones(A, f32), f32(2.0) * noise]).astype(f32)
     shift = np.zeros(1 + 2 * A, f32)
+    if mean_shift is not None:
+        shift[1:1 + A] = mean_shift
     soft = np.concatenate([[False], np.zeros(A, bool), np.ones(A, bool)])
     return scale, shift, soft
 
 
-def forward(theta, X, S, H, L, A, initial_noise):
+def forward(theta, X, S, H, L, A, initial_noise, mean_shift=None):
     """NeuralNetwork::forward of the critic/policy net; returns (out, acts)."""
     layers = unpack(theta, S, H, L, A)
-    scale, shift, soft = output_transform(A, initial_noise)
+    scale, shift, soft = output_transform(A, initial_noise, mean_shift)
     acts = [np.asarray(X, dtype=f32)]
     h = acts[0]
     for W, b in layers[:-1]:
@@ -112,11 +114,11 @@ def forward(theta, X, S, H, L, A, initial_noise):
     return out, acts
 
 
-def backward(theta, acts, out, G, S, H, L, A, initial_noise):
+def backward(theta, acts, out, G, S, H, L, A, initial_noise, mean_shift=None):
     """Output-layer gradient preprocessing (output.cpp.base:170-210), then the
     Linear/Tanh backward; returns the hyperparameter gradient vector."""
     layers = unpack(theta, S, H, L, A)
-    scale, shift, soft = output_transform(A, initial_noise)
+    scale, shift, soft = output_transform(A, initial_noise, mean_shift)
     x = ((out - shift) / scale).astype(f32)
     g = (np.asarray(G, f32) * scale).astype(f32)
     nnx = (x - f32(0.25) / x).astype(np.float64)
@@ -164,19 +166,57 @@ def normal_logp(x, mean, sigma):
     return (norm.astype(np.float64) - 0.5 * d.astype(np.float64) * d.astype(np.float64)).astype(f32)
 
 
-def importance_weight(action, cur, old, A):
-    """continuous.cpp.base:278-297, :385-397 (clamped log weight)."""
+def log_erfc(x):
+    """gsl_sf_log_erfc restated as log(erfc(x)), asymptotic series where erfc
+    underflows (GSL parity unpinned: GSL 2.6 is absent)."""
+    from scipy.special import erfc
+    x = float(x)
+    if x < 26.0:
+        return float(np.log(erfc(x)))
+    x2, h = x * x, 1.0 / (2.0 * x * x)
+    return -x2 - np.log(x) - 0.57236494292470008707 + np.log(1.0 - h + 3.0 * h * h - 15.0 * h * h * h)
+
+
+def normal_logcdf(x, mean, sigma):
+    """auxiliar/math.hpp:297-301 with T = float."""
+    z = f32((np.float64(f32(f32(x) - f32(mean)))) / (np.float64(f32(sigma)) * np.sqrt(2.0)))
+    return f32(np.log(0.5) + log_erfc(-np.float64(z)))
+
+
+def normal_logccdf(x, mean, sigma):
+    """auxiliar/math.hpp:324-328 with T = float."""
+    z = f32((np.float64(f32(f32(x) - f32(mean)))) / (np.float64(f32(sigma)) * np.sqrt(2.0)))
+    return f32(np.log(0.5) + log_erfc(np.float64(z)))
+
+
+def policy_logp(i, a, m, s, bounds):
+    """One action component's log-density (continuous.cpp.base:283-340);
+    bounds = None (Normal) or (lb, ub) arrays (Clipped Normal)."""
+    if bounds is not None:
+        lb, ub = f32(bounds[0][i]), f32(bounds[1][i])
+        if a <= lb:
+            return normal_logcdf(lb, m, s)
+        if ub <= a:
+            return normal_logccdf(ub, m, s)
+    return normal_logp(a, m, s)
+
+
+def importance_weight(action, cur, old, A, bounds=None):
+    """continuous.cpp.base:278-340, :385-397 (clamped log weight)."""
     lc, lo = f32(0.0), f32(0.0)
     for i in range(A):
-        lc = f32(lc + normal_logp(action[i], cur[i], cur[A + i]))
-        lo = f32(lo + normal_logp(action[i], old[i], old[A + i]))
+        lc = f32(lc + policy_logp(i, f32(action[i]), cur[i], cur[A + i], bounds))
+        lo = f32(lo + policy_logp(i, f32(action[i]), old[i], old[A + i], bounds))
     liw = f32(lc - lo)
     liw = min(max(liw, f32(-7.0)), f32(7.0))
     return f32(np.exp(liw))
 
 
-def importance_weight_gradient(action, cur, old, A):
-    """continuous.cpp.base:404-440 (Normal; the log weight is not clamped here)."""
+def importance_weight_gradient(action, cur, old, A, bounds=None):
+    """continuous.cpp.base:404-440 (Normal) and :482-560 (Clipped Normal); the
+    log weight is not clamped here."""
+    if bounds is not None:
+        return _clipped_iw_gradient(action, cur, old, A, bounds)
     g = np.zeros(2 * A, f32)
     lc, lo = f32(0.0), f32(0.0)
     for i in range(A):
@@ -191,8 +231,72 @@ def importance_weight_gradient(action, cur, old, A):
     return (g * iw).astype(f32)
 
 
-def kl_gradient(old, cur, A):
-    """continuous.cpp.base:697-732 (Normal)."""
+def _clipped_iw_gradient(action, cur, old, A, bounds):
+    g = np.zeros(2 * A, f32)
+    lc, lo = f32(0.0), f32(0.0)
+    for i in range(A):
+        a, m, s, om, os_ = f32(action[i]), f32(cur[i]), f32(cur[A + i]), f32(old[i]), f32(old[A + i])
+        lb, ub = f32(bounds[0][i]), f32(bounds[1][i])
+        inv_sig = f32(f32(1.0) / s)
+        dif = f32(a - m)
+        if a <= lb:
+            lcdf = normal_logcdf(lb, m, s)
+            r = f32(np.exp(f32(normal_logp(lb, m, s) - lcdf)))
+            g[i] = -r
+            g[A + i] = f32(f32(-dif * inv_sig) * r)
+            lc, lo = f32(lc + lcdf), f32(lo + normal_logcdf(lb, om, os_))
+        elif ub <= a:
+            lccdf = normal_logccdf(ub, m, s)
+            r = f32(np.exp(f32(normal_logp(ub, m, s) - lccdf)))
+            g[i] = r
+            g[A + i] = f32(f32(dif * inv_sig) * r)
+            lc, lo = f32(lc + lccdf), f32(lo + normal_logccdf(ub, om, os_))
+        else:
+            inv_sig3 = f32(f32(inv_sig * inv_sig) * inv_sig)
+            g[i] = f32(f32(dif * inv_sig) * inv_sig)
+            g[A + i] = f32(f32(f32(dif * dif) * inv_sig3) - inv_sig)
+            lc, lo = f32(lc + normal_logp(a, m, s)), f32(lo + normal_logp(a, om, os_))
+    iw = f32(np.exp(f32(lc - lo)))
+    return (g * iw).astype(f32)
+
+
+def clipped_kl_gradient(old, cur, A, bounds):
+    """continuous.cpp.base:734-777 (Clipped Normal)."""
+    from math import erf
+    g = np.zeros(2 * A, f32)
+    for i in range(A):
+        om, osd, cm, cs = f32(old[i]), f32(old[A + i]), f32(cur[i]), f32(cur[A + i])
+        lb, ub = f32(bounds[0][i]), f32(bounds[1][i])
+        old_var, old_inv_sig, cur_inv_sig = f32(osd * osd), f32(f32(1) / osd), f32(f32(1) / cs)
+        cur_inv_var, cur_inv_sig3 = f32(f32(1) / f32(cs * cs)), f32(f32(1) / f32(f32(cs * cs) * cs))
+        mu_dif = f32(om - cm)
+        inv_sqrt_2pi = f32(np.sqrt(0.5) * np.sqrt(1.0 / np.pi))
+        o_lb, o_ub = f32(f32(lb - om) * old_inv_sig), f32(f32(ub - om) * old_inv_sig)
+        c_lb, c_ub = f32(f32(lb - cm) * cur_inv_sig), f32(f32(ub - cm) * cur_inv_sig)
+        erf_lb, erf_ub = f32(erf(np.sqrt(0.5) * float(o_lb))), f32(erf(np.sqrt(0.5) * float(o_ub)))
+        exp_lb, exp_ub = f32(np.exp(f32(f32(f32(-0.5) * o_lb) * o_lb))), f32(np.exp(f32(f32(f32(-0.5) * o_ub) * o_ub)))
+        cdf_a = f32(np.exp(f32(f32(normal_logcdf(lb, om, osd) + normal_logp(lb, cm, cs)) - normal_logcdf(lb, cm, cs))))
+        ccdf_b = f32(np.exp(f32(f32(normal_logccdf(ub, om, osd) + normal_logp(ub, cm, cs)) - normal_logccdf(ub, cm, cs))))
+        km = cdf_a
+        km = f32(km - f32(f32(f32(f32(0.5) * mu_dif) * cur_inv_var) * f32(erf_ub - erf_lb)))
+        km = f32(km + f32(f32(f32(inv_sqrt_2pi * osd) * cur_inv_var) * f32(exp_ub - exp_lb)))
+        km = f32(km - ccdf_b)
+        ks = f32(c_lb * cdf_a)
+        ks = f32(ks + f32(f32(f32(0.5) * f32(f32(cur_inv_sig - f32(f32(mu_dif * mu_dif) * cur_inv_sig3)) -
+                                               f32(old_var * cur_inv_sig3))) * f32(erf_ub - erf_lb)))
+        ks = f32(ks + f32(f32(f32(inv_sqrt_2pi * cur_inv_sig3) * f32(f32(old_var * o_ub) + f32(f32(2) * osd * mu_dif)))
+                          * exp_ub))
+        ks = f32(ks - f32(f32(f32(inv_sqrt_2pi * cur_inv_sig3) * f32(f32(old_var * o_lb) + f32(f32(2) * osd * mu_dif)))
+                          * exp_lb))
+        ks = f32(ks - f32(c_ub * ccdf_b))
+        g[i], g[A + i] = km, ks
+    return g
+
+
+def kl_gradient(old, cur, A, bounds=None):
+    """continuous.cpp.base:697-732 (Normal); :734-777 for Clipped Normal."""
+    if bounds is not None:
+        return clipped_kl_gradient(old, cur, A, bounds)
     g = np.zeros(2 * A, f32)
     for i in range(A):
         om, osd, cm, cs = f32(old[i]), f32(old[A + i]), f32(cur[i]), f32(cur[A + i])
@@ -216,8 +320,11 @@ class Agent:
 
     def __init__(self, S, A, H=256, L=2, theta=None, *, max_size=4096, discount=0.995, learning_rate=1e-4,
                  iw_truncation=1.0, cutoff_scale=4.0, off_target=0.1, annealing_rate=0.0, refer_beta=0.3,
-                 initial_noise=1.0, l2_enabled=False, l2_importance=1e-4):
+                 initial_noise=1.0, l2_enabled=False, l2_importance=1e-4, bounds=None):
+        """bounds = None: Normal policy; (lb, ub) arrays: Clipped Normal."""
         self.S, self.A, self.H, self.L = S, A, H, L
+        self.bounds = None if bounds is None else (np.broadcast_to(np.asarray(bounds[0], f32), (A,)),
+                                                   np.broadcast_to(np.asarray(bounds[1], f32), (A,)))
         self.theta = np.asarray(theta, f32).copy()
         self.adam = Adam(self.theta.size)
         self.max_size = max_size
@@ -243,8 +350,14 @@ class Agent:
     def size(self):
         return len(self.er["reward"])
 
+    def shift(self):
+        """Bounded distributions shift the means by (ub + lb) / 2 (continuous.cpp.base:20-30, :53-54)."""
+        if self.bounds is None:
+            return None
+        return ((self.bounds[1] + self.bounds[0]) * f32(0.5)).astype(f32)
+
     def policy(self, X):
-        out, _ = forward(self.theta, np.atleast_2d(X), self.S, self.H, self.L, self.A, self.noise)
+        out, _ = forward(self.theta, np.atleast_2d(X), self.S, self.H, self.L, self.A, self.noise, self.shift())
         return out
 
     def _add(self, **kw):
@@ -293,7 +406,7 @@ class Agent:
         returns (G, grad) for inspection."""
         er, A, B = self.er, self.A, len(mb)
         X = np.stack([er["state"][i] for i in mb])
-        out, acts = forward(self.theta, X, self.S, self.H, self.L, A, self.noise)
+        out, acts = forward(self.theta, X, self.S, self.H, self.L, A, self.noise, self.shift())
         # updateExperienceMetadata (agent.cpp.base:599-735)
         delta = 0
         for b in range(B):
@@ -301,7 +414,7 @@ class Agent:
                 continue
             e = mb[b]
             cur = out[b, 1:]
-            iw = importance_weight(er["action"][e], cur, er["exp_pol"][e], A)
+            iw = importance_weight(er["action"][e], cur, er["exp_pol"][e], A, self.bounds)
             tiw = min(self.iw_trunc, iw)
             onp = bool(iw > f32(1.0) / self.cutoff and iw < self.cutoff)
             if er["onp"][e] and not onp:
@@ -347,14 +460,14 @@ class Agent:
                 if er["term"][e] == TRUNCATED:
                     q = f32(q + f32(self.gamma * er["tv"][e]))
                 loss = f32(q - V)
-                pg = importance_weight_gradient(er["action"][e], cur, old, A)
+                pg = importance_weight_gradient(er["action"][e], cur, old, A, self.bounds)
                 G[b, 1:] = (self.beta * loss * pg).astype(f32)
-            klg = kl_gradient(old, cur, A)
+            klg = kl_gradient(old, cur, A, self.bounds)
             G[b, 1:] = (G[b, 1:] + f32(-(f32(1.0) - self.beta)) * klg).astype(f32)
         if not np.all(np.isfinite(G)):
             raise FloatingPointError("Gradient loss returned an invalid value")
         # DeepSupervisor::runGeneration (deepSupervisor.cpp.base:97-161), Direct Gradient
-        grad = backward(self.theta, acts, out, G, self.S, self.H, self.L, A, self.noise)
+        grad = backward(self.theta, acts, out, G, self.S, self.H, self.L, A, self.noise, self.shift())
         if self.l2[0]:
             grad = (grad - self.l2[1] * self.theta).astype(f32)
         self.adam.eta = self.lr
@@ -490,6 +603,8 @@ class Rollouts:
         for e, cart in enumerate(self.carts):
             b = self.buf[e]
             act = np.array([f32(out[e, 1 + i] + f32(out[e, 1 + A + i] * f32(noise[e, i]))) for i in range(A)], f32)
+            if ag.bounds is not None:  # continuous.cpp.base:172-183
+                act = np.minimum(np.maximum(act, ag.bounds[0]), ag.bounds[1]).astype(f32)
             b["states"].append(X[e].copy())
             b["actions"].append(act)
             b["pols"].append(out[e, 1:].copy())

@@ -181,7 +181,9 @@ from vracer_cases import cartpole_vracer  # noqa: E402
     (lambda e: e["Solver"].__setitem__("Mini Batch Sise", 3), "Unrecognized settings"),
     (lambda e: e["Problem"].__setitem__("Environment Kernel", "Pendulum"), "Unknown 'Environment Kernel'"),
     (lambda e: e["Variables"][4].__setitem__("Initial Exploration Noise", -1.0), "initial noise"),
-    (lambda e: e["Solver"]["Policy"].__setitem__("Distribution", "Clipped Normal"), "Policy Distribution"),
+    (lambda e: e["Solver"]["Policy"].__setitem__("Distribution", "Squashed Normal"), "Policy Distribution"),
+    (lambda e: (e["Solver"]["Policy"].__setitem__("Distribution", "Clipped Normal"),
+                e["Variables"][4].__setitem__("Upper Bound", float("inf"))), "non-finite"),
     (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][2].__setitem__("Output Channels", 96), "multiple of 64"),
     (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][1].__setitem__("Function", "Elementwise/ReLU"),
      "Elementwise/Tanh"),

@@ -621,14 +621,15 @@ def test_cmaes_gradient_information_through_the_api():
         korali.Engine().run(experiment(sphere, step=0.0))
 
 
-def test_vracer_cartpole_through_korali_engine():
+@pytest.mark.parametrize("policy", ["Normal", "Clipped Normal"])
+def test_vracer_cartpole_through_korali_engine(policy):
     """examples/learning/reinforcement/cartpole/run-vracer.py's configuration
     (Normal policy, device CartPole kernel) through korali.Engine: generations
     of 10 episodes, policy updates once 1000 experiences are stored, the
     solver state written back (counters, reward history, current policy)."""
     import korali
     from vracer_cases import cartpole_vracer
-    e = cartpole_vracer(max_generations=30, environments=64, hidden=64)
+    e = cartpole_vracer(max_generations=30, environments=64, hidden=64, policy=policy)
     korali.Engine().run(e)
     sv = e["Solver"]
     assert sv["Current Episode"] >= 290

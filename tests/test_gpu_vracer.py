@@ -51,9 +51,17 @@ def test_run_policy_matches_oracle(H, L, n):
     assert np.all(out[:, 2] > 0)
 
 
-def fill_replay(H, L, E, steps, max_size, seed=3):
+CLIP = (np.array([-0.5], f32), np.array([0.5], f32))  # narrow bounds: every clipping branch is taken
+
+
+def clip_kw(clipped):
+    return dict(policy_distribution="Clipped Normal", action_lower_bound=-0.5, action_upper_bound=0.5) if clipped \
+        else {}
+
+
+def fill_replay(H, L, E, steps, max_size, seed=3, bounds=None):
     th = theta_for(H, L, seed)
-    ag = V.Agent(S, A, H, L, th, max_size=max_size)
+    ag = V.Agent(S, A, H, L, th, max_size=max_size, bounds=bounds)
     ro = V.Rollouts(ag, E, max_steps=40)
     for s in range(steps):
         ro.step(V.action_noise(seed, s, E, A))
@@ -86,14 +94,17 @@ def load_replay(d, ag):
     d.set_scalar("experience_count", ag.experience_count)
 
 
-@pytest.mark.parametrize("H,L,B", [(64, 2, 32), (256, 2, 256)])
-def test_policy_updates_match_oracle(H, L, B):
+@pytest.mark.parametrize("H,L,B,clipped", [(64, 2, 32, False), (256, 2, 256, False), (64, 2, 64, True)])
+def test_policy_updates_match_oracle(H, L, B, clipped):
     """VRACER::trainPolicy on a replay memory filled by the oracle's rollouts:
     five updates with given sorted mini-batches (metadata, retrace, loss
     gradient, backward, fAdam and the REF-ER schedule)."""
-    ag, th = fill_replay(H, L, 8, 90, 600)
+    ag, th = fill_replay(H, L, 8, 90, 600, bounds=CLIP if clipped else None)
     d = device(hidden_size=H, hidden_layers=L, environments=8, mini_batch_size=B, replay_maximum_size=600,
-               replay_start_size=100, hyperparameters=th)
+               replay_start_size=100, hyperparameters=th, **clip_kw(clipped))
+    if clipped:
+        acts = np.concatenate(ag.er["action"])
+        assert np.any(acts <= -0.5) and np.any(acts >= 0.5) and np.any(np.abs(acts) < 0.5)
     load_replay(d, ag)
     rng = np.random.default_rng(9)
     for u in range(5):
@@ -115,16 +126,17 @@ def test_policy_updates_match_oracle(H, L, B):
         assert np.isclose(d.scalar("off_policy_cutoff"), float(ag.cutoff), rtol=1e-7)
 
 
-def test_environment_steps_match_oracle():
+@pytest.mark.parametrize("clipped", [False, True])
+def test_environment_steps_match_oracle(clipped):
     """Concurrent CartPole environments with the same action noise: episodes,
     terminations, the replay memory in processEpisode order, initial retrace
     values, relaunch sample ids — 120 steps, eviction included."""
     H, L, E, R = 64, 2, 16, 700
     th = theta_for(H, L, 4, spread=0.6)
-    ag = V.Agent(S, A, H, L, th, max_size=R)
+    ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None)
     ro = V.Rollouts(ag, E, max_steps=40)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=32, replay_maximum_size=R,
-               replay_start_size=R, max_episode_steps=40, hyperparameters=th, seed=4)
+               replay_start_size=R, max_episode_steps=40, hyperparameters=th, seed=4, **clip_kw(clipped))
     rng = np.random.default_rng(5)
     total = 0
     for s in range(120):

@@ -141,3 +141,34 @@ def test_rollouts_and_update_run():
     ids = ag.minibatch_ids(V.minibatch_uniforms(5, 0, 32))
     G, grad = ag.train_policy(ids)
     assert np.all(np.isfinite(G)) and np.all(np.isfinite(grad)) and ag.update_count == 1
+
+
+@pytest.mark.parametrize("a", [-0.5, 0.1, 0.5])  # stored actions are clipped to the bounds
+def test_clipped_normal_iw_gradient_matches_finite_differences(a):
+    """continuous.cpp.base:482-560: below the lower bound the weight is the
+    CDF's, above the upper the CCDF's, inside the density's."""
+    bounds = (np.array([-0.5], f32), np.array([0.5], f32))
+    cm, cs, om, os_ = f32(0.1), f32(0.6), f32(-0.1), f32(0.8)
+    g = V.importance_weight_gradient([f32(a)], [cm, cs], [om, os_], 1, bounds).astype(np.float64)
+    from scipy.stats import norm
+
+    def logp(m, s):
+        if a <= -0.5:
+            return norm.logcdf(-0.5, m, s)
+        if a >= 0.5:
+            return norm.logsf(0.5, m, s)
+        return norm.logpdf(a, m, s)
+
+    iw = np.exp(logp(float(cm), float(cs)) - logp(float(om), float(os_)))
+    e = 1e-5
+    dm = (logp(float(cm) + e, float(cs)) - logp(float(cm) - e, float(cs))) / (2 * e)
+    ds = (logp(float(cm), float(cs) + e) - logp(float(cm), float(cs) - e)) / (2 * e)
+    assert np.isclose(g[0], iw * dm, rtol=2e-3) and np.isclose(g[1], iw * ds, rtol=2e-3)
+
+
+def test_clipped_normal_log_cdf_tails():
+    # auxiliar/math.hpp:297-328 far in the tails (the asymptotic log erfc branch)
+    from scipy.stats import norm
+    for x in (-40.0, -8.0, 0.0, 8.0, 40.0):
+        assert np.isclose(V.normal_logcdf(f32(x), f32(0), f32(1)), norm.logcdf(x), rtol=1e-6, atol=1e-6)
+        assert np.isclose(V.normal_logccdf(f32(x), f32(0), f32(1)), norm.logsf(x), rtol=1e-6, atol=1e-6)
