@@ -107,7 +107,7 @@ __device__ inline float philox_uniform24(unsigned long long seed, unsigned long 
 // ------------------------------------------------------- Normal policy math
 // auxiliar/math.hpp:269-274 with T = float: 2*M_PI and KORALI_EPSILON
 // promote the expressions to double; norm and d are stored as float.
-__device__ inline float normal_logp(float x, float mean, float sigma) {
+__device__ __noinline__ float normal_logp(float x, float mean, float sigma) {
   const float norm = (float)(-0.5 * log(2.0 * M_PI * (double)sigma * (double)sigma));
   const float d = (float)((double)(x - mean) / ((double)sigma + 0.00000000001));
   return (float)((double)norm - 0.5 * (double)d * (double)d);
@@ -116,16 +116,16 @@ __device__ inline float normal_logp(float x, float mean, float sigma) {
 // Clipped Normal pieces (auxiliar/math.hpp:297-328, T = float): z is rounded
 // to float, log(0.5) + log erfc in double.  GSL's gsl_sf_log_erfc is
 // restated as log(erfc(x)) with the asymptotic series where erfc underflows.
-__device__ inline double log_erfc_d(double x) {
+__device__ __noinline__ double log_erfc_d(double x) {
   if (x < 26.0) return log(erfc(x));
   const double x2 = x * x, h = 1.0 / (2.0 * x2);
   return -x2 - log(x) - 0.57236494292470008707 + log(1.0 - h + 3.0 * h * h - 15.0 * h * h * h);
 }
-__device__ inline float normal_logcdf(float x, float mean, float sigma) {
+__device__ __noinline__ float normal_logcdf(float x, float mean, float sigma) {
   const float z = (float)((double)(x - mean) / ((double)sigma * M_SQRT2));
   return (float)(log(0.5) + log_erfc_d(-(double)z));
 }
-__device__ inline float normal_logccdf(float x, float mean, float sigma) {
+__device__ __noinline__ float normal_logccdf(float x, float mean, float sigma) {
   const float z = (float)((double)(x - mean) / ((double)sigma * M_SQRT2));
   return (float)(log(0.5) + log_erfc_d((double)z));
 }
@@ -415,14 +415,16 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
 // updateExperienceMetadata (agent.cpp.base:599-735) + the VRACER loss
 // gradient (VRACER.cpp.base:89-181) + the REF-ER schedule (agent.cpp.base:
 // 221-231), one workgroup: phases separated by workgroup barriers.
-__global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
+__global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                   const float *__restrict__ out, float *__restrict__ G) {
   __shared__ int s_delta;
   __shared__ unsigned s_mb[MAXB + 1];
   const int t = threadIdx.x, nt = blockDim.x, B = P.B, A = P.A, O = P.O;
   // every scalar read once into registers: the replay stores below may alias
   // the state struct for the compiler, which would otherwise reload it per use
-  const float cutoff = st->cutoff, beta = st->beta;
+  const float cutoff = st->cutoff, beta = st->beta, lr = st->lr, b1p = st->b1p, b2p = st->b2p;
+  const long long off0 = st->off_count, upd0 = st->update_count;
+  const unsigned long long size0 = st->size;
   const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
   auto ph = [&](long long i) -> long long {
     unsigned long long q = base + (unsigned long long)i;
@@ -465,37 +467,49 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
   if (delta) atomicAdd(&s_delta, delta);
   __threadfence_block();
   __syncthreads();
+  // stores only: the scalars were read at the start (a read-modify-write on
+  // the state struct here would put global round trips on wave 0's path)
+  const long long off1 = off0 + s_delta;
+  const float off_ratio = (float)off1 / (float)size0;
   if (t == 0) {
-    st->off_count += s_delta;
-    st->off_ratio = (float)st->off_count / (float)st->size;
-    st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)st->update_count);
+    st->off_count = off1;
+    st->off_ratio = off_ratio;
+    st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)upd0);
   }
-  // retrace chains of the oldest mini-batch entries of each episode
+  // retrace chains of the oldest mini-batch entries of each episode; every
+  // input of the chain-start decision is loaded at once (one round trip)
   for (int b = t; b < B; b += nt) {
-    const long long pe = ph(s_mb[b]);
-    if (b < B - 1 && er.ep_id[pe] == er.ep_id[ph(s_mb[b + 1])]) continue;
     const long long end = s_mb[b];
-    long long start = end - er.ep_pos[pe];
+    const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
+    const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
+    const int term = er.term[pe], pos = er.ep_pos[pe];
+    const float tvv = er.tv[pe], retn = er.ret[pnext];
+    if (b < B - 1 && epe == epn) continue;
+    long long start = end - pos;
     if (start < 0) start = 0;
     float retV = 0.0f;
-    if (er.term[pe] == TRUNCATED) retV = er.tv[pe];
-    if (er.term[pe] == NON_TERMINAL) retV = er.ret[ph(end + 1)];
-    // the chain's inputs are loaded 16 entries at a time ahead of the
-    // dependent recurrence (agent.cpp.base:717-733, same operation order)
+    if (term == TRUNCATED) retV = tvv;
+    if (term == NON_TERMINAL) retV = retn;
+    // the chain's inputs are loaded RC entries at a time ahead of the
+    // dependent recurrence (agent.cpp.base:717-733, same operation order);
+    // a short body keeps this one-workgroup kernel inside the instruction cache
+    constexpr int RC = 8;
+    long long pc = ph(end);
     for (long long c = end; c >= start;) {
-      const int n = (int)min(16ll, c - start + 1);
-      float vv[16], tw[16], rw[16];
+      const int n = (int)min((long long)RC, c - start + 1);
+      float vv[RC], tw[RC], rw[RC];
+      long long q = pc;
 #pragma unroll
-      for (int j = 0; j < 16; j++)
-        if (j < n) {
-          const long long pc = ph(c - j);
-          vv[j] = er.v[pc], tw[j] = er.tiw[pc], rw[j] = er.rew[pc];
-        }
+      for (int j = 0; j < RC; j++) {
+        if (j < n) vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
+        q = q == 0 ? (long long)R - 1 : q - 1;
+      }
 #pragma unroll
-      for (int j = 0; j < 16; j++)
+      for (int j = 0; j < RC; j++)
         if (j < n) {
           retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
-          er.ret[ph(c - j)] = retV;
+          er.ret[pc] = retV;
+          pc = pc == 0 ? (long long)R - 1 : pc - 1;
         }
       c -= n;
     }
@@ -504,15 +518,18 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
   __syncthreads();
   for (int b = t; b < B; b += nt) {
     const long long p = ph(s_mb[b]);
-    const float V = er.v[p];
+    // every input loaded at once, the next entry's retrace value included
+    const float V = er.v[p], retp = er.ret[p], retn = er.ret[ph((long long)s_mb[b] + 1)], rew = er.rew[p],
+                tvp = er.tv[p];
+    const int term = er.term[p], onp = er.onp[p];
     const float *cur = er.cur_pol + p * 2 * A, *old = er.exp_pol + p * 2 * A;
     float g[MAXO];
-    g[0] = er.ret[p] - V;
+    g[0] = retp - V;
     for (int i = 1; i < O; i++) g[i] = 0.f;
-    if (er.onp[p]) {
-      float q = er.rew[p];
-      if (er.term[p] == NON_TERMINAL) q += P.gamma * er.ret[ph((long long)s_mb[b] + 1)];
-      if (er.term[p] == TRUNCATED) q += P.gamma * er.tv[p];
+    if (onp) {
+      float q = rew;
+      if (term == NON_TERMINAL) q += P.gamma * retn;
+      if (term == TRUNCATED) q += P.gamma * tvp;
       const float loss = q - V;
       float pg[2 * MAXA];
       float lc = 0.f, lo = 0.f;
@@ -594,13 +611,14 @@ __global__ __launch_bounds__(1024) void k_vr_meta(Params P, State *st, Replay er
   __syncthreads();
   if (t == 0) {
     // the learner's eta for this update, then agent.cpp.base:221-231
-    st->eta = st->lr;
-    st->b1p = st->b1p * 0.9f;
-    st->b2p = st->b2p * 0.999f;
-    st->update_count += 1;
-    st->lr = P.lr0 / (1.0f + P.anneal * (float)st->update_count);
-    if (st->off_ratio > P.off_target) st->beta = (1.0f - st->lr) * st->beta;
-    else st->beta = (1.0f - st->lr) * st->beta + st->lr;
+    st->eta = lr;
+    st->b1p = b1p * 0.9f;
+    st->b2p = b2p * 0.999f;
+    st->update_count = upd0 + 1;
+    const float lr1 = P.lr0 / (1.0f + P.anneal * (float)(upd0 + 1));
+    st->lr = lr1;
+    if (off_ratio > P.off_target) st->beta = (1.0f - lr1) * beta;
+    else st->beta = (1.0f - lr1) * beta + lr1;
   }
 }
 
@@ -1002,7 +1020,7 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   VrStage tu(h, "update");
   hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
   if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
-  hipLaunchKernelGGL(k_vr_meta, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, (const unsigned *)h->mb,
+  hipLaunchKernelGGL(k_vr_meta, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er, (const unsigned *)h->mb,
                      (const float *)h->out, h->G);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
   const size_t rs = h->rowsMax * P.H;
