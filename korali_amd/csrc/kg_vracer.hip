@@ -414,14 +414,22 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
 
 // updateExperienceMetadata (agent.cpp.base:599-735) + the VRACER loss
 // gradient (VRACER.cpp.base:89-181) + the REF-ER schedule (agent.cpp.base:
-// 221-231), one workgroup: phases separated by workgroup barriers.
+// 221-231), one workgroup.  Every mini-batch row's metadata lives in LDS
+// between the phases: the retrace chains take the updated state values and
+// truncated weights of mini-batch entries from LDS and leave each row's
+// retrace value (and its successor's) there, so the gradient phase reads no
+// global memory, and the replay-memory metadata is written once at the end
+// (no global store is waited for at the first barrier).  A == 1.
+constexpr int MB_META = 1024;
 __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
-                                                  const float *__restrict__ out, float *__restrict__ G) {
+                                                 const float *__restrict__ out, float *__restrict__ G) {
+  __shared__ unsigned s_mb[MB_META];
+  __shared__ float s_V[MB_META], s_tiw[MB_META], s_iw[MB_META], s_ret[MB_META], s_retn[MB_META], s_rew[MB_META],
+      s_tv[MB_META], s_act[MB_META], s_cur[2 * MB_META], s_old[2 * MB_META];
+  __shared__ unsigned char s_term[MB_META], s_onp[MB_META], s_uniq[MB_META];
   __shared__ int s_delta;
-  __shared__ unsigned s_mb[MAXB + 1];
-  const int t = threadIdx.x, nt = blockDim.x, B = P.B, A = P.A, O = P.O;
-  // every scalar read once into registers: the replay stores below may alias
-  // the state struct for the compiler, which would otherwise reload it per use
+  const int t = threadIdx.x, nt = blockDim.x, B = P.B, O = P.O;
+  // every scalar read once into registers
   const float cutoff = st->cutoff, beta = st->beta, lr = st->lr, b1p = st->b1p, b2p = st->b2p;
   const long long off0 = st->off_count, upd0 = st->update_count;
   const unsigned long long size0 = st->size;
@@ -432,147 +440,152 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     return (long long)q;
   };
   if (t == 0) s_delta = 0;
-  for (int b = t; b < B; b += nt) s_mb[b] = mb[b];
   __syncthreads();
+  // ---- importance weights and on-policy flags (agent.cpp.base:613-657);
+  // duplicates compute the same values, only the first occurrence counts
   int delta = 0;
   for (int b = t; b < B; b += nt) {
-    if (b > 0 && s_mb[b] == s_mb[b - 1]) continue;
-    const long long p = ph(s_mb[b]);
-    const float *cur = out + (long long)b * O + 1;
-    float lc = 0.f, lo = 0.f;
-    for (int i = 0; i < A; i++) {
-      const float a = er.act[p * A + i];
-      lc += policy_logp(P, i, a, cur[i], cur[A + i]);
-      lo += policy_logp(P, i, a, er.exp_pol[p * 2 * A + i], er.exp_pol[p * 2 * A + A + i]);
-    }
-    float liw = lc - lo;
+    const unsigned id = mb[b];
+    const bool uniq = b == 0 || id != mb[b - 1];
+    const long long p = ph(id);
+    const float a = er.act[p], om = er.exp_pol[2 * p], osd = er.exp_pol[2 * p + 1], rew = er.rew[p];
+    const int was = er.onp[p], term = er.term[p];
+    const float V = out[(long long)b * O], cm = out[(long long)b * O + 1], cs = out[(long long)b * O + 2];
+    const float tvv = term == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
+    float liw = policy_logp(P, 0, a, cm, cs) - policy_logp(P, 0, a, om, osd);
     if (liw > 7.f) liw = 7.f;
     if (liw < -7.f) liw = -7.f;
     if (!isfinite(liw)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_IW);
+    if (!isfinite(V)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_VALUE);
     const float iw = expf(liw);
     const float tiw = iw < P.iw_trunc ? iw : P.iw_trunc;  // std::min(level, iw)
     const int onp = (iw > 1.0f / cutoff) && (iw < cutoff);
-    const int was = er.onp[p];
-    if (was && !onp) delta++;
-    if (!was && onp) delta--;
-    const float V = out[(long long)b * O];
-    if (!isfinite(V)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_VALUE);
-    for (int i = 0; i < 2 * A; i++) er.cur_pol[p * 2 * A + i] = cur[i];
-    er.v[p] = V;
-    er.tv[p] = er.term[p] == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
-    er.iw[p] = iw;
-    er.onp[p] = onp;
-    er.tiw[p] = tiw;
+    if (uniq) {
+      if (was && !onp) delta++;
+      if (!was && onp) delta--;
+    }
+    s_mb[b] = id, s_uniq[b] = uniq;
+    s_V[b] = V, s_tiw[b] = tiw, s_iw[b] = iw, s_rew[b] = rew, s_tv[b] = tvv, s_act[b] = a;
+    s_cur[2 * b] = cm, s_cur[2 * b + 1] = cs, s_old[2 * b] = om, s_old[2 * b + 1] = osd;
+    s_term[b] = (unsigned char)term, s_onp[b] = (unsigned char)onp;
   }
   if (delta) atomicAdd(&s_delta, delta);
-  __threadfence_block();
   __syncthreads();
-  // stores only: the scalars were read at the start (a read-modify-write on
-  // the state struct here would put global round trips on wave 0's path)
   const long long off1 = off0 + s_delta;
   const float off_ratio = (float)off1 / (float)size0;
-  if (t == 0) {
-    st->off_count = off1;
-    st->off_ratio = off_ratio;
-    st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)upd0);
-  }
-  // retrace chains of the oldest mini-batch entries of each episode; every
-  // input of the chain-start decision is loaded at once (one round trip)
+  // ---- retrace chains of the oldest mini-batch entries of each episode
+  // (agent.cpp.base:679-733, same operation order)
   for (int b = t; b < B; b += nt) {
     const long long end = s_mb[b];
     const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
     const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
-    const int term = er.term[pe], pos = er.ep_pos[pe];
-    const float tvv = er.tv[pe], retn = er.ret[pnext];
+    const int pos = er.ep_pos[pe], term = s_term[b];
+    const float retn = er.ret[pnext];
     if (b < B - 1 && epe == epn) continue;
     long long start = end - pos;
     if (start < 0) start = 0;
     float retV = 0.0f;
-    if (term == TRUNCATED) retV = tvv;
+    if (term == TRUNCATED) retV = s_tv[b];
     if (term == NON_TERMINAL) retV = retn;
-    // the chain's inputs are loaded RC entries at a time ahead of the
-    // dependent recurrence (agent.cpp.base:717-733, same operation order);
-    // a short body keeps this one-workgroup kernel inside the instruction cache
-    constexpr int RC = 8;
+    float prev = retn;  // retrace value of the entry after the current one
+    int k = b;          // mini-batch rows of this episode, walked downwards
+    // per chunk: inputs loaded and mini-batch overrides applied first (no
+    // dependence on the recurrence), then the recurrence alone (4 dependent
+    // float operations per entry), then the mini-batch rows' values to LDS
+    constexpr int RC = 16;
     long long pc = ph(end);
     for (long long c = end; c >= start;) {
       const int n = (int)min((long long)RC, c - start + 1);
-      float vv[RC], tw[RC], rw[RC];
+      float vv[RC], tw[RC], rw[RC], rr[RC];
       long long q = pc;
 #pragma unroll
       for (int j = 0; j < RC; j++) {
         if (j < n) vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
         q = q == 0 ? (long long)R - 1 : q - 1;
       }
+      int kk = k;
+      unsigned inmb = 0;
 #pragma unroll
       for (int j = 0; j < RC; j++)
-        if (j < n) {
-          retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
-          er.ret[pc] = retV;
-          pc = pc == 0 ? (long long)R - 1 : pc - 1;
+        if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
+          vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
+          inmb |= 1u << j;
+          while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
         }
+#pragma unroll
+      for (int j = 0; j < RC; j++)
+        if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
+      q = pc;
+#pragma unroll
+      for (int j = 0; j < RC; j++) {
+        if (j < n) er.ret[q] = rr[j];
+        q = q == 0 ? (long long)R - 1 : q - 1;
+      }
+      if (inmb)
+#pragma unroll
+        for (int j = 0; j < RC; j++)
+          if (inmb >> j & 1u) {
+            const float before = j == 0 ? prev : rr[j - 1];
+            while (k >= 0 && (long long)s_mb[k] == c - j) s_ret[k] = rr[j], s_retn[k] = before, k--;
+          }
+      prev = retV;  // the chunk's last entry
+      pc = q;
       c -= n;
     }
   }
-  __threadfence_block();
   __syncthreads();
+  // ---- the VRACER loss gradient (VRACER.cpp.base:104-177), all from LDS;
+  // then the replay memory's metadata (first occurrences)
+  const float klm = -(1.0f - beta);
   for (int b = t; b < B; b += nt) {
-    const long long p = ph(s_mb[b]);
-    // every input loaded at once, the next entry's retrace value included
-    const float V = er.v[p], retp = er.ret[p], retn = er.ret[ph((long long)s_mb[b] + 1)], rew = er.rew[p],
-                tvp = er.tv[p];
-    const int term = er.term[p], onp = er.onp[p];
-    const float *cur = er.cur_pol + p * 2 * A, *old = er.exp_pol + p * 2 * A;
-    float g[MAXO];
-    g[0] = retp - V;
-    for (int i = 1; i < O; i++) g[i] = 0.f;
-    if (onp) {
-      float q = rew;
-      if (term == NON_TERMINAL) q += P.gamma * retn;
-      if (term == TRUNCATED) q += P.gamma * tvp;
+    const float V = s_V[b], cm = s_cur[2 * b], cs = s_cur[2 * b + 1], om = s_old[2 * b], osd = s_old[2 * b + 1];
+    const float a = s_act[b];
+    const int term = s_term[b];
+    float g[3];
+    g[0] = s_ret[b] - V;
+    g[1] = g[2] = 0.f;
+    if (s_onp[b]) {
+      float q = s_rew[b];
+      if (term == NON_TERMINAL) q += P.gamma * s_retn[b];
+      if (term == TRUNCATED) q += P.gamma * s_tv[b];
       const float loss = q - V;
-      float pg[2 * MAXA];
-      float lc = 0.f, lo = 0.f;
-      for (int i = 0; i < A; i++) {
-        const float a = er.act[p * A + i], cm = cur[i], cs = cur[A + i];
-        const float dif = a - cm;
-        if (!P.clipped) {  // continuous.cpp.base:404-440
-          const float inv_var = 1.f / (cs * cs);
-          pg[i] = dif * inv_var;
-          pg[A + i] = (dif * dif) * (inv_var / cs) - 1.f / cs;
-          lc += normal_logp(a, cm, cs);
-          lo += normal_logp(a, old[i], old[A + i]);
-        } else {  // continuous.cpp.base:482-560
-          const float inv_sig = 1.f / cs;
-          if (a <= P.lb[i]) {
-            const float lcdf = normal_logcdf(P.lb[i], cm, cs);
-            const float r = expf(normal_logp(P.lb[i], cm, cs) - lcdf);
-            pg[i] = -r;
-            pg[A + i] = -dif * inv_sig * r;
-            lc += lcdf;
-            lo += normal_logcdf(P.lb[i], old[i], old[A + i]);
-          } else if (P.ub[i] <= a) {
-            const float lccdf = normal_logccdf(P.ub[i], cm, cs);
-            const float r = expf(normal_logp(P.ub[i], cm, cs) - lccdf);
-            pg[i] = r;
-            pg[A + i] = dif * inv_sig * r;
-            lc += lccdf;
-            lo += normal_logccdf(P.ub[i], old[i], old[A + i]);
-          } else {
-            const float inv_sig3 = inv_sig * inv_sig * inv_sig;
-            pg[i] = dif * inv_sig * inv_sig;
-            pg[A + i] = dif * dif * inv_sig3 - inv_sig;
-            lc += normal_logp(a, cm, cs);
-            lo += normal_logp(a, old[i], old[A + i]);
-          }
+      float pg0, pg1, lc, lo;
+      const float dif = a - cm;
+      if (!P.clipped) {  // continuous.cpp.base:404-440
+        const float inv_var = 1.f / (cs * cs);
+        pg0 = dif * inv_var;
+        pg1 = (dif * dif) * (inv_var / cs) - 1.f / cs;
+        lc = normal_logp(a, cm, cs);
+        lo = normal_logp(a, om, osd);
+      } else {  // continuous.cpp.base:482-560
+        const float inv_sig = 1.f / cs;
+        if (a <= P.lb[0]) {
+          const float lcdf = normal_logcdf(P.lb[0], cm, cs);
+          const float r = expf(normal_logp(P.lb[0], cm, cs) - lcdf);
+          pg0 = -r;
+          pg1 = -dif * inv_sig * r;
+          lc = lcdf;
+          lo = normal_logcdf(P.lb[0], om, osd);
+        } else if (P.ub[0] <= a) {
+          const float lccdf = normal_logccdf(P.ub[0], cm, cs);
+          const float r = expf(normal_logp(P.ub[0], cm, cs) - lccdf);
+          pg0 = r;
+          pg1 = dif * inv_sig * r;
+          lc = lccdf;
+          lo = normal_logccdf(P.ub[0], om, osd);
+        } else {
+          const float inv_sig3 = inv_sig * inv_sig * inv_sig;
+          pg0 = dif * inv_sig * inv_sig;
+          pg1 = dif * dif * inv_sig3 - inv_sig;
+          lc = normal_logp(a, cm, cs);
+          lo = normal_logp(a, om, osd);
         }
       }
-      const float iwg = expf(lc - lo);
-      for (int i = 0; i < 2 * A; i++) g[1 + i] = beta * loss * (pg[i] * iwg);
+      const float iwg = expf(0.0f + lc - lo);
+      g[1] = beta * loss * (pg0 * iwg);
+      g[2] = beta * loss * (pg1 * iwg);
     }
-    const float klm = -(1.0f - beta);
-    for (int i = 0; i < A; i++) {
-      const float om = old[i], osd = old[A + i], cm = cur[i], cs = cur[A + i];
+    {
       const float inv_sig = (float)(1. / (double)cs);
       const float inv_var = (float)(1. / (double)(cs * cs));
       const float inv_sig3 = (float)(1. / (double)(cs * cs * cs));
@@ -580,7 +593,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       float kl_mean = d * inv_var;
       float kl_sig = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
       if (P.clipped) {  // continuous.cpp.base:734-777
-        const float lb = P.lb[i], ub = P.ub[i];
+        const float lb = P.lb[0], ub = P.ub[0];
         const float oldVar = osd * osd, oldInvSig = 1.f / osd, curInvSig = 1.f / cs;
         const float curInvVar = 1.f / (cs * cs), curInvSig3 = 1.f / (cs * cs * cs), muDif = om - cm;
         const float invSqrt2Pi = (float)(M_SQRT1_2 * sqrt(M_1_PI));
@@ -600,16 +613,27 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
         kl_sig -= invSqrt2Pi * curInvSig3 * (oldVar * oldAdjLb + 2.f * osd * muDif) * expLb;
         kl_sig -= curAdjUb * ccdfB;
       }
-      g[1 + i] += klm * kl_mean;
-      g[1 + A + i] += klm * kl_sig;
+      g[1] += klm * kl_mean;
+      g[2] += klm * kl_sig;
     }
-    for (int i = 0; i < O; i++) {
+    for (int i = 0; i < 3; i++) {
       if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
       G[(long long)b * O + i] = g[i];
     }
+    if (s_uniq[b]) {
+      const long long p = ph(s_mb[b]);
+      er.cur_pol[2 * p] = cm, er.cur_pol[2 * p + 1] = cs;
+      er.v[p] = V;
+      er.tv[p] = s_tv[b];
+      er.iw[p] = s_iw[b];
+      er.onp[p] = s_onp[b];
+      er.tiw[p] = s_tiw[b];
+    }
   }
-  __syncthreads();
   if (t == 0) {
+    st->off_count = off1;
+    st->off_ratio = off_ratio;
+    st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)upd0);
     // the learner's eta for this update, then agent.cpp.base:221-231
     st->eta = lr;
     st->b1p = b1p * 0.9f;
@@ -1110,7 +1134,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
            "vracer: the device environment is the CartPole of examples/learning/reinforcement/cartpole (4 states, 1 action)");
   KG_CHECK(c->hidden_size % 64 == 0 && c->hidden_size >= 64, "vracer: hidden layer width must be a multiple of 64");
   KG_CHECK(c->hidden_layers >= 1, "vracer: at least one hidden layer");
-  KG_CHECK(c->mini_batch_size >= 2 && c->mini_batch_size <= (size_t)MAXB, "vracer: Mini Batch Size must be 2..2048");
+  KG_CHECK(c->mini_batch_size >= 2 && c->mini_batch_size <= (size_t)MB_META, "vracer: Mini Batch Size must be 2..1024");
   KG_CHECK(c->environments >= 1 && c->environments <= (1u << 20), "vracer: Concurrent Environments out of range");
   KG_CHECK(c->environment_count >= 1, "vracer: Environment Count must be >= 1");
   KG_CHECK(c->replay_maximum_size >= 2 && c->replay_start_size <= c->replay_maximum_size,
