@@ -872,9 +872,13 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     bool own_end = true;
     if ((unsigned long long)(rank + 1) < neps && ev.len[ev.fin_env[rank + 1]] == 1) own_end = false;
     retV = P.gamma * retV + ev.eb_rew[(long long)e * P.T + len - 1];
-    if (own_end) er.ret[((long long)base + endj) % R] = retV;
+    // an entry overwritten later in this same batch (more new experiences
+    // than the capacity) keeps the later entry's values, as the reference's
+    // sequential processEpisode calls leave it
+    const long long survive = (long long)nnew - R;  // new-entry offsets below this were overwritten
+    if (own_end && endj >= survive) er.ret[((long long)base + endj) % R] = retV;
     const long long prevj = endj - 1;
-    if ((long long)base + prevj >= 0) {
+    if ((long long)base + prevj >= 0 && prevj >= survive) {
       float r;
       if (len >= 2) r = ev.eb_rew[(long long)e * P.T + len - 2];
       else if (rank > 0) {

@@ -126,17 +126,18 @@ def test_policy_updates_match_oracle(H, L, B, clipped):
         assert np.isclose(d.scalar("off_policy_cutoff"), float(ag.cutoff), rtol=1e-7)
 
 
-@pytest.mark.parametrize("clipped", [False, True])
-def test_environment_steps_match_oracle(clipped):
+@pytest.mark.parametrize("clipped,R,T", [(False, 700, 40), (True, 700, 40), (False, 40, 5)])
+def test_environment_steps_match_oracle(clipped, R, T):
     """Concurrent CartPole environments with the same action noise: episodes,
     terminations, the replay memory in processEpisode order, initial retrace
-    values, relaunch sample ids — 120 steps, eviction included."""
-    H, L, E, R = 64, 2, 16, 700
+    values, relaunch sample ids — 120 steps, eviction included; (R=40, T=5):
+    one step appends more experiences than the replay memory holds."""
+    H, L, E = 64, 2, 16
     th = theta_for(H, L, 4, spread=0.6)
     ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None)
-    ro = V.Rollouts(ag, E, max_steps=40)
+    ro = V.Rollouts(ag, E, max_steps=T)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=32, replay_maximum_size=R,
-               replay_start_size=R, max_episode_steps=40, hyperparameters=th, seed=4, **clip_kw(clipped))
+               replay_start_size=R, max_episode_steps=T, hyperparameters=th, seed=4, **clip_kw(clipped))
     rng = np.random.default_rng(5)
     total = 0
     for s in range(120):
