@@ -1529,7 +1529,8 @@ void runExperiment(Experiment &e, Conduit &conduit) {
     solver.runGeneration(gen);
     const auto g1 = std::chrono::steady_clock::now();
     if (consoleFreq > 0 && gen % consoleFreq == 0) {
-      solver.printAfter(st.log);
+      // printAfter reads solver state from the device: only when it prints
+      if (st.log.level >= 2) solver.printAfter(st.log);
       st.log.log(3, "Experiment: 0 - Generation Time: %.3fs\n", std::chrono::duration<double>(g1 - g0).count());
     }
     if (fileOut && fileFreq > 0 && gen % fileFreq == 0) save();
