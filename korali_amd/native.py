@@ -231,6 +231,12 @@ class CmaesDevice:
     def update_finalize(self, generation):
         check(self._L.kg_cmaes_update_finalize(self.h, int(generation)))
 
+    def begin_sample(self):
+        """Enqueue the next generation's generator prefetch and the first
+        eigendecomposition phases (workspace only) — what the korali engine
+        does right after each update (kg_cmaes_begin_sample)."""
+        check(self._L.kg_cmaes_begin_sample(self.h))
+
     def generation(self, generation, objective):
         obj = OBJECTIVES[objective.lower()] if isinstance(objective, str) else int(objective)
         check(self._L.kg_cmaes_generation(self.h, int(generation), obj))
