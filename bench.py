@@ -751,6 +751,14 @@ def run_c5(args):
     upd_flops = c5_update_flops(H=H, L=C5["hidden_layers"], B=C5["mini_batch_size"])
     upd_ms = stages.get("update")
     finished = d.get("finished_rewards")
+    # HBM bytes per rollout-GEMM launch from the committed PMC passes (tools/pmc_c5.py)
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", PROFILE_ROUND, "c5_pmc_traffic.csv")
+    if os.path.exists(tf):
+        import csv
+        rows = list(csv.DictReader(open(tf)))
+        if rows:
+            traffic = (float(rows[0]["fetch_KB_x2"]) + float(rows[0]["write_KB"])) * 1024.0
     out = {
         "metric": "VRACER experiences/sec, 4096 concurrent CartPole rollouts, 2x256 policy (C5)",
         "value": exps / elapsed, "unit": "experiences/s", "n_gpus": 1, "steps": args.steps,
@@ -767,7 +775,8 @@ def run_c5(args):
                             "frac": upd_flops / (upd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS if upd_ms else None},
         "roofline": {"kernel": "kg::vr::k_vr_gemm<1> (rollout forward, hidden layer)", "bound": "mfma",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": None,
+                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": traffic,
+                     "traffic_source": f"profiles/{PROFILE_ROUND}/c5_pmc_traffic.csv" if traffic else None,
                      "algorithmic_flops_per_launch": gemm_flops, "avg_launch_ms": gemm_ms},
         "mean_recent_episode_reward": float(np.mean(finished[finished != 0])) if np.any(finished != 0) else None,
     }
