@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 2
+#define KG_ABI_VERSION 3
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -70,7 +70,7 @@ typedef struct {
   double initial_cumulative_covariance;   /* ≤0 or >1 → formula default */
   int is_sigma_bounded;                   /* "Is Sigma Bounded" */
   int diagonal_covariance;                /* "Diagonal Covariance" */
-  int mirrored_sampling;                  /* "Mirrored Sampling" (not yet on device: error) */
+  int mirrored_sampling;                  /* "Mirrored Sampling" (pairs z, -z; CMAES.cpp.base:461-491) */
   double max_infeasible_resamplings;      /* "Termination Criteria/Max Infeasible Resamplings" */
   const double *lower_bound;              /* N, may be NULL → -inf */
   const double *upper_bound;              /* N, may be NULL → +inf */

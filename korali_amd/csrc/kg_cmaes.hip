@@ -2020,6 +2020,14 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
             "pivot-update %llu chain-w0 %llu chain-w3 %llu (A: dnrm2 %llu [of which pre-chain %llu] scalars %llu)\n",
             t[0], t[1], t[2], t[3], steps, rots, t[4], t[5], t[6], t[7], t[16], t[17], t[18], t[19], t[20], t[21],
             t[22], t[23], t[24], t[25], t[26], t[27], t[28], t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15], t[29], t[31], t[30]);
+    fprintf(stderr,
+            "[korali_amd sq tridiag, wave 0] staging %llu nrm2-chain %llu scalars+v %llu wait-A %llu dsymv %llu "
+            "wait-E %llu xv+pivot %llu wait-X %llu\n",
+            t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]);
+    fprintf(stderr,
+            "[korali_amd mw2 tridiag, writer wg] staging %llu barrier %llu nrm2-chain %llu scalars %llu products %llu "
+            "dsymv-chains %llu x-gather %llu xv %llu poll %llu update %llu\n",
+            t[16], t[17], t[18], t[19], t[20], t[21], t[22], t[23], t[24], t[25]);
   }
   return check_errors(h);
 }

@@ -2714,6 +2714,12 @@ __global__ void __launch_bounds__(256) k_publish_dsd(int N, const double *__rest
   }
 }
 
+}  // namespace kg
+
+#include "kg_tridiag.hip"
+
+namespace kg {
+
 // ------------------------------------------------------------------------
 // Orchestration
 size_t eig_mat_bytes(int N) { return (size_t)N * (N + 1) * sizeof(double); }
@@ -2774,23 +2780,41 @@ int EigenSolver::init(int N_, bool hostChase_) {
   // tridiagonalisation: one workgroup with the whole matrix in LDS while it
   // fits (no in-launch hand-offs), multi-workgroup above;
   // KORALI_AMD_TRIDIAG = lds | 1wg | mw forces one
-  tri = t2_fits(N) ? 3 : (t1_fits(N) ? 1 : (lds ? 0 : 2));
+  tri = sq_fits(N) ? 4 : (t2_fits(N) ? 3 : (t1_fits(N) ? 1 : (lds ? 0 : (mw2_fits(N) ? 5 : 2))));
   if (const char *e = getenv("KORALI_AMD_TRIDIAG")) {
+    if (!strcmp(e, "sq") && sq_fits(N)) tri = 4;
+    if (!strcmp(e, "mw2") && mw2_fits(N)) tri = 5;
     if (!strcmp(e, "lds") && eig_use_lds(N)) tri = 0;
     if (!strcmp(e, "1wg") && t1_fits(N)) tri = 1;
     if (!strcmp(e, "1wg2") && t2_fits(N)) tri = 3;
     if (!strcmp(e, "mw")) tri = 2;
   } else if (getenv("KORALI_AMD_EIGEN_MW_MIN") && !lds) {
-    tri = 2;
+    tri = mw2_fits(N) ? 5 : 2;
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
   if (tri == 1)
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(t1_lds_doubles(N) * sizeof(double))));
+  if (tri == 4)
+    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_sq, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sq_lds_doubles(N) * sizeof(double))));
   if (tri == 3)
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(t2_lds_doubles(N) * sizeof(double))));
-  if (!lds || tri == 2) {
+  if (tri == 5) {
+    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)mw2_lds_bytes(N)));
+    // the workgroups hand data to each other inside the launch: they must be
+    // co-resident, which a cooperative launch guarantees (or refuses)
+    int perCU = 0, dev = 0, cus = 0;
+    KG_HIP(hipGetDevice(&dev));
+    KG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    KG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_tridiag_mw2, MW2_TPB,
+                                                        mw2_lds_bytes(N)));
+    KG_CHECK(perCU * cus >= mw2_groups(N), "eigensolver: the multi-workgroup tridiagonalisation's " +
+                                               std::to_string(mw2_groups(N)) + " workgroups cannot be co-resident");
+  }
+  if (!lds || tri == 2 || tri == 5) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)tmw_lds_bytes(N)));
@@ -2835,7 +2859,10 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
-  if (tri == 3)
+  if (tri == 4)
+    hipLaunchKernelGGL(k_tridiag_sq, dim3(1), dim3(SQ_TPB), sq_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
+                       sd, trace);
+  else if (tri == 3)
     hipLaunchKernelGGL(k_tridiag_1wg2, dim3(1), dim3(T2_TPB), t2_lds_doubles(N) * sizeof(double), s, N, C, gH, tau,
                        d, sd, trace);
   else if (tri == 1)
@@ -2844,7 +2871,17 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   else if (tri == 0)
     hipLaunchKernelGGL(k_tridiag<true>, dim3(1), dim3(1024), eig_mat_bytes(N) + tridiag_vec_bytes(N), s, N, C, gA, gH,
                        tau, d, sd, trace);
-  else {
+  else if (tri == 5) {
+    KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
+    int N_ = N;
+    const double *C_ = C;
+    double *gH_ = gH, *tau_ = tau, *d_ = d, *sd_ = sd;
+    unsigned long long *comm_ = comm, *trace_ = trace;
+    unsigned int *errors_ = errors;
+    void *args[] = {&N_, &C_, &gH_, &tau_, &d_, &sd_, &comm_, &errors_, &trace_};
+    KG_HIP(hipLaunchCooperativeKernel((const void *)k_tridiag_mw2, dim3(mw2_groups(N)), dim3(MW2_TPB), args,
+                                      mw2_lds_bytes(N), s));
+  } else {
     KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), tmw_lds_bytes(N), s, N, C, gH, tau, d, sd,
                        comm, errors, trace);

@@ -40,7 +40,7 @@ class EigenSolver {
  private:
   int N = 0, maxRot = 0;
   bool lds = true;
-  int tri = 0;  // tridiagonalisation kernel: 0 k_tridiag (LDS), 1 k_tridiag_1wg, 2 k_tridiag_mw, 3 k_tridiag_1wg2
+  int tri = 0;  // tridiagonalisation kernel: 0 k_tridiag (LDS), 1 k_tridiag_1wg, 2 k_tridiag_mw, 3 k_tridiag_1wg2, 4 k_tridiag_sq, 5 k_tridiag_mw2
   double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
          *chaseWork = nullptr;
   unsigned long long *comm = nullptr;  // in-launch hand-off granules (N > 128 tridiagonalisation)

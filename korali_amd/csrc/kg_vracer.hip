@@ -819,6 +819,23 @@ __global__ __launch_bounds__(1024) void k_vr_scan(Params P, State *st, Envs ev) 
   }
 }
 
+// Eviction accounting of this step's appends (agent.cpp.base:504-506: an
+// evicted off-policy experience decrements the off-policy count), before any
+// new entry is written: the new offsets j < min(new, R) overwrite the slots
+// of the old occupants base + j - R (those >= 0); offsets j >= R overwrite
+// entries of this same batch, which are on-policy.  One workgroup, one
+// atomic per thread.
+__global__ __launch_bounds__(256) void k_vr_evict(Params P, State *st, Replay er) {
+  const unsigned long long base = st->step_base, nnew = st->step_new;
+  const long long R = P.R, cnt = (long long)(nnew < (unsigned long long)R ? nnew : (unsigned long long)R);
+  unsigned long long evicted = 0;
+  for (long long j = threadIdx.x; j < cnt; j += blockDim.x) {
+    const long long prev = (long long)base + j - R;
+    if (prev >= 0 && er.onp[((long long)base + j) % R] == 0) evicted++;
+  }
+  if (evicted) atomicAdd((unsigned long long *)&st->off_count, (unsigned long long)(-(long long)evicted));
+}
+
 // processEpisode (agent.cpp.base:376-572) for every finished episode at once:
 // one workgroup per environment copies its episode into the replay memory,
 // counts evicted off-policy entries, sets the initial retrace values (the
@@ -835,13 +852,14 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
   const unsigned long long base = st->step_base, nnew = st->step_new, ep0 = st->step_episode_base,
                            neps = st->step_episodes, sid0 = st->step_sample_base;
   const long long R = P.R;
+  // the next finished episode (rank + 1) sets our last entry's initial
+  // retrace value when it has one experience: then no placeholder is written
+  // for it here (the two workgroups are not ordered)
+  const bool own_end = !((unsigned long long)(rank + 1) < neps && ev.len[ev.fin_env[rank + 1]] == 1);
   for (int k = t; k < len; k += nt) {
     const long long j = off + k;
-    if ((long long)nnew - j > R) continue;  // overwritten within this batch
+    if ((long long)nnew - j > R) continue;  // overwritten within this batch (evictions: k_vr_evict)
     const long long abs_i = (long long)base + j, p = abs_i % R;
-    const long long prev = abs_i - R;  // absolute index of the evicted occupant
-    if (prev >= 0 && prev < (long long)base && er.onp[p] == 0)
-      atomicAdd((unsigned long long *)&st->off_count, (unsigned long long)(-1ll));
     const long long slot = (long long)e * P.T + k;
     const int tk = k == len - 1 ? term : NON_TERMINAL;
     for (int q = 0; q < S; q++) {
@@ -854,7 +872,7 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     er.env[p] = ev.env_id[e];
     er.term[p] = tk;
     er.exp_v[p] = er.v[p] = ev.eb_v[slot];
-    er.ret[p] = 0.f;
+    if (k != len - 1 || own_end) er.ret[p] = 0.f;
     er.iw[p] = 1.f;
     er.tiw[p] = 1.f;
     er.tv[p] = 0.f;
@@ -868,9 +886,6 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     float retV = 0.0f;
     if (term == TRUNCATED) retV += P.gamma * outF[(long long)e * P.O];
     const long long endj = off + len - 1;
-    // the next finished episode (rank + 1) rewrites our last entry when it has one experience
-    bool own_end = true;
-    if ((unsigned long long)(rank + 1) < neps && ev.len[ev.fin_env[rank + 1]] == 1) own_end = false;
     retV = P.gamma * retV + ev.eb_rew[(long long)e * P.T + len - 1];
     // an entry overwritten later in this same batch (more new experiences
     // than the capacity) keeps the later entry's values, as the reference's
@@ -1237,8 +1252,11 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   // the first launch of every environment: sample ids 0 .. E-1
   hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->ev, h->X, 0ull,
                      (const int *)nullptr);
-  KG_HIP(hipGetLastError());
-  if (vr_read_state(h)) return 1;
+  if (hipGetLastError() != hipSuccess || vr_read_state(h)) {
+    if (!*kg::last_error()) kg::set_error("vracer: initial launches failed");
+    kg_vracer_destroy(h);
+    return 1;
+  }
   *out = h;
   return 0;
 }
@@ -1381,6 +1399,7 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
   h->use_forced_noise = 0;
   if (vr_forward(h, h->X, P.E, h->outF)) return 1;  // V of truncated states (agent.cpp.base:530-545)
   hipLaunchKernelGGL(k_vr_scan, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->ev);
+  hipLaunchKernelGGL(k_vr_evict, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er);
   hipLaunchKernelGGL(k_vr_append, dim3(P.E), dim3(256), 0, h->stream, P, h->st, h->er, h->ev, (const float *)h->outF,
                      h->X);
   KG_HIP(hipGetLastError());

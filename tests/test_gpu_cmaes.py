@@ -212,7 +212,10 @@ def test_unpack_streamed_reflector_rows_bit_exact(monkeypatch, Nv, lam):
             assert np.array_equal(dev[key], o[key]), (g, key)
 
 
-@pytest.mark.parametrize("Nv,lam,kind", [(16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
+@pytest.mark.parametrize("Nv,lam,kind", [(3, 8, "sq"), (5, 16, "sq"), (16, 64, "sq"), (67, 256, "sq"),
+                                         (128, 4096, "sq"), (16, 64, "1wg2"), (128, 4096, "1wg2"),
+                                         (40, 128, "mw2"), (100, 512, "mw2"), (129, 256, "mw2"),
+                                         (16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
                                          (40, 128, "lds")])
 def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
     """Each tridiagonalisation kernel (one workgroup with the matrix in LDS,

@@ -1,0 +1,96 @@
+// ubench_chains.hip — cycles per element of the kg_chains.hpp primitives on
+// gfx950, alone and beside other waves' LDS traffic (s_memtime ticks of
+// wave 0, 512-thread workgroup as in k_tridiag_sq).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
+//     -I korali_amd/csrc -o tools/ubench_chains tools/ubench_chains.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "kg_chains.hpp"
+
+using namespace kg::chains;
+
+__device__ __forceinline__ unsigned la(const double *p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) double *)p;
+}
+
+constexpr int LD = 129;
+
+// mode: 0 kc_add alone, 1 kc_add + 7 waves of LDS read/modify/write traffic,
+// 2 kc_nrm2 alone (no rescale), 3 kc_lock_desc on wave 0 alone,
+// 4 kc_lock_asc on wave 0 alone, 5 four lockstep waves (2 desc + 2 asc),
+// 6 dependent v_add_f64 chain in registers (reference), 7 kc_add_desc alone
+__global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, unsigned long long *ticks) {
+  extern __shared__ __attribute__((aligned(16))) double s[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double *M = s;                     // 144 x 129
+  double *w = M + 144 * LD + 32;     // vector (padded)
+  double *stage = w + 256;           // 256
+  for (int i = tid; i < 144 * LD + 32 + 256 + 256 + 64; i += 512) s[i] = 1.0 / (1 + (i % 97));
+  __syncthreads();
+  double acc = 0.0;
+  unsigned long long t0 = 0, t1 = 0;
+  const int cnt = 128;
+  if (mode == 0 || mode == 1 || mode == 2 || mode == 7) {
+    if (wid == 0) {
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) {
+        if (mode == 2) acc = kc_nrm2(acc + 1.0, la(stage), __builtin_amdgcn_readfirstlane(cnt / 16), 0ull, 0ull);
+        else if (mode == 7) acc = kc_add_desc(acc, la(stage + cnt - 16), __builtin_amdgcn_readfirstlane(cnt / 16));
+        else acc = kc_add(acc, la(stage), __builtin_amdgcn_readfirstlane(cnt / 16));
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    } else if (mode == 1) {
+      for (int r = 0; r < reps * 4; r++)
+        for (int c = lane; c < 128; c += 64) {
+          double *row = M + (size_t)(wid * 16 + (r & 15)) * LD;
+          row[c] += w[c] * w[c + 1] + row[c + 1];
+        }
+    }
+  } else if (mode == 3 || mode == 4 || mode == 5) {
+    const bool active = (mode == 5) ? wid < 4 : wid == 0;
+    if (active) {
+      const bool desc = (mode == 3) || (mode == 5 && wid < 2);
+      const int r = lane + 64 * (wid & 1);
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int k = 0; k < reps; k++) {
+        if (desc) acc += kc_lock_desc(0.0, la(w + 120), la(M + (size_t)r * LD + 120), __builtin_amdgcn_readfirstlane(cnt / 8));
+        else acc += kc_lock_asc<LD * 8>(0.0, la(w), la(M + r), __builtin_amdgcn_readfirstlane(cnt / 8));
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
+  } else if (mode == 6) {
+    if (wid == 0) {
+      double b = stage[lane];
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int k = 0; k < reps * cnt / 16; k++) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) asm volatile("v_add_f64 %0, %0, %1" : "+v"(acc) : "v"(b));
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
+  }
+  out[tid] = acc;
+  if (tid == 0) ticks[mode] = t1 - t0;
+}
+
+int main() {
+  double *out;
+  unsigned long long *ticks;
+  hipMalloc(&out, 512 * sizeof(double));
+  hipMalloc(&ticks, 16 * sizeof(unsigned long long));
+  const size_t lds = (144 * LD + 32 + 256 + 256 + 64) * sizeof(double);
+  hipFuncSetAttribute((const void *)k_bench, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int reps = 200;
+  const char *names[] = {"kc_add alone", "kc_add + 7 LDS waves", "kc_nrm2 alone", "kc_lock_desc alone",
+                         "kc_lock_asc alone", "4 lockstep waves", "register add chain", "kc_add_desc alone"};
+  for (int mode = 0; mode < 8; mode++) {
+    for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
+    hipDeviceSynchronize();
+    unsigned long long t[16];
+    hipMemcpy(t, ticks, sizeof(t), hipMemcpyDeviceToHost);
+    printf("%-24s %8.2f ticks/element\n", names[mode], (double)t[mode] / (reps * 128.0));
+  }
+  return 0;
+}
