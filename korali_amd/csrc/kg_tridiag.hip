@@ -14,7 +14,7 @@
 //   A  wave 0: the pivot row (held in registers since the previous step)
 //      is staged for dnrm2 (DPP prefix maximum, one division per element,
 //      rescale flags as ballots), the ssq chain runs (kc_nrm2), then the
-//      Householder scalars and v, tau v are written; waves 1..7 meanwhile
+//      Householder scalars and v, tau v are written; waves 1-3, 5-7 meanwhile
 //      apply the previous step's rank-2 update to the trailing block.
 //   E  dsymv: four waves, one SIMD each — waves 0/1 the descending chains
 //      of rows j < 64 / j >= 64, waves 2/3 the ascending t2 chains
@@ -22,10 +22,10 @@
 //      the strictly-upper storage, so no lane masks).
 //   X  wave 0: x = acc + tau t2, the xv chain (kc_add), alpha, x += alpha v,
 //      and the NEXT pivot row's rank-2 update straight into its registers.
-//   M  waves 1..7: rank-2 update of rows i+2.. (upper triangle + diagonal).
+//   M  waves 1-3, 5-7: rank-2 update of rows i+2.. (upper triangle + diagonal).
 //
 // Three workgroup barriers per step (after A, after E, after X).  Layout:
-// the strictly upper triangle with row stride 129 (conflict-free row and
+// the strictly upper triangle with row stride 130 (conflict-free row and
 // column walks; 16 zero rows below the matrix absorb the ascending chains'
 // read-ahead), the diagonal and all vectors padded by 16 zeros each side.
 #include "kg_chains.hpp"
@@ -33,7 +33,8 @@
 namespace kg {
 
 constexpr int SQ_TPB = 512;  // 8 waves: <= 256 VGPRs each (the chains' scratch is v[192:255])
-constexpr int SQ_LDA = 129;  // row stride for every N <= 128 (ds_read offsets are immediates)
+constexpr int SQ_LDA = 130;  // row stride for every N <= 128 (ds_read offsets are immediates);
+                             // 130: 16-byte row reads of 64 lanes hit every bank equally
 constexpr int SQ_VP = 16;    // zero padding before / after each vector (chain read-ahead)
 
 __host__ __device__ inline size_t sq_vec(int N) { return (size_t)N + 2 * SQ_VP; }
@@ -57,14 +58,16 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
                                                        double *tauOut, double *dOut, double *sdOut,
                                                        unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, nt = blockDim.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar control flow
   constexpr int lda = SQ_LDA;
   const int VS = (int)sq_vec(N);
   double *M = smem;  // strictly upper triangle, row r at r * lda; rows N .. N+15 zero
   double *vb = M + (size_t)(N + 16) * lda;
   double *dg = vb + SQ_VP;
-  double *vA[2] = {vb + (size_t)1 * VS + SQ_VP, vb + (size_t)2 * VS + SQ_VP};   // v (v_0 = 1), by column
-  double *tvA[2] = {vb + (size_t)3 * VS + SQ_VP, vb + (size_t)4 * VS + SQ_VP};  // tau v
+  // v (v_0 = 1) and tau v by column, double-buffered across steps: buffer p
+  // at vb + (1 + p) VS / vb + (3 + p) VS (plain offsets, not a pointer table,
+  // so every access stays an LDS instruction)
   double *xa = vb + (size_t)5 * VS + SQ_VP;                                      // x after daxpy
   double *xd = vb + (size_t)6 * VS;  // descending chain + diagonal term, by j (rows j >= 64)
   double *t2 = xd + 128;             // ascending chains, by j
@@ -96,23 +99,33 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
   }
   for (int i = 0; i + 2 < N; i++) {
     const int n = N - i - 1, m = n - 1, par = i & 1;
-    double *va = vA[par], *tva = tvA[par];
+    double *va = vb + (size_t)(1 + par) * VS + SQ_VP, *tva = vb + (size_t)(3 + par) * VS + SQ_VP;
     // ---- A (wave 0): dnrm2 of x, the Householder scalars, v and tau v
     if (wid == 0) {
-      const double a0 = lane < m ? fabs(R0) : 0.0, a1 = lane + 64 < m ? fabs(R1) : 0.0;
-      double pm0, pm1;
-      wave_prefix_max2_nonneg(a0, a1, pm0, pm1);
-      const double c0 = readlane_d(pm0, 63);
-      const double b0 = dpp_d<0x138, 0xf>(pm0);            // running max before element lane (lane 0: 0.0)
-      const double b1 = fmax(dpp_d<0x138, 0xf>(pm1), c0);  // before element 64 + lane
-      const bool z0 = a0 != 0.0, z1 = a1 != 0.0;           // zeros are skipped by dnrm2
-      const bool n0 = z0 && b0 < a0, n1 = z1 && b1 < a1;   // a new running maximum
+      // zeros are skipped by dnrm2; the first nonzero element's rescale,
+      // ssq = 1 + 1 (0/a)^2 = 1, is staged as the no-op addend +0.0
+      const double a0 = lane < m ? fabs(R0) : 0.0;
+      double pm0, pm1, carry;
+      unsigned long long k0, k1 = 0;
+      if (m > 64) {  // uniform: both 64-element halves
+        const double a1 = lane + 64 < m ? fabs(R1) : 0.0;
+        wave_prefix_max2_nonneg(a0, a1, pm0, pm1);
+        const double c0 = readlane_d(pm0, 63);
+        const double b1 = fmax(dpp_d<0x138, 0xf>(pm1), c0);  // running max before element 64 + lane
+        const bool z1 = a1 != 0.0 && b1 != 0.0, n1 = z1 && b1 < a1;
+        const double q1 = (z1 ? (n1 ? b1 : a1) : 0.0) / (z1 ? (n1 ? a1 : b1) : 1.0);
+        k1 = __ballot(n1);
+        sv[64 + lane] = n1 ? q1 : q1 * q1;
+        carry = fmax(c0, readlane_d(pm1, 63));
+      } else {
+        pm0 = wave_prefix_max_nonneg(a0);
+        carry = readlane_d(pm0, 63);
+      }
+      const double b0 = dpp_d<0x138, 0xf>(pm0);  // running max before element lane (lane 0: 0.0)
+      const bool z0 = a0 != 0.0 && b0 != 0.0, n0 = z0 && b0 < a0;  // n: a new running maximum
       const double q0 = (z0 ? (n0 ? b0 : a0) : 0.0) / (z0 ? (n0 ? a0 : b0) : 1.0);
-      const double q1 = (z1 ? (n1 ? b1 : a1) : 0.0) / (z1 ? (n1 ? a1 : b1) : 1.0);
-      const unsigned long long k0 = __ballot(n0), k1 = __ballot(n1);
+      k0 = __ballot(n0);
       sv[lane] = n0 ? q0 : q0 * q0;  // elements >= m: +0.0 (no-ops of the chain)
-      sv[64 + lane] = n1 ? q1 : q1 * q1;
-      const double carry = fmax(c0, readlane_d(pm1, 63));
       SQ_MARK(0)
       const double ssq = chains::kc_nrm2(1.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
       const double xnorm = (m == 1) ? fabs(readlane_d(R0, 0)) : carry * sqrt(ssq);
@@ -132,6 +145,7 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int e = lane + 64 * h;
+        if (h == 1 && m <= 64) break;  // uniform
         if (e < m) {
           double t = h ? R1 : R0;
           if (branch != 0) {
@@ -201,22 +215,25 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       const int ca = i + 3 + lane, cb = i + 67 + lane;
       const double ma = ca < N ? row1[ca] : 0.0, mb = cb < N ? row1[cb] : 0.0, malpha = row1[i + 2];
       const double vca = va[ca], vcb = va[cb], valpha = va[i + 2], dgr1 = dg[r1];
+      const bool two = n > 64;  // uniform: a second 64-row half
       double x0 = 0.0, x1 = 0.0, v0 = 0.0, v1 = 0.0;
       if (lane < n) {
         x0 = xdj + tau_i * t2[lane];
         v0 = va[r1 + lane];
       }
-      if (lane + 64 < n) {
-        x1 = xd[64 + lane] + tau_i * t2[64 + lane];
-        v1 = va[r1 + 64 + lane];
-      }
       sv[lane] = x0 * v0;  // +0.0 past the block
-      sv[64 + lane] = x1 * v1;
+      if (two) {
+        if (lane + 64 < n) {
+          x1 = xd[64 + lane] + tau_i * t2[64 + lane];
+          v1 = va[r1 + 64 + lane];
+        }
+        sv[64 + lane] = x1 * v1;
+      }
       const double xv = chains::kc_add(0.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4));
       const double als = -(tau_i / 2.0) * xv;
-      const double xf0 = x0 + als * v0, xf1 = x1 + als * v1;
+      const double xf0 = x0 + als * v0;
       if (lane < n) xa[r1 + lane] = xf0;
-      if (lane + 64 < n) xa[r1 + 64 + lane] = xf1;
+      if (two && lane + 64 < n) xa[r1 + 64 + lane] = x1 + als * v1;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -225,20 +242,45 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       const double nvr = -1.0 * 1.0, nxr = -1.0 * xr1;
       alpha = malpha + (nvr * xa[i + 2] + nxr * valpha);
       R0 = ca < N ? ma + (nvr * xa[ca] + nxr * vca) : 0.0;
-      R1 = cb < N ? mb + (nvr * xa[cb] + nxr * vcb) : 0.0;
+      R1 = (n > 65 && cb < N) ? mb + (nvr * xa[cb] + nxr * vcb) : 0.0;  // (next step's x_e, e >= 64)
       if (lane == 0) dg[r1] = dgr1 + (nvr * xr1 + nxr * 1.0);
     }
     SQ_MARK(6)
     __syncthreads();
     SQ_MARK(7)
-    // ---- M (waves 1..7): rank-2 update of rows i+2.. (upper triangle) and their diagonal
-    if (wid > 0) {
-      for (int r = i + 2 + (wid - 1); r < N; r += 7) {
-        const double nvr = -1.0 * va[r], nxr = -1.0 * xa[r];
-        double *row = M + (size_t)r * lda;
-        for (int c = r + 1 + lane; c < N; c += 64) row[c] += nvr * xa[c] + nxr * va[c];
+    // ---- M (waves 1-3, 5-7; wave 4 shares wave 0's SIMD and stays idle):
+    // rank-2 update of rows i+2.. (upper triangle) and their diagonal
+    if (wid != 0 && wid != 4) {
+      const int wk = wid < 4 ? wid - 1 : wid - 2;  // 0..5
+      // lane = columns c0, c0 + 64 (fixed), rows r = i+2+wk, +6, ...: the
+      // next row's operands are loaded while the current row is updated
+      // (a lane whose column is on/below the diagonal or past N stores into
+      // a dump slot instead of being masked off, no exec-mask branches: row
+      // i, which nothing reads after this step's A phase)
+      const int c0 = i + 3 + lane, c1 = c0 + 64;
+      const double xc0 = xa[c0], vc0 = va[c0], xc1 = xa[c1], vc1 = va[c1];
+      const unsigned dump0 = lds_addr(M + (size_t)i * lda + lane), dump1 = dump0 + 64 * 8;
+      const int r0 = i + 2 + wk;
+      if (r0 < N) {
+        const double *vr = va + r0, *xr = xa + r0;
+        double *row = M + (size_t)r0 * lda;
+        // operands of row r + 6 are loaded before row r is stored (raw: the
+        // negations happen at use, so no load is waited for in its own iteration)
+        double v_ = vr[0], x_ = xr[0], m0 = row[c0], m1 = row[c1];
+#pragma unroll 2
+        for (int r = r0; r < N; r += 6) {
+          vr += 6, xr += 6;
+          double *rown = row + 6 * lda;  // (rows up to N+5 exist: the zero rows)
+          const double vn = vr[0], xn = xr[0], m0n = rown[c0], m1n = rown[c1];
+          const double nv = -1.0 * v_, nx = -1.0 * x_;
+          const unsigned a0 = (c0 > r && c0 < N) ? lds_addr(row + c0) : dump0;
+          const unsigned a1 = (c1 > r && c1 < N) ? lds_addr(row + c1) : dump1;
+          *(__attribute__((address_space(3))) double *)(size_t)a0 = m0 + (nv * xc0 + nx * vc0);
+          *(__attribute__((address_space(3))) double *)(size_t)a1 = m1 + (nv * xc1 + nx * vc1);
+          v_ = vn, x_ = xn, m0 = m0n, m1 = m1n, row = rown;
+        }
       }
-      const int qd = tid - 64;
+      const int qd = wk * 64 + lane;
       if (qd < n - 1) {
         const int r = i + 2 + qd;
         const double nvr = -1.0 * va[r], nxr = -1.0 * xa[r];
@@ -263,7 +305,7 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
 // owner), everything else of the step recomputed redundantly by every
 // workgroup with identical operands.  Compared with k_tridiag_mw (same
 // decomposition) the step's chains run on the kg_chains.hpp primitives:
-//   dnrm2: staged by all four waves (64-element chunks, DPP prefix maxima,
+//   dnrm2: staged by all eight waves (64-element chunks, DPP prefix maxima,
 //          chunk maxima exchanged through LDS), the ssq chain on wave 0
 //          (kc_nrm2, 128 elements per call);
 //   dsymv: products staged zero-padded per row (descending and ascending
@@ -271,7 +313,7 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
 //   xv:    kc_add over the staged products;
 //   x += alpha v is not stored: the rank-2 update recomputes x_f = x + alpha v
 //          per operand (the same rounded value every time).
-constexpr int MW2_TPB = 256;
+constexpr int MW2_TPB = 512;
 constexpr int MW2_PAD = 32;  // zero padding on each side of a staged product row
 __host__ __device__ inline size_t mw2_ps(int N) { return (size_t)N + 2 * MW2_PAD; }
 __host__ __device__ inline size_t mw2_lds_doubles(int N, int RW) {
@@ -294,7 +336,8 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
                                                          unsigned long long *comm, unsigned int *errors,
                                                          unsigned long long *trace) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, nt = blockDim.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar control flow
   const int P = gridDim.x, g = blockIdx.x, RW = (N + P - 1) / P, lda = N + 1, PS = (int)mw2_ps(N);
   double *M = smem;                            // local row k = global row g + k P
   double *Pd = M + (size_t)RW * lda + MW2_PAD;  // descending products of local row k at Pd + k PS, by column
@@ -343,26 +386,26 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
       for (int c = i + 2 + tid; c < N; c += nt) put_granule_dbl(growp + 2 * c, tag, row[c]);
     }
     // ---- dnrm2 staging of x_e = prow[i+2+e], e < m, over 64-element chunks:
-    // chunk k on wave k % 4; chunk maxima through LDS; elements up to the
+    // chunk k on wave k % 8; chunk maxima through LDS; elements up to the
     // next multiple of 16 past m staged as +0.0
     const int nch = (m + 63) >> 6;
-    double pmk[4], ak[4];
+    double pmk[2], ak[2];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int k = wid + 4 * u, e = 64 * k + lane;
+    for (int u = 0; u < 2; u++) {
+      const int k = wid + 8 * u, e = 64 * k + lane;
       ak[u] = (k < nch && e < m) ? fabs(prow[i + 2 + e]) : 0.0;
       pmk[u] = wave_prefix_max_nonneg(ak[u]);
       if (k < nch && lane == 63) cmx[k] = pmk[u];
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int k = wid + 4 * u;
+    for (int u = 0; u < 2; u++) {
+      const int k = wid + 8 * u;
       if (k < nch) {  // uniform
         double carry = 0.0;
         for (int k2 = 0; k2 < k; k2++) carry = fmax(carry, cmx[k2]);
         const double a = ak[u], b = fmax(dpp_d<0x138, 0xf>(pmk[u]), carry);
-        const bool z = a != 0.0, nf = z && b < a;
+        const bool z = a != 0.0 && b != 0.0, nf = z && b < a;  // (first nonzero: no-op +0.0)
         const double qv = (z ? (nf ? b : a) : 0.0) / (z ? (nf ? a : b) : 1.0);
         const unsigned long long bm = __ballot(nf);
         sv[64 * k + lane] = nf ? qv : qv * qv;
@@ -458,7 +501,7 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
     MW2_MARK(4)
     if (tau_i != 0.0) {
       // ---- dsymv chains: one wave per chain (descending / ascending of each owned row)
-      for (int ch = wid; ch < 2 * RW; ch += 4) {
+      for (int ch = wid; ch < 2 * RW; ch += 8) {
         const int k = ch < RW ? ch : ch - RW, r = g + k * P;
         if (r <= i || r >= N) continue;  // uniform
         if (ch < RW) {

@@ -2,13 +2,14 @@
 GSL-order tridiagonalisation as hand-scheduled gfx950 inline assembly.
 
 Why assembly: an ordered double-precision sum is a chain of dependent
-v_add_f64 (8.3 cycles each on MI355X).  A wave issues at most one
-instruction per 4-cycle slot, so everything else the chain needs (its LDS
-loads, address updates, loop control) has to sit in the stall slots between
-two dependent adds, and no wait may stand in front of an add whose operand
-landed long ago.  The compiler's schedule for the same C++ waited before
-every add and branched per element (kg_eigen.hip's round-2 kernels: 20-44
-cycles per element); these loops issue 1.5-3.5 instructions per element.
+v_add_f64.  Measured on MI355X (tools/ubench_chains.hip): ONE wave issues a
+v_add_f64 every ~9.3 cycles whether or not the adds depend on each other
+(4 independent chains: 9.8 cycles per add), so a chain is bound by the
+instruction count of the wave that runs it, ~8-10 cycles per instruction of
+any kind.  These loops therefore carry nothing but the adds, one ds_read2
+per two elements and a few scalar instructions per 16 (kc_add: 15.4 cycles
+per element alone; the compiler's schedule of the same C++ waited and
+branched per element: 20-44).
 
 Each primitive runs whole groups (8 or 16 elements) and relies on the caller
 padding the staged values with +0.0 (an exact no-op for every chain here:
@@ -117,57 +118,58 @@ __device__ __forceinline__ double kc_add_desc(double acc, unsigned p, unsigned g
 
 
 def emit_nrm2():
-    """gslcblas dnrm2's ssq recurrence: element e is ssq += t_e, or (mask bit
-    e set: a new running maximum) ssq = 1 + ssq t_e t_e.  Groups of 16; the
-    16 mask bits of a group select the fast (adds only) or the slow path."""
-    L = ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f",
-         "s_mov_b64 %[m], %[k0]", "s_mov_b32 %[wc], 4"]
-    for k in range(8):
+    """gslcblas dnrm2's ssq recurrence over a block of up to 128 elements,
+    fully unrolled (static LDS offsets, no address updates): element e is
+    ssq += t_e, or (mask bit e set: a new running maximum) ssq = 1 + ssq t_e
+    t_e.  Per 8-element half-group: one s_and_b32 on its 32-bit mask word
+    (SCC = any rescale) and a branch; a half without rescales is 8 plain adds,
+    a half with them tests each element (rescale bodies out of line).  The
+    block ends after 16 g elements (one s_cmp + branch per 16)."""
+    L = []
+    words = ["%[k0l]", "%[k0h]", "%[k1l]", "%[k1h]"]
+    for k in range(8):  # halves 0, 1 in flight
         L.append(f"ds_read2_b64 {q(k)}, %[p] offset0:{2 * k} offset1:{2 * k + 1}")
-    L.append("1:")
-    L += ["s_and_b64 %[t], %[m], 0xffff", "s_lshr_b64 %[m], %[m], 16", "s_cmp_eq_u64 %[t], 0", "s_cbranch_scc0 5f"]
-    # fast path: 16 plain adds, reloads interleaved (as kc_add)
-    for half in range(2):
+    slow = []
+    for hf in range(16):
+        st = 8 * (hf % 2)  # register slots of this half
+        w, sh = words[hf // 4], 8 * (hf % 4)
+        if hf % 2 == 0:
+            L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
         L.append("s_waitcnt lgkmcnt(4)")
+        L += [f"s_and_b32 %[t], {w}, {hex(0xff << sh)}", f"s_cbranch_scc1 {100 + hf}f"]
+        nxt = [f"ds_read2_b64 {q(4 * (hf % 2) + k)}, %[p] offset0:{16 * (hf // 2 + 1) + 8 * (hf % 2) + 2 * k} "
+               f"offset1:{16 * (hf // 2 + 1) + 8 * (hf % 2) + 2 * k + 1}" for k in range(4)]
         for t in range(8):
-            L.append(f"v_add_f64 %[acc], %[acc], {d(8 * half + t)}")
+            L.append(f"v_add_f64 %[acc], %[acc], {d(st + t)}")
             if t % 2 == 1:
-                k = 4 * half + t // 2
-                L.append(f"ds_read2_b64 {q(k)}, %[p] offset0:{16 + 2 * k} offset1:{17 + 2 * k}")
-    L.append("s_branch 6f")
-    # slow path: per-element test of the mask bit, reloads after the group
-    L.append("5:")
-    L.append("s_waitcnt lgkmcnt(4)")
-    for u in range(16):
-        if u == 8:
-            L.append("s_waitcnt lgkmcnt(0)")
-        L += [f"s_bitcmp1_b64 %[t], {u}", f"s_cbranch_scc1 {20 + u}f",
-              f"v_add_f64 %[acc], %[acc], {d(u)}", f"s_branch {40 + u}f",
-              f"{20 + u}:",
-              f"v_mul_f64 %[tmp], %[acc], {d(u)}", f"v_mul_f64 %[tmp], %[tmp], {d(u)}",
-              "v_add_f64 %[acc], 1.0, %[tmp]",
-              f"{40 + u}:"]
-    for k in range(8):
-        L.append(f"ds_read2_b64 {q(k)}, %[p] offset0:{16 + 2 * k} offset1:{17 + 2 * k}")
-    L.append("6:")
-    L += ["v_add_u32 %[p], 0x80, %[p]",
-          "s_sub_u32 %[g], %[g], 1", "s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f",
-          "s_sub_u32 %[wc], %[wc], 1", "s_cmp_lg_u32 %[wc], 0", "s_cbranch_scc1 1b",
-          "s_mov_b64 %[m], %[k1]", "s_mov_b32 %[wc], 4", "s_branch 1b",
-          "9:", "s_waitcnt lgkmcnt(0)"]
+                L.append(nxt[t // 2])
+        L.append(f"{200 + hf}:")
+        # out-of-line slow half
+        slow.append(f"{100 + hf}:")
+        for t in range(8):
+            slow += [f"s_bitcmp1_b32 {w}, {sh + t}", f"s_cbranch_scc1 {300 + 8 * hf + t}f",
+                     f"v_add_f64 %[acc], %[acc], {d(st + t)}", f"{500 + 8 * hf + t}:"]
+        slow += nxt + [f"s_branch {200 + hf}b"]
+        for t in range(8):
+            slow += [f"{300 + 8 * hf + t}:",
+                     f"v_mul_f64 %[tmp], %[acc], {d(st + t)}", f"v_mul_f64 %[tmp], %[tmp], {d(st + t)}",
+                     "v_add_f64 %[acc], 1.0, %[tmp]", f"s_branch {500 + 8 * hf + t}b"]
+    L += ["s_branch 9f"] + slow + ["9:", "s_waitcnt lgkmcnt(0)"]
     return f"""
 // gslcblas dnrm2's ssq recurrence over p[0 .. 16 g) (g <= 8): element e is a
-// new running maximum where bit e of (k1:k0) is set, ssq = 1 + (ssq t) t,
-// else ssq += t (GSL's operation order; SURVEY.md Appendix A)
+// new running maximum where bit e of the 128-bit mask (k1h:k1l:k0h:k0l) is
+// set, ssq = 1 + (ssq t) t, else ssq += t (GSL's operation order; SURVEY.md
+// Appendix A).  Loads run 16 elements past the block.
 __device__ __forceinline__ double kc_nrm2(double acc, unsigned p, unsigned g, unsigned long long k0,
                                           unsigned long long k1) {{
-  unsigned long long m, t;
-  unsigned wc;
+  const unsigned k0l = __builtin_amdgcn_readfirstlane((unsigned)k0), k0h = __builtin_amdgcn_readfirstlane((unsigned)(k0 >> 32));
+  const unsigned k1l = __builtin_amdgcn_readfirstlane((unsigned)k1), k1h = __builtin_amdgcn_readfirstlane((unsigned)(k1 >> 32));
+  unsigned t;
   double tmp;
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [p] "+v"(p), [g] "+s"(g), [m] "=&s"(m), [t] "=&s"(t), [wc] "=&s"(wc), [tmp] "=&v"(tmp)
-      : [k0] "s"(k0), [k1] "s"(k1)
+      : [acc] "+v"(acc), [g] "+s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp)
+      : [p] "v"(p), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
       : "scc", "memory", {CLOBBER});
   return acc;
 }}

@@ -60,6 +60,31 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
       }
       t1 = __builtin_amdgcn_s_memtime();
     }
+  } else if (mode == 8 || mode == 9) {
+    if (wid == 0) {
+      double b = stage[lane], c = b * 0.5, d = b * 0.25, e = b * 0.125, m_ = 1.0000001, tmp;
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int k = 0; k < reps * cnt / 16; k++) {
+        if (mode == 8) {  // 4 independent add chains: issue rate of v_add_f64 (16 adds = 4 elements of each)
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            asm volatile("v_add_f64 %0, %0, %4\n v_add_f64 %1, %1, %4\n v_add_f64 %2, %2, %4\n v_add_f64 %3, %3, %4"
+                         : "+v"(acc), "+v"(c), "+v"(d), "+v"(e) : "v"(b));
+        } else {  // product formed inline: v_mul_f64 + dependent v_add_f64 per element
+#pragma unroll
+          for (int u = 0; u < 16; u++) asm volatile("v_mul_f64 %1, %2, %3\n v_add_f64 %0, %0, %1" : "+v"(acc), "=&v"(tmp) : "v"(b), "v"(m_));
+        }
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+      acc += c + d + e;
+    }
+  } else if (mode == 10 || mode == 11) {  // kc_add on waves 0-3 (10) or on waves 0 and 4 (11) at once
+    const bool active = mode == 10 ? wid < 4 : (wid == 0 || wid == 4);
+    if (active) {
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) acc = kc_add(acc, la(stage), __builtin_amdgcn_readfirstlane(cnt / 16));
+      t1 = __builtin_amdgcn_s_memtime();
+    }
   } else if (mode == 6) {
     if (wid == 0) {
       double b = stage[lane];
@@ -84,8 +109,10 @@ int main() {
   hipFuncSetAttribute((const void *)k_bench, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int reps = 200;
   const char *names[] = {"kc_add alone", "kc_add + 7 LDS waves", "kc_nrm2 alone", "kc_lock_desc alone",
-                         "kc_lock_asc alone", "4 lockstep waves", "register add chain", "kc_add_desc alone"};
-  for (int mode = 0; mode < 8; mode++) {
+                         "kc_lock_asc alone", "4 lockstep waves", "register add chain", "kc_add_desc alone",
+                         "4 indep. add chains (per add)", "inline mul+add chain", "kc_add on waves 0-3",
+                         "kc_add on waves 0 and 4"};
+  for (int mode = 0; mode < 12; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
     unsigned long long t[16];
