@@ -44,8 +44,10 @@ STAGE_FLOPS = {
     "eigen_unpack": 2.0 * N_VARS ** 3,
     "eigen_apply": 6.0 * 1.1 * N_VARS ** 3,
     "transform": 2.0 * LAMBDA * N_VARS ** 2,
-    "covariance": 2.0 * MU * N_VARS ** 2,  # full-GEMM count of the rank-mu sum
-    "rankmu_mfma": 2.0 * MU * N_VARS ** 2,
+    # rank-mu sum: the SYRK count mu N (N+1) (the lower triangle and the
+    # diagonal, 2 flops per term), not the full-GEMM 2 mu N^2
+    "covariance": 1.0 * MU * N_VARS * (N_VARS + 1),
+    "rankmu_mfma": 1.0 * MU * N_VARS * (N_VARS + 1),
     "objective": 8.0 * LAMBDA * N_VARS,
 }
 
@@ -54,7 +56,8 @@ STAGE_FLOPS = {
 STAGE_KERNELS = {
     # a tuple lists alternatives (the kernel the size selects); template
     # instances match their base name
-    "eigen_tridiag": [("kg::k_tridiag_1wg2", "kg::k_tridiag_1wg", "kg::k_tridiag_mw", "kg::k_tridiag")],
+    "eigen_tridiag": [("kg::k_tridiag_sq", "kg::k_tridiag_mw2", "kg::k_tridiag_1wg2", "kg::k_tridiag_1wg",
+                       "kg::k_tridiag_mw", "kg::k_tridiag")],
     "eigen_unpack": [("kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
     "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
     "covariance": [("kg::k_adaptC_exact2", "kg::k_adaptC_combine")],
@@ -95,14 +98,20 @@ def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
 
 def rankmu_roofline(ms, mu, n, csv_name):
     """The rank-mu MFMA kernel (k_rankmu_tile) against the FP64 matrix peak:
-    algorithmic work 2 mu N^2 (the full-GEMM count; the kernel forms only the
-    lower tiles), HIP events around its launch on its own stream."""
-    flops = 2.0 * mu * n * n
+    algorithmic work = the SYRK count mu N (N+1) (lower triangle with the
+    diagonal, 2 flops per term); the kernel executes the lower 64x64 tiles
+    (executed_flops_per_launch, slightly more: the diagonal tiles' upper
+    halves); HIP events around its launch on its own stream."""
+    flops = 1.0 * mu * n * (n + 1)
+    nt = (n + 63) // 64
+    executed = nt * (nt + 1) // 2 * 64 * 64 * 2.0 * mu
     achieved = flops / (ms * 1e-3) / 1e12
     traffic, raw = pmc_traffic("rankmu_mfma", csv_name)
     return {"kernel": "kg::k_rankmu_tile", "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "avg_launch_ms": ms,
-            "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": 8.0 * (mu * n + n * n),
+            "algorithmic_flops_per_launch": flops, "executed_flops_per_launch": executed,
+            "executed_frac": executed / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+            "algorithmic_bytes_per_launch": 8.0 * (mu * n + n * n),
             "traffic": traffic, "traffic_source": f"profiles/{PROFILE_ROUND}/{csv_name}" if traffic else None}
 
 
@@ -397,9 +406,11 @@ def main():
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
-        "roofline": {"kernel": dominant, "bound": "mfma",
-                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the kernel is a "
-                                   "dependent FP64 VALU chain (GSL operation order), far below it by construction",
+        "roofline": {"kernel": {"min_search": "kg::k_tm_nm_search"}.get(dominant, dominant), "stage": dominant,
+                     "bound": "mfma",
+                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is a "
+                                   "chain of dependent rounds (GSL nmsimplex order, two cross-XCD hand-offs per "
+                                   "round), far below it by construction",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_raw_fetch": traffic_raw,
@@ -515,8 +526,16 @@ def run_c3(args):
               "device_search_relaunches": dev["Device Search Relaunches"][0]}
     dev.close()
     flops = c3_stage_flops(C3_N, C3_P)
+    # the annealing search (k_tm_nm_search): per simplex round at least two
+    # candidate points, each P exponentials (~20 flops) + the weight sums'
+    # double-double accumulation (~6 flops) per chain
+    flops["min_search"] = search["device_search_rounds_per_generation"] * 2 * C3_P * 26.0
+    # the dominant stage by time among every stage (GPU time; the annealing
+    # search is the largest since the device search replaced the host loop)
     kernels = {k: v for k, v in stages.items() if k in flops}
-    dominant = max(kernels, key=kernels.get)
+    dominant = max(stages, key=stages.get)
+    if dominant not in flops:
+        dominant = max(kernels, key=kernels.get)
     achieved = flops[dominant] / (stages[dominant] * 1e-3) / 1e12
     c3_traffic, _ = pmc_traffic(dominant, "c3_pmc_traffic.csv")
     out = {
@@ -530,9 +549,11 @@ def run_c3(args):
         "chain_steps_per_sec": done * C3_P / elapsed,
         "stage_ms": stages,
         "annealing_search": search,
-        "roofline": {"kernel": dominant, "bound": "mfma",
-                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the kernel is a "
-                                   "dependent FP64 VALU chain (GSL operation order), far below it by construction",
+        "roofline": {"kernel": {"min_search": "kg::k_tm_nm_search"}.get(dominant, dominant), "stage": dominant,
+                     "bound": "mfma",
+                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is a "
+                                   "chain of dependent rounds (GSL nmsimplex order, two cross-XCD hand-offs per "
+                                   "round), far below it by construction",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": c3_traffic,
                      "traffic_source": f"profiles/{PROFILE_ROUND}/c3_pmc_traffic.csv" if c3_traffic else None,

@@ -19,6 +19,7 @@
 
 #include "../../include/korali_amd.h"
 #include "kg_common.hpp"
+#include "kg_chains.hpp"
 #include "kg_eigen.hpp"
 #include "kg_rng.hpp"
 #include <chrono>
@@ -829,6 +830,116 @@ __global__ void __launch_bounds__(256) k_mean(int N, int mu, const double *__res
   }
 }
 
+// k_mean on the chain primitive: lane c of wave 0 adds w_i y_(i),d0+c in
+// selection order (kc_add: ~15 cycles per product); waves 1-3 stage the next
+// MN2_R products of the 8 dimensions into the other half of a double-buffered
+// LDS ring (transposed: dimension-major, zero past mu) while the chain runs.
+constexpr int MN2_R = 1024, MN2_RS = MN2_R + 32;  // rows per chunk; row stride (the chain reads up to 31 ahead)
+size_t mean2_lds_bytes() { return 2 * (size_t)MN_D * MN2_RS * sizeof(double); }
+__global__ void __launch_bounds__(256) k_mean2(int N, int mu, const double *__restrict__ Y,
+                                               const double *__restrict__ w, double *mean, double *prevMean,
+                                               double *meanUpdate, const CmaesScalars *__restrict__ sc) {
+  extern __shared__ __attribute__((aligned(16))) double pbuf[];  // [2][MN_D][MN2_RS]
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int d0 = blockIdx.x * MN_D;
+  const int nd = (N - d0) < MN_D ? (N - d0) : MN_D;
+  const int nchunks = (mu + MN2_R - 1) / MN2_R;
+  auto stage = [&](int chunk, int t0, int nt) {
+    double *b = pbuf + (size_t)(chunk & 1) * MN_D * MN2_RS;
+    for (int e = t0; e < MN_D * MN2_R; e += nt) {
+      const int r = e >> 3, c = e & 7, i = chunk * MN2_R + r;
+      b[(size_t)c * MN2_RS + r] = (i < mu && c < nd) ? w[i] * Y[(size_t)i * N + d0 + c] : 0.0;
+    }
+  };
+  stage(0, tid, 256);
+  __syncthreads();
+  double acc = 0.0;
+  const int c = lane < nd ? lane : 0;
+  for (int ch = 0; ch < nchunks; ch++) {
+    if (wid == 0) {
+      const int rn = min(MN2_R, mu - ch * MN2_R);
+      const double *b = pbuf + (size_t)(ch & 1) * MN_D * MN2_RS + (size_t)c * MN2_RS;
+      acc = chains::kc_add(acc, lds_addr(b), __builtin_amdgcn_readfirstlane((unsigned)(rn + 15) >> 4));
+    } else if (ch + 1 < nchunks) {
+      stage(ch + 1, tid - 64, 192);
+    }
+    __syncthreads();
+  }
+  if (wid == 0 && lane < nd) {
+    const int d = d0 + lane;
+    const double prev = prevMean[d];  // copied by k_gather_selected
+    mean[d] = acc;
+    meanUpdate[d] = (acc - prev) / sc->sigma;
+  }
+}
+
+// evolution paths for N <= 128 (full covariance): B staged once in LDS (row
+// stride 129: column and row walks both conflict-free), the two ordered
+// matrix-vector chains and the |p_sigma| chain on the chain primitives.
+constexpr int PA2_LD = 129;
+size_t paths2_lds_bytes(int N) { return ((size_t)(N + 16) * PA2_LD + 3 * (size_t)(N + 32)) * sizeof(double); }
+__global__ void __launch_bounds__(256) k_paths2(int N, unsigned long long gen, const double *__restrict__ B,
+                                                const double *__restrict__ D, const double *__restrict__ meanUpdate,
+                                                double *auxBDZ, double *ps, double *pc, CmaesScalars *sc) {
+  extern __shared__ __attribute__((aligned(16))) double psm[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double *Bs = psm;                                // (N+16) x 129, zero padded
+  double *sv = Bs + (size_t)(N + 16) * PA2_LD;     // mean update, zero past N
+  double *aux = sv + N + 32;                       // D^-1 B^T (mean update), zero past N
+  double *pn = aux + N + 32;                       // p_sigma squares, zero past N
+  __shared__ int hs;
+  const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
+  for (int q = tid; q < (N + 16) * PA2_LD; q += 256) {
+    const int e = q / PA2_LD, d = q - e * PA2_LD;
+    Bs[q] = (e < N && d < N) ? B[(size_t)e * N + d] : 0.0;
+  }
+  for (int q = tid; q < 3 * (N + 32); q += 256) sv[q] = (q < N) ? meanUpdate[q] : 0.0;
+  __syncthreads();
+  const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)(N + 7) >> 3);
+  const int d = lane + 64 * (wid & 1);  // waves 0-1: rows d < 128
+  // aux[d] = (sum_e B[e][d] mu[e]) / D[d]   (CMAES.cpp.base:627-636)
+  if (wid < 2) {
+    const double a1 = chains::kc_lock_asc<PA2_LD * 8>(0.0, lds_addr(sv), lds_addr(Bs + d), nb);
+    if (d < N) {
+      const double a = a1 / D[d];
+      aux[d] = a;
+      auxBDZ[d] = a;
+    }
+  }
+  __syncthreads();
+  // p_sigma = (1-c_s) p_sigma + sqrt(c_s (2-c_s) mu_eff) sum_e B[d][e] aux[e]   (:641-656)
+  const double fac = sqrt(cs * (2. - cs) * effMu);
+  if (wid < 2) {
+    const double sum = chains::kc_lock_asc<8>(0.0, lds_addr(aux), lds_addr(Bs + (size_t)d * PA2_LD), nb);
+    if (d < N) {
+      const double p = (1. - cs) * ps[d] + fac * sum;
+      ps[d] = p;
+      pn[d] = p * p;  // std::pow(x, 2.0) == x*x (CR)
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    const double nrm2 = chains::kc_add(0.0, lds_addr(pn), __builtin_amdgcn_readfirstlane((unsigned)(N + 15) >> 4));
+    if (lane == 0) {
+      const double nrm = sqrt(nrm2);
+      sc->psNorm = nrm;
+      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+                                                   sc->chiSquareNumber);
+      hs = hsig;
+      sc->hsig = hsig;
+      const double a = N + 1.3, b = N + 2.0;
+      const double ccov1 = 2.0 / (a * a + effMu);
+      double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (b * b + effMu);
+      if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+      sc->ccov1 = ccov1;
+      sc->ccovmu = ccovmu;
+    }
+  }
+  __syncthreads();
+  const double fac2 = sqrt(cc * (2. - cc) * effMu);
+  for (int q = tid; q < N; q += 256) pc[q] = (1. - cc) * pc[q] + hs * fac2 * meanUpdate[q];
+}
+
 // evolution paths :626-662 (+ the adaptC constants :693-694).  Both
 // matrix-vector products keep the reference's sequential e-order per output;
 // B is staged through LDS in column chunks so row sweeps stay coalesced.
@@ -1622,6 +1733,11 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)
       KG_HIP(hipFuncSetAttribute((const void *)k_paths, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pbytes));
+    KG_HIP(hipFuncSetAttribute((const void *)k_mean2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)mean2_lds_bytes()));
+    if (N <= 128)
+      KG_HIP(hipFuncSetAttribute((const void *)k_paths2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)paths2_lds_bytes(N)));
   }
   if (rc) {
     delete h;
@@ -1866,6 +1982,12 @@ static int cmaes_publish_summary(kg_cmaes_t h) {
 
 static int cmaes_paths(kg_cmaes_t h, size_t generation) {
   const int N = h->N;
+  if (N <= 128 && !h->cfg.diagonal_covariance) {
+    hipLaunchKernelGGL(k_paths2, dim3(1), dim3(256), paths2_lds_bytes(N), h->stream, N, (unsigned long long)generation,
+                       h->B, h->D, h->meanUpdate, h->auxBDZ, h->ps, h->pc, h->sc);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
   const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
   hipLaunchKernelGGL(k_paths, dim3(1), dim3(N <= 1024 ? ((N + 63) / 64) * 64 : 1024), pbytes, h->stream, N,
                      h->cfg.diagonal_covariance, (unsigned long long)generation, h->B, h->D, h->meanUpdate,
@@ -1901,8 +2023,8 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
     KG_HIP(hipEventRecord(h->evC, h->stream2));
-    hipLaunchKernelGGL(k_mean, dim3((N + MN_D - 1) / MN_D), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
-                       h->prevMean, h->meanUpdate, h->sc);
+    hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu, h->Y,
+                       h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     if (h->G)
       hipLaunchKernelGGL(k_mean_gradient, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->cfg.gradient_step_size,
                          h->G, h->idx, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);

@@ -2932,10 +2932,21 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     const unsigned long long seq = ++chaseSeq;
     if (prof) prof(profCtx, "eigen_apply", 0);
     EigRec mr = hmap;
-    // one workgroup per 16 rows + the fetcher workgroup
-    hipLaunchKernelGGL(k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1), dim3(APPLY_TPB), apply_lds_bytes(N),
-                       s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace, dprogDev, seq, mr, dprog);
-    KG_HIP(hipGetLastError());
+    // one workgroup per 16 rows + the fetcher workgroup; the row workgroups
+    // spin on the fetcher's progress word, so the grid is launched
+    // cooperatively (co-residency guaranteed, or the launch fails)
+    {
+      int N_ = N;
+      const double *gQt_ = gQt;
+      double *B_ = B, *D_ = D, *minEig_ = minEig, *maxEig_ = maxEig, *eigenFailures_ = eigenFailures;
+      unsigned int *errors_ = errors;
+      unsigned long long *trace_ = trace, *dprogDev_ = dprogDev, *dprog_ = dprog;
+      unsigned long long seq_ = seq;
+      void *args[] = {&N_, &gQt_, &devRec, &B_, &D_, &minEig_, &maxEig_, &eigenFailures_, &errors_, &trace_,
+                      &dprogDev_, &seq_, &mr, &dprog_};
+      KG_HIP(hipLaunchCooperativeKernel((const void *)k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1),
+                                        dim3(APPLY_TPB), args, apply_lds_bytes(N), s));
+    }
     if (prof) prof(profCtx, "eigen_dsd_wait", 2);
     {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)
       const auto t0 = std::chrono::steady_clock::now();
