@@ -20,12 +20,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KORALI_AMD_ARCH", "gfx950")
 # -ffp-contract=off: no implicit FMA anywhere (bit-faithful replay of the
 # reference's x86-64 SSE2 double arithmetic); explicit fma() is kept.
-# -amdgpu-sdwa-peephole=false: no SDWA (sub-dword addressing) forms.  The
-# peephole emitted v_xor_b32_sdwa in exactly one kernel (the CartPole reset's
-# mt19937 tempering) and that kernel memory-faulted on MI355X with arguments
-# verified intact; with plain VOP2 forms it runs.
+# (No SDWA flag: the two places the SDWA peephole used to fire — the
+# CartPole reset's tempering and k_vr_meta's byte flags, kg_vracer.hip — keep
+# their values opaque to it locally; tests/test_abi.py checks that the code
+# object holds no SDWA instruction.)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}",
-         "-Wno-unused-result", "-mllvm", "-amdgpu-sdwa-peephole=false"]
+         "-Wno-unused-result"]
 
 
 def sources():
@@ -61,9 +61,9 @@ def build(force=False, verbose=False):
 
 
 def build_engine(force=False, verbose=False):
-    srcs = [os.path.join(ENGINE, f) for f in ("json.cpp", "engine.cpp", "likelihood.cpp")]
-    hdrs = [os.path.join(ENGINE, f) for f in ("json.hpp", "korali.hpp")] + [os.path.join(ROOT, "include", "korali_amd.h")]
-    link = ["-L" + PKG, "-lkorali_amd", "-Wl,-rpath,$ORIGIN"]
+    srcs = [os.path.join(ENGINE, f) for f in ("json.cpp", "engine.cpp", "likelihood.cpp", "distributed.cpp")]
+    hdrs = [os.path.join(ENGINE, f) for f in ("json.hpp", "korali.hpp", "distributed.hpp")] + [os.path.join(ROOT, "include", "korali_amd.h")]
+    link = ["-L" + PKG, "-lkorali_amd", "-Wl,-rpath,$ORIGIN", "-ldl"]  # -ldl: librccl is opened at run time
     if force or _stale(ENGINE_LIB, srcs + hdrs + [LIB]):
         _run([CXX] + CXXFLAGS + ["-o", ENGINE_LIB] + srcs + link, verbose)
     pysrc = os.path.join(ENGINE, "pybind.cpp")

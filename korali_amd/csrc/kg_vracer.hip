@@ -159,18 +159,24 @@ __global__ __launch_bounds__(256) void k_vr_fwd_out(int M, int H, int O, const f
                                                     float *__restrict__ out, Params P) {
   const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
-  float acc[MAXO];
-  for (int o = 0; o < O; o++) acc[o] = 0.f;
+  float acc[MAXO];  // (static indices only: loops unrolled to MAXO, o < O guarded)
+#pragma unroll
+  for (int o = 0; o < MAXO; o++) acc[o] = 0.f;
   const float *h = Hs + (long long)m * H;
   for (int i = lane; i < H; i += 64) {
     const float x = h[i];
-    for (int o = 0; o < O; o++) acc[o] += W[o * H + i] * x;
+#pragma unroll
+    for (int o = 0; o < MAXO; o++)
+      if (o < O) acc[o] += W[o * H + i] * x;
   }
-  for (int o = 0; o < O; o++)
-    for (int d = 32; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d, 64);
+#pragma unroll
+  for (int o = 0; o < MAXO; o++)
+    if (o < O)
+      for (int d = 32; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d, 64);
   if (lane < O) {
     float x = 0.f;
-    for (int o = 0; o < O; o++)
+#pragma unroll
+    for (int o = 0; o < MAXO; o++)
       if (o == lane) x = acc[o];
     x = x + b[lane];
     if (P.soft[lane]) x = (float)(0.5 * ((double)x + sqrt(1.0 + (double)x * (double)x)));
@@ -288,22 +294,28 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (long long)Bn * H) return;
   const int b = (int)(t / H), i = (int)(t % H);
-  float dz[MAXO];
+  float dz[MAXO];  // (static indices only: loops unrolled to MAXO, o < O guarded)
   float acc = 0.f;
-  for (int o = 0; o < O; o++) {
-    float x = out[b * O + o], g = G[b * O + o];
-    x = x - P.shift[o];
-    x = x / P.scale[o];
-    g = g * P.scale[o];
-    if (P.soft[o]) {
-      const float nnx = x - 0.25f / x;
-      g = (float)((double)g * 0.5 * (1.0 + (double)nnx / sqrt((double)nnx * (double)nnx + 1.0)));
+#pragma unroll
+  for (int o = 0; o < MAXO; o++) {
+    dz[o] = 0.f;
+    if (o < O) {
+      float x = out[b * O + o], g = G[b * O + o];
+      x = x - P.shift[o];
+      x = x / P.scale[o];
+      g = g * P.scale[o];
+      if (P.soft[o]) {
+        const float nnx = x - 0.25f / x;
+        g = (float)((double)g * 0.5 * (1.0 + (double)nnx / sqrt((double)nnx * (double)nnx + 1.0)));
+      }
+      dz[o] = g;
+      acc += dz[o] * W[o * H + i];
     }
-    dz[o] = g;
-    acc += dz[o] * W[o * H + i];
   }
   if (i == 0)
-    for (int o = 0; o < O; o++) dZ[b * O + o] = dz[o];
+#pragma unroll
+    for (int o = 0; o < MAXO; o++)
+      if (o < O) dZ[b * O + o] = dz[o];
   const float y = Hs[(long long)b * H + i];
   dH[t] = acc * (1.0f - y * y);
 }
@@ -421,6 +433,12 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
 // global memory, and the replay-memory metadata is written once at the end
 // (no global store is waited for at the first barrier).  A == 1.
 constexpr int MB_META = 1024;
+// a byte flag from LDS as a full 32-bit value (keeps compares on it out of SDWA byte-select forms)
+__device__ __forceinline__ int u8v(unsigned char b) {
+  int v = b;
+  asm volatile("" : "+v"(v));
+  return v;
+}
 __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                  const float *__restrict__ out, float *__restrict__ G) {
   __shared__ unsigned s_mb[MB_META];
@@ -479,7 +497,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     const long long end = s_mb[b];
     const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
     const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
-    const int pos = er.ep_pos[pe], term = s_term[b];
+    const int pos = er.ep_pos[pe], term = u8v(s_term[b]);
     const float retn = er.ret[pnext];
     if (b < B - 1 && epe == epn) continue;
     long long start = end - pos;
@@ -540,11 +558,11 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   for (int b = t; b < B; b += nt) {
     const float V = s_V[b], cm = s_cur[2 * b], cs = s_cur[2 * b + 1], om = s_old[2 * b], osd = s_old[2 * b + 1];
     const float a = s_act[b];
-    const int term = s_term[b];
+    const int term = u8v(s_term[b]);
     float g[3];
     g[0] = s_ret[b] - V;
     g[1] = g[2] = 0.f;
-    if (s_onp[b]) {
+    if (u8v(s_onp[b])) {
       float q = s_rew[b];
       if (term == NON_TERMINAL) q += P.gamma * s_retn[b];
       if (term == TRUNCATED) q += P.gamma * s_tv[b];
@@ -620,7 +638,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
       G[(long long)b * O + i] = g[i];
     }
-    if (s_uniq[b]) {
+    if (u8v(s_uniq[b])) {
       const long long p = ph(s_mb[b]);
       er.cur_pol[2 * p] = cm, er.cur_pol[2 * p + 1] = cs;
       er.v[p] = V;
@@ -665,15 +683,30 @@ __device__ inline bool cp_failed(const double *u) {
 }
 // numpy RandomState(seed).uniform(-0.05, 0.05, 4): init_genrand, one twist of
 // the first 8 words, tempering, random_double = (a>>5, b>>6) / 2^53.
+//
+// Every private-array index here is a compile-time constant (unrolled
+// loops): a runtime-indexed write inside the 405-step recurrence (the
+// round-2 form, `if (i <= 8) lo[i] = x`) was if-converted by the compiler
+// into an unconditional VGPR-indexed write v[base + i] with i up to 404 —
+// far past the array — which corrupted other registers and memory-faulted
+// on MI355X.
 __device__ inline void cp_reset(unsigned seed, double *u) {
   unsigned lo[9], hi[8];
   unsigned x = seed;
-  for (int i = 0; i <= 404; i++) {
-    if (i > 0) x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
-    if (i <= 8) lo[i] = x;
-    if (i >= 397) hi[i - 397] = x;
+  lo[0] = x;
+#pragma unroll
+  for (int i = 1; i <= 8; i++) {
+    x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+    lo[i] = x;
+  }
+  for (int i = 9; i < 397; i++) x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+#pragma unroll
+  for (int i = 397; i <= 404; i++) {
+    x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+    hi[i - 397] = x;
   }
   unsigned out[8];
+#pragma unroll
   for (int i = 0; i < 8; i++) {
     const unsigned y = (lo[i] & 0x80000000u) | (lo[i + 1] & 0x7fffffffu);
     unsigned z = hi[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
@@ -681,9 +714,15 @@ __device__ inline void cp_reset(unsigned seed, double *u) {
     z ^= (z << 7) & 0x9d2c5680u;
     z ^= (z << 15) & 0xefc60000u;
     z ^= z >> 18;
+    // opaque to the optimiser: the later >> 5 / >> 6 stay plain shifts (the
+    // SDWA peephole otherwise folds (z >> 24) into a byte-select v_xor_b32_sdwa;
+    // such a build of this kernel memory-faulted on MI355X in round 2, see
+    // DESIGN.md section 9)
+    asm volatile("" : "+v"(z));
     out[i] = z;
   }
   const double low = -0.05, range = 0.05 - -0.05;
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     const double d = ((double)(out[2 * k] >> 5) * 67108864.0 + (double)(out[2 * k + 1] >> 6)) / 9007199254740992.0;
     u[k] = low + range * d;

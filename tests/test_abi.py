@@ -50,3 +50,27 @@ def test_code_object_targets_gfx950():
     from korali_amd import _build
     data = open(_build.LIB, "rb").read()
     assert b"gfx950" in data
+
+
+def test_code_object_has_no_sdwa_or_indexed_register_forms(lib, tmp_path):
+    """No VGPR-indexing mode anywhere: a runtime-indexed private-array write
+    inside a longer loop (round 2's CartPole reset, `if (i <= 8) lo[i] = x`
+    for i < 405) was if-converted into an unconditional indexed register write
+    v[base + i] far past the array, which memory-faulted on MI355X; every
+    private-array index is now a compile-time constant.  And no SDWA forms:
+    the library builds without any -amdgpu-sdwa-peephole switch."""
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not (shutil.which("objcopy") and os.path.exists(f"{llvm}/clang-offload-bundler")):
+        pytest.skip("objcopy / clang-offload-bundler not available")
+    fat, co = tmp_path / "fat.bin", tmp_path / "co.o"
+    from korali_amd import _build
+    subprocess.check_call(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", _build.LIB, str(fat)])
+    subprocess.check_call([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                           "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])
+    dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--mcpu=gfx950", str(co)], check=True,
+                         capture_output=True, text=True).stdout
+    assert "v_add_f64" in dis
+    assert not re.search(r"\bv_\w+_sdwa\b", dis)
+    assert not re.search(r"\bs_set_gpr_idx_on\b|\bv_movrel\w*\b", dis)
