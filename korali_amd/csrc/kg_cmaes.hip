@@ -2091,7 +2091,8 @@ int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
                        h->cfg.diagonal_covariance, h->part + 2 * (size_t)N, h->pc, h->C, h->sc, 1);
     KG_HIP(hipGetLastError());
   }
-  return cmaes_sigma(h);
+  if (cmaes_sigma(h)) return 1;
+  return cmaes_publish_summary(h);  // the termination record, as after kg_cmaes_update
 }
 
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {

@@ -33,6 +33,7 @@
 #include <unistd.h>
 
 #include "../../include/korali_amd.h"
+#include "distributed.hpp"
 #include "korali.hpp"
 
 namespace korali {
@@ -166,6 +167,10 @@ class Conduit {
   Conduit(const Conduit &) = delete;
   Conduit &operator=(const Conduit &) = delete;
 
+  // Distributed: the collectives among the ranks (null for Sequential /
+  // Concurrent); every rank runs the engine on its own GPU
+  std::unique_ptr<Collective> dist;
+
   void evaluateBatch(size_t n, const std::function<void(size_t)> &body) {
     if (pool_.empty() || n <= 1) {
       for (size_t i = 0; i < n; i++) body(i);
@@ -242,10 +247,26 @@ std::unique_ptr<Conduit> makeConduit(Json &js) {
       fail("You need to define at least 1 concurrent job(s) for external models \n");
     return std::unique_ptr<Conduit>(new Conduit((size_t)jobs));
   }
-  if (t == "distributed")
-    fail("The Distributed conduit (MPI worker teams) is not part of the device path: shard the population or the "
-         "TMCMC chains across GPUs with korali_amd.sharded over torch.distributed instead.");
-  fail("Unrecognized conduit type '%s' (Sequential or Concurrent).", c["Type"].getString().c_str());
+  if (t == "distributed") {
+    // distributed.config: Ranks Per Worker (default 1).  The reference farms
+    // samples to worker teams (distributed.cpp.base:31-71); here each rank is
+    // one engine on one GPU and the solver shards its population / chains, so
+    // a team is always one rank.
+    const double rpw = num(c, "Ranks Per Worker", 1);
+    if (rpw != 1)
+      fail("The Distributed conduit runs one rank per GPU: 'Ranks Per Worker' must be 1 (is %g).", rpw);
+    const std::string tr = canon(str(c, "Transport", "RCCL"));
+    if (tr != "rccl" && tr != "host") fail("Conduit 'Transport' must be 'RCCL' or 'Host'.");
+    const double port = num(c, "Bootstrap Port", 0);
+    std::unique_ptr<Conduit> cd(new Conduit(1));
+    try {
+      cd->dist = makeCollective(tr, (int)port);
+    } catch (const std::exception &e) {
+      fail("%s", e.what());
+    }
+    return cd;
+  }
+  fail("Unrecognized conduit type '%s' (Sequential, Concurrent or Distributed).", c["Type"].getString().c_str());
 }
 
 struct VariableSpec {
@@ -510,6 +531,40 @@ void rejectProblemUnrecognised(Json &pb, const std::string &pt) {
   else if (pt == "bayesian/reference") rejectUnrecognised(pb, "Reference", {BAYESIAN_REFERENCE_KEYS}, {});
 }
 
+// ------------------------------------------------------------- sharding
+// The GPU of a Distributed rank: "Device" if given, else LOCAL_RANK modulo
+// the visible devices (torch.distributed.run's one process per GPU).
+int solverDevice(Json &js, const Collective *dist) {
+  if (js.contains("Device")) return (int)js["Device"].getInt();
+  if (!dist) return 0;
+  int n = 0;
+  check(kg_device_count(&n));
+  const char *lr = getenv("LOCAL_RANK");
+  const int l = (lr && *lr) ? atoi(lr) : dist->rank;
+  return n > 0 ? l % n : 0;
+}
+
+// a named device buffer of a solver handle, as the collectives see it
+template <class H>
+SolverBuffer solverBuffer(H h, const char *name, int (*ptr)(H, const char *, void **), int (*stream)(H, void **),
+                          int (*get)(H, const char *, double *, size_t),
+                          int (*set)(H, const char *, const double *, size_t)) {
+  SolverBuffer b;
+  b.devicePtr = [=]() {
+    void *p = nullptr;
+    check(ptr(h, name, &p));
+    return p;
+  };
+  b.stream = [=]() {
+    void *q = nullptr;
+    check(stream(h, &q));
+    return q;
+  };
+  b.get = [=](void *out, size_t bytes) { check(get(h, name, (double *)out, bytes / sizeof(double))); };
+  b.set = [=](void *in, size_t bytes) { check(set(h, name, (const double *)in, bytes / sizeof(double))); };
+  return b;
+}
+
 // ------------------------------------------------------------- CMA-ES
 // CMAES.cpp.base on the device (kg_cmaes_*); state names as in CMAES.config
 const char *CMAES_VECTORS[] = {"Current Mean", "Previous Mean", "Covariance Matrix", "Covariance Eigenvector Matrix",
@@ -534,12 +589,17 @@ struct CmaesModule : SolverModule {
   Json *solverJs = nullptr;
   bool updated = false;  // kg_cmaes_update ran on this handle (its termination record exists)
   bool useGradients = false;  // "Use Gradient Information" (CMAES.cpp.base:82-87, :199, :226, :611-621)
+  // Distributed conduit: this rank samples / evaluates rows [r0, r1) of the
+  // population; the fitness all-gather and the partial-sum all-reduce run
+  // between kg_cmaes_update_partial and _finalize (include/korali_amd.h)
+  Collective *dist = nullptr;
+  size_t r0 = 0, r1 = 0;
 
   ~CmaesModule() override {
     if (h) kg_cmaes_destroy(h);
   }
 
-  CmaesModule(Json &js, Seeder &seeds, bool resume) {
+  CmaesModule(Json &js, Seeder &seeds, bool resume, Collective *dist_) : dist(dist_) {
     Json &sv = js["Solver"];
     Json &pb = js["Problem"];
     solverJs = &sv;
@@ -577,6 +637,19 @@ struct CmaesModule : SolverModule {
            "'Gradient'.");
     if (pb.contains("Constraints") && pb["Constraints"].size() > 0)
       fail("Constrained CMA-ES ('Constraints') is not supported by the device path.");
+    if (dist) {
+      if (mirrored || useGradients)
+        fail("The Distributed conduit shards the population: 'Mirrored Sampling' and 'Use Gradient Information' "
+             "need an unsharded run (Sequential or Concurrent conduit).");
+      if (lam % (size_t)dist->world)
+        fail("The Distributed conduit splits the population evenly: 'Population Size' (%zu) must be a multiple of "
+             "the number of ranks (%d).",
+             lam, dist->world);
+      r0 = lam / dist->world * dist->rank;
+      r1 = r0 + lam / dist->world;
+    } else {
+      r1 = lam;
+    }
     Json &tc = sv["Termination Criteria"];
     maxGenerations = num(tc, "Max Generations", 1e10);
     maxModelEvaluations = num(tc, "Max Model Evaluations", 1e9);
@@ -641,7 +714,9 @@ struct CmaesModule : SolverModule {
     const std::string cu = canon(str(sv, "Covariance Update", "Exact"));
     if (cu != "exact" && cu != "mfma") fail("'Covariance Update' must be 'Exact' or 'MFMA'.");
     c.cov_mode = cu == "mfma" ? KG_COV_MFMA : KG_COV_EXACT;
-    c.device = js.contains("Device") ? (int)js["Device"].getInt() : 0;
+    c.device = solverDevice(js, dist);
+    c.shard_rank = dist ? dist->rank : 0;
+    c.shard_count = dist ? dist->world : 0;
     c.store_bdz = 0;
     c.eigen_device_chase = 0;
     check(kg_cmaes_create(&c, &h));
@@ -674,6 +749,8 @@ struct CmaesModule : SolverModule {
     check(kg_cmaes_sample(h));
     if (objective >= 0) {
       check(kg_cmaes_eval_builtin(h, objective));
+    } else if (dist) {
+      hostEvaluate(gen, r0, r1);
     } else {
       // KORALI_START every sample, KORALI_WAITALL (CMAES.cpp.base:204-224)
       std::vector<double> X(lam * N), F(lam), G(useGradients ? lam * N : 0);
@@ -713,6 +790,17 @@ struct CmaesModule : SolverModule {
       check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
       if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
     }
+    if (dist) {
+      // the exchange steps of the sharded update
+      dist->allGather(buffer("Value Vector"), r1 - r0);
+      check(kg_cmaes_update_partial(h, gen));
+      size_t n = 0;
+      check(kg_cmaes_field_size(h, "Shard Partials", &n));
+      dist->allReduceSum(buffer("Shard Partials"), n);
+      check(kg_cmaes_update_finalize(h, gen));
+      updated = true;
+      return;
+    }
     check(kg_cmaes_update(h, gen));
     updated = true;
     // enqueue the next generation's first half (generator prefetch, the
@@ -720,6 +808,40 @@ struct CmaesModule : SolverModule {
     // before the termination check, so the device never idles while the
     // host decides; device-side errors surface in checkTermination
     check(kg_cmaes_begin_sample(h));
+  }
+
+  SolverBuffer buffer(const char *name) {
+    return solverBuffer<kg_cmaes_t>(h, name, kg_cmaes_device_ptr, kg_cmaes_stream, kg_cmaes_get_field,
+                                    kg_cmaes_set_field);
+  }
+
+  // a rank's share of the host-evaluated population (the Distributed
+  // conduit's worker role, distributed.cpp.base:73-129): rows [a, b) through
+  // the objective / log-posterior, the other rows' values arrive with the
+  // all-gather
+  void hostEvaluate(size_t gen, size_t a, size_t b) {
+    std::vector<double> X(lam * N), F(lam, 0.0);
+    check(kg_cmaes_get_candidates(h, X.data(), N));
+    Function *f = bayesian ? nullptr : &getFunction(fn);
+    for (size_t i = a; i < b; i++) {
+      Sample s;
+      s["Module"] = "Problem";
+      s["Operation"] = "Evaluate";
+      s["Sample Id"] = (unsigned long long)i;
+      s["Current Generation"] = (unsigned long long)gen;
+      std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
+      s["Parameters"] = x;
+      if (bayesian) {
+        bayesian->evaluate(s, x, i);
+      } else {
+        (*f)(s);
+        if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
+        if (!std::isfinite(s["F(x)"].getDouble()))
+          fail("Non finite value of function evaluation detected: %f\n", s["F(x)"].getDouble());
+      }
+      F[i] = s["F(x)"].getDouble();
+    }
+    check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
   }
 
   double field(const char *k) {
@@ -823,13 +945,18 @@ struct TmcmcModule : SolverModule {
   std::vector<double> referenceData;  // Bayesian/Reference
   std::string likelihoodModel;
   double maxGenerations, maxModelEvaluations, targetExponent;
+  // Distributed conduit: this rank advances its share of the chains; the
+  // exchange is one MAX all-reduce between kg_tmcmc_process_partial and
+  // _finalize (include/korali_amd.h)
+  Collective *dist = nullptr;
 
   ~TmcmcModule() override {
     if (h) kg_tmcmc_destroy(h);
   }
 
   TmcmcModule(Json &js, Seeder &seeds, std::vector<uint64_t> &distSeeds,
-              std::vector<std::vector<unsigned char>> &distStates, bool resume) {
+              std::vector<std::vector<unsigned char>> &distStates, bool resume, Collective *dist_)
+      : dist(dist_) {
     Json &sv = js["Solver"];
     Json &pb = js["Problem"];
     const std::string pt = canon(str(pb, "Type", ""));
@@ -844,6 +971,8 @@ struct TmcmcModule : SolverModule {
       fail("Unrecognized value (%s) provided for mandatory setting: ['Version'] required by TMCMC.\n",
            sv["Version"].getString().c_str());
     mtmcmc = version == "mtmcmc";
+    if (mtmcmc && dist)
+      fail("mTMCMC runs unsharded: use the Sequential or Concurrent conduit.");
     // TMCMC.cpp.base:48-55
     if (mtmcmc && !reference) fail("mTMCMC works only for problems of type 'Bayesian/Reference'\n");
     std::vector<VariableSpec> vars = readVariables(js);
@@ -931,7 +1060,9 @@ struct TmcmcModule : SolverModule {
     c.multivariate_seed = seeds.assign(gv);
     c.uniform_seed = seeds.assign(gu);
     c.likelihood = KG_LIK_GAUSSIAN;
-    c.device = js.contains("Device") ? (int)js["Device"].getInt() : 0;
+    c.device = solverDevice(js, dist);
+    c.shard_rank = dist ? dist->rank : 0;
+    c.shard_count = dist ? dist->world : 0;
     c.version = mtmcmc ? 1 : 0;
     c.step_size = num(sv, "Step Size", 0.1);
     c.domain_extension_factor = num(sv, "Domain Extension Factor", 0.2);
@@ -1044,7 +1175,17 @@ struct TmcmcModule : SolverModule {
         check(kg_tmcmc_advance(h, gen, &pending));
       }
     }
-    check(kg_tmcmc_process(h, gen));
+    if (dist) {
+      check(kg_tmcmc_process_partial(h, gen));
+      size_t n = 0;
+      check(kg_tmcmc_field_size(h, "Shard Exchange", &n));
+      dist->allReduceMaxI64(solverBuffer<kg_tmcmc_t>(h, "Shard Exchange", kg_tmcmc_device_ptr, kg_tmcmc_stream,
+                                                     kg_tmcmc_get_field, kg_tmcmc_set_field),
+                            n);
+      check(kg_tmcmc_process_finalize(h, gen));
+    } else {
+      check(kg_tmcmc_process(h, gen));
+    }
     check(kg_tmcmc_synchronize(h));
   }
 
@@ -1458,6 +1599,10 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   flag(fo, "Use Multiple Files", true);
   Json &co = js["Console Output"];
   st.log.set(str(co, "Verbosity", "Normal"));
+  // Distributed: every rank holds the same solver state; rank 0 alone
+  // prints and writes result files (the reference's engine rank)
+  const bool rootRank = !conduit.dist || conduit.dist->rank == 0;
+  if (!rootRank) st.log.level = 0;
   const unsigned long long consoleFreq = uint(co, "Frequency", 1);
   flag(js, "Store Sample Information", false);
   if (!js.contains("Current Generation")) js["Current Generation"] = 0ULL;
@@ -1490,12 +1635,18 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   if (!sv.contains("Type")) fail("No solver type specified ('Solver' / 'Type').");
   const std::string stype = canon(sv["Type"].getString());
   TmcmcModule *tm = nullptr;
+  Collective *dist = conduit.dist.get();
   if (stype == "optimizer/cmaes" || stype == "cmaes") {
-    st.solver.reset(new CmaesModule(js, seeds, resume));
+    st.solver.reset(new CmaesModule(js, seeds, resume, dist));
   } else if (stype == "sampler/tmcmc" || stype == "tmcmc") {
-    tm = new TmcmcModule(js, seeds, distSeeds, distStates, resume);
+    tm = new TmcmcModule(js, seeds, distSeeds, distStates, resume, dist);
     st.solver.reset(tm);
   } else if (stype == "agent/continuous/vracer" || stype == "vracer") {
+    // the device rollouts + update of one learner have no exchange step:
+    // several GPUs run independent replicas
+    if (dist)
+      fail("Agent/Continuous/VRACER does not shard across ranks: run one experiment per GPU with the Sequential "
+           "conduit (independent replicas).");
     st.solver.reset(new VracerModule(js, seeds, resume));
   } else {
     fail("Unrecognized solver type '%s' (the device path provides Optimizer/CMAES, Sampler/TMCMC and "
@@ -1505,7 +1656,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   js["Random Seed"] = seeds.counter;
   SolverModule &solver = *st.solver;
   solver.conduit = &conduit;
-  const bool fileOut = fo["Enabled"].getBool();
+  const bool fileOut = fo["Enabled"].getBool() && rootRank;
   const size_t fileFreq = (size_t)fo["Frequency"].getUInt();
   auto save = [&]() {
     js["Current Generation"] = (unsigned long long)gen;
@@ -1544,6 +1695,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   solver.getConfiguration(sv);
   if (tm) tm->saveDistributions(js);
   if (fileOut) saveState(js, gen);
+  if (conduit.dist) conduit.dist->barrier();  // no rank leaves before the others finished
   st.log.log(1, "--------------------------------------------------------------------\n");
   st.log.log(1, "%s finished correctly.\n", solver.type().c_str());
   for (const auto &m : met) st.log.log(2, "Termination Criterion Met: %s\n", m.c_str());

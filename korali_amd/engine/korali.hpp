@@ -120,8 +120,15 @@ class Experiment {
 };
 
 // Engine (source/engine.hpp): its own JSON holds the conduit,
-//   k["Conduit"]["Type"] = "Sequential" (default) | "Concurrent";
+//   k["Conduit"]["Type"] = "Sequential" (default) | "Concurrent" | "Distributed";
 //   k["Conduit"]["Concurrent Jobs"] = n   (Concurrent: n evaluation threads)
+//   Distributed (one process per GPU, launched by torch.distributed.run or
+//   any launcher that sets RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT /
+//   LOCAL_RANK): the CMA-ES population or the TMCMC chains are sharded over
+//   the ranks, every rank ends with the same solver state, rank 0 writes the
+//   results.  k["Conduit"]["Transport"] = "RCCL" (default) | "Host";
+//   k["Conduit"]["Bootstrap Port"] = p (default MASTER_PORT + 1);
+//   k["Conduit"]["Ranks Per Worker"] must be 1.
 class Engine {
  public:
   Json &operator[](const std::string &key) { return _js[key]; }
@@ -134,6 +141,16 @@ class Engine {
 // The conduit's batch dispatch on its own (tests): body(i) for i < n on
 // `jobs` threads, the lowest failing index's exception rethrown.
 void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &body);
+
+// The Distributed conduit's collectives on host data (tests): rank / world
+// from RANK / WORLD_SIZE, the "Host" transport's TCP bootstrap on `port`.
+// gathered = every rank's `block` in rank order, summed = the element-wise
+// sum over ranks, maxed = the element-wise MAX of the int64 bit patterns.
+struct CollectiveCheck {
+  int rank = 0, world = 1;
+  std::vector<double> gathered, summed, maxed;
+};
+CollectiveCheck collectiveSelfTest(int port, const std::vector<double> &block);
 
 // Bayesian/Reference likelihood models (likelihood.cpp,
 // reference.cpp.base:25-229): the log-likelihood of reference data y given the

@@ -235,6 +235,22 @@ PYBIND11_MODULE(libkorali, m) {
     return toPy(out);
   });
 
+  // test hook: the Distributed conduit's collectives on host data (Host transport)
+  m.def("_collective_selftest", [](int port, const std::vector<double> &block) {
+    korali::CollectiveCheck r;
+    {
+      py::gil_scoped_release nogil;
+      r = korali::collectiveSelfTest(port, block);
+    }
+    py::dict d;
+    d["rank"] = r.rank;
+    d["world"] = r.world;
+    d["gathered"] = r.gathered;
+    d["summed"] = r.summed;
+    d["maxed"] = r.maxed;
+    return d;
+  });
+
   // test hook: the conduit's batch dispatch with a Python body
   m.def("_conduit_evaluate", [](size_t jobs, size_t n, py::function body) {
     py::gil_scoped_release nogil;

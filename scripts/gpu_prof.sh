@@ -1,11 +1,11 @@
 #!/bin/bash
-# round-2 profile session: every GPU step under its own time limit; stop at
-# the first crash / timeout.  Outputs under gpurun_out/r2/ (copied to
-# profiles/r2/ afterwards).
+# Profile session of one round: every GPU step under its own time limit; stop
+# at the first crash / timeout.  Outputs under gpurun_out/$ROUND/ (the
+# summaries are copied to profiles/$ROUND/ afterwards; trace csvs dropped).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=$PWD
-O=$R/gpurun_out/r2
+O=$R/gpurun_out/${ROUND:-r3}
 mkdir -p $O
 step() {
   local name=$1 secs=$2; shift 2
@@ -36,7 +36,13 @@ for s in ${STEPS:-tests}; do
     pmcw4) step pmcw4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 4 --warmup 1 --no-cpu-baseline ;;
     trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c2.py ;;
     trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c4.py ;;
+    vrtests) step vrtests 400 python -u -m pytest $R/tests/test_gpu_vracer.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
+    c5) step c5 300 python $R/bench.py --workload c5 --steps 10 --warmup 2 ;;
+    profc5) step profc5 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
+    pmcf5) step pmcf5 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
+    pmcw5) step pmcw5 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
     pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac
 done
+find $O -name "*kernel_trace.csv" -delete
 echo "session done"

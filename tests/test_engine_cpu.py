@@ -125,7 +125,7 @@ def test_engine_conduit_json_surface():
 
 
 @pytest.mark.parametrize("conduit,msg", [
-    ({"Type": "Distributed"}, "Distributed conduit"),
+    ({"Type": "Distributed", "Ranks Per Worker": 4}, "'Ranks Per Worker' must be 1"),
     ({"Type": "Concurrent", "Concurrent Jobs": 0}, "at least 1 concurrent job"),
     ({"Type": "Pipes"}, "Unrecognized conduit type"),
 ])

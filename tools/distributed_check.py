@@ -1,0 +1,98 @@
+"""One rank of the korali::Engine Distributed conduit check (tests/
+test_gpu_distributed.py launches it with torch.distributed.run): runs the
+experiment on the Distributed conduit, then the same experiment unsharded on
+the Sequential conduit, after 1 and after 6 generations, and writes the
+solver states to <out>/rank<r>.json.  The test compares them (TMCMC:
+bit-identical; CMA-ES: the first generation's samples, fitness and sort
+bit-identical and mean / covariance / sigma within the partial-sum
+tolerance, the 6-generation run close) and every rank's state against rank
+0's (bit-identical).
+
+    distributed_check.py <out dir> cmaes|tmcmc builtin|host RCCL|Host
+"""
+import json
+import os
+import sys
+
+import korali
+
+KEYS = {"cmaes": ["Current Mean", "Covariance Matrix", "Sigma", "Sorting Index", "Best Ever Value",
+                  "Evolution Path", "Conjugate Evolution Path", "Value Vector", "Model Evaluation Count"],
+        "tmcmc": ["Sample Database", "Sample LogLikelihood Database", "Annealing Exponent", "LogEvidence",
+                  "Chain Leaders", "Covariance Matrix", "Model Evaluation Count", "Accepted Samples Count"]}
+
+
+def negative_rosenbrock(s):
+    x = s["Parameters"]
+    s["F(x)"] = -sum(100.0 * (x[i + 1] - x[i] * x[i]) ** 2 + (1.0 - x[i]) ** 2 for i in range(len(x) - 1))
+
+
+def gaussian(s):  # the builtin Gaussian likelihood, -0.5 * sum(x^2)
+    s["logLikelihood"] = -0.5 * sum(v * v for v in s["Parameters"])
+
+
+def experiment(solver, model, gens):
+    e = korali.Experiment()
+    e["Random Seed"] = 4242
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    if solver == "cmaes":
+        N = 16
+        e["Problem"]["Type"] = "Optimization"
+        if model == "builtin":
+            e["Problem"]["Objective Kernel"] = "Negative Rosenbrock"
+        else:
+            e["Problem"]["Objective Function"] = negative_rosenbrock
+        for i in range(N):
+            e["Variables"][i]["Name"] = f"X{i}"
+            e["Variables"][i]["Initial Value"] = 0.0
+            e["Variables"][i]["Initial Standard Deviation"] = 1.0
+        e["Solver"]["Type"] = "Optimizer/CMAES"
+        e["Solver"]["Population Size"] = 64
+        e["Solver"]["Covariance Update"] = "MFMA"  # the rank-mu tiles the sharded update sums per shard
+        e["Solver"]["Termination Criteria"]["Max Generations"] = gens
+    else:
+        e["Problem"]["Type"] = "Bayesian/Custom"
+        if model == "builtin":
+            e["Problem"]["Likelihood Kernel"] = "Gaussian"
+        else:
+            e["Problem"]["Likelihood Model"] = gaussian
+        e["Distributions"][0]["Name"] = "U"
+        e["Distributions"][0]["Type"] = "Univariate/Uniform"
+        e["Distributions"][0]["Minimum"] = -10.0
+        e["Distributions"][0]["Maximum"] = 10.0
+        for i in range(4):
+            e["Variables"][i]["Name"] = f"a{i}"
+            e["Variables"][i]["Prior Distribution"] = "U"
+        e["Solver"]["Type"] = "Sampler/TMCMC"
+        e["Solver"]["Population Size"] = 600
+        e["Solver"]["Max Chain Length"] = 2
+        e["Solver"]["Burn In"] = 1
+        e["Solver"]["Termination Criteria"]["Max Generations"] = gens
+    return e
+
+
+def state(e, solver):
+    return {k: e["Solver"][k] for k in KEYS[solver]} | {"Current Generation": e["Current Generation"]}
+
+
+def main():
+    out, solver, model, transport = sys.argv[1:5]
+    rank = int(os.environ["RANK"])
+    result = {}
+    for gens in (1, 6):  # one generation: same samples; six: the run as a whole
+        k = korali.Engine()
+        k["Conduit"]["Type"] = "Distributed"
+        k["Conduit"]["Transport"] = transport
+        e = experiment(solver, model, gens)
+        k.run(e)
+        u = experiment(solver, model, gens)
+        korali.Engine().run(u)
+        result[str(gens)] = {"sharded": state(e, solver), "unsharded": state(u, solver)}
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump(result, f)
+    print(f"DISTRIBUTED_CHECK rank {rank} done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
