@@ -175,6 +175,14 @@ int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, siz
  * (window624 = 624 consecutive untempered words of a GSL mt19937 stream,
  * not starting at the seeding word 0).  Runs on the host, no device needed. */
 int kg_debug_mt_jump(const uint32_t *window624, uint64_t distance, uint32_t *out624);
+/* The device CartPole (examples/learning/reinforcement/cartpole/_model/
+ * cartpole.py: scipy dopri5 advance, restated in kg_vracer.hip) on given
+ * forces: n trajectories from u0 (n x 4) at t = 0, `steps` advances each with
+ * force[j * steps + k]; u_out (n x steps x 4) the state after every advance,
+ * over (n x steps) 1 where the pole fell or the cart left the track, -1 where
+ * the integration failed.  Runs on `device`. */
+int kg_debug_cartpole(int device, const double *u0, const double *force, size_t n, size_t steps, double *u_out,
+                      int *over);
 
 /* --------------------------------------------------------------- TMCMC */
 typedef struct kg_tmcmc_s *kg_tmcmc_t;

@@ -12,6 +12,8 @@
 // multiply-adds are the explicit fma() calls of the exact two-product.
 #pragma once
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -50,6 +52,28 @@ inline int zero_fill(void *p, size_t bytes) {
   KG_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
   KG_HIP(hipStreamSynchronize(nullptr));
   return 0;
+}
+
+// Grids whose workgroups wait on one another inside the launch (spin
+// hand-offs) go through launch_resident: a cooperative launch, so HIP
+// guarantees co-residency or fails the launch.  KORALI_AMD_PLAIN_LAUNCH=1
+// launches them with hipLaunchKernel after the same occupancy check instead:
+// rocprofv3 (ROCm 7.2) segfaults at process teardown, after writing its
+// output, in any process that made a cooperative launch, so profile runs set
+// it (scripts/gpu_prof.sh).
+inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s) {
+  static const bool plain = [] {
+    const char *e = getenv("KORALI_AMD_PLAIN_LAUNCH");
+    return e && *e && *e != '0';
+  }();
+  if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
+  int dev = 0, cus = 0, per = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, (int)(block.x * block.y * block.z), lds);
+  if (e != hipSuccess) return e;
+  if ((long long)per * cus < (long long)grid.x * grid.y * grid.z) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(f, grid, block, args, lds, s);
 }
 
 // Device-side error flags (bitmask in the scalar block; read back at sync

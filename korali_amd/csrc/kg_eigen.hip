@@ -2879,12 +2879,17 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
     unsigned long long *comm_ = comm, *trace_ = trace;
     unsigned int *errors_ = errors;
     void *args[] = {&N_, &C_, &gH_, &tau_, &d_, &sd_, &comm_, &errors_, &trace_};
-    KG_HIP(hipLaunchCooperativeKernel((const void *)k_tridiag_mw2, dim3(mw2_groups(N)), dim3(MW2_TPB), args,
-                                      mw2_lds_bytes(N), s));
+    KG_HIP(launch_resident((const void *)k_tridiag_mw2, dim3(mw2_groups(N)), dim3(MW2_TPB), args, mw2_lds_bytes(N),
+                           s));
   } else {
     KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), tmw_lds_bytes(N), s, N, C, gH, tau, d, sd,
-                       comm, errors, trace);
+    int N_ = N;
+    const double *C_ = C;
+    double *gH_ = gH, *tau_ = tau, *d_ = d, *sd_ = sd;
+    unsigned long long *comm_ = comm, *trace_ = trace;
+    unsigned int *errors_ = errors;
+    void *args[] = {&N_, &C_, &gH_, &tau_, &d_, &sd_, &comm_, &errors_, &trace_};
+    KG_HIP(launch_resident((const void *)k_tridiag_mw, dim3(tmw_groups(N)), dim3(TMW_TPB), args, tmw_lds_bytes(N), s));
   }
   KG_HIP(hipGetLastError());
   if (prof) prof(profCtx, "eigen_tridiag", 1);
@@ -2944,8 +2949,8 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
       unsigned long long seq_ = seq;
       void *args[] = {&N_, &gQt_, &devRec, &B_, &D_, &minEig_, &maxEig_, &eigenFailures_, &errors_, &trace_,
                       &dprogDev_, &seq_, &mr, &dprog_};
-      KG_HIP(hipLaunchCooperativeKernel((const void *)k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1),
-                                        dim3(APPLY_TPB), args, apply_lds_bytes(N), s));
+      KG_HIP(launch_resident((const void *)k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1),
+                             dim3(APPLY_TPB), args, apply_lds_bytes(N), s));
     }
     if (prof) prof(profCtx, "eigen_dsd_wait", 2);
     {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)

@@ -1821,7 +1821,7 @@ int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmi
     void *args[] = {&Pa, (void *)&llp, (void *)&devp, &rho, &tgt, &tab, &syncp, &outp};
     // co-residency of the controller and its workers is guaranteed by the
     // cooperative launch (it fails rather than under-schedules)
-    if (hipLaunchCooperativeKernel((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream) !=
+    if (launch_resident((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream) !=
         hipSuccess) {
       (void)hipGetLastError();
       h->nmFallbacks++;

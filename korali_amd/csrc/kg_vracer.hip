@@ -44,7 +44,7 @@ constexpr int MAXA = 4;  // action dimensions supported by the device kernels
 constexpr int MAXO = 1 + 2 * MAXA;
 constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
-enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u };
+enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u, ERR_ENV_ODE = 8u };
 
 // Device-resident agent scalars (float where the reference keeps float).
 struct State {
@@ -665,18 +665,144 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
 }
 
 // ---------------------------------------------------------------- CartPole
-// examples/learning/reinforcement/cartpole/_model/cartpole.py (RK4 step of
-// dt = 0.02 in place of scipy's adaptive dopri5) and env.py (3 reward
+// examples/learning/reinforcement/cartpole/_model/cartpole.py (advance: scipy
+// ode 'dopri5' from t to t + 0.02, restated below) and env.py (3 reward
 // variants, reset seeded with numpy's legacy mt19937 by sampleId*1024 + launchId).
+// cartpole.py:37-46 in its operation order (w**2 and costh**2 squared first)
 __device__ inline void cp_system(const double *y, double act, double *d) {
   const double mp = 0.1, mc = 1.0, l = 0.5, g = 9.81;
   const double th = y[2], w = y[3];
   const double c = cos(th), s = sin(th);
   const double tot = mp + mc;
-  const double tmp = (act + l * w * w * s) / tot;
-  const double wdot = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * c * c / tot));
+  const double tmp = (act + l * (w * w) * s) / tot;
+  const double wdot = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * (c * c) / tot));
   const double vdot = tmp - l * wdot * c / tot;
   d[0] = y[1], d[1] = vdot, d[2] = w, d[3] = wdot;
+}
+
+// scipy.integrate.ode 'dopri5' = Hairer & Wanner's DOPRI5 (Dormand-Prince
+// 5(4)) as scipy calls it for one integrate(): rtol 1e-6, atol 1e-12 (ITOL 0),
+// UROUND 2.3e-16, SAFE 0.9, FAC1 0.2, FAC2 10, BETA 0.04 (scipy's beta 0 ->
+// the code's default), HMAX = XEND - X, first step from HINIT, at most 500
+// steps, no dense output; stiffness detection only prints and is left out.
+// Fortran's left-to-right order term by term (oracle/vracer_ref.py
+// dopri5_advance, bit-exact against the reference's own trajectories in
+// tests/golden/cartpole_dopri5.json).  Returns false past NMAX or a vanishing
+// step (scipy reports those as failures).
+namespace dp {
+constexpr double C2 = 0.2, C3 = 0.3, C4 = 0.8, C5 = 8.0 / 9.0, A21 = 0.2;
+constexpr double A31 = 3.0 / 40.0, A32 = 9.0 / 40.0;
+constexpr double A41 = 44.0 / 45.0, A42 = -56.0 / 15.0, A43 = 32.0 / 9.0;
+constexpr double A51 = 19372.0 / 6561.0, A52 = -25360.0 / 2187.0, A53 = 64448.0 / 6561.0, A54 = -212.0 / 729.0;
+constexpr double A61 = 9017.0 / 3168.0, A62 = -355.0 / 33.0, A63 = 46732.0 / 5247.0, A64 = 49.0 / 176.0,
+                 A65 = -5103.0 / 18656.0;
+constexpr double A71 = 35.0 / 384.0, A73 = 500.0 / 1113.0, A74 = 125.0 / 192.0, A75 = -2187.0 / 6784.0,
+                 A76 = 11.0 / 84.0;
+constexpr double E1 = 71.0 / 57600.0, E3 = -71.0 / 16695.0, E4 = 71.0 / 1920.0, E5 = -17253.0 / 339200.0,
+                 E6 = 22.0 / 525.0, E7 = -1.0 / 40.0;
+constexpr double RTOL = 1e-6, ATOL = 1e-12, UROUND = 2.3e-16, SAFE = 0.9, FAC1 = 0.2, FAC2 = 10.0, BETA = 0.04;
+constexpr int NMAX = 500;
+}  // namespace dp
+
+__device__ inline bool cp_dopri5(double *y, double x, double xend, double F) {
+  using namespace dp;
+  double k1[4], k2[4], k3[4], k4[4], k5[4], k6[4], y1[4], ys[4];
+  const double expo1 = 0.2 - BETA * 0.75, facc1 = 1.0 / FAC1, facc2 = 1.0 / FAC2;
+  double facold = 1.0e-4;
+  const double hmax = fabs(xend - x);
+  cp_system(y, F, k1);
+  double h;
+  {  // HINIT
+    double dnf = 0.0, dny = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double sk = ATOL + RTOL * fabs(y[i]);
+      const double a = k1[i] / sk, b = y[i] / sk;
+      dnf = dnf + a * a;
+      dny = dny + b * b;
+    }
+    h = (dnf <= 1.0e-10 || dny <= 1.0e-10) ? 1.0e-6 : sqrt(dny / dnf) * 0.01;
+    h = fmin(h, hmax);
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * k1[i];
+    cp_system(y1, F, k2);
+    double der2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double sk = ATOL + RTOL * fabs(y[i]);
+      const double a = (k2[i] - k1[i]) / sk;
+      der2 = der2 + a * a;
+    }
+    der2 = sqrt(der2) / h;
+    const double der12 = fmax(fabs(der2), sqrt(dnf));
+    const double h1 = der12 <= 1.0e-15 ? fmax(1.0e-6, fabs(h) * 1.0e-3) : pow(0.01 / der12, 1.0 / 5);
+    h = fmin(fmin(100 * fabs(h), h1), hmax);
+  }
+  bool last = false, reject = false;
+  for (int nstep = 0;; nstep++) {
+    if (nstep > NMAX || 0.1 * fabs(h) <= fabs(x) * UROUND) return false;
+    if ((x + 1.01 * h - xend) > 0.0) {
+      h = xend - x;
+      last = true;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * A21 * k1[i];
+    cp_system(y1, F, k2);
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * (A31 * k1[i] + A32 * k2[i]);
+    cp_system(y1, F, k3);
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * (A41 * k1[i] + A42 * k2[i] + A43 * k3[i]);
+    cp_system(y1, F, k4);
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * (A51 * k1[i] + A52 * k2[i] + A53 * k3[i] + A54 * k4[i]);
+    cp_system(y1, F, k5);
+#pragma unroll
+    for (int i = 0; i < 4; i++) ys[i] = y[i] + h * (A61 * k1[i] + A62 * k2[i] + A63 * k3[i] + A64 * k4[i] + A65 * k5[i]);
+    const double xph = x + h;
+    cp_system(ys, F, k6);
+#pragma unroll
+    for (int i = 0; i < 4; i++) y1[i] = y[i] + h * (A71 * k1[i] + A73 * k3[i] + A74 * k4[i] + A75 * k5[i] + A76 * k6[i]);
+    cp_system(y1, F, k2);
+    double err = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double e = (E1 * k1[i] + E3 * k3[i] + E4 * k4[i] + E5 * k5[i] + E6 * k6[i] + E7 * k2[i]) * h;
+      const double sk = ATOL + RTOL * fmax(fabs(y[i]), fabs(y1[i]));
+      const double q = e / sk;
+      err = err + q * q;
+    }
+    err = sqrt(err / 4);
+    const double fac11 = pow(err, expo1);
+    const double fac = fmax(facc2, fmin(facc1, (fac11 / pow(facold, BETA)) / SAFE));
+    double hnew = h / fac;
+    if (err <= 1.0) {
+      facold = fmax(err, 1.0e-4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) k1[i] = k2[i], y[i] = y1[i];
+      x = xph;
+      if (last) return true;
+      if (fabs(hnew) > hmax) hnew = hmax;
+      if (reject) hnew = fmin(fabs(hnew), fabs(h));
+      reject = false;
+    } else {
+      hnew = h / fmin(facc1, fac11 / SAFE);
+      reject = true;
+      last = false;
+    }
+    h = hnew;
+  }
+}
+
+// CartPole::advance (cartpole.py:48-62): F clipped to [-10, 10], the ODE
+// from the environment's time t to t + dt, then t += dt
+__device__ inline bool cp_advance(double *u, double &t, double action) {
+  double F = action;
+  if (F > 10.0) F = 10.0;
+  else if (F < -10.0) F = -10.0;
+  const bool ok = cp_dopri5(u, t, t + 0.02, F);
+  t = t + 0.02;
+  return ok;
 }
 __device__ inline bool cp_failed(const double *u) {
   return fabs(u[0]) > 2.4 || fabs(u[2]) > M_PI / 15;
@@ -731,6 +857,7 @@ __device__ inline void cp_reset(unsigned seed, double *u) {
 
 struct Envs {
   double *u;          // E x 4 CartPole state
+  double *time;       // E: the CartPole's ODE time t (cartpole.py: reset to 0, += dt per advance)
   int *t, *env_id;    // steps taken in the episode, environment id
   unsigned long long *sample;
   float *cum;         // cumulative training reward of the running episode
@@ -749,6 +876,7 @@ __global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long s
   double u[4];
   cp_reset((unsigned)(sid * 1024ull + sid), u);
   for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = u[k], X[e * 4 + k] = (float)u[k];
+  ev.time[e] = 0.0;
   ev.t[e] = 0;
   ev.sample[e] = sid;
   ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
@@ -787,21 +915,13 @@ __global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restri
   for (int i = 0; i < A; i++) ev.eb_act[slot * A + i] = act[i];
   for (int i = 0; i < 2 * A; i++) ev.eb_pol[slot * 2 * A + i] = out[(long long)e * O + 1 + i];
   ev.eb_v[slot] = V;
-  // CartPole::advance: F clipped to [-10, 10], one RK4 step
-  double F = (double)act[0];
-  if (F > 10.0) F = 10.0;
-  else if (F < -10.0) F = -10.0;
-  double y[4], k1[4], k2[4], k3[4], k4[4], tmp[4];
+  double y[4];
+#pragma unroll
   for (int k = 0; k < 4; k++) y[k] = ev.u[e * 4 + k];
-  const double h = 0.02;
-  cp_system(y, F, k1);
-  for (int k = 0; k < 4; k++) tmp[k] = y[k] + 0.5 * h * k1[k];
-  cp_system(tmp, F, k2);
-  for (int k = 0; k < 4; k++) tmp[k] = y[k] + 0.5 * h * k2[k];
-  cp_system(tmp, F, k3);
-  for (int k = 0; k < 4; k++) tmp[k] = y[k] + h * k3[k];
-  cp_system(tmp, F, k4);
-  for (int k = 0; k < 4; k++) y[k] = y[k] + (h / 6.0) * (((k1[k] + 2.0 * k2[k]) + 2.0 * k3[k]) + k4[k]);
+  double tm = ev.time[e];
+  if (!cp_advance(y, tm, (double)act[0])) atomicOr(&st->errors, (unsigned)ERR_ENV_ODE);
+  ev.time[e] = tm;
+#pragma unroll
   for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = y[k], X[e * 4 + k] = (float)y[k];
   const bool failed = cp_failed(y);
   const double r = 1.0 - 1.0 * (failed ? 1.0 : 0.0);
@@ -949,6 +1069,7 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     double u[4];
     cp_reset((unsigned)(sid * 1024ull + sid), u);
     for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = (float)u[q];
+    ev.time[e] = 0.0;
     ev.t[e] = 0;
     ev.sample[e] = sid;
     ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
@@ -973,8 +1094,16 @@ struct kg_vracer_s {
   Params P;
   int device;
   hipStream_t stream;
-  size_t nparam;
-  std::vector<size_t> offW, offb;  // per layer
+  size_t nparam;                   // device hyperparameters (hidden width padded to P.H)
+  std::vector<size_t> offW, offb;  // per layer, device layout
+  // Hidden widths that are not multiples of 64 run padded to P.H = the next
+  // multiple: the padded units have zero weights in and out and a zero bias,
+  // so their activations tanh(0) = 0 contribute nothing and their gradients,
+  // Adam moments and L2 terms stay exactly 0.  The user-facing layout (the
+  // reference's hyperparameter vector, nuser values) maps to the device one
+  // through umap (empty when nothing is padded).
+  size_t nuser;
+  std::vector<size_t> umap;
   float *theta, *grad, *m1, *m2;
   float *X;          // E x S current environment states
   float *Xmb;        // 2B x S mini-batch (+ truncated) states
@@ -1137,6 +1266,7 @@ int vr_read_state(kg_vracer_t h) {
     const unsigned e = h->st_host->errors;
     if (e & ERR_NONFINITE_GRADIENT) kg::set_error("Gradient loss returned an invalid value (VRACER.cpp.base:173-175)");
     else if (e & ERR_NONFINITE_VALUE) kg::set_error("Calculated state value returned an invalid value (agent.cpp.base:629-630)");
+    else if (e & ERR_ENV_ODE) kg::set_error("CartPole: the dopri5 integration failed (more than 500 steps or a vanishing step)");
     else kg::set_error("NaN detected in the calculation of importance weight (continuous.cpp.base:391)");
     return 1;
   }
@@ -1146,6 +1276,7 @@ int vr_read_state(kg_vracer_t h) {
 struct VrField {
   void *ptr;
   size_t elem, count;
+  bool param;  // a hyperparameter-shaped array (user layout <-> device layout)
 };
 bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
   const Params &P = h->P;
@@ -1163,10 +1294,11 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"retrace", h->er.ret, 4, R},            {"importance_weight", h->er.iw, 4, R},
       {"truncated_importance_weight", h->er.tiw, 4, R}, {"truncated_state_value", h->er.tv, 4, R},
       {"on_policy", h->er.onp, 4, R},          {"episode_id", h->er.ep_id, 8, R},
-      {"episode_pos", h->er.ep_pos, 4, R},     {"hyperparameters", h->theta, 4, h->nparam},
-      {"adam_first_moment", h->m1, 4, h->nparam}, {"adam_second_moment", h->m2, 4, h->nparam},
-      {"gradient", h->grad, 4, h->nparam},     {"env_states", h->X, 4, E * P.S},
-      {"env_u", h->ev.u, 8, E * 4},            {"env_steps", h->ev.t, 4, E},
+      {"episode_pos", h->er.ep_pos, 4, R},     {"hyperparameters", h->theta, 4, h->nuser},
+      {"adam_first_moment", h->m1, 4, h->nuser}, {"adam_second_moment", h->m2, 4, h->nuser},
+      {"gradient", h->grad, 4, h->nuser},      {"env_states", h->X, 4, E * P.S},
+      {"env_u", h->ev.u, 8, E * 4},            {"env_time", h->ev.time, 8, E},
+      {"env_steps", h->ev.t, 4, E},
       {"env_ids", h->ev.env_id, 4, E},         {"env_sample_ids", h->ev.sample, 8, E},
       {"finished_rewards", h->ev.rewards, 4, E}, {"finished_env", h->ev.fin_env, 4, E},
       {"mini_batch", h->mb, 4, (size_t)P.B},   {"loss_gradient", h->G, 4, (size_t)P.B * P.O},
@@ -1174,7 +1306,8 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {
-      f = VrField{x.p, x.elem, x.count};
+      f = VrField{x.p, x.elem, x.count,
+                  x.p == h->theta || x.p == h->grad || x.p == h->m1 || x.p == h->m2};
       return true;
     }
   return false;
@@ -1190,7 +1323,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
            "vracer: action size must be 1..4 and state size >= 1");
   KG_CHECK(c->state_size == 4 && c->action_size == 1,
            "vracer: the device environment is the CartPole of examples/learning/reinforcement/cartpole (4 states, 1 action)");
-  KG_CHECK(c->hidden_size % 64 == 0 && c->hidden_size >= 64, "vracer: hidden layer width must be a multiple of 64");
+  KG_CHECK(c->hidden_size >= 1 && c->hidden_size <= 4096, "vracer: hidden layer width must be 1..4096");
   KG_CHECK(c->hidden_layers >= 1, "vracer: at least one hidden layer");
   KG_CHECK(c->mini_batch_size >= 2 && c->mini_batch_size <= (size_t)MB_META, "vracer: Mini Batch Size must be 2..1024");
   KG_CHECK(c->environments >= 1 && c->environments <= (1u << 20), "vracer: Concurrent Environments out of range");
@@ -1212,7 +1345,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   KG_HIP(hipSetDevice(c->device));
   auto *h = new kg_vracer_s();
   Params &P = h->P;
-  P.S = (int)c->state_size, P.A = (int)c->action_size, P.H = (int)c->hidden_size, P.L = (int)c->hidden_layers;
+  P.S = (int)c->state_size, P.A = (int)c->action_size, P.H = (int)((c->hidden_size + 63) / 64 * 64), P.L = (int)c->hidden_layers;
   P.O = 1 + 2 * P.A, P.E = (int)c->environments, P.B = (int)c->mini_batch_size, P.T = (int)c->max_episode_steps;
   P.R = (long long)c->replay_maximum_size;
   P.env_count = (int)c->environment_count;
@@ -1247,6 +1380,25 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
     k += (size_t)sz[l + 1];
   }
   h->nparam = k;
+  // the user layout (hidden width c->hidden_size) and its device positions
+  {
+    const size_t Hu = c->hidden_size;
+    std::vector<size_t> su{(size_t)P.S};
+    for (int l = 0; l < P.L; l++) su.push_back(Hu);
+    su.push_back((size_t)P.O);
+    size_t ku = 0;
+    for (size_t l = 0; l + 1 < su.size(); l++) ku += su[l] * su[l + 1] + su[l + 1];
+    h->nuser = ku;
+    if (Hu != (size_t)P.H) {
+      h->umap.reserve(ku);
+      for (size_t l = 0; l + 1 < su.size(); l++) {
+        const size_t in_d = (size_t)sz[l];  // device row length of this layer's W
+        for (size_t o = 0; o < su[l + 1]; o++)
+          for (size_t i = 0; i < su[l]; i++) h->umap.push_back(h->offW[l] + o * in_d + i);
+        for (size_t o = 0; o < su[l + 1]; o++) h->umap.push_back(h->offb[l] + o);
+      }
+    }
+  }
   h->rowsMax = std::max((size_t)P.E, (size_t)2 * P.B);
   const size_t R = (size_t)P.R, E = (size_t)P.E, ET = E * (size_t)P.T;
   int rc = 0;
@@ -1273,7 +1425,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(er.ret, R * 4), alloc(er.iw, R * 4), alloc(er.tiw, R * 4), alloc(er.tv, R * 4);
   alloc(er.env, R * 4), alloc(er.term, R * 4), alloc(er.onp, R * 4), alloc(er.ep_pos, R * 4), alloc(er.ep_id, R * 8);
   Envs &ev = h->ev;
-  alloc(ev.u, E * 4 * 8), alloc(ev.t, E * 4), alloc(ev.env_id, E * 4), alloc(ev.sample, E * 8), alloc(ev.cum, E * 4);
+  alloc(ev.u, E * 4 * 8), alloc(ev.time, E * 8), alloc(ev.t, E * 4), alloc(ev.env_id, E * 4), alloc(ev.sample, E * 8), alloc(ev.cum, E * 4);
   alloc(ev.fin, E * 4), alloc(ev.len, E * 4), alloc(ev.off, E * 8), alloc(ev.rank, E * 4), alloc(ev.fin_env, E * 4);
   alloc(ev.eb_st, ET * P.S * 4), alloc(ev.eb_act, ET * P.A * 4), alloc(ev.eb_pol, ET * 2 * P.A * 4);
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
@@ -1300,13 +1452,58 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   return 0;
 }
 
+// kg_debug_cartpole: trajectory n advances `steps` times with force[n][k]
+// from u0[n] at t = 0 (the device CartPole of k_vr_env_act)
+__global__ void k_vr_cartpole_debug(size_t n, size_t steps, const double *u0, const double *force, double *u_out,
+                                    int *over) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double y[4], t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) y[k] = u0[j * 4 + k];
+  for (size_t s = 0; s < steps; s++) {
+    const bool ok = cp_advance(y, t, force[j * steps + s]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) u_out[(j * steps + s) * 4 + k] = y[k];
+    over[j * steps + s] = ok ? (cp_failed(y) ? 1 : 0) : -1;
+  }
+}
+
+extern "C" int kg_debug_cartpole(int device, const double *u0, const double *force, size_t n, size_t steps,
+                                 double *u_out, int *over) {
+  KG_CHECK(u0 && force && u_out && over, "kg_debug_cartpole: null argument");
+  KG_CHECK(n >= 1 && steps >= 1 && n * steps <= (1u << 24), "kg_debug_cartpole: 1 <= n * steps <= 2^24");
+  KG_HIP(hipSetDevice(device));
+  double *d = nullptr;
+  int *o = nullptr;
+  const size_t nb = (n * 4 + 2 * n * steps * 4 + n * steps) * sizeof(double);
+  KG_HIP(hipMalloc(&d, nb));
+  double *du0 = d, *dforce = d + n * 4, *dout = dforce + n * steps;
+  o = (int *)(dout + n * steps * 4);
+  int rc = 0;
+  if (hipMemcpy(du0, u0, n * 4 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dforce, force, n * steps * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    rc = 1;
+  if (!rc) {
+    hipLaunchKernelGGL(k_vr_cartpole_debug, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, n, steps, du0, dforce,
+                       dout, o);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(u_out, dout, n * steps * 4 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(over, o, n * steps * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = 1;
+  }
+  (void)hipFree(d);
+  if (rc) kg::set_error("kg_debug_cartpole: device call failed");
+  return rc;
+}
+
 int kg_vracer_destroy(kg_vracer_t h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   void *ptrs[] = {h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
                   h->dHb, h->mb, h->forced_mb, h->forced_noise, h->st, h->er.st, h->er.act, h->er.rew, h->er.tst,
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
-                  h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.t, h->ev.env_id,
+                  h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,
                   h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
                   h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards};
   for (void *p : ptrs)
@@ -1321,7 +1518,7 @@ int kg_vracer_destroy(kg_vracer_t h) {
 
 int kg_vracer_hyperparameter_count(kg_vracer_t h, size_t *n) {
   KG_CHECK(h && n, "vracer: null argument");
-  *n = h->nparam;
+  *n = h->nuser;
   return 0;
 }
 
@@ -1339,6 +1536,14 @@ int kg_vracer_get_field(kg_vracer_t h, const char *name, void *dst, size_t bytes
   VrField f;
   KG_CHECK(vr_field(h, name, f), std::string("vracer: unknown field '") + name + "'");
   KG_CHECK(bytes <= f.elem * f.count, "vracer: field read exceeds its size");
+  if (f.param && !h->umap.empty()) {  // padded hidden width: gather the user layout
+    std::vector<float> dev(h->nparam);
+    KG_HIP(hipMemcpyAsync(dev.data(), f.ptr, h->nparam * 4, hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    float *o = (float *)dst;
+    for (size_t i = 0; i < bytes / 4; i++) o[i] = dev[h->umap[i]];
+    return 0;
+  }
   KG_HIP(hipMemcpyAsync(dst, f.ptr, bytes, hipMemcpyDeviceToHost, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -1349,6 +1554,16 @@ int kg_vracer_set_field(kg_vracer_t h, const char *name, const void *src, size_t
   VrField f;
   KG_CHECK(vr_field(h, name, f), std::string("vracer: unknown field '") + name + "'");
   KG_CHECK(bytes <= f.elem * f.count, "vracer: field write exceeds its size");
+  if (f.param && !h->umap.empty()) {  // padded hidden width: scatter, padding stays 0
+    std::vector<float> dev(h->nparam);
+    KG_HIP(hipMemcpyAsync(dev.data(), f.ptr, h->nparam * 4, hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    const float *in = (const float *)src;
+    for (size_t i = 0; i < bytes / 4; i++) dev[h->umap[i]] = in[i];
+    KG_HIP(hipMemcpyAsync(f.ptr, dev.data(), h->nparam * 4, hipMemcpyHostToDevice, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  }
   KG_HIP(hipMemcpyAsync(f.ptr, src, bytes, hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;

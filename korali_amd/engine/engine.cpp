@@ -1437,8 +1437,8 @@ struct VracerModule : SolverModule {
         fail("Hidden layer pair %zu must be Layer/Linear followed by Layer/Activation with Elementwise/Tanh.", l);
       const size_t oc = (size_t)uint(lin, "Output Channels", 0);
       if (l == 0) H = oc;
-      if (oc != H || H == 0 || H % 64)
-        fail("Hidden layers must share one width that is a multiple of 64 on the device path (layer %zu: %zu).", l, oc);
+      if (oc != H || H == 0)  // widths that are not multiples of 64 run zero-padded (kg_vracer.hip)
+        fail("Hidden layers must share one width on the device path (layer %zu: %zu).", l, oc);
     }
     Json &er = sv["Experience Replay"];
     Json &op = er["Off Policy"];

@@ -37,6 +37,8 @@ dopri5, and the random streams (action noise, mini-batch uniforms) come from
 a counter-based generator (philox4x32-10) instead of GSL's, so tests feed
 the same noise / ids to both sides.
 """
+import math
+
 import numpy as np
 
 f32 = np.float32
@@ -484,49 +486,158 @@ class Agent:
 
 # ------------------------------------------------------------- environment
 class CartPole:
-    """examples/learning/reinforcement/cartpole/_model/cartpole.py with a fixed-step
-    RK4 (one step of dt = 0.02) instead of scipy's adaptive dopri5."""
+    """examples/learning/reinforcement/cartpole/_model/cartpole.py: numpy-seeded
+    reset and scipy's `ode(system).set_integrator('dopri5')` advance, restated
+    below (dopri5_advance); pinned by tests/golden/cartpole_dopri5.json,
+    which the reference's own module produced (tools/make_cartpole_golden.py)."""
 
     dt, x_threshold, th_threshold = 0.02, 2.4, np.pi / 15
 
     def __init__(self):
         self.u = np.zeros(4)
+        self.t = 0.0
         self.step = 0
 
     def reset(self, seed):
         rs = np.random.RandomState(seed)
         self.u = rs.uniform(-0.05, 0.05, 4)
+        self.t = 0.0
         self.step = 0
 
     @staticmethod
     def system(y, act):
+        # cartpole.py:37-46, the same operation order (w**2 and costh**2 squared first)
         mp, mc, l, g = 0.1, 1.0, 0.5, 9.81
         x, v, th, w = y
         c, s = np.cos(th), np.sin(th)
         tot = mp + mc
-        tmp = (act + l * w * w * s) / tot
-        wdot = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * c * c / tot))
+        tmp = (act + l * (w * w) * s) / tot
+        wdot = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * (c * c) / tot))
         vdot = tmp - l * wdot * c / tot
-        return np.array([v, vdot, w, wdot])
+        return [float(v), float(vdot), float(w), float(wdot)]
 
     def failed(self):
         return abs(self.u[0]) > self.x_threshold or abs(self.u[2]) > self.th_threshold
 
     def advance(self, action):
+        # cartpole.py:48-62: F clipped to [-10, 10], ODE from t to t + dt
         F = min(max(float(action), -10.0), 10.0)
-        h = self.dt
-        y = self.u
-        k1 = self.system(y, F)
-        k2 = self.system(y + 0.5 * h * k1, F)
-        k3 = self.system(y + 0.5 * h * k2, F)
-        k4 = self.system(y + h * k3, F)
-        self.u = y + (h / 6.0) * (k1 + 2.0 * k2 + 2.0 * k3 + k4)
+        self.u = np.array(dopri5_advance(lambda y: self.system(y, F), [float(v) for v in self.u], self.t,
+                                         self.t + self.dt))
+        self.t = self.t + self.dt
         self.step += 1
         return self.failed()
 
     def reward(self, env_id):
         r = 1.0 - 1.0 * self.failed()
         return (r, r - 1.0, r * 0.1)[env_id % 3]
+
+
+# scipy.integrate.ode 'dopri5' = E. Hairer & G. Wanner's DOPRI5 (dopri5.f,
+# Dormand-Prince 5(4)), as scipy calls it for one integrate(): rtol 1e-6,
+# atol 1e-12 (scalars: ITOL 0), WORK = (UROUND 0 -> 2.3e-16, SAFE 0.9,
+# FAC1 0.2, FAC2 10, BETA 0 -> 0.04, HMAX 0 -> XEND - X, H 0 -> HINIT),
+# NMAX 500, no dense output.  Stiffness detection only prints, so it is left
+# out.  Fortran's left-to-right evaluation order is kept term by term.
+DP_C2, DP_C3, DP_C4, DP_C5 = 0.2, 0.3, 0.8, 8.0 / 9.0
+DP_A21 = 0.2
+DP_A31, DP_A32 = 3.0 / 40.0, 9.0 / 40.0
+DP_A41, DP_A42, DP_A43 = 44.0 / 45.0, -56.0 / 15.0, 32.0 / 9.0
+DP_A51, DP_A52, DP_A53, DP_A54 = 19372.0 / 6561.0, -25360.0 / 2187.0, 64448.0 / 6561.0, -212.0 / 729.0
+DP_A61, DP_A62, DP_A63, DP_A64, DP_A65 = 9017.0 / 3168.0, -355.0 / 33.0, 46732.0 / 5247.0, 49.0 / 176.0, \
+    -5103.0 / 18656.0
+DP_A71, DP_A73, DP_A74, DP_A75, DP_A76 = 35.0 / 384.0, 500.0 / 1113.0, 125.0 / 192.0, -2187.0 / 6784.0, 11.0 / 84.0
+DP_E1, DP_E3, DP_E4, DP_E5, DP_E6, DP_E7 = 71.0 / 57600.0, -71.0 / 16695.0, 71.0 / 1920.0, -17253.0 / 339200.0, \
+    22.0 / 525.0, -1.0 / 40.0
+DP_RTOL, DP_ATOL, DP_UROUND, DP_SAFE, DP_FAC1, DP_FAC2, DP_BETA, DP_NMAX = 1e-6, 1e-12, 2.3e-16, 0.9, 0.2, 10.0, \
+    0.04, 500
+
+
+def dopri5_hinit(f, x, y, f0, hmax):
+    """DOPRI5's HINIT (initial step: explicit Euler probe, order 5)."""
+    n = len(y)
+    dnf = dny = 0.0
+    for i in range(n):
+        sk = DP_ATOL + DP_RTOL * abs(y[i])
+        dnf = dnf + (f0[i] / sk) ** 2
+        dny = dny + (y[i] / sk) ** 2
+    h = 1.0e-6 if (dnf <= 1.0e-10 or dny <= 1.0e-10) else math.sqrt(dny / dnf) * 0.01
+    h = min(h, hmax)
+    y1 = [y[i] + h * f0[i] for i in range(n)]
+    f1 = f(y1)
+    der2 = 0.0
+    for i in range(n):
+        sk = DP_ATOL + DP_RTOL * abs(y[i])
+        der2 = der2 + ((f1[i] - f0[i]) / sk) ** 2
+    der2 = math.sqrt(der2) / h
+    der12 = max(abs(der2), math.sqrt(dnf))
+    h1 = max(1.0e-6, abs(h) * 1.0e-3) if der12 <= 1.0e-15 else (0.01 / der12) ** (1.0 / 5)
+    return min(100 * abs(h), h1, hmax)
+
+
+def dopri5_advance(f, y, x, xend):
+    """DOPRI5's DOPCOR from x to xend (forward): returns y(xend)."""
+    n = len(y)
+    y = list(y)
+    expo1 = 0.2 - DP_BETA * 0.75
+    facc1, facc2 = 1.0 / DP_FAC1, 1.0 / DP_FAC2
+    facold = 1.0e-4
+    hmax = abs(xend - x)
+    k1 = f(y)
+    h = dopri5_hinit(f, x, y, k1, hmax)
+    last, reject, naccpt, nstep = False, False, 0, 0
+    while True:
+        if nstep > DP_NMAX:
+            raise RuntimeError("dopri5: more than NMAX steps")
+        if 0.1 * abs(h) <= abs(x) * DP_UROUND:
+            raise RuntimeError("dopri5: step size too small")
+        if (x + 1.01 * h - xend) > 0.0:
+            h = xend - x
+            last = True
+        nstep += 1
+        y1 = [y[i] + h * DP_A21 * k1[i] for i in range(n)]
+        k2 = f(y1)
+        y1 = [y[i] + h * (DP_A31 * k1[i] + DP_A32 * k2[i]) for i in range(n)]
+        k3 = f(y1)
+        y1 = [y[i] + h * (DP_A41 * k1[i] + DP_A42 * k2[i] + DP_A43 * k3[i]) for i in range(n)]
+        k4 = f(y1)
+        y1 = [y[i] + h * (DP_A51 * k1[i] + DP_A52 * k2[i] + DP_A53 * k3[i] + DP_A54 * k4[i]) for i in range(n)]
+        k5 = f(y1)
+        ysti = [y[i] + h * (DP_A61 * k1[i] + DP_A62 * k2[i] + DP_A63 * k3[i] + DP_A64 * k4[i] + DP_A65 * k5[i])
+                for i in range(n)]
+        xph = x + h
+        k6 = f(ysti)
+        y1 = [y[i] + h * (DP_A71 * k1[i] + DP_A73 * k3[i] + DP_A74 * k4[i] + DP_A75 * k5[i] + DP_A76 * k6[i])
+              for i in range(n)]
+        k2 = f(y1)
+        k4 = [(DP_E1 * k1[i] + DP_E3 * k3[i] + DP_E4 * k4[i] + DP_E5 * k5[i] + DP_E6 * k6[i] + DP_E7 * k2[i]) * h
+              for i in range(n)]
+        err = 0.0
+        for i in range(n):
+            sk = DP_ATOL + DP_RTOL * max(abs(y[i]), abs(y1[i]))
+            err = err + (k4[i] / sk) ** 2
+        err = math.sqrt(err / n)
+        fac11 = err ** expo1
+        fac = fac11 / facold ** DP_BETA
+        fac = max(facc2, min(facc1, fac / DP_SAFE))
+        hnew = h / fac
+        if err <= 1.0:
+            facold = max(err, 1.0e-4)
+            naccpt += 1
+            k1, y = k2, y1
+            x = xph
+            if last:
+                return y
+            if abs(hnew) > hmax:
+                hnew = hmax
+            if reject:
+                hnew = min(abs(hnew), abs(h))
+            reject = False
+        else:
+            hnew = h / min(facc1, fac11 / DP_SAFE)
+            reject = True
+            last = False
+        h = hnew
 
 
 # ------------------------------------------------------ counter-based streams

@@ -4,6 +4,9 @@
 # summaries are copied to profiles/$ROUND/ afterwards; trace csvs dropped).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+# cooperative grids launched plainly after the same co-residency check:
+# rocprofv3 segfaults at teardown after any cooperative launch (kg_common.hpp)
+export KORALI_AMD_PLAIN_LAUNCH=1
 R=$PWD
 O=$R/gpurun_out/${ROUND:-r3}
 mkdir -p $O
@@ -36,6 +39,8 @@ for s in ${STEPS:-tests}; do
     pmcw4) step pmcw4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 4 --warmup 1 --no-cpu-baseline ;;
     trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c2.py ;;
     trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python $R/tools/trace_c4.py ;;
+    dist) step dist 700 python -u -m pytest $R/tests/test_gpu_distributed.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
+    engvr) step engvr 500 python -u -m pytest $R/tests/test_gpu_engine.py -x -v -k vracer --timeout 300 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
     vrtests) step vrtests 400 python -u -m pytest $R/tests/test_gpu_vracer.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
     c5) step c5 300 python $R/bench.py --workload c5 --steps 10 --warmup 2 ;;
     profc5) step profc5 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;

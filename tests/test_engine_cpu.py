@@ -184,7 +184,7 @@ from vracer_cases import cartpole_vracer  # noqa: E402
     (lambda e: e["Solver"]["Policy"].__setitem__("Distribution", "Squashed Normal"), "Policy Distribution"),
     (lambda e: (e["Solver"]["Policy"].__setitem__("Distribution", "Clipped Normal"),
                 e["Variables"][4].__setitem__("Upper Bound", float("inf"))), "non-finite"),
-    (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][2].__setitem__("Output Channels", 96), "multiple of 64"),
+    (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][2].__setitem__("Output Channels", 96), "one width"),
     (lambda e: e["Solver"]["Neural Network"]["Hidden Layers"][1].__setitem__("Function", "Elementwise/ReLU"),
      "Elementwise/Tanh"),
     (lambda e: e["Solver"]["State Rescaling"].__setitem__("Enabled", True), "State Rescaling"),

@@ -621,6 +621,27 @@ def test_cmaes_gradient_information_through_the_api():
         korali.Engine().run(experiment(sphere, step=0.0))
 
 
+def test_run_vracer_example_configuration_unchanged():
+    """examples/learning/reinforcement/cartpole/run-vracer.py exactly as its
+    defaults run it (50 generations of 10 episodes, 1 concurrent environment,
+    3 environment variants, two 32-wide tanh layers, Clipped Normal policy,
+    learning rate 1e-4, mini-batch 32, replay 1000 / 10000, one update per
+    experience), the host `env` replaced by the device CartPole kernel."""
+    import korali
+    from vracer_cases import cartpole_vracer
+    e = cartpole_vracer()
+    assert e["Solver"]["Neural Network"]["Hidden Layers"][0]["Output Channels"] == 32
+    korali.Engine().run(e)
+    sv = e["Solver"]
+    assert e["Current Generation"] == 50 and sv["Current Episode"] == 500
+    assert sv["Experience Count"] > 1000 and sv["Policy Update Count"] > 0
+    pol = sv["Training"]["Current Policy"]["Policy"]
+    assert len(pol) == (4 * 32 + 32) + (32 * 32 + 32) + (32 * 3 + 3)  # the reference's hyperparameter count
+    assert np.all(np.isfinite(pol))
+    hist = np.array(sv["Training"]["Reward History"])
+    assert hist.size == 500 and np.all(np.isfinite(hist))
+
+
 @pytest.mark.parametrize("policy", ["Normal", "Clipped Normal"])
 def test_vracer_cartpole_through_korali_engine(policy):
     """examples/learning/reinforcement/cartpole/run-vracer.py's configuration

@@ -1,9 +1,11 @@
 """CPU checks of the VRACER oracle (oracle/vracer_ref.py) — the checker of the
-device agent (korali_amd/csrc/kg_vracer.hip).  No reference fixture covers
-VRACER (parity unpinned); these pin the restatement's pieces
+device agent (korali_amd/csrc/kg_vracer.hip).  The CartPole environment is
+pinned to the reference's own module (tests/golden/cartpole_dopri5.json,
+written by tools/make_cartpole_golden.py from cartpole.py with scipy's
+dopri5): resets and trajectories bit-exact.  The agent's pieces are pinned
 against independent definitions: Random123's philox known answers, numpy's
-own RandomState for the CartPole resets, finite differences for the
-backward pass, and the reference's formulas checked term by term."""
+own RandomState for the resets, finite differences for the backward pass,
+and the reference's formulas checked term by term."""
 import os
 import sys
 
@@ -57,6 +59,34 @@ def test_cartpole_reset_equals_numpy_random_state(sid):
     c = V.CartPole()
     c.reset(sid * 1024 + sid)  # env.py: cart.reset(sampleId * 1024 + launchId)
     assert np.array_equal(mt_reset(sid * 1024 + sid), c.u)
+
+
+def cartpole_golden():
+    import json
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "cartpole_dopri5.json")))
+
+
+def test_cartpole_resets_match_reference_goldens():
+    for r in cartpole_golden()["resets"]:
+        c = V.CartPole()
+        c.reset(r["seed"])
+        assert list(c.u) == r["u"], r["seed"]
+        assert list(mt_reset(r["seed"])) == r["u"], r["seed"]  # the device's restatement
+
+
+def test_cartpole_dopri5_matches_reference_trajectories():
+    """The oracle's DOPRI5 restatement reproduces scipy's dopri5 bit for bit
+    on every state of every golden trajectory (clip at +-10 included)."""
+    g = cartpole_golden()
+    assert sum(len(t["u"]) for t in g["trajectories"]) > 500
+    for t in g["trajectories"]:
+        c = V.CartPole()
+        c.reset(t["seed"])
+        assert list(c.u) == t["u0"]
+        for k, (f, u, over, rew) in enumerate(zip(t["force"], t["u"], t["over"], t["reward"])):
+            assert int(c.advance(f)) == over
+            assert list(c.u) == u, (t["seed"], k)
+            assert c.reward(0) == rew
 
 
 def test_backward_matches_finite_differences():

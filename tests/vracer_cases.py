@@ -3,7 +3,10 @@ configuration, on the device CartPole environment kernel."""
 import korali
 
 
-def cartpole_vracer(max_generations=5, environments=64, hidden=64, policy="Normal", kernel="CartPole"):
+def cartpole_vracer(max_generations=50, environments=1, hidden=32, policy="Clipped Normal", kernel="CartPole"):
+    """run-vracer.py with its defaults (50 generations, 1 concurrent
+    environment, two 32-wide tanh layers, Clipped Normal policy); the host
+    `env` function replaced by the device CartPole kernel."""
     e = korali.Experiment()
     e["Problem"]["Type"] = "Reinforcement Learning / Continuous"
     if kernel is None:
