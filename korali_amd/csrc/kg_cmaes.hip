@@ -140,63 +140,154 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
 // sampleSingle (CMAES.cpp.base:494-545): x = m + σ B (D∘z), the B·aux sum in
 // the reference's order (e = 0..N-1 from 0.0, separate multiply and add);
 // isSampleFeasible (optimizer.cpp.base:5-14) folded into the epilogue.
-constexpr int TR_BM = 32, TR_BN = 64, TR_BK = 32;
+constexpr int TR_BK = 32, TR_XCD = 8;
+// Tiles of BM rows x BN columns, (BM/8) x (BN/32) outputs per thread (rows
+// ty PR + p, columns tx PC + q), K in chunks of TR_BK staged through LDS; the
+// next chunk's global loads are issued into registers before the current
+// chunk is summed, so their latency hides behind it.  XCD-aware order: the
+// hardware deals workgroup b to XCD b % 8, so the column tiles of one row
+// tile go to consecutive workgroups of ONE XCD — its Z rows come from HBM
+// once and from that XCD's L2 for the other column tiles (row-major order
+// sends each column tile of a row tile to a different XCD and fetches the
+// row tile N / BN times).  The grid is padded to whole groups of 8 row
+// tiles; surplus workgroups exit.
+template <int BM, int BN>
+inline unsigned tr_grid(int rows, int N) {
+  const int nbm = (rows + BM - 1) / BM, nbn = (N + BN - 1) / BN;
+  return (unsigned)(((nbm + TR_XCD - 1) / TR_XCD) * TR_XCD * nbn);
+}
+template <int BM, int BN>
 __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal, const double *__restrict__ Z,
                                                    const double *__restrict__ B, const double *__restrict__ D,
                                                    const double *__restrict__ mean, CmaesScalars *__restrict__ sc,
                                                    const double *__restrict__ lb, const double *__restrict__ ub,
                                                    double *__restrict__ X, double *__restrict__ BDZ,
                                                    int *__restrict__ infeas, int no_reserve, int mirrored) {
-  __shared__ double Za[TR_BK][TR_BM + 1];
-  __shared__ double Bt[TR_BK][TR_BN + 1];
+  constexpr int PR = BM / 8, PC = BN / 32, ZL = BM * TR_BK / 256, BL = BN * TR_BK / 256;
+  // rows padded by 2 doubles: 16-B aligned, so a thread's PR contiguous rows
+  // and PC contiguous columns come in 16-B reads (ds_read_b128: 256 B per
+  // LDS clock, where the paired ds_read2_b64 moves 128)
+  __shared__ __attribute__((aligned(16))) double Za[TR_BK][BM + 2];
+  __shared__ __attribute__((aligned(16))) double Bt[TR_BK][BN + 2];
   const int tid = threadIdx.x;
-  const int nbn = (N + TR_BN - 1) / TR_BN;
-  const int i0 = (blockIdx.x / nbn) * TR_BM, d0 = (blockIdx.x % nbn) * TR_BN;
-  const int tx = tid & 31, ty = tid >> 5;  // dims tx, tx+32; cands ty + 8p
+  const int nbn = (N + BN - 1) / BN;
+  const int xcd = blockIdx.x % TR_XCD, j = blockIdx.x / TR_XCD;
+  const int rt = (j / nbn) * TR_XCD + xcd, ct = j % nbn;
+  const int i0 = rt * BM, d0 = ct * BN;
+  if (i0 >= rows) return;
+  const int tx = tid & 31, ty = tid >> 5;
   const double sigma = sc->sigma;
-  double acc[4][2];
+  double acc[PR][PC];
 #pragma unroll
-  for (int p = 0; p < 4; p++) acc[p][0] = acc[p][1] = 0.0;
+  for (int p = 0; p < PR; p++)
+#pragma unroll
+    for (int q = 0; q < PC; q++) acc[p][q] = 0.0;
   if (!diagonal) {
-    for (int k0 = 0; k0 < N; k0 += TR_BK) {
-      for (int q = tid; q < TR_BM * TR_BK; q += 256) {
-        const int c = q / TR_BK, kk = q % TR_BK;
-        const int i = i0 + c, e = k0 + kk;
-        // Mirrored Sampling (:461-491): rows 2j and 2j+1 take z_j and -z_j
+    double zr[ZL], br[BL];
+    // element r of this thread's share: flat index tid + 256 r, K fastest
+    // (coalesced along rows of Z and B)
+    auto load = [&](int k0) {
+#pragma unroll
+      for (int r = 0; r < ZL; r++) {
+        const int q = tid + 256 * r, c = q / TR_BK, e = k0 + q % TR_BK, i = i0 + c;
         double z = 0.0;
         if (i < rows && e < N) {
+          // Mirrored Sampling (:461-491): rows 2j and 2j+1 take z_j and -z_j
           z = Z[(size_t)(mirrored ? (i >> 1) : i) * N + e];
           if (mirrored && (i & 1)) z = -z;
+          z = D[e] * z;
         }
-        Za[kk][c] = (i < rows && e < N) ? D[e] * z : 0.0;
+        zr[r] = z;
       }
-      for (int q = tid; q < TR_BN * TR_BK; q += 256) {
-        const int dd = q / TR_BK, kk = q % TR_BK;
-        const int d = d0 + dd, e = k0 + kk;
-        Bt[kk][dd] = (d < N && e < N) ? B[(size_t)d * N + e] : 0.0;
-      }
-      __syncthreads();
-      const int kmax = (N - k0) < TR_BK ? (N - k0) : TR_BK;
-      for (int kk = 0; kk < kmax; kk++) {
-        const double b0 = Bt[kk][tx], b1 = Bt[kk][tx + 32];
 #pragma unroll
-        for (int p = 0; p < 4; p++) {
-          const double a = Za[kk][ty + 8 * p];
-          acc[p][0] += b0 * a;
-          acc[p][1] += b1 * a;
+      for (int r = 0; r < BL; r++) {
+        const int q = tid + 256 * r, dd = q / TR_BK, e = k0 + q % TR_BK, d = d0 + dd;
+        br[r] = (d < N && e < N) ? B[(size_t)d * N + e] : 0.0;
+      }
+    };
+    auto store = [&]() {
+#pragma unroll
+      for (int r = 0; r < ZL; r++) {
+        const int q = tid + 256 * r;
+        Za[q % TR_BK][q / TR_BK] = zr[r];
+      }
+#pragma unroll
+      for (int r = 0; r < BL; r++) {
+        const int q = tid + 256 * r;
+        Bt[q % TR_BK][q / TR_BK] = br[r];
+      }
+    };
+    load(0);
+    store();
+    __syncthreads();
+    for (int k0 = 0; k0 < N; k0 += TR_BK) {
+      const bool more = k0 + TR_BK < N;
+      if (more) load(k0 + TR_BK);
+      const int kmax = (N - k0) < TR_BK ? (N - k0) : TR_BK;
+      // operands of step kk + 1 are read from LDS while step kk is summed
+      double a0[PR], b0[PC], a1[PR], b1[PC];
+      auto fetch = [&](double *a, double *b, int kk) {
+#pragma unroll
+        for (int q = 0; q < PC; q += 2) {
+          const double2 v = *(const double2 *)&Bt[kk][tx * PC + q];
+          b[q] = v.x, b[q + 1] = v.y;
+        }
+#pragma unroll
+        for (int p = 0; p < PR; p += 2) {
+          const double2 v = *(const double2 *)&Za[kk][ty * PR + p];
+          a[p] = v.x, a[p + 1] = v.y;
+        }
+      };
+      // products formed in groups of 8 before their adds: independent
+      // multiplies in flight instead of a mul -> add pair through one
+      // temporary (issue-bound at one wave-op per ~8 cycles per wave)
+      auto madd = [&](const double *a, const double *b) {
+        static_assert((PR * PC) % 8 == 0, "8-product groups");
+#pragma unroll
+        for (int g = 0; g < PR * PC; g += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t[u] = b[(g + u) % PC] * a[(g + u) / PC];
+#pragma unroll
+          for (int u = 0; u < 8; u++) acc[(g + u) / PC][(g + u) % PC] += t[u];
+        }
+      };
+      fetch(a0, b0, 0);
+      if (kmax == TR_BK) {
+        // whole chunk, no conditions in the loop: the waits before each
+        // product group cover only the reads it consumes (lgkmcnt(n), n > 0)
+#pragma unroll 1
+        for (int kk = 0; kk < TR_BK - 2; kk += 2) {
+          fetch(a1, b1, kk + 1);
+          madd(a0, b0);
+          fetch(a0, b0, kk + 2);
+          madd(a1, b1);
+        }
+        fetch(a1, b1, TR_BK - 1);
+        madd(a0, b0);
+        madd(a1, b1);
+      } else {
+#pragma unroll 1
+        for (int kk = 0; kk < kmax; kk++) {
+          fetch(a0, b0, kk);
+          madd(a0, b0);
         }
       }
       __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
     }
   }
 #pragma unroll
-  for (int p = 0; p < 4; p++) {
-    const int i = i0 + ty + 8 * p;
+  for (int p = 0; p < PR; p++) {
+    const int i = i0 + ty * PR + p;
     if (i >= rows) continue;
     int bad = 0;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const int d = d0 + tx + 32 * q;
+    for (int q = 0; q < PC; q++) {
+      const int d = d0 + tx * PC + q;
       if (d >= N) continue;
       double zd = 0.0;
       if (diagonal) {
@@ -1861,12 +1952,13 @@ int kg_cmaes_sample(kg_cmaes_t h) {
   {
     Stage st(h, "transform");
     if (h->R) KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
-    const int nbn = (N + TR_BN - 1) / TR_BN;
     const size_t trows = h->R ? rows : (size_t)(h->r1 - h->r0);  // a shard transforms its own rows only
-    const int nbm = (int)((trows + TR_BM - 1) / TR_BM);
     double *xo = h->R ? h->Xall : h->X + (size_t)h->r0 * N;
     double *bo = h->R ? h->BDZall : (h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr);
-    hipLaunchKernelGGL(k_transform, dim3(nbm * nbn), dim3(256), 0, h->stream, N, (int)trows,
+    // 32 x 64 tiles, 4 x 2 outputs per thread: larger register tiles drop the
+    // kernel to 2 waves per SIMD and measured slower at C4 (1.96 / 2.25 ms
+    // for 32 x 128 / 64 x 64 against 1.73 ms)
+    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N, (int)trows,
                        h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
                        h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
     KG_HIP(hipGetLastError());
