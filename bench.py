@@ -382,6 +382,10 @@ def main():
     F_gen = 2 * LAMBDA * N_VARS ** 2 + 2 * MU * N_VARS ** 2 + 10 * N_VARS ** 3 + 8 * LAMBDA * N_VARS
     B_gen = 8 * (2 * LAMBDA * N_VARS + MU * N_VARS + 4 * N_VARS ** 2) + 24 * LAMBDA
     t_roof = max(F_gen / (FP64_PEAK_TFLOPS * 1e12), B_gen / (HBM_PEAK_GBS * 1e9))
+    # the tridiagonalisation's dependency bound: three ordered chains of
+    # n = N-1-i dependent FP64 adds per Householder step at the measured 14
+    # shader cycles per add (tools/ubench_chain*.hip), 2.4 GHz
+    chain_bound_ms = sum(3 * n for n in range(2, N_VARS)) * 14 / 2.4e9 * 1e3
     out = {
         "metric": "CMA-ES generations/sec + samples/sec, 128-dim Rosenbrock λ=4096, 1→8 GPUs",
         "value": gens_per_s,
@@ -406,11 +410,13 @@ def main():
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
-        "roofline": {"kernel": {"min_search": "kg::k_tm_nm_search"}.get(dominant, dominant), "stage": dominant,
+        "roofline": {"kernel": {"eigen_tridiag": "kg::k_tridiag_sq"}.get(dominant, dominant), "stage": dominant,
                      "bound": "mfma",
-                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is a "
-                                   "chain of dependent rounds (GSL nmsimplex order, two cross-XCD hand-offs per "
-                                   "round), far below it by construction",
+                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is "
+                                   "GSL's Householder tridiagonalisation, three ordered FP64 add chains of length "
+                                   "N-1-i per step (dnrm2, dsymv, ddot) whose order the bit-exact contract fixes, "
+                                   "so it is bound by the dependent-add latency, far below the roof by construction",
+                     "chain_bound_ms": chain_bound_ms,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_raw_fetch": traffic_raw,

@@ -846,6 +846,129 @@ __global__ void __launch_bounds__(256) k_adaptC_exact2(int N, int mu, int diagon
   }
 }
 
+// The same ordered sums with the chain split from its operands.  One
+// workgroup per 4-row x 16-column tile of the lower triangle: wave 0 runs the
+// 64 chains (one per lane, kc_add over quotients staged in LDS, one dependent
+// add per term), waves 1..AX3_P form the next 64 quotients of every chain
+// (Yc / T loads one chunk ahead, the Markstein quotient) meanwhile.  A single
+// wave forming its own quotients issues five FP64 operations per term and is
+// issue-bound well above the add latency; here the add chain is the bound.
+// Tiles of 16-column block cb run on XCD cb % 8 (workgroup slot s -> XCD s % 8),
+// so a column block of Yc is fetched from HBM into one L2.
+constexpr int AX3_P = 7, AX3_K = 64, AX3_S = AX3_K + 1;  // producers, chunk, LDS row stride
+__device__ __forceinline__ int ax3_tiles_in(int N, int cb) {  // row blocks of column block cb
+  const int R = (N + 3) / 4, lo = 4 * cb;
+  return R > lo ? R - lo : 0;
+}
+int ax3_slots(int N) {
+  int mx = 0;
+  for (int x = 0; x < 8; x++) {
+    int cnt = 0;
+    for (int cb = x; 16 * cb < N; cb += 8) cnt += std::max(0, (N + 3) / 4 - 4 * cb);
+    mx = std::max(mx, cnt);
+  }
+  return 8 * mx;
+}
+template <bool kMarkstein>
+__device__ __forceinline__ double ax3_run(double c, const double *__restrict__ Yc, const double *__restrict__ Tt,
+                                          int N, int mu, int d0, int e0, int wid, int lane, double s2, double y,
+                                          double (*Q)[64 * AX3_S + 16]) {
+  const int r = lane >> 4, cc = lane & 15, d = d0 + r, e = e0 + cc;
+  const bool rowok = d < N, colok = e < N;
+  constexpr int KP = (AX3_K + AX3_P - 1) / AX3_P;  // quotients per producer lane per chunk
+  double yA[KP], tA[KP], yB[KP], tB[KP];
+  const int p = wid - 1;
+  auto load = [&](int k0, double(&yv)[KP], double(&tv)[KP]) {
+#pragma unroll
+    for (int u = 0; u < KP; u++) {
+      const int kl = p + AX3_P * u, k = k0 + kl;
+      const bool ok = kl < AX3_K && k < mu;
+      yv[u] = (ok && colok) ? Yc[(size_t)k * N + e] : 0.0;
+      tv[u] = (ok && rowok) ? Tt[(size_t)d * mu + k] : 0.0;
+    }
+  };
+  auto store = [&](int buf, const double(&yv)[KP], const double(&tv)[KP]) {
+#pragma unroll
+    for (int u = 0; u < KP; u++) {
+      const int kl = p + AX3_P * u;
+      if (kl < AX3_K) Q[buf][lane * AX3_S + kl] = rankmu_quot<kMarkstein>(tv[u], yv[u], s2, y);
+    }
+  };
+  auto chain = [&](int k0, int buf) {
+    const int cnt = min(AX3_K, mu - k0), g = cnt >> 4;
+    const double *row = &Q[buf][lane * AX3_S];
+    c = chains::kc_add(c, lds_addr(row), __builtin_amdgcn_readfirstlane((unsigned)g));
+    for (int u = 16 * g; u < cnt; u++) c += row[u];
+  };
+  // producers: in the round where wave 0 sums chunk k, the loads of chunk
+  // k+2 are issued first, then chunk k+1's quotients are formed from the
+  // registers its loads filled one round earlier (two register sets in turn)
+  if (wid > 0) {
+    load(0, yA, tA);
+    if (AX3_K < mu) load(AX3_K, yB, tB);
+    store(0, yA, tA);
+  }
+  __syncthreads();
+  for (int k0 = 0; k0 < mu; k0 += 2 * AX3_K) {
+    // round k0: chunk k0 (buffer 0) summed; chunk k0+K (registers B) formed; chunk k0+2K loaded into A
+    if (wid == 0) chain(k0, 0);
+    else if (k0 + AX3_K < mu) {
+      if (k0 + 2 * AX3_K < mu) load(k0 + 2 * AX3_K, yA, tA);
+      store(1, yB, tB);
+    }
+    __syncthreads();
+    if (k0 + AX3_K >= mu) break;
+    // round k0+K: chunk k0+K (buffer 1) summed; chunk k0+2K (registers A) formed; chunk k0+3K loaded into B
+    if (wid == 0) chain(k0 + AX3_K, 1);
+    else if (k0 + 2 * AX3_K < mu) {
+      if (k0 + 3 * AX3_K < mu) load(k0 + 3 * AX3_K, yB, tB);
+      store(0, yA, tA);
+    }
+    __syncthreads();
+  }
+  return c;
+}
+__global__ void __launch_bounds__(64 * (AX3_P + 1)) k_adaptC_exact3(int N, int mu, int diagonal,
+                                                                    const double *__restrict__ Yc,
+                                                                    const double *__restrict__ Tt,
+                                                                    const double *__restrict__ pc, double *C,
+                                                                    const CmaesScalars *__restrict__ sc) {
+  __shared__ __attribute__((aligned(16))) double Q[2][64 * AX3_S + 16];
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  // slot -> (column block, row block)
+  const int x = blockIdx.x & 7;
+  int j = blockIdx.x >> 3, cb = x, rb = -1;
+  for (; 16 * cb < N; cb += 8) {
+    const int t = ax3_tiles_in(N, cb);
+    if (j < t) {
+      rb = 4 * cb + j;
+      break;
+    }
+    j -= t;
+  }
+  if (rb < 0) return;  // workgroup-uniform: past this XCD's tiles
+  const int d0 = 4 * rb, e0 = 16 * cb;
+  const int d = d0 + (lane >> 4), e = e0 + (lane & 15);
+  const bool active = wid == 0 && d < N && e < N && e <= d && (!diagonal || e == d);
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double s2 = sc->sigma * sc->sigma;
+  double c = 0.0;
+  if (active) {
+    const double Cde = C[(size_t)d * N + e];
+    c = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  }
+  const int ex = (int)((__double_as_longlong(s2) >> 52) & 0x7ff) - 1023;
+  if (__builtin_amdgcn_readfirstlane((int)(sc->rmuOutOfRange == 0u && ex >= -100 && ex <= 100)))
+    c = ax3_run<true>(c, Yc, Tt, N, mu, d0, e0, wid, lane, s2, 1.0 / s2, Q);
+  else
+    c = ax3_run<false>(c, Yc, Tt, N, mu, d0, e0, wid, lane, s2, 0.0, Q);
+  if (active) {
+    C[(size_t)d * N + e] = c;
+    if (e < d) C[(size_t)e * N + d] = c;
+  }
+}
+
 // mean :603-609 and mean update :623-624.  The sum over the μ selected rows
 // is sequential per d (the reference's order); a workgroup owns MN_D columns:
 // all its threads stream the products w_i Y[i][d] into LDS, 256 rows at a
@@ -2131,8 +2254,13 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
       KG_HIP(hipStreamWaitEvent(h->stream, h->evC, 0));
-      hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
-                         h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
+      static const bool old2 = getenv("KORALI_AMD_ADAPTC2") != nullptr;  // A/B switch
+      if (old2)
+        hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
+                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
+      else
+        hipLaunchKernelGGL(k_adaptC_exact3, dim3(ax3_slots(N)), dim3(64 * (AX3_P + 1)), 0, h->stream, N, mu,
+                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
     }
     KG_HIP(hipGetLastError());
   }

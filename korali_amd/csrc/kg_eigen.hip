@@ -2252,29 +2252,44 @@ __global__ void __launch_bounds__(64) k_chase(int N, const double *__restrict__ 
 // nested in the previous one's (a_s >= a_{s-1}, a_s + nb_s <= a_{s-1} +
 // nb_{s-1}); any other step starts a new group.  Every entry still sees the
 // same operations in the same order, so the result is GSL's bit for bit.
-constexpr int APPLY_TEAM = 16, APPLY_ROWS = 16, APPLY_TPB = APPLY_TEAM * APPLY_ROWS;
+// A team is one whole wave (64 steps in flight per row, one row per wave)
+// by default; KORALI_AMD_APPLY_TEAM=16 selects the round-2 layout (16-lane
+// teams, 4 rows per wave) for comparison.  Fewer, longer groups: a group of K
+// nested steps costs about 2K + nb units, so 64-step groups need about half
+// the units of 16-step ones at the CMA-ES shapes.
+constexpr int APPLY_TPB = 256;
+template <int TEAM> struct ApplyGeom {
+  static constexpr int ROWS = APPLY_TPB / TEAM;
+};
+static int apply_team() {
+  static const int t = (getenv("KORALI_AMD_APPLY_TEAM") && atoi(getenv("KORALI_AMD_APPLY_TEAM")) == 16) ? 16 : 64;
+  return t;
+}
+static int apply_rows() { return APPLY_TPB / apply_team(); }
 constexpr int APF = 4;  // apply: rotations prefetched ahead of the systolic replay
 
-// x of lane l-1 (row_shr:1 within each 16-lane DPP row = one team; the
-// team's lane 0 gets 0 and never uses it)
+// x of lane l-1 within the team (16 lanes: row_shr:1 within each DPP row;
+// 64 lanes: wave_shr:1); the team's lane 0 gets 0 and never uses it
+template <int TEAM>
 __device__ inline double dpp_shr1(double x) {
+  constexpr int CTRL = TEAM == 64 ? 0x138 : 0x111;
   const long long v = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), 0x111, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), 0x111, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(v & 0xffffffffLL), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xf, 0xf, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 constexpr int APPLY_HCAP = 256;  // step headers per LDS chunk
 constexpr int APPLY_MINSTEP = 16;  // streamed apply: smallest batch of new steps worth a chunk
 // rotations per LDS chunk: up to 4096, what fits next to the rows (>= N - 1,
 // one whole QR step, for every N the CMA-ES path accepts)
-__host__ __device__ inline int apply_cap(int N) {
+__host__ __device__ inline int apply_cap(int N, int rows) {
   const long long avail =
-      160LL * 1024 - (long long)N * (APPLY_ROWS + 1) * 8 - 8 * APPLY_HCAP - 16 - 8 * APPLY_TPB - 512;
+      160LL * 1024 - (long long)N * (rows + 1) * 8 - 8 * APPLY_HCAP - 16 - 8 * APPLY_TPB - 512;
   const long long c = avail / 16;
   return (int)(c > 4096 ? 4096 : c);
 }
-__host__ __device__ inline size_t apply_lds_bytes(int N) {
-  return (size_t)N * (APPLY_ROWS + 1) * sizeof(double) + 16 * (size_t)apply_cap(N) + 8 * APPLY_HCAP + 16 +
+__host__ __device__ inline size_t apply_lds_bytes(int N, int rows) {
+  return (size_t)N * (rows + 1) * sizeof(double) + 16 * (size_t)apply_cap(N, rows) + 8 * APPLY_HCAP + 16 +
          8 * APPLY_TPB;
 }
 
@@ -2429,7 +2444,7 @@ __device__ void apply_fetcher(int N, EigRec hr, EigRec dr, unsigned long long *h
 // memory, a chunk as soon as the chase has published it (progress word with
 // a per-generation sequence number), so the apply trails the chase by about
 // one chunk instead of starting after it.
-template <bool kStream>
+template <bool kStream, int TEAM>
 __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__restrict__ gQt, EigRec r,
                                                      double *__restrict__ B, double *__restrict__ D, double *minEig,
                                                      double *maxEig, double *eigenFailures, unsigned int *errors,
@@ -2438,11 +2453,12 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   unsigned long long ngroups = 0, nunits = 0, tstart = __builtin_amdgcn_s_memtime();
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lda = N + 1;
+  constexpr int APPLY_ROWS = ApplyGeom<TEAM>::ROWS, APPLY_TEAM = TEAM;
   const int S = APPLY_ROWS + 1;                  // Lq[c * S + kl] = Q[k0 + kl][c]
   const int k0 = blockIdx.x * APPLY_ROWS;
   const int nrows = min(APPLY_ROWS, N - k0);
   double *Lq = smem;
-  const int cap = apply_cap(N);
+  const int cap = apply_cap(N, APPLY_ROWS);
   double *csh = Lq + (size_t)N * S;              // cap (c, s) pairs
   int *hsh = (int *)(csh + 2 * (size_t)cap);      // APPLY_HCAP (a, nb)
   int *chunk = hsh + 2 * APPLY_HCAP;
@@ -2544,30 +2560,65 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     int t = 0, ro = 0;
     while (t < tn) {
       // group of up to APPLY_TEAM nested steps (uniform across the workgroup)
-      int my_a = 0, my_nb = 0, my_d = -1, my_ro = 0;
-      int pa = hsh[2 * t], pnb = hsh[2 * t + 1], pd = 0, pro = ro, T = pnb - 1, K = 1;
-      if (s == 0) {
-        my_a = pa;
-        my_nb = pnb;
-        my_d = 0;
-        my_ro = pro;
-      }
-      while (K < APPLY_TEAM && t + K < tn) {
-        const int a2 = hsh[2 * (t + K)], nb2 = hsh[2 * (t + K) + 1];
-        if (a2 < pa || a2 + nb2 > pa + pnb) break;
-        const int d2 = pd + 2 + (a2 - pa), ro2 = pro + pnb - 1;
-        if (s == K) {
-          my_a = a2;
-          my_nb = nb2;
-          my_d = d2;
-          my_ro = ro2;
+      int my_a = 0, my_nb = 0, my_d = -1, my_ro = 0, T, K, ro_next;
+      if constexpr (TEAM == 64) {
+        // the whole wave is the team: lane s takes step t + s; the group ends
+        // at the first step not nested in its predecessor.  Lags telescope,
+        // d_s = 2 s + a_s - a_0, rotation offsets are a prefix sum of nb - 1.
+        const int tt = t + s;
+        const bool inr = tt < tn;
+        const int a_s = inr ? hsh[2 * tt] : 0, nb_s = inr ? hsh[2 * tt + 1] : 1;
+        const int a_p = __shfl_up(a_s, 1, 64), nb_p = __shfl_up(nb_s, 1, 64);
+        const bool brk = s > 0 && (!inr || a_s < a_p || a_s + nb_s > a_p + nb_p);
+        const unsigned long long bm = __ballot(brk);
+        K = bm ? (int)__builtin_ctzll(bm) : 64;
+        int inc = nb_s - 1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int u = __shfl_up(inc, off, 64);
+          if (s >= off) inc += u;
         }
-        T = max(T, d2 + nb2 - 1);
-        pa = a2;
-        pnb = nb2;
-        pd = d2;
-        pro = ro2;
-        K++;
+        const int a0 = __shfl(a_s, 0, 64);
+        const bool mine = s < K;
+        int tv = mine ? 2 * s + a_s - a0 + nb_s - 1 : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) tv = max(tv, __shfl_xor(tv, off, 64));
+        T = tv;
+        if (mine) {
+          my_a = a_s;
+          my_nb = nb_s;
+          my_d = 2 * s + a_s - a0;
+          my_ro = ro + inc - (nb_s - 1);
+        }
+        ro_next = ro + __shfl(inc, K - 1, 64);
+      } else {
+        int pa = hsh[2 * t], pnb = hsh[2 * t + 1], pd = 0, pro = ro;
+        T = pnb - 1;
+        K = 1;
+        if (s == 0) {
+          my_a = pa;
+          my_nb = pnb;
+          my_d = 0;
+          my_ro = pro;
+        }
+        while (K < APPLY_TEAM && t + K < tn) {
+          const int a2 = hsh[2 * (t + K)], nb2 = hsh[2 * (t + K) + 1];
+          if (a2 < pa || a2 + nb2 > pa + pnb) break;
+          const int d2 = pd + 2 + (a2 - pa), ro2 = pro + pnb - 1;
+          if (s == K) {
+            my_a = a2;
+            my_nb = nb2;
+            my_d = d2;
+            my_ro = ro2;
+          }
+          T = max(T, d2 + nb2 - 1);
+          pa = a2;
+          pnb = nb2;
+          pd = d2;
+          pro = ro2;
+          K++;
+        }
+        ro_next = pro + pnb - 1;
       }
       // Systolic replay: lane s's qj at time tau is exactly the entry lane
       // s-1 finalised at tau-1 ("emit": its rotation output, or its carry
@@ -2599,7 +2650,7 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
 #pragma unroll
         for (int p = 0; p < APF; p++) {
           const int tau = tau0 + p;
-          const double vin = dpp_shr1(emit);
+          const double vin = dpp_shr1<TEAM>(emit);
           const int i = tau - my_d;
           const double c = cR[p], sn = sR[p], qjl = qR[p];
           const int icn = clampi(i + APF);
@@ -2621,7 +2672,7 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
       }
       T -= 1;
       t += K;
-      ro = pro + pnb - 1;
+      ro = ro_next;
       ngroups++;
       nunits += T;
     }
@@ -2802,17 +2853,29 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(t2_lds_doubles(N) * sizeof(double))));
   if (tri == 5) {
-    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)mw2_lds_bytes(N)));
     // the workgroups hand data to each other inside the launch: they must be
-    // co-resident, which a cooperative launch guarantees (or refuses)
+    // co-resident, which a cooperative launch guarantees (or refuses).  With
+    // fewer co-resident slots than workgroups (fewer CUs visible, another
+    // kernel's LDS), each workgroup takes more rows.
     int perCU = 0, dev = 0, cus = 0;
     KG_HIP(hipGetDevice(&dev));
     KG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    KG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_tridiag_mw2, MW2_TPB,
-                                                        mw2_lds_bytes(N)));
-    KG_CHECK(perCU * cus >= mw2_groups(N), "eigensolver: the multi-workgroup tridiagonalisation's " +
-                                               std::to_string(mw2_groups(N)) + " workgroups cannot be co-resident");
+    for (int rw = (N + 255) / 256; rw <= N; rw++) {
+      g_mw2_rw[N] = rw;
+      if (!mw2_fits(N) || mw2_rows(N) != rw) break;  // LDS exhausted (or rows forced by the environment)
+      KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)mw2_lds_bytes(N)));
+      KG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_tridiag_mw2, MW2_TPB,
+                                                          mw2_lds_bytes(N)));
+      if (getenv("KORALI_AMD_DEBUG_OCC"))
+        fprintf(stderr, "[korali_amd] mw2 N=%d rows=%d groups=%d lds=%zu perCU=%d cus=%d\n", N, rw, mw2_groups(N),
+                mw2_lds_bytes(N), perCU, cus);
+      if (perCU * cus >= mw2_groups(N)) break;
+    }
+    KG_CHECK(mw2_fits(N) && perCU * cus >= mw2_groups(N),
+             "eigensolver: the multi-workgroup tridiagonalisation's " + std::to_string(mw2_groups(N)) +
+                 " workgroups cannot be co-resident (" + std::to_string(cus) + " CUs x " + std::to_string(perCU) +
+                 " per CU)");
   }
   if (!lds || tri == 2 || tri == 5) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
@@ -2828,10 +2891,14 @@ int EigenSolver::init(int N_, bool hostChase_) {
   const int attr = 160 * 1024;
   KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
   KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N)));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N)));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N, 4)));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N, 4)));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N, 16)));
+  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)apply_lds_bytes(N, 16)));
   return 0;
 }
 
@@ -2949,8 +3016,9 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
       unsigned long long seq_ = seq;
       void *args[] = {&N_, &gQt_, &devRec, &B_, &D_, &minEig_, &maxEig_, &eigenFailures_, &errors_, &trace_,
                       &dprogDev_, &seq_, &mr, &dprog_};
-      KG_HIP(launch_resident((const void *)k_apply<true>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS + 1),
-                             dim3(APPLY_TPB), args, apply_lds_bytes(N), s));
+      const int rows = apply_rows();
+      KG_HIP(launch_resident(rows == 4 ? (const void *)k_apply<true, 64> : (const void *)k_apply<true, 16>,
+                             dim3((N + rows - 1) / rows + 1), dim3(APPLY_TPB), args, apply_lds_bytes(N, rows), s));
     }
     if (prof) prof(profCtx, "eigen_dsd_wait", 2);
     {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)
@@ -2972,9 +3040,15 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
   } else {
     KG_HIP(hipStreamWaitEvent(s, ev_chase, 0));
     if (prof) prof(profCtx, "eigen_apply", 0);
-    hipLaunchKernelGGL(k_apply<false>, dim3((N + APPLY_ROWS - 1) / APPLY_ROWS), dim3(APPLY_TPB), apply_lds_bytes(N),
-                       s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace,
-                       (unsigned long long *)nullptr, 0ULL, devRec, (unsigned long long *)nullptr);
+    const int rows = apply_rows();
+    if (rows == 4)
+      hipLaunchKernelGGL((k_apply<false, 64>), dim3((N + rows - 1) / rows), dim3(APPLY_TPB), apply_lds_bytes(N, rows),
+                         s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace,
+                         (unsigned long long *)nullptr, 0ULL, devRec, (unsigned long long *)nullptr);
+    else
+      hipLaunchKernelGGL((k_apply<false, 16>), dim3((N + rows - 1) / rows), dim3(APPLY_TPB), apply_lds_bytes(N, rows),
+                         s, N, gQt, devRec, B, D, minEig, maxEig, eigenFailures, errors, trace,
+                         (unsigned long long *)nullptr, 0ULL, devRec, (unsigned long long *)nullptr);
     KG_HIP(hipGetLastError());
   }
   if (prof) prof(profCtx, "eigen_apply", 1);

@@ -320,8 +320,11 @@ __host__ __device__ inline size_t mw2_lds_doubles(int N, int RW) {
   // M | Pd | Pa | prow (+16) | nrow | vloc | tv | xl | sv (+64) | scal, accb, t2b, mskb, cmx (16 each)
   return (size_t)RW * (N + 1) + 2 * (size_t)RW * mw2_ps(N) + (N + 16) + 4 * (size_t)N + (N + 64) + 5 * 16;
 }
+// rows per workgroup chosen at init for the device's co-resident capacity, by N
+// (0: the default); every handle of one N on this device arrives at the same value
+static int g_mw2_rw[1025];
 int mw2_rows(int N) {
-  int rw = (N + 255) / 256;
+  int rw = (N <= 1024 && g_mw2_rw[N] > 0) ? g_mw2_rw[N] : (N + 255) / 256;
   if (const char *e = getenv("KORALI_AMD_TMW_ROWS")) rw = atoi(e);
   if (rw < 1) rw = 1;
   while (rw > 1 && mw2_lds_doubles(N, rw) * sizeof(double) > 150 * 1024) rw--;

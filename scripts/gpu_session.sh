@@ -35,6 +35,12 @@ for s in ${STEPS:-smoke tests bench prof}; do
     shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
     cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
     benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
+    occt) step occ_torch 120 python tools/occ_probe.py exact torch ;;
+    occ) step occ_exact 120 python tools/occ_probe.py exact && step occ_mfma 120 python tools/occ_probe.py mfma ;;
+    benchab) step bench_old 300 env KORALI_AMD_ADAPTC2=1 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_new 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
+    profq) step profq 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    c4t) step c4t 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests/test_gpu_baseline_shapes.py -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
+    benchteam) step bench_t16 300 env KORALI_AMD_APPLY_TEAM=16 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_t64 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac
 done
