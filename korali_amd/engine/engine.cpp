@@ -1349,6 +1349,86 @@ const KeyList RL_KEYS = {"Type", "Environment Function", "Environment Kernel", "
                          "Testing Frequency", "Policy Testing Episodes", "Custom Settings", "Max Episode Steps",
                          "State Vector Size", "Action Vector Size", "State Vector Indexes", "Action Vector Indexes"};
 
+}  // namespace
+
+Json vracerPolicyDescription(Json &js) {
+  Json &sv = js["Solver"];
+  const std::string dist = canon(str(sv["Policy"], "Distribution", "Normal"));
+  const bool normalFamily = dist == "normal" || dist == "squashednormal" || dist == "clippednormal" ||
+                            dist == "truncatednormal";
+  const bool bounded = dist == "squashednormal" || dist == "beta" || dist == "clippednormal" || dist == "truncatednormal";
+  if (!normalFamily && dist != "beta") fail("Unknown policy distribution '%s'.", sv["Policy"]["Distribution"].getString().c_str());
+  std::vector<unsigned long long> sIdx, aIdx;
+  std::vector<float> noise, lbs, ubs;
+  for (size_t i = 0; i < js["Variables"].size(); i++) {
+    Json &v = js["Variables"][i];
+    const std::string t = canon(str(v, "Type", "State"));
+    if (t == "state") sIdx.push_back(i);
+    else if (t == "action") {
+      aIdx.push_back(i);
+      noise.push_back((float)num(v, "Initial Exploration Noise", -1.0));
+      lbs.push_back((float)num(v, "Lower Bound", -INFINITY));
+      ubs.push_back((float)num(v, "Upper Bound", INFINITY));
+    }
+  }
+  const size_t A = aIdx.size();
+  std::vector<float> shifts(A, 0.0f), scales(A, 0.0f), scaling(2 * A), shifting(2 * A);
+  std::vector<std::string> masks(2 * A);
+  for (size_t i = 0; i < A; i++) {
+    if (bounded) {
+      if (!std::isfinite(lbs[i]) || !std::isfinite(ubs[i]))
+        fail("Provided bounds (%f, %f) for action variable %zu are non-finite, but the distribution (%s) is bounded.\n",
+             lbs[i], ubs[i], i, sv["Policy"]["Distribution"].getString().c_str());
+      shifts[i] = (ubs[i] + lbs[i]) * 0.5f;
+      scales[i] = (ubs[i] - lbs[i]) * 0.5f;
+    }
+    if (noise[i] <= 0.0f)
+      fail("Provided initial noise (%f) for action variable %llu is not defined or negative.\n", noise[i], aIdx[i]);
+    scaling[i] = 1.0f, shifting[i] = shifts[i], masks[i] = "Identity";
+    scaling[A + i] = 2.0f * noise[i], shifting[A + i] = 0.0f, masks[A + i] = normalFamily ? "Softplus" : "Sigmoid";
+  }
+  Json out;
+  out["Problem"]["State Vector Size"] = (unsigned long long)sIdx.size();
+  out["Problem"]["Action Vector Size"] = (unsigned long long)A;
+  out["Problem"]["State Vector Indexes"] = sIdx;
+  out["Problem"]["Action Vector Indexes"] = aIdx;
+  out["Solver"]["Action Shifts"] = shifts;
+  out["Solver"]["Action Scales"] = scales;
+  out["Solver"]["Policy"]["Parameter Count"] = (unsigned long long)(2 * A);
+  out["Solver"]["Policy"]["Parameter Scaling"] = scaling;
+  out["Solver"]["Policy"]["Parameter Shifting"] = shifting;
+  out["Solver"]["Policy"]["Parameter Transformation Masks"] = masks;
+  // network: state -> [Linear (H), Tanh] x L -> Linear (value + policy parameters)
+  std::vector<unsigned long long> sizes{(unsigned long long)sIdx.size()};
+  Json &hl = sv["Neural Network"]["Hidden Layers"];
+  for (size_t l = 0; 2 * l < hl.size(); l++) sizes.push_back(uint(hl[2 * l], "Output Channels", 0));
+  sizes.push_back(1 + 2 * A);
+  unsigned long long count = 0;
+  for (size_t l = 0; l + 1 < sizes.size(); l++) count += sizes[l] * sizes[l + 1] + sizes[l + 1];
+  out["Layer Sizes"] = sizes;
+  out["Hyperparameter Count"] = count;
+  return out;
+}
+
+std::vector<float> vracerInitialHyperparameters(const std::vector<size_t> &sizes, unsigned seed) {
+  size_t n = 0;
+  for (size_t l = 0; l + 1 < sizes.size(); l++) n += sizes[l] * sizes[l + 1] + sizes[l + 1];
+  std::vector<float> theta(n);
+  std::mt19937 mt(seed);
+  std::uniform_real_distribution<float> U(-1.0f, 1.0f);
+  size_t k = 0;
+  for (size_t l = 0; l + 1 < sizes.size(); l++) {
+    const size_t ic = sizes[l], oc = sizes[l + 1];
+    const float scale = l + 2 == sizes.size() ? 0.001f : 1.0f;
+    const float xav = std::sqrt(6.0f) / std::sqrt((float)(oc + ic));
+    for (size_t i = 0; i < ic * oc; i++) theta[k++] = scale * xav * U(mt);
+    for (size_t i = 0; i < oc; i++) theta[k++] = 0.0f;
+  }
+  return theta;
+}
+
+namespace {
+
 struct VracerModule : SolverModule {
   kg_vracer_t h = nullptr;
   double maxGenerations = 1e10;
@@ -1358,6 +1438,7 @@ struct VracerModule : SolverModule {
   std::vector<float> rewardHistory;
   float lastReward = 0.f, bestReward = -INFINITY, averageReward = 0.f;
   Json *solverJs = nullptr;
+  Json description;  // vracerPolicyDescription: written into every result file
 
   ~VracerModule() override {
     if (h) kg_vracer_destroy(h);
@@ -1484,20 +1565,12 @@ struct VracerModule : SolverModule {
     // experiment's seed counter), not GSL's: initial weights are not pinned.
     size_t n = 0;
     check(kg_vracer_hyperparameter_count(h, &n));
-    std::vector<float> theta(n);
-    std::mt19937 mt((unsigned)seeds.counter++);
-    std::uniform_real_distribution<float> U(-1.0f, 1.0f);
     std::vector<size_t> sizes{4};
     for (size_t l = 0; l < L; l++) sizes.push_back(H);
     sizes.push_back(3);
-    size_t k = 0;
-    for (size_t l = 0; l + 1 < sizes.size(); l++) {
-      const size_t ic = sizes[l], oc = sizes[l + 1];
-      const float scale = l + 2 == sizes.size() ? 0.001f : 1.0f;
-      const float xav = std::sqrt(6.0f) / std::sqrt((float)(oc + ic));
-      for (size_t i = 0; i < ic * oc; i++) theta[k++] = scale * xav * U(mt);
-      for (size_t i = 0; i < oc; i++) theta[k++] = 0.0f;
-    }
+    std::vector<float> theta = vracerInitialHyperparameters(sizes, (unsigned)seeds.counter++);
+    if (theta.size() != n) fail("VRACER: hyperparameter count mismatch (%zu vs the device's %zu).", theta.size(), n);
+    description = vracerPolicyDescription(js);
     if (sv["Training"].contains("Current Policy") && sv["Training"]["Current Policy"].contains("Policy") &&
         sv["Training"]["Current Policy"]["Policy"].size() == n) {
       auto v = flatten(sv["Training"]["Current Policy"]["Policy"]);
@@ -1563,6 +1636,11 @@ struct VracerModule : SolverModule {
     std::vector<float> theta(n);
     check(kg_vracer_get_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
     sv["Training"]["Current Policy"]["Policy"] = std::vector<double>(theta.begin(), theta.end());
+    Json &ds = description["Solver"];
+    sv["Action Shifts"] = ds["Action Shifts"];
+    sv["Action Scales"] = ds["Action Scales"];
+    for (const char *k : {"Parameter Count", "Parameter Scaling", "Parameter Shifting", "Parameter Transformation Masks"})
+      sv["Policy"][k] = ds["Policy"][k];
   }
 
   void finalize(Json &) override {}

@@ -167,4 +167,17 @@ std::vector<double> referenceFisherInformation(const std::string &model, const s
 // problems); returns the sample's JSON (logPrior, logLikelihood, F(x), ...)
 Json bayesianEvaluate(Json &experiment, const std::vector<double> &x);
 
+// The continuous agent's policy description from an experiment's Variables
+// and Solver (continuous.cpp.base:9-60 initializeAgent; agent.cpp.base:37-90):
+// Problem vector sizes / indexes, Action Shifts / Scales, Policy/Parameter
+// Count / Scaling / Shifting / Transformation Masks, the network's layer
+// widths (state, hidden..., 1 + parameter count) and its hyperparameter
+// count.  Written into VRACER result files; pinned by the reference's
+// tests/python/rlview/abf2d_vracer* files.
+Json vracerPolicyDescription(Json &experiment);
+// Initial hyperparameters ([W (out x in), b] per layer, linear.cpp.base:28-49):
+// Xavier-scaled U(-1, 1) weights (the output layer x 0.001,
+// VRACER.cpp.base:38), zero biases; std::mt19937(seed) uniforms.
+std::vector<float> vracerInitialHyperparameters(const std::vector<size_t> &sizes, unsigned seed);
+
 }  // namespace korali

@@ -251,6 +251,13 @@ PYBIND11_MODULE(libkorali, m) {
     return d;
   });
 
+  // test hooks: the continuous agent's policy description and initial
+  // hyperparameters (pinned against the reference's VRACER result files)
+  m.def("_vracer_policy_description", [](korali::Experiment &e) { return toPy(korali::vracerPolicyDescription(e._js)); });
+  m.def("_vracer_initial_hyperparameters", [](const std::vector<size_t> &sizes, unsigned seed) {
+    return korali::vracerInitialHyperparameters(sizes, seed);
+  });
+
   // test hook: the conduit's batch dispatch with a Python body
   m.def("_conduit_evaluate", [](size_t jobs, size_t n, py::function body) {
     py::gil_scoped_release nogil;

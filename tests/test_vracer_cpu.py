@@ -6,6 +6,7 @@ dopri5): resets and trajectories bit-exact.  The agent's pieces are pinned
 against independent definitions: Random123's philox known answers, numpy's
 own RandomState for the resets, finite differences for the backward pass,
 and the reference's formulas checked term by term."""
+import json
 import os
 import sys
 
@@ -202,3 +203,45 @@ def test_clipped_normal_log_cdf_tails():
     for x in (-40.0, -8.0, 0.0, 8.0, 40.0):
         assert np.isclose(V.normal_logcdf(f32(x), f32(0), f32(1)), norm.logcdf(x), rtol=1e-6, atol=1e-6)
         assert np.isclose(V.normal_logccdf(f32(x), f32(0), f32(1)), norm.logsf(x), rtol=1e-6, atol=1e-6)
+
+
+def test_policy_description_matches_reference_result_files():
+    """The continuous agent's policy description (continuous.cpp.base:9-60)
+    and the network's hyperparameter layout against the reference's own
+    VRACER result files (tests/python/rlview/abf2d_vracer{1,2}, 4 states,
+    3 actions, 2 x 64 tanh; facts extracted by tests/golden/make_vracer_golden.py)."""
+    import korali
+    from korali_amd import libkorali
+    runs = json.load(open(os.path.join(ROOT, "tests", "golden", "vracer_abf2d.json")))
+    for run, r in runs.items():
+        e = korali.Experiment()
+        for i, v in enumerate(r["variables"]):
+            for k, val in v.items():
+                e["Variables"][i][k] = val
+        e["Solver"]["Policy"]["Distribution"] = r["solver"]["Policy"]["Distribution"]
+        e["Solver"]["Neural Network"]["Hidden Layers"] = r["solver"]["Neural Network"]["Hidden Layers"]
+        d = libkorali._vracer_policy_description(e)
+        ex = r["expected"]
+        for k, v in ex["Policy"].items():
+            assert d["Solver"]["Policy"][k] == v, (run, k)
+        assert d["Solver"]["Action Shifts"] == ex["Action Shifts"] and d["Solver"]["Action Scales"] == ex["Action Scales"]
+        for k, v in r["problem"].items():
+            assert d["Problem"][k] == v, (run, k)
+        hp = r["hyperparameters"]
+        assert d["Hyperparameter Count"] == hp["count"] == hp["covered"] == 4935
+        assert d["Layer Sizes"] == hp["layer_sizes"]
+        # initial hyperparameters: [W (out x in), b] per layer, zero biases,
+        # Xavier-bounded weights, the output layer scaled by 0.001 -- the
+        # pattern of the reference's generation-0 vector
+        theta = np.array(libkorali._vracer_initial_hyperparameters(hp["layer_sizes"], 7))
+        assert theta.size == hp["count"]
+        k = 0
+        for L, (ic, oc) in zip(hp["layers"], zip(hp["layer_sizes"][:-1], hp["layer_sizes"][1:])):
+            W, b = theta[k:k + ic * oc], theta[k + ic * oc:k + ic * oc + oc]
+            k += ic * oc + oc
+            bound = np.sqrt(6.0) / np.sqrt(ic + oc) * (0.001 if oc == hp["layer_sizes"][-1] else 1.0)
+            assert L["bias_all_zero"] and np.all(b == 0.0)
+            assert L["weights_nonzero"] == ic * oc and np.all(W != 0.0)
+            # both vectors fill the same Xavier interval (largest |w| within 5% of the bound)
+            assert 0.95 * bound < L["weight_max_abs"] <= bound * (1 + 1e-6)
+            assert 0.95 * bound < np.abs(W).max() <= bound * (1 + 1e-6)
