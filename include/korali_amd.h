@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 3
+#define KG_ABI_VERSION 4
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -93,6 +93,11 @@ typedef struct {
    * kg_cmaes_set_gradients (host-evaluated objectives only, unsharded) */
   int use_gradients;
   double gradient_step_size;
+  /* "Granularity" of each variable (N, may be NULL → all 0 = continuous;
+   * CMAES.cpp.base:44-50, :515-544, :834-867): samples are rounded to it,
+   * discrete mutations drawn from the Uniform Generator, sigma follows the
+   * masked path length.  Not with Mirrored Sampling or sharding. */
+  const double *granularity;
 } kg_cmaes_cfg;
 
 int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);

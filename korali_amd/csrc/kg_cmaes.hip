@@ -35,6 +35,8 @@ struct CmaesScalars {
   double ccov1, ccovmu;
   unsigned int errors, bestFlag;  // bestFlag: best-ever improved this generation
   unsigned int rmuOutOfRange;     // k_rankmu_prep: some rank-mu factor outside the Markstein range
+  // discrete variables (CMAES.cpp.base:34, :106-107, :834-859)
+  double nME, nDM, chiDM;  // Number Masking Matrix Entries, Number Of Discrete Mutations, Chi Square Number DM
 };
 
 // ----------------------------------------------------------------- init
@@ -88,6 +90,9 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
     sc->previousBestValue = sc->bestEverValue;
     sc->currentBestValue = sc->bestEverValue;
     sc->chiSquareNumber = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));
+    sc->chiDM = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));  // :34
+    sc->nME = 0.0;
+    sc->nDM = 0.0;
     sc->bestValidSample = 0;
     const double effMu = s1s2[0] * s1s2[0] / s1s2[1];
     sc->effectiveMu = effMu;
@@ -390,7 +395,8 @@ __global__ void k_gather_rows(int N, int lam, const int *__restrict__ assign, co
 // reference's order) then run on one wave.
 constexpr int OB_C = 64, OB_D = 32;
 __global__ void __launch_bounds__(256) k_objective(int N, int lam, int obj, const double *__restrict__ X,
-                                                   double *__restrict__ F, CmaesScalars *sc) {
+                                                   double *__restrict__ F, CmaesScalars *sc, double addEvals) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->modelEvaluationCount += addEvals;  // (was k_add_evals)
   __shared__ double tile[OB_C][OB_D + 1];
   __shared__ double ctile[OB_C][OB_D + 1];
   const int tid = threadIdx.x;
@@ -435,6 +441,106 @@ __global__ void __launch_bounds__(256) k_objective(int N, int lam, int obj, cons
     __syncthreads();
   }
   if (tid >= OB_C || i >= lam) return;
+  double f;
+  if (obj == KG_OBJ_NEGATIVE_ROSENBROCK)
+    f = -r0;
+  else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
+    const double s1 = r0 / (double)N, s2 = r1 / (double)N;
+    const double e1 = 20. * exp_cr(-0.2 * sqrt(s1));
+    const double e2 = exp_cr(s2);
+    f = e1 + e2 - 20. - 2.718281828459045;
+  } else
+    f = -0.5 * r0;
+  F[i] = f;
+  if (!isfinite(f)) atomicOr(&sc->errors, KG_ERR_NONFINITE_F);
+}
+
+// The same objectives for N <= 128 with each row's ordered sum split from
+// its terms: the 64 rows' X block is loaded with every load in flight at
+// once; waves 1-3 form the terms of 32-column chunks (Rosenbrock's
+// 100 (x_d - x_{d-1}^2)^2 + (1 - x_{d-1})^2, Ackley's x^2 and cos 2 pi x,
+// the sphere's x^2) into LDS while wave 0 adds the previous chunk's terms
+// in order, one add per term (k_objective's single wave formed and added
+// every term itself, issue-bound at ~8 instructions per term).
+constexpr int OB2_R = 64, OB2_NC = 32;  // rows per workgroup; columns per chunk
+__host__ __device__ inline size_t ob2_lds_bytes(int N) {
+  return ((size_t)OB2_R * (N + 1) + 2 * 2 * (size_t)OB2_R * (OB2_NC + 1)) * sizeof(double);
+}
+__global__ void __launch_bounds__(256) k_objective2(int N, int lam, int obj, const double *__restrict__ X,
+                                                    double *__restrict__ F, CmaesScalars *sc, double addEvals) {
+  extern __shared__ __attribute__((aligned(16))) double ob2[];
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->modelEvaluationCount += addEvals;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ld = N + 1, c0 = blockIdx.x * OB2_R;
+  double *Xs = ob2;                                   // [row][d], row stride N + 1
+  double *Ta = Xs + (size_t)OB2_R * ld;               // [2][row][OB2_NC + 1] first terms
+  double *Tb = Ta + 2 * (size_t)OB2_R * (OB2_NC + 1);  // [2][row][OB2_NC + 1] Ackley's cos terms
+  const int tot = OB2_R * N;
+  for (int q0 = tid; q0 < tot; q0 += 32 * 256) {  // N <= 128: one pass, 32 loads in flight per thread
+    double v[32];
+#pragma unroll
+    for (int u = 0; u < 32; u++) {
+      const int q = q0 + u * 256, r = q / N, d = q - r * N;
+      v[u] = (q < tot && c0 + r < lam) ? X[(size_t)(c0 + r) * N + d] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 32; u++) {
+      const int q = q0 + u * 256, r = q / N, d = q - r * N;
+      if (q < tot) Xs[(size_t)r * ld + d] = v[u];
+    }
+  }
+  __syncthreads();
+  const int nch = (N + OB2_NC - 1) / OB2_NC;
+  const double cc = 2. * 3.141592653589793;
+  // producers: terms of chunk ch into buffer ch & 1 (row = lane, columns over waves 1-3)
+  auto form = [&](int ch) {
+    const int b = ch & 1, d0 = ch * OB2_NC, dn = min(OB2_NC, N - d0);
+    double *ta = Ta + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
+    double *tb = Tb + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
+    const double *xr = Xs + (size_t)lane * ld;
+    for (int dd = wid - 1; dd < dn; dd += 3) {
+      const int d = d0 + dd;
+      const double x = xr[d];
+      if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
+        if (d > 0) {
+          const double prev = xr[d - 1];
+          const double tt = x - prev * prev;
+          const double u = 1 - prev;
+          ta[dd] = 100 * (tt * tt) + u * u;
+        }
+      } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
+        ta[dd] = x * x;
+        tb[dd] = cos_cr(cc * x);
+      } else {
+        ta[dd] = x * x;
+      }
+    }
+  };
+  if (wid > 0) form(0);
+  __syncthreads();
+  double r0 = 0.0, r1 = 0.0;
+  for (int ch = 0; ch < nch; ch++) {
+    if (wid == 0) {
+      const int b = ch & 1, d0 = ch * OB2_NC, dn = min(OB2_NC, N - d0);
+      const double *ta = Ta + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
+      const double *tb = Tb + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
+      if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
+        for (int dd = (d0 == 0 ? 1 : 0); dd < dn; dd++) r0 += ta[dd];
+      } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
+        for (int dd = 0; dd < dn; dd++) {
+          r0 += ta[dd];
+          r1 += tb[dd];
+        }
+      } else {
+        for (int dd = 0; dd < dn; dd++) r0 += ta[dd];
+      }
+    } else if (ch + 1 < nch) {
+      form(ch + 1);
+    }
+    __syncthreads();
+  }
+  const int i = c0 + lane;
+  if (wid != 0 || i >= lam) return;
   double f;
   if (obj == KG_OBJ_NEGATIVE_ROSENBROCK)
     f = -r0;
@@ -565,7 +671,14 @@ constexpr int RANK_MAX = 16384;
 __global__ void __launch_bounds__(256) k_rank_sort(int lam, const double *__restrict__ F, unsigned *__restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double rk[];
   __shared__ unsigned part[16][17];
-  for (int q = threadIdx.x; q < lam; q += blockDim.x) rk[q] = F[q];
+  for (int q0 = threadIdx.x; q0 < lam; q0 += 8 * blockDim.x) {  // eight loads in flight per thread
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = (q0 + u * (int)blockDim.x < lam) ? F[q0 + u * blockDim.x] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q0 + u * (int)blockDim.x < lam) rk[q0 + u * blockDim.x] = v[u];
+  }
   __syncthreads();
   const int li = threadIdx.x & 15, p = threadIdx.x >> 4;
   const int i = blockIdx.x * 16 + li;
@@ -583,6 +696,134 @@ __global__ void __launch_bounds__(256) k_rank_sort(int lam, const double *__rest
     for (int q = 0; q < 16; q++) r += part[q][threadIdx.x];
     out[r] = (unsigned)i;
   }
+}
+
+// ------------------------------------------------ discrete variables
+// prepareGeneration's sampling loop with Granularity (CMAES.cpp.base:443-458,
+// sampleSingle :515-544, discretize :861-867) over the transformed rows
+// Xall (every normal row of the stream, in order): sample i takes rows until
+// one is feasible after its discrete mutation and rounding, exactly as the
+// reference redraws; the mutation's uniforms come from U (the Uniform
+// Generator's next words, peeked) in the reference's order, *uUsed of them
+// consumed.  One workgroup, one sample at a time (the uniform walk is
+// sequential); the rounded point is rounded once more as the evaluation does
+// (:208).  Discrete problems are small (the reference example: N = 10,
+// lambda = 8), so the O(lambda) barriers are not on a hot path.
+__device__ __forceinline__ double discretize1(double x, double g) { return g != 0.0 ? round(x / g) * g : x; }
+__global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blocks, int mirrored, double maxRes,
+                                                         const double *__restrict__ Xall,
+                                                         const double *__restrict__ BDZall, double *__restrict__ X,
+                                                         double *__restrict__ BDZ, const double *__restrict__ lb,
+                                                         const double *__restrict__ ub,
+                                                         const double *__restrict__ gran,
+                                                         const double *__restrict__ mask,
+                                                         const double *__restrict__ best, const double *__restrict__ U,
+                                                         unsigned long long ucap, unsigned long long *uUsed,
+                                                         unsigned long long *used, CmaesScalars *sc) {
+  extern __shared__ double xs[];  // 2 N: the unit's samples (one, or a mirrored pair)
+  __shared__ int infeas[2];
+  const int tid = threadIdx.x, per = mirrored ? 2 : 1;
+  const double nDM = sc->nDM, nME = sc->nME;
+  double count = sc->infeasibleSampleCount;
+  int j = 0;
+  unsigned long long u = 0;
+  auto uni = [&]() {  // next uniform (thread 0)
+    const double v = u < ucap ? U[u] : 0.0;
+    u++;
+    return v;
+  };
+  for (int i0 = 0; i0 < lam; i0 += per) {
+    for (;;) {
+      const bool out = j >= blocks;
+      const int blk = out ? blocks - 1 : j;
+      for (int q = tid; q < per * N; q += blockDim.x) xs[q] = Xall[((size_t)blk * per) * N + q];
+      if (tid < 2) infeas[tid] = 0;
+      __syncthreads();
+      if (tid == 0)
+        for (int s = 0; s < per; s++) {  // sampleSingle(i0 + s) in order (:472-473)
+          const int i = i0 + s;
+          double *x = xs + (size_t)s * N;
+          if ((double)(i + 1) < nDM) {
+            const double p_geom = pow_cr(0.7, 1.0 / nME);
+            size_t select = (size_t)floor(uni() * nME);
+            for (int d = 0; d < N; ++d)
+              if ((mask[d] == 1.0) && (select-- == 0)) {
+                double dm = 1.0;
+                while (uni() > p_geom) dm += 1.0;
+                dm *= gran[d];
+                if (uni() > 0.5) dm *= -1.0;
+                x[d] += dm;
+              }
+          } else if ((double)(i + 1) == nDM) {
+            for (int d = 0; d < N; ++d)
+              if (gran[d] != 0.0) x[d] += round(best[d] / gran[d]) * gran[d] - x[d];
+          }
+        }
+      __syncthreads();
+      for (int q = tid; q < per * N; q += blockDim.x) {
+        const int d = q % N;
+        const double x = discretize1(xs[q], gran[d]);
+        xs[q] = x;
+        if (!isfinite(x) || x < lb[d] || x > ub[d]) infeas[q / N] = 1;  // (benign race: every writer stores 1)
+      }
+      __syncthreads();
+      bool accept;
+      if (out) {
+        if (tid == 0) sc->errors |= KG_ERR_RESAMPLE_RESERVE;
+        accept = true;
+      } else {
+        bool anyOk = false;
+        for (int s = 0; s < per; s++) {
+          if (infeas[s]) count += 1;
+          else anyOk = true;
+        }
+        j++;
+        accept = anyOk || !(count < maxRes);
+      }
+      if (accept) {
+        for (int q = tid; q < per * N; q += blockDim.x) {
+          const int d = q % N;
+          X[(size_t)i0 * N + q] = discretize1(xs[q], gran[d]);  // :208 before evaluation
+          if (BDZ) BDZ[(size_t)i0 * N + q] = BDZall[((size_t)blk * per) * N + q];
+        }
+        __syncthreads();
+        break;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    sc->infeasibleSampleCount = count;
+    *used = (unsigned long long)j;
+    if (u > ucap) sc->errors |= KG_ERR_RNG_UNDERRUN;
+    *uUsed = u < ucap ? u : ucap;
+  }
+}
+
+// updateDiscreteMutationMatrix (:834-859), after adaptC with the old sigma
+__global__ void k_discrete_masks(int N, int lam, const double *__restrict__ gran, const double *__restrict__ C,
+                                 double *mask, double *maskSigma, CmaesScalars *sc) {
+  if (threadIdx.x != 0) return;
+  const double sigma = sc->sigma, cs = sc->sigmaCumulationFactor;
+  double entries = (double)(N + 1);
+  for (int d = 0; d < N; ++d) maskSigma[d] = 1.0;
+  for (int d = 0; d < N; ++d)
+    if (sigma * sqrt(C[(size_t)d * N + d]) / sqrt(cs) < 0.2 * gran[d]) {
+      maskSigma[d] = 0.0;
+      entries -= 1.0;
+    }
+  sc->chiDM = sqrt(entries) * (1. - 1. / (4. * entries) + 1. / (21. * entries * entries));
+  double nme = 0.0;
+  for (int d = 0; d < N; ++d) {
+    mask[d] = 0.0;
+    if (2.0 * sigma * sqrt(C[(size_t)d * N + d]) < gran[d]) {
+      mask[d] = 1.0;
+      nme += 1.0;
+    }
+  }
+  sc->nME = nme;
+  const double a = round((double)lam / 10.0 + nme + 1), b = floor((double)lam / 2.0) - 1;
+  sc->nDM = a < b ? a : b;
 }
 
 __global__ void k_copy_idx(int lam, const unsigned *__restrict__ val, unsigned *__restrict__ out) {
@@ -1058,11 +1299,24 @@ __global__ void __launch_bounds__(256) k_mean2(int N, int mu, const double *__re
   const int d0 = blockIdx.x * MN_D;
   const int nd = (N - d0) < MN_D ? (N - d0) : MN_D;
   const int nchunks = (mu + MN2_R - 1) / MN2_R;
+  // eight products' loads in flight per thread (one at a time, each round
+  // trip to L2/HBM would be exposed: the staging, not the chain, was the bound)
   auto stage = [&](int chunk, int t0, int nt) {
     double *b = pbuf + (size_t)(chunk & 1) * MN_D * MN2_RS;
-    for (int e = t0; e < MN_D * MN2_R; e += nt) {
-      const int r = e >> 3, c = e & 7, i = chunk * MN2_R + r;
-      b[(size_t)c * MN2_RS + r] = (i < mu && c < nd) ? w[i] * Y[(size_t)i * N + d0 + c] : 0.0;
+    for (int e0 = t0; e0 < MN_D * MN2_R; e0 += 8 * nt) {
+      double wv[8], yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int e = e0 + u * nt, r = e >> 3, c = e & 7, i = chunk * MN2_R + r;
+        const bool ok = e < MN_D * MN2_R && i < mu && c < nd;
+        wv[u] = ok ? w[i] : 0.0;
+        yv[u] = ok ? Y[(size_t)i * N + d0 + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int e = e0 + u * nt, r = e >> 3, c = e & 7;
+        if (e < MN_D * MN2_R) b[(size_t)c * MN2_RS + r] = wv[u] * yv[u];
+      }
     }
   };
   stage(0, tid, 256);
@@ -1103,9 +1357,19 @@ __global__ void __launch_bounds__(256) k_paths2(int N, unsigned long long gen, c
   double *pn = aux + N + 32;                       // p_sigma squares, zero past N
   __shared__ int hs;
   const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
-  for (int q = tid; q < (N + 16) * PA2_LD; q += 256) {
-    const int e = q / PA2_LD, d = q - e * PA2_LD;
-    Bs[q] = (e < N && d < N) ? B[(size_t)e * N + d] : 0.0;
+  // eight loads in flight per thread (one at a time, the L2 round trips were the kernel's time)
+  for (int q0 = tid; q0 < (N + 16) * PA2_LD; q0 += 8 * 256) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = q0 + u * 256, e = q / PA2_LD, d = q - e * PA2_LD;
+      v[u] = (q < (N + 16) * PA2_LD && e < N && d < N) ? B[(size_t)e * N + d] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = q0 + u * 256;
+      if (q < (N + 16) * PA2_LD) Bs[q] = v[u];
+    }
   }
   for (int q = tid; q < 3 * (N + 32); q += 256) sv[q] = (q < N) ? meanUpdate[q] : 0.0;
   __syncthreads();
@@ -1538,9 +1802,38 @@ __global__ void __launch_bounds__(256) k_shard_finalize(int N, const double *__r
 // :763-772, min/max standard deviation :679-687.  (The reference's max/min
 // diagonal scan uses "else if"; a new maximum can never be a new minimum, so
 // plain extrema are identical.)
+}  // namespace kg
+// what Experiment::run's termination check reads after every generation
+// (engine.cpp CmaesModule::checkTermination), in one host-coherent record
+struct TermSummary {
+  double f[KG_TERMINATION_FIELDS];
+  unsigned int errors, pad;
+  unsigned long long seq;  // written last (system-scope release)
+};
+namespace kg {
+
+// (the same publication protocol as kg_eigen.hip k_publish_dsd: relaxed
+// system-scope stores of the payload, release fence, release store of seq)
+__device__ void summary_store(const CmaesScalars *sc, const StreamState *a, const StreamState *b, TermSummary *out,
+                              unsigned long long seq) {
+  const double f[KG_TERMINATION_FIELDS] = {sc->modelEvaluationCount, sc->infeasibleSampleCount, sc->maxEig,
+                                           sc->minEig, sc->currentMinStd, sc->currentMaxStd, sc->bestEverValue,
+                                           sc->currentBestValue, sc->previousBestValue};
+  for (int i = 0; i < KG_TERMINATION_FIELDS; i++)
+    __hip_atomic_store((unsigned long long *)&out->f[i], (unsigned long long)__double_as_longlong(f[i]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&out->errors, sc->errors | a->errors | b->errors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __atomic_thread_fence(__ATOMIC_RELEASE);
+  __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// updateSigma (+ the termination record: one launch fewer per generation)
 __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded, const double *__restrict__ C,
                                                const double *__restrict__ F, const unsigned *__restrict__ idx,
-                                               const double *__restrict__ minStdUpdate, CmaesScalars *sc) {
+                                               const double *__restrict__ minStdUpdate, CmaesScalars *sc,
+                                               const StreamState *stA, const StreamState *stB, TermSummary *out,
+                                               unsigned long long seq, const double *__restrict__ maskSigma,
+                                               const double *__restrict__ ps) {
   __shared__ double ssig;
   __shared__ int viol;
   __shared__ double red[4][4];
@@ -1548,7 +1841,12 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
   if (tid == 0) {
     const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
     double sigma = sc->sigma;
-    sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
+    if (maskSigma) {  // discrete variables (:729-735)
+      double pathL2 = 0.0;
+      for (int d = 0; d < N; ++d) pathL2 += maskSigma[d] * ps[d] * ps[d];
+      sigma *= exp_cr(cs / ds * (sqrt(pathL2) / sc->chiDM - 1.));
+    } else
+      sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
     if (mu > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
     const double ub = sqrt(sc->trace / N);
     if (sigma > ub && isSigmaBounded) sigma = ub;
@@ -1604,6 +1902,7 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
     sc->sigma = sigma;
     sc->currentMinStd = mns;
     sc->currentMaxStd = mxs;
+    summary_store(sc, stA, stB, out, seq);
   }
 }
 
@@ -1616,28 +1915,6 @@ __global__ void k_add_evals(CmaesScalars *sc, double n) {
 // ===================================================================== ABI
 using namespace kg;
 
-// what Experiment::run's termination check reads after every generation
-// (engine.cpp CmaesModule::checkTermination), in one host-coherent record
-struct TermSummary {
-  double f[KG_TERMINATION_FIELDS];
-  unsigned int errors, pad;
-  unsigned long long seq;  // written last (system-scope release)
-};
-
-// (the same publication protocol as kg_eigen.hip k_publish_dsd: relaxed
-// system-scope stores of the payload, release fence, release store of seq)
-__global__ void k_summary(const CmaesScalars *sc, const StreamState *a, const StreamState *b, TermSummary *out,
-                          unsigned long long seq) {
-  const double f[KG_TERMINATION_FIELDS] = {sc->modelEvaluationCount, sc->infeasibleSampleCount, sc->maxEig,
-                                           sc->minEig, sc->currentMinStd, sc->currentMaxStd, sc->bestEverValue,
-                                           sc->currentBestValue, sc->previousBestValue};
-  for (int i = 0; i < KG_TERMINATION_FIELDS; i++)
-    __hip_atomic_store((unsigned long long *)&out->f[i], (unsigned long long)__double_as_longlong(f[i]),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&out->errors, sc->errors | a->errors | b->errors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __atomic_thread_fence(__ATOMIC_RELEASE);
-  __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 struct kg_cmaes_s {
   kg_cmaes_cfg cfg;
@@ -1662,6 +1939,12 @@ struct kg_cmaes_s {
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
   bool mirrored = false;  // "Mirrored Sampling": blocks of N normals feed two rows
   double *G = nullptr;    // samples' gradients (use_gradients)
+  // discrete variables: Granularity, Masking Matrix (Sigma), the peeked
+  // uniforms of the discrete mutations and how many were used
+  bool hasDiscrete = false;
+  double *gran = nullptr, *mask = nullptr, *maskSigma = nullptr, *ubuf = nullptr, *dzero = nullptr;
+  unsigned long long *uused = nullptr;
+  size_t ucap = 0;
   size_t blocks = 0;      // normal blocks drawn per generation (λ or λ/2, + the reserve R)
   int kslices = 8;  // rank-mu K-slices (rankmu_kslices), a multiple of the 8 XCDs
   // population shards
@@ -1801,6 +2084,9 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
   VEC("Initial Value", h->iv, N)
   VEC("Initial Standard Deviation", h->istd, N)
   VEC("Minimum Standard Deviation Update", h->minstd, N)
+  VEC("Granularity", h->gran, N)
+  VEC("Masking Matrix", h->mask, N)
+  VEC("Masking Matrix Sigma", h->maskSigma, N)
   if (h->BDZ) VEC("BDZ Matrix", h->BDZ, L * N)
   if (h->part) {
     const size_t nt = (N + 15) / 16;
@@ -1830,6 +2116,9 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Hsig", hsig)
   SCA("Eigen Failures", eigenFailures)
+  SCA("Number Masking Matrix Entries", nME)
+  SCA("Number Of Discrete Mutations", nDM)
+  SCA("Chi Square Number Discrete Mutations", chiDM)
 #undef SCA
 #undef VEC
   return false;
@@ -1889,7 +2178,24 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
       istd[i] = (ub[i] - lb[i]) * 0.3;
     }
   }
-  h->R = h->finiteBounds ? std::max(64, L / 4) : 0;
+  std::vector<double> gran(N, 0.0);
+  for (int i = 0; i < N; i++) {
+    if (cfg->granularity) gran[i] = cfg->granularity[i];
+    if (gran[i] < 0.0) {  // CMAES.cpp.base:48
+      set_error("Negative granularity for variable " + std::to_string(i) + ".");
+      delete h;
+      return 1;
+    }
+    if (gran[i] > 0.0) h->hasDiscrete = true;
+  }
+  if (h->hasDiscrete && cfg->shard_count > 1) {
+    set_error("discrete variables (Granularity) run unsharded on the device path");
+    delete h;
+    return 1;
+  }
+  // a reserve of transformed rows for resampling: finite bounds, or discrete
+  // variables (a rounded or mutated sample may leave the bounds or not)
+  h->R = (h->finiteBounds || h->hasDiscrete) ? std::max(64, L / 4) : 0;
   h->shards = cfg->shard_count > 1 ? cfg->shard_count : 1;
   h->shardRank = h->shards > 1 ? cfg->shard_rank : 0;
   if (h->shards > 1 && (L % h->shards != 0 || h->finiteBounds || cfg->shard_rank < 0 ||
@@ -1917,6 +2223,11 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
   if (cfg->use_gradients) rc |= dalloc(&h->G, (size_t)L * N);
+  rc |= dalloc(&h->gran, N) | dalloc(&h->mask, N) | dalloc(&h->maskSigma, N);
+  if (h->hasDiscrete) {
+    h->ucap = 16 * (size_t)L + 1024;  // the mutations' uniforms per generation: ~2-4 per mutated sample
+    rc |= dalloc(&h->ubuf, h->ucap) | dalloc(&h->uused, 1);
+  }
   if (h->R) {
     rc |= dalloc(&h->Xall, xrows * N);
     if (cfg->store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
@@ -1950,6 +2261,9 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     KG_HIP(hipFuncSetAttribute((const void *)k_mean2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)mean2_lds_bytes()));
     if (N <= 128)
+      KG_HIP(hipFuncSetAttribute((const void *)k_objective2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)ob2_lds_bytes(N)));
+    if (N <= 128)
       KG_HIP(hipFuncSetAttribute((const void *)k_paths2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)paths2_lds_bytes(N)));
   }
@@ -1981,8 +2295,11 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   KG_HIP(hipMemcpy(h->iv, iv.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->istd, istd.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->minstd, minstd.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->gran, gran.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  KG_HIP(hipMemset(h->mask, 0, N * sizeof(double)));
+  KG_HIP(hipMemset(h->maskSigma, 0, N * sizeof(double)));
   const size_t words = h->normal.words_for_normals(rows * N);
-  if (h->normal.init(3 * words + 4096) || h->uniform.init(1 << 16)) {
+  if (h->normal.init(3 * words + 4096) || h->uniform.init(std::max<size_t>(1 << 16, 2 * h->ucap + 4096))) {
     delete h;
     return 1;
   }
@@ -2006,7 +2323,8 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->istd, (void *)h->minstd, (void *)h->idx, (void *)h->sortKey, (void *)h->sortVal,
                   (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y, (void *)h->Yc, (void *)h->Tt,
-                  (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G})
+                  (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G,
+                  (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -2085,7 +2403,15 @@ int kg_cmaes_sample(kg_cmaes_t h) {
                        h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
                        h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
     KG_HIP(hipGetLastError());
-    if (h->R) {
+    if (h->hasDiscrete) {
+      if (h->uniform.peek_uniforms(h->ubuf, h->ucap, h->stream)) return 1;
+      hipLaunchKernelGGL(k_discrete_select, dim3(1), dim3(256), 2 * N * sizeof(double), h->stream, N, L,
+                         (int)h->blocks, h->mirrored ? 1 : 0, h->cfg.max_infeasible_resamplings, h->Xall, h->BDZall, h->X, h->BDZ, h->lb, h->ub, h->gran,
+                         h->mask, h->bestEverVars, h->ubuf, (unsigned long long)h->ucap, h->uused, h->usedBlocks,
+                         h->sc);
+      KG_HIP(hipGetLastError());
+      if (h->uniform.consume_words_dev(h->uused, h->stream)) return 1;
+    } else if (h->R) {
       if (h->mirrored)
         hipLaunchKernelGGL(k_select_mirrored, dim3(1), dim3(64), 0, h->stream, L / 2, (int)h->blocks,
                            h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->sc);
@@ -2109,9 +2435,12 @@ int kg_cmaes_eval_builtin(kg_cmaes_t h, int objective) {
   KG_CHECK(objective >= 0 && objective <= 2, "unknown builtin objective");
   Stage st(h, "objective");
   const int rows = h->r1 - h->r0;
-  hipLaunchKernelGGL(k_objective, dim3((rows + OB_C - 1) / OB_C), dim3(256), 0, h->stream, h->N, rows, objective,
-                     h->X + (size_t)h->r0 * h->N, h->F + h->r0, h->sc);
-  hipLaunchKernelGGL(k_add_evals, dim3(1), dim3(1), 0, h->stream, h->sc, (double)h->lam);
+  if (h->N <= 128)
+    hipLaunchKernelGGL(k_objective2, dim3((rows + OB2_R - 1) / OB2_R), dim3(256), ob2_lds_bytes(h->N), h->stream,
+                       h->N, rows, objective, h->X + (size_t)h->r0 * h->N, h->F + h->r0, h->sc, (double)h->lam);
+  else
+    hipLaunchKernelGGL(k_objective, dim3((rows + OB_C - 1) / OB_C), dim3(256), 0, h->stream, h->N, rows, objective,
+                       h->X + (size_t)h->r0 * h->N, h->F + h->r0, h->sc, (double)h->lam);
   KG_HIP(hipGetLastError());
   return 0;
 }
@@ -2181,19 +2510,17 @@ static int cmaes_sigma(kg_cmaes_t h) {
   const int N = h->N, mu = h->mu;
   {
     Stage st(h, "sigma");
+    if (h->hasDiscrete)
+      hipLaunchKernelGGL(k_discrete_masks, dim3(1), dim3(64), 0, h->stream, N, h->lam, h->gran, h->C, h->mask,
+                         h->maskSigma, h->sc);
     hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
-                       h->minstd, h->sc);
+                       h->minstd, h->sc, h->normal.state(), h->uniform.state(), h->summaryDev, ++h->updates,
+                       h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps);
     KG_HIP(hipGetLastError());
   }
   return 0;
 }
 
-static int cmaes_publish_summary(kg_cmaes_t h) {
-  hipLaunchKernelGGL(k_summary, dim3(1), dim3(1), 0, h->stream, h->sc, h->normal.state(), h->uniform.state(),
-                     h->summaryDev, ++h->updates);
-  KG_HIP(hipGetLastError());
-  return 0;
-}
 
 static int cmaes_paths(kg_cmaes_t h, size_t generation) {
   const int N = h->N;
@@ -2222,22 +2549,24 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                        h->sc);
     hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y, h->mean,
                        h->prevMean);
-    // the rank-mu sum (MFMA) or its exact factors need only Y, the weights
-    // and m_prev: they run on the second stream while the mean and the
-    // evolution paths are computed
-    KG_HIP(hipEventRecord(h->evY, h->stream));
-    KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
+    // the rank-mu sum (MFMA) needs only Y, the weights and m_prev: it runs on
+    // the second stream while the mean and the evolution paths are computed.
+    // The exact mode's factors (k_rankmu_prep, ~6 us) run in line: the two
+    // cross-queue waits of a second stream cost more (~7 us each, kernel trace)
     if (h->cfg.cov_mode == KG_COV_MFMA) {
+      KG_HIP(hipEventRecord(h->evY, h->stream));
+      KG_HIP(hipStreamWaitEvent(h->stream2, h->evY, 0));
       Stage st(h, "rankmu_mfma", h->stream2);
       hipLaunchKernelGGL(k_rankmu_tile<false>, dim3(rankmu_grid(N, h->kslices)), dim3(256), 0, h->stream2, N, mu,
                          (const int *)nullptr, h->kslices, h->Y, (const int *)nullptr, h->w, h->prevMean, h->sc,
                          h->covPart);
+      KG_HIP(hipGetLastError());
+      KG_HIP(hipEventRecord(h->evC, h->stream2));
     } else {
       hipLaunchKernelGGL(k_rankmu_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0,
-                         h->stream2, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
+                         h->stream, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
+      KG_HIP(hipGetLastError());
     }
-    KG_HIP(hipGetLastError());
-    KG_HIP(hipEventRecord(h->evC, h->stream2));
     hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu, h->Y,
                        h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     if (h->G)
@@ -2253,7 +2582,6 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
       hipLaunchKernelGGL(k_adaptC_combine, dim3(ntiles), dim3(256), 0, h->stream, N, h->kslices, ntiles,
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
-      KG_HIP(hipStreamWaitEvent(h->stream, h->evC, 0));
       static const bool old2 = getenv("KORALI_AMD_ADAPTC2") != nullptr;  // A/B switch
       if (old2)
         hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
@@ -2264,8 +2592,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
   }
-  if (cmaes_sigma(h)) return 1;
-  return cmaes_publish_summary(h);
+  return cmaes_sigma(h);  // (k_sigma also publishes the termination record)
 }
 
 int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
@@ -2311,8 +2638,7 @@ int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
                        h->cfg.diagonal_covariance, h->part + 2 * (size_t)N, h->pc, h->C, h->sc, 1);
     KG_HIP(hipGetLastError());
   }
-  if (cmaes_sigma(h)) return 1;
-  return cmaes_publish_summary(h);  // the termination record, as after kg_cmaes_update
+  return cmaes_sigma(h);  // (k_sigma also publishes the termination record, as after kg_cmaes_update)
 }
 
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {

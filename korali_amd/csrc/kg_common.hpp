@@ -61,11 +61,26 @@ inline int zero_fill(void *p, size_t bytes) {
 // rocprofv3 (ROCm 7.2) segfaults at process teardown, after writing its
 // output, in any process that made a cooperative launch, so profile runs set
 // it (scripts/gpu_prof.sh).
-inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s) {
-  static const bool plain = [] {
+//
+// prefer_plain: a small grid launched every generation on the handle's
+// stream (the streamed Givens apply, 33 workgroups at N = 128).  ROCm runs
+// cooperative launches on a queue of their own, and the hand-over to and
+// from it cost 12-15 us on each side of the launch (kernel trace, round 3);
+// a plain launch after the same capacity check stays on the stream's queue.
+// The grid is co-resident once dispatched: it fits the device's capacity,
+// and no kernel holds CUs indefinitely (at worst the spinning workgroups
+// wait until a concurrent kernel's workgroups retire).
+inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s,
+                                  bool prefer_plain = false) {
+  static const bool plain_env = [] {
     const char *e = getenv("KORALI_AMD_PLAIN_LAUNCH");
     return e && *e && *e != '0';
   }();
+  static const bool coop_env = [] {
+    const char *e = getenv("KORALI_AMD_COOP_LAUNCH");  // every resident grid cooperative (A/B)
+    return e && *e && *e != '0';
+  }();
+  const bool plain = plain_env || (prefer_plain && !coop_env);
   if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
   int dev = 0, cus = 0, per = 0;
   hipError_t e = hipGetDevice(&dev);

@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "kg_eigen.hpp"
+#include "kg_chains.hpp"
 
 namespace kg {
 
@@ -2037,7 +2038,7 @@ size_t umw_lds_bytes(int N) { return (2 * (size_t)UMW_COLS * (N + 1) + 3 * (size
 // N-i-1 entries), so no step waits on a global load; used while it fits
 // (KORALI_AMD_UNPACK_ALLH=0 forces the streamed rows)
 __host__ __device__ inline size_t umw_hoff(int N, int i) { return (size_t)i * (N - 1) - (size_t)i * (i - 1) / 2; }
-size_t umw_hall_doubles(int N) { return N >= 3 ? umw_hoff(N, N - 2) : 0; }
+__host__ __device__ inline size_t umw_hall_doubles(int N) { return N >= 3 ? umw_hoff(N, N - 2) : 0; }
 bool umw_all_fits(int N) {
   if (const char *e = getenv("KORALI_AMD_UNPACK_ALLH"))
     if (!atoi(e)) return false;
@@ -2129,6 +2130,84 @@ __global__ void __launch_bounds__(UMW_TPB) k_unpack_mw(int N, const double *__re
     const int k = idx / lda, r = idx % lda, c = g + k * P;
     if (c < N) gQt[(size_t)c * lda + r] = Q[idx];
   }
+}
+
+// Phase B for N <= 128 with one WAVE per column of Q: the column lives in
+// registers (lane l holds rows l and l + 64), every reflector row is staged
+// in LDS once, and a step needs no workgroup barrier: the wave writes its
+// products col[i+1+r] h[r] to its own LDS row, runs the ordered chain over
+// them (kc_add, every lane the same wave-uniform sum) and updates its
+// registers.  Same operations in the same order as k_unpack_mw (GSL
+// householder_hm on the identity), so Q is bit-identical.  The chain is
+// padded to whole groups of 16 with +0.0: the sum starts at a column entry,
+// and every zero of Q here is +0.0 (identity entries; x - y of equal values
+// rounds to +0.0), so acc + (+0.0) == acc.
+constexpr int UWV_WAVES = 4, UWV_SV = 128 + 48;  // columns per workgroup; per-wave staging row
+__host__ __device__ inline size_t uwv_lds_bytes(int N) {
+  return (umw_hall_doubles(N) + (size_t)N + (size_t)UWV_WAVES * UWV_SV) * sizeof(double);
+}
+bool uwv_fits(int N) {
+  if (const char *e = getenv("KORALI_AMD_UNPACK"))
+    if (!strcmp(e, "mw")) return false;
+  return N >= 3 && N <= 128 && uwv_lds_bytes(N) <= 150 * 1024;
+}
+__global__ void __launch_bounds__(64 * UWV_WAVES) k_unpack_wv(int N, const double *__restrict__ gH,
+                                                             const double *__restrict__ tau, double *gQt) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, nt = blockDim.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = blockIdx.x * UWV_WAVES + wid;  // this wave's column
+  double *Hs = smem;                              // reflector rows, packed (row i: N - i - 1 entries)
+  double *ts = Hs + umw_hall_doubles(N);          // tau
+  double *sv = ts + N + (size_t)wid * UWV_SV;     // this wave's products (index r, zero beyond)
+  {
+    const int tot = (N - 2) * N;
+    for (int q0 = tid; q0 < tot; q0 += nt * 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * nt, i = q / N, r = q - i * N;
+        v[u] = (q < tot && r < N - i - 1) ? gH[q] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * nt, i = q / N, r = q - i * N;
+        if (q < tot && r < N - i - 1) Hs[umw_hoff(N, i) + r] = v[u];
+      }
+    }
+    for (int i = tid; i < N; i += nt) ts[i] = tau[i];
+    for (int q = lane; q < UWV_SV; q += 64) sv[q] = 0.0;
+  }
+  __syncthreads();
+  if (c >= N) return;  // wave-uniform; no barrier follows
+  // identity column c
+  double q0 = (lane == c) ? 1.0 : 0.0, q1 = (lane + 64 == c) ? 1.0 : 0.0;
+  for (int i = min(c - 1, N - 3); i >= 0; i--) {  // steps i < c touch column c
+    const double ti = ts[i];
+    if (ti == 0.0) continue;  // uniform
+    const int n = N - i - 1;
+    const double *h = Hs + umw_hoff(N, i);
+    const int r0 = lane - i - 1, r1 = lane + 64 - i - 1;  // offsets of this lane's rows in the reflector
+    const double h0 = (r0 >= 1 && r0 < n) ? h[r0] : 0.0, h1 = (r1 >= 1 && r1 < n) ? h[r1] : 0.0;
+    if (r0 >= 1 && r0 < n) sv[r0] = q0 * h0;
+    if (r1 >= 1 && r1 < n) sv[r1] = q1 * h1;
+    // acc = Q[i+1][c] (wave-uniform), then the ordered sum over r = 1 .. n-1
+    const int e = i + 1;
+    const double qe = (e < 64) ? q0 : q1;
+    const double acc = __longlong_as_double(
+        ((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(qe) >> 32), e & 63) << 32) |
+        (unsigned)__builtin_amdgcn_readlane((int)__double_as_longlong(qe), e & 63));
+    const unsigned pa = (unsigned)(size_t)(const __attribute__((address_space(3))) double *)(sv + 1);
+    const double w = chains::kc_add(acc, pa, __builtin_amdgcn_readfirstlane((unsigned)(n - 1 + 15) >> 4));
+    if (r0 == 0) q0 = q0 - ti * w;
+    else if (r0 >= 1 && r0 < n) q0 = q0 - ti * h0 * w;
+    if (r1 == 0) q1 = q1 - ti * w;
+    else if (r1 >= 1 && r1 < n) q1 = q1 - ti * h1 * w;
+  }
+  const int lda = N + 1;
+  if (lane < N) gQt[(size_t)c * lda + lane] = q0;
+  if (lane + 64 <= N) gQt[(size_t)c * lda + lane + 64] = (lane + 64 < N) ? q1 : 0.0;
+  if (lane == 0 && N < 64) gQt[(size_t)c * lda + N] = 0.0;
 }
 
 // ------------------------------------------------------------------------
@@ -2881,6 +2960,9 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)tmw_lds_bytes(N)));
+    if (uwv_fits(N))
+      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_wv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)uwv_lds_bytes(N)));
     if (umw_all_fits(N))
       KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)(umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double))));
@@ -2926,9 +3008,12 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
+  const bool fusedPublish = hostChase && tri == 4;  // the one-workgroup kernel publishes d | sd itself
+  if (fusedPublish) dsdSeq = chaseSeq + 1;
   if (tri == 4)
     hipLaunchKernelGGL(k_tridiag_sq, dim3(1), dim3(SQ_TPB), sq_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
-                       sd, trace);
+                       sd, trace, fusedPublish ? d_dsd_map : (double *)nullptr,
+                       fusedPublish ? dprog + 1 : (unsigned long long *)nullptr, (unsigned long long)dsdSeq);
   else if (tri == 3)
     hipLaunchKernelGGL(k_tridiag_1wg2, dim3(1), dim3(T2_TPB), t2_lds_doubles(N) * sizeof(double), s, N, C, gH, tau,
                        d, sd, trace);
@@ -2962,9 +3047,12 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   if (prof) prof(profCtx, "eigen_tridiag", 1);
   EigRec devRec = dev;
   if (hostChase) {
-    dsdSeq = chaseSeq + 1;
-    hipLaunchKernelGGL(k_publish_dsd, dim3(1), dim3(256), 0, s, N, (const double *)dsd, d_dsd_map, dprog + 1, dsdSeq);
-    KG_HIP(hipGetLastError());
+    if (!fusedPublish) {
+      dsdSeq = chaseSeq + 1;
+      hipLaunchKernelGGL(k_publish_dsd, dim3(1), dim3(256), 0, s, N, (const double *)dsd, d_dsd_map, dprog + 1,
+                         dsdSeq);
+      KG_HIP(hipGetLastError());
+    }
   } else {
     KG_HIP(hipEventRecord(ev_dsd, s));
     KG_HIP(hipStreamWaitEvent(side, ev_dsd, 0));
@@ -2975,6 +3063,9 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   if (prof) prof(profCtx, "eigen_unpack", 0);
   if (lds)
     hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + 2 * N * sizeof(double), s, N, gH, tau, gQt);
+  else if (uwv_fits(N))
+    hipLaunchKernelGGL(k_unpack_wv, dim3((N + UWV_WAVES - 1) / UWV_WAVES), dim3(64 * UWV_WAVES), uwv_lds_bytes(N), s,
+                       N, gH, tau, gQt);
   else if (umw_all_fits(N))
     hipLaunchKernelGGL(k_unpack_mw<true>, dim3(umw_groups(N)), dim3(UMW_TPB),
                        umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double), s, N, gH, tau, gQt);
@@ -3004,9 +3095,10 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     const unsigned long long seq = ++chaseSeq;
     if (prof) prof(profCtx, "eigen_apply", 0);
     EigRec mr = hmap;
-    // one workgroup per 16 rows + the fetcher workgroup; the row workgroups
-    // spin on the fetcher's progress word, so the grid is launched
-    // cooperatively (co-residency guaranteed, or the launch fails)
+    // one workgroup per 4 rows (16 with 16-lane teams) + the fetcher
+    // workgroup; the row workgroups spin on the fetcher's progress word, so
+    // the grid must be co-resident: launch_resident checks the device's
+    // capacity (or fails) and launches it on this stream (see kg_common.hpp)
     {
       int N_ = N;
       const double *gQt_ = gQt;
@@ -3018,7 +3110,8 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
                       &dprogDev_, &seq_, &mr, &dprog_};
       const int rows = apply_rows();
       KG_HIP(launch_resident(rows == 4 ? (const void *)k_apply<true, 64> : (const void *)k_apply<true, 16>,
-                             dim3((N + rows - 1) / rows + 1), dim3(APPLY_TPB), args, apply_lds_bytes(N, rows), s));
+                             dim3((N + rows - 1) / rows + 1), dim3(APPLY_TPB), args, apply_lds_bytes(N, rows), s,
+                             /*prefer_plain=*/true));
     }
     if (prof) prof(profCtx, "eigen_dsd_wait", 2);
     {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)

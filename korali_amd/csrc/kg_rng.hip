@@ -373,7 +373,8 @@ __global__ void k_uniforms(const uint32_t *__restrict__ ring, unsigned long long
   u[i] = mt_temper(ring[j & (R - 1)]) / 4294967296.0;
 }
 
-__global__ void k_consume_words(StreamState *st, unsigned long long words) {
+__global__ void k_consume_words(StreamState *st, unsigned long long words, const unsigned long long *wordsDev) {
+  if (wordsDev) words = *wordsDev;
   if (threadIdx.x != 0 || words == 0) return;
   const unsigned long long p = st->pos + words;
   if (p > st->hi) st->errors |= KG_ERR_RNG_UNDERRUN;
@@ -621,7 +622,22 @@ int MtStream::uniforms(double *u, size_t M, hipStream_t s) {
   if (produce(M + 2, s)) return 1;
   hipLaunchKernelGGL(k_uniforms, dim3((M + 255) / 256), dim3(256), 0, s, ring_, R_, st_, u, (unsigned long long)M);
   KG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_consume_words, dim3(1), dim3(1), 0, s, st_, (unsigned long long)M);
+  hipLaunchKernelGGL(k_consume_words, dim3(1), dim3(1), 0, s, st_, (unsigned long long)M,
+                     (const unsigned long long *)nullptr);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::peek_uniforms(double *u, size_t M, hipStream_t s) {
+  if (M == 0) return 0;
+  if (produce(M + 2, s)) return 1;
+  hipLaunchKernelGGL(k_uniforms, dim3((M + 255) / 256), dim3(256), 0, s, ring_, R_, st_, u, (unsigned long long)M);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
+int MtStream::consume_words_dev(const unsigned long long *words, hipStream_t s) {
+  hipLaunchKernelGGL(k_consume_words, dim3(1), dim3(1), 0, s, st_, 0ULL, words);
   KG_HIP(hipGetLastError());
   return 0;
 }

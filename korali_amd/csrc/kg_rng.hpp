@@ -87,6 +87,10 @@ class MtStream {
 
   // GSL gsl_rng_uniform draws: M uniforms (no zero skip) consumed at once
   int uniforms(double *u, size_t M, hipStream_t s);
+  // the next M uniforms without consuming them, then consume a count the
+  // device decided (variable consumption: CMA-ES discrete mutations)
+  int peek_uniforms(double *u, size_t M, hipStream_t s);
+  int consume_words_dev(const unsigned long long *words, hipStream_t s);
 
   // Launch the producer for this and the next draw on a side stream so it
   // runs concurrently with whatever the main stream does next (the

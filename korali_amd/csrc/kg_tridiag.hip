@@ -54,9 +54,18 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long x) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
+// hdsd / hflag (optional): the host chase's copy of d | sd, written with
+// system-scope stores as the values are final (sd_i at step i, d at the
+// end), then the flag = seq (what k_publish_dsd does after the kernel, one
+// launch earlier on the critical path)
+__device__ __forceinline__ void st_sys_d(double *p, double v) {
+  __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__restrict__ C, double *gH,
                                                        double *tauOut, double *dOut, double *sdOut,
-                                                       unsigned long long *trace) {
+                                                       unsigned long long *trace, double *hdsd,
+                                                       unsigned long long *hflag, unsigned long long seq) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x, lane = tid & 63, nt = blockDim.x;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar control flow
@@ -83,11 +92,23 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
   }
   for (size_t idx = tid; idx < sq_lds_doubles(N); idx += nt) smem[idx] = 0.0;
   __syncthreads();
-  // symmetrise from the lower triangle (CMAES.cpp.base:908-913)
-  for (int idx = tid; idx < N * N; idx += nt) {
-    const int r = idx / N, c = idx - r * N;
-    if (c > r) M[(size_t)r * lda + c] = C[(size_t)c * N + r];
-    else if (c == r) dg[r] = C[(size_t)r * N + r];
+  // symmetrise from the lower triangle (CMAES.cpp.base:908-913); eight
+  // loads in flight per thread
+  for (int idx0 = tid; idx0 < N * N; idx0 += 8 * nt) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = idx0 + u * nt, r = idx / N, c = idx - r * N;
+      v[u] = (idx < N * N && c >= r) ? C[(size_t)c * N + r] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = idx0 + u * nt, r = idx / N, c = idx - r * N;
+      if (idx < N * N) {
+        if (c > r) M[(size_t)r * lda + c] = v[u];
+        else if (c == r) dg[r] = v[u];
+      }
+    }
   }
   __syncthreads();
   // wave 0 holds the pivot row: alpha = M[i][i+1], x_e = M[i][i+2+e] (e = lane, 64 + lane)
@@ -164,6 +185,7 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
         scal[0] = tau_i;
         tauOut[i] = tau_i;
         sdOut[i] = v0out;
+        if (hdsd) st_sys_d(hdsd + N + i, v0out);
       }
       SQ_MARK(2)
     }
@@ -292,8 +314,24 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
 #undef SQ_MARK
   if (tr)
     for (int k = 0; k < 8; k++) trace[8 + k] += tacc[k];
-  for (int r = tid; r < N; r += nt) dOut[r] = dg[r];
-  if (tid == 0) sdOut[N - 2] = alpha;
+  for (int r = tid; r < N; r += nt) {
+    dOut[r] = dg[r];
+    if (hdsd) st_sys_d(hdsd + r, dg[r]);
+  }
+  if (tid == 0) {
+    sdOut[N - 2] = alpha;
+    if (hdsd) {
+      st_sys_d(hdsd + N + (N - 2), alpha);
+      st_sys_d(hdsd + N + (N - 1), 0.0);  // (never read by the chase)
+    }
+  }
+  if (hdsd) {
+    __syncthreads();
+    if (tid == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: the values before the flag
+      __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------

@@ -271,7 +271,7 @@ std::unique_ptr<Conduit> makeConduit(Json &js) {
 
 struct VariableSpec {
   std::string name;
-  double lb, ub, iv, istd, minstd;
+  double lb, ub, iv, istd, minstd, granularity = 0.0;
   int dist = -1;
 };
 
@@ -407,8 +407,7 @@ std::vector<VariableSpec> readVariables(Json &js) {
     s.iv = num(v, "Initial Value", NAN);
     s.istd = num(v, "Initial Standard Deviation", NAN);
     s.minstd = num(v, "Minimum Standard Deviation Update", 0.0);
-    if (num(v, "Granularity", 0.0) != 0.0)
-      fail("Variable '%s': discrete variables (Granularity) are not supported by the device path.", s.name.c_str());
+    s.granularity = num(v, "Granularity", 0.0);
     vs.push_back(s);
   }
   return vs;
@@ -577,6 +576,10 @@ const char *CMAES_SCALARS[] = {"Sigma", "Trace", "Effective Mu", "Cumulative Cov
                                "Current Max Standard Deviation", "Maximum Diagonal Covariance Matrix Element",
                                "Minimum Diagonal Covariance Matrix Element", "Minimum Covariance Eigenvalue",
                                "Maximum Covariance Eigenvalue", "Infeasible Sample Count", "Model Evaluation Count"};
+// discrete variables (CMAES.config; written and restored when some variable has a Granularity)
+const char *CMAES_DISCRETE_VECTORS[] = {"Masking Matrix", "Masking Matrix Sigma"};
+const char *CMAES_DISCRETE_SCALARS[] = {"Number Of Discrete Mutations", "Number Masking Matrix Entries",
+                                        "Chi Square Number Discrete Mutations"};
 
 struct CmaesModule : SolverModule {
   kg_cmaes_t h = nullptr;
@@ -588,6 +591,7 @@ struct CmaesModule : SolverModule {
   double maxGenerations, maxModelEvaluations, maxInfeasible, maxCondition, minStd, maxStd, maxValue, minValueDiff;
   Json *solverJs = nullptr;
   bool updated = false;  // kg_cmaes_update ran on this handle (its termination record exists)
+  bool hasDiscrete = false;   // some variable has a Granularity (CMAES.cpp.base:44-50)
   bool useGradients = false;  // "Use Gradient Information" (CMAES.cpp.base:82-87, :199, :226, :611-621)
   // Distributed conduit: this rank samples / evaluates rows [r0, r1) of the
   // population; the fitness all-gather and the partial-sum all-reduce run
@@ -674,8 +678,11 @@ struct CmaesModule : SolverModule {
       fn = pb["Objective Function"].getUInt();
     }
 
-    std::vector<double> lb(N), ub(N), iv(N), istd(N), minstd(N);
+    std::vector<double> lb(N), ub(N), iv(N), istd(N), minstd(N), gran(N);
     for (size_t i = 0; i < N; i++) {
+      gran[i] = vars[i].granularity;
+      if (gran[i] < 0.0) fail("Negative granularity for variable '%s'.\n", vars[i].name.c_str());  // CMAES.cpp.base:48
+      if (gran[i] > 0.0) hasDiscrete = true;
       lb[i] = vars[i].lb;
       ub[i] = vars[i].ub;
       iv[i] = vars[i].iv;
@@ -709,6 +716,8 @@ struct CmaesModule : SolverModule {
     c.initial_value = iv.data();
     c.initial_std = istd.data();
     c.min_std_update = minstd.data();
+    c.granularity = gran.data();
+    if (hasDiscrete && dist) fail("Discrete variables (Granularity) need an unsharded run (Sequential or Concurrent conduit).");
     c.normal_seed = seeds.assign(gn);
     c.uniform_seed = seeds.assign(gu);
     const std::string cu = canon(str(sv, "Covariance Update", "Exact"));
@@ -742,6 +751,18 @@ struct CmaesModule : SolverModule {
         const double v = sv[k].getDouble();
         check(kg_cmaes_set_field(h, k, &v, 1));
       }
+    if (hasDiscrete) {
+      for (const char *k : CMAES_DISCRETE_VECTORS)
+        if (sv.contains(k) && sv[k].is_array() && sv[k].size() == N) {
+          std::vector<double> v = flatten(sv[k]);
+          check(kg_cmaes_set_field(h, k, v.data(), N));
+        }
+      for (const char *k : CMAES_DISCRETE_SCALARS)
+        if (sv.contains(k) && sv[k].is_number()) {
+          const double v = sv[k].getDouble();
+          check(kg_cmaes_set_field(h, k, &v, 1));
+        }
+    }
   }
 
   void runGeneration(size_t gen) override {
@@ -881,6 +902,17 @@ struct CmaesModule : SolverModule {
       sv[k] = v;
     }
     for (const char *k : CMAES_SCALARS) sv[k] = field(k);
+    if (hasDiscrete) {
+      sv["Has Discrete Variables"] = true;
+      for (const char *k : CMAES_DISCRETE_VECTORS) {
+        std::vector<double> v(N);
+        check(kg_cmaes_get_field(h, k, v.data(), N));
+        sv[k] = v;
+      }
+      for (const char *k : CMAES_DISCRETE_SCALARS) sv[k] = field(k);
+      // updateDiscreteMutationMatrix clears them every update (:859): zero in every result file
+      sv["Discrete Mutations"] = std::vector<double>(lam * N, 0.0);
+    }
     {
       std::vector<double> X(lam * N);
       check(kg_cmaes_get_field(h, "Sample Population", X.data(), X.size()));

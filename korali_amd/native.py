@@ -36,6 +36,7 @@ class _CmaesCfg(C.Structure):
         ("normal_seed", C.c_uint64), ("uniform_seed", C.c_uint64), ("cov_mode", C.c_int), ("device", C.c_int),
         ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int), ("shard_rank", C.c_int), ("shard_count", C.c_int),
         ("use_gradients", C.c_int), ("gradient_step_size", C.c_double),
+        ("granularity", C.POINTER(C.c_double)),
     ]
 
 
@@ -169,14 +170,14 @@ class CmaesDevice:
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
                  initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host", shard_rank=0,
-                 shard_count=1, mirrored=False, gradient_step_size=None):
+                 shard_count=1, mirrored=False, gradient_step_size=None, granularity=None):
         L = lib()
         self.N, self.lam = int(N), int(lam)
         self.mu = int(mu) if mu else self.lam // 2
         self._arrays = [
             _vec(lower_bound, self.N, -np.inf), _vec(upper_bound, self.N, np.inf),
             _vec(initial_value, self.N, np.nan), _vec(initial_std, self.N, np.nan),
-            _vec(min_std_update, self.N, 0.0),
+            _vec(min_std_update, self.N, 0.0), _vec(granularity, self.N, 0.0),
         ]
         cfg = _CmaesCfg()
         cfg.variable_count, cfg.population_size, cfg.mu_value = self.N, self.lam, int(mu)
@@ -189,7 +190,7 @@ class CmaesDevice:
         cfg.use_gradients, cfg.gradient_step_size = int(gradient_step_size is not None), float(gradient_step_size or 0.0)
         cfg.max_infeasible_resamplings = float(max_infeasible_resamplings)
         (cfg.lower_bound, cfg.upper_bound, cfg.initial_value, cfg.initial_std,
-         cfg.min_std_update) = [_dptr(a) for a in self._arrays]
+         cfg.min_std_update, cfg.granularity) = [_dptr(a) for a in self._arrays]
         cfg.normal_seed, cfg.uniform_seed = int(normal_seed), int(uniform_seed)
         cfg.cov_mode = COV_MODES[cov_mode.lower()] if isinstance(cov_mode, str) else int(cov_mode)
         cfg.device, cfg.store_bdz = int(device), int(store_bdz)

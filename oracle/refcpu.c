@@ -1139,6 +1139,12 @@ struct kr_cmaes
   int useGradients;
   double gradientStepSize;
   double *gradients;
+  /* discrete variables (CMAES.cpp.base:34, :44-50, :101-107, :515-544,
+   * :834-867): Granularity per variable, the masking vectors and the
+   * discrete-mutation bookkeeping */
+  double *granularity, *maskingMatrix, *maskingMatrixSigma, *discreteMutations;
+  double numberMaskingMatrixEntries, numberOfDiscreteMutations, chiSquareNumberDiscreteMutations;
+  int hasDiscrete;
 };
 
 kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
@@ -1183,6 +1189,10 @@ kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
   AL(h->auxBDZ, N);
   AL(h->auxAxisLengths, N);
   AL(h->auxEvec, N * N);
+  AL(h->granularity, N);
+  AL(h->maskingMatrix, N);
+  AL(h->maskingMatrixSigma, N);
+  AL(h->discreteMutations, lambda * N);
 #undef AL
   h->sortingIndex = (size_t *)calloc(lambda, sizeof(size_t));
   kr_rng_seed(&h->normal, 0);
@@ -1216,6 +1226,10 @@ void kr_cmaes_free(kr_cmaes *h)
   free(h->auxBDZ);
   free(h->auxAxisLengths);
   free(h->auxEvec);
+  free(h->granularity);
+  free(h->maskingMatrix);
+  free(h->maskingMatrixSigma);
+  free(h->discreteMutations);
   free(h->sortingIndex);
   free(h);
 }
@@ -1251,6 +1265,13 @@ double *kr_cmaes_field(kr_cmaes *h, const char *name, size_t *len)
   VEC("Current Best Variables", h->currentBestVariables, N)
   VEC("Mean Update", h->meanUpdate, N)
   VEC("Auxiliar BDZ Matrix", h->auxBDZ, N)
+  VEC("Granularity", h->granularity, N)
+  VEC("Masking Matrix", h->maskingMatrix, N)
+  VEC("Masking Matrix Sigma", h->maskingMatrixSigma, N)
+  VEC("Discrete Mutations", h->discreteMutations, h->lambda * N)
+  SCA("Number Masking Matrix Entries", numberMaskingMatrixEntries)
+  SCA("Number Of Discrete Mutations", numberOfDiscreteMutations)
+  SCA("Chi Square Number Discrete Mutations", chiSquareNumberDiscreteMutations)
   SCA("Sigma", sigma)
   SCA("Trace", trace)
   SCA("Effective Mu", effectiveMu)
@@ -1377,12 +1398,21 @@ static void cmaes_init_covariance(kr_cmaes *h)
     if (h->minDiagC > h->C[i * N + i]) h->minDiagC = h->C[i * N + i];
 }
 
-/* setInitialConfiguration, CMAES.cpp.base:14-184 (no constraints, no
- * discrete variables) */
+/* setInitialConfiguration, CMAES.cpp.base:14-184 (no constraints) */
 void kr_cmaes_initialize(kr_cmaes *h)
 {
   const size_t N = h->N;
   size_t i;
+  /* :34, :44-50, :101-107 */
+  h->chiSquareNumberDiscreteMutations = sqrt((double)N) * (1. - 1. / (4. * N) + 1. / (21. * N * N));
+  h->hasDiscrete = 0;
+  for (i = 0; i < N; i++)
+    if (h->granularity[i] > 0.0) h->hasDiscrete = 1;
+  memset(h->discreteMutations, 0, sizeof(double) * h->lambda * N);
+  memset(h->maskingMatrix, 0, sizeof(double) * N);
+  memset(h->maskingMatrixSigma, 0, sizeof(double) * N);
+  h->numberMaskingMatrixEntries = 0;
+  h->numberOfDiscreteMutations = 0;
   h->bestEverValue = -INFINITY;
   h->previousBestEverValue = h->bestEverValue;
   h->previousBestValue = h->bestEverValue;
@@ -1447,7 +1477,15 @@ void kr_cmaes_eigen_only(kr_cmaes *h)
   memcpy(h->B, h->auxEvec, sizeof(double) * N * N);
 }
 
-/* sampleSingle, CMAES.cpp.base:494-545 (continuous variables) */
+/* discretize, CMAES.cpp.base:861-867 */
+static void cmaes_discretize(const kr_cmaes *h, double *x)
+{
+  size_t d;
+  for (d = 0; d < h->N; ++d)
+    if (h->granularity[d] != 0.0) x[d] = round(x[d] / h->granularity[d]) * h->granularity[d];
+}
+
+/* sampleSingle, CMAES.cpp.base:494-545 */
 static void cmaes_sample_single(kr_cmaes *h, size_t idx, const double *z)
 {
   const size_t N = h->N;
@@ -1470,6 +1508,37 @@ static void cmaes_sample_single(kr_cmaes *h, size_t idx, const double *z)
       for (e = 0; e < N; ++e) bdz[d] += h->B[d * N + e] * h->auxBDZ[e];
       x[d] = h->currentMean[d] + h->sigma * bdz[d];
     }
+  if (h->hasDiscrete)
+  {
+    /* :515-544: a geometric +-mutation of one masked variable for the first
+     * numberOfDiscreteMutations - 1 samples, the best-ever point rounded for
+     * the next one (uniforms from the solver's Uniform Generator) */
+    if ((double)(idx + 1) < h->numberOfDiscreteMutations)
+    {
+      const double p_geom = kr_pow_cr(0.7, 1.0 / h->numberMaskingMatrixEntries);
+      size_t select = (size_t)floor(kr_ran_flat(&h->uniform, 0.0, 1.0) * h->numberMaskingMatrixEntries);
+      for (d = 0; d < N; ++d)
+        if ((h->maskingMatrix[d] == 1.0) && (select-- == 0))
+        {
+          double dmutation = 1.0;
+          while (kr_ran_flat(&h->uniform, 0.0, 1.0) > p_geom) dmutation += 1.0;
+          dmutation *= h->granularity[d];
+          if (kr_ran_flat(&h->uniform, 0.0, 1.0) > 0.5) dmutation *= -1.0;
+          h->discreteMutations[idx * N + d] = dmutation;
+          x[d] += dmutation;
+        }
+    }
+    else if ((double)(idx + 1) == h->numberOfDiscreteMutations)
+    {
+      for (d = 0; d < N; ++d)
+        if (h->granularity[d] != 0.0)
+        {
+          const double dmutation = round(h->bestEverVariables[d] / h->granularity[d]) * h->granularity[d] - x[d];
+          h->discreteMutations[idx * N + d] = dmutation;
+          x[d] += dmutation;
+        }
+    }
+  }
 }
 
 /* Optimizer::isSampleFeasible, optimizer.cpp.base:5-14 */
@@ -1529,7 +1598,7 @@ void kr_cmaes_sample_only(kr_cmaes *h)
   const size_t N = h->N;
   size_t i, d;
   double *r1 = (double *)malloc(sizeof(double) * N), *r2 = (double *)malloc(sizeof(double) * N);
-  if (!h->mirrored)
+  if (!h->mirrored && !h->hasDiscrete)
   {
     /* fast form: draw every normal first (stream order), transform the
      * samples in parallel, then check feasibility in sample order; on the
@@ -1558,6 +1627,7 @@ void kr_cmaes_sample_only(kr_cmaes *h)
       {
         for (d = 0; d < N; ++d) r1[d] = 0.0 + kr_ran_gaussian(&h->normal, 1.0);
         cmaes_sample_single(h, i, r1);
+        if (h->hasDiscrete) cmaes_discretize(h, h->X + i * N);
         ok = cmaes_feasible(h, h->X + i * N);
         h->infeasibleSampleCount += ok ? 0 : 1;
       } while (ok == 0 && (h->infeasibleSampleCount < h->maxInfeasibleResamplings));
@@ -1578,6 +1648,11 @@ void kr_cmaes_sample_only(kr_cmaes *h)
         }
         cmaes_sample_single(h, i, r1);
         cmaes_sample_single(h, i + 1, r2);
+        if (h->hasDiscrete)
+        {
+          cmaes_discretize(h, h->X + i * N);
+          cmaes_discretize(h, h->X + (i + 1) * N);
+        }
         ok1 = cmaes_feasible(h, h->X + i * N);
         if (!ok1) h->infeasibleSampleCount++;
         ok2 = cmaes_feasible(h, h->X + (i + 1) * N);
@@ -1602,8 +1677,9 @@ void kr_cmaes_evaluate(kr_cmaes *h, int objective)
 #pragma omp parallel for schedule(static)
   for (i = 0; i < (long)h->lambda; i++)
   {
-    const double *x = h->X + (size_t)i * h->N;
+    double *x = h->X + (size_t)i * h->N;
     double f;
+    if (h->hasDiscrete) cmaes_discretize(h, x); /* :208 */
     if (objective == 0) f = kr_obj_negative_rosenbrock(x, h->N);
     else if (objective == 1) f = kr_obj_negative_ackley(x, h->N);
     else f = kr_obj_negative_sphere(x, h->N);
@@ -1739,8 +1815,42 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
       h->minDiagC = h->C[d * N + d];
   }
 
-  /* updateSigma (standard branch) */
-  h->sigma *= kr_exp_cr(h->sigmaCumulationFactor / h->dampFactor * (h->psNorm / h->chiSquareNumber - 1.));
+  /* updateDiscreteMutationMatrix, :834-859 (after adaptC, with the old sigma) */
+  if (h->hasDiscrete)
+  {
+    double entries = (double)(N + 1);
+    for (d = 0; d < N; ++d) h->maskingMatrixSigma[d] = 1.0;
+    for (d = 0; d < N; ++d)
+      if (h->sigma * sqrt(h->C[d * N + d]) / sqrt(h->sigmaCumulationFactor) < 0.2 * h->granularity[d])
+      {
+        h->maskingMatrixSigma[d] = 0.0;
+        entries -= 1.0;
+      }
+    h->chiSquareNumberDiscreteMutations = sqrt(entries) * (1. - 1. / (4. * entries) + 1. / (21. * entries * entries));
+    h->numberMaskingMatrixEntries = 0;
+    for (d = 0; d < N; ++d) h->maskingMatrix[d] = 0.0;
+    for (d = 0; d < N; ++d)
+      if (2.0 * h->sigma * sqrt(h->C[d * N + d]) < h->granularity[d])
+      {
+        h->maskingMatrix[d] = 1.0;
+        h->numberMaskingMatrixEntries += 1.0;
+      }
+    {
+      const double a = round((double)h->lambda / 10.0 + h->numberMaskingMatrixEntries + 1), b = floor((double)h->lambda / 2.0) - 1;
+      h->numberOfDiscreteMutations = a < b ? a : b;
+    }
+    memset(h->discreteMutations, 0, sizeof(double) * h->lambda * N);
+  }
+
+  /* updateSigma :720-761 */
+  if (h->hasDiscrete)
+  {
+    double pathL2 = 0.0;
+    for (d = 0; d < N; ++d) pathL2 += h->maskingMatrixSigma[d] * h->ps[d] * h->ps[d];
+    h->sigma *= kr_exp_cr(h->sigmaCumulationFactor / h->dampFactor * (sqrt(pathL2) / h->chiSquareNumberDiscreteMutations - 1.));
+  }
+  else
+    h->sigma *= kr_exp_cr(h->sigmaCumulationFactor / h->dampFactor * (h->psNorm / h->chiSquareNumber - 1.));
   if (mu > 1 && h->currentBestValue == h->F[h->sortingIndex[mu - 1]]) h->sigma *= kr_exp_cr(0.2 + h->sigmaCumulationFactor / h->dampFactor);
   {
     const double ub = sqrt(h->trace / N);

@@ -19,6 +19,8 @@ step() {
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    occ2) step occ_pair 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest -x -v -s --timeout 250 --timeout-method thread tests/test_cxx_api.py::test_reference_idioms_run_cmaes_direct tests/test_gpu_baseline_shapes.py::test_c4_shape_two_generations_bit_exact ; step occ_coll 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
+    testsdbg) step testsdbg 1100 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -x -v -s -m gpu --timeout 300 --timeout-method thread ;;
     tests) step tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
     trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c4.py ;;
@@ -40,6 +42,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     benchab) step bench_old 300 env KORALI_AMD_ADAPTC2=1 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_new 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     profq) step profq 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     c4t) step c4t 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests/test_gpu_baseline_shapes.py -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
+    benchq) step benchq 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     benchteam) step bench_t16 300 env KORALI_AMD_APPLY_TEAM=16 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_t64 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
   esac

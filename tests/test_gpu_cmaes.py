@@ -356,3 +356,55 @@ def test_gradient_informed_mean_step_matches_oracle_bit_exact():
             assert not np.array_equal(dev["Current Mean"], plain["Current Mean"])
     dev.close()
     plain.close()
+
+
+@pytest.mark.parametrize("Nv,lam,mirrored,bound,gens", [(10, 8, False, (-19.0, 21.0), 120), (12, 32, False, (-2.0, 2.0), 80),
+                                                        (6, 16, True, (-3.0, 3.0), 80), (1, 64, True, (-10.0, 10.0), 10)])
+def test_discrete_variables_match_oracle_bit_exact(Nv, lam, mirrored, bound, gens):
+    """Discrete variables (Granularity; CMAES.cpp.base:44-50, sampleSingle's
+    discrete mutations :515-544, discretize :861-867, the masking update
+    :834-859 and the masked sigma step :729-735): populations, selections,
+    masks, sigma and both generators' states bit-exact vs the oracle.  The
+    first case is examples/optimization/discrete/run-cmaes.py's setup
+    (variables 0, 1, 3, 6 on the integers), the last the reference's
+    statistical corner case 'Discrete with Mirrored Sampling'."""
+    seed = 1701
+    gran = np.zeros(Nv)
+    gran[[i for i in (0, 1, 3, 6) if i < Nv]] = 1.0
+    if Nv == 1:
+        gran[0] = 0.0001
+    if Nv == 12:
+        gran[::2] = 0.25
+    lb, ub = np.full(Nv, bound[0]), np.full(Nv, bound[1])
+    o = R.CMAES(Nv, lam, 0)
+    o["Initial Value"] = np.ones(Nv)
+    o["Initial Standard Deviation"] = (ub - lb) * 0.3
+    o["Lower Bound"], o["Upper Bound"], o["Granularity"] = lb, ub, gran
+    if mirrored:
+        o.option("Mirrored Sampling", 1)
+    R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+    R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+    dev = device_solver(Nv, lam, initial_value=np.ones(Nv), initial_std=(ub - lb) * 0.3, lower_bound=lb,
+                        upper_bound=ub, granularity=gran, mirrored=mirrored, normal_seed=seed, uniform_seed=seed + 1)
+    mutated = 0
+    for g in range(1, gens + 1):
+        o.generation(g, "sphere")
+        dev.generation(g, "sphere")
+        dev.synchronize()
+        X = dev["Sample Population"].reshape(lam, Nv)
+        assert np.array_equal(X, o["Sample Population"].reshape(lam, Nv)), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        for key in ("Current Mean", "Covariance Matrix", "Masking Matrix", "Masking Matrix Sigma"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        for key in ("Sigma", "Infeasible Sample Count", "Number Of Discrete Mutations", "Number Masking Matrix Entries",
+                    "Chi Square Number Discrete Mutations"):
+            assert dev[key][0] == o[key][0], (g, key)
+        # discrete coordinates sit on their grids
+        d = gran > 0
+        assert np.array_equal(X[:, d], np.round(X[:, d] / gran[d]) * gran[d]), g
+        mutated += o["Number Masking Matrix Entries"][0] > 0
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+    assert dev.get_rng(1) == o.rng(1).get_bytes()  # the mutations' uniforms, consumed in the reference's order
+    if Nv >= 10:
+        assert mutated > 0  # masked variables took geometric mutations
+    dev.close()

@@ -83,9 +83,38 @@ def test_statistical_cmaes_correctness(cfg, tol):
 def test_unsupported_features_fail_loudly():
     import korali
     e = cmaes_1d()
-    e["Variables"][0]["Granularity"] = 0.5
-    with pytest.raises(korali.KoraliError, match="Granularity"):
+    e["Problem"]["Constraints"] = [lambda s: None]
+    with pytest.raises(korali.KoraliError, match="Constrained CMA-ES"):
         korali.Engine().run(e)
+    e = cmaes_1d()
+    e["Variables"][0]["Granularity"] = -0.5
+    with pytest.raises(korali.KoraliError, match="Negative granularity"):
+        korali.Engine().run(e)
+
+
+@pytest.mark.parametrize("mirrored", [False, True])
+def test_statistical_cmaes_discrete(mirrored, tmp_path):
+    """tests/statistical/optimizers/correctness/run-cmaes.py, corner case
+    'Discrete with Mirrored Sampling' (Granularity 0.0001, Population Size
+    64, 10 generations): checkMin(e, 0.23246, 1e-3); and the discrete state in
+    the result files."""
+    import json
+    import korali
+    e = cmaes_1d(**{"Population Size": 64, "Mirrored Sampling": mirrored})
+    e["Variables"][0]["Initial Value"] = 1.0
+    e["Variables"][0]["Granularity"] = 0.0001
+    e["Solver"]["Termination Criteria"]["Max Generations"] = 10
+    e["File Output"]["Enabled"] = True
+    e["File Output"]["Path"] = str(tmp_path)
+    korali.Engine().run(e)
+    assert np.isclose(0.23246, e["Solver"]["Best Ever Value"], atol=1e-3)
+    x = e["Solver"]["Best Ever Variables"][0]
+    assert x == round(x / 0.0001) * 0.0001
+    st = json.load(open(tmp_path / "latest"))["Solver"]
+    assert st["Has Discrete Variables"] is True or st["Has Discrete Variables"] == 1
+    for k in ("Masking Matrix", "Masking Matrix Sigma", "Number Of Discrete Mutations", "Number Masking Matrix Entries",
+              "Chi Square Number Discrete Mutations", "Discrete Mutations"):
+        assert k in st, k
 
 
 def test_statistical_tmcmc_gaussian():

@@ -286,3 +286,31 @@ def test_oracle_mtmcmc_posterior_of_the_reference_example():
     m = o["Mean Theta"]
     assert abs(m[0] - 0.907) < 0.25 and abs(m[1] - 2.307) < 0.8 and 0.05 < m[2] < 2.0, m
     assert R.lib().kr_chi2inv_068(3) == 3.505882355768179
+
+
+def test_oracle_discrete_variables_stay_on_their_grid():
+    """The oracle's discrete-variable path (CMAES.cpp.base:515-544, :834-867)
+    on examples/optimization/discrete/run-cmaes.py's setup: discrete
+    coordinates on the integers, masks switching on as sigma shrinks, the
+    Uniform Generator consumed only once discrete mutations exist."""
+    Nv, lam = 10, 8
+    o = R.CMAES(Nv, lam, 0)
+    gran = np.zeros(Nv)
+    gran[[0, 1, 3, 6]] = 1.0
+    o["Initial Value"], o["Lower Bound"], o["Upper Bound"] = np.ones(Nv), np.full(Nv, -19.0), np.full(Nv, 21.0)
+    o["Initial Standard Deviation"] = np.full(Nv, 12.0)
+    o["Granularity"] = gran
+    R.lib().kr_rng_seed(o.rng(0).ptr, 5)
+    R.lib().kr_rng_seed(o.rng(1).ptr, 6)
+    u0 = o.rng(1).get_bytes()
+    o.generation(1, "sphere")
+    assert o.rng(1).get_bytes() == u0  # no discrete mutations in generation 1
+    seen = 0
+    for g in range(1, 200):
+        if g > 1:
+            o.generation(g, "sphere")
+        X = o["Sample Population"].reshape(lam, Nv)
+        assert np.array_equal(X[:, gran > 0], np.round(X[:, gran > 0]))
+        seen += o["Number Masking Matrix Entries"][0] > 0
+        assert o["Number Of Discrete Mutations"][0] <= lam // 2 - 1
+    assert seen > 0 and o.rng(1).get_bytes() != u0
