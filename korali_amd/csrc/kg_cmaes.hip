@@ -1096,7 +1096,14 @@ __global__ void __launch_bounds__(256) k_adaptC_exact2(int N, int mu, int diagon
 // issue-bound well above the add latency; here the add chain is the bound.
 // Tiles of 16-column block cb run on XCD cb % 8 (workgroup slot s -> XCD s % 8),
 // so a column block of Yc is fetched from HBM into one L2.
-constexpr int AX3_P = 7, AX3_K = 64, AX3_S = AX3_K + 1;  // producers, chunk, LDS row stride
+// A workgroup barrier that orders LDS only: __syncthreads' release fence
+// waits for every outstanding global load too (s_waitcnt vmcnt(0)), which
+// would expose the prefetches issued for later chunks at every round
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory"); }
+// row stride 73: odd (two-way bank pairs at most for the consumer's per-lane
+// rows) and >= 70, so every producer slot p + 7 u (u < 10) stores without a
+// branch (slots 64..69 are never summed)
+constexpr int AX3_P = 7, AX3_K = 64, AX3_S = 73;  // producers, chunk, LDS row stride
 __device__ __forceinline__ int ax3_tiles_in(int N, int cb) {  // row blocks of column block cb
   const int R = (N + 3) / 4, lo = 4 * cb;
   return R > lo ? R - lo : 0;
@@ -1132,7 +1139,7 @@ __device__ __forceinline__ double ax3_run(double c, const double *__restrict__ Y
 #pragma unroll
     for (int u = 0; u < KP; u++) {
       const int kl = p + AX3_P * u;
-      if (kl < AX3_K) Q[buf][lane * AX3_S + kl] = rankmu_quot<kMarkstein>(tv[u], yv[u], s2, y);
+      Q[buf][lane * AX3_S + kl] = rankmu_quot<kMarkstein>(tv[u], yv[u], s2, y);
     }
   };
   auto chain = [&](int k0, int buf) {
@@ -1143,29 +1150,32 @@ __device__ __forceinline__ double ax3_run(double c, const double *__restrict__ Y
   };
   // producers: in the round where wave 0 sums chunk k, the loads of chunk
   // k+2 are issued first, then chunk k+1's quotients are formed from the
-  // registers its loads filled one round earlier (two register sets in turn)
+  // registers its loads filled one round earlier (two register sets in
+  // turn).  Producer and consumer waves run separate loops with the same
+  // barrier count, so the compiler keeps each register set in place.
   if (wid > 0) {
     load(0, yA, tA);
-    if (AX3_K < mu) load(AX3_K, yB, tB);
+    load(AX3_K, yB, tB);
     store(0, yA, tA);
-  }
-  __syncthreads();
-  for (int k0 = 0; k0 < mu; k0 += 2 * AX3_K) {
-    // round k0: chunk k0 (buffer 0) summed; chunk k0+K (registers B) formed; chunk k0+2K loaded into A
-    if (wid == 0) chain(k0, 0);
-    else if (k0 + AX3_K < mu) {
-      if (k0 + 2 * AX3_K < mu) load(k0 + 2 * AX3_K, yA, tA);
-      store(1, yB, tB);
+    lds_barrier();
+    for (int k0 = 0; k0 < mu; k0 += 2 * AX3_K) {
+      load(k0 + 2 * AX3_K, yA, tA);  // (rows past mu load zeros)
+      if (k0 + AX3_K < mu) store(1, yB, tB);
+      lds_barrier();
+      if (k0 + AX3_K >= mu) break;
+      load(k0 + 3 * AX3_K, yB, tB);
+      if (k0 + 2 * AX3_K < mu) store(0, yA, tA);
+      lds_barrier();
     }
-    __syncthreads();
-    if (k0 + AX3_K >= mu) break;
-    // round k0+K: chunk k0+K (buffer 1) summed; chunk k0+2K (registers A) formed; chunk k0+3K loaded into B
-    if (wid == 0) chain(k0 + AX3_K, 1);
-    else if (k0 + 2 * AX3_K < mu) {
-      if (k0 + 3 * AX3_K < mu) load(k0 + 3 * AX3_K, yB, tB);
-      store(0, yA, tA);
+  } else {
+    lds_barrier();
+    for (int k0 = 0; k0 < mu; k0 += 2 * AX3_K) {
+      chain(k0, 0);
+      lds_barrier();
+      if (k0 + AX3_K >= mu) break;
+      chain(k0 + AX3_K, 1);
+      lds_barrier();
     }
-    __syncthreads();
   }
   return c;
 }

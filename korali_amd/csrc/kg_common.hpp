@@ -12,6 +12,7 @@
 // multiply-adds are the explicit fma() calls of the exact two-product.
 #pragma once
 
+#include <algorithm>
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
@@ -70,6 +71,32 @@ inline int zero_fill(void *p, size_t bytes) {
 // The grid is co-resident once dispatched: it fits the device's capacity,
 // and no kernel holds CUs indefinitely (at worst the spinning workgroups
 // wait until a concurrent kernel's workgroups retire).
+// Workgroups per CU the kernel's own resources allow (VGPRs of the unified
+// 512-entry file per SIMD lane, at most 8 waves per SIMD, 160 KB of LDS).
+// In some processes (a pytest run that has imported every test module) the
+// runtime's occupancy query returned 0 for grids that fit and run
+// elsewhere; resident_per_cu takes the larger of the two answers.
+inline int own_blocks_per_cu(const void *f, int threads, size_t lds) {
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, f) != hipSuccess) return 0;
+  const int wavesPerWg = (threads + 63) / 64;
+  int vgpr = a.numRegs > 0 ? a.numRegs : 1;
+  vgpr = (vgpr + 7) & ~7;
+  const int wavesPerSimd = std::min(8, 512 / vgpr);
+  const int byWaves = (4 * wavesPerSimd) / wavesPerWg;
+  const size_t ldsTot = a.sharedSizeBytes + lds;
+  const int byLds = ldsTot ? (int)((160 * 1024) / ldsTot) : 32;
+  return std::max(0, std::min(byWaves, byLds));
+}
+inline hipError_t resident_per_cu(const void *f, int threads, size_t lds, int *per, int *runtimePer) {
+  int rt = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&rt, f, threads, lds);
+  if (e != hipSuccess) return e;
+  *per = std::max(rt, own_blocks_per_cu(f, threads, lds));
+  if (runtimePer) *runtimePer = rt;
+  return hipSuccess;
+}
+
 inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **args, size_t lds, hipStream_t s,
                                   bool prefer_plain = false) {
   static const bool plain_env = [] {
@@ -80,12 +107,23 @@ inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **a
     const char *e = getenv("KORALI_AMD_COOP_LAUNCH");  // every resident grid cooperative (A/B)
     return e && *e && *e != '0';
   }();
-  const bool plain = plain_env || (prefer_plain && !coop_env);
-  if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
+  bool plain = plain_env || (prefer_plain && !coop_env);
+  if (!plain) {
+    // the runtime refuses a cooperative launch its occupancy query rejects:
+    // where that query is wrong (see resident_per_cu), launch plain after
+    // the capacity check below
+    int dev = 0, cus = 0, per = 0, rt = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        resident_per_cu(f, (int)(block.x * block.y * block.z), lds, &per, &rt) == hipSuccess &&
+        (long long)rt * cus < (long long)grid.x * grid.y * grid.z)
+      plain = true;
+    if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
+  }
   int dev = 0, cus = 0, per = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, (int)(block.x * block.y * block.z), lds);
+  if (e == hipSuccess) e = resident_per_cu(f, (int)(block.x * block.y * block.z), lds, &per, nullptr);
   if (e != hipSuccess) return e;
   if ((long long)per * cus < (long long)grid.x * grid.y * grid.z) return hipErrorCooperativeLaunchTooLarge;
   return hipLaunchKernel(f, grid, block, args, lds, s);

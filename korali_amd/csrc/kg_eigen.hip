@@ -2944,8 +2944,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
       if (!mw2_fits(N) || mw2_rows(N) != rw) break;  // LDS exhausted (or rows forced by the environment)
       KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)mw2_lds_bytes(N)));
-      KG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_tridiag_mw2, MW2_TPB,
-                                                          mw2_lds_bytes(N)));
+      KG_HIP(resident_per_cu((const void *)k_tridiag_mw2, MW2_TPB, mw2_lds_bytes(N), &perCU, nullptr));
       if (getenv("KORALI_AMD_DEBUG_OCC"))
         fprintf(stderr, "[korali_amd] mw2 N=%d rows=%d groups=%d lds=%zu perCU=%d cus=%d\n", N, rw, mw2_groups(N),
                 mw2_lds_bytes(N), perCU, cus);

@@ -1598,7 +1598,7 @@ void kr_cmaes_sample_only(kr_cmaes *h)
   const size_t N = h->N;
   size_t i, d;
   double *r1 = (double *)malloc(sizeof(double) * N), *r2 = (double *)malloc(sizeof(double) * N);
-  if (!h->mirrored && !h->hasDiscrete)
+  if (!h->mirrored)
   {
     /* fast form: draw every normal first (stream order), transform the
      * samples in parallel, then check feasibility in sample order; on the
@@ -1606,7 +1606,7 @@ void kr_cmaes_sample_only(kr_cmaes *h)
      * reference's sequential resampling loop below */
     kr_rng saved = h->normal;
     double *Z = (double *)malloc(sizeof(double) * N * h->lambda);
-    int all_ok = 1;
+    int all_ok = !h->hasDiscrete; /* discrete variables: the sequential loop below */
     kr_ran_gaussian_n(&h->normal, h->lambda * N, Z);
     cmaes_sample_all(h, Z);
     for (i = 0; i < h->lambda && all_ok; ++i) all_ok = cmaes_feasible(h, h->X + i * N);

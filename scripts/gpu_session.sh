@@ -37,6 +37,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
     cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
     benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
+    dprobe) step dprobe 120 python tools/discrete_probe.py ;;
+    occc) step occ_coll 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
     occt) step occ_torch 120 python tools/occ_probe.py exact torch ;;
     occ) step occ_exact 120 python tools/occ_probe.py exact && step occ_mfma 120 python tools/occ_probe.py mfma ;;
     benchab) step bench_old 300 env KORALI_AMD_ADAPTC2=1 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_new 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
