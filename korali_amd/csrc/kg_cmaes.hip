@@ -2205,7 +2205,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   }
   // a reserve of transformed rows for resampling: finite bounds, or discrete
   // variables (a rounded or mutated sample may leave the bounds or not)
-  h->R = (h->finiteBounds || h->hasDiscrete) ? std::max(64, L / 4) : 0;
+  h->R = (h->finiteBounds || h->hasDiscrete) ? std::max(256, L / 4) : 0;
   h->shards = cfg->shard_count > 1 ? cfg->shard_count : 1;
   h->shardRank = h->shards > 1 ? cfg->shard_rank : 0;
   if (h->shards > 1 && (L % h->shards != 0 || h->finiteBounds || cfg->shard_rank < 0 ||

@@ -1819,9 +1819,12 @@ int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmi
     NmSync *syncp = h->nmSync;
     NmOut *outp = h->dNm;
     void *args[] = {&Pa, (void *)&llp, (void *)&devp, &rho, &tgt, &tab, &syncp, &outp};
-    // co-residency of the controller and its workers is guaranteed by the
-    // cooperative launch (it fails rather than under-schedules)
-    if (launch_resident((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream) !=
+    // the controller and its workers must be co-resident: launch_resident
+    // checks the capacity (or fails rather than under-schedules) and, for
+    // this per-generation 65-workgroup grid, launches it on the handle's
+    // stream instead of ROCm's cooperative queue (kg_common.hpp)
+    if (launch_resident((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream,
+                        /*prefer_plain=*/true) !=
         hipSuccess) {
       (void)hipGetLastError();
       h->nmFallbacks++;

@@ -49,5 +49,5 @@ for s in ${STEPS:-tests}; do
     pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac
 done
-find $O -name "*kernel_trace.csv" -delete
+find $O -name "*kernel_trace.csv" ! -path "*prof_c2*" -delete
 echo "session done"
