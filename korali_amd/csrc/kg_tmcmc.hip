@@ -1927,6 +1927,16 @@ int tm_schedule(kg_tmcmc_s *h) {
   h->rounds = !(B == 0 && nc == P);
   h->step = 0;
   h->maxSteps = 1;
+  if (h->mt) {
+    // mTMCMC (Max Chain Length 1): the WAITANY loop of runGeneration
+    // (:112-144) re-evaluates every chain's unchanged candidate 1 + Burn In
+    // times, and processCandidate runs once per chain after it (:146-155),
+    // so a burn-in only repeats the evaluations (the last one is kept) and
+    // the evaluation count; the step itself is the burn-in-free one
+    KG_CHECK(nc == P, "mTMCMC: every chain runs one step (Max Chain Length 1)");
+    h->rounds = false;
+    h->maxSteps = 1 + (int)B;
+  }
   if (!h->rounds) {
     h->dba = h->ca;
     h->dbb = h->cb;
@@ -2105,8 +2115,6 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
              "Current version of 'mTMCMC' supports only 'Max Chain Length' of 1 (BASIS).");
     KG_CHECK(cfg->step_size >= 0.0, "Step Size lower than 0.0");
     KG_CHECK(cfg->domain_extension_factor >= 0.0, "Domain Extension Factor lower than 0.0");
-    KG_CHECK(cfg->default_burn_in == 0.0 && cfg->per_generation_burn_in_count == 0,
-             "mTMCMC: burn-in is not supported by this implementation");
     KG_CHECK(cfg->shard_count <= 1, "mTMCMC runs unsharded");
     KG_CHECK(cfg->variable_count <= 128, "mTMCMC: at most 128 variables");
   }
@@ -2576,6 +2584,13 @@ int kg_tmcmc_advance(kg_tmcmc_t h, size_t generation, size_t *pending) {
   const int N = h->N, P = h->P;
   KG_CHECK(h->step < h->maxSteps, "kg_tmcmc_advance: every chain has finished this generation");
   const int s = ++h->step;
+  if (!h->rounds && h->mt && s < h->maxSteps) {
+    // mTMCMC burn-in: the same candidates are evaluated again (tm_schedule)
+    h->pendingCount = (size_t)(h->cb - h->ca);
+    h->modelEvaluationCount += (double)h->chainCount;  // the re-started samples (:127)
+    if (pending) *pending = h->pendingCount;
+    return 0;
+  }
   if (!h->rounds) {
     // every chain runs one step: Uniform c, database entry c
     TmStage st(h, "accept");

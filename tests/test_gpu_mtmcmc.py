@@ -183,3 +183,42 @@ def test_engine_mtmcmc_constraints():
     e["Solver"]["Step Size"] = -1.0
     with pytest.raises(Exception, match="Step Size lower than 0.0"):
         korali.Engine().run(e)
+
+
+@pytest.mark.parametrize("burn_in,per_gen", [(2, None), (0, [1, 3])])
+def test_engine_mtmcmc_burn_in(burn_in, per_gen):
+    """mTMCMC with Burn In / Per Generation Burn In (TMCMC.cpp.base:112-155,
+    :229-252, :781-789): the WAITANY loop evaluates each chain's unchanged
+    candidate 1 + Current Burn In times and processCandidate runs once per
+    chain afterwards, so the state equals the burn-in-free run's while the
+    model runs (and Model Evaluation Count grows by) Current Burn In times
+    the population more per generation from generation 2."""
+    import korali
+    calls = {"n": 0}
+
+    def counted(s):
+        calls["n"] += 1
+        model_with_gradients(s)
+
+    P, gens = 200, 4
+    runs = []
+    for b, pg in ((0, None), (burn_in, per_gen)):
+        calls["n"] = 0
+        e = mtmcmc_experiment(P)
+        e["Problem"]["Computational Model"] = counted
+        e["Solver"]["Burn In"] = b
+        if pg is not None:
+            e["Solver"]["Per Generation Burn In"] = pg
+        e["Solver"]["Termination Criteria"]["Max Generations"] = gens
+        korali.Engine().run(e)
+        runs.append((e["Solver"], calls["n"]))
+    (s0, n0), (s1, n1) = runs
+    for k in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Leaders Gradients", "Chain Leaders Covariance",
+              "Sample Database", "Sample LogLikelihood Database", "Covariance Matrix", "Mean Theta"):
+        assert np.array_equal(np.asarray(s0[k], dtype=float), np.asarray(s1[k], dtype=float)), k
+    for k in ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", "Coefficient Of Variation",
+              "Accepted Samples Count"):
+        assert s0[k] == s1[k], k
+    extra = sum((per_gen[g - 2] if per_gen is not None and g - 2 < len(per_gen) else burn_in) for g in range(2, gens + 1))
+    assert s1["Model Evaluation Count"] - s0["Model Evaluation Count"] == extra * P
+    assert n1 - n0 >= extra * P * 0.5  # (chains with an infinite log-prior are not evaluated)
