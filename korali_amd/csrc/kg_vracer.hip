@@ -510,7 +510,9 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     // per chunk: inputs loaded and mini-batch overrides applied first (no
     // dependence on the recurrence), then the recurrence alone (4 dependent
     // float operations per entry), then the mini-batch rows' values to LDS
-    constexpr int RC = 16;
+    // (64-entry chunks: the walk is bound by the chunk's global round trip,
+    // so fewer, wider chunks; episodes are up to Max Episode Steps long)
+    constexpr int RC = 64;
     long long pc = ph(end);
     for (long long c = end; c >= start;) {
       const int n = (int)min((long long)RC, c - start + 1);
@@ -522,12 +524,12 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
         q = q == 0 ? (long long)R - 1 : q - 1;
       }
       int kk = k;
-      unsigned inmb = 0;
+      unsigned long long inmb = 0;
 #pragma unroll
       for (int j = 0; j < RC; j++)
         if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
           vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
-          inmb |= 1u << j;
+          inmb |= 1ull << j;
           while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
         }
 #pragma unroll
@@ -542,7 +544,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       if (inmb)
 #pragma unroll
         for (int j = 0; j < RC; j++)
-          if (inmb >> j & 1u) {
+          if (inmb >> j & 1ull) {
             const float before = j == 0 ? prev : rr[j - 1];
             while (k >= 0 && (long long)s_mb[k] == c - j) s_ret[k] = rr[j], s_retn[k] = before, k--;
           }

@@ -38,6 +38,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
     benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
     dprobe) step dprobe 120 python tools/discrete_probe.py ;;
+    tmt) step tmt 600 python -u -m pytest tests/test_gpu_mtmcmc.py tests/test_gpu_tmcmc.py tests/test_gpu_baseline_shapes.py -x -v --timeout 300 --timeout-method thread ;;
     occc) step occ_coll 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
     occt) step occ_torch 120 python tools/occ_probe.py exact torch ;;
     occ) step occ_exact 120 python tools/occ_probe.py exact && step occ_mfma 120 python tools/occ_probe.py mfma ;;

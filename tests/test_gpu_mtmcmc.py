@@ -93,11 +93,11 @@ def test_mtmcmc_matches_oracle_to_completion(P, seed):
 
 
 def test_mtmcmc_constraints():
-    """TMCMC.cpp.base:48-55 (+ this implementation's burn-in / sharding limits)."""
+    """TMCMC.cpp.base:48-55 (+ this implementation's sharding limit)."""
     from korali_amd.native import KoraliDeviceError, TmcmcDevice
     kw = dict(prior_min=[0.0] * 3, prior_max=[5.0] * 3, version="mTMCMC")
     for bad in (dict(max_chain_length=2), dict(step_size=-1.0), dict(domain_extension_factor=-0.1),
-                dict(default_burn_in=1)):
+                dict(shard_count=2)):
         with pytest.raises(KoraliDeviceError):
             TmcmcDevice(3, 100, **kw, **bad)
     dev = TmcmcDevice(3, 100, **kw)
