@@ -67,14 +67,23 @@ STAGE_KERNELS = {
     # C3 (TMCMC): the weighted mean / covariance stage
     "mean_cov": ["kg::k_tm_factors_mean", "kg::k_tm_wsum<false>", "kg::k_tm_factors_cov", "kg::k_tm_wsum<true>"],
 }
-PROFILE_ROUND = "r2"
+PROFILE_ROUNDS = ("r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
+
+
+def profile_file(name):
+    """(absolute path, repo-relative path) of the newest committed profiles/<round>/<name>."""
+    for r in PROFILE_ROUNDS:
+        path = os.path.join(ROOT, "profiles", r, name)
+        if os.path.exists(path):
+            return path, f"profiles/{r}/{name}"
+    return os.path.join(ROOT, "profiles", PROFILE_ROUNDS[0], name), None
 
 
 def pmc_traffic(stage, csv_name="c2_pmc_traffic.csv"):
     """HBM bytes per launch of a stage's kernels from the committed PMC passes
     (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
     import csv
-    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, csv_name)
+    path, _ = profile_file(csv_name)
     if stage not in STAGE_KERNELS or not os.path.exists(path):
         return None, None
     rows = {r["kernel"]: r for r in csv.DictReader(open(path))}
@@ -112,7 +121,7 @@ def rankmu_roofline(ms, mu, n, csv_name):
             "algorithmic_flops_per_launch": flops, "executed_flops_per_launch": executed,
             "executed_frac": executed / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
             "algorithmic_bytes_per_launch": 8.0 * (mu * n + n * n),
-            "traffic": traffic, "traffic_source": f"profiles/{PROFILE_ROUND}/{csv_name}" if traffic else None}
+            "traffic": traffic, "traffic_source": profile_file(csv_name)[1] if traffic else None}
 
 
 def cpu_model():
@@ -420,7 +429,7 @@ def main():
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_raw_fetch": traffic_raw,
-                     "traffic_source": f"profiles/{PROFILE_ROUND}/c2_pmc_traffic.csv" if traffic else None,
+                     "traffic_source": profile_file("c2_pmc_traffic.csv")[1] if traffic else None,
                      "algorithmic_flops_per_launch": flops, "avg_launch_ms": dom_ms},
     }
     if not args.no_cpu_baseline:
@@ -562,7 +571,7 @@ def run_c3(args):
                                    "round), far below it by construction",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": c3_traffic,
-                     "traffic_source": f"profiles/{PROFILE_ROUND}/c3_pmc_traffic.csv" if c3_traffic else None,
+                     "traffic_source": profile_file("c3_pmc_traffic.csv")[1] if c3_traffic else None,
                      "algorithmic_flops_per_launch": flops[dominant], "avg_launch_ms": stages[dominant]},
     }
     if not args.no_cpu_baseline:
@@ -780,7 +789,7 @@ def run_c5(args):
     finished = d.get("finished_rewards")
     # HBM bytes per rollout-GEMM launch from the committed PMC passes (tools/pmc_c5.py)
     traffic = None
-    tf = os.path.join(ROOT, "profiles", PROFILE_ROUND, "c5_pmc_traffic.csv")
+    tf = profile_file("c5_pmc_traffic.csv")[0]
     if os.path.exists(tf):
         import csv
         rows = list(csv.DictReader(open(tf)))
@@ -803,7 +812,7 @@ def run_c5(args):
         "roofline": {"kernel": "kg::vr::k_vr_gemm<1> (rollout forward, hidden layer)", "bound": "mfma",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": traffic,
-                     "traffic_source": f"profiles/{PROFILE_ROUND}/c5_pmc_traffic.csv" if traffic else None,
+                     "traffic_source": profile_file("c5_pmc_traffic.csv")[1] if traffic else None,
                      "algorithmic_flops_per_launch": gemm_flops, "avg_launch_ms": gemm_ms},
         "mean_recent_episode_reward": float(np.mean(finished[finished != 0])) if np.any(finished != 0) else None,
     }

@@ -215,7 +215,7 @@ def test_engine_mtmcmc_burn_in(burn_in, per_gen):
     (s0, n0), (s1, n1) = runs
     for k in ("Chain Leaders", "Chain Leaders LogLikelihoods", "Chain Leaders Gradients", "Chain Leaders Covariance",
               "Sample Database", "Sample LogLikelihood Database", "Covariance Matrix", "Mean Theta"):
-        assert np.array_equal(np.asarray(s0[k], dtype=float), np.asarray(s1[k], dtype=float)), k
+        assert np.array_equal(np.asarray(s0[k], dtype=float), np.asarray(s1[k], dtype=float), equal_nan=True), k
     for k in ("Annealing Exponent", "Previous Annealing Exponent", "LogEvidence", "Coefficient Of Variation",
               "Accepted Samples Count"):
         assert s0[k] == s1[k], k
