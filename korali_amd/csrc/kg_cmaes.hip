@@ -316,153 +316,6 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
   }
 }
 
-// k_transform, column-lane form (N >= 64): lane = output column d (its B row
-// streamed from L2 straight into registers), a workgroup = PR rows x up to
-// 512 columns, the PR D-scaled Z rows of a K chunk staged in LDS and read as
-// wave-uniform broadcasts.  Every Z row is fetched from HBM exactly once (one
-// workgroup holds all columns of its rows), LDS carries PR doubles per K step
-// per wave as broadcasts (the 2-D tile above moves 48 B per lane per K step
-// and is LDS-bound), and the VALU work per K step is PR multiplies + PR adds
-// per lane with PR independent accumulators.  The sum is the reference's:
-// acc = 0.0 + B[d][0] a_0 + ... in ascending e, a_e = D_e z_e rounded first,
-// separate multiply and add.  K chunks past N add -0.0 products (B = -0.0,
-// a = +0.0), which leave every accumulator unchanged (x + -0.0 = x).
-constexpr int TB_KC = 16;
-template <int PR>
-__global__ void __launch_bounds__(512) k_transform_bc(int N, int rows, const double *__restrict__ Z,
-                                                      const double *__restrict__ B, const double *__restrict__ D,
-                                                      const double *__restrict__ mean, CmaesScalars *__restrict__ sc,
-                                                      const double *__restrict__ lb, const double *__restrict__ ub,
-                                                      double *__restrict__ X, double *__restrict__ BDZ,
-                                                      int *__restrict__ infeas, int no_reserve, int mirrored) {
-  constexpr int ZP = PR + 2;  // row of a K step (16-B aligned, staggered banks)
-  constexpr int KU = PR >= 32 ? 2 : 4;  // K steps unrolled (more hoists every step's reads and spills)
-  __shared__ __attribute__((aligned(16))) double Zs[2][TB_KC][ZP];
-  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r0 = blockIdx.x * PR;
-  const int d = blockIdx.y * 512 + w * 64 + lane;
-  const bool dv = d < N;
-  const double *Bd = B + (size_t)(dv ? d : 0) * N;
-  const double sigma = sc->sigma;
-  constexpr int ZE = PR * TB_KC;  // staged elements per chunk
-  // this thread's share of a chunk's Z elements (K fastest: 128-B runs per row)
-  double zr[(ZE + 63) / 64];
-  auto loadZ = [&](int k0) {
-#pragma unroll
-    for (int u = 0; u < (ZE + 63) / 64; u++) {
-      const int q = tid + u * nt;
-      double z = 0.0;
-      if (q < ZE) {
-        const int p = q / TB_KC, e = k0 + q % TB_KC, i = r0 + p;
-        if (i < rows && e < N) {
-          z = Z[(size_t)(mirrored ? (i >> 1) : i) * N + e];
-          if (mirrored && (i & 1)) z = -z;
-          z = D[e] * z;
-        }
-      }
-      zr[u] = z;
-    }
-  };
-  auto storeZ = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < (ZE + 63) / 64; u++) {
-      const int q = tid + u * nt;
-      if (q < ZE) Zs[buf][q % TB_KC][q / TB_KC] = zr[u];
-    }
-  };
-  double bc[TB_KC];
-  auto loadB = [&](int k0) {
-    if (k0 + TB_KC <= N) {
-#pragma unroll
-      for (int kk = 0; kk < TB_KC; kk += 2) {
-        const double2 v = *(const double2 *)(Bd + k0 + kk);
-        bc[kk] = v.x, bc[kk + 1] = v.y;
-      }
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < TB_KC; kk++) bc[kk] = (k0 + kk < N) ? Bd[k0 + kk] : -0.0;
-    }
-  };
-  double acc[PR];
-#pragma unroll
-  for (int p = 0; p < PR; p++) acc[p] = 0.0;
-  const int nch = (N + TB_KC - 1) / TB_KC;
-  // (ZE may exceed nt for PR * 16 > 512: zr covers it; B row loads need 16-B alignment: N even)
-  loadZ(0);
-  storeZ(0);
-  loadB(0);
-  __syncthreads();
-  for (int c = 0; c < nch; c++) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nch;
-    double bn[TB_KC];
-#pragma unroll
-    for (int kk = 0; kk < TB_KC; kk++) bn[kk] = bc[kk];
-    if (more) {
-      loadZ((c + 1) * TB_KC);
-      loadB((c + 1) * TB_KC);
-    }
-#pragma unroll KU
-    for (int kk = 0; kk < TB_KC; kk++) {
-      const double b = bn[kk];
-      double z[PR];
-#pragma unroll
-      for (int p = 0; p < PR; p += 2) {
-        const double2 v = *(const double2 *)&Zs[buf][kk][p];
-        z[p] = v.x, z[p + 1] = v.y;
-      }
-      // products in groups of 8 before their adds (independent multiplies in flight)
-#pragma unroll
-      for (int g = 0; g < PR; g += 8) {
-        double t[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) t[u] = b * z[g + u];
-#pragma unroll
-        for (int u = 0; u < 8; u++) acc[g + u] += t[u];
-      }
-    }
-    if (more) storeZ(buf ^ 1);
-    __syncthreads();
-  }
-  const double md = dv ? mean[d] : 0.0, lbd = dv ? lb[d] : 0.0, ubd = dv ? ub[d] : 0.0;
-#pragma unroll
-  for (int p = 0; p < PR; p++) {
-    const int i = r0 + p;
-    if (i >= rows) break;  // uniform
-    bool bad = false;
-    if (dv) {
-      const double bdz = acc[p];
-      const double x = md + sigma * bdz;
-      X[(size_t)i * N + d] = x;
-      if (BDZ) BDZ[(size_t)i * N + d] = bdz;
-      bad = !isfinite(x) || x < lbd || x > ubd;
-    }
-    if (__ballot(bad) && lane == __builtin_ffsll((long long)__ballot(bad)) - 1) {
-      if (no_reserve)
-        atomicOr(&sc->errors, KG_ERR_RESAMPLE_RESERVE);
-      else
-        atomicOr(&infeas[i], 1);
-    }
-  }
-}
-
-// transform kernel choice: column-lane form for N >= 64 (rows per workgroup
-// by size), the 2-D tile below that or for the diagonal covariance;
-// KORALI_AMD_TRANSFORM = tile | bc8 | bc16 | bc32 overrides
-static int transform_form(int N, size_t rows, int diagonal) {
-  if (diagonal || N < 64 || (N & 1)) return 0;
-  if (const char *e = getenv("KORALI_AMD_TRANSFORM")) {
-    const std::string s(e);
-    if (s == "tile") return 0;
-    if (s == "bc8") return 8;
-    if (s == "bc16") return 16;
-    if (s == "bc32") return 32;
-  }
-  (void)rows;
-  return 0;
-}
-
 // resampling (prepareGeneration :443-460): candidate i takes the next block
 // whose draw is feasible, or any block once the global infeasible counter
 // reaches Max Infeasible Resamplings.  Sequential (one thread): runs only
@@ -2556,23 +2409,9 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     // 32 x 64 tiles, 4 x 2 outputs per thread: larger register tiles drop the
     // kernel to 2 waves per SIMD and measured slower at C4 (1.96 / 2.25 ms
     // for 32 x 128 / 64 x 64 against 1.73 ms)
-    const int form = transform_form(N, trows, h->cfg.diagonal_covariance);
-    if (form == 0) {
-      hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N,
-                         (int)trows, h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo,
-                         bo, h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
-    } else {
-      // blocks: row groups x 512-column slices; threads: the slice's columns in whole waves
-      const unsigned slices = (unsigned)((N + 511) / 512), waves = (unsigned)(((N < 512 ? N : 512) + 63) / 64);
-      const dim3 grid((unsigned)((trows + form - 1) / form), slices), block(64 * waves);
-#define KG_TB_LAUNCH(PR)                                                                                          \
-  hipLaunchKernelGGL((k_transform_bc<PR>), grid, block, 0, h->stream, N, (int)trows, h->Z, h->B, h->D, h->mean, \
-                     h->sc, h->lb, h->ub, xo, bo, h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0)
-      if (form == 8) KG_TB_LAUNCH(8);
-      else if (form == 32) KG_TB_LAUNCH(32);
-      else KG_TB_LAUNCH(16);
-#undef KG_TB_LAUNCH
-    }
+    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N, (int)trows,
+                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
+                       h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
     KG_HIP(hipGetLastError());
     if (h->hasDiscrete) {
       if (h->uniform.peek_uniforms(h->ubuf, h->ucap, h->stream)) return 1;

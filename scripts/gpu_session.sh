@@ -37,7 +37,6 @@ for s in ${STEPS:-smoke tests bench prof}; do
     shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
     cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
     benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
-    trab) step trab 600 python -u tools/transform_ab.py ${TRAB_ARGS:-} ;;
     pmc5) step pmc5f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc5_fetch" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline && step pmc5w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc5_write" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench5) step bench5 600 python bench.py --workload c5 ;;
     bench3) step bench3 600 python bench.py --workload c3 ;;
