@@ -801,7 +801,7 @@ def run_c5(args):
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C5: VRACER Normal policy, CartPole env (examples/learning/reinforcement/cartpole, "
-                               "RK4), 4096 concurrent environments, 2x256 tanh, mini-batch 256, EBPU 1, "
+                               "scipy dopri5 restated), 4096 concurrent environments, 2x256 tanh, mini-batch 256, EBPU 1, "
                                "replay 262144 (start 131072)", "fill_steps": filled},
         "policy_updates_per_sec": ups / elapsed, "updates": ups, "experiences": exps,
         "stage_ms": stages,
