@@ -96,7 +96,8 @@ typedef struct {
   /* "Granularity" of each variable (N, may be NULL → all 0 = continuous;
    * CMAES.cpp.base:44-50, :515-544, :834-867): samples are rounded to it,
    * discrete mutations drawn from the Uniform Generator, sigma follows the
-   * masked path length.  Not with Mirrored Sampling or sharding. */
+   * masked path length; with or without Mirrored Sampling.  Not with
+   * population sharding (shard_count > 1). */
   const double *granularity;
 } kg_cmaes_cfg;
 

@@ -39,6 +39,14 @@ struct CmaesScalars {
   double nME, nDM, chiDM;  // Number Masking Matrix Entries, Number Of Discrete Mutations, Chi Square Number DM
 };
 
+// Bound on |z| of a GSL polar normal: z = y sqrt(-2 ln r2 / r2) with |y| <=
+// sqrt(r2) and r2 >= 2^-62 (x, y are multiples of 2^-31), so |z| <=
+// sqrt(124 ln 2) = 9.27.  A draw x = m + sigma B (D o z) then satisfies |x_d|
+// <= |m|_inf + sigma * ZMAX * N * max D (|B_de| <= 1), which kg_cmaes_sample
+// compares with DBL_MAX before taking the no-redraw path.
+constexpr double KG_DRAW_ZMAX = 10.0;
+constexpr double KG_DRAW_GUARD_LIMIT = 1e300;
+
 // ----------------------------------------------------------------- init
 // setInitialConfiguration (CMAES.cpp.base:14-184), initMuWeights (:233-284),
 // initCovariance (:286-313); initial values/stds resolved on the host.
@@ -306,10 +314,11 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
       if (!isfinite(x) || x < lb[d] || x > ub[d]) bad = 1;
     }
     if (bad) {
-      // no reserve (all bounds infinite): a non-finite draw would have been
-      // redrawn by the reference loop; report instead of diverging
+      // no_reserve: all bounds infinite and the overflow guard of
+      // kg_cmaes_sample proved every draw of this generation finite, so a bad
+      // row is an internal inconsistency, not a redraw
       if (no_reserve)
-        atomicOr(&sc->errors, KG_ERR_RESAMPLE_RESERVE);
+        atomicOr(&sc->errors, KG_ERR_DRAW_GUARD);
       else
         atomicOr(&infeas[i], 1);
     }
@@ -319,71 +328,77 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
 // resampling (prepareGeneration :443-460): candidate i takes the next block
 // whose draw is feasible, or any block once the global infeasible counter
 // reaches Max Infeasible Resamplings.  Sequential (one thread): runs only
-// when some bound is finite.
-__global__ void k_select(int lam, int blocks, double maxRes, const int *__restrict__ infeas, int *__restrict__ assign,
-                         unsigned long long *__restrict__ used, CmaesScalars *sc) {
+// when some bound is finite (or the overflow guard tripped).  One ROUND
+// walks the blocks transformed so far: candidates [i0, *iEnd) are assigned;
+// when the blocks run out first, *iEnd < lam and the host transforms the
+// next blocks of the stream (kg_cmaes_sample) and walks on from *iEnd with
+// the same infeasible count, so the reference's unbounded do/while loop is
+// followed for any number of redraws.
+__global__ void k_select(int lam, int i0, int blocks, double maxRes, const int *__restrict__ infeas,
+                         int *__restrict__ assign, unsigned long long *__restrict__ used, int *__restrict__ iEnd,
+                         CmaesScalars *sc) {
   if (threadIdx.x != 0) return;
   double count = sc->infeasibleSampleCount;
-  int j = 0;
-  for (int i = 0; i < lam; i++) {
-    for (;;) {
-      if (j >= blocks) {
-        sc->errors |= KG_ERR_RESAMPLE_RESERVE;
-        assign[i] = blocks - 1;
-        break;
-      }
+  int j = 0, i = i0;
+  for (; i < lam; i++) {
+    bool taken = false;
+    while (j < blocks) {
       const int feasible = infeas[j] ? 0 : 1;
       if (!feasible) count += 1;
       const int jj = j++;
       if (feasible || !(count < maxRes)) {
         assign[i] = jj;
+        taken = true;
         break;
       }
     }
+    if (!taken) break;  // blocks exhausted: candidate i continues in the next round
   }
   sc->infeasibleSampleCount = count;
   *used = (unsigned long long)j;
+  *iEnd = i;
 }
 
 // Mirrored Sampling's resampling (:461-491): pair p takes the next block j
 // (rows 2j, 2j+1) of which either draw is feasible; each infeasible draw
-// counts
-__global__ void k_select_mirrored(int pairs, int blocks, double maxRes, const int *__restrict__ infeas,
-                                  int *__restrict__ assign, unsigned long long *__restrict__ used, CmaesScalars *sc) {
+// counts.  Rounds as in k_select (i0, *iEnd are sample indices, even).
+__global__ void k_select_mirrored(int lam, int i0, int blocks, double maxRes, const int *__restrict__ infeas,
+                                  int *__restrict__ assign, unsigned long long *__restrict__ used,
+                                  int *__restrict__ iEnd, CmaesScalars *sc) {
   if (threadIdx.x != 0) return;
   double count = sc->infeasibleSampleCount;
-  int j = 0;
-  for (int p = 0; p < pairs; p++) {
-    for (;;) {
-      if (j >= blocks) {
-        sc->errors |= KG_ERR_RESAMPLE_RESERVE;
-        assign[2 * p] = 2 * (blocks - 1);
-        assign[2 * p + 1] = 2 * (blocks - 1) + 1;
-        break;
-      }
+  int j = 0, i = i0;
+  for (; i < lam; i += 2) {
+    bool taken = false;
+    while (j < blocks) {
       const int ok1 = infeas[2 * j] ? 0 : 1;
       if (!ok1) count += 1;
       const int ok2 = infeas[2 * j + 1] ? 0 : 1;
       if (!ok2) count += 1;
       const int jj = j++;
       if (ok1 || ok2 || !(count < maxRes)) {
-        assign[2 * p] = 2 * jj;
-        assign[2 * p + 1] = 2 * jj + 1;
+        assign[i] = 2 * jj;
+        assign[i + 1] = 2 * jj + 1;
+        taken = true;
         break;
       }
     }
+    if (!taken) break;
   }
   sc->infeasibleSampleCount = count;
   *used = (unsigned long long)j;
+  *iEnd = i;
 }
 
-__global__ void k_gather_rows(int N, int lam, const int *__restrict__ assign, const double *__restrict__ Xall,
-                              double *__restrict__ X, const double *__restrict__ BDZall, double *__restrict__ BDZ) {
+// the rows a round assigned, candidates [i0, *iEnd)
+__global__ void k_gather_rows(int N, int i0, const int *__restrict__ iEnd, const int *__restrict__ assign,
+                              const double *__restrict__ Xall, double *__restrict__ X,
+                              const double *__restrict__ BDZall, double *__restrict__ BDZ) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)lam * N) return;
-  const int i = (int)(t / N), d = (int)(t % N);
-  X[t] = Xall[(size_t)assign[i] * N + d];
-  if (BDZ) BDZ[t] = BDZall[(size_t)assign[i] * N + d];
+  const int i = i0 + (int)(t / N), d = (int)(t % N);
+  if (i >= *iEnd) return;
+  X[(size_t)i * N + d] = Xall[(size_t)assign[i] * N + d];
+  if (BDZ) BDZ[(size_t)i * N + d] = BDZall[(size_t)assign[i] * N + d];
 }
 
 // ------------------------------------------------------------ objective
@@ -710,8 +725,8 @@ __global__ void __launch_bounds__(256) k_rank_sort(int lam, const double *__rest
 // (:208).  Discrete problems are small (the reference example: N = 10,
 // lambda = 8), so the O(lambda) barriers are not on a hot path.
 __device__ __forceinline__ double discretize1(double x, double g) { return g != 0.0 ? round(x / g) * g : x; }
-__global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blocks, int mirrored, double maxRes,
-                                                         const double *__restrict__ Xall,
+__global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int i0start, int blocks, int mirrored,
+                                                         double maxRes, const double *__restrict__ Xall,
                                                          const double *__restrict__ BDZall, double *__restrict__ X,
                                                          double *__restrict__ BDZ, const double *__restrict__ lb,
                                                          const double *__restrict__ ub,
@@ -719,27 +734,38 @@ __global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blo
                                                          const double *__restrict__ mask,
                                                          const double *__restrict__ best, const double *__restrict__ U,
                                                          unsigned long long ucap, unsigned long long *uUsed,
-                                                         unsigned long long *used, CmaesScalars *sc) {
+                                                         unsigned long long *used, int *__restrict__ iEnd,
+                                                         CmaesScalars *sc) {
   extern __shared__ double xs[];  // 2 N: the unit's samples (one, or a mirrored pair)
   __shared__ int infeas[2];
+  __shared__ int overflow;  // the attempt needed more peeked uniforms than U holds
   const int tid = threadIdx.x, per = mirrored ? 2 : 1;
   const double nDM = sc->nDM, nME = sc->nME;
   double count = sc->infeasibleSampleCount;
-  int j = 0;
+  int j = 0, i0 = i0start;
   unsigned long long u = 0;
   auto uni = [&]() {  // next uniform (thread 0)
     const double v = u < ucap ? U[u] : 0.0;
     u++;
     return v;
   };
-  for (int i0 = 0; i0 < lam; i0 += per) {
+  // a round ends at an attempt boundary: when the transformed blocks run out
+  // or an attempt would read past the peeked uniforms (it is then undone and
+  // redone in the next round from the stream position where it started)
+  bool stop = false, outOfUniforms = false;
+  for (; i0 < lam && !stop; i0 += per) {
     for (;;) {
-      const bool out = j >= blocks;
-      const int blk = out ? blocks - 1 : j;
+      if (j >= blocks) {
+        stop = true;
+        break;
+      }
+      const int blk = j;
+      const unsigned long long u0 = u;
       for (int q = tid; q < per * N; q += blockDim.x) xs[q] = Xall[((size_t)blk * per) * N + q];
       if (tid < 2) infeas[tid] = 0;
+      if (tid == 0) overflow = 0;
       __syncthreads();
-      if (tid == 0)
+      if (tid == 0) {
         for (int s = 0; s < per; s++) {  // sampleSingle(i0 + s) in order (:472-473)
           const int i = i0 + s;
           double *x = xs + (size_t)s * N;
@@ -759,7 +785,16 @@ __global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blo
               if (gran[d] != 0.0) x[d] += round(best[d] / gran[d]) * gran[d] - x[d];
           }
         }
+        if (u > ucap) {
+          overflow = 1;
+          u = u0;
+        }
+      }
       __syncthreads();
+      if (overflow) {
+        stop = outOfUniforms = true;
+        break;
+      }
       for (int q = tid; q < per * N; q += blockDim.x) {
         const int d = q % N;
         const double x = discretize1(xs[q], gran[d]);
@@ -767,20 +802,13 @@ __global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blo
         if (!isfinite(x) || x < lb[d] || x > ub[d]) infeas[q / N] = 1;  // (benign race: every writer stores 1)
       }
       __syncthreads();
-      bool accept;
-      if (out) {
-        if (tid == 0) sc->errors |= KG_ERR_RESAMPLE_RESERVE;
-        accept = true;
-      } else {
-        bool anyOk = false;
-        for (int s = 0; s < per; s++) {
-          if (infeas[s]) count += 1;
-          else anyOk = true;
-        }
-        j++;
-        accept = anyOk || !(count < maxRes);
+      bool anyOk = false;
+      for (int s = 0; s < per; s++) {
+        if (infeas[s]) count += 1;
+        else anyOk = true;
       }
-      if (accept) {
+      j++;
+      if (anyOk || !(count < maxRes)) {
         for (int q = tid; q < per * N; q += blockDim.x) {
           const int d = q % N;
           X[(size_t)i0 * N + q] = discretize1(xs[q], gran[d]);  // :208 before evaluation
@@ -791,12 +819,14 @@ __global__ void __launch_bounds__(256) k_discrete_select(int N, int lam, int blo
       }
       __syncthreads();
     }
+    if (stop) break;
   }
   if (tid == 0) {
     sc->infeasibleSampleCount = count;
     *used = (unsigned long long)j;
-    if (u > ucap) sc->errors |= KG_ERR_RNG_UNDERRUN;
-    *uUsed = u < ucap ? u : ucap;
+    *uUsed = u;
+    iEnd[0] = i0 < lam ? i0 : lam;
+    iEnd[1] = outOfUniforms ? 1 : 0;  // the host peeks a larger window before the next round
   }
 }
 
@@ -1817,6 +1847,10 @@ __global__ void __launch_bounds__(256) k_shard_finalize(int N, const double *__r
 // (engine.cpp CmaesModule::checkTermination), in one host-coherent record
 struct TermSummary {
   double f[KG_TERMINATION_FIELDS];
+  // overflow guard of the next draw (kg_cmaes_sample): |m|_inf + sigma * ZMAX
+  // * N * sqrt(a bound on the next axis lengths' max square); NaN if any
+  // input is not finite
+  double guard;
   unsigned int errors, pad;
   unsigned long long seq;  // written last (system-scope release)
 };
@@ -1825,13 +1859,15 @@ namespace kg {
 // (the same publication protocol as kg_eigen.hip k_publish_dsd: relaxed
 // system-scope stores of the payload, release fence, release store of seq)
 __device__ void summary_store(const CmaesScalars *sc, const StreamState *a, const StreamState *b, TermSummary *out,
-                              unsigned long long seq) {
+                              unsigned long long seq, double guard) {
   const double f[KG_TERMINATION_FIELDS] = {sc->modelEvaluationCount, sc->infeasibleSampleCount, sc->maxEig,
                                            sc->minEig, sc->currentMinStd, sc->currentMaxStd, sc->bestEverValue,
                                            sc->currentBestValue, sc->previousBestValue};
   for (int i = 0; i < KG_TERMINATION_FIELDS; i++)
     __hip_atomic_store((unsigned long long *)&out->f[i], (unsigned long long)__double_as_longlong(f[i]),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((unsigned long long *)&out->guard, (unsigned long long)__double_as_longlong(guard),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&out->errors, sc->errors | a->errors | b->errors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __atomic_thread_fence(__ATOMIC_RELEASE);
   __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1843,10 +1879,10 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
                                                const double *__restrict__ minStdUpdate, CmaesScalars *sc,
                                                const StreamState *stA, const StreamState *stB, TermSummary *out,
                                                unsigned long long seq, const double *__restrict__ maskSigma,
-                                               const double *__restrict__ ps) {
+                                               const double *__restrict__ ps, const double *__restrict__ mean) {
   __shared__ double ssig;
   __shared__ int viol;
-  __shared__ double red[4][4];
+  __shared__ double red[4][6];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) {
     const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
@@ -1879,6 +1915,8 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
   __syncthreads();
   const double sigma = ssig;
   double mxd = -INFINITY, mnd = INFINITY, mns = INFINITY, mxs = -INFINITY;
+  // overflow guard inputs: |m|_inf and the trace of C (NaN-propagating sums)
+  double mabs = 0.0, tr = 0.0;
   for (int d = tid; d < N; d += blockDim.x) {
     const double cdd = C[(size_t)d * N + d];
     mxd = fmax(mxd, cdd);
@@ -1886,18 +1924,24 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
     const double s = sigma * sqrt(cdd);
     mns = fmin(mns, s);
     mxs = fmax(mxs, s);
+    mabs += fabs(mean[d]);
+    tr += fabs(cdd);
   }
   for (int off = 32; off > 0; off >>= 1) {
     mxd = fmax(mxd, __shfl_xor(mxd, off, 64));
     mnd = fmin(mnd, __shfl_xor(mnd, off, 64));
     mns = fmin(mns, __shfl_xor(mns, off, 64));
     mxs = fmax(mxs, __shfl_xor(mxs, off, 64));
+    mabs += __shfl_xor(mabs, off, 64);
+    tr += __shfl_xor(tr, off, 64);
   }
   if (lane == 0) {
     red[wid][0] = mxd;
     red[wid][1] = mnd;
     red[wid][2] = mns;
     red[wid][3] = mxs;
+    red[wid][4] = mabs;
+    red[wid][5] = tr;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1906,13 +1950,20 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
       mnd = fmin(mnd, red[w][1]);
       mns = fmin(mns, red[w][2]);
       mxs = fmax(mxs, red[w][3]);
+      mabs += red[w][4];
+      tr += red[w][5];
     }
     sc->maxDiagC = mxd;
     sc->minDiagC = mnd;
     sc->sigma = sigma;
     sc->currentMinStd = mns;
     sc->currentMaxStd = mxs;
-    summary_store(sc, stA, stB, out, seq);
+    // next draw: the axis lengths come from C's eigenvalues (each <= trace
+    // for the PSD update, 1% slack for rounding) or stay the current ones
+    // (a rejected decomposition keeps them, max square = maxEig)
+    const double d2 = fmax(1.01 * tr, sc->maxEig);
+    const double guard = mabs + sigma * KG_DRAW_ZMAX * (double)N * sqrt(d2);
+    summary_store(sc, stA, stB, out, seq, (isfinite(mabs) && isfinite(tr) && isfinite(sigma) && isfinite(sc->maxEig)) ? guard : NAN);
   }
 }
 
@@ -1946,7 +1997,12 @@ struct kg_cmaes_s {
   double *Yc = nullptr, *Tt = nullptr;  // exact rank-mu factors (k_rankmu_prep)
   EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
+  int *selEnd = nullptr;  // a resampling round's end: [next unassigned sample, uniform window exhausted]
   unsigned long long *blockEnd = nullptr, *usedBlocks = nullptr;
+  // state set by the caller (initialize, set_field) since the last update:
+  // the termination record's overflow guard does not describe it
+  bool stateDirty = true;
+  size_t resamplingRounds = 0;  // rounds beyond the first (diagnostics: "Resampling Rounds")
   bool mirrored = false;  // "Mirrored Sampling": blocks of N normals feed two rows
   double *G = nullptr;    // samples' gradients (use_gradients)
   // discrete variables: Granularity, Masking Matrix (Sigma), the peeked
@@ -2055,7 +2111,7 @@ int check_errors(kg_cmaes_s *h) {
   std::string m = "korali_amd CMA-ES device error:";
   if (e & KG_ERR_NONFINITE_F) m += " Non finite value of function evaluation detected.";
   if (e & KG_ERR_RNG_UNDERRUN) m += " RNG stream underrun.";
-  if (e & KG_ERR_RESAMPLE_RESERVE) m += " Infeasible samples exceeded the device resampling reserve.";
+  if (e & KG_ERR_DRAW_GUARD) m += " A draw the overflow guard proved finite was not (internal error).";
   if (e & KG_ERR_ZERO_LIST) m += " Too many zero mt19937 words pending.";
   if (e & KG_ERR_EIGEN) m += " Eigen decomposition did not converge.";
   if (e & KG_ERR_SYNC_TIMEOUT) m += " An in-launch workgroup hand-off timed out.";
@@ -2231,6 +2287,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->mu * N) | dalloc(&h->Tt, (size_t)h->mu * N);
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
   rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
+  rc |= dalloc(&h->selEnd, 2);
   if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
   if (cfg->use_gradients) rc |= dalloc(&h->G, (size_t)L * N);
   rc |= dalloc(&h->gran, N) | dalloc(&h->mask, N) | dalloc(&h->maskSigma, N);
@@ -2262,20 +2319,16 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   }
   memset(h->summary, 0, sizeof(TermSummary));
   if (L <= RANK_MAX && (size_t)L * sizeof(double) > 64 * 1024)
-    KG_HIP(hipFuncSetAttribute((const void *)k_rank_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)((size_t)L * sizeof(double))));
+    KG_HIP(allow_dynamic_lds((const void *)k_rank_sort, (int)((size_t)L * sizeof(double))));
   {
     const size_t pbytes = ((size_t)N * (PA_EC + 1) + N) * sizeof(double);
     if (pbytes > 64 * 1024)
-      KG_HIP(hipFuncSetAttribute((const void *)k_paths, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pbytes));
-    KG_HIP(hipFuncSetAttribute((const void *)k_mean2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)mean2_lds_bytes()));
+      KG_HIP(allow_dynamic_lds((const void *)k_paths, (int)pbytes));
+    KG_HIP(allow_dynamic_lds((const void *)k_mean2, (int)mean2_lds_bytes()));
     if (N <= 128)
-      KG_HIP(hipFuncSetAttribute((const void *)k_objective2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)ob2_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_objective2, (int)ob2_lds_bytes(N)));
     if (N <= 128)
-      KG_HIP(hipFuncSetAttribute((const void *)k_paths2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)paths2_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_paths2, (int)paths2_lds_bytes(N)));
   }
   if (rc) {
     delete h;
@@ -2334,7 +2387,8 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->sc, (void *)h->covPart, (void *)h->infeas,
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y, (void *)h->Yc, (void *)h->Tt,
                   (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G,
-                  (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused})
+                  (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused,
+                  (void *)h->selEnd})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -2353,6 +2407,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
 
 int kg_cmaes_initialize(kg_cmaes_t h) {
   Stage st(h, "init");
+  h->stateDirty = true;
   hipLaunchKernelGGL(k_init, dim3(1), dim3(256), 0, h->stream, h->N, h->lam, h->mu, h->cfg.mu_type,
                      h->cfg.initial_sigma_cumulation_factor, h->cfg.initial_damp_factor,
                      h->cfg.initial_cumulative_covariance, h->iv, h->istd, h->w, h->C, h->B, h->D, h->mean,
@@ -2390,9 +2445,146 @@ int kg_cmaes_begin_sample(kg_cmaes_t h) {
   return 0;
 }
 
-int kg_cmaes_sample(kg_cmaes_t h) {
+// Overflow guard of a generation without finite bounds (and no discrete
+// variables): the reference redraws a sample only when it is not finite
+// (optimizer.cpp.base:5-14), which needs |m| + sigma |B (D o z)| to overflow.
+// *finite = every draw of this generation is provably finite (|z| <=
+// KG_DRAW_ZMAX), so the population is the first lambda blocks of the stream.
+// The bound comes from the last update's termination record (host-coherent,
+// already written when the host chase returns) or, when the caller set the
+// state since (initialize, set_field), from the state itself.
+static int draw_guard(kg_cmaes_t h, bool *finite, bool *stateFinite = nullptr) {
+  double G = NAN;
+  if (!stateFinite && !h->stateDirty && h->updates > 0) {
+    const unsigned long long want = h->updates;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) < want) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+        KG_HIP(hipStreamSynchronize(h->stream));
+        if (check_errors(h)) return 1;
+        KG_CHECK(false, "termination summary never arrived");
+      }
+    }
+    G = h->summary->guard;
+  } else {
+    const int N = h->N;
+    std::vector<double> m(N), D(N);
+    double sigma = 0.0;
+    KG_HIP(hipMemcpyAsync(m.data(), h->mean, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipMemcpyAsync(D.data(), h->D, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipMemcpyAsync(&sigma, &h->sc->sigma, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    double ma = 0.0, dm = 0.0;
+    bool ok = std::isfinite(sigma);
+    for (int d = 0; d < N; d++) {
+      ok = ok && std::isfinite(m[d]) && std::isfinite(D[d]);
+      ma += std::fabs(m[d]);
+      dm = std::max(dm, std::fabs(D[d]));
+    }
+    if (ok) G = ma + sigma * KG_DRAW_ZMAX * (double)N * dm;
+    if (stateFinite) *stateFinite = ok;
+  }
+  *finite = G < KG_DRAW_GUARD_LIMIT;  // false for NaN
+  return 0;
+}
+
+// buffers of the redraw path for a handle created without a reserve
+static int ensure_redraw_buffers(kg_cmaes_t h) {
+  if (h->Xall) return 0;
+  const size_t xrows = h->mirrored ? 2 * h->blocks : h->blocks;
+  if (dalloc(&h->Xall, xrows * h->N)) return 1;
+  if (h->cfg.store_bdz && dalloc(&h->BDZall, xrows * h->N)) return 1;
+  return 0;
+}
+
+// prepareGeneration's redraw loops (CMAES.cpp.base:443-491) in rounds: each
+// round transforms the next `blocks` blocks of the Normal stream (the first
+// round's were drawn beside the eigensolver), walks them in the reference's
+// order from the first unassigned sample, and consumes exactly the blocks the
+// walk used.  When a round runs out of blocks, the next one continues the
+// stream where it stopped, so any number of infeasible draws is followed.
+static int cmaes_resample(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
-  const size_t rows = h->mirrored ? 2 * h->blocks : (size_t)L + h->R;  // transformed rows
+  const size_t nb = h->blocks, xr = h->mirrored ? 2 * nb : nb;
+  const unsigned tgrid = tr_grid<32, 64>((int)xr, N);
+  int i0 = 0;
+  for (int round = 0;; round++) {
+    if (round > 0) {
+      h->resamplingRounds++;
+      Stage st(h, "rng_polar");
+      if (h->normal.polar_normals(h->Z, nb * N, N, h->blockEnd, h->stream)) return 1;
+    }
+    {
+      Stage st(h, "transform");
+      KG_HIP(hipMemsetAsync(h->infeas, 0, xr * sizeof(int), h->stream));
+      hipLaunchKernelGGL((k_transform<32, 64>), dim3(tgrid), dim3(256), 0, h->stream, N, (int)xr,
+                         h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, h->Xall,
+                         h->BDZall, h->infeas, 0, h->mirrored ? 1 : 0);
+      KG_HIP(hipGetLastError());
+      if (h->hasDiscrete) {
+        if (h->uniform.peek_uniforms(h->ubuf, h->ucap, h->stream)) return 1;
+        hipLaunchKernelGGL(k_discrete_select, dim3(1), dim3(256), 2 * N * sizeof(double), h->stream, N, L, i0, (int)nb,
+                           h->mirrored ? 1 : 0, h->cfg.max_infeasible_resamplings, h->Xall, h->BDZall, h->X, h->BDZ,
+                           h->lb, h->ub, h->gran, h->mask, h->bestEverVars, h->ubuf, (unsigned long long)h->ucap,
+                           h->uused, h->usedBlocks, h->selEnd, h->sc);
+        KG_HIP(hipGetLastError());
+        if (h->uniform.consume_words_dev(h->uused, h->stream)) return 1;
+      } else {
+        if (h->mirrored)
+          hipLaunchKernelGGL(k_select_mirrored, dim3(1), dim3(64), 0, h->stream, L, i0, (int)nb,
+                             h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->selEnd, h->sc);
+        else
+          hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, i0, (int)nb,
+                             h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->selEnd, h->sc);
+        KG_HIP(hipGetLastError());
+        const size_t tot = (size_t)(L - i0) * N;
+        hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, i0,
+                           (const int *)h->selEnd, h->assign, h->Xall, h->X, h->BDZall, h->BDZ);
+        KG_HIP(hipGetLastError());
+      }
+    }
+    {
+      Stage st(h, "rng_consume");
+      if (h->normal.consume_normals_dev(h->usedBlocks, N, h->blockEnd, h->stream)) return 1;
+    }
+    int se[2] = {0, 0};
+    KG_HIP(hipMemcpyAsync(se, h->selEnd, sizeof(se), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    if (se[0] >= L) break;
+    if (se[0] == i0) {
+      // a round without progress: either the peeked uniforms were too few
+      // for one attempt (discrete mutations), or no draw of a whole round
+      // was feasible.  The reference keeps redrawing; a distribution that is
+      // not finite would make it redraw forever, which is reported instead.
+      if (se[1]) {
+        const size_t cap = 2 * h->ucap;
+        KG_CHECK(cap + 4096 <= h->uniform.capacity_words() / 2,
+                 "discrete mutations need more uniforms per sample than the device window holds");
+        double *nb2 = nullptr;
+        if (dalloc(&nb2, cap)) return 1;
+        (void)hipFree(h->ubuf);
+        h->ubuf = nb2;
+        h->ucap = cap;
+      } else {
+        bool fin = false, stateFinite = false;
+        if (draw_guard(h, &fin, &stateFinite)) return 1;
+        KG_CHECK(stateFinite, "the sampling distribution (mean, sigma, axis lengths) is not finite: every draw is "
+                              "infeasible and the reference would redraw forever");
+      }
+    }
+    i0 = se[0];
+  }
+  if (!h->R) {
+    // a handle without a reserve consumes exactly its lambda blocks otherwise
+    const unsigned long long used = (unsigned long long)nb;
+    KG_HIP(hipMemcpyAsync(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice, h->stream));
+  }
+  return 0;
+}
+
+int kg_cmaes_sample(kg_cmaes_t h) {
+  const int N = h->N;
   if (!h->sampleBegun && cmaes_draw_begin(h)) return 1;
   h->sampleBegun = false;
   if (cmaes_eigen(h)) return 1;
@@ -2400,38 +2592,31 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     Stage st(h, "rng_polar");  // what of the producer + polar pass the eigensolver did not hide
     if (h->normal.join(h->stream)) return 1;
   }
+  bool redraw = h->R > 0;
+  if (!redraw) {
+    bool finite = false;
+    if (draw_guard(h, &finite)) return 1;
+    if (!finite) {
+      KG_CHECK(h->shards == 1,
+               "a population-sharded handle cannot redraw non-finite samples (overflow guard tripped)");
+      if (ensure_redraw_buffers(h)) return 1;
+      redraw = true;
+    }
+  }
+  if (redraw) return cmaes_resample(h);
   {
     Stage st(h, "transform");
-    if (h->R) KG_HIP(hipMemsetAsync(h->infeas, 0, rows * sizeof(int), h->stream));
-    const size_t trows = h->R ? rows : (size_t)(h->r1 - h->r0);  // a shard transforms its own rows only
-    double *xo = h->R ? h->Xall : h->X + (size_t)h->r0 * N;
-    double *bo = h->R ? h->BDZall : (h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr);
+    // no redraw possible: the population is the first lambda blocks; a shard
+    // transforms its own rows only
+    const size_t trows = (size_t)(h->r1 - h->r0);
+    double *xo = h->X + (size_t)h->r0 * N;
+    double *bo = h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr;
     // 32 x 64 tiles, 4 x 2 outputs per thread: larger register tiles drop the
     // kernel to 2 waves per SIMD and measured slower at C4 (1.96 / 2.25 ms
     // for 32 x 128 / 64 x 64 against 1.73 ms)
-    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N, (int)trows,
-                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
-                       h->infeas, h->R ? 0 : 1, h->mirrored ? 1 : 0);
-    KG_HIP(hipGetLastError());
-    if (h->hasDiscrete) {
-      if (h->uniform.peek_uniforms(h->ubuf, h->ucap, h->stream)) return 1;
-      hipLaunchKernelGGL(k_discrete_select, dim3(1), dim3(256), 2 * N * sizeof(double), h->stream, N, L,
-                         (int)h->blocks, h->mirrored ? 1 : 0, h->cfg.max_infeasible_resamplings, h->Xall, h->BDZall, h->X, h->BDZ, h->lb, h->ub, h->gran,
-                         h->mask, h->bestEverVars, h->ubuf, (unsigned long long)h->ucap, h->uused, h->usedBlocks,
-                         h->sc);
-      KG_HIP(hipGetLastError());
-      if (h->uniform.consume_words_dev(h->uused, h->stream)) return 1;
-    } else if (h->R) {
-      if (h->mirrored)
-        hipLaunchKernelGGL(k_select_mirrored, dim3(1), dim3(64), 0, h->stream, L / 2, (int)h->blocks,
-                           h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->sc);
-      else
-        hipLaunchKernelGGL(k_select, dim3(1), dim3(64), 0, h->stream, L, (int)rows, h->cfg.max_infeasible_resamplings,
-                           h->infeas, h->assign, h->usedBlocks, h->sc);
-      const size_t tot = (size_t)L * N;
-      hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, L, h->assign,
-                         h->Xall, h->X, h->BDZall, h->BDZ);
-    }
+    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N,
+                       (int)trows, h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
+                       h->infeas, 1, h->mirrored ? 1 : 0);
     KG_HIP(hipGetLastError());
   }
   {
@@ -2525,7 +2710,8 @@ static int cmaes_sigma(kg_cmaes_t h) {
                          h->maskSigma, h->sc);
     hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
                        h->minstd, h->sc, h->normal.state(), h->uniform.state(), h->summaryDev, ++h->updates,
-                       h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps);
+                       h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps, h->mean);
+    h->stateDirty = false;  // the record's guard describes the next draw
     KG_HIP(hipGetLastError());
   }
   return 0;
@@ -2733,6 +2919,7 @@ int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t 
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
+  h->stateDirty = true;
   return 0;
 }
 

@@ -12,6 +12,9 @@
 // multiply-adds are the explicit fma() calls of the exact two-product.
 #pragma once
 
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -55,6 +58,23 @@ inline int zero_fill(void *p, size_t bytes) {
   return 0;
 }
 
+// hipFuncAttributeMaxDynamicSharedMemorySize is per kernel and process-wide,
+// while handles of different sizes need different amounts: the attribute only
+// ever grows here (the largest request any handle made).  Round 3 set it per
+// handle, so a smaller handle created after a larger one lowered it below the
+// larger one's launches, and the runtime's occupancy query then answered 0
+// blocks per CU for them (the "occupancy anomaly" of the full pytest process).
+inline hipError_t allow_dynamic_lds(const void *f, size_t bytes) {
+  static std::mutex mtx;
+  static std::map<const void *, size_t> cur;
+  std::lock_guard<std::mutex> lock(mtx);
+  size_t &c = cur[f];
+  if (bytes <= c) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) c = bytes;
+  return e;
+}
+
 // Grids whose workgroups wait on one another inside the launch (spin
 // hand-offs) go through launch_resident: a cooperative launch, so HIP
 // guarantees co-residency or fails the launch.  KORALI_AMD_PLAIN_LAUNCH=1
@@ -63,19 +83,16 @@ inline int zero_fill(void *p, size_t bytes) {
 // output, in any process that made a cooperative launch, so profile runs set
 // it (scripts/gpu_prof.sh).
 //
-// prefer_plain: a small grid launched every generation on the handle's
-// stream (the streamed Givens apply, 33 workgroups at N = 128).  ROCm runs
-// cooperative launches on a queue of their own, and the hand-over to and
-// from it cost 12-15 us on each side of the launch (kernel trace, round 3);
-// a plain launch after the same capacity check stays on the stream's queue.
-// The grid is co-resident once dispatched: it fits the device's capacity,
-// and no kernel holds CUs indefinitely (at worst the spinning workgroups
-// wait until a concurrent kernel's workgroups retire).
-// Workgroups per CU the kernel's own resources allow (VGPRs of the unified
-// 512-entry file per SIMD lane, at most 8 waves per SIMD, 160 KB of LDS).
-// In some processes (a pytest run that has imported every test module) the
-// runtime's occupancy query returned 0 for grids that fit and run
-// elsewhere; resident_per_cu takes the larger of the two answers.
+// prefer_plain: a grid whose waiting workgroups depend only on a workgroup
+// dispatched before them (the streamed Givens apply: every row workgroup
+// waits on the fetcher, workgroup 0), launched every generation on the
+// handle's stream.  ROCm runs cooperative launches on a queue of their own,
+// and the hand-over to and from it cost 12-15 us on each side of the launch
+// (kernel trace, round 3); a plain launch stays on the stream's queue.
+//
+// The capacity is the runtime's occupancy answer; the kernel's own VGPR / LDS
+// arithmetic (own_blocks_per_cu) can only lower it (it ignores AGPR / SGPR
+// limits, so it never allows a launch the runtime would not).
 inline int own_blocks_per_cu(const void *f, int threads, size_t lds) {
   hipFuncAttributes a{};
   if (hipFuncGetAttributes(&a, f) != hipSuccess) return 0;
@@ -92,7 +109,14 @@ inline hipError_t resident_per_cu(const void *f, int threads, size_t lds, int *p
   int rt = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&rt, f, threads, lds);
   if (e != hipSuccess) return e;
-  *per = std::max(rt, own_blocks_per_cu(f, threads, lds));
+  const int own = own_blocks_per_cu(f, threads, lds);
+  if (getenv("KORALI_AMD_DEBUG_OCC")) {
+    hipFuncAttributes a{};
+    (void)hipFuncGetAttributes(&a, f);
+    fprintf(stderr, "[korali_amd occ] f=%p threads=%d dyn_lds=%zu static_lds=%zu max_dyn=%d vgpr=%d runtime=%d own=%d\n",
+            f, threads, lds, (size_t)a.sharedSizeBytes, a.maxDynamicSharedSizeBytes, a.numRegs, rt, own);
+  }
+  *per = std::min(rt, own);
   if (runtimePer) *runtimePer = rt;
   return hipSuccess;
 }
@@ -107,19 +131,8 @@ inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **a
     const char *e = getenv("KORALI_AMD_COOP_LAUNCH");  // every resident grid cooperative (A/B)
     return e && *e && *e != '0';
   }();
-  bool plain = plain_env || (prefer_plain && !coop_env);
-  if (!plain) {
-    // the runtime refuses a cooperative launch its occupancy query rejects:
-    // where that query is wrong (see resident_per_cu), launch plain after
-    // the capacity check below
-    int dev = 0, cus = 0, per = 0, rt = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        resident_per_cu(f, (int)(block.x * block.y * block.z), lds, &per, &rt) == hipSuccess &&
-        (long long)rt * cus < (long long)grid.x * grid.y * grid.z)
-      plain = true;
-    if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
-  }
+  const bool plain = plain_env || (prefer_plain && !coop_env);
+  if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
   int dev = 0, cus = 0, per = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -134,7 +147,7 @@ inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **a
 enum : uint32_t {
   KG_ERR_NONFINITE_F = 1u << 0,     // optimization.cpp.base:32-33
   KG_ERR_RNG_UNDERRUN = 1u << 1,    // producer did not generate enough words
-  KG_ERR_RESAMPLE_RESERVE = 1u << 2,// more infeasible draws than the reserve
+  KG_ERR_DRAW_GUARD = 1u << 2,      // a draw the overflow guard proved finite was not (internal)
   KG_ERR_ZERO_LIST = 1u << 3,       // > KG_MAX_ZERO_WORDS zero MT words pending
   KG_ERR_EIGEN = 1u << 4,           // QR iteration did not converge
   KG_ERR_CHOLESKY = 1u << 5,        // covariance not positive definite

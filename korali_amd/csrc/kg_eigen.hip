@@ -2534,7 +2534,12 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   const int tid = threadIdx.x, lda = N + 1;
   constexpr int APPLY_ROWS = ApplyGeom<TEAM>::ROWS, APPLY_TEAM = TEAM;
   const int S = APPLY_ROWS + 1;                  // Lq[c * S + kl] = Q[k0 + kl][c]
-  const int k0 = blockIdx.x * APPLY_ROWS;
+  // kStream: workgroup 0 is the fetcher and row block rb = blockIdx - 1.  A
+  // plain launch dispatches workgroups in order, so the fetcher every row
+  // workgroup waits on is always already running: the grid needs no
+  // co-residency, even when other processes share the device.
+  const int rb = kStream ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+  const int k0 = rb * APPLY_ROWS;
   const int nrows = min(APPLY_ROWS, N - k0);
   double *Lq = smem;
   const int cap = apply_cap(N, APPLY_ROWS);
@@ -2542,12 +2547,12 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
   int *hsh = (int *)(csh + 2 * (size_t)cap);      // APPLY_HCAP (a, nb)
   int *chunk = hsh + 2 * APPLY_HCAP;
   double *dummy = (double *)(chunk + 4) + threadIdx.x;  // stores of lanes with nothing to store
-  if (kStream && blockIdx.x == gridDim.x - 1) {  // the extra workgroup: fetcher
+  if (kStream && blockIdx.x == 0) {  // the extra workgroup: fetcher
     apply_fetcher(N, hr, r, hprog, prog, seq, errors, chunk);
     return;
   }
   if (!kStream && r.meta[2]) {
-    if (tid == 0 && blockIdx.x == 0) atomicOr(errors, KG_ERR_EIGEN);
+    if (tid == 0 && rb == 0) atomicOr(errors, KG_ERR_EIGEN);
     return;
   }
   for (int idx = tid; idx < N * APPLY_ROWS; idx += APPLY_TPB) {
@@ -2759,7 +2764,7 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     t0 += tn;
     ro0 += nrot;
   }
-  if (trace && tid == 0 && blockIdx.x == 0) {
+  if (trace && tid == 0 && rb == 0) {
     trace[4] += ngroups;
     trace[5] += nunits;
     trace[6] += t0;
@@ -2769,7 +2774,7 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     trace[28] += tfirst;                          // ticks from kernel start to the first batch
   }
   if (kStream && ld_agt(r.meta + 2)) {  // the chase failed after streaming part of its steps
-    if (tid == 0 && blockIdx.x == 0) atomicOr(errors, KG_ERR_EIGEN);
+    if (tid == 0 && rb == 0) atomicOr(errors, KG_ERR_EIGEN);
     return;
   }
   // updateEigensystem: min/max eigenvalue; keep old B, D if min <= 0
@@ -2786,14 +2791,14 @@ __global__ void __launch_bounds__(APPLY_TPB) k_apply(int N, const double *__rest
     mx = fmax(mx, evs[i]);
   }
   if (mn <= 0.0) {
-    if (tid == 0 && blockIdx.x == 0) *eigenFailures += 1.0;
+    if (tid == 0 && rb == 0) *eigenFailures += 1.0;
     return;
   }
   for (int idx = tid; idx < nrows * N; idx += APPLY_TPB) {
     const int kk = idx / N, e = idx % N;
     B[(size_t)(k0 + kk) * N + e] = Lq[(size_t)pms[e] * S + kk];
   }
-  if (blockIdx.x == 0) {
+  if (rb == 0) {
     for (int i = tid; i < N; i += APPLY_TPB) D[i] = sqrt(evs[i]);
     if (tid == 0) {
       *minEig = mn;
@@ -2923,14 +2928,11 @@ int EigenSolver::init(int N_, bool hostChase_) {
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
   if (tri == 1)
-    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(t1_lds_doubles(N) * sizeof(double))));
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_1wg, (int)(t1_lds_doubles(N) * sizeof(double))));
   if (tri == 4)
-    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_sq, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(sq_lds_doubles(N) * sizeof(double))));
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_sq, (int)(sq_lds_doubles(N) * sizeof(double))));
   if (tri == 3)
-    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_1wg2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(t2_lds_doubles(N) * sizeof(double))));
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_1wg2, (int)(t2_lds_doubles(N) * sizeof(double))));
   if (tri == 5) {
     // the workgroups hand data to each other inside the launch: they must be
     // co-resident, which a cooperative launch guarantees (or refuses).  With
@@ -2942,8 +2944,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
     for (int rw = (N + 255) / 256; rw <= N; rw++) {
       g_mw2_rw[N] = rw;
       if (!mw2_fits(N) || mw2_rows(N) != rw) break;  // LDS exhausted (or rows forced by the environment)
-      KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)mw2_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw2, (int)mw2_lds_bytes(N)));
       KG_HIP(resident_per_cu((const void *)k_tridiag_mw2, MW2_TPB, mw2_lds_bytes(N), &perCU, nullptr));
       if (getenv("KORALI_AMD_DEBUG_OCC"))
         fprintf(stderr, "[korali_amd] mw2 N=%d rows=%d groups=%d lds=%zu perCU=%d cus=%d\n", N, rw, mw2_groups(N),
@@ -2957,29 +2958,21 @@ int EigenSolver::init(int N_, bool hostChase_) {
   }
   if (!lds || tri == 2 || tri == 5) {
     KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
-    KG_HIP(hipFuncSetAttribute((const void *)k_tridiag_mw, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)tmw_lds_bytes(N)));
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw, (int)tmw_lds_bytes(N)));
     if (uwv_fits(N))
-      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_wv, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)uwv_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_unpack_wv, (int)uwv_lds_bytes(N)));
     if (umw_all_fits(N))
-      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)(umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double))));
+      KG_HIP(allow_dynamic_lds((const void *)k_unpack_mw<true>, (int)(umw_lds_bytes(N) + umw_hall_doubles(N) * sizeof(double))));
     else
-      KG_HIP(hipFuncSetAttribute((const void *)k_unpack_mw<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)umw_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_unpack_mw<false>, (int)umw_lds_bytes(N)));
   }
   const int attr = 160 * 1024;
-  KG_HIP(hipFuncSetAttribute((const void *)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
-  KG_HIP(hipFuncSetAttribute((const void *)k_unpack<true>, hipFuncAttributeMaxDynamicSharedMemorySize, attr));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N, 4)));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N, 4)));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<false, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N, 16)));
-  KG_HIP(hipFuncSetAttribute((const void *)k_apply<true, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)apply_lds_bytes(N, 16)));
+  KG_HIP(allow_dynamic_lds((const void *)k_tridiag<true>, attr));
+  KG_HIP(allow_dynamic_lds((const void *)k_unpack<true>, attr));
+  KG_HIP(allow_dynamic_lds((const void *)k_apply<false, 64>, (int)apply_lds_bytes(N, 4)));
+  KG_HIP(allow_dynamic_lds((const void *)k_apply<true, 64>, (int)apply_lds_bytes(N, 4)));
+  KG_HIP(allow_dynamic_lds((const void *)k_apply<false, 16>, (int)apply_lds_bytes(N, 16)));
+  KG_HIP(allow_dynamic_lds((const void *)k_apply<true, 16>, (int)apply_lds_bytes(N, 16)));
   return 0;
 }
 
@@ -3094,10 +3087,10 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     const unsigned long long seq = ++chaseSeq;
     if (prof) prof(profCtx, "eigen_apply", 0);
     EigRec mr = hmap;
-    // one workgroup per 4 rows (16 with 16-lane teams) + the fetcher
-    // workgroup; the row workgroups spin on the fetcher's progress word, so
-    // the grid must be co-resident: launch_resident checks the device's
-    // capacity (or fails) and launches it on this stream (see kg_common.hpp)
+    // the fetcher workgroup (0) + one workgroup per 4 rows (16 with 16-lane
+    // teams); the row workgroups spin only on the fetcher's progress word,
+    // and the fetcher is dispatched first, so a plain launch on this stream
+    // is safe (launch_resident still checks the grid fits the device)
     {
       int N_ = N;
       const double *gQt_ = gQt;

@@ -432,8 +432,8 @@ int MtStream::init(size_t capacity_words, size_t parallel_min) {
       if (mt_jump_poly_pow2(lw + l, hp.data() + (size_t)l * MT_POLY_WORDS)) return 1;
     KG_HIP(hipMemcpy(polys_, hp.data(), hp.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     const int lds = (int)mt_chunk_lds_bytes();
-    KG_HIP(hipFuncSetAttribute((const void *)k_mt_chunks, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    KG_HIP(hipFuncSetAttribute((const void *)k_mt_jump_level, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    KG_HIP(allow_dynamic_lds((const void *)k_mt_chunks, lds));
+    KG_HIP(allow_dynamic_lds((const void *)k_mt_jump_level, lds));
     capacity_words += W_;  // production rounds up to whole chunks
   }
   R_ = next_pow2(capacity_words + 2 * MT_N + 4096);

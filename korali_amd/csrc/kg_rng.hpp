@@ -103,6 +103,7 @@ class MtStream {
   int join(hipStream_t main);
 
   StreamState *state() { return st_; }
+  unsigned long long capacity_words() const { return R_; }
   size_t words_for_normals(size_t M) const;
 
  private:

@@ -2217,16 +2217,13 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     KG_HIP(hipMemcpy(h->pairs, pr.data(), pr.size() * sizeof(int2), hipMemcpyHostToDevice));
   }
   {
-    KG_HIP(hipFuncSetAttribute((const void *)k_tm_wsum<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)ws_lds_bytes(N, false)));
-    KG_HIP(hipFuncSetAttribute((const void *)k_tm_wsum<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)ws_lds_bytes(N, true)));
+    KG_HIP(allow_dynamic_lds((const void *)k_tm_wsum<false>, (int)ws_lds_bytes(N, false)));
+    KG_HIP(allow_dynamic_lds((const void *)k_tm_wsum<true>, (int)ws_lds_bytes(N, true)));
     const size_t lbytes = (size_t)N * (N + 1) * sizeof(double) + (size_t)std::max(1, 256 / N) * N * sizeof(double);
     if (lbytes > 64 * 1024) {
-      KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
-      KG_HIP(hipFuncSetAttribute((const void *)k_tm_draw<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lbytes));
-      KG_HIP(hipFuncSetAttribute((const void *)k_tm_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)((size_t)N * (N + 1) * sizeof(double))));
+      KG_HIP(allow_dynamic_lds((const void *)k_tm_draw<false>, (int)lbytes));
+      KG_HIP(allow_dynamic_lds((const void *)k_tm_draw<true>, (int)lbytes));
+      KG_HIP(allow_dynamic_lds((const void *)k_tm_cholesky, (int)((size_t)N * (N + 1) * sizeof(double))));
     }
 
   }

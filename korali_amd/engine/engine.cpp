@@ -720,8 +720,15 @@ struct CmaesModule : SolverModule {
     if (hasDiscrete && dist) fail("Discrete variables (Granularity) need an unsharded run (Sequential or Concurrent conduit).");
     c.normal_seed = seeds.assign(gn);
     c.uniform_seed = seeds.assign(gu);
-    const std::string cu = canon(str(sv, "Covariance Update", "Exact"));
+    // the Distributed conduit shards the update: every rank sums the mean and
+    // rank-mu terms of the selected rows it owns and one all-reduce adds the
+    // partial sums, which is the MFMA mode's (reordered) summation; it is the
+    // default there, and the exact sequential order cannot be requested
+    const std::string cu = canon(str(sv, "Covariance Update", dist ? "MFMA" : "Exact"));
     if (cu != "exact" && cu != "mfma") fail("'Covariance Update' must be 'Exact' or 'MFMA'.");
+    if (dist && cu == "exact")
+      fail("'Covariance Update' = 'Exact' needs an unsharded run (Sequential or Concurrent conduit): the Distributed "
+           "conduit adds per-rank partial sums (MFMA order).");
     c.cov_mode = cu == "mfma" ? KG_COV_MFMA : KG_COV_EXACT;
     c.device = solverDevice(js, dist);
     c.shard_rank = dist ? dist->rank : 0;

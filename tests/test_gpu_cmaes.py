@@ -409,3 +409,146 @@ def test_discrete_variables_match_oracle_bit_exact(Nv, lam, mirrored, bound, gen
     if Nv >= 10:
         assert mutated > 0  # masked variables took geometric mutations
     dev.close()
+
+
+@pytest.mark.parametrize("Nv,lam,s0,mirrored,max_res,gens", [(10, 64, 0.3, False, float("inf"), 12),
+                                                             (10, 64, 0.3, True, float("inf"), 12),
+                                                             (4, 64, 1.0, False, float("inf"), 25),
+                                                             (4, 64, 1.0, True, float("inf"), 25),
+                                                             (10, 64, 0.3, False, 3000.0, 8)])
+def test_resampling_past_the_first_round_matches_oracle_bit_exact(Nv, lam, s0, mirrored, max_res, gens):
+    """prepareGeneration's redraw loop (CMAES.cpp.base:443-491) for any number
+    of infeasible draws: the mean starts ON the upper bound of [-0.5, 0.5]^N
+    and Rosenbrock's optimum (1, ..., 1) lies outside the box, so a generation
+    draws thousands of infeasible samples, far more than the first round's
+    max(256, lambda/4) reserve; the device continues the Normal stream round
+    after round exactly where the reference's do/while would.  Populations,
+    selections, infeasible counts, mean / covariance / sigma and the final
+    generator state bit for bit, plain and mirrored, unlimited and with a
+    finite Max Infeasible Resamplings (reached in generation 1)."""
+    seed = 4242
+    lb, ub, x0 = np.full(Nv, -0.5), np.full(Nv, 0.5), np.full(Nv, 0.5)
+    o = R.CMAES(Nv, lam, 0)
+    o["Initial Value"], o["Initial Standard Deviation"] = x0, np.full(Nv, s0)
+    o["Lower Bound"], o["Upper Bound"] = lb, ub
+    if mirrored:
+        o.option("Mirrored Sampling", 1)
+    o.option("Max Infeasible Resamplings", max_res)
+    R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+    R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+    dev = device_solver(Nv, lam, initial_value=x0, initial_std=np.full(Nv, s0), lower_bound=lb, upper_bound=ub,
+                        mirrored=mirrored, max_infeasible_resamplings=max_res, normal_seed=seed,
+                        uniform_seed=seed + 1)
+    reserve = max(256, lam // 4)
+    prev, most = 0.0, 0.0
+    for g in range(1, gens + 1):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        for key in ("Current Mean", "Covariance Matrix", "Axis Lengths"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        for key in ("Sigma", "Infeasible Sample Count", "Best Ever Value"):
+            assert dev[key][0] == o[key][0], (g, key)
+        cnt = o["Infeasible Sample Count"][0]
+        most = max(most, cnt - prev)
+        prev = cnt
+    # more infeasible draws in one generation than the first round's reserve
+    # holds: the walk continued into later rounds
+    assert most > reserve, most
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+    dev.close()
+
+
+def test_discrete_resampling_past_the_first_round_matches_oracle_bit_exact():
+    """Discrete variables redraw through the same rounds (the walk stops at a
+    block boundary and resumes with the next transformed blocks; its
+    mutations' uniforms are re-peeked from the consumed position)."""
+    Nv, lam, seed, gens = 8, 16, 99, 10
+    lb, ub = np.full(Nv, -1.0), np.full(Nv, 1.0)
+    x0, s0 = np.full(Nv, 1.0), np.full(Nv, 0.8)
+    gran = np.zeros(Nv)
+    gran[::2] = 0.5
+    o = R.CMAES(Nv, lam, 0)
+    o["Initial Value"], o["Initial Standard Deviation"] = x0, s0
+    o["Lower Bound"], o["Upper Bound"], o["Granularity"] = lb, ub, gran
+    R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+    R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+    dev = device_solver(Nv, lam, initial_value=x0, initial_std=s0, lower_bound=lb, upper_bound=ub,
+                        granularity=gran, normal_seed=seed, uniform_seed=seed + 1)
+    prev, most = 0.0, 0.0
+    for g in range(1, gens + 1):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        for key in ("Current Mean", "Covariance Matrix", "Masking Matrix"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        for key in ("Sigma", "Infeasible Sample Count"):
+            assert dev[key][0] == o[key][0], (g, key)
+        cnt = o["Infeasible Sample Count"][0]
+        most = max(most, cnt - prev)
+        prev = cnt
+    assert most > 256, most
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+    assert dev.get_rng(1) == o.rng(1).get_bytes()
+    dev.close()
+
+
+@pytest.mark.parametrize("mirrored", [False, True])
+def test_overflowing_draws_are_redrawn_like_the_reference(mirrored):
+    """Unbounded variables: the reference redraws a sample only when it is
+    not finite (optimizer.cpp.base:5-14).  With sigma = 1e308 about a quarter
+    of the draws overflow; the overflow guard sends the generation through
+    the redraw rounds, and the population, infeasible count and generator
+    state equal the oracle's.  Without the guard tripping (sigma = 1) the
+    population is the first lambda blocks, as before."""
+    Nv, lam, seed = 4, 16, 5
+    for sigma, expect_redraw in ((1e308, True), (1.0, False)):
+        o = R.CMAES(Nv, lam, 0)
+        o["Initial Value"], o["Initial Standard Deviation"] = np.zeros(Nv), np.ones(Nv)
+        if mirrored:
+            o.option("Mirrored Sampling", 1)
+        R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+        R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+        dev = device_solver(Nv, lam, initial_value=np.zeros(Nv), initial_std=np.ones(Nv), mirrored=mirrored,
+                            normal_seed=seed, uniform_seed=seed + 1)
+        o.initialize()
+        dev.initialize()
+        o["Sigma"] = [sigma]
+        dev["Sigma"] = [sigma]
+        o.prepare()
+        dev.sample()
+        dev.synchronize()
+        X = dev["Sample Population"]
+        assert np.all(np.isfinite(X))
+        assert np.array_equal(X, o["Sample Population"])
+        assert dev["Infeasible Sample Count"][0] == o["Infeasible Sample Count"][0]
+        assert (o["Infeasible Sample Count"][0] > 0) == expect_redraw
+        assert dev.get_rng(0) == o.rng(0).get_bytes()
+        dev.close()
+
+
+def test_handles_of_different_sizes_interleaved_bit_exact():
+    """Kernel attributes are process-wide: a large handle (N = 512, the
+    multi-workgroup tridiagonalisation and the streamed apply on a
+    cooperative / capacity-checked launch) created BEFORE a smaller one
+    (N = 200, same kernels, less LDS) must still launch after the small one
+    was created and ran (round 3 lowered the dynamic-LDS limit per handle, and
+    the runtime's occupancy query then answered 0 for the large launches).
+    Interleaved generations, both bit-exact vs the oracle."""
+    big_o, big = oracle_and_device(512, 1024, "rosenbrock", 2)
+    small_o, small = oracle_and_device(200, 512, "rosenbrock", 2)
+    tiny_o, tiny = oracle_and_device(16, 32, "rosenbrock", 2)
+    for g in (1, 2):
+        for o, dev in ((big_o, big), (small_o, small), (tiny_o, tiny)):
+            o.generation(g, "rosenbrock")
+            dev.generation(g, "rosenbrock")
+            dev.synchronize()
+            assert np.array_equal(dev["Sample Population"], o["Sample Population"]), (dev.N, g)
+            for key in ("Covariance Eigenvector Matrix", "Axis Lengths", "Covariance Matrix"):
+                assert np.array_equal(dev[key], o[key]), (dev.N, g, key)
+    for dev in (big, small, tiny):
+        dev.close()
