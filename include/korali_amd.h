@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 4
+#define KG_ABI_VERSION 5
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -99,9 +99,43 @@ typedef struct {
    * masked path length; with or without Mirrored Sampling.  Not with
    * population sharding (shard_count > 1). */
   const double *granularity;
+  /* CCMA-ES (Problem "Constraints"; CMAES.cpp.base:54-68, :132-170,
+   * :315-437, :551-580, :724-731, :774-832).  constraint_count > 0: the
+   * viability regime (viability_population_size samples, viability_mu_value
+   * → half of it) until the mean satisfies every constraint; the constraint
+   * values come from the callback of kg_cmaes_set_constraints.  The four
+   * doubles below are then required (CMAES.config defaults: 1e6, 0.1818,
+   * 0.1, 0.2).  Not with Mirrored Sampling, discrete variables or
+   * sharding. */
+  size_t constraint_count;
+  size_t viability_population_size;
+  size_t viability_mu_value;
+  double max_covariance_matrix_corrections;
+  double target_success_rate;
+  double covariance_matrix_adaption_strength;
+  double global_success_learning_rate;
 } kg_cmaes_cfg;
 
 int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out);
+
+/* Constraint values of `rows` samples (row-major rows x N, host memory):
+ * out[r * constraint_count + c] = constraint c at X[r] (Optimization::
+ * evaluateConstraints, optimization.cpp.base:11-24: the reference runs
+ * sample.run(_constraints[c]) for c in order).  ids[r] = the sample's index
+ * in the population, or (size_t)-1 for the mean (checkMeanAndSetRegime).
+ * Return 0, or nonzero to abort the generation (kg_last_error() then names
+ * the callback). */
+typedef int (*kg_constraint_fn)(const double *X, size_t rows, size_t N, const size_t *ids, double *out, void *ctx);
+int kg_cmaes_set_constraints(kg_cmaes_t h, kg_constraint_fn fn, void *ctx);
+/* CMAES::runGeneration up to the objective with constraints
+ * (CMAES.cpp.base:190-196): checkMeanAndSetRegime, prepareGeneration,
+ * updateConstraints and handleConstraints (covariance shrunk along the
+ * constraint normals on the device, re-decomposed, the violating samples
+ * redrawn from the Normal stream and re-evaluated).  Then evaluate the
+ * current population (kg_cmaes_population_size rows) and kg_cmaes_update. */
+int kg_cmaes_prepare_constrained(kg_cmaes_t h, size_t generation);
+/* the current population / mu (CCMA-ES viability regime: the viability sizes) */
+int kg_cmaes_population_size(kg_cmaes_t h, size_t *lambda, size_t *mu);
 int kg_cmaes_destroy(kg_cmaes_t h);
 int kg_cmaes_initialize(kg_cmaes_t h);
 int kg_cmaes_sample(kg_cmaes_t h);

@@ -37,6 +37,9 @@ struct CmaesScalars {
   unsigned int rmuOutOfRange;     // k_rankmu_prep: some rank-mu factor outside the Markstein range
   // discrete variables (CMAES.cpp.base:34, :106-107, :834-859)
   double nME, nDM, chiDM;  // Number Masking Matrix Entries, Number Of Discrete Mutations, Chi Square Number DM
+  // CCMA-ES (CMAES.cpp.base:147, :724-731, :812-819)
+  double gsr;              // Global Success Rate
+  double resampledCount;   // Resampled Parameter Count (handleConstraints' redraws)
 };
 
 // Bound on |z| of a GSL polar normal: z = y sqrt(-2 ln r2 / r2) with |y| <=
@@ -50,11 +53,16 @@ constexpr double KG_DRAW_GUARD_LIMIT = 1e300;
 // ----------------------------------------------------------------- init
 // setInitialConfiguration (CMAES.cpp.base:14-184), initMuWeights (:233-284),
 // initCovariance (:286-313); initial values/stds resolved on the host.
+// full = 0: only initMuWeights + initCovariance, as checkMeanAndSetRegime
+// does on leaving CCMA-ES's viability regime (:341-345; initCovariance sets
+// the diagonals of C and B and keeps their other entries, as written);
+// constrained: the constrained sigma cumulation factor (:270-273)
 __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType, double initialSigmaCumulationFactor,
                                               double initialDampFactor, double initialCumulativeCovariance,
                                               const double *__restrict__ iv, const double *__restrict__ istd,
                                               double *w, double *C, double *B, double *D, double *mean,
-                                              double *prevMean, double *pc, double *ps, CmaesScalars *sc) {
+                                              double *prevMean, double *pc, double *ps, CmaesScalars *sc, int full,
+                                              int constrained) {
   __shared__ double s1s2[2];
   const int tid = threadIdx.x;
   for (int i = tid; i < mu; i += blockDim.x) {
@@ -69,15 +77,17 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
     }
     w[i] = v;
   }
-  for (int i = tid; i < N * N; i += blockDim.x) {
-    C[i] = 0.0;
-    B[i] = 0.0;
-  }
-  for (int i = tid; i < N; i += blockDim.x) {
-    pc[i] = 0.0;
-    ps[i] = 0.0;
-    mean[i] = iv[i];
-    prevMean[i] = iv[i];
+  if (full) {
+    for (int i = tid; i < N * N; i += blockDim.x) {
+      C[i] = 0.0;
+      B[i] = 0.0;
+    }
+    for (int i = tid; i < N; i += blockDim.x) {
+      pc[i] = 0.0;
+      ps[i] = 0.0;
+      mean[i] = iv[i];
+      prevMean[i] = iv[i];
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -93,15 +103,19 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
   for (int i = tid; i < mu; i += blockDim.x) w[i] /= s1s2[0];
   if (tid == 0) {
     const double Nd = (double)N;
-    sc->bestEverValue = -INFINITY;
-    sc->previousBestEverValue = sc->bestEverValue;
-    sc->previousBestValue = sc->bestEverValue;
-    sc->currentBestValue = sc->bestEverValue;
-    sc->chiSquareNumber = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));
-    sc->chiDM = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));  // :34
-    sc->nME = 0.0;
-    sc->nDM = 0.0;
-    sc->bestValidSample = 0;
+    if (full) {
+      sc->bestEverValue = -INFINITY;
+      sc->previousBestEverValue = sc->bestEverValue;
+      sc->previousBestValue = sc->bestEverValue;
+      sc->currentBestValue = sc->bestEverValue;
+      sc->chiSquareNumber = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));
+      sc->chiDM = sqrt(Nd) * (1. - 1. / (4. * N) + 1. / (21. * N * N));  // :34
+      sc->nME = 0.0;
+      sc->nDM = 0.0;
+      sc->bestValidSample = constrained ? -1.0 : 0.0;
+      sc->gsr = constrained ? 0.5 : -1.0;
+      sc->resampledCount = 0.0;
+    }
     const double effMu = s1s2[0] * s1s2[0] / s1s2[1];
     sc->effectiveMu = effMu;
     if ((initialCumulativeCovariance <= 0) || (initialCumulativeCovariance > 1))
@@ -109,7 +123,8 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
     else
       sc->cumulativeCovariance = initialCumulativeCovariance;
     double cs = initialSigmaCumulationFactor;
-    if (cs <= 0 || cs >= 1) cs = (effMu + 2.0) / (N + effMu + 3.0);
+    if (cs <= 0 || cs >= 1)
+      cs = constrained ? sqrt(effMu) / (sqrt(effMu) + sqrt(Nd)) : (effMu + 2.0) / (N + effMu + 3.0);
     sc->sigmaCumulationFactor = cs;
     double ds = initialDampFactor;
     if (ds <= 0.0) {
@@ -142,10 +157,12 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
       if (mind > C[i * N + i]) mind = C[i * N + i];
     sc->maxDiagC = maxd;
     sc->minDiagC = mind;
-    sc->infeasibleSampleCount = 0;
-    sc->psNorm = 0.0;
-    sc->currentMinStd = INFINITY;
-    sc->currentMaxStd = -INFINITY;
+    if (full) {
+      sc->infeasibleSampleCount = 0;
+      sc->psNorm = 0.0;
+      sc->currentMinStd = INFINITY;
+      sc->currentMaxStd = -INFINITY;
+    }
   }
 }
 
@@ -863,13 +880,30 @@ __global__ void k_copy_idx(int lam, const unsigned *__restrict__ val, unsigned *
 
 // --------------------------------------------------------------- update
 // updateDistribution :547-609 (best bookkeeping, proportional weights)
+// viol (CCMA-ES outside the viability regime): the best valid sample is the
+// LAST sample in sorted order without constraint violations (:551-558, as
+// written)
 __global__ void __launch_bounds__(256) k_update_best(int N, int mu, int muType, unsigned long long gen,
                                                      const double *__restrict__ X, const double *__restrict__ F,
                                                      const unsigned *__restrict__ idx, double *w,
-                                                     double *currBestVars, double *bestEverVars, CmaesScalars *sc) {
+                                                     double *currBestVars, double *bestEverVars, CmaesScalars *sc,
+                                                     const int *__restrict__ viol, int lam) {
   __shared__ int flag;
+  __shared__ unsigned bestIdx;
   const int tid = threadIdx.x;
-  const unsigned i0 = idx[0];
+  if (tid == 0) {
+    unsigned b = idx[0];
+    if (viol) {
+      long best = -1;
+      for (int i = 0; i < lam; i++)
+        if (viol[idx[i]] == 0) best = (long)idx[i];
+      if (best < 0) sc->errors |= KG_ERR_CONSTRAINT;  // the reference reads _valueVector[-1]
+      else b = (unsigned)best;
+    }
+    bestIdx = b;
+  }
+  __syncthreads();
+  const unsigned i0 = bestIdx;
   if (tid == 0) {
     sc->bestValidSample = (double)i0;
     sc->previousBestValue = sc->currentBestValue;
@@ -1879,7 +1913,8 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
                                                const double *__restrict__ minStdUpdate, CmaesScalars *sc,
                                                const StreamState *stA, const StreamState *stB, TermSummary *out,
                                                unsigned long long seq, const double *__restrict__ maskSigma,
-                                               const double *__restrict__ ps, const double *__restrict__ mean) {
+                                               const double *__restrict__ ps, const double *__restrict__ mean,
+                                               int muCfg, int viability, double tsr, double gslr) {
   __shared__ double ssig;
   __shared__ int viol;
   __shared__ double red[4][6];
@@ -1887,13 +1922,18 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
   if (tid == 0) {
     const double cs = sc->sigmaCumulationFactor, ds = sc->dampFactor;
     double sigma = sc->sigma;
-    if (maskSigma) {  // discrete variables (:729-735)
+    if (viability) {  // CCMA-ES viability regime (:724-731)
+      const double gsr = (1 - gslr) * sc->gsr;
+      sc->gsr = gsr;
+      sigma *= exp_cr((gsr - (tsr / (1.0 - tsr)) * (1 - gsr)) / ds);
+    } else if (maskSigma) {  // discrete variables (:729-735)
       double pathL2 = 0.0;
       for (int d = 0; d < N; ++d) pathL2 += maskSigma[d] * ps[d] * ps[d];
       sigma *= exp_cr(cs / ds * (sqrt(pathL2) / sc->chiDM - 1.));
     } else
       sigma *= exp_cr(cs / ds * (sc->psNorm / sc->chiSquareNumber - 1.));
-    if (mu > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
+    // (the configured _muValue; the index uses the current mu, :743)
+    if (muCfg > 1 && sc->currentBestValue == F[idx[mu - 1]]) sigma *= exp_cr(0.2 + cs / ds);
     const double ub = sqrt(sc->trace / N);
     if (sigma > ub && isSigmaBounded) sigma = ub;
     ssig = sigma;
@@ -1967,6 +2007,80 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
   }
 }
 
+// ------------------------------------------------------------- CCMA-ES
+// handleConstraints' covariance correction (:779-804): auxC = C, then for
+// every (violating sample i, constraint c with its viability indicator set)
+// pair in the reference's order: the constraint normal's running
+// approximation v_c = (1 - beta) v_c + beta BDZ_i, v2 = |v_c|^2 (sequential),
+// and auxC -= (cmaf cmaf v_c,d v_c,e) / (v2 cnt_i cnt_i) elementwise.
+__global__ void __launch_bounds__(256) k_ccm_adapt(int N, int npairs, const int *__restrict__ pi,
+                                                   const int *__restrict__ pc_, const double *__restrict__ pcnt,
+                                                   const double *__restrict__ BDZ, double *__restrict__ V, double beta,
+                                                   double cmaf, const double *__restrict__ C, double *__restrict__ auxC) {
+  __shared__ double v2s;
+  const int tid = threadIdx.x;
+  for (int q = tid; q < N * N; q += blockDim.x) auxC[q] = C[q];
+  for (int p = 0; p < npairs; p++) {
+    const int i = pi[p];
+    double *v = V + (size_t)pc_[p] * N;
+    __syncthreads();
+    for (int d = tid; d < N; d += blockDim.x) v[d] = (1.0 - beta) * v[d] + beta * BDZ[(size_t)i * N + d];
+    __syncthreads();
+    if (tid == 0) {
+      double v2 = 0;
+      for (int d = 0; d < N; ++d) v2 += v[d] * v[d];
+      v2s = v2;
+    }
+    __syncthreads();
+    const double den = v2s * pcnt[p] * pcnt[p];
+    for (int q = tid; q < N * N; q += blockDim.x) {
+      const int d = q / N, e = q % N;
+      auxC[q] = auxC[q] - ((cmaf * cmaf * v[d] * v[e]) / den);
+    }
+  }
+}
+
+// handleConstraints' redraws (:806-822) over one round of transformed
+// blocks: list entry k (a violating sample, in index order) takes blocks
+// until one is feasible or the Resampled Parameter Count (+1 per draw, every
+// draw) reaches Max Infeasible Resamplings; entries [k0, *kEnd) are assigned
+// (the rest continue in the next round, as k_select)
+__global__ void k_select_list(int nlist, int k0, int blocks, double maxRes, const int *__restrict__ infeas,
+                              int *__restrict__ assign, unsigned long long *__restrict__ used,
+                              int *__restrict__ kEnd, CmaesScalars *sc) {
+  if (threadIdx.x != 0) return;
+  double count = sc->resampledCount;
+  int j = 0, k = k0;
+  for (; k < nlist; k++) {
+    bool taken = false;
+    while (j < blocks) {
+      count += 1;
+      const int feasible = infeas[j] ? 0 : 1;
+      const int jj = j++;
+      if (feasible || !(count < maxRes)) {
+        assign[k] = jj;
+        taken = true;
+        break;
+      }
+    }
+    if (!taken) break;
+  }
+  sc->resampledCount = count;
+  *used = (unsigned long long)j;
+  kEnd[0] = k;
+}
+
+__global__ void k_gather_list(int N, int k0, const int *__restrict__ kEnd, const int *__restrict__ list,
+                              const int *__restrict__ assign, const double *__restrict__ Xall, double *__restrict__ X,
+                              const double *__restrict__ BDZall, double *__restrict__ BDZ) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = k0 + (int)(t / N), d = (int)(t % N);
+  if (k >= *kEnd) return;
+  const size_t dst = (size_t)list[k] * N + d, src = (size_t)assign[k] * N + d;
+  X[dst] = Xall[src];
+  BDZ[dst] = BDZall[src];
+}
+
 __global__ void k_add_evals(CmaesScalars *sc, double n) {
   if (threadIdx.x == 0) sc->modelEvaluationCount += n;
 }
@@ -1979,7 +2093,19 @@ using namespace kg;
 
 struct kg_cmaes_s {
   kg_cmaes_cfg cfg;
-  int N = 0, lam = 0, mu = 0, R = 0;
+  int N = 0, lam = 0, mu = 0, R = 0;  // lam / mu: the CURRENT population and mu (CCMA-ES regimes)
+  int lamCfg = 0, muCfg = 0, lamMax = 0, muMax = 0;  // configured; allocated (max over the regimes)
+  // CCMA-ES (cfg.constraint_count > 0): host-side constraint bookkeeping
+  // (CMAES.cpp.base:350-437), device-side covariance correction / redraws
+  size_t nc = 0;
+  bool viability = false;  // Is Viability Regime
+  kg_constraint_fn cfn = nullptr;
+  void *cctx = nullptr;
+  std::vector<double> cEval, cInd, cCnt, vBounds, bestCEval;  // [c][i] nc x lamMax, (i), (c)
+  double cEvalCount = 0, adaptCount = 0, maxViolCount = 0;
+  double *V = nullptr, *auxC = nullptr;  // normal approximations (nc x N), corrected covariance
+  int *violDev = nullptr, *pairI = nullptr, *pairC = nullptr, *listDev = nullptr;
+  double *pairCnt = nullptr;
   bool finiteBounds = false;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // the rank-mu sum, concurrent with the mean and the paths
@@ -2185,9 +2311,28 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
   SCA("Number Masking Matrix Entries", nME)
   SCA("Number Of Discrete Mutations", nDM)
   SCA("Chi Square Number Discrete Mutations", chiDM)
+  SCA("Global Success Rate", gsr)
+  SCA("Resampled Parameter Count", resampledCount)
+  if (h->nc) VEC("Normal Constraint Approximation", h->V, h->nc * N)
 #undef SCA
 #undef VEC
   return false;
+}
+
+// the current population and mu (CCMA-ES switches them between regimes):
+// blocks drawn per generation, the unsharded evaluation range, and the block
+// count the no-reserve path consumes (λ, or λ/2 when mirrored)
+int set_current(kg_cmaes_s *h, int lam, int mu) {
+  h->lam = lam;
+  h->mu = mu;
+  h->blocks = (h->mirrored ? (size_t)lam / 2 : (size_t)lam) + h->R;
+  if (h->shards == 1) {
+    h->r0 = 0;
+    h->r1 = lam;
+  }
+  const unsigned long long used = (unsigned long long)(h->mirrored ? lam / 2 : lam);
+  KG_HIP(hipMemcpy(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice));
+  return 0;
 }
 
 }  // namespace
@@ -2209,13 +2354,41 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
            "Invalid setting of Mu Type (Linear, Equal, Logarithmic, or Proportional accepted).");
   KG_HIP(hipSetDevice(cfg->device));
   upload_dd_tables();
+  if (cfg->constraint_count > 0) {  // CCMA-ES checks (CMAES.cpp.base:86-95, :134-141)
+    KG_CHECK(!cfg->mirrored_sampling, "Mirrored Sampling not applicable to problems with constraints");
+    KG_CHECK(cfg->shard_count <= 1, "constrained CMA-ES runs unsharded");
+    KG_CHECK(cfg->viability_population_size >= 1, "'Viability Population Size' must be >= 1");
+    KG_CHECK(cfg->global_success_learning_rate > 0.0 && cfg->global_success_learning_rate <= 1.0,
+             "Invalid Global Success Learning Rate, must be greater than 0.0 and less than 1.0");
+    KG_CHECK(cfg->target_success_rate > 0.0 && cfg->target_success_rate <= 1.0,
+             "Invalid Target Success Rate, must be greater than 0.0 and less than 1.0");
+    KG_CHECK(cfg->covariance_matrix_adaption_strength > 0.0, "Invalid Adaption Size, must be greater than 0.0");
+    if (cfg->granularity)
+      for (size_t i = 0; i < cfg->variable_count; i++)
+        KG_CHECK(cfg->granularity[i] == 0.0, "constrained CMA-ES with discrete variables is not on the device path");
+  }
   auto *h = new kg_cmaes_s();
   h->cfg = *cfg;
-  const int N = (int)cfg->variable_count, L = (int)cfg->population_size;
+  const int N = (int)cfg->variable_count;
   h->N = N;
-  h->lam = L;
-  h->mu = (int)(cfg->mu_value ? cfg->mu_value : cfg->population_size / 2);
-  KG_CHECK(h->mu >= 1 && h->mu <= L, "'Mu Value' must be in [1, Population Size]");
+  h->lamCfg = (int)cfg->population_size;
+  h->muCfg = (int)(cfg->mu_value ? cfg->mu_value : cfg->population_size / 2);
+  KG_CHECK(h->muCfg >= 1 && h->muCfg <= h->lamCfg, "'Mu Value' must be in [1, Population Size]");
+  h->nc = cfg->constraint_count;
+  h->lamMax = h->lamCfg;
+  h->muMax = h->muCfg;
+  if (h->nc) {
+    const int lv = (int)cfg->viability_population_size;
+    const int mv = (int)(cfg->viability_mu_value ? cfg->viability_mu_value : cfg->viability_population_size / 2);
+    KG_CHECK(mv >= 1 && mv <= lv, "'Viability Mu Value' must be in [1, Viability Population Size]");
+    h->lamMax = std::max(h->lamMax, lv);
+    h->muMax = std::max(h->muMax, mv);
+    h->cfg.store_bdz = 1;  // the correction reads the samples' BDZ rows
+  }
+  h->lam = h->lamCfg;
+  h->mu = h->muCfg;
+  // allocations below hold the larger regime
+  const int L = h->lamMax;
   std::vector<double> lb(N, -INFINITY), ub(N, INFINITY), iv(N, NAN), istd(N, NAN), minstd(N, 0.0);
   for (int i = 0; i < N; i++) {
     if (cfg->lower_bound) lb[i] = cfg->lower_bound[i];
@@ -2279,16 +2452,16 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   const size_t xrows = h->mirrored ? 2 * h->blocks : rows;  // transformed rows (Xall, infeasibility flags)
   int rc = 0;
   rc |= dalloc(&h->mean, N) | dalloc(&h->prevMean, N) | dalloc(&h->C, (size_t)N * N) | dalloc(&h->B, (size_t)N * N);
-  rc |= dalloc(&h->D, N) | dalloc(&h->pc, N) | dalloc(&h->ps, N) | dalloc(&h->w, h->mu);
+  rc |= dalloc(&h->D, N) | dalloc(&h->pc, N) | dalloc(&h->ps, N) | dalloc(&h->w, h->muMax);
   rc |= dalloc(&h->X, (size_t)L * N) | dalloc(&h->F, L) | dalloc(&h->Z, rows * N);
   rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
   rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
-  rc |= dalloc(&h->Y, (size_t)h->mu * N);
-  if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->mu * N) | dalloc(&h->Tt, (size_t)h->mu * N);
+  rc |= dalloc(&h->Y, (size_t)h->muMax * N);
+  if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->muMax * N) | dalloc(&h->Tt, (size_t)h->muMax * N);
   rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
   rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
   rc |= dalloc(&h->selEnd, 2);
-  if (cfg->store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
+  if (h->cfg.store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
   if (cfg->use_gradients) rc |= dalloc(&h->G, (size_t)L * N);
   rc |= dalloc(&h->gran, N) | dalloc(&h->mask, N) | dalloc(&h->maskSigma, N);
   if (h->hasDiscrete) {
@@ -2297,16 +2470,26 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   }
   if (h->R) {
     rc |= dalloc(&h->Xall, xrows * N);
-    if (cfg->store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
+    if (h->cfg.store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
   }
   size_t P2 = 1;
   while (P2 < (size_t)L) P2 <<= 1;
   if (P2 < SORT_CHUNK) P2 = SORT_CHUNK;
   rc |= dalloc(&h->sortKey, P2) | dalloc(&h->sortVal, P2);
   const int nt = (N + 15) / 16;
-  h->kslices = rankmu_kslices(N, h->mu);
+  h->kslices = rankmu_kslices(N, h->muMax);
   rc |= dalloc(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
-  rc |= dalloc(&h->kidx, h->mu) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
+  if (h->nc) {
+    rc |= dalloc(&h->V, h->nc * (size_t)N) | dalloc(&h->auxC, (size_t)N * N) | dalloc(&h->violDev, L);
+    rc |= dalloc(&h->pairI, h->nc * (size_t)L) | dalloc(&h->pairC, h->nc * (size_t)L) |
+          dalloc(&h->pairCnt, h->nc * (size_t)L) | dalloc(&h->listDev, L);
+    h->cEval.assign(h->nc * (size_t)L, 0.0);
+    h->cInd.assign(h->nc * (size_t)L, 0.0);
+    h->cCnt.assign(L, 0.0);
+    h->vBounds.assign(h->nc, 0.0);
+    h->bestCEval.assign(h->nc, 0.0);
+  }
+  rc |= dalloc(&h->kidx, h->muMax) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
   if (rc) {
     delete h;
     return 1;
@@ -2348,11 +2531,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
       return 1;
     }
   }
-  {
-    // the no-reserve path consumes exactly λ blocks (λ/2 when mirrored)
-    const unsigned long long used = (unsigned long long)(h->mirrored ? L / 2 : L);
-    KG_HIP(hipMemcpy(h->usedBlocks, &used, sizeof(used), hipMemcpyHostToDevice));
-  }
+  if (set_current(h, h->lamCfg, h->muCfg)) return 1;
   KG_HIP(hipMemcpy(h->lb, lb.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->ub, ub.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->iv, iv.data(), N * sizeof(double), hipMemcpyHostToDevice));
@@ -2388,7 +2567,8 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->assign, (void *)h->blockEnd, (void *)h->usedBlocks, (void *)h->Y, (void *)h->Yc, (void *)h->Tt,
                   (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G,
                   (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused,
-                  (void *)h->selEnd})
+                  (void *)h->selEnd, (void *)h->V, (void *)h->auxC, (void *)h->violDev, (void *)h->pairI,
+                  (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -2408,10 +2588,26 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
 int kg_cmaes_initialize(kg_cmaes_t h) {
   Stage st(h, "init");
   h->stateDirty = true;
+  // setInitialConfiguration (:54-66, :132-170): CCMA-ES starts in the viability regime
+  h->viability = h->nc > 0;
+  if (h->viability) {
+    const int lv = (int)h->cfg.viability_population_size;
+    const int mv = (int)(h->cfg.viability_mu_value ? h->cfg.viability_mu_value : h->cfg.viability_population_size / 2);
+    if (set_current(h, lv, mv)) return 1;
+    std::fill(h->cEval.begin(), h->cEval.end(), 0.0);
+    std::fill(h->cInd.begin(), h->cInd.end(), 0.0);
+    std::fill(h->cCnt.begin(), h->cCnt.end(), 0.0);
+    std::fill(h->vBounds.begin(), h->vBounds.end(), 0.0);
+    std::fill(h->bestCEval.begin(), h->bestCEval.end(), 0.0);
+    h->cEvalCount = h->adaptCount = h->maxViolCount = 0.0;
+    KG_HIP(hipMemsetAsync(h->V, 0, h->nc * (size_t)h->N * sizeof(double), h->stream));
+  } else if (set_current(h, h->lamCfg, h->muCfg)) {
+    return 1;
+  }
   hipLaunchKernelGGL(k_init, dim3(1), dim3(256), 0, h->stream, h->N, h->lam, h->mu, h->cfg.mu_type,
                      h->cfg.initial_sigma_cumulation_factor, h->cfg.initial_damp_factor,
                      h->cfg.initial_cumulative_covariance, h->iv, h->istd, h->w, h->C, h->B, h->D, h->mean,
-                     h->prevMean, h->pc, h->ps, h->sc);
+                     h->prevMean, h->pc, h->ps, h->sc, 1, h->nc > 0 ? 1 : 0);
   KG_HIP(hipGetLastError());
   return 0;
 }
@@ -2436,6 +2632,7 @@ static int cmaes_draw_begin(kg_cmaes_t h) {
 
 int kg_cmaes_begin_sample(kg_cmaes_t h) {
   if (h->sampleBegun) return 0;
+  if (h->nc) return 0;  // CCMA-ES: the regime check may reset C before the next draw
   if (cmaes_draw_begin(h)) return 1;
   h->eig.trace = h->eigTrace;
   if (h->eig.run_begin(h->C, h->cfg.diagonal_covariance, h->B, h->D, &h->sc->minEig, &h->sc->maxEig,
@@ -2492,7 +2689,7 @@ static int draw_guard(kg_cmaes_t h, bool *finite, bool *stateFinite = nullptr) {
 // buffers of the redraw path for a handle created without a reserve
 static int ensure_redraw_buffers(kg_cmaes_t h) {
   if (h->Xall) return 0;
-  const size_t xrows = h->mirrored ? 2 * h->blocks : h->blocks;
+  const size_t xrows = h->mirrored ? 2 * (size_t)(h->lamMax / 2) : (size_t)h->lamMax;  // (no reserve: R = 0)
   if (dalloc(&h->Xall, xrows * h->N)) return 1;
   if (h->cfg.store_bdz && dalloc(&h->BDZall, xrows * h->N)) return 1;
   return 0;
@@ -2710,7 +2907,8 @@ static int cmaes_sigma(kg_cmaes_t h) {
                          h->maskSigma, h->sc);
     hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
                        h->minstd, h->sc, h->normal.state(), h->uniform.state(), h->summaryDev, ++h->updates,
-                       h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps, h->mean);
+                       h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps, h->mean, h->muCfg,
+                       h->viability ? 1 : 0, h->cfg.target_success_rate, h->cfg.global_success_learning_rate);
     h->stateDirty = false;  // the record's guard describes the next draw
     KG_HIP(hipGetLastError());
   }
@@ -2734,15 +2932,220 @@ static int cmaes_paths(kg_cmaes_t h, size_t generation) {
   return 0;
 }
 
+// ------------------------------------------------------------------ CCMA-ES
+// The constraint stages of CMAES::runGeneration (CMAES.cpp.base:190-196).
+// Constraint values are host callbacks (the reference's per-sample Python /
+// C++ functions); their bookkeeping (violation counts, indicators, viability
+// boundaries) is O(lambda x constraints) and stays on this host thread; the
+// covariance correction, its eigendecomposition and the redraws run on the
+// device.
+
+// constraint values of rows `ids` of X (device) or of the mean
+static int ccm_eval(kg_cmaes_t h, const std::vector<size_t> &ids, bool mean, std::vector<double> &out) {
+  KG_CHECK(h->cfn, "constraints configured but kg_cmaes_set_constraints was not called");
+  const size_t N = h->N, rows = mean ? 1 : ids.size();
+  std::vector<double> X(rows * N);
+  if (mean) {
+    KG_HIP(hipMemcpyAsync(X.data(), h->mean, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  } else {
+    for (size_t r = 0; r < rows; r++)
+      KG_HIP(hipMemcpyAsync(X.data() + r * N, h->X + ids[r] * N, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  }
+  KG_HIP(hipStreamSynchronize(h->stream));
+  out.assign(rows * h->nc, 0.0);
+  std::vector<size_t> mid(1, (size_t)-1);
+  if (h->cfn(X.data(), rows, N, mean ? mid.data() : ids.data(), out.data(), h->cctx) != 0) {
+    set_error("constraint evaluation failed");
+    return 1;
+  }
+  for (size_t q = 0; q < out.size(); q++)
+    KG_CHECK(std::isfinite(out[q]), "Non finite value of constraint evaluation " + std::to_string(q % h->nc) +
+                                        " detected: " + std::to_string(out[q]));
+  h->cEvalCount += (double)rows;
+  return 0;
+}
+
+// checkMeanAndSetRegime (:315-348)
+static int ccm_check_mean(kg_cmaes_t h) {
+  if (!h->viability) return 0;
+  std::vector<double> ev;
+  if (ccm_eval(h, {}, true, ev)) return 1;
+  for (size_t c = 0; c < h->nc; c++)
+    if (ev[c] > 0.0) return 0;
+  h->viability = false;
+  std::fill(h->vBounds.begin(), h->vBounds.end(), 0.0);
+  if (set_current(h, h->lamCfg, h->muCfg)) return 1;
+  hipLaunchKernelGGL(k_init, dim3(1), dim3(256), 0, h->stream, h->N, h->lam, h->mu, h->cfg.mu_type,
+                     h->cfg.initial_sigma_cumulation_factor, h->cfg.initial_damp_factor,
+                     h->cfg.initial_cumulative_covariance, h->iv, h->istd, h->w, h->C, h->B, h->D, h->mean,
+                     h->prevMean, h->pc, h->ps, h->sc, 0, 1);
+  KG_HIP(hipGetLastError());
+  h->stateDirty = true;
+  return 0;
+}
+
+// updateConstraints (:350-387)
+static int ccm_update_constraints(kg_cmaes_t h, size_t generation) {
+  const size_t L = h->lam, S = h->lamMax, nc = h->nc;
+  std::vector<size_t> ids(L);
+  for (size_t i = 0; i < L; i++) ids[i] = i;
+  std::vector<double> ev;
+  if (ccm_eval(h, ids, false, ev)) return 1;
+  for (size_t i = 0; i < L; i++) {
+    h->cCnt[i] = 0;
+    for (size_t c = 0; c < nc; c++) h->cEval[c * S + i] = ev[i * nc + c];
+  }
+  h->maxViolCount = 0;
+  for (size_t c = 0; c < nc; c++) {
+    double maxviolation = 0.0;
+    for (size_t i = 0; i < L; ++i) {
+      const double e = h->cEval[c * S + i];
+      if (e > maxviolation) maxviolation = e;
+      if (generation == 1 && h->viability) h->vBounds[c] = maxviolation;
+      if (e > h->vBounds[c] + 1e-12) h->cCnt[i] += 1;
+      if (h->cCnt[i] > h->maxViolCount) h->maxViolCount = h->cCnt[i];
+    }
+  }
+  return 0;
+}
+
+// redraw the listed samples (handleConstraints :806-822) in rounds of the
+// Normal stream, as cmaes_resample
+static int ccm_redraw(kg_cmaes_t h, const std::vector<int> &list) {
+  const int N = h->N, nl = (int)list.size();
+  if (ensure_redraw_buffers(h)) return 1;  // (unbounded variables: no reserve rows yet)
+  const size_t nb = h->blocks;
+  const unsigned tgrid = tr_grid<32, 64>((int)nb, N);
+  KG_HIP(hipMemcpyAsync(h->listDev, list.data(), nl * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  int k0 = 0;
+  for (;;) {
+    if (h->normal.polar_normals(h->Z, nb * N, N, h->blockEnd, h->stream)) return 1;
+    KG_HIP(hipMemsetAsync(h->infeas, 0, nb * sizeof(int), h->stream));
+    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tgrid), dim3(256), 0, h->stream, N, (int)nb,
+                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, h->Xall, h->BDZall,
+                       h->infeas, 0, 0);
+    hipLaunchKernelGGL(k_select_list, dim3(1), dim3(64), 0, h->stream, nl, k0, (int)nb,
+                       h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->selEnd, h->sc);
+    const size_t tot = (size_t)(nl - k0) * N;
+    hipLaunchKernelGGL(k_gather_list, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, N, k0,
+                       (const int *)h->selEnd, (const int *)h->listDev, h->assign, h->Xall, h->X, h->BDZall, h->BDZ);
+    KG_HIP(hipGetLastError());
+    if (h->normal.consume_normals_dev(h->usedBlocks, N, h->blockEnd, h->stream)) return 1;
+    int se[2] = {0, 0};
+    KG_HIP(hipMemcpyAsync(se, h->selEnd, sizeof(se), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    if (se[0] >= nl) break;
+    k0 = se[0];
+  }
+  return 0;
+}
+
+// handleConstraints (:774-832) + reEvaluateConstraints (:389-422)
+static int ccm_handle_constraints(kg_cmaes_t h) {
+  const int N = h->N;
+  const size_t L = h->lam, S = h->lamMax, nc = h->nc;
+  const double beta = 1.0 / (2.0 + N), cmaf = h->cfg.covariance_matrix_adaption_strength / (N + 2.);
+  while (h->maxViolCount > 0) {
+    // the (sample, constraint) pairs in the reference's order; the loop
+    // returns at the pair that takes the count past the maximum
+    std::vector<int> pi, pc;
+    std::vector<double> pcnt;
+    bool truncated = false;
+    for (size_t i = 0; i < L && !truncated; ++i)
+      if (h->cCnt[i] > 0)
+        for (size_t c = 0; c < nc; c++)
+          if (h->cInd[c * S + i] != 0) {
+            h->adaptCount += 1;
+            if (h->adaptCount > h->cfg.max_covariance_matrix_corrections) {
+              truncated = true;
+              break;
+            }
+            pi.push_back((int)i);
+            pc.push_back((int)c);
+            pcnt.push_back(h->cCnt[i]);
+          }
+    const int np = (int)pi.size();
+    if (np) {
+      KG_HIP(hipMemcpyAsync(h->pairI, pi.data(), np * sizeof(int), hipMemcpyHostToDevice, h->stream));
+      KG_HIP(hipMemcpyAsync(h->pairC, pc.data(), np * sizeof(int), hipMemcpyHostToDevice, h->stream));
+      KG_HIP(hipMemcpyAsync(h->pairCnt, pcnt.data(), np * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    }
+    hipLaunchKernelGGL(k_ccm_adapt, dim3(1), dim3(256), 0, h->stream, N, np, h->pairI, h->pairC, h->pairCnt, h->BDZ,
+                       h->V, beta, cmaf, h->C, h->auxC);
+    KG_HIP(hipGetLastError());
+    KG_HIP(hipStreamSynchronize(h->stream));  // (the pair vectors are temporaries)
+    if (truncated) return 0;                  // "max adaptions reached" (:787-791)
+    // updateEigensystem(auxC)
+    if (h->eig.run(h->auxC, h->cfg.diagonal_covariance, h->B, h->D, &h->sc->minEig, &h->sc->maxEig,
+                   &h->sc->eigenFailures, &h->sc->errors, h->stream, eig_prof, h))
+      return 1;
+    std::vector<int> list;
+    for (size_t i = 0; i < L; ++i)
+      if (h->cCnt[i] > 0) list.push_back((int)i);
+    if (ccm_redraw(h, list)) return 1;
+    // reEvaluateConstraints
+    std::vector<size_t> ids(list.begin(), list.end());
+    std::vector<double> ev;
+    if (ccm_eval(h, ids, false, ev)) return 1;
+    h->maxViolCount = 0;
+    for (size_t r = 0; r < ids.size(); r++) {
+      const size_t i = ids[r];
+      h->cCnt[i] = 0;
+      for (size_t c = 0; c < nc; c++) {
+        h->cEval[c * S + i] = ev[r * nc + c];
+        if (ev[r * nc + c] > h->vBounds[c] + 1e-12) {
+          h->cInd[c * S + i] = 1;
+          h->cCnt[i] += 1;
+        } else {
+          h->cInd[c * S + i] = 0;
+        }
+      }
+      if (h->cCnt[i] > h->maxViolCount) h->maxViolCount = h->cCnt[i];
+    }
+  }
+  return 0;
+}
+
+// after updateDistribution: updateViabilityBoundaries (:424-437; the sigma
+// step does not read them) and the best constraint values (:576-579)
+static int ccm_after_update(kg_cmaes_t h) {
+  const size_t L = h->lam, S = h->lamMax, nc = h->nc;
+  std::vector<unsigned> idx(L);
+  CmaesScalars hs;
+  KG_HIP(hipMemcpyAsync(idx.data(), h->idx, L * sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipMemcpyAsync(&hs, h->sc, sizeof(hs), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  if (hs.errors & KG_ERR_CONSTRAINT) return check_errors(h);
+  if (hs.bestFlag)
+    for (size_t c = 0; c < nc; c++) h->bestCEval[c] = h->cEval[c * S + (size_t)hs.bestValidSample];
+  if (h->viability)
+    for (size_t c = 0; c < nc; c++) {
+      double maxviolation = 0.0;
+      for (int i = 0; i < h->mu; ++i)
+        if (h->cEval[c * S + idx[i]] > maxviolation) maxviolation = h->cEval[c * S + idx[i]];
+      const double t = 0.5 * (maxviolation + h->vBounds[c]);
+      const double mn = (t < h->vBounds[c]) ? t : h->vBounds[c];  // std::min
+      h->vBounds[c] = (0.0 < mn) ? mn : 0.0;                     // std::max(0.0, .)
+    }
+  return 0;
+}
+
 int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
   KG_CHECK(h->shards == 1, "a population-sharded handle updates through kg_cmaes_update_partial / _finalize");
   const int N = h->N, mu = h->mu;
   if (cmaes_sort(h)) return 1;
   {
     Stage st(h, "mean_paths");
+    const bool ccm = h->nc > 0 && !h->viability;  // the best VALID sample (:551-558)
+    if (ccm) {
+      std::vector<int> viol(h->lam);
+      for (int i = 0; i < h->lam; i++) viol[i] = h->cCnt[i] > 0 ? 1 : 0;
+      KG_HIP(hipMemcpyAsync(h->violDev, viol.data(), h->lam * sizeof(int), hipMemcpyHostToDevice, h->stream));
+      KG_HIP(hipStreamSynchronize(h->stream));  // (viol is a temporary)
+    }
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
                        (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
-                       h->sc);
+                       h->sc, ccm ? (const int *)h->violDev : (const int *)nullptr, h->lam);
     hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y, h->mean,
                        h->prevMean);
     // the rank-mu sum (MFMA) needs only Y, the weights and m_prev: it runs on
@@ -2788,7 +3191,8 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
   }
-  return cmaes_sigma(h);  // (k_sigma also publishes the termination record)
+  if (cmaes_sigma(h)) return 1;  // (k_sigma also publishes the termination record)
+  return h->nc ? ccm_after_update(h) : 0;
 }
 
 int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
@@ -2798,7 +3202,7 @@ int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
     Stage st(h, "mean_paths");
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
                        (unsigned long long)generation, (const double *)nullptr, h->F, h->idx, h->w, h->currBestVars,
-                       h->bestEverVars, h->sc);
+                       h->bestEverVars, h->sc, (const int *)nullptr, h->lam);
     hipLaunchKernelGGL(k_shard_select, dim3(1), dim3(1024), 0, h->stream, mu, h->r0, h->r1, h->idx, h->kidx,
                        h->shardCnt);
     hipLaunchKernelGGL(k_gather_owned, dim3(mu), dim3(128), 0, h->stream, N, h->X, h->idx, h->kidx, h->shardCnt, h->Y);
@@ -2897,7 +3301,50 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
   return check_errors(h);
 }
 
+// CCMA-ES state kept on the host (CMAES.config internal settings)
+struct HostField {
+  double *p;
+  size_t n;
+  bool writable;
+};
+static bool host_field(kg_cmaes_t h, const std::string &k, HostField &f, double &tmp) {
+  if (!h->nc) return false;
+  const size_t S = h->lamMax;
+  if (k == "Constraint Evaluations") f = {h->cEval.data(), h->nc * S, true};
+  else if (k == "Viability Indicator") f = {h->cInd.data(), h->nc * S, true};
+  else if (k == "Sample Constraint Violation Counts") f = {h->cCnt.data(), S, true};
+  else if (k == "Viability Boundaries") f = {h->vBounds.data(), h->nc, true};
+  else if (k == "Best Constraint Evaluations") f = {h->bestCEval.data(), h->nc, true};
+  else if (k == "Constraint Evaluation Count") f = {&h->cEvalCount, 1, true};
+  else if (k == "Covariance Matrix Adaptation Count") f = {&h->adaptCount, 1, true};
+  else if (k == "Max Constraint Violation Count") f = {&h->maxViolCount, 1, true};
+  else if (k == "Is Viability Regime") {
+    tmp = h->viability ? 1.0 : 0.0;
+    f = {&tmp, 1, true};
+  } else if (k == "Current Population Size") {
+    tmp = h->lam;
+    f = {&tmp, 1, false};
+  } else if (k == "Current Mu Value") {
+    tmp = h->mu;
+    f = {&tmp, 1, false};
+  } else if (k == "Covariance Matrix Adaption Factor") {
+    tmp = h->cfg.covariance_matrix_adaption_strength / (h->N + 2.);
+    f = {&tmp, 1, false};
+  } else if (k == "Normal Vector Learning Rate") {
+    tmp = 1.0 / (2.0 + h->N);
+    f = {&tmp, 1, false};
+  } else
+    return false;
+  return true;
+}
+
 int kg_cmaes_field_size(kg_cmaes_t h, const char *name, size_t *n) {
+  HostField hf;
+  double tmp = 0;
+  if (host_field(h, name, hf, tmp)) {
+    *n = hf.n;
+    return 0;
+  }
   FieldRef r;
   KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
   *n = r.n;
@@ -2905,6 +3352,13 @@ int kg_cmaes_field_size(kg_cmaes_t h, const char *name, size_t *n) {
 }
 
 int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n) {
+  HostField hf;
+  double tmp = 0;
+  if (host_field(h, name, hf, tmp)) {
+    KG_CHECK(n == hf.n, std::string("size mismatch for field ") + name);
+    memcpy(out, hf.p, n * sizeof(double));
+    return 0;
+  }
   FieldRef r;
   KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
@@ -2914,6 +3368,20 @@ int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n) {
 }
 
 int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t n) {
+  HostField hf;
+  double tmp = 0;
+  if (host_field(h, name, hf, tmp)) {
+    KG_CHECK(n == hf.n, std::string("size mismatch for field ") + name);
+    KG_CHECK(hf.writable, std::string("read-only field ") + name);
+    if (std::string(name) == "Is Viability Regime") {  // (resume) the regime's sizes follow
+      h->viability = in[0] != 0.0;
+      const int lv = (int)h->cfg.viability_population_size;
+      const int mv = (int)(h->cfg.viability_mu_value ? h->cfg.viability_mu_value : h->cfg.viability_population_size / 2);
+      return h->viability ? set_current(h, lv, mv) : set_current(h, h->lamCfg, h->muCfg);
+    }
+    memcpy(hf.p, in, n * sizeof(double));
+    return 0;
+  }
   FieldRef r;
   KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
   KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
@@ -2970,6 +3438,27 @@ int kg_cmaes_device_ptr(kg_cmaes_t h, const char *name, void **ptr) {
 
 int kg_cmaes_stream(kg_cmaes_t h, void **stream) {
   *stream = (void *)h->stream;
+  return 0;
+}
+
+int kg_cmaes_set_constraints(kg_cmaes_t h, kg_constraint_fn fn, void *ctx) {
+  KG_CHECK(h->nc > 0, "kg_cmaes_set_constraints: the handle was created with constraint_count = 0");
+  h->cfn = fn;
+  h->cctx = ctx;
+  return 0;
+}
+
+int kg_cmaes_prepare_constrained(kg_cmaes_t h, size_t generation) {
+  if (h->nc && ccm_check_mean(h)) return 1;
+  if (kg_cmaes_sample(h)) return 1;
+  if (!h->nc) return 0;
+  if (ccm_update_constraints(h, generation)) return 1;
+  return ccm_handle_constraints(h);
+}
+
+int kg_cmaes_population_size(kg_cmaes_t h, size_t *lambda, size_t *mu) {
+  if (lambda) *lambda = (size_t)h->lam;
+  if (mu) *mu = (size_t)h->mu;
   return 0;
 }
 

@@ -148,6 +148,7 @@ enum : uint32_t {
   KG_ERR_NONFINITE_F = 1u << 0,     // optimization.cpp.base:32-33
   KG_ERR_RNG_UNDERRUN = 1u << 1,    // producer did not generate enough words
   KG_ERR_DRAW_GUARD = 1u << 2,      // a draw the overflow guard proved finite was not (internal)
+  KG_ERR_CONSTRAINT = 1u << 7,      // CCMA-ES: no sample without constraint violations
   KG_ERR_ZERO_LIST = 1u << 3,       // > KG_MAX_ZERO_WORDS zero MT words pending
   KG_ERR_EIGEN = 1u << 4,           // QR iteration did not converge
   KG_ERR_CHOLESKY = 1u << 5,        // covariance not positive definite

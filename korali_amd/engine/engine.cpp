@@ -576,6 +576,13 @@ const char *CMAES_SCALARS[] = {"Sigma", "Trace", "Effective Mu", "Cumulative Cov
                                "Current Max Standard Deviation", "Maximum Diagonal Covariance Matrix Element",
                                "Minimum Diagonal Covariance Matrix Element", "Minimum Covariance Eigenvalue",
                                "Maximum Covariance Eigenvalue", "Infeasible Sample Count", "Model Evaluation Count"};
+// CCMA-ES state (CMAES.config Internal Settings; written and restored with constraints)
+const char *CMAES_CONSTRAINT_VECTORS[] = {"Viability Boundaries", "Sample Constraint Violation Counts",
+                                          "Best Constraint Evaluations", "Constraint Evaluations",
+                                          "Viability Indicator", "Normal Constraint Approximation"};
+const char *CMAES_CONSTRAINT_SCALARS[] = {"Global Success Rate", "Resampled Parameter Count",
+                                          "Constraint Evaluation Count", "Covariance Matrix Adaptation Count",
+                                          "Max Constraint Violation Count"};
 // discrete variables (CMAES.config; written and restored when some variable has a Granularity)
 const char *CMAES_DISCRETE_VECTORS[] = {"Masking Matrix", "Masking Matrix Sigma"};
 const char *CMAES_DISCRETE_SCALARS[] = {"Number Of Discrete Mutations", "Number Masking Matrix Entries",
@@ -598,6 +605,8 @@ struct CmaesModule : SolverModule {
   // between kg_cmaes_update_partial and _finalize (include/korali_amd.h)
   Collective *dist = nullptr;
   size_t r0 = 0, r1 = 0;
+  std::vector<size_t> constraintFns;  // CCMA-ES (function table indices)
+  size_t curGen = 0;
 
   ~CmaesModule() override {
     if (h) kg_cmaes_destroy(h);
@@ -639,8 +648,13 @@ struct CmaesModule : SolverModule {
     if (useGradients && (pt != "optimization" || pb.contains("Objective Kernel")))
       fail("'Use Gradient Information' needs an Optimization problem with an 'Objective Function' that sets "
            "'Gradient'.");
-    if (pb.contains("Constraints") && pb["Constraints"].size() > 0)
-      fail("Constrained CMA-ES ('Constraints') is not supported by the device path.");
+    // CCMA-ES: Problem "Constraints" = functions evaluated per sample in list
+    // order (optimization.cpp.base:11-24)
+    if (pt == "optimization" && pb.contains("Constraints"))
+      for (size_t c = 0; c < pb["Constraints"].size(); c++) constraintFns.push_back(pb["Constraints"][c].getUInt());
+    if (!constraintFns.empty() && dist)
+      fail("Constrained CMA-ES needs an unsharded run (Sequential or Concurrent conduit).");
+    if (!constraintFns.empty() && mirrored) fail("Mirrored Sampling not applicable to problems with constraints");
     if (dist) {
       if (mirrored || useGradients)
         fail("The Distributed conduit shards the population: 'Mirrored Sampling' and 'Use Gradient Information' "
@@ -735,7 +749,15 @@ struct CmaesModule : SolverModule {
     c.shard_count = dist ? dist->world : 0;
     c.store_bdz = 0;
     c.eigen_device_chase = 0;
+    c.constraint_count = constraintFns.size();
+    c.viability_population_size = uint(sv, "Viability Population Size", 2);
+    c.viability_mu_value = uint(sv, "Viability Mu Value", 0);
+    c.max_covariance_matrix_corrections = num(sv, "Max Covariance Matrix Corrections", 1000000);
+    c.target_success_rate = num(sv, "Target Success Rate", 0.1818);
+    c.covariance_matrix_adaption_strength = num(sv, "Covariance Matrix Adaption Strength", 0.1);
+    c.global_success_learning_rate = num(sv, "Global Success Learning Rate", 0.2);
     check(kg_cmaes_create(&c, &h));
+    if (!constraintFns.empty()) check(kg_cmaes_set_constraints(h, &CmaesModule::constraintCallback, this));
     if (mu == 0) mu = lam / 2;
     unsigned char st[5000];
     if (seeds.range(gn, st)) check(kg_cmaes_set_rng(h, 0, st));
@@ -758,6 +780,28 @@ struct CmaesModule : SolverModule {
         const double v = sv[k].getDouble();
         check(kg_cmaes_set_field(h, k, &v, 1));
       }
+    if (!constraintFns.empty()) {
+      if (sv.contains("Is Viability Regime")) {
+        const double v = sv["Is Viability Regime"].getBool() ? 1.0 : 0.0;
+        check(kg_cmaes_set_field(h, "Is Viability Regime", &v, 1));
+      }
+      for (const char *k : CMAES_CONSTRAINT_VECTORS)
+        if (sv.contains(k) && sv[k].is_array()) {
+          std::vector<double> v = flatten(sv[k]);
+          size_t n = 0;
+          check(kg_cmaes_field_size(h, k, &n));
+          if (v.size() == n) check(kg_cmaes_set_field(h, k, v.data(), n));
+        }
+      for (const char *k : CMAES_CONSTRAINT_SCALARS)
+        if (sv.contains(k) && sv[k].is_number()) {
+          const double v = sv[k].getDouble();
+          check(kg_cmaes_set_field(h, k, &v, 1));
+        }
+      size_t cur = 0;
+      check(kg_cmaes_population_size(h, &cur, nullptr));
+      lam = cur;
+      r1 = lam;
+    }
     if (hasDiscrete) {
       for (const char *k : CMAES_DISCRETE_VECTORS)
         if (sv.contains(k) && sv[k].is_array() && sv[k].size() == N) {
@@ -772,9 +816,55 @@ struct CmaesModule : SolverModule {
     }
   }
 
+  // Optimization::evaluateConstraints for a batch of samples (the mean: id -1),
+  // through the conduit (Sequential, or the Concurrent pool)
+  static int constraintCallback(const double *X, size_t rows, size_t N_, const size_t *ids, double *out, void *ctx) {
+    auto *self = (CmaesModule *)ctx;
+    const size_t nc = self->constraintFns.size();
+    try {
+      self->conduit->evaluateBatch(rows, [&](size_t r) {
+        Sample s;
+        s["Module"] = "Problem";
+        s["Operation"] = "Evaluate Constraints";
+        s["Sample Id"] = (unsigned long long)0;  // (as CMAES.cpp.base:326, :357, :398)
+        s["Current Generation"] = (unsigned long long)self->curGen;
+        s["Parameters"] = std::vector<double>(X + r * N_, X + (r + 1) * N_);
+        for (size_t c = 0; c < nc; c++) {
+          getFunction(self->constraintFns[c])(s);
+          if (!s.contains("F(x)")) fail("The constraint function %zu did not assign 'F(x)'.", c);
+          const double v = s["F(x)"].getDouble();
+          if (!std::isfinite(v)) fail("Non finite value of constraint evaluation %lu detected: %f\n", (unsigned long)c, v);
+          out[r * nc + c] = v;
+        }
+      });
+    } catch (...) {
+      self->pendingError = std::current_exception();
+      return 1;
+    }
+    (void)ids;
+    return 0;
+  }
+  std::exception_ptr pendingError;
+
   void runGeneration(size_t gen) override {
+    curGen = gen;
     if (gen == 1) check(kg_cmaes_initialize(h));
-    check(kg_cmaes_sample(h));
+    if (!constraintFns.empty()) {
+      if (kg_cmaes_prepare_constrained(h, gen) != 0) {
+        if (pendingError) {
+          std::exception_ptr e = pendingError;
+          pendingError = nullptr;
+          std::rethrow_exception(e);
+        }
+        check(1);
+      }
+      size_t cur = 0;
+      check(kg_cmaes_population_size(h, &cur, nullptr));
+      lam = cur;
+      r1 = lam;
+    } else {
+      check(kg_cmaes_sample(h));
+    }
     if (objective >= 0) {
       check(kg_cmaes_eval_builtin(h, objective));
     } else if (dist) {
@@ -909,6 +999,34 @@ struct CmaesModule : SolverModule {
       sv[k] = v;
     }
     for (const char *k : CMAES_SCALARS) sv[k] = field(k);
+    if (!constraintFns.empty()) {
+      sv["Has Constraints"] = true;
+      sv["Is Viability Regime"] = field("Is Viability Regime") != 0.0;
+      sv["Current Population Size"] = (unsigned long long)field("Current Population Size");
+      sv["Current Mu Value"] = (unsigned long long)field("Current Mu Value");
+      sv["Covariance Matrix Adaption Factor"] = field("Covariance Matrix Adaption Factor");
+      sv["Normal Vector Learning Rate"] = field("Normal Vector Learning Rate");
+      for (const char *k : CMAES_CONSTRAINT_VECTORS) {
+        size_t n = 0;
+        check(kg_cmaes_field_size(h, k, &n));
+        std::vector<double> v(n);
+        check(kg_cmaes_get_field(h, k, v.data(), n));
+        const size_t nc = constraintFns.size();
+        if (!strcmp(k, "Constraint Evaluations") || !strcmp(k, "Normal Constraint Approximation"))
+          sv[k] = matrixJson(v, nc, n / nc);
+        else if (!strcmp(k, "Viability Indicator")) {
+          Json m = Json::array();
+          for (size_t c = 0; c < nc; c++) {
+            Json row = Json::array();
+            for (size_t i = 0; i < n / nc; i++) row.push_back(v[c * (n / nc) + i] != 0.0);
+            m.push_back(row);
+          }
+          sv[k] = m;
+        } else
+          sv[k] = v;
+      }
+      for (const char *k : CMAES_CONSTRAINT_SCALARS) sv[k] = field(k);
+    }
     if (hasDiscrete) {
       sv["Has Discrete Variables"] = true;
       for (const char *k : CMAES_DISCRETE_VECTORS) {

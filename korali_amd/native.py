@@ -37,7 +37,16 @@ class _CmaesCfg(C.Structure):
         ("store_bdz", C.c_int), ("eigen_device_chase", C.c_int), ("shard_rank", C.c_int), ("shard_count", C.c_int),
         ("use_gradients", C.c_int), ("gradient_step_size", C.c_double),
         ("granularity", C.POINTER(C.c_double)),
+        ("constraint_count", C.c_size_t), ("viability_population_size", C.c_size_t),
+        ("viability_mu_value", C.c_size_t), ("max_covariance_matrix_corrections", C.c_double),
+        ("target_success_rate", C.c_double), ("covariance_matrix_adaption_strength", C.c_double),
+        ("global_success_learning_rate", C.c_double),
     ]
+
+
+# int (*)(const double *X, size_t rows, size_t N, const size_t *ids, double *out, void *ctx)
+CONSTRAINT_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t),
+                            C.POINTER(C.c_double), C.c_void_p)
 
 
 class _TmcmcCfg(C.Structure):
@@ -63,6 +72,7 @@ EXPORTED = [
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
+    "kg_cmaes_set_constraints", "kg_cmaes_prepare_constrained", "kg_cmaes_population_size",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
     "kg_tmcmc_evaluate", "kg_tmcmc_process", "kg_tmcmc_advance", "kg_tmcmc_get_pending",
@@ -110,6 +120,9 @@ def lib():
         L.kg_cmaes_get_sorting_index.argtypes = [vp, C.POINTER(C.c_uint64)]
         L.kg_cmaes_get_fields.argtypes = [vp, C.POINTER(cp), sz, dp]
         L.kg_cmaes_wait_termination_fields.argtypes = [vp, dp]
+        L.kg_cmaes_set_constraints.argtypes = [vp, CONSTRAINT_FN, vp]
+        L.kg_cmaes_prepare_constrained.argtypes = [vp, sz]
+        L.kg_cmaes_population_size.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
         L.kg_cmaes_get_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_set_rng.argtypes = [vp, ip, vp]
         L.kg_cmaes_device_ptr.argtypes = [vp, cp, C.POINTER(vp)]
@@ -170,17 +183,23 @@ class CmaesDevice:
                  is_sigma_bounded=False, diagonal=False, max_infeasible_resamplings=float("inf"),
                  initial_sigma_cumulation_factor=-1.0, initial_damp_factor=-1.0,
                  initial_cumulative_covariance=-1.0, device=0, store_bdz=False, eigen_chase="host", shard_rank=0,
-                 shard_count=1, mirrored=False, gradient_step_size=None, granularity=None):
+                 shard_count=1, mirrored=False, gradient_step_size=None, granularity=None, constraints=None,
+                 viability_population_size=2, viability_mu_value=0, max_covariance_matrix_corrections=1e6,
+                 target_success_rate=0.1818, covariance_matrix_adaption_strength=0.1,
+                 global_success_learning_rate=0.2):
+        """constraints: CCMA-ES constraint functions c(x) -> float (x: the
+        sample as a list), evaluated in list order per sample; a sample
+        violates c when c(x) > 0 (beyond the viability boundary)."""
         L = lib()
-        self.N, self.lam = int(N), int(lam)
-        self.mu = int(mu) if mu else self.lam // 2
+        self.N, self._lam_cfg = int(N), int(lam)
+        self.mu = int(mu) if mu else self._lam_cfg // 2
         self._arrays = [
             _vec(lower_bound, self.N, -np.inf), _vec(upper_bound, self.N, np.inf),
             _vec(initial_value, self.N, np.nan), _vec(initial_std, self.N, np.nan),
             _vec(min_std_update, self.N, 0.0), _vec(granularity, self.N, 0.0),
         ]
         cfg = _CmaesCfg()
-        cfg.variable_count, cfg.population_size, cfg.mu_value = self.N, self.lam, int(mu)
+        cfg.variable_count, cfg.population_size, cfg.mu_value = self.N, self._lam_cfg, int(mu)
         cfg.mu_type = MU_TYPES[mu_type.lower()] if isinstance(mu_type, str) else int(mu_type)
         cfg.initial_sigma_cumulation_factor = initial_sigma_cumulation_factor
         cfg.initial_damp_factor = initial_damp_factor
@@ -197,10 +216,45 @@ class CmaesDevice:
         cfg.eigen_device_chase = 1 if eigen_chase == "device" else 0
         cfg.shard_rank, cfg.shard_count = int(shard_rank), int(shard_count)
         self.shard_rank, self.shard_count = int(shard_rank), max(1, int(shard_count))
+        self._constraints = list(constraints or [])
+        cfg.constraint_count = len(self._constraints)
+        cfg.viability_population_size, cfg.viability_mu_value = int(viability_population_size), int(viability_mu_value)
+        cfg.max_covariance_matrix_corrections = float(max_covariance_matrix_corrections)
+        cfg.target_success_rate = float(target_success_rate)
+        cfg.covariance_matrix_adaption_strength = float(covariance_matrix_adaption_strength)
+        cfg.global_success_learning_rate = float(global_success_learning_rate)
         h = C.c_void_p()
         check(L.kg_cmaes_create(C.byref(cfg), C.byref(h)))
         self.h = h
         self._L = L
+        if self._constraints:
+            funcs = self._constraints
+
+            def cb(X, rows, n, ids, out, ctx):
+                try:
+                    nc = len(funcs)
+                    for r in range(rows):
+                        x = [float(X[r * n + d]) for d in range(n)]
+                        for c in range(nc):
+                            out[r * nc + c] = float(funcs[c](x))
+                    return 0
+                except Exception:  # reported as a failed evaluation by the library
+                    return 1
+
+            self._cfn = CONSTRAINT_FN(cb)  # kept alive with the handle
+            check(L.kg_cmaes_set_constraints(self.h, self._cfn, None))
+
+    @property
+    def lam(self):
+        """the current population size (CCMA-ES: the viability one in its viability regime)"""
+        n = C.c_size_t()
+        check(self._L.kg_cmaes_population_size(self.h, C.byref(n), None))
+        return n.value
+
+    def prepare_constrained(self, generation):
+        """CCMA-ES: regime check, draw, constraint evaluation and handling
+        (kg_cmaes_prepare_constrained); then evaluate the current population."""
+        check(self._L.kg_cmaes_prepare_constrained(self.h, int(generation)))
 
     def close(self):
         if getattr(self, "h", None):

@@ -1145,6 +1145,24 @@ struct kr_cmaes
   double *granularity, *maskingMatrix, *maskingMatrixSigma, *discreteMutations;
   double numberMaskingMatrixEntries, numberOfDiscreteMutations, chiSquareNumberDiscreteMutations;
   int hasDiscrete;
+  /* configured Population Size / Mu Value; lambda / mu above are the
+   * CURRENT ones (_currentPopulationSize / _currentMuValue), which differ
+   * during CCMA-ES's viability regime */
+  size_t populationSize, muValue, smax, mumax;
+  /* CCMA-ES (Problem "Constraints"; CMAES.cpp.base:54-68, :132-170,
+   * :315-437, :551-580, :724-731, :774-832) */
+  int hasConstraints, isViabilityRegime;
+  size_t nc, viabilityPopulationSize, viabilityMuValue;
+  double maxCovarianceMatrixCorrections, targetSuccessRate, covarianceMatrixAdaptionStrength, globalSuccessLearningRate;
+  double normalVectorLearningRate, covarianceMatrixAdaptionFactor, globalSuccessRate;
+  double constraintEvaluationCount, covarianceMatrixAdaptationCount, maxConstraintViolationCount, resampledParameterCount;
+  double *constraintEvaluations;  /* [c][i], nc x smax */
+  double *viabilityIndicator;     /* [c][i] as 0 / 1 */
+  double *sampleConstraintViolationCounts, *viabilityBoundaries, *normalConstraintApproximation;
+  double *bestConstraintEvaluations, *auxC;
+  kr_constraint_fn constraintFn;
+  void *constraintCtx;
+  int constraintError; /* the reference's out-of-range _bestValidSample (no valid sample) */
 };
 
 kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
@@ -1195,6 +1213,8 @@ kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu)
   AL(h->discreteMutations, lambda * N);
 #undef AL
   h->sortingIndex = (size_t *)calloc(lambda, sizeof(size_t));
+  h->populationSize = h->smax = lambda;
+  h->muValue = h->mumax = h->mu;
   kr_rng_seed(&h->normal, 0);
   kr_rng_seed(&h->uniform, 0);
   return h;
@@ -1231,7 +1251,52 @@ void kr_cmaes_free(kr_cmaes *h)
   free(h->maskingMatrixSigma);
   free(h->discreteMutations);
   free(h->sortingIndex);
+  free(h->constraintEvaluations);
+  free(h->viabilityIndicator);
+  free(h->sampleConstraintViolationCounts);
+  free(h->viabilityBoundaries);
+  free(h->normalConstraintApproximation);
+  free(h->bestConstraintEvaluations);
+  free(h->auxC);
   free(h);
+}
+
+/* Problem "Constraints" (nc functions, evaluated by fn in the reference's
+ * order: sample.run(_constraints[c]) for c = 0..nc-1, optimization.cpp.base:
+ * 11-24) and the CCMA-ES sizes (CMAES.cpp.base:25-30): every per-sample array
+ * grows to max(Population Size, Viability Population Size) */
+void kr_cmaes_set_constraints(kr_cmaes *h, size_t nc, size_t viabilityPopulationSize, size_t viabilityMuValue,
+                              kr_constraint_fn fn, void *ctx)
+{
+  const size_t N = h->N;
+  h->nc = nc;
+  h->hasConstraints = nc > 0;
+  h->constraintFn = fn;
+  h->constraintCtx = ctx;
+  h->viabilityPopulationSize = viabilityPopulationSize;
+  h->viabilityMuValue = viabilityMuValue ? viabilityMuValue : viabilityPopulationSize / 2;
+  h->smax = h->populationSize > viabilityPopulationSize ? h->populationSize : viabilityPopulationSize;
+  h->mumax = h->muValue > h->viabilityMuValue ? h->muValue : h->viabilityMuValue;
+#define RE(p, n) p = (double *)realloc(p, sizeof(double) * (n)), memset(p, 0, sizeof(double) * (n))
+  RE(h->X, h->smax * N);
+  RE(h->BDZ, h->smax * N);
+  RE(h->F, h->smax);
+  RE(h->discreteMutations, h->smax * N);
+  RE(h->muWeights, h->mumax);
+  RE(h->constraintEvaluations, nc * h->smax + 1);
+  RE(h->viabilityIndicator, nc * h->smax + 1);
+  RE(h->sampleConstraintViolationCounts, h->smax);
+  RE(h->viabilityBoundaries, nc + 1);
+  RE(h->normalConstraintApproximation, nc * N + 1);
+  RE(h->bestConstraintEvaluations, nc + 1);
+  RE(h->auxC, N * N);
+#undef RE
+  h->sortingIndex = (size_t *)realloc(h->sortingIndex, sizeof(size_t) * h->smax);
+  if (h->gradients) h->gradients = (double *)realloc(h->gradients, sizeof(double) * h->smax * N);
+  h->maxCovarianceMatrixCorrections = 1000000; /* CMAES.config defaults */
+  h->targetSuccessRate = 0.1818;
+  h->covarianceMatrixAdaptionStrength = 0.1;
+  h->globalSuccessLearningRate = 0.2;
 }
 
 double *kr_cmaes_field(kr_cmaes *h, const char *name, size_t *len)
@@ -1295,6 +1360,26 @@ double *kr_cmaes_field(kr_cmaes *h, const char *name, size_t *len)
   SCA("Model Evaluation Count", modelEvaluationCount)
   SCA("Hsig", hsig)
   SCA("Eigen Failures", eigenFailures)
+  if (h->hasConstraints)
+  {
+    VEC("Constraint Evaluations", h->constraintEvaluations, h->nc * h->smax)
+    VEC("Viability Indicator", h->viabilityIndicator, h->nc * h->smax)
+    VEC("Sample Constraint Violation Counts", h->sampleConstraintViolationCounts, h->lambda)
+    VEC("Viability Boundaries", h->viabilityBoundaries, h->nc)
+    VEC("Normal Constraint Approximation", h->normalConstraintApproximation, h->nc * N)
+    VEC("Best Constraint Evaluations", h->bestConstraintEvaluations, h->nc)
+  }
+  SCA("Global Success Rate", globalSuccessRate)
+  SCA("Covariance Matrix Adaption Factor", covarianceMatrixAdaptionFactor)
+  SCA("Normal Vector Learning Rate", normalVectorLearningRate)
+  SCA("Constraint Evaluation Count", constraintEvaluationCount)
+  SCA("Covariance Matrix Adaptation Count", covarianceMatrixAdaptationCount)
+  SCA("Max Constraint Violation Count", maxConstraintViolationCount)
+  SCA("Resampled Parameter Count", resampledParameterCount)
+  SCA("Max Covariance Matrix Corrections", maxCovarianceMatrixCorrections)
+  SCA("Target Success Rate", targetSuccessRate)
+  SCA("Covariance Matrix Adaption Strength", covarianceMatrixAdaptionStrength)
+  SCA("Global Success Learning Rate", globalSuccessLearningRate)
 #undef VEC
 #undef SCA
   if (len) *len = 0;
@@ -1320,6 +1405,10 @@ void kr_cmaes_set_option(kr_cmaes *h, const char *name, double v)
   }
   else if (strcmp(name, "Gradient Step Size") == 0) h->gradientStepSize = v;
   else if (strcmp(name, "Max Infeasible Resamplings") == 0) h->maxInfeasibleResamplings = v;
+  else if (strcmp(name, "Max Covariance Matrix Corrections") == 0) h->maxCovarianceMatrixCorrections = v;
+  else if (strcmp(name, "Target Success Rate") == 0) h->targetSuccessRate = v;
+  else if (strcmp(name, "Covariance Matrix Adaption Strength") == 0) h->covarianceMatrixAdaptionStrength = v;
+  else if (strcmp(name, "Global Success Learning Rate") == 0) h->globalSuccessLearningRate = v;
 }
 
 /* initMuWeights, CMAES.cpp.base:233-284 (unconstrained branch) */
@@ -1357,7 +1446,12 @@ static void cmaes_init_mu_weights(kr_cmaes *h, size_t numsamplesmu)
 
   h->sigmaCumulationFactor = h->initialSigmaCumulationFactor;
   if (h->sigmaCumulationFactor <= 0 || h->sigmaCumulationFactor >= 1)
-    h->sigmaCumulationFactor = (h->effectiveMu + 2.0) / (N + h->effectiveMu + 3.0);
+  {
+    if (h->hasConstraints) /* :270-273 */
+      h->sigmaCumulationFactor = sqrt(h->effectiveMu) / (sqrt(h->effectiveMu) + sqrt((double)N));
+    else
+      h->sigmaCumulationFactor = (h->effectiveMu + 2.0) / (N + h->effectiveMu + 3.0);
+  }
 
   h->dampFactor = h->initialDampFactor;
   if (h->dampFactor <= 0.0)
@@ -1426,6 +1520,31 @@ void kr_cmaes_initialize(kr_cmaes *h)
   h->bestValidSample = 0;
   memset(h->C, 0, sizeof(double) * N * N);
   memset(h->B, 0, sizeof(double) * N * N);
+  /* :54-66 regime and current sizes; :132-165 constraint state */
+  h->isViabilityRegime = h->hasConstraints;
+  h->lambda = h->isViabilityRegime ? h->viabilityPopulationSize : h->populationSize;
+  h->mu = h->isViabilityRegime ? h->viabilityMuValue : h->muValue;
+  if (h->hasConstraints)
+  {
+    h->globalSuccessRate = 0.5;
+    h->bestValidSample = -1;
+    memset(h->constraintEvaluations, 0, sizeof(double) * h->nc * h->smax);
+    memset(h->viabilityIndicator, 0, sizeof(double) * h->nc * h->smax);
+    memset(h->sampleConstraintViolationCounts, 0, sizeof(double) * h->smax);
+    memset(h->viabilityBoundaries, 0, sizeof(double) * h->nc);
+    memset(h->normalConstraintApproximation, 0, sizeof(double) * h->nc * N);
+    memset(h->bestConstraintEvaluations, 0, sizeof(double) * h->nc);
+    h->normalVectorLearningRate = 1.0 / (2.0 + N);
+    h->covarianceMatrixAdaptionFactor = h->covarianceMatrixAdaptionStrength / (N + 2.);
+  }
+  else
+  {
+    h->globalSuccessRate = -1.0;
+    h->covarianceMatrixAdaptionFactor = -1.0;
+  }
+  h->covarianceMatrixAdaptationCount = 0;
+  h->maxConstraintViolationCount = 0;
+  h->resampledParameterCount = 0;
   cmaes_init_mu_weights(h, h->mu);
   cmaes_init_covariance(h);
   h->infeasibleSampleCount = 0;
@@ -1435,8 +1554,8 @@ void kr_cmaes_initialize(kr_cmaes *h)
   h->currentMaxStd = -INFINITY;
 }
 
-/* updateEigensystem, CMAES.cpp.base:869-890 (+ eigen :896-938) */
-void kr_cmaes_eigen_only(kr_cmaes *h)
+/* updateEigensystem(M), CMAES.cpp.base:869-890 (+ eigen :896-938) */
+static void cmaes_update_eigensystem(kr_cmaes *h, const double *M)
 {
   const size_t N = h->N;
   size_t i, j;
@@ -1445,7 +1564,7 @@ void kr_cmaes_eigen_only(kr_cmaes *h)
   {
     memset(h->auxEvec, 0, sizeof(double) * N * N);
     for (i = 0; i < N; ++i) h->auxEvec[i * N + i] = 1.;
-    for (i = 0; i < N; ++i) h->auxAxisLengths[i] = h->C[i * N + i];
+    for (i = 0; i < N; ++i) h->auxAxisLengths[i] = M[i * N + i];
   }
   else
   {
@@ -1453,8 +1572,8 @@ void kr_cmaes_eigen_only(kr_cmaes *h)
     for (i = 0; i < N; i++)
       for (j = 0; j <= i; j++)
       {
-        data[i * N + j] = h->C[i * N + j];
-        data[j * N + i] = h->C[i * N + j];
+        data[i * N + j] = M[i * N + j];
+        data[j * N + i] = M[i * N + j];
       }
     kr_eigen_symmv(N, data, h->auxAxisLengths, h->auxEvec);
     free(data);
@@ -1476,6 +1595,8 @@ void kr_cmaes_eigen_only(kr_cmaes *h)
   for (i = 0; i < N; i++) h->D[i] = h->auxAxisLengths[i];
   memcpy(h->B, h->auxEvec, sizeof(double) * N * N);
 }
+
+void kr_cmaes_eigen_only(kr_cmaes *h) { cmaes_update_eigensystem(h, h->C); }
 
 /* discretize, CMAES.cpp.base:861-867 */
 static void cmaes_discretize(const kr_cmaes *h, double *x)
@@ -1713,15 +1834,33 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
   g_sort_vec = h->F;
   qsort(h->sortingIndex, h->lambda, sizeof(size_t), cmp_desc);
 
-  h->bestValidSample = (double)h->sortingIndex[0];
-  h->previousBestValue = h->currentBestValue;
-  h->currentBestValue = h->F[h->sortingIndex[0]];
-  for (d = 0; d < N; ++d) h->currentBestVariables[d] = h->X[h->sortingIndex[0] * N + d];
-  if (h->currentBestValue > h->bestEverValue || gen == 1)
   {
-    h->previousBestEverValue = h->bestEverValue;
-    h->bestEverValue = h->currentBestValue;
-    for (d = 0; d < N; ++d) h->bestEverVariables[d] = h->currentBestVariables[d];
+    /* :552-558: with constraints outside the viability regime, the LAST
+     * sample in sorted order without violations (as written) */
+    long best = (long)h->sortingIndex[0];
+    if (h->hasConstraints && !h->isViabilityRegime)
+    {
+      best = -1;
+      for (i = 0; i < h->lambda; i++)
+        if (h->sampleConstraintViolationCounts[h->sortingIndex[i]] == 0) best = (long)h->sortingIndex[i];
+      if (best < 0)
+      {
+        h->constraintError = 1; /* the reference indexes _valueVector[-1] */
+        best = (long)h->sortingIndex[0];
+      }
+    }
+    h->bestValidSample = (double)best;
+    h->previousBestValue = h->currentBestValue;
+    h->currentBestValue = h->F[best];
+    for (d = 0; d < N; ++d) h->currentBestVariables[d] = h->X[(size_t)best * N + d];
+    if (h->currentBestValue > h->bestEverValue || gen == 1)
+    {
+      h->previousBestEverValue = h->bestEverValue;
+      h->bestEverValue = h->currentBestValue;
+      for (d = 0; d < N; ++d) h->bestEverVariables[d] = h->currentBestVariables[d];
+      if (h->hasConstraints)
+        for (k = 0; k < h->nc; k++) h->bestConstraintEvaluations[k] = h->constraintEvaluations[k * h->smax + (size_t)best];
+    }
   }
   if (h->muType == 3)
   {
@@ -1836,14 +1975,35 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
         h->numberMaskingMatrixEntries += 1.0;
       }
     {
-      const double a = round((double)h->lambda / 10.0 + h->numberMaskingMatrixEntries + 1), b = floor((double)h->lambda / 2.0) - 1;
+      const double a = round((double)h->populationSize / 10.0 + h->numberMaskingMatrixEntries + 1),
+                   b = floor((double)h->populationSize / 2.0) - 1;
       h->numberOfDiscreteMutations = a < b ? a : b;
     }
     memset(h->discreteMutations, 0, sizeof(double) * h->lambda * N);
   }
 
+  /* updateViabilityBoundaries :424-437 (viability regime) */
+  if (h->hasConstraints && h->isViabilityRegime)
+    for (k = 0; k < h->nc; k++)
+    {
+      double maxviolation = 0.0, t;
+      for (i = 0; i < mu; ++i)
+        if (h->constraintEvaluations[k * h->smax + h->sortingIndex[i]] > maxviolation)
+          maxviolation = h->constraintEvaluations[k * h->smax + h->sortingIndex[i]];
+      t = 0.5 * (maxviolation + h->viabilityBoundaries[k]);
+      t = (t < h->viabilityBoundaries[k]) ? t : h->viabilityBoundaries[k]; /* std::min(bound, t) */
+      h->viabilityBoundaries[k] = (0.0 < t) ? t : 0.0;                    /* std::max(0.0, .) */
+    }
+
   /* updateSigma :720-761 */
-  if (h->hasDiscrete)
+  if (h->hasConstraints && h->isViabilityRegime)
+  {
+    /* :724-731 */
+    h->globalSuccessRate = (1 - h->globalSuccessLearningRate) * h->globalSuccessRate;
+    h->sigma *= kr_exp_cr((h->globalSuccessRate - (h->targetSuccessRate / (1.0 - h->targetSuccessRate)) * (1 - h->globalSuccessRate)) /
+                          h->dampFactor);
+  }
+  else if (h->hasDiscrete)
   {
     double pathL2 = 0.0;
     for (d = 0; d < N; ++d) pathL2 += h->maskingMatrixSigma[d] * h->ps[d] * h->ps[d];
@@ -1851,7 +2011,9 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
   }
   else
     h->sigma *= kr_exp_cr(h->sigmaCumulationFactor / h->dampFactor * (h->psNorm / h->chiSquareNumber - 1.));
-  if (mu > 1 && h->currentBestValue == h->F[h->sortingIndex[mu - 1]]) h->sigma *= kr_exp_cr(0.2 + h->sigmaCumulationFactor / h->dampFactor);
+  /* (_muValue: the configured one; the index uses the current mu) */
+  if (h->muValue > 1 && h->currentBestValue == h->F[h->sortingIndex[mu - 1]])
+    h->sigma *= kr_exp_cr(0.2 + h->sigmaCumulationFactor / h->dampFactor);
   {
     const double ub = sqrt(h->trace / N);
     if (h->sigma > ub && h->isSigmaBounded) h->sigma = ub;
@@ -1868,6 +2030,169 @@ void kr_cmaes_update(kr_cmaes *h, size_t gen)
     const double s = h->sigma * sqrt(h->C[i * N + i]);
     if (s < h->currentMinStd) h->currentMinStd = s;
     if (s > h->currentMaxStd) h->currentMaxStd = s;
+  }
+}
+
+/* ---- CCMA-ES: the constraint stages of runGeneration (CMAES.cpp.base:186-196) */
+static void cmaes_eval_constraints(kr_cmaes *h, const double *x, double *out)
+{
+  h->constraintFn(x, h->N, out, h->nc, h->constraintCtx);
+  h->constraintEvaluationCount += 1;
+}
+
+/* checkMeanAndSetRegime, :315-348 */
+void kr_cmaes_check_mean_and_set_regime(kr_cmaes *h)
+{
+  size_t c;
+  double *ev;
+  if (!h->isViabilityRegime) return;
+  if (h->hasDiscrete) cmaes_discretize(h, h->currentMean);
+  ev = (double *)malloc(sizeof(double) * (h->nc + 1));
+  cmaes_eval_constraints(h, h->currentMean, ev);
+  for (c = 0; c < h->nc; c++)
+    if (ev[c] > 0.0)
+    {
+      free(ev);
+      return;
+    }
+  free(ev);
+  h->isViabilityRegime = 0;
+  for (c = 0; c < h->nc; c++) h->viabilityBoundaries[c] = 0;
+  h->lambda = h->populationSize;
+  h->mu = h->muValue;
+  cmaes_init_mu_weights(h, h->mu);
+  cmaes_init_covariance(h);
+}
+
+/* updateConstraints, :350-387 */
+void kr_cmaes_update_constraints(kr_cmaes *h, size_t gen)
+{
+  const size_t S = h->smax;
+  size_t i, c;
+  double *ev = (double *)malloc(sizeof(double) * (h->nc + 1));
+  for (i = 0; i < h->lambda; i++)
+  {
+    h->sampleConstraintViolationCounts[i] = 0;
+    if (h->hasDiscrete) cmaes_discretize(h, h->X + i * h->N);
+    cmaes_eval_constraints(h, h->X + i * h->N, ev);
+    for (c = 0; c < h->nc; c++) h->constraintEvaluations[c * S + i] = ev[c];
+  }
+  free(ev);
+  h->maxConstraintViolationCount = 0;
+  for (c = 0; c < h->nc; c++)
+  {
+    double maxviolation = 0.0;
+    for (i = 0; i < h->lambda; ++i)
+    {
+      const double e = h->constraintEvaluations[c * S + i];
+      if (e > maxviolation) maxviolation = e;
+      if (gen == 1 && h->isViabilityRegime) h->viabilityBoundaries[c] = maxviolation;
+      if (e > h->viabilityBoundaries[c] + 1e-12) h->sampleConstraintViolationCounts[i] += 1;
+      if (h->sampleConstraintViolationCounts[i] > h->maxConstraintViolationCount)
+        h->maxConstraintViolationCount = h->sampleConstraintViolationCounts[i];
+    }
+  }
+}
+
+/* reEvaluateConstraints, :389-422 */
+static void cmaes_reevaluate_constraints(kr_cmaes *h)
+{
+  const size_t S = h->smax;
+  size_t i, c;
+  double *ev = (double *)malloc(sizeof(double) * (h->nc + 1));
+  h->maxConstraintViolationCount = 0;
+  for (i = 0; i < h->lambda; ++i)
+    if (h->sampleConstraintViolationCounts[i] > 0)
+    {
+      if (h->hasDiscrete) cmaes_discretize(h, h->X + i * h->N);
+      cmaes_eval_constraints(h, h->X + i * h->N, ev);
+      h->sampleConstraintViolationCounts[i] = 0;
+      for (c = 0; c < h->nc; c++)
+      {
+        h->constraintEvaluations[c * S + i] = ev[c];
+        if (ev[c] > h->viabilityBoundaries[c] + 1e-12)
+        {
+          h->viabilityIndicator[c * S + i] = 1;
+          h->sampleConstraintViolationCounts[i] += 1;
+        }
+        else
+          h->viabilityIndicator[c * S + i] = 0;
+      }
+      if (h->sampleConstraintViolationCounts[i] > h->maxConstraintViolationCount)
+        h->maxConstraintViolationCount = h->sampleConstraintViolationCounts[i];
+    }
+  free(ev);
+}
+
+/* handleConstraints, :774-832: shrink the covariance along the constraint
+ * normals' running approximations, re-decompose it, redraw the violating
+ * samples, re-evaluate them; until no sample violates.  (The viability
+ * indicators read by the first pass are the last re-evaluation's, as in the
+ * reference: updateConstraints does not set them.) */
+void kr_cmaes_handle_constraints(kr_cmaes *h)
+{
+  const size_t N = h->N, S = h->smax;
+  size_t i, c, d, e;
+  double *r = (double *)malloc(sizeof(double) * N);
+  while (h->maxConstraintViolationCount > 0)
+  {
+    memcpy(h->auxC, h->C, sizeof(double) * N * N);
+    for (i = 0; i < h->lambda; ++i)
+      if (h->sampleConstraintViolationCounts[i] > 0)
+        for (c = 0; c < h->nc; c++)
+          if (h->viabilityIndicator[c * S + i] != 0)
+          {
+            double v2 = 0, *v = h->normalConstraintApproximation + c * N;
+            const double cnt = h->sampleConstraintViolationCounts[i];
+            h->covarianceMatrixAdaptationCount += 1;
+            if (h->covarianceMatrixAdaptationCount > h->maxCovarianceMatrixCorrections)
+            {
+              free(r);
+              return;
+            }
+            for (d = 0; d < N; ++d)
+            {
+              v[d] = (1.0 - h->normalVectorLearningRate) * v[d] + h->normalVectorLearningRate * h->BDZ[i * N + d];
+              v2 += v[d] * v[d];
+            }
+            for (d = 0; d < N; ++d)
+              for (e = 0; e < N; ++e)
+                h->auxC[d * N + e] = h->auxC[d * N + e] - ((h->covarianceMatrixAdaptionFactor * h->covarianceMatrixAdaptionFactor * v[d] * v[e]) /
+                                                           (v2 * cnt * cnt));
+          }
+    cmaes_update_eigensystem(h, h->auxC);
+    for (i = 0; i < h->lambda; ++i)
+      if (h->sampleConstraintViolationCounts[i] > 0)
+      {
+        int ok;
+        do
+        {
+          h->resampledParameterCount += 1;
+          for (d = 0; d < N; ++d) r[d] = 0.0 + kr_ran_gaussian(&h->normal, 1.0);
+          cmaes_sample_single(h, i, r);
+          if (h->hasDiscrete) cmaes_discretize(h, h->X + i * N);
+          ok = cmaes_feasible(h, h->X + i * N);
+        } while (ok == 0 && h->resampledParameterCount < h->maxInfeasibleResamplings);
+      }
+    cmaes_reevaluate_constraints(h);
+  }
+  free(r);
+}
+
+int kr_cmaes_constraint_error(kr_cmaes *h) { return h->constraintError; }
+
+/* runGeneration up to the objective (:188-196): regime, prepareGeneration,
+ * updateConstraints + handleConstraints; the caller evaluates the objective
+ * of samples [0, current lambda) and calls kr_cmaes_update */
+void kr_cmaes_ccmaes_prepare(kr_cmaes *h, size_t gen)
+{
+  if (gen == 1) kr_cmaes_initialize(h);
+  if (h->hasConstraints) kr_cmaes_check_mean_and_set_regime(h);
+  kr_cmaes_prepare(h);
+  if (h->hasConstraints)
+  {
+    kr_cmaes_update_constraints(h, gen);
+    kr_cmaes_handle_constraints(h);
   }
 }
 

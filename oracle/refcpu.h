@@ -74,6 +74,8 @@ double kr_loglik_gaussian(const double *x, size_t n);     /* -0.5*sum x^2 */
 
 /* ---------------- CMA-ES (CMAES.cpp.base) ---------------- */
 typedef struct kr_cmaes kr_cmaes;
+/* a sample's constraint values: out[c] for c < nc (Problem "Constraints") */
+typedef void (*kr_constraint_fn)(const double *x, size_t N, double *out, size_t nc, void *ctx);
 kr_cmaes *kr_cmaes_new(size_t N, size_t lambda, size_t mu);
 void kr_cmaes_free(kr_cmaes *h);
 /* named field access: returns a pointer to the double array / scalar and its
@@ -91,6 +93,14 @@ void kr_cmaes_evaluate(kr_cmaes *h, int objective); /* 0 rosen 1 ackley 2 sphere
 void kr_cmaes_update(kr_cmaes *h, size_t generation); /* updateDistribution :547-688 */
 /* whole generation (runGeneration :186-231) with a builtin objective */
 void kr_cmaes_generation(kr_cmaes *h, size_t generation, int objective);
+/* CCMA-ES (CMAES.cpp.base:315-437, :774-832) */
+void kr_cmaes_set_constraints(kr_cmaes *h, size_t nc, size_t viabilityPopulationSize, size_t viabilityMuValue,
+                              kr_constraint_fn fn, void *ctx);
+void kr_cmaes_check_mean_and_set_regime(kr_cmaes *h);
+void kr_cmaes_update_constraints(kr_cmaes *h, size_t generation);
+void kr_cmaes_handle_constraints(kr_cmaes *h);
+void kr_cmaes_ccmaes_prepare(kr_cmaes *h, size_t generation);
+int kr_cmaes_constraint_error(kr_cmaes *h);
 
 /* ---------------- TMCMC (TMCMC.cpp.base) ---------------- */
 typedef struct kr_tmcmc kr_tmcmc;

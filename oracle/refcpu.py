@@ -16,6 +16,10 @@ _LIBS = {}
 _VARIANTS = {"cr": "librefcpu.so", "libm": "librefcpu_libm.so"}
 
 
+# void (*)(const double *x, size_t N, double *out, size_t nc, void *ctx)
+CONSTRAINT_FN = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
@@ -64,6 +68,13 @@ def lib(variant="cr"):
         L.kr_cmaes_evaluate.argtypes = [vp, C.c_int]
         L.kr_cmaes_update.argtypes = [vp, sz]
         L.kr_cmaes_generation.argtypes = [vp, sz, C.c_int]
+        L.kr_cmaes_set_constraints.argtypes = [vp, sz, sz, sz, CONSTRAINT_FN, vp]
+        L.kr_cmaes_check_mean_and_set_regime.argtypes = [vp]
+        L.kr_cmaes_update_constraints.argtypes = [vp, sz]
+        L.kr_cmaes_handle_constraints.argtypes = [vp]
+        L.kr_cmaes_ccmaes_prepare.argtypes = [vp, sz]
+        L.kr_cmaes_constraint_error.argtypes = [vp]
+        L.kr_cmaes_constraint_error.restype = C.c_int
         L.kr_tmcmc_new.argtypes = [sz, sz]
         L.kr_tmcmc_new.restype = vp
         L.kr_tmcmc_free.argtypes = [vp]
@@ -207,6 +218,40 @@ class CMAES:
 
     def generation(self, gen, objective):
         self.L.kr_cmaes_generation(self.h, gen, self.OBJECTIVES[objective])
+
+    # ---- CCMA-ES (Problem "Constraints")
+    def set_constraints(self, constraints, viability_population_size=2, viability_mu_value=0):
+        """constraints: callables c(x) -> float, evaluated in list order per
+        sample (optimization.cpp.base:11-24)."""
+        funcs = list(constraints)
+
+        def cb(x, n, out, nc, ctx):
+            v = [float(x[i]) for i in range(n)]
+            for c in range(nc):
+                out[c] = float(funcs[c](v))
+
+        self._cfn = CONSTRAINT_FN(cb)  # kept alive with the handle
+        self.L.kr_cmaes_set_constraints(self.h, len(funcs), viability_population_size, viability_mu_value,
+                                        self._cfn, None)
+
+    def current_population_size(self):
+        return self.field("Value Vector").size
+
+    def ccmaes_prepare(self, gen):
+        """runGeneration up to the objective (:188-196)."""
+        self.L.kr_cmaes_ccmaes_prepare(self.h, gen)
+
+    def ccmaes_generation(self, gen, objective):
+        """one generation with a Python objective f(x) -> float over the
+        current population (model evaluations counted as the reference)."""
+        self.ccmaes_prepare(gen)
+        lam = self.current_population_size()
+        X = self.field("Sample Population").reshape(lam, self.N)
+        self.field("Value Vector")[:] = [float(objective(list(map(float, x)))) for x in X]
+        self.field("Model Evaluation Count")[0] += lam
+        self.update(gen)
+        if self.L.kr_cmaes_constraint_error(self.h):
+            raise RuntimeError("CCMA-ES: no sample without constraint violations (the reference indexes out of range)")
 
 
 class TMCMC:

@@ -83,8 +83,13 @@ def test_statistical_cmaes_correctness(cfg, tol):
 def test_unsupported_features_fail_loudly():
     import korali
     e = cmaes_1d()
-    e["Problem"]["Constraints"] = [lambda s: None]
-    with pytest.raises(korali.KoraliError, match="Constrained CMA-ES"):
+    e["Problem"]["Constraints"] = [lambda s: None]  # a constraint that sets no F(x)
+    with pytest.raises(korali.KoraliError, match="did not assign 'F\\(x\\)'"):
+        korali.Engine().run(e)
+    e = cmaes_1d()
+    e["Problem"]["Constraints"] = [lambda s: s.__setitem__("F(x)", 1.0)]
+    e["Solver"]["Mirrored Sampling"] = True
+    with pytest.raises(korali.KoraliError, match="Mirrored Sampling not applicable"):
         korali.Engine().run(e)
     e = cmaes_1d()
     e["Variables"][0]["Granularity"] = -0.5

@@ -85,6 +85,38 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
       for (int r = 0; r < reps; r++) acc = kc_add(acc, la(stage), __builtin_amdgcn_readfirstlane(cnt / 16));
       t1 = __builtin_amdgcn_s_memtime();
     }
+  } else if (mode == 12 || mode == 13 || mode == 14 || mode == 15) {
+    // single-lane forms: EXEC = lane 0 only (12 register chain, 13 kc_add),
+    // 14 register chain with a scalar (SGPR pair) operand, full EXEC;
+    // 15 the SGPR-operand chain with EXEC = lane 0
+    if (wid == 0) {
+      const double b = stage[lane];
+      const unsigned long long bb = (unsigned long long)__double_as_longlong(stage[3]);
+      const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)bb), hi = __builtin_amdgcn_readfirstlane((unsigned)(bb >> 32));
+      const double bs = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+      t0 = __builtin_amdgcn_s_memtime();
+      if (mode == 14) {
+        for (int k = 0; k < reps * cnt / 16; k++) {
+#pragma unroll
+          for (int u = 0; u < 16; u++) asm volatile("v_add_f64 %0, %0, %1" : "+v"(acc) : "s"(bs));
+        }
+      } else if (lane == 0) {
+        if (mode == 12) {
+          for (int k = 0; k < reps * cnt / 16; k++) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) asm volatile("v_add_f64 %0, %0, %1" : "+v"(acc) : "v"(b));
+          }
+        } else if (mode == 15) {
+          for (int k = 0; k < reps * cnt / 16; k++) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) asm volatile("v_add_f64 %0, %0, %1" : "+v"(acc) : "s"(bs));
+          }
+        } else {
+          for (int r = 0; r < reps; r++) acc = kc_add(acc, la(stage), __builtin_amdgcn_readfirstlane(cnt / 16));
+        }
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
   } else if (mode == 6) {
     if (wid == 0) {
       double b = stage[lane];
@@ -111,8 +143,9 @@ int main() {
   const char *names[] = {"kc_add alone", "kc_add + 7 LDS waves", "kc_nrm2 alone", "kc_lock_desc alone",
                          "kc_lock_asc alone", "4 lockstep waves", "register add chain", "kc_add_desc alone",
                          "4 indep. add chains (per add)", "inline mul+add chain", "kc_add on waves 0-3",
-                         "kc_add on waves 0 and 4"};
-  for (int mode = 0; mode < 12; mode++) {
+                         "kc_add on waves 0 and 4", "reg chain, exec=lane0", "kc_add, exec=lane0",
+                         "reg chain, sgpr operand", "sgpr chain, exec=lane0"};
+  for (int mode = 0; mode < 16; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
     unsigned long long t[16];
