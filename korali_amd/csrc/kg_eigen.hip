@@ -2927,10 +2927,13 @@ int EigenSolver::init(int N_, bool hostChase_) {
     tri = mw2_fits(N) ? 5 : 2;
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
+  if (const char *e = getenv("KORALI_AMD_SQ_DPP")) sqDpp = *e == '1';
   if (tri == 1)
     KG_HIP(allow_dynamic_lds((const void *)k_tridiag_1wg, (int)(t1_lds_doubles(N) * sizeof(double))));
   if (tri == 4)
-    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_sq, (int)(sq_lds_doubles(N) * sizeof(double))));
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_sq<false>, (int)(sq_lds_doubles(N) * sizeof(double))));
+  if (tri == 4)
+    KG_HIP(allow_dynamic_lds((const void *)k_tridiag_sq<true>, (int)(sq_lds_doubles(N) * sizeof(double))));
   if (tri == 3)
     KG_HIP(allow_dynamic_lds((const void *)k_tridiag_1wg2, (int)(t2_lds_doubles(N) * sizeof(double))));
   if (tri == 5) {
@@ -3002,10 +3005,12 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   if (prof) prof(profCtx, "eigen_tridiag", 0);
   const bool fusedPublish = hostChase && tri == 4;  // the one-workgroup kernel publishes d | sd itself
   if (fusedPublish) dsdSeq = chaseSeq + 1;
-  if (tri == 4)
-    hipLaunchKernelGGL(k_tridiag_sq, dim3(1), dim3(SQ_TPB), sq_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d,
-                       sd, trace, fusedPublish ? d_dsd_map : (double *)nullptr,
+  if (tri == 4) {
+    hipLaunchKernelGGL(sqDpp ? k_tridiag_sq<true> : k_tridiag_sq<false>, dim3(1), dim3(SQ_TPB),
+                       sq_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d, sd, trace,
+                       fusedPublish ? d_dsd_map : (double *)nullptr,
                        fusedPublish ? dprog + 1 : (unsigned long long *)nullptr, (unsigned long long)dsdSeq);
+  }
   else if (tri == 3)
     hipLaunchKernelGGL(k_tridiag_1wg2, dim3(1), dim3(T2_TPB), t2_lds_doubles(N) * sizeof(double), s, N, C, gH, tau,
                        d, sd, trace);

@@ -62,6 +62,11 @@ __device__ __forceinline__ void st_sys_d(double *p, double v) {
   __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// kDpp: the two scalar chains (dnrm2's ssq, xv) run on register-held
+// elements through DPP broadcasts (kc_nrm2_dpp / kc_add_dpp: one VALU
+// instruction per element, no LDS access inside the chain); otherwise they
+// stream the staged elements from LDS (kc_nrm2 / kc_add)
+template <bool kDpp>
 __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__restrict__ C, double *gH,
                                                        double *tauOut, double *dOut, double *sdOut,
                                                        unsigned long long *trace, double *hdsd,
@@ -148,7 +153,15 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       k0 = __ballot(n0);
       sv[lane] = n0 ? q0 : q0 * q0;  // elements >= m: +0.0 (no-ops of the chain)
       SQ_MARK(0)
-      const double ssq = chains::kc_nrm2(1.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
+      double ssq;
+      if (kDpp) {
+        double q[8];  // element 16 k + j in lane j of every row of q[k]
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = sv[16 * k + (lane & 15)];
+        ssq = chains::kc_nrm2_dpp(1.0, q, __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
+      } else {
+        ssq = chains::kc_nrm2(1.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
+      }
       const double xnorm = (m == 1) ? fabs(readlane_d(R0, 0)) : carry * sqrt(ssq);
       SQ_MARK(1)
       double tau_i = 0.0, f1 = 1.0, f2 = 1.0, beta = 0.0;
@@ -251,7 +264,15 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
         }
         sv[64 + lane] = x1 * v1;
       }
-      const double xv = chains::kc_add(0.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4));
+      double xv;
+      if (kDpp) {
+        double q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = sv[16 * k + (lane & 15)];
+        xv = chains::kc_add_dpp(0.0, q, __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4));
+      } else {
+        xv = chains::kc_add(0.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4));
+      }
       const double als = -(tau_i / 2.0) * xv;
       const double xf0 = x0 + als * v0;
       if (lane < n) xa[r1 + lane] = xf0;

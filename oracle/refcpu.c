@@ -894,6 +894,43 @@ static size_t eigen_symmv(size_t N, double *A, double *eval, double *evec, int s
 size_t kr_eigen_symmv(size_t N, double *A, double *eval, double *evec) { return eigen_symmv(N, A, eval, evec, 1); }
 /* gsl_eigen_symmv without gsl_eigen_symmv_sort (TMCMC.cpp.base:468) */
 size_t kr_eigen_symmv_unsorted(size_t N, double *A, double *eval, double *evec) { return eigen_symmv(N, A, eval, evec, 0); }
+
+/* the QR loop of eigen_symmv alone (symmv.c main loop + qrstep) on a given
+ * tridiagonal d / sd (both overwritten): the rotation sequence (c, s) in
+ * order into cs (2 per rotation, up to maxRot) and the unsorted eigenvalues
+ * in d; returns the rotation count (checker of the device library's host
+ * chase, kg_debug_qr_chase) */
+size_t kr_qr_chase(size_t N, double *d, double *sd, double *cs, size_t maxRot)
+{
+  double *gc = (double *)malloc(sizeof(double) * N), *gs = (double *)malloc(sizeof(double) * N);
+  size_t b = N - 1, rot = 0;
+  chop_small_elements(N, d, sd);
+  while (b > 0)
+  {
+    size_t a, k;
+    if (sd[b - 1] == 0.0 || isnan(sd[b - 1]))
+    {
+      b--;
+      continue;
+    }
+    a = b - 1;
+    while (a > 0)
+    {
+      if (sd[a - 1] == 0.0) break;
+      a--;
+    }
+    qrstep(b - a + 1, d + a, sd + a, gc, gs);
+    for (k = 0; k + 1 < b - a + 1 && rot < maxRot; k++, rot++)
+    {
+      cs[2 * rot] = gc[k];
+      cs[2 * rot + 1] = gs[k];
+    }
+    chop_small_elements(b - a + 1, d + a, sd + a);
+  }
+  free(gc);
+  free(gs);
+  return rot;
+}
 static size_t eigen_symmv(size_t N, double *A, double *eval, double *evec, int sort)
 {
   size_t i, steps = 0;

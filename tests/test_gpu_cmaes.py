@@ -213,7 +213,9 @@ def test_unpack_streamed_reflector_rows_bit_exact(monkeypatch, Nv, lam):
 
 
 @pytest.mark.parametrize("Nv,lam,kind", [(3, 8, "sq"), (5, 16, "sq"), (16, 64, "sq"), (67, 256, "sq"),
-                                         (128, 4096, "sq"), (16, 64, "1wg2"), (128, 4096, "1wg2"),
+                                         (128, 4096, "sq"), (3, 8, "sq-dpp"), (5, 16, "sq-dpp"),
+                                         (16, 64, "sq-dpp"), (67, 256, "sq-dpp"), (100, 300, "sq-dpp"),
+                                         (128, 4096, "sq-dpp"), (16, 64, "1wg2"), (128, 4096, "1wg2"),
                                          (40, 128, "mw2"), (100, 512, "mw2"), (129, 256, "mw2"),
                                          (16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
                                          (40, 128, "lds")])
@@ -221,7 +223,8 @@ def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
     """Each tridiagonalisation kernel (one workgroup with the matrix in LDS,
     the multi-workgroup one, the older LDS one) forced: bit-exact B, D and
     the generation's outputs against the oracle."""
-    monkeypatch.setenv("KORALI_AMD_TRIDIAG", kind)
+    monkeypatch.setenv("KORALI_AMD_TRIDIAG", kind.split("-")[0])
+    monkeypatch.setenv("KORALI_AMD_SQ_DPP", "1" if kind.endswith("-dpp") else "0")
     o, dev = oracle_and_device(Nv, lam, "rosenbrock", 4)
     for g in (1, 2, 3, 4):
         o.generation(g, "rosenbrock")

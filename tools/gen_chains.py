@@ -259,6 +259,86 @@ __device__ __forceinline__ double kc_lock_asc(double acc, unsigned pw, unsigned 
 """
 
 
+def emit_dpp_chains():
+    """Chains over staged values held in REGISTERS: element 16 k + j sits in
+    lane j of every row of q[k] (8 VGPR pairs, 128 elements) and reaches the
+    accumulator through a DPP row_newbcast:j operand of v_fmac_f64 (acc = q *
+    1.0 + acc: the product is exact, so this is acc + q rounded once, the
+    same IEEE add as v_add_f64).  No memory operation inside the chain: one
+    VALU instruction per element (kc_add's ds_read2 per two elements, its
+    lgkmcnt waits and the LDS traffic of other waves are gone)."""
+    qs = ", ".join(f"[q{k}] \"v\"(q[{k}])" for k in range(8))
+
+    def fast(e):
+        k, j = e // 16, e % 16
+        return f"v_fmac_f64 %[acc], %[q{k}], %[one] row_newbcast:{j} row_mask:0xf bank_mask:0xf"
+
+    # plain ordered sum
+    L = []
+    for grp in range(8):
+        L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
+        L += [fast(16 * grp + t) for t in range(16)]
+    L += ["9:"]
+    add = f"""
+// acc + e_0 + e_1 + ... + e_(16 g - 1) in order, e_(16 k + j) = lane j of q[k]
+// (g <= 8; elements past the block are +0.0 no-ops)
+__device__ __forceinline__ double kc_add_dpp(double acc, const double (&q)[8], unsigned g) {{
+  const double one = 1.0;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+v"(acc), [g] "+s"(g)
+      : {qs}, [one] "v"(one)
+      : "scc");
+  return acc;
+}}
+"""
+    # dnrm2's ssq recurrence with the rescale mask (as kc_nrm2)
+    words = ["%[k0l]", "%[k0h]", "%[k1l]", "%[k1h]"]
+    L = []
+    slow = []
+    for hf in range(16):
+        w, sh = words[hf // 4], 8 * (hf % 4)
+        if hf % 2 == 0:
+            L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
+        L += [f"s_and_b32 %[t], {w}, {hex(0xff << sh)}", f"s_cbranch_scc1 {100 + hf}f"]
+        L += [fast(8 * hf + t) for t in range(8)]
+        L.append(f"{200 + hf}:")
+        slow.append(f"{100 + hf}:")
+        for t in range(8):
+            e = 8 * hf + t
+            k, j = e // 16, e % 16
+            slow += [f"s_bitcmp1_b32 {w}, {sh + t}", f"s_cbranch_scc1 {300 + e}f", fast(e), f"{500 + e}:"]
+        slow += [f"s_branch {200 + hf}b"]
+        for t in range(8):
+            e = 8 * hf + t
+            k, j = e // 16, e % 16
+            slow += [f"{300 + e}:",
+                     f"v_mov_b64 %[x], %[q{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+                     "v_mul_f64 %[tmp], %[acc], %[x]", "v_mul_f64 %[tmp], %[tmp], %[x]",
+                     "v_add_f64 %[acc], 1.0, %[tmp]", f"s_branch {500 + e}b"]
+    L += ["s_branch 9f"] + slow + ["9:"]
+    nrm2 = f"""
+// gslcblas dnrm2's ssq recurrence over e_0 .. e_(16 g - 1) (g <= 8), the
+// elements in registers as kc_add_dpp: where bit e of the 128-bit mask is
+// set, ssq = 1 + (ssq t) t, else ssq += t (as kc_nrm2)
+__device__ __forceinline__ double kc_nrm2_dpp(double acc, const double (&q)[8], unsigned g, unsigned long long k0,
+                                              unsigned long long k1) {{
+  const unsigned k0l = __builtin_amdgcn_readfirstlane((unsigned)k0), k0h = __builtin_amdgcn_readfirstlane((unsigned)(k0 >> 32));
+  const unsigned k1l = __builtin_amdgcn_readfirstlane((unsigned)k1), k1h = __builtin_amdgcn_readfirstlane((unsigned)(k1 >> 32));
+  const double one = 1.0;
+  unsigned t;
+  double tmp, x;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+v"(acc), [g] "+s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp), [x] "=&v"(x)
+      : {qs}, [one] "v"(one), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
+      : "scc");
+  return acc;
+}}
+"""
+    return add + nrm2
+
+
 def main():
     hdr = f"""// kg_chains.hpp — GENERATED by tools/gen_chains.py; do not edit.
 //
@@ -269,7 +349,7 @@ def main():
 #pragma once
 namespace kg {{
 namespace chains {{
-{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}
+{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}{emit_dpp_chains()}
 }}  // namespace chains
 }}  // namespace kg
 """

@@ -117,6 +117,67 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
       }
       t1 = __builtin_amdgcn_s_memtime();
     }
+  } else if (mode == 16 || mode == 17) {
+    // 128-element chain over DPP row_newbcast broadcasts: the staged values
+    // sit in 8 VGPR pairs (lane j of each row: element 16 k + j) and the chain
+    // is v_fmac_f64 acc, q_k[j], 1.0 (= acc + q exactly) with no memory ops;
+    // 17: seven other waves doing LDS read/modify/write traffic meanwhile
+    if (wid == 0) {
+      double q[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) q[k] = stage[16 * k + (lane & 15)];
+      const double one = 1.0;
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) {
+#define DPPSTEP(K, J) asm volatile("v_fmac_f64 %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(q[K]), "v"(one));
+#define DPPROW(K) DPPSTEP(K,0) DPPSTEP(K,1) DPPSTEP(K,2) DPPSTEP(K,3) DPPSTEP(K,4) DPPSTEP(K,5) DPPSTEP(K,6) DPPSTEP(K,7) \
+                  DPPSTEP(K,8) DPPSTEP(K,9) DPPSTEP(K,10) DPPSTEP(K,11) DPPSTEP(K,12) DPPSTEP(K,13) DPPSTEP(K,14) DPPSTEP(K,15)
+        DPPROW(0) DPPROW(1) DPPROW(2) DPPROW(3) DPPROW(4) DPPROW(5) DPPROW(6) DPPROW(7)
+#undef DPPROW
+#undef DPPSTEP
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    } else if (mode == 17) {
+      for (int r = 0; r < reps * 4; r++)
+        for (int c = lane; c < 128; c += 64) {
+          double *row = M + (size_t)(wid * 16 + (r & 15)) * LD;
+          row[c] += w[c] * w[c + 1] + row[c + 1];
+        }
+    }
+  } else if (mode == 18 || mode == 19) {
+    // dsymv-like per-lane chain: acc_lane += w_t * m_t with w wave-uniform in
+    // SGPRs (18) or broadcast from LDS (19, kc_lock_desc-like), m per lane
+    // from LDS (ds_read2 per two elements)
+    if (wid == 0) {
+      const double *mr = M + (size_t)lane * LD;
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) {
+        for (int c0 = 0; c0 < 128; c0 += 16) {
+          double mv[16], wv[16];
+#pragma unroll
+          for (int u = 0; u < 16; u++) mv[u] = mr[c0 + u];
+          if (mode == 18) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+              const unsigned long long bb = (unsigned long long)__double_as_longlong(w[c0 + u]);
+              const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)bb), hi = __builtin_amdgcn_readfirstlane((unsigned)(bb >> 32));
+              wv[u] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 16; u++) wv[u] = w[c0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 16; u++) {
+            double p;
+            if (mode == 18) asm volatile("v_mul_f64 %0, %1, %2" : "=&v"(p) : "s"(wv[u]), "v"(mv[u]));
+            else asm volatile("v_mul_f64 %0, %1, %2" : "=&v"(p) : "v"(wv[u]), "v"(mv[u]));
+            asm volatile("v_add_f64 %0, %0, %1" : "+v"(acc) : "v"(p));
+          }
+        }
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
   } else if (mode == 6) {
     if (wid == 0) {
       double b = stage[lane];
@@ -136,7 +197,7 @@ int main() {
   double *out;
   unsigned long long *ticks;
   hipMalloc(&out, 512 * sizeof(double));
-  hipMalloc(&ticks, 16 * sizeof(unsigned long long));
+  hipMalloc(&ticks, 32 * sizeof(unsigned long long));
   const size_t lds = (144 * LD + 32 + 256 + 256 + 64) * sizeof(double);
   hipFuncSetAttribute((const void *)k_bench, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int reps = 200;
@@ -144,11 +205,12 @@ int main() {
                          "kc_lock_asc alone", "4 lockstep waves", "register add chain", "kc_add_desc alone",
                          "4 indep. add chains (per add)", "inline mul+add chain", "kc_add on waves 0-3",
                          "kc_add on waves 0 and 4", "reg chain, exec=lane0", "kc_add, exec=lane0",
-                         "reg chain, sgpr operand", "sgpr chain, exec=lane0"};
-  for (int mode = 0; mode < 16; mode++) {
+                         "reg chain, sgpr operand", "sgpr chain, exec=lane0", "dpp-bcast fmac chain",
+                         "dpp-bcast chain + 7 LDS waves", "dsymv lane chain, sgpr w", "dsymv lane chain, lds w"};
+  for (int mode = 0; mode < 20; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
-    unsigned long long t[16];
+    unsigned long long t[32];
     hipMemcpy(t, ticks, sizeof(t), hipMemcpyDeviceToHost);
     printf("%-24s %8.2f ticks/element\n", names[mode], (double)t[mode] / (reps * 128.0));
   }
