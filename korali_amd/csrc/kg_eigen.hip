@@ -2927,6 +2927,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
     tri = mw2_fits(N) ? 5 : 2;
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
+  sqDpp = true;  // measured round 4: 0.495 -> 0.450 ms per C2 tridiagonalisation (bench_sq0 / bench_sq1)
   if (const char *e = getenv("KORALI_AMD_SQ_DPP")) sqDpp = *e == '1';
   if (tri == 1)
     KG_HIP(allow_dynamic_lds((const void *)k_tridiag_1wg, (int)(t1_lds_doubles(N) * sizeof(double))));

@@ -29,7 +29,7 @@ class EigenSolver {
           double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
   bool begun = false;
   int t1flags = 0;  // KORALI_AMD_T1_FLAGS: experiment switches of k_tridiag_1wg
-  bool sqDpp = false;  // k_tridiag_sq's scalar chains on registers / DPP broadcasts (KORALI_AMD_SQ_DPP)
+  bool sqDpp = true;  // k_tridiag_sq's scalar chains on registers / DPP broadcasts (KORALI_AMD_SQ_DPP=0: LDS-streamed)
   unsigned long long *trace = nullptr;  // optional device counters (k_tridiag sub-phases)
   // QR steps / Givens rotations of the last host chase (diagnostics)
   void last_counts(int &steps, int &rotations) const {
