@@ -1284,6 +1284,111 @@ __global__ void __launch_bounds__(64 * (AX3_P + 1)) k_adaptC_exact3(int N, int m
   }
 }
 
+// adaptC's exact rank-mu sums on ROW chains (round 4): every 16-lane row owns
+// one element (d, e) of the lower triangle and runs its ordered chain
+// c += fl(fl(T_kd Yc_ke) / s2) with kc_row16 (lane j of the row forms the
+// quotient of term 16 g + j: one product + the Markstein quotient, then one
+// DPP-broadcast add per term).  Workgroup = 8 waves = a 4 (d) x 8 (e) tile:
+// wave w takes d0 + w/2 and columns e0 + 4 (w%2) + row.  T rows and the Yc
+// columns of the tile are staged through LDS in chunks of AR_K terms
+// (transposed to term-contiguous rows), the next chunk's loads in flight.
+constexpr int AR_K = 128, AR_KS = AR_K + 2;
+__host__ __device__ inline int ar_row_blocks(int N) { return (N + 3) / 4; }
+__host__ __device__ inline int ar_col_blocks_upto(int rb) { return (4 * rb + 3) / 8 + 1; }  // e0 <= d0 + 3
+int ar_tiles(int N) {
+  int t = 0;
+  for (int rb = 0; rb < ar_row_blocks(N); rb++) t += std::min(ar_col_blocks_upto(rb), (N + 7) / 8);
+  return t;
+}
+template <bool kMarkstein>
+__device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int e0, int dl, int el,
+                                         const double *__restrict__ Yc, const double *__restrict__ Tt, double s2,
+                                         double (*Ts)[4][AR_KS], double (*Ys)[8][AR_KS]) {
+  const int tid = threadIdx.x, j = tid & 15;
+  const double y = kMarkstein ? 1.0 / s2 : 0.0;
+  // staging: T rows d0..d0+3 (4 x AR_K) and Yc[k][e0..e0+7] (AR_K x 8)
+  double tv, yv[2];
+  auto load = [&](int k0) {
+    {
+      const int r = tid >> 7, k = k0 + (tid & 127);
+      tv = (d0 + r < N && k < mu) ? Tt[(size_t)(d0 + r) * mu + k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int q = tid + 512 * u, k = k0 + (q >> 3), c = q & 7;
+      yv[u] = (k < mu && e0 + c < N) ? Yc[(size_t)k * N + e0 + c] : 0.0;
+    }
+  };
+  auto store = [&](int b) {
+    Ts[b][tid >> 7][tid & 127] = tv;
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int q = tid + 512 * u;
+      Ys[b][q & 7][q >> 3] = yv[u];
+    }
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int k0 = 0, b = 0; k0 < mu; k0 += AR_K, b ^= 1) {
+    const bool more = k0 + AR_K < mu;
+    if (more) load(k0 + AR_K);
+    const int gn = (min(AR_K, mu - k0) + 15) >> 4;  // (the tail's terms are 0 * 0 / s2 = +0.0)
+    for (int g = 0; g < gn; g++) {
+      const double pr = Ts[b][dl][16 * g + j] * Ys[b][el][16 * g + j];
+      double q;
+      if (kMarkstein) {
+        const double q0 = pr * y;
+        const double r = __builtin_fma(-q0, s2, pr);
+        q = __builtin_fma(r, y, q0);
+      } else {
+        q = pr / s2;
+      }
+      acc = chains::kc_row16(acc, q);
+    }
+    if (more) store(b ^ 1);
+    __syncthreads();
+  }
+  return acc;
+}
+__global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal, const double *__restrict__ Yc,
+                                                    const double *__restrict__ Tt, const double *__restrict__ pc,
+                                                    double *C, const CmaesScalars *__restrict__ sc) {
+  __shared__ double Ts[2][4][AR_KS];
+  __shared__ double Ys[2][8][AR_KS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = lane >> 4, j = lane & 15;
+  // tile index -> (row block, column block), row blocks in order
+  int t = blockIdx.x, rb = 0;
+  const int ncb = (N + 7) / 8;
+  for (;; rb++) {
+    const int c = min(ar_col_blocks_upto(rb), ncb);
+    if (t < c) break;
+    t -= c;
+  }
+  const int d0 = 4 * rb, e0 = 8 * t;
+  const int dl = wid >> 1, el = 4 * (wid & 1) + row;
+  const int d = d0 + dl, e = e0 + el;
+  const bool active = d < N && e < N && e <= d && (!diagonal || e == d);
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double s2 = sc->sigma * sc->sigma;
+  double acc = 0.0;
+  if (active) {
+    const double Cde = C[(size_t)d * N + e];
+    acc = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  }
+  const int ex = (int)((__double_as_longlong(s2) >> 52) & 0x7ff) - 1023;
+  if (__builtin_amdgcn_readfirstlane((int)(sc->rmuOutOfRange == 0u && ex >= -100 && ex <= 100)))
+    acc = ar_run<true>(acc, N, mu, d0, e0, dl, el, Yc, Tt, s2, Ts, Ys);
+  else
+    acc = ar_run<false>(acc, N, mu, d0, e0, dl, el, Yc, Tt, s2, Ts, Ys);
+  if (active && j == 0) {
+    C[(size_t)d * N + e] = acc;
+    if (e < d) C[(size_t)e * N + d] = acc;
+  }
+}
+
 // mean :603-609 and mean update :623-624.  The sum over the μ selected rows
 // is sequential per d (the reference's order); a workgroup owns MN_D columns:
 // all its threads stream the products w_i Y[i][d] into LDS, 256 rows at a
@@ -1413,6 +1518,155 @@ __global__ void __launch_bounds__(256) k_mean2(int N, int mu, const double *__re
     mean[d] = acc;
     meanUpdate[d] = (acc - prev) / sc->sigma;
   }
+}
+
+// k_mean on ROW chains (round 4): every 16-lane row of a wave owns one
+// dimension d and runs its ordered chain mean_d = sum_i w_i y_(i),d with
+// kc_row16 (one v_fmac_f64 DPP broadcast per element: lane j of the row holds
+// the product of element 16 g + j); four chains per wave, sixteen per
+// workgroup.  The selected rows are staged through LDS in chunks of MR_K
+// (coalesced 16-dimension row segments in, dimension-major out), the next
+// chunk's loads in flight while the current one is summed.
+constexpr int MR_K = 128, MR_KS = MR_K + 2;
+__global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__restrict__ Y,
+                                               const double *__restrict__ w, double *mean,
+                                               const double *__restrict__ prevMean, double *meanUpdate,
+                                               const CmaesScalars *__restrict__ sc) {
+  __shared__ double ys[2][16][MR_KS];
+  __shared__ double ws[2][MR_K];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = lane >> 4, j = lane & 15, dl = 4 * wid + row;
+  const int d0 = blockIdx.x * 16;
+  const int nch = (mu + MR_K - 1) / MR_K;
+  // chunk loads: 256 threads x 8 values of the (MR_K x 16) block, + w
+  double ld[8], wl = 0.0;
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = tid + 256 * u, k = q >> 4, c = q & 15, i = ch * MR_K + k;
+      ld[u] = (i < mu && d0 + c < N) ? Y[(size_t)i * N + d0 + c] : 0.0;
+    }
+    const int i = ch * MR_K + tid;
+    wl = (tid < MR_K && i < mu) ? w[i] : 0.0;
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = tid + 256 * u, k = q >> 4, c = q & 15;
+      ys[b][c][k] = ld[u];
+    }
+    if (tid < MR_K) ws[b][tid] = wl;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  double acc = 0.0;
+  for (int ch = 0; ch < nch; ch++) {
+    const int b = ch & 1;
+    if (ch + 1 < nch) load(ch + 1);
+    const int gn = min(MR_K, mu - ch * MR_K + 15) >> 4;  // groups of 16 (the tail is zero-padded)
+    for (int g = 0; g < gn; g++) {
+      const double q = ws[b][16 * g + j] * ys[b][dl][16 * g + j];  // the product, rounded, then added
+      acc = chains::kc_row16(acc, q);
+    }
+    if (ch + 1 < nch) store(b ^ 1);
+    __syncthreads();
+  }
+  const int d = d0 + dl;
+  if (j == 0 && d < N) {
+    mean[d] = acc;
+    meanUpdate[d] = (acc - prevMean[d]) / sc->sigma;  // (prevMean: copied by k_gather_selected)
+  }
+}
+
+// evolution paths for N <= 128 on ROW chains (round 4): one 1024-thread
+// workgroup, 64 row chains per layer (16 waves x 4 rows; two passes at
+// N = 128).  Every B value the two layers read is loaded at the start
+// (layer 1: columns of B, layer 2: rows), so the only waits between them
+// are the workgroup barriers.
+constexpr int PR_T = 1024;
+__global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, const double *__restrict__ B,
+                                                 const double *__restrict__ D, const double *__restrict__ meanUpdate,
+                                                 double *auxBDZ, double *ps, double *pc, CmaesScalars *sc) {
+  __shared__ double mu_s[128 + 16], aux_s[128 + 16], pn_s[128 + 16];
+  __shared__ int hs;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row = lane >> 4, j = lane & 15;
+  const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
+  const int G = (N + 15) >> 4;  // groups of 16 along e
+  // chains of this lane's rows: d = 64 p + 4 wid + row, p = 0, 1
+  double b1[2][8], b2[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const int d = 64 * p + 4 * wid + row;
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      const int e = 16 * g + j;
+      const bool ok = d < N && e < N;
+      b1[p][g] = ok ? B[(size_t)e * N + d] : 0.0;  // B[e][d]: aux = D^-1 B^T mu   (:627-636)
+      b2[p][g] = ok ? B[(size_t)d * N + e] : 0.0;  // B[d][e]: B aux               (:641-651)
+    }
+  }
+  for (int q = tid; q < 128 + 16; q += PR_T) {
+    mu_s[q] = q < N ? meanUpdate[q] : 0.0;
+    pn_s[q] = 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const int d = 64 * p + 4 * wid + row;
+    if (64 * p + 4 * wid >= N) break;  // (wave-uniform)
+    double acc = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; g++)
+      if (g < G) acc = chains::kc_row16(acc, b1[p][g] * mu_s[16 * g + j]);
+    if (j == 0 && d < N) {
+      const double a = acc / D[d];
+      aux_s[d] = a;
+      auxBDZ[d] = a;
+    }
+  }
+  if (tid >= N && tid < 128 + 16) aux_s[tid] = 0.0;
+  __syncthreads();
+  const double fac = sqrt(cs * (2. - cs) * effMu);
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const int d = 64 * p + 4 * wid + row;
+    if (64 * p + 4 * wid >= N) break;
+    double acc = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; g++)
+      if (g < G) acc = chains::kc_row16(acc, b2[p][g] * aux_s[16 * g + j]);
+    if (j == 0 && d < N) {
+      const double pv = (1. - cs) * ps[d] + fac * acc;
+      ps[d] = pv;
+      pn_s[d] = pv * pv;  // std::pow(x, 2.0) == x*x (CR)
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    double q[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) q[k] = pn_s[16 * k + (lane & 15)];
+    const double nrm2 = chains::kc_add_dpp(0.0, q, __builtin_amdgcn_readfirstlane((unsigned)G));
+    if (lane == 0) {
+      const double nrm = sqrt(nrm2);
+      sc->psNorm = nrm;
+      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+                                                   sc->chiSquareNumber);
+      hs = hsig;
+      sc->hsig = hsig;
+      const double a = N + 1.3, b = N + 2.0;
+      const double ccov1 = 2.0 / (a * a + effMu);
+      double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (b * b + effMu);
+      if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+      sc->ccov1 = ccov1;
+      sc->ccovmu = ccovmu;
+    }
+  }
+  __syncthreads();
+  const double fac2 = sqrt(cc * (2. - cc) * effMu);
+  for (int q = tid; q < N; q += PR_T) pc[q] = (1. - cc) * pc[q] + hs * fac2 * meanUpdate[q];
 }
 
 // evolution paths for N <= 128 (full covariance): B staged once in LDS (row
@@ -2916,8 +3170,23 @@ static int cmaes_sigma(kg_cmaes_t h) {
 }
 
 
+// KORALI_AMD_ROWCHAINS=0: the round-3 lockstep-lane mean / paths kernels (A/B)
+static bool row_chains() {
+  static const bool on = [] {
+    const char *e = getenv("KORALI_AMD_ROWCHAINS");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 static int cmaes_paths(kg_cmaes_t h, size_t generation) {
   const int N = h->N;
+  if (N <= 128 && !h->cfg.diagonal_covariance && row_chains()) {
+    hipLaunchKernelGGL(k_paths3, dim3(1), dim3(PR_T), 0, h->stream, N, (unsigned long long)generation, h->B, h->D,
+                       h->meanUpdate, h->auxBDZ, h->ps, h->pc, h->sc);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
   if (N <= 128 && !h->cfg.diagonal_covariance) {
     hipLaunchKernelGGL(k_paths2, dim3(1), dim3(256), paths2_lds_bytes(N), h->stream, N, (unsigned long long)generation,
                        h->B, h->D, h->meanUpdate, h->auxBDZ, h->ps, h->pc, h->sc);
@@ -3166,8 +3435,12 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                          h->stream, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
       KG_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu, h->Y,
-                       h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
+    if (row_chains())
+      hipLaunchKernelGGL(k_mean3, dim3((N + 15) / 16), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
+                         h->prevMean, h->meanUpdate, h->sc);
+    else
+      hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu,
+                         h->Y, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     if (h->G)
       hipLaunchKernelGGL(k_mean_gradient, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->cfg.gradient_step_size,
                          h->G, h->idx, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
@@ -3182,7 +3455,12 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
       static const bool old2 = getenv("KORALI_AMD_ADAPTC2") != nullptr;  // A/B switch
-      if (old2)
+      if (!old2 && row_chains()) {
+        // Markstein quotients when every factor is in range (k_rankmu_prep's
+        // flag, read on the device: the kernel picks the branch per launch)
+        hipLaunchKernelGGL(k_adaptC_row, dim3(ar_tiles(N)), dim3(512), 0, h->stream, N, mu,
+                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
+      } else if (old2)
         hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
                            h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
       else

@@ -273,8 +273,9 @@ def emit_dpp_chains():
         k, j = e // 16, e % 16
         return f"v_fmac_f64 %[acc], %[q{k}], %[one] row_newbcast:{j} row_mask:0xf bank_mask:0xf"
 
-    # plain ordered sum
-    L = []
+    # plain ordered sum (s_nop 1: the two wait states between a VALU write of
+    # a DPP source and its DPP read, in case the compiler formed q by VALU)
+    L = ["s_nop 1"]
     for grp in range(8):
         L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
         L += [fast(16 * grp + t) for t in range(16)]
@@ -294,7 +295,7 @@ __device__ __forceinline__ double kc_add_dpp(double acc, const double (&q)[8], u
 """
     # dnrm2's ssq recurrence with the rescale mask (as kc_nrm2)
     words = ["%[k0l]", "%[k0h]", "%[k1l]", "%[k1h]"]
-    L = []
+    L = ["s_nop 1"]
     slow = []
     for hf in range(16):
         w, sh = words[hf // 4], 8 * (hf % 4)
@@ -336,7 +337,23 @@ __device__ __forceinline__ double kc_nrm2_dpp(double acc, const double (&q)[8], 
   return acc;
 }}
 """
-    return add + nrm2
+    # one row chain step-group: every 16-lane row adds its own lanes 0..15 of q
+    L = ["s_nop 1"] + [f"v_fmac_f64 %[acc], %[q], %[one] row_newbcast:{j} row_mask:0xf bank_mask:0xf"
+                       for j in range(16)]
+    row16 = f"""
+// ROW chains: each 16-lane row r of the wave keeps its own accumulator and
+// adds lanes 16 r + 0, ..., 16 r + 15 of q in that order (four independent
+// ordered chains per wave, one VALU instruction per element)
+__device__ __forceinline__ double kc_row16(double acc, double q) {{
+  const double one = 1.0;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+v"(acc)
+      : [q] "v"(q), [one] "v"(one));
+  return acc;
+}}
+"""
+    return add + nrm2 + row16
 
 
 def main():

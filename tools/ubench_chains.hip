@@ -27,6 +27,7 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
   double *M = s;                     // 144 x 129
   double *w = M + 144 * LD + 32;     // vector (padded)
   double *stage = w + 256;           // 256
+  double *stage2 = M;                // mode 20: 512 values (rows of M, before any mode writes them)
   for (int i = tid; i < 144 * LD + 32 + 256 + 256 + 64; i += 512) s[i] = 1.0 / (1 + (i % 97));
   __syncthreads();
   double acc = 0.0;
@@ -144,6 +145,26 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
           row[c] += w[c] * w[c + 1] + row[c + 1];
         }
     }
+  } else if (mode == 20) {
+    // four independent chains per wave, one per 16-lane row: row r sums
+    // stage[128 r .. 128 r + 127] in order (per-row row_newbcast semantics;
+    // checked against the host's sequential sums below)
+    if (wid == 0) {
+      double q[8];
+      const int r = lane >> 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++) q[k] = stage2[128 * r + 16 * k + (lane & 15)];
+      const double one = 1.0;
+      t0 = __builtin_amdgcn_s_memtime();
+#define DPPSTEP(K, J) asm volatile("v_fmac_f64 %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(q[K]), "v"(one));
+#define DPPROW(K) DPPSTEP(K,0) DPPSTEP(K,1) DPPSTEP(K,2) DPPSTEP(K,3) DPPSTEP(K,4) DPPSTEP(K,5) DPPSTEP(K,6) DPPSTEP(K,7) \
+                  DPPSTEP(K,8) DPPSTEP(K,9) DPPSTEP(K,10) DPPSTEP(K,11) DPPSTEP(K,12) DPPSTEP(K,13) DPPSTEP(K,14) DPPSTEP(K,15)
+      DPPROW(0) DPPROW(1) DPPROW(2) DPPROW(3) DPPROW(4) DPPROW(5) DPPROW(6) DPPROW(7)
+#undef DPPROW
+#undef DPPSTEP
+      t1 = __builtin_amdgcn_s_memtime();
+      t1 = t0 + (t1 - t0) * reps;  // (one pass; scaled to the common per-element report)
+    }
   } else if (mode == 18 || mode == 19) {
     // dsymv-like per-lane chain: acc_lane += w_t * m_t with w wave-uniform in
     // SGPRs (18) or broadcast from LDS (19, kc_lock_desc-like), m per lane
@@ -206,13 +227,25 @@ int main() {
                          "4 indep. add chains (per add)", "inline mul+add chain", "kc_add on waves 0-3",
                          "kc_add on waves 0 and 4", "reg chain, exec=lane0", "kc_add, exec=lane0",
                          "reg chain, sgpr operand", "sgpr chain, exec=lane0", "dpp-bcast fmac chain",
-                         "dpp-bcast chain + 7 LDS waves", "dsymv lane chain, sgpr w", "dsymv lane chain, lds w"};
-  for (int mode = 0; mode < 20; mode++) {
+                         "dpp-bcast chain + 7 LDS waves", "dsymv lane chain, sgpr w", "dsymv lane chain, lds w",
+                         "4 row chains / wave (dpp)"};
+  for (int mode = 0; mode < 21; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
     unsigned long long t[32];
     hipMemcpy(t, ticks, sizeof(t), hipMemcpyDeviceToHost);
     printf("%-24s %8.2f ticks/element\n", names[mode], (double)t[mode] / (reps * 128.0));
+    if (mode == 20) {  // per-row sums vs the host's sequential sums of the same inputs
+      double o[512];
+      hipMemcpy(o, out, sizeof(o), hipMemcpyDeviceToHost);
+      int ok = 1;
+      for (int r = 0; r < 4; r++) {
+        double a = 0.0;
+        for (int e = 0; e < 128; e++) a += 1.0 / (1 + ((128 * r + e) % 97));
+        for (int l = 16 * r; l < 16 * r + 16; l++) ok &= (o[l] == a);
+      }
+      printf("  per-row chains bit-exact vs host: %s\n", ok ? "yes" : "NO");
+    }
   }
   return 0;
 }
