@@ -2948,8 +2948,10 @@ int EigenSolver::init(int N_, bool hostChase_) {
     for (int rw = (N + 255) / 256; rw <= N; rw++) {
       g_mw2_rw[N] = rw;
       if (!mw2_fits(N) || mw2_rows(N) != rw) break;  // LDS exhausted (or rows forced by the environment)
-      KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw2, (int)mw2_lds_bytes(N)));
-      KG_HIP(resident_per_cu((const void *)k_tridiag_mw2, MW2_TPB, mw2_lds_bytes(N), &perCU, nullptr));
+      KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw2<false>, (int)mw2_lds_bytes(N)));
+      KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw2<true>, (int)mw2_lds_bytes(N)));
+      KG_HIP(resident_per_cu(sqDpp ? (const void *)k_tridiag_mw2<true> : (const void *)k_tridiag_mw2<false>, MW2_TPB,
+                             mw2_lds_bytes(N), &perCU, nullptr));
       if (getenv("KORALI_AMD_DEBUG_OCC"))
         fprintf(stderr, "[korali_amd] mw2 N=%d rows=%d groups=%d lds=%zu perCU=%d cus=%d\n", N, rw, mw2_groups(N),
                 mw2_lds_bytes(N), perCU, cus);
@@ -3029,7 +3031,8 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
     unsigned long long *comm_ = comm, *trace_ = trace;
     unsigned int *errors_ = errors;
     void *args[] = {&N_, &C_, &gH_, &tau_, &d_, &sd_, &comm_, &errors_, &trace_};
-    KG_HIP(launch_resident((const void *)k_tridiag_mw2, dim3(mw2_groups(N)), dim3(MW2_TPB), args, mw2_lds_bytes(N),
+    KG_HIP(launch_resident(sqDpp ? (const void *)k_tridiag_mw2<true> : (const void *)k_tridiag_mw2<false>,
+                           dim3(mw2_groups(N)), dim3(MW2_TPB), args, mw2_lds_bytes(N),
                            s));
   } else {
     KG_HIP(hipMemsetAsync(comm, 0, tmw_comm_words(N) * sizeof(unsigned long long), s));

@@ -393,6 +393,9 @@ int mw2_groups(int N) { return (N + mw2_rows(N) - 1) / mw2_rows(N); }
 size_t mw2_lds_bytes(int N) { return mw2_lds_doubles(N, mw2_rows(N)) * sizeof(double); }
 bool mw2_fits(int N) { return N > 16 && N <= 1024 && mw2_lds_doubles(N, mw2_rows(N)) * sizeof(double) <= 150 * 1024; }
 
+// kDpp: the ssq and xv chains on register-held elements (kc_nrm2_dpp /
+// kc_add_dpp, 128 elements per call), as k_tridiag_sq<true>
+template <bool kDpp>
 __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__restrict__ C, double *gH,
                                                          double *tauOut, double *dOut, double *sdOut,
                                                          unsigned long long *comm, unsigned int *errors,
@@ -486,7 +489,14 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
       for (int b = 0; 8 * b < G; b++) {
         const unsigned gb = __builtin_amdgcn_readfirstlane((unsigned)min(8, G - 8 * b));
         const unsigned long long k0 = mskb[2 * b], k1 = (2 * b + 1 < nch) ? mskb[2 * b + 1] : 0ULL;
-        ssq = chains::kc_nrm2(ssq, lds_addr(sv + 128 * b), gb, rfl64(k0), rfl64(k1));
+        if (kDpp) {
+          double q[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) q[k] = sv[min(128 * b + 16 * k + (lane & 15), N + 63)];  // (past 16 gb: unused)
+          ssq = chains::kc_nrm2_dpp(ssq, q, gb, rfl64(k0), rfl64(k1));
+        } else {
+          ssq = chains::kc_nrm2(ssq, lds_addr(sv + 128 * b), gb, rfl64(k0), rfl64(k1));
+        }
       }
       const double alpha = prow[i + 1];
       const double xnorm = (m == 1) ? fabs(prow[i + 2]) : scale * sqrt(ssq);
@@ -596,7 +606,17 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
       __syncthreads();
       if (wid == 0) {
         const unsigned G = __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4);
-        const double xv = chains::kc_add(0.0, lds_addr(sv), G);
+        double xv = 0.0;
+        if (kDpp) {
+          for (unsigned b = 0; 8 * b < G; b++) {
+            double q[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) q[k] = sv[min((int)(128 * b) + 16 * k + (lane & 15), N + 63)];
+            xv = chains::kc_add_dpp(xv, q, __builtin_amdgcn_readfirstlane(min(8u, G - 8 * b)));
+          }
+        } else {
+          xv = chains::kc_add(0.0, lds_addr(sv), G);
+        }
         if (lane == 0) scal[5] = -(tau_i / 2.0) * xv;
       }
       __syncthreads();
