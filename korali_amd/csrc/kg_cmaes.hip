@@ -342,6 +342,132 @@ __global__ void __launch_bounds__(256) k_transform(int N, int rows, int diagonal
   }
 }
 
+// The same transform with the B operand in SCALAR registers (round 4).
+// k_transform's 4 x 2 register tile reads 3 x 16 B of LDS per lane for 16
+// FP64 instructions: at four waves per CU that is 192 B per LDS clock against
+// 128 available, so it runs at half its VALU peak.  Here a lane owns ONE
+// sample row i and a wave C columns d: per k it loads its (D o z)[i][k] from a
+// k-major copy (one coalesced 512-B wave load), and B[d][k] for its C columns
+// is wave-uniform, so it arrives through s_load into SGPRs and feeds v_mul_f64
+// as the scalar operand: no LDS traffic and no per-lane B fetch inside the K
+// loop.  k_prescale_t forms D o z (sign-flipped for the odd rows of Mirrored
+// Sampling), transposed, in one pass; the sum over k stays the reference's
+// sequential order from 0.0 with a separate multiply and add (bit-identical
+// to k_transform).  The tile goes out through LDS as coalesced row segments.
+constexpr int PS_T = 64;
+__global__ void __launch_bounds__(256) k_prescale_t(int N, int rows, int ldz, const double *__restrict__ Z,
+                                                    const double *__restrict__ D, int mirrored,
+                                                    double *__restrict__ dzT) {
+  __shared__ double t[PS_T][PS_T + 1];
+  const int i0 = blockIdx.x * PS_T, k0 = blockIdx.y * PS_T, tid = threadIdx.x;
+#pragma unroll 4
+  for (int r = 0; r < PS_T * PS_T / 256; r++) {
+    const int q = tid + 256 * r, ii = q / PS_T, kk = q % PS_T, i = i0 + ii, k = k0 + kk;
+    double z = 0.0;
+    if (i < rows && k < N) {
+      z = Z[(size_t)(mirrored ? (i >> 1) : i) * N + k];
+      if (mirrored && (i & 1)) z = -z;
+      z = D[k] * z;
+    }
+    t[ii][kk] = z;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = 0; r < PS_T * PS_T / 256; r++) {
+    const int q = tid + 256 * r, kk = q / PS_T, ii = q % PS_T, k = k0 + kk;
+    if (k < N) dzT[(size_t)k * ldz + i0 + ii] = t[ii][kk];  // (rows past `rows`: +0.0)
+  }
+}
+inline int sc_ldz(size_t rows) { return (int)((rows + 63) / 64 * 64); }
+template <int C>
+inline unsigned trs_grid(int rows, int N) {
+  const int nrt = (rows + 63) / 64, ncg = (N + 4 * C - 1) / (4 * C);
+  return (unsigned)(((nrt + TR_XCD - 1) / TR_XCD) * TR_XCD * ncg);
+}
+inline int transform_width() {  // (read per handle: tests switch it per case)
+  const char *e = getenv("KORALI_AMD_TRANSFORM_SC");
+  if (!e || !*e) return 0;
+  const int v = atoi(e);
+  return (v == 8 || v == 16) ? v : 0;
+}
+template <int C>
+__global__ void __launch_bounds__(256) k_transform_sc(int N, int rows, int ldz, const double *__restrict__ dzT,
+                                                      const double *__restrict__ B, const double *__restrict__ mean,
+                                                      CmaesScalars *__restrict__ sc, const double *__restrict__ lb,
+                                                      const double *__restrict__ ub, double *__restrict__ X,
+                                                      double *__restrict__ BDZ, int *__restrict__ infeas,
+                                                      int no_reserve) {
+  constexpr int WC = 4 * C;  // columns per workgroup (4 waves x C)
+  __shared__ double so[64][WC + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware order (as k_transform): the column groups of one 64-row tile
+  // run on one XCD, so its (D o z) rows come from HBM once
+  const int ncg = (N + WC - 1) / WC;
+  const int xcd = blockIdx.x % TR_XCD, j = blockIdx.x / TR_XCD;
+  const int rt = (j / ncg) * TR_XCD + xcd, cg = j % ncg;
+  const int i0 = rt * 64;
+  if (i0 >= rows) return;
+  const int d0 = cg * WC + w * C;
+  const double *Bc[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) Bc[c] = B + (size_t)min(d0 + c, N - 1) * N;  // (columns past N: discarded)
+  double acc[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) acc[c] = 0.0;
+  const double *zp = dzT + i0 + lane;
+  auto step = [&](double z, int k) {
+    double t[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) t[c] = Bc[c][k] * z;
+#pragma unroll
+    for (int c = 0; c < C; c++) acc[c] += t[c];
+  };
+  // groups of 4 k, the next group's z loads in flight while this one is
+  // summed (two register sets in turn: a copy between them would wait for
+  // the loads).  Loads past the last group are clamped to row N - 1 rather
+  // than branched around (a branch makes the compiler wait for them early).
+  const int N4 = N & ~3;
+  double za[4], zb[4];
+  auto load4 = [&](double *z, int k) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) z[u] = zp[(size_t)min(k + u, N - 1) * ldz];
+  };
+  if (N4) load4(za, 0);
+  int k = 0;
+  for (; k + 8 <= N4; k += 8) {
+    load4(zb, k + 4);
+#pragma unroll
+    for (int u = 0; u < 4; u++) step(za[u], k + u);
+    load4(za, k + 8);
+#pragma unroll
+    for (int u = 0; u < 4; u++) step(zb[u], k + 4 + u);
+  }
+  if (k < N4) {  // one group left (already in za)
+#pragma unroll
+    for (int u = 0; u < 4; u++) step(za[u], k + u);
+  }
+  for (int k = N4; k < N; k++) step(zp[(size_t)k * ldz], k);
+#pragma unroll
+  for (int c = 0; c < C; c++) so[lane][w * C + c] = acc[c];
+  __syncthreads();
+  const double sigma = sc->sigma;
+  for (int q = tid; q < 64 * WC; q += 256) {
+    const int r = q / WC, cc = q % WC, i = i0 + r, d = cg * WC + cc;
+    if (i >= rows || d >= N) continue;
+    const double bdz = so[r][cc];
+    const double x = mean[d] + sigma * bdz;
+    X[(size_t)i * N + d] = x;
+    if (BDZ) BDZ[(size_t)i * N + d] = bdz;
+    if (!isfinite(x) || x < lb[d] || x > ub[d]) {
+      if (no_reserve)
+        atomicOr(&sc->errors, KG_ERR_DRAW_GUARD);
+      else
+        atomicOr(&infeas[i], 1);
+    }
+  }
+}
+
 // resampling (prepareGeneration :443-460): candidate i takes the next block
 // whose draw is feasible, or any block once the global infeasible counter
 // reaches Max Infeasible Resamplings.  Sequential (one thread): runs only
@@ -2375,6 +2501,9 @@ struct kg_cmaes_s {
   CmaesScalars *sc = nullptr;
   double *covPart = nullptr, *Y = nullptr;
   double *Yc = nullptr, *Tt = nullptr;  // exact rank-mu factors (k_rankmu_prep)
+  double *dzT = nullptr;                // k_transform_sc: D o z, k-major (ldz rows per k)
+  size_t dzTRows = 0;
+  int trW = 0;                          // k_transform_sc columns per wave (0: k_transform)
   EigenSolver eig;
   int *infeas = nullptr, *assign = nullptr;
   int *selEnd = nullptr;  // a resampling round's end: [next unassigned sample, uniform window exhausted]
@@ -2701,6 +2830,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   h->r0 = h->shardRank * (L / h->shards);
   h->r1 = h->r0 + L / h->shards;
   h->mirrored = cfg->mirrored_sampling != 0;
+  h->trW = transform_width();
   h->blocks = (h->mirrored ? (size_t)L / 2 : (size_t)L) + h->R;
   const size_t rows = (size_t)L + h->R;
   const size_t xrows = h->mirrored ? 2 * h->blocks : rows;  // transformed rows (Xall, infeasibility flags)
@@ -2822,7 +2952,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G,
                   (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused,
                   (void *)h->selEnd, (void *)h->V, (void *)h->auxC, (void *)h->violDev, (void *)h->pairI,
-                  (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev})
+                  (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev, (void *)h->dzT})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -2896,6 +3026,41 @@ int kg_cmaes_begin_sample(kg_cmaes_t h) {
   return 0;
 }
 
+// x = m + sigma B (D o z) for `rows` rows into Xo / Bo (+ infeasibility flags):
+// k_transform_sc (scalar-operand B, KORALI_AMD_TRANSFORM_SC = 8 | 16 columns
+// per wave; 16 spills SGPRs) or k_transform (LDS-tiled, KORALI_AMD_TRANSFORM_SC = 0); the
+// diagonal covariance always takes k_transform's epilogue-only path
+static int cmaes_transform(kg_cmaes_t h, size_t rows, double *Xo, double *Bo, int no_reserve, int mirrored) {
+  const int N = h->N, W = h->cfg.diagonal_covariance ? 0 : h->trW;
+  if (rows == 0) return 0;
+  if (W == 0) {
+    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)rows, N)), dim3(256), 0, h->stream, N,
+                       (int)rows, h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, Xo, Bo,
+                       h->infeas, no_reserve, mirrored);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
+  const int ldz = sc_ldz(rows);
+  if ((size_t)ldz > h->dzTRows) {
+    if (h->dzT) (void)hipFree(h->dzT);
+    h->dzT = nullptr;
+    h->dzTRows = 0;
+    if (dalloc(&h->dzT, (size_t)ldz * N)) return 1;
+    h->dzTRows = (size_t)ldz;
+  }
+  hipLaunchKernelGGL(k_prescale_t, dim3((unsigned)(ldz / PS_T), (unsigned)((N + PS_T - 1) / PS_T)), dim3(256), 0,
+                     h->stream, N, (int)rows, ldz, h->Z, h->D, mirrored, h->dzT);
+  KG_HIP(hipGetLastError());
+  if (W == 8)
+    hipLaunchKernelGGL(k_transform_sc<8>, dim3(trs_grid<8>((int)rows, N)), dim3(256), 0, h->stream, N, (int)rows,
+                       ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
+  else
+    hipLaunchKernelGGL(k_transform_sc<16>, dim3(trs_grid<16>((int)rows, N)), dim3(256), 0, h->stream, N, (int)rows,
+                       ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
+  KG_HIP(hipGetLastError());
+  return 0;
+}
+
 // Overflow guard of a generation without finite bounds (and no discrete
 // variables): the reference redraws a sample only when it is not finite
 // (optimizer.cpp.base:5-14), which needs |m| + sigma |B (D o z)| to overflow.
@@ -2958,7 +3123,6 @@ static int ensure_redraw_buffers(kg_cmaes_t h) {
 static int cmaes_resample(kg_cmaes_t h) {
   const int N = h->N, L = h->lam;
   const size_t nb = h->blocks, xr = h->mirrored ? 2 * nb : nb;
-  const unsigned tgrid = tr_grid<32, 64>((int)xr, N);
   int i0 = 0;
   for (int round = 0;; round++) {
     if (round > 0) {
@@ -2969,10 +3133,7 @@ static int cmaes_resample(kg_cmaes_t h) {
     {
       Stage st(h, "transform");
       KG_HIP(hipMemsetAsync(h->infeas, 0, xr * sizeof(int), h->stream));
-      hipLaunchKernelGGL((k_transform<32, 64>), dim3(tgrid), dim3(256), 0, h->stream, N, (int)xr,
-                         h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, h->Xall,
-                         h->BDZall, h->infeas, 0, h->mirrored ? 1 : 0);
-      KG_HIP(hipGetLastError());
+      if (cmaes_transform(h, xr, h->Xall, h->BDZall, 0, h->mirrored ? 1 : 0)) return 1;
       if (h->hasDiscrete) {
         if (h->uniform.peek_uniforms(h->ubuf, h->ucap, h->stream)) return 1;
         hipLaunchKernelGGL(k_discrete_select, dim3(1), dim3(256), 2 * N * sizeof(double), h->stream, N, L, i0, (int)nb,
@@ -3065,10 +3226,7 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     // 32 x 64 tiles, 4 x 2 outputs per thread: larger register tiles drop the
     // kernel to 2 waves per SIMD and measured slower at C4 (1.96 / 2.25 ms
     // for 32 x 128 / 64 x 64 against 1.73 ms)
-    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tr_grid<32, 64>((int)trows, N)), dim3(256), 0, h->stream, N,
-                       (int)trows, h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, xo, bo,
-                       h->infeas, 1, h->mirrored ? 1 : 0);
-    KG_HIP(hipGetLastError());
+    if (cmaes_transform(h, trows, xo, bo, 1, h->mirrored ? 1 : 0)) return 1;
   }
   {
     Stage st(h, "rng_consume");
@@ -3284,15 +3442,12 @@ static int ccm_redraw(kg_cmaes_t h, const std::vector<int> &list) {
   const int N = h->N, nl = (int)list.size();
   if (ensure_redraw_buffers(h)) return 1;  // (unbounded variables: no reserve rows yet)
   const size_t nb = h->blocks;
-  const unsigned tgrid = tr_grid<32, 64>((int)nb, N);
   KG_HIP(hipMemcpyAsync(h->listDev, list.data(), nl * sizeof(int), hipMemcpyHostToDevice, h->stream));
   int k0 = 0;
   for (;;) {
     if (h->normal.polar_normals(h->Z, nb * N, N, h->blockEnd, h->stream)) return 1;
     KG_HIP(hipMemsetAsync(h->infeas, 0, nb * sizeof(int), h->stream));
-    hipLaunchKernelGGL((k_transform<32, 64>), dim3(tgrid), dim3(256), 0, h->stream, N, (int)nb,
-                       h->cfg.diagonal_covariance, h->Z, h->B, h->D, h->mean, h->sc, h->lb, h->ub, h->Xall, h->BDZall,
-                       h->infeas, 0, 0);
+    if (cmaes_transform(h, nb, h->Xall, h->BDZall, 0, 0)) return 1;
     hipLaunchKernelGGL(k_select_list, dim3(1), dim3(64), 0, h->stream, nl, k0, (int)nb,
                        h->cfg.max_infeasible_resamplings, h->infeas, h->assign, h->usedBlocks, h->selEnd, h->sc);
     const size_t tot = (size_t)(nl - k0) * N;

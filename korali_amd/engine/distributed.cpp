@@ -9,6 +9,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -16,7 +17,10 @@
 #include <cstdint>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 
@@ -151,14 +155,85 @@ class Bootstrap {
   }
 };
 
+// Abort channel: a second star of TCP connections (bootstrap port + 1)
+// watched by a thread of every rank.  A rank that leaves on an exception
+// sends 'A' (the root relays it to every other rank), one that finishes
+// sends 'B'; a connection closed without 'B' (the process died) counts as
+// 'A'.  On 'A' the rank's transport is aborted (RCCL: ncclCommAbort, which
+// ends the collective kernels waiting for the failed rank; Host: the
+// bootstrap sockets are shut down, which ends a blocked recv) and every
+// later collective or engine check throws.  The reference's MPI conduit gets
+// the same from MPI_Abort on a worker error.
+class Watchdog {
+ public:
+  Watchdog(int rank, int world, int port, std::function<void()> onAbort)
+      : links_(rank, world, port), onAbort_(std::move(onAbort)) {
+    if (world > 1) th_ = std::thread([this] { run(); });
+  }
+  ~Watchdog() { close(std::uncaught_exceptions() > 0); }
+  bool aborted() const { return aborted_.load(); }
+  // leave: 'A' when failing, else 'B'; joins the watcher
+  void close(bool failing) {
+    if (closed_.exchange(true)) return;
+    stop_ = true;
+    const char c = failing ? 'A' : 'B';
+    for (size_t k = 0; k < links_.peers.size(); k++)
+      if (links_.peers[k] >= 0) (void)::send(links_.peers[k], &c, 1, MSG_NOSIGNAL);
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  Bootstrap links_;
+  std::function<void()> onAbort_;
+  std::thread th_;
+  std::atomic<bool> stop_{false}, aborted_{false}, closed_{false};
+  void trigger(int from) {
+    if (aborted_.exchange(true)) return;
+    const char c = 'A';
+    if (links_.rank == 0)  // relay to every other rank
+      for (size_t k = 1; k < links_.peers.size(); k++)
+        if ((int)k != from && links_.peers[k] >= 0) (void)::send(links_.peers[k], &c, 1, MSG_NOSIGNAL);
+    if (onAbort_) onAbort_();
+  }
+  void run() {
+    std::vector<pollfd> fds;
+    std::vector<int> who;
+    for (size_t k = 0; k < links_.peers.size(); k++)
+      if (links_.peers[k] >= 0) {
+        fds.push_back({links_.peers[k], POLLIN, 0});
+        who.push_back(links_.rank == 0 ? (int)k : 0);
+      }
+    while (!stop_) {
+      if (::poll(fds.data(), fds.size(), 100) <= 0) continue;
+      for (size_t i = 0; i < fds.size(); i++) {
+        if (fds[i].fd < 0 || !fds[i].revents) continue;
+        char c = 0;
+        const ssize_t k = ::recv(fds[i].fd, &c, 1, 0);
+        if (k == 1 && c == 'B') {
+          fds[i].fd = -1;  // that rank finished: its close is not a failure
+          continue;
+        }
+        fds[i].fd = -1;
+        trigger(who[i]);
+      }
+    }
+  }
+};
+
 class HostCollective : public Collective {
  public:
   Bootstrap boot;
-  HostCollective(int r, int w, int port) : boot(r, w, port) {
+  Watchdog dog;
+  HostCollective(int r, int w, int port)
+      : boot(r, w, port), dog(r, w, port + 1, [this] {
+          for (int fd : boot.peers)
+            if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // a blocked recv returns: the collective throws
+        }) {
     rank = r;
     world = w;
   }
   std::string transport() const override { return "Host"; }
+  bool failed() const override { return dog.aborted(); }
   void allGather(const SolverBuffer &b, size_t count) override {
     std::vector<double> v((size_t)world * count);
     b.get(v.data(), v.size() * sizeof(double));
@@ -190,6 +265,7 @@ typedef int (*CommInitRankFn)(void **, int, NcclId, int);
 typedef int (*AllGatherFn)(const void *, void *, size_t, int, void *, void *);
 typedef int (*AllReduceFn)(const void *, void *, size_t, int, int, void *, void *);
 typedef int (*CommDestroyFn)(void *);
+typedef int (*CommAbortFn)(void *);
 typedef const char *(*ErrorStringFn)(int);
 
 class RcclCollective : public Collective {
@@ -201,7 +277,10 @@ class RcclCollective : public Collective {
   AllGatherFn allGatherFn = nullptr;
   AllReduceFn allReduceFn = nullptr;
   CommDestroyFn commDestroy = nullptr;
+  CommAbortFn commAbort = nullptr;
   ErrorStringFn errorString = nullptr;
+  std::mutex commMu;  // comm creation vs the watchdog's abort
+  std::unique_ptr<Watchdog> dog;
 
   RcclCollective(int r, int w, int port) : boot(r, w, port) {
     rank = r;
@@ -215,26 +294,41 @@ class RcclCollective : public Collective {
     allReduceFn = (AllReduceFn)dlsym(lib, "ncclAllReduce");
     commDestroy = (CommDestroyFn)dlsym(lib, "ncclCommDestroy");
     errorString = (ErrorStringFn)dlsym(lib, "ncclGetErrorString");
-    if (!getUniqueId || !commInitRank || !allGatherFn || !allReduceFn || !commDestroy || !errorString)
+    commAbort = (CommAbortFn)dlsym(lib, "ncclCommAbort");
+    if (!getUniqueId || !commInitRank || !allGatherFn || !allReduceFn || !commDestroy || !errorString || !commAbort)
       dfail("librccl.so lacks an nccl* entry point");
+    dog.reset(new Watchdog(r, w, port + 1, [this] {
+      std::lock_guard<std::mutex> g(commMu);
+      if (comm) commAbort(comm);  // the collective kernels waiting for the failed rank end
+      comm = nullptr;
+    }));
   }
   ~RcclCollective() override {
-    if (comm) commDestroy(comm);
+    const bool failing = std::uncaught_exceptions() > 0;
+    dog->close(failing);  // (tells the other ranks first)
+    std::lock_guard<std::mutex> g(commMu);
+    if (comm) (failing ? commAbort : commDestroy)(comm);
   }
   std::string transport() const override { return "RCCL"; }
+  bool failed() const override { return dog->aborted(); }
   void check(int rc, const char *what) {
+    if (dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
     if (rc != 0) dfail(std::string(what) + ": " + errorString(rc));
   }
   // the communicator is created at the first collective, after the solver
   // handle has selected its GPU (RCCL binds the calling thread's device)
   void ensureComm() {
+    if (dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
     if (comm) return;
     NcclId id{};
     if (rank == 0) check(getUniqueId(&id), "ncclGetUniqueId");
     std::vector<NcclId> all((size_t)world);
     all[(size_t)rank] = id;
     boot.gatherToAll(all.data(), sizeof(NcclId));  // (only the root's entry is used)
-    check(commInitRank(&comm, world, all[0], rank), "ncclCommInitRank");
+    void *c = nullptr;
+    check(commInitRank(&c, world, all[0], rank), "ncclCommInitRank");
+    std::lock_guard<std::mutex> g(commMu);
+    comm = c;
   }
   void allGather(const SolverBuffer &b, size_t count) override {
     ensureComm();
@@ -266,11 +360,23 @@ std::unique_ptr<Collective> makeCollective(const std::string &transport, int por
   dfail("'Transport' must be 'RCCL' or 'Host'");
 }
 
-CollectiveCheck collectiveSelfTest(int port, const std::vector<double> &block) {
+CollectiveCheck collectiveSelfTest(int port, const std::vector<double> &block, int failRank) {
   std::unique_ptr<Collective> c = makeCollective("host", port);
   CollectiveCheck r;
   r.rank = c->rank;
   r.world = c->world;
+  if (failRank >= 0) {
+    // failure propagation: rank failRank throws (its collective leaves with
+    // 'A'); every other rank waits for its watchdog to report it
+    if (c->rank == failRank) dfail("rank " + std::to_string(failRank) + " failed on purpose");
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!c->failed()) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) dfail("the peer failure was not reported");
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    r.peerFailed = true;
+    return r;
+  }
   const size_t n = block.size();
   auto hostBuffer = [](std::vector<double> &v) {
     SolverBuffer b;

@@ -48,6 +48,8 @@ class Collective {
   // element-wise MAX of n int64 (the bit patterns of doubles; exact gather)
   virtual void allReduceMaxI64(const SolverBuffer &b, size_t n) = 0;
   virtual void barrier() = 0;
+  // another rank failed (its abort reached this rank's watchdog)
+  virtual bool failed() const { return false; }
 };
 
 // rank / world from the environment (RANK, WORLD_SIZE); the TCP bootstrap on

@@ -1913,6 +1913,8 @@ void runExperiment(Experiment &e, Conduit &conduit) {
     }
     const auto g0 = std::chrono::steady_clock::now();
     solver.runGeneration(gen);
+    // (a peer's failure aborts this rank's collectives: their results are void)
+    if (conduit.dist && conduit.dist->failed()) fail("Another rank of the Distributed conduit failed.");
     const auto g1 = std::chrono::steady_clock::now();
     if (consoleFreq > 0 && gen % consoleFreq == 0) {
       // printAfter reads solver state from the device: only when it prints

@@ -149,8 +149,11 @@ void conduitEvaluate(size_t jobs, size_t n, const std::function<void(size_t)> &b
 struct CollectiveCheck {
   int rank = 0, world = 1;
   std::vector<double> gathered, summed, maxed;
+  bool peerFailed = false;
 };
-CollectiveCheck collectiveSelfTest(int port, const std::vector<double> &block);
+// failRank >= 0: that rank throws; the others return once their watchdog
+// reports the failure (peerFailed)
+CollectiveCheck collectiveSelfTest(int port, const std::vector<double> &block, int failRank = -1);
 
 // Bayesian/Reference likelihood models (likelihood.cpp,
 // reference.cpp.base:25-229): the log-likelihood of reference data y given the

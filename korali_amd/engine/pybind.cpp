@@ -236,11 +236,11 @@ PYBIND11_MODULE(libkorali, m) {
   });
 
   // test hook: the Distributed conduit's collectives on host data (Host transport)
-  m.def("_collective_selftest", [](int port, const std::vector<double> &block) {
+  m.def("_collective_selftest", [](int port, const std::vector<double> &block, int failRank) {
     korali::CollectiveCheck r;
     {
       py::gil_scoped_release nogil;
-      r = korali::collectiveSelfTest(port, block);
+      r = korali::collectiveSelfTest(port, block, failRank);
     }
     py::dict d;
     d["rank"] = r.rank;
@@ -248,8 +248,9 @@ PYBIND11_MODULE(libkorali, m) {
     d["gathered"] = r.gathered;
     d["summed"] = r.summed;
     d["maxed"] = r.maxed;
+    d["peer_failed"] = r.peerFailed;
     return d;
-  });
+  }, py::arg("port"), py::arg("block"), py::arg("fail_rank") = -1);
 
   // test hooks: the continuous agent's policy description and initial
   // hyperparameters (pinned against the reference's VRACER result files)

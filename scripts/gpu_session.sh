@@ -19,6 +19,7 @@ step() {
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     rs) step rs 600 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests/test_gpu_cmaes.py -x -v --timeout 300 --timeout-method thread -k "resampl or overflow or interleaved or mirrored or discrete" ;;
+    diag) K="test_mirrored_sampling_matches_oracle_bit_exact"; step diag_sq0 300 env KORALI_AMD_SQ_DPP=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ; step diag_row0 300 env KORALI_AMD_ROWCHAINS=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ; step diag_both0 300 env KORALI_AMD_ROWCHAINS=0 KORALI_AMD_SQ_DPP=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ;;
     ub) step ub 120 ./tools/ubench_chains ;;
     rowab) step bench_row0 300 env KORALI_AMD_ROWCHAINS=0 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_row1 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
     sqab) step bench_sq0 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_sq1 300 env KORALI_AMD_SQ_DPP=1 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;

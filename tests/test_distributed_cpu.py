@@ -22,7 +22,11 @@ rank, n = int(sys.argv[1]), int(sys.argv[2])
 rng = np.random.default_rng(100 + rank)
 block = rng.standard_normal(n)
 block[0] = -0.0 if rank % 2 else float(rank)  # signed zero: its bits are INT64_MIN
-r = libkorali._collective_selftest(int(sys.argv[3]), block.tolist())
+try:
+    r = libkorali._collective_selftest(int(sys.argv[3]), block.tolist(), int(sys.argv[4]))
+except Exception as e:
+    print(json.dumps({"error": str(e)}))
+    sys.exit(3)
 print(json.dumps(r))
 """
 
@@ -33,18 +37,18 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(world, n):
+def run_ranks(world, n, fail_rank=-1):
     port = free_port()
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port - 1), PYTHONPATH=ROOT)
-        procs.append(subprocess.Popen([sys.executable, "-c", RANK_SCRIPT, str(rank), str(n), "0"], env=env,
+        procs.append(subprocess.Popen([sys.executable, "-c", RANK_SCRIPT, str(rank), str(n), "0", str(fail_rank)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []
-    for p in procs:
+    for rank, p in enumerate(procs):
         o, e = p.communicate(timeout=120)
-        assert p.returncode == 0, e[-2000:]
+        assert p.returncode == (3 if rank == fail_rank else 0), e[-2000:]
         outs.append(__import__("json").loads(o.strip().splitlines()[-1]))
     return outs
 
@@ -72,6 +76,19 @@ def test_host_transport_collectives(world, n):
         assert np.array_equal(np.array(o["gathered"]), gathered)
         assert np.array_equal(np.array(o["summed"]), summed)  # bit-identical on every rank
         assert np.array_equal(np.array(o["maxed"]).view(np.int64), maxed.view(np.int64))
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 2), (3, 0)])
+def test_rank_failure_reaches_every_rank(world, fail_rank):
+    """A rank that fails tells the others over the abort channel (the
+    watchdog that ends an RCCL rank's collectives with ncclCommAbort): every
+    other rank sees the failure instead of waiting for it forever."""
+    outs = run_ranks(world, 4, fail_rank)
+    for rank, o in enumerate(outs):
+        if rank == fail_rank:
+            assert "failed on purpose" in o["error"]
+        else:
+            assert o["peer_failed"] is True
 
 
 def cmaes_experiment():

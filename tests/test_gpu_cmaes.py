@@ -235,6 +235,42 @@ def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
         assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
 
 
+@pytest.mark.parametrize("Nv,lam,mirrored,bound", [(3, 8, False, None), (10, 64, False, None), (13, 100, True, None),
+                                                  (128, 4096, False, None), (67, 300, False, 1.0),
+                                                  (10, 64, True, 0.5)])
+def test_scalar_operand_transform_bit_exact(monkeypatch, Nv, lam, mirrored, bound):
+    """k_transform_sc (B in scalar registers, D o z prescaled k-major) forced:
+    populations, selections and the updated state bit for bit against the
+    oracle, for N not a multiple of the 4-k groups or of the 32-column
+    workgroup, row counts not a multiple of 64, Mirrored Sampling and the
+    bounded redraw rounds (k_select over the transformed reserve)."""
+    monkeypatch.setenv("KORALI_AMD_TRANSFORM_SC", "8")
+    seed = 99
+    x0 = np.full(Nv, 0.5 if bound == 0.5 else 0.0)
+    o = R.CMAES(Nv, lam, 0)
+    o["Initial Value"], o["Initial Standard Deviation"] = x0, np.full(Nv, 0.3 if bound == 0.5 else 1.0)
+    kw = {}
+    if bound is not None:
+        o["Lower Bound"], o["Upper Bound"] = np.full(Nv, -bound), np.full(Nv, bound)
+        kw = dict(lower_bound=np.full(Nv, -bound), upper_bound=np.full(Nv, bound))
+    if mirrored:
+        o.option("Mirrored Sampling", 1)
+    R.lib().kr_rng_seed(o.rng(0).ptr, seed)
+    R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
+    dev = device_solver(Nv, lam, initial_value=x0, initial_std=np.full(Nv, 0.3 if bound == 0.5 else 1.0),
+                        mirrored=mirrored, normal_seed=seed, uniform_seed=seed + 1, **kw)
+    for g in range(1, 5):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        dev.synchronize()
+        assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
+        assert np.array_equal(dev.sorting_index(), o.sorting_index()), g
+        for key in ("Current Mean", "Covariance Matrix", "Axis Lengths"):
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        assert dev["Infeasible Sample Count"][0] == o["Infeasible Sample Count"][0], g
+    dev.close()
+
+
 @pytest.mark.parametrize("Nv,lam,bound,gens,diag", [(8, 16, None, 20, False), (8, 16, 1.5, 20, False),
                                                     (32, 256, 3.0, 6, False), (16, 64, 2.0, 10, True)])
 def test_mirrored_sampling_matches_oracle_bit_exact(Nv, lam, bound, gens, diag):

@@ -8,7 +8,10 @@ bit-identical and mean / covariance / sigma within the partial-sum
 tolerance, the 6-generation run close) and every rank's state against rank
 0's (bit-identical).
 
-    distributed_check.py <out dir> cmaes|tmcmc builtin|host RCCL|Host
+    distributed_check.py <out dir> cmaes|tmcmc builtin|host|c4 RCCL|Host
+
+model c4 (CMA-ES only): the C4 shape, 512-dim negative Ackley at
+lambda = 65536 (BASELINE.json configs[3]), after 1 and 2 generations.
 """
 import json
 import os
@@ -37,18 +40,20 @@ def experiment(solver, model, gens):
     e["File Output"]["Enabled"] = False
     e["Console Output"]["Verbosity"] = "Silent"
     if solver == "cmaes":
-        N = 16
+        N = 512 if model == "c4" else 16
         e["Problem"]["Type"] = "Optimization"
-        if model == "builtin":
+        if model == "c4":
+            e["Problem"]["Objective Kernel"] = "Negative Ackley"
+        elif model == "builtin":
             e["Problem"]["Objective Kernel"] = "Negative Rosenbrock"
         else:
             e["Problem"]["Objective Function"] = negative_rosenbrock
         for i in range(N):
             e["Variables"][i]["Name"] = f"X{i}"
-            e["Variables"][i]["Initial Value"] = 0.0
+            e["Variables"][i]["Initial Value"] = 2.0 if model == "c4" else 0.0
             e["Variables"][i]["Initial Standard Deviation"] = 1.0
         e["Solver"]["Type"] = "Optimizer/CMAES"
-        e["Solver"]["Population Size"] = 64
+        e["Solver"]["Population Size"] = 65536 if model == "c4" else 64
         e["Solver"]["Covariance Update"] = "MFMA"  # the rank-mu tiles the sharded update sums per shard
         e["Solver"]["Termination Criteria"]["Max Generations"] = gens
     else:
@@ -80,7 +85,7 @@ def main():
     out, solver, model, transport = sys.argv[1:5]
     rank = int(os.environ["RANK"])
     result = {}
-    for gens in (1, 6):  # one generation: same samples; six: the run as a whole
+    for gens in ((1, 2) if model == "c4" else (1, 6)):  # one generation: same samples; six: the run as a whole
         k = korali.Engine()
         k["Conduit"]["Type"] = "Distributed"
         k["Conduit"]["Transport"] = transport
