@@ -1690,7 +1690,7 @@ __device__ __forceinline__ double lds_chain_add(double acc, const double *p, int
 "s_cmp_lt_i32 %[rem], 6\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b5]\n"
 "s_cmp_lt_i32 %[rem], 7\n s_cbranch_scc1 9f\n v_add_f64 %[acc], %[acc], %[b6]\n"
 "9:\n s_waitcnt lgkmcnt(0)\n"
-      : [acc] "+v"(acc), [rem] "+s"(rem), [a0] "=&v"(a[0]), [a1] "=&v"(a[1]), [a2] "=&v"(a[2]), [a3] "=&v"(a[3]), [a4] "=&v"(a[4]), [a5] "=&v"(a[5]), [a6] "=&v"(a[6]), [a7] "=&v"(a[7]), [b0] "=&v"(b[0]), [b1] "=&v"(b[1]), [b2] "=&v"(b[2]), [b3] "=&v"(b[3]), [b4] "=&v"(b[4]), [b5] "=&v"(b[5]), [b6] "=&v"(b[6]), [b7] "=&v"(b[7])
+      : [acc] "+&v"(acc), [rem] "+&s"(rem), [a0] "=&v"(a[0]), [a1] "=&v"(a[1]), [a2] "=&v"(a[2]), [a3] "=&v"(a[3]), [a4] "=&v"(a[4]), [a5] "=&v"(a[5]), [a6] "=&v"(a[6]), [a7] "=&v"(a[7]), [b0] "=&v"(b[0]), [b1] "=&v"(b[1]), [b2] "=&v"(b[2]), [b3] "=&v"(b[3]), [b4] "=&v"(b[4]), [b5] "=&v"(b[5]), [b6] "=&v"(b[6]), [b7] "=&v"(b[7])
       : [va] "v"(va)
       : "scc", "memory");
   return acc;

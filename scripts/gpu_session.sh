@@ -20,6 +20,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     rs) step rs 600 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests/test_gpu_cmaes.py -x -v --timeout 300 --timeout-method thread -k "resampl or overflow or interleaved or mirrored or discrete" ;;
     diag) K="test_mirrored_sampling_matches_oracle_bit_exact"; step diag_sq0 300 env KORALI_AMD_SQ_DPP=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ; step diag_row0 300 env KORALI_AMD_ROWCHAINS=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ; step diag_both0 300 env KORALI_AMD_ROWCHAINS=0 KORALI_AMD_SQ_DPP=0 python -u -m pytest tests/test_gpu_cmaes.py -x -q --timeout 250 --timeout-method thread -k "$K" ;;
+    trsc) step trsc_t 600 python -u -m pytest tests/test_gpu_cmaes.py -x -v --timeout 300 --timeout-method thread -k scalar_operand && step trsc_b0 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step trsc_b8 300 env KORALI_AMD_TRANSFORM_SC=8 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step trsc_c4 300 env KORALI_AMD_TRANSFORM_SC=8 python -u -m pytest tests/test_gpu_baseline_shapes.py -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two && step trsc_c4b 300 env KORALI_AMD_TRANSFORM_SC=8 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    dist) step dist 900 python -u -m pytest tests/test_gpu_distributed.py -x -v --timeout 600 --timeout-method thread ;;
+    dppc) step dppc 120 ./tools/check_dpp_chains && step tri 900 python -u -m pytest tests/test_gpu_cmaes.py -v --timeout 300 --timeout-method thread -k tridiagonalisation_kernels ;;
+    occsys) step occ_sys 300 env KORALI_AMD_HIP_RUNTIME=system KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two && step occ_one 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
     ub) step ub 120 ./tools/ubench_chains ;;
     rowab) step bench_row0 300 env KORALI_AMD_ROWCHAINS=0 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_row1 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
     sqab) step bench_sq0 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_sq1 300 env KORALI_AMD_SQ_DPP=1 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;

@@ -217,6 +217,7 @@ def test_unpack_streamed_reflector_rows_bit_exact(monkeypatch, Nv, lam):
                                          (16, 64, "sq-dpp"), (67, 256, "sq-dpp"), (100, 300, "sq-dpp"),
                                          (128, 4096, "sq-dpp"), (16, 64, "1wg2"), (128, 4096, "1wg2"),
                                          (40, 128, "mw2"), (100, 512, "mw2"), (129, 256, "mw2"),
+                                         (40, 128, "mw2-dpp"), (129, 256, "mw2-dpp"), (200, 400, "mw2-dpp"),
                                          (16, 64, "1wg"), (64, 256, "1wg"), (128, 4096, "1wg"), (100, 512, "mw"),
                                          (40, 128, "lds")])
 def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):

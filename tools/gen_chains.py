@@ -69,7 +69,7 @@ def emit_add():
 __device__ __forceinline__ double kc_add(double acc, unsigned p, unsigned g) {{
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [p] "+v"(p), [g] "+s"(g)
+      : [acc] "+&v"(acc), [p] "+&v"(p), [g] "+&s"(g)
       :
       : "scc", "memory", {CLOBBER});
   return acc;
@@ -109,7 +109,7 @@ def emit_add_desc():
 __device__ __forceinline__ double kc_add_desc(double acc, unsigned p, unsigned g) {{
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [p] "+v"(p), [g] "+s"(g)
+      : [acc] "+&v"(acc), [p] "+&v"(p), [g] "+&s"(g)
       :
       : "scc", "memory", {CLOBBER});
   return acc;
@@ -168,7 +168,7 @@ __device__ __forceinline__ double kc_nrm2(double acc, unsigned p, unsigned g, un
   double tmp;
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [g] "+s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp)
+      : [acc] "+&v"(acc), [g] "+&s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp)
       : [p] "v"(p), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
       : "scc", "memory", {CLOBBER});
   return acc;
@@ -235,7 +235,7 @@ def emit_lock(desc):
 __device__ __forceinline__ double kc_lock_desc(double acc, unsigned pw, unsigned pm, unsigned nb) {{
   asm volatile(
 {body}
-      : [acc] "+v"(acc), [pw] "+v"(pw), [pm] "+v"(pm), [nb] "+s"(nb)
+      : [acc] "+&v"(acc), [pw] "+&v"(pw), [pm] "+&v"(pm), [nb] "+&s"(nb)
       :
       : "scc", "memory", {CLOBBER});
   return acc;
@@ -251,7 +251,7 @@ template <int S>
 __device__ __forceinline__ double kc_lock_asc(double acc, unsigned pw, unsigned pm, unsigned nb) {{
   asm volatile(
 {body}
-      : [acc] "+v"(acc), [pw] "+v"(pw), [pm] "+v"(pm), [nb] "+s"(nb)
+      : [acc] "+&v"(acc), [pw] "+&v"(pw), [pm] "+&v"(pm), [nb] "+&s"(nb)
       : [s8] "i"(8 * S), {offs}
       : "scc", "memory", {CLOBBER});
   return acc;
@@ -287,7 +287,7 @@ __device__ __forceinline__ double kc_add_dpp(double acc, const double (&q)[8], u
   const double one = 1.0;
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [g] "+s"(g)
+      : [acc] "+&v"(acc), [g] "+&s"(g)
       : {qs}, [one] "v"(one)
       : "scc");
   return acc;
@@ -331,7 +331,7 @@ __device__ __forceinline__ double kc_nrm2_dpp(double acc, const double (&q)[8], 
   double tmp, x;
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc), [g] "+s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp), [x] "=&v"(x)
+      : [acc] "+&v"(acc), [g] "+&s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp), [x] "=&v"(x)
       : {qs}, [one] "v"(one), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
       : "scc");
   return acc;
@@ -348,7 +348,7 @@ __device__ __forceinline__ double kc_row16(double acc, double q) {{
   const double one = 1.0;
   asm volatile(
 {asm_block(L)}
-      : [acc] "+v"(acc)
+      : [acc] "+&v"(acc)
       : [q] "v"(q), [one] "v"(one));
   return acc;
 }}
