@@ -24,6 +24,13 @@ for s in ${STEPS:-smoke tests bench prof}; do
     dist) step dist 900 python -u -m pytest tests/test_gpu_distributed.py -x -v --timeout 600 --timeout-method thread ;;
     dppc) step dppc 120 ./tools/check_dpp_chains && step tri 900 python -u -m pytest tests/test_gpu_cmaes.py -v --timeout 300 --timeout-method thread -k tridiagonalisation_kernels ;;
     occsys) step occ_sys 300 env KORALI_AMD_HIP_RUNTIME=system KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two && step occ_one 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
+    c4ab) step c4_sc0 300 env KORALI_AMD_TRANSFORM_SC=0 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline && step c4_sc8 300 env KORALI_AMD_TRANSFORM_SC=8 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    prof4) step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python bench.py --workload c4 --steps 6 --warmup 2 --no-cpu-baseline ;;
+    pmc2) step pmc2f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc2_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline && step pmc2w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc2_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmc4) step pmc4f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    mfma) step mfma2 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma2" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --cov mfma && step mfma4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    trace2dpp) step trace2_dpp0 200 env KORALI_AMD_SQ_DPP=0 KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
     ub) step ub 120 ./tools/ubench_chains ;;
     rowab) step bench_row0 300 env KORALI_AMD_ROWCHAINS=0 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_row1 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
     sqab) step bench_sq0 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_sq1 300 env KORALI_AMD_SQ_DPP=1 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
@@ -31,7 +38,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     occ2) step occ_pair 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest -x -v -s --timeout 250 --timeout-method thread tests/test_cxx_api.py::test_reference_idioms_run_cmaes_direct tests/test_gpu_baseline_shapes.py::test_c4_shape_two_generations_bit_exact ; step occ_coll 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
     testsdbg) step testsdbg 1100 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -x -v -s -m gpu --timeout 300 --timeout-method thread ;;
-    tests) step tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    tests) step tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ;;
     trace2) step trace2 200 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
     trace4) step trace4 300 env KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c4.py ;;
     eng) step eng 900 python -m pytest tests/test_gpu_engine.py -q --maxfail=20 ;;

@@ -248,8 +248,11 @@ def test_scalar_operand_transform_bit_exact(monkeypatch, Nv, lam, mirrored, boun
     monkeypatch.setenv("KORALI_AMD_TRANSFORM_SC", "8")
     seed = 99
     x0 = np.full(Nv, 0.5 if bound == 0.5 else 0.0)
+    # sigma0: bound 0.5 starts ON the bound (~10^3 draws per sample, the
+    # redraw rounds); bound 1.0 at N = 67 leaves ~25% of the draws infeasible
+    s0 = {None: 1.0, 0.5: 0.3, 1.0: 0.35}[bound]
     o = R.CMAES(Nv, lam, 0)
-    o["Initial Value"], o["Initial Standard Deviation"] = x0, np.full(Nv, 0.3 if bound == 0.5 else 1.0)
+    o["Initial Value"], o["Initial Standard Deviation"] = x0, np.full(Nv, s0)
     kw = {}
     if bound is not None:
         o["Lower Bound"], o["Upper Bound"] = np.full(Nv, -bound), np.full(Nv, bound)
@@ -258,7 +261,7 @@ def test_scalar_operand_transform_bit_exact(monkeypatch, Nv, lam, mirrored, boun
         o.option("Mirrored Sampling", 1)
     R.lib().kr_rng_seed(o.rng(0).ptr, seed)
     R.lib().kr_rng_seed(o.rng(1).ptr, seed + 1)
-    dev = device_solver(Nv, lam, initial_value=x0, initial_std=np.full(Nv, 0.3 if bound == 0.5 else 1.0),
+    dev = device_solver(Nv, lam, initial_value=x0, initial_std=np.full(Nv, s0),
                         mirrored=mirrored, normal_seed=seed, uniform_seed=seed + 1, **kw)
     for g in range(1, 5):
         o.generation(g, "rosenbrock")
