@@ -96,8 +96,7 @@ typedef struct {
   /* "Granularity" of each variable (N, may be NULL → all 0 = continuous;
    * CMAES.cpp.base:44-50, :515-544, :834-867): samples are rounded to it,
    * discrete mutations drawn from the Uniform Generator, sigma follows the
-   * masked path length; with or without Mirrored Sampling.  Not with
-   * population sharding (shard_count > 1). */
+   * masked path length; with or without Mirrored Sampling, sharded or not. */
   const double *granularity;
   /* CCMA-ES (Problem "Constraints"; CMAES.cpp.base:54-68, :132-170,
    * :315-437, :551-580, :724-731, :774-832).  constraint_count > 0: the
@@ -178,8 +177,11 @@ int kg_cmaes_begin_sample(kg_cmaes_t h);
 #define KG_TERMINATION_FIELDS 9
 int kg_cmaes_wait_termination_fields(kg_cmaes_t h, double *out);
 /* Population sharding over shard_count ranks (one handle per rank, state
- * replicated, λ % shard_count == 0, unbounded variables).  kg_cmaes_sample
- * and kg_cmaes_eval_builtin then cover only rows [rank λ/S, (rank+1) λ/S);
+ * replicated, λ % shard_count == 0).  kg_cmaes_sample and
+ * kg_cmaes_eval_builtin then cover only rows [rank λ/S, (rank+1) λ/S) (with
+ * finite bounds, discrete variables, Mirrored Sampling or a diagonal
+ * covariance kg_cmaes_sample draws the whole population on every rank: the
+ * redraw walk and the ±z pairs are sequential over it);
  * the caller all-gathers "Value Vector" (λ doubles, shards in rank order),
  * runs kg_cmaes_update_partial, sum-all-reduces "Shard Partials" and
  * finishes with kg_cmaes_update_finalize.  Every rank then holds the same

@@ -2524,6 +2524,7 @@ struct kg_cmaes_s {
   int kslices = 8;  // rank-mu K-slices (rankmu_kslices), a multiple of the 8 XCDs
   // population shards
   int shards = 1, shardRank = 0, r0 = 0, r1 = 0;
+  bool replSample = false;  // sharded, but every rank draws the whole population (kg_cmaes_create)
   int *kidx = nullptr, *shardCnt = nullptr;
   double *part = nullptr;  // "Shard Partials": mean (N), best row (N), rank-mu tiles
   unsigned long long *eigTrace = nullptr;  // KORALI_AMD_TRACE_EIGEN: s_memtime per phase
@@ -2728,7 +2729,6 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   KG_CHECK(cfg->population_size > 1, "'Population Size' must be larger 1.");  // CMAES.cpp.base:26
   KG_CHECK(!cfg->mirrored_sampling || cfg->population_size % 2 == 0,
            "Mirrored Sampling can only be applied with an even Sample Population");  // CMAES.cpp.base:91
-  KG_CHECK(!cfg->mirrored_sampling || cfg->shard_count <= 1, "Mirrored Sampling runs unsharded");
   KG_CHECK(!cfg->use_gradients || cfg->gradient_step_size > 0.0,
            "Gradient Step Size must be larger than 0.0");  // CMAES.cpp.base:86
   KG_CHECK(!cfg->use_gradients || cfg->shard_count <= 1, "Use Gradient Information runs unsharded");
@@ -2810,26 +2810,26 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     }
     if (gran[i] > 0.0) h->hasDiscrete = true;
   }
-  if (h->hasDiscrete && cfg->shard_count > 1) {
-    set_error("discrete variables (Granularity) run unsharded on the device path");
-    delete h;
-    return 1;
-  }
   // a reserve of transformed rows for resampling: finite bounds, or discrete
   // variables (a rounded or mutated sample may leave the bounds or not)
   h->R = (h->finiteBounds || h->hasDiscrete) ? std::max(256, L / 4) : 0;
   h->shards = cfg->shard_count > 1 ? cfg->shard_count : 1;
   h->shardRank = h->shards > 1 ? cfg->shard_rank : 0;
-  if (h->shards > 1 && (L % h->shards != 0 || h->finiteBounds || cfg->shard_rank < 0 ||
-                        cfg->shard_rank >= h->shards || cfg->diagonal_covariance)) {
-    set_error("population sharding needs Population Size divisible by the shard count, unbounded variables, "
-              "a full covariance and 0 <= shard_rank < shard_count");
+  if (h->shards > 1 && (L % h->shards != 0 || cfg->shard_rank < 0 || cfg->shard_rank >= h->shards)) {
+    set_error("population sharding needs Population Size divisible by the shard count and "
+              "0 <= shard_rank < shard_count");
     delete h;
     return 1;
   }
   h->r0 = h->shardRank * (L / h->shards);
   h->r1 = h->r0 + L / h->shards;
   h->mirrored = cfg->mirrored_sampling != 0;
+  // a population whose draw is not "row i = block i" (the redraw walk of
+  // finite bounds and discrete variables, the +-z pairs of Mirrored Sampling)
+  // or that has no B (diagonal covariance) is drawn and transformed whole on
+  // every rank, each rank evaluating and summing its own rows
+  h->replSample = h->shards > 1 &&
+                  (h->finiteBounds || h->hasDiscrete || h->mirrored || cfg->diagonal_covariance);
   h->trW = transform_width();
   h->blocks = (h->mirrored ? (size_t)L / 2 : (size_t)L) + h->R;
   const size_t rows = (size_t)L + h->R;
@@ -3009,7 +3009,7 @@ static int cmaes_draw_begin(kg_cmaes_t h) {
   if (h->normal.prefetch(rows * N, h->stream)) return 1;  // overlaps the eigensolver
   // the polar pass reads only the generator stream: it runs on the
   // producer's side stream too, concurrently with the eigensolver
-  const bool shard = h->shards > 1;
+  const bool shard = h->shards > 1 && !h->replSample;
   return h->normal.polar_normals(h->Z, rows * N, N, h->blockEnd, h->normal.side_stream(),
                                  shard ? (size_t)h->r0 * N : 0, shard ? (size_t)h->r1 * N : (size_t)-1);
 }
@@ -3209,7 +3209,7 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     bool finite = false;
     if (draw_guard(h, &finite)) return 1;
     if (!finite) {
-      KG_CHECK(h->shards == 1,
+      KG_CHECK(h->shards == 1 || h->replSample,
                "a population-sharded handle cannot redraw non-finite samples (overflow guard tripped)");
       if (ensure_redraw_buffers(h)) return 1;
       redraw = true;
@@ -3220,9 +3220,10 @@ int kg_cmaes_sample(kg_cmaes_t h) {
     Stage st(h, "transform");
     // no redraw possible: the population is the first lambda blocks; a shard
     // transforms its own rows only
-    const size_t trows = (size_t)(h->r1 - h->r0);
-    double *xo = h->X + (size_t)h->r0 * N;
-    double *bo = h->BDZ ? h->BDZ + (size_t)h->r0 * N : nullptr;
+    const int t0 = h->replSample ? 0 : h->r0, t1 = h->replSample ? h->lam : h->r1;
+    const size_t trows = (size_t)(t1 - t0);
+    double *xo = h->X + (size_t)t0 * N;
+    double *bo = h->BDZ ? h->BDZ + (size_t)t0 * N : nullptr;
     // 32 x 64 tiles, 4 x 2 outputs per thread: larger register tiles drop the
     // kernel to 2 waves per SIMD and measured slower at C4 (1.96 / 2.25 ms
     // for 32 x 128 / 64 x 64 against 1.73 ms)

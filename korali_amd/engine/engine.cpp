@@ -656,9 +656,9 @@ struct CmaesModule : SolverModule {
       fail("Constrained CMA-ES needs an unsharded run (Sequential or Concurrent conduit).");
     if (!constraintFns.empty() && mirrored) fail("Mirrored Sampling not applicable to problems with constraints");
     if (dist) {
-      if (mirrored || useGradients)
-        fail("The Distributed conduit shards the population: 'Mirrored Sampling' and 'Use Gradient Information' "
-             "need an unsharded run (Sequential or Concurrent conduit).");
+      if (useGradients)
+        fail("The Distributed conduit shards the population: 'Use Gradient Information' needs an unsharded run "
+             "(Sequential or Concurrent conduit).");
       if (lam % (size_t)dist->world)
         fail("The Distributed conduit splits the population evenly: 'Population Size' (%zu) must be a multiple of "
              "the number of ranks (%d).",
@@ -731,7 +731,6 @@ struct CmaesModule : SolverModule {
     c.initial_std = istd.data();
     c.min_std_update = minstd.data();
     c.granularity = gran.data();
-    if (hasDiscrete && dist) fail("Discrete variables (Granularity) need an unsharded run (Sequential or Concurrent conduit).");
     c.normal_seed = seeds.assign(gn);
     c.uniform_seed = seeds.assign(gu);
     // the Distributed conduit shards the update: every rank sums the mean and

@@ -117,7 +117,6 @@ def distributed_engine(**keys):
 @pytest.mark.parametrize("keys,solver,msg", [
     ({"Ranks_Per_Worker": 2}, {}, "'Ranks Per Worker' must be 1"),
     ({"Transport": "MPI"}, {}, "'Transport' must be 'RCCL' or 'Host'"),
-    ({}, {"Mirrored Sampling": True}, "need an unsharded run"),
     ({}, {"Covariance Update": "Exact"}, "needs an unsharded run"),
 ])
 def test_distributed_configuration_errors(monkeypatch, keys, solver, msg):

@@ -19,15 +19,22 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("ranks,N,lam,gens,obj,backend", [(2, 32, 256, 6, "rosenbrock", "gloo"),
-                                                          (4, 200, 1024, 3, "ackley", "gloo"),
-                                                          (1, 64, 512, 4, "rosenbrock", "nccl")])
-def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend):
+@pytest.mark.parametrize("ranks,N,lam,gens,obj,backend,variant", [(2, 32, 256, 6, "rosenbrock", "gloo", "plain"),
+                                                                  (4, 200, 1024, 3, "ackley", "gloo", "plain"),
+                                                                  (1, 64, 512, 4, "rosenbrock", "nccl", "plain"),
+                                                                  (2, 32, 256, 6, "rosenbrock", "gloo", "bounded"),
+                                                                  (2, 32, 256, 6, "rosenbrock", "gloo", "mirrored"),
+                                                                  (3, 24, 192, 6, "rosenbrock", "gloo", "discrete"),
+                                                                  (2, 40, 256, 6, "ackley", "gloo", "diagonal")])
+def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend, variant):
     """gloo: several ranks on the one device, host-staged collectives;
-    nccl: the RCCL zero-copy device transport (one rank: one device here)."""
+    nccl: the RCCL zero-copy device transport (one rank: one device here).
+    Variants bounded / mirrored / discrete / diagonal: every rank draws the
+    whole population (the redraw walk, the +-z pairs and the discrete
+    mutations are sequential over it) and evaluates and sums its own rows."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "tools", "shard_check.py"),
-           str(N), str(lam), str(gens), obj, backend]
+           str(N), str(lam), str(gens), obj, backend, variant]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "SHARD_CHECK PASS" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

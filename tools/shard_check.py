@@ -17,6 +17,10 @@ def main():
     N, lam, gens = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     obj = sys.argv[4] if len(sys.argv) > 4 else "rosenbrock"
     backend = sys.argv[5] if len(sys.argv) > 5 else "gloo"
+    # sampling variant: plain (rows sharded), or one of the configurations
+    # every rank draws whole (finite bounds with redraws, Mirrored Sampling,
+    # discrete variables, diagonal covariance)
+    variant = sys.argv[6] if len(sys.argv) > 6 else "plain"
     if backend == "nccl":
         # RCCL with the zero-copy device transport (one rank per device)
         import torch
@@ -26,6 +30,17 @@ def main():
         dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     kw = dict(initial_value=np.full(N, 1.0), initial_std=np.full(N, 0.7), normal_seed=4321, uniform_seed=4322)
+    if variant == "bounded":  # ~1 in 6 draws of the first generations infeasible at N = 32
+        kw.update(lower_bound=np.full(N, -1.5), upper_bound=np.full(N, 3.0))
+    elif variant == "mirrored":
+        kw.update(mirrored=True)
+    elif variant == "discrete":
+        kw.update(granularity=np.where(np.arange(N) % 3 == 0, 0.25, 0.0), lower_bound=np.full(N, -4.0),
+                  upper_bound=np.full(N, 4.0))
+    elif variant == "diagonal":
+        kw.update(diagonal=True)
+    elif variant != "plain":
+        raise SystemExit(f"unknown variant {variant}")
     sh = ShardedCmaes(N, lam, dist, device=0, transport="device" if backend == "nccl" else "host", **kw)
     ref = CmaesDevice(N, lam, cov_mode="mfma", **kw) if rank == 0 else None
     ok = True
@@ -53,6 +68,9 @@ def main():
                 ok = False
             if not np.array_equal(sh.dev.sorting_index(), ref.sorting_index()):
                 print(f"gen {g}: sorting index differs", flush=True)
+                ok = False
+            if sh.dev["Infeasible Sample Count"][0] != ref["Infeasible Sample Count"][0]:
+                print(f"gen {g}: infeasible sample count differs", flush=True)
                 ok = False
             for k, tol in (("Current Mean", 1e-12), ("Covariance Matrix", 1e-11), ("Sigma", 1e-12),
                            ("Best Ever Variables", 0.0)):
