@@ -40,7 +40,16 @@ struct CmaesScalars {
   // CCMA-ES (CMAES.cpp.base:147, :724-731, :812-819)
   double gsr;              // Global Success Rate
   double resampledCount;   // Resampled Parameter Count (handleConstraints' redraws)
+  // hsig's (1 - c_sigma)^(2 (1 + gen)) (:656), correctly rounded, formed by
+  // k_sigma one generation ahead in a spare wave (the double-double pow is
+  // ~5 us of one lane); valid for generation hsigPowGen and c_sigma hsigPowCs
+  double hsigPow, hsigPowCs, hsigPowGen;
 };
+
+__device__ inline double hsig_pow(const CmaesScalars *sc, double cs, unsigned long long gen) {
+  if (sc->hsigPowGen == (double)gen && sc->hsigPowCs == cs) return sc->hsigPow;
+  return pow_cr(1. - cs, 2.0 * (1.0 + (double)gen));
+}
 
 // Bound on |z| of a GSL polar normal: z = y sqrt(-2 ln r2 / r2) with |y| <=
 // sqrt(r2) and r2 >= 2^-62 (x, y are multiples of 2^-31), so |z| <=
@@ -162,6 +171,7 @@ __global__ void __launch_bounds__(256) k_init(int N, int lam, int mu, int muType
       sc->psNorm = 0.0;
       sc->currentMinStd = INFINITY;
       sc->currentMaxStd = -INFINITY;
+      sc->hsigPowGen = -1.0;
     }
   }
 }
@@ -1656,7 +1666,9 @@ __global__ void __launch_bounds__(256) k_mean2(int N, int mu, const double *__re
 // workgroup.  The selected rows are staged through LDS in chunks of MR_K
 // (coalesced 16-dimension row segments in, dimension-major out), the next
 // chunk's loads in flight while the current one is summed.
-constexpr int MR_K = 128, MR_KS = MR_K + 2;
+// (MR_K = 256: one chunk's sum, 256 x ~9 cycles, covers the next chunk's
+// load latency, which 128-term chunks did not: 20 us at C2)
+constexpr int MR_K = 256, MR_KS = MR_K + 2, MR_U = MR_K * 16 / 256;
 __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__restrict__ Y,
                                                const double *__restrict__ w, double *mean,
                                                const double *__restrict__ prevMean, double *meanUpdate,
@@ -1667,11 +1679,11 @@ __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__re
   const int row = lane >> 4, j = lane & 15, dl = 4 * wid + row;
   const int d0 = blockIdx.x * 16;
   const int nch = (mu + MR_K - 1) / MR_K;
-  // chunk loads: 256 threads x 8 values of the (MR_K x 16) block, + w
-  double ld[8], wl = 0.0;
+  // chunk loads: 256 threads x MR_U values of the (MR_K x 16) block, + w
+  double ld[MR_U], wl = 0.0;
   auto load = [&](int ch) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < MR_U; u++) {
       const int q = tid + 256 * u, k = q >> 4, c = q & 15, i = ch * MR_K + k;
       ld[u] = (i < mu && d0 + c < N) ? Y[(size_t)i * N + d0 + c] : 0.0;
     }
@@ -1680,7 +1692,7 @@ __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__re
   };
   auto store = [&](int b) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < MR_U; u++) {
       const int q = tid + 256 * u, k = q >> 4, c = q & 15;
       ys[b][c][k] = ld[u];
     }
@@ -1781,7 +1793,7 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
     if (lane == 0) {
       const double nrm = sqrt(nrm2);
       sc->psNorm = nrm;
-      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - hsig_pow(sc, cs, gen)) /
                                                    sc->chiSquareNumber);
       hs = hsig;
       sc->hsig = hsig;
@@ -1858,7 +1870,7 @@ __global__ void __launch_bounds__(256) k_paths2(int N, unsigned long long gen, c
     if (lane == 0) {
       const double nrm = sqrt(nrm2);
       sc->psNorm = nrm;
-      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - hsig_pow(sc, cs, gen)) /
                                                    sc->chiSquareNumber);
       hs = hsig;
       sc->hsig = hsig;
@@ -1935,7 +1947,7 @@ __global__ void __launch_bounds__(1024) k_paths(int N, int diagonal, unsigned lo
     for (int d = 0; d < N; ++d) nrm += tile[d] * tile[d];  // std::pow(x, 2.0) == x*x (CR)
     nrm = sqrt(nrm);
     sc->psNorm = nrm;
-    const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - pow_cr(1. - cs, 2.0 * (1.0 + (double)gen))) /
+    const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - hsig_pow(sc, cs, gen)) /
                                                  sc->chiSquareNumber);
     hs = hsig;
     sc->hsig = hsig;
@@ -2297,7 +2309,8 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
                                                const StreamState *stA, const StreamState *stB, TermSummary *out,
                                                unsigned long long seq, const double *__restrict__ maskSigma,
                                                const double *__restrict__ ps, const double *__restrict__ mean,
-                                               int muCfg, int viability, double tsr, double gslr) {
+                                               int muCfg, int viability, double tsr, double gslr,
+                                               unsigned long long nextGen) {
   __shared__ double ssig;
   __shared__ int viol;
   __shared__ double red[4][6];
@@ -2321,6 +2334,12 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
     if (sigma > ub && isSigmaBounded) sigma = ub;
     ssig = sigma;
     viol = 0;
+  }
+  if (tid == 64) {  // (wave 1, beside wave 0's sigma update: the next generation's hsig power)
+    const double cs = sc->sigmaCumulationFactor;
+    sc->hsigPow = pow_cr(1. - cs, 2.0 * (1.0 + (double)nextGen));
+    sc->hsigPowCs = cs;
+    sc->hsigPowGen = (double)nextGen;
   }
   __syncthreads();
   for (int d = tid; d < N; d += blockDim.x)
@@ -3314,7 +3333,7 @@ static int cmaes_sort(kg_cmaes_t h) {
   return 0;
 }
 
-static int cmaes_sigma(kg_cmaes_t h) {
+static int cmaes_sigma(kg_cmaes_t h, size_t gen) {
   const int N = h->N, mu = h->mu;
   {
     Stage st(h, "sigma");
@@ -3324,7 +3343,8 @@ static int cmaes_sigma(kg_cmaes_t h) {
     hipLaunchKernelGGL(k_sigma, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.is_sigma_bounded, h->C, h->F, h->idx,
                        h->minstd, h->sc, h->normal.state(), h->uniform.state(), h->summaryDev, ++h->updates,
                        h->hasDiscrete ? h->maskSigma : (const double *)nullptr, h->ps, h->mean, h->muCfg,
-                       h->viability ? 1 : 0, h->cfg.target_success_rate, h->cfg.global_success_learning_rate);
+                       h->viability ? 1 : 0, h->cfg.target_success_rate, h->cfg.global_success_learning_rate,
+                       (unsigned long long)(gen + 1));
     h->stateDirty = false;  // the record's guard describes the next draw
     KG_HIP(hipGetLastError());
   }
@@ -3628,7 +3648,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
   }
-  if (cmaes_sigma(h)) return 1;  // (k_sigma also publishes the termination record)
+  if (cmaes_sigma(h, generation)) return 1;  // (k_sigma also publishes the termination record)
   return h->nc ? ccm_after_update(h) : 0;
 }
 
@@ -3675,7 +3695,7 @@ int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
                        h->cfg.diagonal_covariance, h->part + 2 * (size_t)N, h->pc, h->C, h->sc, 1);
     KG_HIP(hipGetLastError());
   }
-  return cmaes_sigma(h);  // (k_sigma also publishes the termination record, as after kg_cmaes_update)
+  return cmaes_sigma(h, generation);  // (k_sigma also publishes the termination record, as after kg_cmaes_update)
 }
 
 int kg_cmaes_generation(kg_cmaes_t h, size_t generation, int objective) {
