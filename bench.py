@@ -241,29 +241,26 @@ def engine_rate(steps, warmup, cov):
     """The same C2 experiment through the korali API (C++ engine: termination
     checks and bookkeeping every generation, as Korali's Experiment::run
     does).  Returns (differential, end_to_end):
-    * differential: warm-up generations run first; resumed runs of `short`
-      and `steps` more generations (three of each, medians) cancel the
-      fixed cost of a run() (the device handle re-created from the saved
-      state, its first generation);
+    * differential: fresh k.run(e) of `short` and of `long` generations
+      (three of each, medians); their difference cancels the fixed cost of a
+      run (handle creation, initialisation, the first generation), leaving
+      the engine's per-generation rate;
     * end_to_end: one fresh k.run(e) of `steps` generations, wall clock,
       handle creation and initialisation included."""
     import korali
     k = korali.Engine()
-    e = c2_experiment(cov, warmup)
-    k.run(e)
-    e["Preserve Random Number Generator States"] = True
-    steps = max(steps, 100)
-    short = max(1, steps // 8)
+    k.run(c2_experiment(cov, warmup))  # (first-use costs: module load, code objects)
+    short, long_ = 50, 50 + max(steps, 300)
     med = {}
-    for n in (short, steps):
+    for n in (short, long_):
         ts = []
         for _ in range(3):
-            e["Solver"]["Termination Criteria"]["Max Generations"] = e["Current Generation"] + n
+            f = c2_experiment(cov, n)
             t0 = time.perf_counter()
-            k.run(e)
+            k.run(f)
             ts.append(time.perf_counter() - t0)
         med[n] = sorted(ts)[1]
-    diff = (steps - short) / (med[steps] - med[short])
+    diff = (long_ - short) / (med[long_] - med[short])
     f = c2_experiment(cov, steps)
     t0 = time.perf_counter()
     k.run(f)

@@ -856,7 +856,17 @@ __global__ void __launch_bounds__(256) k_rank_sort(int lam, const double *__rest
   const double ki = (i < lam) ? rk[i] : 0.0;
   const int per = (lam + 15) / 16, j0 = p * per, j1 = min(lam, j0 + per);
   unsigned c = 0;
-  for (int j = j0; j < j1; j++) {
+  int j = j0;
+  // eight keys read before their compares (one LDS round trip per eight:
+  // the one-key loop waited on every read, ~11 of its 21 us at lambda = 4096)
+  for (; j + 8 <= j1; j += 8) {
+    double kj[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) kj[u] = rk[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) c += (kj[u] > ki || (kj[u] == ki && j + u < i)) ? 1u : 0u;
+  }
+  for (; j < j1; j++) {
     const double kj = rk[j];
     c += (kj > ki || (kj == ki && j < i)) ? 1u : 0u;
   }
@@ -1431,7 +1441,9 @@ __global__ void __launch_bounds__(64 * (AX3_P + 1)) k_adaptC_exact3(int N, int m
 // wave w takes d0 + w/2 and columns e0 + 4 (w%2) + row.  T rows and the Yc
 // columns of the tile are staged through LDS in chunks of AR_K terms
 // (transposed to term-contiguous rows), the next chunk's loads in flight.
-constexpr int AR_K = 128, AR_KS = AR_K + 2;
+// (AR_K = 256: a chunk's sums cover the next chunk's load latency; 128-term
+// chunks left the kernel latency-bound, 34 us at C2)
+constexpr int AR_K = 256, AR_KS = AR_K + 2, AR_TU = 4 * AR_K / 512, AR_YU = 8 * AR_K / 512;
 __host__ __device__ inline int ar_row_blocks(int N) { return (N + 3) / 4; }
 __host__ __device__ inline int ar_col_blocks_upto(int rb) { return (4 * rb + 3) / 8 + 1; }  // e0 <= d0 + 3
 int ar_tiles(int N) {
@@ -1446,22 +1458,27 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
   const int tid = threadIdx.x, j = tid & 15;
   const double y = kMarkstein ? 1.0 / s2 : 0.0;
   // staging: T rows d0..d0+3 (4 x AR_K) and Yc[k][e0..e0+7] (AR_K x 8)
-  double tv, yv[2];
+  double tv[AR_TU], yv[AR_YU];
   auto load = [&](int k0) {
-    {
-      const int r = tid >> 7, k = k0 + (tid & 127);
-      tv = (d0 + r < N && k < mu) ? Tt[(size_t)(d0 + r) * mu + k] : 0.0;
+#pragma unroll
+    for (int u = 0; u < AR_TU; u++) {
+      const int q = tid + 512 * u, r = q / AR_K, k = k0 + q % AR_K;
+      tv[u] = (d0 + r < N && k < mu) ? Tt[(size_t)(d0 + r) * mu + k] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < AR_YU; u++) {
       const int q = tid + 512 * u, k = k0 + (q >> 3), c = q & 7;
       yv[u] = (k < mu && e0 + c < N) ? Yc[(size_t)k * N + e0 + c] : 0.0;
     }
   };
   auto store = [&](int b) {
-    Ts[b][tid >> 7][tid & 127] = tv;
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < AR_TU; u++) {
+      const int q = tid + 512 * u;
+      Ts[b][q / AR_K][q % AR_K] = tv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < AR_YU; u++) {
       const int q = tid + 512 * u;
       Ys[b][q & 7][q >> 3] = yv[u];
     }

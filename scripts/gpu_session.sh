@@ -31,6 +31,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmc4) step pmc4f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     mfma) step mfma2 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma2" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --cov mfma && step mfma4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     trace2dpp) step trace2_dpp0 200 env KORALI_AMD_SQ_DPP=0 KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
+    c4p) step prof4p 400 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python bench.py --workload c4 --steps 6 --warmup 2 --no-cpu-baseline && step pmc4fp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4wp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step mfma4p 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     ub) step ub 120 ./tools/ubench_chains ;;
     rowab) step bench_row0 300 env KORALI_AMD_ROWCHAINS=0 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_row1 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
     sqab) step bench_sq0 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_sq1 300 env KORALI_AMD_SQ_DPP=1 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
@@ -52,7 +53,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     c4) step c4 600 python tools/probe_c4.py ${C4_ARGS:-512 65536 3} ;;
     shard) step shard 900 python -m pytest tests/test_gpu_shard.py -q -x ;;
-    cm) step cm 900 python -m pytest tests/test_gpu_cmaes.py -q -x ;;
+    cm) step cm 900 python -u -m pytest tests/test_gpu_cmaes.py tests/test_gpu_baseline_shapes.py -x -v --timeout 150 --timeout-method thread ;;
     benchc4) step benchc4 600 python bench.py --workload c4 --steps ${C4_STEPS:-20} --warmup 3 ;;
     pmc5) step pmc5f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc5_fetch" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline && step pmc5w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc5_write" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench5) step bench5 600 python bench.py --workload c5 ;;
