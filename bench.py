@@ -58,16 +58,17 @@ STAGE_KERNELS = {
     # instances match their base name
     "eigen_tridiag": [("kg::k_tridiag_sq", "kg::k_tridiag_mw2", "kg::k_tridiag_1wg2", "kg::k_tridiag_1wg",
                        "kg::k_tridiag_mw", "kg::k_tridiag")],
-    "eigen_unpack": [("kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
-    "transform": ["kg::k_transform"], "objective": ["kg::k_objective"],
-    "covariance": [("kg::k_adaptC_exact2", "kg::k_adaptC_combine")],
+    "eigen_unpack": [("kg::k_unpack_wv", "kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
+    "transform": [("kg::k_transform_sc", "kg::k_transform")], "objective": [("kg::k_objective2", "kg::k_objective")],
+    "covariance": [("kg::k_adaptC_row", "kg::k_adaptC_exact3", "kg::k_adaptC_exact2", "kg::k_adaptC_combine")],
     "rankmu_mfma": ["kg::k_rankmu_tile"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
-    "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", "kg::k_mean", "kg::k_paths"],
+    "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", ("kg::k_mean3", "kg::k_mean2", "kg::k_mean"),
+                   ("kg::k_paths3", "kg::k_paths2", "kg::k_paths")],
     # C3 (TMCMC): the weighted mean / covariance stage
     "mean_cov": ["kg::k_tm_factors_mean", "kg::k_tm_wsum<false>", "kg::k_tm_factors_cov", "kg::k_tm_wsum<true>"],
 }
-PROFILE_ROUNDS = ("r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
+PROFILE_ROUNDS = ("r4", "r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
 
 
 def profile_file(name):
@@ -435,8 +436,9 @@ def main():
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
         "roofline": {"kernel": {"eigen_tridiag": "kg::k_tridiag_sq"}.get(dominant, dominant), "stage": dominant,
-                     "bound": "mfma",
-                     "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is "
+                     "bound": "mfma", "issued_on": "valu",
+                     "bound_note": "the contract's compute roof, priced at the FP64 peak (MI355X FP64 vector peak == "
+                                   "FP64 matrix peak, so the VALU kernel has the same roof; it issues no MFMA); the stage is "
                                    "GSL's Householder tridiagonalisation, three ordered FP64 add chains of length "
                                    "N-1-i per step (dnrm2, dsymv, ddot) whose order the bit-exact contract fixes, "
                                    "so it is bound by the dependent-add latency, far below the roof by construction",
