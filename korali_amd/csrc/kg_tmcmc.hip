@@ -540,6 +540,7 @@ struct NmSync {
   unsigned long long seq;         // round published by the controller
   unsigned long long done[NM_W];  // round each worker has published
   NmPart part[NM_W][NM_PTS];
+  NmPart part2[2][NM_W][NM_PTS];  // k_tm_nm_sym: by round parity
 };
 struct NmVal {
   double x, y, eps;
@@ -588,6 +589,170 @@ __device__ inline void nm_part_st(NmPart *p, const NmPart &v) {
   nm_std(d + 3, v.q_lo);
   nm_std(d + 4, v.mx);
   nm_std(d + 5, v.flags);
+}
+
+// minSearch's one-dimensional nmsimplex loop (:712-779; the host's
+// min_search below, comparison for comparison) over values that
+// run_round(pts, n) leaves in val[] / spts[] / sbn (it returns true when a
+// hand-off timed out).  Shared by the controller of k_tm_nm_search and every
+// workgroup of k_tm_nm_sym, which all run it on identical values.
+template <class RunRound>
+__device__ __forceinline__ void nm_drive(const NmTab &tab, const NmVal *val, const double *spts, const int &sbn,
+                                         RunRound &run_round, double &X0, double &X1, NmVal &Y0, NmVal &Y1,
+                                         long long &iter, int &lo, int &status, int &nneed, double &need0,
+                                         double &need1) {
+  auto request = [&](const NmVal &v) __attribute__((always_inline)) {
+    // branch-free (keeps need0 / need1 in registers)
+    const bool first = !v.exact && nneed == 0;
+    const bool second = !v.exact && nneed == 1 && __double_as_longlong(v.x) != __double_as_longlong(need0);
+    need0 = first ? v.x : need0;
+    need1 = second ? v.x : need1;
+    nneed += (first || second) ? 1 : 0;
+    status = 1;
+  };
+  // the value at x; `slot` is where the round's batch put x (checked)
+  auto get = [&](double x, NmVal &v, int slot) __attribute__((always_inline)) {
+    bool found = false;
+    if (tab.n > 0) {
+#pragma unroll
+      for (int t = 0; t < NM_TAB; t++)
+        if (!found && t < tab.n && __double_as_longlong(tab.x[t]) == __double_as_longlong(x)) {
+          v = NmVal{x, tab.y[t], 0.0, 1};
+          found = true;
+        }
+      if (found) return;
+    }
+    if (slot < sbn && __double_as_longlong(spts[slot]) == __double_as_longlong(x)) {
+      v = val[slot];
+      found = true;
+    }
+    for (int k = 0; !found && k < sbn; k++)
+      if (__double_as_longlong(spts[k]) == __double_as_longlong(x)) {
+        v = val[k];
+        found = true;
+        break;
+      }
+    if (!found) {
+      double one[NM_PTS] = {x, 0, 0, 0, 0, 0, 0, 0};
+      if (run_round(one, 1)) status = 2;
+      v = val[0];
+    }
+    if (v.exact < 0) {  // degenerate: the host's exact value decides
+      v.exact = 0;
+      request(v);
+    }
+  };
+  // a < b (or a <= b): exact values compare exactly, others on their
+  // intervals; undecidable -> request the inexact operands
+  auto cmp = [&](const NmVal &a, const NmVal &b, bool orEqual) __attribute__((always_inline)) -> bool {
+    if (a.exact && b.exact) return orEqual ? a.y <= b.y : a.y < b.y;
+    if (a.y + a.eps < b.y - b.eps) return true;
+    if (a.y - a.eps > b.y + b.eps) return false;
+    request(a);
+    request(b);
+    return false;
+  };
+  const int MaxIter = 1000;
+  const double Tol = 1e-12;
+  {
+    const double p2[NM_PTS] = {X0, X1, 0, 0, 0, 0, 0, 0};
+    if (run_round(p2, 2)) status = 2;
+    get(X0, Y0, 0);
+    if (!status) get(X1, Y1, 1);
+  }
+  while (status == 0) {
+    iter++;
+    int hi = 0;
+    lo = 0;
+    if (cmp(Y1, Y0, false)) {
+      lo = 1;
+    } else {
+      if (status) break;
+      if (cmp(Y0, Y1, false)) hi = 1;
+    }
+    if (status) break;
+    const double Xhi = hi ? X1 : X0, Xlo = lo ? X1 : X0;
+    const double mp = hi ? X0 : X1;
+    const double xc = mp - (-1.0) * (mp - Xhi);
+    {
+      // every point this iteration may evaluate (the host's batch)
+      double pts[NM_PTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int np = 0;
+      pts[np++] = xc;
+      pts[np++] = mp - (-2.0) * (mp - Xhi);
+      pts[np++] = mp - 0.5 * (mp - Xhi);
+      pts[np++] = mp - 0.5 * (mp - xc);
+      // shrink towards lo, with and without X[hi] = xc (1-D: the vertex != lo)
+      const double Xo = lo ? X0 : X1;  // the vertex that is not lo
+      const double XoR = (hi == lo) ? Xo : xc, XloR = (hi == lo) ? xc : Xlo;
+      pts[np++] = 0.5 * (Xo + Xlo);
+      pts[np++] = 0.5 * (XoR + XloR);
+      if (run_round(pts, np)) status = 2;
+      if (status) break;
+    }
+    NmVal v;
+    get(xc, v, 0);
+    if (status) break;
+    const NmVal Ylo = lo ? Y1 : Y0;
+    const bool better = cmp(v, Ylo, false);
+    if (status) break;
+    if (better) {
+      NmVal v2;
+      const double xc2 = mp - (-2.0) * (mp - Xhi);
+      get(xc2, v2, 1);
+      if (status) break;
+      const bool b2 = cmp(v2, Ylo, false);
+      if (status) break;
+      const double nx = b2 ? xc2 : xc;
+      const NmVal ny = b2 ? v2 : v;
+      if (hi) X1 = nx, Y1 = ny;
+      else X0 = nx, Y0 = ny;
+    } else {
+      const bool worse = cmp(Y0, v, false);  // Y[s_hi], s_hi = 0
+      if (status) break;
+      if (worse) {
+        const bool r1 = cmp(v, hi ? Y1 : Y0, true);
+        if (status) break;
+        if (r1) {
+          if (hi) X1 = xc, Y1 = v;
+          else X0 = xc, Y0 = v;
+        }
+        NmVal v2;
+        const double xh = hi ? X1 : X0;
+        const double xc2 = mp - 0.5 * (mp - xh);
+        get(xc2, v2, r1 ? 3 : 2);
+        if (status) break;
+        const bool r2 = cmp(v2, hi ? Y1 : Y0, true);
+        if (status) break;
+        if (r2) {
+          if (hi) X1 = xc2, Y1 = v2;
+          else X0 = xc2, Y0 = v2;
+        } else {
+          // X[i] = 0.5 (X[i] + X[lo]) for i != lo
+          if (lo == 0) {
+            X1 = 0.5 * (X1 + X0);
+            get(X1, Y1, r1 ? 5 : 4);
+          } else {
+            X0 = 0.5 * (X0 + X1);
+            get(X0, Y0, r1 ? 5 : 4);
+          }
+          if (status) break;
+        }
+      } else {
+        if (hi) X1 = xc, Y1 = v;
+        else X0 = xc, Y0 = v;
+      }
+    }
+    const bool r = cmp(Y1, Y0, false);
+    if (status) break;
+    lo = r ? 1 : 0;
+    const double center = (X0 + X1) / 2;
+    double ssz = 0.0;
+    ssz += fabs(X0 - center);
+    ssz += fabs(X1 - center);
+    if (!(ssz / 2.0 < Tol) && iter < MaxIter) continue;
+    break;
+  }
 }
 
 __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__restrict__ ll,
@@ -679,17 +844,6 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
   __shared__ int sfail;
   unsigned long long round = 0;
   unsigned evals = 0;
-  int status = 0, nneed = 0;
-  double need0 = 0.0, need1 = 0.0;
-  auto request = [&](const NmVal &v) __attribute__((always_inline)) {
-    // branch-free (keeps need0 / need1 in registers)
-    const bool first = !v.exact && nneed == 0;
-    const bool second = !v.exact && nneed == 1 && __double_as_longlong(v.x) != __double_as_longlong(need0);
-    need0 = first ? v.x : need0;
-    need1 = second ? v.x : need1;
-    nneed += (first || second) ? 1 : 0;
-    status = 1;
-  };
   // the last round's points and values stay in LDS (spts, val, sbn) until
   // the next round
   __shared__ int sbn;
@@ -757,158 +911,17 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
       }
     }
     __syncthreads();
-    if (sfail) status = 2;
     tlast = __builtin_amdgcn_s_memrealtime();
     tc0 += rb - ra;
     tc1 += tlast - rb;
+    return sfail != 0;
   };
-  // the value at x; `slot` is where the round's batch put x (checked)
-  auto get = [&](double x, NmVal &v, int slot) __attribute__((always_inline)) {
-    bool found = false;
-    if (tab.n > 0) {
-#pragma unroll
-      for (int t = 0; t < NM_TAB; t++)
-        if (!found && t < tab.n && __double_as_longlong(tab.x[t]) == __double_as_longlong(x)) {
-          v = NmVal{x, tab.y[t], 0.0, 1};
-          found = true;
-        }
-      if (found) return;
-    }
-    if (slot < sbn && __double_as_longlong(spts[slot]) == __double_as_longlong(x)) {
-      v = val[slot];
-      found = true;
-    }
-    for (int k = 0; !found && k < sbn; k++)
-      if (__double_as_longlong(spts[k]) == __double_as_longlong(x)) {
-        v = val[k];
-        found = true;
-        break;
-      }
-    if (!found) {
-      double one[NM_PTS] = {x, 0, 0, 0, 0, 0, 0, 0};
-      run_round(one, 1);
-      v = val[0];
-    }
-    if (v.exact < 0) {  // degenerate: the host's exact value decides
-      v.exact = 0;
-      request(v);
-    }
-  };
-  // a < b (or a <= b): exact values compare exactly, others on their
-  // intervals; undecidable -> request the inexact operands
-  auto cmp = [&](const NmVal &a, const NmVal &b, bool orEqual) __attribute__((always_inline)) -> bool {
-    if (a.exact && b.exact) return orEqual ? a.y <= b.y : a.y < b.y;
-    if (a.y + a.eps < b.y - b.eps) return true;
-    if (a.y - a.eps > b.y + b.eps) return false;
-    request(a);
-    request(b);
-    return false;
-  };
-  const int MaxIter = 1000;
-  const double Tol = 1e-12, Step = 1e-8;
-  double X0 = rho, X1 = rho + Step;
-  NmVal Y0, Y1;
+  double X0 = rho, X1 = rho + 1e-8;  // (GSL step 1e-8)
+  NmVal Y0{}, Y1{};
   long long iter = 0;
-  int lo = 0;
-  {
-    const double p2[NM_PTS] = {X0, X1, 0, 0, 0, 0, 0, 0};
-    run_round(p2, 2);
-    get(X0, Y0, 0);
-    if (!status) get(X1, Y1, 1);
-  }
-  while (status == 0) {
-    iter++;
-    int hi = 0;
-    lo = 0;
-    if (cmp(Y1, Y0, false)) {
-      lo = 1;
-    } else {
-      if (status) break;
-      if (cmp(Y0, Y1, false)) hi = 1;
-    }
-    if (status) break;
-    const double Xhi = hi ? X1 : X0, Xlo = lo ? X1 : X0;
-    const double mp = hi ? X0 : X1;
-    const double xc = mp - (-1.0) * (mp - Xhi);
-    {
-      // every point this iteration may evaluate (the host's batch)
-      double pts[NM_PTS] = {0, 0, 0, 0, 0, 0, 0, 0};
-      int np = 0;
-      pts[np++] = xc;
-      pts[np++] = mp - (-2.0) * (mp - Xhi);
-      pts[np++] = mp - 0.5 * (mp - Xhi);
-      pts[np++] = mp - 0.5 * (mp - xc);
-      // shrink towards lo, with and without X[hi] = xc (1-D: the vertex != lo)
-      const double Xo = lo ? X0 : X1;  // the vertex that is not lo
-      const double XoR = (hi == lo) ? Xo : xc, XloR = (hi == lo) ? xc : Xlo;
-      pts[np++] = 0.5 * (Xo + Xlo);
-      pts[np++] = 0.5 * (XoR + XloR);
-      run_round(pts, np);
-      if (status) break;
-    }
-    NmVal v;
-    get(xc, v, 0);
-    if (status) break;
-    const NmVal Ylo = lo ? Y1 : Y0;
-    const bool better = cmp(v, Ylo, false);
-    if (status) break;
-    if (better) {
-      NmVal v2;
-      const double xc2 = mp - (-2.0) * (mp - Xhi);
-      get(xc2, v2, 1);
-      if (status) break;
-      const bool b2 = cmp(v2, Ylo, false);
-      if (status) break;
-      const double nx = b2 ? xc2 : xc;
-      const NmVal ny = b2 ? v2 : v;
-      if (hi) X1 = nx, Y1 = ny;
-      else X0 = nx, Y0 = ny;
-    } else {
-      const bool worse = cmp(Y0, v, false);  // Y[s_hi], s_hi = 0
-      if (status) break;
-      if (worse) {
-        const bool r1 = cmp(v, hi ? Y1 : Y0, true);
-        if (status) break;
-        if (r1) {
-          if (hi) X1 = xc, Y1 = v;
-          else X0 = xc, Y0 = v;
-        }
-        NmVal v2;
-        const double xh = hi ? X1 : X0;
-        const double xc2 = mp - 0.5 * (mp - xh);
-        get(xc2, v2, r1 ? 3 : 2);
-        if (status) break;
-        const bool r2 = cmp(v2, hi ? Y1 : Y0, true);
-        if (status) break;
-        if (r2) {
-          if (hi) X1 = xc2, Y1 = v2;
-          else X0 = xc2, Y0 = v2;
-        } else {
-          // X[i] = 0.5 (X[i] + X[lo]) for i != lo
-          if (lo == 0) {
-            X1 = 0.5 * (X1 + X0);
-            get(X1, Y1, r1 ? 5 : 4);
-          } else {
-            X0 = 0.5 * (X0 + X1);
-            get(X0, Y0, r1 ? 5 : 4);
-          }
-          if (status) break;
-        }
-      } else {
-        if (hi) X1 = xc, Y1 = v;
-        else X0 = xc, Y0 = v;
-      }
-    }
-    const bool r = cmp(Y1, Y0, false);
-    if (status) break;
-    lo = r ? 1 : 0;
-    const double center = (X0 + X1) / 2;
-    double ssz = 0.0;
-    ssz += fabs(X0 - center);
-    ssz += fabs(X1 - center);
-    if (!(ssz / 2.0 < Tol) && iter < MaxIter) continue;
-    break;
-  }
+  int lo = 0, status = 0, nneed = 0;
+  double need0 = 0.0, need1 = 0.0;
+  nm_drive(tab, val, spts, sbn, run_round, X0, X1, Y0, Y1, iter, lo, status, nneed, need0, need1);
   if (tid == 0) {
     nm_st(&S->quit, 1ull);
     nm_drain();
@@ -930,6 +943,158 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
     out->tc[0] = tc0;
     out->tc[1] = tc1;
     out->tc[2] = tc2 + (__builtin_amdgcn_s_memrealtime() - tlast);
+  }
+}
+
+// The same search with NO controller (round 4): NM_W symmetric workgroups,
+// each holding P/NM_W log-likelihoods in LDS.  A round is ONE hand-off:
+// every workgroup evaluates the round's points on its slice, publishes its
+// partial records (by round parity) and its round flag, waits for every
+// other flag, adds all NM_W records in the fixed tree order, and runs the
+// simplex logic (nm_drive) itself on those identical values, so every
+// workgroup decides the same next points without a broadcast.  (The
+// controller form pays two hand-offs per round: points out, partials in.)
+// Results equal k_tm_nm_search's: the same partials, the same combine, the
+// same logic.
+__global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__restrict__ ll,
+                                                       const TmDev *__restrict__ dev, double rho, double target,
+                                                       NmTab tab, NmSync *__restrict__ S, NmOut *__restrict__ out) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 5, sub = tid & 31;  // point / segment lane of the 32-wide reductions
+  const double llmax = dev->llmaxCv;
+  __shared__ double sll[NM_LDS];
+  __shared__ NmPart red[NM_PTS][NM_TPB];
+  __shared__ NmVal val[NM_PTS];
+  __shared__ double spts[NM_PTS];
+  __shared__ int sfail, sbn;
+  const int w = blockIdx.x, chunk = (P + NM_W - 1) / NM_W;
+  const int i0 = w * chunk < P ? w * chunk : P, i1 = (w + 1) * chunk < P ? (w + 1) * chunk : P;
+  const bool inLds = chunk <= NM_LDS;
+  if (inLds)
+    for (int i = i0 + tid; i < i1; i += NM_TPB) sll[i - i0] = ll[i];
+  unsigned long long round = 0;
+  unsigned evals = 0;
+  unsigned long long tEval = 0, tWait = 0, tRest = 0, tlast = __builtin_amdgcn_s_memrealtime();
+  const dd invP = dd_div(dd{1.0, 0.0}, dd{(double)P, 0.0});
+  auto run_round = [&](const double *pts, int n) __attribute__((always_inline)) {
+    const unsigned long long ra = __builtin_amdgcn_s_memrealtime();
+    tRest += ra - tlast;
+    round++;
+    evals += n;
+    __syncthreads();  // every thread has read the previous round's spts / val (and sll is loaded)
+    if (tid < NM_PTS) spts[tid] = tid < n ? pts[tid] : 0.0;
+    if (tid == 0) sbn = n;
+    // ---- this workgroup's slice (as k_tm_nm_search's workers)
+    NmPart acc[NM_PTS];
+#pragma unroll
+    for (int k = 0; k < NM_PTS; k++) acc[k] = NmPart{0, 0, 0, 0, 0, 0};
+    int fl[NM_PTS];
+#pragma unroll
+    for (int k = 0; k < NM_PTS; k++) fl[k] = 0;
+    for (int i = i0 + tid; i < i1; i += NM_TPB) {
+      const double a = (inLds ? sll[i - i0] : ll[i]) - llmax;
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++) {
+        if (k < n) {
+          const double arg = a * (pts[k] - rho);
+          const double e = exp(arg);
+          fl[k] |= (!isfinite(e) ? 1 : 0) | (arg != 0.0 ? 2 : 0);
+          const double d = e - 1.0;
+          const dd s2 = dd_add(dd{acc[k].s_hi, acc[k].s_lo}, dd{d, 0.0});
+          const dd q2 = dd_add(dd{acc[k].q_hi, acc[k].q_lo}, dd_tp(d, d));
+          acc[k].s_hi = s2.hi, acc[k].s_lo = s2.lo, acc[k].q_hi = q2.hi, acc[k].q_lo = q2.lo;
+          acc[k].mx = e > acc[k].mx ? e : acc[k].mx;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NM_PTS; k++) {
+      acc[k].flags = (double)fl[k];
+      if (k < n) red[k][tid] = acc[k];
+    }
+    __syncthreads();
+    NmPart *mine = S->part2[round & 1][w];
+    if (grp < n) {
+      NmPart v = red[grp][sub];
+      for (int j = 1; j < NM_TPB / 32; j++) v = nm_part_add(v, red[grp][sub + 32 * j]);
+      for (int off = 16; off > 0; off >>= 1) v = nm_part_add(v, nm_part_shfl32(v, off));
+      if (sub == 0) nm_part_st(&mine[grp], v);
+      nm_drain();
+    }
+    __syncthreads();  // every storing wave has drained its stores
+    if (tid == 0) nm_st(&S->done[w], round);
+    const unsigned long long rb = __builtin_amdgcn_s_memrealtime();
+    // ---- every workgroup's records of this round
+    if (wid == 0) {
+      unsigned long long spins = 0;
+      for (;;) {
+        const bool ok = nm_ld(&S->done[lane]) >= round;  // NM_W == 64: one lane per workgroup
+        if (__all(ok)) break;
+        if (++spins >= NM_SPIN_LIMIT) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0) sfail = spins >= NM_SPIN_LIMIT;
+    }
+    __syncthreads();
+    const unsigned long long rc = __builtin_amdgcn_s_memrealtime();
+    if (grp < n) {
+      const int k = grp;
+      NmPart v = nm_part_add(nm_part_ld(&S->part2[round & 1][sub][k]), nm_part_ld(&S->part2[round & 1][sub + 32][k]));
+      for (int off = 16; off > 0; off >>= 1) v = nm_part_add(v, nm_part_shfl32(v, off));
+      if (sub == 0) {
+        const dd Sd{v.s_hi, v.s_lo}, Qd{v.q_hi, v.q_lo};
+        const dd dmean = dd_mul(Sd, invP);
+        const dd ss = dd_add(Qd, dd_mul(dd{-Sd.hi, -Sd.lo}, dmean));
+        const double var = (ss.hi + ss.lo) / (double)(P - 1);
+        const dd mean = dd_add(dmean, dd{1.0, 0.0});
+        const double meand = mean.hi + mean.lo;
+        const double cv = sqrt(var > 0.0 ? var : 0.0) / meand;
+        double c = cv - target;
+        c *= c;
+        const double ratio = v.mx / meand;
+        const double u = 1.1102230246251565e-16, acv = fabs(cv);
+        const double dc = 1e-13 * acv + 32.0 * u * ratio + 4.0 * u * u / (acv > 1e-300 ? acv : 1e-300);
+        const double eps = 2.0 * fabs(cv - target) * dc + dc * dc + 4.0 * u * fabs(c) + 1e-300;
+        const int vf = (int)v.flags;
+        const bool allOne = vf == 0 && P > 1;
+        const bool bad = (vf & 1) || !isfinite(c) || !(meand > 0.0) || !isfinite(ratio) || var < 0.0 ||
+                         !isfinite(eps);
+        const double x = spts[k];
+        val[k] = allOne ? NmVal{x, target * target, 0.0, 1} : NmVal{x, c, eps, bad ? -1 : 0};
+      }
+    }
+    __syncthreads();
+    tlast = __builtin_amdgcn_s_memrealtime();
+    tEval += rb - ra;
+    tWait += rc - rb;
+    return sfail != 0;
+  };
+  double X0 = rho, X1 = rho + 1e-8;  // (GSL step 1e-8)
+  NmVal Y0{}, Y1{};
+  long long iter = 0;
+  int lo = 0, status = 0, nneed = 0;
+  double need0 = 0.0, need1 = 0.0;
+  nm_drive(tab, val, spts, sbn, run_round, X0, X1, Y0, Y1, iter, lo, status, nneed, need0, need1);
+  if (w == 0 && tid == 0) {
+    const NmVal Ylo = lo ? Y1 : Y0;
+    out->X[0] = X0;
+    out->X[1] = X1;
+    out->y[0] = Y0.y;
+    out->y[1] = Y1.y;
+    out->need[0] = need0;
+    out->need[1] = need1;
+    out->iters = iter;
+    out->status = status;
+    out->lo = lo;
+    out->nneed = nneed;
+    out->loExact = status ? 0 : Ylo.exact;
+    out->evals = evals;
+    out->rounds = (unsigned)round;
+    // (controller phases: hand-off wait, combine + logic, evaluation)
+    out->tc[0] = tWait;
+    out->tc[1] = tRest + (__builtin_amdgcn_s_memrealtime() - tlast);
+    out->tc[2] = tEval;
+    out->tw[0] = out->tw[1] = out->tw[2] = 0;
   }
 }
 
@@ -1823,7 +1988,11 @@ int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmi
     // checks the capacity (or fails rather than under-schedules) and, for
     // this per-generation 65-workgroup grid, launches it on the handle's
     // stream instead of ROCm's cooperative queue (kg_common.hpp)
-    if (launch_resident((const void *)k_tm_nm_search, dim3(1 + NM_W), dim3(NM_TPB), args, 0, h->stream,
+    // (KORALI_AMD_NM_SYM=0: the controller form, two hand-offs per round)
+    const char *symEnv = getenv("KORALI_AMD_NM_SYM");  // (read per search: tests switch it)
+    const bool sym = !(symEnv && *symEnv == '0');
+    if (launch_resident(sym ? (const void *)k_tm_nm_sym : (const void *)k_tm_nm_search, dim3(sym ? NM_W : 1 + NM_W),
+                        dim3(NM_TPB), args, 0, h->stream,
                         /*prefer_plain=*/true) !=
         hipSuccess) {
       (void)hipGetLastError();

@@ -135,9 +135,11 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
     search and the oracle."""
     N, P = 6, 1024
     runs = []
-    for exact, host in (("0", "0"), ("1", "0"), ("0", "1")):
+    # (device search: the symmetric form, k_tm_nm_sym, and the controller form, KORALI_AMD_NM_SYM=0)
+    for exact, host, sym in (("0", "0", "1"), ("1", "0", "1"), ("0", "1", "1"), ("0", "0", "0")):
         monkeypatch.setenv("KORALI_AMD_TMCMC_EXACT_SEARCH", exact)
         monkeypatch.setenv("KORALI_AMD_TMCMC_HOST_SEARCH", host)
+        monkeypatch.setenv("KORALI_AMD_NM_SYM", sym)
         dev, o, ndist = seeded_pair(N, P, shared=True, seed=seed, target_cov=target_cov)
         hist = []
         for g in range(1, 30):
@@ -147,7 +149,7 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
             if dev["Annealing Exponent"][0] >= 1.0:
                 break
         runs.append((hist, dev["Exact Search Evaluations"][0]))
-        if exact == "0" and host == "0":
+        if exact == "0" and host == "0" and sym == "1":
             for g in range(1, len(hist) + 1):
                 o.generation(g)
                 assert o["Annealing Exponent"][0] == hist[g - 1][0], g
@@ -156,6 +158,7 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
                 assert o["Covariance Matrix"].tobytes() == hist[g - 1][3], g
     assert runs[0][0] == runs[1][0]
     assert runs[2][0] == runs[1][0]
+    assert runs[3] == runs[0]  # the two device forms: the same searches, the same exact evaluations
     # the interval paths need far fewer exact host evaluations
     assert runs[0][1] < runs[1][1] and runs[2][1] < runs[1][1]
 
