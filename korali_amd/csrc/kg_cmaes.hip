@@ -388,10 +388,12 @@ __global__ void __launch_bounds__(256) k_prescale_t(int N, int rows, int ldz, co
     if (k < N) dzT[(size_t)k * ldz + i0 + ii] = t[ii][kk];  // (rows past `rows`: +0.0)
   }
 }
-inline int sc_ldz(size_t rows) { return (int)((rows + 63) / 64 * 64); }
-template <int C>
+inline int sc_ldz(size_t rows) { return (int)((rows + 127) / 128 * 128); }
+// RPL sample rows per lane (64 RPL per wave): each B value a wave reads
+// through the scalar cache serves RPL rows
+template <int C, int RPL>
 inline unsigned trs_grid(int rows, int N) {
-  const int nrt = (rows + 63) / 64, ncg = (N + 4 * C - 1) / (4 * C);
+  const int nrt = (rows + 64 * RPL - 1) / (64 * RPL), ncg = (N + 4 * C - 1) / (4 * C);
   return (unsigned)(((nrt + TR_XCD - 1) / TR_XCD) * TR_XCD * ncg);
 }
 // default: the scalar-operand form from N = 256 up (C4: 1.55 against 1.70 ms
@@ -399,60 +401,74 @@ inline unsigned trs_grid(int rows, int N) {
 // few 64-row tiles to fill the device, plus the prescale pass)
 inline int transform_width(int N) {  // (read per handle: tests switch it per case)
   const char *e = getenv("KORALI_AMD_TRANSFORM_SC");
-  if (!e || !*e) return N >= 256 ? 8 : 0;
+  if (!e || !*e) return N >= 256 ? 82 : 0;
   const int v = atoi(e);
-  return (v == 8 || v == 16) ? v : 0;
+  return (v == 8 || v == 16 || v == 82) ? v : 0;  // 82: C = 8 columns, 2 rows per lane
 }
-template <int C>
+template <int C, int RPL>
 __global__ void __launch_bounds__(256) k_transform_sc(int N, int rows, int ldz, const double *__restrict__ dzT,
                                                       const double *__restrict__ B, const double *__restrict__ mean,
                                                       CmaesScalars *__restrict__ sc, const double *__restrict__ lb,
                                                       const double *__restrict__ ub, double *__restrict__ X,
                                                       double *__restrict__ BDZ, int *__restrict__ infeas,
                                                       int no_reserve) {
-  constexpr int WC = 4 * C;  // columns per workgroup (4 waves x C)
-  __shared__ double so[64][WC + 1];
+  constexpr int WC = 4 * C, TR = 64 * RPL;  // columns (4 waves x C) and rows per workgroup
+  __shared__ double so[TR][WC + 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware order (as k_transform): the column groups of one 64-row tile
-  // run on one XCD, so its (D o z) rows come from HBM once
+  // XCD-aware order (as k_transform): the column groups of one row tile run
+  // on one XCD, so its (D o z) rows come from HBM once
   const int ncg = (N + WC - 1) / WC;
   const int xcd = blockIdx.x % TR_XCD, j = blockIdx.x / TR_XCD;
   const int rt = (j / ncg) * TR_XCD + xcd, cg = j % ncg;
-  const int i0 = rt * 64;
+  const int i0 = rt * TR;
   if (i0 >= rows) return;
   const int d0 = cg * WC + w * C;
   const double *Bc[C];
 #pragma unroll
   for (int c = 0; c < C; c++) Bc[c] = B + (size_t)min(d0 + c, N - 1) * N;  // (columns past N: discarded)
-  double acc[C];
+  double acc[RPL][C];
 #pragma unroll
-  for (int c = 0; c < C; c++) acc[c] = 0.0;
+  for (int p = 0; p < RPL; p++)
+#pragma unroll
+    for (int c = 0; c < C; c++) acc[p][c] = 0.0;
   const double *zp = dzT + i0 + lane;
-  auto step = [&](double z, int k) {
-    double t[C];
+  auto step = [&](const double *z, int k) {  // z[p]: row i0 + 64 p + lane
+    double t[RPL][C];
 #pragma unroll
-    for (int c = 0; c < C; c++) t[c] = Bc[c][k] * z;
+    for (int c = 0; c < C; c++) {
+      const double b = Bc[c][k];
 #pragma unroll
-    for (int c = 0; c < C; c++) acc[c] += t[c];
+      for (int p = 0; p < RPL; p++) t[p][c] = b * z[p];
+    }
+#pragma unroll
+    for (int p = 0; p < RPL; p++)
+#pragma unroll
+      for (int c = 0; c < C; c++) acc[p][c] += t[p][c];
   };
   // groups of 4 k, the next group's z loads in flight while this one is
   // summed (two register sets in turn: a copy between them would wait for
   // the loads).  Loads past the last group are clamped to row N - 1 rather
   // than branched around (a branch makes the compiler wait for them early).
   const int N4 = N & ~3;
-  double za[4], zb[4];
-  auto load4 = [&](double *z, int k) {
+  double za[4][RPL], zb[4][RPL];
+  auto load4 = [&](double (*z)[RPL], int k) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) z[u] = zp[(size_t)min(k + u, N - 1) * ldz];
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int p = 0; p < RPL; p++) z[u][p] = zp[(size_t)min(k + u, N - 1) * ldz + 64 * p];
   };
   if (N4) load4(za, 0);
   int k = 0;
   for (; k + 8 <= N4; k += 8) {
     load4(zb, k + 4);
+    // (compiler-only fences: B's scalar loads of a group are not hoisted
+    // into the previous one, which ran out of SGPRs and spilled them at RPL 2)
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int u = 0; u < 4; u++) step(za[u], k + u);
     load4(za, k + 8);
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int u = 0; u < 4; u++) step(zb[u], k + 4 + u);
   }
@@ -460,12 +476,19 @@ __global__ void __launch_bounds__(256) k_transform_sc(int N, int rows, int ldz, 
 #pragma unroll
     for (int u = 0; u < 4; u++) step(za[u], k + u);
   }
-  for (int k = N4; k < N; k++) step(zp[(size_t)k * ldz], k);
+  for (int k = N4; k < N; k++) {
+    double z[RPL];
 #pragma unroll
-  for (int c = 0; c < C; c++) so[lane][w * C + c] = acc[c];
+    for (int p = 0; p < RPL; p++) z[p] = zp[(size_t)k * ldz + 64 * p];
+    step(z, k);
+  }
+#pragma unroll
+  for (int p = 0; p < RPL; p++)
+#pragma unroll
+    for (int c = 0; c < C; c++) so[64 * p + lane][w * C + c] = acc[p][c];
   __syncthreads();
   const double sigma = sc->sigma;
-  for (int q = tid; q < 64 * WC; q += 256) {
+  for (int q = tid; q < TR * WC; q += 256) {
     const int r = q / WC, cc = q % WC, i = i0 + r, d = cg * WC + cc;
     if (i >= rows || d >= N) continue;
     const double bdz = so[r][cc];
@@ -3090,12 +3113,15 @@ static int cmaes_transform(kg_cmaes_t h, size_t rows, double *Xo, double *Bo, in
   hipLaunchKernelGGL(k_prescale_t, dim3((unsigned)(ldz / PS_T), (unsigned)((N + PS_T - 1) / PS_T)), dim3(256), 0,
                      h->stream, N, (int)rows, ldz, h->Z, h->D, mirrored, h->dzT);
   KG_HIP(hipGetLastError());
-  if (W == 8)
-    hipLaunchKernelGGL(k_transform_sc<8>, dim3(trs_grid<8>((int)rows, N)), dim3(256), 0, h->stream, N, (int)rows,
-                       ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
+  if (W == 82)
+    hipLaunchKernelGGL((k_transform_sc<8, 2>), dim3(trs_grid<8, 2>((int)rows, N)), dim3(256), 0, h->stream, N,
+                       (int)rows, ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
+  else if (W == 8)
+    hipLaunchKernelGGL((k_transform_sc<8, 1>), dim3(trs_grid<8, 1>((int)rows, N)), dim3(256), 0, h->stream, N,
+                       (int)rows, ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
   else
-    hipLaunchKernelGGL(k_transform_sc<16>, dim3(trs_grid<16>((int)rows, N)), dim3(256), 0, h->stream, N, (int)rows,
-                       ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
+    hipLaunchKernelGGL((k_transform_sc<16, 1>), dim3(trs_grid<16, 1>((int)rows, N)), dim3(256), 0, h->stream, N,
+                       (int)rows, ldz, h->dzT, h->B, h->mean, h->sc, h->lb, h->ub, Xo, Bo, h->infeas, no_reserve);
   KG_HIP(hipGetLastError());
   return 0;
 }

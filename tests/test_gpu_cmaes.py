@@ -239,13 +239,14 @@ def test_tridiagonalisation_kernels_bit_exact(monkeypatch, Nv, lam, kind):
 @pytest.mark.parametrize("Nv,lam,mirrored,bound", [(3, 8, False, None), (10, 64, False, None), (13, 100, True, None),
                                                   (128, 4096, False, None), (67, 300, False, 1.0),
                                                   (10, 64, True, 0.5)])
-def test_scalar_operand_transform_bit_exact(monkeypatch, Nv, lam, mirrored, bound):
+@pytest.mark.parametrize("width", ["8", "82"])
+def test_scalar_operand_transform_bit_exact(monkeypatch, Nv, lam, mirrored, bound, width):
     """k_transform_sc (B in scalar registers, D o z prescaled k-major) forced:
     populations, selections and the updated state bit for bit against the
     oracle, for N not a multiple of the 4-k groups or of the 32-column
     workgroup, row counts not a multiple of 64, Mirrored Sampling and the
     bounded redraw rounds (k_select over the transformed reserve)."""
-    monkeypatch.setenv("KORALI_AMD_TRANSFORM_SC", "8")
+    monkeypatch.setenv("KORALI_AMD_TRANSFORM_SC", width)  # 8 columns per wave, 1 or 2 (82) rows per lane
     seed = 99
     x0 = np.full(Nv, 0.5 if bound == 0.5 else 0.0)
     # sigma0: bound 0.5 starts ON the bound (~10^3 draws per sample, the
