@@ -615,15 +615,96 @@ def c4_cpu_baseline():
                       f"1 warm-up, oracle/refcpu.c -O3 with system libm, 1 thread"}
 
 
+def c4_experiment(generations):
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    e["Problem"]["Objective Kernel"] = "Negative Ackley"
+    for i in range(C4_N):
+        e["Variables"][i]["Name"] = "X" + str(i)
+        e["Variables"][i]["Initial Value"] = 2.0
+        e["Variables"][i]["Initial Standard Deviation"] = 1.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = C4_L
+    e["Solver"]["Covariance Update"] = "MFMA"
+    e["Solver"]["Termination Criteria"]["Max Generations"] = generations
+    e["Random Seed"] = 1337
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    return e
+
+
+def run_c4_engine(args, world, rank):
+    """C4 through korali.Engine with the Distributed conduit (the C++ engine
+    shards the population; RCCL all-gather of fitnesses and sum all-reduce of
+    the mean / rank-mu partials on the handle's stream; Host transport when
+    KORALI_AMD_C4_TRANSPORT=Host).  Fresh runs of `short` and `long`
+    generations (three of each, medians of the slowest rank) cancel the
+    fixed cost of a run: handle creation, the communicator, generation 1."""
+    import korali
+    import socket
+    import torch.distributed as tdist
+    if "MASTER_PORT" not in os.environ:  # (one rank started without torch.distributed.run)
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("RANK", str(rank))
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    tdist.init_process_group("gloo")  # (timing exchange only; the engine brings its own bootstrap + RCCL)
+    transport = os.environ.get("KORALI_AMD_C4_TRANSPORT", "RCCL")
+
+    def run(gens):
+        k = korali.Engine()
+        k["Conduit"]["Type"] = "Distributed"
+        k["Conduit"]["Transport"] = transport
+        e = c4_experiment(gens)
+        tdist.barrier()
+        t0 = time.perf_counter()
+        k.run(e)
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item()), float(e["Solver"]["Best Ever Value"])
+
+    import torch
+    run(max(1, args.warmup))
+    short, long_ = 2, 2 + args.steps
+    med, best = {}, None
+    for n in (short, long_):
+        ts = []
+        for _ in range(3):
+            t, best = run(n)
+            ts.append(t)
+        med[n] = sorted(ts)[1]
+    elapsed = med[long_] - med[short]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "CMA-ES generations/sec, 512-dim Ackley lambda=65536 (C4)", "value": args.steps / elapsed,
+            "unit": "generations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768 Logarithmic, x0=2, "
+                                   "sigma0=1, seed 1337; korali.Engine, Distributed conduit (" + transport + ")",
+                       "parallelism": f"population-shard{world}"},
+            "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
+            "timing": "fresh runs of %d and %d generations, medians over 3, slowest rank" % (short, long_),
+            "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
+    tdist.destroy_process_group()
+
+
 def run_c4(args):
     """BASELINE.json configs[3]: CMA-ES, 512-dim negative Ackley
     (model.py:37-62), λ = 65536, μ = 32768, x0 = 2, σ0 = 1, seed 1337.  With
-    N > 1 ranks the population is sharded (korali_amd/sharded.py: RCCL
-    all-gather of fitnesses, sum all-reduce of the mean / rank-μ partials);
-    total work is fixed, so scaling is strong."""
+    N > 1 ranks (or KORALI_AMD_C4_ENGINE=1) it runs through korali.Engine's
+    Distributed conduit (run_c4_engine); one rank times the C-ABI loop
+    (KORALI_AMD_C4_ENGINE=0 with N > 1: the Python sharded driver,
+    korali_amd/sharded.py).  Total work is fixed, so scaling is strong."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    eng = os.environ.get("KORALI_AMD_C4_ENGINE", "1" if world > 1 else "0") == "1"
+    if eng:
+        return run_c4_engine(args, world, rank)
     import torch
     kw = dict(initial_value=np.full(C4_N, 2.0), initial_std=np.ones(C4_N), normal_seed=1337, uniform_seed=1338)
     dist = None
