@@ -33,6 +33,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     trace2dpp) step trace2_dpp0 200 env KORALI_AMD_SQ_DPP=0 KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
     c4p) step prof4p 400 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python bench.py --workload c4 --steps 6 --warmup 2 --no-cpu-baseline && step pmc4fp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4wp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step mfma4p 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     c4eng) step c4eng 600 env KORALI_AMD_C4_ENGINE=1 python bench.py --workload c4 --steps 8 --warmup 2 --no-cpu-baseline ;;
+    nmab) step nm_sym0 300 env KORALI_AMD_NM_SYM=0 python tools/nm_probe.py 8192 && step nm_sym1 300 env KORALI_AMD_NM_SYM=1 python tools/nm_probe.py 8192 ;;
+    pmc5g) step pmc5gf 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex "k_vr_gemm" -d "$OUT/pmc5_fetch" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline && step pmc5gw 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex "k_vr_gemm" -d "$OUT/pmc5_write" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     ub) step ub 120 ./tools/ubench_chains ;;
     rowab) step bench_row0 300 env KORALI_AMD_ROWCHAINS=0 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_row1 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
     sqab) step bench_sq0 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline && step bench_sq1 300 env KORALI_AMD_SQ_DPP=1 python bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
