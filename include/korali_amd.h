@@ -400,6 +400,16 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences);
 int kg_vracer_train_policy(kg_vracer_t h, size_t updates);
 int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *sorted_ids, size_t count);
 int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates);
+/* Agent::testingGeneration (agent.cpp.base:267-289) on the device CartPole:
+ * one episode per entry, reset with seed sample_ids[j] * 1024 +
+ * launch_ids[j] (env.py), actions = the policy's mode
+ * (generateTestingAction, continuous.cpp.base:219-260: Normal mean, Clipped
+ * Normal mean clipped), environment 0's reward, up to max_episode_steps;
+ * rewards[j] = the episode's cumulative reward ("Testing Reward",
+ * reinforcementLearning.cpp.base:207-255).  Uses the current
+ * hyperparameters; replay memory and agent state are untouched. */
+int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uint64_t *launch_ids, size_t n,
+                            float *rewards);
 int kg_vracer_synchronize(kg_vracer_t h);
 int kg_vracer_stream(kg_vracer_t h, void **stream);
 /* Stage timers (HIP events on the handle's stream): "environment_step",

@@ -1485,7 +1485,10 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
   auto load = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < AR_TU; u++) {
-      const int q = tid + 512 * u, r = q / AR_K, k = k0 + q % AR_K;
+      const int q = tid + 512 * u, r = q / AR_K;
+      int kq = q % AR_K;
+      asm volatile("" : "+v"(kq));  // (an opaque value: no SDWA byte-select form of `q % 256` in its uses)
+      const int k = k0 + kq;
       tv[u] = (d0 + r < N && k < mu) ? Tt[(size_t)(d0 + r) * mu + k] : 0.0;
     }
 #pragma unroll
@@ -1498,7 +1501,9 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
 #pragma unroll
     for (int u = 0; u < AR_TU; u++) {
       const int q = tid + 512 * u;
-      Ts[b][q / AR_K][q % AR_K] = tv[u];
+      int kq = q % AR_K;
+      asm volatile("" : "+v"(kq));
+      Ts[b][q / AR_K][kq] = tv[u];
     }
 #pragma unroll
     for (int u = 0; u < AR_YU; u++) {

@@ -886,6 +886,51 @@ __global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long s
   (void)only_fin;
 }
 
+// Testing episodes (Agent::testingGeneration, agent.cpp.base:267-289;
+// ReinforcementLearning::runTestingEpisode, reinforcementLearning.cpp.base:
+// 207-255): episode j resets CartPole with seed sample_id * 1024 + launch_id
+// (env.py), takes the policy's mode as the action (generateTestingAction,
+// continuous.cpp.base:219-260: the Normal mean; Clipped Normal: the mean
+// clipped to the bounds), and adds the reward of environment 0 (env.py:
+// testing runs environment 0) until the pole falls or max_episode_steps.
+__global__ void k_vr_test_reset(int n, int S, const unsigned long long *__restrict__ sid,
+                                const unsigned long long *__restrict__ lid, double *u, double *tm, int *steps,
+                                int *done, float *cum, float *X) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double y[4];
+  cp_reset((unsigned)(sid[e] * 1024ull + lid[e]), y);
+  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * S + k] = (float)y[k];
+  tm[e] = 0.0;
+  steps[e] = 0;
+  done[e] = 0;
+  cum[e] = 0.f;
+}
+__global__ void k_vr_test_act(Params P, int n, const float *__restrict__ out, double *u, double *tm, int *steps,
+                              int *done, float *cum, float *X, unsigned *errors, int *running) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || done[e]) return;
+  float act = out[(long long)e * P.O + 1];  // the mode (A = 1: the CartPole kernel)
+  if (P.clipped) {
+    if (act >= P.ub[0]) act = P.ub[0];
+    if (act <= P.lb[0]) act = P.lb[0];
+  }
+  double y[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) y[k] = u[e * 4 + k];
+  double t = tm[e];
+  if (!cp_advance(y, t, (double)act)) atomicOr(errors, (unsigned)ERR_ENV_ODE);
+  tm[e] = t;
+#pragma unroll
+  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * P.S + k] = (float)y[k];
+  const bool failed = cp_failed(y);
+  cum[e] += (float)(1.0 - 1.0 * (failed ? 1.0 : 0.0));
+  const int st = steps[e] + 1;
+  steps[e] = st;
+  if (failed || st >= P.T) done[e] = 1;
+  else atomicAdd(running, 1);
+}
+
 // One action of every environment (continuous.cpp.base:95-150 Normal policy:
 // action = mean + sigma N(0,1)); the experience is kept in the episode buffer.
 __global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restrict__ out, float *X,
@@ -1630,6 +1675,68 @@ int kg_vracer_run_policy(kg_vracer_t h, const float *states, size_t n, float *ou
   KG_HIP(hipMemcpyAsync(out, h->out, n * h->P.O * 4, hipMemcpyDeviceToHost, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
+}
+
+int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uint64_t *launch_ids, size_t n,
+                            float *rewards) {
+  KG_CHECK(h && sample_ids && launch_ids && rewards, "vracer: null argument");
+  KG_CHECK(h->P.A == 1 && h->P.S == 4, "vracer: testing episodes run the CartPole kernel (4 states, 1 action)");
+  const size_t chunk = h->rowsMax;  // episodes per batch (the forward's rows)
+  unsigned long long *dsid = nullptr, *dlid = nullptr;
+  double *u = nullptr, *tm = nullptr;
+  int *steps = nullptr, *done = nullptr, *running = nullptr;
+  float *cum = nullptr;
+  unsigned *errs = nullptr;
+  int rc = 0;
+  bool named = false;  // an error message was set
+  auto fail = [&](hipError_t e) {
+    if (e != hipSuccess) rc = 1;
+    return e != hipSuccess;
+  };
+  if (fail(hipMalloc(&dsid, chunk * 8)) || fail(hipMalloc(&dlid, chunk * 8)) || fail(hipMalloc(&u, chunk * 32)) ||
+      fail(hipMalloc(&tm, chunk * 8)) || fail(hipMalloc(&steps, chunk * 4)) || fail(hipMalloc(&done, chunk * 4)) ||
+      fail(hipMalloc(&cum, chunk * 4)) || fail(hipMalloc(&running, 4)) || fail(hipMalloc(&errs, 4)))
+    kg::set_error("vracer: testing buffers could not be allocated"), named = true;
+  for (size_t b0 = 0; rc == 0 && b0 < n; b0 += chunk) {
+    const int m = (int)std::min(chunk, n - b0);
+    const dim3 grid((m + 255) / 256);
+    if (fail(hipMemcpyAsync(dsid, sample_ids + b0, m * 8, hipMemcpyHostToDevice, h->stream)) ||
+        fail(hipMemcpyAsync(dlid, launch_ids + b0, m * 8, hipMemcpyHostToDevice, h->stream)) ||
+        fail(hipMemsetAsync(errs, 0, 4, h->stream)))
+      break;
+    hipLaunchKernelGGL(k_vr_test_reset, grid, dim3(256), 0, h->stream, m, h->P.S, dsid, dlid, u, tm, steps, done,
+                       cum, h->Xs);
+    for (int t = 0; t < h->P.T; t++) {
+      if (vr_forward(h, h->Xs, m, h->out)) {
+        rc = 1, named = true;
+        break;
+      }
+      if (t % 16 == 0 && fail(hipMemsetAsync(running, 0, 4, h->stream))) break;
+      hipLaunchKernelGGL(k_vr_test_act, grid, dim3(256), 0, h->stream, h->P, m, (const float *)h->out, u, tm, steps,
+                         done, cum, h->Xs, errs, running);
+      if (t % 16 == 15) {  // every 16 steps: stop once every episode has ended
+        int r = 0;
+        if (fail(hipMemcpyAsync(&r, running, 4, hipMemcpyDeviceToHost, h->stream)) ||
+            fail(hipStreamSynchronize(h->stream)))
+          break;
+        if (r == 0) break;
+      }
+    }
+    unsigned e = 0;
+    if (rc == 0 && (fail(hipMemcpyAsync(rewards + b0, cum, m * 4, hipMemcpyDeviceToHost, h->stream)) ||
+                    fail(hipMemcpyAsync(&e, errs, 4, hipMemcpyDeviceToHost, h->stream)) ||
+                    fail(hipStreamSynchronize(h->stream))))
+      break;
+    if (e) {
+      kg::set_error("CartPole: the dopri5 integration failed (more than 500 steps or a vanishing step)");
+      rc = 1, named = true;
+    }
+  }
+  for (void *p : {(void *)dsid, (void *)dlid, (void *)u, (void *)tm, (void *)steps, (void *)done, (void *)cum,
+                  (void *)running, (void *)errs})
+    if (p) (void)hipFree(p);
+  if (rc && !named) kg::set_error("vracer: testing episodes failed (HIP error)");
+  return rc;
 }
 
 int kg_vracer_set_action_noise(kg_vracer_t h, const float *noise, size_t n) {

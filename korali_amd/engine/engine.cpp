@@ -1595,6 +1595,9 @@ struct VracerModule : SolverModule {
   float lastReward = 0.f, bestReward = -INFINITY, averageReward = 0.f;
   Json *solverJs = nullptr;
   Json description;  // vracerPolicyDescription: written into every result file
+  bool testing = false, tested = false;  // Mode = Testing
+  std::vector<uint64_t> testingIds;
+  std::vector<float> testingReward;
 
   ~VracerModule() override {
     if (h) kg_vracer_destroy(h);
@@ -1610,7 +1613,19 @@ struct VracerModule : SolverModule {
            pb["Type"].getString().c_str());
     rejectUnrecognised(sv, "VRACER", {SOLVER_KEYS, AGENT_KEYS}, {SOLVER_TERMINATION, AGENT_TERMINATION});
     rejectUnrecognised(pb, "Continuous", {RL_KEYS}, {});
-    if (resume) fail("Resuming a VRACER experiment is not supported by the device path.");
+    const std::string mode = canon(str(sv, "Mode", "Training"));
+    if (mode != "training" && mode != "testing") fail("'Mode' must be 'Training' or 'Testing'.");
+    testing = mode == "testing";
+    // a training run does not resume (the replay memory is not serialized);
+    // Testing runs one generation of the policy the experiment holds
+    if (resume && !testing) fail("Resuming a VRACER training run is not supported by the device path.");
+    if (testing) {
+      Json &tj = sv["Testing"];
+      if (tj.contains("Sample Ids"))
+        for (size_t i = 0; i < tj["Sample Ids"].size(); i++) testingIds.push_back(tj["Sample Ids"][i].getUInt());
+      if (testingIds.empty())
+        fail("For testing, you need to indicate the sample ids to run in the ['Testing']['Sample Ids'] field.\n");
+    }
     if (!pb.contains("Environment Kernel"))
       fail("Problem 'Reinforcement Learning / Continuous' on the device needs 'Environment Kernel' (\"CartPole\": the "
            "environment of examples/learning/reinforcement/cartpole); a host 'Environment Function' cannot run "
@@ -1645,7 +1660,6 @@ struct VracerModule : SolverModule {
     if (nState != 4 || nAction != 1)
       fail("The CartPole environment kernel has 4 state variables and 1 action variable (%zu / %zu given).", nState,
            nAction);
-    if (canon(str(sv, "Mode", "Training")) != "training") fail("Only 'Mode' = 'Training' is supported by the device path.");
     const std::string dist = canon(str(sv["Policy"], "Distribution", "Normal"));
     if (dist != "normal" && dist != "clippednormal")
       fail("Policy Distribution '%s' is not supported by the device path (Normal, Clipped Normal).",
@@ -1732,6 +1746,16 @@ struct VracerModule : SolverModule {
       auto v = flatten(sv["Training"]["Current Policy"]["Policy"]);
       for (size_t i = 0; i < n; i++) theta[i] = (float)v[i];
     }
+    if (testing) {
+      // agent.cpp.base:139-153: the Testing policy (Testing / Current Policy,
+      // else the training policy), the sample ids, one generation
+      Json &tj = sv["Testing"];
+      if (tj.contains("Current Policy") && tj["Current Policy"].contains("Policy") &&
+          tj["Current Policy"]["Policy"].size() == n) {
+        auto v = flatten(tj["Current Policy"]["Policy"]);
+        for (size_t i = 0; i < n; i++) theta[i] = (float)v[i];
+      }
+    }
     check(kg_vracer_set_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
   }
 
@@ -1741,8 +1765,18 @@ struct VracerModule : SolverModule {
     return v;
   }
 
-  // Agent::trainingGeneration (agent.cpp.base:162-265)
+  // Agent::trainingGeneration (agent.cpp.base:162-265), or testingGeneration
+  // (:267-289): one deterministic episode per testing sample id, launch ids
+  // in launch order (a fresh environment per run, reinforcementLearning.cpp.base:67)
   void runGeneration(size_t) override {
+    if (testing) {
+      std::vector<uint64_t> lid(testingIds.size());
+      for (size_t i = 0; i < lid.size(); i++) lid[i] = i;
+      testingReward.assign(testingIds.size(), 0.f);
+      check(kg_vracer_test_episodes(h, testingIds.data(), lid.data(), testingIds.size(), testingReward.data()));
+      tested = true;
+      return;
+    }
     while (sessionEpisodes < episodesPerGeneration * sessionGeneration) {
       size_t added = 0, updates = 0;
       check(kg_vracer_training_step(h, &added, &updates));
@@ -1766,6 +1800,10 @@ struct VracerModule : SolverModule {
   }
 
   void checkTermination(size_t gen, std::vector<std::string> &met) override {
+    if (testing) {  // Max Generations = the current generation + 1 (agent.cpp.base:141-142)
+      if (tested) met.push_back("Max Generations");
+      return;
+    }
     if ((double)gen > maxGenerations) met.push_back("Max Generations");
     if (gen == 1) return;
     if (maxEpisodes > 0 && scalar("current_episode") >= (double)maxEpisodes) met.push_back("Max Episodes");
@@ -1775,6 +1813,10 @@ struct VracerModule : SolverModule {
   }
 
   void getConfiguration(Json &sv) override {
+    if (testing) {
+      sv["Testing"]["Reward"] = std::vector<double>(testingReward.begin(), testingReward.end());
+      return;
+    }
     sv["Current Episode"] = (unsigned long long)scalar("current_episode");
     sv["Experience Count"] = (unsigned long long)scalar("experience_count");
     sv["Policy Update Count"] = (unsigned long long)scalar("policy_update_count");
@@ -1802,6 +1844,14 @@ struct VracerModule : SolverModule {
   void finalize(Json &) override {}
 
   void printAfter(const Logger &log) override {
+    if (testing) {  // agent.cpp.base:1038-1045
+      log.log(1, "Testing Results:\n");
+      for (size_t i = 0; i < testingIds.size(); i++) {
+        log.log(1, " + Sample %llu:\n", (unsigned long long)testingIds[i]);
+        log.log(1, "   + (Average) Cumulative Reward            %f\n", testingReward[i]);
+      }
+      return;
+    }
     log.log(2, "Experience Replay Statistics:\n");
     log.log(2, " + Experience Memory Size:      %.0f/%.0f\n", scalar("size"),
             (*solverJs)["Experience Replay"]["Maximum Size"].getDouble());

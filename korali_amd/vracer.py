@@ -60,6 +60,8 @@ def _lib():
         L.kg_vracer_train_policy.argtypes = [vp, sz]
         L.kg_vracer_train_policy_minibatch.argtypes = [vp, C.POINTER(C.c_uint32), sz]
         L.kg_vracer_training_step.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
+        u64p = C.POINTER(C.c_uint64)
+        L.kg_vracer_test_episodes.argtypes = [vp, u64p, u64p, sz, fp]
         L.kg_vracer_stream.argtypes = [vp, C.POINTER(vp)]
         L.kg_vracer_profile.argtypes = [vp, C.c_int]
         L.kg_vracer_profile_read.argtypes = [vp, cp, C.POINTER(C.c_double), C.POINTER(sz)]
@@ -172,6 +174,17 @@ class VracerDevice:
         n, u = C.c_size_t(), C.c_size_t()
         check(_lib().kg_vracer_training_step(self._h, C.byref(n), C.byref(u)))
         return n.value, u.value
+
+    def test_episodes(self, sample_ids, launch_ids=None):
+        """Testing episodes (Agent::testingGeneration): the cumulative reward of
+        one deterministic CartPole episode per sample id."""
+        sid = np.ascontiguousarray(sample_ids, np.uint64)
+        lid = np.ascontiguousarray(np.arange(sid.size) if launch_ids is None else launch_ids, np.uint64)
+        out = np.empty(sid.size, np.float32)
+        u64p = C.POINTER(C.c_uint64)
+        check(_lib().kg_vracer_test_episodes(self._h, sid.ctypes.data_as(u64p), lid.ctypes.data_as(u64p), sid.size,
+                                             _fptr(out)))
+        return out
 
     def synchronize(self):
         check(_lib().kg_vracer_synchronize(self._h))

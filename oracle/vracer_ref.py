@@ -533,6 +533,36 @@ class CartPole:
         return (r, r - 1.0, r * 0.1)[env_id % 3]
 
 
+def testing_episodes(theta, sample_ids, launch_ids, S, H, L, A, initial_noise, max_steps, clipped=False, lb=None,
+                     ub=None):
+    """Agent::testingGeneration (agent.cpp.base:267-289) with the CartPole
+    environment: ReinforcementLearning::runTestingEpisode
+    (reinforcementLearning.cpp.base:207-255) adds environment 0's reward (the
+    testing branch of env.py) of every step taken with the policy's mode
+    (continuous.cpp.base:219-260: Normal mean; Clipped Normal: clipped to
+    the bounds) until the pole falls or max_steps; reset seed
+    sample_id * 1024 + launch_id (env.py).  Returns the cumulative rewards."""
+    rewards = []
+    for sid, lid in zip(sample_ids, launch_ids):
+        cp = CartPole()
+        cp.reset(int(sid) * 1024 + int(lid))
+        total = f32(0.0)
+        for _ in range(max_steps):
+            out, _ = forward(theta, cp.u.astype(f32)[None, :], S, H, L, A, initial_noise)
+            act = out[0, 1]
+            if clipped:  # (continuous.cpp.base:242-252's order)
+                if act >= f32(ub):
+                    act = f32(ub)
+                if act <= f32(lb):
+                    act = f32(lb)
+            done = cp.advance(float(act))
+            total = f32(total + f32(cp.reward(0)))
+            if done:
+                break
+        rewards.append(total)
+    return np.array(rewards, f32)
+
+
 # scipy.integrate.ode 'dopri5' = E. Hairer & G. Wanner's DOPRI5 (dopri5.f,
 # Dormand-Prince 5(4)), as scipy calls it for one integrate(): rtol 1e-6,
 # atol 1e-12 (scalars: ITOL 0), WORK = (UROUND 0 -> 2.3e-16, SAFE 0.9,

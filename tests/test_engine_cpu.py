@@ -189,6 +189,8 @@ from vracer_cases import cartpole_vracer  # noqa: E402
      "Elementwise/Tanh"),
     (lambda e: e["Solver"]["State Rescaling"].__setitem__("Enabled", True), "State Rescaling"),
     (lambda e: e["Solver"]["Neural Network"].__setitem__("Optimizer", "RMSProp"), "Adam"),
+    (lambda e: e["Solver"].__setitem__("Mode", "Testing"), "Sample Ids"),  # agent.cpp.base:147-149
+    (lambda e: e["Solver"].__setitem__("Mode", "Evaluation"), "'Mode' must be"),
 ])
 def test_vracer_configuration_errors_before_device(edit, msg):
     e = cartpole_vracer()

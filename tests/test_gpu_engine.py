@@ -693,3 +693,32 @@ def test_vracer_cartpole_through_korali_engine(policy):
     assert hist.size == sv["Current Episode"] and np.all(np.isfinite(hist))
     assert len(sv["Training"]["Current Policy"]["Policy"]) == (4 * 64 + 64) + (64 * 64 + 64) + (64 * 3 + 3)
     assert np.isfinite(sv["Training"]["Average Reward"])
+
+
+def test_vracer_testing_mode_after_training():
+    """The reference's testing flow: train, then e["Solver"]["Mode"] =
+    "Testing" with Testing / Sample Ids and run the same experiment again;
+    one generation of deterministic episodes with the trained policy
+    (agent.cpp.base:139-153, 267-289), rewards in Testing / Reward equal to
+    the device's testing episodes run directly with that policy."""
+    import korali
+    from korali_amd.vracer import VracerDevice
+    from vracer_cases import cartpole_vracer
+    e = cartpole_vracer(max_generations=5, environments=16, hidden=32)
+    korali.Engine().run(e)
+    gen = e["Current Generation"]
+    pol = np.array(e["Solver"]["Training"]["Current Policy"]["Policy"], np.float32)
+    e["Solver"]["Mode"] = "Testing"
+    e["Solver"]["Testing"]["Sample Ids"] = list(range(12))
+    korali.Engine().run(e)
+    assert e["Current Generation"] == gen + 1
+    got = np.array(e["Solver"]["Testing"]["Reward"], np.float32)
+    assert got.size == 12 and np.all(got >= 1.0)
+    noise = e["Variables"][4]["Initial Exploration Noise"]
+    bounds = dict(policy_distribution="Clipped Normal", action_lower_bound=e["Variables"][4]["Lower Bound"],
+                  action_upper_bound=e["Variables"][4]["Upper Bound"]) \
+        if e["Solver"]["Policy"]["Distribution"] == "Clipped Normal" else {}
+    d = VracerDevice(hidden_size=32, hidden_layers=2, environments=16, mini_batch_size=32, replay_maximum_size=1024,
+                     replay_start_size=512, initial_exploration_noise=noise, hyperparameters=pol, **bounds)
+    assert np.array_equal(got, d.test_episodes(np.arange(12)))
+    d.close()

@@ -256,3 +256,36 @@ def test_device_cartpole_matches_reference_trajectories():
     print(f"device CartPole vs scipy dopri5: max |diff| {worst:.3e}, {exact} of "
           f"{sum(len(t['u']) for t in tr)} states bit-identical")
     assert worst <= 2e-11
+
+
+@pytest.mark.parametrize("H,L,clipped,spread", [(64, 2, False, 0.0), (64, 2, True, 0.0), (128, 2, False, 0.15),
+                                                (32, 1, True, 0.15)])
+def test_testing_episodes_match_oracle(H, L, clipped, spread):
+    """Testing mode (Agent::testingGeneration): one deterministic CartPole
+    episode per sample id, the policy's mode as the action.  spread 0: every
+    weight but the output biases zero, so the actions do not depend on the
+    float32 forward's summation order and the episodes equal the oracle's
+    exactly; otherwise the mode moves by float32 rounding, which may shift a
+    failure by a step."""
+    n = V.hyperparameter_count(S, H, L, A)
+    rng = np.random.default_rng(5)
+    if spread == 0.0:
+        th = np.zeros(n, f32)
+        th[n - 3:] = np.array([0.1, 0.35 if not clipped else 0.8, 0.0], f32)  # output biases: V, mean, sigma
+    else:
+        th = theta_for(H, L, 7, spread=spread)
+    kw = clip_kw(clipped)
+    d = device(hidden_size=H, hidden_layers=L, environments=64, mini_batch_size=32, replay_maximum_size=1024,
+               replay_start_size=512, initial_exploration_noise=0.5, hyperparameters=th, **kw)
+    sids = np.array([0, 1, 2, 7, 11, 40, 41, 99] + list(range(200, 290)), np.uint64)
+    lids = np.arange(sids.size, dtype=np.uint64)
+    got = d.test_episodes(sids, lids)
+    ref = V.testing_episodes(th, sids, lids, S, H, L, A, 0.5, 500, clipped=clipped,
+                             lb=CLIP[0][0] if clipped else None, ub=CLIP[1][0] if clipped else None)
+    if spread == 0.0:
+        assert np.array_equal(got, ref), (got, ref)
+    else:
+        assert np.abs(got - ref).max() <= 1.0, (got, ref)
+        assert np.mean(got == ref) >= 0.9
+    assert np.all(got >= 1.0)
+    d.close()
