@@ -638,11 +638,13 @@ def run_c4_engine(args, world, rank):
     """C4 through korali.Engine with the Distributed conduit (the C++ engine
     shards the population; RCCL all-gather of fitnesses and sum all-reduce of
     the mean / rank-mu partials on the handle's stream; Host transport when
-    KORALI_AMD_C4_TRANSPORT=Host).  Fresh runs of `short` and `long`
-    generations (three of each, medians of the slowest rank) cancel the
-    fixed cost of a run: handle creation, the communicator, generation 1."""
+    KORALI_AMD_C4_TRANSPORT=Host).  One run of warmup + steps generations;
+    the engine records when each generation completed (its termination check
+    returned, Internal / Generation Completion Times), and the timed region
+    is the last `steps` generations of the slowest rank."""
     import korali
     import socket
+    import torch
     import torch.distributed as tdist
     if "MASTER_PORT" not in os.environ:  # (one rank started without torch.distributed.run)
         with socket.socket() as sk:
@@ -653,30 +655,22 @@ def run_c4_engine(args, world, rank):
     os.environ.setdefault("WORLD_SIZE", str(world))
     tdist.init_process_group("gloo")  # (timing exchange only; the engine brings its own bootstrap + RCCL)
     transport = os.environ.get("KORALI_AMD_C4_TRANSPORT", "RCCL")
-
-    def run(gens):
-        k = korali.Engine()
-        k["Conduit"]["Type"] = "Distributed"
-        k["Conduit"]["Transport"] = transport
-        e = c4_experiment(gens)
-        tdist.barrier()
-        t0 = time.perf_counter()
-        k.run(e)
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        return float(t.item()), float(e["Solver"]["Best Ever Value"])
-
-    import torch
-    run(max(1, args.warmup))
-    short, long_ = 2, 2 + args.steps
-    med, best = {}, None
-    for n in (short, long_):
-        ts = []
-        for _ in range(3):
-            t, best = run(n)
-            ts.append(t)
-        med[n] = sorted(ts)[1]
-    elapsed = med[long_] - med[short]
+    w = max(1, args.warmup)
+    total = w + args.steps
+    k = korali.Engine()
+    k["Conduit"]["Type"] = "Distributed"
+    k["Conduit"]["Transport"] = transport
+    e = c4_experiment(total)
+    tdist.barrier()
+    k.run(e)
+    marks = list(e["Internal"]["Generation Completion Times"])
+    gens = int(e["Current Generation"])
+    if gens != total or len(marks) != total + 1:
+        raise RuntimeError(f"engine ran {gens} generations ({len(marks)} marks), expected {total}")
+    t = torch.tensor([marks[total] - marks[w]], dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    best = float(e["Solver"]["Best Ever Value"])
     if rank == 0:
         print(json.dumps({
             "metric": "CMA-ES generations/sec, 512-dim Ackley lambda=65536 (C4)", "value": args.steps / elapsed,
@@ -687,7 +681,8 @@ def run_c4_engine(args, world, rank):
                                    "sigma0=1, seed 1337; korali.Engine, Distributed conduit (" + transport + ")",
                        "parallelism": f"population-shard{world}"},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
-            "timing": "fresh runs of %d and %d generations, medians over 3, slowest rank" % (short, long_),
+            "timing": "generations %d-%d of one %d-generation engine run (engine completion marks), slowest rank"
+                      % (w + 1, total, total),
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
     tdist.destroy_process_group()
 

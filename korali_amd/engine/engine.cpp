@@ -1952,9 +1952,14 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   if (gen == 0 && fileOut) save();
   gen++;
   std::vector<std::string> met;
+  // marks[i]: seconds from the start of the loop until generation i (1-based
+  // from the first generation of this run) had completed, i.e. until its
+  // termination check returned; marks[0] is the loop's first check
+  std::vector<double> marks;
   for (;;) {
     met.clear();
     solver.checkTermination(gen, met);
+    marks.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     if (!met.empty()) break;
     if (consoleFreq > 0 && gen % consoleFreq == 0) {
       st.log.log(1, "--------------------------------------------------------------------\n");
@@ -1978,6 +1983,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   js["Is Finished"] = true;
   solver.finalize(js);
   js["Current Generation"] = (unsigned long long)gen;
+  js["Internal"]["Generation Completion Times"] = marks;
   solver.getConfiguration(sv);
   if (tm) tm->saveDistributions(js);
   if (fileOut) saveState(js, gen);

@@ -185,6 +185,8 @@ def test_engine_reproduces_reference_result_files(tmp_path):
     e = fixture_experiment(out)
     korali.Engine().run(e)
     assert e["Current Generation"] == 100
+    marks = list(e["Internal"]["Generation Completion Times"])  # (bench.py's C4 engine timing)
+    assert len(marks) == 101 and all(b >= a for a, b in zip(marks, marks[1:]))
     for ref in CM:
         g = ref["Current Generation"]
         if g == 0:
