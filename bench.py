@@ -554,6 +554,7 @@ def run_c3(args):
         if n:
             stages[st] = ms / n
     search = {"generations": g, "exact_host_evaluations_per_generation": dev["Exact Search Evaluations"][0] / g,
+              "of_which_deferred_to_host_worker": dev["Deferred Search Evaluations"][0] / g,
               "device_search_rounds_per_generation": dev["Device Search Rounds"][0] / g,
               "device_search_relaunches": dev["Device Search Relaunches"][0]}
     dev.close()

@@ -27,7 +27,10 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <condition_variable>
 #include <string>
+#include <thread>
+#include <utility>
 #include <tuple>
 #include <vector>
 
@@ -526,6 +529,8 @@ struct NmOut {
   double X[2], y[2], need[2];
   long long iters;
   int status, lo, nneed, loExact;  // status 0 done, 1 exact values needed, 2 no progress (the host searches)
+  int loBad;                        // Ylo's interval is void (degenerate value): only its exact value decides
+  double loEps;                     // |Ylo - exact| <= loEps otherwise
   unsigned evals, rounds;
   // phase times (s_memrealtime, 100 MHz ticks): controller publish+wait,
   // combine, simplex logic; worker 1 wait, evaluate, reduce+publish
@@ -938,6 +943,8 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
     out->lo = lo;
     out->nneed = nneed;
     out->loExact = status ? 0 : Ylo.exact;
+    out->loBad = Ylo.exact < 0;
+    out->loEps = Ylo.eps;
     out->evals = evals;
     out->rounds = (unsigned)round;
     out->tc[0] = tc0;
@@ -1088,6 +1095,8 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     out->lo = lo;
     out->nneed = nneed;
     out->loExact = status ? 0 : Ylo.exact;
+    out->loBad = Ylo.exact < 0;
+    out->loEps = Ylo.eps;
     out->evals = evals;
     out->rounds = (unsigned)round;
     // (controller phases: hand-off wait, combine + logic, evaluation)
@@ -1251,6 +1260,148 @@ __global__ void __launch_bounds__(WS_TPB) k_tm_wsum(int N, int P, const double *
     __syncthreads();
   }
   if (!active) return;
+  if (COV) {
+    const double v = scaling * acc / denom;
+    out[pi * N + pj] = v;
+    out[pj * N + pi] = v;
+  } else {
+    out[pi] = acc;
+  }
+}
+
+// The same ordered sums on ROW chains (round 4, the default): one 16-lane
+// row per output element keeps the accumulator and adds its 16 lanes' terms
+// through DPP row_newbcast operands of v_fmac_f64 (chains::kc_row16, one
+// VALU instruction per term, ~8 cycles instead of the ~14 of a dependent
+// v_add_f64 plus the LDS reads).  The factors are stored TRANSPOSED, one
+// Pp-long row per variable (Pp = P rounded up to WR_D * 16, the pad is
+// +0.0: acc starts at +0.0 and can never be -0.0, so adding +0.0 is a
+// no-op), so a row's 16 lanes read 128 contiguous bytes; each lane keeps
+// WR_D loads in flight (registers, no LDS, no barriers).
+constexpr int WR_D = 32;
+inline int wr_pitch(int P) { return (P + 16 * WR_D - 1) / (16 * WR_D) * (16 * WR_D); }
+__global__ void k_tm_factors_mean_t(int N, int P, int Pp, const double *__restrict__ db,
+                                    const double *__restrict__ w, double *__restrict__ TT) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)N * Pp) return;
+  const int i = (int)(e / Pp), k = (int)(e % Pp);
+  TT[e] = k < P ? db[(size_t)k * N + i] * w[k] : 0.0;
+}
+__global__ void k_tm_factors_cov_t(int N, int P, int Pp, const double *__restrict__ db, const double *__restrict__ w,
+                                   const double *__restrict__ mean, double *__restrict__ WDT,
+                                   double *__restrict__ DT) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)N * Pp) return;
+  const int i = (int)(e / Pp), k = (int)(e % Pp);
+  double wd = 0.0, d = 0.0;
+  if (k < P) {
+    d = db[(size_t)k * N + i] - mean[i];
+    wd = w[k] * d;
+  }
+  WDT[e] = wd;
+  DT[e] = d;
+}
+// One slot: wait for its loads (issued WR_D slots ago: every later load is
+// one of this lane's own), form the term, 16 row-chain steps, reload the
+// slot from the next group.  The loads are issued inside the asm so the
+// compiler's conservative waits cannot drain the queue (it otherwise waits
+// for every load at the loop head).
+#define WR_FMAC16 \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"  \
+  "v_fmac_f64 %[acc], %[t], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"  \
+
+template <int S>
+__device__ __forceinline__ void wr_slot_cov(double &acc, double &qa, double &qb, const double *an, const double *bn,
+                                            double one) {
+  double t;
+  asm volatile(
+      "s_waitcnt vmcnt(%[w])\n"
+      "v_mul_f64 %[t], %[qa], %[qb]\n"
+      "s_nop 1\n" WR_FMAC16
+      "global_load_dwordx2 %[qa], %[pa], off offset:%[off]\n"
+      "global_load_dwordx2 %[qb], %[pb], off offset:%[off]\n"
+      : [acc] "+&v"(acc), [qa] "+&v"(qa), [qb] "+&v"(qb), [t] "=&v"(t)
+      : [pa] "v"(an), [pb] "v"(bn), [one] "v"(one), [off] "i"(S * 128), [w] "i"(2 * WR_D - 2));
+}
+template <int S>
+__device__ __forceinline__ void wr_slot_mean(double &acc, double &qa, const double *an, double one) {
+  asm volatile(
+      "s_waitcnt vmcnt(%[w])\n"
+      "s_nop 1\n" WR_FMAC16
+      "global_load_dwordx2 %[t], %[pa], off offset:%[off]\n"
+      : [acc] "+&v"(acc), [t] "+&v"(qa)
+      : [pa] "v"(an), [one] "v"(one), [off] "i"(S * 128), [w] "i"(WR_D - 1));
+}
+template <bool COV, int... S>
+__device__ __forceinline__ void wr_group(double &acc, double (&qa)[WR_D], double (&qb)[WR_D], const double *an,
+                                         const double *bn, double one, std::integer_sequence<int, S...>) {
+  if (COV)
+    (wr_slot_cov<S>(acc, qa[S], qb[S], an, bn, one), ...);
+  else
+    (wr_slot_mean<S>(acc, qa[S], an, one), ...);
+}
+template <int S>
+__device__ __forceinline__ void wr_load_cov(double &qa, double &qb, const double *a, const double *b) {
+  asm volatile(
+      "global_load_dwordx2 %[qa], %[pa], off offset:%[off]\n"
+      "global_load_dwordx2 %[qb], %[pb], off offset:%[off]\n"
+      : [qa] "=&v"(qa), [qb] "=&v"(qb)
+      : [pa] "v"(a), [pb] "v"(b), [off] "i"(S * 128));
+}
+template <int S>
+__device__ __forceinline__ void wr_load_mean(double &qa, const double *a) {
+  asm volatile("global_load_dwordx2 %[qa], %[pa], off offset:%[off]\n" : [qa] "=&v"(qa) : [pa] "v"(a), [off] "i"(S * 128));
+}
+template <bool COV, int... S>
+__device__ __forceinline__ void wr_prologue(double (&qa)[WR_D], double (&qb)[WR_D], const double *a, const double *b,
+                                            std::integer_sequence<int, S...>) {
+  if (COV)
+    (wr_load_cov<S>(qa[S], qb[S], a, b), ...);
+  else
+    (wr_load_mean<S>(qa[S], a), ...);
+}
+template <bool COV>
+__global__ void __launch_bounds__(64) k_tm_wsum_rows(int N, int Pp, const double *__restrict__ A,
+                                                     const double *__restrict__ B, const int2 *__restrict__ pairs,
+                                                     int nout, double scaling, double denom,
+                                                     double *__restrict__ out) {
+  const int lane = threadIdx.x, l = lane & 15;
+  const int o = blockIdx.x * 4 + (lane >> 4);
+  const int oc = o < nout ? o : nout - 1;  // (a row past the end recomputes the last element, unused)
+  int pi = oc, pj = 0;
+  if (COV) {
+    const int2 ij = pairs[oc];
+    pi = ij.x;
+    pj = ij.y;
+  }
+  const double *a = A + (size_t)pi * Pp + l;
+  const double *b = B + (size_t)pj * Pp + l;
+  const int ns = Pp >> 4;  // 16-term slots, a multiple of WR_D
+  const double one = 1.0;
+  double qa[WR_D], qb[WR_D];
+  wr_prologue<COV>(qa, qb, a, b, std::make_integer_sequence<int, WR_D>{});
+  double acc = 0.0;
+  for (int g = 0; g < ns; g += WR_D) {
+    const int nx = g + WR_D < ns ? g + WR_D : g;  // the last group reloads itself (unused)
+    wr_group<COV>(acc, qa, qb, a + (size_t)nx * 16, b + (size_t)nx * 16, one,
+                  std::make_integer_sequence<int, WR_D>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (o >= nout || l != 0) return;
   if (COV) {
     const double v = scaling * acc / denom;
     out[pi * N + pj] = v;
@@ -1528,6 +1679,69 @@ double cv2_tail(const double *E, size_t n, double target, double *w) {
   return c;
 }
 
+// cv2_tail of the search's stored minimum on a host worker thread: once the
+// device's interval has decided that minimum against the 1e-12 tolerance,
+// its exact value only feeds the reported coefficient of variation, so the
+// x87 recurrences (~180 us at P = 8192) overlap the weights and the
+// multinomial instead of preceding them
+class HostTail {
+ public:
+  ~HostTail() {
+    if (!th_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void start(const double *E, size_t n, double target) {
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    std::lock_guard<std::mutex> lk(mu_);
+    E_ = E;
+    n_ = n;
+    target_ = target;
+    w_.resize(n);
+    busy_ = true;
+    cv_.notify_all();
+  }
+  bool busy() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return busy_;
+  }
+  double wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return !busy_; });
+    return y_;
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return quit_ || busy_; });
+      if (quit_) return;
+      const double *E = E_;
+      const size_t n = n_;
+      const double t = target_;
+      lk.unlock();
+      const double y = cv2_tail(E, n, t, w_.data());
+      lk.lock();
+      y_ = y;
+      busy_ = false;
+      cv_.notify_all();
+    }
+  }
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  const double *E_ = nullptr;
+  size_t n_ = 0;
+  double target_ = 0, y_ = 0;
+  bool busy_ = false, quit_ = false;
+  std::vector<double> w_;
+};
+
 }  // namespace
 }  // namespace kg
 
@@ -1555,7 +1769,8 @@ struct kg_tmcmc_s {
          *negLogWidth = nullptr, *Z = nullptr, *U = nullptr, *Uprior = nullptr, *E = nullptr, *w = nullptr;
   unsigned long long *uoff = nullptr;
   int2 *pairs = nullptr;
-  double *fA = nullptr, *fB = nullptr;  // P x N term factors of the ordered sums (+2 padding)    // upper-triangle (i, j), j >= i, row-major
+  bool wsumLds = false;
+  double *fA = nullptr, *fB = nullptr;  // term factors of the ordered sums (P x N + 2, or N x wr_pitch(P))    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
   unsigned *src = nullptr;
   unsigned char *acc = nullptr, *pend = nullptr;
@@ -1567,6 +1782,12 @@ struct kg_tmcmc_s {
   size_t capU = 0, capZx = 0;
   // pinned host staging
   double *hE = nullptr, *hW = nullptr, *hNsel = nullptr;
+  // the deferred exact minimum (HostTail): hEtail holds its exponentials
+  // (swapped with hE), tailPending until kg_tmcmc_process_finalize collects it
+  double *hEtail = nullptr;
+  HostTail tail;
+  bool tailPending = false, deferTail = true;  // KORALI_AMD_TM_DEFER_TAIL=0: form it before going on
+  double tailDeferred = 0;
   void *hCv = nullptr;                       // CvOut[CV_MAX_PTS + 1] (host)
   double2 *hRec = nullptr, *dRec = nullptr;  // 4 x CV_MAX_PTS+1 records, host-coherent (+ device alias)
   unsigned long long cvSeq = 0;
@@ -1974,6 +2195,10 @@ int cv2_exact(kg_tmcmc_s *h, double exponent, double x, double &y);
 int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmin, double &fmin, size_t &iters) {
   const double Tol = 1e-12;
   const int P = h->P;
+  if (h->tailPending) {  // (a previous finalize that failed before collecting it)
+    (void)h->tail.wait();
+    h->tailPending = false;
+  }
   NmTab tab{};
   for (;;) {
     KG_HIP(hipMemsetAsync(h->nmSync, 0, sizeof(NmSync), h->stream));
@@ -2011,13 +2236,33 @@ int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmi
     for (int q = 0; q < 3; q++) h->nmTime[q] += o.tc[q] * 1e-5, h->nmTime[3 + q] += o.tw[q] * 1e-5;  // ms
     if (o.status == 0) {
       double ylo = o.y[o.lo];
+      bool deferred = false;
       if (!o.loExact) {
-        ylo = cv2_tail(h->hE, P, objCov, h->wtmp.data());
-        h->exactEvals++;
+        // the interval decides ylo <= Tol unless it straddles Tol: above, the
+        // minimum is rejected (fmin = 0, xmin = 0) and its exact value is never
+        // used; below, xmin is known and the exact value (only fmin, for the
+        // coefficient of variation) is formed on the host worker meanwhile
+        const bool ok = !o.loBad && std::isfinite(o.loEps);
+        if (ok && ylo - o.loEps > Tol) {
+          ylo = INFINITY;
+        } else if (ok && ylo + o.loEps <= Tol && o.X[o.lo] < 1.0 && h->deferTail) {
+          std::swap(h->hE, h->hEtail);
+          h->tail.start(h->hEtail, P, objCov);
+          h->tailPending = true;
+          h->exactEvals++;
+          h->tailDeferred++;
+          deferred = true;
+        } else {
+          ylo = cv2_tail(h->hE, P, objCov, h->wtmp.data());
+          h->exactEvals++;
+        }
       }
       fmin = 0;
       xmin = 0.0;
-      if (ylo <= Tol) {
+      if (deferred) {
+        fmin = NAN;  // (collected by kg_tmcmc_process_finalize)
+        xmin = o.X[o.lo];
+      } else if (ylo <= Tol) {
         fmin = ylo;
         xmin = o.X[o.lo];
       }
@@ -2229,6 +2474,7 @@ bool tm_field(kg_tmcmc_s *h, const std::string &k, TmField &r) {
   SCA("Min Search Iterations", minSearchIterations)
   SCA("Current Burn In", currentBurnIn)
   SCA("Exact Search Evaluations", exactEvalsD)
+  SCA("Deferred Search Evaluations", tailDeferred)
   SCA("Device Search Relaunches", nmRelaunchesD)
   SCA("Device Search Evaluations", nmEvalsD)
   SCA("Device Search Rounds", nmRoundsD)
@@ -2346,7 +2592,10 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   h->xchWords = 3 * (PN + 2 * (size_t)P) + h->world;
   if (cfg->shard_count >= 1) rc |= tdalloc(&h->xch, h->xchWords);  // explicitly sharded (even one rank)
   rc |= tdalloc(&h->dev, 1) | tdalloc(&h->pairs, N * (N + 1) / 2);
-  rc |= tdalloc(&h->fA, PN + 2) | tdalloc(&h->fB, PN + 2);
+  {  // (LDS form: P x N + 2; row form: N x wr_pitch(P))
+    const size_t nf = std::max(PN + 2, (size_t)N * wr_pitch(P));
+    rc |= tdalloc(&h->fA, nf) | tdalloc(&h->fB, nf);
+  }
   rc |= tdalloc((char **)&h->cvPart, (CV_MAX_PTS + 1) * CV_BLOCKS * sizeof(CvPart));
   rc |= tdalloc((char **)&h->dNm, sizeof(NmOut)) | tdalloc((char **)&h->nmSync, sizeof(NmSync));
   if (rc) {
@@ -2354,6 +2603,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     return 1;
   }
   KG_HIP(hipHostMalloc(&h->hE, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(hipHostMalloc(&h->hEtail, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hNm, sizeof(NmOut), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
   KG_HIP(hipHostMalloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
@@ -2371,6 +2621,10 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     h->exactSearch = ev && ev[0] == '1';
     const char *hs = getenv("KORALI_AMD_TMCMC_HOST_SEARCH");
     h->hostSearch = hs && hs[0] == '1';
+    const char *ws = getenv("KORALI_AMD_TM_WSUM");  // "lds": the round-2 LDS-tile sums
+    h->wsumLds = ws && strcmp(ws, "lds") == 0;
+    const char *dt = getenv("KORALI_AMD_TM_DEFER_TAIL");
+    h->deferTail = !(dt && dt[0] == '0');
   }
   h->wtmp.resize(P);
   h->nsel.resize(P);
@@ -2454,6 +2708,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
 int kg_tmcmc_destroy(kg_tmcmc_t h) {
   if (!h) return 0;
   (void)hipStreamSynchronize(h->stream);
+  if (h->tailPending) (void)h->tail.wait();
 
   for (void *p : {(void *)h->leaders, (void *)h->leadLL, (void *)h->leadLP, (void *)h->cand, (void *)h->candLL,
                   (void *)h->candLP, (void *)h->chainLen, (void *)h->mean, (void *)h->cov, (void *)h->chol,
@@ -2465,7 +2720,7 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync, (void *)h->mtExtraDev,
                   (void *)h->mtModeDev})
     if (p) (void)hipFree(p);
-  for (void *p : {(void *)h->hE, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
+  for (void *p : {(void *)h->hE, (void *)h->hEtail, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
                   (void *)h->hSch, (void *)h->hLenD, (void *)h->hNm})
     if (p) (void)hipHostFree(p);
   for (auto *r : h->priorRng) delete r;
@@ -2882,6 +3137,7 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
   h->nmRoundsD = (double)h->nmRounds;
   h->nmFallbacksD = (double)h->nmFallbacks;
   h->previousAnnealingExponent = h->annealingExponent;
+  bool cvFromTail = false;
   {
     const double pe = h->previousAnnealingExponent;
     double y = 0;
@@ -2895,7 +3151,9 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
       h->coefficientOfVariation = sqrt(y) + h->cfg.target_cov;
     } else {
       h->annealingExponent = xmin;
-      h->coefficientOfVariation = sqrt(fmin) + h->cfg.target_cov;
+      // (a deferred fmin: collected at the end of this function)
+      if (!h->tailPending) h->coefficientOfVariation = sqrt(fmin) + h->cfg.target_cov;
+      cvFromTail = h->tailPending;
     }
   }
   const double drho = h->annealingExponent - h->previousAnnealingExponent;
@@ -2971,13 +3229,27 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
   {
     TmStage st(h, "mean_cov");
     const int npairs = N * (N + 1) / 2;
-    hipLaunchKernelGGL(k_tm_factors_mean, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->fA);
-    hipLaunchKernelGGL(k_tm_wsum<false>, dim3(nblk(N, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, false), h->stream, N, P,
-                       h->fA, h->fA, h->pairs, N, 0.0, 1.0, h->mean);
-    hipLaunchKernelGGL(k_tm_factors_cov, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->mean,
-                       h->fA, h->fB);
-    hipLaunchKernelGGL(k_tm_wsum<true>, dim3(nblk(npairs, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, true), h->stream,
-                       N, P, h->fA, h->fB, h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
+    if (h->wsumLds) {
+      hipLaunchKernelGGL(k_tm_factors_mean, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->fA);
+      hipLaunchKernelGGL(k_tm_wsum<false>, dim3(nblk(N, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, false), h->stream,
+                         N, P, h->fA, h->fA, h->pairs, N, 0.0, 1.0, h->mean);
+      hipLaunchKernelGGL(k_tm_factors_cov, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->db, h->w, h->mean,
+                         h->fA, h->fB);
+      hipLaunchKernelGGL(k_tm_wsum<true>, dim3(nblk(npairs, WS_LANES)), dim3(WS_TPB), ws_lds_bytes(N, true),
+                         h->stream, N, P, h->fA, h->fB, h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2,
+                         h->cov);
+    } else {
+      const int Pp = wr_pitch(P);
+      const size_t NP = (size_t)N * Pp;
+      hipLaunchKernelGGL(k_tm_factors_mean_t, dim3(nblk(NP, 256)), dim3(256), 0, h->stream, N, P, Pp, h->db, h->w,
+                         h->fA);
+      hipLaunchKernelGGL(k_tm_wsum_rows<false>, dim3((N + 3) / 4), dim3(64), 0, h->stream, N, Pp, h->fA, h->fA,
+                         h->pairs, N, 0.0, 1.0, h->mean);
+      hipLaunchKernelGGL(k_tm_factors_cov_t, dim3(nblk(NP, 256)), dim3(256), 0, h->stream, N, P, Pp, h->db, h->w,
+                         h->mean, h->fA, h->fB);
+      hipLaunchKernelGGL(k_tm_wsum_rows<true>, dim3((npairs + 3) / 4), dim3(64), 0, h->stream, N, Pp, h->fA, h->fB,
+                         h->pairs, npairs, h->cfg.covariance_scaling, 1.0 - sumw2, h->cov);
+    }
     KG_HIP(hipGetLastError());
   }
   {
@@ -2989,6 +3261,11 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
   h->proposalsAcceptanceRate = (1.0 * h->acceptedSamplesCount) / P;
   h->selectionAcceptanceRate = (1.0 * (P - zeroCount)) / P;
   h->chainCount = (double)leaderId;
+  if (h->tailPending) {
+    const double y = h->tail.wait();
+    h->tailPending = false;
+    if (cvFromTail) h->coefficientOfVariation = sqrt(y) + h->cfg.target_cov;
+  }
   // the pinned staging buffers are reused by the next generation's search,
   // which synchronises the stream before touching them
   return 0;

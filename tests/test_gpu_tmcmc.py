@@ -163,6 +163,33 @@ def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov
     assert runs[0][1] < runs[1][1] and runs[2][1] < runs[1][1]
 
 
+@pytest.mark.parametrize("N,P", [(6, 1000), (32, 1024), (3, 37)])
+def test_row_chain_sums_and_deferred_tail_match_oracle(monkeypatch, N, P):
+    """The weighted mean / covariance on row chains (k_tm_wsum_rows, P padded
+    to the slot pitch) and the stored minimum's exact value formed on the
+    host worker (HostTail) against the round-2 LDS-tile sums with the value
+    formed before going on (KORALI_AMD_TM_WSUM=lds, KORALI_AMD_TM_DEFER_TAIL=0)
+    and the oracle: the same bits every generation."""
+    runs = []
+    for wsum, defer in (("rows", "1"), ("lds", "0")):
+        monkeypatch.setenv("KORALI_AMD_TM_WSUM", wsum)
+        monkeypatch.setenv("KORALI_AMD_TM_DEFER_TAIL", defer)
+        dev, o, ndist = seeded_pair(N, P, shared=True, seed=5)
+        hist = []
+        for g in range(1, 40):
+            dev.generation(g)
+            hist.append((dev["Annealing Exponent"][0], dev["Coefficient Of Variation"][0], dev["LogEvidence"][0],
+                         dev["Mean Theta"].tobytes(), dev["Covariance Matrix"].tobytes()))
+            if wsum == "rows":
+                o.generation(g)
+                compare_state(dev, o, g)
+            if dev["Annealing Exponent"][0] >= 1.0:
+                break
+        runs.append((hist, dev["Deferred Search Evaluations"][0]))
+    assert runs[0][0] == runs[1][0]
+    assert runs[1][1] == 0
+
+
 def compare_state(dev, o, g):
     for key in VEC_KEYS:
         assert np.array_equal(dev[key], o[key]), (g, key)
