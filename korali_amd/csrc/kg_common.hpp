@@ -23,6 +23,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <tuple>
 
 namespace kg {
 
@@ -133,12 +134,40 @@ inline hipError_t launch_resident(const void *f, dim3 grid, dim3 block, void **a
   }();
   const bool plain = plain_env || (prefer_plain && !coop_env);
   if (!plain) return hipLaunchCooperativeKernel(f, grid, block, args, (unsigned int)lds, s);
-  int dev = 0, cus = 0, per = 0;
+  // the capacity of (device, kernel, block, LDS), queried once per process:
+  // these grids launch every generation, and the occupancy query costs
+  // tens of microseconds
+  struct Key {
+    int dev;
+    const void *f;
+    unsigned threads;
+    size_t lds;
+    bool operator<(const Key &o) const {
+      return std::tie(dev, f, threads, lds) < std::tie(o.dev, o.f, o.threads, o.lds);
+    }
+  };
+  static std::mutex mu;
+  static std::map<Key, long long> capacity;
+  int dev = 0;
   hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = resident_per_cu(f, (int)(block.x * block.y * block.z), lds, &per, nullptr);
   if (e != hipSuccess) return e;
-  if ((long long)per * cus < (long long)grid.x * grid.y * grid.z) return hipErrorCooperativeLaunchTooLarge;
+  const Key k{dev, f, block.x * block.y * block.z, lds};
+  long long cap = -1;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = capacity.find(k);
+    if (it != capacity.end()) cap = it->second;
+  }
+  if (cap < 0) {
+    int cus = 0, per = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = resident_per_cu(f, (int)k.threads, lds, &per, nullptr);
+    if (e != hipSuccess) return e;
+    cap = (long long)per * cus;
+    std::lock_guard<std::mutex> lk(mu);
+    capacity[k] = cap;
+  }
+  if (cap < (long long)grid.x * grid.y * grid.z) return hipErrorCooperativeLaunchTooLarge;
   return hipLaunchKernel(f, grid, block, args, lds, s);
 }
 

@@ -571,6 +571,16 @@ int MtStream::prefetch(size_t M, hipStream_t main) {
   return 0;
 }
 
+int MtStream::polar_normals_ahead(double *z, size_t M, size_t block_len, hipStream_t main) {
+  if (!side_) return 1;
+  KG_HIP(hipEventRecord(ev_main_, main));
+  KG_HIP(hipStreamWaitEvent(side_, ev_main_, 0));
+  if (polar_normals(z, M, block_len, nullptr, side_)) return 1;
+  KG_HIP(hipEventRecord(ev_side_, side_));
+  prefetch_pending_ = true;
+  return 0;
+}
+
 int MtStream::join(hipStream_t main) {
   if (!side_) return 0;
   KG_HIP(hipEventRecord(ev_side_, side_));

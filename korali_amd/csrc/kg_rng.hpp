@@ -96,6 +96,11 @@ class MtStream {
   // runs concurrently with whatever the main stream does next (the
   // eigendecomposition); polar_normals() then waits for it.
   int prefetch(size_t M_normals, hipStream_t main);
+  // polar_normals() on the side stream, after everything queued on `main`
+  // so far (the stream is not advanced: a later consume_normals() on `main`,
+  // after join(main), takes them).  Returns 1 when no side stream exists yet
+  // (nothing launched, nothing else to do).
+  int polar_normals_ahead(double *z, size_t M, size_t block_len, hipStream_t main);
 
   // the producer's side stream (created by the first prefetch), and a join
   // that makes `main` wait for everything queued on it so far

@@ -974,6 +974,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
   __shared__ NmVal val[NM_PTS];
   __shared__ double spts[NM_PTS];
   __shared__ int sfail, sbn;
+  const unsigned long long tk0 = __builtin_amdgcn_s_memrealtime();
   const int w = blockIdx.x, chunk = (P + NM_W - 1) / NM_W;
   const int i0 = w * chunk < P ? w * chunk : P, i1 = (w + 1) * chunk < P ? (w + 1) * chunk : P;
   const bool inLds = chunk <= NM_LDS;
@@ -981,11 +982,12 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     for (int i = i0 + tid; i < i1; i += NM_TPB) sll[i - i0] = ll[i];
   unsigned long long round = 0;
   unsigned evals = 0;
-  unsigned long long tEval = 0, tWait = 0, tRest = 0, tlast = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tEval = 0, tWait = 0, tRest = 0, tlast = __builtin_amdgcn_s_memrealtime(), tFirst = 0;
   const dd invP = dd_div(dd{1.0, 0.0}, dd{(double)P, 0.0});
   auto run_round = [&](const double *pts, int n) __attribute__((always_inline)) {
     const unsigned long long ra = __builtin_amdgcn_s_memrealtime();
     tRest += ra - tlast;
+    if (round == 0) tFirst = ra;
     round++;
     evals += n;
     __syncthreads();  // every thread has read the previous round's spts / val (and sll is loaded)
@@ -1103,7 +1105,10 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     out->tc[0] = tWait;
     out->tc[1] = tRest + (__builtin_amdgcn_s_memrealtime() - tlast);
     out->tc[2] = tEval;
-    out->tw[0] = out->tw[1] = out->tw[2] = 0;
+    // (workgroup 0: whole kernel, its prologue before the first round)
+    out->tw[0] = __builtin_amdgcn_s_memrealtime() - tk0;
+    out->tw[1] = tFirst - tk0;
+    out->tw[2] = 0;
   }
 }
 
@@ -1786,7 +1791,10 @@ struct kg_tmcmc_s {
   // (swapped with hE), tailPending until kg_tmcmc_process_finalize collects it
   double *hEtail = nullptr;
   HostTail tail;
-  bool tailPending = false, deferTail = true;  // KORALI_AMD_TM_DEFER_TAIL=0: form it before going on
+  bool tailPending = false, deferTail = true;
+  // the next generation's first-step normals (P x N, one rank) formed on the
+  // multivariate side stream during the host multinomial; prepare consumes
+  bool zAhead = false, zAheadOn = true;  // KORALI_AMD_TM_NORMALS_AHEAD=0: off  // KORALI_AMD_TM_DEFER_TAIL=0: form it before going on
   double tailDeferred = 0;
   void *hCv = nullptr;                       // CvOut[CV_MAX_PTS + 1] (host)
   double2 *hRec = nullptr, *dRec = nullptr;  // 4 x CV_MAX_PTS+1 records, host-coherent (+ device alias)
@@ -2625,6 +2633,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     h->wsumLds = ws && strcmp(ws, "lds") == 0;
     const char *dt = getenv("KORALI_AMD_TM_DEFER_TAIL");
     h->deferTail = !(dt && dt[0] == '0');
+    const char *za = getenv("KORALI_AMD_TM_NORMALS_AHEAD");
+    h->zAheadOn = !(za && za[0] == '0');
   }
   h->wtmp.resize(P);
   h->nsel.resize(P);
@@ -2795,6 +2805,10 @@ static int tm_mt_candidates(kg_tmcmc_s *h) {
 int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   const int N = h->N, P = h->P;
   const size_t PN = (size_t)P * N;
+  if (generation == 1 && h->zAhead) {  // (a new run: the normals formed ahead are not its own)
+    if (h->multivariate.join(h->stream)) return 1;
+    h->zAhead = false;
+  }
   if (generation == 1 && tm_initialize(h)) return 1;
   if (tm_sync_dev(h)) return 1;
   // prepareGeneration :161-170
@@ -2838,7 +2852,12 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   } else {
     {
       TmStage st(h, "rng_polar");
-      if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream, h->ca * N, h->cbp * N)) return 1;
+      if (h->zAhead && h->world == 1) {  // formed during the last generation's multinomial
+        if (h->multivariate.join(h->stream)) return 1;
+      } else if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream, h->ca * N, h->cbp * N)) {
+        return 1;
+      }
+      h->zAhead = false;
       if (h->multivariate.consume_normals(PN, N, nullptr, h->stream)) return 1;
       // the next generation's words are produced on the side stream while
       // this generation's search runs on the host
@@ -3163,6 +3182,14 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
                        (double *)nullptr);
     hipLaunchKernelGGL(k_tm_lw_exp, dim3(nblk(P, 256)), dim3(256), 0, h->stream, P, h->dbLL, drho, h->dev, h->E);
     KG_HIP(hipGetLastError());
+    // the next generation's first-step normals do not depend on the
+    // selections (every one of the P chains draws N at its first step, one
+    // rank): form them on the side stream while the host runs the
+    // multinomial (the stream position only advances in prepare, so an
+    // experiment that ends here is unaffected)
+    h->zAhead = false;
+    if (!h->mt && h->world == 1 && h->zAheadOn)
+      h->zAhead = h->multivariate.polar_normals_ahead(h->Z, PN, N, h->stream) == 0;
     KG_HIP(hipMemcpyAsync(h->hE, h->E, (size_t)P * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     KG_HIP(hipMemcpyAsync(h->hDev, h->dev, sizeof(TmDev), hipMemcpyDeviceToHost, h->stream));
     KG_HIP(hipStreamSynchronize(h->stream));
@@ -3348,6 +3375,10 @@ int kg_tmcmc_set_rng(kg_tmcmc_t h, int which, const void *state5000) {
   if (tm_sync_dev(h)) return 1;
   if (which == 0) return h->multinomialRng.load((const unsigned char *)state5000);
   MtStream &m = which == 1 ? h->multivariate : which == 2 ? h->uniform : *h->priorRng[which - 3];
+  if (which == 1 && h->zAhead) {  // the normals formed ahead are from the replaced state
+    if (m.join(h->stream)) return 1;
+    h->zAhead = false;
+  }
   return m.import_gsl(state5000, h->stream);
 }
 

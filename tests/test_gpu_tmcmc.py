@@ -169,11 +169,14 @@ def test_row_chain_sums_and_deferred_tail_match_oracle(monkeypatch, N, P):
     to the slot pitch) and the stored minimum's exact value formed on the
     host worker (HostTail) against the round-2 LDS-tile sums with the value
     formed before going on (KORALI_AMD_TM_WSUM=lds, KORALI_AMD_TM_DEFER_TAIL=0)
-    and the oracle: the same bits every generation."""
-    runs = []
+    and the oracle: the same bits every generation; the next generation's
+    first-step normals formed ahead on the side stream leave the Multivariate
+    generator where the plain order leaves it."""
+    runs, states = [], []
     for wsum, defer in (("rows", "1"), ("lds", "0")):
         monkeypatch.setenv("KORALI_AMD_TM_WSUM", wsum)
         monkeypatch.setenv("KORALI_AMD_TM_DEFER_TAIL", defer)
+        monkeypatch.setenv("KORALI_AMD_TM_NORMALS_AHEAD", defer)  # (first-step normals formed ahead, or not)
         dev, o, ndist = seeded_pair(N, P, shared=True, seed=5)
         hist = []
         for g in range(1, 40):
@@ -186,8 +189,10 @@ def test_row_chain_sums_and_deferred_tail_match_oracle(monkeypatch, N, P):
             if dev["Annealing Exponent"][0] >= 1.0:
                 break
         runs.append((hist, dev["Deferred Search Evaluations"][0]))
+        states.append(bytes(dev.get_rng(1)))  # the Multivariate generator after the run
     assert runs[0][0] == runs[1][0]
     assert runs[1][1] == 0
+    assert states[0] == states[1]
 
 
 def compare_state(dev, o, g):

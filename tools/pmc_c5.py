@@ -1,6 +1,6 @@
 """Summarise the C5 FETCH_SIZE / WRITE_SIZE passes for the rollout-forward
-launches of k_vr_gemm<1> (4096 rows: Grid_Size 262144 work-items), the
-bench's `roofline` kernel; FETCH_SIZE x2 per the gfx950 correction
+launches of k_vr_gemm<1> (4096 rows: the largest Grid_Size among its
+dispatches; the update's launches are smaller), the bench's `roofline` kernel; FETCH_SIZE x2 per the gfx950 correction
 (MI355X_MICROARCH.md, HBM/rocprofv3 section).
 
     python tools/pmc_c5.py <pmc_fetch dir> <pmc_write dir> > profiles/r2/c5_pmc_traffic.csv
@@ -13,11 +13,9 @@ import sys
 
 def load(d, counter):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    out = []
-    for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] == counter and "k_vr_gemm<1>" in r["Kernel_Name"] and int(r["Grid_Size"]) == 262144:
-            out.append(float(r["Counter_Value"]))
-    return out
+    rows = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter and "k_vr_gemm<1>" in r["Kernel_Name"]]
+    grid = max(int(r["Grid_Size"]) for r in rows)
+    return [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == grid]
 
 
 def main():
