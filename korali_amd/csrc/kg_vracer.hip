@@ -196,14 +196,12 @@ __global__ __launch_bounds__(256) void k_vr_fwd_out(int M, int H, int O, const f
 enum : int { EP_STORE = 0, EP_BIAS_TANH = 1, EP_DTANH = 2 };
 constexpr int GT = 32, GK = 256, GP = GT + 1;
 template <int EP>
-__global__ __launch_bounds__(256) void k_vr_gemm(int M, int N, int K, const float *__restrict__ A, long long sam,
-                                                 long long sak, const float *__restrict__ B, long long sbn,
-                                                 long long sbk, float *__restrict__ C, long long ldc,
-                                                 const float *__restrict__ bias, const float *__restrict__ T,
-                                                 long long ldt, int vec) {
-  __shared__ float As[GK][GP];
-  __shared__ float Bs[GK][GP];
-  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+__device__ __forceinline__ void vr_gemm_tile(int M, int N, int K, const float *__restrict__ A, long long sam,
+                                             long long sak, const float *__restrict__ B, long long sbn, long long sbk,
+                                             float *__restrict__ C, long long ldc, const float *__restrict__ bias,
+                                             const float *__restrict__ T, long long ldt, int vec, int bx, int by,
+                                             float (&As)[GK][GP], float (&Bs)[GK][GP]) {
+  const int m0 = by * GT, n0 = bx * GT;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, br = wave >> 1, bc = wave & 1, li = lane & 15,
             lk = lane >> 4;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
@@ -285,6 +283,16 @@ __global__ __launch_bounds__(256) void k_vr_gemm(int M, int N, int K, const floa
     C[row * ldc + col] = v;
   }
 }
+template <int EP>
+__global__ __launch_bounds__(256) void k_vr_gemm(int M, int N, int K, const float *__restrict__ A, long long sam,
+                                                 long long sak, const float *__restrict__ B, long long sbn,
+                                                 long long sbk, float *__restrict__ C, long long ldc,
+                                                 const float *__restrict__ bias, const float *__restrict__ T,
+                                                 long long ldt, int vec) {
+  __shared__ float As[GK][GP];
+  __shared__ float Bs[GK][GP];
+  vr_gemm_tile<EP>(M, N, K, A, sam, sak, B, sbn, sbk, C, ldc, bias, T, ldt, vec, blockIdx.x, blockIdx.y, As, Bs);
+}
 
 // Output-layer backward (output.cpp.base:170-210) and the last Linear's data
 // gradient: dZ = transformed G; dH[b][i] = (sum_o dZ[b][o] W[o][i]) (1 - h^2).
@@ -325,12 +333,11 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
 // (linear.cpp.base:337-350: summed over the batch).  One workgroup per
 // (o, column chunk): CW columns x (256 / CW) batch lanes, partial sums
 // reduced through LDS in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
-                                                        const float *__restrict__ Act, int lda,
-                                                        float *__restrict__ dW, float *__restrict__ db, int CW) {
-  __shared__ float part[256];
-  const int o = blockIdx.x, t = threadIdx.x, lanes = 256 / CW, c = t % CW, l = t / CW;
-  const int i = blockIdx.y * CW + c;
+__device__ __forceinline__ void vr_wgrad_block(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
+                                               const float *__restrict__ Act, int lda, float *__restrict__ dW,
+                                               float *__restrict__ db, int CW, int bx, int by, float *part) {
+  const int o = bx, t = threadIdx.x, lanes = 256 / CW, c = t % CW, l = t / CW;
+  const int i = by * CW + c;
   float acc = 0.f;
   if (i <= Ni)
 #pragma unroll 4
@@ -347,6 +354,64 @@ __global__ __launch_bounds__(256) void k_vr_wgrad_small(int No, int Ni, int Bn, 
   if (l == 0 && i <= Ni) {
     if (i < Ni) dW[o * Ni + i] = part[c];
     else db[o] = part[c];
+  }
+}
+__global__ __launch_bounds__(256) void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
+                                                        const float *__restrict__ Act, int lda,
+                                                        float *__restrict__ dW, float *__restrict__ db, int CW) {
+  __shared__ float part[256];
+  vr_wgrad_block(No, Ni, Bn, G, ldg, Act, lda, dW, db, CW, blockIdx.x, blockIdx.y, part);
+}
+
+// Independent weight-gradient products of one backward step in ONE launch
+// (round 4): the output layer's wgrad, dW_l, db_l and dH_(l-1) only read
+// dZ / dH_l and the activations, so their blocks run side by side instead
+// of as four dependent launches.  Each job's blocks run the same bodies as
+// the separate kernels (identical results); blockIdx selects the job.
+struct VrGemmJob {
+  const float *A, *B, *bias, *T;
+  float *C;
+  long long sam, sak, sbn, sbk, ldc, ldt;
+  int M, N, K, vec, ep, gx, n;
+};
+struct VrWgradJob {
+  const float *G, *Act;
+  float *dW, *db;
+  int No, Ni, Bn, ldg, lda, cw, n;
+};
+struct VrMulti {
+  VrWgradJob w[2];
+  VrGemmJob g[2];
+  int nw, ng;
+};
+__global__ __launch_bounds__(256) void k_vr_multi(VrMulti J) {
+  __shared__ float As[GK][GP];
+  __shared__ float Bs[GK][GP];
+  int b = blockIdx.x;
+  for (int q = 0; q < J.nw; q++) {
+    const VrWgradJob &w = J.w[q];
+    if (b < w.n) {
+      vr_wgrad_block(w.No, w.Ni, w.Bn, w.G, w.ldg, w.Act, w.lda, w.dW, w.db, w.cw, b % w.No, b / w.No, &As[0][0]);
+      return;
+    }
+    b -= w.n;
+  }
+  for (int q = 0; q < J.ng; q++) {
+    const VrGemmJob &g = J.g[q];
+    if (b < g.n) {
+      const int bx = b % g.gx, by = b / g.gx;
+      if (g.ep == EP_STORE)
+        vr_gemm_tile<EP_STORE>(g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbn, g.sbk, g.C, g.ldc, g.bias, g.T, g.ldt,
+                               g.vec, bx, by, As, Bs);
+      else if (g.ep == EP_DTANH)
+        vr_gemm_tile<EP_DTANH>(g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbn, g.sbk, g.C, g.ldc, g.bias, g.T, g.ldt,
+                               g.vec, bx, by, As, Bs);
+      else
+        vr_gemm_tile<EP_BIAS_TANH>(g.M, g.N, g.K, g.A, g.sam, g.sak, g.B, g.sbn, g.sbk, g.C, g.ldc, g.bias, g.T,
+                                   g.ldt, g.vec, bx, by, As, Bs);
+      return;
+    }
+    b -= g.n;
   }
 }
 
@@ -399,17 +464,40 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
     key[i] = id;
   }
   __syncthreads();
-  for (int k = 2; k <= n2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < n2; i += nt) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned a = key[i], c = key[l];
-          if ((a > c) == ((i & k) == 0)) key[i] = c, key[l] = a;
+  if (n2 <= nt) {
+    // one key per thread: the same compare-exchange network, the stages
+    // with partners inside the wave (j < 64) through lane shuffles, the
+    // others through LDS (3 barrier pairs at B = 256 instead of 36 barriers)
+    unsigned x = t < n2 ? key[t] : 0xffffffffu;
+    for (int k = 2; k <= n2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        unsigned y;
+        if (j >= 64) {
+          if (t < n2) key[t] = x;
+          __syncthreads();
+          y = t < n2 ? key[t ^ j] : 0xffffffffu;
+          __syncthreads();
+        } else {
+          y = (unsigned)__shfl_xor((int)x, j, 64);
         }
+        // the pair's lower element keeps the minimum in an ascending block
+        x = (((t & j) == 0) == ((t & k) == 0)) ? min(x, y) : max(x, y);
       }
-      __syncthreads();
-    }
+    if (t < n2) key[t] = x;
+    __syncthreads();
+  } else {
+    for (int k = 2; k <= n2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = t; i < n2; i += nt) {
+          const int l = i ^ j;
+          if (l > i) {
+            const unsigned a = key[i], c = key[l];
+            if ((a > c) == ((i & k) == 0)) key[i] = c, key[l] = a;
+          }
+        }
+        __syncthreads();
+      }
+  }
   const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
   for (int i = t; i < B * P.S; i += nt) {
     const int b = i / P.S, k = i % P.S;
@@ -509,20 +597,27 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     int k = b;          // mini-batch rows of this episode, walked downwards
     // per chunk: inputs loaded and mini-batch overrides applied first (no
     // dependence on the recurrence), then the recurrence alone (4 dependent
-    // float operations per entry), then the mini-batch rows' values to LDS
-    // (16-entry chunks; 64-entry chunks, fewer global round trips per
-    // episode, measured slower: 0.112 vs 0.104 ms per update at C5)
+    // float operations per entry), then the mini-batch rows' values to LDS.
+    // The next chunk's loads are issued before the current chunk's
+    // recurrence (two register sets: 48 loads in flight behind the awaited
+    // ones, inside the 63 of vmcnt), so the latency of the replay memory's
+    // loads overlaps the previous chunk's recurrence (without the prefetch:
+    // 27 us per update at C5)
     constexpr int RC = 16;
-    long long pc = ph(end);
-    for (long long c = end; c >= start;) {
-      const int n = (int)min((long long)RC, c - start + 1);
-      float vv[RC], tw[RC], rw[RC], rr[RC];
-      long long q = pc;
+    // (unconditional: entries past the chunk or the episode are valid slots
+    // of the ring whose values go unused; no branch splits the loads from
+    // the waits, so those stay counted)
+    auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC]) __attribute__((always_inline)) {
+      long long q = p0;
 #pragma unroll
       for (int j = 0; j < RC; j++) {
-        if (j < n) vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
+        vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
         q = q == 0 ? (long long)R - 1 : q - 1;
       }
+    };
+    auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], const float (&rw)[RC])
+                       __attribute__((always_inline)) {
+      const int n = (int)min((long long)RC, c - start + 1);
       int kk = k;
       unsigned long long inmb = 0;
 #pragma unroll
@@ -532,10 +627,11 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
           inmb |= 1ull << j;
           while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
         }
+      float rr[RC];
 #pragma unroll
       for (int j = 0; j < RC; j++)
         if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
-      q = pc;
+      long long q = p0;
 #pragma unroll
       for (int j = 0; j < RC; j++) {
         if (j < n) er.ret[q] = rr[j];
@@ -549,8 +645,27 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
             while (k >= 0 && (long long)s_mb[k] == c - j) s_ret[k] = rr[j], s_retn[k] = before, k--;
           }
       prev = retV;  // the chunk's last entry
-      pc = q;
-      c -= n;
+    };
+    // the chunk after the one at (c, pc): its first entry and physical slot
+    auto next = [&](long long c, long long pc, long long &c1, long long &pc1) __attribute__((always_inline)) {
+      const long long n = min((long long)RC, c - start + 1);
+      c1 = c - n;
+      pc1 = pc >= n ? pc - n : pc - n + (long long)R;
+    };
+    float av[RC], at[RC], ar[RC], bv[RC], bt[RC], br[RC];
+    long long c = end, pc = ph(end);
+    load(pc, av, at, ar);
+    while (c >= start) {
+      long long c1, pc1;
+      next(c, pc, c1, pc1);
+      load(pc1, bv, bt, br);
+      process(c, pc, av, at, ar);
+      c = c1, pc = pc1;
+      if (c < start) break;
+      next(c, pc, c1, pc1);
+      load(pc1, av, at, ar);
+      process(c, pc, bv, bt, br);
+      c = c1, pc = pc1;
     }
   }
   __syncthreads();
@@ -1234,14 +1349,28 @@ int vr_collect(kg_vracer_t h) {
   return 0;
 }
 
+bool vr_gemm_vec(int K, const float *A, long long sam, long long sak, const float *Bm, long long sbn, long long sbk) {
+  auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+  return al(A) && al(Bm) && K % 4 == 0 && (sak == 1 ? sam % 4 == 0 : (sam == 1 && sak % 4 == 0)) &&
+         (sbk == 1 ? sbn % 4 == 0 : (sbn == 1 && sbk % 4 == 0));
+}
 template <int EP>
 void vr_gemm(kg_vracer_t h, int M, int N, int K, const float *A, long long sam, long long sak, const float *Bm,
              long long sbn, long long sbk, float *C, long long ldc, const float *bias, const float *T, long long ldt) {
-  auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
-  const bool vec = al(A) && al(Bm) && K % 4 == 0 && (sak == 1 ? sam % 4 == 0 : (sam == 1 && sak % 4 == 0)) &&
-                   (sbk == 1 ? sbn % 4 == 0 : (sbn == 1 && sbk % 4 == 0));
+  const bool vec = vr_gemm_vec(K, A, sam, sak, Bm, sbn, sbk);
   hipLaunchKernelGGL(k_vr_gemm<EP>, dim3(vr_blocks(N, GT), vr_blocks(M, GT)), dim3(256), 0, h->stream, M, N, K, A, sam,
                      sak, Bm, sbn, sbk, C, ldc, bias, T, ldt, vec ? 1 : 0);
+}
+VrGemmJob vr_gemm_job(int ep, int M, int N, int K, const float *A, long long sam, long long sak, const float *Bm,
+                      long long sbn, long long sbk, float *C, long long ldc, const float *bias, const float *T,
+                      long long ldt) {
+  VrGemmJob g{};
+  g.A = A, g.B = Bm, g.bias = bias, g.T = T, g.C = C;
+  g.sam = sam, g.sak = sak, g.sbn = sbn, g.sbk = sbk, g.ldc = ldc, g.ldt = ldt;
+  g.M = M, g.N = N, g.K = K, g.vec = vr_gemm_vec(K, A, sam, sak, Bm, sbn, sbk) ? 1 : 0, g.ep = ep;
+  g.gx = vr_blocks(N, GT);
+  g.n = g.gx * vr_blocks(M, GT);
+  return g;
 }
 
 int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
@@ -1263,12 +1392,30 @@ int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
   return 0;
 }
 
-void vr_wgrad(kg_vracer_t h, int No, int Ni, int Bn, const float *G, int ldg, const float *Act, int lda, float *dW,
-              float *db) {
+int vr_wgrad_cw(int Ni) {
   int cw = 1;
   while (cw < Ni + 1 && cw < 16) cw <<= 1;  // >= 16 batch lanes: <= B/16 loads per thread
+  return cw;
+}
+void vr_wgrad(kg_vracer_t h, int No, int Ni, int Bn, const float *G, int ldg, const float *Act, int lda, float *dW,
+              float *db) {
+  const int cw = vr_wgrad_cw(Ni);
   hipLaunchKernelGGL(k_vr_wgrad_small, dim3(No, vr_blocks(Ni + 1, cw)), dim3(256), 0, h->stream, No, Ni, Bn, G, ldg, Act,
                      lda, dW, db, cw);
+}
+VrWgradJob vr_wgrad_job(int No, int Ni, int Bn, const float *G, int ldg, const float *Act, int lda, float *dW,
+                        float *db) {
+  VrWgradJob w{};
+  w.G = G, w.Act = Act, w.dW = dW, w.db = db;
+  w.No = No, w.Ni = Ni, w.Bn = Bn, w.ldg = ldg, w.lda = lda, w.cw = vr_wgrad_cw(Ni);
+  w.n = No * vr_blocks(Ni + 1, w.cw);
+  return w;
+}
+void vr_multi(kg_vracer_t h, const VrMulti &J) {
+  int n = 0;
+  for (int q = 0; q < J.nw; q++) n += J.w[q].n;
+  for (int q = 0; q < J.ng; q++) n += J.g[q].n;
+  hipLaunchKernelGGL(k_vr_multi, dim3(n), dim3(256), 0, h->stream, J);
 }
 
 int vr_update(kg_vracer_t h, const unsigned *forced) {
@@ -1286,15 +1433,27 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   hipLaunchKernelGGL(k_vr_bwd_out, dim3(vr_blocks((long long)B * P.H, 256)), dim3(256), 0, h->stream, B, P.H, P.O,
                      (const float *)h->G, (const float *)h->out, (const float *)(h->theta + h->offW[P.L]), lastA, h->dZ,
                      h->dHa, P);
-  vr_wgrad(h, P.O, P.H, B, h->dZ, P.O, lastA, P.H, h->grad + h->offW[P.L], h->grad + h->offb[P.L]);
+  const VrWgradJob outJob =
+      vr_wgrad_job(P.O, P.H, B, h->dZ, P.O, lastA, P.H, h->grad + h->offW[P.L], h->grad + h->offb[P.L]);
+  if (P.L == 1) {
+    VrMulti J{};
+    J.w[J.nw++] = outJob;
+    vr_multi(h, J);
+  }
   float *dcur = h->dHa, *dnext = h->dHb;
   for (int l = P.L - 1; l >= 1; l--) {
     const float *ain = h->acts + (size_t)(l - 1) * rs;
+    VrMulti J{};
+    if (l == P.L - 1) J.w[J.nw++] = outJob;
+    // db_l[o] = sum_b dH[b][o]
+    J.w[J.nw++] = vr_wgrad_job(P.H, 0, B, dcur, P.H, ain, P.H, nullptr, h->grad + h->offb[l]);
     // dW_l[o][i] = sum_b dH[b][o] a_{l-1}[b][i]
-    vr_gemm<EP_STORE>(h, P.H, P.H, B, dcur, 1, P.H, ain, 1, P.H, h->grad + h->offW[l], P.H, nullptr, nullptr, 0);
-    vr_wgrad(h, P.H, 0, B, dcur, P.H, ain, P.H, nullptr, h->grad + h->offb[l]);
+    J.g[J.ng++] = vr_gemm_job(EP_STORE, P.H, P.H, B, dcur, 1, P.H, ain, 1, P.H, h->grad + h->offW[l], P.H, nullptr,
+                              nullptr, 0);
     // dH_{l-1} = (dH W_l) * (1 - a_{l-1}^2)
-    vr_gemm<EP_DTANH>(h, B, P.H, P.H, dcur, P.H, 1, h->theta + h->offW[l], 1, P.H, dnext, P.H, nullptr, ain, P.H);
+    J.g[J.ng++] = vr_gemm_job(EP_DTANH, B, P.H, P.H, dcur, P.H, 1, h->theta + h->offW[l], 1, P.H, dnext, P.H, nullptr,
+                              ain, P.H);
+    vr_multi(h, J);
     float *tmp = dcur;
     dcur = dnext, dnext = tmp;
   }
