@@ -552,6 +552,11 @@ struct NmVal {
   int exact;
 };
 constexpr unsigned long long NM_SPIN_LIMIT = 1ull << 24;
+// c ? a : b field by field (a select of whole structs is lowered through
+// their addresses, which puts the simplex's values in scratch memory)
+__device__ __forceinline__ NmVal nm_sel(bool c, const NmVal &a, const NmVal &b) {
+  return NmVal{c ? a.x : b.x, c ? a.y : b.y, c ? a.eps : b.eps, c ? a.exact : b.exact};
+}
 
 // Hand-offs between the controller and the workers (MI355X_MICROARCH.md,
 // inter-workgroup visibility, the sc1 form): every handed-off byte is
@@ -698,7 +703,7 @@ __device__ __forceinline__ void nm_drive(const NmTab &tab, const NmVal *val, con
     NmVal v;
     get(xc, v, 0);
     if (status) break;
-    const NmVal Ylo = lo ? Y1 : Y0;
+    const NmVal Ylo = nm_sel(lo, Y1, Y0);
     const bool better = cmp(v, Ylo, false);
     if (status) break;
     if (better) {
@@ -709,14 +714,14 @@ __device__ __forceinline__ void nm_drive(const NmTab &tab, const NmVal *val, con
       const bool b2 = cmp(v2, Ylo, false);
       if (status) break;
       const double nx = b2 ? xc2 : xc;
-      const NmVal ny = b2 ? v2 : v;
+      const NmVal ny = nm_sel(b2, v2, v);
       if (hi) X1 = nx, Y1 = ny;
       else X0 = nx, Y0 = ny;
     } else {
       const bool worse = cmp(Y0, v, false);  // Y[s_hi], s_hi = 0
       if (status) break;
       if (worse) {
-        const bool r1 = cmp(v, hi ? Y1 : Y0, true);
+        const bool r1 = cmp(v, nm_sel(hi, Y1, Y0), true);
         if (status) break;
         if (r1) {
           if (hi) X1 = xc, Y1 = v;
@@ -727,7 +732,7 @@ __device__ __forceinline__ void nm_drive(const NmTab &tab, const NmVal *val, con
         const double xc2 = mp - 0.5 * (mp - xh);
         get(xc2, v2, r1 ? 3 : 2);
         if (status) break;
-        const bool r2 = cmp(v2, hi ? Y1 : Y0, true);
+        const bool r2 = cmp(v2, nm_sel(hi, Y1, Y0), true);
         if (status) break;
         if (r2) {
           if (hi) X1 = xc2, Y1 = v2;
@@ -931,7 +936,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
     nm_st(&S->quit, 1ull);
     nm_drain();
     nm_st(&S->seq, round + 1);  // workers leave
-    const NmVal Ylo = lo ? Y1 : Y0;
+    const NmVal Ylo = nm_sel(lo, Y1, Y0);
     out->X[0] = X0;
     out->X[1] = X1;
     out->y[0] = Y0.y;
@@ -982,7 +987,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     for (int i = i0 + tid; i < i1; i += NM_TPB) sll[i - i0] = ll[i];
   unsigned long long round = 0;
   unsigned evals = 0;
-  unsigned long long tEval = 0, tWait = 0, tRest = 0, tlast = __builtin_amdgcn_s_memrealtime(), tFirst = 0;
+  unsigned long long tEval = 0, tWait = 0, tComb = 0, tRest = 0, tlast = __builtin_amdgcn_s_memrealtime(), tFirst = 0;
   const dd invP = dd_div(dd{1.0, 0.0}, dd{(double)P, 0.0});
   auto run_round = [&](const double *pts, int n) __attribute__((always_inline)) {
     const unsigned long long ra = __builtin_amdgcn_s_memrealtime();
@@ -991,7 +996,13 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     round++;
     evals += n;
     __syncthreads();  // every thread has read the previous round's spts / val (and sll is loaded)
-    if (tid < NM_PTS) spts[tid] = tid < n ? pts[tid] : 0.0;
+    if (tid < NM_PTS) {  // (static indices: pts stays in registers, not in scratch)
+      double x = 0.0;
+#pragma unroll
+      for (int k = 0; k < NM_PTS; k++)
+        if (k == tid && k < n) x = pts[k];
+      spts[tid] = x;
+    }
     if (tid == 0) sbn = n;
     // ---- this workgroup's slice (as k_tm_nm_search's workers)
     NmPart acc[NM_PTS];
@@ -1076,6 +1087,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     tlast = __builtin_amdgcn_s_memrealtime();
     tEval += rb - ra;
     tWait += rc - rb;
+    tComb += tlast - rc;
     return sfail != 0;
   };
   double X0 = rho, X1 = rho + 1e-8;  // (GSL step 1e-8)
@@ -1085,7 +1097,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
   double need0 = 0.0, need1 = 0.0;
   nm_drive(tab, val, spts, sbn, run_round, X0, X1, Y0, Y1, iter, lo, status, nneed, need0, need1);
   if (w == 0 && tid == 0) {
-    const NmVal Ylo = lo ? Y1 : Y0;
+    const NmVal Ylo = nm_sel(lo, Y1, Y0);
     out->X[0] = X0;
     out->X[1] = X1;
     out->y[0] = Y0.y;
@@ -1101,14 +1113,15 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     out->loEps = Ylo.eps;
     out->evals = evals;
     out->rounds = (unsigned)round;
-    // (controller phases: hand-off wait, combine + logic, evaluation)
+    // (phases: hand-off wait, simplex logic, evaluation + publish)
     out->tc[0] = tWait;
     out->tc[1] = tRest + (__builtin_amdgcn_s_memrealtime() - tlast);
     out->tc[2] = tEval;
-    // (workgroup 0: whole kernel, its prologue before the first round)
+    // (workgroup 0: whole kernel, its prologue before the first round, the
+    // combine of every round's records)
     out->tw[0] = __builtin_amdgcn_s_memrealtime() - tk0;
     out->tw[1] = tFirst - tk0;
-    out->tw[2] = 0;
+    out->tw[2] = tComb;
   }
 }
 
@@ -2805,9 +2818,12 @@ static int tm_mt_candidates(kg_tmcmc_s *h) {
 int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   const int N = h->N, P = h->P;
   const size_t PN = (size_t)P * N;
-  if (generation == 1 && h->zAhead) {  // (a new run: the normals formed ahead are not its own)
+  if (h->zAhead) {
+    // the normals formed ahead (during the last multinomial) are complete
+    // before this generation's producer is queued behind them on the side
+    // stream; a new run (generation 1) does not use them
     if (h->multivariate.join(h->stream)) return 1;
-    h->zAhead = false;
+    if (generation == 1) h->zAhead = false;
   }
   if (generation == 1 && tm_initialize(h)) return 1;
   if (tm_sync_dev(h)) return 1;
@@ -2852,8 +2868,7 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   } else {
     {
       TmStage st(h, "rng_polar");
-      if (h->zAhead && h->world == 1) {  // formed during the last generation's multinomial
-        if (h->multivariate.join(h->stream)) return 1;
+      if (h->zAhead && h->world == 1) {  // formed during the last generation's multinomial (joined above)
       } else if (h->multivariate.polar_normals(h->Z, PN, N, nullptr, h->stream, h->ca * N, h->cbp * N)) {
         return 1;
       }

@@ -36,6 +36,8 @@ for P in [int(a) for a in sys.argv[1:]] or [1024, 8192]:
           f"logic {1e3 * t[2] / r:.2f}; worker wait {1e3 * t[3] / r:.2f} evaluate {1e3 * t[4] / r:.2f} "
           f"reduce+publish {1e3 * t[5] / r:.2f}; rounds {r:.0f}", flush=True)
     if os.environ.get("KORALI_AMD_NM_SYM", "1") != "0":
-        print(f"P={P} symmetric kernel (workgroup 0): whole launches {t[3]:.3f} ms, prologues {t[4]:.3f} ms "
-              f"(host-timed min_search {tot_ms:.3f} ms)", flush=True)
+        print(f"P={P} symmetric kernel per round (us): hand-off wait {1e3 * t[0] / r:.2f}, simplex logic "
+              f"{1e3 * t[1] / r:.2f}, evaluate + publish {1e3 * t[2] / r:.2f}, combine {1e3 * t[5] / r:.2f}; "
+              f"whole launches {t[3]:.3f} ms, prologues {t[4]:.3f} ms (host-timed min_search {tot_ms:.3f} ms)",
+              flush=True)
     dev.close()
