@@ -333,9 +333,30 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
 // (linear.cpp.base:337-350: summed over the batch).  One workgroup per
 // (o, column chunk): CW columns x (256 / CW) batch lanes, partial sums
 // reduced through LDS in a fixed order (deterministic).
+__device__ __forceinline__ void vr_adam_elem(long long j, float g, float *__restrict__ theta, float *__restrict__ m1,
+                                             float *__restrict__ m2, const State *__restrict__ st, int l2,
+                                             float l2imp) {
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-08f;
+  const float f1 = 1.0f / (1.0f - st->b1p), f2 = 1.0f / (1.0f - st->b2p);
+  if (l2) g -= l2imp * theta[j];
+  const float m = b1 * m1[j] - (1.0f - b1) * g;
+  const float v = b2 * m2[j] + (1.0f - b2) * g * g;
+  m1[j] = m;
+  m2[j] = v;
+  theta[j] -= st->eta / (sqrtf(v * f2) + eps) * m * f1;
+}
+struct VrAdamJob {
+  float *theta, *m1, *m2;
+  const float *grad;
+  const State *st;
+  long long lo, hi;  // the parameters the adam blocks update (the wgrad blocks update their own)
+  int l2;
+  float l2imp;
+};
 __device__ __forceinline__ void vr_wgrad_block(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
                                                const float *__restrict__ Act, int lda, float *__restrict__ dW,
-                                               float *__restrict__ db, int CW, int bx, int by, float *part) {
+                                               float *__restrict__ db, int CW, int bx, int by, float *part,
+                                               const VrAdamJob *adam = nullptr) {
   const int o = bx, t = threadIdx.x, lanes = 256 / CW, c = t % CW, l = t / CW;
   const int i = by * CW + c;
   float acc = 0.f;
@@ -352,8 +373,9 @@ __device__ __forceinline__ void vr_wgrad_block(int No, int Ni, int Bn, const flo
     __syncthreads();
   }
   if (l == 0 && i <= Ni) {
-    if (i < Ni) dW[o * Ni + i] = part[c];
-    else db[o] = part[c];
+    float *gp = i < Ni ? dW + o * Ni + i : db + o;
+    *gp = part[c];
+    if (adam) vr_adam_elem(gp - adam->grad, part[c], adam->theta, adam->m1, adam->m2, adam->st, adam->l2, adam->l2imp);
   }
 }
 __global__ __launch_bounds__(256) void k_vr_wgrad_small(int No, int Ni, int Bn, const float *__restrict__ G, int ldg,
@@ -384,6 +406,19 @@ struct VrMulti {
   VrGemmJob g[2];
   int nw, ng;
 };
+// The input layer's weight gradients and the whole Adam step in one launch:
+// the wgrad blocks apply Adam to the parameters they just reduced (W_0, b_0),
+// the others to every parameter the previous launches' gradients finished
+__global__ __launch_bounds__(256) void k_vr_wgrad_adam(VrWgradJob w, VrAdamJob a) {
+  __shared__ float part[256];
+  const int b = blockIdx.x;
+  if (b < w.n) {
+    vr_wgrad_block(w.No, w.Ni, w.Bn, w.G, w.ldg, w.Act, w.lda, w.dW, w.db, w.cw, b % w.No, b / w.No, part, &a);
+    return;
+  }
+  const long long j = a.lo + (long long)(b - w.n) * 256 + threadIdx.x;
+  if (j < a.hi) vr_adam_elem(j, a.grad[j], a.theta, a.m1, a.m2, a.st, a.l2, a.l2imp);
+}
 __global__ __launch_bounds__(256) void k_vr_multi(VrMulti J) {
   __shared__ float As[GK][GP];
   __shared__ float Bs[GK][GP];
@@ -423,15 +458,7 @@ __global__ void k_vr_adam(long long n, float *__restrict__ theta, const float *_
                           float l2imp) {
   const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-08f;
-  const float f1 = 1.0f / (1.0f - st->b1p), f2 = 1.0f / (1.0f - st->b2p);
-  float g = grad[j];
-  if (l2) g -= l2imp * theta[j];
-  const float m = b1 * m1[j] - (1.0f - b1) * g;
-  const float v = b2 * m2[j] + (1.0f - b2) * g * g;
-  m1[j] = m;
-  m2[j] = v;
-  theta[j] -= st->eta / (sqrtf(v * f2) + eps) * m * f1;
+  vr_adam_elem(j, grad[j], theta, m1, m2, st, l2, l2imp);
 }
 
 // ------------------------------------------------------------ replay memory
@@ -1457,10 +1484,16 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
     float *tmp = dcur;
     dcur = dnext, dnext = tmp;
   }
-  vr_wgrad(h, P.H, P.S, B, dcur, P.H, h->Xmb, P.S, h->grad + h->offW[0], h->grad + h->offb[0]);
-  hipLaunchKernelGGL(k_vr_adam, dim3(vr_blocks((long long)h->nparam, 256)), dim3(256), 0, h->stream,
-                     (long long)h->nparam, h->theta, (const float *)h->grad, h->m1, h->m2, (const State *)h->st, P.l2,
-                     P.l2imp);
+  {
+    // the input layer's gradients (W_0, b_0: the first S H + H parameters),
+    // with Adam on every parameter in the same launch
+    const VrWgradJob w0 = vr_wgrad_job(P.H, P.S, B, dcur, P.H, h->Xmb, P.S, h->grad + h->offW[0], h->grad + h->offb[0]);
+    VrAdamJob a{};
+    a.theta = h->theta, a.m1 = h->m1, a.m2 = h->m2, a.grad = h->grad, a.st = (const State *)h->st;
+    a.lo = (long long)h->offb[0] + P.H, a.hi = (long long)h->nparam, a.l2 = P.l2, a.l2imp = P.l2imp;
+    const int na = (int)vr_blocks(a.hi - a.lo, 256);
+    hipLaunchKernelGGL(k_vr_wgrad_adam, dim3(w0.n + na), dim3(256), 0, h->stream, w0, a);
+  }
   KG_HIP(hipGetLastError());
   return 0;
 }
