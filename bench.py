@@ -66,7 +66,10 @@ STAGE_KERNELS = {
     "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", ("kg::k_mean3", "kg::k_mean2", "kg::k_mean"),
                    ("kg::k_paths3", "kg::k_paths2", "kg::k_paths")],
     # C3 (TMCMC): the weighted mean / covariance stage
-    "mean_cov": ["kg::k_tm_factors_mean", "kg::k_tm_wsum<false>", "kg::k_tm_factors_cov", "kg::k_tm_wsum<true>"],
+    "mean_cov": [("kg::k_tm_factors_mean_t", "kg::k_tm_factors_mean"), ("kg::k_tm_wsum_rows<false>", "kg::k_tm_wsum<false>"),
+                 ("kg::k_tm_factors_cov_t", "kg::k_tm_factors_cov"), ("kg::k_tm_wsum_rows<true>", "kg::k_tm_wsum<true>")],
+    # C3: the annealing search (symmetric form by default)
+    "min_search": [("kg::k_tm_nm_sym", "kg::k_tm_nm_search")],
 }
 PROFILE_ROUNDS = ("r4", "r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
 
@@ -247,7 +250,11 @@ def engine_rate(steps, warmup, cov):
       run (handle creation, initialisation, the first generation), leaving
       the engine's per-generation rate;
     * end_to_end: one fresh k.run(e) of `steps` generations, wall clock,
-      handle creation and initialisation included."""
+      handle creation and initialisation included;
+    * in_run: from that same run, generations `warmup`+1 .. `steps` by the
+      engine's own completion marks (Internal / Generation Completion Times:
+      when each generation's termination check returned), no subtraction
+      of two runs."""
     import korali
     k = korali.Engine()
     k.run(c2_experiment(cov, warmup))  # (first-use costs: module load, code objects)
@@ -266,7 +273,10 @@ def engine_rate(steps, warmup, cov):
     t0 = time.perf_counter()
     k.run(f)
     e2e = steps / (time.perf_counter() - t0)
-    return diff, e2e
+    marks = list(f["Internal"]["Generation Completion Times"])
+    w = min(warmup, steps - 1)
+    in_run = (steps - w) / (marks[steps] - marks[w]) if len(marks) == steps + 1 else None
+    return diff, e2e, in_run
 
 
 def main():
@@ -356,7 +366,7 @@ def main():
 
     best = float(dev["Best Ever Value"][0])
     dev.close()
-    eng, eng_e2e = engine_rate(args.steps, args.warmup, args.cov) if world == 1 else (None, None)
+    eng, eng_e2e, eng_in_run = engine_rate(args.steps, args.warmup, args.cov) if world == 1 else (None, None, None)
     # the other covariance mode on this rank alone (reported beside `value`)
     alt = "mfma" if args.cov == "exact" else "exact"
     adev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
@@ -430,6 +440,7 @@ def main():
         "samples_per_sec": gens_per_s * LAMBDA,
         "engine_generations_per_sec": eng,
         "engine_end_to_end_generations_per_sec": eng_e2e,
+        "engine_in_run_generations_per_sec": eng_in_run,
         f"{alt}_covariance_generations_per_sec_per_gpu": alt_rate,
         "rankmu_mfma_roofline": mfma_kernel,
         "best_ever_value": best,
@@ -582,10 +593,10 @@ def run_c3(args):
         "chain_steps_per_sec": done * C3_P / elapsed,
         "stage_ms": stages,
         "annealing_search": search,
-        "roofline": {"kernel": {"min_search": "kg::k_tm_nm_search"}.get(dominant, dominant), "stage": dominant,
+        "roofline": {"kernel": {"min_search": "kg::k_tm_nm_sym"}.get(dominant, dominant), "stage": dominant,
                      "bound": "mfma",
                      "bound_note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); the stage is a "
-                                   "chain of dependent rounds (GSL nmsimplex order, two cross-XCD hand-offs per "
+                                   "chain of dependent rounds (GSL nmsimplex order, one cross-XCD hand-off per "
                                    "round), far below it by construction",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": c3_traffic,

@@ -217,6 +217,14 @@ int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, siz
  * (window624 = 624 consecutive untempered words of a GSL mt19937 stream,
  * not starting at the seeding word 0).  Runs on the host, no device needed. */
 int kg_debug_mt_jump(const uint32_t *window624, uint64_t distance, uint32_t *out624);
+/* Host-only check of the TMCMC resampling (no device call): `reps`
+ * consecutive gsl_ran_multinomial draws (K categories, N trials) from one
+ * mt19937 seeded with `seed`, by the exact conditional-binomial walk
+ * (n_exact) and by the interval-decided walk the handle uses (n_interval);
+ * each array holds reps * K counts.  Replaces nothing in the reference
+ * (TMCMC.cpp.base:303-309 draws through Multinomial::getSelections). */
+int kg_debug_multinomial(uint64_t seed, size_t K, unsigned N, const double *p, size_t reps, unsigned *n_exact,
+                         unsigned *n_interval);
 /* The device CartPole (examples/learning/reinforcement/cartpole/_model/
  * cartpole.py: scipy dopri5 advance, restated in kg_vracer.hip) on given
  * forces: n trajectories from u0 (n x 4) at t = 0, `steps` advances each with

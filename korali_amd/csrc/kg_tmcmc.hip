@@ -1674,6 +1674,98 @@ void multinomial(HostMt &r, size_t K, unsigned N, const double *p, unsigned *n, 
   }
 }
 
+// multinomial() with the inversion's comparisons decided on certified
+// intervals (round 4).  gsl_ran_binomial's inversion compares the uniform
+// with f0 = pow_uint(q, n) and its successors f_(ix+1) = f_ix s (n - ix) /
+// (ix + 1), subtracting each from u: only the OUTCOME of those comparisons
+// matters (the counts and the stream position), not the values.  Here f0 is
+// exp(n log q), within d0 = (n + 128) 2^-50 + |n log q| 2^-51 of pow_uint's
+// value relative (pow_uint's squarings: <= n 2^-53; log and exp: <= 1 ulp
+// each), and the successors and u carry running bounds; a comparison whose
+// intervals straddle goes through the exact loop from the same uniform, so
+// the result is the reference's bit for bit (KORALI_AMD_TM_MULTINOMIAL=exact:
+// the exact form everywhere; tests/test_multinomial_cpu.py compares both
+// with the oracle).  The walk's dependent chain loses pow_uint's squarings,
+// its branches, and the division per step.
+static double g_inv1[112];
+static const bool g_inv1_init = [] {
+  for (int i = 0; i < 112; i++) g_inv1[i] = 1.0 / (i + 1);
+  return true;
+}();
+unsigned binomial_inv_exact(HostMt &r, double u, double q, double s, bool flip, unsigned n) {
+  const double f0 = pow_uint(q, n);
+  int ix = 0;
+  for (;;) {
+    double f = f0;
+    bool done = false;
+    for (ix = 0; ix <= 110; ++ix) {
+      if (u < f) {
+        done = true;
+        break;
+      }
+      u -= f;
+      f *= s * (n - ix) / (ix + 1);
+    }
+    if (done) break;
+    u = r.uniform();
+  }
+  return flip ? (n - ix) : (unsigned)ix;
+}
+unsigned binomial_inv_interval(HostMt &r, double q, double lq, double s, bool flip, unsigned n) {
+  const double u0 = r.uniform();
+  const double z = (double)n * lq;
+  double F = exp(z);
+  if (F > 1e-280) {
+    double d = (n + 128.0) * 8.881784197001252e-16 + fabs(z) * 4.440892098500626e-16;  // |F - f| <= d f
+    double U = u0, E = 0.0;                                                            // |U - u| <= E
+    for (int ix = 0; ix <= 110; ++ix) {
+      const double lo = F * (1.0 - 2.0 * d), hi = F * (1.0 + 2.0 * d);
+      if (U + E < lo) return flip ? (n - ix) : (unsigned)ix;  // u < f certainly
+      if (!(U - E >= hi)) break;                               // straddles (or NaN): the exact loop
+      const double U1 = U - F;
+      E = E + 2.0 * d * F + 2.220446049250313e-16 * (fabs(U1) + fabs(U)) + 1e-300;
+      U = U1;
+      F = F * (s * (double)(n - ix)) * g_inv1[ix];
+      d = d + 6.661338147750939e-16;  // this step's roundings, both forms
+    }
+  }
+  return binomial_inv_exact(r, u0, q, s, flip, n);
+}
+void multinomial_interval(HostMt &r, size_t K, unsigned N, const double *p, unsigned *n, double *btpeDraws,
+                          std::vector<double> &scratch) {
+  scratch.resize(4 * K);
+  double *po = scratch.data(), *qf = po + K, *sf = po + 2 * K, *lq = po + 3 * K;
+  double norm = 0.0, sum_p = 0.0;
+  for (size_t k = 0; k < K; k++) norm += p[k];
+  // the conditional probabilities do not depend on the draws: formed first
+  for (size_t k = 0; k < K; k++) {
+    const double pk = p[k] / (norm - sum_p);
+    sum_p += p[k];
+    const double pf = pk > 0.5 ? 1.0 - pk : pk;
+    po[k] = pk;
+    qf[k] = 1 - pf;
+    sf[k] = pf / qf[k];
+    lq[k] = log(qf[k]);
+  }
+  unsigned sum_n = 0;
+  size_t k = 0;
+  for (; k < K && sum_n < N; k++) {  // (past sum_n == N every binomial is 0 without a draw)
+    const unsigned m = N - sum_n;
+    unsigned v = 0;
+    if (p[k] > 0.0) {
+      const bool flip = po[k] > 0.5;
+      const double pf = flip ? 1.0 - po[k] : po[k];
+      if (m * pf < 14)
+        v = binomial_inv_interval(r, qf[k], lq[k], sf[k], flip, m);
+      else
+        v = binomial(r, po[k], m, btpeDraws);
+    }
+    n[k] = v;
+    sum_n += v;
+  }
+  for (; k < K; k++) n[k] = 0;
+}
+
 // the serial tail of calculateSquaredCVDifference :683-703 on one search
 // point's exponentials: std::accumulate, normalisation, gsl_stats_mean and
 // gsl_stats_sd_m with their `long double` running recurrences.
@@ -1787,7 +1879,8 @@ struct kg_tmcmc_s {
          *negLogWidth = nullptr, *Z = nullptr, *U = nullptr, *Uprior = nullptr, *E = nullptr, *w = nullptr;
   unsigned long long *uoff = nullptr;
   int2 *pairs = nullptr;
-  bool wsumLds = false;
+  bool wsumLds = false, exactMultinomial = false;  // KORALI_AMD_TM_MULTINOMIAL=exact
+  std::vector<double> mnScratch;
   double *fA = nullptr, *fB = nullptr;  // term factors of the ordered sums (P x N + 2, or N x wr_pitch(P))    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
   unsigned *src = nullptr;
@@ -2646,6 +2739,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     h->wsumLds = ws && strcmp(ws, "lds") == 0;
     const char *dt = getenv("KORALI_AMD_TM_DEFER_TAIL");
     h->deferTail = !(dt && dt[0] == '0');
+    const char *em = getenv("KORALI_AMD_TM_MULTINOMIAL");
+    h->exactMultinomial = em && strcmp(em, "exact") == 0;
     const char *za = getenv("KORALI_AMD_TM_NORMALS_AHEAD");
     h->zAheadOn = !(za && za[0] == '0');
   }
@@ -3219,7 +3314,10 @@ int kg_tmcmc_process_finalize(kg_tmcmc_t h, size_t generation) {
     for (int i = 0; i < P; i++) sw += h->hE[i];
     for (int i = 0; i < P; i++) wt[i] = h->hE[i] / sw;
     h->logEvidence += host_log_cr(sw) + lwmax - host_log_cr((double)P);
-    multinomial(h->multinomialRng, P, (unsigned)P, wt, h->nsel.data(), &h->btpeDraws);
+    if (h->exactMultinomial)
+      multinomial(h->multinomialRng, P, (unsigned)P, wt, h->nsel.data(), &h->btpeDraws);
+    else
+      multinomial_interval(h->multinomialRng, P, (unsigned)P, wt, h->nsel.data(), &h->btpeDraws, h->mnScratch);
     for (int i = 0; i < P; i++) h->hNsel[i] = h->nsel[i];
     for (int i = 0; i < P; i++) wt[i] = wt[i] * h->nsel[i];
     sw = 0.0;
@@ -3439,3 +3537,22 @@ int kg_tmcmc_profile_read(kg_tmcmc_t h, const char *stage, double *ms_total, siz
 }
 
 }  // extern "C"
+
+// host-only check of the multinomial forms (no device call): `reps`
+// consecutive K-category draws of N from one generator seeded with `seed`
+// (GSL mt19937 seeding), exact form into n_exact, interval form into
+// n_interval (reps * K each)
+int kg_debug_multinomial(uint64_t seed, size_t K, unsigned N, const double *p, size_t reps, unsigned *n_exact,
+                         unsigned *n_interval) {
+  KG_CHECK(K > 0 && p && n_exact && n_interval, "kg_debug_multinomial: bad arguments");
+  kg::HostMt a, b;
+  a.seed(seed);
+  b.seed(seed);
+  double bt = 0;
+  std::vector<double> scratch;
+  for (size_t r = 0; r < reps; r++) {
+    kg::multinomial(a, K, N, p, n_exact + r * K, &bt);
+    kg::multinomial_interval(b, K, N, p, n_interval + r * K, &bt, scratch);
+  }
+  return 0;
+}
