@@ -390,6 +390,7 @@ typedef struct {
   int device;
   int policy_distribution;                 /* Policy / Distribution: 0 Normal, 1 Clipped Normal */
   const double *action_lower_bounds, *action_upper_bounds;  /* action_size values (may be NULL for Normal) */
+  int reward_rescaling;                    /* Reward / Rescaling / Enabled (environment_count <= 8) */
 } kg_vracer_config;
 
 int kg_vracer_create(const kg_vracer_config *cfg, kg_vracer_t *out);

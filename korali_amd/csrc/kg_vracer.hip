@@ -43,6 +43,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MAXA = 4;  // action dimensions supported by the device kernels
 constexpr int MAXO = 1 + 2 * MAXA;
 constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
+constexpr int MAXENV = 8;   // environment ids with reward rescaling (Problem / Environment Count)
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
 enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u, ERR_ENV_ODE = 8u };
 
@@ -60,6 +61,10 @@ struct State {
   unsigned long long experience_count;
   unsigned errors, pad1;
   double step_reward_sum;         // cumulative rewards of the episodes finished by the last step
+  // reward rescaling (agent.cpp.base:96-98, :423-437, :557-563), per environment id
+  float rsig[MAXENV];             // getScaledReward's sigma (1.0 unless enabled)
+  float rsum[MAXENV];             // sum of squared rewards in the replay memory
+  long long rcnt[MAXENV];         // experiences in the replay memory
 };
 
 struct Params {  // launch-constant configuration
@@ -72,6 +77,7 @@ struct Params {  // launch-constant configuration
   unsigned long long seed;
   int clipped;                    // Policy Distribution: 0 Normal, 1 Clipped Normal
   float lb[MAXA], ub[MAXA];       // action bounds (Variables' Lower / Upper Bound)
+  int rr;                         // Reward / Rescaling / Enabled
 };
 
 // ---------------------------------------------------------------- philox
@@ -554,6 +560,10 @@ __device__ __forceinline__ int u8v(unsigned char b) {
   asm volatile("" : "+v"(v));
   return v;
 }
+// RR: reward rescaling enabled (every reward through getScaledReward: the
+// divisions are exact no-ops at sigma 1.0, but the retrace walk then also
+// loads each entry's environment id, so the plain form does without)
+template <bool RR>
 __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                  const float *__restrict__ out, float *__restrict__ G) {
   __shared__ unsigned s_mb[MB_META];
@@ -561,6 +571,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       s_tv[MB_META], s_act[MB_META], s_cur[2 * MB_META], s_old[2 * MB_META];
   __shared__ unsigned char s_term[MB_META], s_onp[MB_META], s_uniq[MB_META];
   __shared__ int s_delta;
+  __shared__ float s_rsig[MAXENV];
   const int t = threadIdx.x, nt = blockDim.x, B = P.B, O = P.O;
   // every scalar read once into registers
   const float cutoff = st->cutoff, beta = st->beta, lr = st->lr, b1p = st->b1p, b2p = st->b2p;
@@ -573,6 +584,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     return (long long)q;
   };
   if (t == 0) s_delta = 0;
+  if (RR && t < MAXENV) s_rsig[t] = st->rsig[t];
   __syncthreads();
   // ---- importance weights and on-policy flags (agent.cpp.base:613-657);
   // duplicates compute the same values, only the first occurrence counts
@@ -581,7 +593,8 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     const unsigned id = mb[b];
     const bool uniq = b == 0 || id != mb[b - 1];
     const long long p = ph(id);
-    const float a = er.act[p], om = er.exp_pol[2 * p], osd = er.exp_pol[2 * p + 1], rew = er.rew[p];
+    const float a = er.act[p], om = er.exp_pol[2 * p], osd = er.exp_pol[2 * p + 1],
+                rew = RR ? er.rew[p] / st->rsig[er.env[p]] : er.rew[p];
     const int was = er.onp[p], term = er.term[p];
     const float V = out[(long long)b * O], cm = out[(long long)b * O + 1], cs = out[(long long)b * O + 2];
     const float tvv = term == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
@@ -634,16 +647,22 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     // (unconditional: entries past the chunk or the episode are valid slots
     // of the ring whose values go unused; no branch splits the loads from
     // the waits, so those stay counted)
-    auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC]) __attribute__((always_inline)) {
+    int ea[RC], eb[RC];  // (RR: the entries' environment ids)
+    auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC], int (&en)[RC])
+                    __attribute__((always_inline)) {
       long long q = p0;
 #pragma unroll
       for (int j = 0; j < RC; j++) {
         vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
+        if (RR) en[j] = er.env[q];
         q = q == 0 ? (long long)R - 1 : q - 1;
       }
     };
-    auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], const float (&rw)[RC])
-                       __attribute__((always_inline)) {
+    auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC],
+                       const int (&en)[RC]) __attribute__((always_inline)) {
+      if (RR)
+#pragma unroll
+        for (int j = 0; j < RC; j++) rw[j] = rw[j] / s_rsig[en[j]];  // getScaledReward (agent.cpp.base:720)
       const int n = (int)min((long long)RC, c - start + 1);
       int kk = k;
       unsigned long long inmb = 0;
@@ -681,17 +700,17 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     };
     float av[RC], at[RC], ar[RC], bv[RC], bt[RC], br[RC];
     long long c = end, pc = ph(end);
-    load(pc, av, at, ar);
+    load(pc, av, at, ar, ea);
     while (c >= start) {
       long long c1, pc1;
       next(c, pc, c1, pc1);
-      load(pc1, bv, bt, br);
-      process(c, pc, av, at, ar);
+      load(pc1, bv, bt, br, eb);
+      process(c, pc, av, at, ar, ea);
       c = c1, pc = pc1;
       if (c < start) break;
       next(c, pc, c1, pc1);
-      load(pc1, av, at, ar);
-      process(c, pc, bv, bt, br);
+      load(pc1, av, at, ar, ea);
+      process(c, pc, bv, bt, br, eb);
       c = c1, pc = pc1;
     }
   }
@@ -1011,6 +1030,8 @@ struct Envs {
   int *fin_env;       // environment of the finished episode of each rank
   float *eb_st, *eb_act, *eb_pol, *eb_v, *eb_rew;  // E x T episode buffers
   float *rewards;     // cumulative rewards of the episodes finished by the last step (by rank)
+  float *sigb;        // rank x MAXENV: the rescaling sigmas before that episode (reward rescaling)
+  int *fin_id;        // environment id of the finished episode of each rank
 };
 
 __global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long sample0, const int *only_fin) {
@@ -1184,6 +1205,64 @@ __global__ __launch_bounds__(256) void k_vr_evict(Params P, State *st, Replay er
   if (evicted) atomicAdd((unsigned long long *)&st->off_count, (unsigned long long)(-(long long)evicted));
 }
 
+// Reward rescaling's bookkeeping (agent.cpp.base:423-437, :557-563) for this
+// step's finished episodes in processEpisode order, one thread (the sums
+// are sequential float sums, as the reference's): per experience the new
+// reward's square in and, with the memory full, the evicted one's out; per
+// episode the sigmas before it (its initial retrace values use them) and
+// after it.  Runs before k_vr_append overwrites the evicted slots; only
+// when rescaling is enabled (the sums only feed the sigmas).
+__device__ inline float rr_sigma(float sum, long long cnt) {
+  return (float)(sqrt((double)sum / ((double)(float)cnt + 1e-9)) + 1e-9);
+}
+__global__ void k_vr_reward_sums(Params P, State *st, Replay er, Envs ev) {
+  if (threadIdx.x || blockIdx.x) return;
+  const unsigned long long base = st->step_base, neps = st->step_episodes;
+  const long long R = P.R;
+  // (LDS, not registers: the environment id indexes them)
+  __shared__ float sum[MAXENV], sig[MAXENV];
+  __shared__ long long cnt[MAXENV];
+  for (int i = 0; i < MAXENV; i++) sum[i] = st->rsum[i], cnt[i] = st->rcnt[i], sig[i] = st->rsig[i];
+  // the batch entry at offset j (episodes in rank order): a forward cursor
+  int cr = 0;
+  long long cend = neps ? ev.len[ev.fin_env[0]] : 0, cbeg = 0;
+  for (unsigned long long r = 0; r < neps; r++) {
+    const int e = ev.fin_env[r], id = ev.env_id[e], len = ev.len[e];
+    const long long off = ev.off[e];
+    ev.fin_id[r] = id;
+    for (int i = 0; i < MAXENV; i++) ev.sigb[r * MAXENV + i] = sig[i];
+    for (int k = 0; k < len; k++) {
+      const float rw = ev.eb_rew[(long long)e * P.T + k];
+      sum[id] += rw * rw;
+      cnt[id]++;
+      const long long a = (long long)base + off + k;  // absolute index of the new entry
+      if (a >= R) {                                   // full: the oldest entry a - R leaves
+        const long long old = a - R;
+        float ro;
+        int io;
+        if (old >= (long long)base) {  // an entry of this same batch
+          const long long j = old - (long long)base;
+          while (j >= cend) {
+            cr++;
+            cbeg = cend;
+            cend += ev.len[ev.fin_env[cr]];
+          }
+          const int eo = ev.fin_env[cr];
+          ro = ev.eb_rew[(long long)eo * P.T + (j - cbeg)];
+          io = ev.env_id[eo];
+        } else {
+          ro = er.rew[old % R];
+          io = er.env[old % R];
+        }
+        sum[io] -= ro * ro;
+        cnt[io]--;
+      }
+    }
+    for (int i = 0; i < P.env_count && i < MAXENV; i++) sig[i] = rr_sigma(sum[i], cnt[i]);
+  }
+  for (int i = 0; i < MAXENV; i++) st->rsum[i] = sum[i], st->rcnt[i] = cnt[i], st->rsig[i] = sig[i];
+}
+
 // processEpisode (agent.cpp.base:376-572) for every finished episode at once:
 // one workgroup per environment copies its episode into the replay memory,
 // counts evicted off-policy entries, sets the initial retrace values (the
@@ -1230,11 +1309,15 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
   }
   __syncthreads();
   if (t == 0) {
-    // initial retrace values (agent.cpp.base:520-555)
+    // initial retrace values (agent.cpp.base:520-555), rewards through
+    // getScaledReward with the sigmas before this episode's update
+    const float *sg = P.rr ? ev.sigb + (long long)rank * MAXENV : nullptr;
+    auto scaled = [&](float r, int id) { return sg ? r / sg[id] : r; };
+    const int myid = ev.env_id[e];
     float retV = 0.0f;
     if (term == TRUNCATED) retV += P.gamma * outF[(long long)e * P.O];
     const long long endj = off + len - 1;
-    retV = P.gamma * retV + ev.eb_rew[(long long)e * P.T + len - 1];
+    retV = P.gamma * retV + scaled(ev.eb_rew[(long long)e * P.T + len - 1], myid);
     // an entry overwritten later in this same batch (more new experiences
     // than the capacity) keeps the later entry's values, as the reference's
     // sequential processEpisode calls leave it
@@ -1243,11 +1326,16 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     const long long prevj = endj - 1;
     if ((long long)base + prevj >= 0 && prevj >= survive) {
       float r;
-      if (len >= 2) r = ev.eb_rew[(long long)e * P.T + len - 2];
+      if (len >= 2) r = scaled(ev.eb_rew[(long long)e * P.T + len - 2], myid);
       else if (rank > 0) {
         const int pe = ev.fin_env[rank - 1];
         r = ev.eb_rew[(long long)pe * P.T + ev.len[pe] - 1];
-      } else r = er.rew[((long long)base + prevj) % R];
+        if (sg) r = scaled(r, ev.fin_id[rank - 1]);
+      } else {
+        const long long q = ((long long)base + prevj) % R;
+        r = er.rew[q];
+        if (sg) r = scaled(r, er.env[q]);
+      }
       retV = P.gamma * retV + r;
       er.ret[((long long)base + prevj) % R] = retV;
     }
@@ -1270,6 +1358,7 @@ __global__ void k_vr_init_state(State *st, float lr, float beta, float cutoff) {
   if (threadIdx.x || blockIdx.x) return;
   State s = {};
   s.lr = lr, s.beta = beta, s.cutoff = cutoff, s.eta = lr, s.b1p = 1.0f, s.b2p = 1.0f;
+  for (int i = 0; i < MAXENV; i++) s.rsig[i] = 1.0f;
   *st = s;
 }
 
@@ -1452,7 +1541,8 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   VrStage tu(h, "update");
   hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
   if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
-  hipLaunchKernelGGL(k_vr_meta, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er, (const unsigned *)h->mb,
+  hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er,
+                     (const unsigned *)h->mb,
                      (const float *)h->out, h->G);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
   const size_t rs = h->rowsMax * P.H;
@@ -1542,6 +1632,9 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"finished_rewards", h->ev.rewards, 4, E}, {"finished_env", h->ev.fin_env, 4, E},
       {"mini_batch", h->mb, 4, (size_t)P.B},   {"loss_gradient", h->G, 4, (size_t)P.B * P.O},
       {"policy_output", h->out, 4, h->rowsMax * P.O},
+      {"reward_rescaling_sigma", &h->st->rsig[0], 4, (size_t)MAXENV},
+      {"reward_rescaling_sum", &h->st->rsum[0], 4, (size_t)MAXENV},
+      {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {
@@ -1588,6 +1681,9 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.O = 1 + 2 * P.A, P.E = (int)c->environments, P.B = (int)c->mini_batch_size, P.T = (int)c->max_episode_steps;
   P.R = (long long)c->replay_maximum_size;
   P.env_count = (int)c->environment_count;
+  P.rr = c->reward_rescaling ? 1 : 0;
+  KG_CHECK(!P.rr || (c->environment_count >= 1 && c->environment_count <= (size_t)MAXENV),
+           "vracer: Reward Rescaling on the device supports Environment Count 1..8");
   P.l2 = c->l2_regularization_enabled ? 1 : 0;
   P.gamma = (float)c->discount_factor, P.lr0 = (float)c->learning_rate, P.iw_trunc = (float)c->importance_weight_truncation_level;
   P.cutoff_scale = (float)c->off_policy_cutoff_scale, P.off_target = (float)c->off_policy_target;
@@ -1668,6 +1764,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(ev.fin, E * 4), alloc(ev.len, E * 4), alloc(ev.off, E * 8), alloc(ev.rank, E * 4), alloc(ev.fin_env, E * 4);
   alloc(ev.eb_st, ET * P.S * 4), alloc(ev.eb_act, ET * P.A * 4), alloc(ev.eb_pol, ET * 2 * P.A * 4);
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
+  alloc(ev.sigb, E * MAXENV * 4), alloc(ev.fin_id, E * 4);
   if (!rc && hipHostMalloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
     kg::set_error("vracer: hipHostMalloc failed");
     rc = 1;
@@ -1744,7 +1841,7 @@ int kg_vracer_destroy(kg_vracer_t h) {
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
                   h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,
                   h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
-                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards};
+                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->st_host) (void)hipHostFree(h->st_host);
@@ -1955,6 +2052,7 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
   if (vr_forward(h, h->X, P.E, h->outF)) return 1;  // V of truncated states (agent.cpp.base:530-545)
   hipLaunchKernelGGL(k_vr_scan, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->ev);
   hipLaunchKernelGGL(k_vr_evict, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er);
+  if (P.rr) hipLaunchKernelGGL(k_vr_reward_sums, dim3(1), dim3(64), 0, h->stream, P, h->st, h->er, h->ev);
   hipLaunchKernelGGL(k_vr_append, dim3(P.E), dim3(256), 0, h->stream, P, h->st, h->er, h->ev, (const float *)h->outF,
                      h->X);
   KG_HIP(hipGetLastError());

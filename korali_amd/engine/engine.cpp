@@ -1586,6 +1586,7 @@ std::vector<float> vracerInitialHyperparameters(const std::vector<size_t> &sizes
 namespace {
 
 struct VracerModule : SolverModule {
+  size_t envIds = 1;  // Problem / Environment Count
   kg_vracer_t h = nullptr;
   double maxGenerations = 1e10;
   unsigned long long maxEpisodes = 0, maxExperiences = 0, maxPolicyUpdates = 0, episodesPerGeneration = 1,
@@ -1635,6 +1636,7 @@ struct VracerModule : SolverModule {
            pb["Environment Kernel"].getString().c_str());
     if (uint(pb, "Agents Per Environment", 1) != 1) fail("'Agents Per Environment' > 1 is not supported by the device path.");
     const unsigned long long envCount = uint(pb, "Environment Count", 1);
+    envIds = (size_t)envCount;
     uint(pb, "Actions Between Policy Updates", 0);  // the device policy is always the current one
     const unsigned long long maxSteps = uint(pb, "Max Episode Steps", 500);  // env.py maxSteps
     // variables (reinforcementLearning.cpp.base:40-53; continuous.cpp.base:44-50)
@@ -1669,7 +1671,9 @@ struct VracerModule : SolverModule {
            actLb, actUb, sv["Policy"]["Distribution"].getString().c_str());
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
     if (flag(sv["State Rescaling"], "Enabled", false)) fail("State Rescaling is not supported by the device path.");
-    if (flag(sv["Reward"]["Rescaling"], "Enabled", false)) fail("Reward Rescaling is not supported by the device path.");
+    const bool rewardRescaling = flag(sv["Reward"]["Rescaling"], "Enabled", false);
+    if (rewardRescaling && (envCount < 1 || envCount > 8))
+      fail("Reward Rescaling on the device supports an 'Environment Count' of 1 to 8 (%llu given).", envCount);
     if (flag(sv["Reward"]["Outbound Penalization"], "Enabled", false))
       fail("Reward Outbound Penalization is not supported by the device path.");
     Json &nn = sv["Neural Network"];
@@ -1718,6 +1722,7 @@ struct VracerModule : SolverModule {
     c.l2_regularization_importance = num(sv["L2 Regularization"], "Importance", 1e-4);
     c.initial_exploration_noise = &noise;
     c.policy_distribution = dist == "clippednormal" ? 1 : 0;
+    c.reward_rescaling = rewardRescaling ? 1 : 0;
     c.action_lower_bounds = &actLb, c.action_upper_bounds = &actUb;
     c.seed = seeds.counter++;
     c.device = 0;
@@ -1834,6 +1839,14 @@ struct VracerModule : SolverModule {
     std::vector<float> theta(n);
     check(kg_vracer_get_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
     sv["Training"]["Current Policy"]["Policy"] = std::vector<double>(theta.begin(), theta.end());
+    {  // agent.config:311-320 (per environment id)
+      float sig[8], sum[8];
+      check(kg_vracer_get_field(h, "reward_rescaling_sigma", sig, sizeof sig));
+      check(kg_vracer_get_field(h, "reward_rescaling_sum", sum, sizeof sum));
+      const size_t ne = std::min<size_t>(envIds, 8);
+      sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig, sig + ne);
+      sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum, sum + ne);
+    }
     Json &ds = description["Solver"];
     sv["Action Shifts"] = ds["Action Shifts"];
     sv["Action Scales"] = ds["Action Scales"];

@@ -16,7 +16,7 @@ from .native import KoraliDeviceError, check, lib
 _DTYPES = {
     "environment_id": np.int32, "termination": np.int32, "on_policy": np.int32, "episode_pos": np.int32,
     "env_steps": np.int32, "env_ids": np.int32, "finished_env": np.int32, "mini_batch": np.uint32,
-    "episode_id": np.int64, "env_u": np.float64, "env_sample_ids": np.uint64,
+    "episode_id": np.int64, "env_u": np.float64, "env_sample_ids": np.uint64, "reward_rescaling_count": np.int64,
 }
 
 
@@ -33,6 +33,7 @@ class _VracerCfg(C.Structure):
         ("l2_regularization_importance", C.c_double), ("initial_exploration_noise", C.POINTER(C.c_double)),
         ("seed", C.c_uint64), ("device", C.c_int), ("policy_distribution", C.c_int),
         ("action_lower_bounds", C.POINTER(C.c_double)), ("action_upper_bounds", C.POINTER(C.c_double)),
+        ("reward_rescaling", C.c_int),
     ]
 
 
@@ -84,7 +85,7 @@ class VracerDevice:
                  off_policy_target=0.1, off_policy_annealing_rate=0.0, off_policy_refer_beta=0.3,
                  l2_regularization_enabled=False, l2_regularization_importance=1e-4, initial_exploration_noise=1.0,
                  seed=0, device=0, hyperparameters=None, policy_distribution="Normal", action_lower_bound=-np.inf,
-                 action_upper_bound=np.inf):
+                 action_upper_bound=np.inf, reward_rescaling=False):
         L = _lib()
         self.S, self.A, self.H, self.L = state_size, action_size, hidden_size, hidden_layers
         self.E, self.B, self.O = environments, mini_batch_size, 1 + 2 * action_size
@@ -103,7 +104,7 @@ class VracerDevice:
                          off_policy_annealing_rate, off_policy_refer_beta, int(bool(l2_regularization_enabled)),
                          l2_regularization_importance, noise.ctypes.data_as(C.POINTER(C.c_double)), seed, device,
                          pol, self._lb.ctypes.data_as(C.POINTER(C.c_double)),
-                         self._ub.ctypes.data_as(C.POINTER(C.c_double)))
+                         self._ub.ctypes.data_as(C.POINTER(C.c_double)), int(bool(reward_rescaling)))
         h = C.c_void_p()
         check(L.kg_vracer_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -322,8 +322,11 @@ class Agent:
 
     def __init__(self, S, A, H=256, L=2, theta=None, *, max_size=4096, discount=0.995, learning_rate=1e-4,
                  iw_truncation=1.0, cutoff_scale=4.0, off_target=0.1, annealing_rate=0.0, refer_beta=0.3,
-                 initial_noise=1.0, l2_enabled=False, l2_importance=1e-4, bounds=None):
-        """bounds = None: Normal policy; (lb, ub) arrays: Clipped Normal."""
+                 initial_noise=1.0, l2_enabled=False, l2_importance=1e-4, bounds=None, reward_rescaling=False,
+                 env_count=8):
+        """bounds = None: Normal policy; (lb, ub) arrays: Clipped Normal.
+        reward_rescaling: Reward / Rescaling / Enabled (agent.cpp.base:96-98,
+        :423-437, :557-563; getScaledReward, agent.hpp:711-719)."""
         self.S, self.A, self.H, self.L = S, A, H, L
         self.bounds = None if bounds is None else (np.broadcast_to(np.asarray(bounds[0], f32), (A,)),
                                                    np.broadcast_to(np.asarray(bounds[1], f32), (A,)))
@@ -347,6 +350,13 @@ class Agent:
         self.current_episode = 0
         self.experience_count = 0
         self.er = {k: [] for k in self.FIELDS}
+        # per environment id: the sum of squared rewards and the experience
+        # count in the replay memory (kept whether or not rescaling is on, as
+        # the reference does), and the rescaling sigma (1.0 unless enabled)
+        self.reward_rescaling = bool(reward_rescaling)
+        self.rsum = np.zeros(env_count, f32)
+        self.rcnt = np.zeros(env_count, np.int64)
+        self.rsig = np.ones(env_count, f32)
 
     # ---- helpers
     def size(self):
@@ -362,8 +372,20 @@ class Agent:
         out, _ = forward(self.theta, np.atleast_2d(X), self.S, self.H, self.L, self.A, self.noise, self.shift())
         return out
 
+    def scaled_reward(self, i):
+        """getScaledReward (agent.hpp:711-719) of replay entry i: float division"""
+        return f32(self.er["reward"][i] / self.rsig[self.er["env"][i]])
+
     def _add(self, **kw):
+        # agent.cpp.base:423-437: the new reward's square in, then (memory
+        # full) the evicted one's out
+        r, env = f32(kw["reward"]), kw["env"]
+        self.rsum[env] = f32(self.rsum[env] + f32(r * r))
+        self.rcnt[env] += 1
         if self.size() == self.max_size:
+            ev, rv = self.er["env"][0], f32(self.er["reward"][0])
+            self.rsum[ev] = f32(self.rsum[ev] - f32(rv * rv))
+            self.rcnt[ev] -= 1
             if not self.er["onp"][0]:
                 self.off_count -= 1
             for k in self.FIELDS:
@@ -393,8 +415,12 @@ class Agent:
         # single experience); every other entry keeps the 0.0 placeholder
         # until a mini-batch retrace chain reaches it.  Reproduced as is.
         for e in range(end, max(end - 2, -1), -1):
-            ret = f32(f32(self.gamma * ret) + self.er["reward"][e])
+            ret = f32(f32(self.gamma * ret) + self.scaled_reward(e))
             self.er["ret"][e] = ret
+        if self.reward_rescaling:  # agent.cpp.base:557-563 (float sums, double quotient and sqrt)
+            for i in range(self.rsig.size):
+                q = np.float64(self.rsum[i]) / (np.float64(np.float32(self.rcnt[i])) + 1e-9)
+                self.rsig[i] = f32(np.sqrt(q) + 1e-9)
         self.current_episode += 1
         self.experience_count += n
 
@@ -448,7 +474,7 @@ class Agent:
                 ret = er["ret"][end + 1]
             for c in range(end, start - 1, -1):
                 v = er["v"][c]
-                ret = f32(v + f32(er["tiw"][c] * f32(f32(er["reward"][c] + f32(self.gamma * ret)) - v)))
+                ret = f32(v + f32(er["tiw"][c] * f32(f32(self.scaled_reward(c) + f32(self.gamma * ret)) - v)))
                 er["ret"][c] = ret
         # calculatePolicyGradients (VRACER.cpp.base:89-181)
         G = np.zeros((B, 1 + 2 * A), f32)
@@ -456,7 +482,7 @@ class Agent:
             V, cur, old = er["v"][e], er["cur_pol"][e], er["exp_pol"][e]
             G[b, 0] = f32(er["ret"][e] - V)
             if er["onp"][e]:
-                q = er["reward"][e]
+                q = self.scaled_reward(e)
                 if er["term"][e] == NON_TERMINAL:
                     q = f32(q + f32(self.gamma * er["ret"][e + 1]))
                 if er["term"][e] == TRUNCATED:

@@ -127,18 +127,22 @@ def test_policy_updates_match_oracle(H, L, B, clipped):
         assert np.isclose(d.scalar("off_policy_cutoff"), float(ag.cutoff), rtol=1e-7)
 
 
-@pytest.mark.parametrize("clipped,R,T", [(False, 700, 40), (True, 700, 40), (False, 40, 5)])
-def test_environment_steps_match_oracle(clipped, R, T):
+@pytest.mark.parametrize("clipped,R,T,rr", [(False, 700, 40, False), (True, 700, 40, False), (False, 40, 5, False),
+                                           (False, 700, 40, True), (False, 40, 5, True)])
+def test_environment_steps_match_oracle(clipped, R, T, rr):
     """Concurrent CartPole environments with the same action noise: episodes,
     terminations, the replay memory in processEpisode order, initial retrace
     values, relaunch sample ids — 120 steps, eviction included; (R=40, T=5):
-    one step appends more experiences than the replay memory holds."""
+    one step appends more experiences than the replay memory holds.  rr:
+    Reward Rescaling (the per-environment sums, counts and sigmas in
+    processEpisode order, bit for bit, and the scaled initial retrace)."""
     H, L, E = 64, 2, 16
     th = theta_for(H, L, 4, spread=0.6)
-    ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None)
+    ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None, reward_rescaling=rr)
     ro = V.Rollouts(ag, E, max_steps=T)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=32, replay_maximum_size=R,
-               replay_start_size=R, max_episode_steps=T, hyperparameters=th, seed=4, **clip_kw(clipped))
+               replay_start_size=R, max_episode_steps=T, hyperparameters=th, seed=4, reward_rescaling=rr,
+               **clip_kw(clipped))
     rng = np.random.default_rng(5)
     total = 0
     for s in range(120):
@@ -165,24 +169,32 @@ def test_environment_steps_match_oracle(clipped, R, T):
     close(d.get("retrace")[order], np.array(er["ret"], f32), 1e-5, 1e-5)
     close(d.get("truncated_state").reshape(R, S)[order], np.stack(er["tstate"]), 1e-5, 1e-6)
     assert np.array_equal(d.get("env_sample_ids"), np.array(ro.sample, np.uint64))
+    if rr:
+        assert np.array_equal(d.get("reward_rescaling_count")[:3], ag.rcnt[:3])
+        assert np.array_equal(d.get("reward_rescaling_sum")[:3], ag.rsum[:3])
+        assert np.array_equal(d.get("reward_rescaling_sigma")[:3], ag.rsig[:3])
+        assert np.all(ag.rsig[:3] != 1.0)
     # actions differ in the last float32 bits (reassociated MFMA sums), so do
     # the fp64 states: round 2 measured at most 3.8e-8 after 30 steps
     close(d.get("env_u").reshape(E, 4), np.stack([c.u for c in ro.carts]), 1e-6, 2e-7)
 
 
-def test_training_loop_matches_oracle_end_to_end():
+@pytest.mark.parametrize("rr", [False, True])
+def test_training_loop_matches_oracle_end_to_end(rr):
     """kg_vracer_training_step with the device's own streams (action noise,
     mini-batch uniforms; the oracle draws the same philox blocks) — the
     body of Agent::trainingGeneration: environment step, then as many updates
-    as Experiences Between Policy Updates allows once the start size is reached."""
+    as Experiences Between Policy Updates allows once the start size is
+    reached.  rr: Reward Rescaling (scaled rewards in the retrace chains and
+    the policy gradient's Qret)."""
     H, L, E, R, B = 64, 2, 8, 400, 32
     th = theta_for(H, L, 6)
     seed = 77
-    ag = V.Agent(S, A, H, L, th, max_size=R)
+    ag = V.Agent(S, A, H, L, th, max_size=R, reward_rescaling=rr)
     ro = V.Rollouts(ag, E, max_steps=30)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=B, replay_maximum_size=R,
                replay_start_size=150, max_episode_steps=30, experiences_between_policy_updates=4.0,
-               hyperparameters=th, seed=seed)
+               hyperparameters=th, seed=seed, reward_rescaling=rr)
     session_exp, updates, mb_ctr = 0, 0, 0
     for s in range(70):
         new_ref, _ = ro.step(V.action_noise(seed, s, E, A))
@@ -201,6 +213,8 @@ def test_training_loop_matches_oracle_end_to_end():
     assert updates > 10
     close(d.hyperparameters, ag.theta, 1e-3, 1e-5)
     assert d.scalar("policy_update_count") == ag.update_count
+    if rr:
+        assert np.array_equal(d.get("reward_rescaling_sigma")[:3], ag.rsig[:3])
 
 
 def test_c5_shape_runs():
