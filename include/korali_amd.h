@@ -391,6 +391,7 @@ typedef struct {
   int policy_distribution;                 /* Policy / Distribution: 0 Normal, 1 Clipped Normal */
   const double *action_lower_bounds, *action_upper_bounds;  /* action_size values (may be NULL for Normal) */
   int reward_rescaling;                    /* Reward / Rescaling / Enabled (environment_count <= 8) */
+  int state_rescaling;                     /* State Rescaling / Enabled (state_size <= 8) */
 } kg_vracer_config;
 
 int kg_vracer_create(const kg_vracer_config *cfg, kg_vracer_t *out);
@@ -406,6 +407,11 @@ int kg_vracer_run_policy(kg_vracer_t h, const float *states, size_t n, float *ou
  * environment step's actions instead of the device stream (testing). */
 int kg_vracer_set_action_noise(kg_vracer_t h, const float *noise, size_t n);
 int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences);
+/* Agent::rescaleStates (agent.cpp.base:291-322): the replay memory's state
+ * moments, every stored state rescaled; episodes launched from then on
+ * scale their states with them.  kg_vracer_training_step calls it where the
+ * reference does (agent.cpp.base:204-207). */
+int kg_vracer_rescale_states(kg_vracer_t h);
 int kg_vracer_train_policy(kg_vracer_t h, size_t updates);
 int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *sorted_ids, size_t count);
 int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates);

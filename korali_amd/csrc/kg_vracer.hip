@@ -44,6 +44,7 @@ constexpr int MAXA = 4;  // action dimensions supported by the device kernels
 constexpr int MAXO = 1 + 2 * MAXA;
 constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
 constexpr int MAXENV = 8;   // environment ids with reward rescaling (Problem / Environment Count)
+constexpr int MAXS = 8;     // state dimensions with state rescaling
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
 enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u, ERR_ENV_ODE = 8u };
 
@@ -65,6 +66,9 @@ struct State {
   float rsig[MAXENV];             // getScaledReward's sigma (1.0 unless enabled)
   float rsum[MAXENV];             // sum of squared rewards in the replay memory
   long long rcnt[MAXENV];         // experiences in the replay memory
+  // state rescaling (agent.cpp.base:92-94, :291-322): the moments episodes
+  // launched from now on scale their states with (identity until set)
+  float smean[MAXS], ssdev[MAXS];
 };
 
 struct Params {  // launch-constant configuration
@@ -78,6 +82,7 @@ struct Params {  // launch-constant configuration
   int clipped;                    // Policy Distribution: 0 Normal, 1 Clipped Normal
   float lb[MAXA], ub[MAXA];       // action bounds (Variables' Lower / Upper Bound)
   int rr;                         // Reward / Rescaling / Enabled
+  int srs;                        // State Rescaling / Enabled
 };
 
 // ---------------------------------------------------------------- philox
@@ -1032,15 +1037,25 @@ struct Envs {
   float *rewards;     // cumulative rewards of the episodes finished by the last step (by rank)
   float *sigb;        // rank x MAXENV: the rescaling sigmas before that episode (reward rescaling)
   int *fin_id;        // environment id of the finished episode of each rank
+  float *pm, *ps;     // E x S: the state-rescaling moments the running episode was launched with
 };
+// requestNewPolicy's normalisation (reinforcementLearning.cpp.base:361-370)
+// of environment e's state component k
+__device__ __forceinline__ float vr_scale_state(const Params &P, const Envs &ev, int e, int k, double y) {
+  const float x = (float)y;
+  return P.srs ? (x - ev.pm[e * P.S + k]) / ev.ps[e * P.S + k] : x;
+}
 
-__global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long sample0, const int *only_fin) {
+__global__ void k_vr_env_reset(Params P, const State *st, Envs ev, float *X, unsigned long long sample0,
+                               const int *only_fin) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P.E) return;
   const unsigned long long sid = sample0 + e;
   double u[4];
   cp_reset((unsigned)(sid * 1024ull + sid), u);
-  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = u[k], X[e * 4 + k] = (float)u[k];
+  if (P.srs)
+    for (int k = 0; k < P.S; k++) ev.pm[e * P.S + k] = st->smean[k], ev.ps[e * P.S + k] = st->ssdev[k];
+  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = u[k], X[e * 4 + k] = vr_scale_state(P, ev, e, k, u[k]);
   ev.time[e] = 0.0;
   ev.t[e] = 0;
   ev.sample[e] = sid;
@@ -1056,21 +1071,26 @@ __global__ void k_vr_env_reset(Params P, Envs ev, float *X, unsigned long long s
 // continuous.cpp.base:219-260: the Normal mean; Clipped Normal: the mean
 // clipped to the bounds), and adds the reward of environment 0 (env.py:
 // testing runs environment 0) until the pole falls or max_episode_steps.
-__global__ void k_vr_test_reset(int n, int S, const unsigned long long *__restrict__ sid,
+// (testing agents take the agent's State Rescaling moments, agent.cpp.base:279-280)
+__device__ __forceinline__ float vr_test_state(const Params &P, const State *st, int k, double y) {
+  const float x = (float)y;
+  return P.srs ? (x - st->smean[k]) / st->ssdev[k] : x;
+}
+__global__ void k_vr_test_reset(Params P, const State *st, int n, int S, const unsigned long long *__restrict__ sid,
                                 const unsigned long long *__restrict__ lid, double *u, double *tm, int *steps,
                                 int *done, float *cum, float *X) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   double y[4];
   cp_reset((unsigned)(sid[e] * 1024ull + lid[e]), y);
-  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * S + k] = (float)y[k];
+  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * S + k] = vr_test_state(P, st, k, y[k]);
   tm[e] = 0.0;
   steps[e] = 0;
   done[e] = 0;
   cum[e] = 0.f;
 }
-__global__ void k_vr_test_act(Params P, int n, const float *__restrict__ out, double *u, double *tm, int *steps,
-                              int *done, float *cum, float *X, unsigned *errors, int *running) {
+__global__ void k_vr_test_act(Params P, const State *st, int n, const float *__restrict__ out, double *u, double *tm,
+                              int *steps, int *done, float *cum, float *X, unsigned *errors, int *running) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n || done[e]) return;
   float act = out[(long long)e * P.O + 1];  // the mode (A = 1: the CartPole kernel)
@@ -1085,12 +1105,12 @@ __global__ void k_vr_test_act(Params P, int n, const float *__restrict__ out, do
   if (!cp_advance(y, t, (double)act)) atomicOr(errors, (unsigned)ERR_ENV_ODE);
   tm[e] = t;
 #pragma unroll
-  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * P.S + k] = (float)y[k];
+  for (int k = 0; k < 4; k++) u[e * 4 + k] = y[k], X[e * P.S + k] = vr_test_state(P, st, k, y[k]);
   const bool failed = cp_failed(y);
   cum[e] += (float)(1.0 - 1.0 * (failed ? 1.0 : 0.0));
-  const int st = steps[e] + 1;
-  steps[e] = st;
-  if (failed || st >= P.T) done[e] = 1;
+  const int ns = steps[e] + 1;
+  steps[e] = ns;
+  if (failed || ns >= P.T) done[e] = 1;
   else atomicAdd(running, 1);
 }
 
@@ -1132,7 +1152,7 @@ __global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restri
   if (!cp_advance(y, tm, (double)act[0])) atomicOr(&st->errors, (unsigned)ERR_ENV_ODE);
   ev.time[e] = tm;
 #pragma unroll
-  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = y[k], X[e * 4 + k] = (float)y[k];
+  for (int k = 0; k < 4; k++) ev.u[e * 4 + k] = y[k], X[e * 4 + k] = vr_scale_state(P, ev, e, k, y[k]);
   const bool failed = cp_failed(y);
   const double r = 1.0 - 1.0 * (failed ? 1.0 : 0.0);
   const int vid = ev.env_id[e] % 3;
@@ -1345,7 +1365,9 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     const unsigned long long sid = sid0 + (unsigned long long)rank + (unsigned long long)P.E;
     double u[4];
     cp_reset((unsigned)(sid * 1024ull + sid), u);
-    for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = (float)u[q];
+    if (P.srs)  // the relaunched episode runs with the current moments (agent.cpp.base:186-187)
+      for (int q = 0; q < S; q++) ev.pm[e * S + q] = st->smean[q], ev.ps[e * S + q] = st->ssdev[q];
+    for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = vr_scale_state(P, ev, e, q, u[q]);
     ev.time[e] = 0.0;
     ev.t[e] = 0;
     ev.sample[e] = sid;
@@ -1354,11 +1376,57 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
   }
 }
 
+// rescaleStates (agent.cpp.base:291-322): one lane per state dimension adds
+// the replay memory's states in order (float, the reference's sums), the
+// moments go to the agent state; then every stored state is rescaled (the
+// truncated states are not, as in the reference) and the environments
+// relaunched by the last step, which have not acted yet, take the new
+// moments (the reference relaunches them at the top of the next loop
+// iteration, after this rescaling)
+__global__ void k_vr_srs_moments(Params P, State *st, Replay er) {
+  const int d = threadIdx.x;
+  if (blockIdx.x || d >= P.S) return;
+  const unsigned long long n = st->size, R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+  float sum = 0.0f, sq = 0.0f;
+  for (unsigned long long i = 0; i < n; i++) {
+    unsigned long long q = base + i;
+    if (q >= R) q -= R;
+    const float x = er.st[q * P.S + d];
+    sum += x;
+    sq += x * x;
+  }
+  float m = sum / (float)n;
+  if (!isfinite(m)) m = 0.0f;
+  float sg = sqrtf(sq / (float)n - m * m);
+  if (!isfinite(sg)) sg = 1.0f;
+  if (sg <= 1e-9) sg = 1.0f;
+  st->smean[d] = m;
+  st->ssdev[d] = sg;
+}
+__global__ void k_vr_srs_apply(Params P, const State *st, Replay er, Envs ev, float *X) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)st->size * P.S;
+  if (i < n) {
+    const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+    unsigned long long q = base + (unsigned long long)(i / P.S);
+    if (q >= R) q -= R;
+    const int d = (int)(i % P.S);
+    float *x = er.st + q * P.S + d;
+    *x = (*x - st->smean[d]) / st->ssdev[d];
+  }
+  if (i < (long long)P.E && ev.t[i] == 0) {
+    const int e = (int)i;
+    for (int k = 0; k < P.S; k++) ev.pm[e * P.S + k] = st->smean[k], ev.ps[e * P.S + k] = st->ssdev[k];
+    for (int k = 0; k < 4; k++) X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, ev.u[e * 4 + k]);
+  }
+}
+
 __global__ void k_vr_init_state(State *st, float lr, float beta, float cutoff) {
   if (threadIdx.x || blockIdx.x) return;
   State s = {};
   s.lr = lr, s.beta = beta, s.cutoff = cutoff, s.eta = lr, s.b1p = 1.0f, s.b2p = 1.0f;
   for (int i = 0; i < MAXENV; i++) s.rsig[i] = 1.0f;
+  for (int i = 0; i < MAXS; i++) s.smean[i] = 0.0f, s.ssdev[i] = 1.0f;
   *st = s;
 }
 
@@ -1635,6 +1703,8 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"reward_rescaling_sigma", &h->st->rsig[0], 4, (size_t)MAXENV},
       {"reward_rescaling_sum", &h->st->rsum[0], 4, (size_t)MAXENV},
       {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
+      {"state_rescaling_means", &h->st->smean[0], 4, (size_t)P.S},
+      {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)P.S},
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {
@@ -1682,6 +1752,8 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.R = (long long)c->replay_maximum_size;
   P.env_count = (int)c->environment_count;
   P.rr = c->reward_rescaling ? 1 : 0;
+  P.srs = c->state_rescaling ? 1 : 0;
+  KG_CHECK(!P.srs || c->state_size <= (size_t)MAXS, "vracer: State Rescaling on the device supports up to 8 state variables");
   KG_CHECK(!P.rr || (c->environment_count >= 1 && c->environment_count <= (size_t)MAXENV),
            "vracer: Reward Rescaling on the device supports Environment Count 1..8");
   P.l2 = c->l2_regularization_enabled ? 1 : 0;
@@ -1765,6 +1837,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(ev.eb_st, ET * P.S * 4), alloc(ev.eb_act, ET * P.A * 4), alloc(ev.eb_pol, ET * 2 * P.A * 4);
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
   alloc(ev.sigb, E * MAXENV * 4), alloc(ev.fin_id, E * 4);
+  alloc(ev.pm, (size_t)E * P.S * 4), alloc(ev.ps, (size_t)E * P.S * 4);
   if (!rc && hipHostMalloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
     kg::set_error("vracer: hipHostMalloc failed");
     rc = 1;
@@ -1777,8 +1850,8 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   hipLaunchKernelGGL(k_vr_init_state, dim3(1), dim3(1), 0, h->stream, h->st, P.lr0, (float)c->off_policy_refer_beta,
                      P.cutoff_scale);
   // the first launch of every environment: sample ids 0 .. E-1
-  hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->ev, h->X, 0ull,
-                     (const int *)nullptr);
+  hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, (const State *)h->st,
+                     h->ev, h->X, 0ull, (const int *)nullptr);
   if (hipGetLastError() != hipSuccess || vr_read_state(h)) {
     if (!*kg::last_error()) kg::set_error("vracer: initial launches failed");
     kg_vracer_destroy(h);
@@ -1841,7 +1914,8 @@ int kg_vracer_destroy(kg_vracer_t h) {
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
                   h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,
                   h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
-                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id};
+                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id,
+                  h->ev.pm, h->ev.ps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->st_host) (void)hipHostFree(h->st_host);
@@ -1993,16 +2067,16 @@ int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uin
         fail(hipMemcpyAsync(dlid, launch_ids + b0, m * 8, hipMemcpyHostToDevice, h->stream)) ||
         fail(hipMemsetAsync(errs, 0, 4, h->stream)))
       break;
-    hipLaunchKernelGGL(k_vr_test_reset, grid, dim3(256), 0, h->stream, m, h->P.S, dsid, dlid, u, tm, steps, done,
-                       cum, h->Xs);
+    hipLaunchKernelGGL(k_vr_test_reset, grid, dim3(256), 0, h->stream, h->P, (const State *)h->st, m, h->P.S, dsid,
+                       dlid, u, tm, steps, done, cum, h->Xs);
     for (int t = 0; t < h->P.T; t++) {
       if (vr_forward(h, h->Xs, m, h->out)) {
         rc = 1, named = true;
         break;
       }
       if (t % 16 == 0 && fail(hipMemsetAsync(running, 0, 4, h->stream))) break;
-      hipLaunchKernelGGL(k_vr_test_act, grid, dim3(256), 0, h->stream, h->P, m, (const float *)h->out, u, tm, steps,
-                         done, cum, h->Xs, errs, running);
+      hipLaunchKernelGGL(k_vr_test_act, grid, dim3(256), 0, h->stream, h->P, (const State *)h->st, m,
+                         (const float *)h->out, u, tm, steps, done, cum, h->Xs, errs, running);
       if (t % 16 == 15) {  // every 16 steps: stop once every episode has ended
         int r = 0;
         if (fail(hipMemcpyAsync(&r, running, 4, hipMemcpyDeviceToHost, h->stream)) ||
@@ -2063,6 +2137,19 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
   return 0;
 }
 
+int kg_vracer_rescale_states(kg_vracer_t h) {
+  KG_CHECK(h, "vracer: null argument");
+  const Params &P = h->P;
+  KG_CHECK(P.srs, "vracer: State Rescaling is not enabled for this agent");
+  KG_CHECK(h->st_host->size > 0, "vracer: State Rescaling needs experiences in the replay memory");
+  hipLaunchKernelGGL(k_vr_srs_moments, dim3(1), dim3(64), 0, h->stream, P, h->st, h->er);
+  const long long n = std::max<long long>((long long)h->st_host->size * P.S, P.E);
+  hipLaunchKernelGGL(k_vr_srs_apply, dim3(vr_blocks(n, 256)), dim3(256), 0, h->stream, P, (const State *)h->st, h->er,
+                     h->ev, h->X);
+  KG_HIP(hipGetLastError());
+  return vr_read_state(h);
+}
+
 int kg_vracer_train_policy(kg_vracer_t h, size_t updates) {
   KG_CHECK(h, "vracer: null argument");
   for (size_t u = 0; u < updates; u++)
@@ -2088,8 +2175,10 @@ int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *upda
   if (kg_vracer_environment_step(h, &added)) return 1;
   size_t n = 0;
   // Agent::trainingGeneration (agent.cpp.base:201-231)
-  if (h->st_host->experience_count >= h->start_size)
+  if (h->st_host->experience_count >= h->start_size) {
+    if (h->P.srs && h->st_host->update_count == 0 && kg_vracer_rescale_states(h)) return 1;
     while ((double)h->session_experiences > h->ebpu * (double)(h->session_updates + n) + (double)h->until_start) n++;
+  }
   if (n && kg_vracer_train_policy(h, n)) return 1;
   if (new_experiences) *new_experiences = added;
   if (updates) *updates = n;

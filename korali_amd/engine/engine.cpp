@@ -1670,7 +1670,7 @@ struct VracerModule : SolverModule {
       fail("Provided bounds (%f, %f) for the action variable are non-finite, but the distribution (%s) is bounded.\n",
            actLb, actUb, sv["Policy"]["Distribution"].getString().c_str());
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
-    if (flag(sv["State Rescaling"], "Enabled", false)) fail("State Rescaling is not supported by the device path.");
+    const bool stateRescaling = flag(sv["State Rescaling"], "Enabled", false);
     const bool rewardRescaling = flag(sv["Reward"]["Rescaling"], "Enabled", false);
     if (rewardRescaling && (envCount < 1 || envCount > 8))
       fail("Reward Rescaling on the device supports an 'Environment Count' of 1 to 8 (%llu given).", envCount);
@@ -1723,6 +1723,7 @@ struct VracerModule : SolverModule {
     c.initial_exploration_noise = &noise;
     c.policy_distribution = dist == "clippednormal" ? 1 : 0;
     c.reward_rescaling = rewardRescaling ? 1 : 0;
+    c.state_rescaling = stateRescaling ? 1 : 0;
     c.action_lower_bounds = &actLb, c.action_upper_bounds = &actUb;
     c.seed = seeds.counter++;
     c.device = 0;
@@ -1846,6 +1847,11 @@ struct VracerModule : SolverModule {
       const size_t ne = std::min<size_t>(envIds, 8);
       sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig, sig + ne);
       sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum, sum + ne);
+      float sm[8], ss[8];  // agent.config:326-335 (the CartPole kernel: 4 state variables)
+      check(kg_vracer_get_field(h, "state_rescaling_means", sm, 4 * sizeof(float)));
+      check(kg_vracer_get_field(h, "state_rescaling_sigmas", ss, 4 * sizeof(float)));
+      sv["State Rescaling"]["Means"] = std::vector<double>(sm, sm + 4);
+      sv["State Rescaling"]["Sigmas"] = std::vector<double>(ss, ss + 4);
     }
     Json &ds = description["Solver"];
     sv["Action Shifts"] = ds["Action Shifts"];

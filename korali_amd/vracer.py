@@ -33,7 +33,7 @@ class _VracerCfg(C.Structure):
         ("l2_regularization_importance", C.c_double), ("initial_exploration_noise", C.POINTER(C.c_double)),
         ("seed", C.c_uint64), ("device", C.c_int), ("policy_distribution", C.c_int),
         ("action_lower_bounds", C.POINTER(C.c_double)), ("action_upper_bounds", C.POINTER(C.c_double)),
-        ("reward_rescaling", C.c_int),
+        ("reward_rescaling", C.c_int), ("state_rescaling", C.c_int),
     ]
 
 
@@ -61,6 +61,7 @@ def _lib():
         L.kg_vracer_train_policy.argtypes = [vp, sz]
         L.kg_vracer_train_policy_minibatch.argtypes = [vp, C.POINTER(C.c_uint32), sz]
         L.kg_vracer_training_step.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
+        L.kg_vracer_rescale_states.argtypes = [vp]
         u64p = C.POINTER(C.c_uint64)
         L.kg_vracer_test_episodes.argtypes = [vp, u64p, u64p, sz, fp]
         L.kg_vracer_stream.argtypes = [vp, C.POINTER(vp)]
@@ -85,7 +86,7 @@ class VracerDevice:
                  off_policy_target=0.1, off_policy_annealing_rate=0.0, off_policy_refer_beta=0.3,
                  l2_regularization_enabled=False, l2_regularization_importance=1e-4, initial_exploration_noise=1.0,
                  seed=0, device=0, hyperparameters=None, policy_distribution="Normal", action_lower_bound=-np.inf,
-                 action_upper_bound=np.inf, reward_rescaling=False):
+                 action_upper_bound=np.inf, reward_rescaling=False, state_rescaling=False):
         L = _lib()
         self.S, self.A, self.H, self.L = state_size, action_size, hidden_size, hidden_layers
         self.E, self.B, self.O = environments, mini_batch_size, 1 + 2 * action_size
@@ -104,7 +105,8 @@ class VracerDevice:
                          off_policy_annealing_rate, off_policy_refer_beta, int(bool(l2_regularization_enabled)),
                          l2_regularization_importance, noise.ctypes.data_as(C.POINTER(C.c_double)), seed, device,
                          pol, self._lb.ctypes.data_as(C.POINTER(C.c_double)),
-                         self._ub.ctypes.data_as(C.POINTER(C.c_double)), int(bool(reward_rescaling)))
+                         self._ub.ctypes.data_as(C.POINTER(C.c_double)), int(bool(reward_rescaling)),
+                         int(bool(state_rescaling)))
         h = C.c_void_p()
         check(L.kg_vracer_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -175,6 +177,10 @@ class VracerDevice:
         n, u = C.c_size_t(), C.c_size_t()
         check(_lib().kg_vracer_training_step(self._h, C.byref(n), C.byref(u)))
         return n.value, u.value
+
+    def rescale_states(self):
+        """Agent::rescaleStates (training_step calls it where the reference does)"""
+        check(_lib().kg_vracer_rescale_states(self._h))
 
     def test_episodes(self, sample_ids, launch_ids=None):
         """Testing episodes (Agent::testingGeneration): the cumulative reward of

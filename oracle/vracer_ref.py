@@ -323,7 +323,7 @@ class Agent:
     def __init__(self, S, A, H=256, L=2, theta=None, *, max_size=4096, discount=0.995, learning_rate=1e-4,
                  iw_truncation=1.0, cutoff_scale=4.0, off_target=0.1, annealing_rate=0.0, refer_beta=0.3,
                  initial_noise=1.0, l2_enabled=False, l2_importance=1e-4, bounds=None, reward_rescaling=False,
-                 env_count=8):
+                 env_count=8, state_rescaling=False):
         """bounds = None: Normal policy; (lb, ub) arrays: Clipped Normal.
         reward_rescaling: Reward / Rescaling / Enabled (agent.cpp.base:96-98,
         :423-437, :557-563; getScaledReward, agent.hpp:711-719)."""
@@ -357,6 +357,11 @@ class Agent:
         self.rsum = np.zeros(env_count, f32)
         self.rcnt = np.zeros(env_count, np.int64)
         self.rsig = np.ones(env_count, f32)
+        # State Rescaling (agent.cpp.base:92-94, :204-207, :291-322): the
+        # moments the environments scale their states with (identity until set)
+        self.state_rescaling = bool(state_rescaling)
+        self.smean = np.zeros(S, f32)
+        self.ssdev = np.ones(S, f32)
 
     # ---- helpers
     def size(self):
@@ -423,6 +428,40 @@ class Agent:
                 self.rsig[i] = f32(np.sqrt(q) + 1e-9)
         self.current_episode += 1
         self.experience_count += n
+
+    def rescale_states(self):
+        """rescaleStates (agent.cpp.base:291-322): float sums over the replay
+        memory in order, the moments, then every stored state rescaled (the
+        truncated states are not)"""
+        st = self.er["state"]
+        ssum = np.zeros(self.S, f32)
+        ssq = np.zeros(self.S, f32)
+        for x in st:
+            for d in range(self.S):
+                ssum[d] = f32(ssum[d] + x[d])
+                ssq[d] = f32(ssq[d] + f32(x[d] * x[d]))
+        n = f32(len(st))
+        with np.errstate(all="ignore"):
+            for d in range(self.S):
+                m = f32(ssum[d] / n)
+                if not np.isfinite(m):
+                    m = f32(0.0)
+                sg = f32(np.sqrt(f32(f32(ssq[d] / n) - f32(m * m))))
+                if not np.isfinite(sg):
+                    sg = f32(1.0)
+                if sg <= 1e-9:
+                    sg = f32(1.0)
+                self.smean[d], self.ssdev[d] = m, sg
+        for i in range(len(st)):
+            st[i] = ((st[i] - self.smean) / self.ssdev).astype(f32)
+
+    def maybe_rescale_states(self, start_size):
+        """agent.cpp.base:201-207: at the training loop, once the start size is
+        reached and before the first policy update (every time until then)"""
+        if self.state_rescaling and self.experience_count >= start_size and self.update_count == 0:
+            self.rescale_states()
+            return True
+        return False
 
     def minibatch_ids(self, uniforms):
         """generateMiniBatch (agent.cpp.base:574-597) for given uniforms."""
@@ -756,15 +795,31 @@ class Rollouts:
     def _launch(self, e, sid):
         self.carts[e].reset(sid * 1024 + sid)
         self.sample[e] = sid
+        # the State Rescaling moments the episode runs with (agent.cpp.base:186-187)
+        self.pm = getattr(self, "pm", [None] * self.E)
+        self.ps = getattr(self, "ps", [None] * self.E)
+        self.pm[e], self.ps[e] = self.agent.smean.copy(), self.agent.ssdev.copy()
         self.buf = getattr(self, "buf", [None] * self.E)
         self.buf[e] = dict(states=[], actions=[], rewards=[], pols=[], vals=[], cum=f32(0.0))
 
     def env_id(self, e):
         return self.sample[e] % self.env_count
 
+    def scaled_state(self, e, u):
+        """requestNewPolicy's normalisation (reinforcementLearning.cpp.base:361-370)"""
+        return ((u.astype(f32) - self.pm[e]) / self.ps[e]).astype(f32)
+
+    def relaunched_take_moments(self):
+        """the reference relaunches finished agents at the top of the next loop
+        iteration, after a rescaling in this one: environments that have not
+        acted since their relaunch take the current moments"""
+        for e, c in enumerate(self.carts):
+            if c.step == 0:
+                self.pm[e], self.ps[e] = self.agent.smean.copy(), self.agent.ssdev.copy()
+
     def step(self, noise):
         A, ag = self.agent.A, self.agent
-        X = np.stack([c.u.astype(f32) for c in self.carts])
+        X = np.stack([self.scaled_state(e, c.u) for e, c in enumerate(self.carts)])
         out = ag.policy(X)
         finished = []
         for e, cart in enumerate(self.carts):
@@ -788,7 +843,7 @@ class Rollouts:
         for e, term in finished:
             b = self.buf[e]
             ag.process_episode(self.env_id(e), b["states"], b["actions"], b["rewards"], b["pols"], b["vals"], term,
-                               tstate=self.carts[e].u.astype(f32))
+                               tstate=self.scaled_state(e, self.carts[e].u))
             new += len(b["rewards"])
             rewards.append(b["cum"])
         for e, _ in finished:

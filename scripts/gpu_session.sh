@@ -36,6 +36,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     nmab) step nm_sym0 300 env KORALI_AMD_NM_SYM=0 python tools/nm_probe.py 8192 && step nm_sym1 300 env KORALI_AMD_NM_SYM=1 python tools/nm_probe.py 8192 ;;
     pmc5g) step pmc5gf 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex "k_vr_gemm" -d "$OUT/pmc5_fetch" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline && step pmc5gw 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex "k_vr_gemm" -d "$OUT/pmc5_write" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     ub) step ub 120 ./tools/ubench_chains ;;
+    c3t) step c3t 600 python -u -m pytest tests/test_gpu_baseline_shapes.py -x -v --timeout 150 --timeout-method thread -k "tmcmc" ;;
+    vr) step vr 600 python -u -m pytest tests/test_gpu_vracer.py tests/test_gpu_engine.py -x -q --timeout 150 --timeout-method thread -k "vracer or VRACER" ;;
     pmc3) step pmc3f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc3_fetch" -o run --output-format csv -- python bench.py --workload c3 --steps 10 --warmup 2 --no-cpu-baseline && step pmc3w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc3_write" -o run --output-format csv -- python bench.py --workload c3 --steps 10 --warmup 2 --no-cpu-baseline && python tools/pmc_summary.py "$OUT/pmc3_fetch" "$OUT/pmc3_write" > "$OUT/c3_pmc_traffic.csv" && rm -rf "$OUT/pmc3_fetch" "$OUT/pmc3_write" ;;
     prof3) step prof3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python bench.py --workload c3 --steps 10 --warmup 2 --no-cpu-baseline ;;
     prof5) step prof5 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof5" -o run --output-format csv -- python bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline && rm -f "$OUT"/prof5/run_kernel_trace.csv ;;

@@ -179,28 +179,33 @@ def test_environment_steps_match_oracle(clipped, R, T, rr):
     close(d.get("env_u").reshape(E, 4), np.stack([c.u for c in ro.carts]), 1e-6, 2e-7)
 
 
-@pytest.mark.parametrize("rr", [False, True])
-def test_training_loop_matches_oracle_end_to_end(rr):
+@pytest.mark.parametrize("rr,srs", [(False, False), (True, False), (False, True), (True, True)])
+def test_training_loop_matches_oracle_end_to_end(rr, srs):
     """kg_vracer_training_step with the device's own streams (action noise,
     mini-batch uniforms; the oracle draws the same philox blocks) — the
     body of Agent::trainingGeneration: environment step, then as many updates
     as Experiences Between Policy Updates allows once the start size is
     reached.  rr: Reward Rescaling (scaled rewards in the retrace chains and
-    the policy gradient's Qret)."""
+    the policy gradient's Qret); srs: State Rescaling (the replay memory's
+    moments at the start size, every stored state rescaled, episodes launched
+    from then on scaling their states)."""
     H, L, E, R, B = 64, 2, 8, 400, 32
     th = theta_for(H, L, 6)
     seed = 77
-    ag = V.Agent(S, A, H, L, th, max_size=R, reward_rescaling=rr)
+    ag = V.Agent(S, A, H, L, th, max_size=R, reward_rescaling=rr, state_rescaling=srs)
     ro = V.Rollouts(ag, E, max_steps=30)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=B, replay_maximum_size=R,
                replay_start_size=150, max_episode_steps=30, experiences_between_policy_updates=4.0,
-               hyperparameters=th, seed=seed, reward_rescaling=rr)
-    session_exp, updates, mb_ctr = 0, 0, 0
+               hyperparameters=th, seed=seed, reward_rescaling=rr, state_rescaling=srs)
+    session_exp, updates, mb_ctr, rescaled = 0, 0, 0, 0
     for s in range(70):
         new_ref, _ = ro.step(V.action_noise(seed, s, E, A))
         session_exp += new_ref
         n = 0
         if ag.experience_count >= 150:
+            if ag.maybe_rescale_states(150):
+                ro.relaunched_take_moments()
+                rescaled += 1
             while session_exp > 4.0 * (updates + n) + 150:
                 n += 1
         for _ in range(n):
@@ -215,6 +220,15 @@ def test_training_loop_matches_oracle_end_to_end(rr):
     assert d.scalar("policy_update_count") == ag.update_count
     if rr:
         assert np.array_equal(d.get("reward_rescaling_sigma")[:3], ag.rsig[:3])
+    if srs:
+        assert rescaled >= 1
+        close(d.get("state_rescaling_means"), ag.smean, 1e-5, 1e-6)
+        close(d.get("state_rescaling_sigmas"), ag.ssdev, 1e-5, 1e-6)
+        assert np.all(ag.ssdev != 1.0)
+        n = ag.size()
+        total = int(d.scalar("total"))
+        order = ((total - n) % R + np.arange(n)) % R
+        close(d.get("state").reshape(R, S)[order], np.stack(ag.er["state"]), 1e-4, 1e-5)
 
 
 def test_c5_shape_runs():
