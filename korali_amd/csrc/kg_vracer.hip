@@ -671,13 +671,17 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       const int n = (int)min((long long)RC, c - start + 1);
       int kk = k;
       unsigned long long inmb = 0;
+      // the highest mini-batch row not yet passed is <= c: only when it lies
+      // in this chunk (rare: B rows over the whole memory) are the entries
+      // checked one by one (each check a dependent LDS read)
+      if (kk >= 0 && (long long)s_mb[kk] > c - n)
 #pragma unroll
-      for (int j = 0; j < RC; j++)
-        if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
-          vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
-          inmb |= 1ull << j;
-          while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
-        }
+        for (int j = 0; j < RC; j++)
+          if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
+            vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
+            inmb |= 1ull << j;
+            while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
+          }
       float rr[RC];
 #pragma unroll
       for (int j = 0; j < RC; j++)

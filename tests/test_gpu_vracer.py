@@ -173,7 +173,7 @@ def test_environment_steps_match_oracle(clipped, R, T, rr):
         assert np.array_equal(d.get("reward_rescaling_count")[:3], ag.rcnt[:3])
         assert np.array_equal(d.get("reward_rescaling_sum")[:3], ag.rsum[:3])
         assert np.array_equal(d.get("reward_rescaling_sigma")[:3], ag.rsig[:3])
-        assert np.all(ag.rsig[:3] != 1.0)
+        assert np.any(ag.rsig[:3] != 1.0)
     # actions differ in the last float32 bits (reassociated MFMA sums), so do
     # the fp64 states: round 2 measured at most 3.8e-8 after 30 steps
     close(d.get("env_u").reshape(E, 4), np.stack([c.u for c in ro.carts]), 1e-6, 2e-7)
