@@ -876,10 +876,14 @@ def run_c5(args):
     d.synchronize()
     elapsed = time.perf_counter() - t0
     # stage timers on a few more steps
+    m0 = d.get("meta_phase_ticks").astype(np.float64)
+    u0 = d.scalar("policy_update_count")
     d.profile(True)
     for _ in range(3):
         d.training_step()
     d.synchronize()
+    nu = max(1.0, d.scalar("policy_update_count") - u0)
+    meta_us = ((d.get("meta_phase_ticks").astype(np.float64) - m0) / nu * 0.01).tolist()  # 100 MHz ticks
     stages = {}
     for st in ("environment_step", "update", "gemm_rollout", "gemm_update"):
         ms, cnt = d.profile_read(st)
@@ -911,6 +915,8 @@ def run_c5(args):
                                "replay 262144 (start 131072)", "fill_steps": filled},
         "policy_updates_per_sec": ups / elapsed, "updates": ups, "experiences": exps,
         "stage_ms": stages,
+        "metadata_kernel_phases_us": {"setup_and_importance_weights": meta_us[0], "retrace_chains": meta_us[1],
+                                      "loss_gradient_and_metadata": meta_us[2]},
         "update_roofline": {"flops_per_update": upd_flops, "avg_update_ms": upd_ms,
                             "achieved_tflops": upd_flops / (upd_ms * 1e-3) / 1e12 if upd_ms else None,
                             "peak": FP32_PEAK_TFLOPS,

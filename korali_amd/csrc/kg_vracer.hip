@@ -69,6 +69,9 @@ struct State {
   // state rescaling (agent.cpp.base:92-94, :291-322): the moments episodes
   // launched from now on scale their states with (identity until set)
   float smean[MAXS], ssdev[MAXS];
+  // k_vr_meta's phases (s_memrealtime, 100 MHz ticks, summed over updates):
+  // setup + importance weights, retrace chains, loss gradient + metadata
+  unsigned long long mtr[3];
 };
 
 struct Params {  // launch-constant configuration
@@ -588,6 +591,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     if (q >= R) q -= R;
     return (long long)q;
   };
+  const unsigned long long tm0 = __builtin_amdgcn_s_memrealtime();
   if (t == 0) s_delta = 0;
   if (RR && t < MAXENV) s_rsig[t] = st->rsig[t];
   __syncthreads();
@@ -622,6 +626,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   }
   if (delta) atomicAdd(&s_delta, delta);
   __syncthreads();
+  const unsigned long long tm1 = __builtin_amdgcn_s_memrealtime();
   const long long off1 = off0 + s_delta;
   const float off_ratio = (float)off1 / (float)size0;
   // ---- retrace chains of the oldest mini-batch entries of each episode
@@ -724,6 +729,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     }
   }
   __syncthreads();
+  const unsigned long long tm2 = __builtin_amdgcn_s_memrealtime();
   // ---- the VRACER loss gradient (VRACER.cpp.base:104-177), all from LDS;
   // then the replay memory's metadata (first occurrences)
   const float klm = -(1.0f - beta);
@@ -820,7 +826,10 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
       er.tiw[p] = s_tiw[b];
     }
   }
+  __syncthreads();
   if (t == 0) {
+    const unsigned long long tm3 = __builtin_amdgcn_s_memrealtime();
+    st->mtr[0] += tm1 - tm0, st->mtr[1] += tm2 - tm1, st->mtr[2] += tm3 - tm2;
     st->off_count = off1;
     st->off_ratio = off_ratio;
     st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)upd0);
@@ -1709,6 +1718,7 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
       {"state_rescaling_means", &h->st->smean[0], 4, (size_t)P.S},
       {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)P.S},
+      {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)3},
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {

@@ -16,7 +16,7 @@ from .native import KoraliDeviceError, check, lib
 _DTYPES = {
     "environment_id": np.int32, "termination": np.int32, "on_policy": np.int32, "episode_pos": np.int32,
     "env_steps": np.int32, "env_ids": np.int32, "finished_env": np.int32, "mini_batch": np.uint32,
-    "episode_id": np.int64, "env_u": np.float64, "env_sample_ids": np.uint64, "reward_rescaling_count": np.int64,
+    "episode_id": np.int64, "env_u": np.float64, "env_sample_ids": np.uint64, "reward_rescaling_count": np.int64, "meta_phase_ticks": np.uint64,
 }
 
 
