@@ -658,14 +658,27 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     // of the ring whose values go unused; no branch splits the loads from
     // the waits, so those stay counted)
     int ea[RC], eb[RC];  // (RR: the entries' environment ids)
+    // (a chunk that does not wrap around the ring, the common case, is
+    // addressed from one base with constant offsets: no per-entry 64-bit
+    // wrap arithmetic in this single-wave, instruction-bound walk)
     auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC], int (&en)[RC])
                     __attribute__((always_inline)) {
-      long long q = p0;
+      if (p0 >= RC - 1) {
+        const float *v = er.v + p0, *w = er.tiw + p0, *r = er.rew + p0;
+        const int *ev = er.env + p0;
 #pragma unroll
-      for (int j = 0; j < RC; j++) {
-        vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
-        if (RR) en[j] = er.env[q];
-        q = q == 0 ? (long long)R - 1 : q - 1;
+        for (int j = 0; j < RC; j++) {
+          vv[j] = v[-j], tw[j] = w[-j], rw[j] = r[-j];
+          if (RR) en[j] = ev[-j];
+        }
+      } else {
+        long long q = p0;
+#pragma unroll
+        for (int j = 0; j < RC; j++) {
+          vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
+          if (RR) en[j] = er.env[q];
+          q = q == 0 ? (long long)R - 1 : q - 1;
+        }
       }
     };
     auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC],
@@ -688,14 +701,26 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
             while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
           }
       float rr[RC];
+      const float g = P.gamma;
+      if (n == RC) {  // a full chunk: no per-entry predicate
 #pragma unroll
-      for (int j = 0; j < RC; j++)
-        if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + P.gamma * retV - vv[j]);
-      long long q = p0;
+        for (int j = 0; j < RC; j++) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < RC; j++) {
-        if (j < n) er.ret[q] = rr[j];
-        q = q == 0 ? (long long)R - 1 : q - 1;
+        for (int j = 0; j < RC; j++)
+          if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
+      }
+      if (n == RC && p0 >= RC - 1) {
+        float *rp = er.ret + p0;
+#pragma unroll
+        for (int j = 0; j < RC; j++) rp[-j] = rr[j];
+      } else {
+        long long q = p0;
+#pragma unroll
+        for (int j = 0; j < RC; j++) {
+          if (j < n) er.ret[q] = rr[j];
+          q = q == 0 ? (long long)R - 1 : q - 1;
+        }
       }
       if (inmb)
 #pragma unroll
