@@ -252,7 +252,7 @@ def engine_rate(steps, warmup, cov):
     * end_to_end: one fresh k.run(e) of `steps` generations, wall clock,
       handle creation and initialisation included;
     * in_run: from that same run, generations `warmup`+1 .. `steps` by the
-      engine's own completion marks (Internal / Generation Completion Times:
+      engine's own completion marks (korali._generation_completion_times:
       when each generation's termination check returned), no subtraction
       of two runs."""
     import korali
@@ -273,7 +273,7 @@ def engine_rate(steps, warmup, cov):
     t0 = time.perf_counter()
     k.run(f)
     e2e = steps / (time.perf_counter() - t0)
-    marks = list(f["Internal"]["Generation Completion Times"])
+    marks = korali._generation_completion_times(f)
     w = min(warmup, steps - 1)
     in_run = (steps - w) / (marks[steps] - marks[w]) if len(marks) == steps + 1 else None
     return diff, e2e, in_run
@@ -652,7 +652,7 @@ def run_c4_engine(args, world, rank):
     the mean / rank-mu partials on the handle's stream; Host transport when
     KORALI_AMD_C4_TRANSPORT=Host).  One run of warmup + steps generations;
     the engine records when each generation completed (its termination check
-    returned, Internal / Generation Completion Times), and the timed region
+    returned, korali._generation_completion_times), and the timed region
     is the last `steps` generations of the slowest rank."""
     import korali
     import socket
@@ -675,7 +675,7 @@ def run_c4_engine(args, world, rank):
     e = c4_experiment(total)
     tdist.barrier()
     k.run(e)
-    marks = list(e["Internal"]["Generation Completion Times"])
+    marks = korali._generation_completion_times(e)
     gens = int(e["Current Generation"])
     if gens != total or len(marks) != total + 1:
         raise RuntimeError(f"engine ran {gens} generations ({len(marks)} marks), expected {total}")

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 5
+#define KG_ABI_VERSION 6
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -182,12 +182,36 @@ int kg_cmaes_wait_termination_fields(kg_cmaes_t h, double *out);
  * finite bounds, discrete variables, Mirrored Sampling or a diagonal
  * covariance kg_cmaes_sample draws the whole population on every rank: the
  * redraw walk and the ±z pairs are sequential over it);
- * the caller all-gathers "Value Vector" (λ doubles, shards in rank order),
- * runs kg_cmaes_update_partial, sum-all-reduces "Shard Partials" and
- * finishes with kg_cmaes_update_finalize.  Every rank then holds the same
- * state; mean and rank-μ sums are added per shard (within 1e-12 of the
- * sequential order), the sort and selection are replicated bit-exactly. */
+ * the caller all-gathers "Value Vector" (λ doubles, shards in rank order)
+ * and then runs the update protocol of the handle's covariance mode.
+ *
+ * cov_mode KG_COV_EXACT — the reference's summation order, every rank's state
+ * bit-identical to the unsharded run (CMAES.cpp.base:603-609, :690-718 sum
+ * mean and rank-μ over the selected rows in selection order):
+ *   kg_cmaes_update_partial    replicated sort, best bookkeeping; this rank's
+ *                              selected rows (ascending selection rank) packed
+ *                              into block `rank` of "Shard Rows";
+ *   kg_cmaes_shard_row_count   waits for the packing; *count = doubles per
+ *                              rank block (0: nothing to exchange);
+ *   caller                     in-place all-gather of "Shard Rows", *count
+ *                              doubles per rank (skip when 0);
+ *   kg_cmaes_update_rows       the μ selected rows in selection order on every
+ *                              rank; mean and paths (replicated); the rank-μ
+ *                              chains of this rank's share of the covariance's
+ *                              lower triangle into "Shard Covariance" (packed,
+ *                              entry d (d+1)/2 + e, INT64_MIN bits elsewhere);
+ *   caller                     MAX all-reduce of "Shard Covariance" viewed as
+ *                              int64 (every entry's owner's exact bits);
+ *   kg_cmaes_update_finalize   covariance, σ.
+ *
+ * cov_mode KG_COV_MFMA — per-shard partial sums (within 1e-12 of the
+ * sequential order): kg_cmaes_update_partial, sum all-reduce of "Shard
+ * Partials", kg_cmaes_update_finalize.
+ *
+ * The sort and selection are replicated bit-exactly in both modes. */
 int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation);
+int kg_cmaes_shard_row_count(kg_cmaes_t h, size_t *count);
+int kg_cmaes_update_rows(kg_cmaes_t h, size_t generation);
 int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation);
 int kg_cmaes_synchronize(kg_cmaes_t h); /* waits and reports device-side errors */
 /* named state fields, keys as in the reference's solver JSON

@@ -25,6 +25,9 @@ if _root not in _sys.path:
 
 try:
     from korali_amd.libkorali import Engine, Experiment, KoraliError, Sample, koraliJson  # noqa: F401
+    # timing hook of this engine (not a reference API): the last run's
+    # generation completion marks, kept out of the experiment's JSON
+    from korali_amd.libkorali import _generation_completion_times  # noqa: F401
 except ImportError as _e:  # pragma: no cover
     raise ImportError(f"korali: the native engine is not built ({_e}); run `python -m korali_amd._build`") from _e
 

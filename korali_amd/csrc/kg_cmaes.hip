@@ -1535,15 +1535,21 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
   }
   return acc;
 }
+// tbase: the first tile of this launch (a population-sharded rank computes
+// its share [tbase, tbase + gridDim.x) of the tiles); pack != nullptr: the
+// lower-triangle results go to pack[d (d + 1) / 2 + e] (the sharded
+// exchange buffer, "Shard Covariance") instead of C, entries that adaptC
+// leaves unchanged (diagonal covariance) with their old value
 __global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal, const double *__restrict__ Yc,
                                                     const double *__restrict__ Tt, const double *__restrict__ pc,
-                                                    double *C, const CmaesScalars *__restrict__ sc) {
+                                                    double *C, const CmaesScalars *__restrict__ sc, int tbase,
+                                                    double *__restrict__ pack) {
   __shared__ double Ts[2][4][AR_KS];
   __shared__ double Ys[2][8][AR_KS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = lane >> 4, j = lane & 15;
   // tile index -> (row block, column block), row blocks in order
-  int t = blockIdx.x, rb = 0;
+  int t = blockIdx.x + tbase, rb = 0;
   const int ncb = (N + 7) / 8;
   for (;; rb++) {
     const int c = min(ar_col_blocks_upto(rb), ncb);
@@ -1567,6 +1573,10 @@ __global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal,
     acc = ar_run<true>(acc, N, mu, d0, e0, dl, el, Yc, Tt, s2, Ts, Ys);
   else
     acc = ar_run<false>(acc, N, mu, d0, e0, dl, el, Yc, Tt, s2, Ts, Ys);
+  if (pack) {
+    if (j == 0 && d < N && e <= d) pack[(size_t)d * (d + 1) / 2 + e] = active ? acc : C[(size_t)d * N + e];
+    return;
+  }
   if (active && j == 0) {
     C[(size_t)d * N + e] = acc;
     if (e < d) C[(size_t)e * N + d] = acc;
@@ -2312,6 +2322,107 @@ __global__ void __launch_bounds__(256) k_shard_finalize(int N, const double *__r
   if (sc->bestFlag) bestEverVars[d] = v;
 }
 
+// ---- the exact-order sharded update (cov_mode EXACT).  The reference sums
+// mean and rank-mu over the selected rows in selection order
+// (CMAES.cpp.base:603-609, :690-718); partial sums per shard would reorder
+// them.  Instead every rank receives all mu selected rows: rank o packs the
+// selected rows it owns, ascending selection rank, into block o of the
+// exchange buffer ("Shard Rows", blocks of maxcnt rows), the caller
+// all-gathers the blocks, and every rank unpacks Y in selection order.  Which
+// rank owns selection k, and where in its block row k sits, follow from the
+// replicated sorting index alone (owner = idx[k] / (lambda / S)).
+constexpr int SHARD_MAX = 64;
+// pos[k] = position of selection k in its owner's block; cnt[o] = rows owner
+// o packs; cnt[S] = their maximum (the block size, in rows)
+__global__ void __launch_bounds__(1024) k_shard_positions(int mu, int per, int S, const unsigned *__restrict__ idx,
+                                                          int *__restrict__ pos, int *__restrict__ cnt) {
+  __shared__ int wtot[16][SHARD_MAX];
+  __shared__ int carry[SHARD_MAX];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid < S) carry[tid] = 0;
+  __syncthreads();
+  for (int base = 0; base < mu; base += 1024) {
+    const int k = base + tid;
+    const int o = k < mu ? (int)(idx[k] / (unsigned)per) : -1;
+    int before = 0;
+    for (int q = 0; q < S; q++) {
+      const unsigned long long bal = __ballot(o == q);
+      if (o == q) before = __popcll(bal & ((1ULL << lane) - 1ULL));
+      if (lane == 0) wtot[wid][q] = __popcll(bal);
+    }
+    __syncthreads();
+    if (o >= 0) {
+      int off = carry[o];
+      for (int w = 0; w < wid; w++) off += wtot[w][o];
+      pos[k] = off + before;
+    }
+    __syncthreads();
+    if (tid < S)
+      for (int w = 0; w < 16; w++) carry[tid] += wtot[w][tid];
+    __syncthreads();
+  }
+  if (tid < S) cnt[tid] = carry[tid];
+  __syncthreads();
+  if (tid == 0) {
+    int m = 0;
+    for (int q = 0; q < S; q++) m = max(m, carry[q]);
+    cnt[S] = m;
+  }
+}
+
+// this rank's selected rows into its block of the exchange buffer
+__global__ void __launch_bounds__(128) k_shard_pack(int N, int rank, int per, int S, const unsigned *__restrict__ idx,
+                                                    const int *__restrict__ pos, const int *__restrict__ cnt,
+                                                    const double *__restrict__ X, double *__restrict__ rows) {
+  const int k = blockIdx.x;
+  const unsigned i = idx[k];
+  if ((int)(i / (unsigned)per) != rank) return;
+  const size_t dst = ((size_t)rank * cnt[S] + pos[k]) * N;
+  for (int d = threadIdx.x; d < N; d += blockDim.x) rows[dst + d] = X[(size_t)i * N + d];
+}
+
+// Y in selection order from the gathered blocks (rows == nullptr: every rank
+// holds the whole population in X); m_prev; the best variables (row 0)
+__global__ void __launch_bounds__(128) k_shard_unpack(int N, int per, int S, const unsigned *__restrict__ idx,
+                                                      const int *__restrict__ pos, const int *__restrict__ cnt,
+                                                      const double *__restrict__ rows, const double *__restrict__ X,
+                                                      double *__restrict__ Y, const double *__restrict__ mean,
+                                                      double *__restrict__ prevMean, double *__restrict__ currBestVars,
+                                                      double *__restrict__ bestEverVars,
+                                                      const CmaesScalars *__restrict__ sc) {
+  const int k = blockIdx.x;
+  const unsigned i = idx[k];
+  const double *src = rows ? rows + ((size_t)(i / (unsigned)per) * cnt[S] + pos[k]) * N : X + (size_t)i * N;
+  for (int d = threadIdx.x; d < N; d += blockDim.x) Y[(size_t)k * N + d] = src[d];
+  if (k == 0) {
+    const bool flag = sc->bestFlag != 0u;
+    for (int d = threadIdx.x; d < N; d += blockDim.x) {
+      prevMean[d] = mean[d];
+      const double v = src[d];
+      currBestVars[d] = v;
+      if (flag) bestEverVars[d] = v;
+    }
+  }
+}
+
+// INT64_MIN (the bits of -0.0) everywhere: the MAX all-reduce of the int64
+// view then returns every entry's owner's exact bits
+__global__ void k_fill_min_i64(size_t n, long long *__restrict__ p) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = (long long)0x8000000000000000ULL;
+}
+
+// the gathered lower triangle back into the symmetric C
+__global__ void __launch_bounds__(256) k_shard_cov_unpack(int N, const double *__restrict__ pack, double *C) {
+  const int d = blockIdx.x;
+  const double *row = pack + (size_t)d * (d + 1) / 2;
+  for (int e = threadIdx.x; e <= d; e += blockDim.x) {
+    const double v = row[e];
+    C[(size_t)d * N + e] = v;
+    C[(size_t)e * N + d] = v;
+  }
+}
+
 // adaptC diag extrema :709-717, updateSigma :720-761, numericalErrorTreatment
 // :763-772, min/max standard deviation :679-687.  (The reference's max/min
 // diagonal scan uses "else if"; a new maximum can never be a new minimum, so
@@ -2594,6 +2705,14 @@ struct kg_cmaes_s {
   bool replSample = false;  // sharded, but every rank draws the whole population (kg_cmaes_create)
   int *kidx = nullptr, *shardCnt = nullptr;
   double *part = nullptr;  // "Shard Partials": mean (N), best row (N), rank-mu tiles
+  // exact-order sharded update (cov_mode EXACT): selected-row exchange blocks
+  // ("Shard Rows", S blocks of up to rowsCap rows), the positions / counts of
+  // the blocks, and this rank's share of the new covariance ("Shard Covariance",
+  // the packed lower triangle)
+  int *shardPos = nullptr, *shardCounts = nullptr;
+  double *rows = nullptr, *covPack = nullptr;
+  size_t rowsCap = 0;
+  int rowBlock = -1;  // rows per block of the current generation's exchange (host copy; -1: not yet known)
   unsigned long long *eigTrace = nullptr;  // KORALI_AMD_TRACE_EIGEN: s_memtime per phase
   // termination scalars + error flags of the last update, written by the
   // device into host-coherent memory (kg_cmaes_wait_termination_fields)
@@ -2735,6 +2854,8 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
     const size_t nt = (N + 15) / 16;
     VEC("Shard Partials", h->part, 2 * N + nt * (nt + 1) / 2 * 256)
   }
+  if (h->rows) VEC("Shard Rows", h->rows, (size_t)h->shards * h->rowsCap * N)
+  if (h->covPack) VEC("Shard Covariance", h->covPack, N * (N + 1) / 2)
 #define SCA(key, fld) VEC(key, &h->sc->fld, 1)
   SCA("Sigma", sigma)
   SCA("Trace", trace)
@@ -2882,9 +3003,10 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   h->R = (h->finiteBounds || h->hasDiscrete) ? std::max(256, L / 4) : 0;
   h->shards = cfg->shard_count > 1 ? cfg->shard_count : 1;
   h->shardRank = h->shards > 1 ? cfg->shard_rank : 0;
-  if (h->shards > 1 && (L % h->shards != 0 || cfg->shard_rank < 0 || cfg->shard_rank >= h->shards)) {
-    set_error("population sharding needs Population Size divisible by the shard count and "
-              "0 <= shard_rank < shard_count");
+  if (h->shards > 1 && (L % h->shards != 0 || cfg->shard_rank < 0 || cfg->shard_rank >= h->shards ||
+                        h->shards > SHARD_MAX)) {
+    set_error("population sharding needs Population Size divisible by the shard count, "
+              "0 <= shard_rank < shard_count and at most " + std::to_string(SHARD_MAX) + " shards");
     delete h;
     return 1;
   }
@@ -2941,6 +3063,14 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     h->bestCEval.assign(h->nc, 0.0);
   }
   rc |= dalloc(&h->kidx, h->muMax) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
+  if (cfg->shard_count >= 1 && cfg->cov_mode != KG_COV_MFMA) {
+    // a rank owns lambda / S rows, so it packs at most min(mu, lambda / S)
+    // selected ones; whole-population ranks (replSample) exchange no rows
+    h->rowsCap = h->replSample ? 0 : (size_t)std::min(h->muMax, L / h->shards);
+    rc |= dalloc(&h->shardPos, h->muMax) | dalloc(&h->shardCounts, h->shards + 1) |
+          dalloc(&h->covPack, (size_t)N * (N + 1) / 2);
+    if (h->rowsCap) rc |= dalloc(&h->rows, (size_t)h->shards * h->rowsCap * N);
+  }
   if (rc) {
     delete h;
     return 1;
@@ -3019,7 +3149,8 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->eigTrace, (void *)h->kidx, (void *)h->shardCnt, (void *)h->part, (void *)h->G,
                   (void *)h->gran, (void *)h->mask, (void *)h->maskSigma, (void *)h->ubuf, (void *)h->uused,
                   (void *)h->selEnd, (void *)h->V, (void *)h->auxC, (void *)h->violDev, (void *)h->pairI,
-                  (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev, (void *)h->dzT})
+                  (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev, (void *)h->dzT, (void *)h->shardPos,
+                  (void *)h->shardCounts, (void *)h->rows, (void *)h->covPack})
     if (p) (void)hipFree(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
@@ -3686,7 +3817,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
         // Markstein quotients when every factor is in range (k_rankmu_prep's
         // flag, read on the device: the kernel picks the branch per launch)
         hipLaunchKernelGGL(k_adaptC_row, dim3(ar_tiles(N)), dim3(512), 0, h->stream, N, mu,
-                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
+                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc, 0, (double *)nullptr);
       } else if (old2)
         hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
                            h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
@@ -3703,6 +3834,24 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
 int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
   const int N = h->N, mu = h->mu;
   if (cmaes_sort(h)) return 1;
+  if (h->covPack) {
+    // exact order: best bookkeeping, then this rank's selected rows into its
+    // exchange block
+    Stage st(h, "mean_paths");
+    const int per = h->lam / h->shards;
+    hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
+                       (unsigned long long)generation, (const double *)nullptr, h->F, h->idx, h->w, h->currBestVars,
+                       h->bestEverVars, h->sc, (const int *)nullptr, h->lam);
+    if (h->rows) {
+      hipLaunchKernelGGL(k_shard_positions, dim3(1), dim3(1024), 0, h->stream, mu, per, h->shards, h->idx, h->shardPos,
+                         h->shardCounts);
+      hipLaunchKernelGGL(k_shard_pack, dim3(mu), dim3(128), 0, h->stream, N, h->shardRank, per, h->shards, h->idx,
+                         h->shardPos, h->shardCounts, h->X, h->rows);
+    }
+    KG_HIP(hipGetLastError());
+    h->rowBlock = -1;
+    return 0;
+  }
   {
     Stage st(h, "mean_paths");
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
@@ -3727,8 +3876,69 @@ int kg_cmaes_update_partial(kg_cmaes_t h, size_t generation) {
   return 0;
 }
 
+int kg_cmaes_shard_row_count(kg_cmaes_t h, size_t *count) {
+  KG_CHECK(h->covPack, "kg_cmaes_shard_row_count: the handle is not sharded in the exact covariance mode");
+  KG_CHECK(count, "kg_cmaes_shard_row_count: null argument");
+  if (!h->rows) {
+    h->rowBlock = 0;  // every rank holds the whole population: nothing to exchange
+  } else {
+    int m = 0;
+    KG_HIP(hipMemcpyAsync(&m, h->shardCounts + h->shards, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    KG_HIP(hipStreamSynchronize(h->stream));
+    KG_CHECK(m >= 0 && (size_t)m <= h->rowsCap, "shard row count out of range (internal error)");
+    h->rowBlock = m;
+  }
+  *count = (size_t)h->rowBlock * h->N;
+  return 0;
+}
+
+int kg_cmaes_update_rows(kg_cmaes_t h, size_t generation) {
+  KG_CHECK(h->covPack, "kg_cmaes_update_rows: the handle is not sharded in the exact covariance mode");
+  KG_CHECK(h->rowBlock >= 0, "kg_cmaes_update_rows before kg_cmaes_shard_row_count");
+  const int N = h->N, mu = h->mu;
+  const int per = h->lam / h->shards;
+  {
+    Stage st(h, "mean_paths");
+    hipLaunchKernelGGL(k_shard_unpack, dim3(mu), dim3(128), 0, h->stream, N, per, h->shards, h->idx, h->shardPos,
+                       h->shardCounts, (const double *)h->rows, h->X, h->Y, h->mean, h->prevMean, h->currBestVars,
+                       h->bestEverVars, h->sc);
+    hipLaunchKernelGGL(k_rankmu_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0, h->stream, N,
+                       mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
+    if (row_chains())
+      hipLaunchKernelGGL(k_mean3, dim3((N + 15) / 16), dim3(256), 0, h->stream, N, mu, h->Y, h->w, h->mean,
+                         h->prevMean, h->meanUpdate, h->sc);
+    else
+      hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu, h->Y,
+                         h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
+    KG_HIP(hipGetLastError());
+    if (cmaes_paths(h, generation)) return 1;
+  }
+  {
+    // this rank's contiguous share of the covariance tiles, each element's
+    // chain in the reference's order
+    Stage st(h, "covariance");
+    const size_t npk = (size_t)N * (N + 1) / 2;
+    hipLaunchKernelGGL(k_fill_min_i64, dim3((unsigned)std::min<size_t>((npk + 255) / 256, 1024)), dim3(256), 0,
+                       h->stream, npk, (long long *)h->covPack);
+    const int nt = ar_tiles(N);
+    const int t0 = (int)((long long)nt * h->shardRank / h->shards), t1 = (int)((long long)nt * (h->shardRank + 1) / h->shards);
+    if (t1 > t0)
+      hipLaunchKernelGGL(k_adaptC_row, dim3(t1 - t0), dim3(512), 0, h->stream, N, mu, h->cfg.diagonal_covariance, h->Yc,
+                         h->Tt, h->pc, h->C, h->sc, t0, h->covPack);
+    KG_HIP(hipGetLastError());
+  }
+  h->rowBlock = -1;
+  return 0;
+}
+
 int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
   const int N = h->N;
+  if (h->covPack) {
+    Stage st(h, "covariance");
+    hipLaunchKernelGGL(k_shard_cov_unpack, dim3(N), dim3(256), 0, h->stream, N, (const double *)h->covPack, h->C);
+    KG_HIP(hipGetLastError());
+    return cmaes_sigma(h, generation);
+  }
   {
     Stage st(h, "mean_paths");
     hipLaunchKernelGGL(k_shard_finalize, dim3((N + 255) / 256), dim3(256), 0, h->stream, N, h->part, h->mean,
@@ -3866,7 +4076,8 @@ int kg_cmaes_get_field(kg_cmaes_t h, const char *name, double *out, size_t n) {
   }
   FieldRef r;
   KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
-  KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
+  KG_CHECK(n == r.n || (n < r.n && std::string(name) == "Shard Rows"),  // (exchange blocks: a prefix)
+           std::string("size mismatch for field ") + name);
   KG_HIP(hipMemcpyAsync(out, r.dev, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -3889,7 +4100,7 @@ int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t 
   }
   FieldRef r;
   KG_CHECK(field_ref(h, name, r), std::string("unknown CMA-ES field: ") + name);
-  KG_CHECK(n == r.n, std::string("size mismatch for field ") + name);
+  KG_CHECK(n == r.n || (n < r.n && std::string(name) == "Shard Rows"), std::string("size mismatch for field ") + name);
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   h->stateDirty = true;

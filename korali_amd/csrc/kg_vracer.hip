@@ -43,7 +43,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MAXA = 4;  // action dimensions supported by the device kernels
 constexpr int MAXO = 1 + 2 * MAXA;
 constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
-constexpr int MAXENV = 8;   // environment ids with reward rescaling (Problem / Environment Count)
+constexpr int MAXENV = 64;  // environment ids with reward rescaling (Problem / Environment Count)
 constexpr int MAXS = 8;     // state dimensions with state rescaling
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
 enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u, ERR_ENV_ODE = 8u };
@@ -1109,10 +1109,13 @@ __global__ void k_vr_env_reset(Params P, const State *st, Envs ev, float *X, uns
 // continuous.cpp.base:219-260: the Normal mean; Clipped Normal: the mean
 // clipped to the bounds), and adds the reward of environment 0 (env.py:
 // testing runs environment 0) until the pole falls or max_episode_steps.
-// (testing agents take the agent's State Rescaling moments, agent.cpp.base:279-280)
+// (testing agents take the agent's State Rescaling moments, agent.cpp.base:279-280,
+// and always rescale, reinforcementLearning.cpp.base:361-370: with the
+// defaults 0 / 1 that is the identity)
 __device__ __forceinline__ float vr_test_state(const Params &P, const State *st, int k, double y) {
   const float x = (float)y;
-  return P.srs ? (x - st->smean[k]) / st->ssdev[k] : x;
+  (void)P;
+  return (x - st->smean[k]) / st->ssdev[k];
 }
 __global__ void k_vr_test_reset(Params P, const State *st, int n, int S, const unsigned long long *__restrict__ sid,
                                 const unsigned long long *__restrict__ lid, double *u, double *tm, int *steps,
@@ -1794,7 +1797,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.srs = c->state_rescaling ? 1 : 0;
   KG_CHECK(!P.srs || c->state_size <= (size_t)MAXS, "vracer: State Rescaling on the device supports up to 8 state variables");
   KG_CHECK(!P.rr || (c->environment_count >= 1 && c->environment_count <= (size_t)MAXENV),
-           "vracer: Reward Rescaling on the device supports Environment Count 1..8");
+           "vracer: Reward Rescaling on the device supports Environment Count 1..64");
   P.l2 = c->l2_regularization_enabled ? 1 : 0;
   P.gamma = (float)c->discount_factor, P.lr0 = (float)c->learning_rate, P.iw_trunc = (float)c->importance_weight_truncation_level;
   P.cutoff_scale = (float)c->off_policy_cutoff_scale, P.off_target = (float)c->off_policy_target;

@@ -328,22 +328,34 @@ class RcclCollective : public Collective {
     void *c = nullptr;
     check(commInitRank(&c, world, all[0], rank), "ncclCommInitRank");
     std::lock_guard<std::mutex> g(commMu);
+    if (dog->aborted()) {  // the abort fired while the communicator was being created: it never saw this one
+      commAbort(c);
+      dfail("another rank failed; this rank's collectives were aborted");
+    }
     comm = c;
   }
-  void allGather(const SolverBuffer &b, size_t count) override {
+  // every enqueue holds commMu, so the watchdog's abort cannot free the
+  // communicator between the check and the call
+  template <class F>
+  void enqueue(F &&call, const char *what) {
     ensureComm();
+    std::lock_guard<std::mutex> g(commMu);
+    if (!comm || dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
+    check(call(comm), what);
+  }
+  void allGather(const SolverBuffer &b, size_t count) override {
     double *p = (double *)b.devicePtr();
-    check(allGatherFn(p + (size_t)rank * count, p, count, 8 /* ncclFloat64 */, comm, b.stream()), "ncclAllGather");
+    void *s = b.stream();
+    enqueue([&](void *c) { return allGatherFn(p + (size_t)rank * count, p, count, 8 /* ncclFloat64 */, c, s); },
+            "ncclAllGather");
   }
   void allReduceSum(const SolverBuffer &b, size_t n) override {
-    ensureComm();
-    void *p = b.devicePtr();
-    check(allReduceFn(p, p, n, 8 /* ncclFloat64 */, 0 /* ncclSum */, comm, b.stream()), "ncclAllReduce");
+    void *p = b.devicePtr(), *s = b.stream();
+    enqueue([&](void *c) { return allReduceFn(p, p, n, 8 /* ncclFloat64 */, 0 /* ncclSum */, c, s); }, "ncclAllReduce");
   }
   void allReduceMaxI64(const SolverBuffer &b, size_t n) override {
-    ensureComm();
-    void *p = b.devicePtr();
-    check(allReduceFn(p, p, n, 4 /* ncclInt64 */, 2 /* ncclMax */, comm, b.stream()), "ncclAllReduce");
+    void *p = b.devicePtr(), *s = b.stream();
+    enqueue([&](void *c) { return allReduceFn(p, p, n, 4 /* ncclInt64 */, 2 /* ncclMax */, c, s); }, "ncclAllReduce");
   }
   void barrier() override { boot.barrier(); }
 };

@@ -605,6 +605,7 @@ struct CmaesModule : SolverModule {
   // between kg_cmaes_update_partial and _finalize (include/korali_amd.h)
   Collective *dist = nullptr;
   size_t r0 = 0, r1 = 0;
+  bool exactShards = true;  // the sharded update's protocol (include/korali_amd.h): exact order or partial sums
   std::vector<size_t> constraintFns;  // CCMA-ES (function table indices)
   size_t curGen = 0;
 
@@ -733,16 +734,14 @@ struct CmaesModule : SolverModule {
     c.granularity = gran.data();
     c.normal_seed = seeds.assign(gn);
     c.uniform_seed = seeds.assign(gu);
-    // the Distributed conduit shards the update: every rank sums the mean and
-    // rank-mu terms of the selected rows it owns and one all-reduce adds the
-    // partial sums, which is the MFMA mode's (reordered) summation; it is the
-    // default there, and the exact sequential order cannot be requested
-    const std::string cu = canon(str(sv, "Covariance Update", dist ? "MFMA" : "Exact"));
+    // Exact (default, also under the Distributed conduit): the reference's
+    // summation order; a sharded run all-gathers the selected rows and splits
+    // the rank-mu chains by covariance entry, bit-identical to an unsharded
+    // run.  MFMA: the matrix cores (sharded: per-rank partial sums)
+    const std::string cu = canon(str(sv, "Covariance Update", "Exact"));
     if (cu != "exact" && cu != "mfma") fail("'Covariance Update' must be 'Exact' or 'MFMA'.");
-    if (dist && cu == "exact")
-      fail("'Covariance Update' = 'Exact' needs an unsharded run (Sequential or Concurrent conduit): the Distributed "
-           "conduit adds per-rank partial sums (MFMA order).");
     c.cov_mode = cu == "mfma" ? KG_COV_MFMA : KG_COV_EXACT;
+    exactShards = c.cov_mode == KG_COV_EXACT;
     c.device = solverDevice(js, dist);
     c.shard_rank = dist ? dist->rank : 0;
     c.shard_count = dist ? dist->world : 0;
@@ -912,8 +911,17 @@ struct CmaesModule : SolverModule {
       dist->allGather(buffer("Value Vector"), r1 - r0);
       check(kg_cmaes_update_partial(h, gen));
       size_t n = 0;
-      check(kg_cmaes_field_size(h, "Shard Partials", &n));
-      dist->allReduceSum(buffer("Shard Partials"), n);
+      if (exactShards) {
+        // the selected rows to every rank, then the covariance entries' owners
+        check(kg_cmaes_shard_row_count(h, &n));
+        if (n) dist->allGather(buffer("Shard Rows"), n);
+        check(kg_cmaes_update_rows(h, gen));
+        check(kg_cmaes_field_size(h, "Shard Covariance", &n));
+        dist->allReduceMaxI64(buffer("Shard Covariance"), n);
+      } else {
+        check(kg_cmaes_field_size(h, "Shard Partials", &n));
+        dist->allReduceSum(buffer("Shard Partials"), n);
+      }
       check(kg_cmaes_update_finalize(h, gen));
       updated = true;
       return;
@@ -1423,7 +1431,13 @@ bool dirExists(const std::string &p) {
 struct ExperimentState {
   std::unique_ptr<SolverModule> solver;
   Logger log;
+  // seconds from the start of the last run's loop until each generation's
+  // termination check returned (generationCompletionTimes; kept out of the
+  // experiment's JSON, whose keys the reference's setConfiguration checks)
+  std::vector<double> marks;
 };
+
+std::vector<double> generationCompletionTimes(const Experiment &e) { return e._state->marks; }
 
 Experiment::Experiment() : _state(new ExperimentState()) {}
 
@@ -1597,6 +1611,7 @@ struct VracerModule : SolverModule {
   Json *solverJs = nullptr;
   Json description;  // vracerPolicyDescription: written into every result file
   bool testing = false, tested = false;  // Mode = Testing
+  bool rewardRescaled = false;           // Reward / Rescaling / Enabled
   std::vector<uint64_t> testingIds;
   std::vector<float> testingReward;
 
@@ -1672,8 +1687,9 @@ struct VracerModule : SolverModule {
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
     const bool stateRescaling = flag(sv["State Rescaling"], "Enabled", false);
     const bool rewardRescaling = flag(sv["Reward"]["Rescaling"], "Enabled", false);
-    if (rewardRescaling && (envCount < 1 || envCount > 8))
-      fail("Reward Rescaling on the device supports an 'Environment Count' of 1 to 8 (%llu given).", envCount);
+    if (rewardRescaling && (envCount < 1 || envCount > 64))
+      fail("Reward Rescaling on the device supports an 'Environment Count' of 1 to 64 (%llu given).", envCount);
+    rewardRescaled = rewardRescaling;
     if (flag(sv["Reward"]["Outbound Penalization"], "Enabled", false))
       fail("Reward Outbound Penalization is not supported by the device path.");
     Json &nn = sv["Neural Network"];
@@ -1763,6 +1779,24 @@ struct VracerModule : SolverModule {
       }
     }
     check(kg_vracer_set_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
+    if (testing) {
+      // the agent's rescaling state as the experiment holds it (the reference
+      // restores it with the policy, agent.cpp.base:1266-1274, and hands the
+      // state moments to every testing agent, :279-280)
+      Json &sr = sv["State Rescaling"];
+      if (sr.contains("Means") && sr["Means"].size() == 4 && sr.contains("Sigmas") && sr["Sigmas"].size() == 4) {
+        std::vector<float> m(4), s(4);
+        for (size_t i = 0; i < 4; i++) m[i] = (float)sr["Means"][i].getDouble(), s[i] = (float)sr["Sigmas"][i].getDouble();
+        check(kg_vracer_set_field(h, "state_rescaling_means", m.data(), 4 * sizeof(float)));
+        check(kg_vracer_set_field(h, "state_rescaling_sigmas", s.data(), 4 * sizeof(float)));
+      }
+      Json &rr = sv["Reward"]["Rescaling"];
+      if (rewardRescaled && rr.contains("Sigma") && rr["Sigma"].size() == envIds) {
+        std::vector<float> sg(64, 1.0f);
+        for (size_t i = 0; i < envIds; i++) sg[i] = (float)rr["Sigma"][i].getDouble();
+        check(kg_vracer_set_field(h, "reward_rescaling_sigma", sg.data(), 64 * sizeof(float)));
+      }
+    }
   }
 
   double scalar(const char *name) {
@@ -1840,13 +1874,19 @@ struct VracerModule : SolverModule {
     std::vector<float> theta(n);
     check(kg_vracer_get_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
     sv["Training"]["Current Policy"]["Policy"] = std::vector<double>(theta.begin(), theta.end());
-    {  // agent.config:311-320 (per environment id)
-      float sig[8], sum[8];
-      check(kg_vracer_get_field(h, "reward_rescaling_sigma", sig, sizeof sig));
-      check(kg_vracer_get_field(h, "reward_rescaling_sum", sum, sizeof sum));
-      const size_t ne = std::min<size_t>(envIds, 8);
-      sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig, sig + ne);
-      sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum, sum + ne);
+    {  // agent.config:311-320 (per environment id, Environment Count entries)
+      if (rewardRescaled) {
+        float sig[64], sum[64];
+        check(kg_vracer_get_field(h, "reward_rescaling_sigma", sig, sizeof sig));
+        check(kg_vracer_get_field(h, "reward_rescaling_sum", sum, sizeof sum));
+        sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig, sig + envIds);
+        sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum, sum + envIds);
+      } else {
+        // the sigmas stay 1 without rescaling (agent.cpp.base:97, :557-563);
+        // the squared-reward sums only feed them, and the device keeps them
+        // only when rescaling is enabled, so that key is left out
+        sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(envIds, 1.0);
+      }
       float sm[8], ss[8];  // agent.config:326-335 (the CartPole kernel: 4 state variables)
       check(kg_vracer_get_field(h, "state_rescaling_means", sm, 4 * sizeof(float)));
       check(kg_vracer_get_field(h, "state_rescaling_sigmas", ss, 4 * sizeof(float)));
@@ -2002,7 +2042,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   js["Is Finished"] = true;
   solver.finalize(js);
   js["Current Generation"] = (unsigned long long)gen;
-  js["Internal"]["Generation Completion Times"] = marks;
+  st.marks = marks;
   solver.getConfiguration(sv);
   if (tm) tm->saveDistributions(js);
   if (fileOut) saveState(js, gen);

@@ -178,6 +178,10 @@ Json bayesianEvaluate(Json &experiment, const std::vector<double> &x);
 // count.  Written into VRACER result files; pinned by the reference's
 // tests/python/rlview/abf2d_vracer* files.
 Json vracerPolicyDescription(Json &experiment);
+// the last run's generation completion marks: marks[0] = the loop's first
+// termination check, marks[i] = when generation i's check returned (seconds
+// from the start of the loop; timing hook, not part of the experiment state)
+std::vector<double> generationCompletionTimes(const Experiment &e);
 // Initial hyperparameters ([W (out x in), b] per layer, linear.cpp.base:28-49):
 // Xavier-scaled U(-1, 1) weights (the output layer x 0.001,
 // VRACER.cpp.base:38), zero biases; std::mt19937(seed) uniforms.

@@ -254,6 +254,7 @@ PYBIND11_MODULE(libkorali, m) {
 
   // test hooks: the continuous agent's policy description and initial
   // hyperparameters (pinned against the reference's VRACER result files)
+  m.def("_generation_completion_times", [](korali::Experiment &e) { return korali::generationCompletionTimes(e); });
   m.def("_vracer_policy_description", [](korali::Experiment &e) { return toPy(korali::vracerPolicyDescription(e._js)); });
   m.def("_vracer_initial_hyperparameters", [](const std::vector<size_t> &sizes, unsigned seed) {
     return korali::vracerInitialHyperparameters(sizes, seed);

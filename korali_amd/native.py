@@ -69,6 +69,7 @@ EXPORTED = [
     "kg_cmaes_create", "kg_cmaes_destroy", "kg_cmaes_initialize", "kg_cmaes_sample", "kg_cmaes_eval_builtin",
     "kg_cmaes_get_candidates", "kg_cmaes_set_fitness", "kg_cmaes_set_log_posterior", "kg_cmaes_update", "kg_cmaes_generation",
     "kg_cmaes_begin_sample", "kg_cmaes_wait_termination_fields", "kg_cmaes_set_gradients", "kg_cmaes_update_partial", "kg_cmaes_update_finalize",
+    "kg_cmaes_shard_row_count", "kg_cmaes_update_rows",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
     "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
@@ -111,6 +112,8 @@ def lib():
         L.kg_cmaes_update.argtypes = [vp, sz]
         L.kg_cmaes_update_partial.argtypes = [vp, sz]
         L.kg_cmaes_update_finalize.argtypes = [vp, sz]
+        L.kg_cmaes_shard_row_count.argtypes = [vp, C.POINTER(sz)]
+        L.kg_cmaes_update_rows.argtypes = [vp, sz]
         L.kg_debug_mt_jump.argtypes = [vp, C.c_uint64, vp]
         L.kg_debug_multinomial.argtypes = [C.c_uint64, C.c_size_t, C.c_uint, vp, C.c_size_t, vp, vp]
         L.kg_debug_cartpole.argtypes = [ip, vp, vp, sz, sz, vp, vp]
@@ -288,6 +291,16 @@ class CmaesDevice:
     def update_finalize(self, generation):
         check(self._L.kg_cmaes_update_finalize(self.h, int(generation)))
 
+    def shard_row_count(self):
+        """Doubles per rank block of the "Shard Rows" all-gather (exact-order
+        sharded update; waits for the packing)."""
+        n = C.c_size_t(0)
+        check(self._L.kg_cmaes_shard_row_count(self.h, C.byref(n)))
+        return int(n.value)
+
+    def update_rows(self, generation):
+        check(self._L.kg_cmaes_update_rows(self.h, int(generation)))
+
     def begin_sample(self):
         """Enqueue the next generation's generator prefetch and the first
         eigendecomposition phases (workspace only) — what the korali engine
@@ -344,6 +357,12 @@ class CmaesDevice:
     def __setitem__(self, name, value):
         a = np.ascontiguousarray(np.asarray(value, dtype=np.float64).reshape(-1))
         check(self._L.kg_cmaes_set_field(self.h, name.encode(), _dptr(a), a.size))
+
+    def get_prefix(self, name, n):
+        """The first n doubles of an exchange buffer ("Shard Rows")."""
+        out = np.empty(int(n))
+        check(self._L.kg_cmaes_get_field(self.h, name.encode(), _dptr(out), int(n)))
+        return out
 
     def sorting_index(self):
         out = np.empty(self.lam, dtype=np.uint64)

@@ -13,19 +13,24 @@ CMAES.cpp.base:186-231):
   3. all-gather of the per-candidate fitnesses (λ doubles) — the one
      exchange the selection needs;
   4. replicated sort (identical sorting index everywhere, bit-exact);
-  5. each rank sums the mean and rank-μ terms of the selected rows it owns,
-     plus the best row if it owns it; one sum all-reduce of those partials
-     (2N + N(N+16)/2 doubles); every rank then finishes the update.
+  5. the update, in the handle's covariance mode:
+     * "exact" (default): each rank packs the selected rows it owns
+       (ascending selection rank) and one all-gather hands every rank all μ
+       selected rows; mean and paths are then summed in the reference's
+       order on every rank (CMAES.cpp.base:603-609), the rank-μ chains of
+       the covariance's lower triangle are split by output entry across the
+       ranks, each in the reference's order (:690-718), and one MAX
+       all-reduce over their 64-bit patterns assembles the covariance.  Every
+       rank's state is bit-identical to the unsharded run;
+     * "mfma": each rank sums the mean and rank-μ terms of the selected rows
+       it owns, one sum all-reduce of those partials (2N + N(N+16)/2
+       doubles) — the sums in another order (≤1e-12 relative).
 
 The collectives go through torch.distributed: backend "nccl" is RCCL over
 xGMI on ROCm, and the tensors alias the handle's device buffers (zero copy,
-ordered on the handle's HIP stream).  transport="host" stages the two
-buffers through host memory instead, for the gloo backend (several ranks on
-one device, CPU-only process groups).
-
-Summation order of mean and rank-μ differs from the sequential reference by
-rounding only (≤1e-12 relative; selection and resampling indices are
-bit-exact for identical state), exactly as SURVEY.md §8(e) item 5 states.
+ordered on the handle's HIP stream).  transport="host" stages the buffers
+through host memory instead, for the gloo backend (several ranks on one
+device, CPU-only process groups).
 """
 import numpy as np
 
@@ -88,15 +93,24 @@ class ShardedCmaes:
         self.world = dist.get_world_size(group)
         self.N, self.lam = int(N), int(lam)
         self.r0, self.r1 = shard_range(self.lam, self.world, self.rank)
-        cmaes_kw.setdefault("cov_mode", "mfma")
+        cmaes_kw.setdefault("cov_mode", "exact")
+        self.exact = str(cmaes_kw["cov_mode"]).lower() == "exact"
         self.dev = CmaesDevice(N, lam, shard_rank=self.rank, shard_count=self.world, device=device, **cmaes_kw)
         self.transport = transport
         if transport == "device":
             import torch
             dv = torch.device("cuda", device)
-            self._F = torch.as_tensor(_DeviceArray(self.dev.device_ptr("Value Vector"), self.lam), device=dv)
-            n = self.dev.field_size("Shard Partials")
-            self._P = torch.as_tensor(_DeviceArray(self.dev.device_ptr("Shard Partials"), n), device=dv)
+
+            def view(name, typestr="<f8"):
+                return torch.as_tensor(_DeviceArray(self.dev.device_ptr(name), self.dev.field_size(name), typestr),
+                                       device=dv)
+
+            self._F = view("Value Vector")
+            if self.exact:
+                self._R = view("Shard Rows") if self.dev.field_size("Shard Rows") else None
+                self._C = view("Shard Covariance", "<i8")
+            else:
+                self._P = view("Shard Partials")
             self._stream = torch.cuda.ExternalStream(self.dev.stream(), device=dv)
         elif transport != "host":
             raise ValueError("transport must be 'device' or 'host'")
@@ -109,6 +123,30 @@ class ShardedCmaes:
         else:
             F = self.dev["Value Vector"]
             self.dev["Value Vector"] = allgather_shards(self.dist, F[self.r0:self.r1], self.world, self.group)
+
+    def _exchange_rows(self):
+        n = self.dev.shard_row_count()  # doubles per rank block (0: every rank holds the population)
+        if n == 0 or self.world == 1:
+            return
+        if self.transport == "device":
+            import torch
+            with torch.cuda.stream(self._stream):
+                blk = self._R[self.rank * n:(self.rank + 1) * n].clone()
+                self.dist.all_gather_into_tensor(self._R[:self.world * n], blk, group=self.group)
+        else:
+            R = self.dev.get_prefix("Shard Rows", self.world * n)
+            self.dev["Shard Rows"] = allgather_shards(self.dist, R[self.rank * n:(self.rank + 1) * n], self.world,
+                                                      self.group)
+
+    def _gather_covariance(self):
+        if self.world == 1:
+            return
+        if self.transport == "device":
+            import torch
+            with torch.cuda.stream(self._stream):
+                self.dist.all_reduce(self._C, op=self.dist.ReduceOp.MAX, group=self.group)
+        else:
+            self.dev["Shard Covariance"] = allreduce_max_bits(self.dist, self.dev["Shard Covariance"], self.group)
 
     def _reduce_partials(self):
         if self.transport == "device":
@@ -126,7 +164,12 @@ class ShardedCmaes:
         d.evaluate(objective)
         self._exchange_fitness()
         d.update_partial(generation)
-        self._reduce_partials()
+        if self.exact:
+            self._exchange_rows()
+            d.update_rows(generation)
+            self._gather_covariance()
+        else:
+            self._reduce_partials()
         d.update_finalize(generation)
 
     def synchronize(self):

@@ -117,7 +117,7 @@ def distributed_engine(**keys):
 @pytest.mark.parametrize("keys,solver,msg", [
     ({"Ranks_Per_Worker": 2}, {}, "'Ranks Per Worker' must be 1"),
     ({"Transport": "MPI"}, {}, "'Transport' must be 'RCCL' or 'Host'"),
-    ({}, {"Covariance Update": "Exact"}, "needs an unsharded run"),
+    ({}, {"Covariance Update": "Cholesky"}, "'Covariance Update' must be 'Exact' or 'MFMA'"),
 ])
 def test_distributed_configuration_errors(monkeypatch, keys, solver, msg):
     for v in ("RANK", "WORLD_SIZE"):

@@ -8,8 +8,10 @@ On the one-GPU box: 2 and 4 ranks share the device over the Host transport
 (TCP bootstrap); the RCCL transport runs with one rank (RCCL refuses two
 ranks on one device).  Every rank's state must equal rank 0's bit for bit;
 TMCMC must equal the unsharded run bit for bit; CMA-ES must reproduce the
-unsharded sort exactly and its mean / covariance / sigma within the
-partial-sum tolerance (include/korali_amd.h: shard sums in another order)."""
+unsharded run bit for bit with the exact covariance update (the default; at
+the C4 shape over 4 generations too), and with MFMA its sort exactly and its
+mean / covariance / sigma within the partial-sum tolerance
+(include/korali_amd.h: shard sums in another order)."""
 import json
 import os
 import socket
@@ -29,10 +31,10 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch(tmp_path, ranks, solver, model, transport):
+def launch(tmp_path, ranks, solver, model, transport, cov):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "tools", "distributed_check.py"),
-           str(tmp_path), solver, model, transport]
+           str(tmp_path), solver, model, transport, cov]
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -44,32 +46,29 @@ def close(a, b, rtol):
     return a.shape == b.shape and np.allclose(a, b, rtol=rtol, atol=rtol * max(1.0, np.abs(b).max()))
 
 
-@pytest.mark.parametrize("ranks,solver,model,transport", [
-    (2, "cmaes", "builtin", "Host"), (4, "cmaes", "host", "Host"), (1, "cmaes", "builtin", "RCCL"),
-    (2, "tmcmc", "builtin", "Host"), (3, "tmcmc", "host", "Host"), (1, "tmcmc", "builtin", "RCCL"),
-    (2, "cmaes", "c4", "Host")])
-def test_distributed_conduit(tmp_path, ranks, solver, model, transport):
-    res = launch(tmp_path, ranks, solver, model, transport)
-    for gens in (("1", "2") if model == "c4" else ("1", "6")):
+@pytest.mark.parametrize("ranks,solver,model,transport,cov", [
+    (2, "cmaes", "builtin", "Host", "Exact"), (4, "cmaes", "host", "Host", "Exact"),
+    (1, "cmaes", "builtin", "RCCL", "Exact"), (2, "cmaes", "c4", "Host", "Exact"),
+    (2, "cmaes", "builtin", "Host", "MFMA"), (1, "cmaes", "builtin", "RCCL", "MFMA"),
+    (2, "tmcmc", "builtin", "Host", "-"), (3, "tmcmc", "host", "Host", "-"), (1, "tmcmc", "builtin", "RCCL", "-")])
+def test_distributed_conduit(tmp_path, ranks, solver, model, transport, cov):
+    res = launch(tmp_path, ranks, solver, model, transport, cov)
+    for gens in (("1", "4") if model == "c4" else ("1", "6")):
         for r in res[1:]:
             assert r[gens]["sharded"] == res[0][gens]["sharded"], gens  # replicated: bit-identical on every rank
         s, u = res[0][gens]["sharded"], res[0][gens]["unsharded"]
         assert s["Current Generation"] == u["Current Generation"] == int(gens)
-        if solver == "tmcmc":
-            assert s == u, gens  # exact gather + replicated processGeneration
+        if solver == "tmcmc" or cov == "Exact":
+            # TMCMC: exact gather + replicated processGeneration; CMA-ES exact:
+            # the selected rows gathered, the reference's summation order
+            assert s == u, gens
             continue
         assert s["Model Evaluation Count"] == u["Model Evaluation Count"]
         if gens == "1":  # same state in: each rank's rows sampled / evaluated as the unsharded run's
             assert s["Value Vector"] == u["Value Vector"]
             assert s["Sorting Index"] == u["Sorting Index"]
             assert s["Best Ever Value"] == u["Best Ever Value"]
-        # per-generation partial-sum rounding, carried 6 generations; at the C4
-        # shape (lambda = 65536 Ackley values, many within rounding of each
-        # other) generation 2's samples move by that rounding and the
-        # near-tied ranks reorder, so only the distribution's scale is compared
-        tol = 1e-12 if gens == "1" else (1e-2 if model == "c4" else 1e-7)
-        keys = ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path")
-        if model == "c4" and gens == "2":
-            keys = ("Current Mean", "Covariance Matrix", "Sigma")  # (the paths follow the reordered selection)
-        for k in keys:
+        # MFMA: per-generation partial-sum rounding, carried 6 generations
+        tol = 1e-12 if gens == "1" else 1e-7
+        for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path"):
             assert close(s[k], u[k], tol), (gens, k)

@@ -185,8 +185,11 @@ def test_engine_reproduces_reference_result_files(tmp_path):
     e = fixture_experiment(out)
     korali.Engine().run(e)
     assert e["Current Generation"] == 100
-    marks = list(e["Internal"]["Generation Completion Times"])  # (bench.py's C4 engine timing)
+    marks = korali._generation_completion_times(e)  # (bench.py's C4 engine timing)
     assert len(marks) == 101 and all(b >= a for a, b in zip(marks, marks[1:]))
+    # the timing marks stay out of the saved experiment (the reference's
+    # setConfiguration rejects unknown keys, experiment.cpp:416)
+    assert "Generation Completion Times" not in read_gen(out, 100).get("Internal", {})
     for ref in CM:
         g = ref["Current Generation"]
         if g == 0:
@@ -722,5 +725,37 @@ def test_vracer_testing_mode_after_training():
         if e["Solver"]["Policy"]["Distribution"] == "Clipped Normal" else {}
     d = VracerDevice(hidden_size=32, hidden_layers=2, environments=16, mini_batch_size=32, replay_maximum_size=1024,
                      replay_start_size=512, initial_exploration_noise=noise, hyperparameters=pol, **bounds)
+    assert np.array_equal(got, d.test_episodes(np.arange(12)))
+    d.close()
+
+
+def test_vracer_testing_mode_uses_the_state_rescaling_moments():
+    """Testing after a State-Rescaling training run: the engine restores the
+    experiment's State Rescaling Means / Sigmas into the agent before the
+    testing episodes (agent.cpp.base:1266-1274, handed to every testing agent
+    at :279-280); the rewards equal the device's testing episodes run
+    directly with that policy and those moments."""
+    import korali
+    from korali_amd.vracer import VracerDevice
+    from vracer_cases import cartpole_vracer
+    e = cartpole_vracer(max_generations=5, environments=16, hidden=32)
+    e["Solver"]["State Rescaling"]["Enabled"] = True
+    korali.Engine().run(e)
+    means = np.array(e["Solver"]["State Rescaling"]["Means"], np.float32)
+    sigmas = np.array(e["Solver"]["State Rescaling"]["Sigmas"], np.float32)
+    assert np.any(means != 0.0) and np.any(sigmas != 1.0)  # the moments were formed
+    pol = np.array(e["Solver"]["Training"]["Current Policy"]["Policy"], np.float32)
+    e["Solver"]["Mode"] = "Testing"
+    e["Solver"]["Testing"]["Sample Ids"] = list(range(12))
+    korali.Engine().run(e)
+    got = np.array(e["Solver"]["Testing"]["Reward"], np.float32)
+    noise = e["Variables"][4]["Initial Exploration Noise"]
+    kw = dict(hidden_size=32, hidden_layers=2, environments=16, mini_batch_size=32, replay_maximum_size=1024,
+              replay_start_size=512, initial_exploration_noise=noise, hyperparameters=pol,
+              policy_distribution="Clipped Normal", action_lower_bound=e["Variables"][4]["Lower Bound"],
+              action_upper_bound=e["Variables"][4]["Upper Bound"])
+    d = VracerDevice(**kw)
+    d.set("state_rescaling_means", means)
+    d.set("state_rescaling_sigmas", sigmas)
     assert np.array_equal(got, d.test_episodes(np.arange(12)))
     d.close()

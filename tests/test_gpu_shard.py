@@ -1,7 +1,9 @@
 """Population sharding on one device: S ranks (gloo,
 host-staged collectives) against the unsharded handle — fitness all-gather,
-replicated sort and state bit-identical across ranks, own rows bit-exact,
-mean / covariance / σ within the partial-sum tolerance."""
+replicated sort and state bit-identical across ranks, own rows bit-exact.
+Exact covariance mode (default): every generation's whole state equal to the
+unsharded exact run with np.array_equal, the runs independent (no state
+copied); MFMA mode: mean / covariance / σ within the partial-sum tolerance."""
 import os
 import socket
 import subprocess
@@ -19,14 +21,19 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("ranks,N,lam,gens,obj,backend,variant", [(2, 32, 256, 6, "rosenbrock", "gloo", "plain"),
-                                                                  (4, 200, 1024, 3, "ackley", "gloo", "plain"),
-                                                                  (1, 64, 512, 4, "rosenbrock", "nccl", "plain"),
-                                                                  (2, 32, 256, 6, "rosenbrock", "gloo", "bounded"),
-                                                                  (2, 32, 256, 6, "rosenbrock", "gloo", "mirrored"),
-                                                                  (3, 24, 192, 6, "rosenbrock", "gloo", "discrete"),
-                                                                  (2, 40, 256, 6, "ackley", "gloo", "diagonal")])
-def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend, variant):
+@pytest.mark.parametrize("ranks,N,lam,gens,obj,backend,variant,cov", [
+    (2, 32, 256, 6, "rosenbrock", "gloo", "plain", "exact"),
+    (4, 200, 1024, 4, "ackley", "gloo", "plain", "exact"),
+    (3, 130, 768, 4, "rosenbrock", "gloo", "plain", "exact"),
+    (1, 64, 512, 4, "rosenbrock", "nccl", "plain", "exact"),
+    (2, 32, 256, 6, "rosenbrock", "gloo", "bounded", "exact"),
+    (2, 32, 256, 6, "rosenbrock", "gloo", "mirrored", "exact"),
+    (3, 24, 192, 6, "rosenbrock", "gloo", "discrete", "exact"),
+    (2, 40, 256, 6, "ackley", "gloo", "diagonal", "exact"),
+    (2, 32, 256, 6, "rosenbrock", "gloo", "plain", "mfma"),
+    (4, 200, 1024, 3, "ackley", "gloo", "plain", "mfma"),
+    (1, 64, 512, 4, "rosenbrock", "nccl", "plain", "mfma")])
+def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend, variant, cov):
     """gloo: several ranks on the one device, host-staged collectives;
     nccl: the RCCL zero-copy device transport (one rank: one device here).
     Variants bounded / mirrored / discrete / diagonal: every rank draws the
@@ -34,7 +41,7 @@ def test_sharded_population_matches_unsharded(ranks, N, lam, gens, obj, backend,
     mutations are sequential over it) and evaluates and sums its own rows."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "tools", "shard_check.py"),
-           str(N), str(lam), str(gens), obj, backend, variant]
+           str(N), str(lam), str(gens), obj, backend, variant, cov]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "SHARD_CHECK PASS" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

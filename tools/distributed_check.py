@@ -2,16 +2,16 @@
 test_gpu_distributed.py launches it with torch.distributed.run): runs the
 experiment on the Distributed conduit, then the same experiment unsharded on
 the Sequential conduit, after 1 and after 6 generations, and writes the
-solver states to <out>/rank<r>.json.  The test compares them (TMCMC:
-bit-identical; CMA-ES: the first generation's samples, fitness and sort
-bit-identical and mean / covariance / sigma within the partial-sum
-tolerance, the 6-generation run close) and every rank's state against rank
-0's (bit-identical).
+solver states to <out>/rank<r>.json.  The test compares them (TMCMC and
+CMA-ES with the exact covariance update: bit-identical; CMA-ES with MFMA:
+the first generation's samples, fitness and sort bit-identical and mean /
+covariance / sigma within the partial-sum tolerance) and every rank's state
+against rank 0's (bit-identical).
 
-    distributed_check.py <out dir> cmaes|tmcmc builtin|host|c4 RCCL|Host
+    distributed_check.py <out dir> cmaes|tmcmc builtin|host|c4 RCCL|Host [Exact|MFMA]
 
 model c4 (CMA-ES only): the C4 shape, 512-dim negative Ackley at
-lambda = 65536 (BASELINE.json configs[3]), after 1 and 2 generations.
+lambda = 65536 (BASELINE.json configs[3]), after 1 and 4 generations.
 """
 import json
 import os
@@ -34,7 +34,7 @@ def gaussian(s):  # the builtin Gaussian likelihood, -0.5 * sum(x^2)
     s["logLikelihood"] = -0.5 * sum(v * v for v in s["Parameters"])
 
 
-def experiment(solver, model, gens):
+def experiment(solver, model, gens, cov="Exact"):
     e = korali.Experiment()
     e["Random Seed"] = 4242
     e["File Output"]["Enabled"] = False
@@ -54,7 +54,7 @@ def experiment(solver, model, gens):
             e["Variables"][i]["Initial Standard Deviation"] = 1.0
         e["Solver"]["Type"] = "Optimizer/CMAES"
         e["Solver"]["Population Size"] = 65536 if model == "c4" else 64
-        e["Solver"]["Covariance Update"] = "MFMA"  # the rank-mu tiles the sharded update sums per shard
+        e["Solver"]["Covariance Update"] = cov
         e["Solver"]["Termination Criteria"]["Max Generations"] = gens
     else:
         e["Problem"]["Type"] = "Bayesian/Custom"
@@ -83,15 +83,16 @@ def state(e, solver):
 
 def main():
     out, solver, model, transport = sys.argv[1:5]
+    cov = sys.argv[5] if len(sys.argv) > 5 else "Exact"
     rank = int(os.environ["RANK"])
     result = {}
-    for gens in ((1, 2) if model == "c4" else (1, 6)):  # one generation: same samples; six: the run as a whole
+    for gens in ((1, 4) if model == "c4" else (1, 6)):  # one generation: same samples; more: the run as a whole
         k = korali.Engine()
         k["Conduit"]["Type"] = "Distributed"
         k["Conduit"]["Transport"] = transport
-        e = experiment(solver, model, gens)
+        e = experiment(solver, model, gens, cov)
         k.run(e)
-        u = experiment(solver, model, gens)
+        u = experiment(solver, model, gens, cov)
         korali.Engine().run(u)
         result[str(gens)] = {"sharded": state(e, solver), "unsharded": state(u, solver)}
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:

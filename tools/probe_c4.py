@@ -6,8 +6,9 @@ from korali_amd.native import CmaesDevice
 
 N, L = int(sys.argv[1]) if len(sys.argv) > 1 else 512, int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 gens = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+cov = sys.argv[4] if len(sys.argv) > 4 else "mfma"
 dev = CmaesDevice(N, L, initial_value=np.full(N, 2.0), initial_std=np.ones(N), normal_seed=1337, uniform_seed=1338,
-                  cov_mode="mfma")
+                  cov_mode=cov)
 t0 = time.perf_counter()
 dev.generation(1, "ackley"); dev.synchronize()
 print("gen1 %.1f ms" % ((time.perf_counter() - t0) * 1e3), flush=True)

@@ -1,7 +1,18 @@
 """Population-sharding check (run under torch.distributed.run, gloo, any
 number of ranks on one device): S ranks run a sharded CMA-ES; rank 0 also
 runs the unsharded handle from the same seed and compares every generation.
-Exit code 0 = pass.  Used by tests/test_gpu_shard.py."""
+Exit code 0 = pass.  Used by tests/test_gpu_shard.py.
+
+    shard_check.py N lambda generations objective gloo|nccl variant [exact|mfma]
+
+exact (default): the exact-order sharded update; the sharded run must equal
+the unsharded exact run (the reference's trajectory, which the unsharded
+handle reproduces bit for bit, tests/test_gpu_cmaes.py) in every compared
+field with np.array_equal, generation after generation, with no state
+copied between them.  mfma: per-shard partial sums; each generation is
+compared at the partial-sum tolerance and the sharded ranks then continue
+from the unsharded state (the two summation orders drift apart by rounding,
+which a run carries forward)."""
 import os
 import sys
 
@@ -21,6 +32,7 @@ def main():
     # every rank draws whole (finite bounds with redraws, Mirrored Sampling,
     # discrete variables, diagonal covariance)
     variant = sys.argv[6] if len(sys.argv) > 6 else "plain"
+    cov = sys.argv[7] if len(sys.argv) > 7 else "exact"
     if backend == "nccl":
         # RCCL with the zero-copy device transport (one rank per device)
         import torch
@@ -41,8 +53,8 @@ def main():
         kw.update(diagonal=True)
     elif variant != "plain":
         raise SystemExit(f"unknown variant {variant}")
-    sh = ShardedCmaes(N, lam, dist, device=0, transport="device" if backend == "nccl" else "host", **kw)
-    ref = CmaesDevice(N, lam, cov_mode="mfma", **kw) if rank == 0 else None
+    sh = ShardedCmaes(N, lam, dist, device=0, transport="device" if backend == "nccl" else "host", cov_mode=cov, **kw)
+    ref = CmaesDevice(N, lam, cov_mode=cov, **kw) if rank == 0 else None
     ok = True
     for g in range(1, gens + 1):
         sh.generation(g, obj)
@@ -72,21 +84,34 @@ def main():
             if sh.dev["Infeasible Sample Count"][0] != ref["Infeasible Sample Count"][0]:
                 print(f"gen {g}: infeasible sample count differs", flush=True)
                 ok = False
-            for k, tol in (("Current Mean", 1e-12), ("Covariance Matrix", 1e-11), ("Sigma", 1e-12),
-                           ("Best Ever Variables", 0.0)):
-                a, b = sh.dev[k], ref[k]
-                rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
-                if rel > tol:
-                    print(f"gen {g}: {k} rel diff {rel:.3e} > {tol}", flush=True)
-                    ok = False
-            # teacher-force: continue from the unsharded state on every rank
-            st = {k: ref[k] for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path",
-                                      "Conjugate Evolution Path", "Best Ever Variables", "Best Ever Value")}
+            if cov == "exact":
+                for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path",
+                          "Best Ever Variables", "Best Ever Value", "Current Best Variables", "Axis Lengths",
+                          "Covariance Eigenvector Matrix", "Mean Update"):
+                    if not np.array_equal(sh.dev[k], ref[k]):
+                        print(f"gen {g}: {k} differs from the unsharded exact run", flush=True)
+                        ok = False
+                for which in (0, 1):
+                    if sh.dev.get_rng(which) != ref.get_rng(which):
+                        print(f"gen {g}: generator {which} state differs", flush=True)
+                        ok = False
+                st = None  # no state is copied: the runs proceed independently
+            else:
+                for k, tol in (("Current Mean", 1e-12), ("Covariance Matrix", 1e-11), ("Sigma", 1e-12),
+                               ("Best Ever Variables", 0.0)):
+                    a, b = sh.dev[k], ref[k]
+                    rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+                    if rel > tol:
+                        print(f"gen {g}: {k} rel diff {rel:.3e} > {tol}", flush=True)
+                        ok = False
+                # teacher-force: continue from the unsharded state on every rank
+                st = {k: ref[k] for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path",
+                                          "Conjugate Evolution Path", "Best Ever Variables", "Best Ever Value")}
         else:
             st = None
         box = [st]
         dist.broadcast_object_list(box, src=0)
-        for k, v in box[0].items():
+        for k, v in (box[0] or {}).items():
             sh.dev[k] = v
     flag = [ok]
     dist.broadcast_object_list(flag, src=0)
