@@ -11,9 +11,16 @@ Everything runs on the device; the host only enqueues.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--cov exact|mfma]
 
-N > 1: launched by torch.distributed.run, one process per GPU; every rank
-runs its own C2 experiment (seed 1337 + rank) — "replicas", weak scaling;
+N > 1: one process per GPU — launched by torch.distributed.run (RANK /
+WORLD_SIZE set), or, when WORLD_SIZE is unset, bench.py starts the N rank
+processes itself before touching the GPU.  Every rank runs its own C2
+experiment (seed 1337 + rank) — "replicas", weak scaling, no collective on
+the data path (λ = 4096 fits one GPU many times over; DESIGN.md §6);
 value = total generations/s over all ranks (max-over-ranks wall time).
+Beside it, `c4_sharded`: the C4 experiment (512-dim Ackley, λ = 65536)
+through korali.Engine on one rank and sharded over all N ranks (the
+Distributed conduit, exact covariance order), its rates and speed-up, and
+whether the two runs ended bit-identical.
 
 The JSON line also carries `roofline` for the dominant kernel (algorithmic
 FLOPs per launch / its HIP-event time on the solver's stream) and
@@ -279,6 +286,81 @@ def engine_rate(steps, warmup, cov):
     return diff, e2e, in_run
 
 
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets
+    them) before this process touches the GPU, and exit with the worst
+    return code.  Rank 0 prints the JSON line."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def rank_device(local_rank):
+    """The GPU of a rank: LOCAL_RANK, folded onto the visible devices (several
+    ranks share one device when there are fewer GPUs than ranks)."""
+    import torch
+    n = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+    return local_rank % max(1, n), n
+
+
+def c4_scaling(args, world, rank, dist):
+    """The C4 experiment through korali.Engine on rank 0 alone (Sequential
+    conduit) and sharded over all ranks (Distributed conduit, exact
+    covariance order); generations/s of each over the last `steps`
+    generations (the engine's completion marks, slowest rank), the speed-up,
+    and whether both runs end in the same state bit for bit."""
+    import korali
+    import torch
+    steps, w = max(2, min(args.steps, 10)), 2
+    total = w + steps
+
+    def rate(e):
+        marks = korali._generation_completion_times(e)
+        return marks[total] - marks[w]
+
+    one, state1 = None, None
+    if rank == 0:
+        e1 = c4_experiment(total, "Exact")
+        korali.Engine().run(e1)
+        one = steps / rate(e1)
+        state1 = [e1["Solver"][k] for k in ("Current Mean", "Covariance Matrix", "Sigma")]
+    dist.barrier()
+    devs = rank_device(int(os.environ.get("LOCAL_RANK", "0")))[1]
+    transport = "RCCL" if devs >= world else "Host"  # (RCCL refuses two ranks on one device)
+    k = korali.Engine()
+    k["Conduit"]["Type"] = "Distributed"
+    k["Conduit"]["Transport"] = transport
+    eN = c4_experiment(total, "Exact")
+    k.run(eN)
+    t = torch.tensor([rate(eN)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank != 0:
+        return None
+    many = steps / float(t.item())
+    same = state1 == [eN["Solver"][k] for k in ("Current Mean", "Covariance Matrix", "Sigma")]
+    return {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768, Exact covariance order, "
+                        "korali.Engine", "ranks": world, "transport": transport, "steps": steps, "warmup": w,
+            "generations_per_sec_1_rank": one, f"generations_per_sec_{world}_ranks": many, "speedup": many / one,
+            "bit_identical_to_1_rank": bool(same), "scaling": "strong",
+            "note": "the eigendecomposition (GSL order, ~11.4 ms of an 18.3 ms 1-GPU generation) is replicated on "
+                    "every rank, which bounds the speed-up at about 1.4x for any rank count (DESIGN.md §6)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -292,6 +374,10 @@ def main():
                     help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192; c4: CMA-ES 512-dim Ackley, "
                          "lambda=65536, population sharded over the ranks; c5: VRACER, 4096 CartPole rollouts")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.workload in ("c2", "c4"):
+        sys.exit(spawn_ranks(args.gpus))
+    if args.workload in ("c3", "c5") and args.gpus > 1:
+        raise SystemExit(f"--workload {args.workload} runs on one GPU (replicas only: start one bench per GPU)")
     if args.workload == "c3":
         return run_c3(args)
     if args.workload == "c4":
@@ -303,13 +389,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = 0
     if world > 1:
         import torch
         import torch.distributed as dist_mod
 
         dist = dist_mod
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        device, _ = rank_device(local_rank)
+        torch.cuda.set_device(device)
+        # replicas: the process group only times (barrier, max over ranks);
+        # no collective touches the solver's data
+        dist.init_process_group("gloo")
 
     from korali_amd import _build
     from korali_amd.native import CmaesDevice
@@ -318,8 +408,7 @@ def main():
         _build.build()
 
     dev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
-                      normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=args.cov,
-                      device=local_rank if world > 1 else 0)
+                      normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=args.cov, device=device)
     gen = 0
     for _ in range(args.warmup):
         gen += 1
@@ -328,8 +417,7 @@ def main():
 
     def barrier():
         if dist is not None:
-            import torch
-            torch.cuda.synchronize()
+            dev.synchronize()
             dist.barrier()
 
     barrier()
@@ -342,7 +430,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -370,8 +458,7 @@ def main():
     # the other covariance mode on this rank alone (reported beside `value`)
     alt = "mfma" if args.cov == "exact" else "exact"
     adev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
-                       normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=alt,
-                       device=local_rank if world > 1 else 0)
+                       normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=alt, device=device)
     g2 = 0
     for _ in range(args.warmup):
         g2 += 1
@@ -400,9 +487,9 @@ def main():
             ms = ms / n if pdev is not None else ms
             mfma_kernel = rankmu_roofline(ms, MU, N_VARS, "c2_pmc_traffic.csv")
     adev.close()
+    c4 = c4_scaling(args, world, rank, dist) if dist is not None else None
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
         return
 
     gens_per_s = args.steps * world / elapsed
@@ -443,6 +530,7 @@ def main():
         "engine_in_run_generations_per_sec": eng_in_run,
         f"{alt}_covariance_generations_per_sec_per_gpu": alt_rate,
         "rankmu_mfma_roofline": mfma_kernel,
+        "c4_sharded": c4,
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
@@ -627,7 +715,7 @@ def c4_cpu_baseline():
                       f"1 warm-up, oracle/refcpu.c -O3 with system libm, 1 thread"}
 
 
-def c4_experiment(generations):
+def c4_experiment(generations, cov="MFMA"):
     import korali
     e = korali.Experiment()
     e["Problem"]["Type"] = "Optimization"
@@ -638,7 +726,7 @@ def c4_experiment(generations):
         e["Variables"][i]["Initial Standard Deviation"] = 1.0
     e["Solver"]["Type"] = "Optimizer/CMAES"
     e["Solver"]["Population Size"] = C4_L
-    e["Solver"]["Covariance Update"] = "MFMA"
+    e["Solver"]["Covariance Update"] = cov
     e["Solver"]["Termination Criteria"]["Max Generations"] = generations
     e["Random Seed"] = 1337
     e["File Output"]["Enabled"] = False
@@ -666,13 +754,14 @@ def run_c4_engine(args, world, rank):
     os.environ.setdefault("RANK", str(rank))
     os.environ.setdefault("WORLD_SIZE", str(world))
     tdist.init_process_group("gloo")  # (timing exchange only; the engine brings its own bootstrap + RCCL)
-    transport = os.environ.get("KORALI_AMD_C4_TRANSPORT", "RCCL")
+    transport = os.environ.get("KORALI_AMD_C4_TRANSPORT",
+                               "RCCL" if rank_device(int(os.environ.get("LOCAL_RANK", "0")))[1] >= world else "Host")
     w = max(1, args.warmup)
     total = w + args.steps
     k = korali.Engine()
     k["Conduit"]["Type"] = "Distributed"
     k["Conduit"]["Transport"] = transport
-    e = c4_experiment(total)
+    e = c4_experiment(total, "Exact" if args.cov == "exact" else "MFMA")
     tdist.barrier()
     k.run(e)
     marks = korali._generation_completion_times(e)
@@ -691,7 +780,7 @@ def run_c4_engine(args, world, rank):
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768 Logarithmic, x0=2, "
                                    "sigma0=1, seed 1337; korali.Engine, Distributed conduit (" + transport + ")",
-                       "parallelism": f"population-shard{world}"},
+                       "parallelism": f"population-shard{world}", "covariance_update": args.cov},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
             "timing": "generations %d-%d of one %d-generation engine run (engine completion marks), slowest rank"
                       % (w + 1, total, total),
@@ -720,11 +809,11 @@ def run_c4(args):
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         from korali_amd.sharded import ShardedCmaes
-        solver = ShardedCmaes(C4_N, C4_L, dist, device=local_rank, transport="device", **kw)
+        solver = ShardedCmaes(C4_N, C4_L, dist, device=local_rank, transport="device", cov_mode=args.cov, **kw)
         dev = solver.dev
     else:
         from korali_amd.native import CmaesDevice
-        dev = CmaesDevice(C4_N, C4_L, cov_mode="mfma", **kw)
+        dev = CmaesDevice(C4_N, C4_L, cov_mode=args.cov, **kw)
         solver = dev
 
     def step(g):
@@ -774,7 +863,8 @@ def run_c4(args):
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": "C4: CMA-ES, 512-dim negative Ackley, lambda=65536, mu=32768 Logarithmic, x0=2, "
-                                   "sigma0=1, seed 1337", "parallelism": f"population-shard{world}"},
+                                   "sigma0=1, seed 1337", "parallelism": f"population-shard{world}",
+                       "covariance_update": args.cov},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
             "stage_ms_rank0": stages,
             "rankmu_mfma_roofline": rankmu_roofline(stages["rankmu_mfma"], C4_L // 2, C4_N, "c4_pmc_traffic.csv")
