@@ -1869,16 +1869,19 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
 // stride 129: column and row walks both conflict-free), the two ordered
 // matrix-vector chains and the |p_sigma| chain on the chain primitives.
 constexpr int PA2_LD = 129;
-size_t paths2_lds_bytes(int N) { return ((size_t)(N + 16) * PA2_LD + 3 * (size_t)(N + 32)) * sizeof(double); }
+// (the vectors start 16-byte aligned: kc_lock_asc reads w in pairs)
+__host__ __device__ inline size_t paths2_vec(int N) { return ((size_t)N + 33) & ~(size_t)1; }
+__host__ __device__ inline size_t paths2_bs(int N) { return ((size_t)(N + 16) * PA2_LD + 1) & ~(size_t)1; }
+size_t paths2_lds_bytes(int N) { return (paths2_bs(N) + 3 * paths2_vec(N)) * sizeof(double); }
 __global__ void __launch_bounds__(256) k_paths2(int N, unsigned long long gen, const double *__restrict__ B,
                                                 const double *__restrict__ D, const double *__restrict__ meanUpdate,
                                                 double *auxBDZ, double *ps, double *pc, CmaesScalars *sc) {
   extern __shared__ __attribute__((aligned(16))) double psm[];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   double *Bs = psm;                                // (N+16) x 129, zero padded
-  double *sv = Bs + (size_t)(N + 16) * PA2_LD;     // mean update, zero past N
-  double *aux = sv + N + 32;                       // D^-1 B^T (mean update), zero past N
-  double *pn = aux + N + 32;                       // p_sigma squares, zero past N
+  double *sv = Bs + paths2_bs(N);                  // mean update, zero past N
+  double *aux = sv + paths2_vec(N);                // D^-1 B^T (mean update), zero past N
+  double *pn = aux + paths2_vec(N);                // p_sigma squares, zero past N
   __shared__ int hs;
   const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
   // eight loads in flight per thread (one at a time, the L2 round trips were the kernel's time)
@@ -1895,7 +1898,7 @@ __global__ void __launch_bounds__(256) k_paths2(int N, unsigned long long gen, c
       if (q < (N + 16) * PA2_LD) Bs[q] = v[u];
     }
   }
-  for (int q = tid; q < 3 * (N + 32); q += 256) sv[q] = (q < N) ? meanUpdate[q] : 0.0;
+  for (int q = tid; q < 3 * (int)paths2_vec(N); q += 256) sv[q] = (q < N) ? meanUpdate[q] : 0.0;
   __syncthreads();
   const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)(N + 7) >> 3);
   const int d = lane + 64 * (wid & 1);  // waves 0-1: rows d < 128

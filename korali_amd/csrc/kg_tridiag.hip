@@ -37,7 +37,8 @@ constexpr int SQ_LDA = 130;  // row stride for every N <= 128 (ds_read offsets a
                              // 130: 16-byte row reads of 64 lanes hit every bank equally
 constexpr int SQ_VP = 16;    // zero padding before / after each vector (chain read-ahead)
 
-__host__ __device__ inline size_t sq_vec(int N) { return (size_t)N + 2 * SQ_VP; }
+// (even: every vector starts 16-byte aligned, for the chains' ds_read_b128 pairs)
+__host__ __device__ inline size_t sq_vec(int N) { return ((size_t)N + 2 * SQ_VP + 1) & ~(size_t)1; }
 __host__ __device__ inline size_t sq_lds_doubles(int N) {
   // M (N+16 rows) | dg | va[2] | tva[2] | xa | xd 128 | t2 128 | sv 160 | scal 16
   return (size_t)(N + 16) * SQ_LDA + 6 * sq_vec(N) + 128 + 128 + 160 + 16;
@@ -193,6 +194,7 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       }
       if (lane == 0) {
         gH[(size_t)i * N] = v0out;
+        va[i] = 0.0;  // (the ascending walk may start one column early, at an even column)
         va[i + 1] = 1.0;
         tva[i + 1] = tau_i * 1.0;
         scal[0] = tau_i;
@@ -221,20 +223,25 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       const bool valid = j < n;
       const int r = valid ? i + 1 + j : N;
       if (wid < 2) {
-        // columns c = N-1 down to r+1 (lockstep from N-1 to i+2+64h), then the diagonal term
-        const int T = n - 1 - 64 * h;
-        const unsigned nb = __builtin_amdgcn_readfirstlane(T > 0 ? (unsigned)(T + 7) >> 3 : 0u);
-        const double acc = chains::kc_lock_desc(0.0, lds_addr(tva + (N - 8)), lds_addr(M + (size_t)r * lda + (N - 8)), nb);
+        // columns c = N-1 down to r+1 (lockstep from N-1 to i+2+64h), then the
+        // diagonal term; with N odd the walk starts at the zero column N, so
+        // that every pair it reads is 16-byte aligned
+        const int T = n - 1 - 64 * h, top = N | 1, Tw = T + (top - (N - 1));
+        const unsigned nb = __builtin_amdgcn_readfirstlane(T > 0 ? (unsigned)(Tw + 7) >> 3 : 0u);
+        const double acc =
+            chains::kc_lock_desc(0.0, lds_addr(tva + (top - 7)), lds_addr(M + (size_t)r * lda + (top - 7)), nb);
         if (valid) {
           xdj = acc + tva[r] * dg[r];
           if (h) xd[j] = xdj;
         }
       } else {
-        // columns c = i+1 up to r-1 (lockstep up to the wave's largest row)
-        const int T = (64 * h < n) ? min(n, 64 * h + 64) - 1 : 0;
-        const unsigned nb = __builtin_amdgcn_readfirstlane(T > 0 ? (unsigned)(T + 7) >> 3 : 0u);
+        // columns c = i+1 up to r-1 (lockstep up to the wave's largest row);
+        // from the even column c0 (c0 = i: v_i = 0 this step, a +-0 no-op
+        // product), so that every w pair is 16-byte aligned
+        const int T = (64 * h < n) ? min(n, 64 * h + 64) - 1 : 0, c0 = (i + 1) & ~1, Tw = T + (i + 1 - c0);
+        const unsigned nb = __builtin_amdgcn_readfirstlane(T > 0 ? (unsigned)(Tw + 7) >> 3 : 0u);
         const double acc =
-            chains::kc_lock_asc<SQ_LDA * 8>(0.0, lds_addr(va + i + 1), lds_addr(M + (size_t)(i + 1) * lda + r), nb);
+            chains::kc_lock_asc<SQ_LDA * 8>(0.0, lds_addr(va + c0), lds_addr(M + (size_t)c0 * lda + r), nb);
         if (valid) t2[j] = acc;
       }
     }
@@ -579,12 +586,36 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
         if (ch < RW) {
           // columns c = N-1 down to r+1, then the diagonal term
           const unsigned G = __builtin_amdgcn_readfirstlane((unsigned)(N - 1 - r + 15) >> 4);
-          const double acc = chains::kc_add_desc(0.0, lds_addr(Pd + (size_t)k * PS + (N - 16)), G);
+          double acc = 0.0;
+          if (kDpp) {
+            // 128 staged products per block into registers (element e = column
+            // N-1-e in lane e % 16 of q[e / 16 % 8]), then the DPP chain
+            const double *pd = Pd + (size_t)k * PS;
+            for (unsigned b = 0; 8 * b < G; b++) {
+              double q[8];
+#pragma unroll
+              for (int kk = 0; kk < 8; kk++) q[kk] = pd[max(N - 1 - (int)(128 * b) - 16 * kk - (lane & 15), -MW2_PAD)];
+              acc = chains::kc_add_dpp(acc, q, __builtin_amdgcn_readfirstlane(min(8u, G - 8 * b)));
+            }
+          } else {
+            acc = chains::kc_add_desc(0.0, lds_addr(Pd + (size_t)k * PS + (N - 16)), G);
+          }
           if (lane == 0) accb[k] = acc + tv[r - i - 1] * M[(size_t)k * lda + r];
         } else {
           // columns c = i+1 up to r-1
           const unsigned G = __builtin_amdgcn_readfirstlane((unsigned)(r - i - 1 + 15) >> 4);
-          const double acc = chains::kc_add(0.0, lds_addr(Pa + (size_t)k * PS + (i + 1)), G);
+          double acc = 0.0;
+          if (kDpp) {
+            const double *pa = Pa + (size_t)k * PS;
+            for (unsigned b = 0; 8 * b < G; b++) {
+              double q[8];
+#pragma unroll
+              for (int kk = 0; kk < 8; kk++) q[kk] = pa[min(i + 1 + (int)(128 * b) + 16 * kk + (lane & 15), N + MW2_PAD - 1)];
+              acc = chains::kc_add_dpp(acc, q, __builtin_amdgcn_readfirstlane(min(8u, G - 8 * b)));
+            }
+          } else {
+            acc = chains::kc_add(0.0, lds_addr(Pa + (size_t)k * PS + (i + 1)), G);
+          }
           if (lane == 0) t2b[k] = acc;
         }
       }

@@ -181,18 +181,22 @@ def emit_lock(desc):
     rounded, then added): w wave-uniform (broadcast LDS reads), m per lane.
     8-element batches, the next batch's loads in flight while the current
     one is multiplied and added (set A: w slots 0-7, m 8-15; set B: w
-    16-23, m 24-31)."""
+    16-23, m 24-31).  Pairs of elements come in one ds_read_b128 (4 LDS
+    cycles per wave-instruction, 256 B/clk; ds_read2_b64 takes 8 for the same
+    16 bytes per lane, MI355X_MICROARCH.md §LDS): w always, m of the
+    descending walk (two consecutive columns of the row); the ascending
+    walk's m is a column (one ds_read_b64 per element, 2 cycles).  Callers
+    keep every pair 16-byte aligned."""
 
     def load(setb):
         ws, ms = (16, 24) if setb else (0, 8)
         out = []
         for k in range(4):
-            if desc:  # element t at byte offset (7 - t) * 8 above the batch base
-                o0, o1 = 7 - 2 * k, 6 - 2 * k
-                out.append(f"ds_read2_b64 {q(ws // 2 + k)}, %[pw] offset0:{o0} offset1:{o1}")
-                out.append(f"ds_read2_b64 {q(ms // 2 + k)}, %[pm] offset0:{o0} offset1:{o1}")
+            if desc:  # element t at byte offset (7 - t) * 8 above the batch base: pair k = offsets 6-2k, 7-2k
+                out.append(f"ds_read_b128 {q(ws // 2 + k)}, %[pw] offset:{(6 - 2 * k) * 8}")
+                out.append(f"ds_read_b128 {q(ms // 2 + k)}, %[pm] offset:{(6 - 2 * k) * 8}")
             else:
-                out.append(f"ds_read2_b64 {q(ws // 2 + k)}, %[pw] offset0:{2 * k} offset1:{2 * k + 1}")
+                out.append(f"ds_read_b128 {q(ws // 2 + k)}, %[pw] offset:{16 * k}")
                 out.append(f"ds_read_b64 {d(ms + 2 * k)}, %[pm] offset:%[o{2 * k}]")
                 out.append(f"ds_read_b64 {d(ms + 2 * k + 1)}, %[pm] offset:%[o{2 * k + 1}]")
         if desc:
@@ -209,12 +213,13 @@ def emit_lock(desc):
         li = 0
         per = (len(loads) + 7) // 8
         for t in range(8):
-            out.append(f"v_mul_f64 {d(ws + t)}, {d(ws + t)}, {d(ms + t)}")
+            sl = (t ^ 1) if desc else t  # descending: the pair's high element (the higher column) first
+            out.append(f"v_mul_f64 {d(ws + sl)}, {d(ws + sl)}, {d(ms + sl)}")
             for _ in range(per):  # the other set's loads fill this batch's stall slots
                 if li < len(loads):
                     out.append(loads[li])
                     li += 1
-            out.append(f"v_add_f64 %[acc], %[acc], {d(ws + t)}")
+            out.append(f"v_add_f64 %[acc], %[acc], {d(ws + sl)}")
         out += loads[li:]
         return out
 
@@ -231,7 +236,8 @@ def emit_lock(desc):
 // per-lane chain acc + w[top] m[top] + w[top-1] m[top-1] + ... over 8 nb
 // elements (each product rounded, then added: gslcblas dsymv's descending
 // column walk).  pw / pm = LDS byte addresses of element top-7 (w uniform,
-// m per lane); the loads run one batch below the last element.
+// m per lane), both 16-byte aligned; the loads run one batch below the last
+// element.
 __device__ __forceinline__ double kc_lock_desc(double acc, unsigned pw, unsigned pm, unsigned nb) {{
   asm volatile(
 {body}
@@ -245,8 +251,8 @@ __device__ __forceinline__ double kc_lock_desc(double acc, unsigned pw, unsigned
     return f"""
 // per-lane chain acc + w[0] m[0] + w[1] m[S] + w[2] m[2 S] + ... over 8 nb
 // elements (gslcblas dsymv's ascending t2 walk).  pw = LDS byte address of
-// w[0] (uniform), pm = per-lane LDS byte address of m[0], S = the m stride
-// in bytes; the loads run one batch past the last element.
+// w[0] (uniform, 16-byte aligned), pm = per-lane LDS byte address of m[0],
+// S = the m stride in bytes; the loads run one batch past the last element.
 template <int S>
 __device__ __forceinline__ double kc_lock_asc(double acc, unsigned pw, unsigned pm, unsigned nb) {{
   asm volatile(
@@ -353,7 +359,65 @@ __device__ __forceinline__ double kc_row16(double acc, double q) {{
   return acc;
 }}
 """
-    return add + nrm2 + row16
+    # experimental forms of the ssq recurrence (tools/ubench_chains.hip modes
+    # 21-25 compare them with kc_nrm2_dpp):
+    # (1) per-element check: every element tests its mask bit (no half-level
+    #     fast path), the rescale bodies out of line
+    L = ["s_nop 1"]
+    slow = []
+    for e in range(128):
+        k, j = e // 16, e % 16
+        w, b = words[e // 32], e % 32
+        if e % 16 == 0:
+            L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
+        L += [f"s_bitcmp1_b32 {w}, {b}", f"s_cbranch_scc1 {300 + e}f", fast(e), f"{500 + e}:"]
+        slow += [f"{300 + e}:", f"v_mov_b64 %[x], %[q{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+                 "v_mul_f64 %[tmp], %[acc], %[x]", "v_mul_f64 %[tmp], %[tmp], %[x]",
+                 "v_add_f64 %[acc], 1.0, %[tmp]", f"s_branch {500 + e}b"]
+    L += ["s_branch 9f"] + slow + ["9:"]
+    nrm2c = f"""
+// (experimental) kc_nrm2_dpp with a mask test per element instead of per half
+__device__ __forceinline__ double kc_nrm2_dppc(double acc, const double (&q)[8], unsigned g, unsigned long long k0,
+                                               unsigned long long k1) {{
+  const unsigned k0l = __builtin_amdgcn_readfirstlane((unsigned)k0), k0h = __builtin_amdgcn_readfirstlane((unsigned)(k0 >> 32));
+  const unsigned k1l = __builtin_amdgcn_readfirstlane((unsigned)k1), k1h = __builtin_amdgcn_readfirstlane((unsigned)(k1 >> 32));
+  const double one = 1.0;
+  double tmp, x;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+&v"(acc), [g] "+&s"(g), [tmp] "=&v"(tmp), [x] "=&v"(x)
+      : {qs}, [one] "v"(one), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
+      : "scc");
+  return acc;
+}}
+"""
+    # (2) branch-free: every element as u = ssq a, w = u a, ssq = w + c with
+    #     (a, c) = (t, 1) at a new running maximum and (1, t) elsewhere (ssq
+    #     times 1.0 is exact, so a plain element is ssq + t rounded once)
+    qa = ", ".join(f"[a{k}] \"v\"(a[{k}])" for k in range(8))
+    qc = ", ".join(f"[c{k}] \"v\"(c[{k}])" for k in range(8))
+    L = ["s_nop 1"]
+    for e in range(128):
+        k, j = e // 16, e % 16
+        if e % 16 == 0:
+            L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
+        L += [f"v_mov_b64 %[xa], %[a{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+              f"v_mov_b64 %[xc], %[c{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+              "v_mul_f64 %[tmp], %[acc], %[xa]", "v_mul_f64 %[tmp], %[tmp], %[xa]", "v_add_f64 %[acc], %[tmp], %[xc]"]
+    L += ["9:"]
+    nrm23 = f"""
+// (experimental) the branch-free three-operation form of the ssq recurrence
+__device__ __forceinline__ double kc_nrm2_dpp3(double acc, const double (&a)[8], const double (&c)[8], unsigned g) {{
+  double tmp, xa, xc;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+&v"(acc), [g] "+&s"(g), [tmp] "=&v"(tmp), [xa] "=&v"(xa), [xc] "=&v"(xc)
+      : {qa}, {qc}
+      : "scc");
+  return acc;
+}}
+"""
+    return add + nrm2 + row16 + nrm2c + nrm23
 
 
 def main():

@@ -15,7 +15,7 @@ __device__ __forceinline__ unsigned la(const double *p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) double *)p;
 }
 
-constexpr int LD = 129;
+constexpr int LD = 130;  // (even: 16-byte aligned row pairs for the ds_read_b128 chains)
 
 // mode: 0 kc_add alone, 1 kc_add + 7 waves of LDS read/modify/write traffic,
 // 2 kc_nrm2 alone (no rescale), 3 kc_lock_desc on wave 0 alone,
@@ -199,6 +199,25 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
       }
       t1 = __builtin_amdgcn_s_memtime();
     }
+  } else if (mode >= 21 && mode <= 25) {
+    // the ssq recurrence on register-held elements: kc_nrm2_dpp without /
+    // with three rescale events (elements 5, 40, 90: three different
+    // halves), the per-element-check form without / with them, and the
+    // branch-free three-operation form
+    if (wid == 0) {
+      double q[8], a[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) q[k] = stage[16 * k + (lane & 15)], a[k] = 1.0;
+      const bool ev = mode == 22 || mode == 25;
+      const unsigned long long k0 = ev ? ((1ull << 5) | (1ull << 40)) : 0ull, k1 = ev ? (1ull << 26) : 0ull;
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) {
+        if (mode == 21 || mode == 22) acc = kc_nrm2_dpp(acc + 1.0, q, 8u, k0, k1);
+        else if (mode == 23) acc = kc_nrm2_dpp3(acc + 1.0, a, q, 8u);
+        else acc = kc_nrm2_dppc(acc + 1.0, q, 8u, k0, k1);
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
   } else if (mode == 6) {
     if (wid == 0) {
       double b = stage[lane];
@@ -228,8 +247,9 @@ int main() {
                          "kc_add on waves 0 and 4", "reg chain, exec=lane0", "kc_add, exec=lane0",
                          "reg chain, sgpr operand", "sgpr chain, exec=lane0", "dpp-bcast fmac chain",
                          "dpp-bcast chain + 7 LDS waves", "dsymv lane chain, sgpr w", "dsymv lane chain, lds w",
-                         "4 row chains / wave (dpp)"};
-  for (int mode = 0; mode < 21; mode++) {
+                         "4 row chains / wave (dpp)", "nrm2_dpp, no rescale", "nrm2_dpp, 3 rescales",
+                         "nrm2 branch-free 3-op", "nrm2 per-elt check, none", "nrm2 per-elt check, 3"};
+  for (int mode = 0; mode < 26; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
     unsigned long long t[32];
