@@ -134,7 +134,29 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
       const double a0 = lane < m ? fabs(R0) : 0.0;
       double pm0, pm1, carry;
       unsigned long long k0, k1 = 0;
-      if (m > 64) {  // uniform: both 64-element halves
+      if (kDpp) {
+        // both 64-element halves straight-line (the two quotients' division
+        // sequences interleave); the chain's operands staged twice: c = t
+        // (t = (a/b)^2) or 1.0 at a new running maximum, a = t (t = b/a) there
+        // or 1.0 (kc_nrm2_dpp8: a half holding a rescale runs ssq = (ssq a) a + c
+        // on all its elements, exact for both kinds)
+        const double a1 = lane + 64 < m ? fabs(R1) : 0.0;
+        wave_prefix_max2_nonneg(a0, a1, pm0, pm1);
+        const double c0 = readlane_d(pm0, 63);
+        const double b0 = dpp_d<0x138, 0xf>(pm0);             // running max before element lane (lane 0: 0.0)
+        const double b1 = fmax(dpp_d<0x138, 0xf>(pm1), c0);  // running max before element 64 + lane
+        const bool z0 = a0 != 0.0 && b0 != 0.0, n0 = z0 && b0 < a0;  // n: a new running maximum
+        const bool z1 = a1 != 0.0 && b1 != 0.0, n1 = z1 && b1 < a1;
+        const double q0 = (z0 ? (n0 ? b0 : a0) : 0.0) / (z0 ? (n0 ? a0 : b0) : 1.0);
+        const double q1 = (z1 ? (n1 ? b1 : a1) : 0.0) / (z1 ? (n1 ? a1 : b1) : 1.0);
+        k0 = __ballot(n0);
+        k1 = __ballot(n1);
+        sv[lane] = n0 ? 1.0 : q0 * q0;  // elements >= m: +0.0 (no-ops of the chain)
+        sv[64 + lane] = n1 ? 1.0 : q1 * q1;
+        t2[lane] = n0 ? q0 : 1.0;  // (t2 is free until this step's E phase)
+        t2[64 + lane] = n1 ? q1 : 1.0;
+        carry = fmax(c0, readlane_d(pm1, 63));
+      } else if (m > 64) {  // uniform: both 64-element halves
         const double a1 = lane + 64 < m ? fabs(R1) : 0.0;
         wave_prefix_max2_nonneg(a0, a1, pm0, pm1);
         const double c0 = readlane_d(pm0, 63);
@@ -148,18 +170,20 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
         pm0 = wave_prefix_max_nonneg(a0);
         carry = readlane_d(pm0, 63);
       }
-      const double b0 = dpp_d<0x138, 0xf>(pm0);  // running max before element lane (lane 0: 0.0)
-      const bool z0 = a0 != 0.0 && b0 != 0.0, n0 = z0 && b0 < a0;  // n: a new running maximum
-      const double q0 = (z0 ? (n0 ? b0 : a0) : 0.0) / (z0 ? (n0 ? a0 : b0) : 1.0);
-      k0 = __ballot(n0);
-      sv[lane] = n0 ? q0 : q0 * q0;  // elements >= m: +0.0 (no-ops of the chain)
+      if (!kDpp) {
+        const double b0 = dpp_d<0x138, 0xf>(pm0);  // running max before element lane (lane 0: 0.0)
+        const bool z0 = a0 != 0.0 && b0 != 0.0, n0 = z0 && b0 < a0;  // n: a new running maximum
+        const double q0 = (z0 ? (n0 ? b0 : a0) : 0.0) / (z0 ? (n0 ? a0 : b0) : 1.0);
+        k0 = __ballot(n0);
+        sv[lane] = n0 ? q0 : q0 * q0;  // elements >= m: +0.0 (no-ops of the chain)
+      }
       SQ_MARK(0)
       double ssq;
       if (kDpp) {
-        double q[8];  // element 16 k + j in lane j of every row of q[k]
+        double qa[8], qc[8];  // element 16 k + j in lane j of every row of q[k]
 #pragma unroll
-        for (int k = 0; k < 8; k++) q[k] = sv[16 * k + (lane & 15)];
-        ssq = chains::kc_nrm2_dpp(1.0, q, __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
+        for (int k = 0; k < 8; k++) qc[k] = sv[16 * k + (lane & 15)], qa[k] = t2[16 * k + (lane & 15)];
+        ssq = chains::kc_nrm2_dpp8(1.0, qa, qc, __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
       } else {
         ssq = chains::kc_nrm2(1.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(m + 15) >> 4), k0, k1);
       }
@@ -228,6 +252,8 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
         // that every pair it reads is 16-byte aligned
         const int T = n - 1 - 64 * h, top = N | 1, Tw = T + (top - (N - 1));
         const unsigned nb = __builtin_amdgcn_readfirstlane(T > 0 ? (unsigned)(Tw + 7) >> 3 : 0u);
+        // (w as broadcast LDS pairs: the DPP-broadcast form kc_lock_desc_dpp measured
+        // 28.5 against 23.1 cycles per element with four chain waves, profiles/r5)
         const double acc =
             chains::kc_lock_desc(0.0, lds_addr(tva + (top - 7)), lds_addr(M + (size_t)r * lda + (top - 7)), nb);
         if (valid) {
@@ -281,18 +307,20 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
         xv = chains::kc_add(0.0, lds_addr(sv), __builtin_amdgcn_readfirstlane((unsigned)(n + 15) >> 4));
       }
       const double als = -(tau_i / 2.0) * xv;
-      const double xf0 = x0 + als * v0;
-      if (lane < n) xa[r1 + lane] = xf0;
-      if (two && lane + 64 < n) xa[r1 + 64 + lane] = x1 + als * v1;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // dsyr2 (alpha = -1) on row r1: m += (-v_r1) x_c + (-x_r1) v_c, v_r1 = 1
-      const double xr1 = readlane_d(xf0, 0);
+      const double xf0 = x0 + als * v0, xf1 = x1 + als * v1;  // (+0.0 past the block)
+      if (lane < n) xa[r1 + lane] = xf0;  // (for the M phase's waves)
+      if (two && lane + 64 < n) xa[r1 + 64 + lane] = xf1;
+      // dsyr2 (alpha = -1) on row r1: m += (-v_r1) x_c + (-x_r1) v_c, v_r1 = 1;
+      // x_c of the columns c = i+3+lane (+64) from the registers two lanes up
+      // (DPP wave shifts), not through LDS
+      const double xr1 = readlane_d(xf0, 0), xf1_0 = readlane_d(xf1, 0), xf1_1 = readlane_d(xf1, 1);
+      const double xs0 = dpp_d<0x130, 0xf>(dpp_d<0x130, 0xf>(xf0));  // wave_shl:1 twice: x_(lane+2)
+      const double xs1 = dpp_d<0x130, 0xf>(dpp_d<0x130, 0xf>(xf1));
+      const double xc0 = lane == 62 ? xf1_0 : (lane == 63 ? xf1_1 : xs0);
       const double nvr = -1.0 * 1.0, nxr = -1.0 * xr1;
-      alpha = malpha + (nvr * xa[i + 2] + nxr * valpha);
-      R0 = ca < N ? ma + (nvr * xa[ca] + nxr * vca) : 0.0;
-      R1 = (n > 65 && cb < N) ? mb + (nvr * xa[cb] + nxr * vcb) : 0.0;  // (next step's x_e, e >= 64)
+      alpha = malpha + (nvr * readlane_d(xf0, 1) + nxr * valpha);
+      R0 = ca < N ? ma + (nvr * xc0 + nxr * vca) : 0.0;
+      R1 = (n > 65 && cb < N) ? mb + (nvr * xs1 + nxr * vcb) : 0.0;  // (next step's x_e, e >= 64)
       if (lane == 0) dg[r1] = dgr1 + (nvr * xr1 + nxr * 1.0);
     }
     SQ_MARK(6)
@@ -383,8 +411,8 @@ constexpr int MW2_TPB = 512;
 constexpr int MW2_PAD = 32;  // zero padding on each side of a staged product row
 __host__ __device__ inline size_t mw2_ps(int N) { return (size_t)N + 2 * MW2_PAD; }
 __host__ __device__ inline size_t mw2_lds_doubles(int N, int RW) {
-  // M | Pd | Pa | prow (+16) | nrow | vloc | tv | xl | sv (+64) | scal, accb, t2b, mskb, cmx (16 each)
-  return (size_t)RW * (N + 1) + 2 * (size_t)RW * mw2_ps(N) + (N + 16) + 4 * (size_t)N + (N + 64) + 5 * 16;
+  // M | Pd | Pa | prow (+16) | nrow | vloc | tv | xl | sv (+64) | scal, accb, t2b, mskb, cmx (16 each) | sa (+64)
+  return (size_t)RW * (N + 1) + 2 * (size_t)RW * mw2_ps(N) + (N + 16) + 4 * (size_t)N + (N + 64) + 5 * 16 + (N + 64);
 }
 // rows per workgroup chosen at init for the device's co-resident capacity, by N
 // (0: the default); every handle of one N on this device arrives at the same value
@@ -424,6 +452,7 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
   double *accb = scal + 16, *t2b = accb + 16;
   unsigned long long *mskb = (unsigned long long *)(t2b + 16);
   double *cmx = (double *)(mskb + 16);
+  double *sa = cmx + 16;  // kDpp: the ssq chain's second operand (kc_nrm2_dpp8)
   unsigned long long *gx = comm, *grow = comm + 2 * (size_t)N * N, *abortw = comm + 4 * (size_t)N * N;
   const int writer = (N - 1) % P;  // owns row N-1: runs every step, writes the per-step outputs
 
@@ -480,7 +509,12 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
         const bool z = a != 0.0 && b != 0.0, nf = z && b < a;  // (first nonzero: no-op +0.0)
         const double qv = (z ? (nf ? b : a) : 0.0) / (z ? (nf ? a : b) : 1.0);
         const unsigned long long bm = __ballot(nf);
-        sv[64 * k + lane] = nf ? qv : qv * qv;
+        if (kDpp) {  // c = t or 1.0 at a new running maximum, a = t there or 1.0 (as k_tridiag_sq)
+          sv[64 * k + lane] = nf ? 1.0 : qv * qv;
+          sa[64 * k + lane] = nf ? qv : 1.0;
+        } else {
+          sv[64 * k + lane] = nf ? qv : qv * qv;
+        }
         if (lane == 0) mskb[k] = bm;
       }
     }
@@ -497,10 +531,14 @@ __global__ void __launch_bounds__(MW2_TPB) k_tridiag_mw2(int N, const double *__
         const unsigned gb = __builtin_amdgcn_readfirstlane((unsigned)min(8, G - 8 * b));
         const unsigned long long k0 = mskb[2 * b], k1 = (2 * b + 1 < nch) ? mskb[2 * b + 1] : 0ULL;
         if (kDpp) {
-          double q[8];
+          double qa[8], qc[8];
 #pragma unroll
-          for (int k = 0; k < 8; k++) q[k] = sv[min(128 * b + 16 * k + (lane & 15), N + 63)];  // (past 16 gb: unused)
-          ssq = chains::kc_nrm2_dpp(ssq, q, gb, rfl64(k0), rfl64(k1));
+          for (int k = 0; k < 8; k++) {
+            const int e = min(128 * b + 16 * k + (lane & 15), N + 63);  // (past 16 gb: unused)
+            qc[k] = sv[e];
+            qa[k] = sa[e];
+          }
+          ssq = chains::kc_nrm2_dpp8(ssq, qa, qc, gb, rfl64(k0), rfl64(k1));
         } else {
           ssq = chains::kc_nrm2(ssq, lds_addr(sv + 128 * b), gb, rfl64(k0), rfl64(k1));
         }

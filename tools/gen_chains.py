@@ -265,6 +265,96 @@ __device__ __forceinline__ double kc_lock_asc(double acc, unsigned pw, unsigned 
 """
 
 
+def emit_lock_dpp(desc):
+    """Lockstep per-lane chains as emit_lock, but w reaches every lane through
+    a DPP broadcast from a register instead of a broadcast LDS read: per
+    8-element batch one ds_read_b64 brings w[base + (lane & 7)] into W (each
+    16-lane row holds the batch's 8 values in lanes 0-7), v_mov_b64 ...
+    row_newbcast:j copies element j to every lane, then the rounded product
+    and the ordered add.  LDS traffic per element and wave: m only (a b128 pair
+    per two elements descending, a b64 per element ascending) + 1/8 of a b64.
+    Set A: W v[192:193], m slots v[194:209]; set B: W v[210:211], m v[212:227];
+    broadcast temporaries v[228:231]."""
+    WA, MA, WB, MB, XT = 192, 194, 210, 212, 228
+
+    def ms(mb, sl):
+        return f"v[{mb + 2 * sl}:{mb + 2 * sl + 1}]"
+
+    def load(setb):
+        w, m = (WB, MB) if setb else (WA, MA)
+        out = [f"ds_read_b64 v[{w}:{w + 1}], %[pwl]"]
+        for k in range(4):
+            if desc:  # pair p = 3 - k: columns base + 2p (slot 2p) and base + 2p + 1 (slot 2p + 1), top pair first
+                pp = 3 - k
+                out.append(f"ds_read_b128 v[{m + 4 * pp}:{m + 4 * pp + 3}], %[pm] offset:{16 * pp}")
+            else:
+                out.append(f"ds_read_b64 {ms(m, 2 * k)}, %[pm] offset:%[o{2 * k}]")
+                out.append(f"ds_read_b64 {ms(m, 2 * k + 1)}, %[pm] offset:%[o{2 * k + 1}]")
+        if desc:
+            out += ["v_add_u32 %[pwl], 0xffffffc0, %[pwl]", "v_add_u32 %[pm], 0xffffffc0, %[pm]"]
+        else:
+            out += ["v_add_u32 %[pwl], 0x40, %[pwl]", "v_add_u32 %[pm], %[s8], %[pm]"]
+        return out
+
+    def proc(setb, loads):
+        w, m = (WB, MB) if setb else (WA, MA)
+        out = ["s_waitcnt lgkmcnt(0)"]
+        li = 0
+        per = (len(loads) + 7) // 8
+        for t in range(8):
+            # descending: element t is column base + 7 - t (lane 7 - t of W; m slot (7 - t) in the pairs)
+            j = 7 - t if desc else t
+            sl = j  # slot s holds column base + s (both walks)
+            x = f"v[{XT + 2 * (t % 2)}:{XT + 2 * (t % 2) + 1}]"
+            out.append(f"v_mov_b64 {x}, v[{w}:{w + 1}] row_newbcast:{j} row_mask:0xf bank_mask:0xf")
+            for _ in range(per):
+                if li < len(loads):
+                    out.append(loads[li])
+                    li += 1
+            out.append(f"v_mul_f64 {ms(m, sl)}, {x}, {ms(m, sl)}")
+            out.append(f"v_add_f64 %[acc], %[acc], {ms(m, sl)}")
+        out += loads[li:]
+        return out
+
+    L = ["s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 9f"]
+    L += load(False)
+    L.append("1:")
+    L += proc(False, load(True))
+    L += ["s_sub_u32 %[nb], %[nb], 1", "s_cmp_eq_u32 %[nb], 0", "s_cbranch_scc1 9f"]
+    L += proc(True, load(False))
+    L += ["s_sub_u32 %[nb], %[nb], 1", "s_cmp_lg_u32 %[nb], 0", "s_cbranch_scc1 1b", "9:", "s_waitcnt lgkmcnt(0)"]
+    body = asm_block(L)
+    clob = ", ".join(f'"v{r}"' for r in range(192, 232))
+    if desc:
+        return f"""
+// kc_lock_desc with w broadcast from registers (DPP): pwl = per-lane LDS byte
+// address of w[top - 7 + (lane & 7)], pm = per-lane address of m[top - 7]
+// (16-byte aligned)
+__device__ __forceinline__ double kc_lock_desc_dpp(double acc, unsigned pwl, unsigned pm, unsigned nb) {{
+  asm volatile(
+{body}
+      : [acc] "+&v"(acc), [pwl] "+&v"(pwl), [pm] "+&v"(pm), [nb] "+&s"(nb)
+      :
+      : "scc", "memory", {clob});
+  return acc;
+}}
+"""
+    offs = ", ".join(f'[o{t}] "i"({t} * S)' for t in range(8))
+    return f"""
+// kc_lock_asc with w broadcast from registers (DPP): pwl = per-lane LDS byte
+// address of w[lane & 7], pm = per-lane address of m[0], S the m stride
+template <int S>
+__device__ __forceinline__ double kc_lock_asc_dpp(double acc, unsigned pwl, unsigned pm, unsigned nb) {{
+  asm volatile(
+{body}
+      : [acc] "+&v"(acc), [pwl] "+&v"(pwl), [pm] "+&v"(pm), [nb] "+&s"(nb)
+      : [s8] "i"(8 * S), {offs}
+      : "scc", "memory", {clob});
+  return acc;
+}}
+"""
+
+
 def emit_dpp_chains():
     """Chains over staged values held in REGISTERS: element 16 k + j sits in
     lane j of every row of q[k] (8 VGPR pairs, 128 elements) and reaches the
@@ -417,7 +507,54 @@ __device__ __forceinline__ double kc_nrm2_dpp3(double acc, const double (&a)[8],
   return acc;
 }}
 """
-    return add + nrm2 + row16 + nrm2c + nrm23
+    # (3) kc_nrm2_dpp with the branch-free three-operation form for the
+    #     halves (H = 8) or quarters (H = 4) that hold a rescale: a span
+    #     without one is H plain DPP adds of c, a span with one runs
+    #     u = ssq a, w = u a, ssq = w + c on every element, straight-line
+    def spans(H, name):
+        L = ["s_nop 1"]
+        slow = []
+        nsp = 128 // H
+        for hf in range(nsp):
+            w, sh = words[(hf * H) // 32], (hf * H) % 32
+            if (hf * H) % 16 == 0:
+                L += ["s_cmp_eq_u32 %[g], 0", "s_cbranch_scc1 9f", "s_sub_u32 %[g], %[g], 1"]
+            L += [f"s_and_b32 %[t], {w}, {hex(((1 << H) - 1) << sh)}", f"s_cbranch_scc1 {100 + hf}f"]
+            for t in range(H):
+                e = H * hf + t
+                k, j = e // 16, e % 16
+                L.append(f"v_fmac_f64 %[acc], %[c{k}], %[one] row_newbcast:{j} row_mask:0xf bank_mask:0xf")
+            L.append(f"{200 + hf}:")
+            slow.append(f"{100 + hf}:")
+            for t in range(H):
+                e = H * hf + t
+                k, j = e // 16, e % 16
+                slow += [f"v_mov_b64 %[xa], %[a{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+                         f"v_mov_b64 %[xc], %[c{k}] row_newbcast:{j} row_mask:0xf bank_mask:0xf",
+                         "v_mul_f64 %[tmp], %[acc], %[xa]", "v_mul_f64 %[tmp], %[tmp], %[xa]",
+                         "v_add_f64 %[acc], %[tmp], %[xc]"]
+            slow += [f"s_branch {200 + hf}b"]
+        L += ["s_branch 9f"] + slow + ["9:"]
+        return f"""
+// (experimental) kc_nrm2_dpp over {H}-element spans, a span holding a rescale
+// in the branch-free three-operation form; a[] = t at a new running maximum,
+// else 1.0; c[] = 1.0 there, else t
+__device__ __forceinline__ double {name}(double acc, const double (&a)[8], const double (&c)[8], unsigned g,
+                                         unsigned long long k0, unsigned long long k1) {{
+  const unsigned k0l = __builtin_amdgcn_readfirstlane((unsigned)k0), k0h = __builtin_amdgcn_readfirstlane((unsigned)(k0 >> 32));
+  const unsigned k1l = __builtin_amdgcn_readfirstlane((unsigned)k1), k1h = __builtin_amdgcn_readfirstlane((unsigned)(k1 >> 32));
+  const double one = 1.0;
+  unsigned t;
+  double tmp, xa, xc;
+  asm volatile(
+{asm_block(L)}
+      : [acc] "+&v"(acc), [g] "+&s"(g), [t] "=&s"(t), [tmp] "=&v"(tmp), [xa] "=&v"(xa), [xc] "=&v"(xc)
+      : {qa}, {qc}, [one] "v"(one), [k0l] "s"(k0l), [k0h] "s"(k0h), [k1l] "s"(k1l), [k1h] "s"(k1h)
+      : "scc");
+  return acc;
+}}
+"""
+    return add + nrm2 + row16 + nrm2c + nrm23 + spans(8, "kc_nrm2_dpp8") + spans(4, "kc_nrm2_dpp4")
 
 
 def main():
@@ -430,7 +567,7 @@ def main():
 #pragma once
 namespace kg {{
 namespace chains {{
-{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}{emit_dpp_chains()}
+{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}{emit_lock_dpp(True)}{emit_lock_dpp(False)}{emit_dpp_chains()}
 }}  // namespace chains
 }}  // namespace kg
 """

@@ -199,6 +199,39 @@ __global__ void __launch_bounds__(512) k_bench(int mode, int reps, double *out, 
       }
       t1 = __builtin_amdgcn_s_memtime();
     }
+  } else if (mode == 26 || mode == 27) {
+    // the dsymv lockstep chains with w broadcast from registers (DPP):
+    // 26 kc_lock_desc_dpp on wave 0 alone, 27 four lockstep waves (2 desc + 2 asc)
+    const bool active = (mode == 27) ? wid < 4 : wid == 0;
+    if (active) {
+      const bool desc = (mode == 26) || (mode == 27 && wid < 2);
+      const int r = lane + 64 * (wid & 1);
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int k = 0; k < reps; k++) {
+        if (desc)
+          acc += kc_lock_desc_dpp(0.0, la(w + 120) + ((lane & 7) << 3), la(M + (size_t)r * LD + 120),
+                                  __builtin_amdgcn_readfirstlane(cnt / 8));
+        else
+          acc += kc_lock_asc_dpp<LD * 8>(0.0, la(w) + ((lane & 7) << 3), la(M + r), __builtin_amdgcn_readfirstlane(cnt / 8));
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
+  } else if (mode >= 28 && mode <= 31) {
+    // kc_nrm2_dpp8 / kc_nrm2_dpp4 (three-operation spans) without / with the
+    // three rescales of modes 21-25
+    if (wid == 0) {
+      double q[8], a[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) q[k] = stage[16 * k + (lane & 15)], a[k] = 1.0;
+      const bool ev = mode == 29 || mode == 31;
+      const unsigned long long k0 = ev ? ((1ull << 5) | (1ull << 40)) : 0ull, k1 = ev ? (1ull << 26) : 0ull;
+      t0 = __builtin_amdgcn_s_memtime();
+      for (int r = 0; r < reps; r++) {
+        if (mode <= 29) acc = kc_nrm2_dpp8(acc + 1.0, a, q, 8u, k0, k1);
+        else acc = kc_nrm2_dpp4(acc + 1.0, a, q, 8u, k0, k1);
+      }
+      t1 = __builtin_amdgcn_s_memtime();
+    }
   } else if (mode >= 21 && mode <= 25) {
     // the ssq recurrence on register-held elements: kc_nrm2_dpp without /
     // with three rescale events (elements 5, 40, 90: three different
@@ -248,8 +281,10 @@ int main() {
                          "reg chain, sgpr operand", "sgpr chain, exec=lane0", "dpp-bcast fmac chain",
                          "dpp-bcast chain + 7 LDS waves", "dsymv lane chain, sgpr w", "dsymv lane chain, lds w",
                          "4 row chains / wave (dpp)", "nrm2_dpp, no rescale", "nrm2_dpp, 3 rescales",
-                         "nrm2 branch-free 3-op", "nrm2 per-elt check, none", "nrm2 per-elt check, 3"};
-  for (int mode = 0; mode < 26; mode++) {
+                         "nrm2 branch-free 3-op", "nrm2 per-elt check, none", "nrm2 per-elt check, 3",
+                         "kc_lock_desc_dpp alone", "4 lockstep waves (dpp w)", "nrm2 8-spans, none",
+                         "nrm2 8-spans, 3", "nrm2 4-spans, none", "nrm2 4-spans, 3"};
+  for (int mode = 0; mode < 32; mode++) {
     for (int warm = 0; warm < 2; warm++) hipLaunchKernelGGL(k_bench, dim3(1), dim3(512), lds, 0, mode, reps, out, ticks);
     hipDeviceSynchronize();
     unsigned long long t[32];
