@@ -1,5 +1,12 @@
 // kg_common.hip — error plumbing, double-double constant tables, ABI info.
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 
 #include "../../include/korali_amd.h"
@@ -51,6 +58,41 @@ double host_log_cr(double x) {
   if (x < 2.2250738585072014e-308) return std::log(x);
   const dd r = dd_log_tab(x, host_tables());
   return r.hi + r.lo;
+}
+
+// KORALI_AMD_SEGV_MAPS=1 (diagnostics of faults inside other libraries,
+// e.g. under a profiler): on SIGSEGV write the faulting address, the native
+// backtrace and /proc/self/maps to stderr (so every frame resolves to a
+// library + offset), then die with the default action.  Async-signal-safe
+// calls only (write, open, read; backtrace is preloaded at install time).
+static void segv_diag(int sig, siginfo_t *si, void *) {
+  char buf[4096];
+  int n = snprintf(buf, sizeof buf, "\n[korali_amd SIGSEGV diagnostics] fault address %p\nbacktrace:\n", si ? si->si_addr : nullptr);
+  (void)!write(2, buf, (size_t)n);
+  void *bt[64];
+  const int nb = backtrace(bt, 64);
+  backtrace_symbols_fd(bt, nb, 2);
+  const char mh[] = "/proc/self/maps:\n";
+  (void)!write(2, mh, sizeof mh - 1);
+  const int fd = open("/proc/self/maps", O_RDONLY);
+  if (fd >= 0) {
+    ssize_t k;
+    while ((k = read(fd, buf, sizeof buf)) > 0) (void)!write(2, buf, (size_t)k);
+    close(fd);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) static void install_segv_diag() {
+  const char *e = getenv("KORALI_AMD_SEGV_MAPS");
+  if (!e || *e != '1') return;
+  void *warm[2];
+  (void)backtrace(warm, 2);  // (loads libgcc's unwinder outside the handler)
+  struct sigaction sa {};
+  sa.sa_sigaction = segv_diag;
+  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, nullptr);
 }
 
 }  // namespace kg

@@ -79,10 +79,13 @@ inline hipError_t allow_dynamic_lds(const void *f, size_t bytes) {
 // Grids whose workgroups wait on one another inside the launch (spin
 // hand-offs) go through launch_resident: a cooperative launch, so HIP
 // guarantees co-residency or fails the launch.  KORALI_AMD_PLAIN_LAUNCH=1
-// launches them with hipLaunchKernel after the same occupancy check instead:
-// rocprofv3 (ROCm 7.2) segfaults at process teardown, after writing its
-// output, in any process that made a cooperative launch, so profile runs set
-// it (scripts/gpu_prof.sh).
+// launches them with hipLaunchKernel after the same occupancy check instead
+// (A/B).  Under rocprofv3 (ROCm 7.2) a process that made a cooperative launch
+// dies with SIGSEGV in its exit handlers after the tool wrote its output and
+// finalized: libamdhip64's exit-time teardown calls into libhsa-runtime64
+// through the profiler's already finalized interception (stack in
+// profiles/r5/c4_teardown_segv.txt, KORALI_AMD_SEGV_MAPS=1); the profile
+// files are complete, and plain-launch processes never reach that path.
 //
 // prefer_plain: a grid whose waiting workgroups depend only on a workgroup
 // dispatched before them (the streamed Givens apply: every row workgroup
