@@ -291,6 +291,11 @@ __global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__r
                                                             unsigned long long *__restrict__ block_end,
                                                             unsigned long long k_lo, unsigned long long k_hi) {
   __shared__ unsigned int woff[POLAR_TPB / 64];
+  // the wave's normals in order: a wave's lanes hold consecutive ranges of
+  // normal indices, so each wave stages its normals here and stores them
+  // contiguously (a lane storing its own few 8-byte normals wrote 2.08x the
+  // normals' bytes to HBM at C4, round-4 PMC)
+  __shared__ double zbuf[POLAR_TPB / 64][64 * POLAR_APT];
   const PosView st = pos_view(stp);
   const unsigned long long base = (unsigned long long)blockIdx.x * POLAR_APB + threadIdx.x * POLAR_APT;
   double yv[POLAR_APT], rv[POLAR_APT];
@@ -321,7 +326,9 @@ __global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__r
     }
   }
   __syncthreads();
-  unsigned long long k = offsets[blockIdx.x] + woff[wid] + (x - acc);
+  const unsigned long long kw = offsets[blockIdx.x] + woff[wid];  // the wave's first normal
+  const unsigned int wt = (unsigned int)__shfl(x, 63, 64);          // the wave's normals
+  unsigned long long k = kw + (x - acc);
 #pragma unroll
   for (int q = 0; q < POLAR_APT; q++) {
     if (mask & (1u << q)) {
@@ -331,13 +338,20 @@ __global__ void __launch_bounds__(POLAR_TPB) k_polar_scatter(const uint32_t *__r
         if (k >= k_lo && k < k_hi) {
           const double r2 = rv[q];
           const double g = 1.0 * yv[q] * sqrt(-2.0 * log_cr(r2) / r2);
-          z[k - k_lo] = 0.0 + g;
+          zbuf[wid][k - kw] = 0.0 + g;
         }
         if (block_end && ((k + 1) % block_len) == 0) block_end[(k + 1) / block_len - 1] = base + q;
         if (k == M - 1) stp->last_attempt = base + q;
       }
       k++;
     }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (unsigned int i = lane; i < wt; i += 64) {
+    const unsigned long long kk = kw + i;
+    if (kk < M && kk >= k_lo && kk < k_hi) z[kk - k_lo] = zbuf[wid][i];
   }
 }
 
