@@ -2775,12 +2775,36 @@ void eig_prof(void *ctx, const char *stage, int phase) {
   }
 }
 
+// KORALI_AMD_RUN_PHASES=1: kg_cmaes_create's phases on stderr
+struct CreateClock {
+  bool on = getenv("KORALI_AMD_RUN_PHASES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string text;
+  void mark(const char *phase) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    char b[96];
+    snprintf(b, sizeof(b), " %s=%.3fms", phase, std::chrono::duration<double, std::milli>(n - t).count());
+    text += b;
+    t = n;
+  }
+  ~CreateClock() {
+    if (on) fprintf(stderr, "[korali_amd cmaes create]%s\n", text.c_str());
+  }
+};
+
 template <typename T>
-int dalloc(T **p, size_t n) {
+int dalloc(T **p, size_t n, bool wait = true) {
   if (n == 0) n = 1;
-  KG_HIP(hipMalloc(p, n * sizeof(T)));
-  if (zero_fill(*p, n * sizeof(T))) return 1;
+  KG_HIP(dev_alloc(p, n * sizeof(T)));
+  if (wait ? zero_fill(*p, n * sizeof(T)) : zero_fill_async(*p, n * sizeof(T))) return 1;
   return 0;
+}
+// kg_cmaes_create's buffers: zero fills queued on the null stream, waited for
+// once after the last one
+template <typename T>
+int dalloc_q(T **p, size_t n) {
+  return dalloc(p, n, false);
 }
 
 void gsl_seed_state(uint64_t seed, unsigned char *out5000) {
@@ -3013,6 +3037,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
+  CreateClock clk;
   h->r0 = h->shardRank * (L / h->shards);
   h->r1 = h->r0 + L / h->shards;
   h->mirrored = cfg->mirrored_sampling != 0;
@@ -3027,59 +3052,64 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
   const size_t rows = (size_t)L + h->R;
   const size_t xrows = h->mirrored ? 2 * h->blocks : rows;  // transformed rows (Xall, infeasibility flags)
   int rc = 0;
-  rc |= dalloc(&h->mean, N) | dalloc(&h->prevMean, N) | dalloc(&h->C, (size_t)N * N) | dalloc(&h->B, (size_t)N * N);
-  rc |= dalloc(&h->D, N) | dalloc(&h->pc, N) | dalloc(&h->ps, N) | dalloc(&h->w, h->muMax);
-  rc |= dalloc(&h->X, (size_t)L * N) | dalloc(&h->F, L) | dalloc(&h->Z, rows * N);
-  rc |= dalloc(&h->bestEverVars, N) | dalloc(&h->currBestVars, N) | dalloc(&h->meanUpdate, N) | dalloc(&h->auxBDZ, N);
-  rc |= dalloc(&h->lb, N) | dalloc(&h->ub, N) | dalloc(&h->iv, N) | dalloc(&h->istd, N) | dalloc(&h->minstd, N);
-  rc |= dalloc(&h->Y, (size_t)h->muMax * N);
-  if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc(&h->Yc, (size_t)h->muMax * N) | dalloc(&h->Tt, (size_t)h->muMax * N);
-  rc |= dalloc(&h->idx, L) | dalloc(&h->sc, 1);
-  rc |= dalloc(&h->infeas, xrows) | dalloc(&h->assign, L) | dalloc(&h->blockEnd, rows) | dalloc(&h->usedBlocks, 1);
-  rc |= dalloc(&h->selEnd, 2);
-  if (h->cfg.store_bdz) rc |= dalloc(&h->BDZ, (size_t)L * N);
-  if (cfg->use_gradients) rc |= dalloc(&h->G, (size_t)L * N);
-  rc |= dalloc(&h->gran, N) | dalloc(&h->mask, N) | dalloc(&h->maskSigma, N);
+  rc |= dalloc_q(&h->mean, N) | dalloc_q(&h->prevMean, N) | dalloc_q(&h->C, (size_t)N * N) | dalloc_q(&h->B, (size_t)N * N);
+  rc |= dalloc_q(&h->D, N) | dalloc_q(&h->pc, N) | dalloc_q(&h->ps, N) | dalloc_q(&h->w, h->muMax);
+  rc |= dalloc_q(&h->X, (size_t)L * N) | dalloc_q(&h->F, L) | dalloc_q(&h->Z, rows * N);
+  rc |= dalloc_q(&h->bestEverVars, N) | dalloc_q(&h->currBestVars, N) | dalloc_q(&h->meanUpdate, N) | dalloc_q(&h->auxBDZ, N);
+  rc |= dalloc_q(&h->lb, N) | dalloc_q(&h->ub, N) | dalloc_q(&h->iv, N) | dalloc_q(&h->istd, N) | dalloc_q(&h->minstd, N);
+  rc |= dalloc_q(&h->Y, (size_t)h->muMax * N);
+  if (cfg->cov_mode != KG_COV_MFMA) rc |= dalloc_q(&h->Yc, (size_t)h->muMax * N) | dalloc_q(&h->Tt, (size_t)h->muMax * N);
+  rc |= dalloc_q(&h->idx, L) | dalloc_q(&h->sc, 1);
+  rc |= dalloc_q(&h->infeas, xrows) | dalloc_q(&h->assign, L) | dalloc_q(&h->blockEnd, rows) | dalloc_q(&h->usedBlocks, 1);
+  rc |= dalloc_q(&h->selEnd, 2);
+  if (h->cfg.store_bdz) rc |= dalloc_q(&h->BDZ, (size_t)L * N);
+  if (cfg->use_gradients) rc |= dalloc_q(&h->G, (size_t)L * N);
+  rc |= dalloc_q(&h->gran, N) | dalloc_q(&h->mask, N) | dalloc_q(&h->maskSigma, N);
   if (h->hasDiscrete) {
     h->ucap = 16 * (size_t)L + 1024;  // the mutations' uniforms per generation: ~2-4 per mutated sample
-    rc |= dalloc(&h->ubuf, h->ucap) | dalloc(&h->uused, 1);
+    rc |= dalloc_q(&h->ubuf, h->ucap) | dalloc_q(&h->uused, 1);
   }
   if (h->R) {
-    rc |= dalloc(&h->Xall, xrows * N);
-    if (h->cfg.store_bdz) rc |= dalloc(&h->BDZall, xrows * N);
+    rc |= dalloc_q(&h->Xall, xrows * N);
+    if (h->cfg.store_bdz) rc |= dalloc_q(&h->BDZall, xrows * N);
   }
   size_t P2 = 1;
   while (P2 < (size_t)L) P2 <<= 1;
   if (P2 < SORT_CHUNK) P2 = SORT_CHUNK;
-  rc |= dalloc(&h->sortKey, P2) | dalloc(&h->sortVal, P2);
+  rc |= dalloc_q(&h->sortKey, P2) | dalloc_q(&h->sortVal, P2);
   const int nt = (N + 15) / 16;
   h->kslices = rankmu_kslices(N, h->muMax);
-  rc |= dalloc(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
+  rc |= dalloc_q(&h->covPart, (size_t)h->kslices * (nt * (nt + 1) / 2) * 256);
   if (h->nc) {
-    rc |= dalloc(&h->V, h->nc * (size_t)N) | dalloc(&h->auxC, (size_t)N * N) | dalloc(&h->violDev, L);
-    rc |= dalloc(&h->pairI, h->nc * (size_t)L) | dalloc(&h->pairC, h->nc * (size_t)L) |
-          dalloc(&h->pairCnt, h->nc * (size_t)L) | dalloc(&h->listDev, L);
+    rc |= dalloc_q(&h->V, h->nc * (size_t)N) | dalloc_q(&h->auxC, (size_t)N * N) | dalloc_q(&h->violDev, L);
+    rc |= dalloc_q(&h->pairI, h->nc * (size_t)L) | dalloc_q(&h->pairC, h->nc * (size_t)L) |
+          dalloc_q(&h->pairCnt, h->nc * (size_t)L) | dalloc_q(&h->listDev, L);
     h->cEval.assign(h->nc * (size_t)L, 0.0);
     h->cInd.assign(h->nc * (size_t)L, 0.0);
     h->cCnt.assign(L, 0.0);
     h->vBounds.assign(h->nc, 0.0);
     h->bestCEval.assign(h->nc, 0.0);
   }
-  rc |= dalloc(&h->kidx, h->muMax) | dalloc(&h->shardCnt, 1) | dalloc(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
+  rc |= dalloc_q(&h->kidx, h->muMax) | dalloc_q(&h->shardCnt, 1) | dalloc_q(&h->part, 2 * (size_t)N + (size_t)(nt * (nt + 1) / 2) * 256);
   if (cfg->shard_count >= 1 && cfg->cov_mode != KG_COV_MFMA) {
     // a rank owns lambda / S rows, so it packs at most min(mu, lambda / S)
     // selected ones; whole-population ranks (replSample) exchange no rows
     h->rowsCap = h->replSample ? 0 : (size_t)std::min(h->muMax, L / h->shards);
-    rc |= dalloc(&h->shardPos, h->muMax) | dalloc(&h->shardCounts, h->shards + 1) |
-          dalloc(&h->covPack, (size_t)N * (N + 1) / 2);
-    if (h->rowsCap) rc |= dalloc(&h->rows, (size_t)h->shards * h->rowsCap * N);
+    rc |= dalloc_q(&h->shardPos, h->muMax) | dalloc_q(&h->shardCounts, h->shards + 1) |
+          dalloc_q(&h->covPack, (size_t)N * (N + 1) / 2);
+    if (h->rowsCap) rc |= dalloc_q(&h->rows, (size_t)h->shards * h->rowsCap * N);
+  }
+  if (!rc && hipStreamSynchronize(nullptr) != hipSuccess) {
+    set_error("kg_cmaes_create: zero fills of the device buffers failed");
+    rc = 1;
   }
   if (rc) {
     delete h;
     return 1;
   }
+  clk.mark("buffers");
   if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32);
-  if (hipHostMalloc(&h->summary, sizeof(TermSummary), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+  if (host_alloc(&h->summary, sizeof(TermSummary), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void **)&h->summaryDev, h->summary, 0) != hipSuccess) {
     delete h;
     KG_CHECK(false, "hipHostMalloc of the termination summary failed");
@@ -3101,8 +3131,8 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
-  KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  KG_HIP(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+  KG_HIP(stream_acquire(&h->stream));
+  KG_HIP(stream_acquire(&h->stream2));
   KG_HIP(hipEventCreateWithFlags(&h->evY, hipEventDisableTiming));
   KG_HIP(hipEventCreateWithFlags(&h->evC, hipEventDisableTiming));
   {
@@ -3115,6 +3145,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
       return 1;
     }
   }
+  clk.mark("eigen");
   if (set_current(h, h->lamCfg, h->muCfg)) return 1;
   KG_HIP(hipMemcpy(h->lb, lb.data(), N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->ub, ub.data(), N * sizeof(double), hipMemcpyHostToDevice));
@@ -3129,19 +3160,27 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     delete h;
     return 1;
   }
+  clk.mark("rng_init");
   unsigned char st[5000];
   gsl_seed_state(cfg->normal_seed, st);
   if (h->normal.import_gsl(st, h->stream)) return 1;
+  clk.mark("normal_seed");
   gsl_seed_state(cfg->uniform_seed, st);
   if (h->uniform.import_gsl(st, h->stream)) return 1;
+  clk.mark("uniform_seed");
   *out = h;
   return 0;
 }
 
 int kg_cmaes_destroy(kg_cmaes_t h) {
   if (!h) return 0;
+  // every stream drained before the blocks go back to the cache
   (void)hipStreamSynchronize(h->stream);
-  if (h->summary) (void)hipHostFree(h->summary);
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  h->eig.drain();
+  h->normal.drain();
+  h->uniform.drain();
+  if (h->summary) host_release(h->summary);
   for (void *p : {(void *)h->mean, (void *)h->prevMean, (void *)h->C, (void *)h->B, (void *)h->D, (void *)h->pc,
                   (void *)h->ps, (void *)h->w, (void *)h->X, (void *)h->Xall, (void *)h->BDZ, (void *)h->BDZall,
                   (void *)h->F, (void *)h->Z, (void *)h->bestEverVars, (void *)h->currBestVars,
@@ -3154,18 +3193,18 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
                   (void *)h->selEnd, (void *)h->V, (void *)h->auxC, (void *)h->violDev, (void *)h->pairI,
                   (void *)h->pairC, (void *)h->pairCnt, (void *)h->listDev, (void *)h->dzT, (void *)h->shardPos,
                   (void *)h->shardCounts, (void *)h->rows, (void *)h->covPack})
-    if (p) (void)hipFree(p);
+    if (p) dev_release(p);
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
     (void)hipEventDestroy(std::get<2>(t));
   }
   if (h->stream2) {
     (void)hipStreamSynchronize(h->stream2);
-    (void)hipStreamDestroy(h->stream2);
+    stream_release(h->stream2);
   }
   if (h->evY) (void)hipEventDestroy(h->evY);
   if (h->evC) (void)hipEventDestroy(h->evC);
-  (void)hipStreamDestroy(h->stream);
+  stream_release(h->stream);
   delete h;
   return 0;
 }
@@ -3243,7 +3282,7 @@ static int cmaes_transform(kg_cmaes_t h, size_t rows, double *Xo, double *Bo, in
   }
   const int ldz = sc_ldz(rows);
   if ((size_t)ldz > h->dzTRows) {
-    if (h->dzT) (void)hipFree(h->dzT);
+    if (h->dzT) dev_release(h->dzT, h->stream);
     h->dzT = nullptr;
     h->dzTRows = 0;
     if (dalloc(&h->dzT, (size_t)ldz * N)) return 1;
@@ -3379,7 +3418,7 @@ static int cmaes_resample(kg_cmaes_t h) {
                  "discrete mutations need more uniforms per sample than the device window holds");
         double *nb2 = nullptr;
         if (dalloc(&nb2, cap)) return 1;
-        (void)hipFree(h->ubuf);
+        dev_release(h->ubuf, h->stream);
         h->ubuf = nb2;
         h->ucap = cap;
       } else {
@@ -4116,6 +4155,13 @@ int kg_cmaes_get_fields(kg_cmaes_t h, const char *const *names, size_t count, do
   KG_HIP(hipMemcpyAsync(&hs, h->sc, sizeof(hs), hipMemcpyDeviceToHost, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   for (size_t i = 0; i < count; i++) {
+    HostField hf;
+    double tmp = 0;
+    if (host_field(h, names[i], hf, tmp)) {
+      KG_CHECK(hf.n == 1, std::string("kg_cmaes_get_fields: not a scalar field: ") + names[i]);
+      out[i] = *hf.p;
+      continue;
+    }
     FieldRef r;
     KG_CHECK(field_ref(h, names[i], r), std::string("unknown CMA-ES field: ") + names[i]);
     const char *base = (const char *)h->sc;

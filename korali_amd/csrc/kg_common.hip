@@ -7,7 +7,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <map>
 #include <mutex>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/korali_amd.h"
 #include "kg_common.hpp"
@@ -50,6 +54,152 @@ void upload_dd_tables() {
     ok = hipMemcpyToSymbol(HIP_SYMBOL(c_dd_tab), &t, sizeof(t)) == hipSuccess;
   });
   (void)ok;
+}
+
+// ------------------------------------------------- device block / stream cache
+namespace {
+struct DeviceCache {
+  std::mutex mu;
+  std::unordered_map<void *, std::pair<int, size_t>> live;  // block -> (device, rounded bytes)
+  std::multimap<std::pair<int, size_t>, void *> idle;
+  std::map<int, std::vector<hipStream_t>> streams;
+  std::unordered_map<void *, std::pair<unsigned, size_t>> hostLive;  // pinned block -> (flags, bytes)
+  std::multimap<std::pair<unsigned, size_t>, void *> hostIdle;
+  size_t idleBytes = 0;
+  size_t cap = [] {
+    const char *e = getenv("KORALI_AMD_DEVICE_CACHE_MB");
+    return (e && *e ? (size_t)strtoull(e, nullptr, 10) : (size_t)8192) << 20;
+  }();
+  void drop_idle() {  // under mu
+    for (auto &kv : idle) (void)hipFree(kv.second);
+    idle.clear();
+    for (auto &kv : hostIdle) (void)hipHostFree(kv.second);
+    hostIdle.clear();
+    idleBytes = 0;
+  }
+};
+// never destroyed: blocks may be released from other static destructors
+DeviceCache &device_cache() {
+  static auto *c = new DeviceCache();
+  return *c;
+}
+}  // namespace
+
+hipError_t dev_alloc(void **p, size_t bytes) {
+  const size_t rb = ((bytes ? bytes : 1) + 511) & ~(size_t)511;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  DeviceCache &c = device_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.idle.find({dev, rb});
+  if (it != c.idle.end()) {
+    *p = it->second;
+    c.idle.erase(it);
+    c.idleBytes -= rb;
+  } else {
+    e = hipMalloc(p, rb);
+    if (e == hipErrorOutOfMemory && !c.idle.empty()) {
+      (void)hipGetLastError();
+      c.drop_idle();
+      e = hipMalloc(p, rb);
+    }
+    if (e != hipSuccess) return e;
+  }
+  c.live[*p] = {dev, rb};
+  return hipSuccess;
+}
+
+void dev_release(void *p, hipStream_t drain) {
+  if (!p) return;
+  if (drain) (void)hipStreamSynchronize(drain);
+  DeviceCache &c = device_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.live.find(p);
+  if (it == c.live.end()) {  // not one of ours
+    (void)hipFree(p);
+    return;
+  }
+  const auto key = it->second;
+  c.live.erase(it);
+  if (c.idleBytes + key.second > c.cap) {
+    (void)hipFree(p);
+    return;
+  }
+  c.idle.emplace(key, p);
+  c.idleBytes += key.second;
+}
+
+hipError_t host_alloc(void **p, size_t bytes, unsigned flags) {
+  const size_t rb = ((bytes ? bytes : 1) + 511) & ~(size_t)511;
+  DeviceCache &c = device_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.hostIdle.find({flags, rb});
+  if (it != c.hostIdle.end()) {
+    *p = it->second;
+    c.hostIdle.erase(it);
+    c.idleBytes -= rb;
+    memset(*p, 0, rb);
+  } else {
+    hipError_t e = hipHostMalloc(p, rb, flags);
+    if (e == hipErrorOutOfMemory && !c.hostIdle.empty()) {
+      (void)hipGetLastError();
+      c.drop_idle();
+      e = hipHostMalloc(p, rb, flags);
+    }
+    if (e != hipSuccess) return e;
+  }
+  c.hostLive[*p] = {flags, rb};
+  return hipSuccess;
+}
+
+void host_release(void *p) {
+  if (!p) return;
+  DeviceCache &c = device_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.hostLive.find(p);
+  if (it == c.hostLive.end()) {
+    (void)hipHostFree(p);
+    return;
+  }
+  const auto key = it->second;
+  c.hostLive.erase(it);
+  if (c.idleBytes + key.second > c.cap) {
+    (void)hipHostFree(p);
+    return;
+  }
+  c.hostIdle.emplace(key, p);
+  c.idleBytes += key.second;
+}
+
+hipError_t stream_acquire(hipStream_t *s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  DeviceCache &c = device_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto &v = c.streams[dev];
+    if (c.cap && !v.empty()) {
+      *s = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+void stream_release(hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  int dev = 0;
+  DeviceCache &c = device_cache();
+  if (!c.cap || hipGetDevice(&dev) != hipSuccess) {
+    (void)hipStreamDestroy(s);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(c.mu);
+  c.streams[dev].push_back(s);
 }
 
 double host_log_cr(double x) {

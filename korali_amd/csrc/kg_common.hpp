@@ -49,6 +49,38 @@ const char *last_error();
     }                             \
   } while (0)
 
+// Device blocks and streams of the solver handles come from a process-wide
+// cache: an engine run creates a handle (tens of buffers, two streams) and
+// releases it at the end, and hipMalloc / hipFree / hipStreamCreate cost a few
+// milliseconds per handle -- the fixed cost of a run, against ~1 ms
+// generations (engine fixed cost).
+//   dev_alloc    a block of >= bytes on the current device (cached blocks of
+//                the same rounded size first; on out-of-memory the cache is
+//                emptied and the allocation retried);
+//   dev_release  back to the cache.  The caller has drained every stream
+//                that used the block (the handles' destroy synchronises its
+//                streams first); a mid-life reallocation passes its stream.
+//   stream_acquire / stream_release  non-blocking streams, pooled per device.
+// KORALI_AMD_DEVICE_CACHE_MB bounds the idle bytes kept (default 8192; 0
+// turns the cache off: every release is a hipFree).
+//   host_alloc / host_release  the same for pinned host blocks (hipHostMalloc
+//                flags are part of the key); a reused block is zeroed, as a
+//                fresh one is.
+hipError_t dev_alloc(void **p, size_t bytes);
+template <class T>
+inline hipError_t dev_alloc(T **p, size_t bytes) {
+  return dev_alloc((void **)p, bytes);
+}
+void dev_release(void *p, hipStream_t drain = nullptr);
+hipError_t host_alloc(void **p, size_t bytes, unsigned flags);
+template <class T>
+inline hipError_t host_alloc(T **p, size_t bytes, unsigned flags) {
+  return host_alloc((void **)p, bytes, flags);
+}
+void host_release(void *p);
+hipError_t stream_acquire(hipStream_t *s);
+void stream_release(hipStream_t s);
+
 // Zero-fill device memory and wait for it.  hipMemset runs on the null
 // stream, which does not order against the non-blocking streams the handles
 // launch on: a fill still queued could land after (and clobber) the first
@@ -56,6 +88,12 @@ const char *last_error();
 inline int zero_fill(void *p, size_t bytes) {
   KG_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
   KG_HIP(hipStreamSynchronize(nullptr));
+  return 0;
+}
+// the same fill, not waited for: a handle's create issues all its fills and
+// then waits once on the null stream before any stream-ordered work
+inline int zero_fill_async(void *p, size_t bytes) {
+  KG_HIP(hipMemsetAsync(p, 0, bytes, nullptr));
   return 0;
 }
 

@@ -2868,30 +2868,30 @@ int EigenSolver::init(int N_, bool hostChase_) {
   hostChase = hostChase_;
   maxRot = 8 * N * N + 65536;  // GSL's implicit QR needs ~1.1 N^2 rotations
   const size_t mat = (size_t)N * (N + 1);
-  KG_HIP(hipMalloc(&gA, mat * sizeof(double)));
-  KG_HIP(hipMalloc(&gH, (size_t)N * N * sizeof(double)));
-  KG_HIP(hipMalloc(&gQt, mat * sizeof(double)));
-  KG_HIP(hipMalloc(&gWork, mat * sizeof(double)));
-  KG_HIP(hipMalloc(&tau, (size_t)N * sizeof(double)));
-  KG_HIP(hipMalloc(&dsd, 2 * (size_t)N * sizeof(double)));
-  KG_HIP(hipMalloc(&chaseWork, 4 * (size_t)N * sizeof(double)));
-  KG_HIP(hipMalloc(&dev.hdr, 2 * (size_t)(maxRot + N) * sizeof(int)));
-  KG_HIP(hipMalloc(&dev.cs, 2 * (size_t)maxRot * sizeof(double)));
-  KG_HIP(hipMalloc(&dev.meta, 4 * sizeof(int)));
-  KG_HIP(hipMalloc(&dev.eval, (size_t)N * sizeof(double)));
-  KG_HIP(hipMalloc(&dev.perm, (size_t)N * sizeof(int)));
+  KG_HIP(dev_alloc(&gA, mat * sizeof(double)));
+  KG_HIP(dev_alloc(&gH, (size_t)N * N * sizeof(double)));
+  KG_HIP(dev_alloc(&gQt, mat * sizeof(double)));
+  KG_HIP(dev_alloc(&gWork, mat * sizeof(double)));
+  KG_HIP(dev_alloc(&tau, (size_t)N * sizeof(double)));
+  KG_HIP(dev_alloc(&dsd, 2 * (size_t)N * sizeof(double)));
+  KG_HIP(dev_alloc(&chaseWork, 4 * (size_t)N * sizeof(double)));
+  KG_HIP(dev_alloc(&dev.hdr, 2 * (size_t)(maxRot + N) * sizeof(int)));
+  KG_HIP(dev_alloc(&dev.cs, 2 * (size_t)maxRot * sizeof(double)));
+  KG_HIP(dev_alloc(&dev.meta, 4 * sizeof(int)));
+  KG_HIP(dev_alloc(&dev.eval, (size_t)N * sizeof(double)));
+  KG_HIP(dev_alloc(&dev.perm, (size_t)N * sizeof(int)));
   if (zero_fill(dev.meta, 4 * sizeof(int))) return 1;
   if (hostChase) {
-    KG_HIP(hipHostMalloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    KG_HIP(host_alloc(&h_dsd, 2 * (size_t)N * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
     KG_HIP(hipHostGetDevicePointer((void **)&d_dsd_map, h_dsd, 0));
     // written by the host chase while k_apply<true> reads them: host-coherent, mapped
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
-    KG_HIP(hipHostMalloc(&host.hdr, 2 * (size_t)(maxRot + N) * sizeof(int), fl));
-    KG_HIP(hipHostMalloc(&host.cs, 2 * (size_t)maxRot * sizeof(double), fl));
-    KG_HIP(hipHostMalloc(&host.meta, 4 * sizeof(int), fl));
-    KG_HIP(hipHostMalloc(&host.eval, (size_t)N * sizeof(double), fl));
-    KG_HIP(hipHostMalloc(&host.perm, (size_t)N * sizeof(int), fl));
-    KG_HIP(hipHostMalloc(&hprog, 2 * sizeof(unsigned long long), fl));
+    KG_HIP(host_alloc(&host.hdr, 2 * (size_t)(maxRot + N) * sizeof(int), fl));
+    KG_HIP(host_alloc(&host.cs, 2 * (size_t)maxRot * sizeof(double), fl));
+    KG_HIP(host_alloc(&host.meta, 4 * sizeof(int), fl));
+    KG_HIP(host_alloc(&host.eval, (size_t)N * sizeof(double), fl));
+    KG_HIP(host_alloc(&host.perm, (size_t)N * sizeof(int), fl));
+    KG_HIP(host_alloc(&hprog, 2 * sizeof(unsigned long long), fl));
     hprog[0] = hprog[1] = 0;
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.hdr, host.hdr, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.cs, host.cs, 0));
@@ -2899,13 +2899,13 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.eval, host.eval, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.perm, host.perm, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&dprog, hprog, 0));
-    KG_HIP(hipMalloc(&dprogDev, 2 * sizeof(unsigned long long)));
+    KG_HIP(dev_alloc(&dprogDev, 2 * sizeof(unsigned long long)));
     if (zero_fill(dprogDev, 2 * sizeof(unsigned long long))) return 1;
     KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
     hgc.resize(N);
     hgs.resize(N);
   } else {
-    KG_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    KG_HIP(stream_acquire(&side));
     KG_HIP(hipEventCreateWithFlags(&ev_dsd, hipEventDisableTiming));
     KG_HIP(hipEventCreateWithFlags(&ev_chase, hipEventDisableTiming));
   }
@@ -2963,7 +2963,7 @@ int EigenSolver::init(int N_, bool hostChase_) {
                  " per CU)");
   }
   if (!lds || tri == 2 || tri == 5) {
-    KG_HIP(hipMalloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
+    KG_HIP(dev_alloc(&comm, tmw_comm_words(N) * sizeof(unsigned long long)));
     KG_HIP(allow_dynamic_lds((const void *)k_tridiag_mw, (int)tmw_lds_bytes(N)));
     if (uwv_fits(N))
       KG_HIP(allow_dynamic_lds((const void *)k_unpack_wv, (int)uwv_lds_bytes(N)));
@@ -2982,15 +2982,20 @@ int EigenSolver::init(int N_, bool hostChase_) {
   return 0;
 }
 
+void EigenSolver::drain() {
+  if (side) (void)hipStreamSynchronize(side);
+}
+
 EigenSolver::~EigenSolver() {
+  drain();
   for (void *p : {(void *)gA, (void *)gH, (void *)gQt, (void *)gWork, (void *)tau, (void *)dsd, (void *)chaseWork,
                   (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm, (void *)comm,
                   (void *)dprogDev})
-    if (p) (void)hipFree(p);
+    if (p) dev_release(p);
   for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
                   (void *)host.perm, (void *)hprog})
-    if (p) (void)hipHostFree(p);
-  if (side) (void)hipStreamDestroy(side);
+    if (p) host_release(p);
+  if (side) stream_release(side);
   if (ev_dsd) (void)hipEventDestroy(ev_dsd);
   if (ev_chase) (void)hipEventDestroy(ev_chase);
 }

@@ -17,6 +17,7 @@ typedef void (*ProfileFn)(void *ctx, const char *stage, int phase);
 class EigenSolver {
  public:
   ~EigenSolver();
+  void drain();  // waits for the side stream (device chase)
   // hostChase: run the serial implicit-QR Givens recurrence on the calling
   // host core (overlapped with the device unpack); otherwise on one lane.
   int init(int N, bool hostChase);

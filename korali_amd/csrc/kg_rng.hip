@@ -107,14 +107,14 @@ __device__ inline void mt_combine(const uint32_t *seq, const uint64_t *__restric
   if (t + 512 < MT_N) out[t + 512] = a2;
 }
 
-// seq[624 .. MT_SEQ) from the window seq[0..624); optionally also stored to
+// seq[624 .. lim) from the window seq[0..624); optionally also stored to
 // the ring at absolute positions base + k - 624 (zero words recorded)
 __device__ inline void mt_fill_seq(uint32_t *seq, uint32_t *ring, unsigned long long R, StreamState *st,
-                                   unsigned long long base) {
+                                   unsigned long long base, int lim = MT_SEQ) {
   const int t = threadIdx.x;
-  for (int k0 = MT_N; k0 < MT_SEQ; k0 += 227) {
+  for (int k0 = MT_N; k0 < lim; k0 += 227) {
     const int k = k0 + t;
-    if (t < 227 && k < MT_SEQ) {
+    if (t < 227 && k < lim) {
       const uint32_t v = mt_next(seq[k - 624], seq[k - 623], seq[k - 227]);
       seq[k] = v;
       if (ring) {
@@ -192,18 +192,44 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_chunks(uint32_t *__restrict__ rin
   mt_combine(seq, jumpPoly, seeds + (size_t)((c + K) % (2 * K)) * MT_N);
 }
 
-// initial seeds: chunk c0 + k (2^l <= k < 2^(l+1)) from chunk c0 + k - 2^l
+// initial seeds: chunk c0 + k (2^l <= k < 2^(l+1)) from chunk c0 + k - 2^l.
+// A jump is a XOR over the ~10^4 set bits of its polynomial; the words of
+// the polynomial are split over MT_JUMP_PARTS workgroups per window, each
+// extending the sequence only as far as its terms read and XOR-ing its
+// partial sums into the (zeroed) output window.  Eight levels seed 256
+// chunks once per handle: one workgroup per window made that ~3.2 ms of
+// the handle's creation (C2, KORALI_AMD_RUN_PHASES).
+constexpr int MT_JUMP_PARTS = 16;
 __global__ void __launch_bounds__(MT_TPB) k_mt_jump_level(uint32_t *__restrict__ seeds, unsigned long long K,
                                                          unsigned long long c0, int l,
                                                          const uint64_t *__restrict__ poly) {
   extern __shared__ __attribute__((aligned(16))) uint32_t msm[];
-  const unsigned long long k = (1ULL << l) + blockIdx.x;
+  const unsigned long long k = (1ULL << l) + blockIdx.x / MT_JUMP_PARTS;
+  const int part = (int)(blockIdx.x % MT_JUMP_PARTS);
   if (k >= K) return;
+  const int w0 = part * MT_POLY_WORDS / MT_JUMP_PARTS, w1 = (part + 1) * MT_POLY_WORDS / MT_JUMP_PARTS;
   const uint32_t *src = seeds + (size_t)((c0 + k - (1ULL << l)) % (2 * K)) * MT_N;
   for (int i = threadIdx.x; i < MT_N; i += MT_TPB) msm[i] = src[i];
   __syncthreads();
-  mt_fill_seq(msm, nullptr, 0, nullptr, 0);
-  mt_combine(msm, poly, seeds + (size_t)((c0 + k) % (2 * K)) * MT_N);
+  // terms i < 64 w1 read seq[m + i], m < 624
+  mt_fill_seq(msm, nullptr, 0, nullptr, 0, min(MT_SEQ, MT_N - 1 + 64 * w1));
+  const int t = threadIdx.x;
+  const int m2 = (t + 512 < MT_N) ? t + 512 : MT_N - 1;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int w = w0; w < w1; w++) {
+    uint64_t bits = poly[w];
+    while (bits) {
+      const int i = w * 64 + __builtin_ctzll(bits);
+      bits &= bits - 1;
+      a0 ^= msm[t + i];
+      a1 ^= msm[t + 256 + i];
+      a2 ^= msm[m2 + i];
+    }
+  }
+  uint32_t *out = seeds + (size_t)((c0 + k) % (2 * K)) * MT_N;
+  atomicXor(out + t, a0);
+  atomicXor(out + t + 256, a1);
+  if (t + 512 < MT_N) atomicXor(out + t + 512, a2);
 }
 
 size_t mt_chunk_lds_bytes() { return (size_t)(((MT_SEQ + 3) & ~3) + 1024) * sizeof(uint32_t); }
@@ -408,20 +434,25 @@ unsigned long long next_pow2(unsigned long long x) {
 
 }  // namespace
 
+void MtStream::drain() {
+  if (side_) (void)hipStreamSynchronize(side_);
+}
+
 MtStream::~MtStream() {
-  if (seeds_) (void)hipFree(seeds_);
-  if (polys_) (void)hipFree(polys_);
-  if (plan_) (void)hipFree(plan_);
+  drain();
+  if (seeds_) dev_release(seeds_);
+  if (polys_) dev_release(polys_);
+  if (plan_) dev_release(plan_);
   if (side_) {
     (void)hipStreamSynchronize(side_);
-    (void)hipStreamDestroy(side_);
+    stream_release(side_);
   }
   if (ev_main_) (void)hipEventDestroy(ev_main_);
   if (ev_side_) (void)hipEventDestroy(ev_side_);
-  if (ring_) (void)hipFree(ring_);
-  if (st_) (void)hipFree(st_);
-  if (counts_) (void)hipFree(counts_);
-  if (offsets_) (void)hipFree(offsets_);
+  if (ring_) dev_release(ring_);
+  if (st_) dev_release(st_);
+  if (counts_) dev_release(counts_);
+  if (offsets_) dev_release(offsets_);
 }
 
 int MtStream::init(size_t capacity_words, size_t parallel_min) {
@@ -438,9 +469,9 @@ int MtStream::init(size_t capacity_words, size_t parallel_min) {
     K_ = 256;
     int lk = 0;
     while ((1 << lk) < K_) lk++;
-    KG_HIP(hipMalloc(&seeds_, 2 * (size_t)K_ * MT_N * sizeof(uint32_t)));
-    KG_HIP(hipMalloc(&plan_, sizeof(ChunkPlan)));
-    KG_HIP(hipMalloc(&polys_, (size_t)(lk + 1) * MT_POLY_WORDS * sizeof(uint64_t)));
+    KG_HIP(dev_alloc(&seeds_, 2 * (size_t)K_ * MT_N * sizeof(uint32_t)));
+    KG_HIP(dev_alloc(&plan_, sizeof(ChunkPlan)));
+    KG_HIP(dev_alloc(&polys_, (size_t)(lk + 1) * MT_POLY_WORDS * sizeof(uint64_t)));
     std::vector<uint64_t> hp((size_t)(lk + 1) * MT_POLY_WORDS);
     for (int l = 0; l <= lk; l++)
       if (mt_jump_poly_pow2(lw + l, hp.data() + (size_t)l * MT_POLY_WORDS)) return 1;
@@ -451,18 +482,19 @@ int MtStream::init(size_t capacity_words, size_t parallel_min) {
     capacity_words += W_;  // production rounds up to whole chunks
   }
   R_ = next_pow2(capacity_words + 2 * MT_N + 4096);
-  KG_HIP(hipMalloc(&ring_, R_ * sizeof(uint32_t)));
-  KG_HIP(hipMalloc(&st_, sizeof(StreamState)));
+  KG_HIP(dev_alloc(&ring_, R_ * sizeof(uint32_t)));
+  KG_HIP(dev_alloc(&st_, sizeof(StreamState)));
   if (zero_fill(st_, sizeof(StreamState))) return 1;
   return 0;
 }
 
 int MtStream::ensure_scratch(size_t nb) {
   if (nb <= scratch_blocks_) return 0;
-  if (counts_) KG_HIP(hipFree(counts_));
-  if (offsets_) KG_HIP(hipFree(offsets_));
-  KG_HIP(hipMalloc(&counts_, nb * sizeof(unsigned int)));
-  KG_HIP(hipMalloc(&offsets_, (nb + 1) * sizeof(unsigned long long)));
+  if (counts_ || offsets_) KG_HIP(hipDeviceSynchronize());  // (cached blocks are reused at once)
+  if (counts_) dev_release(counts_);
+  if (offsets_) dev_release(offsets_);
+  KG_HIP(dev_alloc(&counts_, nb * sizeof(unsigned int)));
+  KG_HIP(dev_alloc(&offsets_, (nb + 1) * sizeof(unsigned long long)));
   scratch_blocks_ = nb;
   return 0;
 }
@@ -499,11 +531,13 @@ int MtStream::seed_chunks(unsigned long long pos, hipStream_t s) {
   hipLaunchKernelGGL(k_mt_produce, dim3(1), dim3(MT_TPB), 0, s, ring_, R_, st_, W_ - pos);
   KG_HIP(hipGetLastError());
   const int K = K_;
+  // the levels XOR their partial jumps into zeroed windows
+  KG_HIP(hipMemsetAsync(seeds_, 0, 2 * (size_t)K * MT_N * sizeof(uint32_t), s));
   KG_HIP(hipMemcpyAsync(seeds_ + (size_t)(1 % (2 * K)) * MT_N, ring_ + ((W_ - MT_N) & (R_ - 1)),
                         MT_N * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   for (int l = 0; (1 << l) < K; l++) {
     const int cnt = std::min(1 << l, K - (1 << l));
-    hipLaunchKernelGGL(k_mt_jump_level, dim3(cnt), dim3(MT_TPB), mt_chunk_lds_bytes(), s, seeds_,
+    hipLaunchKernelGGL(k_mt_jump_level, dim3(cnt * MT_JUMP_PARTS), dim3(MT_TPB), mt_chunk_lds_bytes(), s, seeds_,
                        (unsigned long long)K, 1ULL, l, (const uint64_t *)(polys_ + (size_t)l * MT_POLY_WORDS));
     KG_HIP(hipGetLastError());
   }
@@ -572,7 +606,7 @@ size_t MtStream::words_for_normals(size_t M) const {
 
 int MtStream::prefetch(size_t M, hipStream_t main) {
   if (!side_) {
-    KG_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    KG_HIP(stream_acquire(&side_));
     KG_HIP(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
     KG_HIP(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
   }

@@ -56,6 +56,7 @@ class MtStream {
  public:
   MtStream() = default;
   ~MtStream();
+  void drain();  // waits for the side stream's pending production
   // capacity: words the ring must hold beyond the current block.  Streams
   // whose demand reaches `parallel_min` words (1 M: C2 and up) use the
   // chunked multi-workgroup producer (env KORALI_AMD_MT_PARALLEL_MIN / KORALI_AMD_MT_CHUNK_LOG2

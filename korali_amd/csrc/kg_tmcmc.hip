@@ -1990,7 +1990,7 @@ struct HostClock {
 template <typename T>
 int tdalloc(T **p, size_t n) {
   if (n == 0) n = 1;
-  KG_HIP(hipMalloc(p, n * sizeof(T)));
+  KG_HIP(dev_alloc(p, n * sizeof(T)));
   if (zero_fill(*p, n * sizeof(T))) return 1;
   return 0;
 }
@@ -2437,7 +2437,10 @@ double tm_burn_in(const kg_tmcmc_s *h, size_t gen) {
 template <typename T>
 int tm_ensure(T **p, size_t &cap, size_t n) {
   if (n <= cap) return 0;
-  if (*p) KG_HIP(hipFree(*p));
+  if (*p) {
+    KG_HIP(hipDeviceSynchronize());  // (a cached block is reused at once: no kernel may still use it)
+    dev_release(*p);
+  }
   *p = nullptr;
   cap = 0;
   if (tdalloc(p, n)) return 1;
@@ -2716,17 +2719,17 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     delete h;
     return 1;
   }
-  KG_HIP(hipHostMalloc(&h->hE, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hEtail, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hNm, sizeof(NmOut), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hSrc, (size_t)P * sizeof(unsigned), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hSch, (size_t)P * sizeof(ChainSched), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hLenD, (size_t)P * sizeof(double), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hDev, sizeof(TmDev), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc(&h->hCv, (CV_MAX_PTS + 1) * sizeof(CvOut), hipHostMallocDefault));
-  KG_HIP(hipHostMalloc((void **)&h->hRec, 4 * (CV_MAX_PTS + 1) * sizeof(double2),
+  KG_HIP(host_alloc(&h->hE, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hEtail, 2 * (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hNm, sizeof(NmOut), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hW, (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hNsel, (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hSrc, (size_t)P * sizeof(unsigned), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hSch, (size_t)P * sizeof(ChainSched), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hLenD, (size_t)P * sizeof(double), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hDev, sizeof(TmDev), hipHostMallocDefault));
+  KG_HIP(host_alloc(&h->hCv, (CV_MAX_PTS + 1) * sizeof(CvOut), hipHostMallocDefault));
+  KG_HIP(host_alloc((void **)&h->hRec, 4 * (CV_MAX_PTS + 1) * sizeof(double2),
                        hipHostMallocCoherent | hipHostMallocMapped));
   memset(h->hRec, 0, 4 * (CV_MAX_PTS + 1) * sizeof(double2));
   KG_HIP(hipHostGetDevicePointer((void **)&h->dRec, h->hRec, 0));
@@ -2746,7 +2749,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   }
   h->wtmp.resize(P);
   h->nsel.resize(P);
-  KG_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  KG_HIP(stream_acquire(&h->stream));
   KG_HIP(hipMemcpy(h->pmin, cfg->prior_min, N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->pmax, cfg->prior_max, N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->uoff, uoff.data(), N * sizeof(unsigned long long), hipMemcpyHostToDevice));
@@ -2837,16 +2840,16 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->dLen, (void *)h->xch,
                   (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync, (void *)h->mtExtraDev,
                   (void *)h->mtModeDev})
-    if (p) (void)hipFree(p);
+    if (p) dev_release(p);
   for (void *p : {(void *)h->hE, (void *)h->hEtail, (void *)h->hW, (void *)h->hNsel, (void *)h->hSrc, (void *)h->hDev, h->hCv, (void *)h->hRec,
                   (void *)h->hSch, (void *)h->hLenD, (void *)h->hNm})
-    if (p) (void)hipHostFree(p);
+    if (p) host_release(p);
   for (auto *r : h->priorRng) delete r;
   for (auto &t : h->pending) {
     (void)hipEventDestroy(std::get<1>(t));
     (void)hipEventDestroy(std::get<2>(t));
   }
-  (void)hipStreamDestroy(h->stream);
+  stream_release(h->stream);
   delete h;
   return 0;
 }

@@ -1522,7 +1522,7 @@ struct kg_vracer_s {
 namespace {
 
 int vr_alloc(void **p, size_t bytes) {
-  KG_HIP(hipMalloc(p, bytes ? bytes : 16));
+  KG_HIP(dev_alloc(p, bytes ? bytes : 16));
   return kg::zero_fill(*p, bytes ? bytes : 16);
 }
 #define VR_ALLOC(ptr, bytes)                                   \
@@ -1854,7 +1854,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   auto alloc = [&](auto *&p, size_t bytes) {
     if (!rc && vr_alloc((void **)&p, bytes)) rc = 1;
   };
-  hipError_t se = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  hipError_t se = kg::stream_acquire(&h->stream);
   if (se != hipSuccess) {
     delete h;
     kg::set_error(std::string("hipStreamCreate: ") + hipGetErrorString(se));
@@ -1880,7 +1880,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
   alloc(ev.sigb, E * MAXENV * 4), alloc(ev.fin_id, E * 4);
   alloc(ev.pm, (size_t)E * P.S * 4), alloc(ev.ps, (size_t)E * P.S * 4);
-  if (!rc && hipHostMalloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
+  if (!rc && host_alloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
     kg::set_error("vracer: hipHostMalloc failed");
     rc = 1;
   }
@@ -1928,7 +1928,7 @@ extern "C" int kg_debug_cartpole(int device, const double *u0, const double *for
   double *d = nullptr;
   int *o = nullptr;
   const size_t nb = (n * 4 + 2 * n * steps * 4 + n * steps) * sizeof(double);
-  KG_HIP(hipMalloc(&d, nb));
+  KG_HIP(dev_alloc(&d, nb));
   double *du0 = d, *dforce = d + n * 4, *dout = dforce + n * steps;
   o = (int *)(dout + n * steps * 4);
   int rc = 0;
@@ -1943,7 +1943,7 @@ extern "C" int kg_debug_cartpole(int device, const double *u0, const double *for
         hipMemcpy(over, o, n * steps * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
       rc = 1;
   }
-  (void)hipFree(d);
+  dev_release(d);
   if (rc) kg::set_error("kg_debug_cartpole: device call failed");
   return rc;
 }
@@ -1959,11 +1959,11 @@ int kg_vracer_destroy(kg_vracer_t h) {
                   h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id,
                   h->ev.pm, h->ev.ps};
   for (void *p : ptrs)
-    if (p) (void)hipFree(p);
-  if (h->st_host) (void)hipHostFree(h->st_host);
+    if (p) dev_release(p);
+  if (h->st_host) host_release(h->st_host);
   for (auto &e : h->events) (void)hipEventDestroy(e.a), (void)hipEventDestroy(e.b);
   for (auto e : h->pool) (void)hipEventDestroy(e);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->stream) stream_release(h->stream);
   delete h;
   return 0;
 }
@@ -2098,9 +2098,9 @@ int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uin
     if (e != hipSuccess) rc = 1;
     return e != hipSuccess;
   };
-  if (fail(hipMalloc(&dsid, chunk * 8)) || fail(hipMalloc(&dlid, chunk * 8)) || fail(hipMalloc(&u, chunk * 32)) ||
-      fail(hipMalloc(&tm, chunk * 8)) || fail(hipMalloc(&steps, chunk * 4)) || fail(hipMalloc(&done, chunk * 4)) ||
-      fail(hipMalloc(&cum, chunk * 4)) || fail(hipMalloc(&running, 4)) || fail(hipMalloc(&errs, 4)))
+  if (fail(dev_alloc(&dsid, chunk * 8)) || fail(dev_alloc(&dlid, chunk * 8)) || fail(dev_alloc(&u, chunk * 32)) ||
+      fail(dev_alloc(&tm, chunk * 8)) || fail(dev_alloc(&steps, chunk * 4)) || fail(dev_alloc(&done, chunk * 4)) ||
+      fail(dev_alloc(&cum, chunk * 4)) || fail(dev_alloc(&running, 4)) || fail(dev_alloc(&errs, 4)))
     kg::set_error("vracer: testing buffers could not be allocated"), named = true;
   for (size_t b0 = 0; rc == 0 && b0 < n; b0 += chunk) {
     const int m = (int)std::min(chunk, n - b0);
@@ -2139,7 +2139,7 @@ int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uin
   }
   for (void *p : {(void *)dsid, (void *)dlid, (void *)u, (void *)tm, (void *)steps, (void *)done, (void *)cum,
                   (void *)running, (void *)errs})
-    if (p) (void)hipFree(p);
+    if (p) dev_release(p, h->stream);
   if (rc && !named) kg::set_error("vracer: testing episodes failed (HIP error)");
   return rc;
 }

@@ -414,9 +414,12 @@ std::vector<VariableSpec> readVariables(Json &js) {
 }
 
 Json matrixJson(const std::vector<double> &a, size_t rows, size_t cols) {
-  Json m = Json::array();
-  for (size_t r = 0; r < rows; r++) m.push_back(std::vector<double>(a.begin() + r * cols, a.begin() + (r + 1) * cols));
-  return m;
+  std::vector<Json> m;
+  m.reserve(rows);
+  for (size_t r = 0; r < rows; r++) m.emplace_back(std::vector<double>(a.begin() + r * cols, a.begin() + (r + 1) * cols));
+  Json j = Json::array();
+  for (auto &x : m) j.push_back(std::move(x));
+  return j;
 }
 
 std::vector<double> flatten(Json &j) {
@@ -1005,7 +1008,12 @@ struct CmaesModule : SolverModule {
       check(kg_cmaes_get_field(h, k, v.data(), n));
       sv[k] = v;
     }
-    for (const char *k : CMAES_SCALARS) sv[k] = field(k);
+    {
+      constexpr size_t ns = sizeof(CMAES_SCALARS) / sizeof(CMAES_SCALARS[0]);
+      double v[ns];
+      check(kg_cmaes_get_fields(h, CMAES_SCALARS, ns, v));
+      for (size_t i = 0; i < ns; i++) sv[CMAES_SCALARS[i]] = v[i];
+    }
     if (!constraintFns.empty()) {
       sv["Has Constraints"] = true;
       sv["Is Viability Regime"] = field("Is Viability Regime") != 0.0;
@@ -1929,7 +1937,27 @@ struct VracerModule : SolverModule {
   std::string type() const override { return "Agent/Continuous/VRACER"; }
 };
 
+// KORALI_AMD_RUN_PHASES=1: the wall time of each phase of a run on stderr
+// (the engine's fixed cost outside the generation loop)
+struct PhaseClock {
+  bool on = getenv("KORALI_AMD_RUN_PHASES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string text;
+  void mark(const char *phase) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    char b[96];
+    snprintf(b, sizeof(b), " %s=%.3fms", phase, std::chrono::duration<double, std::milli>(n - t).count());
+    text += b;
+    t = n;
+  }
+  ~PhaseClock() {
+    if (on) fprintf(stderr, "[korali_amd run phases]%s\n", text.c_str());
+  }
+};
+
 void runExperiment(Experiment &e, Conduit &conduit) {
+  PhaseClock clk;
   Json &js = e._js;
   ExperimentState &st = *e._state;
   // experiment.config Module Defaults
@@ -1996,6 +2024,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
          "Agent/Continuous/VRACER).",
          sv["Type"].getString().c_str());
   }
+  clk.mark("setup");
   js["Random Seed"] = seeds.counter;
   SolverModule &solver = *st.solver;
   solver.conduit = &conduit;
@@ -2009,6 +2038,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   };
   const auto t0 = std::chrono::steady_clock::now();
   if (gen == 0 && fileOut) save();
+  clk.mark("save0");
   gen++;
   std::vector<std::string> met;
   // marks[i]: seconds from the start of the loop until generation i (1-based
@@ -2038,21 +2068,25 @@ void runExperiment(Experiment &e, Conduit &conduit) {
     gen++;
   }
   const auto t1 = std::chrono::steady_clock::now();
+  clk.mark("loop");
   gen--;
   js["Is Finished"] = true;
   solver.finalize(js);
   js["Current Generation"] = (unsigned long long)gen;
   st.marks = marks;
   solver.getConfiguration(sv);
+  clk.mark("state");
   if (tm) tm->saveDistributions(js);
   if (fileOut) saveState(js, gen);
   if (conduit.dist) conduit.dist->barrier();  // no rank leaves before the others finished
+  clk.mark("files");
   st.log.log(1, "--------------------------------------------------------------------\n");
   st.log.log(1, "%s finished correctly.\n", solver.type().c_str());
   for (const auto &m : met) st.log.log(2, "Termination Criterion Met: %s\n", m.c_str());
   st.log.log(2, "Final Generation: %zu\n", gen);
   st.log.log(2, "Elapsed Time: %.3fs\n", std::chrono::duration<double>(t1 - t0).count());
   st.solver.reset();  // release the device handle
+  clk.mark("release");
 }
 
 }  // namespace

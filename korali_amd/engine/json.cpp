@@ -1,6 +1,8 @@
 // json.cpp — korali::Json (see json.hpp).
 #include "json.hpp"
 
+#include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -48,87 +50,150 @@ Function &getFunction(size_t index) {
   return functionTable()[index];
 }
 
-Json::Json(void (*fn)(Sample &)) : t_(Type::UInt), u_(registerFunction(Function(fn))) {}
+Json::Json(void (*fn)(Sample &)) : t_(Type::UInt) { v_.u = registerFunction(Function(fn)); }
+
+void Json::release() noexcept {
+  switch (t_) {
+    case Type::String: delete v_.s; break;
+    case Type::Array:
+      if (packed_)
+        delete v_.pd;
+      else
+        delete v_.a;
+      break;
+    case Type::Object: delete v_.o; break;
+    default: break;
+  }
+  t_ = Type::Null;
+  packed_ = false;
+  v_.u = 0;
+}
+
+void Json::copyFrom(const Json &o) {
+  switch (o.t_) {
+    case Type::String: v_.s = new std::string(*o.v_.s); break;
+    case Type::Array:
+      if (o.packed_)
+        v_.pd = new std::vector<double>(*o.v_.pd);
+      else
+        v_.a = new std::vector<Json>(*o.v_.a);
+      break;
+    case Type::Object: v_.o = new std::map<std::string, Json>(*o.v_.o); break;
+    default: v_ = o.v_;
+  }
+}
+
+void Json::unpack() const {
+  if (!packed_) return;
+  auto *a = new std::vector<Json>(v_.pd->begin(), v_.pd->end());
+  delete v_.pd;
+  v_.a = a;
+  packed_ = false;
+}
+
+std::vector<Json> &Json::arrayRef() {
+  if (t_ == Type::Null) *this = array();
+  if (t_ != Type::Array) throw std::runtime_error("push_back on a non-array JSON value");
+  unpack();
+  return *v_.a;
+}
+
+const std::map<std::string, Json> &Json::items() const {
+  static const std::map<std::string, Json> none;
+  return t_ == Type::Object ? *v_.o : none;
+}
+
+const std::vector<Json> &Json::elements() const {
+  static const std::vector<Json> none;
+  if (t_ != Type::Array) return none;
+  unpack();
+  return *v_.a;
+}
 
 Json &Json::operator[](const std::string &key) {
-  if (t_ == Type::Null) t_ = Type::Object;
+  if (t_ == Type::Null) *this = object();
   if (t_ != Type::Object)
     throw std::runtime_error("cannot index a JSON " + std::string(typeName(t_)) + " with key '" + key + "'");
-  return o_[key];
+  return (*v_.o)[key];
 }
 
 Json &Json::operator[](size_t idx) {
-  if (t_ == Type::Null) t_ = Type::Array;
+  if (t_ == Type::Null) *this = array();
   if (t_ != Type::Array)
     throw std::runtime_error("cannot index a JSON " + std::string(typeName(t_)) + " with [" + std::to_string(idx) + "]");
-  if (idx >= a_.size()) a_.resize(idx + 1);
-  return a_[idx];
+  unpack();
+  if (idx >= v_.a->size()) v_.a->resize(idx + 1);
+  return (*v_.a)[idx];
 }
 
 const Json &Json::at(const std::string &key) const {
-  if (t_ != Type::Object || !o_.count(key)) throw std::runtime_error("missing key '" + key + "'");
-  return o_.at(key);
+  if (t_ != Type::Object) throw std::runtime_error("missing key '" + key + "'");
+  const auto it = v_.o->find(key);
+  if (it == v_.o->end()) throw std::runtime_error("missing key '" + key + "'");
+  return it->second;
 }
 
 const Json &Json::at(size_t idx) const {
-  if (t_ != Type::Array || idx >= a_.size()) throw std::runtime_error("index out of range");
-  return a_[idx];
+  if (t_ != Type::Array || idx >= size()) throw std::runtime_error("index out of range");
+  unpack();
+  return (*v_.a)[idx];
 }
 
 double Json::getDouble() const {
   switch (t_) {
-    case Type::Double: return d_;
-    case Type::Int: return (double)i_;
-    case Type::UInt: return (double)u_;
-    case Type::Bool: return b_ ? 1.0 : 0.0;
+    case Type::Double: return v_.d;
+    case Type::Int: return (double)v_.i;
+    case Type::UInt: return (double)v_.u;
+    case Type::Bool: return v_.b ? 1.0 : 0.0;
     default: throw std::runtime_error(std::string("expected a number, found a ") + typeName(t_));
   }
 }
 
 long long Json::getInt() const {
   switch (t_) {
-    case Type::Int: return i_;
-    case Type::UInt: return (long long)u_;
+    case Type::Int: return v_.i;
+    case Type::UInt: return (long long)v_.u;
     case Type::Double:
-      if (d_ != std::floor(d_)) throw std::runtime_error("expected an integer, found " + std::to_string(d_));
-      return (long long)d_;
-    case Type::Bool: return b_ ? 1 : 0;
+      if (v_.d != std::floor(v_.d)) throw std::runtime_error("expected an integer, found " + std::to_string(v_.d));
+      return (long long)v_.d;
+    case Type::Bool: return v_.b ? 1 : 0;
     default: throw std::runtime_error(std::string("expected an integer, found a ") + typeName(t_));
   }
 }
 
 unsigned long long Json::getUInt() const {
   switch (t_) {
-    case Type::UInt: return u_;
+    case Type::UInt: return v_.u;
     case Type::Int:
-      if (i_ < 0) throw std::runtime_error("expected a non-negative integer, found " + std::to_string(i_));
-      return (unsigned long long)i_;
+      if (v_.i < 0) throw std::runtime_error("expected a non-negative integer, found " + std::to_string(v_.i));
+      return (unsigned long long)v_.i;
     case Type::Double:
-      if (!(d_ >= 0) || d_ != std::floor(d_))
-        throw std::runtime_error("expected a non-negative integer, found " + std::to_string(d_));
-      return d_ >= 1.8446744073709552e19 ? ~0ULL : (unsigned long long)d_;
-    case Type::Bool: return b_ ? 1 : 0;
+      if (!(v_.d >= 0) || v_.d != std::floor(v_.d))
+        throw std::runtime_error("expected a non-negative integer, found " + std::to_string(v_.d));
+      return v_.d >= 1.8446744073709552e19 ? ~0ULL : (unsigned long long)v_.d;
+    case Type::Bool: return v_.b ? 1 : 0;
     default: throw std::runtime_error(std::string("expected an integer, found a ") + typeName(t_));
   }
 }
 
 bool Json::getBool() const {
-  if (t_ == Type::Bool) return b_;
-  if (t_ == Type::Int) return i_ != 0;
-  if (t_ == Type::UInt) return u_ != 0;
+  if (t_ == Type::Bool) return v_.b;
+  if (t_ == Type::Int) return v_.i != 0;
+  if (t_ == Type::UInt) return v_.u != 0;
   throw std::runtime_error(std::string("expected a boolean, found a ") + typeName(t_));
 }
 
 const std::string &Json::getString() const {
   if (t_ != Type::String) throw std::runtime_error(std::string("expected a string, found a ") + typeName(t_));
-  return s_;
+  return *v_.s;
 }
 
 std::vector<double> Json::getDoubleVector() const {
   if (t_ != Type::Array) throw std::runtime_error(std::string("expected an array, found a ") + typeName(t_));
+  if (packed_) return *v_.pd;
   std::vector<double> v;
-  v.reserve(a_.size());
-  for (const auto &x : a_) v.push_back(x.getDouble());
+  v.reserve(v_.a->size());
+  for (const auto &x : *v_.a) v.push_back(x.getDouble());
   return v;
 }
 
@@ -161,10 +226,12 @@ void dumpDouble(std::string &out, double d) {
   } else if (std::isinf(d)) {
     out += d > 0 ? "Infinity" : "-Infinity";
   } else {
+    // shortest text that reads back to the same double (nlohmann's grisu2
+    // output has the same property)
     char b[32];
-    snprintf(b, sizeof(b), "%.17g", d);
-    out += b;
-    if (!strpbrk(b, ".eE")) out += ".0";
+    const auto r = std::to_chars(b, b + sizeof(b), d);
+    out.append(b, r.ptr);
+    if (std::find_if(b, r.ptr, [](char c) { return c == '.' || c == 'e' || c == 'E'; }) == r.ptr) out += ".0";
   }
 }
 }  // namespace
@@ -177,28 +244,38 @@ void Json::dumpTo(std::string &out, int indent, int level) const {
   };
   switch (t_) {
     case Type::Null: out += "null"; break;
-    case Type::Bool: out += b_ ? "true" : "false"; break;
-    case Type::Int: out += std::to_string(i_); break;
-    case Type::UInt: out += std::to_string(u_); break;
-    case Type::Double: dumpDouble(out, d_); break;
-    case Type::String: dumpString(out, s_); break;
+    case Type::Bool: out += v_.b ? "true" : "false"; break;
+    case Type::Int: out += std::to_string(v_.i); break;
+    case Type::UInt: out += std::to_string(v_.u); break;
+    case Type::Double: dumpDouble(out, v_.d); break;
+    case Type::String: dumpString(out, *v_.s); break;
     case Type::Array: {
       out += '[';
+      if (packed_) {
+        for (size_t k = 0; k < v_.pd->size(); k++) {
+          if (k) out += ',';
+          nl(level + 1);
+          dumpDouble(out, (*v_.pd)[k]);
+        }
+        if (!v_.pd->empty()) nl(level);
+        out += ']';
+        break;
+      }
       bool first = true;
-      for (const auto &x : a_) {
+      for (const auto &x : *v_.a) {
         if (!first) out += ',';
         first = false;
         nl(level + 1);
         x.dumpTo(out, indent, level + 1);
       }
-      if (!a_.empty()) nl(level);
+      if (!v_.a->empty()) nl(level);
       out += ']';
       break;
     }
     case Type::Object: {
       out += '{';
       bool first = true;
-      for (const auto &kv : o_) {
+      for (const auto &kv : *v_.o) {
         if (!first) out += ',';
         first = false;
         nl(level + 1);
@@ -206,7 +283,7 @@ void Json::dumpTo(std::string &out, int indent, int level) const {
         out += indent < 0 ? ":" : ": ";
         kv.second.dumpTo(out, indent, level + 1);
       }
-      if (!o_.empty()) nl(level);
+      if (!v_.o->empty()) nl(level);
       out += '}';
       break;
     }

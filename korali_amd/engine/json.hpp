@@ -33,33 +33,73 @@ class Json {
  public:
   enum class Type { Null, Bool, Int, UInt, Double, String, Array, Object };
 
-  Json() = default;
-  Json(std::nullptr_t) {}
-  Json(bool b) : t_(Type::Bool), b_(b) {}
-  Json(int v) : t_(Type::Int), i_(v) {}
-  Json(long v) : t_(Type::Int), i_(v) {}
-  Json(long long v) : t_(Type::Int), i_(v) {}
-  Json(unsigned v) : t_(Type::UInt), u_(v) {}
-  Json(unsigned long v) : t_(Type::UInt), u_(v) {}
-  Json(unsigned long long v) : t_(Type::UInt), u_(v) {}
-  Json(double v) : t_(Type::Double), d_(v) {}
-  Json(float v) : t_(Type::Double), d_(v) {}
-  Json(const char *s) : t_(Type::String), s_(s) {}
-  Json(const std::string &s) : t_(Type::String), s_(s) {}
+  Json() { v_.u = 0; }
+  Json(std::nullptr_t) { v_.u = 0; }
+  Json(bool b) : t_(Type::Bool) { v_.u = 0, v_.b = b; }
+  Json(int v) : t_(Type::Int) { v_.i = v; }
+  Json(long v) : t_(Type::Int) { v_.i = v; }
+  Json(long long v) : t_(Type::Int) { v_.i = v; }
+  Json(unsigned v) : t_(Type::UInt) { v_.u = v; }
+  Json(unsigned long v) : t_(Type::UInt) { v_.u = v; }
+  Json(unsigned long long v) : t_(Type::UInt) { v_.u = v; }
+  Json(double v) : t_(Type::Double) { v_.d = v; }
+  Json(float v) : t_(Type::Double) { v_.d = v; }
+  Json(const char *s) : t_(Type::String) { v_.s = new std::string(s); }
+  Json(const std::string &s) : t_(Type::String) { v_.s = new std::string(s); }
   Json(void (*fn)(Sample &));  // registers the function, stores its index
+  // an array of doubles is held packed (one contiguous block, no per-element
+  // node) until an element is addressed as a node (operator[], at,
+  // elements(), push_back): vectors and matrices of solver state, the bulk of
+  // every result file, are built, copied, read back and dumped as blocks
   template <typename T>
   Json(const std::vector<T> &v) : t_(Type::Array) {
-    for (const auto &x : v) a_.emplace_back(x);
+    if constexpr (std::is_same<T, double>::value || std::is_same<T, float>::value) {
+      packed_ = true;
+      v_.pd = new std::vector<double>(v.begin(), v.end());
+    } else {
+      v_.a = new std::vector<Json>();
+      v_.a->reserve(v.size());
+      for (const auto &x : v) v_.a->emplace_back(x);
+    }
+  }
+  Json(std::vector<double> &&v) : t_(Type::Array), packed_(true) { v_.pd = new std::vector<double>(std::move(v)); }
+  Json(const Json &o) : t_(o.t_), packed_(o.packed_) { copyFrom(o); }
+  Json(Json &&o) noexcept : t_(o.t_), packed_(o.packed_), v_(o.v_) {
+    o.t_ = Type::Null;
+    o.packed_ = false;
+    o.v_.u = 0;
+  }
+  Json &operator=(const Json &o) {
+    if (this != &o) {
+      Json c(o);
+      swap(c);
+    }
+    return *this;
+  }
+  Json &operator=(Json &&o) noexcept {
+    if (this != &o) {
+      Json c(std::move(o));
+      swap(c);
+    }
+    return *this;
+  }
+  ~Json() { release(); }
+  void swap(Json &o) noexcept {
+    std::swap(t_, o.t_);
+    std::swap(packed_, o.packed_);
+    std::swap(v_, o.v_);
   }
 
   static Json array() {
     Json j;
     j.t_ = Type::Array;
+    j.v_.a = new std::vector<Json>();
     return j;
   }
   static Json object() {
     Json j;
     j.t_ = Type::Object;
+    j.v_.o = new std::map<std::string, Json>();
     return j;
   }
   static Json parse(const std::string &text);
@@ -80,18 +120,20 @@ class Json {
   Json &operator[](int idx) { return (*this)[(size_t)idx]; }
   const Json &at(const std::string &key) const;
   const Json &at(size_t idx) const;
-  bool contains(const std::string &key) const { return t_ == Type::Object && o_.count(key) != 0; }
+  bool contains(const std::string &key) const { return t_ == Type::Object && v_.o->count(key) != 0; }
   void erase(const std::string &key) {
-    if (t_ == Type::Object) o_.erase(key);
+    if (t_ == Type::Object) v_.o->erase(key);
   }
-  size_t size() const { return t_ == Type::Array ? a_.size() : t_ == Type::Object ? o_.size() : 0; }
-  void push_back(const Json &v) {
-    if (t_ == Type::Null) t_ = Type::Array;
-    if (t_ != Type::Array) throw std::runtime_error("push_back on a non-array JSON value");
-    a_.push_back(v);
+  size_t size() const {
+    return t_ == Type::Array ? (packed_ ? v_.pd->size() : v_.a->size()) : t_ == Type::Object ? v_.o->size() : 0;
   }
-  const std::map<std::string, Json> &items() const { return o_; }
-  const std::vector<Json> &elements() const { return a_; }
+  void push_back(const Json &v) { arrayRef().push_back(v); }
+  void push_back(Json &&v) { arrayRef().push_back(std::move(v)); }
+  // the packed doubles of an array held packed, else nullptr (fast paths of
+  // readers that need no nodes)
+  const std::vector<double> *packedDoubles() const { return t_ == Type::Array && packed_ ? v_.pd : nullptr; }
+  const std::map<std::string, Json> &items() const;
+  const std::vector<Json> &elements() const;
 
   double getDouble() const;
   long long getInt() const;
@@ -111,9 +153,9 @@ class Json {
     return get<T>();
   }
   // comparisons with plain values (sample.cpp: `(*_self)["Module"] == "Solver"`)
-  bool operator==(const char *v) const { return is_string() && s_ == v; }
-  bool operator==(const std::string &v) const { return is_string() && s_ == v; }
-  bool operator==(bool v) const { return is_bool() && b_ == v; }
+  bool operator==(const char *v) const { return is_string() && *v_.s == v; }
+  bool operator==(const std::string &v) const { return is_string() && *v_.s == v; }
+  bool operator==(bool v) const { return is_bool() && v_.b == v; }
   bool operator==(double v) const { return is_number() && getDouble() == v; }
   bool operator==(int v) const { return is_number() && getDouble() == (double)v; }
   template <typename T>
@@ -124,14 +166,27 @@ class Json {
   std::string dump(int indent = -1) const;
 
  private:
+  // 16 bytes a node: the tag and one word (a scalar, or the heap-held
+  // string / array / object) -- result files hold 10^5-10^6 numbers
+  // (Sample Population, databases), built and copied every save.  packed_:
+  // an Array held as doubles (pd) rather than nodes (a); unpacking on first
+  // node access changes the representation, not the value, hence mutable.
   Type t_ = Type::Null;
-  bool b_ = false;
-  long long i_ = 0;
-  unsigned long long u_ = 0;
-  double d_ = 0.0;
-  std::string s_;
-  std::vector<Json> a_;
-  std::map<std::string, Json> o_;
+  mutable bool packed_ = false;
+  mutable union {
+    bool b;
+    long long i;
+    unsigned long long u;
+    double d;
+    std::string *s;
+    std::vector<Json> *a;
+    std::vector<double> *pd;
+    std::map<std::string, Json> *o;
+  } v_;
+  void unpack() const;
+  void release() noexcept;
+  void copyFrom(const Json &o);
+  std::vector<Json> &arrayRef();  // null becomes an empty array
   void dumpTo(std::string &out, int indent, int level) const;
 };
 

@@ -29,6 +29,10 @@ py::object toPy(const Json &j) {
     case Json::Type::String: return py::str(j.getString());
     case Json::Type::Array: {
       py::list l;
+      if (const auto *pd = j.packedDoubles()) {
+        for (double d : *pd) l.append(d);
+        return std::move(l);
+      }
       for (const auto &x : j.elements()) l.append(toPy(x));
       return std::move(l);
     }
