@@ -78,7 +78,7 @@ STAGE_KERNELS = {
     # C3: the annealing search (symmetric form by default)
     "min_search": [("kg::k_tm_nm_sym", "kg::k_tm_nm_search")],
 }
-PROFILE_ROUNDS = ("r4", "r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
+PROFILE_ROUNDS = ("r5", "r4", "r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
 
 
 def profile_file(name):
@@ -213,6 +213,7 @@ def cpu_baseline(seconds_budget=6.0):
     arithmetic with an inline objective, no per-sample dispatch); the
     bit-exact build (correctly rounded log/exp, slower) is reported beside it
     on a shorter sample."""
+    progress("cpu baseline (oracle, one pinned core)")
     with pinned_core() as core:
         gens, el = _cmaes_oracle_rate("libm", 10, 100, seconds_budget)
         gens_cr, el_cr = _cmaes_oracle_rate("cr", 2, 10, seconds_budget / 2)
@@ -263,6 +264,7 @@ def engine_rate(steps, warmup, cov):
       when each generation's termination check returned), no subtraction
       of two runs."""
     import korali
+    progress("engine rate (korali.Engine runs of C2)")
     k = korali.Engine()
     k.run(c2_experiment(cov, warmup))  # (first-use costs: module load, code objects)
     short, long_ = 50, 50 + max(steps, 300)
@@ -283,7 +285,103 @@ def engine_rate(steps, warmup, cov):
     marks = korali._generation_completion_times(f)
     w = min(warmup, steps - 1)
     in_run = (steps - w) / (marks[steps] - marks[w]) if len(marks) == steps + 1 else None
-    return diff, e2e, in_run
+    # short runs: the fixed cost against 20 generations (median of five)
+    ts = []
+    for _ in range(5):
+        f = c2_experiment(cov, 20)
+        t0 = time.perf_counter()
+        k.run(f)
+        ts.append(time.perf_counter() - t0)
+    e2e20 = 20 / sorted(ts)[2]
+    return diff, e2e, in_run, e2e20
+
+
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """One line on stderr per phase (a long default run stays visibly alive;
+    the JSON line alone goes to stdout)."""
+    print(f"[bench {time.perf_counter() - _T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+C1_N, C1_LAMBDA, C1_GENS = 8, 16, 1000
+
+
+def c1_experiment(objective):
+    """CMA-ES, 8-dim negative Rosenbrock, lambda=16,
+    x0=0, sigma0=1, Max Generations 1000, seed 1337, through korali.Engine.
+    objective "kernel": the device objective; "python": the reference
+    example's Python model (examples/optimization/model.py negative_rosenbrock)
+    called per sample through the Sequential conduit."""
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Optimization"
+    if objective == "kernel":
+        e["Problem"]["Objective Kernel"] = "Negative Rosenbrock"
+    else:
+        def model(s):
+            x = s["Parameters"]
+            s["F(x)"] = -sum(100.0 * (x[i + 1] - x[i] ** 2) ** 2 + (1.0 - x[i]) ** 2 for i in range(len(x) - 1))
+        e["Problem"]["Objective Function"] = model
+    for i in range(C1_N):
+        e["Variables"][i]["Name"] = "X" + str(i)
+        e["Variables"][i]["Initial Value"] = 0.0
+        e["Variables"][i]["Initial Standard Deviation"] = 1.0
+    e["Solver"]["Type"] = "Optimizer/CMAES"
+    e["Solver"]["Population Size"] = C1_LAMBDA
+    e["Solver"]["Termination Criteria"]["Max Generations"] = C1_GENS
+    e["Random Seed"] = 1337
+    e["File Output"]["Enabled"] = False
+    e["Console Output"]["Verbosity"] = "Silent"
+    return e
+
+
+def c1_line(cpu=True):
+    """C1 beside the reference's CPU arithmetic: whole korali.Engine runs of
+    1000 generations (creation, initialisation and the final state included),
+    median of three, with the device objective and with the Python model;
+    refcpu: the oracle restatement (-O3, system libm, one pinned core) on the
+    same shape."""
+    import korali
+    progress("C1 line (korali.Engine, N=8, lambda=16)")
+    k = korali.Engine()
+    k.run(c1_experiment("kernel"))  # (first-use costs)
+    out = {"workload": "C1: CMA-ES, 8-dim negative Rosenbrock, lambda=16, mu=8, x0=0, sigma0=1, "
+                       "1000 generations, seed 1337, korali.Engine (Sequential conduit)"}
+    for obj in ("kernel", "python"):
+        ts = []
+        for _ in range(3):
+            e = c1_experiment(obj)
+            t0 = time.perf_counter()
+            k.run(e)
+            ts.append(time.perf_counter() - t0)
+        out[f"engine_{obj}_generations_per_sec"] = C1_GENS / sorted(ts)[1]
+    if cpu:
+        progress("C1 refcpu (whole 1000-generation runs, one pinned core)")
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import refcpu as R
+        lib = R.lib("libm")
+        lib.kr_set_threads(1)
+        runs, t0 = 0, time.perf_counter()
+        with pinned_core():
+            # whole runs from a fresh state, like the engine's (a run continued
+            # past its 1000 generations degenerates the covariance)
+            while runs < 3 or time.perf_counter() - t0 < 1.0:
+                o = R.CMAES(C1_N, C1_LAMBDA, C1_LAMBDA // 2, variant="libm")
+                o["Initial Value"] = np.zeros(C1_N)
+                o["Initial Standard Deviation"] = np.ones(C1_N)
+                lib.kr_rng_seed(o.rng(0).ptr, 1337)
+                lib.kr_rng_seed(o.rng(1).ptr, 1338)
+                for g in range(1, C1_GENS + 1):
+                    o.generation(g, "rosenbrock")
+                runs += 1
+        el = time.perf_counter() - t0
+        out["refcpu_generations_per_sec"] = runs * C1_GENS / el
+        out["refcpu_sample"] = (f"{runs} whole C1 runs of {C1_GENS} generations, oracle/refcpu.c -O3 (no -march), "
+                                f"system libm, inline objective, 1 pinned core")
+        out["engine_kernel_vs_refcpu"] = out["engine_kernel_generations_per_sec"] / out["refcpu_generations_per_sec"]
+    return out
 
 
 def free_port():
@@ -407,6 +505,7 @@ def main():
     if not os.path.exists(_build.LIB):
         _build.build()
 
+    progress(f"C2 timed run ({args.steps} generations after {args.warmup} warm-up)")
     dev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
                       normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=args.cov, device=device)
     gen = 0
@@ -454,9 +553,11 @@ def main():
 
     best = float(dev["Best Ever Value"][0])
     dev.close()
-    eng, eng_e2e, eng_in_run = engine_rate(args.steps, args.warmup, args.cov) if world == 1 else (None, None, None)
+    eng, eng_e2e, eng_in_run, eng_e2e20 = (engine_rate(args.steps, args.warmup, args.cov) if world == 1
+                                           else (None, None, None, None))
     # the other covariance mode on this rank alone (reported beside `value`)
     alt = "mfma" if args.cov == "exact" else "exact"
+    progress(f"{alt} covariance rate")
     adev = CmaesDevice(N_VARS, LAMBDA, initial_value=np.zeros(N_VARS), initial_std=np.ones(N_VARS),
                        normal_seed=1337 + 2 * rank, uniform_seed=1338 + 2 * rank, cov_mode=alt, device=device)
     g2 = 0
@@ -488,6 +589,7 @@ def main():
             mfma_kernel = rankmu_roofline(ms, MU, N_VARS, "c2_pmc_traffic.csv")
     adev.close()
     c4 = c4_scaling(args, world, rank, dist) if dist is not None else None
+    c1 = c1_line(cpu=not args.no_cpu_baseline) if world == 1 else None
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -528,9 +630,11 @@ def main():
         "engine_generations_per_sec": eng,
         "engine_end_to_end_generations_per_sec": eng_e2e,
         "engine_in_run_generations_per_sec": eng_in_run,
+        "engine_end_to_end_20_generations_per_sec": eng_e2e20,
         f"{alt}_covariance_generations_per_sec_per_gpu": alt_rate,
         "rankmu_mfma_roofline": mfma_kernel,
         "c4_sharded": c4,
+        "c1": c1,
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
