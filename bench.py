@@ -1077,7 +1077,9 @@ def run_c5(args):
         d.training_step()
     d.synchronize()
     nu = max(1.0, d.scalar("policy_update_count") - u0)
-    meta_us = ((d.get("meta_phase_ticks").astype(np.float64) - m0) / nu * 0.01).tolist()  # 100 MHz ticks
+    mt = (d.get("meta_phase_ticks").astype(np.float64) - m0) / nu
+    meta_us = (mt[:3] * 0.01).tolist()  # 100 MHz ticks
+    walks = {"longest_walk_entries": mt[3], "walked_entries": mt[4], "walks": mt[5]}  # per update
     stages = {}
     for st in ("environment_step", "update", "gemm_rollout", "gemm_update"):
         ms, cnt = d.profile_read(st)
@@ -1111,6 +1113,7 @@ def run_c5(args):
         "stage_ms": stages,
         "metadata_kernel_phases_us": {"setup_and_importance_weights": meta_us[0], "retrace_chains": meta_us[1],
                                       "loss_gradient_and_metadata": meta_us[2]},
+        "retrace_walks_per_update": walks,
         "update_roofline": {"flops_per_update": upd_flops, "avg_update_ms": upd_ms,
                             "achieved_tflops": upd_flops / (upd_ms * 1e-3) / 1e12 if upd_ms else None,
                             "peak": FP32_PEAK_TFLOPS,

@@ -3108,7 +3108,7 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
     return 1;
   }
   clk.mark("buffers");
-  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32);
+  if (getenv("KORALI_AMD_TRACE_EIGEN")) rc |= dalloc(&h->eigTrace, 32 + 8 * (size_t)std::max(N, 128));
   if (host_alloc(&h->summary, sizeof(TermSummary), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void **)&h->summaryDev, h->summary, 0) != hipSuccess) {
     delete h;
@@ -4054,6 +4054,32 @@ int kg_cmaes_synchronize(kg_cmaes_t h) {
             "[korali_amd mw2 tridiag, writer wg] staging %llu barrier %llu nrm2-chain %llu scalars %llu products %llu "
             "dsymv-chains %llu x-gather %llu xv %llu poll %llu update %llu\n",
             t[16], t[17], t[18], t[19], t[20], t[21], t[22], t[23], t[24], t[25]);
+    // the one-workgroup kernel's last launch, step by step: every phase's
+    // ticks fitted as a + b n over the steps (n = N-1-i, the chain length)
+    if (h->eig.tridiag_kind() == 4) {
+      const int steps = h->N - 2;
+      std::vector<unsigned long long> ps(8 * (size_t)steps);
+      KG_HIP(hipMemcpy(ps.data(), h->eigTrace + 32, ps.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      static const char *nm[8] = {"staging", "nrm2-chain", "scalars+v", "wait-A", "dsymv", "wait-E", "xv+pivot", "wait-X"};
+      std::string line = "[korali_amd sq tridiag per step, ticks = a + b n]";
+      for (int k = 0; k < 8; k++) {
+        double sx = 0, sy = 0, sxx = 0, sxy = 0;
+        for (int i = 0; i < steps; i++) {
+          const double x = h->N - 1 - i, y = (double)ps[8 * (size_t)i + k];
+          sx += x, sy += y, sxx += x * x, sxy += x * y;
+        }
+        const double b = (steps * sxy - sx * sy) / (steps * sxx - sx * sx), a = (sy - b * sx) / steps;
+        char buf[96];
+        snprintf(buf, sizeof(buf), " %s a=%.0f b=%.1f", nm[k], a, b);
+        line += buf;
+      }
+      fprintf(stderr, "%s\n", line.c_str());
+      for (int i = 0; i < steps; i += 25) {
+        fprintf(stderr, "[korali_amd sq tridiag step %d, n=%d]", i, h->N - 1 - i);
+        for (int k = 0; k < 8; k++) fprintf(stderr, " %llu", ps[8 * (size_t)i + k]);
+        fprintf(stderr, "\n");
+      }
+    }
   }
   return check_errors(h);
 }

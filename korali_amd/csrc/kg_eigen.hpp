@@ -38,6 +38,7 @@ class EigenSolver {
     rotations = (hostChase && host.meta) ? host.meta[1] : -1;
   }
   bool hostChase = true;
+  int tridiag_kind() const { return tri; }  // (diagnostics)
 
  private:
   int N = 0, maxRot = 0;

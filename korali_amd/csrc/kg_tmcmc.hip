@@ -968,6 +968,11 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_search(int P, const double *__
 // controller form pays two hand-offs per round: points out, partials in.)
 // Results equal k_tm_nm_search's: the same partials, the same combine, the
 // same logic.
+//
+// NMW (16, 32 or 64) workgroups: enough that each thread evaluates about one
+// log-likelihood per point (P / 256 of them), no more -- every extra
+// workgroup is one more arrival to wait for and one more record to add.
+template <int NMW>
 __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__restrict__ ll,
                                                        const TmDev *__restrict__ dev, double rho, double target,
                                                        NmTab tab, NmSync *__restrict__ S, NmOut *__restrict__ out) {
@@ -980,7 +985,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
   __shared__ double spts[NM_PTS];
   __shared__ int sfail, sbn;
   const unsigned long long tk0 = __builtin_amdgcn_s_memrealtime();
-  const int w = blockIdx.x, chunk = (P + NM_W - 1) / NM_W;
+  const int w = blockIdx.x, chunk = (P + NMW - 1) / NMW;
   const int i0 = w * chunk < P ? w * chunk : P, i1 = (w + 1) * chunk < P ? (w + 1) * chunk : P;
   const bool inLds = chunk <= NM_LDS;
   if (inLds)
@@ -1048,7 +1053,7 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     if (wid == 0) {
       unsigned long long spins = 0;
       for (;;) {
-        const bool ok = nm_ld(&S->done[lane]) >= round;  // NM_W == 64: one lane per workgroup
+        const bool ok = lane >= NMW || nm_ld(&S->done[lane]) >= round;  // one lane per workgroup
         if (__all(ok)) break;
         if (++spins >= NM_SPIN_LIMIT) break;
         __builtin_amdgcn_s_sleep(1);
@@ -1059,7 +1064,11 @@ __global__ void __launch_bounds__(NM_TPB) k_tm_nm_sym(int P, const double *__res
     const unsigned long long rc = __builtin_amdgcn_s_memrealtime();
     if (grp < n) {
       const int k = grp;
-      NmPart v = nm_part_add(nm_part_ld(&S->part2[round & 1][sub][k]), nm_part_ld(&S->part2[round & 1][sub + 32][k]));
+      NmPart v = NmPart{0, 0, 0, 0, 0, 0};  // (an exact identity of nm_part_add)
+      if (NMW == 64)
+        v = nm_part_add(nm_part_ld(&S->part2[round & 1][sub][k]), nm_part_ld(&S->part2[round & 1][sub + 32][k]));
+      else if (sub < NMW)
+        v = nm_part_ld(&S->part2[round & 1][sub][k]);
       for (int off = 16; off > 0; off >>= 1) v = nm_part_add(v, nm_part_shfl32(v, off));
       if (sub == 0) {
         const dd Sd{v.s_hi, v.s_lo}, Qd{v.q_hi, v.q_lo};
@@ -2330,7 +2339,17 @@ int min_search_device(kg_tmcmc_s *h, double exponent, double objCov, double &xmi
     // (KORALI_AMD_NM_SYM=0: the controller form, two hand-offs per round)
     const char *symEnv = getenv("KORALI_AMD_NM_SYM");  // (read per search: tests switch it)
     const bool sym = !(symEnv && *symEnv == '0');
-    if (launch_resident(sym ? (const void *)k_tm_nm_sym : (const void *)k_tm_nm_search, dim3(sym ? NM_W : 1 + NM_W),
+    // symmetric workgroups: about one log-likelihood per thread and point
+    // (KORALI_AMD_NM_W = 16 | 32 | 64 forces a count)
+    int nmw = 16;
+    while (nmw < NM_W && (size_t)nmw * NM_TPB < (size_t)P) nmw *= 2;
+    if (const char *e = getenv("KORALI_AMD_NM_W")) {
+      const int v = atoi(e);
+      if (v == 16 || v == 32 || v == 64) nmw = v;
+    }
+    const void *symFn = nmw == 16 ? (const void *)k_tm_nm_sym<16>
+                        : nmw == 32 ? (const void *)k_tm_nm_sym<32> : (const void *)k_tm_nm_sym<64>;
+    if (launch_resident(sym ? symFn : (const void *)k_tm_nm_search, dim3(sym ? nmw : 1 + NM_W),
                         dim3(NM_TPB), args, 0, h->stream,
                         /*prefer_plain=*/true) !=
         hipSuccess) {

@@ -90,10 +90,13 @@ __global__ void __launch_bounds__(SQ_TPB) k_tridiag_sq(int N, const double *__re
   double *scal = sv + 160;
   const bool tr = trace && tid == 0;
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tm = tr ? __builtin_amdgcn_s_memtime() : 0;
+  // (per-step phase times of the last launch at trace[32 + 8 i + k], for
+  // the fixed / per-element split of every phase)
 #define SQ_MARK(k)                                                \
   if (tr) {                                                       \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
     tacc[k] += t_ - tm;                                           \
+    trace[32 + 8 * (size_t)i + (k)] = t_ - tm;                    \
     tm = t_;                                                      \
   }
   for (size_t idx = tid; idx < sq_lds_doubles(N); idx += nt) smem[idx] = 0.0;

@@ -71,7 +71,7 @@ struct State {
   float smean[MAXS], ssdev[MAXS];
   // k_vr_meta's phases (s_memrealtime, 100 MHz ticks, summed over updates):
   // setup + importance weights, retrace chains, loss gradient + metadata
-  unsigned long long mtr[3];
+  unsigned long long mtr[6];  // k_vr_meta: phase ticks x3; sums of the longest walk, walked entries, walks
 };
 
 struct Params {  // launch-constant configuration
@@ -488,9 +488,10 @@ __device__ inline long long phys(const State *s, long long R, long long i) {
 // generateMiniBatch (agent.cpp.base:574-597): B uniforms -> floor(x (size-1)),
 // sorted (bitonic in LDS); gathers the mini-batch states into rows [0, B) and
 // their truncated states into rows [B, 2B) of X.
-__global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Replay er, unsigned *mb,
-                                                       const unsigned *forced, float *X) {
-  __shared__ unsigned key[MAXB];
+// the mini-batch's sorted replay ids into key[0, B) (every thread of the
+// workgroup; the draw counter is advanced by the caller's last kernel)
+__device__ __forceinline__ void vr_minibatch_keys(const Params &P, const State *st, const unsigned *forced,
+                                                  unsigned *key) {
   const int t = threadIdx.x, nt = blockDim.x, B = P.B;
   int n2 = 1;
   while (n2 < B) n2 <<= 1;
@@ -539,6 +540,14 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
         __syncthreads();
       }
   }
+}
+
+__global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Replay er, unsigned *mb,
+                                                       const unsigned *forced, float *X) {
+  __shared__ unsigned key[MAXB];
+  const int t = threadIdx.x, nt = blockDim.x, B = P.B;
+  const unsigned long long ctr = st->mb_counter;
+  vr_minibatch_keys(P, st, forced, key);
   const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
   for (int i = t; i < B * P.S; i += nt) {
     const int b = i / P.S, k = i % P.S;
@@ -553,6 +562,160 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
   if (t == 0) st->mb_counter = ctr + (forced ? 0 : (unsigned long long)B);
 }
 
+// The whole forward pass (input layer, the L-1 hidden H x H layers, the
+// output layer) in ONE launch (round 5): a workgroup owns 16 rows and keeps
+// their activations in LDS between layers, the hidden layers on
+// v_mfma_f32_16x16x4_f32 with the weights streamed through LDS in 64-k
+// chunks.  Every value is formed by the same operations in the same order as
+// k_vr_fwd_in / k_vr_gemm<EP_BIAS_TANH> / k_vr_fwd_out (the same k order and
+// the two interleaved accumulators per 16x16 block, the same lane partial
+// sums and shuffle tree of the output layer): the results are those of the
+// three-kernel form bit for bit, with one launch instead of L + 1 and no
+// activation round trips through HBM between layers (the layers' outputs are
+// still stored for the backward pass).  H <= 256.  MB (a policy update's
+// forward): every workgroup also draws and sorts the mini-batch ids
+// (k_vr_minibatch's vr_minibatch_keys, the same ids everywhere) and gathers
+// its rows -- row b < B the state of mini-batch entry b, row B + b its
+// truncated state -- into LDS and Xmb; workgroup 0 stores the ids.  The draw
+// counter then advances in k_vr_meta (no workgroup may see it move).
+constexpr int FR = 16, FK = 64, FHP = FR + 1, FNP = 256 + 1;
+template <bool MB>
+__global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const float *__restrict__ X,
+                                                      const float *__restrict__ theta, const long long *offs,
+                                                      float *__restrict__ acts, long long rowsMax,
+                                                      float *__restrict__ out, const State *st, Replay er,
+                                                      unsigned *mb, const unsigned *forced, float *Xmb) {
+  __shared__ float Aa[256][FHP], Ab[256][FHP];  // activations [k][row] (the MFMA A operand's layout)
+  __shared__ float Ws[FK][FNP];                 // a 64-k chunk of a layer's weights [k][out column]
+  __shared__ unsigned key[MB ? MAXB : 1];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 15, lk = lane >> 4;
+  const int H = P.H, S = P.S, O = P.O, L = P.L;
+  const int m0 = blockIdx.x * FR;
+  const float *xr = X;  // the input rows (MB: staged in Ws, row stride S)
+  long long xs = (long long)m0 * S;
+  if (MB) {
+    vr_minibatch_keys(P, st, forced, key);
+    const int B = P.B;
+    const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+    float *stg = &Ws[0][0];
+    for (int e = t; e < FR * S; e += 256) {
+      const int r = e / S, i = e % S, m = m0 + r;
+      if (m < M) {
+        const int b = m < B ? m : m - B;
+        unsigned long long q = base + key[b];
+        if (q >= R) q -= R;
+        const float x = (m < B ? er.st : er.tst)[(long long)q * S + i];
+        stg[e] = x;
+        Xmb[(long long)m * S + i] = x;
+      }
+    }
+    if (blockIdx.x == 0)
+      for (int i = t; i < B; i += 256) mb[i] = key[i];
+    __syncthreads();
+    xr = stg, xs = 0;
+  }
+  const int Hp = (H + 15) & ~15;  // columns in whole 16-wide blocks
+  const int Kr = (H + 7) & ~7;    // MFMA k extent (zero rows past H)
+  // ---- input layer (k_vr_fwd_in's per-element loop)
+  {
+    const float *W = theta + offs[0], *b = theta + offs[L + 1];
+    for (int e = t; e < FR * Hp; e += 256) {
+      const int r = e / Hp, o = e % Hp, m = m0 + r;
+      float y = 0.f;
+      if (o < H && m < M) {
+        float acc = 0.f;
+        for (int i = 0; i < S; i++) acc += W[o * S + i] * xr[xs + (long long)r * S + i];
+        y = tanhf(acc + b[o]);
+        acts[(long long)m * H + o] = y;
+      }
+      Aa[o][r] = y;
+    }
+    for (int e = t; e < FR * (256 - Hp); e += 256) Aa[Hp + e / FR][e % FR] = 0.f;
+  }
+  __syncthreads();  // (MB: the staged rows are read before Ws takes weights)
+  float(*cur)[FHP] = Aa;
+  float(*nxt)[FHP] = Ab;
+  // ---- hidden layers l = 1 .. L-1 (k_vr_gemm<EP_BIAS_TANH>: C = tanh(A W^T + b))
+  for (int l = 1; l < L; l++) {
+    const float *W = theta + offs[l], *b = theta + offs[L + 1 + l];
+    f32x4 acc0[4], acc1[4];  // column blocks wave, wave + 4, wave + 8, wave + 12
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc0[q] = f32x4{0.f, 0.f, 0.f, 0.f}, acc1[q] = acc0[q];
+    for (int k0 = 0; k0 < Kr; k0 += FK) {
+      const int kc = min(FK, Kr - k0);
+      __syncthreads();  // the previous chunk's reads (and the layer's activations) are complete
+      // W[n][k0 .. k0+kc) for every column n < Hp (zeros past H)
+      for (int e = t; e < Hp * FK; e += 256) {
+        const int n = e / FK, k = e % FK;
+        Ws[k][n] = (n < H && k < kc && k0 + k < H) ? W[(long long)n * H + k0 + k] : 0.f;
+      }
+      __syncthreads();
+      for (int kk = 0; kk < kc; kk += 8) {
+        const float a0 = cur[k0 + kk + lk][li], a1 = cur[k0 + kk + 4 + lk][li];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int nb = (wave + 4 * q) * 16;
+          if (nb < Hp) {
+            acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, Ws[kk + lk][nb + li], acc0[q], 0, 0, 0);
+            acc1[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, Ws[kk + 4 + lk][nb + li], acc1[q], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // epilogue: C/D layout col = lane & 15, row = 4 (lane >> 4) + reg
+    float *Y = acts + (size_t)l * rowsMax * H;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int nb = (wave + 4 * q) * 16, col = nb + li;
+      if (nb >= Hp) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = lk * 4 + r, m = m0 + row;
+        float v = 0.f;
+        if (col < H) {
+          v = tanhf(acc0[q][r] + acc1[q][r] + b[col]);
+          if (m < M) Y[(long long)m * H + col] = v;
+        }
+        nxt[col][row] = v;
+      }
+    }
+    for (int e = t; e < FR * (256 - Hp); e += 256) nxt[Hp + e / FR][e % FR] = 0.f;
+    float(*tmp)[FHP] = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  __syncthreads();
+  // ---- output layer (k_vr_fwd_out: one wave per row, lane partial sums over
+  // columns lane, lane + 64, ..., the xor-shuffle tree, then the transform)
+  const float *W = theta + offs[L], *bo = theta + offs[2 * L + 1];
+  for (int r = wave; r < FR; r += 4) {
+    const int m = m0 + r;
+    if (m >= M) break;
+    float acc[MAXO];
+#pragma unroll
+    for (int o = 0; o < MAXO; o++) acc[o] = 0.f;
+    for (int i = lane; i < H; i += 64) {
+      const float x = cur[i][r];
+#pragma unroll
+      for (int o = 0; o < MAXO; o++)
+        if (o < O) acc[o] += W[o * H + i] * x;
+    }
+#pragma unroll
+    for (int o = 0; o < MAXO; o++)
+      if (o < O)
+        for (int d = 32; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d, 64);
+    if (lane < O) {
+      float x = 0.f;
+#pragma unroll
+      for (int o = 0; o < MAXO; o++)
+        if (o == lane) x = acc[o];
+      x = x + bo[lane];
+      if (P.soft[lane]) x = (float)(0.5 * ((double)x + sqrt(1.0 + (double)x * (double)x)));
+      out[(long long)m * O + lane] = x * P.scale[lane] + P.shift[lane];
+    }
+  }
+}
+
 // updateExperienceMetadata (agent.cpp.base:599-735) + the VRACER loss
 // gradient (VRACER.cpp.base:89-181) + the REF-ER schedule (agent.cpp.base:
 // 221-231), one workgroup.  Every mini-batch row's metadata lives in LDS
@@ -562,6 +725,9 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
 // global memory, and the replay-memory metadata is written once at the end
 // (no global store is waited for at the first barrier).  A == 1.
 constexpr int MB_META = 1024;
+#ifndef VR_RC
+#define VR_RC 16  // retrace chunk: entries per load round trip of a walk
+#endif
 // a byte flag from LDS as a full 32-bit value (keeps compares on it out of SDWA byte-select forms)
 __device__ __forceinline__ int u8v(unsigned char b) {
   int v = b;
@@ -573,12 +739,13 @@ __device__ __forceinline__ int u8v(unsigned char b) {
 // loads each entry's environment id, so the plain form does without)
 template <bool RR>
 __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
-                                                 const float *__restrict__ out, float *__restrict__ G) {
+                                                 const float *__restrict__ out, float *__restrict__ G,
+                                                 unsigned long long advance) {
   __shared__ unsigned s_mb[MB_META];
   __shared__ float s_V[MB_META], s_tiw[MB_META], s_iw[MB_META], s_ret[MB_META], s_retn[MB_META], s_rew[MB_META],
       s_tv[MB_META], s_act[MB_META], s_cur[2 * MB_META], s_old[2 * MB_META];
   __shared__ unsigned char s_term[MB_META], s_onp[MB_META], s_uniq[MB_META];
-  __shared__ int s_delta;
+  __shared__ int s_delta, s_wmax, s_wtot, s_wcnt;
   __shared__ float s_rsig[MAXENV];
   const int t = threadIdx.x, nt = blockDim.x, B = P.B, O = P.O;
   // every scalar read once into registers
@@ -592,7 +759,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     return (long long)q;
   };
   const unsigned long long tm0 = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_delta = 0;
+  if (t == 0) s_delta = 0, s_wmax = 0, s_wtot = 0, s_wcnt = 0;
   if (RR && t < MAXENV) s_rsig[t] = st->rsig[t];
   __syncthreads();
   // ---- importance weights and on-policy flags (agent.cpp.base:613-657);
@@ -630,127 +797,243 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   const long long off1 = off0 + s_delta;
   const float off_ratio = (float)off1 / (float)size0;
   // ---- retrace chains of the oldest mini-batch entries of each episode
-  // (agent.cpp.base:679-733, same operation order)
-  for (int b = t; b < B; b += nt) {
-    const long long end = s_mb[b];
-    const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
-    const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
-    const int pos = er.ep_pos[pe], term = u8v(s_term[b]);
-    const float retn = er.ret[pnext];
-    if (b < B - 1 && epe == epn) continue;
-    long long start = end - pos;
-    if (start < 0) start = 0;
-    float retV = 0.0f;
-    if (term == TRUNCATED) retV = s_tv[b];
-    if (term == NON_TERMINAL) retV = retn;
-    float prev = retn;  // retrace value of the entry after the current one
-    int k = b;          // mini-batch rows of this episode, walked downwards
-    // per chunk: inputs loaded and mini-batch overrides applied first (no
-    // dependence on the recurrence), then the recurrence alone (4 dependent
-    // float operations per entry), then the mini-batch rows' values to LDS.
-    // The next chunk's loads are issued before the current chunk's
-    // recurrence (two register sets: 48 loads in flight behind the awaited
-    // ones, inside the 63 of vmcnt), so the latency of the replay memory's
-    // loads overlaps the previous chunk's recurrence (without the prefetch:
-    // 27 us per update at C5)
-    constexpr int RC = 16;
-    // (unconditional: entries past the chunk or the episode are valid slots
-    // of the ring whose values go unused; no branch splits the loads from
-    // the waits, so those stay counted)
-    int ea[RC], eb[RC];  // (RR: the entries' environment ids)
-    // (a chunk that does not wrap around the ring, the common case, is
-    // addressed from one base with constant offsets: no per-entry 64-bit
-    // wrap arithmetic in this single-wave, instruction-bound walk)
-    auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC], int (&en)[RC])
-                    __attribute__((always_inline)) {
-      if (p0 >= RC - 1) {
-        const float *v = er.v + p0, *w = er.tiw + p0, *r = er.rew + p0;
-        const int *ev = er.env + p0;
+  // (agent.cpp.base:679-733, same operation order): a walk runs from the
+  // episode's last mini-batch entry down to the episode's start, retV = v +
+  // tiw (r + g retV - v) per entry.  One thread walking its episode through
+  // the replay memory pays one load round trip per 16 entries (19 us of the
+  // kernel's 22 at C5, longest walk ~84 entries).  Staged form: the whole
+  // workgroup first loads every walk's entries into LDS in one strided,
+  // coalesced pass (entry f of the concatenated walks on lane f mod 256),
+  // then each walk runs from LDS, then the retrace values go back in a second
+  // coalesced pass.  The same operations in the same order per walk; walks
+  // whose entries exceed the staging space take the one-thread form below.
+  constexpr int WCAP = 6144;
+  __shared__ float w_v[WCAP], w_t[WCAP], w_r[WCAP];
+  __shared__ unsigned short w_row[WCAP];
+  __shared__ int s_woff[MB_META + 1], s_wst[MB_META], s_wsum[4];
+  {
+    // walking rows (the last mini-batch row of each episode): start, initial
+    // value (into s_ret) and the successor's old value (into s_retn, both
+    // overwritten by the walk); rows [t per, (t + 1) per) on thread t
+    const int per = (B + nt - 1) / nt;
+    int cnt = 0;
+    for (int b = t * per; b < B && b < (t + 1) * per; b++) {
+      const long long end = s_mb[b];
+      const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
+      const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
+      const int pos = er.ep_pos[pe], term = u8v(s_term[b]);
+      const float retn = er.ret[pnext];
+      int L = 0;
+      if (!(b < B - 1 && epe == epn)) {
+        long long start = end - pos;
+        if (start < 0) start = 0;
+        float retV = 0.0f;
+        if (term == TRUNCATED) retV = s_tv[b];
+        if (term == NON_TERMINAL) retV = retn;
+        s_wst[b] = (int)start, s_ret[b] = retV, s_retn[b] = retn;
+        L = (int)(end - start + 1);
+        atomicMax(&s_wmax, L);  // (walk statistics)
+        atomicAdd(&s_wtot, L);
+        atomicAdd(&s_wcnt, 1);
+      }
+      s_woff[b] = L;  // (lengths; offsets after the scan)
+      cnt += L;
+    }
+    int inc = cnt;  // exclusive scan of the per-thread entry counts
 #pragma unroll
-        for (int j = 0; j < RC; j++) {
-          vv[j] = v[-j], tw[j] = w[-j], rw[j] = r[-j];
-          if (RR) en[j] = ev[-j];
-        }
-      } else {
-        long long q = p0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if ((t & 63) >= o) inc += y;
+    }
+    if ((t & 63) == 63) s_wsum[t >> 6] = inc;
+    __syncthreads();
+    int ex = inc - cnt;
+    for (int w = 0; w < (t >> 6); w++) ex += s_wsum[w];
+    for (int b = t * per; b < B && b < (t + 1) * per; b++) {
+      const int L = s_woff[b];
+      s_woff[b] = ex;
+      if (ex + L <= WCAP)
+        for (int f = ex; f < ex + L; f++) w_row[f] = (unsigned short)b;
+      ex += L;
+    }
+    if (t == nt - 1) s_woff[B] = ex;
+    __syncthreads();
+  }
+  const int wtot = s_woff[B];
+  if (wtot <= WCAP) {
+    // entry f of walk b = w_row[f] is replay entry c = mb[b] - (f - off[b])
+    for (int f = t; f < wtot; f += nt) {
+      const int b = w_row[f];
+      const long long q = ph((long long)s_mb[b] - (f - s_woff[b]));
+      w_v[f] = er.v[q], w_t[f] = er.tiw[q];
+      w_r[f] = RR ? er.rew[q] / s_rsig[er.env[q]] : er.rew[q];  // getScaledReward (agent.cpp.base:720)
+    }
+    __syncthreads();
+    const float g = P.gamma;
+    for (int b = t; b < B; b += nt) {
+      const int f0 = s_woff[b], f1 = s_woff[b + 1];
+      if (f1 == f0) continue;
+      const long long end = s_mb[b];
+      float retV = s_ret[b], before = s_retn[b];  // (the successor of the walk's first entry: its old value)
+      int k = b;  // mini-batch rows of this episode, walked downwards
+      int f = f0;
+      // four entries' operands read ahead of the recurrence
+      for (; f + 4 <= f1; f += 4) {
+        float vv[4], tw[4], rw[4];
 #pragma unroll
-        for (int j = 0; j < RC; j++) {
-          vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
-          if (RR) en[j] = er.env[q];
-          q = q == 0 ? (long long)R - 1 : q - 1;
+        for (int j = 0; j < 4; j++) vv[j] = w_v[f + j], tw[j] = w_t[f + j], rw[j] = w_r[f + j];
+        const long long c0 = end - (f - f0);
+        const bool any = k >= 0 && (long long)s_mb[k] > c0 - 4;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (any && k >= 0 && (long long)s_mb[k] == c0 - j) vv[j] = s_V[k], tw[j] = s_tiw[k];  // updated by this kernel
+          retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
+          w_v[f + j] = retV;
+          if (any)
+            while (k >= 0 && (long long)s_mb[k] == c0 - j) s_ret[k] = retV, s_retn[k] = before, k--;
+          before = retV;
         }
       }
-    };
-    auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC],
-                       const int (&en)[RC]) __attribute__((always_inline)) {
-      if (RR)
-#pragma unroll
-        for (int j = 0; j < RC; j++) rw[j] = rw[j] / s_rsig[en[j]];  // getScaledReward (agent.cpp.base:720)
-      const int n = (int)min((long long)RC, c - start + 1);
-      int kk = k;
-      unsigned long long inmb = 0;
-      // the highest mini-batch row not yet passed is <= c: only when it lies
-      // in this chunk (rare: B rows over the whole memory) are the entries
-      // checked one by one (each check a dependent LDS read)
-      if (kk >= 0 && (long long)s_mb[kk] > c - n)
-#pragma unroll
-        for (int j = 0; j < RC; j++)
-          if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
-            vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
-            inmb |= 1ull << j;
-            while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
+      for (; f < f1; f++) {
+        const long long c = end - (f - f0);
+        float vv = w_v[f], tw = w_t[f];
+        const float rw = w_r[f];
+        const bool mbe = k >= 0 && (long long)s_mb[k] == c;
+        if (mbe) vv = s_V[k], tw = s_tiw[k];
+        retV = vv + tw * (rw + g * retV - vv);
+        w_v[f] = retV;
+        while (k >= 0 && (long long)s_mb[k] == c) s_ret[k] = retV, s_retn[k] = before, k--;
+        before = retV;
+      }
+    }
+    __syncthreads();
+    for (int f = t; f < wtot; f += nt) {
+      const int b = w_row[f];
+      er.ret[ph((long long)s_mb[b] - (f - s_woff[b]))] = w_v[f];
+    }
+  } else {
+    // the one-thread walks through the replay memory
+    for (int b = t; b < B; b += nt) {
+      const long long end = s_mb[b];
+      const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
+      const long long epe = er.ep_id[pe], epn = er.ep_id[pn];
+      const int pos = er.ep_pos[pe], term = u8v(s_term[b]);
+      const float retn = er.ret[pnext];
+      if (b < B - 1 && epe == epn) continue;
+      long long start = end - pos;
+      if (start < 0) start = 0;
+      float retV = 0.0f;
+      if (term == TRUNCATED) retV = s_tv[b];
+      if (term == NON_TERMINAL) retV = retn;
+      float prev = retn;  // retrace value of the entry after the current one
+      int k = b;          // mini-batch rows of this episode, walked downwards
+      // per chunk: inputs loaded and mini-batch overrides applied first (no
+      // dependence on the recurrence), then the recurrence alone (4 dependent
+      // float operations per entry), then the mini-batch rows' values to LDS.
+      // The next chunk's loads are issued before the current chunk's
+      // recurrence (two register sets: 48 loads in flight behind the awaited
+      // ones, inside the 63 of vmcnt), so the latency of the replay memory's
+      // loads overlaps the previous chunk's recurrence (without the prefetch:
+      // 27 us per update at C5)
+      constexpr int RC = VR_RC;
+      // (unconditional: entries past the chunk or the episode are valid slots
+      // of the ring whose values go unused; no branch splits the loads from
+      // the waits, so those stay counted)
+      int ea[RC], eb[RC];  // (RR: the entries' environment ids)
+      // (a chunk that does not wrap around the ring, the common case, is
+      // addressed from one base with constant offsets: no per-entry 64-bit
+      // wrap arithmetic in this single-wave, instruction-bound walk)
+      auto load = [&](long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC], int (&en)[RC])
+                      __attribute__((always_inline)) {
+        if (p0 >= RC - 1) {
+          const float *v = er.v + p0, *w = er.tiw + p0, *r = er.rew + p0;
+          const int *ev = er.env + p0;
+  #pragma unroll
+          for (int j = 0; j < RC; j++) {
+            vv[j] = v[-j], tw[j] = w[-j], rw[j] = r[-j];
+            if (RR) en[j] = ev[-j];
           }
-      float rr[RC];
-      const float g = P.gamma;
-      if (n == RC) {  // a full chunk: no per-entry predicate
-#pragma unroll
-        for (int j = 0; j < RC; j++) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < RC; j++)
-          if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
-      }
-      if (n == RC && p0 >= RC - 1) {
-        float *rp = er.ret + p0;
-#pragma unroll
-        for (int j = 0; j < RC; j++) rp[-j] = rr[j];
-      } else {
-        long long q = p0;
-#pragma unroll
-        for (int j = 0; j < RC; j++) {
-          if (j < n) er.ret[q] = rr[j];
-          q = q == 0 ? (long long)R - 1 : q - 1;
-        }
-      }
-      if (inmb)
-#pragma unroll
-        for (int j = 0; j < RC; j++)
-          if (inmb >> j & 1ull) {
-            const float before = j == 0 ? prev : rr[j - 1];
-            while (k >= 0 && (long long)s_mb[k] == c - j) s_ret[k] = rr[j], s_retn[k] = before, k--;
+        } else {
+          long long q = p0;
+  #pragma unroll
+          for (int j = 0; j < RC; j++) {
+            vv[j] = er.v[q], tw[j] = er.tiw[q], rw[j] = er.rew[q];
+            if (RR) en[j] = er.env[q];
+            q = q == 0 ? (long long)R - 1 : q - 1;
           }
-      prev = retV;  // the chunk's last entry
-    };
-    // the chunk after the one at (c, pc): its first entry and physical slot
-    auto next = [&](long long c, long long pc, long long &c1, long long &pc1) __attribute__((always_inline)) {
-      const long long n = min((long long)RC, c - start + 1);
-      c1 = c - n;
-      pc1 = pc >= n ? pc - n : pc - n + (long long)R;
-    };
-    float av[RC], at[RC], ar[RC], bv[RC], bt[RC], br[RC];
-    long long c = end, pc = ph(end);
-    load(pc, av, at, ar, ea);
-    while (c >= start) {
-      long long c1, pc1;
-      next(c, pc, c1, pc1);
-      load(pc1, bv, bt, br, eb);
-      process(c, pc, av, at, ar, ea);
-      c = c1, pc = pc1;
-      if (c < start) break;
-      next(c, pc, c1, pc1);
-      load(pc1, av, at, ar, ea);
-      process(c, pc, bv, bt, br, eb);
-      c = c1, pc = pc1;
+        }
+      };
+      auto process = [&](long long c, long long p0, float (&vv)[RC], float (&tw)[RC], float (&rw)[RC],
+                         const int (&en)[RC]) __attribute__((always_inline)) {
+        if (RR)
+  #pragma unroll
+          for (int j = 0; j < RC; j++) rw[j] = rw[j] / s_rsig[en[j]];  // getScaledReward (agent.cpp.base:720)
+        const int n = (int)min((long long)RC, c - start + 1);
+        int kk = k;
+        unsigned long long inmb = 0;
+        // the highest mini-batch row not yet passed is <= c: only when it lies
+        // in this chunk (rare: B rows over the whole memory) are the entries
+        // checked one by one (each check a dependent LDS read)
+        if (kk >= 0 && (long long)s_mb[kk] > c - n)
+  #pragma unroll
+          for (int j = 0; j < RC; j++)
+            if (j < n && kk >= 0 && (long long)s_mb[kk] == c - j) {
+              vv[j] = s_V[kk], tw[j] = s_tiw[kk];  // updated by this kernel
+              inmb |= 1ull << j;
+              while (kk >= 0 && (long long)s_mb[kk] == c - j) kk--;
+            }
+        float rr[RC];
+        const float g = P.gamma;
+        if (n == RC) {  // a full chunk: no per-entry predicate
+  #pragma unroll
+          for (int j = 0; j < RC; j++) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
+        } else {
+  #pragma unroll
+          for (int j = 0; j < RC; j++)
+            if (j < n) rr[j] = retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
+        }
+        if (n == RC && p0 >= RC - 1) {
+          float *rp = er.ret + p0;
+  #pragma unroll
+          for (int j = 0; j < RC; j++) rp[-j] = rr[j];
+        } else {
+          long long q = p0;
+  #pragma unroll
+          for (int j = 0; j < RC; j++) {
+            if (j < n) er.ret[q] = rr[j];
+            q = q == 0 ? (long long)R - 1 : q - 1;
+          }
+        }
+        if (inmb)
+  #pragma unroll
+          for (int j = 0; j < RC; j++)
+            if (inmb >> j & 1ull) {
+              const float before = j == 0 ? prev : rr[j - 1];
+              while (k >= 0 && (long long)s_mb[k] == c - j) s_ret[k] = rr[j], s_retn[k] = before, k--;
+            }
+        prev = retV;  // the chunk's last entry
+      };
+      // the chunk after the one at (c, pc): its first entry and physical slot
+      auto next = [&](long long c, long long pc, long long &c1, long long &pc1) __attribute__((always_inline)) {
+        const long long n = min((long long)RC, c - start + 1);
+        c1 = c - n;
+        pc1 = pc >= n ? pc - n : pc - n + (long long)R;
+      };
+      float av[RC], at[RC], ar[RC], bv[RC], bt[RC], br[RC];
+      long long c = end, pc = ph(end);
+      load(pc, av, at, ar, ea);
+      while (c >= start) {
+        long long c1, pc1;
+        next(c, pc, c1, pc1);
+        load(pc1, bv, bt, br, eb);
+        process(c, pc, av, at, ar, ea);
+        c = c1, pc = pc1;
+        if (c < start) break;
+        next(c, pc, c1, pc1);
+        load(pc1, av, at, ar, ea);
+        process(c, pc, bv, bt, br, eb);
+        c = c1, pc = pc1;
+      }
     }
   }
   __syncthreads();
@@ -855,8 +1138,10 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   if (t == 0) {
     const unsigned long long tm3 = __builtin_amdgcn_s_memrealtime();
     st->mtr[0] += tm1 - tm0, st->mtr[1] += tm2 - tm1, st->mtr[2] += tm3 - tm2;
+    st->mtr[3] += (unsigned long long)s_wmax, st->mtr[4] += (unsigned long long)s_wtot, st->mtr[5] += (unsigned long long)s_wcnt;
     st->off_count = off1;
     st->off_ratio = off_ratio;
+    st->mb_counter += advance;  // (the draws of a fused forward's mini-batch)
     st->cutoff = P.cutoff_scale / (1.0f + P.anneal * (float)upd0);
     // the learner's eta for this update, then agent.cpp.base:221-231
     st->eta = lr;
@@ -1496,6 +1781,7 @@ struct kg_vracer_s {
   float *Xmb;        // 2B x S mini-batch (+ truncated) states
   float *Xs;         // rowsMax x S run_policy staging
   float *acts;       // L x rowsMax x H activations
+  long long *offs = nullptr;  // offW[0..L], offb[0..L] on the device (k_vr_fwd_fused)
   float *out, *outF; // rowsMax x O
   float *G, *dZ, *dHa, *dHb;
   unsigned *mb, *forced_mb;
@@ -1601,6 +1887,18 @@ VrGemmJob vr_gemm_job(int ep, int M, int N, int K, const float *A, long long sam
 int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
   const Params &P = h->P;
   KG_CHECK((size_t)M <= h->rowsMax, "vracer: forward batch exceeds the allocated rows");
+  // one launch for the whole forward pass (KORALI_AMD_VR_FUSED=0: the
+  // per-layer kernels, bit-identical results; A/B and the equality test)
+  const char *fe = getenv("KORALI_AMD_VR_FUSED");
+  if (P.H <= 256 && !(fe && *fe == '0')) {
+    VrStage tg(h, M == P.E ? "gemm_rollout" : (M == 2 * P.B ? "gemm_update" : "gemm_other"));
+    hipLaunchKernelGGL(k_vr_fwd_fused<false>, dim3(vr_blocks(M, FR)), dim3(256), 0, h->stream, P, M, X,
+                       (const float *)h->theta, (const long long *)h->offs, h->acts, (long long)h->rowsMax, out,
+                       (const State *)nullptr, Replay{}, (unsigned *)nullptr, (const unsigned *)nullptr,
+                       (float *)nullptr);
+    KG_HIP(hipGetLastError());
+    return 0;
+  }
   float *a1 = h->acts;
   hipLaunchKernelGGL(k_vr_fwd_in, dim3(vr_blocks((long long)M * P.H, 256)), dim3(256), 0, h->stream, M, P.S, P.H, X,
                      h->theta + h->offW[0], h->theta + h->offb[0], a1);
@@ -1648,11 +1946,21 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   const int B = P.B;
   KG_CHECK(h->st_host->size >= 2, "vracer: policy updates need at least two experiences in the replay memory");
   VrStage tu(h, "update");
-  hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
-  if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
+  const char *fe = getenv("KORALI_AMD_VR_FUSED");
+  const bool fused = P.H <= 256 && !(fe && *fe == '0');
+  if (fused) {
+    // the mini-batch draw, its gather and the whole forward pass: one launch
+    VrStage tg(h, "gemm_update");
+    hipLaunchKernelGGL(k_vr_fwd_fused<true>, dim3(vr_blocks(2 * B, FR)), dim3(256), 0, h->stream, P, 2 * B,
+                       (const float *)nullptr, (const float *)h->theta, (const long long *)h->offs, h->acts,
+                       (long long)h->rowsMax, h->out, (const State *)h->st, h->er, h->mb, forced, h->Xmb);
+  } else {
+    hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
+    if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
+  }
+  const unsigned long long advance = (fused && !forced) ? (unsigned long long)B : 0ULL;
   hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er,
-                     (const unsigned *)h->mb,
-                     (const float *)h->out, h->G);
+                     (const unsigned *)h->mb, (const float *)h->out, h->G, advance);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
   const size_t rs = h->rowsMax * P.H;
   const float *lastA = h->acts + (size_t)(P.L - 1) * rs;
@@ -1746,7 +2054,7 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
       {"state_rescaling_means", &h->st->smean[0], 4, (size_t)P.S},
       {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)P.S},
-      {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)3},
+      {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)6},
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {
@@ -1863,6 +2171,13 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(h->theta, k * 4), alloc(h->grad, k * 4), alloc(h->m1, k * 4), alloc(h->m2, k * 4);
   alloc(h->X, E * P.S * 4), alloc(h->Xmb, 2 * (size_t)P.B * P.S * 4), alloc(h->Xs, h->rowsMax * P.S * 4);
   alloc(h->acts, (size_t)P.L * h->rowsMax * P.H * 4);
+  alloc(h->offs, 2 * ((size_t)P.L + 1) * sizeof(long long));
+  if (!rc) {
+    std::vector<long long> o;
+    for (auto v : h->offW) o.push_back((long long)v);
+    for (auto v : h->offb) o.push_back((long long)v);
+    if (hipMemcpy(h->offs, o.data(), o.size() * sizeof(long long), hipMemcpyHostToDevice) != hipSuccess) rc = 1;
+  }
   alloc(h->out, h->rowsMax * P.O * 4), alloc(h->outF, h->rowsMax * P.O * 4);
   alloc(h->G, (size_t)P.B * P.O * 4), alloc(h->dZ, (size_t)P.B * P.O * 4);
   alloc(h->dHa, (size_t)P.B * P.H * 4), alloc(h->dHb, (size_t)P.B * P.H * 4);
@@ -1951,7 +2266,7 @@ extern "C" int kg_debug_cartpole(int device, const double *u0, const double *for
 int kg_vracer_destroy(kg_vracer_t h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  void *ptrs[] = {h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
+  void *ptrs[] = {h->offs, h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
                   h->dHb, h->mb, h->forced_mb, h->forced_noise, h->st, h->er.st, h->er.act, h->er.rew, h->er.tst,
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
                   h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,

@@ -11,6 +11,8 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libkorali_amd.so")
+if os.environ.get("KORALI_AMD_LIB_VARIANT"):  # A/B builds (libkorali_amd_<variant>.so, same sources, other -D flags)
+    LIB_PATH = os.path.join(_PKG, f"libkorali_amd_{os.environ['KORALI_AMD_LIB_VARIANT']}.so")
 _LIB = None
 
 MU_TYPES = {"logarithmic": 0, "linear": 1, "equal": 2, "proportional": 3}

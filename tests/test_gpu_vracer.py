@@ -51,6 +51,40 @@ def test_run_policy_matches_oracle(H, L, n):
     assert np.all(out[:, 2] > 0)
 
 
+@pytest.mark.parametrize("H,L,n", [(64, 1, 37), (256, 2, 500), (128, 3, 4096), (32, 2, 300), (100, 1, 77)])
+def test_fused_forward_equals_per_layer_kernels(monkeypatch, H, L, n):
+    """k_vr_fwd_fused (one launch per forward pass) forms every output with the
+    per-layer kernels' operations in their order: equal bit for bit."""
+    th = theta_for(H, L, 1, spread=1.0)
+    d = device(hidden_size=H, hidden_layers=L, environments=4096, mini_batch_size=64, replay_maximum_size=1024,
+               replay_start_size=512, initial_exploration_noise=0.7, hyperparameters=th)
+    X = np.random.default_rng(5).standard_normal((n, S)).astype(f32)
+    fused = d.run_policy(X)
+    monkeypatch.setenv("KORALI_AMD_VR_FUSED", "0")
+    per_layer = d.run_policy(X)
+    assert np.array_equal(fused, per_layer)
+
+
+def test_fused_update_equals_per_layer_kernels(monkeypatch):
+    """Policy updates with drawn mini-batches: the fused draw + forward launch
+    (and the draw counter advanced by the metadata kernel) leaves every
+    hyperparameter, Adam moment and replay field equal to the separate
+    k_vr_minibatch + per-layer forward bit for bit."""
+    ag, th = fill_replay(64, 2, 8, 90, 600)
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("KORALI_AMD_VR_FUSED", fused)
+        d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
+                   replay_start_size=100, hyperparameters=th)
+        load_replay(d, ag)
+        d.train_policy(7)
+        runs.append((d.hyperparameters, d.get("retrace")[:ag.size()], d.get("importance_weight")[:ag.size()],
+                     d.get("loss_gradient")))
+        d.close()
+    for a, b in zip(*runs):
+        assert np.array_equal(a, b)
+
+
 CLIP = (np.array([-0.5], f32), np.array([0.5], f32))  # narrow bounds: every clipping branch is taken
 
 
