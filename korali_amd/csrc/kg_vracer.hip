@@ -734,6 +734,12 @@ __device__ __forceinline__ int u8v(unsigned char b) {
   asm volatile("" : "+v"(v));
   return v;
 }
+// a 16-bit LDS value as a full 32-bit one (no SDWA word selects on it)
+__device__ __forceinline__ int u16v(unsigned short h) {
+  int v = h;
+  asm volatile("" : "+v"(v));
+  return v;
+}
 // RR: reward rescaling enabled (every reward through getScaledReward: the
 // divisions are exact no-ops at sigma 1.0, but the retrace walk then also
 // loads each entry's environment id, so the plain form does without)
@@ -863,7 +869,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   if (wtot <= WCAP) {
     // entry f of walk b = w_row[f] is replay entry c = mb[b] - (f - off[b])
     for (int f = t; f < wtot; f += nt) {
-      const int b = w_row[f];
+      const int b = u16v(w_row[f]);
       const long long q = ph((long long)s_mb[b] - (f - s_woff[b]));
       w_v[f] = er.v[q], w_t[f] = er.tiw[q];
       w_r[f] = RR ? er.rew[q] / s_rsig[er.env[q]] : er.rew[q];  // getScaledReward (agent.cpp.base:720)
@@ -908,7 +914,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     }
     __syncthreads();
     for (int f = t; f < wtot; f += nt) {
-      const int b = w_row[f];
+      const int b = u16v(w_row[f]);
       er.ret[ph((long long)s_mb[b] - (f - s_woff[b]))] = w_v[f];
     }
   } else {
