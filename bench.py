@@ -468,6 +468,8 @@ def main():
                     help="exact (default): bit-exact rank-mu order, the reference's trajectory; mfma: FP64 matrix "
                          "cores, <= 1e-12 per step (reported beside the exact rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 line (profiling runs: keeps the C2 kernels' "
+                                                        "statistics free of the N=8 launches)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2: the BASELINE metric (CMA-ES); c3: TMCMC N=32, P=8192; c4: CMA-ES 512-dim Ackley, "
                          "lambda=65536, population sharded over the ranks; c5: VRACER, 4096 CartPole rollouts")
@@ -589,7 +591,7 @@ def main():
             mfma_kernel = rankmu_roofline(ms, MU, N_VARS, "c2_pmc_traffic.csv")
     adev.close()
     c4 = c4_scaling(args, world, rank, dist) if dist is not None else None
-    c1 = c1_line(cpu=not args.no_cpu_baseline) if world == 1 else None
+    c1 = c1_line(cpu=not args.no_cpu_baseline) if world == 1 and not args.no_c1 else None
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -1079,7 +1081,8 @@ def run_c5(args):
     nu = max(1.0, d.scalar("policy_update_count") - u0)
     mt = (d.get("meta_phase_ticks").astype(np.float64) - m0) / nu
     meta_us = (mt[:3] * 0.01).tolist()  # 100 MHz ticks
-    walks = {"longest_walk_entries": mt[3], "walked_entries": mt[4], "walks": mt[5]}  # per update
+    walks = {"longest_walk_entries": mt[3], "walked_entries": mt[4], "walks": mt[5],  # per update
+             "us_walk_setup": mt[6] * 0.01, "us_staging_loads": mt[7] * 0.01, "us_walks": mt[8] * 0.01}
     stages = {}
     for st in ("environment_step", "update", "gemm_rollout", "gemm_update"):
         ms, cnt = d.profile_read(st)

@@ -71,7 +71,7 @@ struct State {
   float smean[MAXS], ssdev[MAXS];
   // k_vr_meta's phases (s_memrealtime, 100 MHz ticks, summed over updates):
   // setup + importance weights, retrace chains, loss gradient + metadata
-  unsigned long long mtr[6];  // k_vr_meta: phase ticks x3; sums of the longest walk, walked entries, walks
+  unsigned long long mtr[9];  // k_vr_meta: phase ticks x3; sums of the longest walk, walked entries, walks; walk sub-phase ticks x3
 };
 
 struct Params {  // launch-constant configuration
@@ -616,9 +616,29 @@ __global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const flo
   }
   const int Hp = (H + 15) & ~15;  // columns in whole 16-wide blocks
   const int Kr = (H + 7) & ~7;    // MFMA k extent (zero rows past H)
-  // ---- input layer (k_vr_fwd_in's per-element loop)
+  // ---- input layer (k_vr_fwd_in's per-element loop), its operands staged in
+  // LDS first (the rows, W_0 and b_0: every load in flight at once)
   {
     const float *W = theta + offs[0], *b = theta + offs[L + 1];
+    float *stg = &Ws[0][0];
+    const bool staged = FR * S + H * S + H <= FK * FNP;
+    auto copy = [&](float *dst, const float *src, int n) __attribute__((always_inline)) {
+      for (int i0 = t; i0 < n; i0 += 8 * 256) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = i0 + 256 * u < n ? src[i0 + 256 * u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (i0 + 256 * u < n) dst[i0 + 256 * u] = v[u];
+      }
+    };
+    if (staged) {
+      if (!MB) copy(stg, X + (long long)m0 * S, min(FR, M - m0) * S);  // (MB: gathered above)
+      copy(stg + FR * S, W, H * S);
+      copy(stg + FR * S + H * S, b, H);
+      __syncthreads();
+      xr = stg, xs = 0, W = stg + FR * S, b = stg + FR * S + H * S;
+    }
     for (int e = t; e < FR * Hp; e += 256) {
       const int r = e / Hp, o = e % Hp, m = m0 + r;
       float y = 0.f;
@@ -638,16 +658,41 @@ __global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const flo
   // ---- hidden layers l = 1 .. L-1 (k_vr_gemm<EP_BIAS_TANH>: C = tanh(A W^T + b))
   for (int l = 1; l < L; l++) {
     const float *W = theta + offs[l], *b = theta + offs[L + 1 + l];
+    const bool vec4 = H % 64 == 0 && ((uintptr_t)W & 15) == 0;
     f32x4 acc0[4], acc1[4];  // column blocks wave, wave + 4, wave + 8, wave + 12
 #pragma unroll
     for (int q = 0; q < 4; q++) acc0[q] = f32x4{0.f, 0.f, 0.f, 0.f}, acc1[q] = acc0[q];
     for (int k0 = 0; k0 < Kr; k0 += FK) {
       const int kc = min(FK, Kr - k0);
       __syncthreads();  // the previous chunk's reads (and the layer's activations) are complete
-      // W[n][k0 .. k0+kc) for every column n < Hp (zeros past H)
-      for (int e = t; e < Hp * FK; e += 256) {
-        const int n = e / FK, k = e % FK;
-        Ws[k][n] = (n < H && k < kc && k0 + k < H) ? W[(long long)n * H + k0 + k] : 0.f;
+      // W[n][k0 .. k0+kc) for every column n < Hp (zeros past H): all of a
+      // thread's loads in flight before its first LDS store
+      if (vec4 && kc == FK) {
+        float4 rw[16];  // Hp * FK / 4 / 256 <= 16 float4 per thread
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int e = t + 256 * u, n = e >> 4, k = 4 * (e & 15);
+          if (n < Hp) rw[u] = *reinterpret_cast<const float4 *>(W + (long long)n * H + k0 + k);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int e = t + 256 * u, n = e >> 4, k = 4 * (e & 15);
+          if (n < Hp) Ws[k][n] = rw[u].x, Ws[k + 1][n] = rw[u].y, Ws[k + 2][n] = rw[u].z, Ws[k + 3][n] = rw[u].w;
+        }
+      } else {
+        for (int e0 = t; e0 < Hp * FK; e0 += 8 * 256) {
+          float rv[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int e = e0 + 256 * u, n = e / FK, k = e % FK;
+            rv[u] = (e < Hp * FK && n < H && k < kc && k0 + k < H) ? W[(long long)n * H + k0 + k] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int e = e0 + 256 * u;
+            if (e < Hp * FK) Ws[e % FK][e / FK] = rv[u];
+          }
+        }
       }
       __syncthreads();
       for (int kk = 0; kk < kc; kk += 8) {
@@ -684,10 +729,28 @@ __global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const flo
     cur = nxt;
     nxt = tmp;
   }
-  __syncthreads();
   // ---- output layer (k_vr_fwd_out: one wave per row, lane partial sums over
-  // columns lane, lane + 64, ..., the xor-shuffle tree, then the transform)
+  // columns lane, lane + 64, ..., the xor-shuffle tree, then the transform);
+  // W_L and b_L staged in LDS (Ws is free once the last layer's products are done)
   const float *W = theta + offs[L], *bo = theta + offs[2 * L + 1];
+  __syncthreads();
+  if (O * H + O <= FK * FNP) {
+    float *stg = &Ws[0][0];
+    const int n = O * H + O;
+    for (int i0 = t; i0 < n; i0 += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + 256 * u;
+        v[u] = i < O * H ? W[i] : (i < n ? bo[i - O * H] : 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (i0 + 256 * u < n) stg[i0 + 256 * u] = v[u];
+    }
+    W = stg, bo = stg + O * H;
+  }
+  __syncthreads();
   for (int r = wave; r < FR; r += 4) {
     const int m = m0 + r;
     if (m >= M) break;
@@ -746,7 +809,7 @@ __device__ __forceinline__ int u16v(unsigned short h) {
 template <bool RR>
 __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                  const float *__restrict__ out, float *__restrict__ G,
-                                                 unsigned long long advance) {
+                                                 unsigned long long advance, int staged) {
   __shared__ unsigned s_mb[MB_META];
   __shared__ float s_V[MB_META], s_tiw[MB_META], s_iw[MB_META], s_ret[MB_META], s_retn[MB_META], s_rew[MB_META],
       s_tv[MB_META], s_act[MB_META], s_cur[2 * MB_META], s_old[2 * MB_META];
@@ -816,13 +879,15 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   constexpr int WCAP = 6144;
   __shared__ float w_v[WCAP], w_t[WCAP], w_r[WCAP];
   __shared__ unsigned short w_row[WCAP];
-  __shared__ int s_woff[MB_META + 1], s_wst[MB_META], s_wsum[4];
+  __shared__ int s_woff[MB_META + 1], s_fk[MB_META], s_wsum[4];
+  __shared__ float s_wretn[MB_META];
   {
-    // walking rows (the last mini-batch row of each episode): start, initial
-    // value (into s_ret) and the successor's old value (into s_retn, both
-    // overwritten by the walk); rows [t per, (t + 1) per) on thread t
+    // walking rows (the last mini-batch row of each episode): length, initial
+    // value (into s_ret, read by the walk before the rows' values replace it)
+    // and the old value of the entry after the walk's first (s_wretn); rows
+    // [t per, (t + 1) per) on thread t
     const int per = (B + nt - 1) / nt;
-    int cnt = 0;
+    int cnt = 0, lmax = 0, lcnt = 0;
     for (int b = t * per; b < B && b < (t + 1) * per; b++) {
       const long long end = s_mb[b];
       const long long pe = ph(end), pn = ph(b < B - 1 ? (long long)s_mb[b + 1] : end), pnext = ph(end + 1);
@@ -836,11 +901,9 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
         float retV = 0.0f;
         if (term == TRUNCATED) retV = s_tv[b];
         if (term == NON_TERMINAL) retV = retn;
-        s_wst[b] = (int)start, s_ret[b] = retV, s_retn[b] = retn;
+        s_ret[b] = retV, s_wretn[b] = retn;
         L = (int)(end - start + 1);
-        atomicMax(&s_wmax, L);  // (walk statistics)
-        atomicAdd(&s_wtot, L);
-        atomicAdd(&s_wcnt, 1);
+        lmax = max(lmax, L), lcnt++;
       }
       s_woff[b] = L;  // (lengths; offsets after the scan)
       cnt += L;
@@ -850,8 +913,15 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(inc, o, 64);
       if ((t & 63) >= o) inc += y;
+      lmax = max(lmax, __shfl_xor(lmax, o, 64));
+      lcnt += __shfl_xor(lcnt, o, 64);
     }
-    if ((t & 63) == 63) s_wsum[t >> 6] = inc;
+    if ((t & 63) == 63) {
+      s_wsum[t >> 6] = inc;
+      atomicMax(&s_wmax, lmax);  // (walk statistics: one atomic per wave)
+      atomicAdd(&s_wtot, inc);
+      atomicAdd(&s_wcnt, lcnt);
+    }
     __syncthreads();
     int ex = inc - cnt;
     for (int w = 0; w < (t >> 6); w++) ex += s_wsum[w];
@@ -866,53 +936,77 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     __syncthreads();
   }
   const int wtot = s_woff[B];
-  if (wtot <= WCAP) {
+  const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tw1 = tw0, tw2 = tw0;
+  if (staged && wtot <= WCAP) {
     // entry f of walk b = w_row[f] is replay entry c = mb[b] - (f - off[b])
-    for (int f = t; f < wtot; f += nt) {
-      const int b = u16v(w_row[f]);
-      const long long q = ph((long long)s_mb[b] - (f - s_woff[b]));
-      w_v[f] = er.v[q], w_t[f] = er.tiw[q];
-      w_r[f] = RR ? er.rew[q] / s_rsig[er.env[q]] : er.rew[q];  // getScaledReward (agent.cpp.base:720)
+    // (sixteen entries' loads in flight per thread before its LDS stores)
+    for (int f0 = t; f0 < wtot; f0 += 16 * nt) {
+      float lv[16], lt[16], lr[16];
+      int le[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int f = f0 + u * nt;
+        if (f < wtot) {
+          const int b = u16v(w_row[f]);
+          const long long q = ph((long long)s_mb[b] - (f - s_woff[b]));
+          lv[u] = er.v[q], lt[u] = er.tiw[q], lr[u] = er.rew[q];
+          if (RR) le[u] = er.env[q];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int f = f0 + u * nt;
+        if (f < wtot) {
+          w_v[f] = lv[u], w_t[f] = lt[u];
+          w_r[f] = RR ? lr[u] / s_rsig[le[u]] : lr[u];  // getScaledReward (agent.cpp.base:720)
+        }
+      }
     }
     __syncthreads();
+    // every mini-batch row's entry takes the values this kernel updated (the
+    // walk then needs no per-entry check); s_fk: the entry, or -(walk + 1)
+    // when it is the walk's first (its successor's value is the old one)
+    for (int k = t; k < B; k += nt) {
+      int wb = k;
+      while (wb < B - 1 && s_woff[wb + 1] == s_woff[wb]) wb++;  // the walking row of k's episode
+      const int f = s_woff[wb] + (int)((long long)s_mb[wb] - (long long)s_mb[k]);
+      w_v[f] = s_V[k], w_t[f] = s_tiw[k];  // (duplicate rows store the same values)
+      s_fk[k] = f == s_woff[wb] ? -(wb + 1) : f;
+    }
+    __syncthreads();
+    tw1 = __builtin_amdgcn_s_memrealtime();
     const float g = P.gamma;
     for (int b = t; b < B; b += nt) {
       const int f0 = s_woff[b], f1 = s_woff[b + 1];
-      if (f1 == f0) continue;
-      const long long end = s_mb[b];
-      float retV = s_ret[b], before = s_retn[b];  // (the successor of the walk's first entry: its old value)
-      int k = b;  // mini-batch rows of this episode, walked downwards
+      float x = s_ret[b];
       int f = f0;
-      // four entries' operands read ahead of the recurrence
-      for (; f + 4 <= f1; f += 4) {
+      for (; f + 4 <= f1; f += 4) {  // four entries' operands read ahead of the recurrence
         float vv[4], tw[4], rw[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) vv[j] = w_v[f + j], tw[j] = w_t[f + j], rw[j] = w_r[f + j];
-        const long long c0 = end - (f - f0);
-        const bool any = k >= 0 && (long long)s_mb[k] > c0 - 4;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          if (any && k >= 0 && (long long)s_mb[k] == c0 - j) vv[j] = s_V[k], tw[j] = s_tiw[k];  // updated by this kernel
-          retV = vv[j] + tw[j] * (rw[j] + g * retV - vv[j]);
-          w_v[f + j] = retV;
-          if (any)
-            while (k >= 0 && (long long)s_mb[k] == c0 - j) s_ret[k] = retV, s_retn[k] = before, k--;
-          before = retV;
+          x = vv[j] + tw[j] * (rw[j] + g * x - vv[j]);
+          w_v[f + j] = x;
         }
       }
       for (; f < f1; f++) {
-        const long long c = end - (f - f0);
-        float vv = w_v[f], tw = w_t[f];
-        const float rw = w_r[f];
-        const bool mbe = k >= 0 && (long long)s_mb[k] == c;
-        if (mbe) vv = s_V[k], tw = s_tiw[k];
-        retV = vv + tw * (rw + g * retV - vv);
-        w_v[f] = retV;
-        while (k >= 0 && (long long)s_mb[k] == c) s_ret[k] = retV, s_retn[k] = before, k--;
-        before = retV;
+        x = w_v[f] + w_t[f] * (w_r[f] + g * x - w_v[f]);
+        w_v[f] = x;
       }
     }
     __syncthreads();
+    tw2 = __builtin_amdgcn_s_memrealtime();
+    for (int k = t; k < B; k += nt) {
+      const int e = s_fk[k];
+      if (e < 0) {
+        const int wb = -e - 1;
+        s_ret[k] = w_v[s_woff[wb]], s_retn[k] = s_wretn[wb];
+      } else {
+        s_ret[k] = w_v[e], s_retn[k] = w_v[e - 1];
+      }
+    }
     for (int f = t; f < wtot; f += nt) {
       const int b = u16v(w_row[f]);
       er.ret[ph((long long)s_mb[b] - (f - s_woff[b]))] = w_v[f];
@@ -1145,6 +1239,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
     const unsigned long long tm3 = __builtin_amdgcn_s_memrealtime();
     st->mtr[0] += tm1 - tm0, st->mtr[1] += tm2 - tm1, st->mtr[2] += tm3 - tm2;
     st->mtr[3] += (unsigned long long)s_wmax, st->mtr[4] += (unsigned long long)s_wtot, st->mtr[5] += (unsigned long long)s_wcnt;
+    st->mtr[6] += tw0 - tm1, st->mtr[7] += tw1 - tw0, st->mtr[8] += tw2 - tw1;
     st->off_count = off1;
     st->off_ratio = off_ratio;
     st->mb_counter += advance;  // (the draws of a fused forward's mini-batch)
@@ -1893,10 +1988,11 @@ VrGemmJob vr_gemm_job(int ep, int M, int N, int K, const float *A, long long sam
 int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
   const Params &P = h->P;
   KG_CHECK((size_t)M <= h->rowsMax, "vracer: forward batch exceeds the allocated rows");
-  // one launch for the whole forward pass (KORALI_AMD_VR_FUSED=0: the
-  // per-layer kernels, bit-identical results; A/B and the equality test)
+  // KORALI_AMD_VR_FUSED=1: one launch for the whole forward pass (bit-identical
+  // results; measured slower than the per-layer kernels at C5, round 5: kept
+  // for A/B and the equality test)
   const char *fe = getenv("KORALI_AMD_VR_FUSED");
-  if (P.H <= 256 && !(fe && *fe == '0')) {
+  if (P.H <= 256 && fe && *fe == '1') {
     VrStage tg(h, M == P.E ? "gemm_rollout" : (M == 2 * P.B ? "gemm_update" : "gemm_other"));
     hipLaunchKernelGGL(k_vr_fwd_fused<false>, dim3(vr_blocks(M, FR)), dim3(256), 0, h->stream, P, M, X,
                        (const float *)h->theta, (const long long *)h->offs, h->acts, (long long)h->rowsMax, out,
@@ -1947,13 +2043,21 @@ void vr_multi(kg_vracer_t h, const VrMulti &J) {
   hipLaunchKernelGGL(k_vr_multi, dim3(n), dim3(256), 0, h->stream, J);
 }
 
+// KORALI_AMD_VR_STAGED=1: the metadata kernel's retrace walks staged through
+// LDS (measured slower than the one-thread walks at C5, round 5: 24 against
+// 19 us; kept for A/B)
+static bool vr_staged_walks() {
+  const char *e = getenv("KORALI_AMD_VR_STAGED");
+  return e && *e == '1';
+}
+
 int vr_update(kg_vracer_t h, const unsigned *forced) {
   const Params &P = h->P;
   const int B = P.B;
   KG_CHECK(h->st_host->size >= 2, "vracer: policy updates need at least two experiences in the replay memory");
   VrStage tu(h, "update");
   const char *fe = getenv("KORALI_AMD_VR_FUSED");
-  const bool fused = P.H <= 256 && !(fe && *fe == '0');
+  const bool fused = P.H <= 256 && fe && *fe == '1';
   if (fused) {
     // the mini-batch draw, its gather and the whole forward pass: one launch
     VrStage tg(h, "gemm_update");
@@ -1966,7 +2070,7 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   }
   const unsigned long long advance = (fused && !forced) ? (unsigned long long)B : 0ULL;
   hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er,
-                     (const unsigned *)h->mb, (const float *)h->out, h->G, advance);
+                     (const unsigned *)h->mb, (const float *)h->out, h->G, advance, vr_staged_walks() ? 1 : 0);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
   const size_t rs = h->rowsMax * P.H;
   const float *lastA = h->acts + (size_t)(P.L - 1) * rs;
@@ -2060,7 +2164,7 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
       {"state_rescaling_means", &h->st->smean[0], 4, (size_t)P.S},
       {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)P.S},
-      {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)6},
+      {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)9},
   };
   for (auto &x : tab)
     if (!strcmp(x.n, name)) {

@@ -56,7 +56,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     c3) step c3 600 python bench.py --workload c3 --steps ${C3_STEPS:-40} --warmup 3 ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 ;;
     benchx) step benchx 600 python bench.py --steps ${BENCH_STEPS:-200} --warmup 10 --cov exact --no-cpu-baseline ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c1 ;;
     profc3) step profc3 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c3" -o run --output-format csv -- python bench.py --workload c3 --steps 20 --warmup 2 --no-cpu-baseline ;;
     profc4) step profc4 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_c4" -o run --output-format csv -- python bench.py --workload c4 --steps 10 --warmup 2 ;;
     pmcf) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
@@ -80,6 +80,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     benchq) step benchq 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     benchteam) step bench_t16 300 env KORALI_AMD_APPLY_TEAM=16 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_t64 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
+    pmc2s) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1 && step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1 && python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/c2_pmc_traffic.csv" && rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" ;;
+    c5ab) step c5s0 300 env KORALI_AMD_VR_STAGED=0 python bench.py --workload c5 --no-cpu-baseline --steps 60 && step c5s1 300 env KORALI_AMD_VR_STAGED=1 python bench.py --workload c5 --no-cpu-baseline --steps 60 ;;
   esac
 done
 echo "session done"

@@ -59,6 +59,7 @@ def test_fused_forward_equals_per_layer_kernels(monkeypatch, H, L, n):
     d = device(hidden_size=H, hidden_layers=L, environments=4096, mini_batch_size=64, replay_maximum_size=1024,
                replay_start_size=512, initial_exploration_noise=0.7, hyperparameters=th)
     X = np.random.default_rng(5).standard_normal((n, S)).astype(f32)
+    monkeypatch.setenv("KORALI_AMD_VR_FUSED", "1")
     fused = d.run_policy(X)
     monkeypatch.setenv("KORALI_AMD_VR_FUSED", "0")
     per_layer = d.run_policy(X)
@@ -69,11 +70,13 @@ def test_fused_update_equals_per_layer_kernels(monkeypatch):
     """Policy updates with drawn mini-batches: the fused draw + forward launch
     (and the draw counter advanced by the metadata kernel) leaves every
     hyperparameter, Adam moment and replay field equal to the separate
-    k_vr_minibatch + per-layer forward bit for bit."""
+    k_vr_minibatch + per-layer forward bit for bit; so do the retrace walks
+    staged through LDS against the one-thread walks."""
     ag, th = fill_replay(64, 2, 8, 90, 600)
     runs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("KORALI_AMD_VR_FUSED", fused)
+        monkeypatch.setenv("KORALI_AMD_VR_STAGED", fused)
         d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
                    replay_start_size=100, hyperparameters=th)
         load_replay(d, ag)
