@@ -2043,12 +2043,12 @@ void vr_multi(kg_vracer_t h, const VrMulti &J) {
   hipLaunchKernelGGL(k_vr_multi, dim3(n), dim3(256), 0, h->stream, J);
 }
 
-// KORALI_AMD_VR_STAGED=1: the metadata kernel's retrace walks staged through
-// LDS (measured slower than the one-thread walks at C5, round 5: 24 against
-// 19 us; kept for A/B)
+// the metadata kernel's retrace walks staged through LDS (C5, round 5: the
+// walk phase 14.2 against 21.0 us for the one-thread walks through the replay
+// memory; KORALI_AMD_VR_STAGED=0 selects those, A/B and the equality test)
 static bool vr_staged_walks() {
   const char *e = getenv("KORALI_AMD_VR_STAGED");
-  return e && *e == '1';
+  return !(e && *e == '0');
 }
 
 int vr_update(kg_vracer_t h, const unsigned *forced) {

@@ -76,7 +76,7 @@ def test_fused_update_equals_per_layer_kernels(monkeypatch):
     runs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("KORALI_AMD_VR_FUSED", fused)
-        monkeypatch.setenv("KORALI_AMD_VR_STAGED", fused)
+        monkeypatch.setenv("KORALI_AMD_VR_STAGED", fused)  # (staged walks with the fused forward)
         d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
                    replay_start_size=100, hyperparameters=th)
         load_replay(d, ag)
