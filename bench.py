@@ -43,6 +43,14 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector == FP64 matrix (spec)
 HBM_PEAK_GBS = 8000.0
 
 # algorithmic FP64 work per launch of each stage at C2
+def stage_flops(N, lam, mu):
+    """Algorithmic FLOPs per launch of the profiled CMA-ES stages at (N, lambda, mu)."""
+    return {"eigen": (4.0 / 3.0) * N ** 3 + 2.0 * N ** 3 + 6.0 * 1.1 * N ** 3,
+            "eigen_tridiag": (4.0 / 3.0) * N ** 3, "eigen_unpack": 2.0 * N ** 3, "eigen_apply": 6.0 * 1.1 * N ** 3,
+            "transform": 2.0 * lam * N ** 2, "covariance": 1.0 * mu * N * (N + 1),
+            "rankmu_mfma": 1.0 * mu * N * (N + 1), "objective": 8.0 * lam * N}
+
+
 STAGE_FLOPS = {
     # GSL symmv pieces: tridiagonalisation (4/3)N^3, unpack 2N^3 (nominal),
     # Givens application 6 flops * N rows * ~1.1 N^2 rotations
@@ -894,6 +902,27 @@ def run_c4_engine(args, world, rank):
     tdist.destroy_process_group()
 
 
+def c4_roofline(stages):
+    """The dominant device kernel of a C4 generation (HIP-event stage times;
+    the host chase, the eigen aggregate and the second-stream rank-mu MFMA
+    excluded) against the FP64 peak, its HBM bytes per launch from the
+    committed C4 PMC passes."""
+    kern = {k: v for k, v in stages.items() if k not in ("eigen", "eigen_chase_host", "rankmu_mfma")}
+    if not kern:
+        return None
+    dom = max(kern, key=kern.get)
+    flops = stage_flops(C4_N, C4_L, C4_L // 2).get(dom, 0.0)
+    ms = stages[dom]
+    achieved = flops / (ms * 1e-3) / 1e12
+    traffic, _ = pmc_traffic(dom, "c4_pmc_traffic.csv")
+    return {"kernel": {"eigen_tridiag": "kg::k_tridiag_mw2"}.get(dom, dom), "stage": dom, "bound": "mfma",
+            "bound_note": "FP64 compute roof (vector = matrix FP64 peak on MI355X); the tridiagonalisation is a "
+                          "per-step chain in GSL order with one in-launch hand-off per Householder step",
+            "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+            "traffic": traffic, "traffic_source": profile_file("c4_pmc_traffic.csv")[1] if traffic else None,
+            "algorithmic_flops_per_launch": flops, "avg_launch_ms": ms}
+
+
 def run_c4(args):
     """BASELINE.json configs[3]: CMA-ES, 512-dim negative Ackley
     (model.py:37-62), λ = 65536, μ = 32768, x0 = 2, σ0 = 1, seed 1337.  With
@@ -973,6 +1002,7 @@ def run_c4(args):
                        "covariance_update": args.cov},
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
             "stage_ms_rank0": stages,
+            "roofline": c4_roofline(stages),
             "rankmu_mfma_roofline": rankmu_roofline(stages["rankmu_mfma"], C4_L // 2, C4_N, "c4_pmc_traffic.csv")
             if "rankmu_mfma" in stages else None,
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
@@ -1104,6 +1134,17 @@ def run_c5(args):
         rows = list(csv.DictReader(open(tf)))
         if rows:
             traffic = (float(rows[0]["fetch_KB_x2"]) + float(rows[0]["write_KB"])) * 1024.0
+    # HBM bytes of one policy update: every update kernel's FETCH_SIZE x2 +
+    # WRITE_SIZE per dispatch (the kernels dispatched once per update) from the
+    # committed PMC passes over all update kernels (tools/pmc_c5_update.py)
+    upd_traffic, upd_traffic_src = None, None
+    uf, upd_traffic_src = profile_file("c5_pmc_update_traffic.csv")
+    if upd_traffic_src:
+        import csv
+        rows = list(csv.DictReader(open(uf)))
+        top = max(int(r["dispatches"]) for r in rows)
+        upd_traffic = sum((float(r["fetch_KB_x2"]) + float(r["write_KB"])) * 1024.0 for r in rows
+                          if int(r["dispatches"]) * 2 >= top)
     out = {
         "metric": "VRACER experiences/sec, 4096 concurrent CartPole rollouts, 2x256 policy (C5)",
         "value": exps / elapsed, "unit": "experiences/s", "n_gpus": 1, "steps": args.steps,
@@ -1121,11 +1162,20 @@ def run_c5(args):
                             "achieved_tflops": upd_flops / (upd_ms * 1e-3) / 1e12 if upd_ms else None,
                             "peak": FP32_PEAK_TFLOPS,
                             "frac": upd_flops / (upd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS if upd_ms else None},
-        "roofline": {"kernel": "kg::vr::k_vr_gemm<1> (rollout forward, hidden layer)", "bound": "mfma",
-                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": traffic,
-                     "traffic_source": profile_file("c5_pmc_traffic.csv")[1] if traffic else None,
-                     "algorithmic_flops_per_launch": gemm_flops, "avg_launch_ms": gemm_ms},
+        # the metric's dominant work: one policy update (EBPU 1: one per
+        # experience; the rollout GEMM below it is 1/4096 of an experience)
+        "roofline": {"kernel": "VRACER policy update (mini-batch, forward, metadata, backward, Adam: one "
+                               "trainPolicy step, its kernels back to back on the handle's stream)",
+                     "bound": "mfma", "achieved": upd_flops / (upd_ms * 1e-3) / 1e12 if upd_ms else None,
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": upd_flops / (upd_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS if upd_ms else None,
+                     "traffic": upd_traffic, "traffic_source": upd_traffic_src,
+                     "algorithmic_flops_per_launch": upd_flops, "avg_launch_ms": upd_ms},
+        "rollout_gemm_roofline": {"kernel": "kg::vr::k_vr_gemm<1> (rollout forward, hidden layer)", "bound": "mfma",
+                                  "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": achieved / FP32_PEAK_TFLOPS if achieved else None, "traffic": traffic,
+                                  "traffic_source": profile_file("c5_pmc_traffic.csv")[1] if traffic else None,
+                                  "algorithmic_flops_per_launch": gemm_flops, "avg_launch_ms": gemm_ms},
         "mean_recent_episode_reward": float(np.mean(finished[finished != 0])) if np.any(finished != 0) else None,
     }
     if not args.no_cpu_baseline:

@@ -28,7 +28,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     prof4) step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python bench.py --workload c4 --steps 6 --warmup 2 --no-cpu-baseline ;;
     pmc2) step pmc2f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc2_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline && step pmc2w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc2_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
-    pmc4) step pmc4f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc4) step pmc4f 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     mfma) step mfma2 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma2" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --cov mfma && step mfma4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     trace2dpp) step trace2_dpp0 200 env KORALI_AMD_SQ_DPP=0 KORALI_AMD_TRACE_EIGEN=1 python tools/trace_c2.py ;;
     c4p) step prof4p 400 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python bench.py --workload c4 --steps 6 --warmup 2 --no-cpu-baseline && step pmc4fp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4wp 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step mfma4p 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/mfma4" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
@@ -81,6 +81,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     benchteam) step bench_t16 300 env KORALI_AMD_APPLY_TEAM=16 python bench.py --steps 200 --warmup 10 --no-cpu-baseline && step bench_t64 300 python bench.py --steps 200 --warmup 10 --no-cpu-baseline ;;
     pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
     pmc2s) step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1 && step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1 && python tools/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/c2_pmc_traffic.csv" && rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" ;;
+    pmc4s) step pmc4f 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && python tools/pmc_summary.py "$OUT/pmc4_fetch" "$OUT/pmc4_write" > "$OUT/c4_pmc_traffic.csv" && rm -rf "$OUT/pmc4_fetch" "$OUT/pmc4_write" ;;
+    givab) for i in 1 2; do step giv_bf$i 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1 && step giv_br$i 300 env KORALI_AMD_LIB_VARIANT=branchy python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1; done ;;
     c5ab) step c5s0 300 env KORALI_AMD_VR_STAGED=0 python bench.py --workload c5 --no-cpu-baseline --steps 60 && step c5s1 300 env KORALI_AMD_VR_STAGED=1 python bench.py --workload c5 --no-cpu-baseline --steps 60 ;;
   esac
 done
