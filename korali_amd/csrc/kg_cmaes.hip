@@ -1583,6 +1583,122 @@ __global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal,
   }
 }
 
+// adaptC's exact rank-mu sums on LANE chains (round 5): every lane owns one
+// element (d, e) of the lower triangle and runs its whole ordered chain
+// c += fl(fl(T_kd Yc_ke) / s2) itself -- the same terms, quotients and
+// order as k_adaptC_row, so the same bits.  A workgroup is a 16 x 16 tile
+// (d0 + t/16, e0 + t%16) of the lower triangle; T rows and Yc columns are
+// staged through LDS 128 terms at a time, the next chunk's loads in flight.
+// Per term a wave issues five instructions for 64 elements (the row form: 20
+// for 4 elements x 16 terms, its quotients shared out by 16 DPP-broadcast
+// adds), and a tile reads 32 operand streams for 256 elements (the row form:
+// 12 for 32): C4's 131 328 chains of 32 768 terms are issue-bound instead of
+// chain-latency-bound, and the tiles re-read a third of the operands.
+constexpr int AL_T = 16, AL_K = 128, AL_LD = AL_T + 1;
+__host__ __device__ inline int al_blocks(int N) { return (N + AL_T - 1) / AL_T; }
+int al_tiles(int N) { return al_blocks(N) * (al_blocks(N) + 1) / 2; }
+template <bool kMarkstein>
+__device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double *__restrict__ Yc,
+                                       const double *__restrict__ Tt, const double *__restrict__ pc, double *C,
+                                       const CmaesScalars *__restrict__ sc, int tbase, double *__restrict__ pack,
+                                       double (*Ts)[AL_K][AL_LD], double (*Ys)[AL_K][AL_LD]) {
+  const int tid = threadIdx.x, dl = tid >> 4, el = tid & 15;
+  // tile -> (row block bd, column block be <= bd), row blocks in order
+  int t = blockIdx.x + tbase, bd = 0;
+  while (t > bd) t -= ++bd;
+  const int d0 = AL_T * bd, e0 = AL_T * t;
+  const int d = d0 + dl, e = e0 + el;
+  const bool active = d < N && e <= d && (!diagonal || e == d);
+  const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
+  const int hsig = (int)sc->hsig;
+  const double s2 = sc->sigma * sc->sigma, y = kMarkstein ? 1.0 / s2 : 0.0;
+  double acc = 0.0;
+  if (active) {
+    const double Cde = C[(size_t)d * N + e];
+    acc = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
+  }
+  // staging: T rows d0..d0+15 (term-contiguous) and Yc[k][e0..e0+15]
+  constexpr int U = AL_T * AL_K / 256;  // 8 values of each per thread
+  double tv[U], yv[U];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int q = tid + 256 * u, r = q / AL_K, kq = q % AL_K, k = k0 + kq;
+      tv[u] = (d0 + r < N && k < mu) ? Tt[(size_t)(d0 + r) * mu + k] : 0.0;
+      const int kk = k0 + (q >> 4), c = q & 15;
+      yv[u] = (kk < mu && e0 + c < N) ? Yc[(size_t)kk * N + e0 + c] : 0.0;
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int q = tid + 256 * u;
+      Ts[b][q % AL_K][q / AL_K] = tv[u];
+      Ys[b][q >> 4][q & 15] = yv[u];
+    }
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int k0 = 0, b = 0; k0 < mu; k0 += AL_K, b ^= 1) {
+    const bool more = k0 + AL_K < mu;
+    if (more) load(k0 + AL_K);
+    const int kn = min(AL_K, mu - k0);
+    int k = 0;
+    for (; k + 8 <= kn; k += 8) {
+      double q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const double pr = Ts[b][k + u][dl] * Ys[b][k + u][el];
+        if (kMarkstein) {
+          const double q0 = pr * y;
+          const double r = __builtin_fma(-q0, s2, pr);
+          q[u] = __builtin_fma(r, y, q0);
+        } else {
+          q[u] = pr / s2;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc += q[u];
+    }
+    for (; k < kn; k++) {
+      const double pr = Ts[b][k][dl] * Ys[b][k][el];
+      double q;
+      if (kMarkstein) {
+        const double q0 = pr * y;
+        const double r = __builtin_fma(-q0, s2, pr);
+        q = __builtin_fma(r, y, q0);
+      } else {
+        q = pr / s2;
+      }
+      acc += q;
+    }
+    if (more) store(b ^ 1);
+    __syncthreads();
+  }
+  if (pack) {
+    if (d < N && e <= d) pack[(size_t)d * (d + 1) / 2 + e] = active ? acc : C[(size_t)d * N + e];
+    return;
+  }
+  if (active) {
+    C[(size_t)d * N + e] = acc;
+    if (e < d) C[(size_t)e * N + d] = acc;
+  }
+}
+__global__ void __launch_bounds__(256) k_adaptC_lane(int N, int mu, int diagonal, const double *__restrict__ Yc,
+                                                     const double *__restrict__ Tt, const double *__restrict__ pc,
+                                                     double *C, const CmaesScalars *__restrict__ sc, int tbase,
+                                                     double *__restrict__ pack) {
+  __shared__ double Ts[2][AL_K][AL_LD], Ys[2][AL_K][AL_LD];  // [term][d - d0] / [term][e - e0]
+  // Markstein quotients when every factor is in range (as k_adaptC_row)
+  const double s2 = sc->sigma * sc->sigma;
+  const int ex = (int)((__double_as_longlong(s2) >> 52) & 0x7ff) - 1023;
+  if (__builtin_amdgcn_readfirstlane((int)(sc->rmuOutOfRange == 0u && ex >= -100 && ex <= 100)))
+    al_run<true>(N, mu, diagonal, Yc, Tt, pc, C, sc, tbase, pack, Ts, Ys);
+  else
+    al_run<false>(N, mu, diagonal, Yc, Tt, pc, C, sc, tbase, pack, Ts, Ys);
+}
+
 // mean :603-609 and mean update :623-624.  The sum over the μ selected rows
 // is sequential per d (the reference's order); a workgroup owns MN_D columns:
 // all its threads stream the products w_i Y[i][d] into LDS, 256 rows at a
@@ -3574,6 +3690,17 @@ static int cmaes_sigma(kg_cmaes_t h, size_t gen) {
 
 
 // KORALI_AMD_ROWCHAINS=0: the round-3 lockstep-lane mean / paths kernels (A/B)
+// the exact rank-mu sums on lane chains (k_adaptC_lane) from N = 256 up:
+// measured round 5 (gpurun_out/r5z) C4 (N = 512) 3.75 -> 2.14 ms per
+// generation, C2 (N = 128: 36 tiles, a third of the chip) 0.036 -> 0.060 ms,
+// so C2 keeps the row chains (KORALI_AMD_ADAPTC_LANE_MIN moves the switch)
+static bool lane_chains(int N) {
+  static const int from = [] {
+    const char *e = getenv("KORALI_AMD_ADAPTC_LANE_MIN");
+    return e && *e ? atoi(e) : 256;
+  }();
+  return N >= from;
+}
 static bool row_chains() {
   static const bool on = [] {
     const char *e = getenv("KORALI_AMD_ROWCHAINS");
@@ -3855,7 +3982,10 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                          h->cfg.diagonal_covariance, h->covPart, h->pc, h->C, h->sc, 0);
     } else {
       static const bool old2 = getenv("KORALI_AMD_ADAPTC2") != nullptr;  // A/B switch
-      if (!old2 && row_chains()) {
+      if (!old2 && lane_chains(N)) {
+        hipLaunchKernelGGL(k_adaptC_lane, dim3(al_tiles(N)), dim3(256), 0, h->stream, N, mu,
+                           h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc, 0, (double *)nullptr);
+      } else if (!old2 && row_chains()) {
         // Markstein quotients when every factor is in range (k_rankmu_prep's
         // flag, read on the device: the kernel picks the branch per launch)
         hipLaunchKernelGGL(k_adaptC_row, dim3(ar_tiles(N)), dim3(512), 0, h->stream, N, mu,
@@ -3962,9 +4092,13 @@ int kg_cmaes_update_rows(kg_cmaes_t h, size_t generation) {
     const size_t npk = (size_t)N * (N + 1) / 2;
     hipLaunchKernelGGL(k_fill_min_i64, dim3((unsigned)std::min<size_t>((npk + 255) / 256, 1024)), dim3(256), 0,
                        h->stream, npk, (long long *)h->covPack);
-    const int nt = ar_tiles(N);
+    const bool lane = lane_chains(N);
+    const int nt = lane ? al_tiles(N) : ar_tiles(N);
     const int t0 = (int)((long long)nt * h->shardRank / h->shards), t1 = (int)((long long)nt * (h->shardRank + 1) / h->shards);
-    if (t1 > t0)
+    if (t1 > t0 && lane)
+      hipLaunchKernelGGL(k_adaptC_lane, dim3(t1 - t0), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
+                         h->Yc, h->Tt, h->pc, h->C, h->sc, t0, h->covPack);
+    else if (t1 > t0)
       hipLaunchKernelGGL(k_adaptC_row, dim3(t1 - t0), dim3(512), 0, h->stream, N, mu, h->cfg.diagonal_covariance, h->Yc,
                          h->Tt, h->pc, h->C, h->sc, t0, h->covPack);
     KG_HIP(hipGetLastError());
