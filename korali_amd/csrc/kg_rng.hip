@@ -88,20 +88,46 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_produce(uint32_t *__restrict__ ri
 // ---- chunked production (see kg_rng.hpp ChunkPlan, kg_mtjump.hip) ----
 // out[m] = XOR_{i: bit i of poly} seq[m + i], m < 624 (256 threads, three
 // outputs each; the bit loop is uniform, the reads consecutive across lanes)
-__device__ inline void mt_combine(const uint32_t *seq, const uint64_t *__restrict__ poly, uint32_t *out) {
+// the partial combination over the polynomial's words [w0, w1).  The set
+// bits' indices are found on the scalar unit (the polynomial is uniform),
+// eight at a time, so a batch is eight address adds, 24 LDS reads in flight
+// and 24 XORs per wave; a batch's unused slots read the zero pad at
+// MT_ZPAD (XOR with 0).  (One set bit at a time with its three reads waited
+// for, or with per-lane bit arithmetic, made the combine the producer's
+// dominant cost: ~300 us per chunk workgroup at C2, round 5.)
+constexpr int MT_ZPAD = ((MT_SEQ + 3) & ~3) + 1024;  // 768 zero words after the rolling window
+__device__ __forceinline__ void mt_zero_pad(uint32_t *lds) {
+  for (int i = threadIdx.x; i < 768; i += blockDim.x) lds[MT_ZPAD + i] = 0u;
+}
+__device__ __forceinline__ void mt_combine_words(const uint32_t *seq, const uint64_t *__restrict__ poly, int w0,
+                                                 int w1, uint32_t &a0, uint32_t &a1, uint32_t &a2) {
   const int t = threadIdx.x;
-  const int m2 = (t + 512 < MT_N) ? t + 512 : MT_N - 1;
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int w = 0; w < MT_POLY_WORDS; w++) {
-    uint64_t bits = poly[w];
+  for (int w = w0; w < w1; w++) {
+    const uint64_t pw = poly[w];
+    unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)pw), hi = __builtin_amdgcn_readfirstlane((unsigned)(pw >> 32));
+    uint64_t bits = ((uint64_t)hi << 32) | lo;
     while (bits) {
-      const int i = w * 64 + __builtin_ctzll(bits);
-      bits &= bits - 1;
-      a0 ^= seq[t + i];
-      a1 ^= seq[t + 256 + i];
-      a2 ^= seq[m2 + i];
+      int idx[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        idx[u] = bits ? w * 64 + __builtin_ctzll(bits) : MT_ZPAD;
+        bits &= bits - 1;  // (0 stays 0)
+      }
+      uint32_t r0[8], r1[8], r2[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t *p = seq + t + idx[u];
+        r0[u] = p[0], r1[u] = p[256], r2[u] = p[512];  // (lanes t >= 112: p[512] unused)
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) a0 ^= r0[u], a1 ^= r1[u], a2 ^= r2[u];
     }
   }
+}
+__device__ inline void mt_combine(const uint32_t *seq, const uint64_t *__restrict__ poly, uint32_t *out) {
+  const int t = threadIdx.x;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  mt_combine_words(seq, poly, 0, MT_POLY_WORDS, a0, a1, a2);
   out[t] = a0;
   out[t + 256] = a1;
   if (t + 512 < MT_N) out[t + 512] = a2;
@@ -162,6 +188,7 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_chunks(uint32_t *__restrict__ rin
   const ChunkPlan pl = *plan;
   if (blockIdx.x >= pl.n) return;
   const int t = threadIdx.x;
+  mt_zero_pad(msm);
   const unsigned long long c = pl.c_first + blockIdx.x;
   const uint32_t *src = seeds + (size_t)(c % (2 * K)) * MT_N;
   for (int i = t; i < MT_N; i += MT_TPB) seq[i] = src[i];
@@ -209,30 +236,21 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_jump_level(uint32_t *__restrict__
   if (k >= K) return;
   const int w0 = part * MT_POLY_WORDS / MT_JUMP_PARTS, w1 = (part + 1) * MT_POLY_WORDS / MT_JUMP_PARTS;
   const uint32_t *src = seeds + (size_t)((c0 + k - (1ULL << l)) % (2 * K)) * MT_N;
+  mt_zero_pad(msm);
   for (int i = threadIdx.x; i < MT_N; i += MT_TPB) msm[i] = src[i];
   __syncthreads();
   // terms i < 64 w1 read seq[m + i], m < 624
   mt_fill_seq(msm, nullptr, 0, nullptr, 0, min(MT_SEQ, MT_N - 1 + 64 * w1));
   const int t = threadIdx.x;
-  const int m2 = (t + 512 < MT_N) ? t + 512 : MT_N - 1;
   uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int w = w0; w < w1; w++) {
-    uint64_t bits = poly[w];
-    while (bits) {
-      const int i = w * 64 + __builtin_ctzll(bits);
-      bits &= bits - 1;
-      a0 ^= msm[t + i];
-      a1 ^= msm[t + 256 + i];
-      a2 ^= msm[m2 + i];
-    }
-  }
+  mt_combine_words(msm, poly, w0, w1, a0, a1, a2);
   uint32_t *out = seeds + (size_t)((c0 + k) % (2 * K)) * MT_N;
   atomicXor(out + t, a0);
   atomicXor(out + t + 256, a1);
   if (t + 512 < MT_N) atomicXor(out + t + 512, a2);
 }
 
-size_t mt_chunk_lds_bytes() { return (size_t)(((MT_SEQ + 3) & ~3) + 1024) * sizeof(uint32_t); }
+size_t mt_chunk_lds_bytes() { return (size_t)(MT_ZPAD + 768) * sizeof(uint32_t); }
 
 __device__ inline bool polar_pair(const uint32_t *__restrict__ ring, unsigned long long R, const PosView &st,
                                   unsigned long long a, double &y, double &r2) {

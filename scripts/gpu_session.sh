@@ -84,6 +84,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmc4s) step pmc4f 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc4_fetch" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && step pmc4w 300 env KORALI_AMD_PLAIN_LAUNCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc4_write" -o run --output-format csv -- python bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline && python tools/pmc_summary.py "$OUT/pmc4_fetch" "$OUT/pmc4_write" > "$OUT/c4_pmc_traffic.csv" && rm -rf "$OUT/pmc4_fetch" "$OUT/pmc4_write" ;;
     givab) for i in 1 2; do step giv_bf$i 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1 && step giv_br$i 300 env KORALI_AMD_LIB_VARIANT=branchy python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1; done ;;
     laneab) step lane_c2 300 python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1 && step row_c2 300 env KORALI_AMD_ADAPTC_LANE_MIN=100000 python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1 && step lane_c4 300 python bench.py --workload c4 --steps 20 --warmup 3 --no-cpu-baseline && step row_c4 300 env KORALI_AMD_ADAPTC_LANE_MIN=100000 python bench.py --workload c4 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    lwab) for lw in 15 16 17; do step lw$lw 300 env KORALI_AMD_MT_CHUNK_LOG2=$lw python bench.py --steps 300 --warmup 10 --no-cpu-baseline --no-c1 && step plw$lw 300 env KORALI_AMD_MT_CHUNK_LOG2=$lw rocprofv3 --kernel-trace --stats -d "$OUT/plw$lw" -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c1 && rm -f "$OUT/plw$lw/run_kernel_trace.csv"; done ;;
     c5ab) step c5s0 300 env KORALI_AMD_VR_STAGED=0 python bench.py --workload c5 --no-cpu-baseline --steps 60 && step c5s1 300 env KORALI_AMD_VR_STAGED=1 python bench.py --workload c5 --no-cpu-baseline --steps 60 ;;
   esac
 done
