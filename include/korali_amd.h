@@ -183,7 +183,9 @@ int kg_cmaes_wait_termination_fields(kg_cmaes_t h, double *out);
  * covariance kg_cmaes_sample draws the whole population on every rank: the
  * redraw walk and the ±z pairs are sequential over it);
  * the caller all-gathers "Value Vector" (λ doubles, shards in rank order)
- * and then runs the update protocol of the handle's covariance mode.
+ * — with use_gradients also "Gradients" (λ x N doubles, each rank's rows set
+ * by kg_cmaes_set_gradients, shards in rank order) — and then runs the
+ * update protocol of the handle's covariance mode.
  *
  * cov_mode KG_COV_EXACT — the reference's summation order, every rank's state
  * bit-identical to the unsharded run (CMAES.cpp.base:603-609, :690-718 sum

@@ -2994,6 +2994,7 @@ bool field_ref(kg_cmaes_s *h, const std::string &k, FieldRef &r) {
   VEC("Masking Matrix", h->mask, N)
   VEC("Masking Matrix Sigma", h->maskSigma, N)
   if (h->BDZ) VEC("BDZ Matrix", h->BDZ, L * N)
+  if (h->G) VEC("Gradients", h->G, L * N)
   if (h->part) {
     const size_t nt = (N + 15) / 16;
     VEC("Shard Partials", h->part, 2 * N + nt * (nt + 1) / 2 * 256)
@@ -3063,7 +3064,6 @@ int kg_cmaes_create(const kg_cmaes_cfg *cfg, kg_cmaes_t *out) {
            "Mirrored Sampling can only be applied with an even Sample Population");  // CMAES.cpp.base:91
   KG_CHECK(!cfg->use_gradients || cfg->gradient_step_size > 0.0,
            "Gradient Step Size must be larger than 0.0");  // CMAES.cpp.base:86
-  KG_CHECK(!cfg->use_gradients || cfg->shard_count <= 1, "Use Gradient Information runs unsharded");
   KG_CHECK(cfg->variable_count <= 960, "device path supports up to 960 variables");
   KG_CHECK(cfg->mu_type >= 0 && cfg->mu_type <= 3,
            "Invalid setting of Mu Type (Linear, Equal, Logarithmic, or Proportional accepted).");
@@ -4083,6 +4083,9 @@ int kg_cmaes_update_rows(kg_cmaes_t h, size_t generation) {
     else
       hipLaunchKernelGGL(k_mean2, dim3((N + MN_D - 1) / MN_D), dim3(256), mean2_lds_bytes(), h->stream, N, mu, h->Y,
                          h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
+    if (h->G)  // every rank holds the whole population's gradients (the caller's all-gather)
+      hipLaunchKernelGGL(k_mean_gradient, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, mu, h->cfg.gradient_step_size,
+                         h->G, h->idx, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     KG_HIP(hipGetLastError());
     if (cmaes_paths(h, generation)) return 1;
   }
@@ -4120,6 +4123,9 @@ int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
     Stage st(h, "mean_paths");
     hipLaunchKernelGGL(k_shard_finalize, dim3((N + 255) / 256), dim3(256), 0, h->stream, N, h->part, h->mean,
                        h->prevMean, h->meanUpdate, h->currBestVars, h->bestEverVars, h->sc);
+    if (h->G)
+      hipLaunchKernelGGL(k_mean_gradient, dim3((N + 63) / 64), dim3(64), 0, h->stream, N, h->mu,
+                         h->cfg.gradient_step_size, h->G, h->idx, h->w, h->mean, h->prevMean, h->meanUpdate, h->sc);
     KG_HIP(hipGetLastError());
     if (cmaes_paths(h, generation)) return 1;
   }

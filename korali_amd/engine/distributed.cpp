@@ -240,6 +240,7 @@ class HostCollective : public Collective {
     boot.gatherToAll(v.data(), count * sizeof(double));
     b.set(v.data(), v.size() * sizeof(double));
   }
+  void allGatherHost(double *buf, size_t count) override { boot.gatherToAll(buf, count * sizeof(double)); }
   void allReduceSum(const SolverBuffer &b, size_t n) override {
     std::vector<double> v(n);
     b.get(v.data(), n * sizeof(double));
@@ -348,6 +349,10 @@ class RcclCollective : public Collective {
     void *s = b.stream();
     enqueue([&](void *c) { return allGatherFn(p + (size_t)rank * count, p, count, 8 /* ncclFloat64 */, c, s); },
             "ncclAllGather");
+  }
+  void allGatherHost(double *buf, size_t count) override {
+    if (dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
+    boot.gatherToAll(buf, count * sizeof(double));
   }
   void allReduceSum(const SolverBuffer &b, size_t n) override {
     void *p = b.devicePtr(), *s = b.stream();

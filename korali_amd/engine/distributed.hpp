@@ -43,6 +43,9 @@ class Collective {
   virtual std::string transport() const = 0;
   // in place: the buffer holds world * count doubles, this rank's block at [rank count, (rank+1) count)
   virtual void allGather(const SolverBuffer &b, size_t count) = 0;
+  // in place on host memory: buf holds world * count doubles (small
+  // per-sample results, e.g. CCMA-ES constraint values), over the bootstrap
+  virtual void allGatherHost(double *buf, size_t count) = 0;
   // element-wise sum of n doubles
   virtual void allReduceSum(const SolverBuffer &b, size_t n) = 0;
   // element-wise MAX of n int64 (the bit patterns of doubles; exact gather)

@@ -609,6 +609,11 @@ struct CmaesModule : SolverModule {
   Collective *dist = nullptr;
   size_t r0 = 0, r1 = 0;
   bool exactShards = true;  // the sharded update's protocol (include/korali_amd.h): exact order or partial sums
+  // Distributed CCMA-ES: the device state runs replicated (unsharded handle on
+  // every rank: the viability regime changes the population size and the
+  // resampling walk is sequential), the callbacks are split over the ranks
+  // and their values all-gathered (distributed.cpp.base:73-129's worker role)
+  bool replicated = false;
   std::vector<size_t> constraintFns;  // CCMA-ES (function table indices)
   size_t curGen = 0;
 
@@ -656,13 +661,9 @@ struct CmaesModule : SolverModule {
     // order (optimization.cpp.base:11-24)
     if (pt == "optimization" && pb.contains("Constraints"))
       for (size_t c = 0; c < pb["Constraints"].size(); c++) constraintFns.push_back(pb["Constraints"][c].getUInt());
-    if (!constraintFns.empty() && dist)
-      fail("Constrained CMA-ES needs an unsharded run (Sequential or Concurrent conduit).");
+    replicated = dist && !constraintFns.empty();
     if (!constraintFns.empty() && mirrored) fail("Mirrored Sampling not applicable to problems with constraints");
-    if (dist) {
-      if (useGradients)
-        fail("The Distributed conduit shards the population: 'Use Gradient Information' needs an unsharded run "
-             "(Sequential or Concurrent conduit).");
+    if (dist && !replicated) {
       if (lam % (size_t)dist->world)
         fail("The Distributed conduit splits the population evenly: 'Population Size' (%zu) must be a multiple of "
              "the number of ranks (%d).",
@@ -746,8 +747,8 @@ struct CmaesModule : SolverModule {
     c.cov_mode = cu == "mfma" ? KG_COV_MFMA : KG_COV_EXACT;
     exactShards = c.cov_mode == KG_COV_EXACT;
     c.device = solverDevice(js, dist);
-    c.shard_rank = dist ? dist->rank : 0;
-    c.shard_count = dist ? dist->world : 0;
+    c.shard_rank = dist && !replicated ? dist->rank : 0;
+    c.shard_count = dist && !replicated ? dist->world : 0;
     c.store_bdz = 0;
     c.eigen_device_chase = 0;
     c.constraint_count = constraintFns.size();
@@ -823,27 +824,40 @@ struct CmaesModule : SolverModule {
     auto *self = (CmaesModule *)ctx;
     const size_t nc = self->constraintFns.size();
     try {
-      self->conduit->evaluateBatch(rows, [&](size_t r) {
-        Sample s;
-        s["Module"] = "Problem";
-        s["Operation"] = "Evaluate Constraints";
-        s["Sample Id"] = (unsigned long long)0;  // (as CMAES.cpp.base:326, :357, :398)
-        s["Current Generation"] = (unsigned long long)self->curGen;
-        s["Parameters"] = std::vector<double>(X + r * N_, X + (r + 1) * N_);
-        for (size_t c = 0; c < nc; c++) {
-          getFunction(self->constraintFns[c])(s);
-          if (!s.contains("F(x)")) fail("The constraint function %zu did not assign 'F(x)'.", c);
-          const double v = s["F(x)"].getDouble();
-          if (!std::isfinite(v)) fail("Non finite value of constraint evaluation %lu detected: %f\n", (unsigned long)c, v);
-          out[r * nc + c] = v;
-        }
-      });
+      if (self->dist) {  // replicated: this rank's block of rows, then the all-gather
+        Collective &d = *self->dist;
+        const size_t per = (rows + d.world - 1) / d.world, a = std::min(rows, per * d.rank),
+                     b = std::min(rows, a + per);
+        std::vector<double> buf((size_t)d.world * per * nc, 0.0);
+        for (size_t r = a; r < b; r++)
+          self->evaluateConstraints(X + r * N_, N_, buf.data() + ((size_t)d.rank * per + (r - a)) * nc);
+        d.allGatherHost(buf.data(), per * nc);
+        std::copy(buf.begin(), buf.begin() + rows * nc, out);
+        return 0;
+      }
+      self->conduit->evaluateBatch(rows, [&](size_t r) { self->evaluateConstraints(X + r * N_, N_, out + r * nc); });
     } catch (...) {
       self->pendingError = std::current_exception();
       return 1;
     }
     (void)ids;
     return 0;
+  }
+  // Optimization::evaluateConstraints for one sample (optimization.cpp.base:11-24)
+  void evaluateConstraints(const double *x, size_t N_, double *out) {
+    Sample s;
+    s["Module"] = "Problem";
+    s["Operation"] = "Evaluate Constraints";
+    s["Sample Id"] = (unsigned long long)0;  // (as CMAES.cpp.base:326, :357, :398)
+    s["Current Generation"] = (unsigned long long)curGen;
+    s["Parameters"] = std::vector<double>(x, x + N_);
+    for (size_t c = 0; c < constraintFns.size(); c++) {
+      getFunction(constraintFns[c])(s);
+      if (!s.contains("F(x)")) fail("The constraint function %zu did not assign 'F(x)'.", c);
+      const double v = s["F(x)"].getDouble();
+      if (!std::isfinite(v)) fail("Non finite value of constraint evaluation %lu detected: %f\n", (unsigned long)c, v);
+      out[c] = v;
+    }
   }
   std::exception_ptr pendingError;
 
@@ -868,6 +882,8 @@ struct CmaesModule : SolverModule {
     }
     if (objective >= 0) {
       check(kg_cmaes_eval_builtin(h, objective));
+    } else if (replicated) {
+      splitEvaluate(gen);
     } else if (dist) {
       hostEvaluate(gen, r0, r1);
     } else {
@@ -875,43 +891,14 @@ struct CmaesModule : SolverModule {
       std::vector<double> X(lam * N), F(lam), G(useGradients ? lam * N : 0);
       check(kg_cmaes_get_candidates(h, X.data(), N));
       Function *f = bayesian ? nullptr : &getFunction(fn);
-      conduit->evaluateBatch(lam, [&](size_t i) {
-        Sample s;
-        s["Module"] = "Problem";
-        s["Operation"] = useGradients ? "Evaluate With Gradients" : "Evaluate";
-        s["Sample Id"] = (unsigned long long)i;
-        s["Current Generation"] = (unsigned long long)gen;
-        std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
-        s["Parameters"] = x;
-        if (bayesian) {  // Bayesian::evaluate: -Inf outside the prior's support is a valid F(x)
-          bayesian->evaluate(s, x, i);
-          F[i] = s["F(x)"].getDouble();
-          return;
-        }
-        (*f)(s);
-        if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
-        F[i] = s["F(x)"].getDouble();
-        if (useGradients) {  // Optimization::evaluateWithGradients (optimization.cpp.base:47-63)
-          const std::vector<double> g = KORALI_GET(std::vector<double>, s, "Gradient");
-          if (g.size() != N)
-            fail("Size of sample's gradient evaluations vector (%lu) is different from the number of problem "
-                 "variables defined (%lu).\n",
-                 (unsigned long)g.size(), (unsigned long)N);
-          if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
-          for (size_t d = 0; d < N; d++) {
-            if (!std::isfinite(g[d]))
-              fail("Non finite value of gradient evaluation detected for variable %lu: %f\n", (unsigned long)d, g[d]);
-            G[i * N + d] = g[d];
-          }
-        }
-        if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
-      });
+      conduit->evaluateBatch(lam, [&](size_t i) { evaluateSample(gen, i, X, F, G, f); });
       check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
       if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
     }
-    if (dist) {
+    if (dist && !replicated) {
       // the exchange steps of the sharded update
       dist->allGather(buffer("Value Vector"), r1 - r0);
+      if (useGradients) dist->allGather(buffer("Gradients"), (r1 - r0) * N);
       check(kg_cmaes_update_partial(h, gen));
       size_t n = 0;
       if (exactShards) {
@@ -948,28 +935,73 @@ struct CmaesModule : SolverModule {
   // the objective / log-posterior, the other rows' values arrive with the
   // all-gather
   void hostEvaluate(size_t gen, size_t a, size_t b) {
-    std::vector<double> X(lam * N), F(lam, 0.0);
+    std::vector<double> X(lam * N), F(lam, 0.0), G(useGradients ? lam * N : 0, 0.0);
     check(kg_cmaes_get_candidates(h, X.data(), N));
     Function *f = bayesian ? nullptr : &getFunction(fn);
+    for (size_t i = a; i < b; i++) evaluateSample(gen, i, X, F, G, f);
+    check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
+    if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
+  }
+
+  // replicated device state (Distributed CCMA-ES): this rank's block of the
+  // population through the objective, the values (and gradients) all-gathered
+  // over the bootstrap, every rank then sets the whole population's
+  void splitEvaluate(size_t gen) {
+    const size_t W = dist->world, per = (lam + W - 1) / W, a = std::min(lam, per * dist->rank),
+                 b = std::min(lam, a + per), gw = useGradients ? N : 0;
+    std::vector<double> X(lam * N), F(lam, 0.0), G(lam * gw, 0.0);
+    check(kg_cmaes_get_candidates(h, X.data(), N));
+    Function *f = bayesian ? nullptr : &getFunction(fn);
+    for (size_t i = a; i < b; i++) evaluateSample(gen, i, X, F, G, f);
+    std::vector<double> buf(W * per * (1 + gw), 0.0);
     for (size_t i = a; i < b; i++) {
-      Sample s;
-      s["Module"] = "Problem";
-      s["Operation"] = "Evaluate";
-      s["Sample Id"] = (unsigned long long)i;
-      s["Current Generation"] = (unsigned long long)gen;
-      std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
-      s["Parameters"] = x;
-      if (bayesian) {
-        bayesian->evaluate(s, x, i);
-      } else {
-        (*f)(s);
-        if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
-        if (!std::isfinite(s["F(x)"].getDouble()))
-          fail("Non finite value of function evaluation detected: %f\n", s["F(x)"].getDouble());
-      }
-      F[i] = s["F(x)"].getDouble();
+      double *row = buf.data() + (dist->rank * per + (i - a)) * (1 + gw);
+      row[0] = F[i];
+      std::copy(G.begin() + i * gw, G.begin() + (i + 1) * gw, row + 1);
+    }
+    dist->allGatherHost(buf.data(), per * (1 + gw));
+    for (size_t i = 0; i < lam; i++) {
+      const double *row = buf.data() + i * (1 + gw);
+      F[i] = row[0];
+      std::copy(row + 1, row + 1 + gw, G.begin() + i * gw);
     }
     check(bayesian ? kg_cmaes_set_log_posterior(h, F.data()) : kg_cmaes_set_fitness(h, F.data()));
+    if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
+  }
+
+  // one sample through the objective / log-posterior (CMAES.cpp.base:204-224;
+  // with gradients Optimization::evaluateWithGradients, optimization.cpp.base:47-63)
+  void evaluateSample(size_t gen, size_t i, const std::vector<double> &X, std::vector<double> &F,
+                      std::vector<double> &G, Function *f) {
+    Sample s;
+    s["Module"] = "Problem";
+    s["Operation"] = useGradients ? "Evaluate With Gradients" : "Evaluate";
+    s["Sample Id"] = (unsigned long long)i;
+    s["Current Generation"] = (unsigned long long)gen;
+    std::vector<double> x(X.begin() + i * N, X.begin() + (i + 1) * N);
+    s["Parameters"] = x;
+    if (bayesian) {  // Bayesian::evaluate: -Inf outside the prior's support is a valid F(x)
+      bayesian->evaluate(s, x, i);
+      F[i] = s["F(x)"].getDouble();
+      return;
+    }
+    (*f)(s);
+    if (!s.contains("F(x)")) fail("The objective function did not assign 'F(x)' for sample %zu.", i);
+    F[i] = s["F(x)"].getDouble();
+    if (useGradients) {
+      const std::vector<double> g = KORALI_GET(std::vector<double>, s, "Gradient");
+      if (g.size() != N)
+        fail("Size of sample's gradient evaluations vector (%lu) is different from the number of problem "
+             "variables defined (%lu).\n",
+             (unsigned long)g.size(), (unsigned long)N);
+      if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
+      for (size_t d = 0; d < N; d++) {
+        if (!std::isfinite(g[d]))
+          fail("Non finite value of gradient evaluation detected for variable %lu: %f\n", (unsigned long)d, g[d]);
+        G[i * N + d] = g[d];
+      }
+    }
+    if (!std::isfinite(F[i])) fail("Non finite value of function evaluation detected: %f\n", F[i]);
   }
 
   double field(const char *k) {

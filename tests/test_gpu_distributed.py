@@ -11,7 +11,10 @@ TMCMC must equal the unsharded run bit for bit; CMA-ES must reproduce the
 unsharded run bit for bit with the exact covariance update (the default; at
 the C4 shape over 4 generations too), and with MFMA its sort exactly and its
 mean / covariance / sigma within the partial-sum tolerance
-(include/korali_amd.h: shard sums in another order)."""
+(include/korali_amd.h: shard sums in another order).  Use Gradient
+Information runs sharded too: each rank evaluates its rows' gradients, the
+engine all-gathers them.  CCMA-ES (Problem "Constraints") runs replicated, its
+objective and constraint callbacks split over the ranks: bit-identical."""
 import json
 import os
 import socket
@@ -50,6 +53,8 @@ def close(a, b, rtol):
     (2, "cmaes", "builtin", "Host", "Exact"), (4, "cmaes", "host", "Host", "Exact"),
     (1, "cmaes", "builtin", "RCCL", "Exact"), (2, "cmaes", "c4", "Host", "Exact"),
     (2, "cmaes", "builtin", "Host", "MFMA"), (1, "cmaes", "builtin", "RCCL", "MFMA"),
+    (2, "cmaes", "grad", "Host", "Exact"), (2, "cmaes", "grad", "Host", "MFMA"),
+    (3, "cmaes", "ccmaes", "Host", "Exact"), (1, "cmaes", "ccmaes", "RCCL", "Exact"),
     (2, "tmcmc", "builtin", "Host", "-"), (3, "tmcmc", "host", "Host", "-"), (1, "tmcmc", "builtin", "RCCL", "-")])
 def test_distributed_conduit(tmp_path, ranks, solver, model, transport, cov):
     res = launch(tmp_path, ranks, solver, model, transport, cov)

@@ -8,12 +8,21 @@ the first generation's samples, fitness and sort bit-identical and mean /
 covariance / sigma within the partial-sum tolerance) and every rank's state
 against rank 0's (bit-identical).
 
-    distributed_check.py <out dir> cmaes|tmcmc builtin|host|c4 RCCL|Host [Exact|MFMA]
+    distributed_check.py <out dir> cmaes|tmcmc builtin|host|grad|ccmaes|c4 RCCL|Host [Exact|MFMA]
+
+model grad (CMA-ES only): the host Rosenbrock objective with its "Gradient",
+Use Gradient Information on (each rank evaluates its rows' gradients, the
+engine all-gathers them).
+
+model ccmaes (CMA-ES only): run-ccmaes.py's "Mixed" CCMA-ES experiment (host
+objective, 8 constraints): the device state replicated, the objective and
+constraint callbacks split over the ranks and their values all-gathered.
 
 model c4 (CMA-ES only): the C4 shape, 512-dim negative Ackley at
 lambda = 65536 (BASELINE.json configs[3]), after 1 and 4 generations.
 """
 import json
+import math
 import os
 import sys
 
@@ -30,6 +39,34 @@ def negative_rosenbrock(s):
     s["F(x)"] = -sum(100.0 * (x[i + 1] - x[i] * x[i]) ** 2 + (1.0 - x[i]) ** 2 for i in range(len(x) - 1))
 
 
+def rosenbrock_with_gradient(s):  # Optimization::evaluateWithGradients: F(x) and its "Gradient"
+    negative_rosenbrock(s)
+    x = s["Parameters"]
+    g = [0.0] * len(x)
+    for i in range(len(x) - 1):
+        t = x[i + 1] - x[i] * x[i]
+        g[i] += 400.0 * t * x[i] + 2.0 * (1.0 - x[i])
+        g[i + 1] -= 200.0 * t
+    s["Gradient"] = g
+
+
+def ccmaes_model(s):  # tests/ccmaes_cases.py evaluate_model (run-ccmaes.py's helpers)
+    x1, x2 = s["Parameters"]
+    s["F(x)"] = -x1**2 - x2**2 - math.sin(x1)**2 - math.sin(x2)**2
+
+
+def constraint(fn):
+    def c(s):
+        s["F(x)"] = fn(s["Parameters"])
+    return c
+
+
+# run-ccmaes.py's "Mixed" case: active and inactive constraints at the maxima
+CCMAES_CONSTRAINTS = [lambda x: -(x[0] - 1.0), lambda x: -(x[0] - 2.0), lambda x: -(x[1] - 1.0),
+                      lambda x: -(x[1] - 2.0), lambda x: -math.cos(x[0]), lambda x: -math.sin(x[0]),
+                      lambda x: -math.cos(x[1]), lambda x: -math.sin(x[1])]
+
+
 def gaussian(s):  # the builtin Gaussian likelihood, -0.5 * sum(x^2)
     s["logLikelihood"] = -0.5 * sum(v * v for v in s["Parameters"])
 
@@ -39,13 +76,30 @@ def experiment(solver, model, gens, cov="Exact"):
     e["Random Seed"] = 4242
     e["File Output"]["Enabled"] = False
     e["Console Output"]["Verbosity"] = "Silent"
-    if solver == "cmaes":
+    if solver == "cmaes" and model == "ccmaes":  # run-ccmaes.py's experiment
+        e["Problem"]["Type"] = "Optimization"
+        e["Problem"]["Objective Function"] = ccmaes_model
+        e["Problem"]["Constraints"] = [constraint(c) for c in CCMAES_CONSTRAINTS]
+        for i, name in enumerate(("X", "Y")):
+            e["Variables"][i]["Name"] = name
+            e["Variables"][i]["Lower Bound"] = -10.0
+            e["Variables"][i]["Upper Bound"] = +10.0
+        e["Solver"]["Type"] = "Optimizer/CMAES"
+        e["Solver"]["Population Size"] = 8
+        e["Solver"]["Viability Population Size"] = 2
+        e["Solver"]["Is Sigma Bounded"] = 1
+        e["Solver"]["Termination Criteria"]["Max Generations"] = gens
+    elif solver == "cmaes":
         N = 512 if model == "c4" else 16
         e["Problem"]["Type"] = "Optimization"
         if model == "c4":
             e["Problem"]["Objective Kernel"] = "Negative Ackley"
         elif model == "builtin":
             e["Problem"]["Objective Kernel"] = "Negative Rosenbrock"
+        elif model == "grad":
+            e["Problem"]["Objective Function"] = rosenbrock_with_gradient
+            e["Solver"]["Use Gradient Information"] = True
+            e["Solver"]["Gradient Step Size"] = 1e-3
         else:
             e["Problem"]["Objective Function"] = negative_rosenbrock
         for i in range(N):
@@ -77,8 +131,13 @@ def experiment(solver, model, gens, cov="Exact"):
     return e
 
 
-def state(e, solver):
-    return {k: e["Solver"][k] for k in KEYS[solver]} | {"Current Generation": e["Current Generation"]}
+CCMAES_KEYS = ["Viability Boundaries", "Constraint Evaluation Count", "Is Viability Regime", "Constraint Evaluations",
+               "Current Population Size"]
+
+
+def state(e, solver, model):
+    keys = KEYS[solver] + (CCMAES_KEYS if model == "ccmaes" else [])
+    return {k: e["Solver"][k] for k in keys} | {"Current Generation": e["Current Generation"]}
 
 
 def main():
@@ -94,7 +153,7 @@ def main():
         k.run(e)
         u = experiment(solver, model, gens, cov)
         korali.Engine().run(u)
-        result[str(gens)] = {"sharded": state(e, solver), "unsharded": state(u, solver)}
+        result[str(gens)] = {"sharded": state(e, solver, model), "unsharded": state(u, solver, model)}
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
         json.dump(result, f)
     print(f"DISTRIBUTED_CHECK rank {rank} done", flush=True)
