@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 6
+#define KG_ABI_VERSION 7
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -304,6 +304,11 @@ typedef struct {
   int version;
   double step_size;               /* "Step Size" (default 0.1) */
   double domain_extension_factor; /* "Domain Extension Factor" (default 0.2) */
+  /* per variable: 0 Univariate/Uniform prior (prior_min / prior_max =
+   * Minimum / Maximum), 1 Univariate/Normal (prior_min / prior_max = Mean /
+   * Standard Deviation; normal.cpp.base).  Variables sharing a distribution
+   * share its kind.  NULL: every prior Uniform.  mTMCMC: Uniform only. */
+  const int *prior_kind;
 } kg_tmcmc_cfg;
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);

@@ -171,30 +171,47 @@ __global__ void __launch_bounds__(256) k_tm_draw(int N, int c_lo, int P, const d
 
 // generation 1: candidate d of chain c from its prior's generator
 // (TMCMC.cpp.base:216-221, Uniform::getRandomNumber = gsl_ran_flat,
-// univariate/uniform/uniform.cpp.base:30-36): a*(1-u) + b*u.
+// univariate/uniform/uniform.cpp.base:30-36): a*(1-u) + b*u.  Variables with
+// a Normal prior (vkind 1) take the host's sequential draw nrm (tm_normal_priors).
 __global__ void k_tm_prior(int N, int P, const double *__restrict__ U, const unsigned long long *__restrict__ uoff,
                            const int *__restrict__ ustride, const double *__restrict__ pmin,
-                           const double *__restrict__ pmax, double *__restrict__ cand) {
+                           const double *__restrict__ pmax, const int *__restrict__ vkind,
+                           const double *__restrict__ nrm, double *__restrict__ cand) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)P * N) return;
   const int c = (int)(e / N), d = (int)(e % N);
+  if (vkind[d]) {
+    cand[e] = nrm[e];
+    return;
+  }
   const double u = U[uoff[d] + (size_t)c * ustride[d]];
   cand[e] = pmin[d] * (1 - u) + pmax[d] * u;
 }
 
-// Bayesian::evaluate (bayesian.cpp.base:24-84): logPrior = sum of uniform
-// log-densities (-log(b-a) inside, -inf outside; uniform.cpp.base:38-44);
+// Bayesian::evaluate (bayesian.cpp.base:24-84): logPrior = sum of the
+// variables' prior log-densities in variable order — Uniform: -log(b-a)
+// inside, -inf outside (uniform.cpp.base:38-44); Normal: logNormalization -
+// 0.5 d d, d = (x - mean) / sd (normal.cpp.base:17-21; pmin / pmax hold mean
+// and sd);
 // -inf prior -> loglik -inf without evaluating the model; otherwise the
 // builtin Gaussian loglik -0.5*sum x^2 (samplers/mean/model/model.py:32-37).
 __global__ void k_tm_evaluate(int N, int P, int lik, const double *__restrict__ cand,
                               const double *__restrict__ negLogWidth, const double *__restrict__ pmin,
-                              const double *__restrict__ pmax, double *__restrict__ candLL,
-                              double *__restrict__ candLP, const unsigned char *__restrict__ pend) {
+                              const double *__restrict__ pmax, const int *__restrict__ vkind,
+                              double *__restrict__ candLL, double *__restrict__ candLP,
+                              const unsigned char *__restrict__ pend) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P || !pend[c]) return;
   const double *x = cand + (size_t)c * N;
   double lp = 0.0;
-  for (int d = 0; d < N; d++) lp += (x[d] >= pmin[d] && x[d] <= pmax[d]) ? negLogWidth[d] : -INFINITY;
+  for (int d = 0; d < N; d++) {
+    if (vkind[d]) {
+      const double z = (x[d] - pmin[d]) / pmax[d];
+      lp += negLogWidth[d] - 0.5 * z * z;
+    } else {
+      lp += (x[d] >= pmin[d] && x[d] <= pmax[d]) ? negLogWidth[d] : -INFINITY;
+    }
+  }
   candLP[c] = lp;
   double ll = -INFINITY;
   if (!(isinf(lp) && lp < 0)) {
@@ -223,10 +240,13 @@ __global__ void k_tm_pend_init(int P, int lo, int hi, unsigned char *__restrict_
   if (c < P) pend[c] = (c >= lo && c < hi) ? 1 : 0;
 }
 
+// each variable's log-density constant: Uniform -log(b - a); Normal
+// _logNormalization = -0.5 log(2 pi) - log(sd) (normal.cpp.base:40-46)
 __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const double *__restrict__ pmax,
-                                 double *__restrict__ out) {
+                                 const int *__restrict__ vkind, double *__restrict__ out) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d < N) out[d] = -log_cr(pmax[d] - pmin[d]);
+  if (d >= N) return;
+  out[d] = vkind[d] ? -0.5 * log_cr(2 * 3.14159265358979323846) - log_cr(pmax[d]) : -log_cr(pmax[d] - pmin[d]);
 }
 
 // processCandidate + calculateAcceptanceProbability + updateDatabase
@@ -1892,6 +1912,9 @@ struct kg_tmcmc_s {
   std::vector<double> mnScratch;
   double *fA = nullptr, *fB = nullptr;  // term factors of the ordered sums (P x N + 2, or N x wr_pitch(P))    // upper-triangle (i, j), j >= i, row-major
   int *ustride = nullptr;
+  int *vkind = nullptr;         // per variable: 0 Uniform prior, 1 Normal (pmin / pmax = mean / sd)
+  double *priorNrm = nullptr;   // generation 1: the Normal priors' draws (P x N, host-made)
+  std::vector<int> hkind;
   unsigned *src = nullptr;
   unsigned char *acc = nullptr, *pend = nullptr;
   TmDev *dev = nullptr;
@@ -1943,6 +1966,7 @@ struct kg_tmcmc_s {
   std::vector<int> distOf;           // variable -> distribution
   std::vector<size_t> distVars;      // variables per distribution
   std::vector<size_t> distOffset;    // offset of the distribution's draws in Uprior
+  std::vector<int> distKind;         // 0 Uniform, 1 Normal
   // RNGs
   HostMt multinomialRng;
   MtStream multivariate, uniform;
@@ -2668,6 +2692,13 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     KG_CHECK(cfg->domain_extension_factor >= 0.0, "Domain Extension Factor lower than 0.0");
     KG_CHECK(cfg->shard_count <= 1, "mTMCMC runs unsharded");
     KG_CHECK(cfg->variable_count <= 128, "mTMCMC: at most 128 variables");
+    for (size_t d = 0; cfg->prior_kind && d < cfg->variable_count; d++)  // TMCMC.cpp.base:76-77
+      KG_CHECK(cfg->prior_kind[d] == 0, "Only 'Univariate/Uniform' priors allowed (mTMCMC)");
+  }
+  for (size_t d = 0; cfg->prior_kind && d < cfg->variable_count; d++) {
+    KG_CHECK(cfg->prior_kind[d] == 0 || cfg->prior_kind[d] == 1, "prior_kind entries must be 0 (Uniform) or 1 (Normal)");
+    KG_CHECK(cfg->prior_kind[d] == 0 || cfg->prior_max[d] > 0.0,  // normal.cpp.base:38
+             "Incorrect Standard Deviation parameter of Normal distribution");
   }
   KG_HIP(hipSetDevice(cfg->device));
   upload_dd_tables();
@@ -2700,6 +2731,18 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   if (nd == 0) nd = N;
   h->ndist = nd;
   h->distVars.assign(nd, 0);
+  h->distKind.assign(nd, -1);
+  h->hkind.assign(N, 0);
+  for (int d = 0; d < N; d++) {
+    const int k = cfg->prior_kind ? cfg->prior_kind[d] : 0;
+    h->hkind[d] = k;
+    if (h->distKind[h->distOf[d]] >= 0 && h->distKind[h->distOf[d]] != k) {
+      delete h;
+      KG_CHECK(false, "variables sharing a prior distribution must share its kind");
+    }
+    h->distKind[h->distOf[d]] = k;
+  }
+  for (int &k : h->distKind) k = std::max(k, 0);
   std::vector<unsigned long long> uoff(N);
   std::vector<int> ustride(N);
   std::vector<size_t> rank(N);
@@ -2724,6 +2767,12 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   h->capU = P;
   rc |= tdalloc(&h->Uprior, PN) | tdalloc(&h->E, (size_t)(CV_MAX_PTS + 1) * P) | tdalloc(&h->w, P);
   rc |= tdalloc(&h->uoff, N) | tdalloc(&h->ustride, N) | tdalloc(&h->src, P) | tdalloc(&h->acc, P);
+  rc |= tdalloc(&h->vkind, N);
+  for (int k : h->hkind)
+    if (k) {
+      rc |= tdalloc(&h->priorNrm, PN);
+      break;
+    }
   rc |= tdalloc(&h->pend, P) | tdalloc(&h->sch, P) | tdalloc(&h->dLen, P);
   h->xchWords = 3 * (PN + 2 * (size_t)P) + h->world;
   if (cfg->shard_count >= 1) rc |= tdalloc(&h->xch, h->xchWords);  // explicitly sharded (even one rank)
@@ -2773,6 +2822,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   KG_HIP(hipMemcpy(h->pmax, cfg->prior_max, N * sizeof(double), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->uoff, uoff.data(), N * sizeof(unsigned long long), hipMemcpyHostToDevice));
   KG_HIP(hipMemcpy(h->ustride, ustride.data(), N * sizeof(int), hipMemcpyHostToDevice));
+  KG_HIP(hipMemcpy(h->vkind, h->hkind.data(), N * sizeof(int), hipMemcpyHostToDevice));
   {
     std::vector<int2> pr;
     for (int i = 0; i < N; i++)
@@ -2790,7 +2840,8 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
     }
 
   }
-  hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(N, 64)), dim3(64), 0, h->stream, N, h->pmin, h->pmax, h->negLogWidth);
+  hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(N, 64)), dim3(64), 0, h->stream, N, h->pmin, h->pmax, h->vkind,
+                     h->negLogWidth);
   KG_HIP(hipGetLastError());
   // per generation: P x N normals for prepareGeneration and up to
   // P (1 + burn-in) x N for the chains' later steps; one Uniform per step
@@ -2809,7 +2860,7 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   h->priorRng.resize(nd);
   for (int k = 0; k < nd; k++) {
     h->priorRng[k] = new MtStream();
-    if (h->priorRng[k]->init(2 * h->distVars[k] * (size_t)P + 4096)) return 1;
+    if (h->priorRng[k]->init((h->distKind[k] ? 1 : 2 * h->distVars[k] * (size_t)P) + 4096)) return 1;
     seed_state(cfg->prior_seeds ? cfg->prior_seeds[k] : 0, st);
     if (h->priorRng[k]->import_gsl(st, h->stream)) return 1;
   }
@@ -2856,7 +2907,7 @@ int kg_tmcmc_destroy(kg_tmcmc_t h) {
                   (void *)h->pmax, (void *)h->negLogWidth, (void *)h->Z, (void *)h->U, (void *)h->Uprior,
                   (void *)h->E, (void *)h->w, (void *)h->uoff, (void *)h->ustride, (void *)h->src, (void *)h->acc,
                   (void *)h->dev, h->cvPart, (void *)h->pairs, (void *)h->pend, (void *)h->sch, (void *)h->Zx,
-                  (void *)h->dLen, (void *)h->xch,
+                  (void *)h->dLen, (void *)h->xch, (void *)h->vkind, (void *)h->priorNrm,
                   (void *)h->fA, (void *)h->fB, (void *)h->dNm, (void *)h->nmSync, (void *)h->mtExtraDev,
                   (void *)h->mtModeDev})
     if (p) dev_release(p);
@@ -2932,6 +2983,49 @@ static int tm_mt_candidates(kg_tmcmc_s *h) {
   return 0;
 }
 
+// generation 1, Normal priors (Normal::getRandomNumber = mean +
+// gsl_ran_gaussian(sd), normal.cpp.base:30-33): the Marsaglia polar
+// rejection makes each draw's word count data-dependent, and a distribution
+// shared by several variables interleaves them sample-major
+// (TMCMC.cpp.base:215-221), so the P x (its variables) draws run on the host
+// from the distribution's exported generator, which then continues from
+// where they left it.  Once per run.
+static int tm_normal_priors(kg_tmcmc_t h) {
+  const int N = h->N, P = h->P;
+  std::vector<double> mean(N), sd(N), out((size_t)P * N, 0.0);
+  KG_HIP(hipMemcpyAsync(mean.data(), h->pmin, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipMemcpyAsync(sd.data(), h->pmax, N * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  unsigned char st[5000];
+  for (int k = 0; k < h->ndist; k++) {
+    if (!h->distKind[k] || !h->distVars[k]) continue;
+    HostMt g;
+    if (h->priorRng[k]->export_gsl(st, h->stream) || g.load(st)) return 1;
+    auto upos = [&]() {
+      double u;
+      do u = g.uniform();
+      while (u == 0.0);
+      return u;
+    };
+    for (int i = 0; i < P; i++)
+      for (int d = 0; d < N; d++) {
+        if (h->distOf[d] != k) continue;
+        double x, y, r2;
+        do {
+          x = -1 + 2 * upos();
+          y = -1 + 2 * upos();
+          r2 = x * x + y * y;
+        } while (r2 > 1.0 || r2 == 0);
+        out[(size_t)i * N + d] = mean[d] + sd[d] * y * std::sqrt(-2.0 * host_log_cr(r2) / r2);
+      }
+    g.save(st);
+    if (h->priorRng[k]->import_gsl(st, h->stream)) return 1;
+  }
+  KG_HIP(hipMemcpyAsync(h->priorNrm, out.data(), out.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   const int N = h->N, P = h->P;
   const size_t PN = (size_t)P * N;
@@ -2974,11 +3068,13 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
   }
   if (generation == 1) {
     TmStage st(h, "prior_draw");
+    if (h->priorNrm && tm_normal_priors(h)) return 1;
     for (int k = 0; k < h->ndist; k++)
-      if (h->distVars[k] && h->priorRng[k]->uniforms(h->Uprior + h->distOffset[k], h->distVars[k] * (size_t)P, h->stream))
+      if (h->distVars[k] && !h->distKind[k] &&
+          h->priorRng[k]->uniforms(h->Uprior + h->distOffset[k], h->distVars[k] * (size_t)P, h->stream))
         return 1;
     hipLaunchKernelGGL(k_tm_prior, dim3(nblk(PN, 256)), dim3(256), 0, h->stream, N, P, h->Uprior, h->uoff, h->ustride,
-                       h->pmin, h->pmax, h->cand);
+                       h->pmin, h->pmax, h->vkind, h->priorNrm, h->cand);
     KG_HIP(hipGetLastError());
   } else if (h->mt) {
     if (tm_mt_candidates(h)) return 1;
@@ -3017,7 +3113,7 @@ int kg_tmcmc_prepare(kg_tmcmc_t h, size_t generation) {
 int kg_tmcmc_evaluate(kg_tmcmc_t h) {
   TmStage st(h, "evaluate");
   hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, h->cfg.likelihood,
-                     h->cand, h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP, h->pend);
+                     h->cand, h->negLogWidth, h->pmin, h->pmax, h->vkind, h->candLL, h->candLP, h->pend);
   KG_HIP(hipGetLastError());
   return 0;
 }
@@ -3025,7 +3121,7 @@ int kg_tmcmc_evaluate(kg_tmcmc_t h) {
 int kg_tmcmc_evaluate_prior(kg_tmcmc_t h) {
   TmStage st(h, "evaluate");
   hipLaunchKernelGGL(k_tm_evaluate, dim3(nblk(h->P, 128)), dim3(128), 0, h->stream, h->N, h->P, -1, h->cand,
-                     h->negLogWidth, h->pmin, h->pmax, h->candLL, h->candLP, h->pend);
+                     h->negLogWidth, h->pmin, h->pmax, h->vkind, h->candLL, h->candLP, h->pend);
   KG_HIP(hipGetLastError());
   KG_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -3487,7 +3583,7 @@ int kg_tmcmc_set_field(kg_tmcmc_t h, const char *name, const double *in, size_t 
       h->hLen[c] = (unsigned)in[c];
     }
   if (r.dev == h->pmin || r.dev == h->pmax) {
-    hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(h->N, 64)), dim3(64), 0, h->stream, h->N, h->pmin, h->pmax,
+    hipLaunchKernelGGL(k_tm_neglogwidth, dim3(nblk(h->N, 64)), dim3(64), 0, h->stream, h->N, h->pmin, h->pmax, h->vkind,
                        h->negLogWidth);
     KG_HIP(hipGetLastError());
   }

@@ -1153,6 +1153,11 @@ struct TmcmcModule : SolverModule {
   // exchange is one MAX all-reduce between kg_tmcmc_process_partial and
   // _finalize (include/korali_amd.h)
   Collective *dist = nullptr;
+  // Distributed mTMCMC: the handle runs replicated (the gradient / Fisher
+  // proposals are per chain but the handle's proposal stage is unsharded),
+  // each round's likelihood evaluations are split over the ranks and their
+  // values, gradients and Fisher matrices all-gathered
+  bool replicated = false;
 
   ~TmcmcModule() override {
     if (h) kg_tmcmc_destroy(h);
@@ -1175,8 +1180,7 @@ struct TmcmcModule : SolverModule {
       fail("Unrecognized value (%s) provided for mandatory setting: ['Version'] required by TMCMC.\n",
            sv["Version"].getString().c_str());
     mtmcmc = version == "mtmcmc";
-    if (mtmcmc && dist)
-      fail("mTMCMC runs unsharded: use the Sequential or Concurrent conduit.");
+    replicated = mtmcmc && dist;
     // TMCMC.cpp.base:48-55
     if (mtmcmc && !reference) fail("mTMCMC works only for problems of type 'Bayesian/Reference'\n");
     std::vector<VariableSpec> vars = readVariables(js);
@@ -1196,11 +1200,12 @@ struct TmcmcModule : SolverModule {
     maxModelEvaluations = num(tc, "Max Model Evaluations", 1e9);
     targetExponent = num(tc, "Target Annealing Exponent", 1.0);
 
-    // priors: each variable's Univariate/Uniform distribution
+    // priors: each variable's Univariate/Uniform or Univariate/Normal
+    // distribution (Bayesian::evaluateLogPrior, bayesian.cpp.base:24-32)
     Json &ds = js["Distributions"];
     ndist = ds.size();
     std::vector<double> pmin(N), pmax(N);
-    std::vector<int> pdist(N);
+    std::vector<int> pdist(N), pkind(N, 0);
     for (size_t i = 0; i < N; i++) {
       Json &v = js["Variables"][i];
       if (!v.contains("Prior Distribution")) fail("Variable '%s' has no 'Prior Distribution'.", vars[i].name.c_str());
@@ -1209,12 +1214,22 @@ struct TmcmcModule : SolverModule {
       for (size_t d = 0; d < ndist; d++)
         if (ds[d].contains("Name") && ds[d]["Name"].getString() == pn) k = (int)d;
       if (k < 0) fail("Did not find a distribution named '%s'.", pn.c_str());
-      if (canon(ds[k]["Type"].getString()) != "univariate/uniform") {
-        if (mtmcmc) fail("Only 'Univariate/Uniform' priors allowed (is %s).\n", ds[k]["Type"].getString().c_str());
-        fail("The device TMCMC path supports 'Univariate/Uniform' priors (distribution '%s').", pn.c_str());
+      const std::string dt = canon(ds[k]["Type"].getString());
+      if (dt != "univariate/uniform" && mtmcmc)
+        fail("Only 'Univariate/Uniform' priors allowed (is %s).\n", ds[k]["Type"].getString().c_str());
+      if (dt == "univariate/uniform") {
+        pmin[i] = mandatory(ds[k], "Minimum", "Distributions");
+        pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
+      } else if (dt == "univariate/normal") {
+        pkind[i] = 1;
+        pmin[i] = mandatory(ds[k], "Mean", "Distributions");
+        pmax[i] = mandatory(ds[k], "Standard Deviation", "Distributions");
+        if (!(pmax[i] > 0.0))  // normal.cpp.base:38
+          fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", pmax[i]);
+      } else {
+        fail("The device TMCMC path supports 'Univariate/Uniform' and 'Univariate/Normal' priors (distribution '%s').",
+             pn.c_str());
       }
-      pmin[i] = mandatory(ds[k], "Minimum", "Distributions");
-      pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
       pdist[i] = k;
     }
     if (reference) {
@@ -1258,6 +1273,7 @@ struct TmcmcModule : SolverModule {
     c.prior_min = pmin.data();
     c.prior_max = pmax.data();
     c.prior_distribution = pdist.data();
+    c.prior_kind = pkind.data();
     c.distribution_count = ndist;
     c.prior_seeds = distSeeds.data();
     c.multinomial_seed = seeds.assign(gm);
@@ -1265,8 +1281,8 @@ struct TmcmcModule : SolverModule {
     c.uniform_seed = seeds.assign(gu);
     c.likelihood = KG_LIK_GAUSSIAN;
     c.device = solverDevice(js, dist);
-    c.shard_rank = dist ? dist->rank : 0;
-    c.shard_count = dist ? dist->world : 0;
+    c.shard_rank = dist && !replicated ? dist->rank : 0;
+    c.shard_count = dist && !replicated ? dist->world : 0;
     c.version = mtmcmc ? 1 : 0;
     c.step_size = num(sv, "Step Size", 0.1);
     c.domain_extension_factor = num(sv, "Domain Extension Factor", 0.2);
@@ -1350,7 +1366,7 @@ struct TmcmcModule : SolverModule {
           LL[i] = -INFINITY;
           if (pend[i] && !(std::isinf(LP[i]) && LP[i] < 0)) todo.push_back(i);
         }
-        conduit->evaluateBatch(todo.size(), [&](size_t k) {
+        auto evaluate = [&](size_t k) {
           const size_t i = todo[k];
           Sample s;
           s["Module"] = "Problem";
@@ -1373,13 +1389,43 @@ struct TmcmcModule : SolverModule {
             std::copy(g.begin(), g.end(), G.begin() + i * N);
             std::copy(F.begin(), F.end(), FIM.begin() + i * N * N);
           }
-        });
+        };
+        if (replicated) {
+          // this rank's block of the round's evaluations; rows of (logLikelihood,
+          // gradient, Fisher information) all-gathered over the bootstrap
+          const size_t W = dist->world, per = (todo.size() + W - 1) / W,
+                       a = std::min(todo.size(), per * dist->rank), b = std::min(todo.size(), a + per),
+                       gw = grads ? N + N * N : 0;
+          for (size_t k = a; k < b; k++) evaluate(k);
+          std::vector<double> buf(W * per * (1 + gw), 0.0);
+          for (size_t k = a; k < b; k++) {
+            const size_t i = todo[k];
+            double *row = buf.data() + (dist->rank * per + (k - a)) * (1 + gw);
+            row[0] = LL[i];
+            if (grads) {
+              std::copy(G.begin() + i * N, G.begin() + (i + 1) * N, row + 1);
+              std::copy(FIM.begin() + i * N * N, FIM.begin() + (i + 1) * N * N, row + 1 + N);
+            }
+          }
+          if (per) dist->allGatherHost(buf.data(), per * (1 + gw));
+          for (size_t k = 0; k < todo.size(); k++) {
+            const size_t i = todo[k];
+            const double *row = buf.data() + k * (1 + gw);
+            LL[i] = row[0];
+            if (grads) {
+              std::copy(row + 1, row + 1 + N, G.begin() + i * N);
+              std::copy(row + 1 + N, row + 1 + N + N * N, FIM.begin() + i * N * N);
+            }
+          }
+        } else {
+          conduit->evaluateBatch(todo.size(), evaluate);
+        }
         check(kg_tmcmc_set_evaluations(h, LP.data(), LL.data()));
         if (grads) check(kg_tmcmc_set_gradients(h, G.data(), FIM.data()));
         check(kg_tmcmc_advance(h, gen, &pending));
       }
     }
-    if (dist) {
+    if (dist && !replicated) {
       check(kg_tmcmc_process_partial(h, gen));
       size_t n = 0;
       check(kg_tmcmc_field_size(h, "Shard Exchange", &n));

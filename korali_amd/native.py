@@ -63,6 +63,7 @@ class _TmcmcCfg(C.Structure):
         ("device", C.c_int), ("per_generation_burn_in", C.POINTER(C.c_double)),
         ("per_generation_burn_in_count", C.c_size_t), ("shard_rank", C.c_int), ("shard_count", C.c_int),
         ("version", C.c_int), ("step_size", C.c_double), ("domain_extension_factor", C.c_double),
+        ("prior_kind", C.POINTER(C.c_int)),
     ]
 
 
@@ -403,7 +404,8 @@ class CmaesDevice:
 class TmcmcDevice:
     """One TMCMC sampler instance (Version "TMCMC") on one MI355X (kg_tmcmc_t).
 
-    prior_min / prior_max: the Univariate/Uniform prior of every variable;
+    prior_min / prior_max: the Univariate/Uniform prior of every variable
+    (prior_kind[d] = 1: the Univariate/Normal prior's Mean / Standard Deviation);
     prior_distribution[d]: index of the distribution object variable d draws
     from (variables sharing a distribution share its generator); prior_seeds[k]:
     seed of distribution k.  Generator indices for get_rng / set_rng:
@@ -413,7 +415,7 @@ class TmcmcDevice:
                  multinomial_seed=0, multivariate_seed=0, uniform_seed=0, target_cov=1.0, covariance_scaling=0.04,
                  min_annealing_exponent_update=1e-5, max_annealing_exponent_update=1.0, max_chain_length=1,
                  default_burn_in=0, per_generation_burn_in=(), likelihood=0, device=0, shard_rank=0, shard_count=0,
-                 version=0, step_size=0.1, domain_extension_factor=0.2):
+                 version=0, step_size=0.1, domain_extension_factor=0.2, prior_kind=None):
         L = lib()
         self.N, self.P = int(N), int(P)
         pdist = (np.arange(self.N, dtype=np.int32) if prior_distribution is None
@@ -422,7 +424,8 @@ class TmcmcDevice:
         seeds = np.zeros(ndist, dtype=np.uint64) if prior_seeds is None else np.ascontiguousarray(
             np.broadcast_to(np.asarray(prior_seeds, dtype=np.uint64), (ndist,)))
         pgb = np.ascontiguousarray(per_generation_burn_in, dtype=np.float64).reshape(-1)
-        self._arrays = [_vec(prior_min, self.N, 0.0), _vec(prior_max, self.N, 1.0), pdist, seeds, pgb]
+        pkind = None if prior_kind is None else np.ascontiguousarray(prior_kind, dtype=np.int32)
+        self._arrays = [_vec(prior_min, self.N, 0.0), _vec(prior_max, self.N, 1.0), pdist, seeds, pgb, pkind]
         cfg = _TmcmcCfg()
         cfg.variable_count, cfg.population_size = self.N, self.P
         cfg.max_chain_length, cfg.default_burn_in = float(max_chain_length), float(default_burn_in)
@@ -441,6 +444,7 @@ class TmcmcDevice:
         cfg.shard_rank, cfg.shard_count = int(shard_rank), int(shard_count)
         cfg.version = 1 if version in (1, "mTMCMC") else 0
         cfg.step_size, cfg.domain_extension_factor = float(step_size), float(domain_extension_factor)
+        cfg.prior_kind = None if pkind is None else pkind.ctypes.data_as(C.POINTER(C.c_int))
         h = C.c_void_p()
         check(L.kg_tmcmc_create(C.byref(cfg), C.byref(h)))
         self.h = h

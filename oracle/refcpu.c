@@ -2257,6 +2257,7 @@ struct kr_tmcmc
   double *priorMin, *priorMax;
   kr_rng *priorRng;
   int *priorMap; /* variable -> prior distribution (shared distributions share an RNG) */
+  int *priorKind; /* per variable: 0 Uniform [priorMin, priorMax], 1 Normal (priorMin = mean, priorMax = sd) */
   /* state */
   double *leaders, *leadersLL, *leadersLP, *candidates, *candidatesLL, *candidatesLP;
   double *chainLengths, *meanTheta, *cov, *chol;
@@ -2306,6 +2307,7 @@ kr_tmcmc *kr_tmcmc_new(size_t N, size_t P)
 #undef AL
   h->priorRng = (kr_rng *)calloc(N, sizeof(kr_rng));
   h->priorMap = (int *)calloc(N, sizeof(int));
+  h->priorKind = (int *)calloc(N, sizeof(int));
   for (i = 0; i < N; i++)
   {
     h->priorMap[i] = (int)i;
@@ -2326,6 +2328,7 @@ void kr_tmcmc_free(kr_tmcmc *h)
   free(h->priorMax);
   free(h->priorRng);
   free(h->priorMap);
+  free(h->priorKind);
   free(h->leaders);
   free(h->leadersLL);
   free(h->leadersLP);
@@ -2429,6 +2432,15 @@ void kr_tmcmc_set_prior_map(kr_tmcmc *h, const int *map)
 {
   size_t d;
   for (d = 0; d < h->N; d++) h->priorMap[d] = map[d];
+}
+
+/* the variables' prior kinds: 0 Univariate/Uniform, 1 Univariate/Normal
+ * (univariate/normal/normal.cpp.base: Mean / Standard Deviation in
+ * Prior Minimum / Prior Maximum) */
+void kr_tmcmc_set_prior_kinds(kr_tmcmc *h, const int *kinds)
+{
+  size_t d;
+  for (d = 0; d < h->N; d++) h->priorKind[d] = kinds[d];
 }
 
 void kr_tmcmc_set_option(kr_tmcmc *h, const char *name, double v)
@@ -2834,7 +2846,11 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
   {
     if (gen == 1)
     {
-      for (d = 0; d < N; d++) h->candidates[i * N + d] = kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
+      /* TMCMC.cpp.base:218-220: getRandomNumber of each variable's
+       * distribution; Normal: mean + gsl_ran_gaussian(sd) (normal.cpp.base:30-33) */
+      for (d = 0; d < N; d++)
+        h->candidates[i * N + d] = h->priorKind[d] ? h->priorMin[d] + kr_ran_gaussian(&h->priorRng[h->priorMap[d]], h->priorMax[d])
+                                                   : kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
     }
     else if (h->LE)
       mt_generate_candidate(h, i);
@@ -2854,6 +2870,13 @@ static void tm_evaluate_one(kr_tmcmc *h, size_t i)
   double lp = 0.0;
   for (d = 0; d < N; d++)
   {
+    if (h->priorKind[d])
+    { /* normal.cpp.base:17-21, :40-46 */
+      const double logNorm = -0.5 * kr_log_cr(2 * 3.14159265358979323846) - kr_log_cr(h->priorMax[d]);
+      const double z = (x[d] - h->priorMin[d]) / h->priorMax[d];
+      lp += logNorm - 0.5 * z * z;
+      continue;
+    }
     const double aux = -kr_log_cr(h->priorMax[d] - h->priorMin[d]);
     lp += (x[d] >= h->priorMin[d] && x[d] <= h->priorMax[d]) ? aux : -INFINITY;
   }

@@ -86,6 +86,7 @@ def lib(variant="cr"):
         L.kr_tmcmc_rng.restype = vp
         L.kr_tmcmc_set_option.argtypes = [vp, cp, C.c_double]
         L.kr_tmcmc_set_prior_map.argtypes = [vp, C.POINTER(C.c_int)]
+        L.kr_tmcmc_set_prior_kinds.argtypes = [vp, C.POINTER(C.c_int)]
         L.kr_tmcmc_set_per_generation_burn_in.argtypes = [vp, dp, sz]
         L.kr_tmcmc_initialize.argtypes = [vp]
         L.kr_tmcmc_prepare.argtypes = [vp, sz]
@@ -291,6 +292,10 @@ class TMCMC:
     def set_prior_map(self, dist_of_var):
         m = (C.c_int * self.N)(*[int(v) for v in dist_of_var])
         self.L.kr_tmcmc_set_prior_map(self.h, m)
+
+    def set_prior_kinds(self, kinds):  # 0 Uniform, 1 Normal (Prior Minimum / Maximum = Mean / sd)
+        m = (C.c_int * self.N)(*[int(v) for v in kinds])
+        self.L.kr_tmcmc_set_prior_kinds(self.h, m)
 
     def set_per_generation_burn_in(self, values):
         v = np.ascontiguousarray(values, dtype=np.float64)

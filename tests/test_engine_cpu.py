@@ -94,18 +94,26 @@ def test_type_strings_ignore_case_and_whitespace():
         korali.Engine().run(e)
 
 
-def test_tmcmc_prior_validation():
+@pytest.mark.parametrize("dist,params,msg", [
+    ("Univariate/Cauchy", {"Location": 0.0, "Scale": 1.0}, "'Univariate/Uniform' and 'Univariate/Normal' priors"),
+    ("Univariate/Normal", {"Mean": 0.0, "Standard Deviation": -1.0}, "Incorrect Standard Deviation"),
+    ("Univariate/Normal", {"Standard Deviation": 1.0}, "Mean")])
+def test_tmcmc_prior_validation(dist, params, msg):
+    """The device TMCMC path's priors: Uniform and Normal (normal.cpp.base:38
+    rejects sd <= 0); others fail loudly before the device is touched."""
     e = korali.Experiment()
     e["Problem"]["Type"] = "Bayesian/Custom"
     e["Problem"]["Likelihood Model"] = lambda s: None
     e["Distributions"][0]["Name"] = "N 0"
-    e["Distributions"][0]["Type"] = "Univariate/Normal"
+    e["Distributions"][0]["Type"] = dist
+    for k, v in params.items():
+        e["Distributions"][0][k] = v
     e["Variables"][0]["Name"] = "a"
     e["Variables"][0]["Prior Distribution"] = "N 0"
     e["Solver"]["Type"] = "Sampler/TMCMC"
     e["Solver"]["Population Size"] = 100
     e["File Output"]["Enabled"] = False
-    with pytest.raises(korali.KoraliError, match="Univariate/Uniform"):
+    with pytest.raises(korali.KoraliError, match=msg):
         korali.Engine().run(e)
 
 

@@ -14,7 +14,8 @@ mean / covariance / sigma within the partial-sum tolerance
 (include/korali_amd.h: shard sums in another order).  Use Gradient
 Information runs sharded too: each rank evaluates its rows' gradients, the
 engine all-gathers them.  CCMA-ES (Problem "Constraints") runs replicated, its
-objective and constraint callbacks split over the ranks: bit-identical."""
+objective and constraint callbacks split over the ranks: bit-identical; so
+does mTMCMC, its likelihood / gradient / Fisher evaluations split."""
 import json
 import os
 import socket
@@ -55,10 +56,11 @@ def close(a, b, rtol):
     (2, "cmaes", "builtin", "Host", "MFMA"), (1, "cmaes", "builtin", "RCCL", "MFMA"),
     (2, "cmaes", "grad", "Host", "Exact"), (2, "cmaes", "grad", "Host", "MFMA"),
     (3, "cmaes", "ccmaes", "Host", "Exact"), (1, "cmaes", "ccmaes", "RCCL", "Exact"),
-    (2, "tmcmc", "builtin", "Host", "-"), (3, "tmcmc", "host", "Host", "-"), (1, "tmcmc", "builtin", "RCCL", "-")])
+    (2, "tmcmc", "builtin", "Host", "-"), (3, "tmcmc", "host", "Host", "-"), (1, "tmcmc", "builtin", "RCCL", "-"),
+    (3, "tmcmc", "mtmcmc", "Host", "-")])
 def test_distributed_conduit(tmp_path, ranks, solver, model, transport, cov):
     res = launch(tmp_path, ranks, solver, model, transport, cov)
-    for gens in (("1", "4") if model == "c4" else ("1", "6")):
+    for gens in {"c4": ("1", "4"), "mtmcmc": ("1", "3")}.get(model, ("1", "6")):
         for r in res[1:]:
             assert r[gens]["sharded"] == res[0][gens]["sharded"], gens  # replicated: bit-identical on every rank
         s, u = res[0][gens]["sharded"], res[0][gens]["unsharded"]

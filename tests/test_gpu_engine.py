@@ -255,6 +255,33 @@ def test_objective_kernel_equals_callback():
     assert runs[0] == runs[1]
 
 
+def test_tmcmc_normal_prior_through_the_api():
+    """A Univariate/Normal prior through korali.Engine (Bayesian/Custom with
+    a host likelihood): N(0.5, 2^2) prior x exp(-x^2/2) likelihood is the
+    N(0.1, 0.8) posterior; LogEvidence is its closed form
+    log N(0; 0.5, 1 + 4) + 0.5 log(2 pi) within the sampler's noise."""
+    import korali
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lambda s: s.__setitem__("logLikelihood", -0.5 * s["Parameters"][0] ** 2)
+    e["Distributions"][0]["Name"] = "N"
+    e["Distributions"][0]["Type"] = "Univariate/Normal"
+    e["Distributions"][0]["Mean"] = 0.5
+    e["Distributions"][0]["Standard Deviation"] = 2.0
+    e["Variables"][0]["Name"] = "x"
+    e["Variables"][0]["Prior Distribution"] = "N"
+    e["Solver"]["Type"] = "Sampler/TMCMC"
+    e["Solver"]["Population Size"] = 5000
+    e["Random Seed"] = 99
+    e["Console Output"]["Verbosity"] = "Silent"
+    e["File Output"]["Enabled"] = False
+    korali.Engine().run(e)
+    x = np.asarray(e["Solver"]["Sample Database"], dtype=float)
+    assert abs(x.mean() - 0.1) < 0.05 and abs(x.var() - 0.8) < 0.08, (x.mean(), x.var())
+    logz = -0.5 * np.log(2 * np.pi * 5.0) - 0.5 * 0.25 / 5.0 + 0.5 * np.log(2 * np.pi)
+    assert abs(e["Solver"]["LogEvidence"] - logz) < 0.05, (e["Solver"]["LogEvidence"], logz)
+
+
 def test_tmcmc_likelihood_kernel_equals_callback():
     import korali
 

@@ -126,6 +126,52 @@ def test_tmcmc_seeded_run_matches_oracle(N, P, gens, shared):
         assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
 
 
+@pytest.mark.parametrize("mcl,burn", [(1, 0), (3, 1)])
+def test_tmcmc_normal_priors_match_oracle(mcl, burn):
+    """Univariate/Normal priors (normal.cpp.base: mean + gsl_ran_gaussian(sd)
+    draws at generation 1, log-density logNormalization - 0.5 d^2) mixed with
+    Uniform ones, one Normal distribution shared by two variables (its draws
+    interleave sample-major): the whole run bit-exact vs the oracle, the
+    prior generators' exported states included."""
+    from korali_amd.native import TmcmcDevice
+    N, P, seed = 4, 600, 2024
+    pdist, kinds = [0, 1, 2, 2], [1, 0, 1, 1]
+    pmin, pmax = [0.5, -5.0, -1.0, -1.0], [2.0, 5.0, 0.7, 0.7]  # Normal: mean / sd; Uniform: min / max
+    seeds = [seed, seed + 1, seed + 2]
+    sm, sv, su = seed + 3, seed + 4, seed + 5
+    dev = TmcmcDevice(N, P, prior_min=pmin, prior_max=pmax, prior_seeds=seeds, prior_distribution=pdist,
+                      prior_kind=kinds, multinomial_seed=sm, multivariate_seed=sv, uniform_seed=su,
+                      max_chain_length=mcl, default_burn_in=burn)
+    o = R.TMCMC(N, P)
+    o.option("Max Chain Length", mcl)
+    o.option("Default Burn In", burn)
+    o["Prior Minimum"] = pmin
+    o["Prior Maximum"] = pmax
+    o.set_prior_map(pdist)
+    o.set_prior_kinds(kinds)
+    for k in range(3):
+        R.lib().kr_rng_seed(o.rng(3 + k).ptr, seeds[k])
+    R.lib().kr_rng_seed(o.rng(0).ptr, sm)
+    R.lib().kr_rng_seed(o.rng(1).ptr, sv)
+    R.lib().kr_rng_seed(o.rng(2).ptr, su)
+    for g in range(1, 9):
+        dev.generation(g)
+        o.generation(g)
+        dev.synchronize()
+        for key in VEC_KEYS:
+            assert np.array_equal(dev[key], o[key]), (g, key)
+        for key in SCA_KEYS:
+            a, b = dev[key][0], o[key][0]
+            assert a == b or (np.isnan(a) and np.isnan(b)), (g, key, a, b)
+        if g == 1:  # the Normal variables' draws are unbounded and centred on the mean
+            x = np.asarray(dev["Sample Database"]).reshape(-1, N)
+            assert abs(x[:, 0].mean() - 0.5) < 0.3 and abs(x[:, 2].mean() + 1.0) < 0.15
+        if o["Annealing Exponent"][0] >= 1.0:
+            break
+    for which in range(6):
+        assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
+
+
 @pytest.mark.parametrize("seed,target_cov", [(11, 0.5), (12, 2.0), (13, 1.0)])
 def test_tmcmc_interval_search_equals_exact_search(monkeypatch, seed, target_cov):
     """The annealing search decides on interval estimates and falls back to

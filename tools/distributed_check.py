@@ -8,7 +8,7 @@ the first generation's samples, fitness and sort bit-identical and mean /
 covariance / sigma within the partial-sum tolerance) and every rank's state
 against rank 0's (bit-identical).
 
-    distributed_check.py <out dir> cmaes|tmcmc builtin|host|grad|ccmaes|c4 RCCL|Host [Exact|MFMA]
+    distributed_check.py <out dir> cmaes|tmcmc builtin|host|grad|ccmaes|mtmcmc|c4 RCCL|Host [Exact|MFMA]
 
 model grad (CMA-ES only): the host Rosenbrock objective with its "Gradient",
 Use Gradient Information on (each rank evaluates its rows' gradients, the
@@ -17,6 +17,10 @@ engine all-gathers them).
 model ccmaes (CMA-ES only): run-ccmaes.py's "Mixed" CCMA-ES experiment (host
 objective, 8 constraints): the device state replicated, the objective and
 constraint callbacks split over the ranks and their values all-gathered.
+
+model mtmcmc (TMCMC only): run-mtmcmc.py's mTMCMC experiment (Bayesian/
+Reference, gradient / Fisher-information proposals): the device state
+replicated, each round's evaluations split over the ranks.
 
 model c4 (CMA-ES only): the C4 shape, 512-dim negative Ackley at
 lambda = 65536 (BASELINE.json configs[3]), after 1 and 4 generations.
@@ -67,6 +71,17 @@ CCMAES_CONSTRAINTS = [lambda x: -(x[0] - 1.0), lambda x: -(x[0] - 2.0), lambda x
                       lambda x: -math.cos(x[1]), lambda x: -math.sin(x[1])]
 
 
+REF_X, REF_Y = [1.0, 2.0, 3.0, 4.0, 5.0], [3.21, 4.14, 4.94, 6.06, 6.84]
+
+
+def model_with_gradients(s):  # run-mtmcmc.py's _model/model.py: y = a x + b, sd sig, with gradients
+    a, b, sig = s["Parameters"]
+    s["Reference Evaluations"] = [a * x + b for x in REF_X]
+    s["Standard Deviation"] = [sig] * len(REF_X)
+    s["Gradient Mean"] = [[x, 1.0, 0.0] for x in REF_X]
+    s["Gradient Standard Deviation"] = [[0.0, 0.0, 1.0] for x in REF_X]
+
+
 def gaussian(s):  # the builtin Gaussian likelihood, -0.5 * sum(x^2)
     s["logLikelihood"] = -0.5 * sum(v * v for v in s["Parameters"])
 
@@ -110,6 +125,22 @@ def experiment(solver, model, gens, cov="Exact"):
         e["Solver"]["Population Size"] = 65536 if model == "c4" else 64
         e["Solver"]["Covariance Update"] = cov
         e["Solver"]["Termination Criteria"]["Max Generations"] = gens
+    elif model == "mtmcmc":  # run-mtmcmc.py's experiment (P = 500)
+        e["Problem"]["Type"] = "Bayesian/Reference"
+        e["Problem"]["Likelihood Model"] = "Normal"
+        e["Problem"]["Reference Data"] = REF_Y
+        e["Problem"]["Computational Model"] = model_with_gradients
+        e["Distributions"][0]["Name"] = "Uniform 0"
+        e["Distributions"][0]["Type"] = "Univariate/Uniform"
+        e["Distributions"][0]["Minimum"] = 0.0
+        e["Distributions"][0]["Maximum"] = 5.0
+        for i, n in enumerate(("a", "b", "[Sigma]")):
+            e["Variables"][i]["Name"] = n
+            e["Variables"][i]["Prior Distribution"] = "Uniform 0"
+        e["Solver"]["Type"] = "Sampler/TMCMC"
+        e["Solver"]["Version"] = "mTMCMC"
+        e["Solver"]["Population Size"] = 500
+        e["Solver"]["Termination Criteria"]["Max Generations"] = gens
     else:
         e["Problem"]["Type"] = "Bayesian/Custom"
         if model == "builtin":
@@ -135,9 +166,15 @@ CCMAES_KEYS = ["Viability Boundaries", "Constraint Evaluation Count", "Is Viabil
                "Current Population Size"]
 
 
+MTMCMC_KEYS = ["Chain Leaders Errors", "Chain Leaders Covariance"]
+
+
 def state(e, solver, model):
-    keys = KEYS[solver] + (CCMAES_KEYS if model == "ccmaes" else [])
+    keys = KEYS[solver] + {"ccmaes": CCMAES_KEYS, "mtmcmc": MTMCMC_KEYS}.get(model, [])
     return {k: e["Solver"][k] for k in keys} | {"Current Generation": e["Current Generation"]}
+
+
+GENS = {"c4": (1, 4), "mtmcmc": (1, 3)}  # (mtmcmc reaches annealing exponent 1 at generation 5)
 
 
 def main():
@@ -145,7 +182,7 @@ def main():
     cov = sys.argv[5] if len(sys.argv) > 5 else "Exact"
     rank = int(os.environ["RANK"])
     result = {}
-    for gens in ((1, 4) if model == "c4" else (1, 6)):  # one generation: same samples; more: the run as a whole
+    for gens in GENS.get(model, (1, 6)):  # one generation: same samples; more: the run as a whole
         k = korali.Engine()
         k["Conduit"]["Type"] = "Distributed"
         k["Conduit"]["Transport"] = transport
