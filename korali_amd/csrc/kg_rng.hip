@@ -124,14 +124,6 @@ __device__ __forceinline__ void mt_combine_words(const uint32_t *seq, const uint
     }
   }
 }
-__device__ inline void mt_combine(const uint32_t *seq, const uint64_t *__restrict__ poly, uint32_t *out) {
-  const int t = threadIdx.x;
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  mt_combine_words(seq, poly, 0, MT_POLY_WORDS, a0, a1, a2);
-  out[t] = a0;
-  out[t + 256] = a1;
-  if (t + 512 < MT_N) out[t + 512] = a2;
-}
 
 // seq[624 .. lim) from the window seq[0..624); optionally also stored to
 // the ring at absolute positions base + k - 624 (zero words recorded)
@@ -179,19 +171,50 @@ __global__ void k_mt_plan(StreamState *st, ChunkPlan *plan, unsigned long long a
   st->hi = hi + n * W;
 }
 
+// Seed windows live in 3K slots (chunk c's in slot c mod 3K).  Workgroups
+// [0, K) produce chunks; workgroups K + q parts + r jump chunk q's start
+// window K W words ahead, part r of the polynomial's words each, XOR-ing
+// into slot (c + K) mod 3K, which the producer of chunk c - K zeroed in an
+// earlier launch (a launch holds at most K consecutive chunks, so the slots
+// read (c), written (c + K) and zeroed (c + 2K) by one launch are disjoint).
+// (One workgroup producing AND jumping made the ~10^4-term combine the
+// chunk's critical path: 214 us per C2 launch, round 5.)
 __global__ void __launch_bounds__(MT_TPB) k_mt_chunks(uint32_t *__restrict__ ring, unsigned long long R,
                                                      StreamState *st, const ChunkPlan *__restrict__ plan,
                                                      uint32_t *__restrict__ seeds, unsigned long long K,
-                                                     unsigned long long W, const uint64_t *__restrict__ jumpPoly) {
+                                                     unsigned long long W, const uint64_t *__restrict__ jumpPoly,
+                                                     int parts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t msm[];
   uint32_t *seq = msm, *roll = msm + ((MT_SEQ + 3) & ~3);
   const ChunkPlan pl = *plan;
-  if (blockIdx.x >= pl.n) return;
   const int t = threadIdx.x;
-  mt_zero_pad(msm);
+  if (blockIdx.x >= K) {
+    const unsigned long long q = (blockIdx.x - K) / parts;
+    const int part = (int)((blockIdx.x - K) % parts);
+    if (q >= pl.n) return;
+    const unsigned long long c = pl.c_first + q;
+    const int w0 = part * MT_POLY_WORDS / parts, w1 = (part + 1) * MT_POLY_WORDS / parts;
+    const uint32_t *src = seeds + (size_t)(c % (3 * K)) * MT_N;
+    mt_zero_pad(msm);
+    for (int i = t; i < MT_N; i += MT_TPB) seq[i] = src[i];
+    __syncthreads();
+    mt_fill_seq(seq, nullptr, 0, nullptr, 0, min(MT_SEQ, MT_N - 1 + 64 * w1));  // terms i < 64 w1
+    uint32_t a0 = 0, a1 = 0, a2 = 0;
+    mt_combine_words(seq, jumpPoly, w0, w1, a0, a1, a2);
+    uint32_t *out = seeds + (size_t)((c + K) % (3 * K)) * MT_N;
+    atomicXor(out + t, a0);
+    atomicXor(out + t + 256, a1);
+    if (t + 512 < MT_N) atomicXor(out + t + 512, a2);
+    return;
+  }
+  if (blockIdx.x >= pl.n) return;
   const unsigned long long c = pl.c_first + blockIdx.x;
-  const uint32_t *src = seeds + (size_t)(c % (2 * K)) * MT_N;
+  const uint32_t *src = seeds + (size_t)(c % (3 * K)) * MT_N;
   for (int i = t; i < MT_N; i += MT_TPB) seq[i] = src[i];
+  {  // chunk c - K's window: read in an earlier launch; chunk c + K's jump fills it
+    uint32_t *old = seeds + (size_t)((c + 2 * K) % (3 * K)) * MT_N;
+    for (int i = t; i < MT_N; i += MT_TPB) old[i] = 0u;
+  }
   __syncthreads();
   const unsigned long long base = c * W;
   mt_fill_seq(seq, ring, R, st, base);  // words base .. base + MT_SEQ - 625
@@ -215,8 +238,6 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_chunks(uint32_t *__restrict__ rin
     }
     __syncthreads();
   }
-  // seed chunk c + K: jump this chunk's start window by K*W words
-  mt_combine(seq, jumpPoly, seeds + (size_t)((c + K) % (2 * K)) * MT_N);
 }
 
 // initial seeds: chunk c0 + k (2^l <= k < 2^(l+1)) from chunk c0 + k - 2^l.
@@ -235,7 +256,7 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_jump_level(uint32_t *__restrict__
   const int part = (int)(blockIdx.x % MT_JUMP_PARTS);
   if (k >= K) return;
   const int w0 = part * MT_POLY_WORDS / MT_JUMP_PARTS, w1 = (part + 1) * MT_POLY_WORDS / MT_JUMP_PARTS;
-  const uint32_t *src = seeds + (size_t)((c0 + k - (1ULL << l)) % (2 * K)) * MT_N;
+  const uint32_t *src = seeds + (size_t)((c0 + k - (1ULL << l)) % (3 * K)) * MT_N;
   mt_zero_pad(msm);
   for (int i = threadIdx.x; i < MT_N; i += MT_TPB) msm[i] = src[i];
   __syncthreads();
@@ -244,7 +265,7 @@ __global__ void __launch_bounds__(MT_TPB) k_mt_jump_level(uint32_t *__restrict__
   const int t = threadIdx.x;
   uint32_t a0 = 0, a1 = 0, a2 = 0;
   mt_combine_words(msm, poly, w0, w1, a0, a1, a2);
-  uint32_t *out = seeds + (size_t)((c0 + k) % (2 * K)) * MT_N;
+  uint32_t *out = seeds + (size_t)((c0 + k) % (3 * K)) * MT_N;
   atomicXor(out + t, a0);
   atomicXor(out + t + 256, a1);
   if (t + 512 < MT_N) atomicXor(out + t + 512, a2);
@@ -485,9 +506,10 @@ int MtStream::init(size_t capacity_words, size_t parallel_min) {
     KG_CHECK(lw >= 15 && lw <= 26, "KORALI_AMD_MT_CHUNK_LOG2 must be in [15, 26]");
     W_ = 1ULL << lw;
     K_ = 256;
+    if (const char *e = getenv("KORALI_AMD_MT_CHUNK_PARTS")) parts_ = std::min(64, std::max(1, atoi(e)));  // (A/B)
     int lk = 0;
     while ((1 << lk) < K_) lk++;
-    KG_HIP(dev_alloc(&seeds_, 2 * (size_t)K_ * MT_N * sizeof(uint32_t)));
+    KG_HIP(dev_alloc(&seeds_, 3 * (size_t)K_ * MT_N * sizeof(uint32_t)));
     KG_HIP(dev_alloc(&plan_, sizeof(ChunkPlan)));
     KG_HIP(dev_alloc(&polys_, (size_t)(lk + 1) * MT_POLY_WORDS * sizeof(uint64_t)));
     std::vector<uint64_t> hp((size_t)(lk + 1) * MT_POLY_WORDS);
@@ -550,8 +572,8 @@ int MtStream::seed_chunks(unsigned long long pos, hipStream_t s) {
   KG_HIP(hipGetLastError());
   const int K = K_;
   // the levels XOR their partial jumps into zeroed windows
-  KG_HIP(hipMemsetAsync(seeds_, 0, 2 * (size_t)K * MT_N * sizeof(uint32_t), s));
-  KG_HIP(hipMemcpyAsync(seeds_ + (size_t)(1 % (2 * K)) * MT_N, ring_ + ((W_ - MT_N) & (R_ - 1)),
+  KG_HIP(hipMemsetAsync(seeds_, 0, 3 * (size_t)K * MT_N * sizeof(uint32_t), s));
+  KG_HIP(hipMemcpyAsync(seeds_ + (size_t)(1 % (3 * K)) * MT_N, ring_ + ((W_ - MT_N) & (R_ - 1)),
                         MT_N * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   for (int l = 0; (1 << l) < K; l++) {
     const int cnt = std::min(1 << l, K - (1 << l));
@@ -570,9 +592,10 @@ int MtStream::produce_chunks(unsigned long long ahead, hipStream_t s) {
   for (unsigned long long q = 0; q < launches; q++) {
     hipLaunchKernelGGL(k_mt_plan, dim3(1), dim3(1), 0, s, st_, plan_, ahead, R_, W_, (unsigned long long)K_);
     KG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_mt_chunks, dim3(K_), dim3(MT_TPB), mt_chunk_lds_bytes(), s, ring_, R_, st_,
+    const int parts = parts_;
+    hipLaunchKernelGGL(k_mt_chunks, dim3(K_ * (1 + parts)), dim3(MT_TPB), mt_chunk_lds_bytes(), s, ring_, R_, st_,
                        (const ChunkPlan *)plan_, seeds_, (unsigned long long)K_, W_,
-                       (const uint64_t *)(polys_ + (size_t)lk * MT_POLY_WORDS));
+                       (const uint64_t *)(polys_ + (size_t)lk * MT_POLY_WORDS), parts);
     KG_HIP(hipGetLastError());
   }
   return 0;

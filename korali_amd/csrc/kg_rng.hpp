@@ -127,6 +127,7 @@ class MtStream {
   bool par_ = false;
   unsigned long long W_ = 0;  // chunk words (power of two, >= MT_SEQ)
   int K_ = 0;                 // chunks per launch / seed lead
+  int parts_ = 8;             // workgroups sharing each chunk's seed jump
   uint32_t *seeds_ = nullptr; // [2K][624]
   uint64_t *polys_ = nullptr; // x^(2^l W) mod P, l = 0..log2 K
   ChunkPlan *plan_ = nullptr;

@@ -1897,6 +1897,7 @@ struct kg_vracer_s {
   struct Ev {
     std::string stage;
     hipEvent_t a, b;
+    size_t weight;  // stage instances the interval covers (a graph of updates: its length)
   };
   std::vector<Ev> events;
   std::vector<hipEvent_t> pool;
@@ -1904,6 +1905,11 @@ struct kg_vracer_s {
   // session counters of Agent::trainingGeneration (agent.cpp.base:176-235)
   unsigned long long session_experiences, session_updates, until_start, start_size;
   double ebpu;
+  // trainPolicy's updates replayed from one captured graph of upd_graph_n
+  // back-to-back updates (their kernels read all varying state from device
+  // memory, so one capture serves every later update)
+  hipGraphExec_t upd_graph = nullptr;
+  int upd_graph_n = 0;
 };
 
 namespace {
@@ -1923,7 +1929,7 @@ unsigned vr_blocks(long long n, int bs) { return (unsigned)((n + bs - 1) / bs); 
 struct VrStage {
   kg_vracer_t h;
   size_t idx = (size_t)-1;
-  VrStage(kg_vracer_t h_, const char *name) : h(h_) {
+  VrStage(kg_vracer_t h_, const char *name, size_t weight = 1) : h(h_) {
     if (!h->prof) return;
     auto take = [&]() {
       hipEvent_t e = nullptr;
@@ -1938,7 +1944,7 @@ struct VrStage {
     hipEvent_t a = take(), b = take();
     if (!a || !b) return;
     if (hipEventRecord(a, h->stream) != hipSuccess) return;
-    h->events.push_back({name, a, b});
+    h->events.push_back({name, a, b, weight});
     idx = h->events.size() - 1;
   }
   ~VrStage() {
@@ -1953,7 +1959,7 @@ int vr_collect(kg_vracer_t h) {
     KG_HIP(hipEventElapsedTime(&ms, e.a, e.b));
     auto &t = h->totals[e.stage];
     t.first += ms;
-    t.second += 1;
+    t.second += e.weight;
     h->pool.push_back(e.a);
     h->pool.push_back(e.b);
   }
@@ -2376,6 +2382,7 @@ extern "C" int kg_debug_cartpole(int device, const double *u0, const double *for
 int kg_vracer_destroy(kg_vracer_t h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->upd_graph) (void)hipGraphExecDestroy(h->upd_graph);
   void *ptrs[] = {h->offs, h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
                   h->dHb, h->mb, h->forced_mb, h->forced_noise, h->st, h->er.st, h->er.act, h->er.rew, h->er.tst,
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
@@ -2617,9 +2624,56 @@ int kg_vracer_rescale_states(kg_vracer_t h) {
   return vr_read_state(h);
 }
 
+// updates per captured graph (KORALI_AMD_VR_GRAPH; 0: every update launched
+// kernel by kernel).  The fused forward pass advances a host-chosen cursor,
+// so it is never captured.
+static int vr_graph_len(const Params &P) {
+  const char *e = getenv("KORALI_AMD_VR_GRAPH");
+  const int n = e ? atoi(e) : 64;
+  const char *fe = getenv("KORALI_AMD_VR_FUSED");
+  if (P.H <= 256 && fe && *fe == '1') return 0;
+  return n < 0 ? 0 : n > 256 ? 256 : n;
+}
+
+static int vr_capture_updates(kg_vracer_t h, int n) {
+  const int prof = h->prof;
+  h->prof = 0;  // no stage events inside the graph
+  hipGraph_t g = nullptr;
+  KG_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = 0;
+  for (int i = 0; i < n && !rc; i++) rc = vr_update(h, nullptr);
+  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  h->prof = prof;
+  if (rc || e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    KG_CHECK(rc == 0 && e == hipSuccess, "vracer: capturing the policy updates failed");
+    return 1;
+  }
+  const hipError_t ie = hipGraphInstantiate(&h->upd_graph, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  KG_HIP(ie);
+  h->upd_graph_n = n;
+  return 0;
+}
+
 int kg_vracer_train_policy(kg_vracer_t h, size_t updates) {
   KG_CHECK(h, "vracer: null argument");
-  for (size_t u = 0; u < updates; u++)
+  size_t u = 0;
+  const int G = vr_graph_len(h->P);
+  if (G > 0 && updates >= (size_t)G) {
+    KG_CHECK(h->st_host->size >= 2, "vracer: policy updates need at least two experiences in the replay memory");
+    if (h->upd_graph && h->upd_graph_n != G) {
+      KG_HIP(hipStreamSynchronize(h->stream));
+      KG_HIP(hipGraphExecDestroy(h->upd_graph));
+      h->upd_graph = nullptr;
+    }
+    if (!h->upd_graph && vr_capture_updates(h, G)) return 1;
+    for (; u + G <= updates; u += G) {
+      VrStage tu(h, "update", (size_t)G);
+      KG_HIP(hipGraphLaunch(h->upd_graph, h->stream));
+    }
+  }
+  for (; u < updates; u++)
     if (vr_update(h, nullptr)) return 1;
   h->session_updates += updates;
   return 0;

@@ -163,6 +163,26 @@ def test_large_population_sort_matches_numpy():
     assert np.array_equal(dev.sorting_index(), ref)
 
 
+@pytest.mark.parametrize("parts", ["1", "8", "13"])
+def test_chunked_mt_producer_wraps_the_seed_slots(monkeypatch, parts):
+    """Past 3K chunks (K = 256 chunks per launch, seed windows in 3K slots
+    reused in turn; 45 generations of N = 64, lambda = 4096 draw ~30 M words
+    in 2^15-word chunks): the chunk jumps split over 1, 8 or 13 workgroups
+    keep the population and the exported generator state bit-exact."""
+    monkeypatch.setenv("KORALI_AMD_MT_PARALLEL_MIN", "0")
+    monkeypatch.setenv("KORALI_AMD_MT_CHUNK_LOG2", "15")
+    monkeypatch.setenv("KORALI_AMD_MT_CHUNK_PARTS", parts)
+    o, dev = oracle_and_device(64, 4096, "rosenbrock", 45)
+    for g in range(1, 46):
+        o.generation(g, "rosenbrock")
+        dev.generation(g, "rosenbrock")
+        if g % 5 == 0 or g == 45:
+            dev.synchronize()
+            assert np.array_equal(dev["Sample Population"], o["Sample Population"]), g
+    assert np.array_equal(dev["Current Mean"], o["Current Mean"])
+    assert dev.get_rng(0) == o.rng(0).get_bytes()
+
+
 @pytest.mark.parametrize("log2w", [15, 17])
 def test_chunked_mt_producer_bit_exact(monkeypatch, log2w):
     """The multi-workgroup mt19937 producer (chunks of 2^log2w words seeded

@@ -88,6 +88,29 @@ def test_fused_update_equals_per_layer_kernels(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("glen", ["4", "5"])
+def test_graph_replayed_updates_equal_kernel_launches(monkeypatch, glen):
+    """trainPolicy's updates replayed from a captured graph of glen updates
+    (11 updates: whole graphs, then the rest launched kernel by kernel) leave
+    the hyperparameters, Adam moments, retrace values and importance weights
+    equal to launching every update's kernels, bit for bit."""
+    ag, th = fill_replay(64, 2, 8, 90, 600)
+    runs = []
+    monkeypatch.setenv("KORALI_AMD_VR_FUSED", "0")
+    for g in (glen, "0"):
+        monkeypatch.setenv("KORALI_AMD_VR_GRAPH", g)
+        d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
+                   replay_start_size=100, hyperparameters=th)
+        load_replay(d, ag)
+        d.train_policy(11)
+        d.train_policy(int(glen))  # the captured graph replayed again
+        runs.append((d.hyperparameters, d.get("retrace")[:ag.size()], d.get("importance_weight")[:ag.size()],
+                     d.get("loss_gradient")))
+        d.close()
+    for a, b in zip(*runs):
+        assert np.array_equal(a, b)
+
+
 CLIP = (np.array([-0.5], f32), np.array([0.5], f32))  # narrow bounds: every clipping branch is taken
 
 
