@@ -456,6 +456,17 @@ int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *upda
  * hyperparameters; replay memory and agent state are untouched. */
 int kg_vracer_test_episodes(kg_vracer_t h, const uint64_t *sample_ids, const uint64_t *launch_ids, size_t n,
                             float *rewards);
+/* The agent's whole training state in one binary file (replaces
+ * Agent::serializeExperienceReplay / deserializeExperienceReplay,
+ * agent.cpp.base:849-976, which write the replay memory to
+ * <result path>/state.json): the replay memory, the concurrent environments'
+ * episodes in flight, the policy, its Adam moments, the agent's scalars and
+ * counters, plus user_bytes of the caller's own (the engine's session
+ * counters).  kg_vracer_load_state needs a handle created with the same
+ * configuration (the seed may differ: the saved one is restored) and
+ * continues the saved run bit for bit. */
+int kg_vracer_save_state(kg_vracer_t h, const char *path, const void *user, size_t user_bytes);
+int kg_vracer_load_state(kg_vracer_t h, const char *path, void *user, size_t user_capacity, size_t *user_bytes);
 int kg_vracer_synchronize(kg_vracer_t h);
 int kg_vracer_stream(kg_vracer_t h, void **stream);
 /* Stage timers (HIP events on the handle's stream): "environment_step",

@@ -1910,6 +1910,8 @@ struct kg_vracer_s {
   // memory, so one capture serves every later update)
   hipGraphExec_t upd_graph = nullptr;
   int upd_graph_n = 0;
+  // every device buffer in allocation order (kg_vracer_save_state / _load_state)
+  std::vector<std::pair<void **, size_t>> bufs;
 };
 
 namespace {
@@ -2277,6 +2279,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   int rc = 0;
   auto alloc = [&](auto *&p, size_t bytes) {
     if (!rc && vr_alloc((void **)&p, bytes)) rc = 1;
+    if (!rc) h->bufs.push_back({(void **)&p, bytes ? bytes : 16});
   };
   hipError_t se = kg::stream_acquire(&h->stream);
   if (se != hipSuccess) {
@@ -2704,6 +2707,104 @@ int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *upda
   if (new_experiences) *new_experiences = added;
   if (updates) *updates = n;
   return 0;
+}
+
+// The agent's whole training state (Agent::serializeExperienceReplay /
+// deserializeExperienceReplay, agent.cpp.base:849-976, which write the replay
+// memory to <result path>/state.json): here every device buffer — the replay
+// memory, the concurrent environments' episodes in flight, the policy and its
+// Adam moments, the agent scalars and counters — and the host session
+// counters, in one binary file, so that a resumed run continues bit for bit.
+namespace {
+constexpr char VR_STATE_MAGIC[8] = {'K', 'G', 'V', 'R', 'S', 'T', '0', '1'};
+struct VrHostState {
+  unsigned long long session_experiences, session_updates, until_start, start_size;
+  double ebpu;
+  int use_forced_noise;
+};
+}  // namespace
+
+int kg_vracer_save_state(kg_vracer_t h, const char *path, const void *user, size_t user_bytes) {
+  KG_CHECK(h && path && (user || !user_bytes), "vracer: null argument");
+  KG_HIP(hipStreamSynchronize(h->stream));
+  FILE *f = fopen(path, "wb");
+  KG_CHECK(f, std::string("vracer: cannot write the training state file ") + path);
+  bool ok = fwrite(VR_STATE_MAGIC, 1, 8, f) == 8;
+  const unsigned long long psz = sizeof(Params), nb = h->bufs.size(), ub = user_bytes;
+  ok = ok && fwrite(&psz, 8, 1, f) == 1 && fwrite(&h->P, sizeof(Params), 1, f) == 1 && fwrite(&nb, 8, 1, f) == 1;
+  for (auto &b : h->bufs) {
+    const unsigned long long n = b.second;
+    ok = ok && fwrite(&n, 8, 1, f) == 1;
+  }
+  const VrHostState hs{h->session_experiences, h->session_updates, h->until_start, h->start_size, h->ebpu,
+                       h->use_forced_noise};
+  ok = ok && fwrite(&hs, sizeof hs, 1, f) == 1 && fwrite(&ub, 8, 1, f) == 1;
+  if (ub) ok = ok && fwrite(user, 1, ub, f) == ub;
+  std::vector<unsigned char> tmp;
+  for (auto &b : h->bufs) {
+    if (!ok) break;
+    tmp.resize(b.second);
+    if (hipMemcpy(tmp.data(), *b.first, b.second, hipMemcpyDeviceToHost) != hipSuccess) {
+      fclose(f);
+      KG_CHECK(false, "vracer: reading a device buffer for the training state failed");
+    }
+    ok = fwrite(tmp.data(), 1, b.second, f) == b.second;
+  }
+  ok = (fclose(f) == 0) && ok;
+  KG_CHECK(ok, std::string("vracer: writing the training state file failed: ") + path);
+  return 0;
+}
+
+int kg_vracer_load_state(kg_vracer_t h, const char *path, void *user, size_t user_capacity, size_t *user_bytes) {
+  KG_CHECK(h && path, "vracer: null argument");
+  FILE *f = fopen(path, "rb");
+  KG_CHECK(f, std::string("Trying to resume training or test policy but could not find or deserialize agent's state "
+                          "from file ") + path);
+  auto bad = [&](const char *why) {
+    fclose(f);
+    kg::set_error(std::string("vracer: training state file ") + path + ": " + why);
+    return 1;
+  };
+  char magic[8];
+  unsigned long long psz = 0, nb = 0, ub = 0;
+  Params Pf;
+  if (fread(magic, 1, 8, f) != 8 || memcmp(magic, VR_STATE_MAGIC, 8) != 0) return bad("not a VRACER state file");
+  if (fread(&psz, 8, 1, f) != 1 || psz != sizeof(Params) || fread(&Pf, sizeof(Params), 1, f) != 1)
+    return bad("agent layout mismatch");
+  {  // the same agent apart from the seed (a resumed experiment's seed counter moved on)
+    Params a = h->P, b = Pf;
+    a.seed = b.seed = 0;
+    if (memcmp(&a, &b, sizeof(Params)) != 0) return bad("saved by an agent of another configuration");
+  }
+  if (fread(&nb, 8, 1, f) != 1 || nb != h->bufs.size()) return bad("buffer count mismatch");
+  for (auto &b : h->bufs) {
+    unsigned long long n = 0;
+    if (fread(&n, 8, 1, f) != 1 || n != b.second) return bad("buffer size mismatch");
+  }
+  VrHostState hs;
+  if (fread(&hs, sizeof hs, 1, f) != 1 || fread(&ub, 8, 1, f) != 1) return bad("truncated");
+  std::vector<unsigned char> u(ub);
+  if (ub && fread(u.data(), 1, ub, f) != ub) return bad("truncated");
+  if (ub > user_capacity) return bad("user block larger than the caller's buffer");
+  KG_HIP(hipStreamSynchronize(h->stream));
+  std::vector<unsigned char> tmp;
+  for (auto &b : h->bufs) {
+    tmp.resize(b.second);
+    if (fread(tmp.data(), 1, b.second, f) != b.second) return bad("truncated");
+    if (hipMemcpy(*b.first, tmp.data(), b.second, hipMemcpyHostToDevice) != hipSuccess) return bad("upload failed");
+  }
+  fclose(f);
+  h->P.seed = Pf.seed;
+  if (h->upd_graph) {  // (captured with the old parameters)
+    KG_HIP(hipGraphExecDestroy(h->upd_graph));
+    h->upd_graph = nullptr;
+  }
+  h->session_experiences = hs.session_experiences, h->session_updates = hs.session_updates;
+  h->until_start = hs.until_start, h->start_size = hs.start_size, h->ebpu = hs.ebpu;
+  h->use_forced_noise = hs.use_forced_noise;
+  if (ub) memcpy(user, u.data(), ub);
+  if (user_bytes) *user_bytes = ub;
+  return vr_read_state(h);
 }
 
 int kg_vracer_synchronize(kg_vracer_t h) {

@@ -391,6 +391,8 @@ struct SolverModule {
   virtual void finalize(Json &js) = 0;
   virtual void printAfter(const Logger &log) = 0;
   virtual std::string type() const = 0;
+  // beside each result file, in its directory (VRACER: the training state)
+  virtual void saveFiles(const std::string &dir) { (void)dir; }
 };
 
 namespace {
@@ -1554,11 +1556,16 @@ void makeDirs(const std::string &path) {
     }
 }
 
-void saveState(Json &js, size_t gen) {
-  Json &fo = js["File Output"];
-  std::string path = fo["Path"].getString();
+std::string resultPath(Json &js) {
+  std::string path = js["File Output"]["Path"].getString();
   if (path.empty()) path = ".";
   if (path[0] != '/') path = "./" + path;  // experiment.cpp.base:136
+  return path;
+}
+
+void saveState(Json &js, size_t gen) {
+  Json &fo = js["File Output"];
+  const std::string path = resultPath(js);
   makeDirs(path);
   char name[64];
   if (fo["Use Multiple Files"].getBool())
@@ -1698,6 +1705,7 @@ struct VracerModule : SolverModule {
   Json description;  // vracerPolicyDescription: written into every result file
   bool testing = false, tested = false;  // Mode = Testing
   bool rewardRescaled = false;           // Reward / Rescaling / Enabled
+  bool serialize = true;                 // Experience Replay / Serialize: the training state beside the results
   std::vector<uint64_t> testingIds;
   std::vector<float> testingReward;
 
@@ -1718,9 +1726,8 @@ struct VracerModule : SolverModule {
     const std::string mode = canon(str(sv, "Mode", "Training"));
     if (mode != "training" && mode != "testing") fail("'Mode' must be 'Training' or 'Testing'.");
     testing = mode == "testing";
-    // a training run does not resume (the replay memory is not serialized);
-    // Testing runs one generation of the policy the experiment holds
-    if (resume && !testing) fail("Resuming a VRACER training run is not supported by the device path.");
+    // Testing runs one generation of the policy the experiment holds; a
+    // resumed training run loads <result path>/state.bin (below)
     if (testing) {
       Json &tj = sv["Testing"];
       if (tj.contains("Sample Ids"))
@@ -1809,7 +1816,7 @@ struct VracerModule : SolverModule {
     if (maxSize == 0) maxSize = (size_t)(std::pow(2, 14) * std::sqrt(4.0 + 1.0));  // agent.cpp.base:37-38
     if (startSize == 0) startSize = maxSize;
     er["Maximum Size"] = (unsigned long long)maxSize, er["Start Size"] = (unsigned long long)startSize;
-    flag(er, "Serialize", true);
+    serialize = flag(er, "Serialize", true);
     c.replay_maximum_size = maxSize, c.replay_start_size = startSize;
     c.max_episode_steps = (size_t)maxSteps;
     c.experiences_between_policy_updates = mandatory(sv, "Experiences Between Policy Updates", "VRACER");
@@ -1865,6 +1872,22 @@ struct VracerModule : SolverModule {
       }
     }
     check(kg_vracer_set_field(h, "hyperparameters", theta.data(), n * sizeof(float)));
+    if (resume && !testing) {
+      // Agent::deserializeExperienceReplay (agent.cpp.base:903-976) + the
+      // training statistics the result file holds
+      const std::string file = resultPath(js) + "/state.bin";
+      unsigned long long blob[2] = {0, 1};
+      size_t got = 0;
+      check(kg_vracer_load_state(h, file.c_str(), blob, sizeof blob, &got));
+      if (got == sizeof blob) sessionEpisodes = blob[0], sessionGeneration = blob[1];
+      Json &tr = sv["Training"];
+      if (tr.contains("Reward History"))
+        for (size_t i = 0; i < tr["Reward History"].size(); i++)
+          rewardHistory.push_back((float)tr["Reward History"][i].getDouble());
+      lastReward = (float)num(tr, "Last Reward", 0.0);
+      bestReward = (float)num(tr, "Best Reward", -INFINITY);
+      averageReward = (float)num(tr, "Average Reward", 0.0);
+    }
     if (testing) {
       // the agent's rescaling state as the experiment holds it (the reference
       // restores it with the policy, agent.cpp.base:1266-1274, and hands the
@@ -1987,6 +2010,14 @@ struct VracerModule : SolverModule {
   }
 
   void finalize(Json &) override {}
+
+  // Agent::serializeExperienceReplay (agent.cpp.base:849-901) each time the
+  // results are written (training runs with Experience Replay / Serialize)
+  void saveFiles(const std::string &dir) override {
+    if (testing || !serialize) return;
+    const unsigned long long blob[2] = {sessionEpisodes, sessionGeneration};
+    check(kg_vracer_save_state(h, (dir + "/state.bin").c_str(), blob, sizeof blob));
+  }
 
   void printAfter(const Logger &log) override {
     if (testing) {  // agent.cpp.base:1038-1045
@@ -2113,6 +2144,7 @@ void runExperiment(Experiment &e, Conduit &conduit) {
     solver.getConfiguration(sv);
     if (tm) tm->saveDistributions(js);
     saveState(js, gen);
+    solver.saveFiles(resultPath(js));
   };
   const auto t0 = std::chrono::steady_clock::now();
   if (gen == 0 && fileOut) save();
@@ -2155,7 +2187,10 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   solver.getConfiguration(sv);
   clk.mark("state");
   if (tm) tm->saveDistributions(js);
-  if (fileOut) saveState(js, gen);
+  if (fileOut) {
+    saveState(js, gen);
+    solver.saveFiles(resultPath(js));
+  }
   if (conduit.dist) conduit.dist->barrier();  // no rank leaves before the others finished
   clk.mark("files");
   st.log.log(1, "--------------------------------------------------------------------\n");

@@ -88,7 +88,7 @@ EXPORTED = [
     "kg_vracer_get_field", "kg_vracer_set_field", "kg_vracer_get_scalar", "kg_vracer_set_scalar",
     "kg_vracer_run_policy", "kg_vracer_set_action_noise", "kg_vracer_environment_step", "kg_vracer_train_policy",
     "kg_vracer_train_policy_minibatch", "kg_vracer_training_step", "kg_vracer_test_episodes", "kg_vracer_rescale_states", "kg_vracer_synchronize", "kg_vracer_stream",
-    "kg_vracer_profile", "kg_vracer_profile_read",
+    "kg_vracer_profile", "kg_vracer_profile_read", "kg_vracer_save_state", "kg_vracer_load_state",
 ]
 
 

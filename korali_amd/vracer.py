@@ -58,6 +58,8 @@ def _lib():
         L.kg_vracer_run_policy.argtypes = [vp, fp, sz, fp]
         L.kg_vracer_set_action_noise.argtypes = [vp, fp, sz]
         L.kg_vracer_environment_step.argtypes = [vp, C.POINTER(sz)]
+        L.kg_vracer_save_state.argtypes = [vp, cp, vp, sz]
+        L.kg_vracer_load_state.argtypes = [vp, cp, vp, sz, C.POINTER(sz)]
         L.kg_vracer_train_policy.argtypes = [vp, sz]
         L.kg_vracer_train_policy_minibatch.argtypes = [vp, C.POINTER(C.c_uint32), sz]
         L.kg_vracer_training_step.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
@@ -195,6 +197,15 @@ class VracerDevice:
 
     def synchronize(self):
         check(_lib().kg_vracer_synchronize(self._h))
+
+    def save_state(self, path):
+        """The whole training state (kg_vracer_save_state)."""
+        check(_lib().kg_vracer_save_state(self._h, str(path).encode(), None, 0))
+
+    def load_state(self, path):
+        """Continue the run saved in `path` (same configuration)."""
+        n = C.c_size_t(0)
+        check(_lib().kg_vracer_load_state(self._h, str(path).encode(), None, 0, C.byref(n)))
 
     def profile(self, enable=True):
         check(_lib().kg_vracer_profile(self._h, int(bool(enable))))

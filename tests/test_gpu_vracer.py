@@ -377,3 +377,46 @@ def test_testing_episodes_match_oracle(H, L, clipped, spread):
         assert np.mean(got == ref) >= 0.9
     assert np.all(got >= 1.0)
     d.close()
+
+
+def test_engine_training_resume_is_bit_exact(tmp_path):
+    """Experiment.loadState of a VRACER training run's latest result file
+    (+ the training state the engine writes beside it, state.bin: replay
+    memory, the episodes in flight, policy and Adam moments, counters;
+    agent.cpp.base:849-976 serialize / deserialize the replay memory the
+    same way) continues it: 3 + 3 generations end exactly like 6."""
+    import json
+    import os
+    import korali
+    from vracer_cases import cartpole_vracer
+
+    def experiment(gens, out):
+        e = cartpole_vracer(max_generations=gens, environments=4, hidden=32)
+        e["Solver"]["Experience Replay"]["Start Size"] = 150
+        e["File Output"]["Enabled"] = True
+        e["File Output"]["Path"] = str(out)
+        return e
+
+    a = experiment(6, tmp_path / "a")
+    korali.Engine().run(a)
+    korali.Engine().run(experiment(3, tmp_path / "b"))
+    assert os.path.exists(tmp_path / "b" / "state.bin")
+    r = korali.Experiment()
+    assert r.loadState(str(tmp_path / "b" / "latest"))
+    r["Solver"]["Termination Criteria"]["Max Generations"] = 6
+    korali.Engine().run(r)
+    sa = json.load(open(tmp_path / "a" / "latest"))["Solver"]
+    sb = json.load(open(tmp_path / "b" / "latest"))["Solver"]
+    assert sb["Policy Update Count"] > 0 and sa["Policy Update Count"] == sb["Policy Update Count"]
+    for k in ("Experience Count", "Current Episode", "Current Learning Rate"):
+        assert sa[k] == sb[k], k
+    assert sa["Training"]["Current Policy"]["Policy"] == sb["Training"]["Current Policy"]["Policy"]
+    assert sa["Training"]["Reward History"] == sb["Training"]["Reward History"]
+    assert sa["Experience Replay"]["Off Policy"] == sb["Experience Replay"]["Off Policy"]
+    # a missing training state fails as the reference does (agent.cpp.base:914-915)
+    os.remove(tmp_path / "b" / "state.bin")
+    r2 = korali.Experiment()
+    assert r2.loadState(str(tmp_path / "b" / "latest"))
+    r2["Solver"]["Termination Criteria"]["Max Generations"] = 8
+    with pytest.raises(korali.KoraliError, match="could not find or deserialize agent's state"):
+        korali.Engine().run(r2)
