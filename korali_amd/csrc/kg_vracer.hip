@@ -562,6 +562,46 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
   if (t == 0) st->mb_counter = ctr + (forced ? 0 : (unsigned long long)B);
 }
 
+// The mini-batch draw fused with the input layer (round 5): every workgroup
+// draws and sorts the B ids (vr_minibatch_keys: the same ids everywhere),
+// gathers its MI rows -- row b < B the state of mini-batch entry b, row B + b
+// its truncated state -- into Xmb and forms their input-layer activations
+// exactly as k_vr_fwd_in does (same products, same order, tanhf(acc + b)).
+// Workgroup 0 stores the ids; the draw counter advances in k_vr_meta.  Saves
+// k_vr_fwd_in's launch and its dependency on a one-workgroup draw.
+constexpr int MI = 8;
+__global__ __launch_bounds__(256) void k_vr_minibatch_in(Params P, const State *st, Replay er, unsigned *mb,
+                                                        const unsigned *forced, float *Xmb, const float *__restrict__ W,
+                                                        const float *__restrict__ bias, float *__restrict__ Y) {
+  __shared__ unsigned key[MAXB];
+  __shared__ float xs[MI * 16];
+  const int t = threadIdx.x, B = P.B, S = P.S, H = P.H, M = 2 * B;
+  vr_minibatch_keys(P, st, forced, key);
+  const int m0 = blockIdx.x * MI;
+  const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+  for (int e = t; e < MI * S; e += 256) {
+    const int r = e / S, i = e % S, m = m0 + r;
+    if (m < M) {
+      const int b = m < B ? m : m - B;
+      unsigned long long q = base + key[b];
+      if (q >= R) q -= R;
+      const float x = (m < B ? er.st : er.tst)[(long long)q * S + i];
+      xs[e] = x;
+      Xmb[(long long)m * S + i] = x;
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int i = t; i < B; i += 256) mb[i] = key[i];
+  __syncthreads();
+  for (int e = t; e < MI * H; e += 256) {
+    const int r = e / H, o = e % H, m = m0 + r;
+    if (m >= M) break;
+    float acc = 0.f;
+    for (int i = 0; i < S; i++) acc += W[o * S + i] * xs[r * S + i];
+    Y[(long long)m * H + o] = tanhf(acc + bias[o]);
+  }
+}
+
 // The whole forward pass (input layer, the L-1 hidden H x H layers, the
 // output layer) in ONE launch (round 5): a workgroup owns 16 rows and keeps
 // their activations in LDS between layers, the hidden layers on
@@ -1993,7 +2033,7 @@ VrGemmJob vr_gemm_job(int ep, int M, int N, int K, const float *A, long long sam
   return g;
 }
 
-int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
+int vr_forward(kg_vracer_t h, const float *X, int M, float *out, bool input_done = false) {
   const Params &P = h->P;
   KG_CHECK((size_t)M <= h->rowsMax, "vracer: forward batch exceeds the allocated rows");
   // KORALI_AMD_VR_FUSED=1: one launch for the whole forward pass (bit-identical
@@ -2010,8 +2050,9 @@ int vr_forward(kg_vracer_t h, const float *X, int M, float *out) {
     return 0;
   }
   float *a1 = h->acts;
-  hipLaunchKernelGGL(k_vr_fwd_in, dim3(vr_blocks((long long)M * P.H, 256)), dim3(256), 0, h->stream, M, P.S, P.H, X,
-                     h->theta + h->offW[0], h->theta + h->offb[0], a1);
+  if (!input_done)
+    hipLaunchKernelGGL(k_vr_fwd_in, dim3(vr_blocks((long long)M * P.H, 256)), dim3(256), 0, h->stream, M, P.S, P.H, X,
+                       h->theta + h->offW[0], h->theta + h->offb[0], a1);
   VrStage tg(h, M == P.E ? "gemm_rollout" : (M == 2 * P.B ? "gemm_update" : "gemm_other"));
   for (int l = 1; l < P.L; l++) {
     float *prev = h->acts + (size_t)(l - 1) * h->rowsMax * P.H, *cur = h->acts + (size_t)l * h->rowsMax * P.H;
@@ -2054,6 +2095,16 @@ void vr_multi(kg_vracer_t h, const VrMulti &J) {
 // the metadata kernel's retrace walks staged through LDS (C5, round 5: the
 // walk phase 14.2 against 21.0 us for the one-thread walks through the replay
 // memory; KORALI_AMD_VR_STAGED=0 selects those, A/B and the equality test)
+// the mini-batch draw fused with the input layer (k_vr_minibatch_in,
+// KORALI_AMD_VR_DRAW_IN=1; bit-identical, measured slower at C5, round 5:
+// 10.6 us against 7.1 + 5.0 for the two kernels it replaces, but 65.2 against
+// 64.3 us per graph-replayed update -- every workgroup repeats the draw and
+// sort, ~5 us of latency; kept for A/B and the equality test)
+static bool vr_draw_in() {
+  const char *e = getenv("KORALI_AMD_VR_DRAW_IN");
+  return e && *e == '1';
+}
+
 static bool vr_staged_walks() {
   const char *e = getenv("KORALI_AMD_VR_STAGED");
   return !(e && *e == '0');
@@ -2072,11 +2123,17 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
     hipLaunchKernelGGL(k_vr_fwd_fused<true>, dim3(vr_blocks(2 * B, FR)), dim3(256), 0, h->stream, P, 2 * B,
                        (const float *)nullptr, (const float *)h->theta, (const long long *)h->offs, h->acts,
                        (long long)h->rowsMax, h->out, (const State *)h->st, h->er, h->mb, forced, h->Xmb);
+  } else if (vr_draw_in() && P.S <= 16) {
+    hipLaunchKernelGGL(k_vr_minibatch_in, dim3(vr_blocks(2 * B, MI)), dim3(256), 0, h->stream, P, (const State *)h->st,
+                       h->er, h->mb, forced, h->Xmb, (const float *)(h->theta + h->offW[0]),
+                       (const float *)(h->theta + h->offb[0]), h->acts);
+    if (vr_forward(h, h->Xmb, 2 * B, h->out, true)) return 1;
   } else {
     hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
     if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
   }
-  const unsigned long long advance = (fused && !forced) ? (unsigned long long)B : 0ULL;
+  const bool drawIn = !fused && vr_draw_in() && P.S <= 16;
+  const unsigned long long advance = ((fused || drawIn) && !forced) ? (unsigned long long)B : 0ULL;
   hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er,
                      (const unsigned *)h->mb, (const float *)h->out, h->G, advance, vr_staged_walks() ? 1 : 0);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows

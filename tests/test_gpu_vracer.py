@@ -88,6 +88,27 @@ def test_fused_update_equals_per_layer_kernels(monkeypatch):
         assert np.array_equal(a, b)
 
 
+def test_draw_with_input_layer_equals_separate_kernels(monkeypatch):
+    """The mini-batch draw fused with the input layer (k_vr_minibatch_in,
+    many workgroups, the draw counter advanced by k_vr_meta) against the
+    one-workgroup draw + k_vr_fwd_in (the default): every update's results
+    bit for bit."""
+    ag, th = fill_replay(64, 2, 8, 90, 600)
+    runs = []
+    monkeypatch.setenv("KORALI_AMD_VR_FUSED", "0")
+    for v in ("1", "0"):
+        monkeypatch.setenv("KORALI_AMD_VR_DRAW_IN", v)
+        d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
+                   replay_start_size=100, hyperparameters=th)
+        load_replay(d, ag)
+        d.train_policy(9)
+        runs.append((d.hyperparameters, d.get("retrace")[:ag.size()], d.get("importance_weight")[:ag.size()],
+                     d.get("loss_gradient")))
+        d.close()
+    for a, b in zip(*runs):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("glen", ["4", "5"])
 def test_graph_replayed_updates_equal_kernel_launches(monkeypatch, glen):
     """trainPolicy's updates replayed from a captured graph of glen updates
