@@ -304,12 +304,21 @@ typedef struct {
   int version;
   double step_size;               /* "Step Size" (default 0.1) */
   double domain_extension_factor; /* "Domain Extension Factor" (default 0.2) */
-  /* per variable: 0 Univariate/Uniform prior (prior_min / prior_max =
-   * Minimum / Maximum), 1 Univariate/Normal (prior_min / prior_max = Mean /
-   * Standard Deviation; normal.cpp.base).  Variables sharing a distribution
-   * share its kind.  NULL: every prior Uniform.  mTMCMC: Uniform only. */
+  /* per variable, enum kg_prior_kind (prior_min / prior_max = the
+   * distribution's two parameters as listed there).  Variables sharing a
+   * distribution share its kind.  NULL: every prior Uniform.  mTMCMC:
+   * Uniform only. */
   const int *prior_kind;
 } kg_tmcmc_cfg;
+
+enum kg_prior_kind {
+  KG_PRIOR_UNIFORM = 0,     /* Minimum, Maximum (uniform.cpp.base) */
+  KG_PRIOR_NORMAL = 1,      /* Mean, Standard Deviation (normal.cpp.base) */
+  KG_PRIOR_EXPONENTIAL = 2, /* Location, Mean (exponential.cpp.base) */
+  KG_PRIOR_LAPLACE = 3,     /* Mean, Width (laplace.cpp.base) */
+  KG_PRIOR_CAUCHY = 4,      /* Location, Scale (cauchy.cpp.base) */
+  KG_PRIOR_LOGNORMAL = 5    /* Mu, Sigma (logNormal.cpp.base) */
+};
 
 int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out);
 int kg_tmcmc_destroy(kg_tmcmc_t h);

@@ -205,11 +205,37 @@ __global__ void k_tm_evaluate(int N, int P, int lik, const double *__restrict__ 
   const double *x = cand + (size_t)c * N;
   double lp = 0.0;
   for (int d = 0; d < N; d++) {
-    if (vkind[d]) {
-      const double z = (x[d] - pmin[d]) / pmax[d];
-      lp += negLogWidth[d] - 0.5 * z * z;
-    } else {
-      lp += (x[d] >= pmin[d] && x[d] <= pmax[d]) ? negLogWidth[d] : -INFINITY;
+    const double a = pmin[d], b = pmax[d], c = negLogWidth[d];
+    switch (vkind[d]) {
+      case KG_PRIOR_NORMAL: {
+        const double z = (x[d] - a) / b;
+        lp += c - 0.5 * z * z;
+        break;
+      }
+      case KG_PRIOR_EXPONENTIAL: {  // exponential.cpp.base: -log(mean) - (x - location) / mean
+        const double y = x[d] - a;
+        lp += y < 0 ? -INFINITY : c - y / b;
+        break;
+      }
+      case KG_PRIOR_LAPLACE:  // laplace.cpp.base: aux - |x - mean| / width
+        lp += c - fabs(x[d] - a) / b;
+        break;
+      case KG_PRIOR_CAUCHY: {  // cauchy.cpp.base: aux - log(1 + (x - loc)^2 / scale^2)
+        const double y = x[d] - a;
+        lp += c - log_cr(1. + y * y / (b * b));
+        break;
+      }
+      case KG_PRIOR_LOGNORMAL: {  // logNormal.cpp.base: aux - log x - 0.5 d^2, d = (log x - mu) / sigma
+        if (x[d] <= 0) {
+          lp += -INFINITY;
+        } else {
+          const double lx = log_cr(x[d]), z = (lx - a) / b;
+          lp += c - lx - 0.5 * z * z;
+        }
+        break;
+      }
+      default:
+        lp += (x[d] >= a && x[d] <= b) ? c : -INFINITY;
     }
   }
   candLP[c] = lp;
@@ -240,13 +266,23 @@ __global__ void k_tm_pend_init(int P, int lo, int hi, unsigned char *__restrict_
   if (c < P) pend[c] = (c >= lo && c < hi) ? 1 : 0;
 }
 
-// each variable's log-density constant: Uniform -log(b - a); Normal
-// _logNormalization = -0.5 log(2 pi) - log(sd) (normal.cpp.base:40-46)
+// each variable's log-density constant (the distributions' updateDistribution
+// / getLogDensity): Uniform -log(b - a); Normal and LogNormal -0.5 log(2 pi)
+// - log(sd); Exponential -log(mean); Laplace -log(2 width); Cauchy
+// -log(scale pi)
 __global__ void k_tm_neglogwidth(int N, const double *__restrict__ pmin, const double *__restrict__ pmax,
                                  const int *__restrict__ vkind, double *__restrict__ out) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= N) return;
-  out[d] = vkind[d] ? -0.5 * log_cr(2 * 3.14159265358979323846) - log_cr(pmax[d]) : -log_cr(pmax[d] - pmin[d]);
+  const double pi = 3.14159265358979323846, b = pmax[d];
+  switch (vkind[d]) {
+    case KG_PRIOR_NORMAL:
+    case KG_PRIOR_LOGNORMAL: out[d] = -0.5 * log_cr(2 * pi) - log_cr(b); break;
+    case KG_PRIOR_EXPONENTIAL: out[d] = -log_cr(b); break;
+    case KG_PRIOR_LAPLACE: out[d] = -log_cr(2. * b); break;
+    case KG_PRIOR_CAUCHY: out[d] = -log_cr(b * pi); break;
+    default: out[d] = -log_cr(b - pmin[d]);
+  }
 }
 
 // processCandidate + calculateAcceptanceProbability + updateDatabase
@@ -2696,9 +2732,10 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
       KG_CHECK(cfg->prior_kind[d] == 0, "Only 'Univariate/Uniform' priors allowed (mTMCMC)");
   }
   for (size_t d = 0; cfg->prior_kind && d < cfg->variable_count; d++) {
-    KG_CHECK(cfg->prior_kind[d] == 0 || cfg->prior_kind[d] == 1, "prior_kind entries must be 0 (Uniform) or 1 (Normal)");
-    KG_CHECK(cfg->prior_kind[d] == 0 || cfg->prior_max[d] > 0.0,  // normal.cpp.base:38
-             "Incorrect Standard Deviation parameter of Normal distribution");
+    KG_CHECK(cfg->prior_kind[d] >= KG_PRIOR_UNIFORM && cfg->prior_kind[d] <= KG_PRIOR_LOGNORMAL,
+             "prior_kind entries must be KG_PRIOR_UNIFORM .. KG_PRIOR_LOGNORMAL");
+    KG_CHECK(cfg->prior_kind[d] == KG_PRIOR_UNIFORM || cfg->prior_max[d] > 0.0,  // the distributions' updateDistribution
+             "Incorrect scale parameter (Standard Deviation / Mean / Width / Scale / Sigma) of a prior distribution");
   }
   KG_HIP(hipSetDevice(cfg->device));
   upload_dd_tables();
@@ -2983,13 +3020,15 @@ static int tm_mt_candidates(kg_tmcmc_s *h) {
   return 0;
 }
 
-// generation 1, Normal priors (Normal::getRandomNumber = mean +
-// gsl_ran_gaussian(sd), normal.cpp.base:30-33): the Marsaglia polar
-// rejection makes each draw's word count data-dependent, and a distribution
-// shared by several variables interleaves them sample-major
-// (TMCMC.cpp.base:215-221), so the P x (its variables) draws run on the host
-// from the distribution's exported generator, which then continues from
-// where they left it.  Once per run.
+// generation 1, non-Uniform priors (getRandomNumber of Normal = mean +
+// gsl_ran_gaussian(sd), normal.cpp.base:30-33; Exponential location +
+// gsl_ran_exponential(mean); Laplace mean + gsl_ran_laplace(width); Cauchy
+// location + gsl_ran_cauchy(scale); LogNormal gsl_ran_lognormal(mu, sigma) --
+// GSL 2.6 randist): rejection loops make a draw's word count data-dependent,
+// and a distribution shared by several variables interleaves them
+// sample-major (TMCMC.cpp.base:215-221), so the P x (its variables) draws
+// run on the host from the distribution's exported generator, which then
+// continues from where they left it.  Once per run.
 static int tm_normal_priors(kg_tmcmc_t h) {
   const int N = h->N, P = h->P;
   std::vector<double> mean(N), sd(N), out((size_t)P * N, 0.0);
@@ -3007,16 +3046,55 @@ static int tm_normal_priors(kg_tmcmc_t h) {
       while (u == 0.0);
       return u;
     };
+    const double pi = 3.14159265358979323846;
     for (int i = 0; i < P; i++)
       for (int d = 0; d < N; d++) {
         if (h->distOf[d] != k) continue;
-        double x, y, r2;
-        do {
-          x = -1 + 2 * upos();
-          y = -1 + 2 * upos();
-          r2 = x * x + y * y;
-        } while (r2 > 1.0 || r2 == 0);
-        out[(size_t)i * N + d] = mean[d] + sd[d] * y * std::sqrt(-2.0 * host_log_cr(r2) / r2);
+        const double a = mean[d], b = sd[d];
+        double v = 0.0;
+        switch (h->distKind[k]) {
+          case KG_PRIOR_NORMAL: {
+            double x, y, r2;
+            do {
+              x = -1 + 2 * upos();
+              y = -1 + 2 * upos();
+              r2 = x * x + y * y;
+            } while (r2 > 1.0 || r2 == 0);
+            v = a + b * y * std::sqrt(-2.0 * host_log_cr(r2) / r2);
+            break;
+          }
+          case KG_PRIOR_EXPONENTIAL: {
+            const double u = g.uniform();
+            v = a + -b * std::log1p(-u);
+            break;
+          }
+          case KG_PRIOR_LAPLACE: {
+            double u;
+            do u = 2 * g.uniform() - 1.0;
+            while (u == 0.0);
+            v = a + (u < 0 ? b * host_log_cr(-u) : -b * host_log_cr(u));
+            break;
+          }
+          case KG_PRIOR_CAUCHY: {
+            double u;
+            do u = g.uniform();
+            while (u == 0.5);
+            v = a + b * std::tan(pi * u);
+            break;
+          }
+          case KG_PRIOR_LOGNORMAL: {
+            double x, y, r2;
+            do {
+              x = -1 + 2 * g.uniform();
+              y = -1 + 2 * g.uniform();
+              r2 = x * x + y * y;
+            } while (r2 > 1.0 || r2 == 0);
+            const double normal = x * std::sqrt(-2.0 * host_log_cr(r2) / r2);
+            v = std::exp(b * normal + a);
+            break;
+          }
+        }
+        out[(size_t)i * N + d] = v;
       }
     g.save(st);
     if (h->priorRng[k]->import_gsl(st, h->stream)) return 1;

@@ -1222,15 +1222,30 @@ struct TmcmcModule : SolverModule {
       if (dt == "univariate/uniform") {
         pmin[i] = mandatory(ds[k], "Minimum", "Distributions");
         pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
-      } else if (dt == "univariate/normal") {
-        pkind[i] = 1;
-        pmin[i] = mandatory(ds[k], "Mean", "Distributions");
-        pmax[i] = mandatory(ds[k], "Standard Deviation", "Distributions");
-        if (!(pmax[i] > 0.0))  // normal.cpp.base:38
-          fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", pmax[i]);
       } else {
-        fail("The device TMCMC path supports 'Univariate/Uniform' and 'Univariate/Normal' priors (distribution '%s').",
-             pn.c_str());
+        // the two parameters of each supported distribution and its
+        // updateDistribution check (exponential has none: a mean <= 0 fails here)
+        struct Kind {
+          const char *type, *a, *b, *what;
+          int kind;
+        };
+        static const Kind kinds[] = {
+            {"univariate/normal", "Mean", "Standard Deviation", "Standard Deviation parameter of Normal", KG_PRIOR_NORMAL},
+            {"univariate/exponential", "Location", "Mean", "Mean parameter of Exponential", KG_PRIOR_EXPONENTIAL},
+            {"univariate/laplace", "Mean", "Width", "Width parameter of Laplace", KG_PRIOR_LAPLACE},
+            {"univariate/cauchy", "Location", "Scale", "Scale parameter of Cauchy", KG_PRIOR_CAUCHY},
+            {"univariate/lognormal", "Mu", "Sigma", "Sigma parameter of LogNormal", KG_PRIOR_LOGNORMAL}};
+        const Kind *kd = nullptr;
+        for (const Kind &q : kinds)
+          if (dt == q.type) kd = &q;
+        if (!kd)
+          fail("The device TMCMC path supports 'Univariate/Uniform', 'Univariate/Normal', 'Univariate/Exponential', "
+               "'Univariate/Laplace', 'Univariate/Cauchy' and 'Univariate/LogNormal' priors (distribution '%s').",
+               pn.c_str());
+        pkind[i] = kd->kind;
+        pmin[i] = mandatory(ds[k], kd->a, "Distributions");
+        pmax[i] = mandatory(ds[k], kd->b, "Distributions");
+        if (!(pmax[i] > 0.0)) fail("Incorrect %s distribution: %f.\n", kd->what, pmax[i]);
       }
       pdist[i] = k;
     }

@@ -368,6 +368,51 @@ double kr_ran_gaussian(kr_rng *r, double sigma)
   return sigma * y * sqrt(-2.0 * kr_log_cr(r2) / r2);
 }
 
+/* GSL 2.6 randist samplers behind the other univariate priors
+ * (exponential.c, laplace.c, cauchy.c, lognormal.c; Korali
+ * univariate/{exponential,laplace,cauchy,logNormal}/*.cpp.base getRandomNumber).
+ * log1p, tan and exp are the host libm's (as the device library's host
+ * draws); log is the correctly rounded one, as everywhere in this file. */
+double kr_ran_exponential(kr_rng *r, double mu)
+{
+  double u = kr_rng_uniform(r);
+  return -mu * log1p(-u);
+}
+
+double kr_ran_laplace(kr_rng *r, double a)
+{
+  double u;
+  do
+  {
+    u = 2 * kr_rng_uniform(r) - 1.0;
+  } while (u == 0.0);
+  if (u < 0) return a * kr_log_cr(-u);
+  return -a * kr_log_cr(u);
+}
+
+double kr_ran_cauchy(kr_rng *r, double a)
+{
+  double u;
+  do
+  {
+    u = kr_rng_uniform(r);
+  } while (u == 0.5);
+  return a * tan(3.14159265358979323846 * u);
+}
+
+double kr_ran_lognormal(kr_rng *r, double zeta, double sigma)
+{
+  double u, v, r2, normal;
+  do
+  {
+    u = -1 + 2 * kr_rng_uniform(r);
+    v = -1 + 2 * kr_rng_uniform(r);
+    r2 = u * u + v * v;
+  } while (r2 > 1.0 || r2 == 0);
+  normal = u * sqrt(-2.0 * kr_log_cr(r2) / r2);
+  return exp(sigma * normal + zeta);
+}
+
 /* gsl_ran_flat; Korali univariate/uniform/uniform.cpp.base:30-36 */
 double kr_ran_flat(kr_rng *r, double a, double b)
 {
@@ -2257,7 +2302,9 @@ struct kr_tmcmc
   double *priorMin, *priorMax;
   kr_rng *priorRng;
   int *priorMap; /* variable -> prior distribution (shared distributions share an RNG) */
-  int *priorKind; /* per variable: 0 Uniform [priorMin, priorMax], 1 Normal (priorMin = mean, priorMax = sd) */
+  int *priorKind; /* per variable: 0 Uniform [priorMin, priorMax], 1 Normal (mean, sd), 2 Exponential
+                   * (location, mean), 3 Laplace (mean, width), 4 Cauchy (location, scale), 5 LogNormal
+                   * (mu, sigma): priorMin / priorMax hold the two parameters */
   /* state */
   double *leaders, *leadersLL, *leadersLP, *candidates, *candidatesLL, *candidatesLP;
   double *chainLengths, *meanTheta, *cov, *chol;
@@ -2849,8 +2896,21 @@ void kr_tmcmc_prepare(kr_tmcmc *h, size_t gen)
       /* TMCMC.cpp.base:218-220: getRandomNumber of each variable's
        * distribution; Normal: mean + gsl_ran_gaussian(sd) (normal.cpp.base:30-33) */
       for (d = 0; d < N; d++)
-        h->candidates[i * N + d] = h->priorKind[d] ? h->priorMin[d] + kr_ran_gaussian(&h->priorRng[h->priorMap[d]], h->priorMax[d])
-                                                   : kr_ran_flat(&h->priorRng[h->priorMap[d]], h->priorMin[d], h->priorMax[d]);
+      {
+        kr_rng *g = &h->priorRng[h->priorMap[d]];
+        const double a = h->priorMin[d], b = h->priorMax[d];
+        double v;
+        switch (h->priorKind[d])
+        {
+        case 1: v = a + kr_ran_gaussian(g, b); break;
+        case 2: v = a + kr_ran_exponential(g, b); break;
+        case 3: v = a + kr_ran_laplace(g, b); break;
+        case 4: v = a + kr_ran_cauchy(g, b); break;
+        case 5: v = kr_ran_lognormal(g, a, b); break;
+        default: v = kr_ran_flat(g, a, b);
+        }
+        h->candidates[i * N + d] = v;
+      }
     }
     else if (h->LE)
       mt_generate_candidate(h, i);
@@ -2870,12 +2930,43 @@ static void tm_evaluate_one(kr_tmcmc *h, size_t i)
   double lp = 0.0;
   for (d = 0; d < N; d++)
   {
-    if (h->priorKind[d])
+    const double a = h->priorMin[d], b = h->priorMax[d], pi = 3.14159265358979323846;
+    switch (h->priorKind[d])
+    {
+    case 1:
     { /* normal.cpp.base:17-21, :40-46 */
-      const double logNorm = -0.5 * kr_log_cr(2 * 3.14159265358979323846) - kr_log_cr(h->priorMax[d]);
-      const double z = (x[d] - h->priorMin[d]) / h->priorMax[d];
+      const double logNorm = -0.5 * kr_log_cr(2 * pi) - kr_log_cr(b);
+      const double z = (x[d] - a) / b;
       lp += logNorm - 0.5 * z * z;
       continue;
+    }
+    case 2:
+    { /* exponential.cpp.base getLogDensity */
+      const double y = x[d] - a;
+      lp += y < 0 ? -INFINITY : -kr_log_cr(b) - y / b;
+      continue;
+    }
+    case 3: /* laplace.cpp.base: aux = -log(2 width) */
+      lp += -kr_log_cr(2. * b) - fabs(x[d] - a) / b;
+      continue;
+    case 4:
+    { /* cauchy.cpp.base: aux = -log(scale pi) */
+      const double y = x[d] - a;
+      lp += -kr_log_cr(b * pi) - kr_log_cr(1. + y * y / (b * b));
+      continue;
+    }
+    case 5:
+    { /* logNormal.cpp.base: aux = -0.5 log(2 pi) - log(sigma) */
+      if (x[d] <= 0)
+      {
+        lp += -INFINITY;
+        continue;
+      }
+      const double aux = -0.5 * kr_log_cr(2 * pi) - kr_log_cr(b), lx = kr_log_cr(x[d]), z = (lx - a) / b;
+      lp += aux - lx - 0.5 * z * z;
+      continue;
+    }
+    default: break;
     }
     const double aux = -kr_log_cr(h->priorMax[d] - h->priorMin[d]);
     lp += (x[d] >= h->priorMin[d] && x[d] <= h->priorMax[d]) ? aux : -INFINITY;

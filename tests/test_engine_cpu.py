@@ -95,7 +95,8 @@ def test_type_strings_ignore_case_and_whitespace():
 
 
 @pytest.mark.parametrize("dist,params,msg", [
-    ("Univariate/Cauchy", {"Location": 0.0, "Scale": 1.0}, "'Univariate/Uniform' and 'Univariate/Normal' priors"),
+    ("Univariate/Beta", {"Alpha": 2.0, "Beta": 2.0}, "'Univariate/Uniform', 'Univariate/Normal'"),
+    ("Univariate/Laplace", {"Mean": 0.0, "Width": 0.0}, "Incorrect Width parameter of Laplace"),
     ("Univariate/Normal", {"Mean": 0.0, "Standard Deviation": -1.0}, "Incorrect Standard Deviation"),
     ("Univariate/Normal", {"Standard Deviation": 1.0}, "Mean")])
 def test_tmcmc_prior_validation(dist, params, msg):

@@ -126,19 +126,27 @@ def test_tmcmc_seeded_run_matches_oracle(N, P, gens, shared):
         assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
 
 
-@pytest.mark.parametrize("mcl,burn", [(1, 0), (3, 1)])
-def test_tmcmc_normal_priors_match_oracle(mcl, burn):
+PRIOR_SETS = {
+    # variable -> distribution, kind (enum kg_prior_kind), the two parameters
+    "normal": ([0, 1, 2, 2], [1, 0, 1, 1], [0.5, -5.0, -1.0, -1.0], [2.0, 5.0, 0.7, 0.7]),
+    "all": ([0, 1, 2, 3, 4, 4], [2, 3, 4, 5, 1, 1], [-1.0, 0.3, 0.0, 0.0, -1.0, -1.0], [2.0, 1.5, 0.5, 0.5, 0.7, 0.7]),
+}
+
+
+@pytest.mark.parametrize("mcl,burn,priors", [(1, 0, "normal"), (3, 1, "normal"), (1, 0, "all"), (2, 1, "all")])
+def test_tmcmc_normal_priors_match_oracle(mcl, burn, priors):
     """Univariate/Normal priors (normal.cpp.base: mean + gsl_ran_gaussian(sd)
     draws at generation 1, log-density logNormalization - 0.5 d^2) mixed with
     Uniform ones, one Normal distribution shared by two variables (its draws
-    interleave sample-major): the whole run bit-exact vs the oracle, the
+    interleave sample-major); and Exponential, Laplace, Cauchy and LogNormal
+    priors beside a shared Normal: the whole run bit-exact vs the oracle, the
     prior generators' exported states included."""
     from korali_amd.native import TmcmcDevice
-    N, P, seed = 4, 600, 2024
-    pdist, kinds = [0, 1, 2, 2], [1, 0, 1, 1]
-    pmin, pmax = [0.5, -5.0, -1.0, -1.0], [2.0, 5.0, 0.7, 0.7]  # Normal: mean / sd; Uniform: min / max
-    seeds = [seed, seed + 1, seed + 2]
-    sm, sv, su = seed + 3, seed + 4, seed + 5
+    pdist, kinds, pmin, pmax = PRIOR_SETS[priors]
+    N, P, seed = len(pdist), 600, 2024
+    nd = max(pdist) + 1
+    seeds = [seed + k for k in range(nd)]
+    sm, sv, su = seed + nd, seed + nd + 1, seed + nd + 2
     dev = TmcmcDevice(N, P, prior_min=pmin, prior_max=pmax, prior_seeds=seeds, prior_distribution=pdist,
                       prior_kind=kinds, multinomial_seed=sm, multivariate_seed=sv, uniform_seed=su,
                       max_chain_length=mcl, default_burn_in=burn)
@@ -149,7 +157,7 @@ def test_tmcmc_normal_priors_match_oracle(mcl, burn):
     o["Prior Maximum"] = pmax
     o.set_prior_map(pdist)
     o.set_prior_kinds(kinds)
-    for k in range(3):
+    for k in range(nd):
         R.lib().kr_rng_seed(o.rng(3 + k).ptr, seeds[k])
     R.lib().kr_rng_seed(o.rng(0).ptr, sm)
     R.lib().kr_rng_seed(o.rng(1).ptr, sv)
@@ -163,12 +171,15 @@ def test_tmcmc_normal_priors_match_oracle(mcl, burn):
         for key in SCA_KEYS:
             a, b = dev[key][0], o[key][0]
             assert a == b or (np.isnan(a) and np.isnan(b)), (g, key, a, b)
-        if g == 1:  # the Normal variables' draws are unbounded and centred on the mean
+        if g == 1 and priors == "normal":  # the Normal variables' draws are unbounded and centred on the mean
             x = np.asarray(dev["Sample Database"]).reshape(-1, N)
             assert abs(x[:, 0].mean() - 0.5) < 0.3 and abs(x[:, 2].mean() + 1.0) < 0.15
+        if g == 1 and priors == "all":  # Exponential >= location, LogNormal > 0, Laplace around its mean
+            x = np.asarray(dev["Sample Database"]).reshape(-1, N)
+            assert x[:, 0].min() >= -1.0 and x[:, 3].min() > 0 and abs(np.median(x[:, 1]) - 0.3) < 0.3
         if o["Annealing Exponent"][0] >= 1.0:
             break
-    for which in range(6):
+    for which in range(3 + nd):
         assert dev.get_rng(which).hex().upper() == o.rng(which).to_hex(), which
 
 
