@@ -285,8 +285,8 @@ struct VariableSpec {
 // Reference 'Computational Model' + likelihood model (likelihood.cpp).
 struct BayesianEvaluator {
   struct Prior {
-    bool normal;
-    double a, b, aux;  // uniform: min, max, -log(max - min); normal: mean, sd, log-normalisation
+    int kind;          // enum kg_prior_kind
+    double a, b, aux;  // the distribution's two parameters and its log-density constant
   };
   std::vector<Prior> priors;
   bool reference = false;
@@ -326,13 +326,38 @@ struct BayesianEvaluator {
         p.b = mandatory(ds[k], "Maximum", "Distributions");
         p.aux = p.b - p.a <= 0.0 ? NAN : -std::log(p.b - p.a);
       } else if (t == "univariate/normal") {
-        p.normal = true;
+        p.kind = KG_PRIOR_NORMAL;
         p.a = mandatory(ds[k], "Mean", "Distributions");
         p.b = mandatory(ds[k], "Standard Deviation", "Distributions");
         if (!(p.b > 0.0)) fail("Incorrect Standard Deviation parameter of Normal distribution: %f.\n", p.b);
         p.aux = -0.5 * std::log(2 * M_PI) - std::log(p.b);
+      } else if (t == "univariate/exponential") {  // exponential.cpp.base
+        p.kind = KG_PRIOR_EXPONENTIAL;
+        p.a = mandatory(ds[k], "Location", "Distributions");
+        p.b = mandatory(ds[k], "Mean", "Distributions");
+        p.aux = -std::log(p.b);
+      } else if (t == "univariate/laplace") {  // laplace.cpp.base
+        p.kind = KG_PRIOR_LAPLACE;
+        p.a = mandatory(ds[k], "Mean", "Distributions");
+        p.b = mandatory(ds[k], "Width", "Distributions");
+        if (p.b <= 0.0) fail("Incorrect Width parameter of Laplace distribution: %f.\n", p.b);
+        p.aux = -std::log(2. * p.b);
+      } else if (t == "univariate/cauchy") {  // cauchy.cpp.base
+        p.kind = KG_PRIOR_CAUCHY;
+        p.a = mandatory(ds[k], "Location", "Distributions");
+        p.b = mandatory(ds[k], "Scale", "Distributions");
+        if (p.b <= 0) fail("Incorrect Scale parameter of Cauchy distribution: %f.\n", p.b);
+        p.aux = -std::log(p.b * M_PI);
+      } else if (t == "univariate/lognormal") {  // logNormal.cpp.base
+        p.kind = KG_PRIOR_LOGNORMAL;
+        p.a = mandatory(ds[k], "Mu", "Distributions");
+        p.b = mandatory(ds[k], "Sigma", "Distributions");
+        if (p.b <= 0.0) fail("Incorrect Sigma parameter of LogNormal distribution: %f.\n", p.b);
+        p.aux = -0.5 * std::log(2 * M_PI) - std::log(p.b);
       } else {
-        fail("Bayesian problems on this path support 'Univariate/Uniform' and 'Univariate/Normal' priors (distribution '%s').",
+        fail("Bayesian problems on this path support 'Univariate/Uniform', 'Univariate/Normal', "
+             "'Univariate/Exponential', 'Univariate/Laplace', 'Univariate/Cauchy' and 'Univariate/LogNormal' priors "
+             "(distribution '%s').",
              pn.c_str());
       }
       priors.push_back(p);
@@ -344,11 +369,27 @@ struct BayesianEvaluator {
     double logPrior = 0.0;
     for (size_t i = 0; i < x.size(); i++) {
       const Prior &p = priors[i];
-      if (p.normal) {
-        const double d = (x[i] - p.a) / p.b;
-        logPrior += p.aux - 0.5 * d * d;
-      } else {
-        logPrior += (x[i] >= p.a && x[i] <= p.b) ? p.aux : -INFINITY;
+      switch (p.kind) {  // the distributions' getLogDensity
+        case KG_PRIOR_NORMAL: {
+          const double d = (x[i] - p.a) / p.b;
+          logPrior += p.aux - 0.5 * d * d;
+          break;
+        }
+        case KG_PRIOR_EXPONENTIAL:
+          logPrior += x[i] - p.a < 0 ? -INFINITY : p.aux - (x[i] - p.a) / p.b;
+          break;
+        case KG_PRIOR_LAPLACE: logPrior += p.aux - std::fabs(x[i] - p.a) / p.b; break;
+        case KG_PRIOR_CAUCHY: logPrior += p.aux - std::log(1. + (x[i] - p.a) * (x[i] - p.a) / (p.b * p.b)); break;
+        case KG_PRIOR_LOGNORMAL: {
+          if (x[i] <= 0) {
+            logPrior += -INFINITY;
+            break;
+          }
+          const double lx = std::log(x[i]), d = (lx - p.a) / p.b;
+          logPrior += p.aux - lx - 0.5 * d * d;
+          break;
+        }
+        default: logPrior += (x[i] >= p.a && x[i] <= p.b) ? p.aux : -INFINITY;
       }
     }
     s["logPrior"] = logPrior;

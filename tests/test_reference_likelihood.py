@@ -155,7 +155,7 @@ def test_sample_entries_extend_in_place():
 def test_cmaes_bayesian_prior_validation_before_device():
     e = reference_experiment()
     e["Solver"] = {"Type": "Optimizer/CMAES", "Population Size": 8}
-    e["Distributions"][2]["Type"] = "Univariate/Exponential"
+    e["Distributions"][2]["Type"] = "Univariate/Beta"
     with pytest.raises(korali.KoraliError, match="Univariate/Normal"):
         korali.Engine().run(e)
 
@@ -200,6 +200,35 @@ def test_bayesian_evaluate_custom_with_normal_prior():
     assert out["logPrior"] == (-0.5 * math.log(2 * math.pi) - math.log(2.0)) - 0.5 * d * d
     assert out["F(x)"] == out["logPrior"] + (-0.5)
     assert out["logPrior"] == pytest.approx(st.norm.logpdf(0.5, 1.0, 2.0), rel=1e-15)
+
+
+@pytest.mark.parametrize("dist,params,x,ref", [
+    ("Univariate/Exponential", {"Location": -1.0, "Mean": 2.0}, 0.5, lambda x: st.expon.logpdf(x, -1.0, 2.0)),
+    ("Univariate/Laplace", {"Mean": 0.3, "Width": 1.5}, -0.4, lambda x: st.laplace.logpdf(x, 0.3, 1.5)),
+    ("Univariate/Cauchy", {"Location": 0.0, "Scale": 0.5}, 0.7, lambda x: st.cauchy.logpdf(x, 0.0, 0.5)),
+    ("Univariate/LogNormal", {"Mu": 0.2, "Sigma": 0.5}, 1.3, lambda x: st.lognorm.logpdf(x, 0.5, scale=math.exp(0.2)))])
+def test_bayesian_evaluate_custom_with_other_priors(dist, params, x, ref):
+    """The other univariate priors' getLogDensity (exponential / laplace /
+    cauchy / logNormal .cpp.base) in the MAP evaluator: the reference's
+    expression order exactly, and the density itself against scipy."""
+    e = korali.Experiment()
+    e["Problem"]["Type"] = "Bayesian/Custom"
+    e["Problem"]["Likelihood Model"] = lambda s: s.__setitem__("logLikelihood", 0.0)
+    e["Distributions"][0]["Name"] = "P"
+    e["Distributions"][0]["Type"] = dist
+    for k, v in params.items():
+        e["Distributions"][0][k] = v
+    e["Variables"][0]["Name"] = "x"
+    e["Variables"][0]["Prior Distribution"] = "P"
+    lp = L._bayesian_evaluate(e, [x])["logPrior"]
+    a, b = list(params.values())
+    exact = {"Univariate/Exponential": lambda: -math.log(b) - (x - a) / b,
+             "Univariate/Laplace": lambda: -math.log(2.0 * b) - abs(x - a) / b,
+             "Univariate/Cauchy": lambda: -math.log(b * math.pi) - math.log(1.0 + (x - a) * (x - a) / (b * b)),
+             "Univariate/LogNormal": lambda: (-0.5 * math.log(2 * math.pi) - math.log(b)) - math.log(x)
+             - 0.5 * ((math.log(x) - a) / b) ** 2}[dist]()
+    assert lp == exact
+    assert lp == pytest.approx(ref(x), rel=1e-13)
 
 
 @pytest.mark.parametrize("dist,drop", [("Univariate/Normal", "Standard Deviation"), ("Univariate/Normal", "Mean"),
