@@ -1590,11 +1590,18 @@ struct HostMt {
     mti = MT_N;
   }
   uint32_t get() {
-    if (mti >= MT_N) {
-      for (int k = 0; k < MT_N; k++) mt[k] = mt_next(mt[k], mt[(k + 1) % MT_N], mt[(k + MT_M) % MT_N]);
-      mti = 0;
-    }
+    if (mti >= MT_N) refill();
     return mt_temper(mt[mti++]);
+  }
+  // the block regeneration in GSL's three ranges (no index wrap inside the
+  // loops: the multinomial's walk draws ~P words per generation on the
+  // host's critical path)
+  void refill() {
+    int k = 0;
+    for (; k < MT_N - MT_M; k++) mt[k] = mt_next(mt[k], mt[k + 1], mt[k + MT_M]);
+    for (; k < MT_N - 1; k++) mt[k] = mt_next(mt[k], mt[k + 1], mt[k + MT_M - MT_N]);
+    mt[MT_N - 1] = mt_next(mt[MT_N - 1], mt[0], mt[MT_M - 1]);
+    mti = 0;
   }
   double uniform() { return get() / 4294967296.0; }
   void save(unsigned char *b) const {
