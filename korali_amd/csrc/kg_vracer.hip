@@ -847,7 +847,7 @@ __device__ __forceinline__ int u16v(unsigned short h) {
 // divisions are exact no-ops at sigma 1.0, but the retrace walk then also
 // loads each entry's environment id, so the plain form does without)
 template <bool RR>
-__global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
+__global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er, const unsigned *mb,
                                                  const float *__restrict__ out, float *__restrict__ G,
                                                  unsigned long long advance, int staged) {
   __shared__ unsigned s_mb[MB_META];
@@ -919,7 +919,7 @@ __global__ __launch_bounds__(256) void k_vr_meta(Params P, State *st, Replay er,
   constexpr int WCAP = 6144;
   __shared__ float w_v[WCAP], w_t[WCAP], w_r[WCAP];
   __shared__ unsigned short w_row[WCAP];
-  __shared__ int s_woff[MB_META + 1], s_fk[MB_META], s_wsum[4];
+  __shared__ int s_woff[MB_META + 1], s_fk[MB_META], s_wsum[16];  // (one per wave, up to 1024 threads)
   __shared__ float s_wretn[MB_META];
   {
     // walking rows (the last mini-batch row of each episode): length, initial
@@ -2134,7 +2134,16 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
   }
   const bool drawIn = !fused && vr_draw_in() && P.S <= 16;
   const unsigned long long advance = ((fused || drawIn) && !forced) ? (unsigned long long)B : 0ULL;
-  hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er,
+  // threads of the one-workgroup metadata kernel: 512 stage every walk entry
+  // of a C5 update (~5 500) in one pass of 16 loads in flight per thread
+  // (staging 4.7 -> 2.9 us, update 64.1 -> 60.8 us, round 5; 1024 would cap
+  // the kernel at 128 VGPRs and spill; KORALI_AMD_VR_META_TPB=256 for A/B)
+  static const int metaTpb = [] {
+    const char *e = getenv("KORALI_AMD_VR_META_TPB");
+    const int v = e ? atoi(e) : 512;
+    return (v == 256 || v == 512) ? v : 512;
+  }();
+  hipLaunchKernelGGL(P.rr ? k_vr_meta<true> : k_vr_meta<false>, dim3(1), dim3(metaTpb), 0, h->stream, P, h->st, h->er,
                      (const unsigned *)h->mb, (const float *)h->out, h->G, advance, vr_staged_walks() ? 1 : 0);
   // backward (DeepSupervisor, Direct Gradient) on the B mini-batch rows
   const size_t rs = h->rowsMax * P.H;
