@@ -491,11 +491,11 @@ __device__ inline long long phys(const State *s, long long R, long long i) {
 // the mini-batch's sorted replay ids into key[0, B) (every thread of the
 // workgroup; the draw counter is advanced by the caller's last kernel)
 __device__ __forceinline__ void vr_minibatch_keys(const Params &P, const State *st, const unsigned *forced,
-                                                  unsigned *key) {
+                                                  unsigned *key, unsigned long long ctr_ahead = 0) {
   const int t = threadIdx.x, nt = blockDim.x, B = P.B;
   int n2 = 1;
   while (n2 < B) n2 <<= 1;
-  const unsigned long long ctr = st->mb_counter;
+  const unsigned long long ctr = st->mb_counter + ctr_ahead;
   const float sz1 = (float)(st->size - 1);
   for (int i = t; i < n2; i += nt) {
     unsigned id = 0xffffffffu;
@@ -560,6 +560,42 @@ __global__ __launch_bounds__(1024) void k_vr_minibatch(Params P, State *st, Repl
   for (int i = t; i < B; i += nt) mb[i] = key[i];
   __syncthreads();
   if (t == 0) st->mb_counter = ctr + (forced ? 0 : (unsigned long long)B);
+}
+
+// A graph of policy updates (kg_vracer_train_policy) draws its mini-batches
+// up front: workgroup u draws and sorts update u's ids from the draw counter
+// + u B (the replay memory's size does not change between the environment
+// steps, and each update's k_vr_meta advances the counter by B), so the ids
+// are those the updates would draw one by one.
+__global__ __launch_bounds__(256) void k_vr_draw_ahead(Params P, const State *st, unsigned *keys) {
+  __shared__ unsigned key[MAXB];
+  vr_minibatch_keys(P, st, (const unsigned *)nullptr, key, (unsigned long long)blockIdx.x * P.B);
+  for (int i = threadIdx.x; i < P.B; i += blockDim.x) keys[(size_t)blockIdx.x * P.B + i] = key[i];
+}
+
+// ... and each update then gathers its rows while forming the input layer
+// (k_vr_minibatch's gather + k_vr_fwd_in's products, same order, one launch):
+// thread (m, o) loads row m's state (row b < B: entry b's state, row B + b
+// its truncated state), writes it to Xmb (o = 0) and forms tanh(W x + b)[o].
+__global__ void k_vr_gather_in(Params P, const State *st, Replay er, const unsigned *__restrict__ keys,
+                               unsigned *mb, float *Xmb, const float *__restrict__ W, const float *__restrict__ bias,
+                               float *__restrict__ Y) {
+  const int B = P.B, S = P.S, H = P.H;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2LL * B * H) return;
+  const int m = (int)(e / H), o = (int)(e % H), b = m < B ? m : m - B;
+  const unsigned long long R = (unsigned long long)P.R, base = (st->total - st->size) % R;
+  unsigned long long q = base + keys[b];
+  if (q >= R) q -= R;
+  const float *src = (m < B ? er.st : er.tst) + (long long)q * S;
+  float x[MAXS];
+  for (int i = 0; i < S; i++) x[i] = src[i];
+  if (o == 0)
+    for (int i = 0; i < S; i++) Xmb[(long long)m * S + i] = x[i];
+  if (e < B) mb[e] = keys[e];
+  float acc = 0.f;
+  for (int i = 0; i < S; i++) acc += W[o * S + i] * x[i];
+  Y[e] = tanhf(acc + bias[o]);
 }
 
 // The mini-batch draw fused with the input layer (round 5): every workgroup
@@ -1950,6 +1986,8 @@ struct kg_vracer_s {
   // memory, so one capture serves every later update)
   hipGraphExec_t upd_graph = nullptr;
   int upd_graph_n = 0;
+  unsigned *drawKeys = nullptr;  // the graph's mini-batch ids, drawn up front (upd_graph_n x B)
+  size_t drawCap = 0;
   // every device buffer in allocation order (kg_vracer_save_state / _load_state)
   std::vector<std::pair<void **, size_t>> bufs;
 };
@@ -2110,7 +2148,7 @@ static bool vr_staged_walks() {
   return !(e && *e == '0');
 }
 
-int vr_update(kg_vracer_t h, const unsigned *forced) {
+int vr_update(kg_vracer_t h, const unsigned *forced, const unsigned *drawn = nullptr) {
   const Params &P = h->P;
   const int B = P.B;
   KG_CHECK(h->st_host->size >= 2, "vracer: policy updates need at least two experiences in the replay memory");
@@ -2123,6 +2161,11 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
     hipLaunchKernelGGL(k_vr_fwd_fused<true>, dim3(vr_blocks(2 * B, FR)), dim3(256), 0, h->stream, P, 2 * B,
                        (const float *)nullptr, (const float *)h->theta, (const long long *)h->offs, h->acts,
                        (long long)h->rowsMax, h->out, (const State *)h->st, h->er, h->mb, forced, h->Xmb);
+  } else if (drawn) {  // ids drawn ahead by the graph's k_vr_draw_ahead
+    hipLaunchKernelGGL(k_vr_gather_in, dim3(vr_blocks(2LL * B * P.H, 256)), dim3(256), 0, h->stream, P,
+                       (const State *)h->st, h->er, drawn, h->mb, h->Xmb, (const float *)(h->theta + h->offW[0]),
+                       (const float *)(h->theta + h->offb[0]), h->acts);
+    if (vr_forward(h, h->Xmb, 2 * B, h->out, true)) return 1;
   } else if (vr_draw_in() && P.S <= 16) {
     hipLaunchKernelGGL(k_vr_minibatch_in, dim3(vr_blocks(2 * B, MI)), dim3(256), 0, h->stream, P, (const State *)h->st,
                        h->er, h->mb, forced, h->Xmb, (const float *)(h->theta + h->offW[0]),
@@ -2132,8 +2175,8 @@ int vr_update(kg_vracer_t h, const unsigned *forced) {
     hipLaunchKernelGGL(k_vr_minibatch, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->er, h->mb, forced, h->Xmb);
     if (vr_forward(h, h->Xmb, 2 * B, h->out)) return 1;
   }
-  const bool drawIn = !fused && vr_draw_in() && P.S <= 16;
-  const unsigned long long advance = ((fused || drawIn) && !forced) ? (unsigned long long)B : 0ULL;
+  const bool drawIn = !fused && !drawn && vr_draw_in() && P.S <= 16;
+  const unsigned long long advance = ((fused || drawIn || drawn) && !forced) ? (unsigned long long)B : 0ULL;
   // threads of the one-workgroup metadata kernel: 512 stage every walk entry
   // of a C5 update (~5 500) in one pass of 16 loads in flight per thread
   // (staging 4.7 -> 2.9 us, update 64.1 -> 60.8 us, round 5; 1024 would cap
@@ -2452,6 +2495,7 @@ int kg_vracer_destroy(kg_vracer_t h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->upd_graph) (void)hipGraphExecDestroy(h->upd_graph);
+  if (h->drawKeys) kg::dev_release(h->drawKeys);
   void *ptrs[] = {h->offs, h->theta, h->grad, h->m1, h->m2, h->X, h->Xmb, h->Xs, h->acts, h->out, h->outF, h->G, h->dZ, h->dHa,
                   h->dHb, h->mb, h->forced_mb, h->forced_noise, h->st, h->er.st, h->er.act, h->er.rew, h->er.tst,
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
@@ -2693,6 +2737,13 @@ int kg_vracer_rescale_states(kg_vracer_t h) {
   return vr_read_state(h);
 }
 
+// a graph's mini-batches drawn up front (k_vr_draw_ahead + k_vr_gather_in;
+// KORALI_AMD_VR_DRAW_AHEAD=1; default: k_vr_minibatch + k_vr_fwd_in per update)
+static bool vr_draw_ahead() {
+  const char *e = getenv("KORALI_AMD_VR_DRAW_AHEAD");
+  return e && *e == '1';
+}
+
 // updates per captured graph (KORALI_AMD_VR_GRAPH; 0: every update launched
 // kernel by kernel).  The fused forward pass advances a host-chosen cursor,
 // so it is never captured.
@@ -2707,10 +2758,23 @@ static int vr_graph_len(const Params &P) {
 static int vr_capture_updates(kg_vracer_t h, int n) {
   const int prof = h->prof;
   h->prof = 0;  // no stage events inside the graph
+  const size_t nk = (size_t)n * h->P.B;
+  if (h->drawCap < nk) {  // (before the capture: no allocation inside it)
+    if (h->drawKeys) kg::dev_release(h->drawKeys);
+    h->drawKeys = nullptr;
+    h->drawCap = 0;
+    KG_HIP(kg::dev_alloc((void **)&h->drawKeys, nk * sizeof(unsigned)));
+    h->drawCap = nk;
+  }
   hipGraph_t g = nullptr;
   KG_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   int rc = 0;
-  for (int i = 0; i < n && !rc; i++) rc = vr_update(h, nullptr);
+  if (vr_draw_ahead()) {
+    hipLaunchKernelGGL(k_vr_draw_ahead, dim3(n), dim3(256), 0, h->stream, h->P, (const State *)h->st, h->drawKeys);
+    for (int i = 0; i < n && !rc; i++) rc = vr_update(h, nullptr, h->drawKeys + (size_t)i * h->P.B);
+  } else {
+    for (int i = 0; i < n && !rc; i++) rc = vr_update(h, nullptr);
+  }
   const hipError_t e = hipStreamEndCapture(h->stream, &g);
   h->prof = prof;
   if (rc || e != hipSuccess || !g) {

@@ -52,6 +52,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     c5di) for v in 0 1; do step c5_di$v 300 env KORALI_AMD_VR_DRAW_IN=$v python bench.py --workload c5 --steps 60 --warmup 5 --no-cpu-baseline || exit 1; done ;;
     metat) for v in 512; do step vrt_m$v 600 env KORALI_AMD_VR_META_TPB=$v python -u -m pytest tests/test_gpu_vracer.py -x -q --timeout 300 --timeout-method thread || exit 1; done ;;
     metab) for v in 256 512; do step c5_m$v 300 env KORALI_AMD_VR_META_TPB=$v python bench.py --workload c5 --steps 60 --warmup 5 --no-cpu-baseline || exit 1; done ;;
+    c5da) for v in 1 0; do step c5_da$v 300 env KORALI_AMD_VR_DRAW_AHEAD=$v python bench.py --workload c5 --steps 60 --warmup 5 --no-cpu-baseline || exit 1; done ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     occ2) step occ_pair 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest -x -v -s --timeout 250 --timeout-method thread tests/test_cxx_api.py::test_reference_idioms_run_cmaes_direct tests/test_gpu_baseline_shapes.py::test_c4_shape_two_generations_bit_exact ; step occ_coll 300 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -m gpu -x -v -s --timeout 250 --timeout-method thread -k c4_shape_two ;;
     testsdbg) step testsdbg 1100 env KORALI_AMD_DEBUG_OCC=1 python -u -m pytest tests -x -v -s -m gpu --timeout 300 --timeout-method thread ;;

@@ -109,8 +109,8 @@ def test_draw_with_input_layer_equals_separate_kernels(monkeypatch):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("glen", ["4", "5"])
-def test_graph_replayed_updates_equal_kernel_launches(monkeypatch, glen):
+@pytest.mark.parametrize("glen,ahead", [("4", "0"), ("5", "0"), ("4", "1"), ("5", "1")])
+def test_graph_replayed_updates_equal_kernel_launches(monkeypatch, glen, ahead):
     """trainPolicy's updates replayed from a captured graph of glen updates
     (11 updates: whole graphs, then the rest launched kernel by kernel) leave
     the hyperparameters, Adam moments, retrace values and importance weights
@@ -118,6 +118,7 @@ def test_graph_replayed_updates_equal_kernel_launches(monkeypatch, glen):
     ag, th = fill_replay(64, 2, 8, 90, 600)
     runs = []
     monkeypatch.setenv("KORALI_AMD_VR_FUSED", "0")
+    monkeypatch.setenv("KORALI_AMD_VR_DRAW_AHEAD", ahead)  # (the graph's mini-batches drawn up front)
     for g in (glen, "0"):
         monkeypatch.setenv("KORALI_AMD_VR_GRAPH", g)
         d = device(hidden_size=64, hidden_layers=2, environments=8, mini_batch_size=64, replay_maximum_size=600,
