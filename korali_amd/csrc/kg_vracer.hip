@@ -177,11 +177,25 @@ __global__ __launch_bounds__(256) void k_vr_fwd_out(int M, int H, int O, const f
 #pragma unroll
   for (int o = 0; o < MAXO; o++) acc[o] = 0.f;
   const float *h = Hs + (long long)m * H;
-  for (int i = lane; i < H; i += 64) {
-    const float x = h[i];
+  // four columns' loads in flight per lane before their products (each
+  // lane's sums still run over its columns in ascending order)
+  constexpr int U = 4;
+  for (int i0 = lane; i0 < H; i0 += 64 * U) {
+    float xs[U], ws[U][MAXO];
 #pragma unroll
-    for (int o = 0; o < MAXO; o++)
-      if (o < O) acc[o] += W[o * H + i] * x;
+    for (int u = 0; u < U; u++) {
+      const int i = i0 + 64 * u;
+      xs[u] = i < H ? h[i] : 0.f;
+#pragma unroll
+      for (int o = 0; o < MAXO; o++) ws[u][o] = (o < O && i < H) ? W[o * H + i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (i0 + 64 * u < H) {
+#pragma unroll
+        for (int o = 0; o < MAXO; o++)
+          if (o < O) acc[o] += ws[u][o] * xs[u];
+      }
   }
 #pragma unroll
   for (int o = 0; o < MAXO; o++)
@@ -588,13 +602,22 @@ __global__ void k_vr_gather_in(Params P, const State *st, Replay er, const unsig
   unsigned long long q = base + keys[b];
   if (q >= R) q -= R;
   const float *src = (m < B ? er.st : er.tst) + (long long)q * S;
-  float x[MAXS];
-  for (int i = 0; i < S; i++) x[i] = src[i];
-  if (o == 0)
-    for (int i = 0; i < S; i++) Xmb[(long long)m * S + i] = x[i];
+  float x[MAXS], w[MAXS];  // (unrolled with guards: registers, every load in flight)
+#pragma unroll
+  for (int i = 0; i < MAXS; i++) {
+    x[i] = i < S ? src[i] : 0.f;
+    w[i] = i < S ? W[o * S + i] : 0.f;
+  }
+  if (o == 0) {
+#pragma unroll
+    for (int i = 0; i < MAXS; i++)
+      if (i < S) Xmb[(long long)m * S + i] = x[i];
+  }
   if (e < B) mb[e] = keys[e];
   float acc = 0.f;
-  for (int i = 0; i < S; i++) acc += W[o * S + i] * x[i];
+#pragma unroll
+  for (int i = 0; i < MAXS; i++)
+    if (i < S) acc += w[i] * x[i];
   Y[e] = tanhf(acc + bias[o]);
 }
 
