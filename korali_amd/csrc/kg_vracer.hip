@@ -331,12 +331,21 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
   if (t >= (long long)Bn * H) return;
   const int b = (int)(t / H), i = (int)(t % H);
   float dz[MAXO];  // (static indices only: loops unrolled to MAXO, o < O guarded)
+  float xo[MAXO], go[MAXO], wo[MAXO];
+  // every operand's load in flight first (the arithmetic below is unchanged)
+#pragma unroll
+  for (int o = 0; o < MAXO; o++) {
+    xo[o] = o < O ? out[b * O + o] : 0.f;
+    go[o] = o < O ? G[b * O + o] : 0.f;
+    wo[o] = o < O ? W[o * H + i] : 0.f;
+  }
+  const float y = Hs[(long long)b * H + i];
   float acc = 0.f;
 #pragma unroll
   for (int o = 0; o < MAXO; o++) {
     dz[o] = 0.f;
     if (o < O) {
-      float x = out[b * O + o], g = G[b * O + o];
+      float x = xo[o], g = go[o];
       x = x - P.shift[o];
       x = x / P.scale[o];
       g = g * P.scale[o];
@@ -345,14 +354,13 @@ __global__ void k_vr_bwd_out(int Bn, int H, int O, const float *__restrict__ G, 
         g = (float)((double)g * 0.5 * (1.0 + (double)nnx / sqrt((double)nnx * (double)nnx + 1.0)));
       }
       dz[o] = g;
-      acc += dz[o] * W[o * H + i];
+      acc += dz[o] * wo[o];
     }
   }
   if (i == 0)
 #pragma unroll
     for (int o = 0; o < MAXO; o++)
       if (o < O) dZ[b * O + o] = dz[o];
-  const float y = Hs[(long long)b * H + i];
   dH[t] = acc * (1.0f - y * y);
 }
 
