@@ -243,6 +243,13 @@ int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, siz
  * (window624 = 624 consecutive untempered words of a GSL mt19937 stream,
  * not starting at the seeding word 0).  Runs on the host, no device needed. */
 int kg_debug_mt_jump(const uint32_t *window624, uint64_t distance, uint32_t *out624);
+/* The host core's tridiagonalisation (phase A of CMAES::eigen,
+ * CMAES.cpp.base:896-938 → gsl_linalg_symmtd_decomp, run every generation
+ * from prepareGeneration :441) on a given matrix: C row-major N x N (lower
+ * triangle read); H (N x N): row i < N-2 = column i below the diagonal
+ * (H[i][0] = sd[i], the reflector's entries after it), tau (N), d (N),
+ * sd (N).  Runs on the host, no device needed. */
+int kg_debug_host_tridiag(size_t N, const double *C, double *H, double *tau, double *d, double *sd);
 /* Host-only check of the TMCMC resampling (no device call): `reps`
  * consecutive gsl_ran_multinomial draws (K categories, N trials) from one
  * mt19937 seeded with `seed`, by the exact conditional-binomial walk

@@ -29,7 +29,14 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offlo
 
 
 def sources():
-    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp")))
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".cpp", ".inc")))
+
+
+# host-core code of the library (the GSL-order tridiagonalisation,
+# kg_host_tridiag.cpp): g++, no FMA, one body per instruction set
+HOST_SRC = os.path.join(CSRC, "kg_host_tridiag.cpp")
+HOST_OBJ = os.path.join(CSRC, "kg_host_tridiag.o")
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-math-errno", "-Wall", "-Wno-psabi"]
 
 
 def _stale(target, deps):
@@ -55,7 +62,8 @@ def _run(cmd, verbose):
 def build(force=False, verbose=False):
     deps = sources() + [os.path.join(ROOT, "include", "korali_amd.h")]
     if force or _stale(LIB, deps):
-        _run([HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip")], verbose)
+        _run(["g++"] + HOST_FLAGS + ["-c", "-o", HOST_OBJ, HOST_SRC], verbose)
+        _run([HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip"), "-Wl," + HOST_OBJ], verbose)
     build_engine(force, verbose)
     return LIB
 

@@ -2854,6 +2854,65 @@ __global__ void __launch_bounds__(256) k_publish_dsd(int N, const double *__rest
   }
 }
 
+// tri == 6: the covariance's lower triangle into host-coherent memory (rows
+// of stride ldh, 16-byte stores of column pairs (c, c+1), c even, c <= r),
+// then a sequence flag the host tridiagonalisation busy-polls.
+__global__ void __launch_bounds__(1024) k_publish_c(int N, const double *__restrict__ C, double *hC, int ldh,
+                                                    unsigned long long *hflag, unsigned long long seq) {
+  const int pr = (N + 1) / 2;  // column pairs per row
+  for (int q = threadIdx.x; q < N * pr; q += blockDim.x) {
+    const int r = q / pr, c = 2 * (q - r * pr);
+    if (c > r) continue;
+    double2 v;
+    v.x = C[(size_t)r * N + c];
+    v.y = (c + 1 < N) ? C[(size_t)r * N + c + 1] : 0.0;
+    *(double2 *)(hC + (size_t)r * ldh + c) = v;
+  }
+  __threadfence_system();  // every thread's stores before the flag (system scope)
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// tri == 6: waits for the host tridiagonalisation's flag, then copies the
+// reflectors (row i: the N-1-i entries the unpack reads) and tau[0..N-2)
+// from host-coherent memory into the device workspace (system-scope loads:
+// no stale line of an earlier generation; 16 in flight per thread).
+__global__ void __launch_bounds__(256) k_fetch_h(int N, const double *hH, double *gH, double *tau,
+                                                 const unsigned long long *hflag, unsigned long long seq,
+                                                 unsigned int *errors) {
+  __shared__ int st;
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    for (unsigned spins = 0;; spins++) {
+      if (__hip_atomic_load(hflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) break;
+      if (spins > KG_SPIN_LIMIT) {
+        atomicOr(errors, KG_ERR_SYNC_TIMEOUT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    st = ok;
+  }
+  __syncthreads();
+  if (!st) return;
+  const int tot = (N - 2) * N;
+  for (int q0 = threadIdx.x; q0 < tot; q0 += 256 * 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int q = q0 + u * 256, i = q / N, r = q - i * N;
+      v[u] = (q < tot && r < N - 1 - i) ? ld_sys(hH + q) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int q = q0 + u * 256, i = q / N, r = q - i * N;
+      if (q < tot && r < N - 1 - i) gH[q] = v[u];
+    }
+  }
+  for (int i = threadIdx.x; i < N - 2; i += 256) tau[i] = ld_sys(hH + (size_t)N * N + i);
+}
+
 }  // namespace kg
 
 #include "kg_tridiag.hip"
@@ -2896,8 +2955,8 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(host_alloc(&host.meta, 4 * sizeof(int), fl));
     KG_HIP(host_alloc(&host.eval, (size_t)N * sizeof(double), fl));
     KG_HIP(host_alloc(&host.perm, (size_t)N * sizeof(int), fl));
-    KG_HIP(host_alloc(&hprog, 2 * sizeof(unsigned long long), fl));
-    hprog[0] = hprog[1] = 0;
+    KG_HIP(host_alloc(&hprog, 4 * sizeof(unsigned long long), fl));
+    hprog[0] = hprog[1] = hprog[2] = hprog[3] = 0;
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.hdr, host.hdr, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.cs, host.cs, 0));
     KG_HIP(hipHostGetDevicePointer((void **)&hmap.meta, host.meta, 0));
@@ -2930,6 +2989,24 @@ int EigenSolver::init(int N_, bool hostChase_) {
     if (!strcmp(e, "mw")) tri = 2;
   } else if (getenv("KORALI_AMD_EIGEN_MW_MIN") && !lds) {
     tri = mw2_fits(N) ? 5 : 2;
+  }
+  // the host core's tridiagonalisation (kg_host_tridiag.cpp) wherever the
+  // chase runs there too, up to KORALI_AMD_HOST_TRIDIAG_MAX (default 512;
+  // KORALI_AMD_TRIDIAG=host | a device kind forces one)
+  {
+    int hmax = 512;
+    if (const char *e = getenv("KORALI_AMD_HOST_TRIDIAG_MAX")) hmax = atoi(e);
+    const char *e = getenv("KORALI_AMD_TRIDIAG");
+    if (hostChase && N >= 3 && ((e && !strcmp(e, "host")) || (!e && N <= hmax))) tri = 6;
+  }
+  if (tri == 6) {
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    ldc = (N + 1) & ~1;
+    KG_HIP(host_alloc(&h_C, (size_t)N * ldc * sizeof(double), fl));
+    KG_HIP(hipHostGetDevicePointer((void **)&d_C_map, h_C, 0));
+    KG_HIP(host_alloc(&h_H, ((size_t)N * N + N) * sizeof(double), fl));
+    KG_HIP(hipHostGetDevicePointer((void **)&d_H_map, h_H, 0));
+    KG_CHECK(htri.init(N) == 0, "eigensolver: host tridiagonalisation workspace");
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
   sqDpp = true;  // measured round 4: 0.495 -> 0.450 ms per C2 tridiagonalisation (bench_sq0 / bench_sq1)
@@ -2998,7 +3075,7 @@ EigenSolver::~EigenSolver() {
                   (void *)dprogDev})
     if (p) dev_release(p);
   for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
-                  (void *)host.perm, (void *)hprog})
+                  (void *)host.perm, (void *)hprog, (void *)h_C, (void *)h_H})
     if (p) host_release(p);
   if (side) stream_release(side);
   if (ev_dsd) (void)hipEventDestroy(ev_dsd);
@@ -3013,6 +3090,14 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
                            double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
   begun = true;
   if (diagonal) return 0;  // k_eigen_diag runs in run_finish
+  if (tri == 6) {  // C to the host core; the rest waits for it in run_finish
+    cSeq = chaseSeq + 1;
+    if (prof) prof(profCtx, "eigen_publish_c", 0);
+    hipLaunchKernelGGL(k_publish_c, dim3(1), dim3(1024), 0, s, N, C, d_C_map, ldc, dprog + 2, cSeq);
+    KG_HIP(hipGetLastError());
+    if (prof) prof(profCtx, "eigen_publish_c", 1);
+    return 0;
+  }
   const size_t matb = lds ? eig_mat_bytes(N) : 0;
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
@@ -3071,6 +3156,12 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
     KG_HIP(hipGetLastError());
     KG_HIP(hipEventRecord(ev_chase, side));
   }
+  return launch_unpack(s, prof, profCtx);
+}
+
+// Phase B: Q from the reflectors in gH / tau (symmtd_unpack)
+int EigenSolver::launch_unpack(hipStream_t s, ProfileFn prof, void *profCtx) {
+  const size_t matb = lds ? eig_mat_bytes(N) : 0;
   if (prof) prof(profCtx, "eigen_unpack", 0);
   if (lds)
     hipLaunchKernelGGL(k_unpack<true>, dim3(1), dim3(1024), matb + 2 * N * sizeof(double), s, N, gH, tau, gQt);
@@ -3104,6 +3195,16 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     // the apply kernel is queued behind the unpack and consumes the Givens
     // rotations as this core's serial chase publishes them
     const unsigned long long seq = ++chaseSeq;
+    if (tri == 6) {
+      // the reflectors' copy and the unpack are queued now and start the
+      // moment the host core publishes them
+      if (prof) prof(profCtx, "eigen_fetch_h", 0);
+      hipLaunchKernelGGL(k_fetch_h, dim3(1), dim3(256), 0, s, N, (const double *)d_H_map, gH, tau,
+                         (const unsigned long long *)(dprog + 3), seq, errors);
+      KG_HIP(hipGetLastError());
+      if (prof) prof(profCtx, "eigen_fetch_h", 1);
+      if (launch_unpack(s, prof, profCtx)) return 1;
+    }
     if (prof) prof(profCtx, "eigen_apply", 0);
     EigRec mr = hmap;
     // the fetcher workgroup (0) + one workgroup per 4 rows (16 with 16-lane
@@ -3124,6 +3225,26 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
                              dim3((N + rows - 1) / rows + 1), dim3(APPLY_TPB), args, apply_lds_bytes(N, rows), s,
                              /*prefer_plain=*/true));
     }
+    if (tri == 6) {
+      if (prof) prof(profCtx, "eigen_c_wait", 2);
+      const auto t0 = std::chrono::steady_clock::now();
+      while (__atomic_load_n(hprog + 2, __ATOMIC_ACQUIRE) != cSeq) {  // busy-wait for C (µs)
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+          KG_HIP(hipStreamSynchronize(s));
+          KG_CHECK(false, "eigensolver: the covariance never arrived on the host");
+        }
+      }
+      if (prof) prof(profCtx, "eigen_c_wait", 3);
+      if (prof) prof(profCtx, "eigen_tridiag_host", 2);
+      const auto t1 = std::chrono::steady_clock::now();
+      htri.run(h_C, ldc, h_H, h_H + (size_t)N * N, h_dsd, h_dsd + N);
+      last_host_tridiag_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+      __builtin_ia32_sfence();
+      __atomic_store_n(hprog + 3, seq, __ATOMIC_RELEASE);  // the device copies H / tau and unpacks
+      __builtin_ia32_sfence();
+      if (prof) prof(profCtx, "eigen_tridiag_host", 3);
+    } else {
     if (prof) prof(profCtx, "eigen_dsd_wait", 2);
     {  // busy-wait for the tridiagonal (µs, not an interrupt wake-up)
       const auto t0 = std::chrono::steady_clock::now();
@@ -3136,6 +3257,7 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
       }
     }
     if (prof) prof(profCtx, "eigen_dsd_wait", 3);
+    }
     if (prof) prof(profCtx, "eigen_chase_host", 2);
     EigRec hr = host;
     chase_publish(hprog, chase_word(seq, 0, 0));
@@ -3166,3 +3288,17 @@ int EigenSolver::run(const double *C, int diagonal, double *B, double *D, double
 }
 
 }  // namespace kg
+
+extern "C" int kg_debug_host_tridiag(size_t N, const double *C, double *H, double *tau, double *d, double *sd) {
+  if (!C || !H || !tau || !d || !sd || N == 0 || N > 65536) {
+    kg::set_error("kg_debug_host_tridiag: null argument or bad order");
+    return 1;
+  }
+  kg::HostTridiag t;
+  if (t.init((int)N)) {
+    kg::set_error("kg_debug_host_tridiag: out of memory");
+    return 1;
+  }
+  t.run(C, (int)N, H, tau, d, sd);
+  return 0;
+}

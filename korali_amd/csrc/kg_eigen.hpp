@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "kg_common.hpp"
+#include "kg_host_tridiag.hpp"
 
 namespace kg {
 
@@ -39,11 +40,21 @@ class EigenSolver {
   }
   bool hostChase = true;
   int tridiag_kind() const { return tri; }  // (diagnostics)
+  // host-core tridiagonalisation (tri == 6): wall time of the last one (ms)
+  double last_host_tridiag_ms = 0.0;
 
  private:
   int N = 0, maxRot = 0;
   bool lds = true;
-  int tri = 0;  // tridiagonalisation kernel: 0 k_tridiag (LDS), 1 k_tridiag_1wg, 2 k_tridiag_mw, 3 k_tridiag_1wg2, 4 k_tridiag_sq, 5 k_tridiag_mw2
+  int tri = 0;  // tridiagonalisation kernel: 0 k_tridiag (LDS), 1 k_tridiag_1wg, 2 k_tridiag_mw, 3 k_tridiag_1wg2, 4 k_tridiag_sq, 5 k_tridiag_mw2, 6 host core
+  int launch_unpack(hipStream_t s, ProfileFn prof, void *profCtx);
+  // tri == 6: C's lower triangle reaches the host through host-coherent
+  // memory (k_publish_c), the host writes the reflectors + tau back
+  // (k_fetch_h copies them to gH / tau ahead of the unpack)
+  HostTridiag htri;
+  double *h_C = nullptr, *d_C_map = nullptr, *h_H = nullptr, *d_H_map = nullptr;
+  int ldc = 0;  // row stride of h_C (even: 16-byte rows)
+  unsigned long long cSeq = 0;
   double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
          *chaseWork = nullptr;
   unsigned long long *comm = nullptr;  // in-launch hand-off granules (N > 128 tridiagonalisation)

@@ -804,6 +804,10 @@ static void symmtd_decomp(size_t N, double *A, double *tau)
   }
 }
 
+/* gsl_linalg_symmtd_decomp alone (checker of the device library's host
+ * tridiagonalisation, kg_debug_host_tridiag); tau needs N - 1 entries */
+void kr_symmtd_decomp(size_t N, double *A, double *tau) { symmtd_decomp(N, A, tau); }
+
 /* gsl_linalg_householder_hm(tau, h (h0 := 1), Q[i+1:, i+1:]) */
 static void householder_hm(size_t n, double tau, const double *h, size_t hinc, double *Q, size_t lda)
 {

@@ -57,6 +57,7 @@ double kr_dnrm2(size_t n, const double *x, size_t inc);
  * destroyed; evec row-major, column i = eigenvector i.  Returns #qrsteps. */
 size_t kr_eigen_symmv(size_t n, double *A, double *eval, double *evec);
 size_t kr_eigen_symmv_unsorted(size_t n, double *A, double *eval, double *evec);
+void kr_symmtd_decomp(size_t N, double *A, double *tau); /* linalg/symmtd.c alone */
 size_t kr_qr_chase(size_t N, double *d, double *sd, double *cs, size_t maxRot);
 double kr_chi2inv_068(size_t n); /* gsl_cdf_chisq_Pinv(0.68, n), n <= 128 */
 int kr_cholesky(size_t n, double *A); /* 0 ok, 1 not positive definite */

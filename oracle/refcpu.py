@@ -48,6 +48,7 @@ def lib(variant="cr"):
         L.kr_eigen_symmv.argtypes = [sz, dp, dp, dp]
         L.kr_eigen_symmv.restype = sz
         L.kr_qr_chase.argtypes = [sz, dp, dp, dp, sz]
+        L.kr_symmtd_decomp.argtypes = [sz, dp, dp]
         L.kr_qr_chase.restype = sz
         L.kr_cholesky.argtypes = [sz, dp]
         L.kr_cholesky.restype = C.c_int
