@@ -2855,23 +2855,39 @@ __global__ void __launch_bounds__(256) k_publish_dsd(int N, const double *__rest
 }
 
 // tri == 6: the covariance's lower triangle into host-coherent memory (rows
-// of stride ldh, 16-byte stores of column pairs (c, c+1), c even, c <= r),
-// then a sequence flag the host tridiagonalisation busy-polls.
-__global__ void __launch_bounds__(1024) k_publish_c(int N, const double *__restrict__ C, double *hC, int ldh,
-                                                    unsigned long long *hflag, unsigned long long seq) {
-  const int pr = (N + 1) / 2;  // column pairs per row
-  for (int q = threadIdx.x; q < N * pr; q += blockDim.x) {
-    const int r = q / pr, c = 2 * (q - r * pr);
-    if (c > r) continue;
-    double2 v;
-    v.x = C[(size_t)r * N + c];
-    v.y = (c + 1 < N) ? C[(size_t)r * N + c + 1] : 0.0;
-    *(double2 *)(hC + (size_t)r * ldh + c) = v;
+// of stride ldh, 16-byte stores of column pairs (c, c+1), c even, c <= r;
+// one wave per row, rows dealt round-robin over the workgroups), then a
+// sequence flag the host tridiagonalisation busy-polls.  Every thread fences
+// its stores at system scope before its workgroup counts itself done; the
+// last workgroup to finish (device-scope counter, reset by it for the next
+// launch) publishes the flag.
+constexpr int PUBC_WAVES = 4;
+__global__ void __launch_bounds__(64 * PUBC_WAVES) k_publish_c(int N, const double *__restrict__ C, double *hC, int ldh,
+                                                               unsigned long long *hflag, unsigned long long seq,
+                                                               unsigned int *done) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = gridDim.x * PUBC_WAVES;
+  for (int r = blockIdx.x * PUBC_WAVES + w; r < N; r += nw) {
+    const double *src = C + (size_t)r * N;
+    double *dst = hC + (size_t)r * ldh;
+    for (int c = 2 * lane; c <= r; c += 128) {
+      double2 v;
+      v.x = src[c];
+      v.y = (c + 1 < N) ? src[c + 1] : 0.0;
+      *(double2 *)(dst + c) = v;
+    }
   }
-  __threadfence_system();  // every thread's stores before the flag (system scope)
+  __threadfence_system();  // this thread's stores before the count (system scope)
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {  // every workgroup's stores are out
+      __threadfence_system();
+      *done = 0;
+      __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
+inline int pubc_groups(int N) { return std::max(1, std::min(64, (N + PUBC_WAVES - 1) / PUBC_WAVES)); }
 
 // tri == 6: waits for the host tridiagonalisation's flag, then copies the
 // reflectors (row i: the N-1-i entries the unpack reads) and tau[0..N-2)
@@ -3007,6 +3023,8 @@ int EigenSolver::init(int N_, bool hostChase_) {
     KG_HIP(host_alloc(&h_H, ((size_t)N * N + N) * sizeof(double), fl));
     KG_HIP(hipHostGetDevicePointer((void **)&d_H_map, h_H, 0));
     KG_CHECK(htri.init(N) == 0, "eigensolver: host tridiagonalisation workspace");
+    KG_HIP(dev_alloc(&pubDone, 64));
+    if (zero_fill(pubDone, 64)) return 1;
   }
   if (const char *e = getenv("KORALI_AMD_T1_FLAGS")) t1flags = atoi(e);
   sqDpp = true;  // measured round 4: 0.495 -> 0.450 ms per C2 tridiagonalisation (bench_sq0 / bench_sq1)
@@ -3072,7 +3090,7 @@ EigenSolver::~EigenSolver() {
   drain();
   for (void *p : {(void *)gA, (void *)gH, (void *)gQt, (void *)gWork, (void *)tau, (void *)dsd, (void *)chaseWork,
                   (void *)dev.hdr, (void *)dev.cs, (void *)dev.meta, (void *)dev.eval, (void *)dev.perm, (void *)comm,
-                  (void *)dprogDev})
+                  (void *)dprogDev, (void *)pubDone})
     if (p) dev_release(p);
   for (void *p : {(void *)h_dsd, (void *)host.hdr, (void *)host.cs, (void *)host.meta, (void *)host.eval,
                   (void *)host.perm, (void *)hprog, (void *)h_C, (void *)h_H})
@@ -3093,7 +3111,8 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   if (tri == 6) {  // C to the host core; the rest waits for it in run_finish
     cSeq = chaseSeq + 1;
     if (prof) prof(profCtx, "eigen_publish_c", 0);
-    hipLaunchKernelGGL(k_publish_c, dim3(1), dim3(1024), 0, s, N, C, d_C_map, ldc, dprog + 2, cSeq);
+    hipLaunchKernelGGL(k_publish_c, dim3(pubc_groups(N)), dim3(64 * PUBC_WAVES), 0, s, N, C, d_C_map, ldc, dprog + 2,
+                       cSeq, pubDone);
     KG_HIP(hipGetLastError());
     if (prof) prof(profCtx, "eigen_publish_c", 1);
     return 0;

@@ -54,6 +54,7 @@ class EigenSolver {
   HostTridiag htri;
   double *h_C = nullptr, *d_C_map = nullptr, *h_H = nullptr, *d_H_map = nullptr;
   int ldc = 0;  // row stride of h_C (even: 16-byte rows)
+  unsigned int *pubDone = nullptr;  // k_publish_c's workgroup counter (device memory)
   unsigned long long cSeq = 0;
   double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
          *chaseWork = nullptr;

@@ -2741,8 +2741,10 @@ int kg_tmcmc_create(const kg_tmcmc_cfg *cfg, kg_tmcmc_t *out) {
   for (size_t d = 0; cfg->prior_kind && d < cfg->variable_count; d++) {
     KG_CHECK(cfg->prior_kind[d] >= KG_PRIOR_UNIFORM && cfg->prior_kind[d] <= KG_PRIOR_LOGNORMAL,
              "prior_kind entries must be KG_PRIOR_UNIFORM .. KG_PRIOR_LOGNORMAL");
-    KG_CHECK(cfg->prior_kind[d] == KG_PRIOR_UNIFORM || cfg->prior_max[d] > 0.0,  // the distributions' updateDistribution
-             "Incorrect scale parameter (Standard Deviation / Mean / Width / Scale / Sigma) of a prior distribution");
+    // the distributions' updateDistribution checks (exponential.cpp.base has none)
+    KG_CHECK(cfg->prior_kind[d] == KG_PRIOR_UNIFORM || cfg->prior_kind[d] == KG_PRIOR_EXPONENTIAL ||
+                 cfg->prior_max[d] > 0.0,
+             "Incorrect scale parameter (Standard Deviation / Width / Scale / Sigma) of a prior distribution");
   }
   KG_HIP(hipSetDevice(cfg->device));
   upload_dd_tables();

@@ -27,6 +27,7 @@
 #include "kg_common.hpp"
 #include "../../include/korali_amd.h"
 
+#include <unistd.h>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2889,8 +2890,11 @@ struct VrHostState {
 int kg_vracer_save_state(kg_vracer_t h, const char *path, const void *user, size_t user_bytes) {
   KG_CHECK(h && path && (user || !user_bytes), "vracer: null argument");
   KG_HIP(hipStreamSynchronize(h->stream));
-  FILE *f = fopen(path, "wb");
-  KG_CHECK(f, std::string("vracer: cannot write the training state file ") + path);
+  // written to <path>.tmp, flushed and synced, then renamed over <path>: a
+  // crash during a save leaves the previous checkpoint intact
+  const std::string tmpPath = std::string(path) + ".tmp";
+  FILE *f = fopen(tmpPath.c_str(), "wb");
+  KG_CHECK(f, std::string("vracer: cannot write the training state file ") + tmpPath);
   bool ok = fwrite(VR_STATE_MAGIC, 1, 8, f) == 8;
   const unsigned long long psz = sizeof(Params), nb = h->bufs.size(), ub = user_bytes;
   ok = ok && fwrite(&psz, 8, 1, f) == 1 && fwrite(&h->P, sizeof(Params), 1, f) == 1 && fwrite(&nb, 8, 1, f) == 1;
@@ -2908,12 +2912,16 @@ int kg_vracer_save_state(kg_vracer_t h, const char *path, const void *user, size
     tmp.resize(b.second);
     if (hipMemcpy(tmp.data(), *b.first, b.second, hipMemcpyDeviceToHost) != hipSuccess) {
       fclose(f);
+      remove(tmpPath.c_str());
       KG_CHECK(false, "vracer: reading a device buffer for the training state failed");
     }
     ok = fwrite(tmp.data(), 1, b.second, f) == b.second;
   }
+  ok = ok && fflush(f) == 0 && fsync(fileno(f)) == 0;
   ok = (fclose(f) == 0) && ok;
-  KG_CHECK(ok, std::string("vracer: writing the training state file failed: ") + path);
+  if (!ok) remove(tmpPath.c_str());
+  KG_CHECK(ok, std::string("vracer: writing the training state file failed: ") + tmpPath);
+  KG_CHECK(rename(tmpPath.c_str(), path) == 0, std::string("vracer: cannot move the training state into ") + path);
   return 0;
 }
 
@@ -2948,14 +2956,18 @@ int kg_vracer_load_state(kg_vracer_t h, const char *path, void *user, size_t use
   std::vector<unsigned char> u(ub);
   if (ub && fread(u.data(), 1, ub, f) != ub) return bad("truncated");
   if (ub > user_capacity) return bad("user block larger than the caller's buffer");
-  KG_HIP(hipStreamSynchronize(h->stream));
-  std::vector<unsigned char> tmp;
-  for (auto &b : h->bufs) {
-    tmp.resize(b.second);
-    if (fread(tmp.data(), 1, b.second, f) != b.second) return bad("truncated");
-    if (hipMemcpy(*b.first, tmp.data(), b.second, hipMemcpyHostToDevice) != hipSuccess) return bad("upload failed");
+  // every buffer is read into host memory before the first upload: a short
+  // or truncated file leaves the handle untouched
+  std::vector<std::vector<unsigned char>> all(h->bufs.size());
+  for (size_t i = 0; i < h->bufs.size(); i++) {
+    all[i].resize(h->bufs[i].second);
+    if (fread(all[i].data(), 1, all[i].size(), f) != all[i].size()) return bad("truncated");
   }
   fclose(f);
+  KG_HIP(hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i < h->bufs.size(); i++)
+    KG_CHECK(hipMemcpy(*h->bufs[i].first, all[i].data(), all[i].size(), hipMemcpyHostToDevice) == hipSuccess,
+             std::string("vracer: training state file ") + path + ": upload failed");
   h->P.seed = Pf.seed;
   if (h->upd_graph) {  // (captured with the old parameters)
     KG_HIP(hipGraphExecDestroy(h->upd_graph));

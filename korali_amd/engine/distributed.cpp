@@ -280,7 +280,15 @@ class RcclCollective : public Collective {
   CommDestroyFn commDestroy = nullptr;
   CommAbortFn commAbort = nullptr;
   ErrorStringFn errorString = nullptr;
-  std::mutex commMu;  // comm creation vs the watchdog's abort
+  // commMu guards `comm` and the in-flight count; it is never held across an
+  // RCCL call, so the watchdog's abort can always run.  A call that is in
+  // flight when the abort fires (e.g. blocked in the lazy connection set-up
+  // to the failed peer) is what ncclCommAbort exists to unblock: the abort
+  // then runs outside the lock, concurrently with it, the call returns an
+  // error and the rank leaves through check().
+  std::mutex commMu;
+  int inFlight = 0;
+  bool commAborted = false;
   std::unique_ptr<Watchdog> dog;
 
   RcclCollective(int r, int w, int port) : boot(r, w, port) {
@@ -298,17 +306,30 @@ class RcclCollective : public Collective {
     commAbort = (CommAbortFn)dlsym(lib, "ncclCommAbort");
     if (!getUniqueId || !commInitRank || !allGatherFn || !allReduceFn || !commDestroy || !errorString || !commAbort)
       dfail("librccl.so lacks an nccl* entry point");
-    dog.reset(new Watchdog(r, w, port + 1, [this] {
+    dog.reset(new Watchdog(r, w, port + 1, [this] { abortComm(); }));
+  }
+  // the watchdog's abort: marks the communicator aborted (no new call can
+  // take it) and aborts it -- under the lock when nothing is in flight,
+  // outside it when a call is (that call is unblocked by it)
+  void abortComm() {
+    void *c = nullptr;
+    {
       std::lock_guard<std::mutex> g(commMu);
-      if (comm) commAbort(comm);  // the collective kernels waiting for the failed rank end
-      comm = nullptr;
-    }));
+      if (!comm || commAborted) return;
+      commAborted = true;
+      if (inFlight == 0) {
+        commAbort(comm);
+        return;
+      }
+      c = comm;
+    }
+    commAbort(c);
   }
   ~RcclCollective() override {
     const bool failing = std::uncaught_exceptions() > 0;
-    dog->close(failing);  // (tells the other ranks first)
+    dog->close(failing);  // (tells the other ranks first; joins the watchdog)
     std::lock_guard<std::mutex> g(commMu);
-    if (comm) (failing ? commAbort : commDestroy)(comm);
+    if (comm && !commAborted) (failing ? commAbort : commDestroy)(comm);
   }
   std::string transport() const override { return "RCCL"; }
   bool failed() const override { return dog->aborted(); }
@@ -320,7 +341,10 @@ class RcclCollective : public Collective {
   // handle has selected its GPU (RCCL binds the calling thread's device)
   void ensureComm() {
     if (dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
-    if (comm) return;
+    {
+      std::lock_guard<std::mutex> g(commMu);
+      if (comm) return;
+    }
     NcclId id{};
     if (rank == 0) check(getUniqueId(&id), "ncclGetUniqueId");
     std::vector<NcclId> all((size_t)world);
@@ -328,21 +352,35 @@ class RcclCollective : public Collective {
     boot.gatherToAll(all.data(), sizeof(NcclId));  // (only the root's entry is used)
     void *c = nullptr;
     check(commInitRank(&c, world, all[0], rank), "ncclCommInitRank");
-    std::lock_guard<std::mutex> g(commMu);
-    if (dog->aborted()) {  // the abort fired while the communicator was being created: it never saw this one
+    bool late = false;
+    {
+      std::lock_guard<std::mutex> g(commMu);
+      late = dog->aborted();
+      if (!late) comm = c;
+    }
+    if (late) {  // the abort fired while the communicator was being created: it never saw this one
       commAbort(c);
       dfail("another rank failed; this rank's collectives were aborted");
     }
-    comm = c;
   }
-  // every enqueue holds commMu, so the watchdog's abort cannot free the
-  // communicator between the check and the call
+  // takes the communicator under the lock (counted in flight), runs the RCCL
+  // call without it
   template <class F>
   void enqueue(F &&call, const char *what) {
     ensureComm();
-    std::lock_guard<std::mutex> g(commMu);
-    if (!comm || dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
-    check(call(comm), what);
+    void *c = nullptr;
+    {
+      std::lock_guard<std::mutex> g(commMu);
+      if (!comm || commAborted || dog->aborted()) dfail("another rank failed; this rank's collectives were aborted");
+      c = comm;
+      inFlight++;
+    }
+    const int rc = call(c);
+    {
+      std::lock_guard<std::mutex> g(commMu);
+      inFlight--;
+    }
+    check(rc, what);
   }
   void allGather(const SolverBuffer &b, size_t count) override {
     double *p = (double *)b.devicePtr();

@@ -53,6 +53,28 @@ void check(int rc) {
   if (rc != 0) fail("%s", kg_last_error());
 }
 
+// A replicated evaluation under the Distributed conduit: `local` evaluates
+// this rank's share into its block of `buf`, then every rank all-gathers
+// `count` doubles per rank -- even a rank whose share threw, so no rank is
+// left waiting in the bootstrap -- and one failure flag per rank; a failure
+// anywhere is raised on every rank after the gathers (the failing rank's own
+// error there, the others name it).
+void replicatedGather(Collective &d, std::vector<double> &buf, size_t count, const std::function<void()> &local) {
+  std::exception_ptr err;
+  try {
+    local();
+  } catch (...) {
+    err = std::current_exception();
+  }
+  if (count) d.allGatherHost(buf.data(), count);
+  std::vector<double> flags((size_t)d.world, 0.0);
+  flags[(size_t)d.rank] = err ? 1.0 : 0.0;
+  d.allGatherHost(flags.data(), 1);
+  if (err) std::rethrow_exception(err);
+  for (int r = 0; r < d.world; r++)
+    if (flags[(size_t)r] != 0.0) fail("rank %d failed while evaluating its share of the samples (see its error).", r);
+}
+
 // Module::getModule: whitespace removed, case-insensitive compare
 std::string canon(const std::string &s) {
   std::string r;
@@ -872,9 +894,10 @@ struct CmaesModule : SolverModule {
         const size_t per = (rows + d.world - 1) / d.world, a = std::min(rows, per * d.rank),
                      b = std::min(rows, a + per);
         std::vector<double> buf((size_t)d.world * per * nc, 0.0);
-        for (size_t r = a; r < b; r++)
-          self->evaluateConstraints(X + r * N_, N_, buf.data() + ((size_t)d.rank * per + (r - a)) * nc);
-        d.allGatherHost(buf.data(), per * nc);
+        replicatedGather(d, buf, per * nc, [&] {
+          for (size_t r = a; r < b; r++)
+            self->evaluateConstraints(X + r * N_, N_, buf.data() + ((size_t)d.rank * per + (r - a)) * nc);
+        });
         std::copy(buf.begin(), buf.begin() + rows * nc, out);
         return 0;
       }
@@ -995,14 +1018,15 @@ struct CmaesModule : SolverModule {
     std::vector<double> X(lam * N), F(lam, 0.0), G(lam * gw, 0.0);
     check(kg_cmaes_get_candidates(h, X.data(), N));
     Function *f = bayesian ? nullptr : &getFunction(fn);
-    for (size_t i = a; i < b; i++) evaluateSample(gen, i, X, F, G, f);
     std::vector<double> buf(W * per * (1 + gw), 0.0);
-    for (size_t i = a; i < b; i++) {
-      double *row = buf.data() + (dist->rank * per + (i - a)) * (1 + gw);
-      row[0] = F[i];
-      std::copy(G.begin() + i * gw, G.begin() + (i + 1) * gw, row + 1);
-    }
-    dist->allGatherHost(buf.data(), per * (1 + gw));
+    replicatedGather(*dist, buf, per * (1 + gw), [&] {
+      for (size_t i = a; i < b; i++) evaluateSample(gen, i, X, F, G, f);
+      for (size_t i = a; i < b; i++) {
+        double *row = buf.data() + (dist->rank * per + (i - a)) * (1 + gw);
+        row[0] = F[i];
+        std::copy(G.begin() + i * gw, G.begin() + (i + 1) * gw, row + 1);
+      }
+    });
     for (size_t i = 0; i < lam; i++) {
       const double *row = buf.data() + i * (1 + gw);
       F[i] = row[0];
@@ -1265,14 +1289,15 @@ struct TmcmcModule : SolverModule {
         pmax[i] = mandatory(ds[k], "Maximum", "Distributions");
       } else {
         // the two parameters of each supported distribution and its
-        // updateDistribution check (exponential has none: a mean <= 0 fails here)
+        // updateDistribution check (exponential.cpp.base has none: a Mean <= 0
+        // is accepted, its log-density is then NaN / infinite as the reference's)
         struct Kind {
           const char *type, *a, *b, *what;
           int kind;
         };
         static const Kind kinds[] = {
             {"univariate/normal", "Mean", "Standard Deviation", "Standard Deviation parameter of Normal", KG_PRIOR_NORMAL},
-            {"univariate/exponential", "Location", "Mean", "Mean parameter of Exponential", KG_PRIOR_EXPONENTIAL},
+            {"univariate/exponential", "Location", "Mean", nullptr, KG_PRIOR_EXPONENTIAL},
             {"univariate/laplace", "Mean", "Width", "Width parameter of Laplace", KG_PRIOR_LAPLACE},
             {"univariate/cauchy", "Location", "Scale", "Scale parameter of Cauchy", KG_PRIOR_CAUCHY},
             {"univariate/lognormal", "Mu", "Sigma", "Sigma parameter of LogNormal", KG_PRIOR_LOGNORMAL}};
@@ -1286,7 +1311,7 @@ struct TmcmcModule : SolverModule {
         pkind[i] = kd->kind;
         pmin[i] = mandatory(ds[k], kd->a, "Distributions");
         pmax[i] = mandatory(ds[k], kd->b, "Distributions");
-        if (!(pmax[i] > 0.0)) fail("Incorrect %s distribution: %f.\n", kd->what, pmax[i]);
+        if (kd->what && !(pmax[i] > 0.0)) fail("Incorrect %s distribution: %f.\n", kd->what, pmax[i]);
       }
       pdist[i] = k;
     }
@@ -1454,18 +1479,19 @@ struct TmcmcModule : SolverModule {
           const size_t W = dist->world, per = (todo.size() + W - 1) / W,
                        a = std::min(todo.size(), per * dist->rank), b = std::min(todo.size(), a + per),
                        gw = grads ? N + N * N : 0;
-          for (size_t k = a; k < b; k++) evaluate(k);
           std::vector<double> buf(W * per * (1 + gw), 0.0);
-          for (size_t k = a; k < b; k++) {
-            const size_t i = todo[k];
-            double *row = buf.data() + (dist->rank * per + (k - a)) * (1 + gw);
-            row[0] = LL[i];
-            if (grads) {
-              std::copy(G.begin() + i * N, G.begin() + (i + 1) * N, row + 1);
-              std::copy(FIM.begin() + i * N * N, FIM.begin() + (i + 1) * N * N, row + 1 + N);
+          replicatedGather(*dist, buf, per * (1 + gw), [&] {
+            for (size_t k = a; k < b; k++) evaluate(k);
+            for (size_t k = a; k < b; k++) {
+              const size_t i = todo[k];
+              double *row = buf.data() + (dist->rank * per + (k - a)) * (1 + gw);
+              row[0] = LL[i];
+              if (grads) {
+                std::copy(G.begin() + i * N, G.begin() + (i + 1) * N, row + 1);
+                std::copy(FIM.begin() + i * N * N, FIM.begin() + (i + 1) * N * N, row + 1 + N);
+              }
             }
-          }
-          if (per) dist->allGatherHost(buf.data(), per * (1 + gw));
+          });
           for (size_t k = 0; k < todo.size(); k++) {
             const size_t i = todo[k];
             const double *row = buf.data() + k * (1 + gw);

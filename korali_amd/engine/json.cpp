@@ -1,6 +1,9 @@
 // json.cpp — korali::Json (see json.hpp).
 #include "json.hpp"
 
+#include <atomic>
+#include <mutex>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -10,6 +13,14 @@
 #include <mutex>
 
 namespace korali {
+
+struct Json::Packed {
+  std::vector<double> d;
+  std::atomic<std::vector<Json> *> nodes{nullptr};  // built by a const reader, then immutable
+  explicit Packed(std::vector<double> &&v) : d(std::move(v)) {}
+  ~Packed() { delete nodes.load(); }
+};
+
 
 namespace {
 // never destroyed: entries may hold Python callables, which must not be
@@ -57,7 +68,7 @@ void Json::release() noexcept {
     case Type::String: delete v_.s; break;
     case Type::Array:
       if (packed_)
-        delete v_.pd;
+        delete v_.pk;
       else
         delete v_.a;
       break;
@@ -74,7 +85,7 @@ void Json::copyFrom(const Json &o) {
     case Type::String: v_.s = new std::string(*o.v_.s); break;
     case Type::Array:
       if (o.packed_)
-        v_.pd = new std::vector<double>(*o.v_.pd);
+        v_.pk = makePacked(std::vector<double>(o.v_.pk->d));
       else
         v_.a = new std::vector<Json>(*o.v_.a);
       break;
@@ -83,12 +94,36 @@ void Json::copyFrom(const Json &o) {
   }
 }
 
-void Json::unpack() const {
+
+Json::Packed *Json::makePacked(std::vector<double> &&v) { return new Packed(std::move(v)); }
+
+size_t Json::size() const {
+  return t_ == Type::Array ? (packed_ ? v_.pk->d.size() : v_.a->size()) : t_ == Type::Object ? v_.o->size() : 0;
+}
+
+const std::vector<double> *Json::packedDoubles() const { return t_ == Type::Array && packed_ ? &v_.pk->d : nullptr; }
+
+void Json::unpack() {
   if (!packed_) return;
-  auto *a = new std::vector<Json>(v_.pd->begin(), v_.pd->end());
-  delete v_.pd;
+  std::vector<Json> *a = v_.pk->nodes.exchange(nullptr);
+  if (!a) a = new std::vector<Json>(v_.pk->d.begin(), v_.pk->d.end());
+  delete v_.pk;
   v_.a = a;
   packed_ = false;
+}
+
+const std::vector<Json> &Json::constNodes() const {
+  if (!packed_) return *v_.a;
+  std::vector<Json> *n = v_.pk->nodes.load(std::memory_order_acquire);
+  if (n) return *n;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  n = v_.pk->nodes.load(std::memory_order_relaxed);
+  if (!n) {
+    n = new std::vector<Json>(v_.pk->d.begin(), v_.pk->d.end());
+    v_.pk->nodes.store(n, std::memory_order_release);
+  }
+  return *n;
 }
 
 std::vector<Json> &Json::arrayRef() {
@@ -106,8 +141,7 @@ const std::map<std::string, Json> &Json::items() const {
 const std::vector<Json> &Json::elements() const {
   static const std::vector<Json> none;
   if (t_ != Type::Array) return none;
-  unpack();
-  return *v_.a;
+  return constNodes();
 }
 
 Json &Json::operator[](const std::string &key) {
@@ -135,8 +169,7 @@ const Json &Json::at(const std::string &key) const {
 
 const Json &Json::at(size_t idx) const {
   if (t_ != Type::Array || idx >= size()) throw std::runtime_error("index out of range");
-  unpack();
-  return (*v_.a)[idx];
+  return constNodes()[idx];
 }
 
 double Json::getDouble() const {
@@ -190,7 +223,7 @@ const std::string &Json::getString() const {
 
 std::vector<double> Json::getDoubleVector() const {
   if (t_ != Type::Array) throw std::runtime_error(std::string("expected an array, found a ") + typeName(t_));
-  if (packed_) return *v_.pd;
+  if (packed_) return v_.pk->d;
   std::vector<double> v;
   v.reserve(v_.a->size());
   for (const auto &x : *v_.a) v.push_back(x.getDouble());
@@ -252,12 +285,12 @@ void Json::dumpTo(std::string &out, int indent, int level) const {
     case Type::Array: {
       out += '[';
       if (packed_) {
-        for (size_t k = 0; k < v_.pd->size(); k++) {
+        for (size_t k = 0; k < v_.pk->d.size(); k++) {
           if (k) out += ',';
           nl(level + 1);
-          dumpDouble(out, (*v_.pd)[k]);
+          dumpDouble(out, v_.pk->d[k]);
         }
-        if (!v_.pd->empty()) nl(level);
+        if (!v_.pk->d.empty()) nl(level);
         out += ']';
         break;
       }

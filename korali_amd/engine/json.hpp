@@ -55,14 +55,14 @@ class Json {
   Json(const std::vector<T> &v) : t_(Type::Array) {
     if constexpr (std::is_same<T, double>::value || std::is_same<T, float>::value) {
       packed_ = true;
-      v_.pd = new std::vector<double>(v.begin(), v.end());
+      v_.pk = makePacked(std::vector<double>(v.begin(), v.end()));
     } else {
       v_.a = new std::vector<Json>();
       v_.a->reserve(v.size());
       for (const auto &x : v) v_.a->emplace_back(x);
     }
   }
-  Json(std::vector<double> &&v) : t_(Type::Array), packed_(true) { v_.pd = new std::vector<double>(std::move(v)); }
+  Json(std::vector<double> &&v) : t_(Type::Array), packed_(true) { v_.pk = makePacked(std::move(v)); }
   Json(const Json &o) : t_(o.t_), packed_(o.packed_) { copyFrom(o); }
   Json(Json &&o) noexcept : t_(o.t_), packed_(o.packed_), v_(o.v_) {
     o.t_ = Type::Null;
@@ -124,14 +124,12 @@ class Json {
   void erase(const std::string &key) {
     if (t_ == Type::Object) v_.o->erase(key);
   }
-  size_t size() const {
-    return t_ == Type::Array ? (packed_ ? v_.pd->size() : v_.a->size()) : t_ == Type::Object ? v_.o->size() : 0;
-  }
+  size_t size() const;
   void push_back(const Json &v) { arrayRef().push_back(v); }
   void push_back(Json &&v) { arrayRef().push_back(std::move(v)); }
   // the packed doubles of an array held packed, else nullptr (fast paths of
   // readers that need no nodes)
-  const std::vector<double> *packedDoubles() const { return t_ == Type::Array && packed_ ? v_.pd : nullptr; }
+  const std::vector<double> *packedDoubles() const;
   const std::map<std::string, Json> &items() const;
   const std::vector<Json> &elements() const;
 
@@ -169,21 +167,27 @@ class Json {
   // 16 bytes a node: the tag and one word (a scalar, or the heap-held
   // string / array / object) -- result files hold 10^5-10^6 numbers
   // (Sample Population, databases), built and copied every save.  packed_:
-  // an Array held as doubles (pd) rather than nodes (a); unpacking on first
-  // node access changes the representation, not the value, hence mutable.
+  // an Array held as doubles (pk) rather than nodes (a).  A const reader that
+  // needs nodes (at(i), elements()) gets them built once beside the doubles
+  // under a lock and published atomically -- const reads never change the
+  // representation, so several threads may read one Json (the Concurrent
+  // conduit's workers); a non-const access converts to nodes.
+  struct Packed;
+  static Packed *makePacked(std::vector<double> &&v);
   Type t_ = Type::Null;
-  mutable bool packed_ = false;
-  mutable union {
+  bool packed_ = false;
+  union {
     bool b;
     long long i;
     unsigned long long u;
     double d;
     std::string *s;
     std::vector<Json> *a;
-    std::vector<double> *pd;
+    Packed *pk;
     std::map<std::string, Json> *o;
   } v_;
-  void unpack() const;
+  void unpack();                                // packed -> nodes (non-const paths)
+  const std::vector<Json> &constNodes() const;  // the nodes of an array, packed or not
   void release() noexcept;
   void copyFrom(const Json &o);
   std::vector<Json> &arrayRef();  // null becomes an empty array

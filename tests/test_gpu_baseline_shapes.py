@@ -9,11 +9,11 @@
 * the BTPE branch of gsl_ran_binomial inside the multinomial resampling
   (n p >= 14), counted on both sides and required to have run;
 * λ = 65536 population sharding over 2 gloo ranks against the unsharded
-  handle (tools/shard_check.py).
+  handle (tools/shard_check.py, the default Exact covariance mode: the
+  selected rows all-gathered, the rank-μ chains split by covariance tile and
+  returned through the MAX-bits all-reduce).
 
-Bar: bit-exact (np.array_equal / ==) everywhere except the sharded run's
-partial-sum mean / covariance (1e-12 / 1e-11 relative, documented in
-DESIGN.md §6).
+Bar: bit-exact (np.array_equal / ==) everywhere, the sharded run included.
 """
 import os
 import socket

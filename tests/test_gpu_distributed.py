@@ -79,3 +79,12 @@ def test_distributed_conduit(tmp_path, ranks, solver, model, transport, cov):
         tol = 1e-12 if gens == "1" else 1e-7
         for k in ("Current Mean", "Covariance Matrix", "Sigma", "Evolution Path", "Conjugate Evolution Path"):
             assert close(s[k], u[k], tol), (gens, k)
+
+
+def test_replicated_callback_failure_reaches_every_rank(tmp_path):
+    """Distributed CCMA-ES (replicated handle, constraint callbacks split over
+    the ranks): rank 1's constraint raises; rank 1 reports its own error and
+    rank 0 one naming rank 1 -- after the gathers, so neither waits forever."""
+    res = launch(tmp_path, 2, "cmaes", "ccmaes_fail", "Host", "Exact")
+    assert res[1]["error"] and "on purpose on rank 1" in res[1]["error"]
+    assert res[0]["error"] and "rank 1 failed" in res[0]["error"]

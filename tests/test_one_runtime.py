@@ -32,3 +32,30 @@ def test_korali_then_torch_maps_one_hip_runtime():
 
 def test_native_then_torch_maps_one_hip_runtime():
     assert mapped("korali_amd.native", "torch") == (1, 1)
+
+
+PRELOADED = r"""
+import ctypes, sys
+ctypes.CDLL("/opt/rocm/lib/libhsa-runtime64.so.1", mode=ctypes.RTLD_GLOBAL)  # as rocprofv3's tool does
+import korali_amd.native as n
+n.lib()
+maps = open("/proc/self/maps").read().splitlines()
+libs = {l.split()[-1] for l in maps if "libamdhip64" in l or "libhsa-runtime64" in l}
+print(sorted(libs))
+"""
+
+
+def test_a_preloaded_system_hsa_keeps_its_hip_runtime():
+    """under rocprofv3 the tool maps /opt/rocm's HSA first: the package must
+    then bind to /opt/rocm's HIP too, not load torch's on top (two HSA
+    runtimes faulted at exit, profiles/r5/c4_teardown_segv.txt)"""
+    if not os.path.exists("/opt/rocm/lib/libhsa-runtime64.so.1"):
+        return
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("KORALI_AMD_HIP_RUNTIME", None)
+    out = subprocess.run([sys.executable, "-c", PRELOADED], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    libs = eval(out.stdout.strip().splitlines()[-1])
+    assert len([p for p in libs if "amdhip64" in p]) == 1, libs
+    assert len([p for p in libs if "hsa-runtime64" in p]) == 1, libs
+    assert not any("torch" in p for p in libs), libs

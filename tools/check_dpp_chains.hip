@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "kg_chains.hpp"
+#include "kg_chains_experimental.hpp"
 
 using namespace kg::chains;
 

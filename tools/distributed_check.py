@@ -86,15 +86,30 @@ def gaussian(s):  # the builtin Gaussian likelihood, -0.5 * sum(x^2)
     s["logLikelihood"] = -0.5 * sum(v * v for v in s["Parameters"])
 
 
+_FAIL_CALLS = [0]
+
+
+def failing_constraint(s):
+    """ccmaes_fail: rank 1's constraint callback raises on its 40th call
+    (a replicated CCMA-ES evaluation: every rank must leave with an error,
+    none may be left waiting in the bootstrap gather)"""
+    _FAIL_CALLS[0] += 1
+    if int(os.environ["RANK"]) == 1 and _FAIL_CALLS[0] >= 40:
+        raise RuntimeError("constraint failed on purpose on rank 1")
+    s["F(x)"] = CCMAES_CONSTRAINTS[0](s["Parameters"])
+
+
 def experiment(solver, model, gens, cov="Exact"):
     e = korali.Experiment()
     e["Random Seed"] = 4242
     e["File Output"]["Enabled"] = False
     e["Console Output"]["Verbosity"] = "Silent"
-    if solver == "cmaes" and model == "ccmaes":  # run-ccmaes.py's experiment
+    if solver == "cmaes" and model in ("ccmaes", "ccmaes_fail"):  # run-ccmaes.py's experiment
         e["Problem"]["Type"] = "Optimization"
         e["Problem"]["Objective Function"] = ccmaes_model
         e["Problem"]["Constraints"] = [constraint(c) for c in CCMAES_CONSTRAINTS]
+        if model == "ccmaes_fail":
+            e["Problem"]["Constraints"] = [failing_constraint] + e["Problem"]["Constraints"][1:]
         for i, name in enumerate(("X", "Y")):
             e["Variables"][i]["Name"] = name
             e["Variables"][i]["Lower Bound"] = -10.0
@@ -182,6 +197,19 @@ def main():
     cov = sys.argv[5] if len(sys.argv) > 5 else "Exact"
     rank = int(os.environ["RANK"])
     result = {}
+    if model == "ccmaes_fail":
+        k = korali.Engine()
+        k["Conduit"]["Type"] = "Distributed"
+        k["Conduit"]["Transport"] = transport
+        try:
+            k.run(experiment(solver, model, 6, cov))
+            result["error"] = None
+        except Exception as ex:  # noqa: BLE001 -- the test reads the message
+            result["error"] = str(ex)
+        with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+            json.dump(result, f)
+        print(f"DISTRIBUTED_CHECK rank {rank} done", flush=True)
+        return
     for gens in GENS.get(model, (1, 6)):  # one generation: same samples; more: the run as a whole
         k = korali.Engine()
         k["Conduit"]["Type"] = "Distributed"

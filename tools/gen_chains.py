@@ -25,6 +25,7 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "korali_amd", "csrc", "kg_chains.hpp")
+OUT_EXP = os.path.join(ROOT, "tools", "kg_chains_experimental.hpp")
 
 S0 = 192  # first scratch VGPR
 
@@ -554,26 +555,49 @@ __device__ __forceinline__ double {name}(double acc, const double (&a)[8], const
   return acc;
 }}
 """
-    return add + nrm2 + row16 + nrm2c + nrm23 + spans(8, "kc_nrm2_dpp8") + spans(4, "kc_nrm2_dpp4")
+    # the product calls kc_add_dpp, kc_row16 and kc_nrm2_dpp8; the other forms
+    # are measured by tools/ubench_chains.hip / checked by check_dpp_chains.hip
+    return (add + row16 + spans(8, "kc_nrm2_dpp8"),
+            nrm2 + nrm2c + nrm23 + spans(4, "kc_nrm2_dpp4"))
 
 
 def main():
+    dpp_product, dpp_experimental = emit_dpp_chains()
     hdr = f"""// kg_chains.hpp — GENERATED by tools/gen_chains.py; do not edit.
 //
 // Ordered FP64 chains of the GSL-order tridiagonalisation as hand-scheduled
 // gfx950 assembly (see the generator's docstring for why and how).  Every
 // chain keeps the reference's operation order; +,* are IEEE correctly
-// rounded on gfx950, so the results equal the oracle's bit for bit.
+// rounded on gfx950, so the results equal the oracle's bit for bit.  Only the
+// forms the product kernels call live here; the measured alternatives are in
+// tools/kg_chains_experimental.hpp.
 #pragma once
 namespace kg {{
 namespace chains {{
-{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}{emit_lock_dpp(True)}{emit_lock_dpp(False)}{emit_dpp_chains()}
+{emit_add()}{emit_add_desc()}{emit_nrm2()}{emit_lock(True)}{emit_lock(False)}{dpp_product}
 }}  // namespace chains
 }}  // namespace kg
 """
     with open(OUT, "w") as f:
         f.write(hdr)
     print("wrote", OUT)
+    exp = f"""// kg_chains_experimental.hpp — GENERATED by tools/gen_chains.py; do not edit.
+//
+// Chain forms measured against the product's (tools/ubench_chains.hip,
+// tools/check_dpp_chains.hip) and not called by any product kernel:
+// the DPP lockstep forms, the per-half / per-
+// element / branch-free / quarter-span variants of the dnrm2 recurrence.
+// Include after korali_amd/csrc/kg_chains.hpp.
+#pragma once
+namespace kg {{
+namespace chains {{
+{emit_lock_dpp(True)}{emit_lock_dpp(False)}{dpp_experimental}
+}}  // namespace chains
+}}  // namespace kg
+"""
+    with open(OUT_EXP, "w") as f:
+        f.write(exp)
+    print("wrote", OUT_EXP)
 
 
 if __name__ == "__main__":

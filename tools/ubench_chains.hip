@@ -8,6 +8,7 @@
 #include <cstdio>
 
 #include "kg_chains.hpp"
+#include "kg_chains_experimental.hpp"
 
 using namespace kg::chains;
 
