@@ -45,8 +45,9 @@ HBM_PEAK_GBS = 8000.0
 # algorithmic FP64 work per launch of each stage at C2
 def stage_flops(N, lam, mu):
     """Algorithmic FLOPs per launch of the profiled CMA-ES stages at (N, lambda, mu)."""
-    return {"eigen": (4.0 / 3.0) * N ** 3 + 2.0 * N ** 3 + 6.0 * 1.1 * N ** 3,
-            "eigen_tridiag": (4.0 / 3.0) * N ** 3, "eigen_unpack": 2.0 * N ** 3, "eigen_apply": 6.0 * 1.1 * N ** 3,
+    return {"eigen": (8.0 / 3.0) * N ** 3 + 6.0 * 1.1 * N ** 3,
+            "eigen_tridiag": (4.0 / 3.0) * N ** 3, "eigen_unpack": (4.0 / 3.0) * N ** 3,
+            "eigen_apply": 6.0 * 1.1 * N ** 3,
             "transform": 2.0 * lam * N ** 2, "covariance": 1.0 * mu * N * (N + 1),
             "rankmu_mfma": 1.0 * mu * N * (N + 1), "objective": 8.0 * lam * N}
 
@@ -54,9 +55,9 @@ def stage_flops(N, lam, mu):
 STAGE_FLOPS = {
     # GSL symmv pieces: tridiagonalisation (4/3)N^3, unpack 2N^3 (nominal),
     # Givens application 6 flops * N rows * ~1.1 N^2 rotations
-    "eigen": (4.0 / 3.0) * N_VARS ** 3 + 2.0 * N_VARS ** 3 + 6.0 * 1.1 * N_VARS ** 3,
+    "eigen": (8.0 / 3.0) * N_VARS ** 3 + 6.0 * 1.1 * N_VARS ** 3,
     "eigen_tridiag": (4.0 / 3.0) * N_VARS ** 3,
-    "eigen_unpack": 2.0 * N_VARS ** 3,
+    "eigen_unpack": (4.0 / 3.0) * N_VARS ** 3,  # householder_hm over N-2 reflectors: sum of 4 n^2
     "eigen_apply": 6.0 * 1.1 * N_VARS ** 3,
     "transform": 2.0 * LAMBDA * N_VARS ** 2,
     # rank-mu sum: the SYRK count mu N (N+1) (the lower triangle and the
@@ -75,7 +76,7 @@ STAGE_KERNELS = {
                        "kg::k_tridiag_mw", "kg::k_tridiag")],
     "eigen_unpack": [("kg::k_unpack_wv", "kg::k_unpack_mw", "kg::k_unpack")], "eigen_apply": ["kg::k_apply"],
     "transform": [("kg::k_transform_sc", "kg::k_transform")], "objective": [("kg::k_objective2", "kg::k_objective")],
-    "covariance": [("kg::k_adaptC_row", "kg::k_adaptC_exact3", "kg::k_adaptC_exact2", "kg::k_adaptC_combine")],
+    "covariance": ["kg::k_rankmu_prep", ("kg::k_adaptC_lane", "kg::k_adaptC_row", "kg::k_adaptC_exact3", "kg::k_adaptC_exact2")],
     "rankmu_mfma": ["kg::k_rankmu_tile"],
     "rng_polar": ["kg::k_polar_count", "kg::k_scan_counts", "kg::k_polar_scatter"],
     "mean_paths": ["kg::k_update_best", "kg::k_gather_selected", ("kg::k_mean3", "kg::k_mean2", "kg::k_mean"),
@@ -88,7 +89,27 @@ STAGE_KERNELS = {
 }
 # stages timed on the host core (wall clock), not device kernels
 HOST_STAGES = ("eigen_chase_host", "eigen_tridiag_host", "eigen_c_wait", "eigen_dsd_wait")
-PROFILE_ROUNDS = ("r5", "r4", "r3", "r2")  # newest first: a PMC summary is read from the newest round that holds it
+# device stages whose duration the host sets: k_fetch_h spins until the host
+# tridiagonalisation publishes the reflectors, k_apply replays the rotations
+# as the host chase publishes them (its event time is the chase's)
+HOST_FED = ("eigen_fetch_h", "eigen_apply", "eigen_publish_c")
+# what bounds each stage that can come out dominant (the roofline's note)
+STAGE_NOTES = {
+    "eigen_unpack": "symmtd_unpack (Q from the N-2 Householder reflectors, householder_hm): per reflector an "
+                    "ordered dot chain per column of Q in GSL order, so latency-bound far below the FP64 roof; it "
+                    "runs beside the host core's Givens chase, off the generation's critical path",
+    "eigen_tridiag": "GSL's Householder tridiagonalisation on the device (KORALI_AMD_TRIDIAG=sq/mw2): three ordered "
+                     "FP64 add chains per step whose order the bit-exact contract fixes",
+    "covariance": "adaptC's exact rank-mu sums: one ordered chain of mu Markstein quotients per lower-triangle "
+                  "entry (the reference's order), so chain- and issue-bound, not HBM-bound",
+    "mean_paths": "the mean / evolution paths: ordered sums over the mu selected rows (latency-bound chains)",
+    "transform": "x = m + sigma B (D o z): FP64 VALU (no FMA, bit-exact), the ordered K loop per output",
+}
+PROFILE_ROUNDS = ("r6", "r5", "r4", "r3", "r2")
+# the kernel behind a stage as rocprof names it (C2 shapes)
+STAGE_KERNEL_NAME = {"eigen_tridiag": "kg::k_tridiag_sq", "eigen_unpack": "kg::k_unpack_wv",
+                     "covariance": "kg::k_adaptC_row", "transform": "kg::k_transform",
+                     "mean_paths": "kg::k_mean3 + kg::k_paths3 + kg::k_gather_selected + kg::k_update_best"}  # newest first: a PMC summary is read from the newest round that holds it
 
 
 def profile_file(name):
@@ -646,7 +667,7 @@ def main():
 
     gens_per_s = args.steps * world / elapsed
     # rankmu_mfma runs on the second stream, beside mean_paths
-    kernels = {k: v for k, v in stages.items() if k not in HOST_STAGES + ("eigen", "rankmu_mfma")}
+    kernels = {k: v for k, v in stages.items() if k not in HOST_STAGES + HOST_FED + ("eigen", "rankmu_mfma")}
     dominant = max(kernels, key=kernels.get)
     dom_ms = stages[dominant]
     flops = STAGE_FLOPS.get(dominant, 0.0)
@@ -688,14 +709,12 @@ def main():
         "best_ever_value": best,
         "stage_ms": stages,
         "generation_roofline": {"T_roof_us": t_roof * 1e6, "frac": t_roof / (elapsed / args.steps * world / world)},
-        "roofline": {"kernel": {"eigen_tridiag": "kg::k_tridiag_sq"}.get(dominant, dominant), "stage": dominant,
+        "roofline": {"kernel": STAGE_KERNEL_NAME.get(dominant, dominant), "stage": dominant,
                      "bound": "mfma", "issued_on": "valu",
                      "bound_note": "the contract's compute roof, priced at the FP64 peak (MI355X FP64 vector peak == "
-                                   "FP64 matrix peak, so the VALU kernel has the same roof; it issues no MFMA); the stage is "
-                                   "GSL's Householder tridiagonalisation, three ordered FP64 add chains of length "
-                                   "N-1-i per step (dnrm2, dsymv, ddot) whose order the bit-exact contract fixes, "
-                                   "so it is bound by the dependent-add latency, far below the roof by construction",
-                     "chain_bound_ms": chain_bound_ms,
+                                   "FP64 matrix peak, so the VALU kernel has the same roof; it issues no MFMA); "
+                                   + STAGE_NOTES.get(dominant, ""),
+                     "tridiag_device_chain_bound_ms": chain_bound_ms,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_raw_fetch": traffic_raw,
@@ -947,7 +966,7 @@ def c4_roofline(stages):
     the host chase, the eigen aggregate and the second-stream rank-mu MFMA
     excluded) against the FP64 peak, its HBM bytes per launch from the
     committed C4 PMC passes."""
-    kern = {k: v for k, v in stages.items() if k not in HOST_STAGES + ("eigen", "rankmu_mfma")}
+    kern = {k: v for k, v in stages.items() if k not in HOST_STAGES + HOST_FED + ("eigen", "rankmu_mfma")}
     if not kern:
         return None
     dom = max(kern, key=kern.get)
@@ -955,9 +974,10 @@ def c4_roofline(stages):
     ms = stages[dom]
     achieved = flops / (ms * 1e-3) / 1e12
     traffic, _ = pmc_traffic(dom, "c4_pmc_traffic.csv")
-    return {"kernel": {"eigen_tridiag": "kg::k_tridiag_mw2"}.get(dom, dom), "stage": dom, "bound": "mfma",
-            "bound_note": "FP64 compute roof (vector = matrix FP64 peak on MI355X); the tridiagonalisation is a "
-                          "per-step chain in GSL order with one in-launch hand-off per Householder step",
+    names = {"eigen_tridiag": "kg::k_tridiag_mw2", "covariance": "kg::k_adaptC_lane", "eigen_unpack": "kg::k_unpack_mw",
+             "transform": "kg::k_prescale_t + kg::k_transform_sc"}
+    return {"kernel": names.get(dom, dom), "stage": dom, "bound": "mfma",
+            "bound_note": "FP64 compute roof (vector = matrix FP64 peak on MI355X); " + STAGE_NOTES.get(dom, ""),
             "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
             "traffic": traffic, "traffic_source": profile_file("c4_pmc_traffic.csv")[1] if traffic else None,
             "algorithmic_flops_per_launch": flops, "avg_launch_ms": ms}

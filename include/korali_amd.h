@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 7
+#define KG_ABI_VERSION 8
 
 const char *kg_last_error(void);
 int kg_abi_version(void);
@@ -266,6 +266,12 @@ int kg_debug_multinomial(uint64_t seed, size_t K, unsigned N, const double *p, s
  * the integration failed.  Runs on `device`. */
 int kg_debug_cartpole(int device, const double *u0, const double *force, size_t n, size_t steps, double *u_out,
                       int *over);
+/* kg_debug_cartpole from time t0[j] (NULL: 0) instead of 0, the time after
+ * the last advance in t_out (n, may be NULL): one environment step at a time
+ * on the device's dynamics (a host 'Environment Function' equal to the
+ * CartPole kernel, tests/test_gpu_vracer_host_env.py). */
+int kg_debug_cartpole_at(int device, const double *u0, const double *t0, const double *force, size_t n, size_t steps,
+                         double *u_out, double *t_out, int *over);
 
 /* --------------------------------------------------------------- TMCMC */
 typedef struct kg_tmcmc_s *kg_tmcmc_t;
@@ -439,6 +445,9 @@ typedef struct {
   const double *action_lower_bounds, *action_upper_bounds;  /* action_size values (may be NULL for Normal) */
   int reward_rescaling;                    /* Reward / Rescaling / Enabled (environment_count <= 8) */
   int state_rescaling;                     /* State Rescaling / Enabled (state_size <= 8) */
+  int host_environment;                    /* 1: a host 'Environment Function' feeds the steps
+                                              (kg_vracer_host_*); any state_size, action_size <= 4;
+                                              0: the device CartPole (4 states, 1 action) */
 } kg_vracer_config;
 
 int kg_vracer_create(const kg_vracer_config *cfg, kg_vracer_t *out);
@@ -460,6 +469,34 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences);
  * reference does (agent.cpp.base:204-207). */
 int kg_vracer_rescale_states(kg_vracer_t h);
 int kg_vracer_train_policy(kg_vracer_t h, size_t updates);
+/* the policy updates the experiences collected so far call for
+ * (Agent::trainingGeneration, agent.cpp.base:201-231: State Rescaling at the
+ * first update, then as many updates as Experiences Between Policy Updates
+ * allows); kg_vracer_training_step = kg_vracer_environment_step + this */
+int kg_vracer_train_pending(kg_vracer_t h, size_t *updates);
+/* Host environments (a user 'Environment Function', run by the engine as a
+ * coroutine per environment: reinforcementLearning.cpp.base:58-83,
+ * :130-200, :276-340).  The device keeps the policy, the episode buffers and
+ * the replay memory exactly as for the CartPole kernel; the transitions come
+ * from the host:
+ *   kg_vracer_host_launch   the first launch of every environment: its
+ *                           initial state (E x S, raw: rescaled on the
+ *                           device) and Environment Id (E);
+ *   kg_vracer_host_act      the policy's action of every environment
+ *                           (E x A, continuous.cpp.base:95-150), the
+ *                           experience kept in the episode buffer;
+ *   kg_vracer_host_feed     each environment's reward, state after the
+ *                           action (E x S raw; an ended episode's last
+ *                           state), termination (0 non terminal, 1 Terminal,
+ *                           2 Truncated) and, for the ended ones, the next
+ *                           launch's initial state (E x S) and Environment Id
+ *                           (E); then Agent::processEpisode of the ended
+ *                           episodes in environment order (agent.cpp.base:376-572).
+ *                           Launches take sample ids in launch order. */
+int kg_vracer_host_launch(kg_vracer_t h, const float *states, const int *env_ids);
+int kg_vracer_host_act(kg_vracer_t h, float *actions);
+int kg_vracer_host_feed(kg_vracer_t h, const float *rewards, const float *states, const int *terminations,
+                        const float *next_states, const int *next_env_ids, size_t *new_experiences);
 int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *sorted_ids, size_t count);
 int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates);
 /* Agent::testingGeneration (agent.cpp.base:267-289) on the device CartPole:

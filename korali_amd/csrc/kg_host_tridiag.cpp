@@ -50,6 +50,19 @@
 
 #define KGI __attribute__((always_inline)) inline
 
+// KG_HT_PHASES (tools/host_tridiag_phases.cpp): time-stamp counters per phase
+// into kg_ht_phases[]: 0 the copy of C, 1 column i with the pending update,
+// 2 dnrm2, 3 the Householder scalars and v, 4 the fused row pass, 5 x.v and w
+#ifdef KG_HT_PHASES
+#include <x86intrin.h>
+extern unsigned long long kg_ht_phases[8];
+#define KG_HT_T(v) const unsigned long long v = __rdtsc()
+#define KG_HT_ACC(k, v) kg_ht_phases[k] += __rdtsc() - (v)
+#else
+#define KG_HT_T(v)
+#define KG_HT_ACC(k, v)
+#endif
+
 namespace kg {
 
 namespace ht_avx512 {

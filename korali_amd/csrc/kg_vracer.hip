@@ -47,7 +47,13 @@ constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metad
 constexpr int MAXENV = 64;  // environment ids with reward rescaling (Problem / Environment Count)
 constexpr int MAXS = 8;     // state dimensions with state rescaling
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
-enum : unsigned { ERR_NONFINITE_GRADIENT = 1u, ERR_NONFINITE_VALUE = 2u, ERR_NONFINITE_IW = 4u, ERR_ENV_ODE = 8u };
+enum : unsigned {
+  ERR_NONFINITE_GRADIENT = 1u,
+  ERR_NONFINITE_VALUE = 2u,
+  ERR_NONFINITE_IW = 4u,
+  ERR_ENV_ODE = 8u,
+  ERR_EPISODE_LONG = 16u  // a host environment's episode outgrew max_episode_steps
+};
 
 // Device-resident agent scalars (float where the reference keeps float).
 struct State {
@@ -87,6 +93,7 @@ struct Params {  // launch-constant configuration
   float lb[MAXA], ub[MAXA];       // action bounds (Variables' Lower / Upper Bound)
   int rr;                         // Reward / Rescaling / Enabled
   int srs;                        // State Rescaling / Enabled
+  int host;                       // a host 'Environment Function' feeds the environment steps
 };
 
 // ---------------------------------------------------------------- philox
@@ -1570,6 +1577,7 @@ struct Envs {
   float *sigb;        // rank x MAXENV: the rescaling sigmas before that episode (reward rescaling)
   int *fin_id;        // environment id of the finished episode of each rank
   float *pm, *ps;     // E x S: the state-rescaling moments the running episode was launched with
+  float *hraw;        // E x S: a host environment's raw launch state (State Rescaling re-scales it)
 };
 // requestNewPolicy's normalisation (reinforcementLearning.cpp.base:361-370)
 // of environment e's state component k
@@ -1700,6 +1708,95 @@ __global__ void k_vr_env_act(Params P, State *st, Envs ev, const float *__restri
   ev.fin[e] = failed ? TERMINAL : (steps >= P.T ? TRUNCATED : NON_TERMINAL);
 }
 
+// ---- host-fed environments (a user 'Environment Function',
+// reinforcementLearning.cpp.base:58-83, :276-340).  The engine runs each
+// environment's function as a coroutine (a thread handing control back and
+// forth at Sample::update); the device keeps the policy, the episode buffers
+// and the replay memory exactly as for the CartPole kernel, only the state
+// transitions come from the host.
+//
+// the first launch of every environment: its initial state (raw, rescaled
+// here with the moments it is launched with) and its Environment Id
+__global__ void k_vr_host_launch(Params P, const State *st, Envs ev, float *X, const float *__restrict__ states,
+                                 const int *__restrict__ env_ids) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E) return;
+  if (P.srs)
+    for (int k = 0; k < P.S; k++) ev.pm[e * P.S + k] = st->smean[k], ev.ps[e * P.S + k] = st->ssdev[k];
+  for (int k = 0; k < P.S; k++) {
+    const float x = states[(long long)e * P.S + k];
+    ev.hraw[(long long)e * P.S + k] = x;
+    X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, x);
+  }
+  ev.t[e] = 0;
+  ev.sample[e] = (unsigned long long)e;
+  ev.env_id[e] = env_ids[e];
+  ev.cum[e] = 0.f;
+}
+
+// the policy's action for every environment's current state (as the first
+// half of k_vr_env_act: continuous.cpp.base:95-150), the experience kept in
+// the episode buffer and the action handed to the host
+__global__ void k_vr_host_act(Params P, State *st, Envs ev, const float *__restrict__ out, const float *__restrict__ X,
+                              const float *__restrict__ forced_noise, float *__restrict__ actions) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E) return;
+  const int A = P.A, S = P.S, O = P.O;
+  const int t = ev.t[e];
+  if (t >= P.T) {  // (k_vr_host_feed flags it; nothing is stored past the buffer)
+    for (int i = 0; i < A; i++) actions[e * A + i] = 0.f;
+    return;
+  }
+  const long long slot = (long long)e * P.T + t;
+  float act[MAXA];
+  for (int i = 0; i < A; i += 2) {
+    float n0, n1;
+    if (forced_noise) {
+      n0 = forced_noise[e * A + i];
+      n1 = i + 1 < A ? forced_noise[e * A + i + 1] : 0.f;
+    } else {
+      philox_normals(P.seed, 0x4E4Fu, st->env_step, (unsigned)(e * MAXA + i), n0, n1);
+    }
+    act[i] = out[(long long)e * O + 1 + i] + out[(long long)e * O + 1 + A + i] * n0;
+    if (i + 1 < A) act[i + 1] = out[(long long)e * O + 2 + i] + out[(long long)e * O + 2 + A + i] * n1;
+  }
+  if (P.clipped)  // continuous.cpp.base:172-183
+    for (int i = 0; i < A; i++) {
+      if (act[i] >= P.ub[i]) act[i] = P.ub[i];
+      if (act[i] <= P.lb[i]) act[i] = P.lb[i];
+    }
+  for (int k = 0; k < S; k++) ev.eb_st[slot * S + k] = X[(long long)e * S + k];
+  for (int i = 0; i < A; i++) ev.eb_act[slot * A + i] = act[i], actions[e * A + i] = act[i];
+  for (int i = 0; i < 2 * A; i++) ev.eb_pol[slot * 2 * A + i] = out[(long long)e * O + 1 + i];
+  ev.eb_v[slot] = out[(long long)e * O];
+}
+
+// what each environment returned for its action: reward, state after it
+// (raw; for an episode that ended, its last state: the truncated state),
+// termination (0 non terminal, 1 terminal, 2 truncated) -- the second half
+// of k_vr_env_act
+__global__ void k_vr_host_feed(Params P, State *st, Envs ev, float *X, const float *__restrict__ rewards,
+                               const float *__restrict__ states, const int *__restrict__ terms) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.E) return;
+  const int t = ev.t[e];
+  if (t >= P.T) {
+    atomicOr(&st->errors, (unsigned)ERR_EPISODE_LONG);
+    ev.fin[e] = NON_TERMINAL;
+    return;
+  }
+  const long long slot = (long long)e * P.T + t;
+  const float rew = rewards[e];
+  ev.eb_rew[slot] = rew;
+  ev.cum[e] += rew;
+  for (int k = 0; k < P.S; k++) X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, states[(long long)e * P.S + k]);
+  const int steps = t + 1;
+  ev.t[e] = steps;
+  ev.len[e] = steps;
+  const int term = terms[e];
+  ev.fin[e] = term == 1 ? TERMINAL : (term == 2 ? TRUNCATED : NON_TERMINAL);
+}
+
 // Finished episodes in environment order (the order attendAgent visits them):
 // exclusive prefix of their lengths, ranks, and the scalar bookkeeping.
 __global__ __launch_bounds__(1024) void k_vr_scan(Params P, State *st, Envs ev) {
@@ -1824,7 +1921,8 @@ __global__ void k_vr_reward_sums(Params P, State *st, Replay er, Envs ev) {
 // reference's last-two-entries window, see oracle/vracer_ref.py) and resets
 // the environment for its next launch.
 __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay er, Envs ev,
-                                                   const float *__restrict__ outF, float *X) {
+                                                   const float *__restrict__ outF, float *X,
+                                                   const float *__restrict__ hnext, const int *__restrict__ hnext_id) {
   const int e = blockIdx.x;
   const int term = ev.fin[e];
   if (!term) return;
@@ -1896,17 +1994,26 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     }
     ev.rewards[rank] = ev.cum[e];
     atomicAdd(&st->step_reward_sum, (double)ev.cum[e]);
-    // reset for the next launch (env.py: cart.reset(sampleId * 1024 + launchId))
+    // the next launch: sample id sid0 + rank + E (launch id = sample id)
     const unsigned long long sid = sid0 + (unsigned long long)rank + (unsigned long long)P.E;
-    double u[4];
-    cp_reset((unsigned)(sid * 1024ull + sid), u);
     if (P.srs)  // the relaunched episode runs with the current moments (agent.cpp.base:186-187)
       for (int q = 0; q < S; q++) ev.pm[e * S + q] = st->smean[q], ev.ps[e * S + q] = st->ssdev[q];
-    for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = vr_scale_state(P, ev, e, q, u[q]);
+    if (hnext) {  // a host environment: the initial state its function returned at its first update
+      for (int q = 0; q < S; q++) {
+        const float x = hnext[(long long)e * S + q];
+        ev.hraw[(long long)e * S + q] = x;
+        X[(long long)e * S + q] = vr_scale_state(P, ev, e, q, x);
+      }
+      ev.env_id[e] = hnext_id[e];
+    } else {  // CartPole (env.py: cart.reset(sampleId * 1024 + launchId))
+      double u[4];
+      cp_reset((unsigned)(sid * 1024ull + sid), u);
+      for (int q = 0; q < 4; q++) ev.u[e * 4 + q] = u[q], X[(long long)e * S + q] = vr_scale_state(P, ev, e, q, u[q]);
+      ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
+    }
     ev.time[e] = 0.0;
     ev.t[e] = 0;
     ev.sample[e] = sid;
-    ev.env_id[e] = (int)(sid % (unsigned long long)P.env_count);
     ev.cum[e] = 0.f;
   }
 }
@@ -1952,7 +2059,10 @@ __global__ void k_vr_srs_apply(Params P, const State *st, Replay er, Envs ev, fl
   if (i < (long long)P.E && ev.t[i] == 0) {
     const int e = (int)i;
     for (int k = 0; k < P.S; k++) ev.pm[e * P.S + k] = st->smean[k], ev.ps[e * P.S + k] = st->ssdev[k];
-    for (int k = 0; k < 4; k++) X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, ev.u[e * 4 + k]);
+    if (P.host)
+      for (int k = 0; k < P.S; k++) X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, ev.hraw[(long long)e * P.S + k]);
+    else
+      for (int k = 0; k < 4; k++) X[(long long)e * P.S + k] = vr_scale_state(P, ev, e, k, ev.u[e * 4 + k]);
   }
 }
 
@@ -1996,6 +2106,10 @@ struct kg_vracer_s {
   unsigned *mb, *forced_mb;
   float *forced_noise;
   int use_forced_noise;
+  // host environments: states / next launches' states (E x S), rewards,
+  // actions (E x A), terminations and environment ids (E) staged on the device
+  float *h_states = nullptr, *h_next = nullptr, *h_rew = nullptr, *h_act = nullptr;
+  int *h_term = nullptr, *h_ids = nullptr;
   State *st, *st_host;
   Replay er;
   Envs ev;
@@ -2272,6 +2386,8 @@ int vr_read_state(kg_vracer_t h) {
     if (e & ERR_NONFINITE_GRADIENT) kg::set_error("Gradient loss returned an invalid value (VRACER.cpp.base:173-175)");
     else if (e & ERR_NONFINITE_VALUE) kg::set_error("Calculated state value returned an invalid value (agent.cpp.base:629-630)");
     else if (e & ERR_ENV_ODE) kg::set_error("CartPole: the dopri5 integration failed (more than 500 steps or a vanishing step)");
+    else if (e & ERR_EPISODE_LONG)
+      kg::set_error("An environment's episode exceeded 'Max Episode Steps' (the device's episode buffer); raise it");
     else kg::set_error("NaN detected in the calculation of importance weight (continuous.cpp.base:391)");
     return 1;
   }
@@ -2311,8 +2427,8 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"reward_rescaling_sigma", &h->st->rsig[0], 4, (size_t)MAXENV},
       {"reward_rescaling_sum", &h->st->rsum[0], 4, (size_t)MAXENV},
       {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
-      {"state_rescaling_means", &h->st->smean[0], 4, (size_t)P.S},
-      {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)P.S},
+      {"state_rescaling_means", &h->st->smean[0], 4, (size_t)std::min(P.S, MAXS)},
+      {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)std::min(P.S, MAXS)},
       {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)9},
   };
   for (auto &x : tab)
@@ -2332,7 +2448,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   KG_CHECK(c && out, "vracer: null argument");
   KG_CHECK(c->state_size >= 1 && c->action_size >= 1 && c->action_size <= (size_t)MAXA,
            "vracer: action size must be 1..4 and state size >= 1");
-  KG_CHECK(c->state_size == 4 && c->action_size == 1,
+  KG_CHECK(c->host_environment || (c->state_size == 4 && c->action_size == 1),
            "vracer: the device environment is the CartPole of examples/learning/reinforcement/cartpole (4 states, 1 action)");
   KG_CHECK(c->hidden_size >= 1 && c->hidden_size <= 4096, "vracer: hidden layer width must be 1..4096");
   KG_CHECK(c->hidden_layers >= 1, "vracer: at least one hidden layer");
@@ -2362,6 +2478,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.env_count = (int)c->environment_count;
   P.rr = c->reward_rescaling ? 1 : 0;
   P.srs = c->state_rescaling ? 1 : 0;
+  P.host = c->host_environment ? 1 : 0;
   KG_CHECK(!P.srs || c->state_size <= (size_t)MAXS, "vracer: State Rescaling on the device supports up to 8 state variables");
   KG_CHECK(!P.rr || (c->environment_count >= 1 && c->environment_count <= (size_t)MAXENV),
            "vracer: Reward Rescaling on the device supports Environment Count 1..64");
@@ -2442,6 +2559,10 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(h->G, (size_t)P.B * P.O * 4), alloc(h->dZ, (size_t)P.B * P.O * 4);
   alloc(h->dHa, (size_t)P.B * P.H * 4), alloc(h->dHb, (size_t)P.B * P.H * 4);
   alloc(h->mb, (size_t)P.B * 4), alloc(h->forced_mb, (size_t)P.B * 4), alloc(h->forced_noise, E * P.A * 4);
+  if (c->host_environment) {
+    alloc(h->h_states, E * P.S * 4), alloc(h->h_next, E * P.S * 4), alloc(h->h_rew, E * 4), alloc(h->h_act, E * P.A * 4);
+    alloc(h->h_term, E * 4), alloc(h->h_ids, E * 4);
+  }
   alloc(h->st, sizeof(State));
   Replay &er = h->er;
   alloc(er.st, R * P.S * 4), alloc(er.act, R * P.A * 4), alloc(er.rew, R * 4), alloc(er.tst, R * P.S * 4);
@@ -2455,6 +2576,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
   alloc(ev.sigb, E * MAXENV * 4), alloc(ev.fin_id, E * 4);
   alloc(ev.pm, (size_t)E * P.S * 4), alloc(ev.ps, (size_t)E * P.S * 4);
+  if (P.host) alloc(ev.hraw, (size_t)E * P.S * 4);
   if (!rc && host_alloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
     kg::set_error("vracer: hipHostMalloc failed");
     rc = 1;
@@ -2466,9 +2588,11 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   }
   hipLaunchKernelGGL(k_vr_init_state, dim3(1), dim3(1), 0, h->stream, h->st, P.lr0, (float)c->off_policy_refer_beta,
                      P.cutoff_scale);
-  // the first launch of every environment: sample ids 0 .. E-1
-  hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, (const State *)h->st,
-                     h->ev, h->X, 0ull, (const int *)nullptr);
+  // the first launch of every environment: sample ids 0 .. E-1 (a host
+  // environment's come with kg_vracer_host_launch)
+  if (!P.host)
+    hipLaunchKernelGGL(k_vr_env_reset, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, (const State *)h->st,
+                       h->ev, h->X, 0ull, (const int *)nullptr);
   if (hipGetLastError() != hipSuccess || vr_read_state(h)) {
     if (!*kg::last_error()) kg::set_error("vracer: initial launches failed");
     kg_vracer_destroy(h);
@@ -2478,13 +2602,14 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   return 0;
 }
 
-// kg_debug_cartpole: trajectory n advances `steps` times with force[n][k]
-// from u0[n] at t = 0 (the device CartPole of k_vr_env_act)
-__global__ void k_vr_cartpole_debug(size_t n, size_t steps, const double *u0, const double *force, double *u_out,
-                                    int *over) {
+// kg_debug_cartpole_at: trajectory j advances `steps` times with
+// force[j][k] from u0[j] at time t0[j] (0 without t0); the time after the
+// last advance in t_out[j] (the device CartPole of k_vr_env_act)
+__global__ void k_vr_cartpole_debug(size_t n, size_t steps, const double *u0, const double *t0, const double *force,
+                                    double *u_out, double *t_out, int *over) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  double y[4], t = 0.0;
+  double y[4], t = t0 ? t0[j] : 0.0;
 #pragma unroll
   for (int k = 0; k < 4; k++) y[k] = u0[j * 4 + k];
   for (size_t s = 0; s < steps; s++) {
@@ -2493,34 +2618,41 @@ __global__ void k_vr_cartpole_debug(size_t n, size_t steps, const double *u0, co
     for (int k = 0; k < 4; k++) u_out[(j * steps + s) * 4 + k] = y[k];
     over[j * steps + s] = ok ? (cp_failed(y) ? 1 : 0) : -1;
   }
+  if (t_out) t_out[j] = t;
 }
 
-extern "C" int kg_debug_cartpole(int device, const double *u0, const double *force, size_t n, size_t steps,
-                                 double *u_out, int *over) {
+extern "C" int kg_debug_cartpole_at(int device, const double *u0, const double *t0, const double *force, size_t n,
+                                    size_t steps, double *u_out, double *t_out, int *over) {
   KG_CHECK(u0 && force && u_out && over, "kg_debug_cartpole: null argument");
   KG_CHECK(n >= 1 && steps >= 1 && n * steps <= (1u << 24), "kg_debug_cartpole: 1 <= n * steps <= 2^24");
   KG_HIP(hipSetDevice(device));
   double *d = nullptr;
-  int *o = nullptr;
-  const size_t nb = (n * 4 + 2 * n * steps * 4 + n * steps) * sizeof(double);
+  const size_t nb = (n * 4 + 2 * n + n * steps + n * steps * 4 + n * steps) * sizeof(double);
   KG_HIP(dev_alloc(&d, nb));
-  double *du0 = d, *dforce = d + n * 4, *dout = dforce + n * steps;
-  o = (int *)(dout + n * steps * 4);
+  double *du0 = d, *dt0 = du0 + n * 4, *dt1 = dt0 + n, *dforce = dt1 + n, *dout = dforce + n * steps;
+  int *o = (int *)(dout + n * steps * 4);
   int rc = 0;
   if (hipMemcpy(du0, u0, n * 4 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      (t0 && hipMemcpy(dt0, t0, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(dforce, force, n * steps * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
     rc = 1;
   if (!rc) {
-    hipLaunchKernelGGL(k_vr_cartpole_debug, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, n, steps, du0, dforce,
-                       dout, o);
+    hipLaunchKernelGGL(k_vr_cartpole_debug, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, n, steps, du0,
+                       t0 ? (const double *)dt0 : nullptr, dforce, dout, dt1, o);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(u_out, dout, n * steps * 4 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(over, o, n * steps * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(over, o, n * steps * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+        (t_out && hipMemcpy(t_out, dt1, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
       rc = 1;
   }
   dev_release(d);
   if (rc) kg::set_error("kg_debug_cartpole: device call failed");
   return rc;
+}
+
+extern "C" int kg_debug_cartpole(int device, const double *u0, const double *force, size_t n, size_t steps,
+                                 double *u_out, int *over) {
+  return kg_debug_cartpole_at(device, u0, nullptr, force, n, steps, u_out, nullptr, over);
 }
 
 int kg_vracer_destroy(kg_vracer_t h) {
@@ -2534,7 +2666,7 @@ int kg_vracer_destroy(kg_vracer_t h) {
                   h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,
                   h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
                   h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id,
-                  h->ev.pm, h->ev.ps};
+                  h->ev.pm, h->ev.ps, h->ev.hraw};
   for (void *p : ptrs)
     if (p) dev_release(p);
   if (h->st_host) host_release(h->st_host);
@@ -2735,6 +2867,7 @@ int kg_vracer_set_action_noise(kg_vracer_t h, const float *noise, size_t n) {
 
 int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
   KG_CHECK(h, "vracer: null argument");
+  KG_CHECK(!h->P.host, "vracer: a host environment steps through kg_vracer_host_act / kg_vracer_host_feed");
   const Params &P = h->P;
   {
   VrStage te(h, "environment_step");
@@ -2747,8 +2880,76 @@ int kg_vracer_environment_step(kg_vracer_t h, size_t *new_experiences) {
   hipLaunchKernelGGL(k_vr_evict, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er);
   if (P.rr) hipLaunchKernelGGL(k_vr_reward_sums, dim3(1), dim3(64), 0, h->stream, P, h->st, h->er, h->ev);
   hipLaunchKernelGGL(k_vr_append, dim3(P.E), dim3(256), 0, h->stream, P, h->st, h->er, h->ev, (const float *)h->outF,
-                     h->X);
+                     h->X, (const float *)nullptr, (const int *)nullptr);
   KG_HIP(hipGetLastError());
+  }
+  if (vr_read_state(h)) return 1;
+  h->session_experiences += h->st_host->step_new;
+  if (new_experiences) *new_experiences = (size_t)h->st_host->step_new;
+  return 0;
+}
+
+int kg_vracer_host_launch(kg_vracer_t h, const float *states, const int *env_ids) {
+  KG_CHECK(h && states && env_ids, "vracer: null argument");
+  const Params &P = h->P;
+  KG_CHECK(P.host, "vracer: the agent was created for the CartPole kernel, not a host environment");
+  for (int e = 0; e < P.E; e++)
+    KG_CHECK(env_ids[e] >= 0 && env_ids[e] < P.env_count, "Environment Id provided (" + std::to_string(env_ids[e]) +
+                                                              ") exceeds the maximum environment count defined (>= " +
+                                                              std::to_string(P.env_count) + ").");
+  KG_HIP(hipMemcpyAsync(h->h_states, states, (size_t)P.E * P.S * 4, hipMemcpyHostToDevice, h->stream));
+  KG_HIP(hipMemcpyAsync(h->h_ids, env_ids, (size_t)P.E * 4, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_vr_host_launch, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, (const State *)h->st,
+                     h->ev, h->X, (const float *)h->h_states, (const int *)h->h_ids);
+  KG_HIP(hipGetLastError());
+  return vr_read_state(h);
+}
+
+int kg_vracer_host_act(kg_vracer_t h, float *actions) {
+  KG_CHECK(h && actions, "vracer: null argument");
+  const Params &P = h->P;
+  KG_CHECK(P.host, "vracer: the agent was created for the CartPole kernel, not a host environment");
+  {
+    VrStage te(h, "environment_step");
+    if (vr_forward(h, h->X, P.E, h->out)) return 1;
+    hipLaunchKernelGGL(k_vr_host_act, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->st, h->ev,
+                       (const float *)h->out, (const float *)h->X,
+                       h->use_forced_noise ? (const float *)h->forced_noise : nullptr, h->h_act);
+    KG_HIP(hipGetLastError());
+  }
+  h->use_forced_noise = 0;
+  KG_HIP(hipMemcpyAsync(actions, h->h_act, (size_t)P.E * P.A * 4, hipMemcpyDeviceToHost, h->stream));
+  KG_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kg_vracer_host_feed(kg_vracer_t h, const float *rewards, const float *states, const int *terminations,
+                        const float *next_states, const int *next_env_ids, size_t *new_experiences) {
+  KG_CHECK(h && rewards && states && terminations && next_states && next_env_ids, "vracer: null argument");
+  const Params &P = h->P;
+  KG_CHECK(P.host, "vracer: the agent was created for the CartPole kernel, not a host environment");
+  for (int e = 0; e < P.E; e++) {
+    KG_CHECK(terminations[e] >= 0 && terminations[e] <= 2, "vracer: terminations must be 0, 1 (Terminal) or 2 (Truncated)");
+    KG_CHECK(terminations[e] == 0 || (next_env_ids[e] >= 0 && next_env_ids[e] < P.env_count),
+             "Environment Id provided (" + std::to_string(next_env_ids[e]) +
+                 ") exceeds the maximum environment count defined (>= " + std::to_string(P.env_count) + ").");
+  }
+  {
+    VrStage te(h, "environment_step");
+    KG_HIP(hipMemcpyAsync(h->h_rew, rewards, (size_t)P.E * 4, hipMemcpyHostToDevice, h->stream));
+    KG_HIP(hipMemcpyAsync(h->h_states, states, (size_t)P.E * P.S * 4, hipMemcpyHostToDevice, h->stream));
+    KG_HIP(hipMemcpyAsync(h->h_term, terminations, (size_t)P.E * 4, hipMemcpyHostToDevice, h->stream));
+    KG_HIP(hipMemcpyAsync(h->h_next, next_states, (size_t)P.E * P.S * 4, hipMemcpyHostToDevice, h->stream));
+    KG_HIP(hipMemcpyAsync(h->h_ids, next_env_ids, (size_t)P.E * 4, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(k_vr_host_feed, dim3(vr_blocks(P.E, 256)), dim3(256), 0, h->stream, P, h->st, h->ev, h->X,
+                       (const float *)h->h_rew, (const float *)h->h_states, (const int *)h->h_term);
+    if (vr_forward(h, h->X, P.E, h->outF)) return 1;  // V of truncated states (agent.cpp.base:530-545)
+    hipLaunchKernelGGL(k_vr_scan, dim3(1), dim3(1024), 0, h->stream, P, h->st, h->ev);
+    hipLaunchKernelGGL(k_vr_evict, dim3(1), dim3(256), 0, h->stream, P, h->st, h->er);
+    if (P.rr) hipLaunchKernelGGL(k_vr_reward_sums, dim3(1), dim3(64), 0, h->stream, P, h->st, h->er, h->ev);
+    hipLaunchKernelGGL(k_vr_append, dim3(P.E), dim3(256), 0, h->stream, P, h->st, h->er, h->ev,
+                       (const float *)h->outF, h->X, (const float *)h->h_next, (const int *)h->h_ids);
+    KG_HIP(hipGetLastError());
   }
   if (vr_read_state(h)) return 1;
   h->session_experiences += h->st_host->step_new;
@@ -2856,10 +3057,8 @@ int kg_vracer_train_policy_minibatch(kg_vracer_t h, const uint32_t *ids, size_t 
   return 0;
 }
 
-int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates) {
+int kg_vracer_train_pending(kg_vracer_t h, size_t *updates) {
   KG_CHECK(h, "vracer: null argument");
-  size_t added = 0;
-  if (kg_vracer_environment_step(h, &added)) return 1;
   size_t n = 0;
   // Agent::trainingGeneration (agent.cpp.base:201-231)
   if (h->st_host->experience_count >= h->start_size) {
@@ -2867,8 +3066,17 @@ int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *upda
     while ((double)h->session_experiences > h->ebpu * (double)(h->session_updates + n) + (double)h->until_start) n++;
   }
   if (n && kg_vracer_train_policy(h, n)) return 1;
-  if (new_experiences) *new_experiences = added;
   if (updates) *updates = n;
+  return 0;
+}
+
+int kg_vracer_training_step(kg_vracer_t h, size_t *new_experiences, size_t *updates) {
+  KG_CHECK(h, "vracer: null argument");
+  KG_CHECK(!h->P.host, "vracer: a host environment steps through kg_vracer_host_act / kg_vracer_host_feed");
+  size_t added = 0;
+  if (kg_vracer_environment_step(h, &added)) return 1;
+  if (kg_vracer_train_pending(h, updates)) return 1;
+  if (new_experiences) *new_experiences = added;
   return 0;
 }
 

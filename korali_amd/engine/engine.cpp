@@ -25,6 +25,7 @@
 #include <exception>
 #include <fstream>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <sstream>
@@ -1774,6 +1775,121 @@ std::vector<float> vracerInitialHyperparameters(const std::vector<size_t> &sizes
 
 namespace {
 
+// A user 'Environment Function' run as a coroutine (the reference's
+// co_create / co_switch, reinforcementLearning.cpp.base:66-88, :282-298,
+// :332-336): the function runs on a thread of its own and control passes
+// back and forth at every Sample::update and when the function returns, so
+// exactly one side runs at a time.  Abandoning a running function (its
+// episode ended with Termination set but the function did not return, or the
+// engine is leaving) makes its pending update() throw, which unwinds it.
+class EnvCoroutine {
+ public:
+  Sample s;
+
+  ~EnvCoroutine() { stop(); }
+  bool finished() const { return done_; }
+
+  // starts fn(s) and runs it up to its first update() (or its end)
+  void launch(size_t fn) {
+    stop();
+    done_ = false, abort_ = false, err_ = nullptr, envTurn_ = true;
+    s._yield = [this] { yieldToEngine(); };
+    th_ = std::thread([this, fn] {
+      try {
+        getFunction(fn)(s);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(m_);
+        if (!abort_) err_ = std::current_exception();
+      }
+      std::lock_guard<std::mutex> g(m_);
+      done_ = true, envTurn_ = false;
+      cv_.notify_all();
+    });
+    waitEngineTurn();
+  }
+
+  // runs the function from its pending update() to the next one (or its end)
+  void resume() {
+    if (done_) fail("Resuming a finished agent\n");
+    {
+      std::lock_guard<std::mutex> g(m_);
+      envTurn_ = true;
+    }
+    cv_.notify_all();
+    waitEngineTurn();
+  }
+
+  // abandons a function still running (its pending update() throws) and joins
+  void stop() {
+    if (!th_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      if (!done_) abort_ = true, envTurn_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+
+ private:
+  void yieldToEngine() {  // the function's thread, inside Sample::update
+    std::unique_lock<std::mutex> g(m_);
+    if (abort_) throw KoraliError("[Korali] Error: the environment's episode was abandoned by the engine.");
+    envTurn_ = false;
+    cv_.notify_all();
+    cv_.wait(g, [this] { return envTurn_; });
+    if (abort_) throw KoraliError("[Korali] Error: the environment's episode was abandoned by the engine.");
+  }
+  void waitEngineTurn() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return !envTurn_; });
+    if (err_) {
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+  std::thread th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool envTurn_ = false, done_ = true, abort_ = false;
+  std::exception_ptr err_;
+};
+
+// ReinforcementLearning::runEnvironment's checks of what the function returned
+// (reinforcementLearning.cpp.base:343-392, one agent per environment)
+void readEnvState(Sample &s, size_t S, float *out) {
+  if (!s.contains("State") || !s["State"].is_array())
+    fail("Agent state variable returned by the environment is not a vector.\n");
+  Json &st = s["State"];
+  if (st.size() != S) fail("Agents state vector %lu returned with the wrong size: %lu, expected: %lu.\n", 0ul,
+                           (unsigned long)st.size(), (unsigned long)S);
+  for (size_t j = 0; j < S; j++) {
+    const float v = (float)st[j].getDouble();
+    if (!std::isfinite(v)) fail("Agent %lu state variable %lu returned an invalid value: %f\n", 0ul, (unsigned long)j, v);
+    out[j] = v;
+  }
+}
+float readEnvReward(Sample &s) {
+  if (!s.contains("Reward") || !s["Reward"].is_number()) fail("Agent reward variable returned by the environment is not a number.\n");
+  const float r = (float)s["Reward"].getDouble();
+  if (!std::isfinite(r)) fail("Agent %lu reward returned an invalid value: %f\n", 0ul, r);
+  return r;
+}
+// 0 Non Terminal, 1 Terminal, 2 Truncated (__environmentWrapper's checks,
+// reinforcementLearning.cpp.base:77-83)
+int readEnvTermination(EnvCoroutine &c) {
+  const std::string t = c.s.contains("Termination") && c.s["Termination"].is_string() ? c.s["Termination"].getString() : "";
+  if (t == "Non Terminal") {
+    if (c.finished())
+      fail("Environment function terminated, but agent termination status (success or truncated) was not set.\n");
+    return 0;
+  }
+  if (t == "Terminal") return 1;
+  if (t == "Truncated") return 2;
+  fail("Environment function terminated, but agent termination status (%s) is neither 'Terminal' nor 'Truncated'.\n",
+       t.c_str());
+}
+
 struct VracerModule : SolverModule {
   size_t envIds = 1;  // Problem / Environment Count
   kg_vracer_t h = nullptr;
@@ -1790,8 +1906,18 @@ struct VracerModule : SolverModule {
   bool serialize = true;                 // Experience Replay / Serialize: the training state beside the results
   std::vector<uint64_t> testingIds;
   std::vector<float> testingReward;
+  size_t nState = 4, nAction = 1, concurrent = 1;
+  // a host 'Environment Function' (without 'Environment Kernel'): one
+  // coroutine per concurrent environment
+  bool hostEnv = false, clipped = false;
+  size_t envFn = 0;
+  Json customSettings = Json::object();
+  std::vector<double> actLbs, actUbs;
+  std::vector<std::unique_ptr<EnvCoroutine>> envs;
+  unsigned long long nextSampleId = 0, nextLaunchId = 0;  // agent.cpp.base:186; reinforcementLearning.cpp.base:71
 
   ~VracerModule() override {
+    envs.clear();  // (the functions unwind before the agent goes)
     if (h) kg_vracer_destroy(h);
   }
 
@@ -1817,21 +1943,29 @@ struct VracerModule : SolverModule {
       if (testingIds.empty())
         fail("For testing, you need to indicate the sample ids to run in the ['Testing']['Sample Ids'] field.\n");
     }
-    if (!pb.contains("Environment Kernel"))
-      fail("Problem 'Reinforcement Learning / Continuous' on the device needs 'Environment Kernel' (\"CartPole\": the "
-           "environment of examples/learning/reinforcement/cartpole); a host 'Environment Function' cannot run "
-           "inside the device rollouts.");
-    if (canon(pb["Environment Kernel"].getString()) != "cartpole")
-      fail("Unknown 'Environment Kernel' '%s' (the device provides \"CartPole\").",
-           pb["Environment Kernel"].getString().c_str());
+    // the environment: the device CartPole ('Environment Kernel'), else the
+    // user's 'Environment Function' on the host
+    if (pb.contains("Environment Kernel")) {
+      if (canon(pb["Environment Kernel"].getString()) != "cartpole")
+        fail("Unknown 'Environment Kernel' '%s' (the device provides \"CartPole\").",
+             pb["Environment Kernel"].getString().c_str());
+    } else if (pb.contains("Environment Function")) {
+      hostEnv = true;
+      envFn = (size_t)pb["Environment Function"].getUInt();
+      if (pb.contains("Custom Settings")) customSettings = pb["Custom Settings"];
+    } else {
+      fail(" + No value provided for mandatory setting: ['Environment Function'] required by reinforcementLearning.\n");
+    }
     if (uint(pb, "Agents Per Environment", 1) != 1) fail("'Agents Per Environment' > 1 is not supported by the device path.");
     const unsigned long long envCount = uint(pb, "Environment Count", 1);
     envIds = (size_t)envCount;
     uint(pb, "Actions Between Policy Updates", 0);  // the device policy is always the current one
-    const unsigned long long maxSteps = uint(pb, "Max Episode Steps", 500);  // env.py maxSteps
+    // the episode buffer: env.py's maxSteps for the CartPole kernel; a host
+    // function ends its episodes itself, up to this many steps
+    const unsigned long long maxSteps = uint(pb, "Max Episode Steps", hostEnv ? 10000 : 500);
     // variables (reinforcementLearning.cpp.base:40-53; continuous.cpp.base:44-50)
-    size_t nState = 0, nAction = 0;
-    double noise = 0.0, actLb = -INFINITY, actUb = INFINITY;
+    nState = 0, nAction = 0;
+    std::vector<double> noises;
     if (!js.contains("Variables") || js["Variables"].size() == 0) fail("No variables have been defined.");
     for (size_t i = 0; i < js["Variables"].size(); i++) {
       Json &v = js["Variables"][i];
@@ -1839,26 +1973,30 @@ struct VracerModule : SolverModule {
       if (t == "state") nState++;
       else if (t == "action") {
         nAction++;
-        noise = num(v, "Initial Exploration Noise", -1.0);
+        const double noise = num(v, "Initial Exploration Noise", -1.0);
         if (noise <= 0.0)
           fail("Provided initial noise (%f) for action variable %zu is not defined or negative.\n", noise, i);
         const double lb = num(v, "Lower Bound", -INFINITY), ub = num(v, "Upper Bound", INFINITY);
         if (ub - lb <= 0.0) fail("Upper (%f) and Lower Bound (%f) of action variable %zu invalid.\n", ub, lb, i);
-        actLb = lb, actUb = ub;
+        noises.push_back(noise), actLbs.push_back(lb), actUbs.push_back(ub);
       } else fail("Variable %zu: unknown Type '%s' (State or Action).", i, v["Type"].getString().c_str());
     }
     if (nAction == 0) fail("No action variables have been defined.\n");
     if (nState == 0) fail("No state variables have been defined.\n");
-    if (nState != 4 || nAction != 1)
+    if (!hostEnv && (nState != 4 || nAction != 1))
       fail("The CartPole environment kernel has 4 state variables and 1 action variable (%zu / %zu given).", nState,
            nAction);
+    if (nAction > 4) fail("The device policy supports up to 4 action variables (%zu given).", nAction);
     const std::string dist = canon(str(sv["Policy"], "Distribution", "Normal"));
     if (dist != "normal" && dist != "clippednormal")
       fail("Policy Distribution '%s' is not supported by the device path (Normal, Clipped Normal).",
            sv["Policy"]["Distribution"].getString().c_str());
-    if (dist == "clippednormal" && !(std::isfinite(actLb) && std::isfinite(actUb)))  // continuous.cpp.base:20-26
-      fail("Provided bounds (%f, %f) for the action variable are non-finite, but the distribution (%s) is bounded.\n",
-           actLb, actUb, sv["Policy"]["Distribution"].getString().c_str());
+    clipped = dist == "clippednormal";
+    if (clipped)  // continuous.cpp.base:20-26
+      for (size_t i = 0; i < nAction; i++)
+        if (!(std::isfinite(actLbs[i]) && std::isfinite(actUbs[i])))
+          fail("Provided bounds (%f, %f) for action variable %zu are non-finite, but the distribution (%s) is bounded.\n",
+               actLbs[i], actUbs[i], i, sv["Policy"]["Distribution"].getString().c_str());
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
     const bool stateRescaling = flag(sv["State Rescaling"], "Enabled", false);
     const bool rewardRescaling = flag(sv["Reward"]["Rescaling"], "Enabled", false);
@@ -1889,8 +2027,9 @@ struct VracerModule : SolverModule {
     Json &er = sv["Experience Replay"];
     Json &op = er["Off Policy"];
     kg_vracer_config c{};
-    c.state_size = 4, c.action_size = 1, c.hidden_size = H, c.hidden_layers = L;
-    c.environments = (size_t)uint(sv, "Concurrent Environments", 1);
+    c.state_size = nState, c.action_size = nAction, c.hidden_size = H, c.hidden_layers = L;
+    c.host_environment = hostEnv ? 1 : 0;
+    c.environments = concurrent = (size_t)uint(sv, "Concurrent Environments", 1);
     c.environment_count = (size_t)envCount;
     c.mini_batch_size = (size_t)uint(sv["Mini Batch"], "Size", 256);
     str(sv["Mini Batch"], "Strategy", "Uniform");
@@ -1911,11 +2050,11 @@ struct VracerModule : SolverModule {
     c.off_policy_refer_beta = num(op, "REFER Beta", 0.3);
     c.l2_regularization_enabled = flag(sv["L2 Regularization"], "Enabled", false) ? 1 : 0;
     c.l2_regularization_importance = num(sv["L2 Regularization"], "Importance", 1e-4);
-    c.initial_exploration_noise = &noise;
-    c.policy_distribution = dist == "clippednormal" ? 1 : 0;
+    c.initial_exploration_noise = noises.data();
+    c.policy_distribution = clipped ? 1 : 0;
     c.reward_rescaling = rewardRescaling ? 1 : 0;
     c.state_rescaling = stateRescaling ? 1 : 0;
-    c.action_lower_bounds = &actLb, c.action_upper_bounds = &actUb;
+    c.action_lower_bounds = actLbs.data(), c.action_upper_bounds = actUbs.data();
     c.seed = seeds.counter++;
     c.device = 0;
     episodesPerGeneration = uint(sv, "Episodes Per Generation", 1);
@@ -1932,9 +2071,9 @@ struct VracerModule : SolverModule {
     // experiment's seed counter), not GSL's: initial weights are not pinned.
     size_t n = 0;
     check(kg_vracer_hyperparameter_count(h, &n));
-    std::vector<size_t> sizes{4};
+    std::vector<size_t> sizes{nState};
     for (size_t l = 0; l < L; l++) sizes.push_back(H);
-    sizes.push_back(3);
+    sizes.push_back(1 + 2 * nAction);
     std::vector<float> theta = vracerInitialHyperparameters(sizes, (unsigned)seeds.counter++);
     if (theta.size() != n) fail("VRACER: hyperparameter count mismatch (%zu vs the device's %zu).", theta.size(), n);
     description = vracerPolicyDescription(js);
@@ -1958,10 +2097,14 @@ struct VracerModule : SolverModule {
       // Agent::deserializeExperienceReplay (agent.cpp.base:903-976) + the
       // training statistics the result file holds
       const std::string file = resultPath(js) + "/state.bin";
-      unsigned long long blob[2] = {0, 1};
+      unsigned long long blob[3] = {0, 1, 0};
       size_t got = 0;
       check(kg_vracer_load_state(h, file.c_str(), blob, sizeof blob, &got));
-      if (got == sizeof blob) sessionEpisodes = blob[0], sessionGeneration = blob[1];
+      if (got >= 2 * sizeof(unsigned long long)) sessionEpisodes = blob[0], sessionGeneration = blob[1];
+      // a host environment's episodes in flight are not part of the state:
+      // its environments launch afresh (the reference's agents in flight are
+      // lost with the run as well), with the sample ids continuing
+      if (got == sizeof blob) nextSampleId = blob[2];
       Json &tr = sv["Training"];
       if (tr.contains("Reward History"))
         for (size_t i = 0; i < tr["Reward History"].size(); i++)
@@ -1975,11 +2118,12 @@ struct VracerModule : SolverModule {
       // restores it with the policy, agent.cpp.base:1266-1274, and hands the
       // state moments to every testing agent, :279-280)
       Json &sr = sv["State Rescaling"];
-      if (sr.contains("Means") && sr["Means"].size() == 4 && sr.contains("Sigmas") && sr["Sigmas"].size() == 4) {
-        std::vector<float> m(4), s(4);
-        for (size_t i = 0; i < 4; i++) m[i] = (float)sr["Means"][i].getDouble(), s[i] = (float)sr["Sigmas"][i].getDouble();
-        check(kg_vracer_set_field(h, "state_rescaling_means", m.data(), 4 * sizeof(float)));
-        check(kg_vracer_set_field(h, "state_rescaling_sigmas", s.data(), 4 * sizeof(float)));
+      const size_t S = std::min<size_t>(nState, 8);  // (the device keeps 8 moments)
+      if (sr.contains("Means") && sr["Means"].size() == nState && sr.contains("Sigmas") && sr["Sigmas"].size() == nState) {
+        std::vector<float> m(8, 0.f), s(8, 1.f);
+        for (size_t i = 0; i < S; i++) m[i] = (float)sr["Means"][i].getDouble(), s[i] = (float)sr["Sigmas"][i].getDouble();
+        check(kg_vracer_set_field(h, "state_rescaling_means", m.data(), S * sizeof(float)));
+        check(kg_vracer_set_field(h, "state_rescaling_sigmas", s.data(), S * sizeof(float)));
       }
       Json &rr = sv["Reward"]["Rescaling"];
       if (rewardRescaled && rr.contains("Sigma") && rr["Sigma"].size() == envIds) {
@@ -1999,8 +2143,110 @@ struct VracerModule : SolverModule {
   // Agent::trainingGeneration (agent.cpp.base:162-265), or testingGeneration
   // (:267-289): one deterministic episode per testing sample id, launch ids
   // in launch order (a fresh environment per run, reinforcementLearning.cpp.base:67)
+  // initializeEnvironment + the first runEnvironment of runTrainingEpisode /
+  // runTestingEpisode (reinforcementLearning.cpp.base:90-130, :211-225,
+  // :261-293): a new episode of the function up to its first state
+  void launchEnv(EnvCoroutine &c, unsigned long long sampleId, bool training, float *state, int *envId) {
+    c.stop();
+    c.s._js = Json::object();
+    c.s["Module"] = "Problem";
+    c.s["Operation"] = training ? "Run Training Episode" : "Run Testing Episode";
+    c.s["Sample Id"] = sampleId;
+    c.s["Launch Id"] = nextLaunchId++;
+    c.s["Mode"] = training ? "Training" : "Testing";
+    c.s["Custom Settings"] = customSettings;
+    c.s["Reward"] = 0.0;
+    c.s["Termination"] = "Non Terminal";
+    c.s["Environment Id"] = 0ull;
+    c.launch(envFn);
+    readEnvState(c.s, nState, state);
+    if (readEnvTermination(c) != 0)  // (no action taken: the reference would send an empty episode)
+      fail("Environment function terminated before its first 'update()': an episode needs at least one action.\n");
+    if (!c.s["Environment Id"].is_number()) fail("'Environment Id' returned by the environment is not a number.\n");
+    const unsigned long long id = c.s["Environment Id"].getUInt();
+    if (id >= envIds)  // reinforcementLearning.cpp.base:131-134
+      fail("Environment Id provided (%lu) exceeds the maximum environment count defined (>= %lu).\n",
+           (unsigned long)id, (unsigned long)envIds);
+    if (envId) *envId = (int)id;
+  }
+
+  // the first launch of every concurrent environment (agent.cpp.base:178-190)
+  void launchHostEnvs() {
+    const size_t E = concurrent;
+    envs.clear();
+    std::vector<float> st(E * nState);
+    std::vector<int> ids(E);
+    for (size_t e = 0; e < E; e++) {
+      envs.emplace_back(new EnvCoroutine());
+      launchEnv(*envs[e], nextSampleId++, true, st.data() + e * nState, ids.data() + e);
+    }
+    check(kg_vracer_host_launch(h, st.data(), ids.data()));
+  }
+
+  // one action of every environment (the CartPole kernel's
+  // kg_vracer_environment_step with the transitions from the functions):
+  // the policy's actions, each function run to its next update() (or its
+  // end), ended episodes relaunched in environment order, then the device's
+  // episode bookkeeping and replay-memory appends
+  void hostEnvironmentStep() {
+    const size_t E = envs.size(), S = nState, A = nAction;
+    std::vector<float> act(E * A), rew(E), st(E * S), next(E * S, 0.f);
+    std::vector<int> term(E), nextId(E, 0);
+    check(kg_vracer_host_act(h, act.data()));
+    for (size_t e = 0; e < E; e++) {
+      EnvCoroutine &c = *envs[e];
+      c.s["Action"] = std::vector<float>(act.begin() + e * A, act.begin() + (e + 1) * A);
+      c.resume();
+      readEnvState(c.s, S, st.data() + e * S);
+      rew[e] = readEnvReward(c.s);
+      term[e] = readEnvTermination(c);
+    }
+    for (size_t e = 0; e < E; e++)
+      if (term[e]) launchEnv(*envs[e], nextSampleId++, true, next.data() + e * S, nextId.data() + e);
+    size_t added = 0;
+    check(kg_vracer_host_feed(h, rew.data(), st.data(), term.data(), next.data(), nextId.data(), &added));
+  }
+
+  // runTestingEpisode (reinforcementLearning.cpp.base:211-259) per testing
+  // sample: the policy's mode (generateTestingAction, continuous.cpp.base:
+  // 219-260) on the state rescaled with the agent's moments (:365-376)
+  void hostTestingEpisodes() {
+    const size_t S = nState, A = nAction, O = 1 + 2 * A, SM = std::min<size_t>(S, 8);
+    std::vector<float> mean(S, 0.f), sdev(S, 1.f), st(S), out(O);
+    check(kg_vracer_get_field(h, "state_rescaling_means", mean.data(), SM * sizeof(float)));
+    check(kg_vracer_get_field(h, "state_rescaling_sigmas", sdev.data(), SM * sizeof(float)));
+    testingReward.assign(testingIds.size(), 0.f);
+    nextLaunchId = 0;
+    for (size_t j = 0; j < testingIds.size(); j++) {
+      EnvCoroutine c;
+      launchEnv(c, testingIds[j], false, st.data(), nullptr);
+      float total = 0.f;
+      for (;;) {
+        for (size_t k = 0; k < S; k++) st[k] = (st[k] - mean[k]) / sdev[k];
+        check(kg_vracer_run_policy(h, st.data(), 1, out.data()));
+        std::vector<float> a(out.begin() + 1, out.begin() + 1 + A);
+        if (clipped)
+          for (size_t i = 0; i < A; i++) {
+            if (a[i] >= (float)actUbs[i]) a[i] = (float)actUbs[i];
+            if (a[i] <= (float)actLbs[i]) a[i] = (float)actLbs[i];
+          }
+        c.s["Action"] = a;
+        c.resume();
+        readEnvState(c.s, S, st.data());
+        total += readEnvReward(c.s);
+        if (readEnvTermination(c)) break;
+      }
+      testingReward[j] = total;
+    }
+  }
+
   void runGeneration(size_t) override {
     if (testing) {
+      if (hostEnv) {
+        hostTestingEpisodes();
+        tested = true;
+        return;
+      }
       std::vector<uint64_t> lid(testingIds.size());
       for (size_t i = 0; i < lid.size(); i++) lid[i] = i;
       testingReward.assign(testingIds.size(), 0.f);
@@ -2008,9 +2254,15 @@ struct VracerModule : SolverModule {
       tested = true;
       return;
     }
+    if (hostEnv && envs.empty()) launchHostEnvs();
     while (sessionEpisodes < episodesPerGeneration * sessionGeneration) {
       size_t added = 0, updates = 0;
-      check(kg_vracer_training_step(h, &added, &updates));
+      if (hostEnv) {
+        hostEnvironmentStep();
+        check(kg_vracer_train_pending(h, &updates));
+      } else {
+        check(kg_vracer_training_step(h, &added, &updates));
+      }
       const size_t finished = (size_t)scalar("step_episodes");
       if (finished) {
         std::vector<float> r(finished);
@@ -2049,6 +2301,8 @@ struct VracerModule : SolverModule {
       return;
     }
     sv["Current Episode"] = (unsigned long long)scalar("current_episode");
+    // the next launch's sample id (agent.cpp.base:186)
+    sv["Current Sample ID"] = hostEnv ? nextSampleId : (unsigned long long)(scalar("current_sample_id") + (double)concurrent);
     sv["Experience Count"] = (unsigned long long)scalar("experience_count");
     sv["Policy Update Count"] = (unsigned long long)scalar("policy_update_count");
     sv["Current Learning Rate"] = scalar("learning_rate");
@@ -2078,11 +2332,14 @@ struct VracerModule : SolverModule {
         // only when rescaling is enabled, so that key is left out
         sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(envIds, 1.0);
       }
-      float sm[8], ss[8];  // agent.config:326-335 (the CartPole kernel: 4 state variables)
-      check(kg_vracer_get_field(h, "state_rescaling_means", sm, 4 * sizeof(float)));
-      check(kg_vracer_get_field(h, "state_rescaling_sigmas", ss, 4 * sizeof(float)));
-      sv["State Rescaling"]["Means"] = std::vector<double>(sm, sm + 4);
-      sv["State Rescaling"]["Sigmas"] = std::vector<double>(ss, ss + 4);
+      // agent.config:326-335 (the device keeps the moments of up to 8 state
+      // variables: State Rescaling needs S <= 8; without it they are 0 / 1)
+      const size_t SM = std::min<size_t>(nState, 8);
+      std::vector<float> sm(nState, 0.f), ss(nState, 1.f);
+      check(kg_vracer_get_field(h, "state_rescaling_means", sm.data(), SM * sizeof(float)));
+      check(kg_vracer_get_field(h, "state_rescaling_sigmas", ss.data(), SM * sizeof(float)));
+      sv["State Rescaling"]["Means"] = std::vector<double>(sm.begin(), sm.end());
+      sv["State Rescaling"]["Sigmas"] = std::vector<double>(ss.begin(), ss.end());
     }
     Json &ds = description["Solver"];
     sv["Action Shifts"] = ds["Action Shifts"];
@@ -2097,7 +2354,7 @@ struct VracerModule : SolverModule {
   // results are written (training runs with Experience Replay / Serialize)
   void saveFiles(const std::string &dir) override {
     if (testing || !serialize) return;
-    const unsigned long long blob[2] = {sessionEpisodes, sessionGeneration};
+    const unsigned long long blob[3] = {sessionEpisodes, sessionGeneration, nextSampleId};
     check(kg_vracer_save_state(h, (dir + "/state.bin").c_str(), blob, sizeof blob));
   }
 
@@ -2198,6 +2455,13 @@ void runExperiment(Experiment &e, Conduit &conduit) {
   const std::string stype = canon(sv["Type"].getString());
   TmcmcModule *tm = nullptr;
   Collective *dist = conduit.dist.get();
+  // the solver goes with the run, failed or not: its device handle, and a
+  // host environment's coroutines, which must unwind while the caller (the
+  // Python binding) has the GIL released
+  struct SolverRelease {
+    ExperimentState &st;
+    ~SolverRelease() { st.solver.reset(); }
+  } release{st};
   if (stype == "optimizer/cmaes" || stype == "cmaes") {
     st.solver.reset(new CmaesModule(js, seeds, resume, dist));
   } else if (stype == "sampler/tmcmc" || stype == "tmcmc") {

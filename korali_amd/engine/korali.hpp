@@ -48,11 +48,15 @@ class Sample {
   Json &operator[](const std::string &key) { return _js[key]; }
   Json &operator[](size_t key) { return _js[key]; }
   bool contains(const std::string &key) const { return _js.contains(key); }
-  // Sample::update (sample.cpp:31-34) hands control back to the engine so it
-  // can process messages the model sent mid-evaluation.  CMA-ES and TMCMC
-  // exchange no such messages and every sample runs to completion on the
-  // evaluating thread, so there is nothing to hand over: a no-op.
-  void update() {}
+  // Sample::update (sample.cpp:31-34) hands control back to the engine.  A
+  // reinforcement-learning environment function runs as a coroutine
+  // (reinforcementLearning.cpp.base:58-83): there update() returns once the
+  // engine has set the next "Action".  CMA-ES and TMCMC samples run to
+  // completion on the evaluating thread: no handler, a no-op.
+  void update() {
+    if (_yield) _yield();
+  }
+  std::function<void()> _yield;  // set by the engine for coroutine samples
 
   template <typename T, typename... Key>
   T get(const char *fileName, int lineNumber, const Key &...key) {

@@ -184,7 +184,12 @@ PYBIND11_MODULE(libkorali, m) {
            })
       .def("__setitem__", [](korali::Sample &s, const std::string &k, py::handle v) { s[k] = toJson(v); })
       .def("__contains__", [](korali::Sample &s, const std::string &k) { return s.contains(k); })
-      .def("update", &korali::Sample::update);
+      // an environment function's update() waits for the engine: the GIL is
+      // released meanwhile (the engine thread never holds it)
+      .def("update", [](korali::Sample &s) {
+        py::gil_scoped_release nogil;
+        s.update();
+      });
 
   py::class_<korali::Experiment>(m, "Experiment")
       .def(py::init<>())

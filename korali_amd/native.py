@@ -83,6 +83,7 @@ EXPORTED = [
     "kg_tmcmc_process_partial", "kg_tmcmc_process_finalize", "kg_tmcmc_device_ptr", "kg_tmcmc_stream", "kg_tmcmc_evaluate_prior", "kg_tmcmc_get_candidates", "kg_tmcmc_set_evaluations",
     "kg_tmcmc_set_gradients",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump", "kg_debug_multinomial", "kg_debug_cartpole",
+    "kg_debug_cartpole_at",
     "kg_debug_host_tridiag",
     # VRACER (korali_amd/vracer.py binds their argument types)
     "kg_vracer_create", "kg_vracer_destroy", "kg_vracer_hyperparameter_count", "kg_vracer_field_size",
@@ -90,6 +91,7 @@ EXPORTED = [
     "kg_vracer_run_policy", "kg_vracer_set_action_noise", "kg_vracer_environment_step", "kg_vracer_train_policy",
     "kg_vracer_train_policy_minibatch", "kg_vracer_training_step", "kg_vracer_test_episodes", "kg_vracer_rescale_states", "kg_vracer_synchronize", "kg_vracer_stream",
     "kg_vracer_profile", "kg_vracer_profile_read", "kg_vracer_save_state", "kg_vracer_load_state",
+    "kg_vracer_train_pending", "kg_vracer_host_launch", "kg_vracer_host_act", "kg_vracer_host_feed",
 ]
 
 
@@ -121,6 +123,7 @@ def lib():
         L.kg_debug_mt_jump.argtypes = [vp, C.c_uint64, vp]
         L.kg_debug_multinomial.argtypes = [C.c_uint64, C.c_size_t, C.c_uint, vp, C.c_size_t, vp, vp]
         L.kg_debug_cartpole.argtypes = [ip, vp, vp, sz, sz, vp, vp]
+        L.kg_debug_cartpole_at.argtypes = [ip, vp, vp, vp, sz, sz, vp, vp, vp]
         L.kg_debug_host_tridiag.argtypes = [sz, vp, vp, vp, vp, vp]
         L.kg_cmaes_generation.argtypes = [vp, sz, ip]
         L.kg_cmaes_field_size.argtypes = [vp, cp, C.POINTER(sz)]

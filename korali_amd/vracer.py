@@ -33,7 +33,7 @@ class _VracerCfg(C.Structure):
         ("l2_regularization_importance", C.c_double), ("initial_exploration_noise", C.POINTER(C.c_double)),
         ("seed", C.c_uint64), ("device", C.c_int), ("policy_distribution", C.c_int),
         ("action_lower_bounds", C.POINTER(C.c_double)), ("action_upper_bounds", C.POINTER(C.c_double)),
-        ("reward_rescaling", C.c_int), ("state_rescaling", C.c_int),
+        ("reward_rescaling", C.c_int), ("state_rescaling", C.c_int), ("host_environment", C.c_int),
     ]
 
 
@@ -64,6 +64,11 @@ def _lib():
         L.kg_vracer_train_policy_minibatch.argtypes = [vp, C.POINTER(C.c_uint32), sz]
         L.kg_vracer_training_step.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
         L.kg_vracer_rescale_states.argtypes = [vp]
+        L.kg_vracer_train_pending.argtypes = [vp, C.POINTER(sz)]
+        ip = C.POINTER(C.c_int)
+        L.kg_vracer_host_launch.argtypes = [vp, fp, ip]
+        L.kg_vracer_host_act.argtypes = [vp, fp]
+        L.kg_vracer_host_feed.argtypes = [vp, fp, fp, ip, fp, ip, C.POINTER(sz)]
         u64p = C.POINTER(C.c_uint64)
         L.kg_vracer_test_episodes.argtypes = [vp, u64p, u64p, sz, fp]
         L.kg_vracer_stream.argtypes = [vp, C.POINTER(vp)]
@@ -88,7 +93,7 @@ class VracerDevice:
                  off_policy_target=0.1, off_policy_annealing_rate=0.0, off_policy_refer_beta=0.3,
                  l2_regularization_enabled=False, l2_regularization_importance=1e-4, initial_exploration_noise=1.0,
                  seed=0, device=0, hyperparameters=None, policy_distribution="Normal", action_lower_bound=-np.inf,
-                 action_upper_bound=np.inf, reward_rescaling=False, state_rescaling=False):
+                 action_upper_bound=np.inf, reward_rescaling=False, state_rescaling=False, host_environment=False):
         L = _lib()
         self.S, self.A, self.H, self.L = state_size, action_size, hidden_size, hidden_layers
         self.E, self.B, self.O = environments, mini_batch_size, 1 + 2 * action_size
@@ -108,7 +113,7 @@ class VracerDevice:
                          l2_regularization_importance, noise.ctypes.data_as(C.POINTER(C.c_double)), seed, device,
                          pol, self._lb.ctypes.data_as(C.POINTER(C.c_double)),
                          self._ub.ctypes.data_as(C.POINTER(C.c_double)), int(bool(reward_rescaling)),
-                         int(bool(state_rescaling)))
+                         int(bool(state_rescaling)), int(bool(host_environment)))
         h = C.c_void_p()
         check(L.kg_vracer_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 def test_abi_version(lib):
     lib.kg_abi_version.restype = ctypes.c_int
-    assert lib.kg_abi_version() == 7
+    assert lib.kg_abi_version() == 8
 
 
 def test_code_object_targets_gfx950():

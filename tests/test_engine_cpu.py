@@ -210,7 +210,28 @@ def test_vracer_configuration_errors_before_device(edit, msg):
         korali.Engine().run(e)
 
 
-def test_vracer_needs_device_environment():
+def test_vracer_needs_an_environment():
+    """Neither the device CartPole ('Environment Kernel') nor a host
+    'Environment Function': the reference's mandatory-setting error
+    (reinforcementLearning.cpp.base:473)."""
     e = cartpole_vracer(kernel=None)
-    with pytest.raises(korali.KoraliError, match="Environment Kernel"):
+    del_env = korali.Experiment()
+    for k in ("Type", "Environment Count", "Actions Between Policy Updates"):
+        del_env["Problem"][k] = e["Problem"][k]
+    e["Problem"] = del_env["Problem"]
+    with pytest.raises(korali.KoraliError, match=r"\['Environment Function'\] required"):
+        korali.Engine().run(e)
+
+
+@pytest.mark.parametrize("edit,msg", [
+    # a host environment takes any state size, up to 4 action variables
+    (lambda e: [e["Variables"][5 + i].__setitem__(k, v) for i in range(4)
+                for k, v in (("Type", "Action"), ("Initial Exploration Noise", 1.0), ("Lower Bound", -1.0),
+                             ("Upper Bound", 1.0))], "up to 4 action variables"),
+    (lambda e: e["Variables"][5].__setitem__("Type", "Sensor"), "unknown Type"),
+])
+def test_vracer_host_environment_configuration_errors(edit, msg):
+    e = cartpole_vracer(kernel=None)
+    edit(e)
+    with pytest.raises(korali.KoraliError, match=msg):
         korali.Engine().run(e)
