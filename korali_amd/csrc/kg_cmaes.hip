@@ -692,6 +692,33 @@ __global__ void __launch_bounds__(256) k_objective2(int N, int lam, int obj, con
     double *ta = Ta + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
     double *tb = Tb + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
     const double *xr = Xs + (size_t)lane * ld;
+    if (obj != KG_OBJ_NEGATIVE_ACKLEY) {  // every operand of the wave's columns read first, then the terms
+      constexpr int PU = (OB2_NC + 2) / 3;
+      double xs[PU], xp[PU];
+#pragma unroll
+      for (int u = 0; u < PU; u++) {
+        const int dd = wid - 1 + 3 * u, d = d0 + dd;
+        xs[u] = dd < dn ? xr[d] : 0.0;
+        xp[u] = (dd < dn && d > 0) ? xr[d - 1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < PU; u++) {
+        const int dd = wid - 1 + 3 * u, d = d0 + dd;
+        if (dd >= dn) break;
+        const double x = xs[u];
+        if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
+          if (d > 0) {
+            const double prev = xp[u];
+            const double tt = x - prev * prev;
+            const double uu = 1 - prev;
+            ta[dd] = 100 * (tt * tt) + uu * uu;
+          }
+        } else {
+          ta[dd] = x * x;
+        }
+      }
+      return;
+    }
     for (int dd = wid - 1; dd < dn; dd += 3) {
       const int d = d0 + dd;
       const double x = xr[d];
@@ -719,7 +746,17 @@ __global__ void __launch_bounds__(256) k_objective2(int N, int lam, int obj, con
       const double *ta = Ta + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
       const double *tb = Tb + (size_t)b * OB2_R * (OB2_NC + 1) + (size_t)lane * (OB2_NC + 1);
       if (obj == KG_OBJ_NEGATIVE_ROSENBROCK) {
-        for (int dd = (d0 == 0 ? 1 : 0); dd < dn; dd++) r0 += ta[dd];
+        // eight terms read before their adds (one LDS round trip per eight,
+        // the adds in column order as before)
+        int dd = d0 == 0 ? 1 : 0;
+        for (; dd + 8 <= dn; dd += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) t[u] = ta[dd + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) r0 += t[u];
+        }
+        for (; dd < dn; dd++) r0 += ta[dd];
       } else if (obj == KG_OBJ_NEGATIVE_ACKLEY) {
         for (int dd = 0; dd < dn; dd++) {
           r0 += ta[dd];
@@ -1170,6 +1207,84 @@ __global__ void __launch_bounds__(256) k_rankmu_prep(int N, int mu, const double
     if (d < N && k < mu) Tt[(size_t)d * mu + k] = tile[tx][r];
   }
   if (__syncthreads_or(!ok) && threadIdx.x == 0) atomicOr(&sc->rmuOutOfRange, 1u);
+}
+
+// k_update_best + k_gather_selected + k_rankmu_prep in one launch (the plain
+// exact-mode update: no constraints, weights fixed at initialisation): tile
+// (k0, d0) of the selected rows is read straight from the population through
+// the sorting index into Y, Yc and T; workgroup (0, 0) also does the best
+// bookkeeping, and the workgroups of the first row tile copy m into m_prev.
+// m_prev is read by nothing in this launch (the factors take m itself, equal
+// to m_prev until k_mean3 writes m).  The out-of-range flag is cleared by the
+// previous update's k_sigma (or k_init), not here: a clear inside this launch
+// could land after another workgroup's set.
+__global__ void __launch_bounds__(256) k_select_prep(int N, int mu, unsigned long long gen,
+                                                     const double *__restrict__ X, const double *__restrict__ F,
+                                                     const unsigned *__restrict__ idx, const double *__restrict__ w,
+                                                     const double *__restrict__ mean, double *__restrict__ prevMean,
+                                                     double *__restrict__ Y, double *__restrict__ currBestVars,
+                                                     double *__restrict__ bestEverVars, CmaesScalars *sc,
+                                                     double *__restrict__ Yc, double *__restrict__ Tt) {
+  __shared__ double tile[RP_T][RP_T + 1];
+  __shared__ unsigned sidx[RP_T];
+  const int k0 = blockIdx.x * RP_T, d0 = blockIdx.y * RP_T;
+  const int tx = threadIdx.x % RP_T, ty = threadIdx.x / RP_T;  // 32 x 8
+  if (threadIdx.x < RP_T) sidx[threadIdx.x] = (k0 + (int)threadIdx.x < mu) ? idx[k0 + threadIdx.x] : 0u;
+  const double effMu = sc->effectiveMu, ca = N + 1.3, cb = N + 2.0;
+  const double ccov1 = 2.0 / (ca * ca + effMu);
+  double ccovmu = 2.0 * (effMu - 2. + 1. / effMu) / (cb * cb + effMu);
+  if (1.0 - ccov1 < ccovmu) ccovmu = 1.0 - ccov1;
+  __syncthreads();
+  bool ok = true;
+  double xv[RP_T / 8];
+#pragma unroll
+  for (int u = 0; u < RP_T / 8; u++) {  // every row's load in flight before the first use
+    const int r = ty + 8 * u, k = k0 + r, d = d0 + tx;
+    xv[u] = (k < mu && d < N) ? X[(size_t)sidx[r] * N + d] : 0.0;
+  }
+  const double md = d0 + tx < N ? mean[d0 + tx] : 0.0;
+#pragma unroll
+  for (int u = 0; u < RP_T / 8; u++) {
+    const int r = ty + 8 * u, k = k0 + r, d = d0 + tx;
+    double t = 0.0;
+    if (k < mu && d < N) {
+      Y[(size_t)k * N + d] = xv[u];
+      const double yc = xv[u] - md;
+      Yc[(size_t)k * N + d] = yc;
+      t = (ccovmu * w[k]) * yc;
+      ok = ok && rmu_in_range(yc) && rmu_in_range(t);
+    }
+    tile[r][tx] = t;
+  }
+  if (k0 == 0 && ty == 0 && d0 + tx < N) prevMean[d0 + tx] = md;
+  __syncthreads();
+  for (int r = ty; r < RP_T; r += 8) {
+    const int d = d0 + r, k = k0 + tx;
+    if (d < N && k < mu) Tt[(size_t)d * mu + k] = tile[tx][r];
+  }
+  if (__syncthreads_or(!ok) && threadIdx.x == 0) atomicOr(&sc->rmuOutOfRange, 1u);
+  if (blockIdx.x || blockIdx.y) return;
+  // updateDistribution's best bookkeeping (:547-560), as k_update_best
+  __shared__ int flag;
+  if (threadIdx.x == 0) {
+    const unsigned i0 = sidx[0];
+    sc->bestValidSample = (double)i0;
+    sc->previousBestValue = sc->currentBestValue;
+    sc->currentBestValue = F[i0];
+    flag = (sc->currentBestValue > sc->bestEverValue || gen == 1) ? 1 : 0;
+    sc->bestFlag = (unsigned)flag;
+    if (flag) {
+      sc->previousBestEverValue = sc->bestEverValue;
+      sc->bestEverValue = sc->currentBestValue;
+    }
+  }
+  __syncthreads();
+  const unsigned i0 = sidx[0];
+  for (int d = threadIdx.x; d < N; d += blockDim.x) {
+    const double v = X[(size_t)i0 * N + d];
+    currBestVars[d] = v;
+    if (flag) bestEverVars[d] = v;
+  }
 }
 
 // one wave per row d (4 rows per workgroup), one lane per column e (64
@@ -2674,6 +2789,7 @@ __global__ void __launch_bounds__(256) k_sigma(int N, int mu, int isSigmaBounded
     sc->maxDiagC = mxd;
     sc->minDiagC = mnd;
     sc->sigma = sigma;
+    sc->rmuOutOfRange = 0u;  // (read by this update's adaptC; the next k_select_prep may set it)
     sc->currentMinStd = mns;
     sc->currentMaxStd = mxs;
     // next draw: the axis lengths come from C's eigenvalues (each <= trace
@@ -3940,11 +4056,28 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
       KG_HIP(hipMemcpyAsync(h->violDev, viol.data(), h->lam * sizeof(int), hipMemcpyHostToDevice, h->stream));
       KG_HIP(hipStreamSynchronize(h->stream));  // (viol is a temporary)
     }
+    // one launch for the best bookkeeping, the gather and the exact factors
+    // when nothing between them needs a grid-wide order (no constraints, no
+    // proportional weights, a k_sigma already cleared the range flag;
+    // KORALI_AMD_FUSED_SELECT=0: the three kernels)
+    static const bool fusedSel = [] {
+      const char *e = getenv("KORALI_AMD_FUSED_SELECT");
+      return !(e && *e == '0');
+    }();
+    const bool fused = fusedSel && !ccm && h->nc == 0 && h->cfg.mu_type != KG_MU_PROPORTIONAL &&
+                       h->cfg.cov_mode != KG_COV_MFMA && h->updates > 0;
+    if (fused) {
+      hipLaunchKernelGGL(k_select_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0, h->stream,
+                         N, mu, (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->mean, h->prevMean, h->Y,
+                         h->currBestVars, h->bestEverVars, h->sc, h->Yc, h->Tt);
+      KG_HIP(hipGetLastError());
+    } else {
     hipLaunchKernelGGL(k_update_best, dim3(1), dim3(256), 0, h->stream, N, mu, h->cfg.mu_type,
                        (unsigned long long)generation, h->X, h->F, h->idx, h->w, h->currBestVars, h->bestEverVars,
                        h->sc, ccm ? (const int *)h->violDev : (const int *)nullptr, h->lam);
     hipLaunchKernelGGL(k_gather_selected, dim3(mu), dim3(128), 0, h->stream, N, mu, h->X, h->idx, h->Y, h->mean,
                        h->prevMean);
+    }
     // the rank-mu sum (MFMA) needs only Y, the weights and m_prev: it runs on
     // the second stream while the mean and the evolution paths are computed.
     // The exact mode's factors (k_rankmu_prep, ~6 us) run in line: the two
@@ -3958,7 +4091,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                          h->covPart);
       KG_HIP(hipGetLastError());
       KG_HIP(hipEventRecord(h->evC, h->stream2));
-    } else {
+    } else if (!fused) {
       hipLaunchKernelGGL(k_rankmu_prep, dim3((mu + RP_T - 1) / RP_T, (N + RP_T - 1) / RP_T), dim3(256), 0,
                          h->stream, N, mu, h->Y, h->w, h->prevMean, h->sc, h->Yc, h->Tt);
       KG_HIP(hipGetLastError());
@@ -3999,6 +4132,21 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
                            h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc);
     }
     KG_HIP(hipGetLastError());
+  }
+  // C is final here (k_sigma and the termination record only read it): with
+  // the tridiagonalisation on the host core, the next eigendecomposition's
+  // hand-off (k_publish_c) goes ahead of k_sigma, so the host starts on C
+  // while sigma and the record are computed.  (CCMA-ES may still reset C in
+  // ccm_after_update; KORALI_AMD_EARLY_PUBLISH=0 restores the old order.)
+  static const bool early = [] {
+    const char *e = getenv("KORALI_AMD_EARLY_PUBLISH");
+    return !(e && *e == '0');
+  }();
+  if (early && !h->nc && h->eig.host_tridiag() && !h->cfg.diagonal_covariance) {
+    h->eig.trace = h->eigTrace;
+    if (h->eig.run_begin(h->C, 0, h->B, h->D, &h->sc->minEig, &h->sc->maxEig, &h->sc->eigenFailures,
+                         &h->sc->errors, h->stream, eig_prof, h))
+      return 1;
   }
   if (cmaes_sigma(h, generation)) return 1;  // (k_sigma also publishes the termination record)
   return h->nc ? ccm_after_update(h) : 0;
@@ -4313,6 +4461,7 @@ int kg_cmaes_set_field(kg_cmaes_t h, const char *name, const double *in, size_t 
   KG_HIP(hipMemcpyAsync(r.dev, in, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
   KG_HIP(hipStreamSynchronize(h->stream));
   h->stateDirty = true;
+  h->eig.invalidate();  // a decomposition issued ahead (kg_cmaes_update / _begin_sample) saw the old state
   return 0;
 }
 

@@ -3106,10 +3106,11 @@ EigenSolver::~EigenSolver() {
 // decomposition with run_finish.
 int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
                            double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx) {
+  if (begun) return 0;  // (already issued for this C: kg_cmaes_update publishes it ahead of k_sigma)
   begun = true;
   if (diagonal) return 0;  // k_eigen_diag runs in run_finish
   if (tri == 6) {  // C to the host core; the rest waits for it in run_finish
-    cSeq = chaseSeq + 1;
+    cSeq = ++pubSeq;  // (a new value per publication: a re-published C is never mistaken for the last one)
     if (prof) prof(profCtx, "eigen_publish_c", 0);
     hipLaunchKernelGGL(k_publish_c, dim3(pubc_groups(N)), dim3(64 * PUBC_WAVES), 0, s, N, C, d_C_map, ldc, dprog + 2,
                        cSeq, pubDone);
@@ -3121,7 +3122,7 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   double *d = dsd, *sd = dsd + N;
   if (prof) prof(profCtx, "eigen_tridiag", 0);
   const bool fusedPublish = hostChase && tri == 4;  // the one-workgroup kernel publishes d | sd itself
-  if (fusedPublish) dsdSeq = chaseSeq + 1;
+  if (fusedPublish) dsdSeq = ++pubSeq;  // (unique per publication, as cSeq)
   if (tri == 4) {
     hipLaunchKernelGGL(sqDpp ? k_tridiag_sq<true> : k_tridiag_sq<false>, dim3(1), dim3(SQ_TPB),
                        sq_lds_doubles(N) * sizeof(double), s, N, C, gH, tau, d, sd, trace,
@@ -3163,7 +3164,7 @@ int EigenSolver::run_begin(const double *C, int diagonal, double *B, double *D, 
   EigRec devRec = dev;
   if (hostChase) {
     if (!fusedPublish) {
-      dsdSeq = chaseSeq + 1;
+      dsdSeq = ++pubSeq;
       hipLaunchKernelGGL(k_publish_dsd, dim3(1), dim3(256), 0, s, N, (const double *)dsd, d_dsd_map, dprog + 1,
                          dsdSeq);
       KG_HIP(hipGetLastError());

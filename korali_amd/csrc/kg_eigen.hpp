@@ -30,6 +30,12 @@ class EigenSolver {
   int run_finish(const double *C, int diagonal, double *B, double *D, double *minEig, double *maxEig,
           double *eigenFailures, unsigned int *errors, hipStream_t s, ProfileFn prof, void *profCtx);
   bool begun = false;
+  // the caller changed C after run_begin: the next run() starts over
+  // (phase A again; a host hand-off is published again under a new sequence)
+  void invalidate() { begun = false; }
+  // C reaches the host core for the tridiagonalisation (tri == 6): run_begin
+  // only publishes C, so a caller may issue it as soon as C is final
+  bool host_tridiag() const { return tri == 6; }
   int t1flags = 0;  // KORALI_AMD_T1_FLAGS: experiment switches of k_tridiag_1wg
   bool sqDpp = true;  // k_tridiag_sq's scalar chains on registers / DPP broadcasts (KORALI_AMD_SQ_DPP=0: LDS-streamed)
   unsigned long long *trace = nullptr;  // optional device counters (k_tridiag sub-phases)
@@ -55,7 +61,7 @@ class EigenSolver {
   double *h_C = nullptr, *d_C_map = nullptr, *h_H = nullptr, *d_H_map = nullptr;
   int ldc = 0;  // row stride of h_C (even: 16-byte rows)
   unsigned int *pubDone = nullptr;  // k_publish_c's workgroup counter (device memory)
-  unsigned long long cSeq = 0;
+  unsigned long long cSeq = 0, pubSeq = 0;  // sequence of the C hand-off the host waits for; publications so far
   double *gA = nullptr, *gH = nullptr, *gQt = nullptr, *gWork = nullptr, *tau = nullptr, *dsd = nullptr,
          *chaseWork = nullptr;
   unsigned long long *comm = nullptr;  // in-launch hand-off granules (N > 128 tridiagonalisation)

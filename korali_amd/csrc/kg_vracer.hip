@@ -894,6 +894,77 @@ __global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const flo
   }
 }
 
+// One action component's importance-weight gradient factors, before the
+// weight's scaling, and its log-densities under the current and the
+// experience's policy (continuous.cpp.base:404-440 Normal, :482-560 Clipped
+// Normal; component i's bounds)
+__device__ inline void iw_grad_terms(const Params &P, int i, float a, float cm, float cs, float om, float osd,
+                                     float &pg0, float &pg1, float &lc, float &lo) {
+  const float dif = a - cm;
+  if (!P.clipped) {
+    const float inv_var = 1.f / (cs * cs);
+    pg0 = dif * inv_var;
+    pg1 = (dif * dif) * (inv_var / cs) - 1.f / cs;
+    lc = normal_logp(a, cm, cs);
+    lo = normal_logp(a, om, osd);
+    return;
+  }
+  const float inv_sig = 1.f / cs, lb = P.lb[i], ub = P.ub[i];
+  if (a <= lb) {
+    const float lcdf = normal_logcdf(lb, cm, cs);
+    const float r = expf(normal_logp(lb, cm, cs) - lcdf);
+    pg0 = -r;
+    pg1 = -dif * inv_sig * r;
+    lc = lcdf;
+    lo = normal_logcdf(lb, om, osd);
+  } else if (ub <= a) {
+    const float lccdf = normal_logccdf(ub, cm, cs);
+    const float r = expf(normal_logp(ub, cm, cs) - lccdf);
+    pg0 = r;
+    pg1 = dif * inv_sig * r;
+    lc = lccdf;
+    lo = normal_logccdf(ub, om, osd);
+  } else {
+    const float inv_sig3 = inv_sig * inv_sig * inv_sig;
+    pg0 = dif * inv_sig * inv_sig;
+    pg1 = dif * dif * inv_sig3 - inv_sig;
+    lc = normal_logp(a, cm, cs);
+    lo = normal_logp(a, om, osd);
+  }
+}
+
+// One action component's KL-divergence gradient with respect to the current
+// mean and sigma (continuous.cpp.base:697-732 Normal, :734-777 Clipped Normal)
+__device__ inline void kl_grad_terms(const Params &P, int i, float cm, float cs, float om, float osd, float &km,
+                                     float &ks) {
+  const float inv_sig = (float)(1. / (double)cs);
+  const float inv_var = (float)(1. / (double)(cs * cs));
+  const float inv_sig3 = (float)(1. / (double)(cs * cs * cs));
+  const float d = cm - om;
+  km = d * inv_var;
+  ks = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
+  if (!P.clipped) return;
+  const float lb = P.lb[i], ub = P.ub[i];
+  const float oldVar = osd * osd, oldInvSig = 1.f / osd, curInvSig = 1.f / cs;
+  const float curInvVar = 1.f / (cs * cs), curInvSig3 = 1.f / (cs * cs * cs), muDif = om - cm;
+  const float invSqrt2Pi = (float)(M_SQRT1_2 * sqrt(M_1_PI));
+  const float oldAdjLb = (lb - om) * oldInvSig, oldAdjUb = (ub - om) * oldInvSig;
+  const float curAdjLb = (lb - cm) * curInvSig, curAdjUb = (ub - cm) * curInvSig;
+  const float erfLb = (float)erf(M_SQRT1_2 * (double)oldAdjLb), erfUb = (float)erf(M_SQRT1_2 * (double)oldAdjUb);
+  const float expLb = expf(-0.5f * oldAdjLb * oldAdjLb), expUb = expf(-0.5f * oldAdjUb * oldAdjUb);
+  const float cdfA = expf(normal_logcdf(lb, om, osd) + normal_logp(lb, cm, cs) - normal_logcdf(lb, cm, cs));
+  const float ccdfB = expf(normal_logccdf(ub, om, osd) + normal_logp(ub, cm, cs) - normal_logccdf(ub, cm, cs));
+  km = cdfA;
+  km -= 0.5f * muDif * curInvVar * (erfUb - erfLb);
+  km += invSqrt2Pi * osd * curInvVar * (expUb - expLb);
+  km -= ccdfB;
+  ks = curAdjLb * cdfA;
+  ks += 0.5f * (curInvSig - muDif * muDif * curInvSig3 - oldVar * curInvSig3) * (erfUb - erfLb);
+  ks += invSqrt2Pi * curInvSig3 * (oldVar * oldAdjUb + 2.f * osd * muDif) * expUb;
+  ks -= invSqrt2Pi * curInvSig3 * (oldVar * oldAdjLb + 2.f * osd * muDif) * expLb;
+  ks -= curAdjUb * ccdfB;
+}
+
 // updateExperienceMetadata (agent.cpp.base:599-735) + the VRACER loss
 // gradient (VRACER.cpp.base:89-181) + the REF-ER schedule (agent.cpp.base:
 // 221-231), one workgroup.  Every mini-batch row's metadata lives in LDS
@@ -901,7 +972,9 @@ __global__ __launch_bounds__(256) void k_vr_fwd_fused(Params P, int M, const flo
 // truncated weights of mini-batch entries from LDS and leave each row's
 // retrace value (and its successor's) there, so the gradient phase reads no
 // global memory, and the replay-memory metadata is written once at the end
-// (no global store is waited for at the first barrier).  A == 1.
+// (no global store is waited for at the first barrier).  One action
+// component's operands live in LDS; with more, the gradient phase reads them
+// from the replay memory and the forward's output.
 constexpr int MB_META = 1024;
 #ifndef VR_RC
 #define VR_RC 16  // retrace chunk: entries per load round trip of a walk
@@ -953,12 +1026,24 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
     const unsigned id = mb[b];
     const bool uniq = b == 0 || id != mb[b - 1];
     const long long p = ph(id);
-    const float a = er.act[p], om = er.exp_pol[2 * p], osd = er.exp_pol[2 * p + 1],
+    const float a = er.act[p * P.A], om = er.exp_pol[2 * P.A * p], osd = er.exp_pol[2 * P.A * p + P.A],
                 rew = RR ? er.rew[p] / st->rsig[er.env[p]] : er.rew[p];
     const int was = er.onp[p], term = er.term[p];
-    const float V = out[(long long)b * O], cm = out[(long long)b * O + 1], cs = out[(long long)b * O + 2];
+    const float V = out[(long long)b * O], cm = out[(long long)b * O + 1], cs = out[(long long)b * O + 1 + P.A];
     const float tvv = term == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
-    float liw = policy_logp(P, 0, a, cm, cs) - policy_logp(P, 0, a, om, osd);
+    float liw;
+    if (P.A == 1) {
+      liw = policy_logp(P, 0, a, cm, cs) - policy_logp(P, 0, a, om, osd);
+    } else {  // calculateImportanceWeight's sums over the action components, in order
+      const int A = P.A;
+      float lc = 0.0f, lo = 0.0f;
+      for (int i = 0; i < A; i++) {
+        const float ai = er.act[p * A + i];
+        lc += policy_logp(P, i, ai, out[(long long)b * O + 1 + i], out[(long long)b * O + 1 + A + i]);
+        lo += policy_logp(P, i, ai, er.exp_pol[p * 2 * A + i], er.exp_pol[p * 2 * A + A + i]);
+      }
+      liw = lc - lo;
+    }
     if (liw > 7.f) liw = 7.f;
     if (liw < -7.f) liw = -7.f;
     if (!isfinite(liw)) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_IW);
@@ -1256,92 +1341,73 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
   // ---- the VRACER loss gradient (VRACER.cpp.base:104-177), all from LDS;
   // then the replay memory's metadata (first occurrences)
   const float klm = -(1.0f - beta);
+  const int A = P.A;
   for (int b = t; b < B; b += nt) {
-    const float V = s_V[b], cm = s_cur[2 * b], cs = s_cur[2 * b + 1], om = s_old[2 * b], osd = s_old[2 * b + 1];
-    const float a = s_act[b];
+    const long long p = ph(s_mb[b]);
+    // action component i of row b: the stored action, the current policy (the
+    // forward's output) and the experience's policy; one component from LDS
+    auto comp = [&](int i, float &a, float &cm, float &cs, float &om, float &osd) __attribute__((always_inline)) {
+      if (A == 1) {
+        a = s_act[b], cm = s_cur[2 * b], cs = s_cur[2 * b + 1], om = s_old[2 * b], osd = s_old[2 * b + 1];
+      } else {
+        a = er.act[p * A + i], cm = out[(long long)b * O + 1 + i], cs = out[(long long)b * O + 1 + A + i];
+        om = er.exp_pol[p * 2 * A + i], osd = er.exp_pol[p * 2 * A + A + i];
+      }
+    };
+    const float V = s_V[b];
     const int term = u8v(s_term[b]);
-    float g[3];
+    float g[MAXO];
+#pragma unroll
+    for (int i = 0; i < MAXO; i++) g[i] = 0.f;
     g[0] = s_ret[b] - V;
-    g[1] = g[2] = 0.f;
     if (u8v(s_onp[b])) {
       float q = s_rew[b];
       if (term == NON_TERMINAL) q += P.gamma * s_retn[b];
       if (term == TRUNCATED) q += P.gamma * s_tv[b];
       const float loss = q - V;
-      float pg0, pg1, lc, lo;
-      const float dif = a - cm;
-      if (!P.clipped) {  // continuous.cpp.base:404-440
-        const float inv_var = 1.f / (cs * cs);
-        pg0 = dif * inv_var;
-        pg1 = (dif * dif) * (inv_var / cs) - 1.f / cs;
-        lc = normal_logp(a, cm, cs);
-        lo = normal_logp(a, om, osd);
-      } else {  // continuous.cpp.base:482-560
-        const float inv_sig = 1.f / cs;
-        if (a <= P.lb[0]) {
-          const float lcdf = normal_logcdf(P.lb[0], cm, cs);
-          const float r = expf(normal_logp(P.lb[0], cm, cs) - lcdf);
-          pg0 = -r;
-          pg1 = -dif * inv_sig * r;
-          lc = lcdf;
-          lo = normal_logcdf(P.lb[0], om, osd);
-        } else if (P.ub[0] <= a) {
-          const float lccdf = normal_logccdf(P.ub[0], cm, cs);
-          const float r = expf(normal_logp(P.ub[0], cm, cs) - lccdf);
-          pg0 = r;
-          pg1 = dif * inv_sig * r;
-          lc = lccdf;
-          lo = normal_logccdf(P.ub[0], om, osd);
-        } else {
-          const float inv_sig3 = inv_sig * inv_sig * inv_sig;
-          pg0 = dif * inv_sig * inv_sig;
-          pg1 = dif * dif * inv_sig3 - inv_sig;
-          lc = normal_logp(a, cm, cs);
-          lo = normal_logp(a, om, osd);
+      // calculateImportanceWeightGradient: per component the factors, the
+      // log-densities summed in component order, then the weight
+      float pg[2 * MAXA], lcs = 0.0f, los = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MAXA; i++)
+        if (i < A) {
+          float a, cm, cs, om, osd, lc, lo;
+          comp(i, a, cm, cs, om, osd);
+          iw_grad_terms(P, i, a, cm, cs, om, osd, pg[i], pg[MAXA + i], lc, lo);
+          lcs += lc;
+          los += lo;
         }
+      const float iwg = expf(lcs - los);
+#pragma unroll
+      for (int i = 0; i < MAXA; i++)
+        if (i < A) {
+          g[1 + i] = beta * loss * (pg[i] * iwg);
+          g[1 + A + i] = beta * loss * (pg[MAXA + i] * iwg);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MAXA; i++)
+      if (i < A) {
+        float a, cm, cs, om, osd, km, ks;
+        comp(i, a, cm, cs, om, osd);
+        kl_grad_terms(P, i, cm, cs, om, osd, km, ks);
+        g[1 + i] += klm * km;
+        g[1 + A + i] += klm * ks;
       }
-      const float iwg = expf(0.0f + lc - lo);
-      g[1] = beta * loss * (pg0 * iwg);
-      g[2] = beta * loss * (pg1 * iwg);
-    }
-    {
-      const float inv_sig = (float)(1. / (double)cs);
-      const float inv_var = (float)(1. / (double)(cs * cs));
-      const float inv_sig3 = (float)(1. / (double)(cs * cs * cs));
-      const float d = cm - om;
-      float kl_mean = d * inv_var;
-      float kl_sig = -inv_sig3 * osd * osd + -(d * d) * inv_sig3 + inv_sig;
-      if (P.clipped) {  // continuous.cpp.base:734-777
-        const float lb = P.lb[0], ub = P.ub[0];
-        const float oldVar = osd * osd, oldInvSig = 1.f / osd, curInvSig = 1.f / cs;
-        const float curInvVar = 1.f / (cs * cs), curInvSig3 = 1.f / (cs * cs * cs), muDif = om - cm;
-        const float invSqrt2Pi = (float)(M_SQRT1_2 * sqrt(M_1_PI));
-        const float oldAdjLb = (lb - om) * oldInvSig, oldAdjUb = (ub - om) * oldInvSig;
-        const float curAdjLb = (lb - cm) * curInvSig, curAdjUb = (ub - cm) * curInvSig;
-        const float erfLb = (float)erf(M_SQRT1_2 * (double)oldAdjLb), erfUb = (float)erf(M_SQRT1_2 * (double)oldAdjUb);
-        const float expLb = expf(-0.5f * oldAdjLb * oldAdjLb), expUb = expf(-0.5f * oldAdjUb * oldAdjUb);
-        const float cdfA = expf(normal_logcdf(lb, om, osd) + normal_logp(lb, cm, cs) - normal_logcdf(lb, cm, cs));
-        const float ccdfB = expf(normal_logccdf(ub, om, osd) + normal_logp(ub, cm, cs) - normal_logccdf(ub, cm, cs));
-        kl_mean = cdfA;
-        kl_mean -= 0.5f * muDif * curInvVar * (erfUb - erfLb);
-        kl_mean += invSqrt2Pi * osd * curInvVar * (expUb - expLb);
-        kl_mean -= ccdfB;
-        kl_sig = curAdjLb * cdfA;
-        kl_sig += 0.5f * (curInvSig - muDif * muDif * curInvSig3 - oldVar * curInvSig3) * (erfUb - erfLb);
-        kl_sig += invSqrt2Pi * curInvSig3 * (oldVar * oldAdjUb + 2.f * osd * muDif) * expUb;
-        kl_sig -= invSqrt2Pi * curInvSig3 * (oldVar * oldAdjLb + 2.f * osd * muDif) * expLb;
-        kl_sig -= curAdjUb * ccdfB;
+#pragma unroll
+    for (int i = 0; i < MAXO; i++)
+      if (i < O) {
+        if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
+        G[(long long)b * O + i] = g[i];
       }
-      g[1] += klm * kl_mean;
-      g[2] += klm * kl_sig;
-    }
-    for (int i = 0; i < 3; i++) {
-      if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
-      G[(long long)b * O + i] = g[i];
-    }
     if (u8v(s_uniq[b])) {
-      const long long p = ph(s_mb[b]);
-      er.cur_pol[2 * p] = cm, er.cur_pol[2 * p + 1] = cs;
+#pragma unroll
+      for (int i = 0; i < MAXA; i++)
+        if (i < A) {
+          float a, cm, cs, om, osd;
+          comp(i, a, cm, cs, om, osd);
+          er.cur_pol[p * 2 * A + i] = cm, er.cur_pol[p * 2 * A + A + i] = cs;
+        }
       er.v[p] = V;
       er.tv[p] = s_tv[b];
       er.iw[p] = s_iw[b];

@@ -209,6 +209,63 @@ def test_policy_updates_match_oracle(H, L, B, clipped):
         assert np.isclose(d.scalar("off_policy_cutoff"), float(ag.cutoff), rtol=1e-7)
 
 
+def fill_synthetic(Sx, Ax, H, L, n_eps, seed, bounds=None, max_size=600):
+    """An oracle agent's replay memory filled with synthetic episodes of Sx
+    state and Ax action variables (a host environment's shapes): states and
+    rewards from a seeded generator, actions drawn from the agent's own
+    policy (clipped to the bounds), the policy and value stored as
+    processEpisode stores them; terminal and truncated endings alternate."""
+    n = V.hyperparameter_count(Sx, H, L, Ax)
+    rng = np.random.default_rng(seed)
+    th = (V.initial_hyperparameters(Sx, H, L, Ax, rng.uniform(-1, 1, n))
+          + 0.15 * rng.standard_normal(n) / np.sqrt(H)).astype(f32)
+    ag = V.Agent(Sx, Ax, H, L, th, max_size=max_size, bounds=bounds)
+    for ep in range(n_eps):
+        T = int(rng.integers(1, 30))
+        states = rng.uniform(-1, 1, (T, Sx)).astype(f32)
+        out = ag.policy(states)
+        acts = (out[:, 1:1 + Ax] + out[:, 1 + Ax:] * rng.standard_normal((T, Ax)).astype(f32)).astype(f32)
+        if bounds is not None:
+            acts = np.clip(acts, bounds[0], bounds[1]).astype(f32)
+        rewards = rng.normal(0, 1, T).astype(f32)
+        term = V.TERMINAL if ep % 2 else V.TRUNCATED
+        ag.process_episode(ep % 3, states, acts, rewards, out[:, 1:], out[:, 0], term,
+                           tstate=rng.uniform(-1, 1, Sx).astype(f32))
+    return ag, th
+
+
+@pytest.mark.parametrize("Sx,Ax,clipped", [(3, 2, False), (3, 2, True), (5, 4, True), (2, 3, False)])
+def test_multi_action_policy_updates_match_oracle(Sx, Ax, clipped):
+    """VRACER::trainPolicy with several action components (a host
+    environment's agent): the importance weights and their gradients sum the
+    components' log-densities in order (continuous.cpp.base:278-397,
+    :399-560), the KL gradient is per component (:697-777); five updates
+    against the oracle as test_policy_updates_match_oracle."""
+    H, L, B = 64, 2, 64
+    bounds = (np.full(Ax, -0.5, f32), np.full(Ax, 0.5, f32)) if clipped else None
+    ag, th = fill_synthetic(Sx, Ax, H, L, 60, 11, bounds)
+    kw = dict(policy_distribution="Clipped Normal", action_lower_bound=-0.5, action_upper_bound=0.5) if clipped \
+        else {}
+    d = device(state_size=Sx, action_size=Ax, hidden_size=H, hidden_layers=L, environments=8, mini_batch_size=B,
+               replay_maximum_size=600, replay_start_size=100, hyperparameters=th, host_environment=True, **kw)
+    if clipped:
+        acts = np.concatenate(ag.er["action"])
+        assert np.any(acts <= -0.5) and np.any(acts >= 0.5) and np.any(np.abs(acts) < 0.5)
+    load_replay(d, ag)
+    rng = np.random.default_rng(5)
+    for u in range(5):
+        ids = np.sort(rng.integers(0, ag.size() - 1, B)).astype(np.uint32)
+        G, grad = ag.train_policy([int(i) for i in ids])
+        d.train_minibatch(ids)
+        close(d.get("loss_gradient").reshape(B, -1), G, 1e-3, 1e-4)
+        close(d.get("gradient"), grad, 2e-3, 2e-3 * np.abs(grad).max())
+        close(d.hyperparameters, ag.theta, 1e-4, 1e-6)
+        assert np.array_equal(d.get("on_policy")[:ag.size()], np.array(ag.er["onp"], np.int32))
+        close(d.get("importance_weight")[:ag.size()], np.array(ag.er["iw"], f32), 1e-4, 1e-6)
+        close(d.get("cur_policy").reshape(-1, 2 * Ax)[:ag.size()], np.stack(ag.er["cur_pol"]), 1e-4, 1e-6)
+        assert d.scalar("off_policy_count") == ag.off_count
+
+
 @pytest.mark.parametrize("clipped,R,T,rr", [(False, 700, 40, False), (True, 700, 40, False), (False, 40, 5, False),
                                            (False, 700, 40, True), (False, 40, 5, True)])
 def test_environment_steps_match_oracle(clipped, R, T, rr):
