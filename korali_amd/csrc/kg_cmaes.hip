@@ -1966,6 +1966,8 @@ __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__re
   const int row = lane >> 4, j = lane & 15, dl = 4 * wid + row;
   const int d0 = blockIdx.x * 16;
   const int nch = (mu + MR_K - 1) / MR_K;
+  // the epilogue's operands, read now rather than after the chain
+  const double pmd = (j == 0 && d0 + dl < N) ? prevMean[d0 + dl] : 0.0, sig = sc->sigma;
   // chunk loads: 256 threads x MR_U values of the (MR_K x 16) block, + w
   double ld[MR_U], wl = 0.0;
   auto load = [&](int ch) {
@@ -1993,6 +1995,9 @@ __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__re
     const int b = ch & 1;
     if (ch + 1 < nch) load(ch + 1);
     const int gn = min(MR_K, mu - ch * MR_K + 15) >> 4;  // groups of 16 (the tail is zero-padded)
+    // (a software-pipelined form -- group g + 1's product and g + 2's LDS
+    // reads issued right after group g's adds -- measured slower here and in
+    // k_adaptC_row, round 6: 50.0 / 40.9 against 48.0 / 36.3 us)
     for (int g = 0; g < gn; g++) {
       const double q = ws[b][16 * g + j] * ys[b][dl][16 * g + j];  // the product, rounded, then added
       acc = chains::kc_row16(acc, q);
@@ -2003,7 +2008,7 @@ __global__ void __launch_bounds__(256) k_mean3(int N, int mu, const double *__re
   const int d = d0 + dl;
   if (j == 0 && d < N) {
     mean[d] = acc;
-    meanUpdate[d] = (acc - prevMean[d]) / sc->sigma;  // (prevMean: copied by k_gather_selected)
+    meanUpdate[d] = (acc - pmd) / sig;  // (prevMean: copied by k_gather_selected / k_select_prep)
   }
 }
 
@@ -2021,6 +2026,16 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = lane >> 4, j = lane & 15;
   const double cs = sc->sigmaCumulationFactor, effMu = sc->effectiveMu, cc = sc->cumulativeCovariance;
+  // every other operand read up front with B (one round of loads, not one per phase)
+  const double chi = sc->chiSquareNumber, hpGen = sc->hsigPowGen, hpCs = sc->hsigPowCs, hp = sc->hsigPow;
+  const double pcq = tid < N ? pc[tid] : 0.0, muq = tid < N ? meanUpdate[tid] : 0.0;
+  double Dd[2], psd[2];
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const int d = 64 * p + 4 * wid + row;
+    Dd[p] = (j == 0 && d < N) ? D[d] : 1.0;
+    psd[p] = (j == 0 && d < N) ? ps[d] : 0.0;
+  }
   const int G = (N + 15) >> 4;  // groups of 16 along e
   // chains of this lane's rows: d = 64 p + 4 wid + row, p = 0, 1
   double b1[2][8], b2[2][8];
@@ -2049,7 +2064,7 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
     for (int g = 0; g < 8; g++)
       if (g < G) acc = chains::kc_row16(acc, b1[p][g] * mu_s[16 * g + j]);
     if (j == 0 && d < N) {
-      const double a = acc / D[d];
+      const double a = acc / Dd[p];
       aux_s[d] = a;
       auxBDZ[d] = a;
     }
@@ -2066,7 +2081,7 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
     for (int g = 0; g < 8; g++)
       if (g < G) acc = chains::kc_row16(acc, b2[p][g] * aux_s[16 * g + j]);
     if (j == 0 && d < N) {
-      const double pv = (1. - cs) * ps[d] + fac * acc;
+      const double pv = (1. - cs) * psd[p] + fac * acc;
       ps[d] = pv;
       pn_s[d] = pv * pv;  // std::pow(x, 2.0) == x*x (CR)
     }
@@ -2080,8 +2095,8 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
     if (lane == 0) {
       const double nrm = sqrt(nrm2);
       sc->psNorm = nrm;
-      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - hsig_pow(sc, cs, gen)) /
-                                                   sc->chiSquareNumber);
+      const double hpw = (hpGen == (double)gen && hpCs == cs) ? hp : pow_cr(1. - cs, 2.0 * (1.0 + (double)gen));
+      const int hsig = (1.4 + 2.0 / (N + 1) > nrm / sqrt(1. - hpw) / chi);
       hs = hsig;
       sc->hsig = hsig;
       const double a = N + 1.3, b = N + 2.0;
@@ -2094,7 +2109,7 @@ __global__ void __launch_bounds__(PR_T) k_paths3(int N, unsigned long long gen, 
   }
   __syncthreads();
   const double fac2 = sqrt(cc * (2. - cc) * effMu);
-  for (int q = tid; q < N; q += PR_T) pc[q] = (1. - cc) * pc[q] + hs * fac2 * meanUpdate[q];
+  if (tid < N) pc[tid] = (1. - cc) * pcq + hs * fac2 * muq;  // (N <= 128 < PR_T)
 }
 
 // evolution paths for N <= 128 (full covariance): B staged once in LDS (row

@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B of environment switches on the C2 bench line: each argument is one
+# setting ("-" = defaults, or VAR=VALUE[,VAR=VALUE]); prints generations/s and
+# the per-stage device times of each.  Every run under its own time limit.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/ab
+for cfg in "$@"; do
+  envs=()
+  [ "$cfg" != "-" ] && IFS=, read -ra envs <<< "$cfg"
+  timeout -k 10 200 env "${envs[@]}" python bench.py --steps ${STEPS_AB:-200} --warmup 10 --no-cpu-baseline --no-c1 \
+    > gpurun_out/ab/run.log 2>&1 || { echo "FAILED $cfg"; tail -5 gpurun_out/ab/run.log; exit 1; }
+  python3 - "$cfg" <<'PY'
+import json, sys
+d = [json.loads(l) for l in open("gpurun_out/ab/run.log") if l.startswith("{")][-1]
+st = {k: round(v * 1e3, 1) for k, v in d["stage_ms"].items()}
+print(f"{sys.argv[1]:40s} {d['value']:8.1f} gen/s  {st}", flush=True)
+PY
+done
