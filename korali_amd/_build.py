@@ -36,7 +36,7 @@ def sources():
 # kg_host_tridiag.cpp): g++, no FMA, one body per instruction set
 HOST_SRC = os.path.join(CSRC, "kg_host_tridiag.cpp")
 HOST_OBJ = os.path.join(CSRC, "kg_host_tridiag.o")
-HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-math-errno", "-Wall", "-Wno-psabi"]
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-ffp-contract=off", "-fno-math-errno", "-Wall", "-Wno-psabi"]
 
 
 def _stale(target, deps):
@@ -63,7 +63,7 @@ def build(force=False, verbose=False):
     deps = sources() + [os.path.join(ROOT, "include", "korali_amd.h")]
     if force or _stale(LIB, deps):
         _run(["g++"] + HOST_FLAGS + ["-c", "-o", HOST_OBJ, HOST_SRC], verbose)
-        _run([HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip"), "-Wl," + HOST_OBJ], verbose)
+        _run([HIPCC] + FLAGS + ["-o", LIB, os.path.join(CSRC, "korali_amd.hip"), "-Wl," + HOST_OBJ, "-pthread"], verbose)
     build_engine(force, verbose)
     return LIB
 

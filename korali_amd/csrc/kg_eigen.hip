@@ -3247,6 +3247,7 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     }
     if (tri == 6) {
       if (prof) prof(profCtx, "eigen_c_wait", 2);
+      htri.wake();  // (the helper threads of a multi-threaded pass spin from here on)
       const auto t0 = std::chrono::steady_clock::now();
       while (__atomic_load_n(hprog + 2, __ATOMIC_ACQUIRE) != cSeq) {  // busy-wait for C (µs)
         __builtin_ia32_pause();

@@ -1356,10 +1356,12 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
     };
     const float V = s_V[b];
     const int term = u8v(s_term[b]);
-    float g[MAXO];
+    // (means and sigmas in separate register arrays: every index a
+    // compile-time constant, no indexed register access)
+    float gm[MAXA], gs[MAXA];
 #pragma unroll
-    for (int i = 0; i < MAXO; i++) g[i] = 0.f;
-    g[0] = s_ret[b] - V;
+    for (int i = 0; i < MAXA; i++) gm[i] = gs[i] = 0.f;
+    const float g0 = s_ret[b] - V;
     if (u8v(s_onp[b])) {
       float q = s_rew[b];
       if (term == NON_TERMINAL) q += P.gamma * s_retn[b];
@@ -1367,13 +1369,13 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
       const float loss = q - V;
       // calculateImportanceWeightGradient: per component the factors, the
       // log-densities summed in component order, then the weight
-      float pg[2 * MAXA], lcs = 0.0f, los = 0.0f;
+      float pm[MAXA], ps[MAXA], lcs = 0.0f, los = 0.0f;
 #pragma unroll
       for (int i = 0; i < MAXA; i++)
         if (i < A) {
           float a, cm, cs, om, osd, lc, lo;
           comp(i, a, cm, cs, om, osd);
-          iw_grad_terms(P, i, a, cm, cs, om, osd, pg[i], pg[MAXA + i], lc, lo);
+          iw_grad_terms(P, i, a, cm, cs, om, osd, pm[i], ps[i], lc, lo);
           lcs += lc;
           los += lo;
         }
@@ -1381,8 +1383,8 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
 #pragma unroll
       for (int i = 0; i < MAXA; i++)
         if (i < A) {
-          g[1 + i] = beta * loss * (pg[i] * iwg);
-          g[1 + A + i] = beta * loss * (pg[MAXA + i] * iwg);
+          gm[i] = beta * loss * (pm[i] * iwg);
+          gs[i] = beta * loss * (ps[i] * iwg);
         }
     }
 #pragma unroll
@@ -1391,15 +1393,19 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
         float a, cm, cs, om, osd, km, ks;
         comp(i, a, cm, cs, om, osd);
         kl_grad_terms(P, i, cm, cs, om, osd, km, ks);
-        g[1 + i] += klm * km;
-        g[1 + A + i] += klm * ks;
+        gm[i] += klm * km;
+        gs[i] += klm * ks;
       }
+    unsigned bad = !isfinite(g0);
+    G[(long long)b * O] = g0;
 #pragma unroll
-    for (int i = 0; i < MAXO; i++)
-      if (i < O) {
-        if (!isfinite(g[i])) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
-        G[(long long)b * O + i] = g[i];
+    for (int i = 0; i < MAXA; i++)
+      if (i < A) {
+        bad |= !isfinite(gm[i]) | !isfinite(gs[i]);
+        G[(long long)b * O + 1 + i] = gm[i];
+        G[(long long)b * O + 1 + A + i] = gs[i];
       }
+    if (bad) atomicOr(&st->errors, (unsigned)ERR_NONFINITE_GRADIENT);
     if (u8v(s_uniq[b])) {
 #pragma unroll
       for (int i = 0; i < MAXA; i++)

@@ -83,3 +83,22 @@ def test_host_tridiag_zero_columns_and_tiny_scales():
 def test_host_tridiag_is_deterministic_across_sizes_in_one_process():
     for N in (40, 8, 130, 40):
         _check(_spd(N, 11 + N))
+
+
+@pytest.mark.parametrize("threads", [2, 3, 5])
+@pytest.mark.parametrize("N", [9, 16, 17, 33, 70, 128, 200, 257])
+def test_multi_threaded_pass_matches_oracle_bit_exact(monkeypatch, N, threads):
+    """The pass split over helper threads (two blocked copies of the lower
+    triangle: column sums down column blocks, row chains along row blocks,
+    the same operands in the same order per element) equals the oracle bit
+    for bit, for any thread count, block remainders included."""
+    monkeypatch.setenv("KORALI_AMD_HOST_TRIDIAG_THREADS", str(threads))
+    C = _spd(N, N + threads)
+    C[np.triu_indices(N, 1)] = np.nan
+    _check(C)
+
+
+def test_multi_threaded_pass_zero_columns_and_tiny_scales(monkeypatch):
+    monkeypatch.setenv("KORALI_AMD_HOST_TRIDIAG_THREADS", "3")
+    test_host_tridiag_zero_columns_and_tiny_scales()
+    _check(_spd(512, 9))

@@ -1,6 +1,6 @@
 // Phase times of the host tridiagonalisation (kg_host_tridiag.cpp built with
 // KG_HT_PHASES) on a Wishart matrix: build and run on the box's core,
-//   g++ -O3 -std=c++17 -ffp-contract=off -fno-math-errno -Wno-psabi -DKG_HT_PHASES \
+//   g++ -O3 -std=c++17 -pthread -ffp-contract=off -fno-math-errno -Wno-psabi -DKG_HT_PHASES \
 //       -I korali_amd/csrc -o tools/host_tridiag_phases tools/host_tridiag_phases.cpp \
 //       korali_amd/csrc/kg_host_tridiag.cpp
 //   tools/host_tridiag_phases 128 400
