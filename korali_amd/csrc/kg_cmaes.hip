@@ -4058,6 +4058,23 @@ static int ccm_after_update(kg_cmaes_t h) {
   return 0;
 }
 
+// C is final once the covariance update has run (k_sigma and the
+// termination record only read it): with the tridiagonalisation on the host
+// core, the next eigendecomposition's hand-off (k_publish_c) goes ahead of
+// k_sigma, so the host starts on C while sigma and the record are computed.
+// (CCMA-ES may still reset C in ccm_after_update; KORALI_AMD_EARLY_PUBLISH=0
+// restores the order publish-after-sigma.)
+static int early_publish(kg_cmaes_t h) {
+  static const bool early = [] {
+    const char *e = getenv("KORALI_AMD_EARLY_PUBLISH");
+    return !(e && *e == '0');
+  }();
+  if (!early || h->nc || !h->eig.host_tridiag() || h->cfg.diagonal_covariance) return 0;
+  h->eig.trace = h->eigTrace;
+  return h->eig.run_begin(h->C, 0, h->B, h->D, &h->sc->minEig, &h->sc->maxEig, &h->sc->eigenFailures, &h->sc->errors,
+                          h->stream, eig_prof, h);
+}
+
 int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
   KG_CHECK(h->shards == 1, "a population-sharded handle updates through kg_cmaes_update_partial / _finalize");
   const int N = h->N, mu = h->mu;
@@ -4148,21 +4165,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
     }
     KG_HIP(hipGetLastError());
   }
-  // C is final here (k_sigma and the termination record only read it): with
-  // the tridiagonalisation on the host core, the next eigendecomposition's
-  // hand-off (k_publish_c) goes ahead of k_sigma, so the host starts on C
-  // while sigma and the record are computed.  (CCMA-ES may still reset C in
-  // ccm_after_update; KORALI_AMD_EARLY_PUBLISH=0 restores the old order.)
-  static const bool early = [] {
-    const char *e = getenv("KORALI_AMD_EARLY_PUBLISH");
-    return !(e && *e == '0');
-  }();
-  if (early && !h->nc && h->eig.host_tridiag() && !h->cfg.diagonal_covariance) {
-    h->eig.trace = h->eigTrace;
-    if (h->eig.run_begin(h->C, 0, h->B, h->D, &h->sc->minEig, &h->sc->maxEig, &h->sc->eigenFailures,
-                         &h->sc->errors, h->stream, eig_prof, h))
-      return 1;
-  }
+  if (early_publish(h)) return 1;
   if (cmaes_sigma(h, generation)) return 1;  // (k_sigma also publishes the termination record)
   return h->nc ? ccm_after_update(h) : 0;
 }
@@ -4280,6 +4283,7 @@ int kg_cmaes_update_finalize(kg_cmaes_t h, size_t generation) {
     Stage st(h, "covariance");
     hipLaunchKernelGGL(k_shard_cov_unpack, dim3(N), dim3(256), 0, h->stream, N, (const double *)h->covPack, h->C);
     KG_HIP(hipGetLastError());
+    if (early_publish(h)) return 1;
     return cmaes_sigma(h, generation);
   }
   {
