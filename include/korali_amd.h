@@ -250,6 +250,14 @@ int kg_debug_mt_jump(const uint32_t *window624, uint64_t distance, uint32_t *out
  * (H[i][0] = sd[i], the reflector's entries after it), tau (N), d (N),
  * sd (N).  Runs on the host, no device needed. */
 int kg_debug_host_tridiag(size_t N, const double *C, double *H, double *tau, double *d, double *sd);
+/* The host core's Givens chase (phase C of the eigendecomposition, GSL
+ * eigen/symmv.c + qrstep.c as kg_eigen.hip's qr_chase) on the tridiagonal
+ * (d[N], sd[N-1]) reps times: sorted eigenvalues (ABS_ASC) and their
+ * permutation, counts[3] = {QR steps, rotations, overflow}, the first cs_cap
+ * rotation values (c, s pairs) and the mean wall time per chase.  fused
+ * selects the sweep with the chop test folded in.  CPU only (no device code). */
+int kg_debug_host_chase(size_t N, const double *d, const double *sd, int fused, size_t reps, double *eval, int *perm,
+                        double *cs, size_t cs_cap, int *counts, double *ns_per_chase);
 /* Host-only check of the TMCMC resampling (no device call): `reps`
  * consecutive gsl_ran_multinomial draws (K categories, N trials) from one
  * mt19937 seeded with `seed`, by the exact conditional-binomial walk

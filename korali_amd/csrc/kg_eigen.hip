@@ -249,6 +249,87 @@ __host__ __device__ void qrstep(int n, double *d, double *sd, double *gc, double
   sd[k - 1] = bk;
 }
 
+// qrstep with the chase's bookkeeping folded into the sweep: each rotation
+// goes straight to the rotation record (cs: c, s pairs), and chop_small's
+// test of index k-1 (|sd[k-1]| < eps (|d[k-1]| + |d[k]|)) runs at iteration
+// k, when d[k-1], d[k] and sd[k-1] hold their final values of this step --
+// the same values chop_small reads after the step, so the same zeros.  The
+// sweep never reads sd[k-1] again after iteration k.  The tests sit off the
+// rotation chain (the core runs them in the shadow of its divisions), where
+// the separate pass and the copy were ~15% of the chase.
+__host__ __device__ void qrstep_fused(int n, double *d, double *sd, double *cs) {
+  double x, z, ak, bk, zk, ap, bp, aq, bq;
+  double mu;
+  {
+    const double ta = d[n - 2], tb = d[n - 1], tab = sd[n - 2];
+    const double dt = (ta - tb) / 2.0;
+    if (dt > 0)
+      mu = tb - tab * (tab / (dt + hypot_fdlibm(dt, tab)));
+    else if (dt == 0)
+      mu = tb - fabs(tab);
+    else
+      mu = tb + tab * (tab / ((-dt) + hypot_fdlibm(dt, tab)));
+  }
+  if (EPS * fabs(mu) > (fabs(d[0]) + fabs(sd[0]))) mu = 0;
+  x = d[0] - mu;
+  z = sd[0];
+  ak = 0;
+  bk = 0;
+  zk = 0;
+  ap = d[0];
+  bp = sd[0];
+  aq = d[1];
+  if (n == 2) {
+    double c, s;
+    create_givens(x, z, c, s);
+    cs[0] = c;
+    cs[1] = s;
+    const double ap1 = c * (c * ap - s * bp) + s * (s * aq - c * bp);
+    const double bp1 = c * (s * ap + c * bp) - s * (s * bp + c * aq);
+    const double aq1 = s * (s * ap + c * bp) + c * (s * bp + c * aq);
+    d[0] = ap1;
+    sd[0] = bp1;
+    d[1] = aq1;
+    if (fabs(bp1) < EPS * (fabs(ap1) + fabs(aq1))) sd[0] = 0.0;
+    return;
+  }
+  bq = sd[1];
+  double dn = d[n - 1 < 2 ? n - 1 : 2], sdn = sd[n - 2 < 2 ? n - 2 : 2];
+  double dprev = 0.0;  // d[k - 1] as written at iteration k - 1
+  int k;
+  for (k = 0; k < n - 1; k++) {
+    const double dpf = d[(k + 3 < n - 1) ? k + 3 : n - 1];
+    const double sdpf = sd[(k + 3 < n - 2) ? k + 3 : n - 2];
+    double c, s;
+    create_givens(x, z, c, s);
+    cs[2 * k] = c;
+    cs[2 * k + 1] = s;
+    const double bk1 = c * bk - s * zk;
+    const double ap1 = c * (c * ap - s * bp) + s * (s * aq - c * bp);
+    const double bp1 = c * (s * ap + c * bp) - s * (s * bp + c * aq);
+    const double zp1 = -s * bq;
+    const double aq1 = s * (s * ap + c * bp) + c * (s * bp + c * aq);
+    const double bq1 = c * bq;
+    ak = ap1;
+    bk = bp1;
+    zk = zp1;
+    ap = aq1;
+    bp = bq1;
+    if (k < n - 2) aq = dn;
+    if (k < n - 3) bq = sdn;
+    dn = dpf;
+    sdn = sdpf;
+    d[k] = ak;
+    if (k > 0) sd[k - 1] = (fabs(bk1) < EPS * (fabs(dprev) + fabs(ak))) ? 0.0 : bk1;
+    if (k < n - 2) sd[k + 1] = bp;
+    dprev = ak;
+    x = bk;
+    z = zk;
+  }
+  d[k] = ap;
+  sd[k - 1] = (fabs(bk) < EPS * (fabs(dprev) + fabs(ap))) ? 0.0 : bk;
+}
+
 // DPP lane moves of a double (both halves; lanes without a source get 0.0)
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ double dpp_d(double x) {
@@ -2251,7 +2332,8 @@ __host__ __device__ inline void chase_publish(unsigned long long *prog, unsigned
 }
 
 __host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, int maxRot, double *gc, double *gs,
-                                        unsigned long long *prog = nullptr, unsigned long long seq = 0) {
+                                        unsigned long long *prog = nullptr, unsigned long long seq = 0,
+                                        int every = 1, bool fused = false) {
   chop_small(N, d, sd);
   int b = N - 1, steps = 0, rot = 0, err = 0;
   while (b > 0) {
@@ -2269,17 +2351,21 @@ __host__ __device__ inline int qr_chase(int N, double *d, double *sd, EigRec r, 
       err = 1;
       break;
     }
-    qrstep(nb, d + a, sd + a, gc, gs);
-    for (int k = 0; k + 1 < nb; k++) {
-      r.cs[2 * (rot + k)] = gc[k];
-      r.cs[2 * (rot + k) + 1] = gs[k];
+    if (fused) {
+      qrstep_fused(nb, d + a, sd + a, r.cs + 2 * (size_t)rot);  // (rotations written in place, chop folded in)
+    } else {
+      qrstep(nb, d + a, sd + a, gc, gs);
+      for (int k = 0; k + 1 < nb; k++) {
+        r.cs[2 * (rot + k)] = gc[k];
+        r.cs[2 * (rot + k) + 1] = gs[k];
+      }
     }
     r.hdr[2 * steps] = a;
     r.hdr[2 * steps + 1] = nb;
     steps++;
     rot += nb - 1;
-    chase_publish(prog, chase_word(seq, 0, (unsigned long long)steps));
-    chop_small(nb, d + a, sd + a);
+    if (steps % every == 0) chase_publish(prog, chase_word(seq, 0, (unsigned long long)steps));
+    if (!fused) chop_small(nb, d + a, sd + a);
   }
   // gsl_eigen_symmv_sort(ABS_ASC): selection sort, strict < on |e|
   for (int i = 0; i < N; i++) {
@@ -3282,7 +3368,18 @@ int EigenSolver::run_finish(const double *C, int diagonal, double *B, double *D,
     if (prof) prof(profCtx, "eigen_chase_host", 2);
     EigRec hr = host;
     chase_publish(hprog, chase_word(seq, 0, 0));
-    qr_chase(N, h_dsd, h_dsd + N, hr, maxRot, hgc.data(), hgs.data(), hprog, seq);
+    // the progress word every `every` QR steps (KORALI_AMD_CHASE_PUBLISH_EVERY;
+    // each write after a device poll of its line costs the core a miss)
+    static const int every = [] {
+      const char *e = getenv("KORALI_AMD_CHASE_PUBLISH_EVERY");
+      const int v = e ? atoi(e) : 1;
+      return v < 1 ? 1 : v;
+    }();
+    static const bool fused = [] {  // KORALI_AMD_CHASE_FUSED=0: the separate chop pass and rotation copy
+      const char *e = getenv("KORALI_AMD_CHASE_FUSED");
+      return !(e && *e == '0');
+    }();
+    qr_chase(N, h_dsd, h_dsd + N, hr, maxRot, hgc.data(), hgs.data(), hprog, seq, every, fused);
     if (prof) prof(profCtx, "eigen_chase_host", 3);
   } else {
     KG_HIP(hipStreamWaitEvent(s, ev_chase, 0));
@@ -3321,5 +3418,34 @@ extern "C" int kg_debug_host_tridiag(size_t N, const double *C, double *H, doubl
     return 1;
   }
   t.run(C, (int)N, H, tau, d, sd);
+  return 0;
+}
+
+// The host core's Givens chase (phase C, the product's qr_chase) on a given
+// tridiagonal, `reps` times: the sorted eigenvalues and permutation, the
+// QR-step and rotation counts, the first cs_cap rotation values and the mean
+// wall time per chase.  fused: the sweep with the chop test and the rotation
+// record folded in (qrstep_fused), else qrstep + copy + chop_small.  CPU only.
+extern "C" int kg_debug_host_chase(size_t N, const double *d, const double *sd, int fused, size_t reps, double *eval,
+                                   int *perm, double *cs, size_t cs_cap, int *counts, double *ns_per_chase) {
+  if (!d || !sd || !eval || !perm || !counts || N < 1 || N > 65536 || reps < 1) {
+    kg::set_error("kg_debug_host_chase: null argument or bad order");
+    return 1;
+  }
+  const int n = (int)N, maxRot = 8 * n * n + 65536;
+  std::vector<int> hdr(2 * (size_t)(maxRot + n)), meta(4);
+  std::vector<double> csv(2 * (size_t)maxRot), wd(N), wsd(N), gc(N), gs(N);
+  kg::EigRec r{hdr.data(), csv.data(), meta.data(), eval, perm};
+  double tot = 0.0;
+  for (size_t k = 0; k < reps; k++) {
+    std::copy(d, d + N, wd.begin());
+    std::copy(sd, sd + N - 1, wsd.begin());
+    const auto t0 = std::chrono::steady_clock::now();
+    kg::qr_chase(n, wd.data(), wsd.data(), r, maxRot, gc.data(), gs.data(), nullptr, 0, 1, fused != 0);
+    tot += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+  }
+  counts[0] = meta[0], counts[1] = meta[1], counts[2] = meta[2];
+  if (cs) std::copy(csv.begin(), csv.begin() + std::min<size_t>(cs_cap, 2 * (size_t)meta[1]), cs);
+  if (ns_per_chase) *ns_per_chase = tot / (double)reps;
   return 0;
 }

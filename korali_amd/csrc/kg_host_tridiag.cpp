@@ -48,6 +48,7 @@
 #include <x86intrin.h>
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstddef>
@@ -210,6 +211,7 @@ struct HostTridiagPool {
   alignas(64) std::atomic<unsigned> done{0};
   alignas(64) std::atomic<int> awake{0};
   std::atomic<bool> quit{false};
+  long spin_us = 3000;  // KORALI_AMD_HOST_TRIDIAG_SPIN_US
   std::mutex mu;
   std::condition_variable cv;
 
@@ -221,19 +223,24 @@ struct HostTridiagPool {
       (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
     }
     unsigned seen = 0;
+    auto last = std::chrono::steady_clock::now();  // end of the last phase this thread worked on
     for (;;) {
       unsigned e;
       unsigned spins = 0;
       while ((e = epoch.load(std::memory_order_acquire)) == seen) {
         _mm_pause();
-        // idle between decompositions: sleep after ~0.2-0.5 ms of spinning
-        if (++spins > 4096 && !awake.load(std::memory_order_relaxed)) {
+        // between decompositions the helpers keep spinning for spin_us (a
+        // futex wake-up of a core in a deep idle state took longer than the
+        // covariance's way to the host: measured 90 -> 300 us tridiagonal),
+        // then sleep until the next wake()
+        if ((++spins & 1023) == 0 && !awake.load(std::memory_order_relaxed) &&
+            std::chrono::steady_clock::now() - last > std::chrono::microseconds(spin_us)) {
           std::unique_lock<std::mutex> lk(mu);
           cv.wait(lk, [&] {
             return epoch.load(std::memory_order_acquire) != seen || awake.load(std::memory_order_relaxed) ||
                    quit.load(std::memory_order_relaxed);
           });
-          spins = 0;
+          last = std::chrono::steady_clock::now();
         }
         if (quit.load(std::memory_order_relaxed)) return;
       }
@@ -241,6 +248,7 @@ struct HostTridiagPool {
       if (quit.load(std::memory_order_relaxed)) return;
       fn(job, t);
       done.fetch_add(1, std::memory_order_release);
+      last = std::chrono::steady_clock::now();
     }
   }
   // every thread (the caller as thread 0) runs fn(job, t); returns when all are done
@@ -377,6 +385,7 @@ int pool_init(HostTridiag &w, int P) {
   const int N = w.N;
   p->P = P, p->N = N, p->NB = (N + 7) / 8, p->L = p->NB * 8 + 16;
   p->fn = pick_pass();
+  if (const char *e = std::getenv("KORALI_AMD_HOST_TRIDIAG_SPIN_US")) p->spin_us = std::atol(e);
   for (int c = 0; c < p->NB; c++) {
     p->colblk.push_back((double *)std::aligned_alloc(64, (size_t)(N - 8 * c) * 64));
     const int kn = 8 * c + 8 < N ? 8 * c + 8 : N;

@@ -84,7 +84,7 @@ EXPORTED = [
     "kg_tmcmc_set_gradients",
     "kg_tmcmc_profile", "kg_tmcmc_profile_read", "kg_debug_mt_jump", "kg_debug_multinomial", "kg_debug_cartpole",
     "kg_debug_cartpole_at",
-    "kg_debug_host_tridiag",
+    "kg_debug_host_tridiag", "kg_debug_host_chase",
     # VRACER (korali_amd/vracer.py binds their argument types)
     "kg_vracer_create", "kg_vracer_destroy", "kg_vracer_hyperparameter_count", "kg_vracer_field_size",
     "kg_vracer_get_field", "kg_vracer_set_field", "kg_vracer_get_scalar", "kg_vracer_set_scalar",
@@ -125,6 +125,7 @@ def lib():
         L.kg_debug_cartpole.argtypes = [ip, vp, vp, sz, sz, vp, vp]
         L.kg_debug_cartpole_at.argtypes = [ip, vp, vp, vp, sz, sz, vp, vp, vp]
         L.kg_debug_host_tridiag.argtypes = [sz, vp, vp, vp, vp, vp]
+        L.kg_debug_host_chase.argtypes = [sz, vp, vp, C.c_int, sz, vp, vp, vp, sz, vp, vp]
         L.kg_cmaes_generation.argtypes = [vp, sz, ip]
         L.kg_cmaes_field_size.argtypes = [vp, cp, C.POINTER(sz)]
         L.kg_cmaes_get_field.argtypes = [vp, cp, dp, sz]

@@ -7,6 +7,7 @@ mkdir -p gpurun_out/ab
 for cfg in "$@"; do
   envs=()
   [ "$cfg" != "-" ] && IFS=, read -ra envs <<< "$cfg"
+  thr0=$(grep -E "nr_throttled|throttled_usec" /sys/fs/cgroup/cpu.stat 2>/dev/null | tr '\n' ' ')
   timeout -k 10 200 env "${envs[@]}" python bench.py --steps ${STEPS_AB:-200} --warmup 10 --no-cpu-baseline --no-c1 \
     > gpurun_out/ab/run.log 2>&1 || { echo "FAILED $cfg"; tail -5 gpurun_out/ab/run.log; exit 1; }
   python3 - "$cfg" <<'PY'
@@ -15,4 +16,5 @@ d = [json.loads(l) for l in open("gpurun_out/ab/run.log") if l.startswith("{")][
 st = {k: round(v * 1e3, 1) for k, v in d["stage_ms"].items()}
 print(f"{sys.argv[1]:40s} {d['value']:8.1f} gen/s  {st}", flush=True)
 PY
+  echo "   cgroup before: $thr0 after: $(grep -E "nr_throttled|throttled_usec" /sys/fs/cgroup/cpu.stat 2>/dev/null | tr '\n' ' ')"
 done
