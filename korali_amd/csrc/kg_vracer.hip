@@ -44,7 +44,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MAXA = 4;  // action dimensions supported by the device kernels
 constexpr int MAXO = 1 + 2 * MAXA;
 constexpr int MAXB = 2048;  // mini-batch size limit (one-workgroup sort / metadata)
-constexpr int MAXENV = 64;  // environment ids with reward rescaling (Problem / Environment Count)
+constexpr int MAXENV = 64;  // reward rescaling: up to this many environment ids are staged in LDS (any count runs)
 constexpr int MAXS = 8;     // state dimensions with state rescaling
 enum : int { NON_TERMINAL = 0, TERMINAL = 1, TRUNCATED = 2 };
 enum : unsigned {
@@ -67,12 +67,9 @@ struct State {
   unsigned long long env_step;    // philox counter of the action noise
   unsigned long long step_new, step_base, step_episodes, step_episode_base, step_sample_base;
   unsigned long long experience_count;
-  unsigned errors, pad1;
+  unsigned errors;
+  unsigned rr_all;                // reward rescaling: every id's sigma recomputed once (the first episode's update)
   double step_reward_sum;         // cumulative rewards of the episodes finished by the last step
-  // reward rescaling (agent.cpp.base:96-98, :423-437, :557-563), per environment id
-  float rsig[MAXENV];             // getScaledReward's sigma (1.0 unless enabled)
-  float rsum[MAXENV];             // sum of squared rewards in the replay memory
-  long long rcnt[MAXENV];         // experiences in the replay memory
   // state rescaling (agent.cpp.base:92-94, :291-322): the moments episodes
   // launched from now on scale their states with (identity until set)
   float smean[MAXS], ssdev[MAXS];
@@ -510,6 +507,11 @@ struct Replay {
   float *st, *act, *rew, *tst, *exp_pol, *cur_pol, *exp_v, *v, *ret, *iw, *tiw, *tv;
   int *env, *term, *onp, *ep_pos;
   long long *ep_id;
+  // reward rescaling (agent.cpp.base:96-98, :423-437, :557-563), one entry
+  // per environment id (Problem / Environment Count)
+  float *rsig;      // getScaledReward's sigma (1.0 until the first update)
+  float *rsum;      // sum of squared rewards in the replay memory
+  long long *rcnt;  // experiences in the replay memory
 };
 __device__ inline long long phys(const State *s, long long R, long long i) {
   return (long long)((s->total - s->size + (unsigned long long)i) % (unsigned long long)R);
@@ -1017,7 +1019,8 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
   };
   const unsigned long long tm0 = __builtin_amdgcn_s_memrealtime();
   if (t == 0) s_delta = 0, s_wmax = 0, s_wtot = 0, s_wcnt = 0;
-  if (RR && t < MAXENV) s_rsig[t] = st->rsig[t];
+  const bool rsl = P.env_count <= MAXENV;  // the sigmas staged in LDS (else read from the replay memory's table)
+  if (RR && rsl && t < P.env_count) s_rsig[t] = er.rsig[t];
   __syncthreads();
   // ---- importance weights and on-policy flags (agent.cpp.base:613-657);
   // duplicates compute the same values, only the first occurrence counts
@@ -1027,7 +1030,7 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
     const bool uniq = b == 0 || id != mb[b - 1];
     const long long p = ph(id);
     const float a = er.act[p * P.A], om = er.exp_pol[2 * P.A * p], osd = er.exp_pol[2 * P.A * p + P.A],
-                rew = RR ? er.rew[p] / st->rsig[er.env[p]] : er.rew[p];
+                rew = RR ? er.rew[p] / er.rsig[er.env[p]] : er.rew[p];
     const int was = er.onp[p], term = er.term[p];
     const float V = out[(long long)b * O], cm = out[(long long)b * O + 1], cs = out[(long long)b * O + 1 + P.A];
     const float tvv = term == TRUNCATED ? out[(long long)(B + b) * O] : 0.0f;
@@ -1159,7 +1162,7 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
         const int f = f0 + u * nt;
         if (f < wtot) {
           w_v[f] = lv[u], w_t[f] = lt[u];
-          w_r[f] = RR ? lr[u] / s_rsig[le[u]] : lr[u];  // getScaledReward (agent.cpp.base:720)
+          w_r[f] = RR ? lr[u] / (rsl ? s_rsig[le[u]] : er.rsig[le[u]]) : lr[u];  // getScaledReward (agent.cpp.base:720)
         }
       }
     }
@@ -1267,7 +1270,7 @@ __global__ __launch_bounds__(512) void k_vr_meta(Params P, State *st, Replay er,
                          const int (&en)[RC]) __attribute__((always_inline)) {
         if (RR)
   #pragma unroll
-          for (int j = 0; j < RC; j++) rw[j] = rw[j] / s_rsig[en[j]];  // getScaledReward (agent.cpp.base:720)
+          for (int j = 0; j < RC; j++) rw[j] = rw[j] / (rsl ? s_rsig[en[j]] : er.rsig[en[j]]);  // getScaledReward (agent.cpp.base:720)
         const int n = (int)min((long long)RC, c - start + 1);
         int kk = k;
         unsigned long long inmb = 0;
@@ -1646,7 +1649,7 @@ struct Envs {
   int *fin_env;       // environment of the finished episode of each rank
   float *eb_st, *eb_act, *eb_pol, *eb_v, *eb_rew;  // E x T episode buffers
   float *rewards;     // cumulative rewards of the episodes finished by the last step (by rank)
-  float *sigb;        // rank x MAXENV: the rescaling sigmas before that episode (reward rescaling)
+  float *sig2;        // rank x 2: the rescaling sigmas of the episode's id and of the entry before it, before its update
   int *fin_id;        // environment id of the finished episode of each rank
   float *pm, *ps;     // E x S: the state-rescaling moments the running episode was launched with
   float *hraw;        // E x S: a host environment's raw launch state (State Rescaling re-scales it)
@@ -1943,48 +1946,82 @@ __global__ void k_vr_reward_sums(Params P, State *st, Replay er, Envs ev) {
   if (threadIdx.x || blockIdx.x) return;
   const unsigned long long base = st->step_base, neps = st->step_episodes;
   const long long R = P.R;
-  // (LDS, not registers: the environment id indexes them)
-  __shared__ float sum[MAXENV], sig[MAXENV];
-  __shared__ long long cnt[MAXENV];
-  for (int i = 0; i < MAXENV; i++) sum[i] = st->rsum[i], cnt[i] = st->rcnt[i], sig[i] = st->rsig[i];
+  const int EC = P.env_count;
+  // (LDS, not registers: the environment id indexes them; more ids than
+  // MAXENV work on the replay memory's tables in place)
+  __shared__ float ssum[MAXENV], ssig[MAXENV];
+  __shared__ long long scnt[MAXENV];
+  const bool lds = EC <= MAXENV;
+  float *sum = lds ? ssum : er.rsum, *sig = lds ? ssig : er.rsig;
+  long long *cnt = lds ? scnt : er.rcnt;
+  if (lds)
+    for (int i = 0; i < EC; i++) sum[i] = er.rsum[i], cnt[i] = er.rcnt[i], sig[i] = er.rsig[i];
   // the batch entry at offset j (episodes in rank order): a forward cursor
   int cr = 0;
   long long cend = neps ? ev.len[ev.fin_env[0]] : 0, cbeg = 0;
+  // the id of the new entry's evicted predecessor (memory full), or -1
+  auto evicted = [&](long long a, float &ro) -> int {
+    if (a < R) return -1;
+    const long long old = a - R;
+    if (old >= (long long)base) {  // an entry of this same batch
+      const long long j = old - (long long)base;
+      while (j >= cend) {
+        cr++;
+        cbeg = cend;
+        cend += ev.len[ev.fin_env[cr]];
+      }
+      const int eo = ev.fin_env[cr];
+      ro = ev.eb_rew[(long long)eo * P.T + (j - cbeg)];
+      return ev.env_id[eo];
+    }
+    ro = er.rew[old % R];
+    return er.env[old % R];
+  };
   for (unsigned long long r = 0; r < neps; r++) {
     const int e = ev.fin_env[r], id = ev.env_id[e], len = ev.len[e];
     const long long off = ev.off[e];
     ev.fin_id[r] = id;
-    for (int i = 0; i < MAXENV; i++) ev.sigb[r * MAXENV + i] = sig[i];
+    // the sigmas before this episode's update that its initial retrace values
+    // read (k_vr_append): its own id's and the previous entry's
+    int pid = id;
+    if (len < 2) pid = r > 0 ? ev.fin_id[r - 1] : (base >= 1 ? er.env[((long long)base - 1) % R] : id);
+    ev.sig2[2 * r] = sig[id];
+    ev.sig2[2 * r + 1] = sig[pid];
+    const int cr0 = cr;
+    const long long cb0 = cbeg, ce0 = cend;
     for (int k = 0; k < len; k++) {
       const float rw = ev.eb_rew[(long long)e * P.T + k];
       sum[id] += rw * rw;
       cnt[id]++;
-      const long long a = (long long)base + off + k;  // absolute index of the new entry
-      if (a >= R) {                                   // full: the oldest entry a - R leaves
-        const long long old = a - R;
-        float ro;
-        int io;
-        if (old >= (long long)base) {  // an entry of this same batch
-          const long long j = old - (long long)base;
-          while (j >= cend) {
-            cr++;
-            cbeg = cend;
-            cend += ev.len[ev.fin_env[cr]];
-          }
-          const int eo = ev.fin_env[cr];
-          ro = ev.eb_rew[(long long)eo * P.T + (j - cbeg)];
-          io = ev.env_id[eo];
-        } else {
-          ro = er.rew[old % R];
-          io = er.env[old % R];
-        }
+      float ro;
+      const int io = evicted((long long)base + off + k, ro);  // full: the oldest entry a - R leaves
+      if (io >= 0) {
         sum[io] -= ro * ro;
         cnt[io]--;
       }
     }
-    for (int i = 0; i < P.env_count && i < MAXENV; i++) sig[i] = rr_sigma(sum[i], cnt[i]);
+    // every id's sigma after the episode (agent.cpp.base:557-563); an id whose
+    // sums did not change keeps the value it has, so after the first
+    // episode's full pass only this episode's id and the evicted entries' ids
+    // are recomputed
+    if (!st->rr_all) {
+      for (int i = 0; i < EC; i++) sig[i] = rr_sigma(sum[i], cnt[i]);
+      st->rr_all = 1;
+    } else {
+      sig[id] = rr_sigma(sum[id], cnt[id]);
+      const int cr1 = cr;
+      const long long cb1 = cbeg, ce1 = cend;
+      cr = cr0, cbeg = cb0, cend = ce0;
+      for (int k = 0; k < len; k++) {
+        float ro;
+        const int io = evicted((long long)base + off + k, ro);
+        if (io >= 0) sig[io] = rr_sigma(sum[io], cnt[io]);
+      }
+      cr = cr1, cbeg = cb1, cend = ce1;
+    }
   }
-  for (int i = 0; i < MAXENV; i++) st->rsum[i] = sum[i], st->rcnt[i] = cnt[i], st->rsig[i] = sig[i];
+  if (lds)
+    for (int i = 0; i < EC; i++) er.rsum[i] = sum[i], er.rcnt[i] = cnt[i], er.rsig[i] = sig[i];
 }
 
 // processEpisode (agent.cpp.base:376-572) for every finished episode at once:
@@ -2036,13 +2073,15 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
   if (t == 0) {
     // initial retrace values (agent.cpp.base:520-555), rewards through
     // getScaledReward with the sigmas before this episode's update
-    const float *sg = P.rr ? ev.sigb + (long long)rank * MAXENV : nullptr;
-    auto scaled = [&](float r, int id) { return sg ? r / sg[id] : r; };
-    const int myid = ev.env_id[e];
+    // (the sigmas before this episode's update: of its own id, and of the
+    // entry before its first when it has one experience; k_vr_reward_sums)
+    const float sgs = P.rr ? ev.sig2[2 * (long long)rank] : 1.0f, sgp = P.rr ? ev.sig2[2 * (long long)rank + 1] : 1.0f;
+    const bool sg = P.rr != 0;
+    auto scaled = [&](float r, bool own) { return sg ? r / (own ? sgs : sgp) : r; };
     float retV = 0.0f;
     if (term == TRUNCATED) retV += P.gamma * outF[(long long)e * P.O];
     const long long endj = off + len - 1;
-    retV = P.gamma * retV + scaled(ev.eb_rew[(long long)e * P.T + len - 1], myid);
+    retV = P.gamma * retV + scaled(ev.eb_rew[(long long)e * P.T + len - 1], true);
     // an entry overwritten later in this same batch (more new experiences
     // than the capacity) keeps the later entry's values, as the reference's
     // sequential processEpisode calls leave it
@@ -2051,15 +2090,13 @@ __global__ __launch_bounds__(256) void k_vr_append(Params P, State *st, Replay e
     const long long prevj = endj - 1;
     if ((long long)base + prevj >= 0 && prevj >= survive) {
       float r;
-      if (len >= 2) r = scaled(ev.eb_rew[(long long)e * P.T + len - 2], myid);
+      if (len >= 2) r = scaled(ev.eb_rew[(long long)e * P.T + len - 2], true);
       else if (rank > 0) {
         const int pe = ev.fin_env[rank - 1];
-        r = ev.eb_rew[(long long)pe * P.T + ev.len[pe] - 1];
-        if (sg) r = scaled(r, ev.fin_id[rank - 1]);
+        r = scaled(ev.eb_rew[(long long)pe * P.T + ev.len[pe] - 1], false);
       } else {
         const long long q = ((long long)base + prevj) % R;
-        r = er.rew[q];
-        if (sg) r = scaled(r, er.env[q]);
+        r = scaled(er.rew[q], false);
       }
       retV = P.gamma * retV + r;
       er.ret[((long long)base + prevj) % R] = retV;
@@ -2142,7 +2179,6 @@ __global__ void k_vr_init_state(State *st, float lr, float beta, float cutoff) {
   if (threadIdx.x || blockIdx.x) return;
   State s = {};
   s.lr = lr, s.beta = beta, s.cutoff = cutoff, s.eta = lr, s.b1p = 1.0f, s.b2p = 1.0f;
-  for (int i = 0; i < MAXENV; i++) s.rsig[i] = 1.0f;
   for (int i = 0; i < MAXS; i++) s.smean[i] = 0.0f, s.ssdev[i] = 1.0f;
   *st = s;
 }
@@ -2496,9 +2532,9 @@ bool vr_field(kg_vracer_t h, const char *name, VrField &f) {
       {"finished_rewards", h->ev.rewards, 4, E}, {"finished_env", h->ev.fin_env, 4, E},
       {"mini_batch", h->mb, 4, (size_t)P.B},   {"loss_gradient", h->G, 4, (size_t)P.B * P.O},
       {"policy_output", h->out, 4, h->rowsMax * P.O},
-      {"reward_rescaling_sigma", &h->st->rsig[0], 4, (size_t)MAXENV},
-      {"reward_rescaling_sum", &h->st->rsum[0], 4, (size_t)MAXENV},
-      {"reward_rescaling_count", &h->st->rcnt[0], 8, (size_t)MAXENV},
+      {"reward_rescaling_sigma", h->er.rsig, 4, (size_t)P.env_count},
+      {"reward_rescaling_sum", h->er.rsum, 4, (size_t)P.env_count},
+      {"reward_rescaling_count", h->er.rcnt, 8, (size_t)P.env_count},
       {"state_rescaling_means", &h->st->smean[0], 4, (size_t)std::min(P.S, MAXS)},
       {"state_rescaling_sigmas", &h->st->ssdev[0], 4, (size_t)std::min(P.S, MAXS)},
       {"meta_phase_ticks", &h->st->mtr[0], 8, (size_t)9},
@@ -2552,8 +2588,7 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   P.srs = c->state_rescaling ? 1 : 0;
   P.host = c->host_environment ? 1 : 0;
   KG_CHECK(!P.srs || c->state_size <= (size_t)MAXS, "vracer: State Rescaling on the device supports up to 8 state variables");
-  KG_CHECK(!P.rr || (c->environment_count >= 1 && c->environment_count <= (size_t)MAXENV),
-           "vracer: Reward Rescaling on the device supports Environment Count 1..64");
+  KG_CHECK(c->environment_count >= 1, "vracer: Environment Count must be at least 1");
   P.l2 = c->l2_regularization_enabled ? 1 : 0;
   P.gamma = (float)c->discount_factor, P.lr0 = (float)c->learning_rate, P.iw_trunc = (float)c->importance_weight_truncation_level;
   P.cutoff_scale = (float)c->off_policy_cutoff_scale, P.off_target = (float)c->off_policy_target;
@@ -2641,12 +2676,18 @@ int kg_vracer_create(const kg_vracer_config *c, kg_vracer_t *out) {
   alloc(er.exp_pol, R * 2 * P.A * 4), alloc(er.cur_pol, R * 2 * P.A * 4), alloc(er.exp_v, R * 4), alloc(er.v, R * 4);
   alloc(er.ret, R * 4), alloc(er.iw, R * 4), alloc(er.tiw, R * 4), alloc(er.tv, R * 4);
   alloc(er.env, R * 4), alloc(er.term, R * 4), alloc(er.onp, R * 4), alloc(er.ep_pos, R * 4), alloc(er.ep_id, R * 8);
+  const size_t EC = (size_t)P.env_count;
+  alloc(er.rsig, EC * 4), alloc(er.rsum, EC * 4), alloc(er.rcnt, EC * 8);
+  if (!rc) {  // getScaledReward's sigma starts at 1.0 for every id (agent.cpp.base:96-98)
+    const std::vector<float> ones(EC, 1.0f);
+    if (hipMemcpy(er.rsig, ones.data(), EC * 4, hipMemcpyHostToDevice) != hipSuccess) rc = 1;
+  }
   Envs &ev = h->ev;
   alloc(ev.u, E * 4 * 8), alloc(ev.time, E * 8), alloc(ev.t, E * 4), alloc(ev.env_id, E * 4), alloc(ev.sample, E * 8), alloc(ev.cum, E * 4);
   alloc(ev.fin, E * 4), alloc(ev.len, E * 4), alloc(ev.off, E * 8), alloc(ev.rank, E * 4), alloc(ev.fin_env, E * 4);
   alloc(ev.eb_st, ET * P.S * 4), alloc(ev.eb_act, ET * P.A * 4), alloc(ev.eb_pol, ET * 2 * P.A * 4);
   alloc(ev.eb_v, ET * 4), alloc(ev.eb_rew, ET * 4), alloc(ev.rewards, E * 4);
-  alloc(ev.sigb, E * MAXENV * 4), alloc(ev.fin_id, E * 4);
+  alloc(ev.sig2, E * 2 * 4), alloc(ev.fin_id, E * 4);
   alloc(ev.pm, (size_t)E * P.S * 4), alloc(ev.ps, (size_t)E * P.S * 4);
   if (P.host) alloc(ev.hraw, (size_t)E * P.S * 4);
   if (!rc && host_alloc((void **)&h->st_host, sizeof(State), hipHostMallocDefault) != hipSuccess) {
@@ -2737,8 +2778,8 @@ int kg_vracer_destroy(kg_vracer_t h) {
                   h->er.exp_pol, h->er.cur_pol, h->er.exp_v, h->er.v, h->er.ret, h->er.iw, h->er.tiw, h->er.tv,
                   h->er.env, h->er.term, h->er.onp, h->er.ep_pos, h->er.ep_id, h->ev.u, h->ev.time, h->ev.t, h->ev.env_id,
                   h->ev.sample, h->ev.cum, h->ev.fin, h->ev.len, h->ev.off, h->ev.rank, h->ev.fin_env, h->ev.eb_st,
-                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sigb, h->ev.fin_id,
-                  h->ev.pm, h->ev.ps, h->ev.hraw};
+                  h->ev.eb_act, h->ev.eb_pol, h->ev.eb_v, h->ev.eb_rew, h->ev.rewards, h->ev.sig2, h->ev.fin_id,
+                  h->ev.pm, h->ev.ps, h->ev.hraw, h->er.rsig, h->er.rsum, h->er.rcnt};
   for (void *p : ptrs)
     if (p) dev_release(p);
   if (h->st_host) host_release(h->st_host);

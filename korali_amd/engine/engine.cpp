@@ -2000,8 +2000,7 @@ struct VracerModule : SolverModule {
     if (uint(sv, "Time Sequence Length", 1) != 1) fail("'Time Sequence Length' > 1 is not supported by the device path.");
     const bool stateRescaling = flag(sv["State Rescaling"], "Enabled", false);
     const bool rewardRescaling = flag(sv["Reward"]["Rescaling"], "Enabled", false);
-    if (rewardRescaling && (envCount < 1 || envCount > 64))
-      fail("Reward Rescaling on the device supports an 'Environment Count' of 1 to 64 (%llu given).", envCount);
+    if (envCount < 1) fail("'Environment Count' must be at least 1 (%llu given).", envCount);
     rewardRescaled = rewardRescaling;
     if (flag(sv["Reward"]["Outbound Penalization"], "Enabled", false))
       fail("Reward Outbound Penalization is not supported by the device path.");
@@ -2127,9 +2126,9 @@ struct VracerModule : SolverModule {
       }
       Json &rr = sv["Reward"]["Rescaling"];
       if (rewardRescaled && rr.contains("Sigma") && rr["Sigma"].size() == envIds) {
-        std::vector<float> sg(64, 1.0f);
+        std::vector<float> sg(envIds, 1.0f);
         for (size_t i = 0; i < envIds; i++) sg[i] = (float)rr["Sigma"][i].getDouble();
-        check(kg_vracer_set_field(h, "reward_rescaling_sigma", sg.data(), 64 * sizeof(float)));
+        check(kg_vracer_set_field(h, "reward_rescaling_sigma", sg.data(), envIds * sizeof(float)));
       }
     }
   }
@@ -2321,11 +2320,11 @@ struct VracerModule : SolverModule {
     sv["Training"]["Current Policy"]["Policy"] = std::vector<double>(theta.begin(), theta.end());
     {  // agent.config:311-320 (per environment id, Environment Count entries)
       if (rewardRescaled) {
-        float sig[64], sum[64];
-        check(kg_vracer_get_field(h, "reward_rescaling_sigma", sig, sizeof sig));
-        check(kg_vracer_get_field(h, "reward_rescaling_sum", sum, sizeof sum));
-        sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig, sig + envIds);
-        sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum, sum + envIds);
+        std::vector<float> sig(envIds), sum(envIds);
+        check(kg_vracer_get_field(h, "reward_rescaling_sigma", sig.data(), envIds * sizeof(float)));
+        check(kg_vracer_get_field(h, "reward_rescaling_sum", sum.data(), envIds * sizeof(float)));
+        sv["Reward"]["Rescaling"]["Sigma"] = std::vector<double>(sig.begin(), sig.end());
+        sv["Reward"]["Rescaling"]["Sum Squared Rewards"] = std::vector<double>(sum.begin(), sum.end());
       } else {
         // the sigmas stay 1 without rescaling (agent.cpp.base:97, :557-563);
         // the squared-reward sums only feed them, and the device keeps them

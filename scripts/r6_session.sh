@@ -48,7 +48,8 @@ for s in ${STEPS:-tests}; do
     pmcf) step pmcf 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1 ;;
     pmcw) step pmcw 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c1
           pmcsum pmc_fetch pmc_write c2_pmc_traffic.csv ;;
-    pmcm) step pmcm 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --cov mfma --no-cpu-baseline ;;
+    pmcm) step pmcm 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 2 --cov mfma --no-cpu-baseline
+          python $R/tools/pmc_mfma_summary.py $O/pmc_mfma > $O/c2_mfma_counters.csv && find $O/pmc_mfma -name "*counter_collection.csv" -delete; cat $O/c2_mfma_counters.csv ;;
     pmcf3) step pmcf3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c3 -o run --output-format csv -- python $R/bench.py --workload c3 --steps 12 --warmup 1 --no-cpu-baseline ;;
     pmcw3) step pmcw3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c3 -o run --output-format csv -- python $R/bench.py --workload c3 --steps 12 --warmup 1 --no-cpu-baseline
            pmcsum pmc_fetch_c3 pmc_write_c3 c3_pmc_traffic.csv ;;
@@ -65,7 +66,8 @@ for s in ${STEPS:-tests}; do
     pmcf5) step pmcf5 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
     pmcw5) step pmcw5 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline
            pmcsum pmc_fetch_c5 pmc_write_c5 c5_pmc_traffic.csv ;;
-    pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --cov mfma --no-cpu-baseline
+           python $R/tools/pmc_mfma_summary.py $O/pmc_mfma_c4 > $O/c4_mfma_counters.csv && find $O/pmc_mfma_c4 -name "*counter_collection.csv" -delete; cat $O/c4_mfma_counters.csv ;;
   esac
 done
 echo "session done"

@@ -198,7 +198,7 @@ from vracer_cases import cartpole_vracer  # noqa: E402
      "Elementwise/Tanh"),
     (lambda e: e["Solver"]["Reward"]["Outbound Penalization"].__setitem__("Enabled", True), "Outbound Penalization"),
     (lambda e: (e["Solver"]["Reward"]["Rescaling"].__setitem__("Enabled", True),
-                e["Problem"].__setitem__("Environment Count", 65)), "Reward Rescaling"),
+                e["Problem"].__setitem__("Environment Count", 0)), "Environment Count"),
     (lambda e: e["Solver"]["Neural Network"].__setitem__("Optimizer", "RMSProp"), "Adam"),
     (lambda e: e["Solver"].__setitem__("Mode", "Testing"), "Sample Ids"),  # agent.cpp.base:147-149
     (lambda e: e["Solver"].__setitem__("Mode", "Evaluation"), "'Mode' must be"),

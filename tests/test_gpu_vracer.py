@@ -266,22 +266,26 @@ def test_multi_action_policy_updates_match_oracle(Sx, Ax, clipped):
         assert d.scalar("off_policy_count") == ag.off_count
 
 
-@pytest.mark.parametrize("clipped,R,T,rr", [(False, 700, 40, False), (True, 700, 40, False), (False, 40, 5, False),
-                                           (False, 700, 40, True), (False, 40, 5, True)])
-def test_environment_steps_match_oracle(clipped, R, T, rr):
+@pytest.mark.parametrize("clipped,R,T,rr,K", [(False, 700, 40, False, 3), (True, 700, 40, False, 3),
+                                             (False, 40, 5, False, 3), (False, 700, 40, True, 3),
+                                             (False, 40, 5, True, 3), (False, 700, 40, True, 100),
+                                             (False, 40, 5, True, 257)])
+def test_environment_steps_match_oracle(clipped, R, T, rr, K):
     """Concurrent CartPole environments with the same action noise: episodes,
     terminations, the replay memory in processEpisode order, initial retrace
     values, relaunch sample ids — 120 steps, eviction included; (R=40, T=5):
     one step appends more experiences than the replay memory holds.  rr:
     Reward Rescaling (the per-environment sums, counts and sigmas in
-    processEpisode order, bit for bit, and the scaled initial retrace)."""
+    processEpisode order, bit for bit, and the scaled initial retrace); K:
+    Environment Count (above 64 the per-id tables stay in device memory)."""
     H, L, E = 64, 2, 16
     th = theta_for(H, L, 4, spread=0.6)
-    ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None, reward_rescaling=rr)
-    ro = V.Rollouts(ag, E, max_steps=T)
+    ag = V.Agent(S, A, H, L, th, max_size=R, bounds=CLIP if clipped else None, reward_rescaling=rr,
+                 env_count=max(K, 8))
+    ro = V.Rollouts(ag, E, env_count=K, max_steps=T)
     d = device(hidden_size=H, hidden_layers=L, environments=E, mini_batch_size=32, replay_maximum_size=R,
                replay_start_size=R, max_episode_steps=T, hyperparameters=th, seed=4, reward_rescaling=rr,
-               **clip_kw(clipped))
+               environment_count=K, **clip_kw(clipped))
     rng = np.random.default_rng(5)
     total = 0
     for s in range(120):
@@ -309,10 +313,10 @@ def test_environment_steps_match_oracle(clipped, R, T, rr):
     close(d.get("truncated_state").reshape(R, S)[order], np.stack(er["tstate"]), 1e-5, 1e-6)
     assert np.array_equal(d.get("env_sample_ids"), np.array(ro.sample, np.uint64))
     if rr:
-        assert np.array_equal(d.get("reward_rescaling_count")[:3], ag.rcnt[:3])
-        assert np.array_equal(d.get("reward_rescaling_sum")[:3], ag.rsum[:3])
-        assert np.array_equal(d.get("reward_rescaling_sigma")[:3], ag.rsig[:3])
-        assert np.any(ag.rsig[:3] != 1.0)
+        assert np.array_equal(d.get("reward_rescaling_count")[:K], ag.rcnt[:K])
+        assert np.array_equal(d.get("reward_rescaling_sum")[:K], ag.rsum[:K])
+        assert np.array_equal(d.get("reward_rescaling_sigma")[:K], ag.rsig[:K])
+        assert np.any(ag.rsig[:K] != 1.0)
     # actions differ in the last float32 bits (reassociated MFMA sums), so do
     # the fp64 states: round 2 measured at most 3.8e-8 after 30 steps
     close(d.get("env_u").reshape(E, 4), np.stack([c.u for c in ro.carts]), 1e-6, 2e-7)
