@@ -62,9 +62,12 @@ for s in ${STEPS:-tests}; do
     engvr) step engvr 500 python -u -m pytest $R/tests/test_gpu_engine.py -x -v -k vracer --timeout 300 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
     vrtests) step vrtests 400 python -u -m pytest $R/tests/test_gpu_vracer.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider --rootdir $R ;;
     c5) step c5 300 python $R/bench.py --workload c5 --steps 10 --warmup 2 ;;
-    profc5) step profc5 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
-    pmcf5) step pmcf5 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
-    pmcw5) step pmcw5 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline
+    # (graph-replayed updates crash inside rocprofv3's graph interception with
+    #  /opt/rocm's HIP, profiles/r6/c5_profiler_graph_segv.txt: the profiled
+    #  C5 runs launch the update kernels one by one, KORALI_AMD_VR_GRAPH=0)
+    profc5) step profc5 300 env KORALI_AMD_VR_GRAPH=0 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
+    pmcf5) step pmcf5 300 env KORALI_AMD_VR_GRAPH=0 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline ;;
+    pmcw5) step pmcw5 300 env KORALI_AMD_VR_GRAPH=0 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_c5 -o run --output-format csv -- python $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline
            pmcsum pmc_fetch_c5 pmc_write_c5 c5_pmc_traffic.csv ;;
     pmcm4) step pmcm4 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma_c4 -o run --output-format csv -- python $R/bench.py --workload c4 --steps 5 --warmup 1 --cov mfma --no-cpu-baseline
            python $R/tools/pmc_mfma_summary.py $O/pmc_mfma_c4 > $O/c4_mfma_counters.csv && find $O/pmc_mfma_c4 -name "*counter_collection.csv" -delete; cat $O/c4_mfma_counters.csv ;;
