@@ -523,8 +523,9 @@ def c4_scaling(args, world, rank, dist):
                         "korali.Engine", "ranks": world, "transport": transport, "steps": steps, "warmup": w,
             "generations_per_sec_1_rank": one, f"generations_per_sec_{world}_ranks": many, "speedup": many / one,
             "bit_identical_to_1_rank": bool(same), "scaling": "strong",
-            "note": "the eigendecomposition (GSL order, ~11.4 ms of an 18.3 ms 1-GPU generation) is replicated on "
-                    "every rank, which bounds the speed-up at about 1.4x for any rank count (DESIGN.md §6)"}
+            "note": "the eigendecomposition (GSL order: host tridiagonalisation ~1.3 ms on 6 threads + Givens chase "
+                    "~4.4 ms of an ~11.8 ms 1-GPU generation, profiles/r6/bench_c4.json) is replicated on every rank, "
+                    "which bounds the speed-up at about 1.5x for any rank count (DESIGN.md §6)"}
 
 
 def main():
