@@ -484,6 +484,31 @@ def rank_device(local_rank):
     return local_rank % max(1, n), n
 
 
+EXCHANGE_STAGES = ("exchange_fitness", "exchange_rows", "exchange_covariance", "exchange_partials")
+
+
+def exchange_ms(e, dist):
+    """The sharded update's exchange collectives, device time per generation
+    (HIP events around each RCCL call on the handle's stream, the engine's
+    KORALI_AMD_EXCHANGE_PROFILE=1; mean over the run's generations), max over
+    ranks.  None when the engine did not record them."""
+    import torch
+    got = {}
+    try:
+        em = e["Results"]["Exchange Milliseconds"]
+        for st in EXCHANGE_STAGES:
+            try:
+                got[st] = float(em[st])
+            except (KeyError, TypeError, IndexError, ValueError):
+                pass
+    except (KeyError, TypeError):
+        pass
+    v = torch.tensor([got.get(st, -1.0) for st in EXCHANGE_STAGES], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    out = {st: float(x) for st, x in zip(EXCHANGE_STAGES, v.tolist()) if x >= 0}
+    return out or None
+
+
 def c4_scaling(args, world, rank, dist):
     """The C4 experiment through korali.Engine on rank 0 alone (Sequential
     conduit) and sharded over all ranks (Distributed conduit, exact
@@ -512,7 +537,9 @@ def c4_scaling(args, world, rank, dist):
     k["Conduit"]["Type"] = "Distributed"
     k["Conduit"]["Transport"] = transport
     eN = c4_experiment(total, "Exact")
+    os.environ.setdefault("KORALI_AMD_EXCHANGE_PROFILE", "1")
     k.run(eN)
+    exch = exchange_ms(eN, dist)
     t = torch.tensor([rate(eN)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank != 0:
@@ -523,6 +550,7 @@ def c4_scaling(args, world, rank, dist):
                         "korali.Engine", "ranks": world, "transport": transport, "steps": steps, "warmup": w,
             "generations_per_sec_1_rank": one, f"generations_per_sec_{world}_ranks": many, "speedup": many / one,
             "bit_identical_to_1_rank": bool(same), "scaling": "strong",
+            "exchange_ms_per_generation": exch,
             "note": "the eigendecomposition (GSL order: host tridiagonalisation ~1.3 ms on 6 threads + Givens chase "
                     "~4.4 ms of an ~11.8 ms 1-GPU generation, profiles/r6/bench_c4.json) is replicated on every rank, "
                     "which bounds the speed-up at about 1.5x for any rank count (DESIGN.md §6)"}
@@ -928,6 +956,7 @@ def run_c4_engine(args, world, rank):
     os.environ.setdefault("RANK", str(rank))
     os.environ.setdefault("WORLD_SIZE", str(world))
     tdist.init_process_group("gloo")  # (timing exchange only; the engine brings its own bootstrap + RCCL)
+    os.environ.setdefault("KORALI_AMD_EXCHANGE_PROFILE", "1")
     transport = os.environ.get("KORALI_AMD_C4_TRANSPORT",
                                "RCCL" if rank_device(int(os.environ.get("LOCAL_RANK", "0")))[1] >= world else "Host")
     w = max(1, args.warmup)
@@ -946,6 +975,7 @@ def run_c4_engine(args, world, rank):
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     elapsed = float(t.item())
     best = float(e["Solver"]["Best Ever Value"])
+    exch = exchange_ms(e, tdist)
     if rank == 0:
         print(json.dumps({
             "metric": "CMA-ES generations/sec, 512-dim Ackley lambda=65536 (C4)", "value": args.steps / elapsed,
@@ -958,6 +988,7 @@ def run_c4_engine(args, world, rank):
             "samples_per_sec": args.steps / elapsed * C4_L, "best_ever_value": best,
             "timing": "generations %d-%d of one %d-generation engine run (engine completion marks), slowest rank"
                       % (w + 1, total, total),
+            "exchange_ms_per_generation": exch or None,
             "cpu_baseline": None if args.no_cpu_baseline else c4_cpu_baseline()}), flush=True)
     tdist.destroy_process_group()
 

@@ -236,6 +236,11 @@ int kg_cmaes_stream(kg_cmaes_t h, void **stream);
  * events on the handle's stream; enable with kg_cmaes_profile(h, 1). */
 int kg_cmaes_profile(kg_cmaes_t h, int enable);
 int kg_cmaes_profile_read(kg_cmaes_t h, const char *stage, double *ms_total, size_t *count);
+/* A stage bracketed by the caller (phase 0 = begin, 1 = end): an event pair
+ * on the handle's stream, read back with kg_cmaes_profile_read -- the C++
+ * engine's exchange steps (collectives enqueued on this stream) under
+ * KORALI_AMD_EXCHANGE_PROFILE=1.  Returns 1 for an end without a begin. */
+int kg_cmaes_profile_mark(kg_cmaes_t h, const char *stage, int phase);
 
 /* ------------------------------------------------------------ testing */
 /* Host reference of the mt19937 jump-ahead the chunked device producer

@@ -1575,32 +1575,46 @@ __global__ void __launch_bounds__(64 * (AX3_P + 1)) k_adaptC_exact3(int N, int m
 // one element (d, e) of the lower triangle and runs its ordered chain
 // c += fl(fl(T_kd Yc_ke) / s2) with kc_row16 (lane j of the row forms the
 // quotient of term 16 g + j: one product + the Markstein quotient, then one
-// DPP-broadcast add per term).  Workgroup = 8 waves = a 4 (d) x 8 (e) tile:
-// wave w takes d0 + w/2 and columns e0 + 4 (w%2) + row.  T rows and the Yc
-// columns of the tile are staged through LDS in chunks of AR_K terms
-// (transposed to term-contiguous rows), the next chunk's loads in flight.
+// DPP-broadcast add per term).  Workgroup = a 4 (d) x AR_TC (e) tile, one
+// wave per 4 elements: wave w takes d0 + w / (AR_TC/4) and columns
+// e0 + 4 (w % (AR_TC/4)) + row.  T rows and the Yc columns of the tile are
+// staged through LDS in chunks of AR_K terms (transposed to term-contiguous
+// rows), the next chunk's loads in flight.
 // (AR_K = 256: a chunk's sums cover the next chunk's load latency; 128-term
 // chunks left the kernel latency-bound, 34 us at C2)
-constexpr int AR_K = 256, AR_KS = AR_K + 2, AR_TU = 4 * AR_K / 512, AR_YU = 8 * AR_K / 512;
+// Round 6: AR_TC = 4 (4-wave workgroups; 8 before, the same 30.3 vs 30.4 us
+// at C2).  What sets C2's 30 us is issue: one DPP-broadcast FP64 add per term
+// for 4 elements + a quarter of a quotient, ~2 500 instructions per wave and
+// 2 064 waves on 1 024 SIMDs.  Measured round 6 (profiles/r6/README.md): the
+// next group's quotient interleaved into the adds (31.96 us), and quad chains
+// (4 lanes per element, 32-bit quad_perm moves + plain adds, 46.9 us) do not
+// beat it -- every split of 8 256 chains of 2 048 ordered terms over lanes
+// leaves the busiest SIMD about 8 000 FP64 instructions.
+#ifndef KG_AR_TC
+#define KG_AR_TC 4
+#endif
+constexpr int AR_TC = KG_AR_TC, AR_NT = 64 * AR_TC, AR_K = 256, AR_KS = AR_K + 2, AR_TU = 4 * AR_K / AR_NT,
+              AR_YU = AR_TC * AR_K / AR_NT;
+static_assert(AR_TC == 4 || AR_TC == 8, "4 x 4 or 4 x 8 tiles");
 __host__ __device__ inline int ar_row_blocks(int N) { return (N + 3) / 4; }
-__host__ __device__ inline int ar_col_blocks_upto(int rb) { return (4 * rb + 3) / 8 + 1; }  // e0 <= d0 + 3
+__host__ __device__ inline int ar_col_blocks_upto(int rb) { return (4 * rb + 3) / AR_TC + 1; }  // e0 <= d0 + 3
 int ar_tiles(int N) {
   int t = 0;
-  for (int rb = 0; rb < ar_row_blocks(N); rb++) t += std::min(ar_col_blocks_upto(rb), (N + 7) / 8);
+  for (int rb = 0; rb < ar_row_blocks(N); rb++) t += std::min(ar_col_blocks_upto(rb), (N + AR_TC - 1) / AR_TC);
   return t;
 }
 template <bool kMarkstein>
 __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int e0, int dl, int el,
                                          const double *__restrict__ Yc, const double *__restrict__ Tt, double s2,
-                                         double (*Ts)[4][AR_KS], double (*Ys)[8][AR_KS]) {
+                                         double (*Ts)[4][AR_KS], double (*Ys)[AR_TC][AR_KS]) {
   const int tid = threadIdx.x, j = tid & 15;
   const double y = kMarkstein ? 1.0 / s2 : 0.0;
-  // staging: T rows d0..d0+3 (4 x AR_K) and Yc[k][e0..e0+7] (AR_K x 8)
+  // staging: T rows d0..d0+3 (4 x AR_K) and Yc[k][e0..e0+AR_TC-1] (AR_K x AR_TC)
   double tv[AR_TU], yv[AR_YU];
   auto load = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < AR_TU; u++) {
-      const int q = tid + 512 * u, r = q / AR_K;
+      const int q = tid + AR_NT * u, r = q / AR_K;
       int kq = q % AR_K;
       asm volatile("" : "+v"(kq));  // (an opaque value: no SDWA byte-select form of `q % 256` in its uses)
       const int k = k0 + kq;
@@ -1608,22 +1622,22 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
     }
 #pragma unroll
     for (int u = 0; u < AR_YU; u++) {
-      const int q = tid + 512 * u, k = k0 + (q >> 3), c = q & 7;
+      const int q = tid + AR_NT * u, k = k0 + q / AR_TC, c = q % AR_TC;
       yv[u] = (k < mu && e0 + c < N) ? Yc[(size_t)k * N + e0 + c] : 0.0;
     }
   };
   auto store = [&](int b) {
 #pragma unroll
     for (int u = 0; u < AR_TU; u++) {
-      const int q = tid + 512 * u;
+      const int q = tid + AR_NT * u;
       int kq = q % AR_K;
       asm volatile("" : "+v"(kq));
       Ts[b][q / AR_K][kq] = tv[u];
     }
 #pragma unroll
     for (int u = 0; u < AR_YU; u++) {
-      const int q = tid + 512 * u;
-      Ys[b][q & 7][q >> 3] = yv[u];
+      const int q = tid + AR_NT * u;
+      Ys[b][q % AR_TC][q / AR_TC] = yv[u];
     }
   };
   load(0);
@@ -1655,24 +1669,24 @@ __device__ __forceinline__ double ar_run(double acc, int N, int mu, int d0, int 
 // lower-triangle results go to pack[d (d + 1) / 2 + e] (the sharded
 // exchange buffer, "Shard Covariance") instead of C, entries that adaptC
 // leaves unchanged (diagonal covariance) with their old value
-__global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal, const double *__restrict__ Yc,
+__global__ void __launch_bounds__(AR_NT) k_adaptC_row(int N, int mu, int diagonal, const double *__restrict__ Yc,
                                                     const double *__restrict__ Tt, const double *__restrict__ pc,
                                                     double *C, const CmaesScalars *__restrict__ sc, int tbase,
                                                     double *__restrict__ pack) {
   __shared__ double Ts[2][4][AR_KS];
-  __shared__ double Ys[2][8][AR_KS];
+  __shared__ double Ys[2][AR_TC][AR_KS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row = lane >> 4, j = lane & 15;
   // tile index -> (row block, column block), row blocks in order
   int t = blockIdx.x + tbase, rb = 0;
-  const int ncb = (N + 7) / 8;
+  const int ncb = (N + AR_TC - 1) / AR_TC;
   for (;; rb++) {
     const int c = min(ar_col_blocks_upto(rb), ncb);
     if (t < c) break;
     t -= c;
   }
-  const int d0 = 4 * rb, e0 = 8 * t;
-  const int dl = wid >> 1, el = 4 * (wid & 1) + row;
+  const int d0 = 4 * rb, e0 = AR_TC * t;
+  const int dl = wid / (AR_TC / 4), el = 4 * (wid % (AR_TC / 4)) + row;
   const int d = d0 + dl, e = e0 + el;
   const bool active = d < N && e < N && e <= d && (!diagonal || e == d);
   const double ccov1 = sc->ccov1, ccovmu = sc->ccovmu, cc = sc->cumulativeCovariance;
@@ -1709,14 +1723,25 @@ __global__ void __launch_bounds__(512) k_adaptC_row(int N, int mu, int diagonal,
 // adds), and a tile reads 32 operand streams for 256 elements (the row form:
 // 12 for 32): C4's 131 328 chains of 32 768 terms are issue-bound instead of
 // chain-latency-bound, and the tiles re-read a third of the operands.
-constexpr int AL_T = 16, AL_K = 64, AL_LD = AL_T + 1;  // (64-term chunks: 35 KB of LDS, four workgroups per CU)
+// Round 6: both staged operands are held term-contiguous ([row][term], rows
+// padded to 66 doubles so the 16 rows a ds_read_b128 lane group touches start
+// in distinct bank quads) and read two terms per ds_read_b128: 4 LDS-array
+// cycles per wave and term instead of 8 for the [term][row] images, whose
+// paired reads the compiler merged into ds_read2_b64 (8 cycles per pair).
+// At C4 the busiest CUs hold three tiles (528 tiles on 256 CUs), so the LDS
+// array, not the FP64 issue, had set the kernel's time.
+#ifndef KG_AL_K
+#define KG_AL_K 64
+#endif
+constexpr int AL_T = 16, AL_K = KG_AL_K, AL_KP = AL_K + 2;  // (64-term chunks: 34 KB of LDS, four workgroups per CU)
+static_assert(AL_K % 2 == 0, "two terms per ds_read_b128");
 __host__ __device__ inline int al_blocks(int N) { return (N + AL_T - 1) / AL_T; }
 int al_tiles(int N) { return al_blocks(N) * (al_blocks(N) + 1) / 2; }
 template <bool kMarkstein>
 __device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double *__restrict__ Yc,
                                        const double *__restrict__ Tt, const double *__restrict__ pc, double *C,
                                        const CmaesScalars *__restrict__ sc, int tbase, double *__restrict__ pack,
-                                       double (*Ts)[AL_K][AL_LD], double (*Ys)[AL_K][AL_LD]) {
+                                       double (*Ts)[AL_T][AL_KP], double (*Ys)[AL_T][AL_KP]) {
   const int tid = threadIdx.x, dl = tid >> 4, el = tid & 15;
   // tile -> (row block bd, column block be <= bd), row blocks in order (an
   // XCD-grouped order measured the same at C4, round 5: 1.97 vs 1.99 ms)
@@ -1733,8 +1758,8 @@ __device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double
     const double Cde = C[(size_t)d * N + e];
     acc = (1 - ccov1 - ccovmu) * Cde + ccov1 * (pc[d] * pc[e] + (1 - hsig) * cc * (2. - cc) * Cde);
   }
-  // staging: T rows d0..d0+15 (term-contiguous) and Yc[k][e0..e0+15]
-  constexpr int U = AL_T * AL_K / 256;  // 8 values of each per thread
+  // staging: T rows d0..d0+15 and Yc[k][e0..e0+15], both as [row][term]
+  constexpr int U = AL_T * AL_K / 256;  // 4 values of each per thread
   double tv[U], yv[U];
   auto load = [&](int k0) {
 #pragma unroll
@@ -1749,9 +1774,17 @@ __device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int q = tid + 256 * u;
-      Ts[b][q % AL_K][q / AL_K] = tv[u];
-      Ys[b][q >> 4][q & 15] = yv[u];
+      Ts[b][q / AL_K][q % AL_K] = tv[u];
+      Ys[b][q & 15][q >> 4] = yv[u];
     }
+  };
+  auto quot = [&](double pr) __attribute__((always_inline)) {
+    if (kMarkstein) {
+      const double q0 = pr * y;
+      const double r = __builtin_fma(-q0, s2, pr);
+      return __builtin_fma(r, y, q0);
+    }
+    return pr / s2;
   };
   load(0);
   store(0);
@@ -1760,35 +1793,26 @@ __device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double
     const bool more = k0 + AL_K < mu;
     if (more) load(k0 + AL_K);
     const int kn = min(AL_K, mu - k0);
+    const double2 *tr = reinterpret_cast<const double2 *>(&Ts[b][dl][0]);
+    const double2 *yr = reinterpret_cast<const double2 *>(&Ys[b][el][0]);
     int k = 0;
     for (; k + 8 <= kn; k += 8) {
+      double2 tp[4], yp[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        tp[u] = tr[k / 2 + u];
+        yp[u] = yr[k / 2 + u];
+      }
       double q[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const double pr = Ts[b][k + u][dl] * Ys[b][k + u][el];
-        if (kMarkstein) {
-          const double q0 = pr * y;
-          const double r = __builtin_fma(-q0, s2, pr);
-          q[u] = __builtin_fma(r, y, q0);
-        } else {
-          q[u] = pr / s2;
-        }
+      for (int u = 0; u < 4; u++) {
+        q[2 * u] = quot(tp[u].x * yp[u].x);
+        q[2 * u + 1] = quot(tp[u].y * yp[u].y);
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) acc += q[u];
     }
-    for (; k < kn; k++) {
-      const double pr = Ts[b][k][dl] * Ys[b][k][el];
-      double q;
-      if (kMarkstein) {
-        const double q0 = pr * y;
-        const double r = __builtin_fma(-q0, s2, pr);
-        q = __builtin_fma(r, y, q0);
-      } else {
-        q = pr / s2;
-      }
-      acc += q;
-    }
+    for (; k < kn; k++) acc += quot(Ts[b][dl][k] * Ys[b][el][k]);
     if (more) store(b ^ 1);
     __syncthreads();
   }
@@ -1805,7 +1829,7 @@ __global__ void __launch_bounds__(256) k_adaptC_lane(int N, int mu, int diagonal
                                                      const double *__restrict__ Tt, const double *__restrict__ pc,
                                                      double *C, const CmaesScalars *__restrict__ sc, int tbase,
                                                      double *__restrict__ pack) {
-  __shared__ double Ts[2][AL_K][AL_LD], Ys[2][AL_K][AL_LD];  // [term][d - d0] / [term][e - e0]
+  __shared__ __attribute__((aligned(16))) double Ts[2][AL_T][AL_KP], Ys[2][AL_T][AL_KP];  // [d - d0][term] / [e - e0][term]
   // Markstein quotients when every factor is in range (as k_adaptC_row)
   const double s2 = sc->sigma * sc->sigma;
   const int ex = (int)((__double_as_longlong(s2) >> 52) & 0x7ff) - 1023;
@@ -2974,6 +2998,7 @@ struct kg_cmaes_s {
   // profiling
   bool profile = false;
   std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> pending;
+  std::map<std::string, hipEvent_t> openMarks;  // kg_cmaes_profile_mark begun, not ended
   std::map<std::string, std::pair<double, size_t>> prof;
 };
 
@@ -3446,6 +3471,7 @@ int kg_cmaes_destroy(kg_cmaes_t h) {
     (void)hipEventDestroy(std::get<1>(t));
     (void)hipEventDestroy(std::get<2>(t));
   }
+  for (auto &m : h->openMarks) (void)hipEventDestroy(m.second);
   if (h->stream2) {
     (void)hipStreamSynchronize(h->stream2);
     stream_release(h->stream2);
@@ -4154,7 +4180,7 @@ int kg_cmaes_update(kg_cmaes_t h, size_t generation) {
       } else if (!old2 && row_chains()) {
         // Markstein quotients when every factor is in range (k_rankmu_prep's
         // flag, read on the device: the kernel picks the branch per launch)
-        hipLaunchKernelGGL(k_adaptC_row, dim3(ar_tiles(N)), dim3(512), 0, h->stream, N, mu,
+        hipLaunchKernelGGL(k_adaptC_row, dim3(ar_tiles(N)), dim3(AR_NT), 0, h->stream, N, mu,
                            h->cfg.diagonal_covariance, h->Yc, h->Tt, h->pc, h->C, h->sc, 0, (double *)nullptr);
       } else if (old2)
         hipLaunchKernelGGL(k_adaptC_exact2, dim3((N + 3) / 4, (N + 63) / 64), dim3(256), 0, h->stream, N, mu,
@@ -4269,7 +4295,7 @@ int kg_cmaes_update_rows(kg_cmaes_t h, size_t generation) {
       hipLaunchKernelGGL(k_adaptC_lane, dim3(t1 - t0), dim3(256), 0, h->stream, N, mu, h->cfg.diagonal_covariance,
                          h->Yc, h->Tt, h->pc, h->C, h->sc, t0, h->covPack);
     else if (t1 > t0)
-      hipLaunchKernelGGL(k_adaptC_row, dim3(t1 - t0), dim3(512), 0, h->stream, N, mu, h->cfg.diagonal_covariance, h->Yc,
+      hipLaunchKernelGGL(k_adaptC_row, dim3(t1 - t0), dim3(AR_NT), 0, h->stream, N, mu, h->cfg.diagonal_covariance, h->Yc,
                          h->Tt, h->pc, h->C, h->sc, t0, h->covPack);
     KG_HIP(hipGetLastError());
   }
@@ -4564,6 +4590,27 @@ int kg_cmaes_population_size(kg_cmaes_t h, size_t *lambda, size_t *mu) {
 
 int kg_cmaes_profile(kg_cmaes_t h, int enable) {
   h->profile = enable != 0;
+  return 0;
+}
+
+int kg_cmaes_profile_mark(kg_cmaes_t h, const char *stage, int phase) {
+  if (!h || !stage || (phase != 0 && phase != 1)) return 1;
+  hipEvent_t e;
+  KG_HIP(hipEventCreate(&e));
+  KG_HIP(hipEventRecord(e, h->stream));
+  if (phase == 0) {
+    auto it = h->openMarks.find(stage);
+    if (it != h->openMarks.end()) (void)hipEventDestroy(it->second);
+    h->openMarks[stage] = e;
+    return 0;
+  }
+  auto it = h->openMarks.find(stage);
+  if (it == h->openMarks.end()) {
+    (void)hipEventDestroy(e);
+    return 1;
+  }
+  h->pending.emplace_back(stage, it->second, e);
+  h->openMarks.erase(it);
   return 0;
 }
 

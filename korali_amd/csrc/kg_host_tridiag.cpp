@@ -47,6 +47,7 @@
 #include <unistd.h>
 #include <x86intrin.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -165,10 +166,62 @@ bool claim_cpu(int cpu, std::vector<int> &fds) {
   fds.push_back(fd);
   return true;
 }
+// Per-CPU busy fraction over a short window from /proc/stat (empty when it is
+// unreadable): on a shared host, cores another process keeps busy make slow
+// helpers (a spinning helper preempted stalls every step of the pass).
+std::vector<double> cpu_busy(int window_ms) {
+  auto sample = [](std::vector<std::pair<unsigned long long, unsigned long long>> &v) {
+    v.assign(CPU_SETSIZE, {0, 0});
+    std::string t = read_text("/proc/stat");
+    size_t i = 0;
+    while ((i = t.find("\ncpu", i)) != std::string::npos) {
+      i += 4;
+      if (i >= t.size() || t[i] < '0' || t[i] > '9') continue;
+      char *end = nullptr;
+      const long c = std::strtol(t.c_str() + i, &end, 10);
+      unsigned long long f[8] = {0}, tot = 0;
+      const char *q = end;
+      for (int k = 0; k < 8; k++) {
+        f[k] = std::strtoull(q, &end, 10);
+        if (end == q) break;
+        q = end;
+        tot += f[k];
+      }
+      if (c >= 0 && c < CPU_SETSIZE) v[c] = {tot, f[3] + f[4]};  // (idle + iowait)
+    }
+  };
+  std::vector<std::pair<unsigned long long, unsigned long long>> a, b;
+  sample(a);
+  std::this_thread::sleep_for(std::chrono::milliseconds(window_ms));
+  sample(b);
+  std::vector<double> busy(CPU_SETSIZE, 0.0);
+  bool any = false;
+  for (int c = 0; c < CPU_SETSIZE; c++) {
+    const unsigned long long dt = b[c].first - a[c].first, di = b[c].second - a[c].second;
+    if (dt == 0) continue;
+    any = true;
+    busy[c] = 1.0 - (double)di / (double)dt;
+  }
+  if (!any) busy.clear();
+  return busy;
+}
 std::vector<int> helper_cpus(int want, std::vector<int> &fds) {
   std::vector<int> out;
   cpu_set_t mask;
   if (want <= 0 || sched_getaffinity(0, sizeof mask, &mask)) return out;
+  // idle cores first within each candidate list (stable: topology order
+  // among equally idle ones); KORALI_AMD_HOST_TRIDIAG_BUSY_MS=0 skips the probe
+  const char *bm = std::getenv("KORALI_AMD_HOST_TRIDIAG_BUSY_MS");
+  const std::vector<double> busy = cpu_busy(bm ? std::atoi(bm) : 20);
+  auto by_idle = [&](std::vector<int> v) {
+    if (!busy.empty())
+      std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
+        const bool bx = x >= 0 && x < (int)busy.size() && busy[x] > 0.25;
+        const bool by = y >= 0 && y < (int)busy.size() && busy[y] > 0.25;
+        return bx < by;
+      });
+    return v;
+  };
   const int me = sched_getcpu();
   const std::string sys = "/sys/devices/system/cpu/cpu";
   std::set<int> used;  // physical cores taken (their SMT siblings too)
@@ -186,11 +239,11 @@ std::vector<int> helper_cpus(int want, std::vector<int> &fds) {
       out.push_back(c);
     }
   };
-  if (me >= 0) consider(parse_cpu_list(read_text(sys + std::to_string(me) + "/cache/index3/shared_cpu_list")));
+  if (me >= 0) consider(by_idle(parse_cpu_list(read_text(sys + std::to_string(me) + "/cache/index3/shared_cpu_list"))));
   std::vector<int> all;
   for (int c = 0; c < CPU_SETSIZE; c++)
     if (CPU_ISSET(c, &mask)) all.push_back(c);
-  consider(all);
+  consider(by_idle(all));
   return out;
 }
 }  // namespace

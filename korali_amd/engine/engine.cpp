@@ -675,6 +675,7 @@ struct CmaesModule : SolverModule {
   Collective *dist = nullptr;
   size_t r0 = 0, r1 = 0;
   bool exactShards = true;  // the sharded update's protocol (include/korali_amd.h): exact order or partial sums
+  bool exchangeProfile = false;  // KORALI_AMD_EXCHANGE_PROFILE=1: time the exchange collectives
   // Distributed CCMA-ES: the device state runs replicated (unsharded handle on
   // every rank: the viability regime changes the population size and the
   // resampling walk is sequential), the callbacks are split over the ranks
@@ -825,6 +826,10 @@ struct CmaesModule : SolverModule {
     c.covariance_matrix_adaption_strength = num(sv, "Covariance Matrix Adaption Strength", 0.1);
     c.global_success_learning_rate = num(sv, "Global Success Learning Rate", 0.2);
     check(kg_cmaes_create(&c, &h));
+    {
+      const char *ep = getenv("KORALI_AMD_EXCHANGE_PROFILE");
+      exchangeProfile = ep && *ep == '1';
+    }
     if (!constraintFns.empty()) check(kg_cmaes_set_constraints(h, &CmaesModule::constraintCallback, this));
     if (mu == 0) mu = lam / 2;
     unsigned char st[5000];
@@ -963,21 +968,34 @@ struct CmaesModule : SolverModule {
       if (useGradients) check(kg_cmaes_set_gradients(h, G.data()));
     }
     if (dist && !replicated) {
-      // the exchange steps of the sharded update
+      // the exchange steps of the sharded update; with
+      // KORALI_AMD_EXCHANGE_PROFILE=1 each is bracketed by stream events
+      // (device time of the collective, "Exchange Milliseconds" in the results)
+      auto mark = [&](const char *stage, int phase) {
+        if (exchangeProfile) check(kg_cmaes_profile_mark(h, stage, phase));
+      };
+      mark("exchange_fitness", 0);
       dist->allGather(buffer("Value Vector"), r1 - r0);
       if (useGradients) dist->allGather(buffer("Gradients"), (r1 - r0) * N);
+      mark("exchange_fitness", 1);
       check(kg_cmaes_update_partial(h, gen));
       size_t n = 0;
       if (exactShards) {
         // the selected rows to every rank, then the covariance entries' owners
         check(kg_cmaes_shard_row_count(h, &n));
+        mark("exchange_rows", 0);
         if (n) dist->allGather(buffer("Shard Rows"), n);
+        mark("exchange_rows", 1);
         check(kg_cmaes_update_rows(h, gen));
         check(kg_cmaes_field_size(h, "Shard Covariance", &n));
+        mark("exchange_covariance", 0);
         dist->allReduceMaxI64(buffer("Shard Covariance"), n);
+        mark("exchange_covariance", 1);
       } else {
         check(kg_cmaes_field_size(h, "Shard Partials", &n));
+        mark("exchange_partials", 0);
         dist->allReduceSum(buffer("Shard Partials"), n);
+        mark("exchange_partials", 1);
       }
       check(kg_cmaes_update_finalize(h, gen));
       updated = true;
@@ -1173,6 +1191,14 @@ struct CmaesModule : SolverModule {
   }
 
   void finalize(Json &js) override {
+    if (exchangeProfile) {
+      for (const char *st : {"exchange_fitness", "exchange_rows", "exchange_covariance", "exchange_partials"}) {
+        double ms = 0;
+        size_t cnt = 0;
+        check(kg_cmaes_profile_read(h, st, &ms, &cnt));
+        if (cnt) js["Results"]["Exchange Milliseconds"][st] = ms / (double)cnt;
+      }
+    }
     // CMAES::finalize (CMAES.cpp.base:994-999)
     js["Results"]["Best Sample"]["F(x)"] = field("Best Ever Value");
     std::vector<double> b(N);

@@ -75,7 +75,7 @@ EXPORTED = [
     "kg_cmaes_shard_row_count", "kg_cmaes_update_rows",
     "kg_cmaes_synchronize", "kg_cmaes_field_size", "kg_cmaes_get_field", "kg_cmaes_set_field",
     "kg_cmaes_get_fields", "kg_cmaes_get_sorting_index", "kg_cmaes_get_rng", "kg_cmaes_set_rng", "kg_cmaes_device_ptr",
-    "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read",
+    "kg_cmaes_stream", "kg_cmaes_profile", "kg_cmaes_profile_read", "kg_cmaes_profile_mark",
     "kg_cmaes_set_constraints", "kg_cmaes_prepare_constrained", "kg_cmaes_population_size",
     "kg_tmcmc_create", "kg_tmcmc_destroy", "kg_tmcmc_generation", "kg_tmcmc_synchronize", "kg_tmcmc_field_size",
     "kg_tmcmc_get_field", "kg_tmcmc_set_field", "kg_tmcmc_get_rng", "kg_tmcmc_set_rng", "kg_tmcmc_prepare",
@@ -142,6 +142,7 @@ def lib():
         L.kg_cmaes_stream.argtypes = [vp, C.POINTER(vp)]
         L.kg_cmaes_profile.argtypes = [vp, ip]
         L.kg_cmaes_profile_read.argtypes = [vp, cp, dp, C.POINTER(sz)]
+        L.kg_cmaes_profile_mark.argtypes = [vp, cp, ip]
         L.kg_tmcmc_create.argtypes = [C.POINTER(_TmcmcCfg), C.POINTER(vp)]
         for f in ("kg_tmcmc_destroy", "kg_tmcmc_synchronize", "kg_tmcmc_evaluate", "kg_tmcmc_evaluate_prior"):
             getattr(L, f).argtypes = [vp]
