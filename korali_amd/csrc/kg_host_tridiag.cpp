@@ -213,6 +213,12 @@ std::vector<int> helper_cpus(int want, std::vector<int> &fds) {
   // among equally idle ones); KORALI_AMD_HOST_TRIDIAG_BUSY_MS=0 skips the probe
   const char *bm = std::getenv("KORALI_AMD_HOST_TRIDIAG_BUSY_MS");
   const std::vector<double> busy = cpu_busy(bm ? std::atoi(bm) : 20);
+  if (std::getenv("KORALI_AMD_HOST_TRIDIAG_VERBOSE") && !busy.empty()) {
+    int nb = 0, n = 0;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &mask)) n++, nb += busy[c] > 0.25;
+    std::fprintf(stderr, "[host tridiag] %d of %d allowed cpus busy over the probe window\n", nb, n);
+  }
   auto by_idle = [&](std::vector<int> v) {
     if (!busy.empty())
       std::stable_sort(v.begin(), v.end(), [&](int x, int y) {
@@ -453,6 +459,11 @@ int pool_init(HostTridiag &w, int P) {
   const bool pin = !std::getenv("KORALI_AMD_HOST_TRIDIAG_NOPIN");
   const std::vector<int> cpus = helper_cpus(pin ? P - 1 : 0, p->lockFds);
   if (pin) p->P = P = 1 + (int)cpus.size();
+  if (std::getenv("KORALI_AMD_HOST_TRIDIAG_VERBOSE")) {
+    std::fprintf(stderr, "[host tridiag] caller on cpu %d, %d helper(s) on cpus", sched_getcpu(), P - 1);
+    for (int c : cpus) std::fprintf(stderr, " %d", c);
+    std::fprintf(stderr, "\n");
+  }
   if (P == 1) return 0;
   for (int t = 1; t < P; t++) {
     const int cpu = pin ? cpus[t - 1] : -1;
