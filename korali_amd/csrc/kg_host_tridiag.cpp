@@ -209,10 +209,14 @@ std::vector<int> helper_cpus(int want, std::vector<int> &fds) {
   std::vector<int> out;
   cpu_set_t mask;
   if (want <= 0 || sched_getaffinity(0, sizeof mask, &mask)) return out;
-  // idle cores first within each candidate list (stable: topology order
-  // among equally idle ones); KORALI_AMD_HOST_TRIDIAG_BUSY_MS=0 skips the probe
+  // KORALI_AMD_HOST_TRIDIAG_BUSY_MS=<ms>: idle cores first within each
+  // candidate list (stable: topology order among equally idle ones), from a
+  // /proc/stat window of that length.  Off by default: the window is paid at
+  // every handle creation (20 ms against a 20-generation C2 run's ~11 ms),
+  // /proc/stat counts in 10 ms ticks, and a same-box C4 A/B showed no gain.
   const char *bm = std::getenv("KORALI_AMD_HOST_TRIDIAG_BUSY_MS");
-  const std::vector<double> busy = cpu_busy(bm ? std::atoi(bm) : 20);
+  const int window = bm ? std::atoi(bm) : 0;
+  const std::vector<double> busy = window > 0 ? cpu_busy(window) : std::vector<double>();
   if (std::getenv("KORALI_AMD_HOST_TRIDIAG_VERBOSE") && !busy.empty()) {
     int nb = 0, n = 0;
     for (int c = 0; c < CPU_SETSIZE; c++)
