@@ -407,6 +407,12 @@ class CmaesDevice:
         check(self._L.kg_cmaes_profile_read(self.h, stage.encode(), C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def profile_mark(self, stage, phase):
+        """kg_cmaes_profile_mark: phase 0 begins, 1 ends a caller-bracketed
+        stage on the handle's stream; returns the C-ABI status (1: an end
+        without a begin)."""
+        return int(self._L.kg_cmaes_profile_mark(self.h, stage.encode(), int(phase)))
+
 
 class TmcmcDevice:
     """One TMCMC sampler instance (Version "TMCMC") on one MI355X (kg_tmcmc_t).

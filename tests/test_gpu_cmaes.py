@@ -616,3 +616,22 @@ def test_handles_of_different_sizes_interleaved_bit_exact():
                 assert np.array_equal(dev[key], o[key]), (dev.N, g, key)
     for dev in (big, small, tiny):
         dev.close()
+
+
+@pytest.mark.gpu
+def test_profile_mark_brackets_a_stage():
+    """kg_cmaes_profile_mark (the engine's exchange timing): begin / end pairs
+    on the handle's stream accumulate into one stage; an end without a begin
+    is refused."""
+    dev = device_solver(8, 16, initial_value=np.zeros(8), initial_std=np.ones(8), normal_seed=1, uniform_seed=2)
+    try:
+        assert dev.profile_mark("exchange_test", 1) == 1
+        for g in range(1, 3):
+            assert dev.profile_mark("exchange_test", 0) == 0
+            dev.generation(g, "rosenbrock")
+            assert dev.profile_mark("exchange_test", 1) == 0
+        ms, n = dev.profile_read("exchange_test")
+        assert n == 2 and ms > 0.0
+        assert dev.profile_read("exchange_test") == (0.0, 0)
+    finally:
+        dev.close()
