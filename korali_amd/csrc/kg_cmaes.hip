@@ -1796,18 +1796,27 @@ __device__ __forceinline__ void al_run(int N, int mu, int diagonal, const double
     const double2 *tr = reinterpret_cast<const double2 *>(&Ts[b][dl][0]);
     const double2 *yr = reinterpret_cast<const double2 *>(&Ys[b][el][0]);
     int k = 0;
-    for (; k + 8 <= kn; k += 8) {
-      double2 tp[4], yp[4];
+    // the next 8 terms' reads issued before this 8's adds (the index clamped
+    // into the row on the last pass): two or three waves per SIMD do not
+    // cover an LDS round trip per group
+    double2 tp[4], yp[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        tp[u] = tr[k / 2 + u];
-        yp[u] = yr[k / 2 + u];
-      }
+    for (int u = 0; u < 4; u++) {
+      tp[u] = tr[u];
+      yp[u] = yr[u];
+    }
+    for (; k + 8 <= kn; k += 8) {
       double q[8];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         q[2 * u] = quot(tp[u].x * yp[u].x);
         q[2 * u + 1] = quot(tp[u].y * yp[u].y);
+      }
+      const int nk = min(k + 8, AL_K - 8);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        tp[u] = tr[nk / 2 + u];
+        yp[u] = yr[nk / 2 + u];
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) acc += q[u];
